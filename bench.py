@@ -1,0 +1,167 @@
+#!/usr/bin/env python3
+"""Headline benchmark: whole-node images/s of ResNet-50 data-parallel training
+with Gaussian-k gradient sparsification at density 0.1% on MI355X.
+
+Metric (BASELINE.json): "images/sec (whole node) ResNet-50 k=0.1% at 1/2/4/8
+MI355X; effective grad compression ratio".  One process per GPU; launched
+by ``torch.distributed.run`` for N > 1 (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*).
+
+Each timed step is the FULL training step: zero_grad, forward (bf16
+autocast, channels_last), backward, per-bucket fused Gaussian-k compression
+with error feedback, packed all-gather over RCCL, scatter-add average, fused
+momentum-SGD update of every parameter.  The compressor also runs at N = 1
+(world of one) so the per-GPU work is identical at every N (weak scaling).
+Data: synthetic ImageNet-shaped batches generated on the device; weights:
+random init.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch-size B]
+       [--compressor gaussian] [--density 0.001] [--model resnet50]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+METRIC = "images/sec (whole node) ResNet-50 k=0.1% at 1/2/4/8 MI355X; effective grad compression ratio"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch-size", type=int, default=int(os.environ.get("GKSGD_BENCH_BS", "256")))
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--compressor", default="gaussian")
+    ap.add_argument("--density", type=float, default=0.001)
+    ap.add_argument("--threshold", type=int, default=524288000, help="bucket threshold (elements), reference default")
+    ap.add_argument("--amp", default="bf16", choices=["bf16", "none"])
+    ap.add_argument("--no-channels-last", action="store_true")
+    ap.add_argument("--dense", action="store_true", help="dense RCCL all-reduce comparator (compressor none)")
+    ap.add_argument("--no-native-rccl", action="store_true")
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args()
+
+
+def main() -> int:
+    args = parse()
+    from gaussiank_sgd_amd import ops
+    from gaussiank_sgd_amd.compression import compressors
+    from gaussiank_sgd_amd.parallel import comm
+    from gaussiank_sgd_amd.parallel.distributed_optimizer import DistributedOptimizer
+    from gaussiank_sgd_amd.train import DLTrainer
+
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and world_env == 1:
+        # self-launch: start torch.distributed.run as a child (never exec after touching the GPU)
+        import subprocess
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+               "--master-addr", "127.0.0.1", "--master-port", os.environ.get("MASTER_PORT", "29533"),
+               os.path.abspath(__file__)] + sys.argv[1:]
+        return subprocess.call(cmd)
+
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if not torch.cuda.is_available():
+        print("bench.py needs a GPU", file=sys.stderr)
+        return 2
+    torch.cuda.set_device(local_rank)
+    comm.init()
+    P = comm.size()
+    rank = comm.rank()
+    if not ops.load():
+        raise RuntimeError("native extension missing: run `python -m gaussiank_sgd_amd.ops.build`")
+    torch.backends.cudnn.benchmark = True
+
+    dataset = "imagenet" if args.model in ("resnet50", "resnet18", "resnet34", "resnet101", "resnet152",
+                                           "vgg16i") else None
+    trainer = DLTrainer(rank, P, dnn=args.model, dataset=dataset or "imagenet", batch_size=args.batch_size,
+                        lr=0.1, nworkers=P, device="cuda", amp=None if args.amp == "none" else "bf16",
+                        channels_last=not args.no_channels_last, seed=0)
+    comp_name = "none" if args.dense else args.compressor
+    is_sparse = not args.dense and comp_name not in ("none", "bucket")
+    opt = DistributedOptimizer(trainer.optimizer, named_parameters=trainer.net.named_parameters(),
+                               compression=compressors[comp_name], is_sparse=is_sparse, density=args.density,
+                               threshold=args.threshold, compress_single_rank=True, density_warmup=False,
+                               native_rccl=not args.no_native_rccl)
+    comm.broadcast_parameters(trainer.net.state_dict(), root_rank=0)
+    trainer.update_optimizer(opt)
+    trainer.display = 10 ** 9  # no host-syncing log lines inside the timed loop
+    nparams = sum(p.numel() for p in trainer.net.parameters() if p.requires_grad)
+
+    def step():
+        opt.zero_grad()
+        trainer.train(1)
+        trainer.update_model()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    opt._collect_selected()  # drop warm-up counts
+    comm.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    comm.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if P > 1:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    elapsed = float(t)
+    loss = trainer.current_loss()
+    counts = opt._collect_selected()
+    sel = (sum(counts) / max(1, args.steps)) if counts else 0.0
+    if is_sparse and sel > 0:
+        ratio = (nparams * 4.0) / (sel * 8.0)
+    else:
+        ratio = 1.0
+    ms = elapsed / args.steps * 1e3
+    imgs = P * args.batch_size * args.steps / elapsed
+    out = {
+        "metric": METRIC,
+        "value": round(imgs, 2),
+        "unit": "images/s",
+        "n_gpus": P,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16" if args.amp == "bf16" else "fp32",
+        "data": "synthetic (ImageNet-shaped 3x224x224, on-device), random-init weights",
+        "config": {
+            "model": args.model,
+            "global_batch": P * args.batch_size,
+            "per_gpu_batch": args.batch_size,
+            "seq_len": None,
+            "image_size": 224,
+            "parallelism": "dp%d" % P,
+            "compressor": comp_name,
+            "density": args.density if is_sparse else 1.0,
+            "buckets": len(opt.arena.buckets),
+            "exchange": opt._exchanger.kind if opt._exchanger is not None else "none",
+        },
+        "effective_compression_ratio": round(ratio, 1),
+        "selected_per_step": round(sel, 1),
+        "params": nparams,
+        "final_loss": round(loss, 4) if loss == loss else None,
+    }
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    comm.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,158 @@
+"""On-device synthetic datasets with the reference's shapes.
+
+| dataset   | sample            | classes / vocab | train samples |
+|-----------|-------------------|-----------------|---------------|
+| imagenet  | 3x224x224 fp32    | 1000            | 1,281,167     |
+| cifar10   | 3x32x32           | 10              | 50,000        |
+| mnist     | 1x28x28 (32x32 for lenet) | 10      | 60,000        |
+| ptb       | 35 tokens         | 10,000          | 929,589 tokens|
+| wikipedia | 512 tokens (MLM)  | 30,522          | 1,000,000     |
+
+``learnable=True`` makes labels a fixed function of the inputs (argmax of a
+random projection / next-token shift) so convergence tests see the loss fall.
+A small pool of batches is generated once on the device and cycled.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+
+
+@dataclass(frozen=True)
+class DatasetSpec:
+    name: str
+    shape: Tuple[int, ...]
+    num_classes: int
+    train_samples: int
+    test_samples: int
+    kind: str  # image | tokens | mlm
+
+
+DATASETS = {
+    "imagenet": DatasetSpec("imagenet", (3, 224, 224), 1000, 1281167, 50000, "image"),
+    "cifar10": DatasetSpec("cifar10", (3, 32, 32), 10, 50000, 10000, "image"),
+    "mnist": DatasetSpec("mnist", (1, 28, 28), 10, 60000, 10000, "image"),
+    "mnist32": DatasetSpec("mnist32", (1, 32, 32), 10, 60000, 10000, "image"),
+    "ptb": DatasetSpec("ptb", (35,), 10000, 929589, 82430, "tokens"),
+    "wikipedia": DatasetSpec("wikipedia", (512,), 30522, 1000000, 10000, "mlm"),
+}
+
+
+class SyntheticData:
+    def __init__(self, dataset: str, batch_size: int, device="cpu", seed: int = 0, pool: int = 4,
+                 learnable: bool = False, seq_len: Optional[int] = None, channels_last: bool = False,
+                 dtype: torch.dtype = torch.float32, vocab_size: Optional[int] = None):
+        if dataset not in DATASETS:
+            raise ValueError("Unsupport dataset: %s" % dataset)
+        self.spec = DATASETS[dataset]
+        self.batch_size = int(batch_size)
+        self.device = torch.device(device)
+        self.learnable = learnable
+        self.seq_len = seq_len or (self.spec.shape[0] if self.spec.kind != "image" else None)
+        self.vocab = vocab_size or self.spec.num_classes
+        g = torch.Generator(device="cpu")
+        g.manual_seed(1234 + seed)
+        self._batches = []
+        proj = None
+        if learnable and self.spec.kind == "image":
+            feat = int(np.prod(self.spec.shape))
+            proj = torch.randn(feat, self.spec.num_classes, generator=g) / feat ** 0.5
+        for _ in range(max(1, pool)):
+            self._batches.append(self._make(g, proj, channels_last, dtype))
+        self._i = 0
+
+    def _make(self, g, proj, channels_last, dtype):
+        B = self.batch_size
+        s = self.spec
+        if s.kind == "image":
+            x = torch.randn((B,) + s.shape, generator=g)
+            if proj is not None:
+                y = (x.reshape(B, -1) @ proj).argmax(1)
+            else:
+                y = torch.randint(0, s.num_classes, (B,), generator=g)
+            x = x.to(self.device, dtype)
+            if channels_last and x.dim() == 4:
+                x = x.contiguous(memory_format=torch.channels_last)
+            return x, y.to(self.device)
+        if s.kind == "tokens":
+            T = self.seq_len
+            if self.learnable:
+                start = torch.randint(0, self.vocab, (1, B), generator=g)
+                steps = torch.arange(T + 1).unsqueeze(1)
+                seq = (start + steps) % self.vocab
+            else:
+                seq = torch.randint(0, self.vocab, (T + 1, B), generator=g)
+            return seq[:-1].to(self.device), seq[1:].to(self.device)
+        # masked LM
+        T = self.seq_len
+        ids = torch.randint(5, self.vocab, (B, T), generator=g)
+        labels = torch.full((B, T), -100, dtype=torch.int64)
+        mask = torch.rand((B, T), generator=g) < 0.15
+        labels[mask] = ids[mask]
+        ids = ids.clone()
+        ids[mask] = 4  # [MASK]
+        return ids.to(self.device), labels.to(self.device)
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        b = self._batches[self._i % len(self._batches)]
+        self._i += 1
+        return b
+
+    def get_batch(self):
+        return next(self)
+
+    def num_samples(self) -> int:
+        if self.spec.kind == "tokens":
+            return self.spec.train_samples // self.seq_len
+        return self.spec.train_samples
+
+    def test_batches(self, n: int = 2):
+        return [self._batches[i % len(self._batches)] for i in range(n)]
+
+
+class NpzDataset:
+    """Real data from ``<path>`` holding ``x`` and ``y`` arrays (numpy, no pickle)."""
+
+    def __init__(self, path: str, batch_size: int, device="cpu", rank: int = 0, world: int = 1, seed: int = 0):
+        d = np.load(path, allow_pickle=False)
+        self.x = torch.from_numpy(d["x"])
+        self.y = torch.from_numpy(d["y"]).long()
+        self.batch_size = batch_size
+        self.device = torch.device(device)
+        self.rank, self.world = rank, world
+        self.epoch = 0
+        self.seed = seed
+        self._order = None
+        self._pos = 0
+        self._reshuffle()
+
+    def _reshuffle(self):
+        g = torch.Generator()
+        g.manual_seed(self.seed + self.epoch)
+        perm = torch.randperm(self.x.shape[0], generator=g)
+        self._order = perm[self.rank::self.world]
+        self._pos = 0
+
+    def num_samples(self) -> int:
+        return int(self.x.shape[0])
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        if self._pos + self.batch_size > self._order.numel():
+            self.epoch += 1
+            self._reshuffle()
+        idx = self._order[self._pos:self._pos + self.batch_size]
+        self._pos += self.batch_size
+        return self.x[idx].to(self.device, non_blocking=True), self.y[idx].to(self.device, non_blocking=True)
+
+
+def make_data(dataset: str, batch_size: int, device="cpu", **kw) -> SyntheticData:
+    return SyntheticData(dataset, batch_size, device, **kw)

@@ -1,0 +1,112 @@
+"""BERT-base masked-language model (BASELINE config 5; not in the reference).
+
+Standard BERT-base: vocab 30522, hidden 768, 12 layers, 12 heads, FFN 3072,
+512 positions, GELU, post-LN, MLM head tied to the word embeddings
+(~110M parameters).  Attention uses ``F.scaled_dot_product_attention`` (the
+ROCm flash-attention path); run under bf16 autocast.  Gradients stay fp32 in
+the flat arena, so compression is unaffected by the compute dtype.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+@dataclass
+class BertConfig:
+    vocab_size: int = 30522
+    hidden: int = 768
+    layers: int = 12
+    heads: int = 12
+    intermediate: int = 3072
+    max_position: int = 512
+    type_vocab: int = 2
+    dropout: float = 0.1
+    ln_eps: float = 1e-12
+
+
+class BertLayer(nn.Module):
+    def __init__(self, c: BertConfig):
+        super().__init__()
+        self.heads = c.heads
+        self.qkv = nn.Linear(c.hidden, 3 * c.hidden)
+        self.attn_out = nn.Linear(c.hidden, c.hidden)
+        self.ln1 = nn.LayerNorm(c.hidden, eps=c.ln_eps)
+        self.ffn_in = nn.Linear(c.hidden, c.intermediate)
+        self.ffn_out = nn.Linear(c.intermediate, c.hidden)
+        self.ln2 = nn.LayerNorm(c.hidden, eps=c.ln_eps)
+        self.drop = nn.Dropout(c.dropout)
+        self.p = c.dropout
+
+    def forward(self, x, attn_mask=None):
+        B, T, H = x.shape
+        qkv = self.qkv(x).view(B, T, 3, self.heads, H // self.heads).permute(2, 0, 3, 1, 4)
+        q, k, v = qkv[0], qkv[1], qkv[2]
+        a = F.scaled_dot_product_attention(q, k, v, attn_mask=attn_mask, dropout_p=self.p if self.training else 0.0)
+        a = a.transpose(1, 2).reshape(B, T, H)
+        x = self.ln1(x + self.drop(self.attn_out(a)))
+        h = self.ffn_out(F.gelu(self.ffn_in(x)))
+        return self.ln2(x + self.drop(h))
+
+
+class BertForMaskedLM(nn.Module):
+    def __init__(self, c: BertConfig = None):
+        super().__init__()
+        c = c or BertConfig()
+        self.config = c
+        self.word_embeddings = nn.Embedding(c.vocab_size, c.hidden)
+        self.position_embeddings = nn.Embedding(c.max_position, c.hidden)
+        self.token_type_embeddings = nn.Embedding(c.type_vocab, c.hidden)
+        self.emb_ln = nn.LayerNorm(c.hidden, eps=c.ln_eps)
+        self.emb_drop = nn.Dropout(c.dropout)
+        self.encoder = nn.ModuleList([BertLayer(c) for _ in range(c.layers)])
+        self.mlm_dense = nn.Linear(c.hidden, c.hidden)
+        self.mlm_ln = nn.LayerNorm(c.hidden, eps=c.ln_eps)
+        self.mlm_bias = nn.Parameter(torch.zeros(c.vocab_size))
+        self.name = "bert"
+        self.apply(self._init)
+
+    @staticmethod
+    def _init(m):
+        if isinstance(m, (nn.Linear, nn.Embedding)):
+            nn.init.normal_(m.weight, mean=0.0, std=0.02)
+        if isinstance(m, nn.Linear) and m.bias is not None:
+            nn.init.zeros_(m.bias)
+        if isinstance(m, nn.LayerNorm):
+            nn.init.ones_(m.weight)
+            nn.init.zeros_(m.bias)
+
+    def forward(self, input_ids, token_type_ids=None, attention_mask=None):
+        B, T = input_ids.shape
+        pos = torch.arange(T, device=input_ids.device).unsqueeze(0)
+        tt = token_type_ids if token_type_ids is not None else torch.zeros_like(input_ids)
+        x = self.word_embeddings(input_ids) + self.position_embeddings(pos) + self.token_type_embeddings(tt)
+        x = self.emb_drop(self.emb_ln(x))
+        mask = None
+        if attention_mask is not None:
+            mask = attention_mask[:, None, None, :].to(torch.bool)
+        for layer in self.encoder:
+            x = layer(x, mask)
+        h = self.mlm_ln(F.gelu(self.mlm_dense(x)))
+        return F.linear(h, self.word_embeddings.weight, self.mlm_bias)
+
+
+class MaskedLMLoss(nn.Module):
+    """Cross entropy over masked positions (labels == -100 ignored)."""
+
+    def forward(self, logits, labels):
+        return F.cross_entropy(logits.reshape(-1, logits.shape[-1]).float(), labels.reshape(-1), ignore_index=-100)
+
+
+def bert_base(**kw):
+    return BertForMaskedLM(BertConfig(**kw))
+
+
+def bert_tiny(**kw):
+    d = dict(vocab_size=1024, hidden=64, layers=2, heads=2, intermediate=128, max_position=128)
+    d.update(kw)
+    return BertForMaskedLM(BertConfig(**d))

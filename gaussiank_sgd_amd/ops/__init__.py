@@ -1,0 +1,536 @@
+"""Python front-end of the gfx950 kernel library (``gaussiank_sgd_amd/_C.so``).
+
+Dispatch rule: GPU tensors ALWAYS go to the HIP kernels; if the extension is
+missing on a GPU box the call raises (no silent eager fallback).  CPU tensors
+run a pure-torch mirror of the same pipeline with identical semantics -- this
+is what the gloo/CPU tests exercise and what the GPU numerics tests compare
+against.
+
+Packed record layout (one per rank and bucket, int32 words)::
+
+    [0] sent  [1] total  [2] chosen candidate  [3] threshold (fp32 bits)
+    [4 : 4+k_cap]            int32 indices (ascending)
+    [4+k_cap : 4+2*k_cap]    fp32 values (bit-cast)
+"""
+from __future__ import annotations
+
+import os
+import threading
+from pathlib import Path
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+_LIB = Path(__file__).resolve().parents[1] / "_C.so"
+_lock = threading.Lock()
+_loaded = False
+_load_error: Optional[BaseException] = None
+
+MODE_GAUSSIAN = 0
+MODE_REDSYNC = 1
+MODE_REDSYNCTRIM = 2
+MODE_TOPK = 3
+MODE_RANDOMK = 4
+MODE_THRESHOLD = 5
+MODE_DGC = 6
+
+MAX_CAND = 16
+CHUNK_ELEMS = 16384
+REC_HDR = 4
+
+
+def load(build_if_missing: bool = False) -> bool:
+    """Load the native extension once.  Returns True when available."""
+    global _loaded, _load_error
+    if _loaded:
+        return True
+    with _lock:
+        if _loaded:
+            return True
+        try:
+            if not _LIB.exists() and build_if_missing:
+                from . import build as _b
+                _b.build()
+            torch.ops.load_library(str(_LIB))
+            _loaded = True
+        except BaseException as e:  # noqa: BLE001
+            _load_error = e
+    return _loaded
+
+
+def native_available() -> bool:
+    return load()
+
+
+def library_path() -> str:
+    return str(_LIB)
+
+
+def require_native(t: torch.Tensor) -> None:
+    if t.is_cuda and not load():
+        raise RuntimeError(
+            "gaussiank_sgd_amd native extension (%s) is not loadable on a GPU device: %r. "
+            "Build it with `python -m gaussiank_sgd_amd.ops.build`." % (_LIB, _load_error))
+
+
+def _ops():
+    return torch.ops.gksgd
+
+
+# ---------------------------------------------------------------------------
+# per-bucket device buffers
+# ---------------------------------------------------------------------------
+class CompressBuffers:
+    """ctrl block + workspace + packed send record for one bucket."""
+
+    def __init__(self, k_cap: int, device: torch.device):
+        device = torch.device(device)
+        self.k_cap = int(k_cap)
+        self.device = device
+        if device.type == "cuda":
+            require_native(torch.empty(0, device=device))
+            ctrl_b = int(_ops().ctrl_bytes())
+            ws_b = int(_ops().workspace_bytes())
+        else:
+            ctrl_b, ws_b = 512, 256
+        # 256-byte alignment: the caching allocator returns >=512-byte aligned blocks
+        self.ctrl = torch.zeros((ctrl_b + 7) // 8, dtype=torch.float64, device=device)
+        self.ws = torch.zeros((ws_b + 255) // 256 * 64, dtype=torch.float32, device=device)
+        self.record = torch.zeros(REC_HDR + 2 * self.k_cap, dtype=torch.int32, device=device)
+        self.stats = torch.zeros(4, dtype=torch.float32, device=device)
+
+    def header(self) -> torch.Tensor:
+        return self.record[:REC_HDR]
+
+    def indices(self) -> torch.Tensor:
+        return self.record[REC_HDR:REC_HDR + self.k_cap]
+
+    def values(self) -> torch.Tensor:
+        return self.record[REC_HDR + self.k_cap:].view(torch.float32)
+
+
+def record_views(rec: torch.Tensor, k_cap: int) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    return rec[..., :REC_HDR], rec[..., REC_HDR:REC_HDR + k_cap], rec[..., REC_HDR + k_cap:].view(torch.float32)
+
+
+# ---------------------------------------------------------------------------
+# CPU mirror helpers
+# ---------------------------------------------------------------------------
+_M32 = 0xFFFFFFFF
+
+
+def hash_u32(idx: torch.Tensor, seed: int) -> torch.Tensor:
+    """Bit-exact mirror of gk::hash_u32 (murmur3 fmix32 of a Weyl sequence)."""
+    i = idx.to(torch.int64) & _M32
+    h = (i * 0x9E3779B1 + ((seed & _M32) * 0x85EBCA77 & _M32) + 0x27D4EB2F) & _M32
+    h = h ^ (h >> 16)
+    h = (h * 0x85EBCA6B) & _M32
+    h = h ^ (h >> 13)
+    h = (h * 0xC2B2AE35) & _M32
+    h = h ^ (h >> 16)
+    return h
+
+
+def abs_key(x: torch.Tensor) -> torch.Tensor:
+    return x.contiguous().view(torch.int32).to(torch.int64) & 0x7FFFFFFF
+
+
+def _bound_from_threshold(t: float) -> int:
+    import struct
+    tf = struct.unpack("f", struct.pack("f", t))[0] if t == t and abs(t) < 3.5e38 else t
+    if not (tf >= 0.0):
+        if tf < 0.0:
+            return 0
+        return 0x7FC00001
+    if tf == float("inf"):
+        return 0x7F800001
+    bits = struct.unpack("I", struct.pack("f", tf))[0] & 0x7FFFFFFF
+    return bits + 1
+
+
+def _f32(x: float) -> float:
+    import struct
+    if x != x or abs(x) == float("inf"):
+        return x
+    if abs(x) >= 3.4028235677973366e38:
+        return float("inf") if x > 0 else float("-inf")
+    return struct.unpack("f", struct.pack("f", x))[0]
+
+
+def _candidates(mode: int, loops: int, z: float, fixed_thr: float, stats: Tuple[float, float, float, float]):
+    """Candidate thresholds (|x| units) and key bounds, mirroring finalize_kernel."""
+    mean, std, meanabs, maxabs = stats
+    thr: List[float] = []
+    if mode == MODE_GAUSSIAN:
+        t0 = mean + z * std
+        for s in range(loops):
+            for b in range(s + 1):
+                a = s - b
+                t = t0
+                for _ in range(b):
+                    t *= 1.5
+                for _ in range(a):
+                    t *= 0.5
+                thr.append(_f32(t))
+    elif mode in (MODE_REDSYNC, MODE_REDSYNCTRIM):
+        mv = torch.tensor(meanabs, dtype=torch.float32)
+        Mv = torch.tensor(maxabs, dtype=torch.float32)
+        diff = Mv - mv
+        if mode == MODE_REDSYNC:
+            lo = [0.0] * 7
+            hi = [0.0] * 7
+            lo[0], hi[0] = 0.0, 1.0
+            for i in range(7):
+                mid = lo[i] + (hi[i] - lo[i]) / 2
+                t = mv + torch.tensor(mid, dtype=torch.float32) * diff
+                thr.append(float(t))
+                if 2 * i + 2 < 7:
+                    lo[2 * i + 1], hi[2 * i + 1] = lo[i], mid
+                    lo[2 * i + 2], hi[2 * i + 2] = mid, hi[i]
+        else:
+            ratio = 1.0 - 0.2
+            for _ in range(MAX_CAND):
+                t = mv + torch.tensor(ratio, dtype=torch.float32) * diff
+                thr.append(float(t))
+                ratio = ratio - 0.2
+    elif mode == MODE_THRESHOLD:
+        thr.append(_f32(fixed_thr))
+    return thr
+
+
+def _decide(mode: int, loops: int, k: int, counts: Sequence[int]) -> int:
+    if mode == MODE_GAUSSIAN:
+        a = b = 0
+        for loop in range(loops):
+            c = counts[(a + b) * (a + b + 1) // 2 + b]
+            if loop == loops - 1:
+                break
+            if c < 2 * k / 3:
+                a += 1
+            elif c > 4 * k / 3:
+                b += 1
+            else:
+                break
+        return (a + b) * (a + b + 1) // 2 + b
+    if mode == MODE_REDSYNC:
+        node = 0
+        for depth in range(3):
+            c = counts[node]
+            if c > k and 2 * k > c:
+                break
+            if depth == 2:
+                break
+            node = 2 * node + 1 if c < k / 2 else 2 * node + 2
+        return node
+    if mode == MODE_REDSYNCTRIM:
+        for j, c in enumerate(counts):
+            if c >= k:
+                return j
+        return len(counts) - 1
+    return 0
+
+
+def _radix_topk_mask(keys: torch.Tensor, eligible: torch.Tensor, k: int) -> Tuple[torch.Tensor, int, int]:
+    """Exact top-k by key with ties broken by lowest index (mirror of radix path).
+
+    Returns (mask, K, quota): mask selects key > K plus the first `quota`
+    elements with key == K in index order.
+    """
+    ek = keys[eligible]
+    keff = min(int(k), int(ek.numel()))
+    if keff <= 0:
+        return torch.zeros_like(keys, dtype=torch.bool), 0, 0
+    K = int(torch.topk(ek, keff).values[-1])
+    gt = eligible & (keys > K)
+    eq = eligible & (keys == K)
+    quota = keff - int(gt.sum())
+    eq_idx = torch.nonzero(eq).view(-1)[:quota]
+    mask = gt.clone()
+    mask[eq_idx] = True
+    return mask, K, quota
+
+
+def compress_cpu_(g: torch.Tensor, r: torch.Tensor, bufs: CompressBuffers, mode: int, ec: bool, zero_g: bool,
+                  loops: int, z: float, k: int, k_cap: int, seed: int = 0, fixed_thr: float = 0.0,
+                  sample_p: float = 0.01, n_stats: int = 0) -> None:
+    """Pure-torch mirror of gk::compress (same record layout and semantics)."""
+    with torch.no_grad():
+        acc = g + r if ec else g.clone()
+        r.copy_(acc)
+        if zero_g:
+            g.zero_()
+        n = acc.numel()
+        nst = int(n_stats) if n_stats and n_stats > 0 else n
+        a64 = acc.double()
+        s = float(a64.sum())
+        ss = float((a64 * a64).sum())
+        mean = s / nst
+        var = (ss - s * s / nst) / (nst - 1) if nst > 1 else float("nan")
+        std = max(var, 0.0) ** 0.5 if var == var else float("nan")
+        absacc = acc.abs()
+        meanabs = float(absacc.double().sum()) / nst
+        maxabs = float(absacc.max()) if n else 0.0
+        stats = (mean, std, meanabs, maxabs)
+        bufs.stats.copy_(torch.tensor(stats, dtype=torch.float32))
+        k = max(int(k), 1)
+        if mode in (MODE_GAUSSIAN, MODE_REDSYNC, MODE_REDSYNCTRIM, MODE_THRESHOLD):
+            thr = _candidates(mode, loops, z, fixed_thr, stats)
+            keys = abs_key(acc)
+            bounds = [_bound_from_threshold(t) for t in thr]
+            counts = [int((keys >= b).sum()) for b in bounds]
+            chosen = _decide(mode, loops, k, counts)
+            mask = keys >= bounds[chosen]
+            thr_chosen = thr[chosen]
+        elif mode in (MODE_TOPK, MODE_RANDOMK):
+            idx = torch.arange(n, dtype=torch.int64)
+            if mode == MODE_RANDOMK:
+                keys = hash_u32(idx, seed)
+                keys = torch.where(keys == 0xFFFFFFFF, torch.full_like(keys, 0xFFFFFFFE), keys)
+            else:
+                keys = abs_key(acc)
+            mask, K, _ = _radix_topk_mask(keys, torch.ones(n, dtype=torch.bool), k)
+            chosen = 0
+            thr_chosen = float(torch.tensor([K & 0x7FFFFFFF], dtype=torch.int32).view(torch.float32))
+        elif mode == MODE_DGC:
+            idx = torch.arange(n, dtype=torch.int64)
+            p = sample_p * 4294967296.0
+            sthr = 0xFFFFFFFF if p >= 4294967295.0 else int(p)
+            sampled = hash_u32(idx, seed) < sthr
+            keys = abs_key(acc)
+            skeys = torch.where(sampled, keys + 1, torch.zeros_like(keys))
+            smask, Ks, _ = _radix_topk_mask(skeys, sampled, k)
+            cand0 = keys >= Ks
+            if int(cand0.sum()) > 4 * k / 3:
+                mask, K, _ = _radix_topk_mask(keys, torch.ones(n, dtype=torch.bool), k)
+                chosen = 1
+                thr_chosen = float(torch.tensor([K], dtype=torch.int32).view(torch.float32))
+            else:
+                mask = cand0
+                chosen = 0
+                thr_chosen = float(torch.tensor([max(Ks - 1, 0)], dtype=torch.int32).view(torch.float32))
+        else:
+            raise ValueError("bad mode %d" % mode)
+        sel = torch.nonzero(mask).view(-1)
+        total = int(sel.numel())
+        sent = min(total, k_cap)
+        sel = sel[:sent]
+        rec = bufs.record
+        rec.zero_()
+        rec[0] = sent
+        rec[1] = min(total, 0x7FFFFFFF)
+        rec[2] = chosen
+        rec[3] = torch.tensor([thr_chosen], dtype=torch.float32).view(torch.int32)[0]
+        rec[REC_HDR:REC_HDR + sent] = sel.to(torch.int32)
+        rec[REC_HDR + k_cap:REC_HDR + k_cap + sent] = acc[sel].view(torch.int32)
+        r[sel] = 0.0
+
+
+def compress_(g: torch.Tensor, r: torch.Tensor, bufs: CompressBuffers, mode: int, ec: bool = True,
+              zero_g: bool = True, loops: int = 3, z: float = 0.0, k: int = 1, k_cap: Optional[int] = None,
+              seed: int = 0, fixed_thr: float = 0.0, sample_p: float = 0.01, n_stats: int = 0) -> None:
+    """Sparsify ``g`` (+ residual ``r``) into ``bufs.record``.  Async on GPU.
+
+    ``n_stats``: element count used for mean/std (the real, unpadded bucket
+    size; padding elements are zeros and do not change the sums).
+    """
+    k_cap = bufs.k_cap if k_cap is None else int(k_cap)
+    if g.is_cuda:
+        require_native(g)
+        _ops().compress(g, r, bufs.ctrl, bufs.ws, bufs.record, int(mode), bool(ec), bool(zero_g), int(loops),
+                        float(z), float(fixed_thr), float(sample_p), int(k), int(k_cap), int(seed) & 0xFFFFFFFF,
+                        int(n_stats), bufs.stats)
+    else:
+        compress_cpu_(g, r, bufs, mode, ec, zero_g, loops, z, k, k_cap, seed, fixed_thr, sample_p, n_stats)
+
+
+def ctrl_fields(bufs: CompressBuffers) -> dict:
+    """Decode the GkCtrl block (host sync; tests/diagnostics only)."""
+    raw = bufs.ctrl.detach().cpu()
+    d = raw.numpy().view("float64")
+    out = {"sum": d[0], "sumsq": d[1], "sumabs": d[2], "maxabs_raw": d[3], "mean": d[4], "std": d[5],
+           "meanabs": d[6], "maxabs": d[7]}
+    u32 = raw.numpy().view("uint32")
+    out["bounds"] = [int(x) for x in u32[16:16 + MAX_CAND]]
+    out["ncand"] = int(raw.numpy().view("int32")[16 + MAX_CAND])
+    out["chosen"] = int(raw.numpy().view("int32")[17 + MAX_CAND])
+    return out
+
+
+# ---------------------------------------------------------------------------
+# aggregation
+# ---------------------------------------------------------------------------
+def scatter_add_records_(dst: torch.Tensor, records: torch.Tensor, P: int, k_cap: int, scale: float,
+                         deterministic: bool = False) -> None:
+    """dst[idx_r] += val_r * scale for every rank r (records [P, 4+2k_cap])."""
+    if dst.is_cuda:
+        require_native(dst)
+        _ops().scatter_add_records(dst, records.contiguous(), int(P), int(k_cap), float(scale), bool(deterministic))
+        return
+    rec = records.view(P, REC_HDR + 2 * k_cap)
+    for r in range(P):
+        cnt = int(rec[r, 0])
+        idx = rec[r, REC_HDR:REC_HDR + cnt].long()
+        val = rec[r, REC_HDR + k_cap:REC_HDR + k_cap + cnt].view(torch.float32)
+        dst.index_add_(0, idx, val * scale)
+
+
+def fill_zero_(dst: torch.Tensor) -> None:
+    if dst.is_cuda:
+        require_native(dst)
+        _ops().fill_zero(dst)
+    else:
+        dst.zero_()
+
+
+# ---------------------------------------------------------------------------
+# sign-bucket compressor
+# ---------------------------------------------------------------------------
+def sign_bucket_compress_(x: torch.Tensor, mask: torch.Tensor, means: torch.Tensor, ws: Optional[torch.Tensor]) -> None:
+    if x.is_cuda:
+        require_native(x)
+        _ops().sign_bucket_compress(x, mask, means, ws)
+        return
+    pos = x >= 0
+    mask.copy_(pos.to(torch.uint8))
+    mp = x[pos].mean() if bool(pos.any()) else torch.zeros((), dtype=x.dtype)
+    mn = x[~pos].mean() if bool((~pos).any()) else torch.zeros((), dtype=x.dtype)
+    means[0] = mp
+    means[1] = mn
+    x.sub_(torch.where(pos, means[0], means[1]))
+
+
+def sign_bucket_decompress_(x: torch.Tensor, mask: torch.Tensor, means: torch.Tensor) -> None:
+    if x.is_cuda:
+        require_native(x)
+        _ops().sign_bucket_decompress(x, mask, means)
+        return
+    x.add_(torch.where(mask.bool(), means[0], means[1]))
+
+
+def sign_bucket_ws(device) -> Optional[torch.Tensor]:
+    device = torch.device(device)
+    if device.type != "cuda":
+        return None
+    require_native(torch.empty(0, device=device))
+    nb = int(_ops().sign_bucket_workspace_bytes())
+    return torch.zeros((nb + 7) // 8, dtype=torch.float64, device=device)
+
+
+# ---------------------------------------------------------------------------
+# fused optimizers
+# ---------------------------------------------------------------------------
+def make_chunk_table(segments: Sequence[Tuple[int, int, int, int]], device) -> torch.Tensor:
+    """segments: (start, numel, group, seg_id) -> int64[nchunks*2] chunk table."""
+    words: List[int] = []
+    for start, numel, group, seg in segments:
+        off = 0
+        while off < numel:
+            ln = min(CHUNK_ELEMS, numel - off)
+            words.append(start + off)
+            words.append((ln & 0xFFFFFFFF) | ((group & 0xFFFF) << 32) | ((seg & 0x7FFF) << 48))
+            off += ln
+    return torch.tensor(words, dtype=torch.int64, device=device)
+
+
+def _decode_chunks(chunks: torch.Tensor):
+    c = chunks.view(-1, 2).cpu()
+    out = []
+    for start, w in c.tolist():
+        out.append((start, w & 0xFFFFFFFF, (w >> 32) & 0xFFFF, (w >> 48) & 0x7FFF))
+    return out
+
+
+def fused_sgd_(w: torch.Tensor, m: Optional[torch.Tensor], g: torch.Tensor, chunks: torch.Tensor,
+               groups: Sequence[dict], zero_grad: bool = True, grad_scale: Optional[torch.Tensor] = None) -> None:
+    """groups: dicts with lr, momentum, dampening, weight_decay, nesterov, first_step."""
+    if w.is_cuda:
+        require_native(w)
+        _ops().fused_sgd(w, m, g, chunks, [float(p["lr"]) for p in groups], [float(p["momentum"]) for p in groups],
+                         [float(p.get("dampening", 0.0)) for p in groups],
+                         [float(p.get("weight_decay", 0.0)) for p in groups],
+                         [int(bool(p.get("nesterov", False))) for p in groups],
+                         [int(bool(p.get("first_step", False))) for p in groups], bool(zero_grad), grad_scale)
+        return
+    gs = float(grad_scale) if grad_scale is not None else 1.0
+    for start, ln, gi, _ in _decode_chunks(chunks):
+        p = groups[gi]
+        ws = w[start:start + ln]
+        d = g[start:start + ln] * gs
+        wd = float(p.get("weight_decay", 0.0))
+        if wd != 0:
+            d = d + wd * ws
+        mom = float(p["momentum"])
+        if mom != 0:
+            ms = m[start:start + ln]
+            if p.get("first_step", False):
+                ms.copy_(d)
+            else:
+                ms.mul_(mom).add_(d, alpha=1 - float(p.get("dampening", 0.0)))
+            d = d + mom * ms if p.get("nesterov", False) else ms
+        ws.add_(d, alpha=-float(p["lr"]))
+        if zero_grad:
+            g[start:start + ln].zero_()
+
+
+def segmented_sumsq_(w: torch.Tensor, g: torch.Tensor, chunks: torch.Tensor, out: torch.Tensor) -> None:
+    if w.is_cuda:
+        require_native(w)
+        _ops().segmented_sumsq(w, g, chunks, out)
+        return
+    for start, ln, _, seg in _decode_chunks(chunks):
+        out[2 * seg] += float((w[start:start + ln].double() ** 2).sum())
+        out[2 * seg + 1] += float((g[start:start + ln].double() ** 2).sum())
+
+
+def fused_lars_(w: torch.Tensor, m: torch.Tensor, g: torch.Tensor, chunks: torch.Tensor, seg_sumsq: torch.Tensor,
+                groups: Sequence[dict]) -> None:
+    if w.is_cuda:
+        require_native(w)
+        _ops().fused_lars(w, m, g, chunks, seg_sumsq, [float(p["lr"]) for p in groups],
+                          [float(p["momentum"]) for p in groups], [float(p["weight_decay"]) for p in groups],
+                          [float(p["eeta"]) for p in groups], [float(p["epsilon"]) for p in groups])
+        return
+    for start, ln, gi, seg in _decode_chunks(chunks):
+        p = groups[gi]
+        wn = float(seg_sumsq[2 * seg]) ** 0.5
+        gn = float(seg_sumsq[2 * seg + 1]) ** 0.5
+        trust = 1.0
+        if wn > 0 and gn > 0:
+            trust = p["eeta"] * wn / (gn + p["weight_decay"] * wn + p["epsilon"])
+        trust = min(max(trust, 0.0), 50.0)
+        ws = w[start:start + ln]
+        d = (g[start:start + ln] + p["weight_decay"] * ws).clamp_(-10.0, 10.0)
+        ms = m[start:start + ln]
+        ms.mul_(p["momentum"]).add_(d, alpha=p["lr"] * trust)
+        ws.sub_(ms)
+
+
+def clip_grad_norm_(g: torch.Tensor, max_norm: float, ws: Optional[torch.Tensor] = None,
+                    coef: Optional[torch.Tensor] = None, norm: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Global-norm clip of a flat gradient arena, no host sync on GPU.  Returns the norm tensor."""
+    if norm is None:
+        norm = torch.zeros(1, dtype=torch.float32, device=g.device)
+    if coef is None:
+        coef = torch.zeros(1, dtype=torch.float32, device=g.device)
+    if g.is_cuda:
+        require_native(g)
+        if ws is None:
+            ws = torch.zeros(1024, dtype=torch.float64, device=g.device)
+        _ops().clip_grad_norm(g, float(max_norm), ws, coef, norm)
+        return norm
+    nrm = float(g.double().norm())
+    c = min(1.0, max_norm / (nrm + 1e-6))
+    norm.fill_(nrm)
+    coef.fill_(c)
+    if c < 1.0:
+        g.mul_(c)
+    return norm
+
+
+# ---------------------------------------------------------------------------
+# RCCL engine
+# ---------------------------------------------------------------------------
+def rccl_engine_class():
+    if not load():
+        raise RuntimeError("native extension unavailable: %r" % (_load_error,))
+    return torch.classes.gksgd.RcclEngine

@@ -1,0 +1,358 @@
+// Torch op registrations for the gfx950 kernel library and the RCCL engine.
+//
+// Ops are registered under the `gksgd` namespace (torch.ops.gksgd.*) and run
+// asynchronously on the current HIP stream of the tensors' device.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/custom_class.h>
+#include <torch/library.h>
+
+#include <cstring>
+#include <vector>
+
+#include "comm/rccl_engine.h"
+#include "kernels/gk_kernels.h"
+
+namespace {
+
+hipStream_t cur_stream(const at::Tensor& t) {
+  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+void check_dev(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+void check_f32(const at::Tensor& t, const char* name) {
+  check_dev(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kFloat, name, " must be float32");
+}
+
+// ---------------------------------------------------------------------------
+// compressor pipeline
+// ---------------------------------------------------------------------------
+int64_t ctrl_bytes() { return (int64_t)sizeof(gk::GkCtrl); }
+int64_t workspace_bytes() { return (int64_t)gk::compress_workspace_bytes(0); }
+
+void compress(at::Tensor g, at::Tensor r, at::Tensor ctrl, at::Tensor ws, at::Tensor record, int64_t mode, bool ec,
+              bool zero_g, int64_t loops, double z, double fixed_thr, double sample_p, int64_t k, int64_t k_cap,
+              int64_t seed, int64_t n_stats, c10::optional<at::Tensor> stats_out) {
+  check_f32(g, "g");
+  check_f32(r, "r");
+  check_dev(ctrl, "ctrl");
+  check_dev(ws, "ws");
+  check_dev(record, "record");
+  TORCH_CHECK(g.numel() == r.numel(), "g and r must have the same numel");
+  TORCH_CHECK(ctrl.nbytes() >= sizeof(gk::GkCtrl), "ctrl buffer too small");
+  TORCH_CHECK(ws.nbytes() >= gk::compress_workspace_bytes(g.numel()), "workspace too small");
+  TORCH_CHECK(record.scalar_type() == at::kInt, "record must be int32");
+  TORCH_CHECK(k_cap >= 1 && record.numel() >= 4 + 2 * k_cap, "record must hold 4 + 2*k_cap int32");
+  TORCH_CHECK(g.numel() < (int64_t)0x7fffffff, "bucket too large for int32 indices");
+  TORCH_CHECK(mode >= 0 && mode <= 6, "bad mode");
+  TORCH_CHECK(loops >= 1 && loops * (loops + 1) / 2 <= gk::kMaxCand, "loops out of range");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(ctrl.data_ptr()) & 7) == 0, "ctrl must be 8-byte aligned");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(ws.data_ptr()) & 255) == 0, "ws must be 256-byte aligned");
+  c10::hip::HIPGuard guard(g.device());
+  gk::CompressArgs a;
+  a.g = g.data_ptr<float>();
+  a.r = r.data_ptr<float>();
+  a.n = g.numel();
+  a.n_stats = n_stats;
+  a.mode = (int)mode;
+  a.ec = ec ? 1 : 0;
+  a.zero_g = zero_g ? 1 : 0;
+  a.loops = (int)loops;
+  a.z = z;
+  a.fixed_thr = fixed_thr;
+  a.sample_p = sample_p;
+  a.k = k < 1 ? 1 : k;
+  a.k_cap = k_cap;
+  a.seed = (uint32_t)(seed & 0xffffffff);
+  a.ctrl = ctrl.data_ptr();
+  a.ws = ws.data_ptr();
+  a.record = record.data_ptr<int32_t>();
+  a.stats_out = nullptr;
+  if (stats_out.has_value()) {
+    check_f32(*stats_out, "stats_out");
+    TORCH_CHECK(stats_out->numel() >= 4, "stats_out needs 4 floats");
+    a.stats_out = stats_out->data_ptr<float>();
+  }
+  gk::compress(a, cur_stream(g));
+}
+
+void tensor_stats(at::Tensor x, at::Tensor ctrl, at::Tensor ws) {
+  check_f32(x, "x");
+  check_dev(ctrl, "ctrl");
+  check_dev(ws, "ws");
+  TORCH_CHECK(ctrl.nbytes() >= sizeof(gk::GkCtrl), "ctrl buffer too small");
+  c10::hip::HIPGuard guard(x.device());
+  gk::tensor_stats(x.data_ptr<float>(), x.numel(), ctrl.data_ptr(), ws.data_ptr(), cur_stream(x));
+}
+
+// ---------------------------------------------------------------------------
+// aggregation / bucket compressor
+// ---------------------------------------------------------------------------
+void scatter_add_records(at::Tensor dst, at::Tensor records, int64_t P, int64_t k_cap, double scale,
+                         bool deterministic) {
+  check_f32(dst, "dst");
+  check_dev(records, "records");
+  TORCH_CHECK(records.scalar_type() == at::kInt, "records must be int32");
+  TORCH_CHECK(records.numel() >= P * (4 + 2 * k_cap), "records too small for P x (4 + 2 k_cap)");
+  c10::hip::HIPGuard guard(dst.device());
+  gk::scatter_add_records(dst.data_ptr<float>(), dst.numel(), records.data_ptr<int32_t>(), (int)P, k_cap,
+                          (float)scale, deterministic ? 1 : 0, cur_stream(dst));
+}
+
+void fill_zero(at::Tensor dst) {
+  check_f32(dst, "dst");
+  c10::hip::HIPGuard guard(dst.device());
+  gk::fill_zero(dst.data_ptr<float>(), dst.numel(), cur_stream(dst));
+}
+
+int64_t sign_bucket_workspace_bytes() { return (int64_t)gk::sign_bucket_workspace_bytes(0); }
+
+void sign_bucket_compress(at::Tensor x, at::Tensor mask, at::Tensor means, at::Tensor ws) {
+  check_f32(x, "x");
+  check_dev(mask, "mask");
+  check_f32(means, "means");
+  check_dev(ws, "ws");
+  TORCH_CHECK(mask.scalar_type() == at::kByte && mask.numel() >= x.numel(), "mask must be uint8[n]");
+  TORCH_CHECK(means.numel() >= 2, "means needs 2 floats");
+  c10::hip::HIPGuard guard(x.device());
+  gk::sign_bucket_compress(x.data_ptr<float>(), x.numel(), mask.data_ptr<uint8_t>(), means.data_ptr<float>(),
+                           ws.data_ptr(), cur_stream(x));
+}
+
+void sign_bucket_decompress(at::Tensor x, at::Tensor mask, at::Tensor means) {
+  check_f32(x, "x");
+  check_dev(mask, "mask");
+  check_f32(means, "means");
+  c10::hip::HIPGuard guard(x.device());
+  gk::sign_bucket_decompress(x.data_ptr<float>(), x.numel(), mask.data_ptr<uint8_t>(), means.data_ptr<float>(),
+                             cur_stream(x));
+}
+
+// ---------------------------------------------------------------------------
+// fused optimizers
+// ---------------------------------------------------------------------------
+void check_chunks(const at::Tensor& chunks) {
+  check_dev(chunks, "chunks");
+  TORCH_CHECK(chunks.scalar_type() == at::kLong && chunks.numel() % 2 == 0,
+              "chunks must be int64[nchunks*2] (start, len|group<<32|seg<<48)");
+}
+
+void fused_sgd(at::Tensor w, c10::optional<at::Tensor> m, at::Tensor g, at::Tensor chunks, std::vector<double> lr,
+               std::vector<double> momentum, std::vector<double> dampening, std::vector<double> weight_decay,
+               std::vector<int64_t> nesterov, std::vector<int64_t> first_step, bool zero_grad,
+               c10::optional<at::Tensor> grad_scale) {
+  check_f32(w, "w");
+  check_f32(g, "g");
+  check_chunks(chunks);
+  const size_t ng = lr.size();
+  TORCH_CHECK(ng >= 1 && ng <= (size_t)gk::kMaxGroups, "1..8 param groups supported");
+  TORCH_CHECK(momentum.size() == ng && dampening.size() == ng && weight_decay.size() == ng && nesterov.size() == ng &&
+                  first_step.size() == ng,
+              "hyper-parameter lists must have one entry per group");
+  TORCH_CHECK(w.numel() == g.numel(), "w/g size mismatch");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(w.data_ptr()) & 15) == 0 &&
+                  (reinterpret_cast<uintptr_t>(g.data_ptr()) & 15) == 0,
+              "arenas must be 16-byte aligned");
+  gk::SgdArgs a;
+  a.w = w.data_ptr<float>();
+  a.g = g.data_ptr<float>();
+  a.m = nullptr;
+  if (m.has_value() && m->defined()) {
+    check_f32(*m, "m");
+    TORCH_CHECK(m->numel() == w.numel(), "momentum arena size mismatch");
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(m->data_ptr()) & 15) == 0, "momentum arena must be 16-byte aligned");
+    a.m = m->data_ptr<float>();
+  }
+  for (size_t i = 0; i < ng; ++i) {
+    a.groups[i].lr = (float)lr[i];
+    a.groups[i].momentum = (float)momentum[i];
+    a.groups[i].dampening = (float)dampening[i];
+    a.groups[i].weight_decay = (float)weight_decay[i];
+    a.groups[i].nesterov = (int)nesterov[i];
+    a.groups[i].first_step = (int)first_step[i];
+    TORCH_CHECK(a.groups[i].momentum == 0.f || a.m != nullptr, "momentum arena required");
+  }
+  a.ngroups = (int)ng;
+  a.chunks = reinterpret_cast<const gk::Chunk*>(chunks.data_ptr<int64_t>());
+  a.nchunks = (int)(chunks.numel() / 2);
+  a.zero_grad = zero_grad ? 1 : 0;
+  a.grad_scale = nullptr;
+  if (grad_scale.has_value() && grad_scale->defined()) {
+    check_f32(*grad_scale, "grad_scale");
+    a.grad_scale = grad_scale->data_ptr<float>();
+  }
+  c10::hip::HIPGuard guard(w.device());
+  gk::fused_sgd(a, cur_stream(w));
+}
+
+void segmented_sumsq(at::Tensor w, at::Tensor g, at::Tensor chunks, at::Tensor out) {
+  check_f32(w, "w");
+  check_f32(g, "g");
+  check_chunks(chunks);
+  check_dev(out, "out");
+  TORCH_CHECK(out.scalar_type() == at::kDouble, "out must be float64[2*nseg]");
+  c10::hip::HIPGuard guard(w.device());
+  gk::segmented_sumsq(w.data_ptr<float>(), g.data_ptr<float>(),
+                      reinterpret_cast<const gk::Chunk*>(chunks.data_ptr<int64_t>()), (int)(chunks.numel() / 2),
+                      out.data_ptr<double>(), cur_stream(w));
+}
+
+void fused_lars(at::Tensor w, at::Tensor m, at::Tensor g, at::Tensor chunks, at::Tensor seg_sumsq,
+                std::vector<double> lr, std::vector<double> momentum, std::vector<double> weight_decay,
+                std::vector<double> eeta, std::vector<double> epsilon) {
+  check_f32(w, "w");
+  check_f32(m, "m");
+  check_f32(g, "g");
+  check_chunks(chunks);
+  check_dev(seg_sumsq, "seg_sumsq");
+  const size_t ng = lr.size();
+  TORCH_CHECK(ng >= 1 && ng <= (size_t)gk::kMaxGroups, "1..8 param groups supported");
+  gk::LarsArgs a;
+  a.w = w.data_ptr<float>();
+  a.m = m.data_ptr<float>();
+  a.g = g.data_ptr<float>();
+  a.chunks = reinterpret_cast<const gk::Chunk*>(chunks.data_ptr<int64_t>());
+  a.nchunks = (int)(chunks.numel() / 2);
+  a.seg_sumsq = seg_sumsq.data_ptr<double>();
+  for (size_t i = 0; i < ng; ++i) {
+    a.lr[i] = (float)lr[i];
+    a.momentum[i] = (float)momentum[i];
+    a.weight_decay[i] = (float)weight_decay[i];
+    a.eeta[i] = (float)eeta[i];
+    a.epsilon[i] = (float)epsilon[i];
+  }
+  a.ngroups = (int)ng;
+  c10::hip::HIPGuard guard(w.device());
+  gk::fused_lars(a, cur_stream(w));
+}
+
+void clip_grad_norm(at::Tensor g, double max_norm, at::Tensor ws, at::Tensor coef, at::Tensor norm) {
+  check_f32(g, "g");
+  check_dev(ws, "ws");
+  check_f32(coef, "coef");
+  check_f32(norm, "norm");
+  TORCH_CHECK(ws.scalar_type() == at::kDouble && ws.numel() >= 1024, "ws must be float64[>=1024]");
+  c10::hip::HIPGuard guard(g.device());
+  gk::clip_grad_norm(g.data_ptr<float>(), g.numel(), (float)max_norm, ws.data_ptr<double>(), coef.data_ptr<float>(),
+                     norm.data_ptr<float>(), cur_stream(g));
+}
+
+// ---------------------------------------------------------------------------
+// RCCL engine (torch custom class)
+// ---------------------------------------------------------------------------
+ncclDataType_t to_nccl(at::ScalarType t) {
+  switch (t) {
+    case at::kFloat: return ncclFloat32;
+    case at::kHalf: return ncclFloat16;
+    case at::kBFloat16: return ncclBfloat16;
+    case at::kDouble: return ncclFloat64;
+    case at::kInt: return ncclInt32;
+    case at::kLong: return ncclInt64;
+    case at::kByte: return ncclUint8;
+    default: TORCH_CHECK(false, "unsupported dtype for RCCL");
+  }
+  return ncclFloat32;
+}
+
+struct RcclEngine : torch::CustomClassHolder {
+  gk::RcclComm comm;
+
+  static at::Tensor unique_id() {
+    std::vector<uint8_t> id = gk::RcclComm::make_unique_id();
+    at::Tensor t = at::empty({(int64_t)id.size()}, at::TensorOptions().dtype(at::kByte));
+    std::memcpy(t.data_ptr<uint8_t>(), id.data(), id.size());
+    return t;
+  }
+
+  void init(at::Tensor uid, int64_t rank, int64_t world, int64_t device) {
+    TORCH_CHECK(!uid.is_cuda() && uid.scalar_type() == at::kByte, "uid must be a CPU uint8 tensor");
+    at::Tensor c = uid.contiguous();
+    std::vector<uint8_t> v(c.data_ptr<uint8_t>(), c.data_ptr<uint8_t>() + c.numel());
+    comm.init(v, (int)rank, (int)world, (int)device);
+  }
+
+  void allgather(at::Tensor send, at::Tensor recv) {
+    check_dev(send, "send");
+    check_dev(recv, "recv");
+    TORCH_CHECK(recv.nbytes() == send.nbytes() * (size_t)comm.world(), "recv must be world x send bytes");
+    c10::hip::HIPGuard guard(send.device());
+    comm.allgather_bytes(send.data_ptr(), recv.data_ptr(), send.nbytes(), cur_stream(send));
+  }
+
+  void allreduce(at::Tensor t, int64_t op) {
+    check_dev(t, "t");
+    c10::hip::HIPGuard guard(t.device());
+    ncclRedOp_t o = op == 0 ? ncclSum : (op == 1 ? ncclAvg : (op == 2 ? ncclMax : ncclMin));
+    comm.allreduce(t.data_ptr(), (size_t)t.numel(), to_nccl(t.scalar_type()), o, cur_stream(t));
+  }
+
+  void broadcast(at::Tensor t, int64_t root) {
+    check_dev(t, "t");
+    c10::hip::HIPGuard guard(t.device());
+    comm.broadcast(t.data_ptr(), (size_t)t.numel(), to_nccl(t.scalar_type()), (int)root, cur_stream(t));
+  }
+
+  void group_start() { comm.group_start(); }
+  void group_end() { comm.group_end(); }
+  void destroy() { comm.destroy(); }
+  int64_t rank() const { return comm.rank(); }
+  int64_t world() const { return comm.world(); }
+};
+
+}  // namespace
+
+TORCH_LIBRARY(gksgd, m) {
+  m.def("ctrl_bytes() -> int", &ctrl_bytes);
+  m.def("workspace_bytes() -> int", &workspace_bytes);
+  m.def(
+      "compress(Tensor(a!) g, Tensor(b!) r, Tensor(c!) ctrl, Tensor(d!) ws, Tensor(e!) record, int mode, bool ec, "
+      "bool zero_g, int loops, float z, float fixed_thr, float sample_p, int k, int k_cap, int seed, "
+      "int n_stats, Tensor(f!)? stats_out=None) -> ()");
+  m.def("tensor_stats(Tensor x, Tensor(a!) ctrl, Tensor(b!) ws) -> ()");
+  m.def("scatter_add_records(Tensor(a!) dst, Tensor records, int P, int k_cap, float scale, bool deterministic) -> ()");
+  m.def("fill_zero(Tensor(a!) dst) -> ()");
+  m.def("sign_bucket_workspace_bytes() -> int", &sign_bucket_workspace_bytes);
+  m.def("sign_bucket_compress(Tensor(a!) x, Tensor(b!) mask, Tensor(c!) means, Tensor(d!) ws) -> ()");
+  m.def("sign_bucket_decompress(Tensor(a!) x, Tensor mask, Tensor means) -> ()");
+  m.def(
+      "fused_sgd(Tensor(a!) w, Tensor(b!)? m, Tensor(c!) g, Tensor chunks, float[] lr, float[] momentum, "
+      "float[] dampening, float[] weight_decay, int[] nesterov, int[] first_step, bool zero_grad, "
+      "Tensor? grad_scale=None) -> ()");
+  m.def("segmented_sumsq(Tensor w, Tensor g, Tensor chunks, Tensor(a!) out) -> ()");
+  m.def(
+      "fused_lars(Tensor(a!) w, Tensor(b!) m, Tensor g, Tensor chunks, Tensor seg_sumsq, float[] lr, "
+      "float[] momentum, float[] weight_decay, float[] eeta, float[] epsilon) -> ()");
+  m.def("clip_grad_norm(Tensor(a!) g, float max_norm, Tensor(b!) ws, Tensor(c!) coef, Tensor(d!) norm) -> ()");
+
+  m.class_<RcclEngine>("RcclEngine")
+      .def(torch::init<>())
+      .def_static("unique_id", &RcclEngine::unique_id)
+      .def("init", &RcclEngine::init)
+      .def("allgather", &RcclEngine::allgather)
+      .def("allreduce", &RcclEngine::allreduce)
+      .def("broadcast", &RcclEngine::broadcast)
+      .def("group_start", &RcclEngine::group_start)
+      .def("group_end", &RcclEngine::group_end)
+      .def("destroy", &RcclEngine::destroy)
+      .def("rank", &RcclEngine::rank)
+      .def("world", &RcclEngine::world);
+}
+
+TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
+  m.impl("compress", &compress);
+  m.impl("tensor_stats", &tensor_stats);
+  m.impl("scatter_add_records", &scatter_add_records);
+  m.impl("fill_zero", &fill_zero);
+  m.impl("sign_bucket_compress", &sign_bucket_compress);
+  m.impl("sign_bucket_decompress", &sign_bucket_decompress);
+  m.impl("fused_sgd", &fused_sgd);
+  m.impl("segmented_sumsq", &segmented_sumsq);
+  m.impl("fused_lars", &fused_lars);
+  m.impl("clip_grad_norm", &clip_grad_norm);
+}

@@ -1,0 +1,813 @@
+// Fused sparsification pipeline for gfx950.
+//
+// One compress() call turns a gradient bucket into a packed sparse record
+// with no host synchronisation:
+//
+//   stats   (grid)   acc = g (+ r); r <- acc; g <- 0; per-block sum, sum^2,
+//                    sum|x|, max|x|                          [K1+K2, fused]
+//   radix   (grid)   3 histogram passes (11/11/10 key bits) for exact top-k,
+//                    random-k (hash keys) and DGC            [K6, K8]
+//   finalize(1 WG)   reduce statistics, build the candidate-threshold ladder
+//                    of the selected mode (or the radix key)  [K3]
+//   count   (grid)   per-block counts of |x| > t_j for ALL candidates in one
+//                    pass, counters in registers             [K4]
+//   decide  (1 WG)   replay the reference's refinement decision tree on the
+//                    totals, exclusive scan of per-block counts -> offsets
+//   select  (grid)   ballot/popcount block scan, writes ascending indices +
+//                    values into the record, zeroes sent entries of r [K5]
+//
+// Reference semantics reproduced (compression.py):
+//   gaussian  :358-389  threshold mu + |ppf(ratio/2)| * sigma, <=3 loops
+//   gaussian2 :405-435  same, <=5 loops, no residual add
+//   redsync   :623-691, redsynctrim :694-738, dgcsampling :555-620
+// Deviation (documented in SURVEY 2.3/7.4): the record holds at most k_cap
+// entries; selected elements beyond k_cap stay in the residual.
+#include "common.h"
+#include "gk_kernels.h"
+
+namespace gk {
+namespace {
+
+constexpr int kTileElems = kBlock * 16;  // 4 float4 per thread per tile
+constexpr int kKeyAbs = 0, kKeyHash = 1, kKeySample = 2;
+constexpr int kHistSet = kRadixBins0 + kRadixBins1 + kRadixBins2;
+
+struct Ws {
+  double* partials;   // kMaxStatsBlocks * 4
+  uint32_t* blockcnt; // kMaxCountBlocks * kMaxCand
+  int64_t* offsets;   // kMaxCountBlocks
+  int64_t* eqtake;    // kMaxCountBlocks
+  int64_t* blocksel;  // kMaxCountBlocks
+  uint32_t* hist;     // 2 * kHistSet (set 0: exact/hash, set 1: DGC sample)
+};
+
+__host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+__host__ __device__ inline Ws carve(void* base) {
+  char* p = reinterpret_cast<char*>(base);
+  Ws w;
+  size_t o = 0;
+  w.partials = reinterpret_cast<double*>(p + o); o = align_up(o + sizeof(double) * kMaxStatsBlocks * 4, 256);
+  w.blockcnt = reinterpret_cast<uint32_t*>(p + o); o = align_up(o + sizeof(uint32_t) * kMaxCountBlocks * kMaxCand, 256);
+  w.offsets = reinterpret_cast<int64_t*>(p + o); o = align_up(o + sizeof(int64_t) * kMaxCountBlocks, 256);
+  w.eqtake = reinterpret_cast<int64_t*>(p + o); o = align_up(o + sizeof(int64_t) * kMaxCountBlocks, 256);
+  w.blocksel = reinterpret_cast<int64_t*>(p + o); o = align_up(o + sizeof(int64_t) * kMaxCountBlocks, 256);
+  w.hist = reinterpret_cast<uint32_t*>(p + o);
+  return w;
+}
+
+size_t ws_bytes() {
+  size_t o = 0;
+  o = align_up(o + sizeof(double) * kMaxStatsBlocks * 4, 256);
+  o = align_up(o + sizeof(uint32_t) * kMaxCountBlocks * kMaxCand, 256);
+  o = align_up(o + sizeof(int64_t) * kMaxCountBlocks, 256) * 1;
+  o = align_up(o + sizeof(int64_t) * kMaxCountBlocks, 256);
+  o = align_up(o + sizeof(int64_t) * kMaxCountBlocks, 256);
+  o += sizeof(uint32_t) * 2 * kHistSet;
+  return align_up(o, 256);
+}
+
+// --------------------------------------------------------------------------
+// block scans
+// --------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v) {
+  const int l = lane_id();
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    uint64_t o = __shfl_up(v, off, 64);
+    if (l >= off) v += o;
+  }
+  return v;
+}
+
+// Exclusive scan over the 256 threads of the block, in thread order.
+__device__ __forceinline__ uint64_t block_excl_scan_u64(uint64_t v, uint64_t* sh /*>=4*/, uint64_t* total) {
+  const uint64_t inc = wave_incl_scan_u64(v);
+  __syncthreads();
+  if (lane_id() == 63) sh[wave_id()] = inc;
+  __syncthreads();
+  uint64_t before = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kWavesPerBlock; ++w) {
+    const uint64_t s = sh[w];
+    if (w < wave_id()) before += s;
+    tot += s;
+  }
+  *total = tot;
+  return before + inc - v;
+}
+
+// Find the digit holding the kr-th largest key (1-based) in a histogram of
+// nbins (multiple of 256).  Result broadcast to every thread.
+__device__ void radix_find(const uint32_t* hist, int nbins, int64_t kr, uint64_t* sh, int* digit_out,
+                           int64_t* kr_out) {
+  const int per = nbins / kBlock;
+  const int t = threadIdx.x;
+  const int hi = nbins - t * per;
+  uint64_t ls = 0;
+  for (int q = 0; q < per; ++q) ls += hist[hi - 1 - q];
+  uint64_t tot;
+  const uint64_t before = block_excl_scan_u64(ls, sh, &tot);
+  __shared__ int s_digit;
+  __shared__ int64_t s_kr;
+  if (t == 0) { s_digit = 0; s_kr = kr; }
+  __syncthreads();
+  if ((int64_t)before < kr && kr <= (int64_t)(before + ls)) {
+    int64_t cum = (int64_t)before;
+    for (int q = 0; q < per; ++q) {
+      const int d = hi - 1 - q;
+      const int64_t h = hist[d];
+      if (cum + h >= kr) { s_digit = d; s_kr = kr - cum; break; }
+      cum += h;
+    }
+  }
+  __syncthreads();
+  *digit_out = s_digit;
+  *kr_out = s_kr;
+  __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t bound_from_threshold(float t) {
+  // elements with |x| > t  <=>  abs_key(x) >= bound   (non-NaN x)
+  if (!(t >= 0.0f)) {
+    if (t < 0.0f) return 0u;          // every element selected
+    return 0x7fc00001u;               // NaN threshold: nothing selected
+  }
+  return (__float_as_uint(t) & 0x7fffffffu) + 1u;
+}
+
+template <int KEYKIND>
+__device__ __forceinline__ uint32_t key_of(int64_t i, float x, uint32_t seed) {
+  if (KEYKIND == kKeyHash) {
+    uint32_t h = hash_u32((uint32_t)i, seed);
+    return h == 0xffffffffu ? 0xfffffffeu : h;
+  }
+  return abs_key(x);
+}
+
+template <bool VEC>
+__device__ __forceinline__ void load4(const float* __restrict__ p, int64_t e, int64_t n, float v[4]) {
+  if (VEC) {
+    if (e < n) {
+      const float4 f = *reinterpret_cast<const float4*>(p + e);
+      v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+    } else {
+      v[0] = v[1] = v[2] = v[3] = 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = (e + q < n) ? p[e + q] : 0.f;
+  }
+}
+
+// --------------------------------------------------------------------------
+// K1+K2: residual add + moments
+// --------------------------------------------------------------------------
+template <bool VEC, bool EC, bool WRITE_R, bool ZERO_G>
+__global__ __launch_bounds__(kBlock) void stats_kernel(float* __restrict__ g, float* __restrict__ r, int64_t n,
+                                                       double* __restrict__ partials) {
+  float s = 0.f, ss = 0.f, sa = 0.f, mx = 0.f;
+  const int64_t tid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  if (VEC) {
+    const int64_t n4 = n >> 2;
+    float4* g4 = reinterpret_cast<float4*>(g);
+    float4* r4 = reinterpret_cast<float4*>(r);
+    for (int64_t i = tid; i < n4; i += stride) {
+      float4 a = g4[i];
+      if (EC) {
+        const float4 rv = r4[i];
+        a.x += rv.x; a.y += rv.y; a.z += rv.z; a.w += rv.w;
+      }
+      if (WRITE_R) r4[i] = a;
+      if (ZERO_G) g4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      s += (a.x + a.y) + (a.z + a.w);
+      ss += (a.x * a.x + a.y * a.y) + (a.z * a.z + a.w * a.w);
+      const float ax = fabsf(a.x), ay = fabsf(a.y), az = fabsf(a.z), aw = fabsf(a.w);
+      sa += (ax + ay) + (az + aw);
+      mx = fmaxf(mx, fmaxf(fmaxf(ax, ay), fmaxf(az, aw)));
+    }
+  } else {
+    for (int64_t i = tid; i < n; i += stride) {
+      float a = g[i];
+      if (EC) a += r[i];
+      if (WRITE_R) r[i] = a;
+      if (ZERO_G) g[i] = 0.f;
+      s += a;
+      ss += a * a;
+      sa += fabsf(a);
+      mx = fmaxf(mx, fabsf(a));
+    }
+  }
+  __shared__ double sh[kWavesPerBlock];
+  __shared__ float shf[kWavesPerBlock];
+  const double bs = block_sum((double)s, sh);
+  const double bss = block_sum((double)ss, sh);
+  const double bsa = block_sum((double)sa, sh);
+  const float bmx = block_max(mx, shf);
+  if (threadIdx.x == 0) {
+    partials[blockIdx.x * 4 + 0] = bs;
+    partials[blockIdx.x * 4 + 1] = bss;
+    partials[blockIdx.x * 4 + 2] = bsa;
+    partials[blockIdx.x * 4 + 3] = (double)bmx;
+  }
+}
+
+// --------------------------------------------------------------------------
+// radix histogram passes
+// --------------------------------------------------------------------------
+template <int PASS>
+__device__ __forceinline__ uint32_t radix_digit(uint32_t key) {
+  if (PASS == 0) return key >> 21;
+  if (PASS == 1) return (key >> 10) & 0x7ffu;
+  return key & 0x3ffu;
+}
+
+template <int PASS, int KEYKIND, bool VEC>
+__global__ __launch_bounds__(kBlock) void radix_hist_kernel(const float* __restrict__ x, int64_t n, uint32_t seed,
+                                                            uint32_t sample_thr, int64_t k, uint32_t* hist_set) {
+  constexpr int NB = PASS == 0 ? kRadixBins0 : (PASS == 1 ? kRadixBins1 : kRadixBins2);
+  __shared__ uint32_t sh_hist[kWavesPerBlock][NB];
+  __shared__ uint64_t sh_scan[kWavesPerBlock];
+  uint32_t* hist0 = hist_set;
+  uint32_t* hist1 = hist_set + kRadixBins0;
+  uint32_t* hist2 = hist1 + kRadixBins1;
+  uint32_t prefix = 0;
+  if (PASS >= 1) {
+    // eligible total (DGC sample size) and k_eff
+    uint64_t loc = 0;
+    for (int b = threadIdx.x; b < kRadixBins0; b += kBlock) loc += hist0[b];
+    uint64_t tot;
+    (void)block_excl_scan_u64(loc, sh_scan, &tot);
+    int64_t kr = k < (int64_t)tot ? k : (int64_t)tot;
+    if (kr < 1) kr = 1;
+    int d0; int64_t kr1;
+    radix_find(hist0, kRadixBins0, kr, sh_scan, &d0, &kr1);
+    prefix = (uint32_t)d0;
+    if (PASS == 2) {
+      int d1; int64_t kr2;
+      radix_find(hist1, kRadixBins1, kr1, sh_scan, &d1, &kr2);
+      prefix = (prefix << 11) | (uint32_t)d1;
+    }
+  }
+  for (int i = threadIdx.x; i < kWavesPerBlock * NB; i += kBlock) (&sh_hist[0][0])[i] = 0u;
+  __syncthreads();
+  uint32_t* my = sh_hist[wave_id()];
+  const int64_t tid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  const int64_t n4 = (n + 3) >> 2;
+  for (int64_t i4 = tid; i4 < n4; i4 += stride) {
+    const int64_t e = i4 << 2;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (KEYKIND != kKeyHash) load4<VEC>(x, e, n, v);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t idx = e + q;
+      if (idx >= n) continue;
+      uint32_t key;
+      if (KEYKIND == kKeySample) {
+        if (hash_u32((uint32_t)idx, seed) >= sample_thr) continue;
+        key = abs_key(v[q]) + 1u;
+      } else {
+        key = key_of<KEYKIND>(idx, v[q], seed);
+      }
+      bool elig = true;
+      if (PASS == 1) elig = (key >> 21) == prefix;
+      if (PASS == 2) elig = (key >> 10) == prefix;
+      if (elig) atomicAdd(&my[radix_digit<PASS>(key)], 1u);
+    }
+  }
+  __syncthreads();
+  uint32_t* out = PASS == 0 ? hist0 : (PASS == 1 ? hist1 : hist2);
+  for (int b = threadIdx.x; b < NB; b += kBlock) {
+    const uint32_t c = sh_hist[0][b] + sh_hist[1][b] + sh_hist[2][b] + sh_hist[3][b];
+    if (c) atomicAdd(&out[b], c);
+  }
+}
+
+// Derive the final key (k-th largest) and the tie quota from three hists.
+__device__ void radix_resolve(const uint32_t* hist_set, int64_t k, uint64_t* sh, uint32_t* key_out,
+                              int64_t* kremain_out, int64_t* keff_out) {
+  const uint32_t* hist0 = hist_set;
+  const uint32_t* hist1 = hist_set + kRadixBins0;
+  const uint32_t* hist2 = hist1 + kRadixBins1;
+  uint64_t loc = 0;
+  for (int b = threadIdx.x; b < kRadixBins0; b += kBlock) loc += hist0[b];
+  uint64_t tot;
+  (void)block_excl_scan_u64(loc, sh, &tot);
+  int64_t keff = k < (int64_t)tot ? k : (int64_t)tot;
+  int64_t kr = keff < 1 ? 1 : keff;
+  int d0, d1, d2;
+  int64_t kr1, kr2, kr3;
+  radix_find(hist0, kRadixBins0, kr, sh, &d0, &kr1);
+  radix_find(hist1, kRadixBins1, kr1, sh, &d1, &kr2);
+  radix_find(hist2, kRadixBins2, kr2, sh, &d2, &kr3);
+  *key_out = ((uint32_t)d0 << 21) | ((uint32_t)d1 << 10) | (uint32_t)d2;
+  *kremain_out = kr3;
+  *keff_out = keff;
+}
+
+// --------------------------------------------------------------------------
+// finalize: statistics + candidate ladder (1 workgroup)
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void finalize_kernel(GkCtrl* __restrict__ ctrl, const double* __restrict__ partials,
+                                                          int nparts, int64_t n, int mode, int loops, double z,
+                                                          double fixed_thr, int64_t k, const uint32_t* hist_exact,
+                                                          const uint32_t* hist_sample, float* stats_out) {
+  __shared__ double sh[kWavesPerBlock];
+  __shared__ float shf[kWavesPerBlock];
+  __shared__ uint64_t sh_scan[kWavesPerBlock];
+  double s = 0, ss = 0, sa = 0;
+  float mx = 0.f;
+  for (int b = threadIdx.x; b < nparts; b += kBlock) {
+    s += partials[b * 4 + 0];
+    ss += partials[b * 4 + 1];
+    sa += partials[b * 4 + 2];
+    mx = fmaxf(mx, (float)partials[b * 4 + 3]);
+  }
+  s = block_sum(s, sh);
+  ss = block_sum(ss, sh);
+  sa = block_sum(sa, sh);
+  mx = block_max(mx, shf);
+
+  uint32_t rkey[2] = {0u, 0u};
+  int64_t rkrem[2] = {0, 0}, rkeff[2] = {0, 0};
+  if (mode == kModeTopK || mode == kModeRandomK || mode == kModeDGC)
+    radix_resolve(hist_exact, k, sh_scan, &rkey[1], &rkrem[1], &rkeff[1]);
+  if (mode == kModeDGC) radix_resolve(hist_sample, k, sh_scan, &rkey[0], &rkrem[0], &rkeff[0]);
+
+  if (threadIdx.x != 0) return;
+  const double nd = (double)n;
+  const double mean = s / nd;
+  const double var = (ss - s * s / nd) / (nd - 1.0);
+  const double stdev = sqrt(var > 0.0 ? var : 0.0);
+  const double meanabs = sa / nd;
+  ctrl->raw[0] = s; ctrl->raw[1] = ss; ctrl->raw[2] = sa; ctrl->raw[3] = (double)mx;
+  ctrl->mean = mean; ctrl->stdev = stdev; ctrl->meanabs = meanabs; ctrl->maxabs = (double)mx;
+  if (stats_out) {
+    stats_out[0] = (float)mean; stats_out[1] = (float)stdev; stats_out[2] = (float)meanabs; stats_out[3] = mx;
+  }
+  for (int j = 0; j < kMaxCand; ++j) { ctrl->bound[j] = 0xffffffffu; ctrl->cand_thr[j] = 0.0; }
+  int nc = 0;
+  if (mode == kModeGaussian) {
+    // candidates t0 * 1.5^b * 0.5^a for a + b <= loops - 1, index tri(a+b) + b
+    const double t0 = mean + z * stdev;
+    for (int sdeg = 0; sdeg < loops; ++sdeg) {
+      for (int b = 0; b <= sdeg; ++b) {
+        const int a = sdeg - b;
+        double t = t0;
+        for (int q = 0; q < b; ++q) t *= 1.5;
+        for (int q = 0; q < a; ++q) t *= 0.5;
+        if (nc < kMaxCand) {
+          ctrl->bound[nc] = bound_from_threshold((float)t);
+          ctrl->cand_thr[nc] = t;
+        }
+        ++nc;
+      }
+    }
+  } else if (mode == kModeRedSync || mode == kModeRedSyncTrim) {
+    const float mean_val = (float)meanabs;
+    const float max_val = mx;
+    const float diff = __fsub_rn(max_val, mean_val);
+    if (mode == kModeRedSync) {
+      // heap-ordered binary-search tree of ratios, depth 3 (r - l halves 1 -> 0.125)
+      double lo[7], hi[7];
+      lo[0] = 0.0; hi[0] = 1.0;
+      for (int i = 0; i < 7; ++i) {
+        const double mid = lo[i] + (hi[i] - lo[i]) / 2;
+        const float t = __fadd_rn(mean_val, __fmul_rn((float)mid, diff));
+        ctrl->bound[i] = bound_from_threshold(t);
+        ctrl->cand_thr[i] = (double)t;
+        if (2 * i + 2 < 7) {
+          lo[2 * i + 1] = lo[i]; hi[2 * i + 1] = mid;   // nnz < k/2: r = mid
+          lo[2 * i + 2] = mid;   hi[2 * i + 2] = hi[i]; // otherwise: l = mid
+        }
+      }
+      nc = 7;
+    } else {
+      double ratio = 1.0 - 0.2;
+      for (int j = 0; j < kMaxCand; ++j) {
+        const float t = __fadd_rn(mean_val, __fmul_rn((float)ratio, diff));
+        ctrl->bound[j] = bound_from_threshold(t);
+        ctrl->cand_thr[j] = (double)t;
+        ratio = ratio - 0.2;
+      }
+      nc = kMaxCand;
+    }
+  } else if (mode == kModeThreshold) {
+    ctrl->bound[0] = bound_from_threshold((float)fixed_thr);
+    ctrl->cand_thr[0] = fixed_thr;
+    nc = 1;
+  } else if (mode == kModeTopK || mode == kModeRandomK) {
+    ctrl->bound[0] = rkey[1] + 1u;  // key > K
+    ctrl->bound[1] = rkey[1];       // key >= K
+    ctrl->cand_thr[0] = (double)__uint_as_float(rkey[1] & 0x7fffffffu);
+    nc = 2;
+  } else if (mode == kModeDGC) {
+    // sampled keys are abs_key + 1: |x| > thr  <=>  abs_key >= Ks
+    ctrl->bound[0] = rkey[0];
+    ctrl->bound[1] = rkey[1] + 1u;
+    ctrl->bound[2] = rkey[1];
+    ctrl->cand_thr[0] = rkey[0] ? (double)__uint_as_float(rkey[0] - 1u) : 0.0;
+    ctrl->cand_thr[1] = (double)__uint_as_float(rkey[1] & 0x7fffffffu);
+    nc = 3;
+  }
+  ctrl->ncand = nc < kMaxCand ? nc : kMaxCand;
+  ctrl->radix_key[0] = rkey[0]; ctrl->radix_key[1] = rkey[1];
+  ctrl->radix_kremain[0] = rkrem[0]; ctrl->radix_kremain[1] = rkrem[1];
+  ctrl->k_eff = rkeff[1];
+}
+
+// --------------------------------------------------------------------------
+// K4: one-pass multi-threshold count (counters in registers)
+// --------------------------------------------------------------------------
+template <int KEYKIND, bool VEC>
+__global__ __launch_bounds__(kBlock) void count_kernel(const float* __restrict__ x, int64_t n, uint32_t seed,
+                                                       const GkCtrl* __restrict__ ctrl, int64_t chunk_tiles,
+                                                       uint32_t* __restrict__ blockcnt) {
+  uint32_t bnd[kMaxCand];
+#pragma unroll
+  for (int j = 0; j < kMaxCand; ++j) bnd[j] = __builtin_amdgcn_readfirstlane(ctrl->bound[j]);
+  uint32_t cnt[kMaxCand];
+#pragma unroll
+  for (int j = 0; j < kMaxCand; ++j) cnt[j] = 0u;
+  const int64_t ntiles = (n + kTileElems - 1) / kTileElems;
+  const int64_t t0 = (int64_t)blockIdx.x * chunk_tiles;
+  const int64_t t1 = t0 + chunk_tiles < ntiles ? t0 + chunk_tiles : ntiles;
+  for (int64_t tile = t0; tile < t1; ++tile) {
+    const int64_t base = tile * kTileElems;
+#pragma unroll
+    for (int j4 = 0; j4 < 4; ++j4) {
+      const int64_t e = base + j4 * (kBlock * 4) + threadIdx.x * 4;
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      if (KEYKIND != kKeyHash) load4<VEC>(x, e, n, v);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool valid = e + q < n;
+        const uint32_t key = key_of<KEYKIND>(e + q, v[q], seed);
+#pragma unroll
+        for (int j = 0; j < kMaxCand; ++j) cnt[j] += (valid && key >= bnd[j]) ? 1u : 0u;
+      }
+    }
+  }
+  __shared__ uint32_t sh[kWavesPerBlock][kMaxCand];
+#pragma unroll
+  for (int j = 0; j < kMaxCand; ++j) {
+    const uint32_t w = wave_sum(cnt[j]);
+    if (lane_id() == 0) sh[wave_id()][j] = w;
+  }
+  __syncthreads();
+  if (threadIdx.x < kMaxCand) {
+    const int j = threadIdx.x;
+    blockcnt[blockIdx.x * kMaxCand + j] = sh[0][j] + sh[1][j] + sh[2][j] + sh[3][j];
+  }
+}
+
+// --------------------------------------------------------------------------
+// decide: replay the reference decision tree, offsets per block (1 WG)
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void decide_kernel(GkCtrl* __restrict__ ctrl, const uint32_t* __restrict__ blockcnt,
+                                                        int G, int mode, int loops, int64_t k, int64_t k_cap,
+                                                        int64_t* __restrict__ offsets, int64_t* __restrict__ eqtake,
+                                                        int64_t* __restrict__ blocksel, int32_t* __restrict__ hdr) {
+  __shared__ uint64_t sh_tot[kWavesPerBlock][kMaxCand];
+  __shared__ uint64_t sh_scan[kWavesPerBlock];
+  __shared__ int s_chosen, s_gt, s_ge;
+  __shared__ int64_t s_quota;
+  const int nc = ctrl->ncand;
+  // totals per candidate
+  uint64_t loc[kMaxCand];
+#pragma unroll
+  for (int j = 0; j < kMaxCand; ++j) loc[j] = 0;
+  for (int b = threadIdx.x; b < G; b += kBlock) {
+#pragma unroll
+    for (int j = 0; j < kMaxCand; ++j) loc[j] += blockcnt[b * kMaxCand + j];
+  }
+#pragma unroll
+  for (int j = 0; j < kMaxCand; ++j) {
+    const uint64_t w = wave_sum(loc[j]);
+    if (lane_id() == 0) sh_tot[wave_id()][j] = w;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t tot[kMaxCand];
+    for (int j = 0; j < kMaxCand; ++j)
+      tot[j] = (int64_t)(sh_tot[0][j] + sh_tot[1][j] + sh_tot[2][j] + sh_tot[3][j]);
+    int chosen = 0, gt = 0, ge = -1;
+    int64_t quota = 0;
+    const double kd = (double)k;
+    if (mode == kModeGaussian) {
+      int a = 0, b = 0;
+      for (int loop = 0; loop < loops; ++loop) {
+        const int64_t c = tot[(a + b) * (a + b + 1) / 2 + b];
+        if (loop == loops - 1) break;
+        if ((double)c < 2.0 * kd / 3.0) ++a;
+        else if ((double)c > 4.0 * kd / 3.0) ++b;
+        else break;
+      }
+      chosen = (a + b) * (a + b + 1) / 2 + b;
+    } else if (mode == kModeRedSync) {
+      int node = 0;
+      for (int depth = 0; depth < 3; ++depth) {
+        const int64_t c = tot[node];
+        if (c > k && 2 * k > c) break;
+        if (depth == 2) break;
+        node = ((double)c < kd / 2.0) ? 2 * node + 1 : 2 * node + 2;
+      }
+      chosen = node;
+    } else if (mode == kModeRedSyncTrim) {
+      chosen = nc - 1;
+      for (int j = 0; j < nc; ++j) if (tot[j] >= k) { chosen = j; break; }
+    } else if (mode == kModeThreshold) {
+      chosen = 0;
+    } else if (mode == kModeTopK || mode == kModeRandomK) {
+      chosen = 0; gt = 0; ge = 1; quota = ctrl->radix_kremain[1];
+    } else if (mode == kModeDGC) {
+      if ((double)tot[0] > 4.0 * kd / 3.0) { chosen = 1; gt = 1; ge = 2; quota = ctrl->radix_kremain[1]; }
+      else chosen = 0;
+    }
+    if (ge < 0) gt = chosen;
+    s_chosen = chosen; s_gt = gt; s_ge = ge; s_quota = quota;
+    ctrl->chosen = chosen;
+    ctrl->sel_bound = ctrl->bound[gt];
+    ctrl->eq_key = ge >= 0 ? ctrl->bound[ge] : 0xffffffffu;
+    ctrl->eq_quota = ge >= 0 ? quota : 0;
+    ctrl->thr = (float)ctrl->cand_thr[chosen];
+  }
+  __syncthreads();
+  const int gt = s_gt, ge = s_ge;
+  const int64_t quota = s_quota;
+  // each thread owns up to 4 consecutive blocks
+  constexpr int kPer = kMaxCountBlocks / kBlock;
+  int64_t gtc[kPer], eqc[kPer];
+  uint64_t eq_loc = 0;
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int b = threadIdx.x * kPer + q;
+    gtc[q] = 0; eqc[q] = 0;
+    if (b < G) {
+      gtc[q] = blockcnt[b * kMaxCand + gt];
+      if (ge >= 0) eqc[q] = (int64_t)blockcnt[b * kMaxCand + ge] - gtc[q];
+    }
+    eq_loc += eqc[q];
+  }
+  uint64_t eq_tot;
+  uint64_t eq_before = block_excl_scan_u64(eq_loc, sh_scan, &eq_tot);
+  int64_t take[kPer];
+  uint64_t sel_loc = 0;
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    int64_t rem = quota - (int64_t)eq_before;
+    if (rem < 0) rem = 0;
+    take[q] = eqc[q] < rem ? eqc[q] : rem;
+    eq_before += eqc[q];
+    sel_loc += gtc[q] + take[q];
+  }
+  uint64_t sel_tot;
+  uint64_t sel_before = block_excl_scan_u64(sel_loc, sh_scan, &sel_tot);
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int b = threadIdx.x * kPer + q;
+    if (b < G) {
+      offsets[b] = (int64_t)sel_before;
+      eqtake[b] = take[q];
+      blocksel[b] = gtc[q] + take[q];
+    }
+    sel_before += gtc[q] + take[q];
+  }
+  if (threadIdx.x == 0) {
+    const int64_t total = (int64_t)sel_tot;
+    const int64_t sent = total < k_cap ? total : k_cap;
+    ctrl->total = total;
+    ctrl->sent = sent;
+    hdr[0] = (int32_t)sent;
+    hdr[1] = (int32_t)(total > 0x7fffffff ? 0x7fffffff : total);
+    hdr[2] = s_chosen;
+    hdr[3] = __float_as_int(ctrl->thr);
+  }
+}
+
+// --------------------------------------------------------------------------
+// K5: select + compact (ascending indices) + residual write-back
+// --------------------------------------------------------------------------
+template <int KEYKIND, bool VEC>
+__global__ __launch_bounds__(kBlock) void select_kernel(float* __restrict__ r, int64_t n, uint32_t seed,
+                                                        const GkCtrl* __restrict__ ctrl, int64_t chunk_tiles,
+                                                        const int64_t* __restrict__ offsets,
+                                                        const int64_t* __restrict__ eqtake,
+                                                        const int64_t* __restrict__ blocksel, int64_t k_cap,
+                                                        int32_t* __restrict__ out_idx, float* __restrict__ out_val) {
+  const int64_t my_sel = blocksel[blockIdx.x];
+  int64_t running = offsets[blockIdx.x];
+  if (my_sel == 0 || running >= k_cap) return;  // block-uniform
+  const uint32_t bound = __builtin_amdgcn_readfirstlane(ctrl->sel_bound);
+  const uint32_t eqkey = __builtin_amdgcn_readfirstlane(ctrl->eq_key);
+  const int64_t my_eq = eqtake[blockIdx.x];
+  int64_t eq_running = 0;
+  __shared__ uint32_t sh_tot[4][kWavesPerBlock];
+  __shared__ uint32_t sh_eq[4][kWavesPerBlock];
+  const int64_t ntiles = (n + kTileElems - 1) / kTileElems;
+  const int64_t t0 = (int64_t)blockIdx.x * chunk_tiles;
+  const int64_t t1 = t0 + chunk_tiles < ntiles ? t0 + chunk_tiles : ntiles;
+  const int w = wave_id();
+  for (int64_t tile = t0; tile < t1 && running < k_cap; ++tile) {
+    const int64_t base = tile * kTileElems;
+    float v[4][4];
+    uint32_t selm[4], eqm[4];
+#pragma unroll
+    for (int j4 = 0; j4 < 4; ++j4) {
+      const int64_t e = base + j4 * (kBlock * 4) + threadIdx.x * 4;
+      load4<VEC>(r, e, n, v[j4]);
+      selm[j4] = 0; eqm[j4] = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool valid = e + q < n;
+        const uint32_t key = key_of<KEYKIND>(e + q, v[j4][q], seed);
+        if (valid && key >= bound) selm[j4] |= 1u << q;
+        if (valid && my_eq > 0 && key == eqkey) eqm[j4] |= 1u << q;
+      }
+    }
+    // ties (radix modes): take the first `my_eq` key==eqkey elements of this block
+    if (my_eq > 0) {
+      uint32_t pre[4];
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4) {
+        uint32_t tot;
+        pre[j4] = wave_excl_prefix_small<3>(__popc(eqm[j4]), &tot);
+        if (lane_id() == 0) sh_eq[j4][w] = tot;
+      }
+      __syncthreads();
+      int64_t acc = eq_running;
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4) {
+        int64_t before = acc;
+        for (int ww = 0; ww < kWavesPerBlock; ++ww) {
+          if (ww < w) before += sh_eq[j4][ww];
+          acc += sh_eq[j4][ww];
+        }
+        int64_t rank = before + pre[j4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (eqm[j4] & (1u << q)) {
+            if (rank < my_eq) selm[j4] |= 1u << q;
+            ++rank;
+          }
+        }
+      }
+      eq_running = acc;
+      __syncthreads();
+    }
+    uint32_t pre[4];
+#pragma unroll
+    for (int j4 = 0; j4 < 4; ++j4) {
+      uint32_t tot;
+      pre[j4] = wave_excl_prefix_small<3>(__popc(selm[j4]), &tot);
+      if (lane_id() == 0) sh_tot[j4][w] = tot;
+    }
+    __syncthreads();
+    int64_t acc = running;
+#pragma unroll
+    for (int j4 = 0; j4 < 4; ++j4) {
+      int64_t before = acc;
+      for (int ww = 0; ww < kWavesPerBlock; ++ww) {
+        if (ww < w) before += sh_tot[j4][ww];
+        acc += sh_tot[j4][ww];
+      }
+      if (selm[j4]) {
+        int64_t pos = before + pre[j4];
+        const int64_t e = base + j4 * (kBlock * 4) + threadIdx.x * 4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (selm[j4] & (1u << q)) {
+            if (pos < k_cap) {
+              out_idx[pos] = (int32_t)(e + q);
+              out_val[pos] = v[j4][q];
+              r[e + q] = 0.f;
+            }
+            ++pos;
+          }
+        }
+      }
+    }
+    running = acc;
+    __syncthreads();
+  }
+}
+
+template <int KEYKIND>
+void launch_count_select(const CompressArgs& a, const Ws& w, bool vec, int G, int64_t chunk_tiles, GkCtrl* ctrl,
+                         int32_t* out_idx, float* out_val, hipStream_t s) {
+  if (vec)
+    hipLaunchKernelGGL((count_kernel<KEYKIND, true>), dim3(G), dim3(kBlock), 0, s, a.r, a.n, a.seed, ctrl,
+                       chunk_tiles, w.blockcnt);
+  else
+    hipLaunchKernelGGL((count_kernel<KEYKIND, false>), dim3(G), dim3(kBlock), 0, s, a.r, a.n, a.seed, ctrl,
+                       chunk_tiles, w.blockcnt);
+  hipLaunchKernelGGL(decide_kernel, dim3(1), dim3(kBlock), 0, s, ctrl, w.blockcnt, G, a.mode, a.loops, a.k,
+                     a.k_cap, w.offsets, w.eqtake, w.blocksel, a.record);
+  if (vec)
+    hipLaunchKernelGGL((select_kernel<KEYKIND, true>), dim3(G), dim3(kBlock), 0, s, a.r, a.n, a.seed, ctrl,
+                       chunk_tiles, w.offsets, w.eqtake, w.blocksel, a.k_cap, out_idx, out_val);
+  else
+    hipLaunchKernelGGL((select_kernel<KEYKIND, false>), dim3(G), dim3(kBlock), 0, s, a.r, a.n, a.seed, ctrl,
+                       chunk_tiles, w.offsets, w.eqtake, w.blocksel, a.k_cap, out_idx, out_val);
+}
+
+template <int KEYKIND>
+void launch_radix(const float* x, int64_t n, uint32_t seed, uint32_t sample_thr, int64_t k, uint32_t* set, bool vec,
+                  hipStream_t s) {
+  const int64_t n4 = (n + 3) / 4;
+  int Gh = (int)ceil_div(n4, (int64_t)kBlock * 8);
+  if (Gh < 1) Gh = 1;
+  if (Gh > 512) Gh = 512;
+#define GK_RADIX_PASS(P)                                                                                         \
+  if (vec)                                                                                                       \
+    hipLaunchKernelGGL((radix_hist_kernel<P, KEYKIND, true>), dim3(Gh), dim3(kBlock), 0, s, x, n, seed, sample_thr, \
+                       k, set);                                                                                  \
+  else                                                                                                           \
+    hipLaunchKernelGGL((radix_hist_kernel<P, KEYKIND, false>), dim3(Gh), dim3(kBlock), 0, s, x, n, seed,          \
+                       sample_thr, k, set);
+  GK_RADIX_PASS(0)
+  GK_RADIX_PASS(1)
+  GK_RADIX_PASS(2)
+#undef GK_RADIX_PASS
+}
+
+}  // namespace
+
+size_t compress_workspace_bytes(int64_t /*n*/) { return ws_bytes(); }
+
+void compress(const CompressArgs& a, hipStream_t s) {
+  const Ws w = carve(a.ws);
+  GkCtrl* ctrl = reinterpret_cast<GkCtrl*>(a.ctrl);
+  int32_t* out_idx = a.record + 4;
+  float* out_val = reinterpret_cast<float*>(a.record + 4 + a.k_cap);
+  if (a.n <= 0) {
+    hipMemsetAsync(a.record, 0, sizeof(int32_t) * 4, s);
+    return;
+  }
+  const bool vec_gr = ((reinterpret_cast<uintptr_t>(a.g) | reinterpret_cast<uintptr_t>(a.r)) & 15) == 0 && (a.n % 4) == 0;
+  const bool vec_r = (reinterpret_cast<uintptr_t>(a.r) & 15) == 0 && (a.n % 4) == 0;
+
+  // 1. stats (+ residual add, residual write, gradient zeroing)
+  int Gs = (int)ceil_div(a.n, (int64_t)kBlock * 16);
+  if (Gs < 1) Gs = 1;
+  if (Gs > kMaxStatsBlocks) Gs = kMaxStatsBlocks;
+#define GK_STATS(VEC, EC, ZG)                                                                                     \
+  hipLaunchKernelGGL((stats_kernel<VEC, EC, true, ZG>), dim3(Gs), dim3(kBlock), 0, s, a.g, a.r, a.n, w.partials);
+  if (vec_gr) {
+    if (a.ec) { if (a.zero_g) { GK_STATS(true, true, true) } else { GK_STATS(true, true, false) } }
+    else { if (a.zero_g) { GK_STATS(true, false, true) } else { GK_STATS(true, false, false) } }
+  } else {
+    if (a.ec) { if (a.zero_g) { GK_STATS(false, true, true) } else { GK_STATS(false, true, false) } }
+    else { if (a.zero_g) { GK_STATS(false, false, true) } else { GK_STATS(false, false, false) } }
+  }
+#undef GK_STATS
+
+  // 2. radix histograms (exact / hash / sample)
+  uint32_t* hist_exact = w.hist;
+  uint32_t* hist_sample = w.hist + kHistSet;
+  const int64_t keff = a.k < a.n ? a.k : a.n;
+  if (a.mode == kModeTopK || a.mode == kModeRandomK || a.mode == kModeDGC) {
+    hipMemsetAsync(w.hist, 0, sizeof(uint32_t) * 2 * kHistSet, s);
+    if (a.mode == kModeRandomK) launch_radix<kKeyHash>(a.r, a.n, a.seed, 0u, keff, hist_exact, vec_r, s);
+    else launch_radix<kKeyAbs>(a.r, a.n, a.seed, 0u, keff, hist_exact, vec_r, s);
+    if (a.mode == kModeDGC) {
+      double p = a.sample_p * 4294967296.0;
+      uint32_t thr = p >= 4294967295.0 ? 0xffffffffu : (uint32_t)p;
+      launch_radix<kKeySample>(a.r, a.n, a.seed, thr, a.k, hist_sample, vec_r, s);
+    }
+  }
+
+  // 3. finalize
+  const int64_t n_stats = a.n_stats > 0 ? a.n_stats : a.n;
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(kBlock), 0, s, ctrl, w.partials, Gs, n_stats, a.mode, a.loops, a.z,
+                     a.fixed_thr, keff, hist_exact, hist_sample, a.stats_out);
+
+  // 4-6. count, decide, select
+  const int64_t ntiles = ceil_div(a.n, (int64_t)kTileElems);
+  int G = (int)(ntiles < kMaxCountBlocks ? ntiles : kMaxCountBlocks);
+  const int64_t chunk_tiles = ceil_div(ntiles, (int64_t)G);
+  G = (int)ceil_div(ntiles, chunk_tiles);
+  if (a.mode == kModeRandomK)
+    launch_count_select<kKeyHash>(a, w, vec_r, G, chunk_tiles, ctrl, out_idx, out_val, s);
+  else
+    launch_count_select<kKeyAbs>(a, w, vec_r, G, chunk_tiles, ctrl, out_idx, out_val, s);
+}
+
+void tensor_stats(const float* x, int64_t n, void* ctrl, void* ws, hipStream_t s) {
+  const Ws w = carve(ws);
+  int Gs = (int)ceil_div(n, (int64_t)kBlock * 16);
+  if (Gs < 1) Gs = 1;
+  if (Gs > kMaxStatsBlocks) Gs = kMaxStatsBlocks;
+  float* xx = const_cast<float*>(x);
+  const bool vec = (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (n % 4) == 0;
+  if (vec)
+    hipLaunchKernelGGL((stats_kernel<true, false, false, false>), dim3(Gs), dim3(kBlock), 0, s, xx, xx, n, w.partials);
+  else
+    hipLaunchKernelGGL((stats_kernel<false, false, false, false>), dim3(Gs), dim3(kBlock), 0, s, xx, xx, n, w.partials);
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(kBlock), 0, s, reinterpret_cast<GkCtrl*>(ctrl), w.partials, Gs, n,
+                     (int)kModeThreshold, 1, 0.0, 0.0, (int64_t)1, w.hist, w.hist, (float*)nullptr);
+}
+
+}  // namespace gk

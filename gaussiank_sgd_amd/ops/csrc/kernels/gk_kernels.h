@@ -1,0 +1,153 @@
+// Host-side launcher API of the gfx950 kernel library.
+//
+// Every launcher is asynchronous on the given stream, performs no host
+// synchronisation and no allocation (workspaces are passed in), so any
+// sequence of them can be captured into a hipGraph.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace gk {
+
+// ---------------------------------------------------------------------------
+// Threshold-selection modes of the fused compressor pipeline.
+// ---------------------------------------------------------------------------
+enum Mode : int {
+  kModeGaussian = 0,      // mu + z*sigma, <= `loops` x0.5/x1.5 refinements (compression.py:358-389,405-435)
+  kModeRedSync = 1,       // binary search of mean|x| + r(max|x|-mean|x|) (compression.py:623-691)
+  kModeRedSyncTrim = 2,   // r = 0.8, 0.6, ... until nnz >= k (compression.py:694-738)
+  kModeTopK = 3,          // exact top-k by radix select on |x|
+  kModeRandomK = 4,       // k smallest hashes: a uniformly random k-subset
+  kModeThreshold = 5,     // fixed threshold |x| > t
+  kModeDGC = 6,           // 1% sample threshold, exact top-k when > 4k/3 (compression.py:555-620)
+};
+
+constexpr int kMaxCand = 16;
+constexpr int kMaxCountBlocks = 1024;
+constexpr int kMaxStatsBlocks = 2048;
+constexpr int kRadixBins0 = 2048;  // key bits [31:21]
+constexpr int kRadixBins1 = 2048;  // key bits [20:10]
+constexpr int kRadixBins2 = 1024;  // key bits [9:0]
+
+// Device-resident control block of one compression call.  Lives in a
+// caller-provided buffer of sizeof(GkCtrl) bytes.
+struct GkCtrl {
+  double raw[4];        // sum, sumsq, sum|x|, max|x|
+  double mean, stdev, meanabs, maxabs;
+  uint32_t bound[kMaxCand];   // candidate j selects key >= bound[j]
+  int32_t ncand;
+  int32_t chosen;
+  uint32_t sel_bound;   // select key >= sel_bound ...
+  uint32_t eq_key;      // ... or key == eq_key within eq_quota (radix ties)
+  int64_t eq_quota;
+  int64_t total;        // true number selected
+  int64_t sent;         // min(total, k_cap)
+  int64_t k_eff;
+  float thr;            // chosen threshold (|x| units) for logging
+  int32_t pad0;
+  uint32_t radix_key[2];      // [0] sampled (DGC), [1] exact
+  int64_t radix_kremain[2];
+  double cand_thr[kMaxCand];  // candidate thresholds in |x| units (logging/tests)
+};
+
+struct CompressArgs {
+  float* g = nullptr;          // raw gradient bucket; zeroed when zero_g
+  float* r = nullptr;          // residual in; (g + r) then new residual out
+  int64_t n = 0;
+  int64_t n_stats = 0;          // elements used to normalise statistics (<=0: n)
+  int mode = kModeGaussian;
+  int ec = 1;                  // add residual before selection
+  int zero_g = 1;
+  int loops = 3;               // gaussian refinement iterations
+  double z = 0.0;              // gaussian |z| multiplier
+  double fixed_thr = 0.0;      // kModeThreshold
+  double sample_p = 0.01;      // kModeDGC
+  int64_t k = 1;
+  int64_t k_cap = 1;
+  uint32_t seed = 0;
+  void* ctrl = nullptr;        // GkCtrl
+  void* ws = nullptr;          // gk_compress_workspace_bytes(n)
+  int32_t* record = nullptr;   // [4 + 2*k_cap] int32: hdr | idx | val(fp32 bits)
+  float* stats_out = nullptr;  // optional [4] copy of mean, std, meanabs, maxabs (fp32)
+};
+
+size_t compress_workspace_bytes(int64_t n);
+void compress(const CompressArgs& a, hipStream_t stream);
+
+// Stand-alone statistics (no residual) for tests / the bucket planner.
+void tensor_stats(const float* x, int64_t n, void* ctrl, void* ws, hipStream_t stream);
+
+// ---------------------------------------------------------------------------
+// Sparse aggregation: dst[idx] += val * scale for every rank's record.
+// records: [P][4 + 2*k_cap] int32.  Atomic (default) or per-rank ordered.
+// ---------------------------------------------------------------------------
+void scatter_add_records(float* dst, int64_t n, const int32_t* records, int P, int64_t k_cap,
+                         float scale, int deterministic, hipStream_t stream);
+void fill_zero(float* dst, int64_t n, hipStream_t stream);
+
+// ---------------------------------------------------------------------------
+// Sign-bucket mean compressor (BucketCompressor, compression.py:227-312).
+// ---------------------------------------------------------------------------
+size_t sign_bucket_workspace_bytes(int64_t n);
+// means_out[2] = {mean(x>=0), mean(x<0)}; x -= mean per bucket; mask[i]=x>=0
+void sign_bucket_compress(float* x, int64_t n, uint8_t* mask, float* means_out, void* ws,
+                          hipStream_t stream);
+void sign_bucket_decompress(float* x, int64_t n, const uint8_t* mask, const float* means,
+                            hipStream_t stream);
+
+// ---------------------------------------------------------------------------
+// Fused optimizers over a chunk table (multi-tensor apply over flat arenas).
+// ---------------------------------------------------------------------------
+struct Chunk {
+  int64_t start;      // element offset in the arenas
+  int32_t len;        // elements (<= kChunkElems)
+  int16_t group;      // param-group id (hyper-parameters)
+  int16_t seg;        // tensor id (LARS trust ratios)
+};
+constexpr int kChunkElems = 16384;
+constexpr int kMaxGroups = 8;
+
+struct SgdGroup {
+  float lr, momentum, dampening, weight_decay;
+  int nesterov;
+  int first_step;     // momentum buffer not yet initialised -> buf = d
+  float pad0, pad1;
+};
+struct SgdArgs {
+  float* w = nullptr;
+  float* m = nullptr;        // may be null when no group uses momentum
+  float* g = nullptr;
+  const Chunk* chunks = nullptr;
+  int nchunks = 0;
+  SgdGroup groups[kMaxGroups];
+  int ngroups = 0;
+  int zero_grad = 1;
+  const float* grad_scale = nullptr;  // optional device scalar (clip coefficient)
+};
+void fused_sgd(const SgdArgs& a, hipStream_t stream);
+
+// Per-segment sum of squares: out[2*seg] += sum w^2, out[2*seg+1] += sum g^2.
+void segmented_sumsq(const float* w, const float* g, const Chunk* chunks, int nchunks, double* out,
+                     hipStream_t stream);
+
+struct LarsArgs {
+  float* w = nullptr;
+  float* m = nullptr;        // 'acceleration' buffer (initialised to ones, lars.py:116-118)
+  const float* g = nullptr;
+  const Chunk* chunks = nullptr;
+  int nchunks = 0;
+  const double* seg_sumsq = nullptr;  // from segmented_sumsq
+  float lr[kMaxGroups], momentum[kMaxGroups], weight_decay[kMaxGroups], eeta[kMaxGroups],
+      epsilon[kMaxGroups];
+  int ngroups = 0;
+};
+void fused_lars(const LarsArgs& a, hipStream_t stream);
+
+// Global-norm gradient clipping without a host sync: computes
+// coef = min(1, max_norm / (||g|| + 1e-6)) into coef_out and scales g.
+void clip_grad_norm(float* g, int64_t n, float max_norm, double* ws, float* coef_out,
+                    float* norm_out, hipStream_t stream);
+
+}  // namespace gk

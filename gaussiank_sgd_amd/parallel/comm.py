@@ -1,0 +1,367 @@
+"""Horovod-compatible communication facade over torch.distributed (RCCL / gloo).
+
+Parity: reference ``distributed_optimizer.py:21-26`` re-exports Horovod's
+``init, size, local_size, rank, local_rank, broadcast, allreduce_async_,
+allgather_async, broadcast_async_, synchronize`` and defines
+``broadcast_parameters`` / ``broadcast_optimizer_state`` (:588-736); the
+trainer also uses ``mpi4py`` ``COMM_WORLD.bcast`` (dist_trainer.py:16-17,40)
+-> ``broadcast_object`` here.
+
+Design: one process per GPU.  ``init()`` reads the torchrun variables
+(RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR) or, for mpirun launches, the
+OpenMPI ones (OMPI_COMM_WORLD_*).  On GPUs the backend is ``nccl`` (= RCCL on
+ROCm over xGMI), on CPU ``gloo``.  Async handles wrap torch Work objects; for
+RCCL ``synchronize`` only makes the current HIP stream wait (no host block),
+matching how the hot path is meant to run.  A world of one process needs no
+process group at all.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from typing import Any, Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+_state: Dict[str, Any] = {"initialized": False, "rank": 0, "size": 1, "local_rank": 0, "local_size": 1,
+                          "backend": None, "owns_pg": False}
+
+
+def _env_int(*names: str, default: int) -> int:
+    for n in names:
+        v = os.environ.get(n)
+        if v is not None and v != "":
+            return int(v)
+    return default
+
+
+def init(backend: Optional[str] = None, timeout_s: Optional[float] = None, device: Optional[str] = None) -> None:
+    """Initialise the world (idempotent).  Equivalent of ``hvd.init()``."""
+    if _state["initialized"]:
+        return
+    rank = _env_int("RANK", "OMPI_COMM_WORLD_RANK", "PMI_RANK", default=0)
+    size = _env_int("WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE", default=1)
+    local_rank = _env_int("LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", default=rank)
+    local_size = _env_int("LOCAL_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_SIZE", default=size)
+    if dist.is_available() and dist.is_initialized():
+        rank, size = dist.get_rank(), dist.get_world_size()
+        _state["backend"] = dist.get_backend()
+    elif size > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        os.environ["RANK"] = str(rank)
+        os.environ["WORLD_SIZE"] = str(size)
+        if backend is None:
+            want_gpu = device != "cpu" and torch.cuda.device_count() > 0
+            backend = "nccl" if want_gpu else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
+        kw = {}
+        t = timeout_s if timeout_s is not None else float(os.environ.get("GKSGD_COLLECTIVE_TIMEOUT_S", "1800"))
+        kw["timeout"] = datetime.timedelta(seconds=t)
+        if backend == "nccl":
+            kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
+        dist.init_process_group(backend=backend, **kw)
+        _state["backend"] = backend
+        _state["owns_pg"] = True
+    _state.update(initialized=True, rank=rank, size=size, local_rank=local_rank, local_size=local_size)
+
+
+def shutdown() -> None:
+    if _state["owns_pg"] and dist.is_initialized():
+        dist.destroy_process_group()
+    _state.update(initialized=False, rank=0, size=1, local_rank=0, local_size=1, backend=None, owns_pg=False)
+
+
+def is_initialized() -> bool:
+    return _state["initialized"]
+
+
+def size() -> int:
+    return _state["size"]
+
+
+def rank() -> int:
+    return _state["rank"]
+
+
+def local_rank() -> int:
+    return _state["local_rank"]
+
+
+def local_size() -> int:
+    return _state["local_size"]
+
+
+def backend() -> Optional[str]:
+    return _state["backend"]
+
+
+def _distributed() -> bool:
+    return _state["size"] > 1 and dist.is_initialized()
+
+
+class Handle:
+    """Async handle: ``synchronize(handle)`` returns the output tensor."""
+
+    __slots__ = ("work", "output", "post")
+
+    def __init__(self, work, output, post=None):
+        self.work = work
+        self.output = output
+        self.post = post
+
+
+def synchronize(handle: Handle) -> torch.Tensor:
+    if handle.work is not None:
+        handle.work.wait()
+        handle.work = None
+    if handle.post is not None:
+        handle.output = handle.post(handle.output)
+        handle.post = None
+    return handle.output
+
+
+def barrier() -> None:
+    if _distributed():
+        if backend() == "nccl":
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()
+
+
+# ----------------------------------------------------------------------------
+# collectives
+# ----------------------------------------------------------------------------
+def allreduce_async_(tensor: torch.Tensor, average: bool = True, name: Optional[str] = None) -> Handle:
+    if not _distributed():
+        return Handle(None, tensor)
+    if average and backend() == "nccl":
+        work = dist.all_reduce(tensor, op=dist.ReduceOp.AVG, async_op=True)
+        return Handle(work, tensor)
+    work = dist.all_reduce(tensor, op=dist.ReduceOp.SUM, async_op=True)
+    if average:
+        n = size()
+        return Handle(work, tensor, post=lambda t: t.div_(n))
+    return Handle(work, tensor)
+
+
+def allreduce_(tensor: torch.Tensor, average: bool = True, name: Optional[str] = None) -> torch.Tensor:
+    return synchronize(allreduce_async_(tensor, average, name))
+
+
+def allreduce(tensor: torch.Tensor, average: bool = True, name: Optional[str] = None) -> torch.Tensor:
+    return allreduce_(tensor.clone(), average, name)
+
+
+def allgather_into_(out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
+    """Fixed-size all-gather: out = concat over ranks of inp (out numel = P * inp numel)."""
+    if not _distributed():
+        out.view(-1)[: inp.numel()].copy_(inp.view(-1))
+        return None
+    if backend() == "gloo":
+        chunks = list(out.view(size(), -1).unbind(0))
+        return dist.all_gather(chunks, inp.view(-1).contiguous(), async_op=async_op)
+    return dist.all_gather_into_tensor(out.view(-1), inp.view(-1).contiguous(), async_op=async_op)
+
+
+def allgather_async(tensor: torch.Tensor, name: Optional[str] = None) -> Handle:
+    """Horovod semantics: first dimension may differ per rank; result is the concat."""
+    if not _distributed():
+        return Handle(None, tensor.clone())
+    t = tensor.contiguous()
+    n0 = torch.tensor([t.shape[0] if t.dim() > 0 else 1], dtype=torch.int64, device=t.device)
+    sizes = torch.zeros(size(), dtype=torch.int64, device=t.device)
+    allgather_into_(sizes, n0)
+    sizes_l = [int(x) for x in sizes.cpu().tolist()]
+    mx = max(sizes_l)
+    rest = tuple(t.shape[1:])
+    padded = torch.zeros((mx,) + rest, dtype=t.dtype, device=t.device)
+    if t.shape[0] > 0:
+        padded[: t.shape[0]].copy_(t)
+    out = torch.empty((size() * mx,) + rest, dtype=t.dtype, device=t.device)
+    work = allgather_into_(out, padded, async_op=True)
+
+    def post(o):
+        parts = [o[i * mx: i * mx + s] for i, s in enumerate(sizes_l)]
+        return torch.cat(parts, 0)
+
+    return Handle(work, out, post)
+
+
+def allgather(tensor: torch.Tensor, name: Optional[str] = None) -> torch.Tensor:
+    return synchronize(allgather_async(tensor, name))
+
+
+def broadcast_async_(tensor: torch.Tensor, root_rank: int, name: Optional[str] = None) -> Handle:
+    if not _distributed():
+        return Handle(None, tensor)
+    work = dist.broadcast(tensor, src=root_rank, async_op=True)
+    return Handle(work, tensor)
+
+
+def broadcast_(tensor: torch.Tensor, root_rank: int, name: Optional[str] = None) -> torch.Tensor:
+    return synchronize(broadcast_async_(tensor, root_rank, name))
+
+
+def broadcast(tensor: torch.Tensor, root_rank: int, name: Optional[str] = None) -> torch.Tensor:
+    return broadcast_(tensor.clone(), root_rank, name)
+
+
+def broadcast_object(obj: Any, root: int = 0) -> Any:
+    """Replacement for mpi4py ``COMM_WORLD.bcast`` (dist_trainer.py:40)."""
+    if not _distributed():
+        return obj
+    lst = [obj]
+    dist.broadcast_object_list(lst, src=root)
+    return lst[0]
+
+
+def broadcast_parameters(params, root_rank: int = 0) -> None:
+    """Broadcast a state_dict / named_parameters from root (distributed_optimizer.py:588-617).
+
+    Tensors sharing one storage (our flat arenas) are broadcast once per
+    storage, so a whole model normally costs one or two collectives.
+    """
+    if isinstance(params, dict):
+        items = sorted(params.items())
+    elif isinstance(params, list):
+        items = params
+    else:
+        raise ValueError("invalid params of type: %s" % type(params))
+    if not _distributed():
+        return
+    seen = {}
+    handles: List[Handle] = []
+    for name, p in items:
+        t = p.data if hasattr(p, "data") else p
+        if not torch.is_tensor(t):
+            continue
+        st = t.untyped_storage()
+        key = (st.data_ptr(), st.nbytes())
+        if st.nbytes() > 0 and key in seen:
+            continue
+        arena = getattr(p, "_gk_arena", None)
+        if arena is not None:
+            key = (arena.data_ptr(), arena.numel())
+            if key in seen:
+                continue
+            seen[key] = True
+            handles.append(broadcast_async_(arena, root_rank, name))
+            continue
+        seen[key] = True
+        if t.is_contiguous():
+            handles.append(broadcast_async_(t, root_rank, name))
+        else:
+            tmp = t.contiguous()
+            broadcast_(tmp, root_rank, name)
+            t.copy_(tmp)
+    for h in handles:
+        synchronize(h)
+
+
+def broadcast_optimizer_state(optimizer: torch.optim.Optimizer, root_rank: int = 0) -> None:
+    """Broadcast optimizer hyper-parameters and state from root (distributed_optimizer.py:620-736)."""
+    if not _distributed():
+        return
+    sd = optimizer.state_dict()
+    scalars = {"param_groups": [{k: v for k, v in g.items() if k != "params"} for g in sd["param_groups"]]}
+    scalars = broadcast_object(scalars, root_rank)
+    for g, src in zip(optimizer.param_groups, scalars["param_groups"]):
+        for k, v in src.items():
+            g[k] = v
+    for group in optimizer.param_groups:
+        for p in group["params"]:
+            st = optimizer.state.get(p, {})
+            flags = broadcast_object(sorted(k for k, v in st.items() if torch.is_tensor(v)), root_rank)
+            for k in flags:
+                if k not in st:
+                    st[k] = torch.zeros_like(p.data)
+                    optimizer.state[p] = st
+                broadcast_(st[k], root_rank)
+
+
+# ----------------------------------------------------------------------------
+# native RCCL engine
+# ----------------------------------------------------------------------------
+class RcclCommunicator:
+    """Own RCCL communicator (C++ ``gk::RcclComm``) bootstrapped through the
+    torch.distributed store.  Collectives run on the CALLER's current stream."""
+
+    def __init__(self, device: torch.device):
+        from .. import ops
+        cls = ops.rccl_engine_class()
+        self.engine = cls()
+        self.device = torch.device(device)
+        self.world = size()
+        self.rank = rank()
+        if self.rank == 0:
+            uid = cls.unique_id()
+        else:
+            uid = None
+        uid_list = broadcast_object(uid.tolist() if uid is not None else None, 0)
+        uid_t = torch.tensor(uid_list, dtype=torch.uint8)
+        self.engine.init(uid_t, self.rank, self.world, self.device.index or 0)
+
+    def allgather_(self, out: torch.Tensor, inp: torch.Tensor) -> None:
+        self.engine.allgather(inp, out)
+
+    def allreduce_(self, t: torch.Tensor, average: bool = True) -> None:
+        self.engine.allreduce(t, 1 if average else 0)
+
+    def broadcast_(self, t: torch.Tensor, root: int = 0) -> None:
+        self.engine.broadcast(t, root)
+
+    def destroy(self) -> None:
+        self.engine.destroy()
+
+
+class Exchanger:
+    """Stream-ordered fixed-size collectives used by the hot path.
+
+    backend 'rccl-native' -> RcclCommunicator, 'torch' -> torch.distributed,
+    'local' -> world of one (copies).  All calls are issued on the current
+    stream and return without blocking the host.
+    """
+
+    def __init__(self, device: torch.device, prefer_native: bool = True):
+        self.device = torch.device(device)
+        self.P = size()
+        self.native: Optional[RcclCommunicator] = None
+        self.kind = "local"
+        if self.P > 1:
+            self.kind = "torch"
+            if prefer_native and self.device.type == "cuda" and os.environ.get("GKSGD_NATIVE_RCCL", "1") == "1":
+                try:
+                    self.native = RcclCommunicator(self.device)
+                    self.kind = "rccl-native"
+                except Exception as e:  # pragma: no cover - GPU only
+                    from ..settings import logger
+                    logger.warning("native RCCL engine unavailable (%s); using torch.distributed", e)
+                    self.native = None
+
+    def allgather_(self, out: torch.Tensor, inp: torch.Tensor) -> None:
+        if self.kind == "local":
+            if out.data_ptr() != inp.data_ptr():
+                out.view(-1)[: inp.numel()].copy_(inp.view(-1))
+        elif self.native is not None:
+            self.native.allgather_(out, inp)
+        else:
+            allgather_into_(out, inp, async_op=False)
+
+    def allreduce_(self, t: torch.Tensor, average: bool = True) -> None:
+        if self.kind == "local":
+            return
+        if self.native is not None:
+            self.native.allreduce_(t, average)
+        else:
+            allreduce_(t, average)
+
+    def broadcast_(self, t: torch.Tensor, root: int = 0) -> None:
+        if self.kind == "local":
+            return
+        if self.native is not None:
+            self.native.broadcast_(t, root)
+        else:
+            broadcast_(t, root)

@@ -1,0 +1,301 @@
+"""Numerics of every HIP kernel against plain PyTorch fp32/fp64 references.
+
+Run on the MI355X box: ``pytest -m gpu``.
+"""
+import math
+
+import pytest
+import torch
+
+from gaussiank_sgd_amd import ops
+from gaussiank_sgd_amd.compression import reference
+from gaussiank_sgd_amd.utils.stats import gaussian_z
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(n, seed=0, dist="normal", scale=1e-3):
+    g = torch.Generator().manual_seed(seed)
+    if dist == "normal":
+        x = torch.randn(n, generator=g) * scale
+        r = torch.randn(n, generator=g) * scale * 0.3
+    else:
+        x = torch.distributions.StudentT(2.0).sample((n,)) * scale
+        r = torch.zeros(n)
+    return x, r
+
+
+def _run_both(x, r, mode, k, k_cap, ec=True, loops=3, z=0.0, seed=0, device=None):
+    gb, rb = ops.CompressBuffers(k_cap, device), ops.CompressBuffers(k_cap, "cpu")
+    xg, rg = x.clone().to(device), r.clone().to(device)
+    xc, rc = x.clone(), r.clone()
+    ops.compress_(xg, rg, gb, mode, ec=ec, zero_g=True, loops=loops, z=z, k=k, k_cap=k_cap, seed=seed)
+    ops.compress_(xc, rc, rb, mode, ec=ec, zero_g=True, loops=loops, z=z, k=k, k_cap=k_cap, seed=seed)
+    torch.cuda.synchronize()
+    return (xg.cpu(), rg.cpu(), gb.record.cpu(), gb.stats.cpu()), (xc, rc, rb.record, rb.stats)
+
+
+def _sel(rec, k_cap):
+    sent = int(rec[0])
+    idx = rec[4:4 + sent].long()
+    val = rec[4 + k_cap:4 + k_cap + sent].view(torch.float32)
+    return sent, int(rec[1]), idx, val
+
+
+@pytest.mark.parametrize("n", [1 << 20, 1_000_003, 4096 * 7 + 5, 100])
+@pytest.mark.parametrize("loops,ec", [(3, True), (5, False)])
+def test_gaussian_pipeline(cuda, n, loops, ec):
+    x, r = _pair(n, seed=n % 97)
+    ratio = 0.001 if n > 10000 else 0.05
+    k = max(int(n * ratio), 1)
+    k_cap = 2 * k
+    (xg, rg, recg, stg), (xc, rc, recc, stc) = _run_both(x, r, ops.MODE_GAUSSIAN, k, k_cap, ec, loops,
+                                                         gaussian_z(ratio), device=cuda)
+    acc = (x + r) if ec else x.clone()
+    # statistics vs torch
+    assert abs(float(stg[0]) - float(acc.double().mean())) < 1e-6 * max(1e-3, float(acc.abs().max()))
+    assert math.isclose(float(stg[1]), float(acc.double().std()), rel_tol=1e-5)
+    # gradient zeroed, selection consistent with the chosen threshold
+    assert float(xg.abs().sum()) == 0.0
+    sent, total, idx, val = _sel(recg, k_cap)
+    thr = float(recg[3:4].view(torch.float32))
+    mask = acc.abs() > thr
+    expect = mask.nonzero().view(-1)
+    assert total == int(mask.sum())
+    assert torch.equal(idx, expect[:sent])
+    assert torch.equal(val, acc[idx])
+    res_expect = acc.clone()
+    res_expect[idx] = 0
+    assert torch.equal(rg, res_expect)
+    # CPU mirror agrees on the decision (same candidate)
+    assert int(recg[2]) == int(recc[2])
+    assert abs(int(recg[1]) - int(recc[1])) <= max(2, total // 1000)
+
+
+def test_gaussian_matches_reference_oracle(cuda):
+    n = 1 << 18
+    x, r = _pair(n, seed=3)
+    ratio = 0.001
+    k = int(n * ratio)
+    bufs = ops.CompressBuffers(4 * k, cuda)
+    xg, rg = x.clone().to(cuda), r.clone().to(cuda)
+    ops.compress_(xg, rg, bufs, ops.MODE_GAUSSIAN, ec=True, zero_g=True, loops=3, z=gaussian_z(ratio), k=k,
+                  k_cap=4 * k)
+    torch.cuda.synchronize()
+    st = bufs.stats.cpu()
+    acc, idx, vals, res = reference.gaussian(x, r, ratio, loops=3, ec=True,
+                                             stats=(float(st[0]), float(st[1])))
+    sent, total, gidx, gval = _sel(bufs.record.cpu(), 4 * k)
+    assert total == idx.numel()
+    assert torch.equal(gidx, idx[:sent])
+    assert torch.equal(rg.cpu(), res) if sent == total else True
+
+
+@pytest.mark.parametrize("n", [1 << 20, 333_333])
+def test_topk_exact(cuda, n):
+    x, r = _pair(n, seed=5, dist="t")
+    k = max(int(n * 0.001), 1)
+    (xg, rg, recg, _), (xc, rc, recc, _) = _run_both(x, r, ops.MODE_TOPK, k, k, device=cuda)
+    acc = x + r
+    _, idx, vals, res = reference.topk_exact(x, r, 0.001)
+    sent, total, gidx, gval = _sel(recg, k)
+    assert sent == total == k
+    assert torch.equal(gidx, idx)
+    assert torch.equal(gval, acc[idx])
+    assert torch.equal(rg, res)
+    assert torch.equal(recg, recc)
+
+
+def test_topk_ties_lowest_index(cuda):
+    n = 50_000
+    x = torch.zeros(n)
+    x[::7] = 1.0  # many exact ties
+    r = torch.zeros(n)
+    k = 100
+    (xg, rg, recg, _), (xc, rc, recc, _) = _run_both(x, r, ops.MODE_TOPK, k, k, device=cuda)
+    sent, total, gidx, _ = _sel(recg, k)
+    assert sent == k
+    assert torch.equal(gidx, torch.arange(0, 7 * k, 7))
+    assert torch.equal(recg, recc)
+
+
+def test_randomk_hash_parity(cuda):
+    n = 500_000
+    x, r = _pair(n, seed=9)
+    k = 500
+    (xg, rg, recg, _), (xc, rc, recc, _) = _run_both(x, r, ops.MODE_RANDOMK, k, k, ec=False, seed=12345,
+                                                     device=cuda)
+    assert torch.equal(recg, recc)
+    sent, total, idx, _ = _sel(recg, k)
+    assert sent == k and idx.unique().numel() == k
+
+
+@pytest.mark.parametrize("mode", [ops.MODE_REDSYNC, ops.MODE_REDSYNCTRIM, ops.MODE_DGC])
+def test_threshold_modes_vs_mirror(cuda, mode):
+    n = 400_000
+    x, r = _pair(n, seed=11, dist="t")
+    k = 400
+    k_cap = 4 * k if mode != ops.MODE_REDSYNCTRIM else n
+    (xg, rg, recg, _), (xc, rc, recc, _) = _run_both(x, r, mode, k, k_cap, seed=77, device=cuda)
+    assert int(recg[2]) == int(recc[2])
+    assert abs(int(recg[1]) - int(recc[1])) <= 2
+    sent, total, idx, val = _sel(recg, k_cap)
+    acc = x + r
+    assert torch.equal(val, acc[idx])
+    assert bool((idx[1:] > idx[:-1]).all())
+
+
+def test_kcap_overflow_stays_in_residual(cuda):
+    n = 1 << 16
+    x, r = _pair(n, seed=13)
+    k_cap = 10
+    bufs = ops.CompressBuffers(k_cap, cuda)
+    xg, rg = x.clone().to(cuda), r.clone().to(cuda)
+    ops.compress_(xg, rg, bufs, ops.MODE_THRESHOLD, ec=True, zero_g=True, k=5, k_cap=k_cap, fixed_thr=0.0)
+    torch.cuda.synchronize()
+    sent, total, idx, val = _sel(bufs.record.cpu(), k_cap)
+    acc = x + r
+    nz = (acc.abs() > 0).nonzero().view(-1)
+    assert sent == k_cap and total == nz.numel()
+    assert torch.equal(idx, nz[:k_cap])
+    # conservation: acc == scatter(sent) + residual
+    rebuilt = rg.cpu().clone()
+    rebuilt[idx] += val
+    assert torch.equal(rebuilt, acc)
+
+
+@pytest.mark.parametrize("deterministic", [False, True])
+def test_scatter_add_unequal_counts_and_duplicates(cuda, deterministic):
+    n, P, k_cap = 100_000, 4, 3000
+    g = torch.Generator().manual_seed(1)
+    recs = torch.zeros(P, 4 + 2 * k_cap, dtype=torch.int32)
+    per_rank = []
+    for p in range(P):
+        cnt = 1000 + 500 * p
+        idx = torch.randperm(20_000, generator=g)[:cnt].sort().values  # overlapping index ranges
+        val = torch.randn(cnt, generator=g)
+        recs[p, 0] = cnt
+        recs[p, 4:4 + cnt] = idx.int()
+        recs[p, 4 + k_cap:4 + k_cap + cnt] = val.view(torch.int32)
+        per_rank.append((idx, val))
+    expect = reference.sparse_aggregate(n, per_rank, P)
+    dst = torch.zeros(n, device=cuda)
+    ops.scatter_add_records_(dst, recs.to(cuda), P, k_cap, 1.0 / P, deterministic)
+    torch.cuda.synchronize()
+    assert torch.allclose(dst.cpu(), expect, atol=1e-6, rtol=1e-5)
+    if deterministic:
+        dst2 = torch.zeros(n, device=cuda)
+        ops.scatter_add_records_(dst2, recs.to(cuda), P, k_cap, 1.0 / P, True)
+        assert torch.equal(dst, dst2)
+
+
+def test_fused_sgd_vs_torch(cuda):
+    torch.manual_seed(0)
+    shapes = [(64, 3, 3, 3), (64,), (1000, 64), (1000,), (7,)]
+    groups_cfg = [dict(lr=0.1, momentum=0.9, dampening=0.0, weight_decay=1e-4, nesterov=False),
+                  dict(lr=0.05, momentum=0.875, dampening=0.1, weight_decay=0.0, nesterov=False),
+                  dict(lr=0.02, momentum=0.9, dampening=0.0, weight_decay=5e-4, nesterov=True)]
+    assign = [0, 1, 0, 1, 2]
+    params = [torch.randn(s) for s in shapes]
+    ref_params = [p.clone().requires_grad_(True) for p in params]
+    opt = torch.optim.SGD([{"params": [ref_params[i] for i in range(5) if assign[i] == gi], **cfg}
+                           for gi, cfg in enumerate(groups_cfg)], lr=0.1)
+    pad = lambda n: (n + 63) // 64 * 64
+    offs, o = [], 0
+    for s in shapes:
+        offs.append(o)
+        o += pad(math.prod(s))
+    w = torch.zeros(o, device=cuda)
+    m = torch.zeros(o, device=cuda)
+    gr = torch.zeros(o, device=cuda)
+    for i, p in enumerate(params):
+        w[offs[i]:offs[i] + p.numel()] = p.view(-1).to(cuda)
+    chunks = ops.make_chunk_table([(offs[i], pad(params[i].numel()), assign[i], i) for i in range(5)], cuda)
+    for step in range(3):
+        grads = [torch.randn(s) for s in shapes]
+        for i, gg in enumerate(grads):
+            ref_params[i].grad = gg.clone()
+            gr[offs[i]:offs[i] + gg.numel()] = gg.view(-1).to(cuda)
+        opt.step()
+        hp = [dict(cfg, first_step=(step == 0)) for cfg in groups_cfg]
+        ops.fused_sgd_(w, m, gr, chunks, hp, zero_grad=True)
+        torch.cuda.synchronize()
+        assert float(gr.abs().sum()) == 0.0
+        for i, p in enumerate(ref_params):
+            got = w[offs[i]:offs[i] + p.numel()].cpu().view(p.shape)
+            assert torch.allclose(got, p.detach(), atol=1e-6, rtol=1e-5), (step, i)
+
+
+def test_fused_lars_vs_reference(cuda):
+    from gaussiank_sgd_amd.optim.lars import LARS
+    torch.manual_seed(1)
+    shapes = [(128, 64), (64,), (10, 128)]
+    params = [torch.randn(s).requires_grad_(True) for s in shapes]
+    opt = LARS(params, lr=0.1, momentum=0.9, weight_decay=5e-4, eeta=1e-3, epsilon=1e-5)
+    pad = lambda n: (n + 63) // 64 * 64
+    offs, o = [], 0
+    for s in shapes:
+        offs.append(o)
+        o += pad(math.prod(s))
+    w = torch.zeros(o, device=cuda)
+    m = torch.ones(o, device=cuda)
+    gr = torch.zeros(o, device=cuda)
+    for i, p in enumerate(params):
+        w[offs[i]:offs[i] + p.numel()] = p.detach().view(-1).to(cuda)
+    chunks = ops.make_chunk_table([(offs[i], pad(params[i].numel()), 0, i) for i in range(3)], cuda)
+    ss = torch.zeros(6, dtype=torch.float64, device=cuda)
+    hp = [dict(lr=0.1, momentum=0.9, weight_decay=5e-4, eeta=1e-3, epsilon=1e-5)]
+    for step in range(3):
+        for i, p in enumerate(params):
+            gg = torch.randn(p.shape)
+            p.grad = gg.clone()
+            gr[offs[i]:offs[i] + gg.numel()] = gg.view(-1).to(cuda)
+        opt.step()
+        ss.zero_()
+        ops.segmented_sumsq_(w, gr, chunks, ss)
+        ops.fused_lars_(w, m, gr, chunks, ss, hp)
+        torch.cuda.synchronize()
+        for i, p in enumerate(params):
+            got = w[offs[i]:offs[i] + p.numel()].cpu().view(p.shape)
+            assert torch.allclose(got, p.detach(), atol=1e-5, rtol=1e-5), (step, i)
+
+
+def test_clip_grad_norm(cuda):
+    x = torch.randn(300_001) * 3
+    g = x.clone().to(cuda)
+    norm = ops.clip_grad_norm_(g, 5.0)
+    torch.cuda.synchronize()
+    ref = x.clone()
+    rn = torch.nn.utils.clip_grad_norm_([torch.nn.Parameter(torch.zeros(1))], 1.0)  # API smoke
+    n = float(x.double().norm())
+    assert math.isclose(float(norm), n, rel_tol=1e-5)
+    assert torch.allclose(g.cpu(), ref * (5.0 / (n + 1e-6)), rtol=1e-5, atol=1e-7)
+
+
+def test_sign_bucket(cuda):
+    x = torch.randn(123_457)
+    res, means, pos = reference.sign_bucket_mean(x)
+    g = x.clone().to(cuda)
+    mask = torch.zeros(x.numel(), dtype=torch.uint8, device=cuda)
+    mm = torch.zeros(2, device=cuda)
+    ops.sign_bucket_compress_(g, mask, mm, ops.sign_bucket_ws(cuda))
+    torch.cuda.synchronize()
+    assert torch.allclose(mm.cpu(), means, rtol=1e-5, atol=1e-7)
+    assert torch.equal(mask.cpu().bool(), pos)
+    assert torch.allclose(g.cpu(), res, atol=1e-6)
+    ops.sign_bucket_decompress_(g, mask, mm)
+    torch.cuda.synchronize()
+    assert torch.allclose(g.cpu(), x, atol=1e-6)
+
+
+def test_rccl_engine_world1(cuda):
+    cls = ops.rccl_engine_class()
+    e = cls()
+    e.init(cls.unique_id(), 0, 1, 0)
+    t = torch.arange(10, dtype=torch.float32, device=cuda)
+    out = torch.zeros(10, device=cuda)
+    e.allgather(t, out)
+    e.allreduce(t, 1)
+    torch.cuda.synchronize()
+    assert torch.equal(out, t)
+    e.destroy()
