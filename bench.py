@@ -75,7 +75,7 @@ def main() -> int:
     rank = comm.rank()
     if not ops.load():
         raise RuntimeError("native extension missing: run `python -m gaussiank_sgd_amd.ops.build`")
-    torch.backends.cudnn.benchmark = True
+    torch.backends.cudnn.benchmark = os.environ.get("GKSGD_CUDNN_BENCHMARK", "0") == "1"
 
     dataset = "imagenet" if args.model in ("resnet50", "resnet18", "resnet34", "resnet101", "resnet152",
                                            "vgg16i") else None
