@@ -3,7 +3,7 @@
 // Ops are registered under the `gksgd` namespace (torch.ops.gksgd.*) and run
 // asynchronously on the current HIP stream of the tensors' device.
 #include <ATen/ATen.h>
-#include <c10/hip/HIPGuard.h>
+#include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/custom_class.h>
 #include <torch/library.h>
@@ -54,7 +54,7 @@ void compress(at::Tensor g, at::Tensor r, at::Tensor ctrl, at::Tensor ws, at::Te
   TORCH_CHECK(loops >= 1 && loops * (loops + 1) / 2 <= gk::kMaxCand, "loops out of range");
   TORCH_CHECK((reinterpret_cast<uintptr_t>(ctrl.data_ptr()) & 7) == 0, "ctrl must be 8-byte aligned");
   TORCH_CHECK((reinterpret_cast<uintptr_t>(ws.data_ptr()) & 255) == 0, "ws must be 256-byte aligned");
-  c10::hip::HIPGuard guard(g.device());
+  c10::DeviceGuard guard(g.device());
   gk::CompressArgs a;
   a.g = g.data_ptr<float>();
   a.r = r.data_ptr<float>();
@@ -87,7 +87,7 @@ void tensor_stats(at::Tensor x, at::Tensor ctrl, at::Tensor ws) {
   check_dev(ctrl, "ctrl");
   check_dev(ws, "ws");
   TORCH_CHECK(ctrl.nbytes() >= sizeof(gk::GkCtrl), "ctrl buffer too small");
-  c10::hip::HIPGuard guard(x.device());
+  c10::DeviceGuard guard(x.device());
   gk::tensor_stats(x.data_ptr<float>(), x.numel(), ctrl.data_ptr(), ws.data_ptr(), cur_stream(x));
 }
 
@@ -100,14 +100,14 @@ void scatter_add_records(at::Tensor dst, at::Tensor records, int64_t P, int64_t 
   check_dev(records, "records");
   TORCH_CHECK(records.scalar_type() == at::kInt, "records must be int32");
   TORCH_CHECK(records.numel() >= P * (4 + 2 * k_cap), "records too small for P x (4 + 2 k_cap)");
-  c10::hip::HIPGuard guard(dst.device());
+  c10::DeviceGuard guard(dst.device());
   gk::scatter_add_records(dst.data_ptr<float>(), dst.numel(), records.data_ptr<int32_t>(), (int)P, k_cap,
                           (float)scale, deterministic ? 1 : 0, cur_stream(dst));
 }
 
 void fill_zero(at::Tensor dst) {
   check_f32(dst, "dst");
-  c10::hip::HIPGuard guard(dst.device());
+  c10::DeviceGuard guard(dst.device());
   gk::fill_zero(dst.data_ptr<float>(), dst.numel(), cur_stream(dst));
 }
 
@@ -120,7 +120,7 @@ void sign_bucket_compress(at::Tensor x, at::Tensor mask, at::Tensor means, at::T
   check_dev(ws, "ws");
   TORCH_CHECK(mask.scalar_type() == at::kByte && mask.numel() >= x.numel(), "mask must be uint8[n]");
   TORCH_CHECK(means.numel() >= 2, "means needs 2 floats");
-  c10::hip::HIPGuard guard(x.device());
+  c10::DeviceGuard guard(x.device());
   gk::sign_bucket_compress(x.data_ptr<float>(), x.numel(), mask.data_ptr<uint8_t>(), means.data_ptr<float>(),
                            ws.data_ptr(), cur_stream(x));
 }
@@ -129,7 +129,7 @@ void sign_bucket_decompress(at::Tensor x, at::Tensor mask, at::Tensor means) {
   check_f32(x, "x");
   check_dev(mask, "mask");
   check_f32(means, "means");
-  c10::hip::HIPGuard guard(x.device());
+  c10::DeviceGuard guard(x.device());
   gk::sign_bucket_decompress(x.data_ptr<float>(), x.numel(), mask.data_ptr<uint8_t>(), means.data_ptr<float>(),
                              cur_stream(x));
 }
@@ -187,7 +187,7 @@ void fused_sgd(at::Tensor w, c10::optional<at::Tensor> m, at::Tensor g, at::Tens
     check_f32(*grad_scale, "grad_scale");
     a.grad_scale = grad_scale->data_ptr<float>();
   }
-  c10::hip::HIPGuard guard(w.device());
+  c10::DeviceGuard guard(w.device());
   gk::fused_sgd(a, cur_stream(w));
 }
 
@@ -197,7 +197,7 @@ void segmented_sumsq(at::Tensor w, at::Tensor g, at::Tensor chunks, at::Tensor o
   check_chunks(chunks);
   check_dev(out, "out");
   TORCH_CHECK(out.scalar_type() == at::kDouble, "out must be float64[2*nseg]");
-  c10::hip::HIPGuard guard(w.device());
+  c10::DeviceGuard guard(w.device());
   gk::segmented_sumsq(w.data_ptr<float>(), g.data_ptr<float>(),
                       reinterpret_cast<const gk::Chunk*>(chunks.data_ptr<int64_t>()), (int)(chunks.numel() / 2),
                       out.data_ptr<double>(), cur_stream(w));
@@ -228,7 +228,7 @@ void fused_lars(at::Tensor w, at::Tensor m, at::Tensor g, at::Tensor chunks, at:
     a.epsilon[i] = (float)epsilon[i];
   }
   a.ngroups = (int)ng;
-  c10::hip::HIPGuard guard(w.device());
+  c10::DeviceGuard guard(w.device());
   gk::fused_lars(a, cur_stream(w));
 }
 
@@ -238,7 +238,7 @@ void clip_grad_norm(at::Tensor g, double max_norm, at::Tensor ws, at::Tensor coe
   check_f32(coef, "coef");
   check_f32(norm, "norm");
   TORCH_CHECK(ws.scalar_type() == at::kDouble && ws.numel() >= 1024, "ws must be float64[>=1024]");
-  c10::hip::HIPGuard guard(g.device());
+  c10::DeviceGuard guard(g.device());
   gk::clip_grad_norm(g.data_ptr<float>(), g.numel(), (float)max_norm, ws.data_ptr<double>(), coef.data_ptr<float>(),
                      norm.data_ptr<float>(), cur_stream(g));
 }
@@ -281,20 +281,20 @@ struct RcclEngine : torch::CustomClassHolder {
     check_dev(send, "send");
     check_dev(recv, "recv");
     TORCH_CHECK(recv.nbytes() == send.nbytes() * (size_t)comm.world(), "recv must be world x send bytes");
-    c10::hip::HIPGuard guard(send.device());
+    c10::DeviceGuard guard(send.device());
     comm.allgather_bytes(send.data_ptr(), recv.data_ptr(), send.nbytes(), cur_stream(send));
   }
 
   void allreduce(at::Tensor t, int64_t op) {
     check_dev(t, "t");
-    c10::hip::HIPGuard guard(t.device());
+    c10::DeviceGuard guard(t.device());
     ncclRedOp_t o = op == 0 ? ncclSum : (op == 1 ? ncclAvg : (op == 2 ? ncclMax : ncclMin));
     comm.allreduce(t.data_ptr(), (size_t)t.numel(), to_nccl(t.scalar_type()), o, cur_stream(t));
   }
 
   void broadcast(at::Tensor t, int64_t root) {
     check_dev(t, "t");
-    c10::hip::HIPGuard guard(t.device());
+    c10::DeviceGuard guard(t.device());
     comm.broadcast(t.data_ptr(), (size_t)t.numel(), to_nccl(t.scalar_type()), (int)root, cur_stream(t));
   }
 

@@ -232,31 +232,25 @@ def broadcast_parameters(params, root_rank: int = 0) -> None:
         raise ValueError("invalid params of type: %s" % type(params))
     if not _distributed():
         return
-    seen = {}
+    seen = set()
     handles: List[Handle] = []
     for name, p in items:
         t = p.data if hasattr(p, "data") else p
-        if not torch.is_tensor(t):
+        if not torch.is_tensor(t) or t.numel() == 0:
             continue
         st = t.untyped_storage()
         key = (st.data_ptr(), st.nbytes())
-        if st.nbytes() > 0 and key in seen:
+        if key in seen:
             continue
-        arena = getattr(p, "_gk_arena", None)
-        if arena is not None:
-            key = (arena.data_ptr(), arena.numel())
-            if key in seen:
-                continue
-            seen[key] = True
-            handles.append(broadcast_async_(arena, root_rank, name))
-            continue
-        seen[key] = True
-        if t.is_contiguous():
-            handles.append(broadcast_async_(t, root_rank, name))
+        seen.add(key)
+        # Tensors that are views of one storage (our flat arenas) are broadcast
+        # as ONE flat tensor over the whole storage.
+        n = st.nbytes() // t.element_size()
+        if t.is_contiguous() and t.storage_offset() == 0 and t.numel() == n:
+            flat = t
         else:
-            tmp = t.contiguous()
-            broadcast_(tmp, root_rank, name)
-            t.copy_(tmp)
+            flat = t.new_empty(0).set_(st, 0, (n,), (1,))
+        handles.append(broadcast_async_(flat, root_rank, name))
     for h in handles:
         synchronize(h)
 

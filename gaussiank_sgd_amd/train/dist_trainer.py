@@ -1,0 +1,181 @@
+"""Distributed training entry point (``ssgd``) with the reference's CLI.
+
+Parity: reference dist_trainer.py:23-136 -- same flags and defaults
+(``--batch-size --nsteps-update --nworkers --nwpernode --dataset --dnn
+--data-dir --saved-dir --lr --max-epochs --pretrain --num-steps --compressor
+--density --threshold``), same log directory naming
+(``logs/allreduce-<prefix>-thres-<thr/1024>kbytes/<dnn>-n<P>-bs<B>-lr<lr>-ns<n>-ds<d>``),
+per-rank log file ``<host>-<rank>.log``, the epoch/iteration loop with
+gradient accumulation (``optimizer.local``), clip-after-synchronize for
+LSTMs, and the throughput line ``Time per iteration including communication:
+%f, Speed: %f images/s``.
+
+Launch one process per GPU: ``torchrun --nproc-per-node N -m
+gaussiank_sgd_amd.train.dist_trainer ...`` (or mpirun: OMPI_* variables are
+understood).  New flags: ``--synthetic`` (always on: no datasets offline),
+``--amp bf16``, ``--channels-last``, ``--density-warmup/--no-density-warmup``,
+``--deterministic``, ``--max-iters``, ``--compress-single-rank``.
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import os
+import time
+
+import numpy as np
+import torch
+
+from .. import settings, utils
+from ..compression import compressors
+from ..parallel import distributed_optimizer as hvd
+from ..settings import formatter, logger
+from .trainer import DLTrainer, _support_datasets, _support_dnns
+
+
+def ssgd(dnn, dataset, data_dir, nworkers, lr, batch_size, nsteps_update, max_epochs, nwpernode, pretrain,
+         num_steps, compressor, density, threshold, gradient_path=None, amp=None, channels_last=False,
+         density_warmup=True, deterministic=False, max_iters=None, compress_single_rank=False, saved_dir="."):
+    rank = hvd.rank()
+    device = "cpu"
+    if torch.cuda.is_available():
+        torch.cuda.set_device(hvd.local_rank() % torch.cuda.device_count())
+        device = "cuda"
+    if rank != 0:
+        pretrain = None
+    trainer = DLTrainer(rank, nworkers, dist=False, batch_size=batch_size, is_weak_scaling=True, ngpus=1,
+                        data_dir=data_dir, dataset=dataset, dnn=dnn, lr=lr, nworkers=nworkers, prefix="allreduce",
+                        pretrain=pretrain, num_steps=num_steps, device=device, amp=amp,
+                        channels_last=channels_last, seed=rank, weights_dir=os.path.join(saved_dir, "weights"))
+    init = torch.tensor([trainer.get_train_epoch(), trainer.get_train_iter()], dtype=torch.int64,
+                        device=trainer.device)
+    init = hvd.broadcast(init, root_rank=0)
+    trainer.set_train_epoch(int(init[0]))
+    trainer.set_train_iter(int(init[1]))
+    is_sparse = density < 1
+
+    if settings.ADAPTIVE_MERGE or settings.ADAPTIVE_SPARSE:
+        from ..utils.profiler import benchmark
+        seq_layernames, layerwise_times, layerwise_sizes = benchmark(trainer)
+        layerwise_times = hvd.broadcast_object(list(layerwise_times), 0)
+        if rank == 0:
+            logger.info("layerwise backward times: %s", list(layerwise_times))
+            logger.info("layerwise backward sizes: %s", list(layerwise_sizes))
+        logger.info("Bencharmked backward time: %f", float(np.sum(layerwise_times)))
+        logger.info("Model size: %d", int(np.sum(layerwise_sizes)))
+    else:
+        seq_layernames, layerwise_times = None, None
+
+    norm_clip = None
+    if dnn == "lstm":
+        norm_clip = 0.25
+    elif dnn == "lstman4":
+        norm_clip = 400
+
+    optimizer = hvd.DistributedOptimizer(trainer.optimizer, named_parameters=trainer.net.named_parameters(),
+                                         compression=compressors[compressor], is_sparse=is_sparse, density=density,
+                                         seq_layernames=seq_layernames, layerwise_times=layerwise_times,
+                                         norm_clip=None, threshold=threshold, writer=None,
+                                         gradient_path=gradient_path, density_warmup=density_warmup,
+                                         deterministic=deterministic, compress_single_rank=compress_single_rank)
+    if getattr(trainer, "_pending_compression", None):
+        optimizer.load_compression_state(trainer._pending_compression)
+    hvd.broadcast_parameters(trainer.net.state_dict(), root_rank=0)
+    trainer.update_optimizer(optimizer)
+    iters_per_epoch = max(1, trainer.get_num_of_training_samples() // (nworkers * batch_size * nsteps_update))
+    times = []
+    logger.info("max_epochs: %d", max_epochs)
+    display = 40 if iters_per_epoch > 40 else max(1, iters_per_epoch - 1)
+    done = 0
+    for epoch in range(max_epochs):
+        hidden = None
+        if dnn == "lstm":
+            hidden = trainer.net.init_hidden()
+        for i in range(iters_per_epoch):
+            s = time.time()
+            optimizer.zero_grad()
+            for j in range(nsteps_update):
+                optimizer.local = j < nsteps_update - 1 and nsteps_update > 1
+                if dnn == "lstm":
+                    _, hidden = trainer.train(1, hidden=hidden)
+                else:
+                    trainer.train(1)
+            if norm_clip is not None:
+                optimizer.synchronize()
+                optimizer.clip_grad_norm_(norm_clip)
+            trainer.update_model()
+            times.append(time.time() - s)
+            if i % display == 0 and i > 0:
+                if trainer.is_cuda:
+                    torch.cuda.synchronize()
+                time_per_iter = float(np.mean(times))
+                logger.warning("Time per iteration including communication: %f, Speed: %f images/s", time_per_iter,
+                               batch_size * nsteps_update / time_per_iter)
+                times = []
+            done += 1
+            if max_iters is not None and done >= max_iters:
+                optimizer.increase_one_epoch()
+                return trainer, optimizer
+        optimizer.increase_one_epoch()
+    return trainer, optimizer
+
+
+def build_parser():
+    p = argparse.ArgumentParser(description="AllReduce trainer")
+    p.add_argument("--batch-size", type=int, default=32)
+    p.add_argument("--nsteps-update", type=int, default=1)
+    p.add_argument("--nworkers", type=int, default=None, help="defaults to the launched world size")
+    p.add_argument("--nwpernode", type=int, default=1, help="Number of workers per node")
+    p.add_argument("--dataset", type=str, default="imagenet", choices=_support_datasets)
+    p.add_argument("--dnn", type=str, default="resnet50", choices=_support_dnns)
+    p.add_argument("--data-dir", type=str, default="./data")
+    p.add_argument("--saved-dir", type=str, default=".")
+    p.add_argument("--lr", type=float, default=0.1)
+    p.add_argument("--max-epochs", type=int, default=settings.MAX_EPOCHS)
+    p.add_argument("--pretrain", type=str, default=None)
+    p.add_argument("--num-steps", type=int, default=35)
+    p.add_argument("--compressor", type=str, default="gaussian", choices=[k for k in compressors if k])
+    p.add_argument("--density", type=float, default=1)
+    p.add_argument("--threshold", type=int, default=524288000)
+    # MI355X build additions
+    p.add_argument("--amp", type=str, default=None, choices=[None, "bf16", "fp16"])
+    p.add_argument("--channels-last", action="store_true")
+    p.add_argument("--no-density-warmup", action="store_true")
+    p.add_argument("--deterministic", action="store_true")
+    p.add_argument("--compress-single-rank", action="store_true")
+    p.add_argument("--max-iters", type=int, default=None)
+    p.add_argument("--logdir-root", type=str, default="./logs")
+    return p
+
+
+def main(argv=None):
+    args = build_parser().parse_args(argv)
+    hvd.init()
+    nworkers = args.nworkers or hvd.size()
+    batch_size = args.batch_size * args.nsteps_update
+    prefix = settings.PREFIX
+    if args.density < 1:
+        prefix = "comp-" + args.compressor + "-" + prefix
+    logdir = "allreduce-%s-thres-%dkbytes/%s-n%d-bs%d-lr%.4f-ns%d-ds%s" % (
+        prefix, args.threshold / 1024, args.dnn, nworkers, batch_size, args.lr, args.nsteps_update, str(args.density))
+    relative_path = os.path.join(args.logdir_root, logdir)
+    utils.create_path(relative_path)
+    gradient_path = None
+    if settings.LOGGING_GRADIENTS:
+        gradient_path = "%s/gradients/%s" % (args.saved_dir, logdir)
+        utils.create_path(gradient_path)
+    rank = hvd.rank()
+    logfile = os.path.join(relative_path, settings.hostname + "-" + str(rank) + ".log")
+    hdlr = logging.FileHandler(logfile)
+    hdlr.setFormatter(formatter)
+    logger.addHandler(hdlr)
+    logger.info("Configurations: %s", args)
+    return ssgd(args.dnn, args.dataset, args.data_dir, nworkers, args.lr, args.batch_size, args.nsteps_update,
+                args.max_epochs, args.nwpernode, args.pretrain, args.num_steps, args.compressor, args.density,
+                args.threshold, gradient_path, amp=args.amp, channels_last=args.channels_last,
+                density_warmup=not args.no_density_warmup, deterministic=args.deterministic,
+                max_iters=args.max_iters, compress_single_rank=args.compress_single_rank, saved_dir=args.saved_dir)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,157 @@
+"""CPU tests: the torch mirror of the fused pipeline vs the reference-semantics
+oracles, record layout, conservation, and the compressor registry API."""
+import math
+
+import pytest
+import torch
+
+from gaussiank_sgd_amd import ops
+from gaussiank_sgd_amd.compression import compressors, reference
+from gaussiank_sgd_amd.utils.stats import gaussian_z, gen_threshold_from_normal_distribution, norm_ppf
+
+
+def _mirror(x, r, mode, k, k_cap, ec=True, loops=3, z=0.0, seed=0, fixed=0.0):
+    b = ops.CompressBuffers(k_cap, "cpu")
+    g, rr = x.clone(), r.clone()
+    ops.compress_(g, rr, b, mode, ec=ec, zero_g=True, loops=loops, z=z, k=k, k_cap=k_cap, seed=seed,
+                  fixed_thr=fixed)
+    rec = b.record
+    sent = int(rec[0])
+    return g, rr, rec, rec[4:4 + sent].long(), rec[4 + k_cap:4 + k_cap + sent].view(torch.float32), b
+
+
+def test_norm_ppf_matches_scipy():
+    stats = pytest.importorskip("scipy.stats")
+    for p in [1e-9, 1e-4, 0.0005, 0.01, 0.3, 0.5, 0.9, 0.999]:
+        assert abs(norm_ppf(p) - float(stats.norm.ppf(p))) < 1e-12 * max(1, abs(norm_ppf(p))) + 1e-14
+
+
+def test_gaussian_threshold_selfcheck():
+    # reference compression.py:757-777: recover a 3-sigma threshold from its p-value
+    g = torch.Generator().manual_seed(0)
+    d = torch.randn(200_000, generator=g, dtype=torch.float64) * 0.5
+    std, mean = float(d.std()), float(d.mean())
+    thres = 3 * std
+    pvalue = 1 - float((d.abs() >= thres).sum()) / d.numel()
+    _, right = gen_threshold_from_normal_distribution(pvalue, mean, std)
+    assert abs(right - thres) / thres < 0.03
+
+
+@pytest.mark.parametrize("loops,ec", [(3, True), (5, False)])
+@pytest.mark.parametrize("dist", ["normal", "t"])
+def test_gaussian_mirror_equals_reference(loops, ec, dist):
+    g = torch.Generator().manual_seed(1)
+    n = 100_000
+    if dist == "normal":
+        x = torch.randn(n, generator=g) * 1e-2
+    else:
+        x = torch.distributions.StudentT(2.0).sample((n,)) * 1e-2
+    r = torch.randn(n, generator=g) * 1e-3
+    ratio = 0.001
+    k = int(n * ratio)
+    _, rr, rec, idx, val, b = _mirror(x, r, ops.MODE_GAUSSIAN, k, n, ec, loops, gaussian_z(ratio))
+    st = b.stats
+    acc, ridx, rval, rres = reference.gaussian(x, r, ratio, loops=loops, ec=ec,
+                                               stats=(float(st[0]), float(st[1])))
+    assert torch.equal(idx, ridx)
+    assert torch.equal(val, rval)
+    assert torch.equal(rr, rres)
+
+
+def test_topk_mirror_equals_exact_and_torch_topk_set():
+    g = torch.Generator().manual_seed(2)
+    n = 50_000
+    x = torch.randn(n, generator=g)
+    r = torch.zeros(n)
+    k = 50
+    _, rr, rec, idx, val, _ = _mirror(x, r, ops.MODE_TOPK, k, k)
+    _, tidx = torch.topk(x.abs(), k)
+    assert set(idx.tolist()) == set(tidx.tolist())
+    assert bool((idx[1:] > idx[:-1]).all())
+
+
+@pytest.mark.parametrize("mode", ["redsync", "redsynctrim"])
+def test_redsync_mirror_vs_reference(mode):
+    g = torch.Generator().manual_seed(3)
+    n = 80_000
+    x = torch.distributions.StudentT(3.0).sample((n,))
+    r = torch.zeros(n)
+    k = 80
+    m = ops.MODE_REDSYNC if mode == "redsync" else ops.MODE_REDSYNCTRIM
+    _, rr, rec, idx, val, _ = _mirror(x, r, m, k, n)
+    fn = reference.redsync if mode == "redsync" else reference.redsynctrim
+    _, ridx, _, _ = fn(x, r, 0.001)
+    # thresholds are computed from fp32 mean/max that can differ by 1 ulp: allow +-1 element
+    assert abs(idx.numel() - ridx.numel()) <= 1
+    assert len(set(idx.tolist()) ^ set(ridx.tolist())) <= 1
+
+
+def test_conservation_and_cap():
+    g = torch.Generator().manual_seed(4)
+    n = 10_000
+    x = torch.randn(n, generator=g)
+    r = torch.randn(n, generator=g) * 0.1
+    k_cap = 7
+    _, rr, rec, idx, val, _ = _mirror(x, r, ops.MODE_THRESHOLD, 5, k_cap, fixed=1.0)
+    acc = x + r
+    assert int(rec[0]) == k_cap and int(rec[1]) == int((acc.abs() > 1.0).sum())
+    rebuilt = rr.clone()
+    rebuilt[idx] += val
+    assert torch.equal(rebuilt, acc)
+
+
+def test_dgc_mirror_semantics():
+    g = torch.Generator().manual_seed(5)
+    n = 200_000
+    x = torch.randn(n, generator=g)
+    r = torch.zeros(n)
+    k = 200
+    _, rr, rec, idx, val, _ = _mirror(x, r, ops.MODE_DGC, k, 4 * k, seed=42)
+    total = int(rec[1])
+    assert 0 < total <= math.ceil(4 * k / 3) or total == k
+
+
+def test_scatter_cpu_unequal_counts():
+    P, k_cap, n = 3, 10, 50
+    recs = torch.zeros(P, 4 + 2 * k_cap, dtype=torch.int32)
+    per = []
+    for p in range(P):
+        cnt = 3 + 2 * p
+        idx = torch.arange(cnt) * 2
+        val = torch.full((cnt,), float(p + 1))
+        recs[p, 0] = cnt
+        recs[p, 4:4 + cnt] = idx.int()
+        recs[p, 4 + k_cap:4 + k_cap + cnt] = val.view(torch.int32)
+        per.append((idx, val))
+    dst = torch.zeros(n)
+    ops.scatter_add_records_(dst, recs, P, k_cap, 1.0 / P)
+    assert torch.allclose(dst, reference.sparse_aggregate(n, per, P))
+
+
+def test_registry_api_compat():
+    for name in ["topk", "topk2", "gaussian", "gaussian2", "randomk", "randomkec", "dgcsampling", "redsync",
+                 "redsynctrim", "topk_legacy"]:
+        c = compressors[name]
+        c.clear()
+        t = torch.randn(5000)
+        orig = t.clone()
+        out, idx, vals = c.compress(t, "layer", ratio=0.01)
+        assert out is t
+        assert idx.dtype == torch.int64 and vals.numel() == idx.numel() > 0
+        assert torch.equal(vals, t[idx])
+        if getattr(c, "ec", False) or name == "topk_legacy":
+            assert torch.equal(t, orig)  # first call: residual was zero
+        res = c.residuals["layer"]
+        assert float(res[idx].abs().sum()) == 0.0
+    t = torch.randn(100)
+    out, ctx, means = compressors["bucket"].compress(t.clone(), "b")
+    assert ctx is None and means.numel() == 2
+    out, ctx, sel = compressors["none"].compress(t, "n")
+    assert sel is t
+
+
+def test_topk_legacy_is_uniform_101():
+    t = torch.randn(20_000)
+    _, idx, _, _ = reference.uniform_abs_topk(t, None, 0.001, ec=False)
+    sorted_index = t.abs().argsort()
+    assert torch.equal(idx, sorted_index[::101][-20:])

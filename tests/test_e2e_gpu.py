@@ -50,7 +50,8 @@ def test_resnet20_gaussian_loss_decreases(cuda):
         losses.append(t.current_loss())
     assert losses[-1] < losses[0]
     counts = opt._collect_selected()
-    assert len(counts) == 30 and all(c > 0 for c in counts)
+    nb = len(opt.arena.buckets)
+    assert len(counts) == 30 * nb and sum(counts) > 0
 
 
 def test_resnet50_step_bf16(cuda):
