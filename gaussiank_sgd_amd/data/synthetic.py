@@ -38,6 +38,8 @@ DATASETS = {
     "mnist32": DatasetSpec("mnist32", (1, 32, 32), 10, 60000, 10000, "image"),
     "ptb": DatasetSpec("ptb", (35,), 10000, 929589, 82430, "tokens"),
     "wikipedia": DatasetSpec("wikipedia", (512,), 30522, 1000000, 10000, "mlm"),
+    # AN4 spectrograms: 161 frequency bins x ~2 s of 10 ms frames, 29 characters (CTC blank = 0)
+    "an4": DatasetSpec("an4", (1, 161, 200), 29, 948, 130, "speech"),
 }
 
 
@@ -77,6 +79,15 @@ class SyntheticData:
             if channels_last and x.dim() == 4:
                 x = x.contiguous(memory_format=torch.channels_last)
             return x, y.to(self.device)
+        if s.kind == "speech":
+            x = torch.randn((B,) + s.shape, generator=g)
+            T = s.shape[-1]
+            in_lens = torch.randint(T // 2, T + 1, (B,), generator=g)
+            in_lens[0] = T
+            tgt_lens = torch.randint(5, 25, (B,), generator=g)
+            targets = torch.randint(1, s.num_classes, (int(tgt_lens.sum()),), generator=g)
+            return x.to(self.device, dtype), (targets.to(self.device), tgt_lens.to(self.device),
+                                              in_lens.to(self.device))
         if s.kind == "tokens":
             T = self.seq_len
             if self.learnable:

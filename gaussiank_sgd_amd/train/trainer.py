@@ -98,6 +98,8 @@ class DLTrainer:
         self.average_iter = 0
         if self.dnn.startswith("bert"):
             self.criterion = MaskedLMLoss()
+        elif self.dnn == "lstman4":
+            self.criterion = nn.CTCLoss(blank=0, reduction="sum", zero_infinity=True)
         else:
             self.criterion = nn.CrossEntropyLoss()
         weight_decay = 1e-4
@@ -235,6 +237,11 @@ class DLTrainer:
             elif self.dnn.startswith("bert"):
                 outputs = self.net(inputs)
                 loss = self.criterion(outputs, labels)
+            elif self.dnn == "lstman4":
+                targets, tgt_lens, in_lens = labels
+                outputs, out_lens = self.net(inputs, in_lens)
+                logp = outputs.float().log_softmax(-1).transpose(0, 1)  # T x N x C
+                loss = self.criterion(logp, targets, out_lens, tgt_lens) / inputs.size(0)
             else:
                 outputs = self.net(inputs)
                 loss = self.criterion(outputs.float(), labels)
@@ -280,7 +287,7 @@ class DLTrainer:
             inputs, labels = d[0], d[1]
             if inputs.device != self.device:
                 inputs = inputs.to(self.device, non_blocking=True)
-                labels = labels.to(self.device, non_blocking=True)
+                labels = labels.to(self.device, non_blocking=True) if torch.is_tensor(labels) else labels
             self.iotime += time.time() - ss
             sf = time.time()
             outputs, loss, hidden = self.forward_loss(inputs, labels, hidden)
@@ -325,7 +332,7 @@ class DLTrainer:
             if self.dnn == "lstm":
                 costs += float(loss) * self.num_steps
                 steps += self.num_steps
-            elif not self.dnn.startswith("bert"):
+            elif not self.dnn.startswith("bert") and self.dnn != "lstman4":
                 k5 = min(5, outputs.shape[1])
                 a1, a5 = self.cal_accuracy(outputs.float(), labels, topk=(1, k5))
                 top1.append(float(a1))
@@ -333,6 +340,8 @@ class DLTrainer:
         test_loss = float(np.mean(losses)) if losses else 0.0
         if self.dnn == "lstm":
             acc, acc5 = float(np.exp(costs / max(1, steps))), 0.0
+        elif self.dnn == "lstman4":
+            acc, acc5 = test_loss, 0.0
         elif self.dnn.startswith("bert"):
             acc, acc5 = float(np.exp(test_loss)), 0.0
         else:

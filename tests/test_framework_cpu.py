@@ -1,0 +1,174 @@
+"""CPU tests of the framework plumbing: buckets/arena, planners, schedules,
+density warm-up, checkpoint/resume (with residuals + momentum), the CLI entry
+point, layer-wise profiler, evaluation and the log-parsing plot tool."""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from gaussiank_sgd_amd.compression import compressors
+from gaussiank_sgd_amd.parallel import distributed_optimizer as hvd
+from gaussiank_sgd_amd.parallel.buckets import GradArena, group_with_threshold
+from gaussiank_sgd_amd.parallel.planner import models_for, plan_mgs, plan_mgwfbp
+from gaussiank_sgd_amd.train import DLTrainer
+from gaussiank_sgd_amd.train import schedules
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_group_with_threshold_reference_rule():
+    keys = ["a", "b", "c", "d"]
+    sizes = {"a": 10, "b": 20, "c": 30, "d": 40}
+    assert group_with_threshold(keys, sizes, 0) == [["d"], ["c"], ["b"], ["a"]]
+    assert group_with_threshold(keys, sizes, 65) == [["d", "c"], ["b", "a"]]
+    assert group_with_threshold(keys, sizes, 524288000) == [["d", "c", "b", "a"]]
+
+
+def test_arena_views_and_alignment():
+    net = torch.nn.Sequential(torch.nn.Linear(7, 5), torch.nn.Linear(5, 3))
+    named = list(net.named_parameters())
+    keys = [k for k, _ in named]
+    arena = GradArena(named, group_with_threshold(keys, {k: p.numel() for k, p in named}, 10 ** 9))
+    for k, p in named:
+        assert p.data.data_ptr() == arena.weight_views[k].data_ptr()
+        assert p.grad.data_ptr() == arena.grad_views[k].data_ptr()
+        assert (p.data.data_ptr() - arena.weights.data_ptr()) % 256 == 0
+    x = torch.randn(4, 7)
+    net(x).sum().backward()
+    assert float(arena.grads.abs().sum()) > 0
+    b = arena.buckets[0]
+    assert b.numel == sum(p.numel() for _, p in named)
+    assert b.span % 64 == 0
+
+
+def test_planners_produce_partitions():
+    names = ["l%d" % i for i in range(8)]
+    sizes = [1000, 200000, 5000, 300000, 100, 4000000, 10, 25000]
+    times = [1e-4, 3e-4, 1e-4, 5e-4, 1e-5, 2e-3, 1e-5, 2e-4]
+    for P in (2, 8):
+        ar, alpha, ct, ag = models_for(P, 0.001, "mi355x")
+        g1, _ = plan_mgwfbp(names, times, sizes, ar, alpha)
+        g2, _ = plan_mgs(names, times, sizes, ct, ag)
+        for groups in (g1, g2):
+            flat = [k for g in groups for k in g]
+            assert sorted(flat) == sorted(names) and len(flat) == len(names)
+            assert flat[0] == "l7"  # backward order
+        ar, alpha, ct, ag = models_for(P, 0.001, "reference")
+        g3, _ = plan_mgs(names, times, sizes, ct, ag)
+        assert sorted(k for g in g3 for k in g) == sorted(names)
+
+
+def test_lr_schedules():
+    assert schedules.general_lr(0.1, 10, 0, 100, "cifar10", warmup=False) == 0.1
+    assert abs(schedules.general_lr(0.1, 90, 0, 100, "cifar10", warmup=False) - 0.01) < 1e-12
+    assert abs(schedules.general_lr(0.1, 35, 0, 100, "imagenet", warmup=False) - 0.01) < 1e-12
+    w0 = schedules.general_lr(0.1, 0, 0, 100, "cifar10", warmup=True)
+    w1 = schedules.general_lr(0.1, 2, 250, 100, "cifar10", warmup=True)
+    assert w0 == pytest.approx(0.1 / 500) and w0 < w1 < 0.1
+    assert schedules.lstm_ptb_lr(22.0, 70) == pytest.approx(22.0 * 0.01)
+    s = schedules.AN4Schedule(1.0)
+    assert s(0) == 1.0 and s(1) == pytest.approx(1 / 1.01)
+
+
+def _trainer(tmp, comp="gaussian", density=0.01, **kw):
+    torch.manual_seed(0)
+    hvd.init()
+    t = DLTrainer(0, 1, dnn="fcn5net", dataset="mnist", batch_size=16, lr=0.1, device="cpu", learnable_data=True,
+                  weights_dir=str(tmp), **kw)
+    opt = hvd.DistributedOptimizer(t.optimizer, named_parameters=t.net.named_parameters(),
+                                   compression=compressors[comp], is_sparse=True, density=density,
+                                   compress_single_rank=True)
+    t.update_optimizer(opt)
+    return t, opt
+
+
+def test_density_warmup_schedule(tmp_path):
+    t, opt = _trainer(tmp_path)
+    assert opt.get_current_density() == 0.015625
+    opt.increase_one_epoch()
+    assert opt.get_current_density() == 0.004
+    opt.increase_one_epoch()
+    opt.increase_one_epoch()
+    assert opt.get_current_density() == 0.001
+
+
+def test_gradient_accumulation_local_steps(tmp_path):
+    t, opt = _trainer(tmp_path)
+    w0 = opt.arena.weights.clone()
+    opt.zero_grad()
+    opt.local = True
+    t.train(1)
+    assert all(b.ready == 0 for b in opt.arena.buckets)  # no exchange on local steps
+    opt.local = False
+    t.train(1)
+    t.update_model()
+    assert not torch.equal(w0, opt.arena.weights)
+
+
+def test_checkpoint_resume_roundtrip(tmp_path):
+    t, opt = _trainer(tmp_path)
+    for _ in range(3):
+        opt.zero_grad()
+        t.train(1)
+        t.update_model()
+    st = t.checkpoint_state()
+    fn = os.path.join(str(tmp_path), "ck.pth")
+    t.save_checkpoint(st, fn)
+    res0 = opt.arena.residuals.clone()
+    mom0 = opt.arena.momentum.clone()
+    w0 = opt.arena.weights.clone()
+    t2, opt2 = _trainer(tmp_path)
+    t2.load_model_from_file(fn)
+    assert torch.equal(opt2.arena.weights, w0)
+    assert torch.equal(opt2.arena.momentum, mom0)
+    assert torch.equal(opt2.arena.residuals, res0)
+    assert t2.train_iter == t.train_iter
+    # both continue identically
+    for tt, oo in ((t, opt), (t2, opt2)):
+        oo.zero_grad()
+        tt.train(1, data=t.data.test_batches(1)[0])
+        tt.update_model()
+    assert torch.allclose(opt.arena.weights, opt2.arena.weights, atol=1e-7)
+    ck = torch.load(fn, weights_only=True)
+    assert {"iter", "epoch", "state"} <= set(ck)
+
+
+def test_layerwise_profiler(tmp_path):
+    from gaussiank_sgd_amd.utils.profiler import benchmark
+    t, _ = _trainer(tmp_path)
+    keys, times, sizes = benchmark(t, warmup=1, iterations=3)
+    assert keys == [k for k, _ in t.net.named_parameters()]
+    assert len(times) == len(keys) and all(x >= 0 for x in times)
+    assert sizes == [p.numel() for p in t.net.parameters()]
+
+
+def test_dist_trainer_cli_and_plot(tmp_path):
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    cmd = [sys.executable, "-m", "gaussiank_sgd_amd.train.dist_trainer", "--dnn", "fcn5net", "--dataset", "mnist",
+           "--batch-size", "32", "--density", "0.01", "--compressor", "gaussian", "--max-epochs", "1",
+           "--max-iters", "45", "--compress-single-rank", "--logdir-root", str(tmp_path / "logs"),
+           "--saved-dir", str(tmp_path)]
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=300, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "Speed:" in r.stderr
+    logs = []
+    for d, _, fs in os.walk(tmp_path / "logs"):
+        logs += [os.path.join(d, f) for f in fs if f.endswith(".log")]
+    assert logs
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import plot
+    data = plot.read_log(logs[0])
+    assert data["speed"] and data["selected"]
+
+
+def test_evaluate_checkpoints(tmp_path):
+    from gaussiank_sgd_amd.train.evaluate import evaluate
+    t, _ = _trainer(tmp_path)
+    d = t.checkpoint_dir()
+    for e in (1, 2):
+        t.train_epoch = e
+        t.save_checkpoint(t.checkpoint_state(), os.path.join(d, "fcn5net-rank0-epoch%d.pth" % e))
+    best, ep, res = evaluate("fcn5net", "mnist", d, 3, batch_size=16, device="cpu", num_batches=1)
+    assert set(res) == {1, 2} and ep in (1, 2)
