@@ -9,7 +9,9 @@ MI355X notes: run with ``memory_format=torch.channels_last`` and bf16
 autocast so MIOpen picks its NHWC implicit-GEMM (MFMA) convolutions; the
 final BN of every bottleneck is zero-initialised (``zero_init_residual``) as
 is standard for large-batch data-parallel training (off by default for
-parity).
+parity).  Every BatchNorm is a ``BNAct`` (ops/bn.py): BN + residual add +
+ReLU run as fused gfx950 kernels in training (same parameters/state_dict
+keys as nn.BatchNorm2d; plain torch ops on CPU / in eval).
 """
 from __future__ import annotations
 
@@ -17,6 +19,8 @@ from typing import List, Optional, Type, Union
 
 import torch
 import torch.nn as nn
+
+from ..ops.bn import BNAct
 
 
 def conv3x3(inp: int, out: int, stride: int = 1, groups: int = 1, dilation: int = 1) -> nn.Conv2d:
@@ -33,17 +37,15 @@ class BasicBlock(nn.Module):
     def __init__(self, inplanes, planes, stride=1, downsample=None, groups=1, base_width=64):
         super().__init__()
         self.conv1 = conv3x3(inplanes, planes, stride)
-        self.bn1 = nn.BatchNorm2d(planes)
-        self.relu = nn.ReLU(inplace=True)
+        self.bn1 = BNAct(planes, act="relu")
         self.conv2 = conv3x3(planes, planes)
-        self.bn2 = nn.BatchNorm2d(planes)
+        self.bn2 = BNAct(planes, act="relu")
         self.downsample = downsample
 
     def forward(self, x):
         identity = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.bn2(self.conv2(out))
-        return self.relu(out + identity)
+        out = self.bn1(self.conv1(x))
+        return self.bn2(self.conv2(out), identity)
 
 
 class Bottleneck(nn.Module):
@@ -53,20 +55,18 @@ class Bottleneck(nn.Module):
         super().__init__()
         width = int(planes * (base_width / 64.0)) * groups
         self.conv1 = conv1x1(inplanes, width)
-        self.bn1 = nn.BatchNorm2d(width)
+        self.bn1 = BNAct(width, act="relu")
         self.conv2 = conv3x3(width, width, stride, groups)
-        self.bn2 = nn.BatchNorm2d(width)
+        self.bn2 = BNAct(width, act="relu")
         self.conv3 = conv1x1(width, planes * self.expansion)
-        self.bn3 = nn.BatchNorm2d(planes * self.expansion)
-        self.relu = nn.ReLU(inplace=True)
+        self.bn3 = BNAct(planes * self.expansion, act="relu")
         self.downsample = downsample
 
     def forward(self, x):
         identity = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.relu(self.bn2(self.conv2(out)))
-        out = self.bn3(self.conv3(out))
-        return self.relu(out + identity)
+        out = self.bn1(self.conv1(x))
+        out = self.bn2(self.conv2(out))
+        return self.bn3(self.conv3(out), identity)
 
 
 class ResNet(nn.Module):
@@ -78,8 +78,7 @@ class ResNet(nn.Module):
         self.groups = groups
         self.base_width = width_per_group
         self.conv1 = nn.Conv2d(3, 64, kernel_size=7, stride=2, padding=3, bias=False)
-        self.bn1 = nn.BatchNorm2d(64)
-        self.relu = nn.ReLU(inplace=True)
+        self.bn1 = BNAct(64, act="relu")
         self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
         self.layer1 = self._make_layer(block, 64, layers[0])
         self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
@@ -91,7 +90,7 @@ class ResNet(nn.Module):
         for m in self.modules():
             if isinstance(m, nn.Conv2d):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
-            elif isinstance(m, nn.BatchNorm2d):
+            elif isinstance(m, nn.BatchNorm2d):  # includes BNAct
                 nn.init.ones_(m.weight)
                 nn.init.zeros_(m.bias)
         if zero_init_residual:
@@ -105,7 +104,7 @@ class ResNet(nn.Module):
         downsample = None
         if stride != 1 or self.inplanes != planes * block.expansion:
             downsample = nn.Sequential(conv1x1(self.inplanes, planes * block.expansion, stride),
-                                       nn.BatchNorm2d(planes * block.expansion))
+                                       BNAct(planes * block.expansion))
         layers = [block(self.inplanes, planes, stride, downsample, self.groups, self.base_width)]
         self.inplanes = planes * block.expansion
         for _ in range(1, blocks):
@@ -113,7 +112,7 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.maxpool(self.bn1(self.conv1(x)))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)

@@ -33,6 +33,7 @@ HIP_SOURCES = [
     "kernels/compress.hip",
     "kernels/scatter.hip",
     "kernels/optim.hip",
+    "kernels/bn_act.hip",
 ]
 CXX_SOURCES = [
     "comm/rccl_engine.cpp",

@@ -244,6 +244,92 @@ void clip_grad_norm(at::Tensor g, double max_norm, at::Tensor ws, at::Tensor coe
 }
 
 // ---------------------------------------------------------------------------
+// fused batch norm + add + relu (channels-last)
+// ---------------------------------------------------------------------------
+int64_t channels_of(const at::Tensor& x) { return x.dim() == 4 ? x.size(1) : x.size(-1); }
+
+void check_cl(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  if (t.dim() == 4) {
+    TORCH_CHECK(t.is_contiguous(at::MemoryFormat::ChannelsLast), name, " must be channels_last contiguous");
+  } else {
+    TORCH_CHECK(t.dim() == 2 && t.is_contiguous(), name, " must be 4-D channels_last or 2-D [M, C]");
+  }
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kFloat, name, " must be bf16 or fp32");
+}
+
+const float* opt_f32(const c10::optional<at::Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->is_cuda(), "expected fp32 GPU tensor");
+  return t->data_ptr<float>();
+}
+
+float* opt_f32_mut(const c10::optional<at::Tensor>& t) { return const_cast<float*>(opt_f32(t)); }
+
+int64_t bn_workspace_floats(int64_t M, int64_t C, int64_t elem_bytes) {
+  return (int64_t)gk::bn_workspace_floats(M, (int)C, (int)elem_bytes);
+}
+
+bool bn_supported(int64_t C, int64_t elem_bytes) { return gk::bn_supported((int)C, (int)elem_bytes); }
+
+void bn_act_forward(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, c10::optional<at::Tensor> w,
+                    c10::optional<at::Tensor> b, c10::optional<at::Tensor> run_mean,
+                    c10::optional<at::Tensor> run_var, at::Tensor save_mean, at::Tensor save_invstd,
+                    at::Tensor scale, at::Tensor shift, at::Tensor ws, double eps, double momentum, bool relu) {
+  check_cl(x, "x");
+  check_cl(y, "y");
+  const int64_t C = channels_of(x);
+  const int64_t M = x.numel() / C;
+  const int eb = x.element_size();
+  TORCH_CHECK(gk::bn_supported((int)C, eb), "channel count not supported by the fused kernel");
+  TORCH_CHECK(y.scalar_type() == x.scalar_type() && y.numel() == x.numel(), "y must match x");
+  const void* rp = nullptr;
+  if (res.has_value() && res->defined()) {
+    check_cl(*res, "residual");
+    TORCH_CHECK(res->scalar_type() == x.scalar_type() && res->numel() == x.numel(), "residual must match x");
+    rp = res->data_ptr();
+  }
+  for (const at::Tensor* t : {&save_mean, &save_invstd, &scale, &shift})
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->numel() >= C && t->is_cuda(), "stat buffers: fp32[C]");
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() >= (int64_t)gk::bn_workspace_floats(M, (int)C, eb),
+              "workspace too small");
+  c10::DeviceGuard guard(x.device());
+  gk::bn_act_forward(x.data_ptr(), rp, y.data_ptr(), M, (int)C, eb, opt_f32(w), opt_f32(b), (float)eps,
+                     (float)momentum, opt_f32_mut(run_mean), opt_f32_mut(run_var), save_mean.data_ptr<float>(),
+                     save_invstd.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(),
+                     ws.data_ptr<float>(), relu ? 1 : 0, cur_stream(x));
+}
+
+void bn_act_backward(at::Tensor dy, c10::optional<at::Tensor> y, at::Tensor x, at::Tensor dx,
+                     c10::optional<at::Tensor> dres, c10::optional<at::Tensor> w, at::Tensor mean, at::Tensor invstd,
+                     at::Tensor dgamma, at::Tensor dbeta, at::Tensor ws, bool relu) {
+  check_cl(dy, "dy");
+  check_cl(x, "x");
+  check_cl(dx, "dx");
+  const int64_t C = channels_of(x);
+  const int64_t M = x.numel() / C;
+  const int eb = x.element_size();
+  TORCH_CHECK(dy.scalar_type() == x.scalar_type() && dx.scalar_type() == x.scalar_type(), "dtype mismatch");
+  const void* yp = nullptr;
+  if (relu) {
+    TORCH_CHECK(y.has_value() && y->defined(), "relu backward needs y");
+    check_cl(*y, "y");
+    yp = y->data_ptr();
+  }
+  void* rp = nullptr;
+  if (dres.has_value() && dres->defined()) {
+    check_cl(*dres, "dres");
+    rp = dres->data_ptr();
+  }
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() >= (int64_t)gk::bn_workspace_floats(M, (int)C, eb),
+              "workspace too small");
+  c10::DeviceGuard guard(x.device());
+  gk::bn_act_backward(dy.data_ptr(), yp, x.data_ptr(), dx.data_ptr(), rp, M, (int)C, eb, opt_f32(w),
+                      mean.data_ptr<float>(), invstd.data_ptr<float>(), dgamma.data_ptr<float>(),
+                      dbeta.data_ptr<float>(), ws.data_ptr<float>(), relu ? 1 : 0, cur_stream(x));
+}
+
+// ---------------------------------------------------------------------------
 // RCCL engine (torch custom class)
 // ---------------------------------------------------------------------------
 ncclDataType_t to_nccl(at::ScalarType t) {
@@ -330,6 +416,16 @@ TORCH_LIBRARY(gksgd, m) {
       "float[] momentum, float[] weight_decay, float[] eeta, float[] epsilon) -> ()");
   m.def("clip_grad_norm(Tensor(a!) g, float max_norm, Tensor(b!) ws, Tensor(c!) coef, Tensor(d!) norm) -> ()");
 
+  m.def("bn_workspace_floats(int M, int C, int elem_bytes) -> int", &bn_workspace_floats);
+  m.def("bn_supported(int C, int elem_bytes) -> bool", &bn_supported);
+  m.def(
+      "bn_act_forward(Tensor x, Tensor? res, Tensor(a!) y, Tensor? w, Tensor? b, Tensor(b!)? run_mean, "
+      "Tensor(c!)? run_var, Tensor(d!) save_mean, Tensor(e!) save_invstd, Tensor(f!) scale, Tensor(g!) shift, "
+      "Tensor(h!) ws, float eps, float momentum, bool relu) -> ()");
+  m.def(
+      "bn_act_backward(Tensor dy, Tensor? y, Tensor x, Tensor(a!) dx, Tensor(b!)? dres, Tensor? w, Tensor mean, "
+      "Tensor invstd, Tensor(c!) dgamma, Tensor(d!) dbeta, Tensor(e!) ws, bool relu) -> ()");
+
   m.class_<RcclEngine>("RcclEngine")
       .def(torch::init<>())
       .def_static("unique_id", &RcclEngine::unique_id)
@@ -355,4 +451,6 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("segmented_sumsq", &segmented_sumsq);
   m.impl("fused_lars", &fused_lars);
   m.impl("clip_grad_norm", &clip_grad_norm);
+  m.impl("bn_act_forward", &bn_act_forward);
+  m.impl("bn_act_backward", &bn_act_backward);
 }

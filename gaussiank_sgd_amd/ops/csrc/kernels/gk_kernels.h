@@ -150,4 +150,17 @@ void fused_lars(const LarsArgs& a, hipStream_t stream);
 void clip_grad_norm(float* g, int64_t n, float max_norm, double* ws, float* coef_out,
                     float* norm_out, hipStream_t stream);
 
+// ---------------------------------------------------------------------------
+// Fused batch norm (training) + residual add + ReLU, channels-last [M, C].
+// elem_bytes: 2 (bf16) or 4 (fp32).  ws: bn_workspace_floats() floats.
+// ---------------------------------------------------------------------------
+size_t bn_workspace_floats(int64_t M, int C, int elem_bytes);
+bool bn_supported(int C, int elem_bytes);
+void bn_act_forward(const void* x, const void* res, void* y, int64_t M, int C, int elem_bytes, const float* w,
+                    const float* b, float eps, float momentum, float* run_mean, float* run_var, float* save_mean,
+                    float* save_invstd, float* scale, float* shift, float* ws, int relu, hipStream_t stream);
+void bn_act_backward(const void* dy, const void* y, const void* x, void* dx, void* dres, int64_t M, int C,
+                     int elem_bytes, const float* w, const float* mean, const float* invstd, float* dgamma,
+                     float* dbeta, float* ws, int relu, hipStream_t stream);
+
 }  // namespace gk

@@ -1,0 +1,71 @@
+"""Fused BN + residual + ReLU kernels vs nn.BatchNorm2d + add + relu (fp32 reference)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from gaussiank_sgd_amd.ops.bn import BNAct
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(8, 64, 14, 14), (4, 256, 7, 7), (2, 2048, 3, 3), (3, 96, 5, 5)])
+@pytest.mark.parametrize("relu,res", [(True, True), (True, False), (False, False)])
+def test_bnact_matches_torch(cuda, dtype, shape, relu, res):
+    torch.manual_seed(0)
+    N, C, H, W = shape
+    bn = BNAct(C, act="relu" if relu else None).to(cuda)
+    ref = torch.nn.BatchNorm2d(C).to(cuda)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+        ref.weight.copy_(bn.weight)
+        ref.bias.copy_(bn.bias)
+    x0 = (torch.randn(shape, device=cuda) * 2 + 0.3).to(dtype).contiguous(memory_format=torch.channels_last)
+    r0 = torch.randn(shape, device=cuda).to(dtype).contiguous(memory_format=torch.channels_last) if res else None
+    g0 = torch.randn(shape, device=cuda).to(dtype).contiguous(memory_format=torch.channels_last)
+    x = x0.clone().requires_grad_(True)
+    r = r0.clone().requires_grad_(True) if res else None
+    y = bn(x, r)
+    y.backward(g0)
+    xr = x0.float().clone().requires_grad_(True)
+    rr = r0.float().clone().requires_grad_(True) if res else None
+    yr = ref(xr)
+    if res:
+        yr = yr + rr
+    if relu:
+        yr = F.relu(yr)
+    yr.backward(g0.float())
+    tol = dict(atol=2e-2, rtol=2e-2) if dtype == torch.bfloat16 else dict(atol=1e-4, rtol=1e-4)
+    assert y.dtype == dtype and y.is_contiguous(memory_format=torch.channels_last)
+    assert torch.allclose(y.float(), yr, **tol)
+    assert torch.allclose(x.grad.float(), xr.grad, **(dict(atol=5e-2, rtol=5e-2) if dtype == torch.bfloat16 else tol))
+    if res:
+        assert torch.allclose(r.grad.float(), rr.grad, **tol)
+    assert torch.allclose(bn.weight.grad, ref.weight.grad, rtol=2e-2 if dtype == torch.bfloat16 else 1e-4,
+                          atol=2e-1 if dtype == torch.bfloat16 else 1e-3)
+    assert torch.allclose(bn.bias.grad, ref.bias.grad, rtol=2e-2 if dtype == torch.bfloat16 else 1e-4,
+                          atol=2e-1 if dtype == torch.bfloat16 else 1e-3)
+    assert torch.allclose(bn.running_mean, ref.running_mean, atol=1e-3, rtol=1e-3)
+    assert torch.allclose(bn.running_var, ref.running_var, atol=1e-3, rtol=1e-3)
+    assert int(bn.num_batches_tracked) == 1
+
+
+def test_resnet50_fused_vs_unfused(cuda):
+    from gaussiank_sgd_amd.models import resnet50
+    from gaussiank_sgd_amd.ops.bn import BNAct
+    torch.manual_seed(0)
+    m1 = resnet50(num_classes=10).to(cuda).to(memory_format=torch.channels_last)
+    m2 = resnet50(num_classes=10).to(cuda).to(memory_format=torch.channels_last)
+    m2.load_state_dict(m1.state_dict())
+    for m in m2.modules():
+        if isinstance(m, BNAct):
+            m.fused = False
+    x = torch.randn(4, 3, 64, 64, device=cuda).contiguous(memory_format=torch.channels_last)
+    y1 = m1(x)
+    y2 = m2(x)
+    assert torch.allclose(y1, y2, atol=1e-3, rtol=1e-3)
+    y1.sum().backward()
+    y2.sum().backward()
+    for (n, p1), (_, p2) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert torch.allclose(p1.grad, p2.grad, atol=1e-2, rtol=1e-2), n
