@@ -143,6 +143,42 @@ __global__ __launch_bounds__(kBlock) void bn_stats_kernel(const T* __restrict__ 
   }
 }
 
+// Per-channel reduction of the [gy][C] partials: a workgroup owns kFinC
+// channels; its 256 threads split the gy rows 8 ways (coalesced 128-B reads),
+// then combine the 8 partial sums in fp64 through LDS.
+constexpr int kFinC = 32;
+constexpr int kFinParts = kBlock / kFinC;
+
+__device__ __forceinline__ void reduce_partials2(const float* __restrict__ pa, const float* __restrict__ pb, int gy,
+                                                 int C, double* out_a, double* out_b, bool* owner, int* c_out) {
+  __shared__ double sh[2][kFinParts][kFinC];
+  const int cl = threadIdx.x % kFinC;
+  const int part = threadIdx.x / kFinC;
+  const int c = blockIdx.x * kFinC + cl;
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+    for (int j = part; j < gy; j += kFinParts) {
+      a += pa[(int64_t)j * C + c];
+      b += pb[(int64_t)j * C + c];
+    }
+  }
+  sh[0][part][cl] = a;
+  sh[1][part][cl] = b;
+  __syncthreads();
+  *owner = part == 0 && c < C;
+  *c_out = c;
+  if (part == 0) {
+    double sa = 0.0, sb = 0.0;
+#pragma unroll
+    for (int p = 0; p < kFinParts; ++p) {
+      sa += sh[0][p][cl];
+      sb += sh[1][p][cl];
+    }
+    *out_a = sa;
+    *out_b = sb;
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void bn_finalize_kernel(const float* __restrict__ psum,
                                                              const float* __restrict__ psq, int gy, int64_t M, int C,
                                                              const float* __restrict__ w, const float* __restrict__ b,
@@ -150,13 +186,11 @@ __global__ __launch_bounds__(kBlock) void bn_finalize_kernel(const float* __rest
                                                              float* __restrict__ run_var, float* __restrict__ save_mean,
                                                              float* __restrict__ save_invstd, float* __restrict__ scale,
                                                              float* __restrict__ shift) {
-  const int c = blockIdx.x * kBlock + threadIdx.x;
-  if (c >= C) return;
   double s = 0.0, q = 0.0;
-  for (int j = 0; j < gy; ++j) {
-    s += psum[(int64_t)j * C + c];
-    q += psq[(int64_t)j * C + c];
-  }
+  bool owner;
+  int c;
+  reduce_partials2(psum, psq, gy, C, &s, &q, &owner, &c);
+  if (!owner) return;
   const double mean = s / (double)M;
   double var = q / (double)M - mean * mean;
   if (var < 0.0) var = 0.0;
@@ -259,13 +293,11 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const T* __restri
 __global__ __launch_bounds__(kBlock) void bn_bwd_finalize_kernel(const float* __restrict__ pdb,
                                                                  const float* __restrict__ pdg, int gy, int C,
                                                                  float* __restrict__ dbeta, float* __restrict__ dgamma) {
-  const int c = blockIdx.x * kBlock + threadIdx.x;
-  if (c >= C) return;
   double a = 0.0, b = 0.0;
-  for (int j = 0; j < gy; ++j) {
-    a += pdb[(int64_t)j * C + c];
-    b += pdg[(int64_t)j * C + c];
-  }
+  bool owner;
+  int c;
+  reduce_partials2(pdb, pdg, gy, C, &a, &b, &owner, &c);
+  if (!owner) return;
   dbeta[c] = (float)a;
   dgamma[c] = (float)b;
 }
@@ -315,7 +347,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(const T* __restric
   }
 }
 
-constexpr int kTargetBlocks = 2048;
+constexpr int kTargetBlocks = 1024;
 
 }  // namespace
 
@@ -337,7 +369,7 @@ void bn_forward_t(const T* x, const T* res, T* y, int64_t M, int C, const float*
   float* psum = ws;
   float* psq = ws + (int64_t)g.gy * C;
   hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(g.gx, g.gy), dim3(kBlock), 0, s, x, M, C, g, psum, psq);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + kBlock - 1) / kBlock), dim3(kBlock), 0, s, psum, psq, g.gy, M, C,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(kBlock), 0, s, psum, psq, g.gy, M, C,
                      w, b, eps, momentum, run_mean, run_var, save_mean, save_invstd, scale, shift);
   if (relu && res)
     hipLaunchKernelGGL((bn_apply_kernel<T, true, true>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, x, res, y, M, C, g,
@@ -366,7 +398,7 @@ void bn_backward_t(const T* dy, const T* y, const T* x, T* dx, T* dres, int64_t 
   else
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, dy, y, x, M, C, g,
                        mean, invstd, pdb, pdg);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kBlock - 1) / kBlock), dim3(kBlock), 0, s, pdb, pdg, g.gy, C,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(kBlock), 0, s, pdb, pdg, g.gy, C,
                      dbeta, dgamma);
 #define GK_BWD_APPLY(R, D)                                                                                       \
   hipLaunchKernelGGL((bn_bwd_apply_kernel<T, R, D>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, dy, y, x, dx, dres, M, \

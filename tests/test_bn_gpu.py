@@ -52,20 +52,27 @@ def test_bnact_matches_torch(cuda, dtype, shape, relu, res):
 
 
 def test_resnet50_fused_vs_unfused(cuda):
+    """Whole-network gradients: fused (fp32) error vs an fp64 reference must be
+    no worse than MIOpen's (fp32) error -- deep BN stacks amplify rounding, so
+    the comparison is relative to the vendor path, not absolute."""
     from gaussiank_sgd_amd.models import resnet50
     from gaussiank_sgd_amd.ops.bn import BNAct
     torch.manual_seed(0)
     m1 = resnet50(num_classes=10).to(cuda).to(memory_format=torch.channels_last)
     m2 = resnet50(num_classes=10).to(cuda).to(memory_format=torch.channels_last)
+    m3 = resnet50(num_classes=10).to(cuda).double().to(memory_format=torch.channels_last)
     m2.load_state_dict(m1.state_dict())
-    for m in m2.modules():
+    m3.load_state_dict(m1.state_dict())
+    for m in list(m2.modules()) + list(m3.modules()):
         if isinstance(m, BNAct):
             m.fused = False
-    x = torch.randn(4, 3, 64, 64, device=cuda).contiguous(memory_format=torch.channels_last)
-    y1 = m1(x)
-    y2 = m2(x)
-    assert torch.allclose(y1, y2, atol=1e-3, rtol=1e-3)
-    y1.sum().backward()
-    y2.sum().backward()
-    for (n, p1), (_, p2) in zip(m1.named_parameters(), m2.named_parameters()):
-        assert torch.allclose(p1.grad, p2.grad, atol=1e-2, rtol=1e-2), n
+    x = torch.randn(8, 3, 96, 96, device=cuda).contiguous(memory_format=torch.channels_last)
+    ys = [m1(x), m2(x), m3(x.double())]
+    for y in ys:
+        y.sum().backward()
+    assert torch.allclose(ys[0].double(), ys[2], atol=1e-3, rtol=1e-3)
+    for (n, p1), (_, p2), (_, p3) in zip(m1.named_parameters(), m2.named_parameters(), m3.named_parameters()):
+        ref = p3.grad
+        e_fused = float((p1.grad.double() - ref).norm() / (ref.norm() + 1e-30))
+        e_vendor = float((p2.grad.double() - ref).norm() / (ref.norm() + 1e-30))
+        assert e_fused <= 3 * e_vendor + 1e-4, (n, e_fused, e_vendor)
