@@ -36,6 +36,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch-size", type=int, default=int(os.environ.get("GKSGD_BENCH_BS", "256")))
+    ap.add_argument("--cudnn-benchmark", action="store_true", help="MIOpen find (exhaustive conv algorithm search)")
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--compressor", default="gaussian")
     ap.add_argument("--density", type=float, default=0.001)
@@ -75,7 +76,7 @@ def main() -> int:
     rank = comm.rank()
     if not ops.load():
         raise RuntimeError("native extension missing: run `python -m gaussiank_sgd_amd.ops.build`")
-    torch.backends.cudnn.benchmark = os.environ.get("GKSGD_CUDNN_BENCHMARK", "0") == "1"
+    torch.backends.cudnn.benchmark = args.cudnn_benchmark or os.environ.get("GKSGD_CUDNN_BENCHMARK", "0") == "1"
 
     dataset = "imagenet" if args.model in ("resnet50", "resnet18", "resnet34", "resnet101", "resnet152",
                                            "vgg16i") else None

@@ -144,9 +144,10 @@ __global__ __launch_bounds__(kBlock) void bn_stats_kernel(const T* __restrict__ 
 }
 
 // Per-channel reduction of the [gy][C] partials: a workgroup owns kFinC
-// channels; its 256 threads split the gy rows 8 ways (coalesced 128-B reads),
-// then combine the 8 partial sums in fp64 through LDS.
-constexpr int kFinC = 32;
+// channels; its 256 threads split the gy rows kFinParts ways and keep 8 loads
+// in flight per thread (the partials are L2-resident; an un-pipelined loop is
+// latency-bound), then combine the partial sums in fp64 through LDS.
+constexpr int kFinC = 16;
 constexpr int kFinParts = kBlock / kFinC;
 
 __device__ __forceinline__ void reduce_partials2(const float* __restrict__ pa, const float* __restrict__ pb, int gy,
@@ -157,7 +158,21 @@ __device__ __forceinline__ void reduce_partials2(const float* __restrict__ pa, c
   const int c = blockIdx.x * kFinC + cl;
   double a = 0.0, b = 0.0;
   if (c < C) {
-    for (int j = part; j < gy; j += kFinParts) {
+    int j = part;
+    for (; j + 7 * kFinParts < gy; j += 8 * kFinParts) {
+      float va[8], vb[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        va[u] = pa[(int64_t)(j + u * kFinParts) * C + c];
+        vb[u] = pb[(int64_t)(j + u * kFinParts) * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        a += va[u];
+        b += vb[u];
+      }
+    }
+    for (; j < gy; j += kFinParts) {
       a += pa[(int64_t)j * C + c];
       b += pb[(int64_t)j * C + c];
     }

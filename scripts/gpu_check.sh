@@ -28,6 +28,9 @@ fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
   step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 5 --warmup 3
 fi
+if [ "$MODE" = find ]; then
+  step bench_find 900 python bench.py --steps 20 --warmup 10 --cudnn-benchmark --json-out $OUT/bench_find.json
+fi
 if [ "$MODE" = sweep ]; then
   for bs in ${SWEEP_BS:-128 512}; do
     step bench_bs$bs 600 python bench.py --steps 20 --warmup 10 --batch-size $bs --json-out $OUT/bench_bs$bs.json
