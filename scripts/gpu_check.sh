@@ -30,6 +30,9 @@ if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
 fi
 if [ "$MODE" = find ]; then
   step bench_find 900 python bench.py --steps 20 --warmup 10 --cudnn-benchmark --json-out $OUT/bench_find.json
+  mkdir -p $OUT/tuning && cp -r tuning/miopen $OUT/tuning/ && ls -la $OUT/tuning/miopen ~/.cache/miopen 2>/dev/null | head -20
+  du -sh ~/.cache/miopen 2>/dev/null || true
+  step bench_after_find 600 python bench.py --steps 20 --warmup 10 --json-out $OUT/bench_after_find.json
 fi
 if [ "$MODE" = sweep ]; then
   for bs in ${SWEEP_BS:-128 512}; do
