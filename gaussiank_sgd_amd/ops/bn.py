@@ -5,7 +5,8 @@ state_dict keys) whose ``forward(x, residual=None)`` computes
 ``act(bn(x) + residual)``.  In training mode on the GPU, with a
 channels-last bf16/fp32 input, it runs the gfx950 kernels of
 ``csrc/kernels/bn_act.hip`` (3 launches forward, 3 backward, ReLU mask and
-residual gradient folded into the BN passes).  Everywhere else (CPU, eval,
+residual gradient folded into the BN passes; the ReLU mask is kept as one
+bit per element instead of saving the output).  Everywhere else (CPU, eval,
 NCHW input) it falls back to ``F.batch_norm`` + add + relu with identical
 semantics, so models built with it run anywhere.
 """
@@ -39,16 +40,19 @@ class _BNActFn(torch.autograd.Function):
             residual = residual.to(x.dtype)
         if residual is not None and not residual.is_contiguous(memory_format=_CL):
             residual = residual.contiguous(memory_format=_CL)
-        _ops().bn_act_forward(x, residual, y, weight, bias, running_mean, running_var, stats[0], stats[1], stats[2],
-                              stats[3], ws, float(eps), float(momentum), bool(relu))
+        mask = None
+        if relu:
+            mask = torch.empty(int(_ops().bn_mask_bytes(M, C, eb)), dtype=torch.uint8, device=x.device)
+        _ops().bn_act_forward(x, residual, y, mask, weight, bias, running_mean, running_var, stats[0], stats[1],
+                              stats[2], stats[3], ws, float(eps), float(momentum), bool(relu))
         ctx.relu = bool(relu)
         ctx.has_res = residual is not None
-        ctx.save_for_backward(x, y if relu else None, weight, stats[0], stats[1])
+        ctx.save_for_backward(x, mask, weight, stats[0], stats[1])
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, weight, mean, invstd = ctx.saved_tensors
+        x, mask, weight, mean, invstd = ctx.saved_tensors
         C = x.shape[1]
         M = x.numel() // C
         dy = dy.contiguous(memory_format=_CL)
@@ -59,7 +63,7 @@ class _BNActFn(torch.autograd.Function):
         g = torch.empty(2, C, dtype=torch.float32, device=x.device)
         ws = torch.empty(int(_ops().bn_workspace_floats(M, C, x.element_size())), dtype=torch.float32,
                          device=x.device)
-        _ops().bn_act_backward(dy, y, x, dx, dres, weight, mean, invstd, g[0], g[1], ws, ctx.relu)
+        _ops().bn_act_backward(dy, mask, x, dx, dres, weight, mean, invstd, g[0], g[1], ws, ctx.relu)
         dgamma = g[0] if weight is not None and ctx.needs_input_grad[2] else None
         dbeta = g[1] if ctx.needs_input_grad[3] else None
         return dx, dres, dgamma, dbeta, None, None, None, None, None

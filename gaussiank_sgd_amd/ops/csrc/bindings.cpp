@@ -272,7 +272,12 @@ int64_t bn_workspace_floats(int64_t M, int64_t C, int64_t elem_bytes) {
 
 bool bn_supported(int64_t C, int64_t elem_bytes) { return gk::bn_supported((int)C, (int)elem_bytes); }
 
-void bn_act_forward(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, c10::optional<at::Tensor> w,
+int64_t bn_mask_bytes(int64_t M, int64_t C, int64_t elem_bytes) {
+  return (int64_t)gk::bn_mask_bytes(M, (int)C, (int)elem_bytes);
+}
+
+void bn_act_forward(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, c10::optional<at::Tensor> mask,
+                    c10::optional<at::Tensor> w,
                     c10::optional<at::Tensor> b, c10::optional<at::Tensor> run_mean,
                     c10::optional<at::Tensor> run_var, at::Tensor save_mean, at::Tensor save_invstd,
                     at::Tensor scale, at::Tensor shift, at::Tensor ws, double eps, double momentum, bool relu) {
@@ -293,14 +298,21 @@ void bn_act_forward(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, c
     TORCH_CHECK(t->scalar_type() == at::kFloat && t->numel() >= C && t->is_cuda(), "stat buffers: fp32[C]");
   TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() >= (int64_t)gk::bn_workspace_floats(M, (int)C, eb),
               "workspace too small");
+  uint8_t* mp = nullptr;
+  if (relu) {
+    TORCH_CHECK(mask.has_value() && mask->defined() && mask->scalar_type() == at::kByte && mask->is_cuda() &&
+                    mask->numel() >= (int64_t)gk::bn_mask_bytes(M, (int)C, eb),
+                "relu needs a uint8 mask of bn_mask_bytes");
+    mp = mask->data_ptr<uint8_t>();
+  }
   c10::DeviceGuard guard(x.device());
-  gk::bn_act_forward(x.data_ptr(), rp, y.data_ptr(), M, (int)C, eb, opt_f32(w), opt_f32(b), (float)eps,
+  gk::bn_act_forward(x.data_ptr(), rp, y.data_ptr(), mp, M, (int)C, eb, opt_f32(w), opt_f32(b), (float)eps,
                      (float)momentum, opt_f32_mut(run_mean), opt_f32_mut(run_var), save_mean.data_ptr<float>(),
                      save_invstd.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(),
                      ws.data_ptr<float>(), relu ? 1 : 0, cur_stream(x));
 }
 
-void bn_act_backward(at::Tensor dy, c10::optional<at::Tensor> y, at::Tensor x, at::Tensor dx,
+void bn_act_backward(at::Tensor dy, c10::optional<at::Tensor> mask, at::Tensor x, at::Tensor dx,
                      c10::optional<at::Tensor> dres, c10::optional<at::Tensor> w, at::Tensor mean, at::Tensor invstd,
                      at::Tensor dgamma, at::Tensor dbeta, at::Tensor ws, bool relu) {
   check_cl(dy, "dy");
@@ -310,11 +322,12 @@ void bn_act_backward(at::Tensor dy, c10::optional<at::Tensor> y, at::Tensor x, a
   const int64_t M = x.numel() / C;
   const int eb = x.element_size();
   TORCH_CHECK(dy.scalar_type() == x.scalar_type() && dx.scalar_type() == x.scalar_type(), "dtype mismatch");
-  const void* yp = nullptr;
+  const uint8_t* mp = nullptr;
   if (relu) {
-    TORCH_CHECK(y.has_value() && y->defined(), "relu backward needs y");
-    check_cl(*y, "y");
-    yp = y->data_ptr();
+    TORCH_CHECK(mask.has_value() && mask->defined() && mask->scalar_type() == at::kByte &&
+                    mask->numel() >= (int64_t)gk::bn_mask_bytes(M, (int)C, eb),
+                "relu backward needs the forward's mask");
+    mp = mask->data_ptr<uint8_t>();
   }
   void* rp = nullptr;
   if (dres.has_value() && dres->defined()) {
@@ -324,7 +337,7 @@ void bn_act_backward(at::Tensor dy, c10::optional<at::Tensor> y, at::Tensor x, a
   TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() >= (int64_t)gk::bn_workspace_floats(M, (int)C, eb),
               "workspace too small");
   c10::DeviceGuard guard(x.device());
-  gk::bn_act_backward(dy.data_ptr(), yp, x.data_ptr(), dx.data_ptr(), rp, M, (int)C, eb, opt_f32(w),
+  gk::bn_act_backward(dy.data_ptr(), mp, x.data_ptr(), dx.data_ptr(), rp, M, (int)C, eb, opt_f32(w),
                       mean.data_ptr<float>(), invstd.data_ptr<float>(), dgamma.data_ptr<float>(),
                       dbeta.data_ptr<float>(), ws.data_ptr<float>(), relu ? 1 : 0, cur_stream(x));
 }
@@ -418,12 +431,13 @@ TORCH_LIBRARY(gksgd, m) {
 
   m.def("bn_workspace_floats(int M, int C, int elem_bytes) -> int", &bn_workspace_floats);
   m.def("bn_supported(int C, int elem_bytes) -> bool", &bn_supported);
+  m.def("bn_mask_bytes(int M, int C, int elem_bytes) -> int", &bn_mask_bytes);
   m.def(
-      "bn_act_forward(Tensor x, Tensor? res, Tensor(a!) y, Tensor? w, Tensor? b, Tensor(b!)? run_mean, "
+      "bn_act_forward(Tensor x, Tensor? res, Tensor(a!) y, Tensor(i!)? mask, Tensor? w, Tensor? b, Tensor(b!)? run_mean, "
       "Tensor(c!)? run_var, Tensor(d!) save_mean, Tensor(e!) save_invstd, Tensor(f!) scale, Tensor(g!) shift, "
       "Tensor(h!) ws, float eps, float momentum, bool relu) -> ()");
   m.def(
-      "bn_act_backward(Tensor dy, Tensor? y, Tensor x, Tensor(a!) dx, Tensor(b!)? dres, Tensor? w, Tensor mean, "
+      "bn_act_backward(Tensor dy, Tensor? mask, Tensor x, Tensor(a!) dx, Tensor(b!)? dres, Tensor? w, Tensor mean, "
       "Tensor invstd, Tensor(c!) dgamma, Tensor(d!) dbeta, Tensor(e!) ws, bool relu) -> ()");
 
   m.class_<RcclEngine>("RcclEngine")

@@ -156,10 +156,12 @@ void clip_grad_norm(float* g, int64_t n, float max_norm, double* ws, float* coef
 // ---------------------------------------------------------------------------
 size_t bn_workspace_floats(int64_t M, int C, int elem_bytes);
 bool bn_supported(int C, int elem_bytes);
-void bn_act_forward(const void* x, const void* res, void* y, int64_t M, int C, int elem_bytes, const float* w,
-                    const float* b, float eps, float momentum, float* run_mean, float* run_var, float* save_mean,
-                    float* save_invstd, float* scale, float* shift, float* ws, int relu, hipStream_t stream);
-void bn_act_backward(const void* dy, const void* y, const void* x, void* dx, void* dres, int64_t M, int C,
+size_t bn_mask_bytes(int64_t M, int C, int elem_bytes);
+void bn_act_forward(const void* x, const void* res, void* y, uint8_t* mask, int64_t M, int C, int elem_bytes,
+                    const float* w, const float* b, float eps, float momentum, float* run_mean, float* run_var,
+                    float* save_mean, float* save_invstd, float* scale, float* shift, float* ws, int relu,
+                    hipStream_t stream);
+void bn_act_backward(const void* dy, const uint8_t* mask, const void* x, void* dx, void* dres, int64_t M, int C,
                      int elem_bytes, const float* w, const float* mean, const float* invstd, float* dgamma,
                      float* dbeta, float* ws, int relu, hipStream_t stream);
 
