@@ -40,4 +40,13 @@ if [ "$MODE" = sweep ]; then
   done
   step bench_dense 600 python bench.py --steps 20 --warmup 10 --dense --json-out $OUT/bench_dense.json
 fi
+
+# find-db for additional batch sizes: FIND_BS="384 512" bash scripts/gpu_check.sh findbs
+if [ "$MODE" = findbs ]; then
+  for bs in ${FIND_BS:-512}; do
+    step find_bs$bs 900 python bench.py --steps 10 --warmup 5 --batch-size $bs --cudnn-benchmark --json-out $OUT/find_bs$bs.json
+    step bench_bs$bs 600 python bench.py --steps 20 --warmup 10 --batch-size $bs --json-out $OUT/bench_bs$bs.json
+  done
+  mkdir -p $OUT/tuning && cp -r tuning/miopen $OUT/tuning/
+fi
 echo done
