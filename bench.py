@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--no-channels-last", action="store_true")
     ap.add_argument("--dense", action="store_true", help="dense RCCL all-reduce comparator (compressor none)")
     ap.add_argument("--no-native-rccl", action="store_true")
+    ap.add_argument("--no-shadow", action="store_true",
+                    help="disable bf16 shadow weights / direct arena gradients (plain autocast)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -96,6 +98,9 @@ def main() -> int:
                                threshold=args.threshold, compress_single_rank=True, density_warmup=False,
                                native_rccl=not args.no_native_rccl)
     comm.broadcast_parameters(trainer.net.state_dict(), root_rank=0)
+    if args.amp == "bf16" and not args.no_shadow:
+        from gaussiank_sgd_amd.parallel import install_bf16_shadow
+        install_bf16_shadow(trainer.net, opt)
     trainer.update_optimizer(opt)
     trainer.display = 10 ** 9  # no host-syncing log lines inside the timed loop
     nparams = sum(p.numel() for p in trainer.net.parameters() if p.requires_grad)

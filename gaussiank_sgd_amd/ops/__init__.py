@@ -440,17 +440,42 @@ def _decode_chunks(chunks: torch.Tensor):
     return out
 
 
+def accum_grad_(dst: torch.Tensor, src: torch.Tensor) -> None:
+    """dst (fp32 arena view) += src (bf16/fp32 gradient with the same strides)."""
+    if dst.is_cuda and src.dtype in (torch.bfloat16, torch.float32) and dst.stride() == src.stride():
+        require_native(dst)
+        _ops().accum_grad(dst, src)
+    else:
+        dst.add_(src.to(dst.dtype))
+
+
+def cast_bf16_(dst: torch.Tensor, src: torch.Tensor) -> None:
+    if dst.is_cuda:
+        require_native(dst)
+        _ops().cast_bf16(dst, src)
+    else:
+        dst.copy_(src)
+
+
 def fused_sgd_(w: torch.Tensor, m: Optional[torch.Tensor], g: torch.Tensor, chunks: torch.Tensor,
-               groups: Sequence[dict], zero_grad: bool = True, grad_scale: Optional[torch.Tensor] = None) -> None:
-    """groups: dicts with lr, momentum, dampening, weight_decay, nesterov, first_step."""
+               groups: Sequence[dict], zero_grad: bool = True, grad_scale: Optional[torch.Tensor] = None,
+               w_bf16: Optional[torch.Tensor] = None) -> None:
+    """groups: dicts with lr, momentum, dampening, weight_decay, nesterov, first_step.
+
+    ``w_bf16``: optional bf16 shadow arena rewritten from the new weights in
+    the same pass (the compute copy used by bf16 convolutions / GEMMs).
+    """
     if w.is_cuda:
         require_native(w)
         _ops().fused_sgd(w, m, g, chunks, [float(p["lr"]) for p in groups], [float(p["momentum"]) for p in groups],
                          [float(p.get("dampening", 0.0)) for p in groups],
                          [float(p.get("weight_decay", 0.0)) for p in groups],
                          [int(bool(p.get("nesterov", False))) for p in groups],
-                         [int(bool(p.get("first_step", False))) for p in groups], bool(zero_grad), grad_scale)
+                         [int(bool(p.get("first_step", False))) for p in groups], bool(zero_grad), grad_scale,
+                         w_bf16)
         return
+    if w_bf16 is not None:
+        raise ValueError("bf16 shadow weights are a GPU feature")
     gs = float(grad_scale) if grad_scale is not None else 1.0
     for start, ln, gi, _ in _decode_chunks(chunks):
         p = groups[gi]

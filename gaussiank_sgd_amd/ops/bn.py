@@ -29,7 +29,12 @@ def _ops():
 
 class _BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, relu):
+    def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, relu, direct=None):
+        # direct = (gw_view, gb_view): weight/bias gradients are accumulated
+        # straight into the optimizer's fp32 arena by the backward kernel and
+        # None is returned for them, so AccumulateGrad launches nothing (its
+        # post-accumulate hook still fires and reports readiness).
+        ctx.direct = direct
         C = x.shape[1]
         M = x.numel() // C
         eb = x.element_size()
@@ -63,10 +68,14 @@ class _BNActFn(torch.autograd.Function):
         g = torch.empty(2, C, dtype=torch.float32, device=x.device)
         ws = torch.empty(int(_ops().bn_workspace_floats(M, C, x.element_size())), dtype=torch.float32,
                          device=x.device)
+        if ctx.direct is not None:
+            gw, gb = ctx.direct
+            _ops().bn_act_backward(dy, mask, x, dx, dres, weight, mean, invstd, g[0], g[1], ws, ctx.relu, gw, gb)
+            return dx, dres, None, None, None, None, None, None, None, None
         _ops().bn_act_backward(dy, mask, x, dx, dres, weight, mean, invstd, g[0], g[1], ws, ctx.relu)
         dgamma = g[0] if weight is not None and ctx.needs_input_grad[2] else None
         dbeta = g[1] if ctx.needs_input_grad[3] else None
-        return dx, dres, dgamma, dbeta, None, None, None, None, None
+        return dx, dres, dgamma, dbeta, None, None, None, None, None, None
 
 
 _supported_cache = {}
@@ -107,8 +116,9 @@ class BNAct(nn.BatchNorm2d):
                 mom = 1.0 / float(self.num_batches_tracked)
             else:
                 mom = self.momentum
+            direct = getattr(self, "_gk_direct", None)
             return _BNActFn.apply(x, residual, self.weight, self.bias, self.running_mean, self.running_var, mom,
-                                  self.eps, relu)
+                                  self.eps, relu, direct)
         out = super().forward(x)
         if residual is not None:
             out = out + residual

@@ -146,7 +146,7 @@ void check_chunks(const at::Tensor& chunks) {
 void fused_sgd(at::Tensor w, c10::optional<at::Tensor> m, at::Tensor g, at::Tensor chunks, std::vector<double> lr,
                std::vector<double> momentum, std::vector<double> dampening, std::vector<double> weight_decay,
                std::vector<int64_t> nesterov, std::vector<int64_t> first_step, bool zero_grad,
-               c10::optional<at::Tensor> grad_scale) {
+               c10::optional<at::Tensor> grad_scale, c10::optional<at::Tensor> w_bf16) {
   check_f32(w, "w");
   check_f32(g, "g");
   check_chunks(chunks);
@@ -186,6 +186,12 @@ void fused_sgd(at::Tensor w, c10::optional<at::Tensor> m, at::Tensor g, at::Tens
   if (grad_scale.has_value() && grad_scale->defined()) {
     check_f32(*grad_scale, "grad_scale");
     a.grad_scale = grad_scale->data_ptr<float>();
+  }
+  if (w_bf16.has_value() && w_bf16->defined()) {
+    TORCH_CHECK(w_bf16->scalar_type() == at::kBFloat16 && w_bf16->numel() == w.numel() && w_bf16->is_contiguous() &&
+                    (reinterpret_cast<uintptr_t>(w_bf16->data_ptr()) & 15) == 0,
+                "w_bf16 must be a 16-byte aligned contiguous bf16 arena of w's size");
+    a.w_bf16 = reinterpret_cast<uint16_t*>(w_bf16->data_ptr());
   }
   c10::DeviceGuard guard(w.device());
   gk::fused_sgd(a, cur_stream(w));
@@ -314,7 +320,8 @@ void bn_act_forward(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, c
 
 void bn_act_backward(at::Tensor dy, c10::optional<at::Tensor> mask, at::Tensor x, at::Tensor dx,
                      c10::optional<at::Tensor> dres, c10::optional<at::Tensor> w, at::Tensor mean, at::Tensor invstd,
-                     at::Tensor dgamma, at::Tensor dbeta, at::Tensor ws, bool relu) {
+                     at::Tensor dgamma, at::Tensor dbeta, at::Tensor ws, bool relu,
+                     c10::optional<at::Tensor> gw_acc, c10::optional<at::Tensor> gb_acc) {
   check_cl(dy, "dy");
   check_cl(x, "x");
   check_cl(dx, "dx");
@@ -339,7 +346,32 @@ void bn_act_backward(at::Tensor dy, c10::optional<at::Tensor> mask, at::Tensor x
   c10::DeviceGuard guard(x.device());
   gk::bn_act_backward(dy.data_ptr(), mp, x.data_ptr(), dx.data_ptr(), rp, M, (int)C, eb, opt_f32(w),
                       mean.data_ptr<float>(), invstd.data_ptr<float>(), dgamma.data_ptr<float>(),
-                      dbeta.data_ptr<float>(), ws.data_ptr<float>(), relu ? 1 : 0, cur_stream(x));
+                      dbeta.data_ptr<float>(), ws.data_ptr<float>(), relu ? 1 : 0, opt_f32_mut(gw_acc),
+                      opt_f32_mut(gb_acc), cur_stream(x));
+}
+
+// ---------------------------------------------------------------------------
+// direct-to-arena gradient accumulation / bf16 shadow weights
+// ---------------------------------------------------------------------------
+void accum_grad(at::Tensor dst, at::Tensor src) {
+  TORCH_CHECK(dst.is_cuda() && src.is_cuda(), "GPU tensors required");
+  TORCH_CHECK(dst.scalar_type() == at::kFloat, "dst must be fp32");
+  TORCH_CHECK(src.scalar_type() == at::kBFloat16 || src.scalar_type() == at::kFloat, "src must be bf16 or fp32");
+  TORCH_CHECK(dst.numel() == src.numel(), "size mismatch");
+  TORCH_CHECK(dst.strides() == src.strides() && dst.is_non_overlapping_and_dense() &&
+                  src.is_non_overlapping_and_dense(),
+              "dst/src must be dense with identical strides");
+  c10::DeviceGuard guard(dst.device());
+  gk::accum_grad(dst.data_ptr<float>(), src.data_ptr(), dst.numel(), (int)src.element_size(), cur_stream(dst));
+}
+
+void cast_bf16(at::Tensor dst, at::Tensor src) {
+  TORCH_CHECK(dst.is_cuda() && src.is_cuda() && dst.scalar_type() == at::kBFloat16 &&
+                  src.scalar_type() == at::kFloat && dst.numel() == src.numel() && dst.is_contiguous() &&
+                  src.is_contiguous(),
+              "cast_bf16: contiguous bf16 dst, fp32 src");
+  c10::DeviceGuard guard(dst.device());
+  gk::cast_bf16(reinterpret_cast<uint16_t*>(dst.data_ptr()), src.data_ptr<float>(), dst.numel(), cur_stream(dst));
 }
 
 // ---------------------------------------------------------------------------
@@ -422,7 +454,7 @@ TORCH_LIBRARY(gksgd, m) {
   m.def(
       "fused_sgd(Tensor(a!) w, Tensor(b!)? m, Tensor(c!) g, Tensor chunks, float[] lr, float[] momentum, "
       "float[] dampening, float[] weight_decay, int[] nesterov, int[] first_step, bool zero_grad, "
-      "Tensor? grad_scale=None) -> ()");
+      "Tensor? grad_scale=None, Tensor(d!)? w_bf16=None) -> ()");
   m.def("segmented_sumsq(Tensor w, Tensor g, Tensor chunks, Tensor(a!) out) -> ()");
   m.def(
       "fused_lars(Tensor(a!) w, Tensor(b!) m, Tensor g, Tensor chunks, Tensor seg_sumsq, float[] lr, "
@@ -438,7 +470,10 @@ TORCH_LIBRARY(gksgd, m) {
       "Tensor(h!) ws, float eps, float momentum, bool relu) -> ()");
   m.def(
       "bn_act_backward(Tensor dy, Tensor? mask, Tensor x, Tensor(a!) dx, Tensor(b!)? dres, Tensor? w, Tensor mean, "
-      "Tensor invstd, Tensor(c!) dgamma, Tensor(d!) dbeta, Tensor(e!) ws, bool relu) -> ()");
+      "Tensor invstd, Tensor(c!) dgamma, Tensor(d!) dbeta, Tensor(e!) ws, bool relu, Tensor(f!)? gw_acc=None, "
+      "Tensor(g!)? gb_acc=None) -> ()");
+  m.def("accum_grad(Tensor(a!) dst, Tensor src) -> ()");
+  m.def("cast_bf16(Tensor(a!) dst, Tensor src) -> ()");
 
   m.class_<RcclEngine>("RcclEngine")
       .def(torch::init<>())
@@ -467,4 +502,6 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("clip_grad_norm", &clip_grad_norm);
   m.impl("bn_act_forward", &bn_act_forward);
   m.impl("bn_act_backward", &bn_act_backward);
+  m.impl("accum_grad", &accum_grad);
+  m.impl("cast_bf16", &cast_bf16);
 }

@@ -314,7 +314,9 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const T* __restri
 
 __global__ __launch_bounds__(kBlock) void bn_bwd_finalize_kernel(const float* __restrict__ pdb,
                                                                  const float* __restrict__ pdg, int gy, int C,
-                                                                 float* __restrict__ dbeta, float* __restrict__ dgamma) {
+                                                                 float* __restrict__ dbeta, float* __restrict__ dgamma,
+                                                                 float* __restrict__ gb_acc,
+                                                                 float* __restrict__ gw_acc) {
   double a = 0.0, b = 0.0;
   bool owner;
   int c;
@@ -322,6 +324,9 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_finalize_kernel(const float* __
   if (!owner) return;
   dbeta[c] = (float)a;
   dgamma[c] = (float)b;
+  // direct-to-arena parameter gradients (AccumulateGrad semantics)
+  if (gb_acc) gb_acc[c] += (float)a;
+  if (gw_acc) gw_acc[c] += (float)b;
 }
 
 template <typename T, bool RELU, bool DRES>
@@ -410,7 +415,7 @@ void bn_forward_t(const T* x, const T* res, T* y, uint8_t* mask, int64_t M, int 
 template <typename T>
 void bn_backward_t(const T* dy, const uint8_t* mask, const T* x, T* dx, T* dres, int64_t M, int C, const float* w,
                    const float* mean, const float* invstd, float* dgamma, float* dbeta, float* ws, int relu,
-                   hipStream_t s) {
+                   float* gw_acc, float* gb_acc, hipStream_t s) {
   const Geo g = make_geo<T>(M, C, kTargetBlocks);
   float* pdb = ws;
   float* pdg = ws + (int64_t)g.gy * C;
@@ -421,7 +426,7 @@ void bn_backward_t(const T* dy, const uint8_t* mask, const T* x, T* dx, T* dres,
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, dy, mask, x, M, C, g,
                        mean, invstd, pdb, pdg);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(kBlock), 0, s, pdb, pdg, g.gy, C,
-                     dbeta, dgamma);
+                     dbeta, dgamma, gb_acc, gw_acc);
 #define GK_BWD_APPLY(R, D)                                                                                       \
   hipLaunchKernelGGL((bn_bwd_apply_kernel<T, R, D>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, dy, mask, x, dx, dres, M, \
                      C, g, w, mean, invstd, dbeta, dgamma)
@@ -448,13 +453,13 @@ void bn_act_forward(const void* x, const void* res, void* y, uint8_t* mask, int6
 
 void bn_act_backward(const void* dy, const uint8_t* mask, const void* x, void* dx, void* dres, int64_t M, int C,
                      int elem_bytes, const float* w, const float* mean, const float* invstd, float* dgamma,
-                     float* dbeta, float* ws, int relu, hipStream_t s) {
+                     float* dbeta, float* ws, int relu, float* gw_acc, float* gb_acc, hipStream_t s) {
   if (elem_bytes == 2)
     bn_backward_t<uint16_t>((const uint16_t*)dy, mask, (const uint16_t*)x, (uint16_t*)dx, (uint16_t*)dres, M, C, w,
-                            mean, invstd, dgamma, dbeta, ws, relu, s);
+                            mean, invstd, dgamma, dbeta, ws, relu, gw_acc, gb_acc, s);
   else
     bn_backward_t<float>((const float*)dy, mask, (const float*)x, (float*)dx, (float*)dres, M, C, w, mean, invstd,
-                         dgamma, dbeta, ws, relu, s);
+                         dgamma, dbeta, ws, relu, gw_acc, gb_acc, s);
 }
 
 }  // namespace gk

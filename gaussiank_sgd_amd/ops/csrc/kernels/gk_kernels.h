@@ -125,8 +125,15 @@ struct SgdArgs {
   int ngroups = 0;
   int zero_grad = 1;
   const float* grad_scale = nullptr;  // optional device scalar (clip coefficient)
+  uint16_t* w_bf16 = nullptr;         // optional bf16 shadow of w written in the same pass
 };
 void fused_sgd(const SgdArgs& a, hipStream_t stream);
+
+// dst[i] += float(src[i]) for a bf16 (src_bytes 2) or fp32 (4) gradient: the
+// fused "cast + AccumulateGrad" of a parameter gradient into its fp32 arena slot.
+void accum_grad(float* dst, const void* src, int64_t n, int src_bytes, hipStream_t stream);
+// dst = bf16(src) (shadow refresh)
+void cast_bf16(uint16_t* dst, const float* src, int64_t n, hipStream_t stream);
 
 // Per-segment sum of squares: out[2*seg] += sum w^2, out[2*seg+1] += sum g^2.
 void segmented_sumsq(const float* w, const float* g, const Chunk* chunks, int nchunks, double* out,
@@ -163,6 +170,6 @@ void bn_act_forward(const void* x, const void* res, void* y, uint8_t* mask, int6
                     hipStream_t stream);
 void bn_act_backward(const void* dy, const uint8_t* mask, const void* x, void* dx, void* dres, int64_t M, int C,
                      int elem_bytes, const float* w, const float* mean, const float* invstd, float* dgamma,
-                     float* dbeta, float* ws, int relu, hipStream_t stream);
+                     float* dbeta, float* ws, int relu, float* gw_acc, float* gb_acc, hipStream_t stream);
 
 }  // namespace gk

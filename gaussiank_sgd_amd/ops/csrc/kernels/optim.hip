@@ -22,6 +22,13 @@
 namespace gk {
 namespace {
 
+__device__ __forceinline__ uint16_t f2bf(float f) {  // round-to-nearest-even, NaN kept quiet
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
 __device__ __forceinline__ float sgd_elem(float w, float& m, float g, const SgdGroup& p, float gs) {
   float d = g * gs;
   if (p.weight_decay != 0.f) d = fmaf(p.weight_decay, w, d);
@@ -57,13 +64,53 @@ __global__ __launch_bounds__(kBlock) void fused_sgd_kernel(SgdArgs a) {
     w4[i] = wv;
     if (use_m) m4[i] = mv;
     if (a.zero_grad) g4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.w_bf16) {
+      const uint32_t lo = (uint32_t)f2bf(wv.x) | ((uint32_t)f2bf(wv.y) << 16);
+      const uint32_t hi = (uint32_t)f2bf(wv.z) | ((uint32_t)f2bf(wv.w) << 16);
+      reinterpret_cast<uint2*>(a.w_bf16 + c.start)[i] = make_uint2(lo, hi);
+    }
   }
   for (int i = (n4 << 2) + threadIdx.x; i < c.len; i += kBlock) {
     float mv = (use_m && !p.first_step) ? m[i] : 0.f;
     w[i] = sgd_elem(w[i], mv, g[i], p, gs);
     if (use_m) m[i] = mv;
     if (a.zero_grad) g[i] = 0.f;
+    if (a.w_bf16) a.w_bf16[c.start + i] = f2bf(w[i]);
   }
+}
+
+__global__ __launch_bounds__(kBlock) void accum_grad_bf16_kernel(float* __restrict__ dst,
+                                                                 const uint16_t* __restrict__ src, int64_t n,
+                                                                 int vec) {
+  const int64_t tid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  const int64_t n8 = vec ? (n >> 3) : 0;
+  for (int64_t i = tid; i < n8; i += stride) {
+    const uint4 u = reinterpret_cast<const uint4*>(src)[i];
+    float4 a = reinterpret_cast<float4*>(dst)[2 * i];
+    float4 b = reinterpret_cast<float4*>(dst)[2 * i + 1];
+    a.x += __uint_as_float(u.x << 16); a.y += __uint_as_float(u.x & 0xffff0000u);
+    a.z += __uint_as_float(u.y << 16); a.w += __uint_as_float(u.y & 0xffff0000u);
+    b.x += __uint_as_float(u.z << 16); b.y += __uint_as_float(u.z & 0xffff0000u);
+    b.z += __uint_as_float(u.w << 16); b.w += __uint_as_float(u.w & 0xffff0000u);
+    reinterpret_cast<float4*>(dst)[2 * i] = a;
+    reinterpret_cast<float4*>(dst)[2 * i + 1] = b;
+  }
+  for (int64_t i = (n8 << 3) + tid; i < n; i += stride) dst[i] += __uint_as_float(((uint32_t)src[i]) << 16);
+}
+
+__global__ __launch_bounds__(kBlock) void accum_grad_f32_kernel(float* __restrict__ dst, const float* __restrict__ src,
+                                                                int64_t n) {
+  const int64_t tid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = tid; i < n; i += stride) dst[i] += src[i];
+}
+
+__global__ __launch_bounds__(kBlock) void cast_bf16_kernel(uint16_t* __restrict__ dst, const float* __restrict__ src,
+                                                           int64_t n) {
+  const int64_t tid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = tid; i < n; i += stride) dst[i] = f2bf(src[i]);
 }
 
 __global__ __launch_bounds__(kBlock) void segmented_sumsq_kernel(const float* __restrict__ w,
@@ -181,6 +228,27 @@ __global__ __launch_bounds__(kBlock) void scale_kernel(float* __restrict__ x, in
 void fused_sgd(const SgdArgs& a, hipStream_t s) {
   if (a.nchunks <= 0) return;
   hipLaunchKernelGGL(fused_sgd_kernel, dim3(a.nchunks), dim3(kBlock), 0, s, a);
+}
+
+void accum_grad(float* dst, const void* src, int64_t n, int src_bytes, hipStream_t s) {
+  if (n <= 0) return;
+  int64_t G = ceil_div(n, (int64_t)kBlock * 8);
+  if (G < 1) G = 1;
+  if (G > 2048) G = 2048;
+  const bool vec = ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) == 0;
+  if (src_bytes == 2)  // unaligned pointers: the scalar tail loop covers every element
+    hipLaunchKernelGGL(accum_grad_bf16_kernel, dim3((int)G), dim3(kBlock), 0, s, dst, (const uint16_t*)src, n,
+                       vec ? 1 : 0);
+  else
+    hipLaunchKernelGGL(accum_grad_f32_kernel, dim3((int)G), dim3(kBlock), 0, s, dst, (const float*)src, n);
+}
+
+void cast_bf16(uint16_t* dst, const float* src, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  int64_t G = ceil_div(n, (int64_t)kBlock * 8);
+  if (G < 1) G = 1;
+  if (G > 2048) G = 2048;
+  hipLaunchKernelGGL(cast_bf16_kernel, dim3((int)G), dim3(kBlock), 0, s, dst, src, n);
 }
 
 void segmented_sumsq(const float* w, const float* g, const Chunk* chunks, int nchunks, double* out, hipStream_t s) {

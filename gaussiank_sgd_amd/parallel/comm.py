@@ -218,6 +218,15 @@ def broadcast_object(obj: Any, root: int = 0) -> Any:
     return lst[0]
 
 
+# storage data_ptr -> callbacks run after a broadcast overwrote that storage
+# (the bf16 shadow arena re-casts itself from the fp32 weight arena).
+_storage_listeners: Dict[int, List] = {}
+
+
+def on_storage_overwritten(ptr: int, fn) -> None:
+    _storage_listeners.setdefault(int(ptr), []).append(fn)
+
+
 def broadcast_parameters(params, root_rank: int = 0) -> None:
     """Broadcast a state_dict / named_parameters from root (distributed_optimizer.py:588-617).
 
@@ -253,6 +262,9 @@ def broadcast_parameters(params, root_rank: int = 0) -> None:
         handles.append(broadcast_async_(flat, root_rank, name))
     for h in handles:
         synchronize(h)
+    for ptr, _ in seen:
+        for fn in _storage_listeners.get(ptr, ()):
+            fn()
 
 
 def broadcast_optimizer_state(optimizer: torch.optim.Optimizer, root_rank: int = 0) -> None:

@@ -245,6 +245,34 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         return hook
 
     # ------------------------------------------------------------------
+    # bf16 shadow weights (parallel/shadow.py)
+    # ------------------------------------------------------------------
+    def _ensure_shadow(self) -> torch.Tensor:
+        arena = self._arena
+        if getattr(arena, "shadow", None) is None:
+            arena.shadow = torch.empty(arena.total, dtype=torch.bfloat16, device=arena.device)
+            comm.on_storage_overwritten(arena.weights.untyped_storage().data_ptr(), self.refresh_shadow)
+        return arena.shadow
+
+    def refresh_shadow(self) -> None:
+        """Re-cast the bf16 shadow from the fp32 master weights."""
+        shadow = getattr(self._arena, "shadow", None)
+        if shadow is not None:
+            with torch.no_grad():
+                ops.cast_bf16_(shadow, self._arena.weights)
+
+    def _make_sink(self, key):
+        arena = self._arena
+        gv = arena.grad_views[key]
+        p = self._named_parameters[key]
+
+        def sink(grad):
+            if p.grad is None or p.grad.data_ptr() != gv.data_ptr():
+                arena.check_grad(key, p)
+            ops.accum_grad_(gv, grad)
+        return sink
+
+    # ------------------------------------------------------------------
     # density schedule / logging (reference :136-160)
     # ------------------------------------------------------------------
     def increase_one_epoch(self):
@@ -574,7 +602,7 @@ class _DistributedOptimizer(torch.optim.Optimizer):
                                "weight_decay": g.get("weight_decay", 0.0), "nesterov": g.get("nesterov", False),
                                "first_step": self._group_first[gi] and g["momentum"] != 0})
             ops.fused_sgd_(arena.weights, arena.momentum, arena.grads, self._chunks, groups,
-                           zero_grad=self._zero_grad_in_step)
+                           zero_grad=self._zero_grad_in_step, w_bf16=getattr(arena, "shadow", None))
             if any(self._group_first):
                 self._group_first = [False] * len(self._group_first)
                 self._adopt_state()
@@ -586,6 +614,7 @@ class _DistributedOptimizer(torch.optim.Optimizer):
             ops.fused_lars_(arena.weights, arena.momentum, arena.grads, self._chunks, self._seg_sumsq, groups)
             if self._zero_grad_in_step:
                 ops.fill_zero_(arena.grads)
+            self.refresh_shadow()
         self._grads_zero = self._zero_grad_in_step
 
     def step(self, closure=None):
@@ -600,7 +629,9 @@ class _DistributedOptimizer(torch.optim.Optimizer):
                 self._fused_step()
             return loss
         self._grads_zero = False
-        return super(self.__class__, self).step(closure)
+        loss = super(self.__class__, self).step(closure)
+        self.refresh_shadow()
+        return loss
 
     def zero_grad(self, set_to_none: bool = True):
         """Gradients are views of the arena: zero it (never set to None)."""

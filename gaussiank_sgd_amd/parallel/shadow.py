@@ -1,0 +1,104 @@
+"""bf16 shadow weights + direct-to-arena gradients (mixed precision "O2" on MI355X).
+
+Under bf16 autocast, every step PyTorch (a) casts each fp32 conv/linear
+weight to bf16 in forward, (b) casts each bf16 weight gradient back to fp32
+in backward and (c) adds it into ``p.grad`` with a separate AccumulateGrad
+kernel -- three small launches per parameter, ~1.5 ms per ResNet-50 step on
+MI355X (profiles/r01_resnet50_bs256_fusedbn_kernel_stats.csv).
+
+``install_bf16_shadow`` removes all three:
+  * the fused SGD kernel writes a bf16 copy of the new weights ("shadow
+    arena") in the same pass that updates the fp32 master weights, and
+    conv/linear modules compute with views of that shadow arena;
+  * the shadow view's backward accumulates the bf16 gradient straight into
+    the fp32 gradient arena (one fused cast+add kernel) and returns None for
+    the fp32 parameter, so AccumulateGrad launches nothing; its
+    post-accumulate hook still fires afterwards and reports the parameter
+    ready to the bucket engine exactly as on the plain path;
+  * ``BNAct`` modules get the same direct path for gamma/beta: the BN backward
+    kernel adds them into the arena.
+Outside autocast (or on the CPU) modules fall back to their fp32 parameters,
+so the model stays usable for evaluation and CPU tests.
+"""
+from __future__ import annotations
+
+import types
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops.bn import BNAct
+
+
+class _ShadowWeight(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, param, shadow, sink):
+        ctx.sink = sink
+        return shadow.view_as(shadow)
+
+    @staticmethod
+    def backward(ctx, grad):
+        ctx.sink(grad)
+        return None, None, None
+
+
+def _shadow(module: nn.Module, name: str, x: torch.Tensor):
+    info = module._gk_shadow.get(name)
+    p = getattr(module, name)
+    if info is None or not x.is_cuda or not torch.is_autocast_enabled("cuda"):
+        return p
+    shadow, sink = info
+    if torch.is_grad_enabled() and p.requires_grad:
+        return _ShadowWeight.apply(p, shadow, sink)
+    return shadow
+
+
+def _conv_forward(self, x):
+    w = _shadow(self, "weight", x)
+    b = _shadow(self, "bias", x) if self.bias is not None else None
+    return self._conv_forward(x, w, b)
+
+
+def _linear_forward(self, x):
+    w = _shadow(self, "weight", x)
+    b = _shadow(self, "bias", x) if self.bias is not None else None
+    return F.linear(x, w, b)
+
+
+def install_bf16_shadow(model: nn.Module, opt) -> int:
+    """Attach the shadow path to ``model``'s Conv2d / Linear / BNAct modules.
+
+    ``opt`` is the DistributedOptimizer owning the arenas.  Returns the number
+    of parameters that now bypass AccumulateGrad.
+    """
+    arena = opt.arena
+    if arena.device.type != "cuda":
+        return 0
+    shadow = opt._ensure_shadow()
+    names = opt._parameter_names
+    count = 0
+    for mod in model.modules():
+        if isinstance(mod, (nn.Conv2d, nn.Linear)) and type(mod).forward in (nn.Conv2d.forward, nn.Linear.forward):
+            table = {}
+            for pname in ("weight", "bias"):
+                p = getattr(mod, pname, None)
+                if p is None or p not in names:
+                    continue
+                key = names[p]
+                table[pname] = (arena.view_of(shadow, key), opt._make_sink(key))
+                count += 1
+            if table:
+                mod._gk_shadow = table
+                mod.forward = types.MethodType(_conv_forward if isinstance(mod, nn.Conv2d) else _linear_forward, mod)
+        elif isinstance(mod, BNAct) and mod.affine:
+            if mod.weight in names and mod.bias in names:
+                kw, kb = names[mod.weight], names[mod.bias]
+                mod._gk_direct = (arena.grad_views[kw], arena.grad_views[kb])
+                count += 2
+    opt.refresh_shadow()
+    if not getattr(model, "_gk_shadow_hooked", False):
+        # model.load_state_dict copies into the fp32 arena: keep the shadow in sync
+        model.register_load_state_dict_post_hook(lambda m, keys: opt.refresh_shadow())
+        model._gk_shadow_hooked = True
+    return count

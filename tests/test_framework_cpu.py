@@ -172,3 +172,26 @@ def test_evaluate_checkpoints(tmp_path):
         t.save_checkpoint(t.checkpoint_state(), os.path.join(d, "fcn5net-rank0-epoch%d.pth" % e))
     best, ep, res = evaluate("fcn5net", "mnist", d, 3, batch_size=16, device="cpu", num_batches=1)
     assert set(res) == {1, 2} and ep in (1, 2)
+
+
+def test_post_accumulate_hook_fires_for_direct_grads():
+    """The bf16 shadow / fused-BN direct paths return None for the fp32
+    parameter and rely on its post-accumulate hook still firing (readiness)."""
+    from gaussiank_sgd_amd.parallel.shadow import _ShadowWeight
+    p = torch.nn.Parameter(torch.ones(4))
+    fired = []
+    p.register_post_accumulate_grad_hook(lambda q: fired.append(q.grad))
+    sink_got = []
+    y = _ShadowWeight.apply(p, torch.full((4,), 2.0), sink_got.append)
+    (y * 3).sum().backward()
+    assert len(fired) == 1 and fired[0] is None
+    assert torch.equal(sink_got[0], torch.full((4,), 3.0))
+
+
+def test_install_shadow_is_noop_on_cpu():
+    from gaussiank_sgd_amd.models import resnet50
+    from gaussiank_sgd_amd.parallel import install_bf16_shadow
+    net = resnet50(num_classes=10)
+    opt = hvd.DistributedOptimizer(torch.optim.SGD(net.parameters(), lr=0.1, momentum=0.9),
+                                   named_parameters=net.named_parameters(), compression=compressors["none"])
+    assert install_bf16_shadow(net, opt) == 0
