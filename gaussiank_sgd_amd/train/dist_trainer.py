@@ -35,7 +35,8 @@ from .trainer import DLTrainer, _support_datasets, _support_dnns
 
 def ssgd(dnn, dataset, data_dir, nworkers, lr, batch_size, nsteps_update, max_epochs, nwpernode, pretrain,
          num_steps, compressor, density, threshold, gradient_path=None, amp=None, channels_last=False,
-         density_warmup=True, deterministic=False, max_iters=None, compress_single_rank=False, saved_dir="."):
+         density_warmup=True, deterministic=False, max_iters=None, compress_single_rank=False, saved_dir=".",
+         bf16_shadow=True):
     rank = hvd.rank()
     device = "cpu"
     if torch.cuda.is_available():
@@ -81,6 +82,9 @@ def ssgd(dnn, dataset, data_dir, nworkers, lr, batch_size, nsteps_update, max_ep
     if getattr(trainer, "_pending_compression", None):
         optimizer.load_compression_state(trainer._pending_compression)
     hvd.broadcast_parameters(trainer.net.state_dict(), root_rank=0)
+    if bf16_shadow and amp == "bf16" and trainer.is_cuda:
+        from ..parallel import install_bf16_shadow
+        install_bf16_shadow(trainer.net, optimizer)
     trainer.update_optimizer(optimizer)
     iters_per_epoch = max(1, trainer.get_num_of_training_samples() // (nworkers * batch_size * nsteps_update))
     times = []
@@ -144,6 +148,8 @@ def build_parser():
     p.add_argument("--deterministic", action="store_true")
     p.add_argument("--compress-single-rank", action="store_true")
     p.add_argument("--max-iters", type=int, default=None)
+    p.add_argument("--no-bf16-shadow", action="store_true",
+                   help="with --amp bf16: keep plain autocast casts instead of the bf16 shadow weight arena")
     p.add_argument("--logdir-root", type=str, default="./logs")
     return p
 
@@ -174,7 +180,8 @@ def main(argv=None):
                 args.max_epochs, args.nwpernode, args.pretrain, args.num_steps, args.compressor, args.density,
                 args.threshold, gradient_path, amp=args.amp, channels_last=args.channels_last,
                 density_warmup=not args.no_density_warmup, deterministic=args.deterministic,
-                max_iters=args.max_iters, compress_single_rank=args.compress_single_rank, saved_dir=args.saved_dir)
+                max_iters=args.max_iters, compress_single_rank=args.compress_single_rank, saved_dir=args.saved_dir,
+                bf16_shadow=not args.no_bf16_shadow)
 
 
 if __name__ == "__main__":
