@@ -41,7 +41,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch-size", type=int, default=int(os.environ.get("GKSGD_BENCH_BS", "256")))
+    ap.add_argument("--batch-size", type=int, default=int(os.environ.get("GKSGD_BENCH_BS", "512")))
     ap.add_argument("--cudnn-benchmark", action="store_true", help="MIOpen find (exhaustive conv algorithm search)")
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--compressor", default="gaussian")

@@ -49,4 +49,12 @@ if [ "$MODE" = findbs ]; then
   done
   mkdir -p $OUT/tuning && cp -r tuning/miopen $OUT/tuning/
 fi
+# targeted: GPU tests of given files + bench A/B + profile
+#   TESTS="tests/test_shadow_gpu.py" AB="--no-shadow" bash scripts/gpu_check.sh ab
+if [ "$MODE" = ab ]; then
+  step pytest_sel 600 python -m pytest ${TESTS:-tests/test_shadow_gpu.py} -x -q
+  step bench_a 600 python bench.py --steps 20 --warmup 10 --json-out $OUT/bench_a.json
+  step bench_b 600 python bench.py --steps 20 --warmup 10 ${AB:---no-shadow} --json-out $OUT/bench_b.json
+  step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 5 --warmup 3
+fi
 echo done
