@@ -43,7 +43,8 @@ class BasicBlock(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        identity = x if self.downsample is None else self.downsample(x)
+        x, xs = x if isinstance(x, tuple) else (x, x)   # (main, shortcut) handles, see BNAct twin
+        identity = xs if self.downsample is None else self.downsample(xs)
         out = self.bn1(self.conv1(x))
         return self.bn2(self.conv2(out), identity)
 
@@ -63,7 +64,8 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        identity = x if self.downsample is None else self.downsample(x)
+        x, xs = x if isinstance(x, tuple) else (x, x)   # (main, shortcut) handles, see BNAct twin
+        identity = xs if self.downsample is None else self.downsample(xs)
         out = self.bn1(self.conv1(x))
         out = self.bn2(self.conv2(out))
         return self.bn3(self.conv3(out), identity)
@@ -78,8 +80,10 @@ class ResNet(nn.Module):
         self.groups = groups
         self.base_width = width_per_group
         self.conv1 = nn.Conv2d(3, 64, kernel_size=7, stride=2, padding=3, bias=False)
-        self.bn1 = BNAct(64, act="relu")
-        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        # stem BN + ReLU + 3x3/s2 max-pool run as one fused kernel pass (BNAct pool=...);
+        # ``maxpool`` stays as an attribute (no parameters) for module-path compatibility.
+        self.bn1 = BNAct(64, act="relu", pool=(3, 2, 1))
+        self.maxpool = nn.Identity()
         self.layer1 = self._make_layer(block, 64, layers[0])
         self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
         self.layer3 = self._make_layer(block, 256, layers[2], stride=2)
@@ -93,6 +97,13 @@ class ResNet(nn.Module):
             elif isinstance(m, nn.BatchNorm2d):  # includes BNAct
                 nn.init.ones_(m.weight)
                 nn.init.zeros_(m.bias)
+        # Every block output except the last feeds the next block twice (conv1 and
+        # shortcut): let the producing BN hand out two handles so the backward
+        # sums the two gradients inside the fused BN passes (no add kernel).
+        blocks = [b for layer in (self.layer1, self.layer2, self.layer3, self.layer4) for b in layer]
+        self.bn1.twin = True
+        for b in blocks[:-1]:
+            (b.bn3 if isinstance(b, Bottleneck) else b.bn2).twin = True
         if zero_init_residual:
             for m in self.modules():
                 if isinstance(m, Bottleneck):

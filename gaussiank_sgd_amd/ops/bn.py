@@ -27,14 +27,30 @@ def _ops():
     return torch.ops.gksgd
 
 
+def _grad_pair(grads, like):
+    """(dy, dy2) from the output gradients of a (possibly twin-output) Function."""
+    gs = [g for g in grads if g is not None]
+    out = []
+    for g in gs:
+        g = g.contiguous(memory_format=_CL)
+        if g.dtype != like.dtype:
+            g = g.to(like.dtype)
+        out.append(g)
+    return (out + [None, None])[:2]
+
+
 class _BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, relu, direct=None):
+    def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, relu, direct=None,
+                nbt=None, twin=False):
         # direct = (gw_view, gb_view): weight/bias gradients are accumulated
         # straight into the optimizer's fp32 arena by the backward kernel and
         # None is returned for them, so AccumulateGrad launches nothing (its
         # post-accumulate hook still fires and reports readiness).
+        # twin: return the output twice (ResNet: next block's conv1 input and
+        # its shortcut); the backward sums both gradients inside the BN passes.
         ctx.direct = direct
+        ctx.set_materialize_grads(False)
         C = x.shape[1]
         M = x.numel() // C
         eb = x.element_size()
@@ -49,33 +65,78 @@ class _BNActFn(torch.autograd.Function):
         if relu:
             mask = torch.empty(int(_ops().bn_mask_bytes(M, C, eb)), dtype=torch.uint8, device=x.device)
         _ops().bn_act_forward(x, residual, y, mask, weight, bias, running_mean, running_var, stats[0], stats[1],
-                              stats[2], stats[3], ws, float(eps), float(momentum), bool(relu))
+                              stats[2], stats[3], ws, float(eps), float(momentum), bool(relu), nbt)
         ctx.relu = bool(relu)
         ctx.has_res = residual is not None
         ctx.save_for_backward(x, mask, weight, stats[0], stats[1])
-        return y
+        return (y, y.view_as(y)) if twin else y
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, *grads):
         x, mask, weight, mean, invstd = ctx.saved_tensors
+        dy, dy2 = _grad_pair(grads, x)
+        if dy is None:
+            return (None,) * 12
         C = x.shape[1]
         M = x.numel() // C
-        dy = dy.contiguous(memory_format=_CL)
-        if dy.dtype != x.dtype:
-            dy = dy.to(x.dtype)
         dx = torch.empty_like(x, memory_format=_CL)
-        dres = torch.empty_like(x, memory_format=_CL) if ctx.has_res else None
+        dres = torch.empty_like(x, memory_format=_CL) if ctx.has_res and ctx.needs_input_grad[1] else None
         g = torch.empty(2, C, dtype=torch.float32, device=x.device)
         ws = torch.empty(int(_ops().bn_workspace_floats(M, C, x.element_size())), dtype=torch.float32,
                          device=x.device)
+        gw, gb = ctx.direct if ctx.direct is not None else (None, None)
+        _ops().bn_act_backward(dy, mask, x, dx, dres, weight, mean, invstd, g[0], g[1], ws, ctx.relu, gw, gb, dy2)
         if ctx.direct is not None:
-            gw, gb = ctx.direct
-            _ops().bn_act_backward(dy, mask, x, dx, dres, weight, mean, invstd, g[0], g[1], ws, ctx.relu, gw, gb)
-            return dx, dres, None, None, None, None, None, None, None, None
-        _ops().bn_act_backward(dy, mask, x, dx, dres, weight, mean, invstd, g[0], g[1], ws, ctx.relu)
+            return dx, dres, None, None, None, None, None, None, None, None, None, None
         dgamma = g[0] if weight is not None and ctx.needs_input_grad[2] else None
         dbeta = g[1] if ctx.needs_input_grad[3] else None
-        return dx, dres, dgamma, dbeta, None, None, None, None, None, None
+        return dx, dres, dgamma, dbeta, None, None, None, None, None, None, None, None
+
+
+class _BNReLUPoolFn(torch.autograd.Function):
+    """maxpool(relu(bn(x))) with the pool folded into the BN passes (bn_act.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, pool, direct=None, nbt=None,
+                twin=False):
+        ctx.set_materialize_grads(False)
+        k, st, pad = pool
+        N, C, H, W = x.shape
+        OH = (H + 2 * pad - k) // st + 1
+        OW = (W + 2 * pad - k) // st + 1
+        y = torch.empty((N, C, OH, OW), dtype=x.dtype, device=x.device, memory_format=_CL)
+        amax = torch.empty(N * C * OH * OW, dtype=torch.uint8, device=x.device)
+        stats = torch.empty(4, C, dtype=torch.float32, device=x.device)
+        M = N * H * W
+        ws = torch.empty(int(_ops().bn_workspace_floats(M, C, x.element_size())), dtype=torch.float32,
+                         device=x.device)
+        _ops().bn_relu_pool_forward(x, y, amax, weight, bias, running_mean, running_var, stats[0], stats[1],
+                                    stats[2], stats[3], ws, float(eps), float(momentum), k, st, pad, nbt)
+        ctx.pool = (k, st, pad)
+        ctx.direct = direct
+        ctx.save_for_backward(x, amax, weight, stats[0], stats[1])
+        return (y, y.view_as(y)) if twin else y
+
+    @staticmethod
+    def backward(ctx, *grads):
+        x, amax, weight, mean, invstd = ctx.saved_tensors
+        dy, dy2 = _grad_pair(grads, x)
+        if dy is None:
+            return (None,) * 11
+        k, st, pad = ctx.pool
+        C = x.shape[1]
+        M = x.numel() // C
+        dx = torch.empty_like(x, memory_format=_CL)
+        g = torch.empty(2, C, dtype=torch.float32, device=x.device)
+        ws = torch.empty(int(_ops().bn_workspace_floats(M, C, x.element_size())), dtype=torch.float32,
+                         device=x.device)
+        gw, gb = ctx.direct if ctx.direct is not None else (None, None)
+        _ops().bn_relu_pool_backward(dy, amax, x, dx, weight, mean, invstd, g[0], g[1], ws, k, st, pad, gw, gb, dy2)
+        if ctx.direct is not None:
+            return (dx,) + (None,) * 10
+        dgamma = g[0] if weight is not None and ctx.needs_input_grad[1] else None
+        dbeta = g[1] if ctx.needs_input_grad[2] else None
+        return (dx, dgamma, dbeta) + (None,) * 8
 
 
 _supported_cache = {}
@@ -97,34 +158,54 @@ def fused_bn_available(x: torch.Tensor) -> bool:
 
 
 class BNAct(nn.BatchNorm2d):
-    """BatchNorm2d with optional fused residual add and ReLU."""
+    """BatchNorm2d with optional fused residual add, ReLU and trailing max-pool.
+
+    ``pool=(k, s, p)`` (requires ``act="relu"``) appends ``max_pool2d(k, s, p)``:
+    the fused path never writes the full-resolution activation and gathers the
+    pool gradient inside the BN backward (the ResNet stem).
+    """
 
     def __init__(self, num_features: int, act: Optional[str] = None, eps: float = 1e-5, momentum: float = 0.1,
-                 affine: bool = True, track_running_stats: bool = True, fused: bool = True):
+                 affine: bool = True, track_running_stats: bool = True, fused: bool = True,
+                 pool: Optional[tuple] = None, twin: bool = False):
         super().__init__(num_features, eps=eps, momentum=momentum, affine=affine,
                          track_running_stats=track_running_stats)
         assert act in (None, "relu")
+        assert pool is None or (act == "relu" and len(pool) == 3)
         self.act = act
         self.fused = fused
+        self.pool = tuple(pool) if pool is not None else None
+        # twin: forward returns (out, out) -- two handles on one output whose
+        # gradients the fused backward sums on load (ResNet block outputs feed
+        # both the next conv1 and the next shortcut).
+        self.twin = twin
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
         relu = self.act == "relu"
-        if self.training and self.fused and self.track_running_stats and fused_bn_available(x):
-            if self.num_batches_tracked is not None:
-                self.num_batches_tracked.add_(1)
+        pool = self.pool
+        if self.training and self.fused and self.track_running_stats and fused_bn_available(x) and \
+                (pool is None or (residual is None and x.numel() // x.shape[1] < 2 ** 32)):
+            nbt = self.num_batches_tracked
             if self.momentum is None:
-                mom = 1.0 / float(self.num_batches_tracked)
+                nbt.add_(1)
+                mom = 1.0 / float(nbt)  # host sync, as in nn.BatchNorm2d's cumulative mode
+                nbt = None
             else:
-                mom = self.momentum
+                mom = self.momentum     # the finalize kernel increments num_batches_tracked
             direct = getattr(self, "_gk_direct", None)
+            if pool is not None:
+                return _BNReLUPoolFn.apply(x, self.weight, self.bias, self.running_mean, self.running_var, mom,
+                                           self.eps, pool, direct, nbt, self.twin)
             return _BNActFn.apply(x, residual, self.weight, self.bias, self.running_mean, self.running_var, mom,
-                                  self.eps, relu, direct)
+                                  self.eps, relu, direct, nbt, self.twin)
         out = super().forward(x)
         if residual is not None:
             out = out + residual
         if relu:
             out = F.relu(out)
-        return out
+        if pool is not None:
+            out = F.max_pool2d(out, pool[0], pool[1], pool[2])
+        return (out, out) if self.twin else out
 
     def extra_repr(self) -> str:
-        return super().extra_repr() + ", act=%s" % self.act
+        return super().extra_repr() + ", act=%s" % self.act + (", pool=%s" % (self.pool,) if self.pool else "")

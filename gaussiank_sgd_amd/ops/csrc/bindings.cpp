@@ -272,6 +272,20 @@ const float* opt_f32(const c10::optional<at::Tensor>& t) {
 
 float* opt_f32_mut(const c10::optional<at::Tensor>& t) { return const_cast<float*>(opt_f32(t)); }
 
+// optional tensor that must have `ref`'s dtype, shape and channels-last layout
+const void* opt_like(const c10::optional<at::Tensor>& t, const at::Tensor& ref, const char* name) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  check_cl(*t, name);
+  TORCH_CHECK(t->scalar_type() == ref.scalar_type() && t->sizes() == ref.sizes(), name, " must match dy");
+  return t->data_ptr();
+}
+
+int64_t* opt_i64(const c10::optional<at::Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->scalar_type() == at::kLong && t->numel() == 1 && t->is_cuda(), "expected int64[1] GPU tensor");
+  return t->data_ptr<int64_t>();
+}
+
 int64_t bn_workspace_floats(int64_t M, int64_t C, int64_t elem_bytes) {
   return (int64_t)gk::bn_workspace_floats(M, (int)C, (int)elem_bytes);
 }
@@ -286,7 +300,8 @@ void bn_act_forward(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, c
                     c10::optional<at::Tensor> w,
                     c10::optional<at::Tensor> b, c10::optional<at::Tensor> run_mean,
                     c10::optional<at::Tensor> run_var, at::Tensor save_mean, at::Tensor save_invstd,
-                    at::Tensor scale, at::Tensor shift, at::Tensor ws, double eps, double momentum, bool relu) {
+                    at::Tensor scale, at::Tensor shift, at::Tensor ws, double eps, double momentum, bool relu,
+                    c10::optional<at::Tensor> nbt) {
   check_cl(x, "x");
   check_cl(y, "y");
   const int64_t C = channels_of(x);
@@ -315,13 +330,14 @@ void bn_act_forward(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, c
   gk::bn_act_forward(x.data_ptr(), rp, y.data_ptr(), mp, M, (int)C, eb, opt_f32(w), opt_f32(b), (float)eps,
                      (float)momentum, opt_f32_mut(run_mean), opt_f32_mut(run_var), save_mean.data_ptr<float>(),
                      save_invstd.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(),
-                     ws.data_ptr<float>(), relu ? 1 : 0, cur_stream(x));
+                     ws.data_ptr<float>(), relu ? 1 : 0, opt_i64(nbt), cur_stream(x));
 }
 
 void bn_act_backward(at::Tensor dy, c10::optional<at::Tensor> mask, at::Tensor x, at::Tensor dx,
                      c10::optional<at::Tensor> dres, c10::optional<at::Tensor> w, at::Tensor mean, at::Tensor invstd,
                      at::Tensor dgamma, at::Tensor dbeta, at::Tensor ws, bool relu,
-                     c10::optional<at::Tensor> gw_acc, c10::optional<at::Tensor> gb_acc) {
+                     c10::optional<at::Tensor> gw_acc, c10::optional<at::Tensor> gb_acc,
+                     c10::optional<at::Tensor> dy2) {
   check_cl(dy, "dy");
   check_cl(x, "x");
   check_cl(dx, "dx");
@@ -344,10 +360,78 @@ void bn_act_backward(at::Tensor dy, c10::optional<at::Tensor> mask, at::Tensor x
   TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() >= (int64_t)gk::bn_workspace_floats(M, (int)C, eb),
               "workspace too small");
   c10::DeviceGuard guard(x.device());
-  gk::bn_act_backward(dy.data_ptr(), mp, x.data_ptr(), dx.data_ptr(), rp, M, (int)C, eb, opt_f32(w),
+  const void* d2 = opt_like(dy2, dy, "dy2");
+  gk::bn_act_backward(dy.data_ptr(), d2, mp, x.data_ptr(), dx.data_ptr(), rp, M, (int)C, eb, opt_f32(w),
                       mean.data_ptr<float>(), invstd.data_ptr<float>(), dgamma.data_ptr<float>(),
                       dbeta.data_ptr<float>(), ws.data_ptr<float>(), relu ? 1 : 0, opt_f32_mut(gw_acc),
                       opt_f32_mut(gb_acc), cur_stream(x));
+}
+
+gk::PoolGeo pool_geo(const at::Tensor& x, const at::Tensor& y, int64_t k, int64_t st, int64_t pad) {
+  TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && x.size(0) == y.size(0) && x.size(1) == y.size(1), "pool shapes");
+  gk::PoolGeo pg;
+  pg.H = (int)x.size(2);
+  pg.W = (int)x.size(3);
+  pg.OH = (int)y.size(2);
+  pg.OW = (int)y.size(3);
+  pg.k = (int)k;
+  pg.s = (int)st;
+  pg.p = (int)pad;
+  TORCH_CHECK(k >= 1 && k <= 15 && st >= 1 && pad >= 0 && 2 * pad <= k, "unsupported pool window");
+  TORCH_CHECK(pg.OH == (pg.H + 2 * pg.p - pg.k) / pg.s + 1 && pg.OW == (pg.W + 2 * pg.p - pg.k) / pg.s + 1,
+              "pool output shape mismatch (ceil_mode unsupported)");
+  TORCH_CHECK(x.numel() / x.size(1) < (int64_t(1) << 32), "N*H*W must be < 2^32");
+  return pg;
+}
+
+void bn_relu_pool_forward(at::Tensor x, at::Tensor y, at::Tensor amax, c10::optional<at::Tensor> w,
+                          c10::optional<at::Tensor> b, c10::optional<at::Tensor> run_mean,
+                          c10::optional<at::Tensor> run_var, at::Tensor save_mean, at::Tensor save_invstd,
+                          at::Tensor scale, at::Tensor shift, at::Tensor ws, double eps, double momentum, int64_t k,
+                          int64_t st, int64_t pad, c10::optional<at::Tensor> nbt) {
+  check_cl(x, "x");
+  check_cl(y, "y");
+  TORCH_CHECK(x.dim() == 4 && y.scalar_type() == x.scalar_type(), "y must be 4-D with x's dtype");
+  const gk::PoolGeo pg = pool_geo(x, y, k, st, pad);
+  const int64_t C = x.size(1);
+  const int64_t M = x.numel() / C;
+  const int eb = x.element_size();
+  TORCH_CHECK(gk::bn_supported((int)C, eb), "channel count not supported by the fused kernel");
+  TORCH_CHECK(amax.scalar_type() == at::kByte && amax.is_cuda() && amax.numel() >= y.numel(), "amax: uint8[y.numel]");
+  for (const at::Tensor* t : {&save_mean, &save_invstd, &scale, &shift})
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->numel() >= C && t->is_cuda(), "stat buffers: fp32[C]");
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() >= (int64_t)gk::bn_workspace_floats(M, (int)C, eb),
+              "workspace too small");
+  c10::DeviceGuard guard(x.device());
+  gk::bn_relu_pool_forward(x.data_ptr(), y.data_ptr(), amax.data_ptr<uint8_t>(), x.size(0), (int)C, pg, eb,
+                           opt_f32(w), opt_f32(b), (float)eps, (float)momentum, opt_f32_mut(run_mean),
+                           opt_f32_mut(run_var), save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(),
+                           scale.data_ptr<float>(), shift.data_ptr<float>(), ws.data_ptr<float>(), opt_i64(nbt),
+                           cur_stream(x));
+}
+
+void bn_relu_pool_backward(at::Tensor dy, at::Tensor amax, at::Tensor x, at::Tensor dx, c10::optional<at::Tensor> w,
+                           at::Tensor mean, at::Tensor invstd, at::Tensor dgamma, at::Tensor dbeta, at::Tensor ws,
+                           int64_t k, int64_t st, int64_t pad, c10::optional<at::Tensor> gw_acc,
+                           c10::optional<at::Tensor> gb_acc, c10::optional<at::Tensor> dy2) {
+  check_cl(dy, "dy");
+  check_cl(x, "x");
+  check_cl(dx, "dx");
+  TORCH_CHECK(dy.scalar_type() == x.scalar_type() && dx.scalar_type() == x.scalar_type(), "dtype mismatch");
+  TORCH_CHECK(dx.sizes() == x.sizes(), "dx must match x");
+  const gk::PoolGeo pg = pool_geo(x, dy, k, st, pad);
+  const int64_t C = x.size(1);
+  const int64_t M = x.numel() / C;
+  const int eb = x.element_size();
+  TORCH_CHECK(amax.scalar_type() == at::kByte && amax.numel() >= dy.numel(), "amax: uint8[dy.numel]");
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() >= (int64_t)gk::bn_workspace_floats(M, (int)C, eb),
+              "workspace too small");
+  c10::DeviceGuard guard(x.device());
+  const void* d2 = opt_like(dy2, dy, "dy2");
+  gk::bn_relu_pool_backward(dy.data_ptr(), d2, amax.data_ptr<uint8_t>(), x.data_ptr(), dx.data_ptr(), x.size(0), (int)C,
+                            pg, eb, opt_f32(w), mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                            dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), ws.data_ptr<float>(),
+                            opt_f32_mut(gw_acc), opt_f32_mut(gb_acc), cur_stream(x));
 }
 
 // ---------------------------------------------------------------------------
@@ -467,11 +551,19 @@ TORCH_LIBRARY(gksgd, m) {
   m.def(
       "bn_act_forward(Tensor x, Tensor? res, Tensor(a!) y, Tensor(i!)? mask, Tensor? w, Tensor? b, Tensor(b!)? run_mean, "
       "Tensor(c!)? run_var, Tensor(d!) save_mean, Tensor(e!) save_invstd, Tensor(f!) scale, Tensor(g!) shift, "
-      "Tensor(h!) ws, float eps, float momentum, bool relu) -> ()");
+      "Tensor(h!) ws, float eps, float momentum, bool relu, Tensor(j!)? nbt=None) -> ()");
+  m.def(
+      "bn_relu_pool_forward(Tensor x, Tensor(a!) y, Tensor(b!) amax, Tensor? w, Tensor? b, Tensor(c!)? run_mean, "
+      "Tensor(d!)? run_var, Tensor(e!) save_mean, Tensor(f!) save_invstd, Tensor(g!) scale, Tensor(h!) shift, "
+      "Tensor(i!) ws, float eps, float momentum, int k, int s, int p, Tensor(j!)? nbt=None) -> ()");
+  m.def(
+      "bn_relu_pool_backward(Tensor dy, Tensor amax, Tensor x, Tensor(a!) dx, Tensor? w, Tensor mean, "
+      "Tensor invstd, Tensor(b!) dgamma, Tensor(c!) dbeta, Tensor(d!) ws, int k, int s, int p, "
+      "Tensor(e!)? gw_acc=None, Tensor(f!)? gb_acc=None, Tensor? dy2=None) -> ()");
   m.def(
       "bn_act_backward(Tensor dy, Tensor? mask, Tensor x, Tensor(a!) dx, Tensor(b!)? dres, Tensor? w, Tensor mean, "
       "Tensor invstd, Tensor(c!) dgamma, Tensor(d!) dbeta, Tensor(e!) ws, bool relu, Tensor(f!)? gw_acc=None, "
-      "Tensor(g!)? gb_acc=None) -> ()");
+      "Tensor(g!)? gb_acc=None, Tensor? dy2=None) -> ()");
   m.def("accum_grad(Tensor(a!) dst, Tensor src) -> ()");
   m.def("cast_bf16(Tensor(a!) dst, Tensor src) -> ()");
 
@@ -502,6 +594,8 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("clip_grad_norm", &clip_grad_norm);
   m.impl("bn_act_forward", &bn_act_forward);
   m.impl("bn_act_backward", &bn_act_backward);
+  m.impl("bn_relu_pool_forward", &bn_relu_pool_forward);
+  m.impl("bn_relu_pool_backward", &bn_relu_pool_backward);
   m.impl("accum_grad", &accum_grad);
   m.impl("cast_bf16", &cast_bf16);
 }

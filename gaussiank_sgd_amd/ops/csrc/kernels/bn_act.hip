@@ -202,11 +202,12 @@ __global__ __launch_bounds__(kBlock) void bn_finalize_kernel(const float* __rest
                                                              float eps, float momentum, float* __restrict__ run_mean,
                                                              float* __restrict__ run_var, float* __restrict__ save_mean,
                                                              float* __restrict__ save_invstd, float* __restrict__ scale,
-                                                             float* __restrict__ shift) {
+                                                             float* __restrict__ shift, int64_t* __restrict__ nbt) {
   double s = 0.0, q = 0.0;
   bool owner;
   int c;
   reduce_partials2(psum, psq, gy, C, &s, &q, &owner, &c);
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;  // BatchNorm num_batches_tracked
   if (!owner) return;
   const double mean = s / (double)M;
   double var = q / (double)M - mean * mean;
@@ -261,12 +262,168 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const T* __restrict__ 
   }
 }
 
+__device__ __forceinline__ float round_bf16(float f) { return __uint_as_float((uint32_t)f32_to_bf16(f) << 16); }
+
+// Fused BN apply + ReLU + max-pool (the ResNet stem): one thread per 16-byte
+// channel vector of one OUTPUT pixel walks its k x k window, normalises each
+// input on the fly and keeps the max of the (dtype-rounded) pre-ReLU values.
+// max(relu(z)) == relu(max(z)), so the ReLU needs no mask of its own: the
+// window position of the max is stored as one byte per output element
+// (0xff when the max is <= 0, i.e. the ReLU blocks the gradient).  The
+// full-resolution BN output is never written.  Window scan order and the
+// strict '>' (first max wins, NaN propagates) match at::max_pool2d.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void bn_relu_pool_kernel(const T* __restrict__ x, T* __restrict__ y,
+                                                              uint8_t* __restrict__ amax, int64_t P, int C, PoolGeo pg,
+                                                              const float* __restrict__ scale,
+                                                              const float* __restrict__ shift) {
+  constexpr int V = Vec<T>::N;
+  const int cv = C / V;
+  const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (t >= P * cv) return;
+  const int64_t op = t / cv;
+  const int c0 = (int)(t - op * cv) * V;
+  const int64_t ohw = (int64_t)pg.OH * pg.OW;
+  const int64_t n = op / ohw;
+  const int rem = (int)(op - n * ohw);
+  const int oh = rem / pg.OW, ow = rem - (rem / pg.OW) * pg.OW;
+  float sc[V], sf[V], m[V];
+  uint32_t idx[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    sc[i] = scale[c0 + i];
+    sf[i] = shift[c0 + i];
+    m[i] = -INFINITY;
+    idx[i] = 0xffu;
+  }
+  for (int kh = 0; kh < pg.k; ++kh) {
+    const int ih = oh * pg.s - pg.p + kh;
+    if (ih < 0 || ih >= pg.H) continue;
+    for (int kw = 0; kw < pg.k; ++kw) {
+      const int iw = ow * pg.s - pg.p + kw;
+      if (iw < 0 || iw >= pg.W) continue;
+      float v[V];
+      Vec<T>::load(x + ((n * pg.H + ih) * pg.W + iw) * C + c0, v);
+      const uint32_t pos = (uint32_t)(kh * pg.k + kw);
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        float z = fmaf(v[i], sc[i], sf[i]);
+        if (sizeof(T) == 2) z = round_bf16(z);
+        if (z > m[i] || z != z) {
+          m[i] = z;
+          idx[i] = pos;
+        }
+      }
+    }
+  }
+  float o[V];
+  uint32_t packed[2] = {0u, 0u};
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    o[i] = m[i] > 0.f ? m[i] : (m[i] != m[i] ? m[i] : 0.f);
+    const uint32_t b = m[i] > 0.f ? idx[i] : 0xffu;
+    packed[i / 4] |= b << (8 * (i % 4));
+  }
+  Vec<T>::store(y + op * C + c0, o);
+  if (V == 8)
+    *reinterpret_cast<uint2*>(amax + op * C + c0) = make_uint2(packed[0], packed[1]);
+  else
+    *reinterpret_cast<uint32_t*>(amax + op * C + c0) = packed[0];
+}
+
 // ---------------------------------------------------------------------------
 // backward
+//
+// The upstream gradient dz of the BN output is produced by a "source":
+//   DyPlain: dy (optionally gated by the forward's 1-bit ReLU mask);
+//   DyPool : gathered from the max-pool output gradient -- input pixel (h, w)
+//            receives dy_pool[oh, ow] from every window whose stored argmax is
+//            (h, w); the full-resolution pool gradient is never materialised.
 // ---------------------------------------------------------------------------
-template <typename T, bool RELU>
-__global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ mask,
-                                                               const T* __restrict__ x, int64_t M, int C, Geo g,
+//   TWIN   : the BN output was consumed twice (ResNet: next block's conv1 and
+//            its residual / downsample path); the two gradients dy + dy2 are
+//            summed on load instead of by a separate add kernel.
+template <typename T, bool RELU, bool TWIN>
+struct DyPlain {
+  const T* dy;
+  const T* dy2;
+  const uint8_t* mask;
+  __device__ __forceinline__ void load(int64_t r, int C, int c0, float* d) const {
+    constexpr int V = Vec<T>::N;
+    Vec<T>::load(dy + r * C + c0, d);
+    if (TWIN) {
+      float e[V];
+      Vec<T>::load(dy2 + r * C + c0, e);
+#pragma unroll
+      for (int i = 0; i < V; ++i) d[i] += e[i];
+    }
+    if (RELU) {
+      const uint32_t bits = (uint32_t)mask[r * (C / V) + c0 / V];
+#pragma unroll
+      for (int i = 0; i < V; ++i) d[i] = ((bits >> i) & 1u) ? d[i] : 0.f;
+    }
+  }
+};
+
+template <typename T, bool TWIN>
+struct DyPool {
+  const T* dy;          // [N, OH, OW, C]
+  const T* dy2;         // optional second consumer's gradient, same shape
+  const uint8_t* amax;  // [N, OH, OW, C]
+  PoolGeo pg;
+  __device__ __forceinline__ void load(int64_t r, int C, int c0, float* d) const {
+    constexpr int V = Vec<T>::N;
+#pragma unroll
+    for (int i = 0; i < V; ++i) d[i] = 0.f;
+    const uint32_t hw = (uint32_t)(pg.H * pg.W);
+    const uint32_t ru = (uint32_t)r;  // M < 2^32 (host check)
+    const uint32_t n = ru / hw;
+    const int rem = (int)(ru - n * hw);
+    const int ih = rem / pg.W, iw = rem - (rem / pg.W) * pg.W;
+    const int ah = ih + pg.p, aw = iw + pg.p;
+    int oh0 = ah - pg.k + 1;
+    oh0 = oh0 <= 0 ? 0 : (oh0 + pg.s - 1) / pg.s;
+    int oh1 = ah / pg.s;
+    if (oh1 > pg.OH - 1) oh1 = pg.OH - 1;
+    int ow0 = aw - pg.k + 1;
+    ow0 = ow0 <= 0 ? 0 : (ow0 + pg.s - 1) / pg.s;
+    int ow1 = aw / pg.s;
+    if (ow1 > pg.OW - 1) ow1 = pg.OW - 1;
+    for (int oh = oh0; oh <= oh1; ++oh) {
+      for (int ow = ow0; ow <= ow1; ++ow) {
+        const uint32_t pos = (uint32_t)((ah - oh * pg.s) * pg.k + (aw - ow * pg.s));
+        const int64_t o = (((int64_t)n * pg.OH + oh) * pg.OW + ow) * C + c0;
+        uint32_t a[2];
+        if (V == 8) {
+          const uint2 u = *reinterpret_cast<const uint2*>(amax + o);
+          a[0] = u.x;
+          a[1] = u.y;
+        } else {
+          a[0] = *reinterpret_cast<const uint32_t*>(amax + o);
+          a[1] = 0xffffffffu;
+        }
+        bool any = false;
+#pragma unroll
+        for (int i = 0; i < V; ++i) any |= ((a[i / 4] >> (8 * (i % 4))) & 0xffu) == pos;
+        if (!any) continue;
+        float g[V];
+        Vec<T>::load(dy + o, g);
+        if (TWIN) {
+          float e[V];
+          Vec<T>::load(dy2 + o, e);
+#pragma unroll
+          for (int i = 0; i < V; ++i) g[i] += e[i];
+        }
+#pragma unroll
+        for (int i = 0; i < V; ++i)
+          if (((a[i / 4] >> (8 * (i % 4))) & 0xffu) == pos) d[i] += g[i];
+      }
+    }
+  }
+};
+
+template <typename T, typename Src>
+__global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(Src src, const T* __restrict__ x, int64_t M, int C, Geo g,
                                                                const float* __restrict__ mean,
                                                                const float* __restrict__ invstd,
                                                                float* __restrict__ pdb, float* __restrict__ pdg) {
@@ -282,12 +439,11 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const T* __restri
   if (r1 > M) r1 = M;
   for (int64_t r = (lane_r < g.rl ? r0 + lane_r : r1); r < r1; r += g.rl) {
     float d[V], xv[V];
-    Vec<T>::load(dy + r * C + c0, d);
+    src.load(r, C, c0, d);
     Vec<T>::load(x + r * C + c0, xv);
-    const uint32_t bits = RELU ? (uint32_t)mask[r * (C / V) + c0 / V] : 0xffu;
 #pragma unroll
     for (int i = 0; i < V; ++i) {
-      const float dz = ((bits >> i) & 1u) ? d[i] : 0.f;
+      const float dz = d[i];
       sb[i] += dz;
       sg[i] = fmaf(dz, (xv[i] - mu[i]) * is[i], sg[i]);
     }
@@ -329,9 +485,8 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_finalize_kernel(const float* __
   if (gw_acc) gw_acc[c] += (float)b;
 }
 
-template <typename T, bool RELU, bool DRES>
-__global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ mask,
-                                                              const T* __restrict__ x, T* __restrict__ dx,
+template <typename T, typename Src, bool DRES>
+__global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(Src src, const T* __restrict__ x, T* __restrict__ dx,
                                                               T* __restrict__ dres, int64_t M, int C, Geo g,
                                                               const float* __restrict__ w,
                                                               const float* __restrict__ mean,
@@ -359,13 +514,11 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(const T* __restric
   if (r1 > M) r1 = M;
   for (int64_t r = (lane_r < g.rl ? r0 + lane_r : r1); r < r1; r += g.rl) {
     float d[V], xv[V], o[V];
-    Vec<T>::load(dy + r * C + c0, d);
+    src.load(r, C, c0, d);
     Vec<T>::load(x + r * C + c0, xv);
-    const uint32_t bits = RELU ? (uint32_t)mask[r * (C / V) + c0 / V] : 0xffu;
 #pragma unroll
     for (int i = 0; i < V; ++i) {
-      const float dz = ((bits >> i) & 1u) ? d[i] : 0.f;
-      d[i] = dz;
+      const float dz = d[i];
       const float xh = (xv[i] - mu[i]) * is[i];
       o[i] = k1[i] * (dz - k2[i] - xh * k3[i]);
     }
@@ -389,52 +542,64 @@ bool bn_supported(int C, int elem_bytes) {
 }
 
 template <typename T>
-void bn_forward_t(const T* x, const T* res, T* y, uint8_t* mask, int64_t M, int C, const float* w, const float* b, float eps,
-                  float momentum, float* run_mean, float* run_var, float* save_mean, float* save_invstd,
-                  float* scale, float* shift, float* ws, int relu, hipStream_t s) {
+void bn_stats_t(const T* x, int64_t M, int C, const float* w, const float* b, float eps, float momentum,
+                float* run_mean, float* run_var, float* save_mean, float* save_invstd, float* scale, float* shift,
+                float* ws, int64_t* nbt, hipStream_t s) {
   const Geo g = make_geo<T>(M, C, kTargetBlocks);
   float* psum = ws;
   float* psq = ws + (int64_t)g.gy * C;
   hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(g.gx, g.gy), dim3(kBlock), 0, s, x, M, C, g, psum, psq);
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(kBlock), 0, s, psum, psq, g.gy, M, C,
-                     w, b, eps, momentum, run_mean, run_var, save_mean, save_invstd, scale, shift);
-  if (relu && res)
-    hipLaunchKernelGGL((bn_apply_kernel<T, true, true>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, x, res, y, mask, M, C, g,
-                       scale, shift);
-  else if (relu)
-    hipLaunchKernelGGL((bn_apply_kernel<T, true, false>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, x, res, y, mask, M, C, g,
-                       scale, shift);
-  else if (res)
-    hipLaunchKernelGGL((bn_apply_kernel<T, false, true>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, x, res, y, mask, M, C, g,
-                       scale, shift);
-  else
-    hipLaunchKernelGGL((bn_apply_kernel<T, false, false>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, x, res, y, mask, M, C, g,
-                       scale, shift);
+                     w, b, eps, momentum, run_mean, run_var, save_mean, save_invstd, scale, shift, nbt);
 }
 
 template <typename T>
-void bn_backward_t(const T* dy, const uint8_t* mask, const T* x, T* dx, T* dres, int64_t M, int C, const float* w,
-                   const float* mean, const float* invstd, float* dgamma, float* dbeta, float* ws, int relu,
-                   float* gw_acc, float* gb_acc, hipStream_t s) {
+void bn_forward_t(const T* x, const T* res, T* y, uint8_t* mask, int64_t M, int C, const float* w, const float* b, float eps,
+                  float momentum, float* run_mean, float* run_var, float* save_mean, float* save_invstd,
+                  float* scale, float* shift, float* ws, int relu, int64_t* nbt, hipStream_t s) {
+  const Geo g = make_geo<T>(M, C, kTargetBlocks);
+  bn_stats_t<T>(x, M, C, w, b, eps, momentum, run_mean, run_var, save_mean, save_invstd, scale, shift, ws, nbt, s);
+#define GK_APPLY(R, D)                                                                                             \
+  hipLaunchKernelGGL((bn_apply_kernel<T, R, D>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, x, res, y, mask, M, C, g, scale, \
+                     shift)
+  if (relu && res) GK_APPLY(true, true);
+  else if (relu) GK_APPLY(true, false);
+  else if (res) GK_APPLY(false, true);
+  else GK_APPLY(false, false);
+#undef GK_APPLY
+}
+
+template <typename T, typename Src>
+void bn_backward_src(Src src, const T* x, T* dx, T* dres, int64_t M, int C, const float* w, const float* mean,
+                     const float* invstd, float* dgamma, float* dbeta, float* ws, float* gw_acc, float* gb_acc,
+                     hipStream_t s) {
   const Geo g = make_geo<T>(M, C, kTargetBlocks);
   float* pdb = ws;
   float* pdg = ws + (int64_t)g.gy * C;
-  if (relu)
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, dy, mask, x, M, C, g,
-                       mean, invstd, pdb, pdg);
-  else
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, dy, mask, x, M, C, g,
-                       mean, invstd, pdb, pdg);
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, Src>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, src, x, M, C, g, mean,
+                     invstd, pdb, pdg);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(kBlock), 0, s, pdb, pdg, g.gy, C,
                      dbeta, dgamma, gb_acc, gw_acc);
-#define GK_BWD_APPLY(R, D)                                                                                       \
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, R, D>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, dy, mask, x, dx, dres, M, \
-                     C, g, w, mean, invstd, dbeta, dgamma)
-  if (relu && dres) GK_BWD_APPLY(true, true);
-  else if (relu) GK_BWD_APPLY(true, false);
-  else if (dres) GK_BWD_APPLY(false, true);
-  else GK_BWD_APPLY(false, false);
-#undef GK_BWD_APPLY
+  if (dres)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, Src, true>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, src, x, dx, dres, M,
+                       C, g, w, mean, invstd, dbeta, dgamma);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, Src, false>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, src, x, dx, dres,
+                       M, C, g, w, mean, invstd, dbeta, dgamma);
+}
+
+template <typename T>
+void bn_backward_t(const T* dy, const T* dy2, const uint8_t* mask, const T* x, T* dx, T* dres, int64_t M, int C,
+                   const float* w, const float* mean, const float* invstd, float* dgamma, float* dbeta, float* ws,
+                   int relu, float* gw_acc, float* gb_acc, hipStream_t s) {
+#define GK_BWD(R, TW)                                                                                              \
+  bn_backward_src<T>(DyPlain<T, R, TW>{dy, dy2, mask}, x, dx, dres, M, C, w, mean, invstd, dgamma, dbeta, ws, gw_acc, \
+                     gb_acc, s)
+  if (relu && dy2) GK_BWD(true, true);
+  else if (relu) GK_BWD(true, false);
+  else if (dy2) GK_BWD(false, true);
+  else GK_BWD(false, false);
+#undef GK_BWD
 }
 
 size_t bn_mask_bytes(int64_t M, int C, int elem_bytes) { return (size_t)M * (size_t)(C / (elem_bytes == 2 ? 8 : 4)); }
@@ -442,24 +607,73 @@ size_t bn_mask_bytes(int64_t M, int C, int elem_bytes) { return (size_t)M * (siz
 void bn_act_forward(const void* x, const void* res, void* y, uint8_t* mask, int64_t M, int C, int elem_bytes,
                     const float* w, const float* b, float eps, float momentum, float* run_mean, float* run_var,
                     float* save_mean, float* save_invstd, float* scale, float* shift, float* ws, int relu,
-                    hipStream_t s) {
+                    int64_t* nbt, hipStream_t s) {
   if (elem_bytes == 2)
     bn_forward_t<uint16_t>((const uint16_t*)x, (const uint16_t*)res, (uint16_t*)y, mask, M, C, w, b, eps, momentum,
-                           run_mean, run_var, save_mean, save_invstd, scale, shift, ws, relu, s);
+                           run_mean, run_var, save_mean, save_invstd, scale, shift, ws, relu, nbt, s);
   else
     bn_forward_t<float>((const float*)x, (const float*)res, (float*)y, mask, M, C, w, b, eps, momentum, run_mean,
-                        run_var, save_mean, save_invstd, scale, shift, ws, relu, s);
+                        run_var, save_mean, save_invstd, scale, shift, ws, relu, nbt, s);
 }
 
-void bn_act_backward(const void* dy, const uint8_t* mask, const void* x, void* dx, void* dres, int64_t M, int C,
-                     int elem_bytes, const float* w, const float* mean, const float* invstd, float* dgamma,
-                     float* dbeta, float* ws, int relu, float* gw_acc, float* gb_acc, hipStream_t s) {
+void bn_act_backward(const void* dy, const void* dy2, const uint8_t* mask, const void* x, void* dx, void* dres,
+                     int64_t M, int C, int elem_bytes, const float* w, const float* mean, const float* invstd,
+                     float* dgamma, float* dbeta, float* ws, int relu, float* gw_acc, float* gb_acc, hipStream_t s) {
   if (elem_bytes == 2)
-    bn_backward_t<uint16_t>((const uint16_t*)dy, mask, (const uint16_t*)x, (uint16_t*)dx, (uint16_t*)dres, M, C, w,
-                            mean, invstd, dgamma, dbeta, ws, relu, gw_acc, gb_acc, s);
+    bn_backward_t<uint16_t>((const uint16_t*)dy, (const uint16_t*)dy2, mask, (const uint16_t*)x, (uint16_t*)dx,
+                            (uint16_t*)dres, M, C, w, mean, invstd, dgamma, dbeta, ws, relu, gw_acc, gb_acc, s);
   else
-    bn_backward_t<float>((const float*)dy, mask, (const float*)x, (float*)dx, (float*)dres, M, C, w, mean, invstd,
-                         dgamma, dbeta, ws, relu, gw_acc, gb_acc, s);
+    bn_backward_t<float>((const float*)dy, (const float*)dy2, mask, (const float*)x, (float*)dx, (float*)dres, M, C, w,
+                         mean, invstd, dgamma, dbeta, ws, relu, gw_acc, gb_acc, s);
+}
+
+// ---------------------------------------------------------------------------
+// BN + ReLU + max-pool
+// ---------------------------------------------------------------------------
+void bn_relu_pool_forward(const void* x, void* y, uint8_t* amax, int64_t N, int C, PoolGeo pg, int elem_bytes,
+                          const float* w, const float* b, float eps, float momentum, float* run_mean, float* run_var,
+                          float* save_mean, float* save_invstd, float* scale, float* shift, float* ws, int64_t* nbt,
+                          hipStream_t s) {
+  const int64_t M = N * pg.H * pg.W;
+  const int64_t P = N * pg.OH * pg.OW;
+  const int V = elem_bytes == 2 ? 8 : 4;
+  const int64_t threads = P * (C / V);
+  const dim3 grid((unsigned)((threads + kBlock - 1) / kBlock));
+  if (elem_bytes == 2) {
+    bn_stats_t<uint16_t>((const uint16_t*)x, M, C, w, b, eps, momentum, run_mean, run_var, save_mean, save_invstd,
+                         scale, shift, ws, nbt, s);
+    hipLaunchKernelGGL(bn_relu_pool_kernel<uint16_t>, grid, dim3(kBlock), 0, s, (const uint16_t*)x, (uint16_t*)y, amax,
+                       P, C, pg, scale, shift);
+  } else {
+    bn_stats_t<float>((const float*)x, M, C, w, b, eps, momentum, run_mean, run_var, save_mean, save_invstd, scale,
+                       shift, ws, nbt, s);
+    hipLaunchKernelGGL(bn_relu_pool_kernel<float>, grid, dim3(kBlock), 0, s, (const float*)x, (float*)y, amax, P, C, pg,
+                       scale, shift);
+  }
+}
+
+template <typename T>
+void bn_pool_backward_t(const T* dy, const T* dy2, const uint8_t* amax, const T* x, T* dx, int64_t M, int C, PoolGeo pg,
+                        const float* w, const float* mean, const float* invstd, float* dgamma, float* dbeta, float* ws,
+                        float* gw_acc, float* gb_acc, hipStream_t s) {
+  if (dy2)
+    bn_backward_src<T>(DyPool<T, true>{dy, dy2, amax, pg}, x, dx, (T*)nullptr, M, C, w, mean, invstd, dgamma, dbeta,
+                       ws, gw_acc, gb_acc, s);
+  else
+    bn_backward_src<T>(DyPool<T, false>{dy, dy2, amax, pg}, x, dx, (T*)nullptr, M, C, w, mean, invstd, dgamma, dbeta,
+                       ws, gw_acc, gb_acc, s);
+}
+
+void bn_relu_pool_backward(const void* dy, const void* dy2, const uint8_t* amax, const void* x, void* dx, int64_t N,
+                           int C, PoolGeo pg, int elem_bytes, const float* w, const float* mean, const float* invstd,
+                           float* dgamma, float* dbeta, float* ws, float* gw_acc, float* gb_acc, hipStream_t s) {
+  const int64_t M = N * pg.H * pg.W;
+  if (elem_bytes == 2)
+    bn_pool_backward_t<uint16_t>((const uint16_t*)dy, (const uint16_t*)dy2, amax, (const uint16_t*)x, (uint16_t*)dx, M,
+                                 C, pg, w, mean, invstd, dgamma, dbeta, ws, gw_acc, gb_acc, s);
+  else
+    bn_pool_backward_t<float>((const float*)dy, (const float*)dy2, amax, (const float*)x, (float*)dx, M, C, pg, w, mean,
+                              invstd, dgamma, dbeta, ws, gw_acc, gb_acc, s);
 }
 
 }  // namespace gk

@@ -167,9 +167,27 @@ size_t bn_mask_bytes(int64_t M, int C, int elem_bytes);
 void bn_act_forward(const void* x, const void* res, void* y, uint8_t* mask, int64_t M, int C, int elem_bytes,
                     const float* w, const float* b, float eps, float momentum, float* run_mean, float* run_var,
                     float* save_mean, float* save_invstd, float* scale, float* shift, float* ws, int relu,
-                    hipStream_t stream);
-void bn_act_backward(const void* dy, const uint8_t* mask, const void* x, void* dx, void* dres, int64_t M, int C,
-                     int elem_bytes, const float* w, const float* mean, const float* invstd, float* dgamma,
-                     float* dbeta, float* ws, int relu, float* gw_acc, float* gb_acc, hipStream_t stream);
+                    int64_t* nbt, hipStream_t stream);
+// dy2 (optional): a second upstream gradient of the same output, summed on load.
+void bn_act_backward(const void* dy, const void* dy2, const uint8_t* mask, const void* x, void* dx, void* dres,
+                     int64_t M, int C, int elem_bytes, const float* w, const float* mean, const float* invstd,
+                     float* dgamma, float* dbeta, float* ws, int relu, float* gw_acc, float* gb_acc,
+                     hipStream_t stream);
+
+// BN (training) + ReLU + k x k / stride s / pad p max-pool, channels-last
+// [N, H, W, C] -> [N, OH, OW, C].  amax: one byte per OUTPUT element (window
+// position of the max, 0xff when the ReLU blocks the gradient).  The backward
+// gathers the pool gradient straight into the BN backward passes.
+// Requires N*H*W < 2^32.
+struct PoolGeo {
+  int H, W, OH, OW, k, s, p;
+};
+void bn_relu_pool_forward(const void* x, void* y, uint8_t* amax, int64_t N, int C, PoolGeo pg, int elem_bytes,
+                          const float* w, const float* b, float eps, float momentum, float* run_mean, float* run_var,
+                          float* save_mean, float* save_invstd, float* scale, float* shift, float* ws, int64_t* nbt,
+                          hipStream_t stream);
+void bn_relu_pool_backward(const void* dy, const void* dy2, const uint8_t* amax, const void* x, void* dx, int64_t N,
+                           int C, PoolGeo pg, int elem_bytes, const float* w, const float* mean, const float* invstd,
+                           float* dgamma, float* dbeta, float* ws, float* gw_acc, float* gb_acc, hipStream_t stream);
 
 }  // namespace gk

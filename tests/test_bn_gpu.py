@@ -76,3 +76,62 @@ def test_resnet50_fused_vs_unfused(cuda):
         e_fused = float((p1.grad.double() - ref).norm() / (ref.norm() + 1e-30))
         e_vendor = float((p2.grad.double() - ref).norm() / (ref.norm() + 1e-30))
         assert e_fused <= 3 * e_vendor + 1e-4, (n, e_fused, e_vendor)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape,pool", [((2, 64, 32, 32), (3, 2, 1)), ((3, 16, 17, 13), (3, 2, 1)),
+                                        ((2, 32, 16, 16), (2, 2, 0)), ((2, 8, 9, 11), (3, 1, 1))])
+def test_bn_relu_maxpool_matches_torch(cuda, dtype, shape, pool):
+    """Fused BN + ReLU + max-pool (argmax bytes, gathered backward) vs
+    BatchNorm2d + relu + max_pool2d in fp32."""
+    torch.manual_seed(0)
+    N, C, H, W = shape
+    bn = BNAct(C, act="relu", pool=pool).to(cuda)
+    ref = torch.nn.BatchNorm2d(C).to(cuda)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+        ref.weight.copy_(bn.weight)
+        ref.bias.copy_(bn.bias)
+    x0 = (torch.randn(shape, device=cuda) * 2 + 0.3).to(dtype).contiguous(memory_format=torch.channels_last)
+    x = x0.clone().requires_grad_(True)
+    y = bn(x)
+    g0 = torch.randn(y.shape, device=cuda).to(dtype).contiguous(memory_format=torch.channels_last)
+    y.backward(g0)
+    xr = x0.float().clone().requires_grad_(True)
+    yr = F.max_pool2d(F.relu(ref(xr)), *pool)
+    yr.backward(g0.float())
+    assert y.shape == yr.shape and y.dtype == dtype and y.is_contiguous(memory_format=torch.channels_last)
+    if dtype == torch.float32:
+        assert torch.allclose(y, yr, atol=1e-4, rtol=1e-4)
+        assert torch.allclose(x.grad, xr.grad, atol=1e-4, rtol=1e-4)
+        assert torch.allclose(bn.weight.grad, ref.weight.grad, atol=1e-3, rtol=1e-4)
+        assert torch.allclose(bn.bias.grad, ref.bias.grad, atol=1e-3, rtol=1e-4)
+    else:
+        assert torch.allclose(y.float(), yr, atol=3e-2, rtol=2e-2)
+        err = float((x.grad.float() - xr.grad).norm() / xr.grad.norm())
+        assert err < 3e-2, err
+        for a, b in ((bn.weight.grad, ref.weight.grad), (bn.bias.grad, ref.bias.grad)):
+            assert float((a - b).norm() / b.norm()) < 3e-2
+    assert torch.allclose(bn.running_mean, ref.running_mean, atol=1e-3, rtol=1e-3)
+    assert torch.allclose(bn.running_var, ref.running_var, atol=1e-3, rtol=1e-3)
+    assert int(bn.num_batches_tracked) == 1
+
+
+@pytest.mark.parametrize("pool", [None, (3, 2, 1)])
+def test_bnact_twin_sums_both_gradients(cuda, pool):
+    """twin=True: two handles on one output; the fused backward sums dy + dy2."""
+    torch.manual_seed(0)
+    N, C, H, W = 2, 32, 12, 12
+    bn = BNAct(C, act="relu", pool=pool, twin=True).to(cuda)
+    ref = BNAct(C, act="relu", pool=pool, twin=True, fused=False).to(cuda)
+    x0 = torch.randn(N, C, H, W, device=cuda).contiguous(memory_format=torch.channels_last)
+    outs = []
+    for m in (bn, ref):
+        x = x0.clone().requires_grad_(True)
+        a, b = m(x)
+        g1 = torch.linspace(-1, 1, a.numel(), device=cuda).view_as(a)
+        ((a * g1).sum() + (b * b).sum()).backward()
+        outs.append((a.detach(), x.grad, m.weight.grad, m.bias.grad))
+    for u, v in zip(*outs):
+        assert torch.allclose(u, v, atol=1e-4, rtol=1e-4)

@@ -195,3 +195,15 @@ def test_install_shadow_is_noop_on_cpu():
     opt = hvd.DistributedOptimizer(torch.optim.SGD(net.parameters(), lr=0.1, momentum=0.9),
                                    named_parameters=net.named_parameters(), compression=compressors["none"])
     assert install_bf16_shadow(net, opt) == 0
+
+
+def test_bnact_pool_fallback_matches_torch():
+    from gaussiank_sgd_amd.ops.bn import BNAct
+    torch.manual_seed(0)
+    bn = BNAct(8, act="relu", pool=(3, 2, 1))
+    ref = torch.nn.BatchNorm2d(8)
+    x = torch.randn(2, 8, 9, 9)
+    y = bn(x)
+    yr = torch.nn.functional.max_pool2d(torch.relu(ref(x)), 3, 2, 1)
+    assert y.shape == (2, 8, 5, 5) and torch.allclose(y, yr, atol=1e-6)
+    assert set(bn.state_dict()) == set(ref.state_dict())
