@@ -474,8 +474,6 @@ def fused_sgd_(w: torch.Tensor, m: Optional[torch.Tensor], g: torch.Tensor, chun
                          [int(bool(p.get("first_step", False))) for p in groups], bool(zero_grad), grad_scale,
                          w_bf16)
         return
-    if w_bf16 is not None:
-        raise ValueError("bf16 shadow weights are a GPU feature")
     gs = float(grad_scale) if grad_scale is not None else 1.0
     for start, ln, gi, _ in _decode_chunks(chunks):
         p = groups[gi]
@@ -493,6 +491,8 @@ def fused_sgd_(w: torch.Tensor, m: Optional[torch.Tensor], g: torch.Tensor, chun
                 ms.mul_(mom).add_(d, alpha=1 - float(p.get("dampening", 0.0)))
             d = d + mom * ms if p.get("nesterov", False) else ms
         ws.add_(d, alpha=-float(p["lr"]))
+        if w_bf16 is not None:
+            w_bf16[start:start + ln].copy_(ws)
         if zero_grad:
             g[start:start + ln].zero_()
 

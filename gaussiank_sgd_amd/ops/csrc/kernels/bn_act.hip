@@ -365,12 +365,39 @@ struct DyPlain {
   }
 };
 
-template <typename T, bool TWIN>
+// WM = 2: at most 2 windows per dimension cover an input pixel (k <= 2s, e.g.
+// the 3x3/s2 stem pool): the <= 4 candidate windows are fixed, so all their
+// argmax bytes and gradient vectors are loaded up front (independent loads in
+// flight) and matched afterwards.  WM = 0: generic k, s (runtime loops).
+template <typename T, bool TWIN, int WM>
 struct DyPool {
   const T* dy;          // [N, OH, OW, C]
   const T* dy2;         // optional second consumer's gradient, same shape
   const uint8_t* amax;  // [N, OH, OW, C]
   PoolGeo pg;
+
+  __device__ __forceinline__ void load_amax(int64_t o, uint32_t* a) const {
+    constexpr int V = Vec<T>::N;
+    if (V == 8) {
+      const uint2 u = *reinterpret_cast<const uint2*>(amax + o);
+      a[0] = u.x;
+      a[1] = u.y;
+    } else {
+      a[0] = *reinterpret_cast<const uint32_t*>(amax + o);
+      a[1] = 0xffffffffu;
+    }
+  }
+  __device__ __forceinline__ void load_g(int64_t o, float* g) const {
+    constexpr int V = Vec<T>::N;
+    Vec<T>::load(dy + o, g);
+    if (TWIN) {
+      float e[V];
+      Vec<T>::load(dy2 + o, e);
+#pragma unroll
+      for (int i = 0; i < V; ++i) g[i] += e[i];
+    }
+  }
+
   __device__ __forceinline__ void load(int64_t r, int C, int c0, float* d) const {
     constexpr int V = Vec<T>::N;
 #pragma unroll
@@ -389,34 +416,47 @@ struct DyPool {
     ow0 = ow0 <= 0 ? 0 : (ow0 + pg.s - 1) / pg.s;
     int ow1 = aw / pg.s;
     if (ow1 > pg.OW - 1) ow1 = pg.OW - 1;
-    for (int oh = oh0; oh <= oh1; ++oh) {
-      for (int ow = ow0; ow <= ow1; ++ow) {
-        const uint32_t pos = (uint32_t)((ah - oh * pg.s) * pg.k + (aw - ow * pg.s));
-        const int64_t o = (((int64_t)n * pg.OH + oh) * pg.OW + ow) * C + c0;
-        uint32_t a[2];
-        if (V == 8) {
-          const uint2 u = *reinterpret_cast<const uint2*>(amax + o);
-          a[0] = u.x;
-          a[1] = u.y;
-        } else {
-          a[0] = *reinterpret_cast<const uint32_t*>(amax + o);
-          a[1] = 0xffffffffu;
-        }
-        bool any = false;
+    const int64_t nbase = (int64_t)n * pg.OH;
+    if (WM == 2) {
+      uint32_t a[4][2];
+      float g[4][V];
+      uint32_t pos[4];
 #pragma unroll
-        for (int i = 0; i < V; ++i) any |= ((a[i / 4] >> (8 * (i % 4))) & 0xffu) == pos;
-        if (!any) continue;
-        float g[V];
-        Vec<T>::load(dy + o, g);
-        if (TWIN) {
-          float e[V];
-          Vec<T>::load(dy2 + o, e);
+      for (int j = 0; j < 4; ++j) {
+        const int oh = oh1 - 1 + (j >> 1), ow = ow1 - 1 + (j & 1);
+        const bool valid = oh >= oh0 && ow >= ow0;
+        pos[j] = (uint32_t)((ah - oh * pg.s) * pg.k + (aw - ow * pg.s));
+        a[j][0] = a[j][1] = 0xffffffffu;
 #pragma unroll
-          for (int i = 0; i < V; ++i) g[i] += e[i];
+        for (int i = 0; i < V; ++i) g[j][i] = 0.f;
+        if (valid) {
+          const int64_t o = ((nbase + oh) * pg.OW + ow) * C + c0;
+          load_amax(o, a[j]);
+          load_g(o, g[j]);
         }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int i = 0; i < V; ++i)
-          if (((a[i / 4] >> (8 * (i % 4))) & 0xffu) == pos) d[i] += g[i];
+          if (((a[j][i / 4] >> (8 * (i % 4))) & 0xffu) == pos[j]) d[i] += g[j][i];
+      return;
+    }
+    for (int oh = oh0; oh <= oh1; ++oh) {
+      for (int ow = ow0; ow <= ow1; ++ow) {
+        const uint32_t p = (uint32_t)((ah - oh * pg.s) * pg.k + (aw - ow * pg.s));
+        const int64_t o = ((nbase + oh) * pg.OW + ow) * C + c0;
+        uint32_t a[2];
+        load_amax(o, a);
+        bool any = false;
+#pragma unroll
+        for (int i = 0; i < V; ++i) any |= ((a[i / 4] >> (8 * (i % 4))) & 0xffu) == p;
+        if (!any) continue;
+        float g[V];
+        load_g(o, g);
+#pragma unroll
+        for (int i = 0; i < V; ++i)
+          if (((a[i / 4] >> (8 * (i % 4))) & 0xffu) == p) d[i] += g[i];
       }
     }
   }
@@ -528,11 +568,14 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(Src src, const T* 
 }
 
 constexpr int kTargetBlocks = 1024;
+constexpr int kPoolTargetBlocks = 4096;
 
 }  // namespace
 
 size_t bn_workspace_floats(int64_t M, int C, int elem_bytes) {
-  const Geo g = elem_bytes == 2 ? make_geo<uint16_t>(M, C, kTargetBlocks) : make_geo<float>(M, C, kTargetBlocks);
+  // sized for the larger (pool-backward) grid so one workspace fits every pass
+  const Geo g =
+      elem_bytes == 2 ? make_geo<uint16_t>(M, C, kPoolTargetBlocks) : make_geo<float>(M, C, kPoolTargetBlocks);
   return (size_t)2 * g.gy * C;
 }
 
@@ -572,8 +615,8 @@ void bn_forward_t(const T* x, const T* res, T* y, uint8_t* mask, int64_t M, int 
 template <typename T, typename Src>
 void bn_backward_src(Src src, const T* x, T* dx, T* dres, int64_t M, int C, const float* w, const float* mean,
                      const float* invstd, float* dgamma, float* dbeta, float* ws, float* gw_acc, float* gb_acc,
-                     hipStream_t s) {
-  const Geo g = make_geo<T>(M, C, kTargetBlocks);
+                     hipStream_t s, int target_blocks = kTargetBlocks) {
+  const Geo g = make_geo<T>(M, C, target_blocks);
   float* pdb = ws;
   float* pdg = ws + (int64_t)g.gy * C;
   hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, Src>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, src, x, M, C, g, mean,
@@ -652,16 +695,28 @@ void bn_relu_pool_forward(const void* x, void* y, uint8_t* amax, int64_t N, int 
   }
 }
 
+template <typename T, bool TWIN>
+void bn_pool_backward_tw(const T* dy, const T* dy2, const uint8_t* amax, const T* x, T* dx, int64_t M, int C,
+                         PoolGeo pg, const float* w, const float* mean, const float* invstd, float* dgamma,
+                         float* dbeta, float* ws, float* gw_acc, float* gb_acc, hipStream_t s) {
+  // the gather is latency-bound: use more workgroups than the plain BN passes
+  if ((pg.k + pg.s - 1) / pg.s <= 2)
+    bn_backward_src<T>(DyPool<T, TWIN, 2>{dy, dy2, amax, pg}, x, dx, (T*)nullptr, M, C, w, mean, invstd, dgamma,
+                       dbeta, ws, gw_acc, gb_acc, s, kPoolTargetBlocks);
+  else
+    bn_backward_src<T>(DyPool<T, TWIN, 0>{dy, dy2, amax, pg}, x, dx, (T*)nullptr, M, C, w, mean, invstd, dgamma,
+                       dbeta, ws, gw_acc, gb_acc, s, kPoolTargetBlocks);
+}
+
 template <typename T>
 void bn_pool_backward_t(const T* dy, const T* dy2, const uint8_t* amax, const T* x, T* dx, int64_t M, int C, PoolGeo pg,
                         const float* w, const float* mean, const float* invstd, float* dgamma, float* dbeta, float* ws,
                         float* gw_acc, float* gb_acc, hipStream_t s) {
   if (dy2)
-    bn_backward_src<T>(DyPool<T, true>{dy, dy2, amax, pg}, x, dx, (T*)nullptr, M, C, w, mean, invstd, dgamma, dbeta,
-                       ws, gw_acc, gb_acc, s);
+    bn_pool_backward_tw<T, true>(dy, dy2, amax, x, dx, M, C, pg, w, mean, invstd, dgamma, dbeta, ws, gw_acc, gb_acc, s);
   else
-    bn_backward_src<T>(DyPool<T, false>{dy, dy2, amax, pg}, x, dx, (T*)nullptr, M, C, w, mean, invstd, dgamma, dbeta,
-                       ws, gw_acc, gb_acc, s);
+    bn_pool_backward_tw<T, false>(dy, dy2, amax, x, dx, M, C, pg, w, mean, invstd, dgamma, dbeta, ws, gw_acc, gb_acc,
+                                  s);
 }
 
 void bn_relu_pool_backward(const void* dy, const void* dy2, const uint8_t* amax, const void* x, void* dx, int64_t N,

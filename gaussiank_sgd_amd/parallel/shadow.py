@@ -17,8 +17,9 @@ MI355X (profiles/r01_resnet50_bs256_fusedbn_kernel_stats.csv).
     ready to the bucket engine exactly as on the plain path;
   * ``BNAct`` modules get the same direct path for gamma/beta: the BN backward
     kernel adds them into the arena.
-Outside autocast (or on the CPU) modules fall back to their fp32 parameters,
-so the model stays usable for evaluation and CPU tests.
+Outside bf16 autocast modules fall back to their fp32 parameters, so the
+model stays usable for fp32 evaluation.  (CPU autocast works too -- the ops
+have PyTorch fallbacks -- which is how the CPU tests check the wiring.)
 """
 from __future__ import annotations
 
@@ -46,7 +47,8 @@ class _ShadowWeight(torch.autograd.Function):
 def _shadow(module: nn.Module, name: str, x: torch.Tensor):
     info = module._gk_shadow.get(name)
     p = getattr(module, name)
-    if info is None or not x.is_cuda or not torch.is_autocast_enabled("cuda"):
+    dev = x.device.type
+    if info is None or not torch.is_autocast_enabled(dev) or torch.get_autocast_dtype(dev) != torch.bfloat16:
         return p
     shadow, sink = info
     if torch.is_grad_enabled() and p.requires_grad:
@@ -73,8 +75,6 @@ def install_bf16_shadow(model: nn.Module, opt) -> int:
     of parameters that now bypass AccumulateGrad.
     """
     arena = opt.arena
-    if arena.device.type != "cuda":
-        return 0
     shadow = opt._ensure_shadow()
     names = opt._parameter_names
     count = 0

@@ -57,4 +57,15 @@ if [ "$MODE" = ab ]; then
   step bench_b 600 python bench.py --steps 20 --warmup 10 ${AB:---no-shadow} --json-out $OUT/bench_b.json
   step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 5 --warmup 3
 fi
+# MIOpen solver A/B: the ASM implicit-GEMM bwd/wrw solvers need a zero-fill
+# (SubTensorOpWithScalar) of their output before every call.
+if [ "$MODE" = solvers ]; then
+  step bench_base 600 python bench.py --steps 20 --warmup 10 --json-out $OUT/bench_base.json
+  MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_BWD_GTC_XDLOPS_NHWC=0 \
+    step bench_nobwd 600 python bench.py --steps 20 --warmup 10 --json-out $OUT/bench_nobwd.json
+  MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_WRW_GTC_XDLOPS_NHWC=0 \
+    step bench_nowrw 600 python bench.py --steps 20 --warmup 10 --json-out $OUT/bench_nowrw.json
+  MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_BWD_GTC_XDLOPS_NHWC=0 MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_WRW_GTC_XDLOPS_NHWC=0 \
+    step bench_noboth 600 python bench.py --steps 20 --warmup 10 --json-out $OUT/bench_noboth.json
+fi
 echo done

@@ -188,22 +188,35 @@ def test_post_accumulate_hook_fires_for_direct_grads():
     assert torch.equal(sink_got[0], torch.full((4,), 3.0))
 
 
-def test_install_shadow_is_noop_on_cpu():
-    from gaussiank_sgd_amd.models import resnet50
+def test_shadow_matches_autocast_cpu():
+    """bf16 shadow weights + direct arena grads == plain bf16 autocast (CPU)."""
+    from gaussiank_sgd_amd.models import resnet18
     from gaussiank_sgd_amd.parallel import install_bf16_shadow
-    net = resnet50(num_classes=10)
-    opt = hvd.DistributedOptimizer(torch.optim.SGD(net.parameters(), lr=0.1, momentum=0.9),
-                                   named_parameters=net.named_parameters(), compression=compressors["none"])
-    assert install_bf16_shadow(net, opt) == 0
 
+    def run(shadow):
+        torch.manual_seed(0)
+        net = resnet18(num_classes=10)
+        opt = hvd.DistributedOptimizer(torch.optim.SGD(net.parameters(), lr=0.01, momentum=0.9),
+                                       named_parameters=net.named_parameters(), compression=compressors["none"])
+        n = install_bf16_shadow(net, opt) if shadow else 0
+        g = torch.Generator().manual_seed(1)
+        losses = []
+        for _ in range(2):
+            x = torch.randn(4, 3, 32, 32, generator=g)
+            y = torch.randint(0, 10, (4,), generator=g)
+            opt.zero_grad()
+            with torch.autocast("cpu", dtype=torch.bfloat16):
+                loss = torch.nn.functional.cross_entropy(net(x), y)
+            loss.backward()
+            grads = opt.arena.grads.clone()
+            opt.step()
+            losses.append(float(loss))
+        return n, losses, grads, opt
 
-def test_bnact_pool_fallback_matches_torch():
-    from gaussiank_sgd_amd.ops.bn import BNAct
-    torch.manual_seed(0)
-    bn = BNAct(8, act="relu", pool=(3, 2, 1))
-    ref = torch.nn.BatchNorm2d(8)
-    x = torch.randn(2, 8, 9, 9)
-    y = bn(x)
-    yr = torch.nn.functional.max_pool2d(torch.relu(ref(x)), 3, 2, 1)
-    assert y.shape == (2, 8, 5, 5) and torch.allclose(y, yr, atol=1e-6)
-    assert set(bn.state_dict()) == set(ref.state_dict())
+    _, la, ga, oa = run(False)
+    n, lb, gb, ob = run(True)
+    assert n == sum(1 for _ in resnet18(num_classes=10).parameters())  # conv/fc via shadow, BN direct
+    assert la == lb
+    assert torch.equal(ga, gb)
+    assert torch.equal(oa.arena.weights, ob.arena.weights)
+    assert torch.equal(ob.arena.shadow, ob.arena.weights.to(torch.bfloat16))

@@ -218,12 +218,42 @@ def test_fused_sgd_vs_torch(cuda):
             gr[offs[i]:offs[i] + gg.numel()] = gg.view(-1).to(cuda)
         opt.step()
         hp = [dict(cfg, first_step=(step == 0)) for cfg in groups_cfg]
-        ops.fused_sgd_(w, m, gr, chunks, hp, zero_grad=True)
+        shadow = torch.zeros(o, dtype=torch.bfloat16, device=cuda)
+        ops.fused_sgd_(w, m, gr, chunks, hp, zero_grad=True, w_bf16=shadow)
         torch.cuda.synchronize()
         assert float(gr.abs().sum()) == 0.0
+        assert torch.equal(shadow, w.to(torch.bfloat16))  # RNE cast written in the same pass
         for i, p in enumerate(ref_params):
             got = w[offs[i]:offs[i] + p.numel()].cpu().view(p.shape)
             assert torch.allclose(got, p.detach(), atol=1e-6, rtol=1e-5), (step, i)
+
+
+@pytest.mark.parametrize("n,off", [(1 << 20, 0), (12345, 0), (4097, 3), (7, 1)])
+def test_accum_grad_and_cast_bf16(cuda, n, off):
+    torch.manual_seed(0)
+    base = torch.randn(n + off, device=cuda)
+    dst = base[off:]                     # possibly unaligned fp32 view
+    src = torch.randn(n + off, device=cuda).to(torch.bfloat16)[off:]
+    want = dst.clone() + src.float()
+    ops.accum_grad_(dst, src)
+    assert torch.equal(dst, want)
+    src32 = torch.randn(n, device=cuda)
+    want = dst.clone() + src32
+    ops.accum_grad_(dst, src32)
+    assert torch.equal(dst, want)
+    sh = torch.empty(n, dtype=torch.bfloat16, device=cuda)
+    ops.cast_bf16_(sh, dst)
+    assert torch.equal(sh, dst.to(torch.bfloat16))
+
+
+def test_accum_grad_channels_last(cuda):
+    w = torch.zeros(64, 32, 3, 3, device=cuda).to(memory_format=torch.channels_last)
+    g = torch.randn(64, 32, 3, 3, device=cuda).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    ops.accum_grad_(w, g)
+    assert torch.equal(w, g.float())
+    g2 = torch.randn(64, 32, 3, 3, device=cuda).to(torch.bfloat16)  # contiguous: different strides
+    ops.accum_grad_(w, g2)
+    assert torch.allclose(w, g.float() + g2.float())
 
 
 def test_fused_lars_vs_reference(cuda):

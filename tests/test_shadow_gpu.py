@@ -24,34 +24,42 @@ def _make(cuda, shadow, compressor):
     return net, opt, n
 
 
-def _run(net, opt, cuda, steps=3):
+def _grads(net, opt, cuda):
     g = torch.Generator(device=cuda).manual_seed(1)
-    losses = []
-    for _ in range(steps):
-        x = torch.randn(16, 3, 64, 64, device=cuda, generator=g).contiguous(memory_format=torch.channels_last)
-        y = torch.randint(0, 10, (16,), device=cuda, generator=g)
-        opt.zero_grad()
-        with torch.autocast("cuda", dtype=torch.bfloat16):
-            loss = torch.nn.functional.cross_entropy(net(x), y)
-        loss.backward()
-        opt.step()
-        losses.append(float(loss))
-    return losses
+    x = torch.randn(16, 3, 64, 64, device=cuda, generator=g).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (16,), device=cuda, generator=g)
+    opt.zero_grad()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        loss = torch.nn.functional.cross_entropy(net(x), y)
+    loss.backward()
+    opt.synchronize()
+    grads = opt.arena.grads.clone()
+    opt.step()
+    return float(loss), grads
+
+
+def _rel(a, b):
+    return float((a - b).norm() / (b.norm() + 1e-30))
 
 
 @pytest.mark.parametrize("compressor", ["none", "gaussian"])
 def test_shadow_matches_autocast(cuda, compressor):
-    net_a, opt_a, _ = _make(cuda, False, compressor)
-    net_b, opt_b, n = _make(cuda, True, compressor)
-    assert n == sum(1 for _ in net_b.parameters())
-    la = _run(net_a, opt_a, cuda)
-    lb = _run(net_b, opt_b, cuda)
-    assert la == pytest.approx(lb, rel=1e-2, abs=1e-2)
-    wa, wb = opt_a.arena.weights, opt_b.arena.weights
-    rel = float((wa - wb).norm() / wa.norm())
-    assert rel < 1e-3, rel
+    """MIOpen's split-K weight-gradient kernels accumulate with atomics, so two
+    identical plain-autocast runs already differ slightly; the shadow path must
+    stay within a small multiple of that run-to-run noise."""
+    runs = []
+    for shadow in (False, False, True):
+        net, opt, n = _make(cuda, shadow, compressor)
+        loss, grads = _grads(net, opt, cuda)
+        runs.append((loss, grads, opt))
+    (la, ga, oa), (la2, ga2, _), (lb, gb, ob) = runs
+    assert n == sum(1 for _ in net.parameters())
+    assert la == pytest.approx(lb, rel=1e-3)
+    noise = _rel(ga2, ga)
+    err = _rel(gb, ga)
+    assert err <= 3 * noise + 2e-3, (err, noise)
     # the shadow tracks the master weights exactly (RNE cast in the SGD kernel)
-    assert torch.equal(opt_b.arena.shadow, wb.to(torch.bfloat16))
+    assert torch.equal(ob.arena.shadow, ob.arena.weights.to(torch.bfloat16))
 
 
 def test_shadow_refresh_on_load_state_dict(cuda):
