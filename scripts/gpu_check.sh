@@ -61,11 +61,9 @@ fi
 # (SubTensorOpWithScalar) of their output before every call.
 if [ "$MODE" = solvers ]; then
   step bench_base 600 python bench.py --steps 20 --warmup 10 --json-out $OUT/bench_base.json
-  MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_BWD_GTC_XDLOPS_NHWC=0 \
-    step bench_nobwd 600 python bench.py --steps 20 --warmup 10 --json-out $OUT/bench_nobwd.json
-  MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_WRW_GTC_XDLOPS_NHWC=0 \
-    step bench_nowrw 600 python bench.py --steps 20 --warmup 10 --json-out $OUT/bench_nowrw.json
-  MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_BWD_GTC_XDLOPS_NHWC=0 MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_WRW_GTC_XDLOPS_NHWC=0 \
-    step bench_noboth 600 python bench.py --steps 20 --warmup 10 --json-out $OUT/bench_noboth.json
+  step bench_nobwd 600 env MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_BWD_GTC_XDLOPS_NHWC=0 python bench.py --steps 20 --warmup 10 --json-out $OUT/bench_nobwd.json
+  step bench_nowrw 600 env MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_WRW_GTC_XDLOPS_NHWC=0 python bench.py --steps 20 --warmup 10 --json-out $OUT/bench_nowrw.json
+  step bench_noboth 600 env MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_BWD_GTC_XDLOPS_NHWC=0 \
+    MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_WRW_GTC_XDLOPS_NHWC=0 python bench.py --steps 20 --warmup 10 --json-out $OUT/bench_noboth.json
 fi
 echo done
