@@ -35,13 +35,28 @@ import torch  # noqa: E402
 
 METRIC = "images/sec (whole node) ResNet-50 k=0.1% at 1/2/4/8 MI355X; effective grad compression ratio"
 
+# Secondary BASELINE configs (--model): dataset, default per-GPU batch,
+# throughput unit, tokens per sample (sequence models), data description.
+MODELS = {
+    "resnet50": ("imagenet", 512, "images/s", 1, "synthetic (ImageNet-shaped 3x224x224, on-device)"),
+    "resnet18": ("imagenet", 512, "images/s", 1, "synthetic (ImageNet-shaped 3x224x224, on-device)"),
+    "resnet101": ("imagenet", 256, "images/s", 1, "synthetic (ImageNet-shaped 3x224x224, on-device)"),
+    "vgg16i": ("imagenet", 128, "images/s", 1, "synthetic (ImageNet-shaped 3x224x224, on-device)"),
+    "vgg16": ("cifar10", 512, "images/s", 1, "synthetic (CIFAR-shaped 3x32x32, on-device)"),
+    "resnet20": ("cifar10", 512, "images/s", 1, "synthetic (CIFAR-shaped 3x32x32, on-device)"),
+    "lstm": ("ptb", 128, "tokens/s", 35, "synthetic (PTB-shaped: vocab 10k, 35-step BPTT, on-device)"),
+    "bert": ("wikipedia", 32, "tokens/s", 512, "synthetic (BERT MLM, vocab 30522, seq 512, on-device)"),
+    "fcn5net": ("mnist", 1024, "images/s", 1, "synthetic (MNIST-shaped 1x28x28, on-device)"),
+}
+
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch-size", type=int, default=int(os.environ.get("GKSGD_BENCH_BS", "512")))
+    ap.add_argument("--batch-size", type=int, default=None,
+                    help="per-GPU batch (default: per model; ResNet-50 512, env GKSGD_BENCH_BS)")
     ap.add_argument("--cudnn-benchmark", action="store_true", help="MIOpen find (exhaustive conv algorithm search)")
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--compressor", default="gaussian")
@@ -86,9 +101,12 @@ def main() -> int:
         raise RuntimeError("native extension missing: run `python -m gaussiank_sgd_amd.ops.build`")
     torch.backends.cudnn.benchmark = args.cudnn_benchmark or os.environ.get("GKSGD_CUDNN_BENCHMARK", "0") == "1"
 
-    dataset = "imagenet" if args.model in ("resnet50", "resnet18", "resnet34", "resnet101", "resnet152",
-                                           "vgg16i") else None
-    trainer = DLTrainer(rank, P, dnn=args.model, dataset=dataset or "imagenet", batch_size=args.batch_size,
+    if args.model not in MODELS:
+        raise SystemExit("bench.py --model must be one of %s" % sorted(MODELS))
+    dataset, default_bs, unit, tok_per_sample, data_desc = MODELS[args.model]
+    if args.batch_size is None:
+        args.batch_size = int(os.environ.get("GKSGD_BENCH_BS", default_bs)) if args.model == "resnet50" else default_bs
+    trainer = DLTrainer(rank, P, dnn=args.model, dataset=dataset, batch_size=args.batch_size,
                         lr=0.1, nworkers=P, device="cuda", amp=None if args.amp == "none" else "bf16",
                         channels_last=not args.no_channels_last, seed=0)
     comp_name = "none" if args.dense else args.compressor
@@ -105,9 +123,18 @@ def main() -> int:
     trainer.display = 10 ** 9  # no host-syncing log lines inside the timed loop
     nparams = sum(p.numel() for p in trainer.net.parameters() if p.requires_grad)
 
+    state = {"hidden": None}
+    clip = 0.25 if args.model == "lstm" else None  # reference dist_trainer.py:80-85
+
     def step():
         opt.zero_grad()
-        trainer.train(1)
+        if args.model == "lstm":
+            _, state["hidden"] = trainer.train(1, hidden=state["hidden"])
+        else:
+            trainer.train(1)
+        if clip is not None:
+            opt.synchronize()
+            opt.clip_grad_norm_(clip)
         trainer.update_model()
 
     for _ in range(args.warmup):
@@ -134,11 +161,13 @@ def main() -> int:
     else:
         ratio = 1.0
     ms = elapsed / args.steps * 1e3
-    imgs = P * args.batch_size * args.steps / elapsed
+    imgs = P * args.batch_size * tok_per_sample * args.steps / elapsed
+    metric = METRIC if args.model == "resnet50" else "%s (whole node) %s k=%g%% on MI355X" % (
+        unit, args.model, 100.0 * (args.density if is_sparse else 1.0))
     out = {
-        "metric": METRIC,
+        "metric": metric,
         "value": round(imgs, 2),
-        "unit": "images/s",
+        "unit": unit,
         "n_gpus": P,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -147,13 +176,13 @@ def main() -> int:
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "bf16" if args.amp == "bf16" else "fp32",
-        "data": "synthetic (ImageNet-shaped 3x224x224, on-device), random-init weights",
+        "data": data_desc + ", random-init weights",
         "config": {
             "model": args.model,
             "global_batch": P * args.batch_size,
             "per_gpu_batch": args.batch_size,
-            "seq_len": None,
-            "image_size": 224,
+            "seq_len": tok_per_sample if tok_per_sample > 1 else None,
+            "image_size": {"imagenet": 224, "cifar10": 32, "mnist": 28}.get(dataset),
             "parallelism": "dp%d" % P,
             "compressor": comp_name,
             "density": args.density if is_sparse else 1.0,

@@ -66,4 +66,11 @@ if [ "$MODE" = solvers ]; then
   step bench_noboth 600 env MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_BWD_GTC_XDLOPS_NHWC=0 \
     MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_WRW_GTC_XDLOPS_NHWC=0 python bench.py --steps 20 --warmup 10 --json-out $OUT/bench_noboth.json
 fi
+# secondary BASELINE configs (1 GPU) + dense comparator
+if [ "$MODE" = models ]; then
+  for m in ${MODELS:-vgg16 lstm bert fcn5net}; do
+    step bench_$m 600 python bench.py --model $m --steps 20 --warmup 5 --json-out $OUT/bench_$m.json
+  done
+  step bench_dense 600 python bench.py --steps 20 --warmup 10 --dense --json-out $OUT/bench_dense.json
+fi
 echo done
