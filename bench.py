@@ -200,6 +200,8 @@ def main() -> int:
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
+    if opt._exchanger is not None:
+        opt._exchanger.close()
     comm.shutdown()
     return 0
 

@@ -371,3 +371,12 @@ class Exchanger:
             self.native.broadcast_(t, root)
         else:
             broadcast_(t, root)
+
+    def close(self) -> None:
+        """Release the native communicator (after the device is idle)."""
+        if self.native is not None:
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+            self.native.destroy()
+            self.native = None
+            self.kind = "torch"
