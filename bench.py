@@ -66,6 +66,9 @@ def parse():
     ap.add_argument("--no-channels-last", action="store_true")
     ap.add_argument("--dense", action="store_true", help="dense RCCL all-reduce comparator (compressor none)")
     ap.add_argument("--no-native-rccl", action="store_true")
+    ap.add_argument("--no-momentum-correction", action="store_true",
+                    help="plain momentum SGD on the aggregate instead of DGC momentum correction "
+                         "(BASELINE config: GaussianK k=0.1%% + momentum correction)")
     ap.add_argument("--no-shadow", action="store_true",
                     help="disable bf16 shadow weights / direct arena gradients (plain autocast)")
     ap.add_argument("--json-out", default=None)
@@ -114,7 +117,8 @@ def main() -> int:
     opt = DistributedOptimizer(trainer.optimizer, named_parameters=trainer.net.named_parameters(),
                                compression=compressors[comp_name], is_sparse=is_sparse, density=args.density,
                                threshold=args.threshold, compress_single_rank=True, density_warmup=False,
-                               native_rccl=not args.no_native_rccl)
+                               native_rccl=not args.no_native_rccl,
+                               momentum_correction=is_sparse and not args.no_momentum_correction)
     comm.broadcast_parameters(trainer.net.state_dict(), root_rank=0)
     if args.amp == "bf16" and not args.no_shadow:
         from gaussiank_sgd_amd.parallel import install_bf16_shadow
@@ -188,6 +192,7 @@ def main() -> int:
             "density": args.density if is_sparse else 1.0,
             "buckets": len(opt.arena.buckets),
             "exchange": opt._exchanger.kind if opt._exchanger is not None else "none",
+            "momentum_correction": bool(opt._mc),
         },
         "effective_compression_ratio": round(ratio, 1),
         "selected_per_step": round(sel, 1),

@@ -440,6 +440,36 @@ def _decode_chunks(chunks: torch.Tensor):
     return out
 
 
+def momentum_correct_(u: torch.Tensor, g: torch.Tensor, w: torch.Tensor, chunks: torch.Tensor, begin: int,
+                      count: int, groups: Sequence[dict], chunk_list=None) -> None:
+    """DGC momentum correction over chunks [begin, begin+count): u = mu*u + g + wd*w; g = u.
+
+    ``groups``: dicts with ``momentum`` and ``weight_decay`` per param group.
+    ``chunk_list``: decoded chunks (CPU path; avoids a device->host copy).
+    """
+    if u.is_cuda:
+        require_native(u)
+        _ops().momentum_correct(u, g, w, chunks, int(begin), int(count), [float(p["momentum"]) for p in groups],
+                                [float(p.get("weight_decay", 0.0)) for p in groups])
+        return
+    cl = chunk_list if chunk_list is not None else _decode_chunks(chunks)
+    for start, ln, gi, _ in cl[begin:begin + count]:
+        p = groups[gi]
+        us, gs, ws = u[start:start + ln], g[start:start + ln], w[start:start + ln]
+        us.mul_(float(p["momentum"])).add_(gs).add_(ws, alpha=float(p.get("weight_decay", 0.0)))
+        gs.copy_(us)
+
+
+def mask_records_(u: torch.Tensor, record: torch.Tensor, k_cap: int) -> None:
+    """Momentum factor masking: u[idx] = 0 for the indices one rank sent."""
+    if u.is_cuda:
+        require_native(u)
+        _ops().mask_records(u, record, int(k_cap))
+        return
+    cnt = int(record[0])
+    u[record[REC_HDR:REC_HDR + cnt].long()] = 0.0
+
+
 def accum_grad_(dst: torch.Tensor, src: torch.Tensor) -> None:
     """dst (fp32 arena view) += src (bf16/fp32 gradient with the same strides)."""
     if dst.is_cuda and src.dtype in (torch.bfloat16, torch.float32) and dst.stride() == src.stride():

@@ -435,6 +435,44 @@ void bn_relu_pool_backward(at::Tensor dy, at::Tensor amax, at::Tensor x, at::Ten
 }
 
 // ---------------------------------------------------------------------------
+// DGC momentum correction + momentum factor masking
+// ---------------------------------------------------------------------------
+void momentum_correct(at::Tensor u, at::Tensor g, at::Tensor w, at::Tensor chunks, int64_t begin, int64_t count,
+                      std::vector<double> momentum, std::vector<double> weight_decay) {
+  check_f32(u, "u");
+  check_f32(g, "g");
+  check_f32(w, "w");
+  check_chunks(chunks);
+  TORCH_CHECK(u.numel() == g.numel() && w.numel() == g.numel(), "arena size mismatch");
+  for (const at::Tensor* t : {&u, &g, &w})
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0, "arenas must be 16-byte aligned");
+  TORCH_CHECK(begin >= 0 && count >= 0 && (begin + count) * 2 <= chunks.numel(), "chunk range out of bounds");
+  const size_t ng = momentum.size();
+  TORCH_CHECK(ng >= 1 && ng <= (size_t)gk::kMaxGroups && weight_decay.size() == ng, "1..8 param groups");
+  gk::McArgs a;
+  a.u = u.data_ptr<float>();
+  a.g = g.data_ptr<float>();
+  a.w = w.data_ptr<float>();
+  a.chunks = reinterpret_cast<const gk::Chunk*>(chunks.data_ptr<int64_t>()) + begin;
+  a.nchunks = (int)count;
+  for (size_t i = 0; i < ng; ++i) {
+    a.momentum[i] = (float)momentum[i];
+    a.weight_decay[i] = (float)weight_decay[i];
+  }
+  c10::DeviceGuard guard(u.device());
+  gk::momentum_correct(a, cur_stream(u));
+}
+
+void mask_records(at::Tensor u, at::Tensor record, int64_t k_cap) {
+  check_f32(u, "u");
+  TORCH_CHECK(record.scalar_type() == at::kInt && record.is_contiguous() && record.is_cuda() &&
+                  record.numel() >= gk::kRecHdr + 2 * k_cap,
+              "record: int32[4 + 2*k_cap]");
+  c10::DeviceGuard guard(u.device());
+  gk::mask_records(u.data_ptr<float>(), record.data_ptr<int32_t>(), k_cap, cur_stream(u));
+}
+
+// ---------------------------------------------------------------------------
 // direct-to-arena gradient accumulation / bf16 shadow weights
 // ---------------------------------------------------------------------------
 void accum_grad(at::Tensor dst, at::Tensor src) {
@@ -565,6 +603,10 @@ TORCH_LIBRARY(gksgd, m) {
       "Tensor invstd, Tensor(c!) dgamma, Tensor(d!) dbeta, Tensor(e!) ws, bool relu, Tensor(f!)? gw_acc=None, "
       "Tensor(g!)? gb_acc=None, Tensor? dy2=None) -> ()");
   m.def("accum_grad(Tensor(a!) dst, Tensor src) -> ()");
+  m.def(
+      "momentum_correct(Tensor(a!) u, Tensor(b!) g, Tensor w, Tensor chunks, int begin, int count, "
+      "float[] momentum, float[] weight_decay) -> ()");
+  m.def("mask_records(Tensor(a!) u, Tensor record, int k_cap) -> ()");
   m.def("cast_bf16(Tensor(a!) dst, Tensor src) -> ()");
 
   m.class_<RcclEngine>("RcclEngine")
@@ -597,5 +639,7 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("bn_relu_pool_forward", &bn_relu_pool_forward);
   m.impl("bn_relu_pool_backward", &bn_relu_pool_backward);
   m.impl("accum_grad", &accum_grad);
+  m.impl("momentum_correct", &momentum_correct);
+  m.impl("mask_records", &mask_records);
   m.impl("cast_bf16", &cast_bf16);
 }

@@ -25,6 +25,7 @@ enum Mode : int {
 };
 
 constexpr int kMaxCand = 16;
+constexpr int kRecHdr = 4;   // packed record header words: sent, total, chosen, thr
 constexpr int kMaxCountBlocks = 1024;
 constexpr int kMaxStatsBlocks = 2048;
 constexpr int kRadixBins0 = 2048;  // key bits [31:21]
@@ -128,6 +129,20 @@ struct SgdArgs {
   uint16_t* w_bf16 = nullptr;         // optional bf16 shadow of w written in the same pass
 };
 void fused_sgd(const SgdArgs& a, hipStream_t stream);
+
+// DGC momentum correction over a chunk range: u = mu*u + g + wd*w; g = u.
+struct McArgs {
+  float* u = nullptr;
+  float* g = nullptr;
+  const float* w = nullptr;
+  const Chunk* chunks = nullptr;
+  int nchunks = 0;
+  float momentum[kMaxGroups];
+  float weight_decay[kMaxGroups];
+};
+void momentum_correct(const McArgs& a, hipStream_t stream);
+// momentum factor masking: u[idx] = 0 for the indices of one packed record
+void mask_records(float* u, const int32_t* record, int64_t k_cap, hipStream_t stream);
 
 // dst[i] += float(src[i]) for a bf16 (src_bytes 2) or fp32 (4) gradient: the
 // fused "cast + AccumulateGrad" of a parameter gradient into its fp32 arena slot.

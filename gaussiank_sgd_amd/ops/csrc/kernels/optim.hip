@@ -79,6 +79,43 @@ __global__ __launch_bounds__(kBlock) void fused_sgd_kernel(SgdArgs a) {
   }
 }
 
+// DGC momentum correction: u = mu*u + (g + wd*w); g = u (the compressor then
+// sparsifies the locally accumulated velocity instead of the raw gradient).
+__global__ __launch_bounds__(kBlock) void momentum_correct_kernel(McArgs a) {
+  const Chunk c = a.chunks[blockIdx.x];
+  const float mu = a.momentum[c.group];
+  const float wd = a.weight_decay[c.group];
+  float* u = a.u + c.start;
+  float* g = a.g + c.start;
+  const float* w = a.w + c.start;
+  const int n4 = c.len >> 2;
+  for (int i = threadIdx.x; i < n4; i += kBlock) {
+    float4 uv = reinterpret_cast<float4*>(u)[i];
+    const float4 gv = reinterpret_cast<const float4*>(g)[i];
+    const float4 wv = reinterpret_cast<const float4*>(w)[i];
+    uv.x = fmaf(mu, uv.x, fmaf(wd, wv.x, gv.x));
+    uv.y = fmaf(mu, uv.y, fmaf(wd, wv.y, gv.y));
+    uv.z = fmaf(mu, uv.z, fmaf(wd, wv.z, gv.z));
+    uv.w = fmaf(mu, uv.w, fmaf(wd, wv.w, gv.w));
+    reinterpret_cast<float4*>(u)[i] = uv;
+    reinterpret_cast<float4*>(g)[i] = uv;
+  }
+  for (int i = (n4 << 2) + threadIdx.x; i < c.len; i += kBlock) {
+    const float uv = fmaf(mu, u[i], fmaf(wd, w[i], g[i]));
+    u[i] = uv;
+    g[i] = uv;
+  }
+}
+
+// Momentum factor masking: u[idx] = 0 for every index this rank sent.
+__global__ __launch_bounds__(kBlock) void mask_records_kernel(float* __restrict__ u, const int32_t* __restrict__ rec,
+                                                              int64_t k_cap) {
+  const int64_t sent = rec[0];
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < sent && i < k_cap;
+       i += (int64_t)gridDim.x * kBlock)
+    u[rec[kRecHdr + i]] = 0.f;
+}
+
 __global__ __launch_bounds__(kBlock) void accum_grad_bf16_kernel(float* __restrict__ dst,
                                                                  const uint16_t* __restrict__ src, int64_t n,
                                                                  int vec) {
@@ -228,6 +265,18 @@ __global__ __launch_bounds__(kBlock) void scale_kernel(float* __restrict__ x, in
 void fused_sgd(const SgdArgs& a, hipStream_t s) {
   if (a.nchunks <= 0) return;
   hipLaunchKernelGGL(fused_sgd_kernel, dim3(a.nchunks), dim3(kBlock), 0, s, a);
+}
+
+void momentum_correct(const McArgs& a, hipStream_t s) {
+  if (a.nchunks <= 0) return;
+  hipLaunchKernelGGL(momentum_correct_kernel, dim3(a.nchunks), dim3(kBlock), 0, s, a);
+}
+
+void mask_records(float* u, const int32_t* record, int64_t k_cap, hipStream_t s) {
+  int64_t G = ceil_div(k_cap, (int64_t)kBlock);
+  if (G < 1) G = 1;
+  if (G > 1024) G = 1024;
+  hipLaunchKernelGGL(mask_records_kernel, dim3((int)G), dim3(kBlock), 0, s, u, record, k_cap);
 }
 
 void accum_grad(float* dst, const void* src, int64_t n, int src_bytes, hipStream_t s) {

@@ -97,6 +97,10 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         self._overlap = bool(opts.get("overlap", _env_flag("GKSGD_OVERLAP", True)))
         self._prefer_native_rccl = bool(opts.get("native_rccl", True))
         self._planner_preset = opts.get("planner_preset", "mi355x")
+        # DGC momentum correction (Lin et al. 2018): momentum is accumulated
+        # locally BEFORE sparsification and the global update is plain SGD.
+        self._mc = bool(opts.get("momentum_correction", _env_flag("GKSGD_MOMENTUM_CORRECTION", False)))
+        self._mc_applied = False
         self._base_cls = opts.get("base_cls", None)
         self._state_dirty = False
 
@@ -132,6 +136,11 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         self._sel_n = 0
         self._setup_exchange()
         self._setup_fused_update()
+        if self._mc:
+            if not (self._fused_sparse and self._fused_kind == "sgd"):
+                raise ValueError("momentum_correction needs a fused sparse compressor and torch.optim.SGD "
+                                 "(fused update path)")
+            self._arena.velocity = torch.zeros(self._arena.total, dtype=torch.float32, device=self._arena.device)
         if self._hooks_on:
             self._register_hooks()
 
@@ -365,10 +374,18 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         k_cap = min(comp.k_cap_for(k, b.numel), b.bufs.k_cap)
         r = b.slice(self._arena.residuals)
         seed = comp.next_seed(self._rank)
+        arena = self._arena
+        if self._mc:
+            begin, count = self._bucket_chunks[b.index]
+            ops.momentum_correct_(arena.velocity, arena.grads, arena.weights, self._chunks, begin, count,
+                                  self.param_groups, self._chunk_list)
+            self._mc_applied = True
         ops.compress_(g, r, b.bufs, comp.mode, ec=comp.ec, zero_g=True, loops=comp.loops, z=comp.z_for(density),
                       k=k, k_cap=k_cap, seed=seed, sample_p=getattr(comp, "sample_p", 0.01), n_stats=b.numel)
         rec_words = ops.REC_HDR + 2 * k_cap
         rec = b.bufs.record[:rec_words]
+        if self._mc:
+            ops.mask_records_(b.slice(arena.velocity), rec, k_cap)  # momentum factor masking
         t1 = self._timer()
         if self._world > 1:
             gathered = b.gathered[: self._world * rec_words]
@@ -544,7 +561,25 @@ class _DistributedOptimizer(torch.optim.Optimizer):
             for p in g["params"]:
                 if p in self._parameter_names:
                     group_of_key[self._parameter_names[p]] = gi
-        self._chunks = ops.make_chunk_table(self._arena.segments(group_of_key), self._device)
+        segs = self._arena.segments(group_of_key)
+        self._chunks = ops.make_chunk_table(segs, self._device)
+        # per-bucket [begin, count) ranges of the chunk table (segments are in bucket order)
+        self._bucket_chunks = []
+        self._chunk_list = []
+        pos = 0
+        seg_at = {sg[0]: sg for sg in segs}
+        for b in self._arena.buckets:
+            begin = pos
+            for o in b.offsets:
+                start = b.start + o
+                seg = seg_at[start]
+                off = 0
+                while off < seg[1]:
+                    ln = min(ops.CHUNK_ELEMS, seg[1] - off)
+                    self._chunk_list.append((start + off, ln, seg[2], seg[3]))
+                    off += ln
+                    pos += 1
+            self._bucket_chunks.append((begin, pos - begin))
         self._nseg = sum(len(b.keys) for b in self._arena.buckets)
         self._group_first = [True] * len(self.param_groups)
         if self._fused_kind == "lars":
@@ -591,11 +626,17 @@ class _DistributedOptimizer(torch.optim.Optimizer):
 
     def _fused_step(self):
         arena = self._arena
-        if self._state_dirty or (self._fused_kind == "sgd" and arena.momentum is None) or \
-                (self._fused_kind == "lars" and arena.momentum is None):
+        if not self._mc_applied and (self._state_dirty or arena.momentum is None):
             self._adopt_state()
         arena.reattach()
-        if self._fused_kind == "sgd":
+        if self._fused_kind == "sgd" and self._mc_applied:
+            # momentum + weight decay were applied locally before sparsification
+            groups = [{"lr": g["lr"], "momentum": 0.0, "dampening": 0.0, "weight_decay": 0.0, "nesterov": False,
+                       "first_step": False} for g in self.param_groups]
+            ops.fused_sgd_(arena.weights, None, arena.grads, self._chunks, groups, zero_grad=self._zero_grad_in_step,
+                           w_bf16=getattr(arena, "shadow", None))
+            self._mc_applied = False
+        elif self._fused_kind == "sgd":
             groups = []
             for gi, g in enumerate(self.param_groups):
                 groups.append({"lr": g["lr"], "momentum": g["momentum"], "dampening": g.get("dampening", 0.0),
@@ -656,19 +697,25 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         if self._arena.residuals is not None:
             st["residuals"] = {b.name: self._unpad(b, b.slice(self._arena.residuals)).detach().cpu()
                                for b in self._arena.buckets}
+        if getattr(self._arena, "velocity", None) is not None:
+            st["velocity"] = {b.name: self._unpad(b, b.slice(self._arena.velocity)).detach().cpu()
+                              for b in self._arena.buckets}
         return st
 
     def load_compression_state(self, st: dict) -> None:
         self.train_epoch = int(st.get("train_epoch", self.train_epoch))
         self.train_iter = int(st.get("train_iter", self.train_iter))
-        res = st.get("residuals")
-        if res and self._arena.residuals is not None:
+        for key, arena_t in (("residuals", self._arena.residuals),
+                             ("velocity", getattr(self._arena, "velocity", None))):
+            res = st.get(key)
+            if not res or arena_t is None:
+                continue
             with torch.no_grad():
                 for b in self._arena.buckets:
                     if b.name not in res:
                         continue
                     flat = res[b.name].to(self._device)
-                    dst = b.slice(self._arena.residuals)
+                    dst = b.slice(arena_t)
                     pos = 0
                     for k, o in zip(b.keys, b.offsets):
                         n = self._named_parameters[k].numel()

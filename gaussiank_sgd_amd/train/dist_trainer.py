@@ -36,7 +36,7 @@ from .trainer import DLTrainer, _support_datasets, _support_dnns
 def ssgd(dnn, dataset, data_dir, nworkers, lr, batch_size, nsteps_update, max_epochs, nwpernode, pretrain,
          num_steps, compressor, density, threshold, gradient_path=None, amp=None, channels_last=False,
          density_warmup=True, deterministic=False, max_iters=None, compress_single_rank=False, saved_dir=".",
-         bf16_shadow=True):
+         bf16_shadow=True, momentum_correction=False, k_cap_factor=None, overlap=True, dump_grad_every=None):
     rank = hvd.rank()
     device = "cpu"
     if torch.cuda.is_available():
@@ -67,6 +67,10 @@ def ssgd(dnn, dataset, data_dir, nworkers, lr, batch_size, nsteps_update, max_ep
     else:
         seq_layernames, layerwise_times = None, None
 
+    if k_cap_factor is not None:
+        compressors[compressor].kcap_factor = float(k_cap_factor)
+    if dump_grad_every is not None:
+        settings.DUMP_GRAD_EVERY = int(dump_grad_every)
     norm_clip = None
     if dnn == "lstm":
         norm_clip = 0.25
@@ -78,7 +82,8 @@ def ssgd(dnn, dataset, data_dir, nworkers, lr, batch_size, nsteps_update, max_ep
                                          seq_layernames=seq_layernames, layerwise_times=layerwise_times,
                                          norm_clip=None, threshold=threshold, writer=None,
                                          gradient_path=gradient_path, density_warmup=density_warmup,
-                                         deterministic=deterministic, compress_single_rank=compress_single_rank)
+                                         deterministic=deterministic, compress_single_rank=compress_single_rank,
+                                         momentum_correction=momentum_correction, overlap=overlap)
     if getattr(trainer, "_pending_compression", None):
         optimizer.load_compression_state(trainer._pending_compression)
     hvd.broadcast_parameters(trainer.net.state_dict(), root_rank=0)
@@ -148,6 +153,17 @@ def build_parser():
     p.add_argument("--deterministic", action="store_true")
     p.add_argument("--compress-single-rank", action="store_true")
     p.add_argument("--max-iters", type=int, default=None)
+    p.add_argument("--momentum-correction", action="store_true",
+                   help="DGC momentum correction + momentum factor masking (local momentum before sparsification)")
+    p.add_argument("--k-cap-factor", type=float, default=None,
+                   help="record capacity k_cap = factor * k (Gaussian-k may select more than k)")
+    p.add_argument("--bucket-mb", type=float, default=None,
+                   help="bucket size in MB of fp32 gradients (overrides --threshold)")
+    p.add_argument("--no-overlap", action="store_true", help="exchange buckets at synchronize(), not in backward")
+    p.add_argument("--dump-grad-every", type=int, default=None,
+                   help="with settings.LOGGING_GRADIENTS: dump every N iterations (async D2H)")
+    p.add_argument("--synthetic", action="store_true", default=True,
+                   help="synthetic on-device data (always on: no datasets offline)")
     p.add_argument("--no-bf16-shadow", action="store_true",
                    help="with --amp bf16: keep plain autocast casts instead of the bf16 shadow weight arena")
     p.add_argument("--logdir-root", type=str, default="./logs")
@@ -170,6 +186,9 @@ def main(argv=None):
     if settings.LOGGING_GRADIENTS:
         gradient_path = "%s/gradients/%s" % (args.saved_dir, logdir)
         utils.create_path(gradient_path)
+    threshold = args.threshold
+    if args.bucket_mb is not None:
+        threshold = int(args.bucket_mb * 1024 * 1024 / 4)
     rank = hvd.rank()
     logfile = os.path.join(relative_path, settings.hostname + "-" + str(rank) + ".log")
     hdlr = logging.FileHandler(logfile)
@@ -178,10 +197,11 @@ def main(argv=None):
     logger.info("Configurations: %s", args)
     return ssgd(args.dnn, args.dataset, args.data_dir, nworkers, args.lr, args.batch_size, args.nsteps_update,
                 args.max_epochs, args.nwpernode, args.pretrain, args.num_steps, args.compressor, args.density,
-                args.threshold, gradient_path, amp=args.amp, channels_last=args.channels_last,
+                threshold, gradient_path, amp=args.amp, channels_last=args.channels_last,
                 density_warmup=not args.no_density_warmup, deterministic=args.deterministic,
                 max_iters=args.max_iters, compress_single_rank=args.compress_single_rank, saved_dir=args.saved_dir,
-                bf16_shadow=not args.no_bf16_shadow)
+                bf16_shadow=not args.no_bf16_shadow, momentum_correction=args.momentum_correction,
+                k_cap_factor=args.k_cap_factor, overlap=not args.no_overlap, dump_grad_every=args.dump_grad_every)
 
 
 if __name__ == "__main__":

@@ -220,3 +220,49 @@ def test_shadow_matches_autocast_cpu():
     assert torch.equal(ga, gb)
     assert torch.equal(oa.arena.weights, ob.arena.weights)
     assert torch.equal(ob.arena.shadow, ob.arena.weights.to(torch.bfloat16))
+
+
+def test_momentum_correction_matches_dgc_formula():
+    """DGC momentum correction (u = mu*u + g + wd*w; sparsify u + residual;
+    mask u at the sent indices; plain SGD on the aggregate) vs a hand-written
+    single-rank oracle (CPU fallbacks of the same ops)."""
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(32, 64), torch.nn.ReLU(), torch.nn.Linear(64, 8))
+    ref = [p.detach().clone() for p in net.parameters()]
+    mu, wd, lr, density = 0.9, 1e-4, 0.1, 0.05
+    base = torch.optim.SGD(net.parameters(), lr=lr, momentum=mu, weight_decay=wd)
+    opt = hvd.DistributedOptimizer(base, named_parameters=net.named_parameters(), compression=compressors["topk"],
+                                   is_sparse=True, density=density, compress_single_rank=True, density_warmup=False,
+                                   momentum_correction=True, threshold=10 ** 9)
+    arena = opt.arena
+    b = arena.buckets[0]
+    n_flat = b.span
+    u = torch.zeros(n_flat)
+    v = torch.zeros(n_flat)
+    w = torch.zeros(n_flat)
+    for k, o in zip(b.keys, b.offsets):
+        w[o:o + arena.named[k].numel()] = arena.named[k].detach().view(-1)
+    g = torch.Generator().manual_seed(3)
+    for step in range(4):
+        x = torch.randn(16, 32, generator=g)
+        raw = torch.autograd.grad(net(x).pow(2).mean(), [arena.named[k] for k in b.keys])
+        grad = torch.zeros(n_flat)
+        for gr, o in zip(raw, b.offsets):
+            grad[o:o + gr.numel()] = gr.reshape(-1)
+        opt.zero_grad()
+        net(x).pow(2).mean().backward()
+        opt.step()
+        # oracle
+        u = mu * u + grad + wd * w
+        acc = v + u
+        k = max(int(b.numel * density), 1)
+        idx = torch.topk(acc.abs(), k).indices
+        upd = torch.zeros_like(acc)
+        upd[idx] = acc[idx]
+        v = acc.clone()
+        v[idx] = 0
+        u[idx] = 0
+        w = w - lr * upd
+        got = b.slice(arena.weights)
+        assert torch.allclose(got, w, atol=1e-6), step
+        assert torch.allclose(b.slice(arena.velocity), u, atol=1e-6)

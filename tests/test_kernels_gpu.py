@@ -329,3 +329,36 @@ def test_rccl_engine_world1(cuda):
     torch.cuda.synchronize()
     assert torch.equal(out, t)
     e.destroy()
+
+
+def test_momentum_correct_and_mask(cuda):
+    """DGC momentum correction over a chunk range + momentum factor masking."""
+    torch.manual_seed(0)
+    pad = lambda n: (n + 63) // 64 * 64
+    sizes = [40000, 100, 7]
+    offs, o = [], 0
+    for n in sizes:
+        offs.append(o)
+        o += pad(n)
+    chunks = ops.make_chunk_table([(offs[i], pad(sizes[i]), i % 2, i) for i in range(3)], cuda)
+    nchunks = chunks.numel() // 2
+    groups = [dict(momentum=0.9, weight_decay=1e-4), dict(momentum=0.5, weight_decay=0.0)]
+    u = torch.randn(o, device=cuda)
+    g = torch.randn(o, device=cuda)
+    w = torch.randn(o, device=cuda)
+    uc, gc, wc = u.cpu(), g.cpu(), w.cpu()
+    cl = ops._decode_chunks(chunks)
+    begin, count = 1, nchunks - 1          # skip the first chunk: it must stay untouched
+    ops.momentum_correct_(u, g, w, chunks, begin, count, groups)
+    ops.momentum_correct_(uc, gc, wc, chunks, begin, count, groups, cl)
+    torch.cuda.synchronize()
+    assert torch.allclose(u.cpu(), uc, atol=1e-6, rtol=1e-6)
+    assert torch.allclose(g.cpu(), gc, atol=1e-6, rtol=1e-6)
+    k_cap = 64
+    rec = torch.zeros(ops.REC_HDR + 2 * k_cap, dtype=torch.int32)
+    idx = torch.randperm(o)[:50].sort().values.int()
+    rec[0] = 50
+    rec[ops.REC_HDR:ops.REC_HDR + 50] = idx
+    ops.mask_records_(u, rec.to(cuda), k_cap)
+    uc[idx.long()] = 0
+    assert torch.equal(u.cpu(), uc)
