@@ -1,0 +1,109 @@
+"""Property tests (hypothesis) of the compression record contract.
+
+The CPU mirror implements exactly the semantics the gfx950 kernels are
+parity-tested against (tests/test_kernels_gpu.py), so these properties pin
+the contract for both:
+  * conservation: acc == scatter(record) + residual_new, bit-exact;
+  * sent <= k_cap, indices unique and ascending, values == acc[idx];
+  * decompress == (1/P) * index_add over ranks for unequal counts / duplicates;
+  * Gaussian-k on Gaussian input lands in [2k/3, 4k/3].
+"""
+import math
+
+import pytest
+import torch
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
+
+from gaussiank_sgd_amd import ops
+from gaussiank_sgd_amd.compression import reference
+from gaussiank_sgd_amd.utils.stats import gaussian_z
+
+SETTINGS = settings(max_examples=25, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+
+MODES = [ops.MODE_GAUSSIAN, ops.MODE_TOPK, ops.MODE_RANDOMK, ops.MODE_REDSYNC, ops.MODE_REDSYNCTRIM,
+         ops.MODE_THRESHOLD, ops.MODE_DGC]
+
+
+def _compress(x, r, mode, k, k_cap, ec, seed):
+    b = ops.CompressBuffers(k_cap, "cpu")
+    g, rr = x.clone(), r.clone()
+    z = gaussian_z(k / x.numel()) if mode == ops.MODE_GAUSSIAN else 0.0
+    ops.compress_(g, rr, b, mode, ec=ec, zero_g=True, loops=3, z=z, k=k, k_cap=k_cap, seed=seed,
+                  fixed_thr=0.5)
+    rec = b.record
+    sent = int(rec[0])
+    idx = rec[ops.REC_HDR:ops.REC_HDR + sent].long()
+    val = rec[ops.REC_HDR + k_cap:ops.REC_HDR + k_cap + sent].view(torch.float32)
+    return g, rr, rec, idx, val
+
+
+@SETTINGS
+@given(n=st.integers(1, 5000), mode=st.sampled_from(MODES), density=st.floats(0.001, 0.3),
+       cap_factor=st.floats(0.5, 3.0), ec=st.booleans(), seed=st.integers(0, 2 ** 31 - 1),
+       heavy=st.booleans())
+def test_record_contract(n, mode, density, cap_factor, ec, seed, heavy):
+    gen = torch.Generator().manual_seed(seed)
+    x = torch.randn(n, generator=gen)
+    if heavy:
+        x = x / torch.rand(n, generator=gen).clamp_min(1e-3)  # heavy tails
+    r = torch.randn(n, generator=gen) * 0.3
+    k = max(int(n * density), 1)
+    k_cap = max(1, min(n, int(math.ceil(cap_factor * k))))
+    g, rr, rec, idx, val = _compress(x, r, mode, k, k_cap, ec, seed)
+    acc = x + r if ec else x
+    sent, total = int(rec[0]), int(rec[1])
+    # capacity and counts
+    assert 0 <= sent <= k_cap and sent == min(total, k_cap)
+    # unique ascending indices inside the buffer, values are the accumulated gradient
+    if sent:
+        assert int(idx.min()) >= 0 and int(idx.max()) < n
+        assert bool((idx[1:] > idx[:-1]).all())
+        assert torch.equal(val, acc[idx])
+    # the raw gradient buffer is consumed
+    assert float(g.abs().sum()) == 0.0
+    # conservation: what was sent + what stays in the residual == acc, bit-exact
+    rebuilt = rr.clone()
+    rebuilt[idx] += val
+    assert torch.equal(rebuilt, acc)
+    assert float(rr[idx].abs().sum()) == 0.0
+
+
+@SETTINGS
+@given(P=st.integers(1, 6), n=st.integers(1, 300), k_cap=st.integers(1, 40), seed=st.integers(0, 10 ** 6))
+def test_decompress_equals_index_add(P, n, k_cap, seed):
+    """Unequal per-rank counts and duplicate indices ACROSS ranks (SURVEY §2.3 regression)."""
+    gen = torch.Generator().manual_seed(seed)
+    recs = torch.zeros(P, ops.REC_HDR + 2 * k_cap, dtype=torch.int32)
+    per = []
+    for p in range(P):
+        cnt = int(torch.randint(0, min(k_cap, n) + 1, (1,), generator=gen))
+        idx = torch.randperm(n, generator=gen)[:cnt].sort().values
+        val = torch.randn(cnt, generator=gen)
+        recs[p, 0] = cnt
+        recs[p, ops.REC_HDR:ops.REC_HDR + cnt] = idx.int()
+        recs[p, ops.REC_HDR + k_cap:ops.REC_HDR + k_cap + cnt] = val.view(torch.int32)
+        per.append((idx, val))
+    dst = torch.zeros(n)
+    ops.scatter_add_records_(dst, recs, P, k_cap, 1.0 / P)
+    want = torch.zeros(n, dtype=torch.float64)
+    for idx, val in per:
+        want.index_add_(0, idx, val.double())
+    want /= P
+    assert torch.allclose(dst.double(), want, atol=1e-6, rtol=1e-6)
+    assert torch.allclose(dst, reference.sparse_aggregate(n, per, P), atol=1e-6)
+
+
+@SETTINGS
+@given(n=st.integers(20_000, 200_000), density=st.sampled_from([0.001, 0.004, 0.01, 0.015625, 0.05]),
+       seed=st.integers(0, 10 ** 6))
+def test_gaussian_k_lands_near_k(n, density, seed):
+    gen = torch.Generator().manual_seed(seed)
+    x = torch.randn(n, generator=gen) * 1e-3
+    r = torch.zeros(n)
+    k = max(int(n * density), 1)
+    if k < 20:  # too few expected hits for a concentration statement
+        return
+    _, _, rec, _, _ = _compress(x, r, ops.MODE_GAUSSIAN, k, 4 * k, True, seed)
+    total = int(rec[1])
+    assert 2 * k / 3 <= total <= 4 * k / 3, (total, k)
