@@ -1,8 +1,13 @@
-"""bf16 shadow weights + direct arena gradients vs plain autocast.
+"""bf16 shadow weights + direct arena gradients on the GPU.
 
-Both paths round the fp32 master weights to bf16 with round-to-nearest-even,
-run the same bf16 convolutions and add the same bf16 gradients into fp32, so
-the trajectories must agree to within MIOpen's run-to-run noise.
+MIOpen's convolutions are not bitwise repeatable run to run (split-K
+kernels accumulate with atomics; scripts/debug/determinism_probe.py shows two
+identical ResNet-50 forwards differing from the first 1x1 conv on), and a
+random-init ResNet at toy sizes amplifies that noise, so end-to-end "two
+training runs agree" is not a usable oracle here.  The CPU test
+(test_framework_cpu.py::test_shadow_matches_autocast_cpu) checks end-to-end
+bitwise equality with deterministic kernels; these GPU tests check each
+mechanism against the autograd value computed in the SAME pass.
 """
 import pytest
 import torch
@@ -10,60 +15,108 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _make(cuda, shadow, compressor):
+def _opt(net, compressor="none"):
     from gaussiank_sgd_amd.compression import compressors
-    from gaussiank_sgd_amd.models import resnet50
-    from gaussiank_sgd_amd.parallel import DistributedOptimizer, install_bf16_shadow
+    from gaussiank_sgd_amd.parallel import DistributedOptimizer
+    base = torch.optim.SGD(net.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    return DistributedOptimizer(base, named_parameters=net.named_parameters(), compression=compressors[compressor],
+                                is_sparse=compressor != "none", density=0.01, compress_single_rank=True,
+                                density_warmup=False)
+
+
+def test_conv_sink_accumulates_miopen_grad(cuda):
+    """The shadow view's backward adds exactly the bf16 weight gradient MIOpen
+    produced into the fp32 arena (and AccumulateGrad adds nothing)."""
+    from gaussiank_sgd_amd.parallel import install_bf16_shadow
     torch.manual_seed(0)
-    net = resnet50(num_classes=10).to(cuda).to(memory_format=torch.channels_last)
-    base = torch.optim.SGD(net.parameters(), lr=0.002, momentum=0.9, weight_decay=1e-4)
-    opt = DistributedOptimizer(base, named_parameters=net.named_parameters(), compression=compressors[compressor],
-                               is_sparse=compressor != "none", density=0.01, compress_single_rank=True,
-                               density_warmup=False)
-    n = install_bf16_shadow(net, opt) if shadow else 0
-    return net, opt, n
-
-
-def _grads(net, opt, cuda):
-    g = torch.Generator(device=cuda).manual_seed(1)
-    x = torch.randn(16, 3, 64, 64, device=cuda, generator=g).contiguous(memory_format=torch.channels_last)
-    y = torch.randint(0, 10, (16,), device=cuda, generator=g)
+    net = torch.nn.Sequential(torch.nn.Conv2d(16, 32, 3, padding=1, bias=True)).to(cuda).to(
+        memory_format=torch.channels_last)
+    opt = _opt(net)
+    install_bf16_shadow(net, opt)
+    conv = net[0]
+    seen = {}
+    sinks = conv._gk_shadow
+    for name, (view, sink) in list(sinks.items()):
+        def spy(grad, sink=sink, name=name):
+            seen[name] = grad.detach().clone()
+            sink(grad)
+        sinks[name] = (view, spy)
+    x = torch.randn(8, 16, 20, 20, device=cuda).contiguous(memory_format=torch.channels_last)
     opt.zero_grad()
     with torch.autocast("cuda", dtype=torch.bfloat16):
-        loss = torch.nn.functional.cross_entropy(net(x), y)
-    loss.backward()
-    opt.synchronize()
-    grads = opt.arena.grads.clone()
-    opt.step()
-    return float(loss), grads
+        y = net(x)
+    assert y.dtype == torch.bfloat16
+    y.float().square().mean().backward()
+    torch.cuda.synchronize()
+    assert set(seen) == {"weight", "bias"}
+    assert torch.equal(conv.weight.grad, seen["weight"].float())
+    assert torch.equal(conv.bias.grad, seen["bias"].float())
+    assert conv.weight.grad.data_ptr() == opt.arena.grad_views["0.weight"].data_ptr()
 
 
-def _rel(a, b):
-    return float((a - b).norm() / (b.norm() + 1e-30))
+def test_bn_direct_equals_autograd(cuda):
+    """BNAct with arena-direct gamma/beta gradients == the plain autograd path
+    (same deterministic fused kernels)."""
+    from gaussiank_sgd_amd.ops.bn import BNAct
+    torch.manual_seed(0)
+    C = 64
+    x0 = torch.randn(4, C, 14, 14, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    r0 = torch.randn_like(x0)
+    g0 = torch.randn_like(x0)
+    res = []
+    for direct in (False, True):
+        bn = BNAct(C, act="relu").to(cuda)
+        gw = torch.full((C,), 0.25, device=cuda)   # arena slots start non-zero: must ACCUMULATE
+        gb = torch.full((C,), -0.5, device=cuda)
+        if direct:
+            bn._gk_direct = (gw, gb)
+        x = x0.clone().requires_grad_(True)
+        r = r0.clone().requires_grad_(True)
+        bn(x, r).backward(g0)
+        if direct:
+            assert bn.weight.grad is None and bn.bias.grad is None
+            res.append((x.grad, r.grad, gw - 0.25, gb + 0.5))
+        else:
+            res.append((x.grad, r.grad, bn.weight.grad, bn.bias.grad))
+    for a, b in zip(*res):
+        assert torch.allclose(a.float(), b.float(), atol=1e-6, rtol=1e-6)
 
 
 @pytest.mark.parametrize("compressor", ["none", "gaussian"])
-def test_shadow_matches_autocast(cuda, compressor):
-    """MIOpen's split-K weight-gradient kernels accumulate with atomics, so two
-    identical plain-autocast runs already differ slightly; the shadow path must
-    stay within a small multiple of that run-to-run noise."""
-    runs = []
-    for shadow in (False, False, True):
-        net, opt, n = _make(cuda, shadow, compressor)
-        loss, grads = _grads(net, opt, cuda)
-        runs.append((loss, grads, opt))
-    (la, ga, oa), (la2, ga2, _), (lb, gb, ob) = runs
+def test_shadow_resnet50_training(cuda, compressor):
+    from gaussiank_sgd_amd.models import resnet50
+    from gaussiank_sgd_amd.parallel import install_bf16_shadow
+    torch.manual_seed(0)
+    net = resnet50(num_classes=10).to(cuda).to(memory_format=torch.channels_last)
+    opt = _opt(net, compressor)
+    n = install_bf16_shadow(net, opt)
     assert n == sum(1 for _ in net.parameters())
-    assert la == pytest.approx(lb, rel=1e-3)
-    noise = _rel(ga2, ga)
-    err = _rel(gb, ga)
-    assert err <= 3 * noise + 2e-3, (err, noise)
+    g = torch.Generator(device=cuda).manual_seed(1)
+    x = torch.randn(32, 3, 64, 64, device=cuda, generator=g).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (32,), device=cuda, generator=g)
+    losses = []
+    for _ in range(8):   # memorise one batch: the loss must fall
+        opt.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = torch.nn.functional.cross_entropy(net(x), y)
+        loss.backward()
+        if compressor == "none":
+            gnorm = float(opt.arena.grads.norm())
+            assert gnorm > 0 and gnorm == gnorm
+        opt.step()
+        losses.append(float(loss))
+    assert losses[-1] < losses[0], losses
     # the shadow tracks the master weights exactly (RNE cast in the SGD kernel)
-    assert torch.equal(ob.arena.shadow, ob.arena.weights.to(torch.bfloat16))
+    assert torch.equal(opt.arena.shadow, opt.arena.weights.to(torch.bfloat16))
 
 
 def test_shadow_refresh_on_load_state_dict(cuda):
-    net, opt, _ = _make(cuda, True, "none")
+    from gaussiank_sgd_amd.models import resnet50
+    from gaussiank_sgd_amd.parallel import install_bf16_shadow
+    torch.manual_seed(0)
+    net = resnet50(num_classes=10).to(cuda).to(memory_format=torch.channels_last)
+    opt = _opt(net)
+    install_bf16_shadow(net, opt)
     sd = {k: v.clone() for k, v in net.state_dict().items()}
     for v in sd.values():
         if v.is_floating_point():
