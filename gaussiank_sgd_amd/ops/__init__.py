@@ -470,9 +470,17 @@ def mask_records_(u: torch.Tensor, record: torch.Tensor, k_cap: int) -> None:
     u[record[REC_HDR:REC_HDR + cnt].long()] = 0.0
 
 
+def _same_order(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """Same shape and the same element order in memory (size-1 dims ignored)."""
+    if a.shape != b.shape:
+        return False
+    return all(n == 1 or sa == sb for n, sa, sb in zip(a.shape, a.stride(), b.stride()))
+
+
 def accum_grad_(dst: torch.Tensor, src: torch.Tensor) -> None:
-    """dst (fp32 arena view) += src (bf16/fp32 gradient with the same strides)."""
-    if dst.is_cuda and src.dtype in (torch.bfloat16, torch.float32) and dst.stride() == src.stride():
+    """dst (fp32 arena view) += src (bf16/fp32 gradient with the same element order)."""
+    if dst.is_cuda and src.dtype in (torch.bfloat16, torch.float32) and _same_order(dst, src) and \
+            src.is_non_overlapping_and_dense():
         require_native(dst)
         _ops().accum_grad(dst, src)
     else:

@@ -479,10 +479,12 @@ void accum_grad(at::Tensor dst, at::Tensor src) {
   TORCH_CHECK(dst.is_cuda() && src.is_cuda(), "GPU tensors required");
   TORCH_CHECK(dst.scalar_type() == at::kFloat, "dst must be fp32");
   TORCH_CHECK(src.scalar_type() == at::kBFloat16 || src.scalar_type() == at::kFloat, "src must be bf16 or fp32");
-  TORCH_CHECK(dst.numel() == src.numel(), "size mismatch");
-  TORCH_CHECK(dst.strides() == src.strides() && dst.is_non_overlapping_and_dense() &&
-                  src.is_non_overlapping_and_dense(),
-              "dst/src must be dense with identical strides");
+  TORCH_CHECK(dst.sizes() == src.sizes(), "shape mismatch");
+  bool same = true;  // identical element order: strides agree on every dim of size > 1
+  for (int64_t d = 0; d < dst.dim(); ++d)
+    if (dst.size(d) > 1 && dst.stride(d) != src.stride(d)) same = false;
+  TORCH_CHECK(same && dst.is_non_overlapping_and_dense() && src.is_non_overlapping_and_dense(),
+              "dst/src must be dense with the same element order");
   c10::DeviceGuard guard(dst.device());
   gk::accum_grad(dst.data_ptr<float>(), src.data_ptr(), dst.numel(), (int)src.element_size(), cur_stream(dst));
 }

@@ -243,9 +243,9 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         bi = self._arena.key_to_bucket[key]
 
         def hook(param):
+            self._grads_zero = False
             if self.local:
                 return
-            self._grads_zero = False
             self._arena.check_grad(key, param)
             b = self._arena.buckets[bi]
             b.ready += 1
@@ -675,8 +675,11 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         return loss
 
     def zero_grad(self, set_to_none: bool = True):
-        """Gradients are views of the arena: zero it (never set to None)."""
-        if self._grads_zero:
+        """Gradients are views of the arena: zero it (never set to None).
+
+        With readiness hooks installed the arena is known to be clean after a
+        fused step (which zeroes it) until a hook fires, so the fill is skipped."""
+        if self._grads_zero and self._hooks_on:
             return
         with torch.no_grad():
             ops.fill_zero_(self._arena.grads)
