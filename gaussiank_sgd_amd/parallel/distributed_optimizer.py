@@ -143,6 +143,11 @@ class _DistributedOptimizer(torch.optim.Optimizer):
             self._arena.velocity = torch.zeros(self._arena.total, dtype=torch.float32, device=self._arena.device)
         if self._hooks_on:
             self._register_hooks()
+        self._watchdog = None
+        wd_s = float(opts.get("watchdog_s", os.environ.get("GKSGD_WATCHDOG_S", "0")) or 0)
+        if wd_s > 0:
+            from ..utils.watchdog import Watchdog
+            self._watchdog = Watchdog(wd_s, self.describe_state)
 
     # ------------------------------------------------------------------
     # planning
@@ -658,7 +663,18 @@ class _DistributedOptimizer(torch.optim.Optimizer):
             self.refresh_shadow()
         self._grads_zero = self._zero_grad_in_step
 
+    def describe_state(self) -> str:
+        """Bucket readiness / launch state (for the hang watchdog)."""
+        lines = ["rank %d/%d iter %d epoch %d local=%s" % (self._rank, self._world, self.train_iter,
+                                                          self.train_epoch, self.local)]
+        for b in self._arena.buckets:
+            lines.append("  bucket %d: %d/%d params ready, launched=%s, numel=%d" % (
+                b.index, b.ready, len(b.params), b.launched, b.numel))
+        return "\n".join(lines)
+
     def step(self, closure=None):
+        if self._watchdog is not None:
+            self._watchdog.kick()
         if not self.local:
             self.synchronize()
         if self._fused_kind is not None:

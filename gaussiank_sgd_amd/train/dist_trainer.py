@@ -36,7 +36,8 @@ from .trainer import DLTrainer, _support_datasets, _support_dnns
 def ssgd(dnn, dataset, data_dir, nworkers, lr, batch_size, nsteps_update, max_epochs, nwpernode, pretrain,
          num_steps, compressor, density, threshold, gradient_path=None, amp=None, channels_last=False,
          density_warmup=True, deterministic=False, max_iters=None, compress_single_rank=False, saved_dir=".",
-         bf16_shadow=True, momentum_correction=False, k_cap_factor=None, overlap=True, dump_grad_every=None):
+         bf16_shadow=True, momentum_correction=False, k_cap_factor=None, overlap=True, dump_grad_every=None,
+         metrics_dir=None):
     rank = hvd.rank()
     device = "cpu"
     if torch.cuda.is_available():
@@ -92,6 +93,9 @@ def ssgd(dnn, dataset, data_dir, nworkers, lr, batch_size, nsteps_update, max_ep
         install_bf16_shadow(trainer.net, optimizer)
     trainer.update_optimizer(optimizer)
     iters_per_epoch = max(1, trainer.get_num_of_training_samples() // (nworkers * batch_size * nsteps_update))
+    from ..utils.watchdog import JsonlMetrics
+    metrics = JsonlMetrics(os.path.join(metrics_dir or ".", "metrics-rank%d.jsonl" % rank))
+    nparams = sum(p.numel() for p in trainer.net.parameters() if p.requires_grad)
     times = []
     logger.info("max_epochs: %d", max_epochs)
     display = 40 if iters_per_epoch > 40 else max(1, iters_per_epoch - 1)
@@ -118,8 +122,19 @@ def ssgd(dnn, dataset, data_dir, nworkers, lr, batch_size, nsteps_update, max_ep
                 if trainer.is_cuda:
                     torch.cuda.synchronize()
                 time_per_iter = float(np.mean(times))
+                speed = batch_size * nsteps_update / time_per_iter
                 logger.warning("Time per iteration including communication: %f, Speed: %f images/s", time_per_iter,
-                               batch_size * nsteps_update / time_per_iter)
+                               speed)
+                sel = optimizer._collect_selected() if hasattr(optimizer, "_collect_selected") else []
+                optimizer._selected_num_gradients = list(sel)  # keep for the epoch summary
+                per_iter_sel = float(np.mean(sel)) * len(optimizer.arena.buckets) if sel else 0.0
+                metrics.write(iter=int(trainer.get_train_iter()), epoch=epoch, rank=rank, time_per_iter=time_per_iter,
+                              samples_per_s=speed, samples_per_s_node=speed * nworkers,
+                              density=optimizer.get_current_density(),
+                              selected_per_iter=per_iter_sel,
+                              compression_ratio=(nparams * 4.0 / (per_iter_sel * 8.0)) if per_iter_sel else 1.0,
+                              loss=float(trainer.current_loss()),
+                              hbm_gb=(torch.cuda.max_memory_allocated() / 2 ** 30) if trainer.is_cuda else 0.0)
                 times = []
             done += 1
             if max_iters is not None and done >= max_iters:
@@ -201,7 +216,8 @@ def main(argv=None):
                 density_warmup=not args.no_density_warmup, deterministic=args.deterministic,
                 max_iters=args.max_iters, compress_single_rank=args.compress_single_rank, saved_dir=args.saved_dir,
                 bf16_shadow=not args.no_bf16_shadow, momentum_correction=args.momentum_correction,
-                k_cap_factor=args.k_cap_factor, overlap=not args.no_overlap, dump_grad_every=args.dump_grad_every)
+                k_cap_factor=args.k_cap_factor, overlap=not args.no_overlap, dump_grad_every=args.dump_grad_every,
+                metrics_dir=relative_path)
 
 
 if __name__ == "__main__":

@@ -161,6 +161,13 @@ def test_dist_trainer_cli_and_plot(tmp_path):
     import plot
     data = plot.read_log(logs[0])
     assert data["speed"] and data["selected"]
+    jl = []
+    for d, _, fs in os.walk(tmp_path / "logs"):
+        jl += [os.path.join(d, f) for f in fs if f.endswith(".jsonl")]
+    assert jl
+    import json
+    rows = [json.loads(line) for line in open(jl[0])]
+    assert rows and rows[-1]["samples_per_s"] > 0 and rows[-1]["compression_ratio"] > 1
 
 
 def test_evaluate_checkpoints(tmp_path):
@@ -291,3 +298,17 @@ def test_shadow_gemm_1x1_path_cpu(monkeypatch):
     assert y1.shape == y0.shape and y1.is_contiguous(memory_format=torch.channels_last)
     assert torch.allclose(y0, y1, atol=5e-2, rtol=2e-2)
     assert float((g0 - g1).norm() / g0.norm()) < 2e-2
+
+
+def test_watchdog_reports_stall(caplog):
+    import time as _t
+    from gaussiank_sgd_amd.utils.watchdog import Watchdog
+    wd = Watchdog(0.2, lambda: "bucket 0: 3/5 params ready")
+    try:
+        _t.sleep(0.8)
+        assert wd.stalls == 1
+        wd.kick()
+        _t.sleep(0.05)
+        assert wd.stalls == 1
+    finally:
+        wd.stop()
