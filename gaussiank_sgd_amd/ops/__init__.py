@@ -477,10 +477,22 @@ def _same_order(a: torch.Tensor, b: torch.Tensor) -> bool:
     return all(n == 1 or sa == sb for n, sa, sb in zip(a.shape, a.stride(), b.stride()))
 
 
+def _dense(t: torch.Tensor) -> bool:
+    """Non-overlapping and dense: some permutation of the dims is contiguous."""
+    dims = sorted((st, n) for n, st in zip(t.shape, t.stride()) if n != 1)
+    expect = 1
+    for st, n in dims:
+        if st != expect:
+            return False
+        expect *= n
+    return True
+
+
 def accum_grad_(dst: torch.Tensor, src: torch.Tensor) -> None:
     """dst (fp32 arena view) += src (bf16/fp32 gradient with the same element order)."""
-    if dst.is_cuda and src.dtype in (torch.bfloat16, torch.float32) and _same_order(dst, src) and \
-            src.is_non_overlapping_and_dense():
+    native_ok = src.dtype in (torch.bfloat16, torch.float32) and _same_order(dst, src) and _dense(src) and \
+        _dense(dst)
+    if dst.is_cuda and native_ok:
         require_native(dst)
         _ops().accum_grad(dst, src)
     else:

@@ -312,3 +312,16 @@ def test_watchdog_reports_stall(caplog):
         assert wd.stalls == 1
     finally:
         wd.stop()
+
+
+def test_dense_and_order_helpers():
+    from gaussiank_sgd_amd import ops
+    a = torch.zeros(4, 3, 2, 2).to(memory_format=torch.channels_last)
+    b = torch.zeros(4, 3, 2, 2)
+    assert ops._dense(a) and ops._dense(b) and not ops._dense(b[:, :, :1, :])
+    assert ops._same_order(a, a) and not ops._same_order(a, b)
+    w1 = torch.zeros(8, 4, 1, 1).to(memory_format=torch.channels_last)
+    assert ops._same_order(w1, torch.zeros(8, 4, 1, 1))   # 1x1: size-1 dims ignored
+    dst = torch.zeros(8, 4, 1, 1)
+    ops.accum_grad_(dst, torch.ones(8, 4, 1, 1, dtype=torch.bfloat16))
+    assert float(dst.sum()) == 32
