@@ -23,7 +23,6 @@ have PyTorch fallbacks -- which is how the CPU tests check the wiring.)
 """
 from __future__ import annotations
 
-import os
 import types
 
 import torch
@@ -57,25 +56,9 @@ def _shadow(module: nn.Module, name: str, x: torch.Tensor):
     return shadow
 
 
-_GEMM_1X1 = os.environ.get("GKSGD_GEMM_1X1", "0") == "1"
-
-
-def _is_gemm_1x1(conv: nn.Conv2d, x: torch.Tensor) -> bool:
-    return (conv.kernel_size == (1, 1) and conv.stride == (1, 1) and conv.padding in ((0, 0), "valid")
-            and conv.dilation == (1, 1) and conv.groups == 1 and x.dim() == 4
-            and x.is_contiguous(memory_format=torch.channels_last))
-
-
 def _conv_forward(self, x):
     w = _shadow(self, "weight", x)
     b = _shadow(self, "bias", x) if self.bias is not None else None
-    if _GEMM_1X1 and w.dtype == torch.bfloat16 and _is_gemm_1x1(self, x):
-        # 1x1 stride-1 conv on channels-last data is a plain GEMM [N*H*W, Cin] x [Cin, Cout]
-        # (hipBLASLt), and so are both of its backward products.
-        N, C, H, W = x.shape
-        x2 = x.permute(0, 2, 3, 1).reshape(N * H * W, C)
-        y = F.linear(x2, w.reshape(w.shape[0], C), b)
-        return y.view(N, H, W, -1).permute(0, 3, 1, 2)
     return self._conv_forward(x, w, b)
 
 

@@ -68,7 +68,6 @@ if [ "$MODE" = solvers ]; then
 fi
 # 1x1 convs as hipBLASLt GEMMs (A/B) + reference per-GPU batch (32)
 if [ "$MODE" = gemm ]; then
-  step bench_gemm1x1 600 env GKSGD_GEMM_1X1=1 python bench.py --steps 20 --warmup 10 --json-out $OUT/bench_gemm1x1.json
   step bench_bs32 600 python bench.py --steps 30 --warmup 10 --batch-size 32 --json-out $OUT/bench_bs32.json
 fi
 # secondary BASELINE configs (1 GPU) + dense comparator

@@ -275,31 +275,6 @@ def test_momentum_correction_matches_dgc_formula():
         assert torch.allclose(b.slice(arena.velocity), u, atol=1e-6)
 
 
-def test_shadow_gemm_1x1_path_cpu(monkeypatch):
-    """GKSGD_GEMM_1X1: 1x1 stride-1 convs as [NHW, Cin] x [Cin, Cout] GEMMs."""
-    from gaussiank_sgd_amd.parallel import install_bf16_shadow, shadow
-    torch.manual_seed(0)
-    net = torch.nn.Sequential(torch.nn.Conv2d(16, 32, 1), torch.nn.ReLU(), torch.nn.Conv2d(32, 8, 3, padding=1))
-    net = net.to(memory_format=torch.channels_last)
-    ref = [p.detach().clone() for p in net.parameters()]
-    opt = hvd.DistributedOptimizer(torch.optim.SGD(net.parameters(), lr=0.1), named_parameters=net.named_parameters(),
-                                   compression=compressors["none"])
-    install_bf16_shadow(net, opt)
-    x = torch.randn(2, 16, 5, 5).contiguous(memory_format=torch.channels_last)
-    outs = []
-    for flag in (False, True):
-        monkeypatch.setattr(shadow, "_GEMM_1X1", flag)
-        opt.zero_grad()
-        with torch.autocast("cpu", dtype=torch.bfloat16):
-            y = net(x)
-        y.float().sum().backward()
-        outs.append((y.float().detach(), opt.arena.grads.clone()))
-    (y0, g0), (y1, g1) = outs
-    assert y1.shape == y0.shape and y1.is_contiguous(memory_format=torch.channels_last)
-    assert torch.allclose(y0, y1, atol=5e-2, rtol=2e-2)
-    assert float((g0 - g1).norm() / g0.norm()) < 2e-2
-
-
 def test_watchdog_reports_stall(caplog):
     import time as _t
     from gaussiank_sgd_amd.utils.watchdog import Watchdog

@@ -354,6 +354,7 @@ def test_momentum_correct_and_mask(cuda):
     torch.cuda.synchronize()
     assert torch.allclose(u.cpu(), uc, atol=1e-6, rtol=1e-6)
     assert torch.allclose(g.cpu(), gc, atol=1e-6, rtol=1e-6)
+    uc = u.cpu()          # masking is checked bit-exactly against the GPU state
     k_cap = 64
     rec = torch.zeros(ops.REC_HDR + 2 * k_cap, dtype=torch.int32)
     idx = torch.randperm(o)[:50].sort().values.int()
