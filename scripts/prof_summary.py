@@ -51,7 +51,7 @@ def main():
         w = csv.writer(f)
         w.writerow(["name", "calls", "avg_us", "pct", "ms_per_step"])
         for r in rows[:a.top]:
-            name = re.sub(r"\(.*", "", r["Name"]).replace("(anonymous namespace)::", "")[:160]
+            name = re.sub(r"\(.*", "", r["Name"].replace("(anonymous namespace)::", ""))[:160]
             t = float(r["TotalDurationNs"])
             w.writerow([name, r["Calls"], "%.1f" % (float(r["AverageNs"]) / 1e3), "%.2f" % (100 * t / tot),
                         "%.3f" % (t / 1e6 / a.steps)])
