@@ -65,3 +65,32 @@ def test_resnet50_step_bf16(cuda):
     assert t.current_loss() == t.current_loss()
     b = opt.arena.buckets[0]
     assert int(b.bufs.record[0]) > 0
+
+
+@pytest.mark.parametrize("comp", ["gaussian", "topk"])
+def test_overlap_on_off_bitwise_deterministic(cuda, comp):
+    """Deterministic mode: exchanging on the side comm stream during backward
+    (overlap on) and at synchronize() (overlap off) give bitwise-equal weights.
+    fcn5net runs on hipBLASLt GEMMs (repeatable), unlike MIOpen convolutions."""
+    results = []
+    for overlap in (True, False):
+        torch.manual_seed(0)
+        comm.init()
+        t = DLTrainer(0, 1, dnn="fcn5net", dataset="mnist", batch_size=64, lr=0.05, device="cuda",
+                      learnable_data=True)
+        opt = DistributedOptimizer(t.optimizer, named_parameters=t.net.named_parameters(),
+                                   compression=compressors[comp], is_sparse=True, density=0.01,
+                                   compress_single_rank=True, density_warmup=False, deterministic=True,
+                                   overlap=overlap, threshold=50_000)
+        t.update_optimizer(opt)
+        assert len(opt.arena.buckets) > 1
+        g = torch.Generator(device="cuda").manual_seed(5)
+        for _ in range(4):
+            x = torch.randn(64, 1, 28, 28, device="cuda", generator=g)
+            y = torch.randint(0, 10, (64,), device="cuda", generator=g)
+            opt.zero_grad()
+            t.train(1, data=(x, y))
+            t.update_model()
+        torch.cuda.synchronize()
+        results.append(opt.arena.weights.clone())
+    assert torch.equal(results[0], results[1])
