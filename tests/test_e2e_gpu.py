@@ -81,7 +81,7 @@ def test_overlap_on_off_bitwise_deterministic(cuda, comp):
         opt = DistributedOptimizer(t.optimizer, named_parameters=t.net.named_parameters(),
                                    compression=compressors[comp], is_sparse=True, density=0.01,
                                    compress_single_rank=True, density_warmup=False, deterministic=True,
-                                   overlap=overlap, threshold=50_000)
+                                   overlap=overlap, threshold=10_000)
         t.update_optimizer(opt)
         assert len(opt.arena.buckets) > 1
         g = torch.Generator(device="cuda").manual_seed(5)
