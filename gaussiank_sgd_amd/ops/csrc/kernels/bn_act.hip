@@ -567,6 +567,135 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(Src src, const T* 
   }
 }
 
+// Tile-ordered pool backward (k <= 2s, s == 2: the 3x3/s2 stem pool).  The
+// input plane is partitioned into s x s tiles, tile (th, tw) owning input rows
+// th*s-p .. th*s-p+s-1 (and the same for columns); exactly the windows
+// oh in {th-1, th} x ow in {tw-1, tw} can reach a tile, so one thread loads
+// those <= 4 argmax/gradient vectors ONCE and produces dz for all s*s pixels
+// it owns (4x fewer gathers than the per-pixel DyPool path, no division per
+// pixel).  APPLY=false: per-block partial sums of dz and dz*xhat (same
+// [gy][C] partial layout as bn_bwd_reduce_kernel, finished by
+// bn_bwd_finalize_kernel); APPLY=true: dx = scale*(dz - mean(dz) - xhat*mean(dz*xhat)).
+template <typename T, bool TWIN, bool APPLY>
+__global__ __launch_bounds__(kBlock) void bn_pool_tile_kernel(const T* __restrict__ dy, const T* __restrict__ dy2,
+                                                              const uint8_t* __restrict__ amax,
+                                                              const T* __restrict__ x, T* __restrict__ dx,
+                                                              int64_t ntiles, int C, PoolGeo pg, int TH, int TW, Geo g,
+                                                              int64_t M, const float* __restrict__ w,
+                                                              const float* __restrict__ mean,
+                                                              const float* __restrict__ invstd,
+                                                              const float* __restrict__ dbeta,
+                                                              const float* __restrict__ dgamma,
+                                                              float* __restrict__ pdb, float* __restrict__ pdg) {
+  constexpr int V = Vec<T>::N;
+  constexpr int S = 2;
+  const int tc = threadIdx.x % g.tpr;
+  const int lane_r = threadIdx.x / g.tpr;
+  const int c0 = blockIdx.x * g.ct + tc * V;
+  const float invM = 1.f / (float)M;
+  float mu[V], is[V], k1[V], k2[V], k3[V], sb[V], sg[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int c = c0 + i;
+    mu[i] = mean[c];
+    is[i] = invstd[c];
+    sb[i] = sg[i] = 0.f;
+    if (APPLY) {
+      k1[i] = (w ? w[c] : 1.f) * is[i];
+      k2[i] = dbeta[c] * invM;
+      k3[i] = dgamma[c] * invM;
+    }
+  }
+  const int64_t r0 = (int64_t)blockIdx.y * g.rows_per_block;
+  int64_t r1 = r0 + g.rows_per_block;
+  if (r1 > ntiles) r1 = ntiles;
+  const int tplane = TH * TW;
+  for (int64_t t = (lane_r < g.rl ? r0 + lane_r : r1); t < r1; t += g.rl) {
+    const int64_t n = t / tplane;
+    const int rem = (int)(t - n * tplane);
+    const int th = rem / TW, tw = rem - (rem / TW) * TW;
+    // the <= 4 windows that reach this tile
+    uint32_t a[4][2];
+    float gv[4][V];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int oh = th - 1 + (j >> 1), ow = tw - 1 + (j & 1);
+      a[j][0] = a[j][1] = 0xffffffffu;
+#pragma unroll
+      for (int i = 0; i < V; ++i) gv[j][i] = 0.f;
+      if (oh >= 0 && oh < pg.OH && ow >= 0 && ow < pg.OW) {
+        const int64_t o = ((n * pg.OH + oh) * pg.OW + ow) * C + c0;
+        if (V == 8) {
+          const uint2 u = *reinterpret_cast<const uint2*>(amax + o);
+          a[j][0] = u.x;
+          a[j][1] = u.y;
+        } else {
+          a[j][0] = *reinterpret_cast<const uint32_t*>(amax + o);
+        }
+        Vec<T>::load(dy + o, gv[j]);
+        if (TWIN) {
+          float e[V];
+          Vec<T>::load(dy2 + o, e);
+#pragma unroll
+          for (int i = 0; i < V; ++i) gv[j][i] += e[i];
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < S * S; ++q) {
+      const int ih = th * S - pg.p + (q / S), iw = tw * S - pg.p + (q % S);
+      if (ih < 0 || ih >= pg.H || iw < 0 || iw >= pg.W) continue;
+      float d[V];
+#pragma unroll
+      for (int i = 0; i < V; ++i) d[i] = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int kh = ih - ((th - 1 + (j >> 1)) * S - pg.p);
+        const int kw = iw - ((tw - 1 + (j & 1)) * S - pg.p);
+        if (kh < 0 || kh >= pg.k || kw < 0 || kw >= pg.k) continue;
+        const uint32_t pos = (uint32_t)(kh * pg.k + kw);
+#pragma unroll
+        for (int i = 0; i < V; ++i)
+          if (((a[j][i / 4] >> (8 * (i % 4))) & 0xffu) == pos) d[i] += gv[j][i];
+      }
+      const int64_t xo = ((n * pg.H + ih) * pg.W + iw) * C + c0;
+      float xv[V];
+      Vec<T>::load(x + xo, xv);
+      if (APPLY) {
+        float o[V];
+#pragma unroll
+        for (int i = 0; i < V; ++i) o[i] = k1[i] * (d[i] - k2[i] - (xv[i] - mu[i]) * is[i] * k3[i]);
+        Vec<T>::store(dx + xo, o);
+      } else {
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+          sb[i] += d[i];
+          sg[i] = fmaf(d[i], (xv[i] - mu[i]) * is[i], sg[i]);
+        }
+      }
+    }
+  }
+  if (APPLY) return;
+  __shared__ float sh[2][kBlock * 8];
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    sh[0][threadIdx.x * V + i] = sb[i];
+    sh[1][threadIdx.x * V + i] = sg[i];
+  }
+  __syncthreads();
+  for (int cl = threadIdx.x; cl < g.ct; cl += kBlock) {
+    const int tt = cl / V, i = cl % V;
+    float s0 = 0.f, s1 = 0.f;
+    for (int l = 0; l < g.rl; ++l) {
+      s0 += sh[0][(l * g.tpr + tt) * V + i];
+      s1 += sh[1][(l * g.tpr + tt) * V + i];
+    }
+    const int c = blockIdx.x * g.ct + cl;
+    pdb[(int64_t)blockIdx.y * C + c] = s0;
+    pdg[(int64_t)blockIdx.y * C + c] = s1;
+  }
+}
+
 constexpr int kTargetBlocks = 1024;
 constexpr int kPoolTargetBlocks = 4096;
 
@@ -699,7 +828,25 @@ template <typename T, bool TWIN>
 void bn_pool_backward_tw(const T* dy, const T* dy2, const uint8_t* amax, const T* x, T* dx, int64_t M, int C,
                          PoolGeo pg, const float* w, const float* mean, const float* invstd, float* dgamma,
                          float* dbeta, float* ws, float* gw_acc, float* gb_acc, hipStream_t s) {
-  // the gather is latency-bound: use more workgroups than the plain BN passes
+  if (pg.s == 2 && pg.k <= 4) {  // every window reaching tile th has oh in {th-1, th}
+    // tile-ordered fast path (3x3/s2 stem pool)
+    const int TH = (pg.H + pg.p + pg.s - 1) / pg.s, TW = (pg.W + pg.p + pg.s - 1) / pg.s;
+    const int64_t N = M / ((int64_t)pg.H * pg.W);
+    const int64_t ntiles = N * TH * TW;
+    const Geo g = make_geo<T>(ntiles, C, kPoolTargetBlocks);
+    float* pdb = ws;
+    float* pdg = ws + (int64_t)g.gy * C;
+    hipLaunchKernelGGL((bn_pool_tile_kernel<T, TWIN, false>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, dy, dy2, amax, x,
+                       (T*)nullptr, ntiles, C, pg, TH, TW, g, M, w, mean, invstd, (const float*)nullptr,
+                       (const float*)nullptr, pdb, pdg);
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(kBlock), 0, s, pdb, pdg, g.gy, C,
+                       dbeta, dgamma, gb_acc, gw_acc);
+    hipLaunchKernelGGL((bn_pool_tile_kernel<T, TWIN, true>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, dy, dy2, amax, x,
+                       dx, ntiles, C, pg, TH, TW, g, M, w, mean, invstd, dbeta, dgamma, (float*)nullptr,
+                       (float*)nullptr);
+    return;
+  }
+  // generic k, s: per-pixel gather (latency-bound: more workgroups than the plain BN passes)
   if ((pg.k + pg.s - 1) / pg.s <= 2)
     bn_backward_src<T>(DyPool<T, TWIN, 2>{dy, dy2, amax, pg}, x, dx, (T*)nullptr, M, C, w, mean, invstd, dgamma,
                        dbeta, ws, gw_acc, gb_acc, s, kPoolTargetBlocks);
