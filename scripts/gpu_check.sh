@@ -66,6 +66,16 @@ if [ "$MODE" = solvers ]; then
   step bench_noboth 600 env MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_BWD_GTC_XDLOPS_NHWC=0 \
     MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_WRW_GTC_XDLOPS_NHWC=0 python bench.py --steps 20 --warmup 10 --json-out $OUT/bench_noboth.json
 fi
+# MIOpen kernel-parameter tuning (perf-db) for the bench shapes: exhaustive
+# search per convolution, written into the repo's user db (tuning/miopen).
+# Progress goes to a growing log under gpurun_out (the call is not idle).
+if [ "$MODE" = tune ]; then
+  echo "=== tune ($(date +%T))"
+  timeout -k 10 ${TUNE_S:-1000} env MIOPEN_FIND_ENFORCE=SEARCH MIOPEN_LOG_LEVEL=5 python bench.py --steps 2 --warmup 1 \
+    --cudnn-benchmark --json-out $OUT/tune.json > $OUT/tune.log 2>&1
+  echo "tune rc=$?"
+  mkdir -p $OUT/tuning && cp -r tuning/miopen $OUT/tuning/ && ls -la $OUT/tuning/miopen
+fi
 # 1x1 convs as hipBLASLt GEMMs (A/B) + reference per-GPU batch (32)
 if [ "$MODE" = gemm ]; then
   step bench_bs32 600 python bench.py --steps 30 --warmup 10 --batch-size 32 --json-out $OUT/bench_bs32.json
