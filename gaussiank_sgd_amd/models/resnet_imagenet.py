@@ -20,7 +20,7 @@ from typing import List, Optional, Type, Union
 import torch
 import torch.nn as nn
 
-from ..ops.bn import BNAct
+from ..ops.bn import BNAct, global_avg_pool
 
 
 def conv3x3(inp: int, out: int, stride: int = 1, groups: int = 1, dilation: int = 1) -> nn.Conv2d:
@@ -125,8 +125,7 @@ class ResNet(nn.Module):
     def forward(self, x):
         x = self.maxpool(self.bn1(self.conv1(x)))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
-        x = torch.flatten(self.avgpool(x), 1)
-        return self.fc(x)
+        return self.fc(global_avg_pool(x))   # == flatten(avgpool(x)), channels-last backward
 
 
 def resnet18(num_classes=1000, **kw):

@@ -209,3 +209,26 @@ class BNAct(nn.BatchNorm2d):
 
     def extra_repr(self) -> str:
         return super().extra_repr() + ", act=%s" % self.act + (", pool=%s" % (self.pool,) if self.pool else "")
+
+
+class _GlobalAvgPoolCL(torch.autograd.Function):
+    """mean over H, W whose backward writes a channels-last gradient directly
+    (the generic adaptive_avg_pool2d backward yields NCHW, and the fused BN
+    backward that consumes it would need a transposing copy)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.shape = x.shape
+        return x.mean(dim=(2, 3))
+
+    @staticmethod
+    def backward(ctx, g):
+        N, C, H, W = ctx.shape
+        return (g / (H * W))[:, :, None, None].expand(N, C, H, W).contiguous(memory_format=_CL)
+
+
+def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
+    """[N, C, H, W] -> [N, C]; channels-last aware backward."""
+    if x.dim() == 4 and x.is_contiguous(memory_format=_CL) and x.requires_grad:
+        return _GlobalAvgPoolCL.apply(x)
+    return x.mean(dim=(2, 3))

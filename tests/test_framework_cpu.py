@@ -328,3 +328,15 @@ def test_resnet20_selected_count_schedule():
         got.append(opt._collect_selected())
         opt.increase_one_epoch()
     assert got == [[4214], [1078], [269]]
+
+
+def test_global_avg_pool_cl():
+    from gaussiank_sgd_amd.ops.bn import global_avg_pool
+    x = torch.randn(2, 8, 5, 3).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    y = global_avg_pool(x)
+    ref = torch.nn.functional.adaptive_avg_pool2d(x, 1).flatten(1)
+    assert torch.allclose(y, ref, atol=1e-6)
+    g = torch.randn(2, 8)
+    (gx,) = torch.autograd.grad(y, x, g)
+    (gr,) = torch.autograd.grad(ref, x, g)
+    assert gx.is_contiguous(memory_format=torch.channels_last) and torch.allclose(gx, gr, atol=1e-6)
