@@ -19,7 +19,7 @@ from gaussiank_sgd_amd import ops
 from gaussiank_sgd_amd.compression import reference
 from gaussiank_sgd_amd.utils.stats import gaussian_z
 
-SETTINGS = settings(max_examples=25, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+SETTINGS = settings(max_examples=25, deadline=None, derandomize=True, suppress_health_check=[HealthCheck.too_slow])
 
 MODES = [ops.MODE_GAUSSIAN, ops.MODE_TOPK, ops.MODE_RANDOMK, ops.MODE_REDSYNC, ops.MODE_REDSYNCTRIM,
          ops.MODE_THRESHOLD, ops.MODE_DGC]
