@@ -1,0 +1,113 @@
+#!/usr/bin/env python3
+"""Per-convolution roofline report for ResNet-50 at the bench batch size.
+
+For every distinct convolution of ResNet-50 (bf16, channels-last, MIOpen via
+torch) this times forward, backward-data and backward-weight and compares
+each against its roofline: max(FLOPs / 2.5 PFLOP/s dense bf16,
+compulsory bytes / 6.3 TB/s achievable HBM).  Shows where the vendor
+convolutions leave time on the table (the input to custom-kernel work).
+
+Usage (GPU): python bench/convs.py [--batch 512] [--json-out FILE]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+from collections import Counter
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+_HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(_HERE, "tuning", "miopen"))
+
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+PEAK = 2.5e15
+HBM = 6.3e12
+
+
+def resnet50_convs(batch: int):
+    """(N, Cin, H, W, Cout, k, stride, pad) with multiplicity."""
+    from gaussiank_sgd_amd.models import resnet50
+    net = resnet50(num_classes=1000)
+    shapes = Counter()
+    hooks = []
+
+    def mk(mod):
+        def h(m, inp, out):
+            x = inp[0]
+            shapes[(batch, x.shape[1], x.shape[2], x.shape[3], m.out_channels, m.kernel_size[0], m.stride[0],
+                    m.padding[0])] += 1
+        return h
+    for m in net.modules():
+        if isinstance(m, torch.nn.Conv2d):
+            hooks.append(m.register_forward_hook(mk(m)))
+    with torch.no_grad():
+        net.eval()(torch.zeros(1, 3, 224, 224))
+    for h in hooks:
+        h.remove()
+    return shapes
+
+
+def timeit(fn, iters=10):
+    for _ in range(2):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters * 1e-3
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--json-out", default=None)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    rows = []
+    tot = {"fwd": [0.0, 0.0], "dgrad": [0.0, 0.0], "wgrad": [0.0, 0.0]}
+    for (N, C, H, W, K, k, s, p), mult in sorted(resnet50_convs(args.batch).items()):
+        x = torch.randn(N, C, H, W, device=dev, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        w = torch.randn(K, C, k, k, device=dev, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        y = F.conv2d(x, w, stride=s, padding=p)
+        OH, OW = y.shape[2], y.shape[3]
+        dy = torch.randn_like(y)
+        flops = 2.0 * N * OH * OW * K * C * k * k
+        bx, bw, by = x.numel() * 2, w.numel() * 2, y.numel() * 2
+        xg = x.detach().requires_grad_(True)
+        wg = w.detach().requires_grad_(True)
+        yg = F.conv2d(xg, wg, stride=s, padding=p)
+        cases = {
+            "fwd": (lambda: F.conv2d(x, w, stride=s, padding=p), bx + bw + by),
+            "dgrad": (lambda: torch.autograd.grad(yg, xg, dy, retain_graph=True), by + bw + bx),
+            "wgrad": (lambda: torch.autograd.grad(yg, wg, dy, retain_graph=True), by + bx + bw),
+        }
+        for name, (fn, nbytes) in cases.items():
+            t = timeit(fn)
+            roof = max(flops / PEAK, nbytes / HBM)
+            tot[name][0] += t * mult
+            tot[name][1] += roof * mult
+            r = dict(op=name, N=N, Cin=C, H=H, W=W, Cout=K, k=k, stride=s, count=mult, us=round(t * 1e6, 1),
+                     roofline_us=round(roof * 1e6, 1), eff=round(roof / t, 3),
+                     tflops=round(flops / t / 1e12, 1), bound="compute" if flops / PEAK > nbytes / HBM else "memory")
+            rows.append(r)
+            print(json.dumps(r), flush=True)
+        del x, w, y, dy, xg, wg, yg
+    for name, (t, roof) in tot.items():
+        print("TOTAL %-5s %.2f ms per step (roofline %.2f ms, efficiency %.0f%%)" % (name, t * 1e3, roof * 1e3,
+                                                                                   100 * roof / t))
+    if args.json_out:
+        with open(args.json_out, "w") as f:
+            json.dump({"rows": rows, "totals_ms": {k: [v[0] * 1e3, v[1] * 1e3] for k, v in tot.items()}}, f,
+                      indent=1)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
