@@ -68,6 +68,8 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--gemm", action="store_true",
+                    help="also time the stride-1 1x1 convs as plain torch.mm (hipBLASLt) GEMMs")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     rows = []
@@ -98,6 +100,20 @@ def main() -> int:
                      tflops=round(flops / t / 1e12, 1), bound="compute" if flops / PEAK > nbytes / HBM else "memory")
             rows.append(r)
             print(json.dumps(r), flush=True)
+        if args.gemm and k == 1 and s == 1:
+            M = N * H * W
+            X = x.permute(0, 2, 3, 1).reshape(M, C)
+            Wm = w.reshape(K, C)
+            DY = dy.permute(0, 2, 3, 1).reshape(M, K)
+            for name, fn, nbytes in (("mm_fwd", lambda: X @ Wm.t(), bx + bw + by),
+                                     ("mm_dgrad", lambda: DY @ Wm, bx + bw + by),
+                                     ("mm_wgrad", lambda: DY.t() @ X, bx + bw + by)):
+                t = timeit(fn)
+                roof = max(flops / PEAK, nbytes / HBM)
+                r = dict(op=name, N=N, Cin=C, H=H, W=W, Cout=K, k=k, stride=s, count=mult, us=round(t * 1e6, 1),
+                         roofline_us=round(roof * 1e6, 1), eff=round(roof / t, 3))
+                rows.append(r)
+                print(json.dumps(r), flush=True)
         del x, w, y, dy, xg, wg, yg
     for name, (t, roof) in tot.items():
         print("TOTAL %-5s %.2f ms per step (roofline %.2f ms, efficiency %.0f%%)" % (name, t * 1e3, roof * 1e3,
