@@ -199,6 +199,10 @@ def main() -> int:
         "params": nparams,
         "final_loss": round(loss, 4) if loss == loss else None,
     }
+    if rank == 0 and os.environ.get("GKSGD_GEMM_DUMP"):
+        from gaussiank_sgd_amd.ops.conv1x1 import tuned_choices
+        with open(os.environ["GKSGD_GEMM_DUMP"], "w") as f:
+            json.dump([[list(k), list(v)] for k, v in tuned_choices().items()], f)
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)

@@ -90,6 +90,8 @@ def main() -> int:
             "dgrad": (lambda: torch.autograd.grad(yg, xg, dy, retain_graph=True), by + bw + bx),
             "wgrad": (lambda: torch.autograd.grad(yg, wg, dy, retain_graph=True), by + bx + bw),
         }
+        if C == 3:
+            del cases["dgrad"]   # the stem's input (the image batch) needs no gradient in training
         for name, (fn, nbytes) in cases.items():
             t = timeit(fn)
             roof = max(flops / PEAK, nbytes / HBM)

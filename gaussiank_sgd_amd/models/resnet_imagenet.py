@@ -21,6 +21,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.bn import BNAct, global_avg_pool
+from ..ops.conv1x1 import Conv1x1
 
 
 def conv3x3(inp: int, out: int, stride: int = 1, groups: int = 1, dilation: int = 1) -> nn.Conv2d:
@@ -28,7 +29,8 @@ def conv3x3(inp: int, out: int, stride: int = 1, groups: int = 1, dilation: int 
 
 
 def conv1x1(inp: int, out: int, stride: int = 1) -> nn.Conv2d:
-    return nn.Conv2d(inp, out, 1, stride=stride, bias=False)
+    # nn.Conv2d subclass: stride-1 training runs the autotuned MFMA GEMMs (ops/conv1x1.py)
+    return Conv1x1(inp, out, stride)
 
 
 class BasicBlock(nn.Module):

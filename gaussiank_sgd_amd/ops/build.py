@@ -34,6 +34,7 @@ HIP_SOURCES = [
     "kernels/scatter.hip",
     "kernels/optim.hip",
     "kernels/bn_act.hip",
+    "kernels/gemm.hip",
 ]
 CXX_SOURCES = [
     "comm/rccl_engine.cpp",

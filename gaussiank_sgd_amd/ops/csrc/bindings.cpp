@@ -560,7 +560,48 @@ struct RcclEngine : torch::CustomClassHolder {
   int64_t world() const { return comm.world(); }
 };
 
+// ---------------------------------------------------------------------------
+// 1x1-convolution GEMMs (gemm.hip)
+// ---------------------------------------------------------------------------
+bool gemm_supported(int64_t N, int64_t K) { return gk::gemm_supported(N, K); }
+
+void check_rows(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 2, name, " must be a 2-D bf16 GPU tensor");
+  TORCH_CHECK(t.stride(1) == 1 && t.stride(0) % 8 == 0, name, " rows must be contiguous, 16-byte aligned");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+}
+
+// C[M, N] = A[M, K] . B[N, K]^T
+void gemm_nt(at::Tensor A, at::Tensor B, at::Tensor C, int64_t cfg, int64_t max_blocks) {
+  check_rows(A, "A");
+  check_rows(B, "B");
+  check_rows(C, "C");
+  const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
+  TORCH_CHECK(B.size(1) == K && C.size(0) == M && C.size(1) == N, "gemm_nt: shape mismatch");
+  TORCH_CHECK(gk::gemm_supported(N, K), "gemm_nt: N and K must be multiples of 64");
+  TORCH_CHECK(M > 0, "gemm_nt: empty M");
+  c10::DeviceGuard guard(A.device());
+  gk::gemm_nt_bf16(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), M, (int)N,
+                   (int)K, (int)cfg, (int)max_blocks, cur_stream(A));
+}
+
+// W[N, K] += G[M, N]^T . X[M, K]   (fp32 W, float atomics)
+void gemm_tn_acc(at::Tensor G, at::Tensor X, at::Tensor W, int64_t cfg, int64_t splits) {
+  check_rows(G, "G");
+  check_rows(X, "X");
+  TORCH_CHECK(W.is_cuda() && W.scalar_type() == at::kFloat && W.dim() == 2 && W.stride(1) == 1,
+              "W must be a 2-D fp32 GPU tensor with contiguous rows");
+  const int64_t M = G.size(0), N = G.size(1), K = X.size(1);
+  TORCH_CHECK(X.size(0) == M && W.size(0) == N && W.size(1) == K, "gemm_tn_acc: shape mismatch");
+  TORCH_CHECK(gk::gemm_supported(N, K), "gemm_tn_acc: N and K must be multiples of 64");
+  if (M == 0) return;
+  c10::DeviceGuard guard(G.device());
+  gk::gemm_tn_acc_f32(G.data_ptr(), G.stride(0), X.data_ptr(), X.stride(0), W.data_ptr<float>(), W.stride(0), M,
+                      (int)N, (int)K, (int)cfg, (int)splits, cur_stream(G));
+}
+
 }  // namespace
+
 
 TORCH_LIBRARY(gksgd, m) {
   m.def("ctrl_bytes() -> int", &ctrl_bytes);
@@ -610,6 +651,9 @@ TORCH_LIBRARY(gksgd, m) {
       "float[] momentum, float[] weight_decay) -> ()");
   m.def("mask_records(Tensor(a!) u, Tensor record, int k_cap) -> ()");
   m.def("cast_bf16(Tensor(a!) dst, Tensor src) -> ()");
+  m.def("gemm_supported(int N, int K) -> bool", &gemm_supported);
+  m.def("gemm_nt(Tensor A, Tensor B, Tensor(a!) C, int cfg=0, int max_blocks=0) -> ()");
+  m.def("gemm_tn_acc(Tensor G, Tensor X, Tensor(a!) W, int cfg=0, int splits=0) -> ()");
 
   m.class_<RcclEngine>("RcclEngine")
       .def(torch::init<>())
@@ -644,4 +688,6 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("momentum_correct", &momentum_correct);
   m.impl("mask_records", &mask_records);
   m.impl("cast_bf16", &cast_bf16);
+  m.impl("gemm_nt", &gemm_nt);
+  m.impl("gemm_tn_acc", &gemm_tn_acc);
 }

@@ -1,0 +1,490 @@
+// MFMA GEMMs for 1x1 convolutions on channels-last (NHWC) activations, gfx950.
+//
+// A stride-1 1x1 convolution over NHWC data is a plain GEMM over the
+// M = N*H*W pixel rows:
+//   forward      Y[M, Cout] = X[M, Cin]  . W[Cout, Cin]^T          (gemm_nt)
+//   grad-input  dX[M, Cin]  = dY[M, Cout] . Wt[Cin, Cout]^T        (gemm_nt, Wt = W^T)
+//   grad-weight dW[Cout, Cin] += dY[M, Cout]^T . X[M, Cin]         (gemm_tn, split over M)
+// MIOpen/hipBLASLt run these ResNet-50 shapes at 20-65 % of their HBM
+// roofline and the tall-skinny grad-weight reduction at ~10 %
+// (profiles/r01_resnet50_conv_roofline_bs512.txt), so they get their own
+// kernels here.
+//
+// gemm_nt: 64*WM*WN threads, each wave owns a 64x64 output tile made of 4x4
+//   v_mfma_f32_16x16x32_bf16 tiles.  Operands are K-contiguous, staged
+//   global -> LDS with 16-byte global_load_lds (LDS-DMA) into 128-byte rows
+//   (one 64-deep K slice) whose 16-byte chunks are XOR-swizzled by
+//   (row >> 1) & 7, which makes every ds_read_b128 fragment read bank-conflict
+//   free.  The MFMA is issued "swapped" (weight rows as the A operand, pixel
+//   rows as B), so each lane ends with 4 consecutive output channels of one
+//   pixel and writes them as one 8-byte store.  The grid is persistent over
+//   M tiles and the two LDS stages are pipelined across tile boundaries, so
+//   the next tile's loads are in flight during the current tile's MFMAs and
+//   stores (the K = 64 layers have a single K step per tile).
+// gemm_tn: reduction over the pixel dimension M; both operands are
+//   M-major, so fragments are read with ds_read_b64_tr_b16 (the gfx950 LDS
+//   transpose read: 4 rows x 16 columns of 16-bit data delivered column-wise).
+//   Each block reduces a contiguous slice of M for one output tile and adds
+//   its fp32 partial into the (gradient-arena) output with float atomics.
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+#include "gk_kernels.h"
+
+namespace gk {
+namespace {
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+#define GK_LDS __attribute__((address_space(3)))
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+
+// two fp32 -> packed bf16x2, round-to-nearest-even (one v_cvt_pk_bf16_f32)
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{lo, hi}, bf16x2_t));
+}
+
+__device__ __forceinline__ void glds16(const void* src, GK_LDS void* dst) {
+  __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
+}
+
+__device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
+
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n: waits until at most n of
+// this wave's vector-memory operations (loads, stores, LDS-DMA; they retire
+// in issue order) are still in flight.
+template <int N>
+__device__ __forceinline__ void vmcnt_le() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+__device__ __forceinline__ void wait_vmcnt(int n) {
+#define GK_VMW(k) \
+  case k: vmcnt_le<k>(); break;
+  switch (n) {
+    GK_VMW(0) GK_VMW(1) GK_VMW(2) GK_VMW(3) GK_VMW(4) GK_VMW(5) GK_VMW(6) GK_VMW(7) GK_VMW(8) GK_VMW(9)
+    GK_VMW(10) GK_VMW(11) GK_VMW(12) GK_VMW(13) GK_VMW(14) GK_VMW(15) GK_VMW(16) GK_VMW(17) GK_VMW(18)
+    GK_VMW(19) GK_VMW(20) GK_VMW(21) GK_VMW(22) GK_VMW(23) GK_VMW(24) GK_VMW(25) GK_VMW(26) GK_VMW(27)
+    GK_VMW(28) GK_VMW(29) GK_VMW(30) GK_VMW(31) GK_VMW(32) GK_VMW(33) GK_VMW(34) GK_VMW(35) GK_VMW(36)
+    GK_VMW(37) GK_VMW(38) GK_VMW(39) GK_VMW(40)
+    default: vmcnt_le<0>(); break;
+  }
+#undef GK_VMW
+}
+
+// --------------------------------------------------------------------------
+// gemm_nt
+// --------------------------------------------------------------------------
+// BRES: the block's whole weight panel [BN x K] stays resident in LDS (it is
+// the same for every M tile of the persistent loop); only A is streamed.
+// NS: LDS stages; NS = 3 keeps two K slices in flight behind the one being
+// multiplied.
+template <int WM, int WN, bool BRES>
+struct NtCfg {
+  static constexpr int NW = WM * WN;
+  static constexpr int THREADS = 64 * NW;
+  static constexpr int BM = 64 * WM;
+  static constexpr int BN = 64 * WN;
+  static constexpr int ASTAGE = BM * 128;         // bytes: BM rows x 64 bf16
+  static constexpr int BSTAGE = BN * 128;
+  static constexpr int STAGE = BRES ? ASTAGE : ASTAGE + BSTAGE;
+  static constexpr int INSTS = STAGE / 1024;      // 1-KiB LDS-DMA instructions per stage
+  static_assert(INSTS % NW == 0, "stage split");
+  static constexpr int LPW = INSTS / NW;          // LDS-DMA instructions per wave per stage
+  static constexpr int NST = 8;                   // 16-byte epilogue stores per wave per tile
+  static_assert(LPW + 2 * NST <= 40, "wait_vmcnt range");
+  static int lds_bytes(int K, int ns) { return ns * STAGE + (BRES ? BN * K * 2 : 0); }
+};
+
+template <int WM, int WN, bool BRES, int NS>
+__global__ void __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(WM * WN >= 8 ? 1 : 2)))
+gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
+               uint16_t* __restrict__ C, int64_t ldc, int64_t M, int K) {
+  using Cfg = NtCfg<WM, WN, BRES>;
+  static_assert(NS == 2 || NS == 3, "stages");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int n0 = blockIdx.y * Cfg::BN;
+  const int64_t mtiles = (M + Cfg::BM - 1) / Cfg::BM;
+  const int nk = K >> 6;
+  // this block's work: M tiles blockIdx.x, +gridDim.x, ...; each has nk K slices
+  const int64_t my_tiles = blockIdx.x < mtiles ? (mtiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+  const int64_t T = my_tiles * nk;
+  if (T == 0) return;
+  char* stage_base = smem + (BRES ? Cfg::BN * K * 2 : 0);
+
+  if (BRES) {  // weight panel: slice ks at smem + ks*BSTAGE, rows swizzled as the streamed tiles
+    const int per = Cfg::BN / 8;
+    for (int i = wave; i < nk * per; i += Cfg::NW) {
+      const int ks = i / per, ri = i % per;
+      const int r = ri * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ swz(r);
+      glds16(B + (int64_t)(n0 + r) * ldb + ks * 64 + c * 8, (GK_LDS char*)smem + ks * Cfg::BSTAGE + ri * 1024);
+    }
+  }
+
+  auto stage = [&](int64_t t) {
+    const int64_t mt = blockIdx.x + (t / nk) * gridDim.x;
+    const int k0 = (int)(t % nk) << 6;
+    const int64_t m0 = mt * Cfg::BM;
+    GK_LDS char* base = (GK_LDS char*)stage_base + (int)(t % NS) * Cfg::STAGE;
+#pragma unroll
+    for (int j = 0; j < Cfg::LPW; ++j) {
+      const int i = wave + j * Cfg::NW;
+      const int r = i * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ swz(r);
+      const uint16_t* src;
+      if (BRES || i * 8 < Cfg::BM) {
+        int64_t gr = m0 + r;
+        gr = gr < M ? gr : M - 1;
+        src = A + gr * lda + k0 + c * 8;
+      } else {
+        src = B + (int64_t)(n0 + r - Cfg::BM) * ldb + k0 + c * 8;
+      }
+      glds16(src, base + i * 1024);
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  stage(0);
+  if (NS == 3 && T > 1) stage(1);
+  const int fr = lane & 15, fq = lane >> 4;
+  // stores issued by the last two steps (0 when none, or when a partial tile
+  // drained its stores with vmcnt(0) right away)
+  int st1 = 0, st2 = 0;
+  for (int64_t t = 0; t < T; ++t) {
+    // ops issued after stage(t), in order: NS=2: stores(t-1);
+    // NS=3: stores(t-2), stage(t+1), stores(t-1).  Retire stage(t) only.
+    if (NS == 2) wait_vmcnt(st1);
+    else wait_vmcnt(st2 + (t + 1 < T ? Cfg::LPW : 0) + st1);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + NS - 1 < T) stage(t + NS - 1);
+    const int ks = (int)(t % nk);
+    const char* As = stage_base + (int)(t % NS) * Cfg::STAGE;
+    const char* Bs = BRES ? smem + ks * Cfg::BSTAGE : As + Cfg::ASTAGE;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int c = kk * 4 + fq;
+      bf16x8 av[4], bv[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int ra = wm * 64 + s * 16 + fr;
+        av[s] = *reinterpret_cast<const bf16x8*>(As + ra * 128 + ((c ^ swz(ra)) << 4));
+        const int rb = wn * 64 + s * 16 + fr;
+        bv[s] = *reinterpret_cast<const bf16x8*>(Bs + rb * 128 + ((c ^ swz(rb)) << 4));
+      }
+#pragma unroll
+      for (int ms = 0; ms < 4; ++ms)
+#pragma unroll
+        for (int ns = 0; ns < 4; ++ns)
+          acc[ms][ns] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv[ns], av[ms], acc[ms][ns], 0, 0, 0);
+    }
+    st2 = st1;
+    st1 = 0;
+    if (ks == nk - 1) {
+      // lane holds C[m = fr][n = 4*fq + r] of every 16x16 subtile.  Lanes fq and
+      // fq^1 swap halves of the subtile pair (2p, 2p+1) so each lane owns 8
+      // consecutive channels: one 16-byte store per lane per pair.
+      const int64_t mt = blockIdx.x + (t / nk) * gridDim.x;
+      const int64_t mbase = mt * Cfg::BM;
+      const bool full = mbase + Cfg::BM <= M;
+      const bool odd = fq & 1;
+#pragma unroll
+      for (int ms = 0; ms < 4; ++ms) {
+        const int64_t m = mbase + wm * 64 + ms * 16 + fr;
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr) {
+          const f32x4 va = acc[ms][2 * pr], vb = acc[ms][2 * pr + 1];
+          const uint32_t a0 = pack_bf16x2(va[0], va[1]), a1 = pack_bf16x2(va[2], va[3]);
+          const uint32_t b0 = pack_bf16x2(vb[0], vb[1]), b1 = pack_bf16x2(vb[2], vb[3]);
+          const uint32_t r0 = (uint32_t)__shfl_xor((int)(odd ? a0 : b0), 16, 64);
+          const uint32_t r1 = (uint32_t)__shfl_xor((int)(odd ? a1 : b1), 16, 64);
+          const uint4 v = odd ? make_uint4(r0, r1, b0, b1) : make_uint4(a0, a1, r0, r1);
+          const int n = n0 + wn * 64 + pr * 32 + (odd ? 16 + 4 * (fq - 1) : 4 * fq);
+          if (full || m < M) *reinterpret_cast<uint4*>(C + m * ldc + n) = v;
+        }
+#pragma unroll
+        for (int ns = 0; ns < 4; ++ns) acc[ms][ns] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      if (full) st1 = Cfg::NST;
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // skipped stores: keep the counts exact
+    }
+  }
+}
+
+template <int WM, int WN, bool BRES, int NS>
+void launch_nt(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, uint16_t* C, int64_t ldc, int64_t M,
+               int N, int K, int max_blocks, hipStream_t stream) {
+  using Cfg = NtCfg<WM, WN, BRES>;
+  const int ntiles = N / Cfg::BN;
+  const int64_t mtiles = (M + Cfg::BM - 1) / Cfg::BM;
+  const int lds = Cfg::lds_bytes(K, NS);
+  const int per_cu = (160 * 1024) / lds > 0 ? (160 * 1024) / lds : 1;
+  int64_t gx = ((int64_t)256 * per_cu + ntiles - 1) / ntiles;
+  if (max_blocks > 0) gx = max_blocks;
+  if (gx < 1) gx = 1;
+  if (gx > mtiles) gx = mtiles;
+  dim3 grid((unsigned)gx, (unsigned)ntiles);
+  static bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<WM, WN, BRES, NS>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL((gemm_nt_kernel<WM, WN, BRES, NS>), grid, dim3(Cfg::THREADS), lds, stream, A, lda, B, ldb, C,
+                     ldc, M, K);
+}
+
+template <int WM, int WN>
+void launch_nt_any(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, uint16_t* C, int64_t ldc,
+                   int64_t M, int N, int K, int max_blocks, int bres, int ns, hipStream_t stream) {
+  // keep the weight panel resident when it fits next to the two A stages
+  if (bres < 0) bres = (64 * WN) * K * 2 <= 64 * 1024;
+  if (bres && NtCfg<WM, WN, true>::lds_bytes(K, 2) > 160 * 1024) bres = 0;
+  constexpr int L = 160 * 1024;
+  if (bres) {
+    if (ns != 2 && NtCfg<WM, WN, true>::lds_bytes(K, 3) <= L) launch_nt<WM, WN, true, 3>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, stream);
+    else launch_nt<WM, WN, true, 2>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, stream);
+  } else {
+    if (ns != 2 && NtCfg<WM, WN, false>::lds_bytes(K, 3) <= L) launch_nt<WM, WN, false, 3>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, stream);
+    else launch_nt<WM, WN, false, 2>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, stream);
+  }
+}
+
+// --------------------------------------------------------------------------
+// gemm_tn: W[N, K] += G[M, N]^T . X[M, K]
+// --------------------------------------------------------------------------
+template <int WN, int WK, int NS_ = 2>
+struct TnCfg {
+  static constexpr int NW = WN * WK;
+  static constexpr int THREADS = 64 * NW;
+  static constexpr int BN = 64 * WN;                 // output rows (G columns)
+  static constexpr int BK = 64 * WK;                 // output cols (X columns)
+  static constexpr int GROW = BN * 2;                // bytes per staged G row
+  static constexpr int XROW = BK * 2;
+  static constexpr int GBYTES = 64 * GROW;           // 64 pixel rows per stage
+  static constexpr int STAGE = 64 * (GROW + XROW);
+  static constexpr int NS = NS_;                     // LDS stages (3: two slices in flight)
+  static constexpr int LDS = NS * STAGE;
+  static constexpr int GINSTS = GBYTES / 1024;
+  static constexpr int INSTS = STAGE / 1024;
+  static_assert(INSTS % NW == 0, "stage split");
+  static constexpr int LPW = INSTS / NW;
+};
+
+// LDS image of a [64 rows][RB bytes] tile for transposed reads: 16-byte chunk
+// c of row r is stored at chunk c ^ tr_swz(r).  A ds_read_b64_tr_b16 half-wave
+// touches rows {R..R+3, R+8..R+11} x 32 bytes; the XOR spreads those 16
+// (row, chunk) pairs over 16 distinct 16-byte bank slots.
+template <int RB>
+__device__ __forceinline__ int tr_swz(int r) {
+  if (RB == 128) return 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1));
+  return 2 * ((r & 3) | (((r >> 3) & 1) << 2));
+}
+
+// Transposed fragment: lane l (group g = l>>4, li = l&15) gets rows
+// r0 + 8g + 0..7 of column c0 + li of the swizzled [rows][RB] bf16 image, as
+// the 8 k-elements of a 16x16x32 MFMA operand.  c0 is a multiple of 16.
+template <int RB>
+__device__ __forceinline__ bf16x8 tr_frag(const char* tile, int r0, int c0, int lane) {
+  const int g = lane >> 4, li = lane & 15;
+  const int q = li >> 2, p = li & 3;
+  const int col = c0 + 4 * p;
+  const int ra = r0 + 8 * g + q, rb = ra + 4;
+  const char* a0 = tile + ra * RB + ((((col >> 3) ^ tr_swz<RB>(ra)) << 4) | ((col & 7) << 1));
+  const char* a1 = tile + rb * RB + ((((col >> 3) ^ tr_swz<RB>(rb)) << 4) | ((col & 7) << 1));
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((GK_LDS bf16x4*)(GK_LDS char*)a0);
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((GK_LDS bf16x4*)(GK_LDS char*)a1);
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <int WN, int WK, int NS>
+__global__ void __launch_bounds__(64 * WN * WK) __attribute__((amdgpu_waves_per_eu(2)))
+gemm_tn_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __restrict__ X, int64_t ldx,
+               float* __restrict__ W, int64_t ldw, int64_t M, int64_t rows_per_split) {
+  using Cfg = TnCfg<WN, WK, NS>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wn = wave / WK, wk = wave % WK;
+  const int n0 = blockIdx.x * Cfg::BN;
+  const int c0 = blockIdx.y * Cfg::BK;
+  const int64_t mbeg = (int64_t)blockIdx.z * rows_per_split;
+  int64_t mend = mbeg + rows_per_split;
+  if (mend > M) mend = M;
+  if (mbeg >= mend) return;
+  const int T = (int)((mend - mbeg + 63) >> 6);
+
+  auto stage = [&](int t) {
+    const int64_t m0 = mbeg + (int64_t)t * 64;
+    GK_LDS char* base = (GK_LDS char*)smem + (t % Cfg::NS) * Cfg::STAGE;
+#pragma unroll
+    for (int j = 0; j < Cfg::INSTS / Cfg::NW; ++j) {
+      const int i = wave + j * Cfg::NW;
+      const uint16_t* src;
+      if (i < Cfg::GINSTS) {
+        constexpr int CPR = Cfg::GROW / 16;               // 16-byte chunks per row
+        const int e = i * 64 + lane;
+        const int r = e / CPR;
+        int64_t gr = m0 + r;
+        gr = gr < M ? gr : M - 1;
+        src = G + gr * ldg + n0 + ((e % CPR) ^ tr_swz<Cfg::GROW>(r)) * 8;
+      } else {
+        constexpr int CPR = Cfg::XROW / 16;
+        const int e = (i - Cfg::GINSTS) * 64 + lane;
+        const int r = e / CPR;
+        int64_t gr = m0 + r;
+        gr = gr < M ? gr : M - 1;
+        src = X + gr * ldx + c0 + ((e % CPR) ^ tr_swz<Cfg::XROW>(r)) * 8;
+      }
+      glds16(src, base + i * 1024);
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  stage(0);
+  if (NS == 3 && T > 1) stage(1);
+  for (int t = 0; t < T; ++t) {
+    // retire slice t (with NS = 3, slice t+1 stays in flight)
+    if (NS == 3) wait_vmcnt(t + 1 < T ? Cfg::LPW : 0);
+    else wait_vmcnt(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + NS - 1 < T) stage(t + NS - 1);
+    const char* Gs = smem + (t % Cfg::NS) * Cfg::STAGE;
+    const char* Xs = Gs + Cfg::GBYTES;
+    const int64_t m0 = mbeg + (int64_t)t * 64;
+    const bool tail = m0 + 64 > mend;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 gv[4], xv[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        gv[s] = tr_frag<Cfg::GROW>(Gs, kk * 32, wn * 64 + s * 16, lane);
+        xv[s] = tr_frag<Cfg::XROW>(Xs, kk * 32, wk * 64 + s * 16, lane);
+      }
+      if (tail) {  // rows past this split's end contribute nothing
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int64_t m = m0 + kk * 32 + 8 * (lane >> 4) + j;
+          if (m >= mend) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) gv[s][j] = 0;
+          }
+        }
+      }
+#pragma unroll
+      for (int ns = 0; ns < 4; ++ns)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+          acc[ns][ks] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gv[ns], xv[ks], acc[ns][ks], 0, 0, 0);
+    }
+  }
+  // D[i = n][j = c]: lane holds column c = .. + (lane&15), rows n = .. + 4*(lane>>4) + r
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int ns = 0; ns < 4; ++ns)
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int c = c0 + wk * 64 + ks * 16 + fr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wn * 64 + ns * 16 + fq * 4 + r;
+        atomicAdd(W + (int64_t)n * ldw + c, acc[ns][ks][r]);
+      }
+    }
+}
+
+template <int WN, int WK, int NS>
+void launch_tn(const uint16_t* G, int64_t ldg, const uint16_t* X, int64_t ldx, float* W, int64_t ldw, int64_t M,
+               int N, int K, int splits, hipStream_t stream) {
+  using Cfg = TnCfg<WN, WK, NS>;
+  const int tiles = (N / Cfg::BN) * (K / Cfg::BK);
+  if (splits <= 0) {
+    const int64_t target = 1024;
+    splits = (int)((target + tiles - 1) / tiles);
+  }
+  int64_t rows = (M + splits - 1) / splits;
+  rows = (rows + 63) / 64 * 64;
+  if (rows < 256) rows = 256;
+  const int64_t nsplit = (M + rows - 1) / rows;
+  dim3 grid((unsigned)(N / Cfg::BN), (unsigned)(K / Cfg::BK), (unsigned)nsplit);
+  static bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_kernel<WN, WK, NS>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS) == hipSuccess;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL((gemm_tn_kernel<WN, WK, NS>), grid, dim3(Cfg::THREADS), Cfg::LDS, stream, G, ldg, X, ldx, W, ldw,
+                     M, rows);
+}
+
+}  // namespace
+
+bool gemm_supported(int64_t N, int64_t K) { return N >= 64 && K >= 64 && N % 64 == 0 && K % 64 == 0; }
+
+void gemm_nt_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N,
+                  int K, int cfg, int max_blocks, hipStream_t stream) {
+  // cfg = tile + 10 * panel (1: resident, 2: streamed) + 100 * stages (1: two, 2: three); 0 digits = auto
+  const int bres = (cfg / 10) % 10 == 0 ? -1 : ((cfg / 10) % 10 == 1 ? 1 : 0);
+  const int ns = (cfg / 100) % 10 == 1 ? 2 : 3;
+  cfg %= 10;
+  auto a = static_cast<const uint16_t*>(A);
+  auto b = static_cast<const uint16_t*>(B);
+  auto c = static_cast<uint16_t*>(C);
+  if (cfg <= 0) cfg = N % 256 == 0 ? 3 : (N % 128 == 0 ? 2 : 1);
+  static const int cfg_bn[5] = {64, 64, 128, 256, 128};
+  if (cfg > 4 || N % cfg_bn[cfg] != 0) cfg = 1;   // the tile must divide N (B rows are not clamped)
+  switch (cfg) {
+    case 1: launch_nt_any<4, 1>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, stream); break;   // 256 x 64
+    case 2: launch_nt_any<4, 2>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, stream); break;   // 256 x 128
+    case 3: launch_nt_any<2, 4>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, stream); break;   // 128 x 256
+    case 4: launch_nt_any<2, 2>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, stream); break;   // 128 x 128
+    default: launch_nt_any<4, 1>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, stream); break;
+  }
+}
+
+template <int WN, int WK>
+void launch_tn_any(const uint16_t* G, int64_t ldg, const uint16_t* X, int64_t ldx, float* W, int64_t ldw, int64_t M,
+                   int N, int K, int splits, int ns, hipStream_t stream) {
+  if (ns == 3) launch_tn<WN, WK, 3>(G, ldg, X, ldx, W, ldw, M, N, K, splits, stream);
+  else launch_tn<WN, WK, 2>(G, ldg, X, ldx, W, ldw, M, N, K, splits, stream);
+}
+
+void gemm_tn_acc_f32(const void* G, int64_t ldg, const void* X, int64_t ldx, float* W, int64_t ldw, int64_t M,
+                     int N, int K, int cfg, int splits, hipStream_t stream) {
+  const int ns = (cfg / 10) % 10 == 2 ? 3 : 2;   // cfg = tile + 10 * (1: two stages, 2: three)
+  cfg %= 10;
+  auto g = static_cast<const uint16_t*>(G);
+  auto x = static_cast<const uint16_t*>(X);
+  if (cfg <= 0) {
+    const bool n2 = N % 128 == 0, k2 = K % 128 == 0;
+    cfg = n2 && k2 ? 4 : (n2 ? (N % 256 == 0 ? 5 : 2) : (k2 ? (K % 256 == 0 ? 6 : 3) : 1));
+  }
+  static const int cfg_bn[7] = {64, 64, 128, 64, 128, 256, 64};
+  static const int cfg_bk[7] = {64, 64, 64, 128, 128, 64, 256};
+  if (cfg > 6 || N % cfg_bn[cfg] != 0 || K % cfg_bk[cfg] != 0) cfg = 1;   // tiles must divide N and K
+  switch (cfg) {
+    case 1: launch_tn_any<1, 1>(g, ldg, x, ldx, W, ldw, M, N, K, splits, ns, stream); break;
+    case 2: launch_tn_any<2, 1>(g, ldg, x, ldx, W, ldw, M, N, K, splits, ns, stream); break;
+    case 3: launch_tn_any<1, 2>(g, ldg, x, ldx, W, ldw, M, N, K, splits, ns, stream); break;
+    case 4: launch_tn_any<2, 2>(g, ldg, x, ldx, W, ldw, M, N, K, splits, ns, stream); break;
+    case 5: launch_tn_any<4, 1>(g, ldg, x, ldx, W, ldw, M, N, K, splits, ns, stream); break;
+    case 6: launch_tn_any<1, 4>(g, ldg, x, ldx, W, ldw, M, N, K, splits, ns, stream); break;
+    default: launch_tn_any<1, 1>(g, ldg, x, ldx, W, ldw, M, N, K, splits, ns, stream); break;
+  }
+}
+
+}  // namespace gk

@@ -205,4 +205,18 @@ void bn_relu_pool_backward(const void* dy, const void* dy2, const uint8_t* amax,
                            int C, PoolGeo pg, int elem_bytes, const float* w, const float* mean, const float* invstd,
                            float* dgamma, float* dbeta, float* ws, float* gw_acc, float* gb_acc, hipStream_t stream);
 
+// ---------------------------------------------------------------------------
+// MFMA GEMMs for 1x1 convolutions over channels-last activations (gemm.hip).
+// bf16 operands, fp32 accumulation.  N, K multiples of 64 (gemm_supported).
+//   gemm_nt_bf16   : C[M, N] (bf16)  = A[M, K] . B[N, K]^T
+//   gemm_tn_acc_f32: W[N, K] (fp32) += G[M, N]^T . X[M, K]   (float atomics)
+// cfg <= 0 picks the tile shape from N (and K); max_blocks / splits <= 0
+// pick the grid.
+// ---------------------------------------------------------------------------
+bool gemm_supported(int64_t N, int64_t K);
+void gemm_nt_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N,
+                  int K, int cfg, int max_blocks, hipStream_t stream);
+void gemm_tn_acc_f32(const void* G, int64_t ldg, const void* X, int64_t ldx, float* W, int64_t ldw, int64_t M,
+                     int N, int K, int cfg, int splits, hipStream_t stream);
+
 }  // namespace gk

@@ -280,10 +280,17 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         gv = arena.grad_views[key]
         p = self._named_parameters[key]
 
-        def sink(grad):
+        def check():
             if p.grad is None or p.grad.data_ptr() != gv.data_ptr():
                 arena.check_grad(key, p)
+
+        def sink(grad):
+            check()
             ops.accum_grad_(gv, grad)
+        # kernels that accumulate into the arena themselves (ops/conv1x1.py)
+        # call check() and write grad_view directly
+        sink.grad_view = gv
+        sink.check = check
         return sink
 
     # ------------------------------------------------------------------

@@ -30,6 +30,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.bn import BNAct
+from ..ops.conv1x1 import Conv1x1
 
 
 class _ShadowWeight(torch.autograd.Function):
@@ -79,7 +80,17 @@ def install_bf16_shadow(model: nn.Module, opt) -> int:
     names = opt._parameter_names
     count = 0
     for mod in model.modules():
-        if isinstance(mod, (nn.Conv2d, nn.Linear)) and type(mod).forward in (nn.Conv2d.forward, nn.Linear.forward):
+        if isinstance(mod, Conv1x1):
+            # its own forward reads the shadow view and (GEMM path) adds the fp32
+            # weight gradient straight into the arena; other strides fall back
+            # to the plain shadow conv
+            p = mod.weight
+            if p in names:
+                key = names[p]
+                mod._gk_shadow = {"weight": (arena.view_of(shadow, key), opt._make_sink(key))}
+                mod._gk_slow = types.MethodType(_conv_forward, mod)
+                count += 1
+        elif isinstance(mod, (nn.Conv2d, nn.Linear)) and type(mod).forward in (nn.Conv2d.forward, nn.Linear.forward):
             table = {}
             for pname in ("weight", "bias"):
                 p = getattr(mod, pname, None)
