@@ -199,10 +199,15 @@ def main() -> int:
         "params": nparams,
         "final_loss": round(loss, 4) if loss == loss else None,
     }
+    if rank == 0 and os.environ.get("GKSGD_GEMM_SAVE"):
+        from gaussiank_sgd_amd.ops.conv1x1 import save_choices
+        save_choices(os.environ["GKSGD_GEMM_SAVE"])
     if rank == 0 and os.environ.get("GKSGD_GEMM_DUMP"):
-        from gaussiank_sgd_amd.ops.conv1x1 import tuned_choices
+        from gaussiank_sgd_amd.ops.conv1x1 import tuned_choices, tuning_log
+        log = tuning_log()
         with open(os.environ["GKSGD_GEMM_DUMP"], "w") as f:
-            json.dump([[list(k), list(v)] for k, v in tuned_choices().items()], f)
+            json.dump([[list(k), list(v), [[list(t), r] for t, r in log.get(k, [])]]
+                       for k, v in tuned_choices().items()], f)
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)

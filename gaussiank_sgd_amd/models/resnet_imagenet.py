@@ -21,15 +21,16 @@ import torch
 import torch.nn as nn
 
 from ..ops.bn import BNAct, global_avg_pool
-from ..ops.conv1x1 import Conv1x1
+from ..ops.conv1x1 import Conv1x1, Conv3x3
 
 
 def conv3x3(inp: int, out: int, stride: int = 1, groups: int = 1, dilation: int = 1) -> nn.Conv2d:
-    return nn.Conv2d(inp, out, 3, stride=stride, padding=dilation, groups=groups, bias=False, dilation=dilation)
+    # nn.Conv2d subclass: training runs the autotuned implicit-GEMM MFMA kernels (ops/conv1x1.py)
+    return Conv3x3(inp, out, stride, groups, dilation)
 
 
 def conv1x1(inp: int, out: int, stride: int = 1) -> nn.Conv2d:
-    # nn.Conv2d subclass: stride-1 training runs the autotuned MFMA GEMMs (ops/conv1x1.py)
+    # nn.Conv2d subclass: training runs the autotuned MFMA GEMMs (ops/conv1x1.py)
     return Conv1x1(inp, out, stride)
 
 

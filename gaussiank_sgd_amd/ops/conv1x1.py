@@ -1,24 +1,30 @@
-"""Stride-1 1x1 convolution on channels-last bf16 activations through the
-MFMA GEMMs of ``csrc/kernels/gemm.hip``, autotuned per shape against MIOpen.
+"""Convolutions on channels-last bf16 activations through the MFMA GEMMs of
+``csrc/kernels/gemm.hip``, autotuned per shape against MIOpen.
 
-A 1x1 convolution over NHWC data is a GEMM over the ``M = N*H*W`` pixel rows
-(forward ``Y = X W^T``, grad-input ``dX = dY W``, grad-weight
-``dW += dY^T X``).  For every distinct (direction, M, Cin, Cout) the first
-call times a small set of kernel configurations *and* the MIOpen
-convolution with HIP events and keeps the fastest (``GKSGD_GEMM_TUNE=0``
-skips the search and uses the heuristic default of the HIP kernel).  The
-grad-weight kernel adds its fp32 result straight into the optimizer's
+* 1x1, stride 1: a plain GEMM over the ``M = N*H*W`` pixel rows (forward
+  ``Y = X W^T``, grad-input ``dX = dY W``, grad-weight ``dW += dY^T X``).
+* KxK (and strided 1x1): implicit GEMM -- the A-operand rows are gathered
+  straight from the NHWC input per filter tap by the LDS-DMA loads (padding
+  reads a zero row), K = KH*KW*C tap-major like a channels-last weight.
+  Stride-1 grad-input is the forward convolution of dY with the flipped,
+  transposed weight; grad-weight is the transposed GEMM over gathered rows.
+
+For every distinct (direction, geometry) the first call times a small set of
+kernel configurations *and* the MIOpen convolution with HIP events and keeps
+the fastest (``GKSGD_GEMM_TUNE=0`` skips the search and uses the HIP
+kernel's heuristic default; ``GKSGD_FASTCONV=0`` disables the path).  The
+grad-weight kernels add their fp32 result straight into the optimizer's
 gradient arena (float atomics) when the module is on the bf16-shadow path
 (``parallel/shadow.py``), so no bf16 weight gradient is materialised.
 
-Reference parity: the reference's ResNets use ``nn.Conv2d(k=1)``
-(models/resnet.py / torchvision Bottleneck); ``Conv1x1`` is a drop-in
+Reference parity: the reference's ResNets use ``nn.Conv2d``
+(models/resnet.py / torchvision Bottleneck); ``FastConv2d`` is a drop-in
 ``nn.Conv2d`` subclass with identical parameters and state_dict keys.
 """
 from __future__ import annotations
 
 import os
-from typing import Callable, Dict, List, Optional, Tuple
+from typing import Callable, Dict, List, Tuple
 
 import torch
 import torch.nn as nn
@@ -28,14 +34,24 @@ from . import load
 
 _CL = torch.channels_last
 _TUNE = os.environ.get("GKSGD_GEMM_TUNE", "1") != "0"
+_ENABLED = os.environ.get("GKSGD_FASTCONV", "1") != "0"
 _choices: Dict[tuple, tuple] = {}
-# candidate kernel configurations (see gemm.hip: cfg digits = tile + 10*panel + 100*stages)
+_timings: Dict[tuple, list] = {}      # key -> [(tag, ms or error)] of the search
+# candidate kernel configurations (gemm.hip: cfg digits = tile + 10*panel + 100*stages)
 _NT_CFGS = [0, 1, 2, 3, 4, 11, 13, 21, 22, 23, 24, 111, 113, 121, 122, 123, 124]
-_TN_CFGS = [(c, s) for c in (0, 1, 2, 3, 4, 5, 6, 21, 24, 25) for s in (0, 64, 256)]
+_TN_CFGS = [(c, s) for c in (1, 2, 3, 4, 5, 6, 7, 8, 21, 22, 23, 24, 27) for s in (0, 128)]
+_zeros: Dict[torch.device, torch.Tensor] = {}
 
 
 def _g():
     return torch.ops.gksgd
+
+
+def _zero(dev: torch.device) -> torch.Tensor:
+    z = _zeros.get(dev)
+    if z is None:
+        z = _zeros[dev] = torch.zeros(256, dtype=torch.bfloat16, device=dev)
+    return z
 
 
 def _time(fn: Callable[[], None], reps: int = 5) -> float:
@@ -58,27 +74,63 @@ def _pick(key: tuple, cands: List[Tuple[tuple, Callable[[], None]]]) -> tuple:
     if not _TUNE or len(cands) == 1:
         _choices[key] = cands[0][0]
         return cands[0][0]
-    best, best_t = None, float("inf")
+    best, best_t = cands[-1][0], float("inf")
+    log = _timings.setdefault(key, [])
     for tag, fn in cands:
         try:
             t = _time(fn)
-        except RuntimeError:
+        except RuntimeError as e:
+            log.append((tag, "error: %s" % str(e).splitlines()[0][:200]))
             continue
+        log.append((tag, round(t, 4)))
         if t < best_t:
             best, best_t = tag, t
     _choices[key] = best
     return best
 
 
+def tuning_log() -> Dict[tuple, list]:
+    """Per key, every candidate's measured ms (or its error) from the search."""
+    return dict(_timings)
+
+
+def load_choices(path: str) -> int:
+    """Seed the autotune cache from a JSON file written by save_choices()."""
+    import json
+    try:
+        with open(path) as f:
+            rows = json.load(f)
+    except (OSError, ValueError):
+        return 0
+    for k, v in rows:
+        _choices.setdefault(tuple(k), tuple(v))
+    return len(rows)
+
+
+def save_choices(path: str) -> None:
+    import json
+    with open(path, "w") as f:
+        json.dump([[list(k), list(v)] for k, v in sorted(_choices.items(), key=str)], f, indent=0)
+
+
+_CACHE = os.environ.get("GKSGD_GEMM_CACHE", os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(
+    os.path.abspath(__file__)))), "tuning", "gemm_choices.json"))
+if _TUNE and _CACHE and os.path.exists(_CACHE) and os.environ.get("GKSGD_GEMM_RETUNE", "0") == "0":
+    load_choices(_CACHE)
+
+
 def tuned_choices() -> Dict[tuple, tuple]:
-    """(direction, M, Cin, Cout) -> chosen (impl, cfg, grid/splits)."""
+    """(direction, geometry...) -> chosen (impl, cfg, grid/splits)."""
     return dict(_choices)
 
 
 def supported(x: torch.Tensor, conv: nn.Conv2d) -> bool:
-    return (x.is_cuda and x.dim() == 4 and conv.stride == (1, 1) and conv.padding == (0, 0)
-            and conv.groups == 1 and conv.bias is None and x.is_contiguous(memory_format=_CL)
-            and conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0 and x.shape[0] * x.shape[2] * x.shape[3] > 0)
+    k = conv.kernel_size
+    return (_ENABLED and x.is_cuda and x.dim() == 4 and k[0] == k[1] and k[0] in (1, 3) and
+            conv.stride[0] == conv.stride[1] and conv.stride[0] in (1, 2) and
+            conv.padding == (k[0] // 2, k[0] // 2) and conv.dilation == (1, 1) and conv.groups == 1 and
+            conv.bias is None and conv.padding_mode == "zeros" and x.is_contiguous(memory_format=_CL) and
+            conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0 and x.numel() > 0)
 
 
 def _rows(t: torch.Tensor) -> torch.Tensor:
@@ -87,79 +139,105 @@ def _rows(t: torch.Tensor) -> torch.Tensor:
     return t.permute(0, 2, 3, 1).reshape(N * H * W, C)
 
 
-def _fwd(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    N, C, H, W = x.shape
-    K = w.shape[0]
-    M = N * H * W
-    y = torch.empty((N, K, H, W), dtype=torch.bfloat16, device=x.device, memory_format=_CL)
-    X, Y, Wm = _rows(x), _rows(y), w.reshape(K, C)
+def _geom(x_shape, w: torch.Tensor, s: int):
+    N, C, H, W = x_shape
+    K, k = w.shape[0], w.shape[2]
+    p = k // 2
+    OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    return N, C, H, W, K, k, p, OH, OW
+
+
+def _fwd(x: torch.Tensor, w: torch.Tensor, s: int) -> torch.Tensor:
+    N, C, H, W, K, k, p, OH, OW = _geom(x.shape, w, s)
+    y = torch.empty((N, K, OH, OW), dtype=torch.bfloat16, device=x.device, memory_format=_CL)
     g = _g()
-    cands = [(("hip", c, 0), (lambda c=c: g.gemm_nt(X, Wm, Y, c, 0))) for c in _NT_CFGS]
-    cands.append((("miopen", 0, 0), lambda: F.conv2d(x, w)))
-    ch = _pick(("fwd", M, C, K), cands)
+    if k == 1 and s == 1:
+        X, Y, Wm = _rows(x), _rows(y), w.reshape(K, C)
+        run = lambda c, mb: g.gemm_nt(X, Wm, Y, c, mb)  # noqa: E731
+    else:
+        z = _zero(x.device)
+        run = lambda c, mb: g.conv_nt(x, w, y, z, s, p, c, mb)  # noqa: E731
+    cands = [(("hip", c, 0), (lambda c=c: run(c, 0))) for c in _NT_CFGS]
+    cands.append((("miopen", 0, 0), lambda: F.conv2d(x, w, stride=s, padding=p)))
+    ch = _pick(("fwd", N, C, H, W, K, k, s), cands)
     if ch[0] == "miopen":
-        return F.conv2d(x, w).contiguous(memory_format=_CL)
-    g.gemm_nt(X, Wm, Y, ch[1], ch[2])
+        return F.conv2d(x, w, stride=s, padding=p).contiguous(memory_format=_CL)
+    run(ch[1], ch[2])
     return y
 
 
-def _dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape) -> torch.Tensor:
-    N, C, H, W = x_shape
-    K = w.shape[0]
-    M = N * H * W
-    dx = torch.empty((N, C, H, W), dtype=torch.bfloat16, device=dy.device, memory_format=_CL)
-    DY, DX = _rows(dy), _rows(dx)
-    Wt = w.reshape(K, C).t().contiguous()
+def _dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int) -> torch.Tensor:
+    N, C, H, W, K, k, p, OH, OW = _geom(x_shape, w, s)
     g = _g()
 
+    xs = torch.empty(x_shape, dtype=torch.bfloat16, device=dy.device, memory_format=_CL)   # shape only
+
     def miopen():
-        return torch.ops.aten.convolution_backward(dy, dx, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+        return torch.ops.aten.convolution_backward(dy, xs, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
                                                    [True, False, False])[0]
-    cands = [(("hip", c, 0), (lambda c=c: g.gemm_nt(DY, Wt, DX, c, 0))) for c in _NT_CFGS]
+    cands = []
+    dx = None
+    if s == 1:
+        dx = xs
+        if k == 1:
+            DY, DX = _rows(dy), _rows(dx)
+            Wt = w.reshape(K, C).t().contiguous()
+            run = lambda c: g.gemm_nt(DY, Wt, DX, c, 0)  # noqa: E731
+        else:
+            # dX = conv(dY, W') with W'[c][kh][kw][k] = W[k][KH-1-kh][KW-1-kw][c]
+            wf = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=_CL)
+            z = _zero(dy.device)
+            run = lambda c: g.conv_nt(dy, wf, dx, z, 1, p, c, 0)  # noqa: E731
+        cands = [(("hip", c, 0), (lambda c=c: run(c))) for c in _NT_CFGS]
     cands.append((("miopen", 0, 0), miopen))
-    ch = _pick(("dgrad", M, C, K), cands)
+    ch = _pick(("dgrad", N, C, H, W, K, k, s), cands)
     if ch[0] == "miopen":
         return miopen().contiguous(memory_format=_CL)
-    g.gemm_nt(DY, Wt, DX, ch[1], ch[2])
+    run(ch[1])
     return dx
 
 
-def _wgrad_into(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, out_f32: torch.Tensor) -> None:
-    """out_f32[K, C] += dW (fp32)."""
-    N, C, H, W = x.shape
-    K = w.shape[0]
-    M = N * H * W
-    DY, X = _rows(dy), _rows(x)
+def _wgrad_into(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, s: int, out_f32: torch.Tensor) -> None:
+    """out_f32 ([K, C, k, k] channels-last fp32) += dW."""
+    N, C, H, W, K, k, p, OH, OW = _geom(x.shape, w, s)
     g = _g()
-    scratch = torch.zeros(K, C, dtype=torch.float32, device=x.device)
+    key = ("wgrad", N, C, H, W, K, k, s)
+    scratch = torch.zeros_like(out_f32) if key not in _choices else None
 
     def miopen():
-        return torch.ops.aten.convolution_backward(dy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+        return torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
                                                    [False, True, False])[1]
-    cands = [(("hip", c, s), (lambda c=c, s=s: g.gemm_tn_acc(DY, X, scratch, c, s))) for c, s in _TN_CFGS]
+    if k == 1 and s == 1:
+        DY, X = _rows(dy), _rows(x)
+        run = lambda o, c, sp: g.gemm_tn_acc(DY, X, o.view(K, C), c, sp)  # noqa: E731
+    else:
+        z = _zero(x.device)
+        run = lambda o, c, sp: g.conv_tn_acc(dy, x, o, z, s, p, c, sp)  # noqa: E731
+    cands = [(("hip", c, sp), (lambda c=c, sp=sp: run(scratch, c, sp))) for c, sp in _TN_CFGS]
     cands.append((("miopen", 0, 0), miopen))
-    ch = _pick(("wgrad", M, C, K), cands)
+    ch = _pick(key, cands)
     if ch[0] == "miopen":
         from . import accum_grad_
-        accum_grad_(out_f32, miopen().reshape(K, C))
+        accum_grad_(out_f32, miopen().contiguous(memory_format=_CL))
         return
-    g.gemm_tn_acc(DY, X, out_f32, ch[1], ch[2])
+    run(out_f32, ch[1], ch[2])
 
 
-class _Conv1x1Fn(torch.autograd.Function):
-    """y = conv1x1(x, w_bf16).  ``param`` is the fp32 master weight; with a
+class _FastConvFn(torch.autograd.Function):
+    """y = conv(x, w_bf16).  ``param`` is the fp32 master weight; with a
     ``sink`` (bf16-shadow path) its gradient is added into the optimizer's
     fp32 arena in the backward and None is returned for it."""
 
     @staticmethod
-    def forward(ctx, x, param, w_bf16, sink):
+    def forward(ctx, x, param, w_bf16, sink, stride):
         if x.dtype != torch.bfloat16:
             x = x.to(torch.bfloat16)
         x = x.contiguous(memory_format=_CL)
         w = w_bf16 if w_bf16 is not None else param.detach().to(torch.bfloat16)
         w = w.contiguous(memory_format=_CL)
-        y = _fwd(x, w)
+        y = _fwd(x, w, stride)
         ctx.sink = sink
+        ctx.stride = stride
         ctx.param_dtype = param.dtype
         ctx.save_for_backward(x, w)
         return y
@@ -167,28 +245,30 @@ class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
+        s = ctx.stride
         dy = dy.to(torch.bfloat16).contiguous(memory_format=_CL)
-        dx = _dgrad(dy, w, x.shape) if ctx.needs_input_grad[0] else None
+        dx = _dgrad(dy, w, x.shape, s) if ctx.needs_input_grad[0] else None
         gparam = None
         if ctx.needs_input_grad[1]:
-            K, C = w.shape[0], w.shape[1]
             sink = ctx.sink
-            if sink is not None and getattr(sink, "grad_view", None) is not None:
+            if sink is not None and getattr(sink, "grad_view", None) is not None and \
+                    sink.grad_view.is_contiguous(memory_format=_CL):
                 sink.check()
-                _wgrad_into(dy, x, w, sink.grad_view.view(K, C))
+                _wgrad_into(dy, x, w, s, sink.grad_view)
             else:
-                out = torch.zeros(K, C, dtype=torch.float32, device=x.device)
-                _wgrad_into(dy, x, w, out)
-                gparam = out.view(K, C, 1, 1).to(ctx.param_dtype)
-        return dx, gparam, None, None
+                out = torch.zeros(w.shape, dtype=torch.float32, device=x.device).contiguous(memory_format=_CL)
+                _wgrad_into(dy, x, w, s, out)
+                if sink is not None:
+                    sink(out)
+                else:
+                    gparam = out.to(ctx.param_dtype)
+        return dx, gparam, None, None, None
 
 
-class Conv1x1(nn.Conv2d):
-    """``nn.Conv2d(in, out, 1, stride, bias=False)`` whose stride-1 training
-    path on a GPU runs the autotuned MFMA GEMMs (bf16 compute, as autocast)."""
-
-    def __init__(self, inp: int, out: int, stride: int = 1):
-        super().__init__(inp, out, 1, stride=stride, bias=False)
+class FastConv2d(nn.Conv2d):
+    """``nn.Conv2d`` whose bias-free 1x1 / 3x3 (stride 1 or 2, 'same'
+    padding) training path on a GPU runs the autotuned MFMA kernels (bf16
+    compute, as autocast); everything else is the stock convolution."""
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         dev = x.device.type
@@ -201,6 +281,21 @@ class Conv1x1(nn.Conv2d):
             w_bf16, sink = (info[0], info[1]) if use_shadow else (None, None)
             if not torch.is_grad_enabled() or not self.weight.requires_grad:
                 sink = None
-            return _Conv1x1Fn.apply(x, self.weight, w_bf16, sink)
+            return _FastConvFn.apply(x, self.weight, w_bf16, sink, self.stride[0])
         slow = getattr(self, "_gk_slow", None)
         return slow(x) if slow is not None else super().forward(x)
+
+
+class Conv1x1(FastConv2d):
+    """``nn.Conv2d(in, out, 1, stride, bias=False)``."""
+
+    def __init__(self, inp: int, out: int, stride: int = 1):
+        super().__init__(inp, out, 1, stride=stride, bias=False)
+
+
+class Conv3x3(FastConv2d):
+    """``nn.Conv2d(in, out, 3, stride, padding=1, bias=False)``."""
+
+    def __init__(self, inp: int, out: int, stride: int = 1, groups: int = 1, dilation: int = 1):
+        super().__init__(inp, out, 3, stride=stride, padding=dilation, groups=groups, bias=False,
+                         dilation=dilation)

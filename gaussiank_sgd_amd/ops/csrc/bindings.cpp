@@ -600,6 +600,63 @@ void gemm_tn_acc(at::Tensor G, at::Tensor X, at::Tensor W, int64_t cfg, int64_t 
                       (int)N, (int)K, (int)cfg, (int)splits, cur_stream(G));
 }
 
+// implicit-GEMM convolution over NHWC bf16 (x: [N, C, H, W] channels-last,
+// w: [Cout, C, KH, KW] channels-last, y: [N, Cout, OH, OW] channels-last)
+void check_conv(const at::Tensor& x, const at::Tensor& w, const at::Tensor& zero) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv: x must be a channels-last bf16 GPU tensor");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 &&
+                  w.is_contiguous(at::MemoryFormat::ChannelsLast) && w.size(1) == x.size(1),
+              "conv: w must be a channels-last bf16 [Cout, C, KH, KW] GPU tensor");
+  TORCH_CHECK(x.size(1) % 64 == 0 && w.size(0) % 64 == 0, "conv: C and Cout must be multiples of 64");
+  TORCH_CHECK(zero.is_cuda() && zero.scalar_type() == at::kBFloat16 && zero.numel() >= 64 && zero.is_contiguous(),
+              "conv: zero must hold >= 64 bf16");
+}
+
+void conv_nt(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor zero, int64_t stride, int64_t pad, int64_t cfg,
+             int64_t max_blocks) {
+  check_conv(x, w, zero);
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t Co = w.size(0), KH = w.size(2), KW = w.size(3);
+  const int64_t OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
+  TORCH_CHECK(y.is_cuda() && y.scalar_type() == at::kBFloat16 && y.dim() == 4 &&
+                  y.is_contiguous(at::MemoryFormat::ChannelsLast) && y.size(0) == N && y.size(1) == Co &&
+                  y.size(2) == OH && y.size(3) == OW,
+              "conv_nt: y must be channels-last bf16 [N, Cout, OH, OW]");
+  const int64_t M = N * OH * OW;
+  TORCH_CHECK(M > 0 && M < (int64_t(1) << 32), "conv_nt: M out of range");
+  c10::DeviceGuard guard(x.device());
+  gk::conv_nt_bf16(x.data_ptr(), zero.data_ptr(), (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)stride, (int)pad,
+                   (int)KH, (int)KW, w.data_ptr(), y.data_ptr(), M, (int)Co, (int)cfg, (int)max_blocks, cur_stream(x));
+}
+
+// wout: fp32 [Cout, C, KH, KW] channels-last (memory [Cout][KH][KW][C]); += dW
+void conv_tn_acc(at::Tensor dy, at::Tensor x, at::Tensor wout, at::Tensor zero, int64_t stride, int64_t pad,
+                 int64_t cfg, int64_t splits) {
+  TORCH_CHECK(wout.is_cuda() && wout.scalar_type() == at::kFloat && wout.dim() == 4 &&
+                  wout.is_contiguous(at::MemoryFormat::ChannelsLast) && wout.size(1) == x.size(1),
+              "conv_tn_acc: wout must be a channels-last fp32 [Cout, C, KH, KW] tensor");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t Co = wout.size(0), KH = wout.size(2), KW = wout.size(3);
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  C % 64 == 0 && Co % 64 == 0,
+              "conv_tn_acc: x must be channels-last bf16 with C, Cout % 64 == 0");
+  TORCH_CHECK(zero.is_cuda() && zero.scalar_type() == at::kBFloat16 && zero.numel() >= 64, "conv_tn_acc: zero");
+  const int64_t OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
+  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 &&
+                  dy.is_contiguous(at::MemoryFormat::ChannelsLast) && dy.size(0) == N && dy.size(1) == Co &&
+                  dy.size(2) == OH && dy.size(3) == OW,
+              "conv_tn_acc: dy must be channels-last bf16 [N, Cout, OH, OW]");
+  const int64_t M = N * OH * OW;
+  TORCH_CHECK(M < (int64_t(1) << 32), "conv_tn_acc: M out of range");
+  if (M == 0) return;
+  c10::DeviceGuard guard(x.device());
+  gk::conv_tn_acc_f32(dy.data_ptr(), x.data_ptr(), zero.data_ptr(), (int)H, (int)W, (int)C, (int)OH, (int)OW,
+                      (int)stride, (int)pad, (int)KH, (int)KW, wout.data_ptr<float>(), M, (int)Co, (int)cfg,
+                      (int)splits, cur_stream(x));
+}
+
 }  // namespace
 
 
@@ -654,6 +711,8 @@ TORCH_LIBRARY(gksgd, m) {
   m.def("gemm_supported(int N, int K) -> bool", &gemm_supported);
   m.def("gemm_nt(Tensor A, Tensor B, Tensor(a!) C, int cfg=0, int max_blocks=0) -> ()");
   m.def("gemm_tn_acc(Tensor G, Tensor X, Tensor(a!) W, int cfg=0, int splits=0) -> ()");
+  m.def("conv_nt(Tensor x, Tensor w, Tensor(a!) y, Tensor zero, int stride, int pad, int cfg=0, int max_blocks=0) -> ()");
+  m.def("conv_tn_acc(Tensor dy, Tensor x, Tensor(a!) wout, Tensor zero, int stride, int pad, int cfg=0, int splits=0) -> ()");
 
   m.class_<RcclEngine>("RcclEngine")
       .def(torch::init<>())
@@ -690,4 +749,6 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("cast_bf16", &cast_bf16);
   m.impl("gemm_nt", &gemm_nt);
   m.impl("gemm_tn_acc", &gemm_tn_acc);
+  m.impl("conv_nt", &conv_nt);
+  m.impl("conv_tn_acc", &conv_tn_acc);
 }

@@ -73,6 +73,29 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 #undef GK_VMW
 }
 
+// Implicit-GEMM convolution: row m of the A operand is output pixel
+// (n, oh, ow) and K slice k0 (64 channels) is tap (kh, kw) of input channels
+// c0..c0+63 (K = KH*KW*C, tap-major, matching a channels-last [Cout][KH][KW][C]
+// weight).  Out-of-image taps read a zero row (padding) -- LDS-DMA cannot write
+// zeros itself.
+struct ConvGeo {
+  const uint16_t* zero;   // >= 64 zero bf16
+  int H, W, C, OH, OW, S, P, KW;
+};
+
+__device__ __forceinline__ const uint16_t* conv_row(const uint16_t* X, const ConvGeo& g, int64_t m, int k0,
+                                                    int chunk) {
+  const int tap = k0 / g.C, c0 = k0 - tap * g.C;
+  const int kh = tap / g.KW, kw = tap - kh * g.KW;
+  const uint32_t ohw = (uint32_t)(g.OH * g.OW);
+  const uint32_t mu = (uint32_t)m;
+  const uint32_t n = mu / ohw, rem = mu - n * ohw;
+  const uint32_t oh = rem / (uint32_t)g.OW, ow = rem - oh * (uint32_t)g.OW;
+  const int ih = (int)oh * g.S - g.P + kh, iw = (int)ow * g.S - g.P + kw;
+  if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W) return g.zero + chunk * 8;
+  return X + (((int64_t)n * g.H + ih) * g.W + iw) * g.C + c0 + chunk * 8;
+}
+
 // --------------------------------------------------------------------------
 // gemm_nt
 // --------------------------------------------------------------------------
@@ -97,12 +120,13 @@ struct NtCfg {
   static int lds_bytes(int K, int ns) { return ns * STAGE + (BRES ? BN * K * 2 : 0); }
 };
 
-template <int WM, int WN, bool BRES, int NS>
+template <int WM, int WN, bool BRES, int NS, bool GATHER>
 __global__ void __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(WM * WN >= 8 ? 1 : 2)))
 gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
-               uint16_t* __restrict__ C, int64_t ldc, int64_t M, int K) {
+               uint16_t* __restrict__ C, int64_t ldc, int64_t M, int K, ConvGeo geo) {
   using Cfg = NtCfg<WM, WN, BRES>;
   static_assert(NS == 2 || NS == 3, "stages");
+  constexpr int LPW = Cfg::LPW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -112,7 +136,7 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
   const int nk = K >> 6;
   // this block's work: M tiles blockIdx.x, +gridDim.x, ...; each has nk K slices
   const int64_t my_tiles = blockIdx.x < mtiles ? (mtiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
-  const int64_t T = my_tiles * nk;
+  const int T = (int)(my_tiles * nk);
   if (T == 0) return;
   char* stage_base = smem + (BRES ? Cfg::BN * K * 2 : 0);
 
@@ -126,25 +150,85 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
     }
   }
 
-  auto stage = [&](int64_t t) {
-    const int64_t mt = blockIdx.x + (t / nk) * gridDim.x;
-    const int k0 = (int)(t % nk) << 6;
-    const int64_t m0 = mt * Cfg::BM;
-    GK_LDS char* base = (GK_LDS char*)stage_base + (int)(t % NS) * Cfg::STAGE;
+  // ---- staging cursor: every per-lane address is set up once per M tile (A
+  // rows) or once per kernel (B rows); a K step only adds the slice offset.
+  // Instruction j of this wave fills staged rows i*8 .. i*8+7, i = wave + j*NW:
+  // A rows while i*8 < BM, B rows after (streamed panel only).
+  const uint16_t* ptr[LPW];   // A: row (or gathered pixel) base + chunk; B: row base + chunk
+  int ih0[LPW], iw0[LPW];     // gather: input position of tap (0, 0)
 #pragma unroll
-    for (int j = 0; j < Cfg::LPW; ++j) {
+  for (int j = 0; j < LPW; ++j) {
+    const int i = wave + j * Cfg::NW;
+    const int r = i * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ swz(r);
+    ptr[j] = (BRES || i * 8 < Cfg::BM) ? nullptr : B + (int64_t)(n0 + r - Cfg::BM) * ldb + c * 8;
+    ih0[j] = iw0[j] = 0;
+  }
+  auto set_rows = [&](int64_t mt) {
+    const int64_t m0 = mt * Cfg::BM;
+#pragma unroll
+    for (int j = 0; j < LPW; ++j) {
       const int i = wave + j * Cfg::NW;
-      const int r = i * 8 + (lane >> 3);
-      const int c = (lane & 7) ^ swz(r);
-      const uint16_t* src;
       if (BRES || i * 8 < Cfg::BM) {
+        const int r = i * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ swz(r);
         int64_t gr = m0 + r;
         gr = gr < M ? gr : M - 1;
-        src = A + gr * lda + k0 + c * 8;
+        if (GATHER) {
+          const uint32_t ohw = (uint32_t)(geo.OH * geo.OW);
+          const uint32_t mu = (uint32_t)gr;
+          const uint32_t n = mu / ohw, rem = mu - n * ohw;
+          const uint32_t oh = rem / (uint32_t)geo.OW, ow = rem - oh * (uint32_t)geo.OW;
+          ih0[j] = (int)oh * geo.S - geo.P;
+          iw0[j] = (int)ow * geo.S - geo.P;
+          ptr[j] = A + (((int64_t)n * geo.H + ih0[j]) * geo.W + iw0[j]) * geo.C + c * 8;
+        } else {
+          ptr[j] = A + gr * lda + c * 8;
+        }
+      }
+    }
+  };
+  int64_t s_mt = blockIdx.x;    // tile of the next stage to issue
+  int s_ks = 0;                 // its K slice
+  int s_kh = 0, s_kw = 0, s_c0 = 0;   // gather: tap and channel offset of that slice
+  int s_t = 0;
+  int s_buf = 0;                // LDS stage of the next issue (s_t % NS)
+  set_rows(s_mt);
+  auto stage = [&]() {
+    GK_LDS char* base = (GK_LDS char*)stage_base + s_buf * Cfg::STAGE;
+    const int k0 = s_ks << 6;
+#pragma unroll
+    for (int j = 0; j < LPW; ++j) {
+      const int i = wave + j * Cfg::NW;
+      const uint16_t* src;
+      if (BRES || i * 8 < Cfg::BM) {
+        if (GATHER) {
+          const int ih = ih0[j] + s_kh, iw = iw0[j] + s_kw;
+          const bool ok = (unsigned)ih < (unsigned)geo.H && (unsigned)iw < (unsigned)geo.W;
+          const int c = (lane & 7) ^ swz(i * 8 + (lane >> 3));
+          src = ok ? ptr[j] + (int64_t)(s_kh * geo.W + s_kw) * geo.C + s_c0 : geo.zero + c * 8;
+        } else {
+          src = ptr[j] + k0;
+        }
       } else {
-        src = B + (int64_t)(n0 + r - Cfg::BM) * ldb + k0 + c * 8;
+        src = ptr[j] + k0;
       }
       glds16(src, base + i * 1024);
+    }
+    ++s_t;
+    s_buf = s_buf + 1 == NS ? 0 : s_buf + 1;
+    if (GATHER) {
+      s_c0 += 64;
+      if (s_c0 == geo.C) {
+        s_c0 = 0;
+        if (++s_kw == geo.KW) { s_kw = 0; ++s_kh; }
+      }
+    }
+    if (++s_ks == nk) {
+      s_ks = 0;
+      s_kh = s_kw = s_c0 = 0;
+      s_mt += gridDim.x;
+      if (s_t < T) set_rows(s_mt);
     }
   };
 
@@ -154,22 +238,25 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  stage(0);
-  if (NS == 3 && T > 1) stage(1);
+  stage();
+  if (NS == 3 && T > 1) stage();
   const int fr = lane & 15, fq = lane >> 4;
   // stores issued by the last two steps (0 when none, or when a partial tile
   // drained its stores with vmcnt(0) right away)
   int st1 = 0, st2 = 0;
-  for (int64_t t = 0; t < T; ++t) {
+  int ks = 0;
+  int buf = 0;
+  int64_t mt = blockIdx.x;
+  for (int t = 0; t < T; ++t) {
     // ops issued after stage(t), in order: NS=2: stores(t-1);
     // NS=3: stores(t-2), stage(t+1), stores(t-1).  Retire stage(t) only.
     if (NS == 2) wait_vmcnt(st1);
-    else wait_vmcnt(st2 + (t + 1 < T ? Cfg::LPW : 0) + st1);
+    else wait_vmcnt(st2 + (t + 1 < T ? LPW : 0) + st1);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (t + NS - 1 < T) stage(t + NS - 1);
-    const int ks = (int)(t % nk);
-    const char* As = stage_base + (int)(t % NS) * Cfg::STAGE;
+    if (s_t < T) stage();
+    const char* As = stage_base + buf * Cfg::STAGE;
+    buf = buf + 1 == NS ? 0 : buf + 1;
     const char* Bs = BRES ? smem + ks * Cfg::BSTAGE : As + Cfg::ASTAGE;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -190,12 +277,13 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
     }
     st2 = st1;
     st1 = 0;
-    if (ks == nk - 1) {
+    if (++ks == nk) {
+      ks = 0;
       // lane holds C[m = fr][n = 4*fq + r] of every 16x16 subtile.  Lanes fq and
       // fq^1 swap halves of the subtile pair (2p, 2p+1) so each lane owns 8
       // consecutive channels: one 16-byte store per lane per pair.
-      const int64_t mt = blockIdx.x + (t / nk) * gridDim.x;
       const int64_t mbase = mt * Cfg::BM;
+      mt += gridDim.x;
       const bool full = mbase + Cfg::BM <= M;
       const bool odd = fq & 1;
 #pragma unroll
@@ -221,9 +309,9 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
   }
 }
 
-template <int WM, int WN, bool BRES, int NS>
+template <int WM, int WN, bool BRES, int NS, bool GATHER>
 void launch_nt(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, uint16_t* C, int64_t ldc, int64_t M,
-               int N, int K, int max_blocks, hipStream_t stream) {
+               int N, int K, int max_blocks, const ConvGeo& geo, hipStream_t stream) {
   using Cfg = NtCfg<WM, WN, BRES>;
   const int ntiles = N / Cfg::BN;
   const int64_t mtiles = (M + Cfg::BM - 1) / Cfg::BM;
@@ -235,50 +323,64 @@ void launch_nt(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, u
   if (gx > mtiles) gx = mtiles;
   dim3 grid((unsigned)gx, (unsigned)ntiles);
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<WM, WN, BRES, NS>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<WM, WN, BRES, NS, GATHER>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL((gemm_nt_kernel<WM, WN, BRES, NS>), grid, dim3(Cfg::THREADS), lds, stream, A, lda, B, ldb, C,
-                     ldc, M, K);
+  hipLaunchKernelGGL((gemm_nt_kernel<WM, WN, BRES, NS, GATHER>), grid, dim3(Cfg::THREADS), lds, stream, A, lda, B,
+                     ldb, C, ldc, M, K, geo);
 }
 
-template <int WM, int WN>
+template <int WM, int WN, bool GATHER>
 void launch_nt_any(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, uint16_t* C, int64_t ldc,
-                   int64_t M, int N, int K, int max_blocks, int bres, int ns, hipStream_t stream) {
+                   int64_t M, int N, int K, int max_blocks, int bres, int ns, const ConvGeo& geo, hipStream_t stream) {
   // keep the weight panel resident when it fits next to the two A stages
   if (bres < 0) bres = (64 * WN) * K * 2 <= 64 * 1024;
   if (bres && NtCfg<WM, WN, true>::lds_bytes(K, 2) > 160 * 1024) bres = 0;
   constexpr int L = 160 * 1024;
   if (bres) {
-    if (ns != 2 && NtCfg<WM, WN, true>::lds_bytes(K, 3) <= L) launch_nt<WM, WN, true, 3>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, stream);
-    else launch_nt<WM, WN, true, 2>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, stream);
+    if (ns != 2 && NtCfg<WM, WN, true>::lds_bytes(K, 3) <= L) launch_nt<WM, WN, true, 3, GATHER>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stream);
+    else launch_nt<WM, WN, true, 2, GATHER>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stream);
   } else {
-    if (ns != 2 && NtCfg<WM, WN, false>::lds_bytes(K, 3) <= L) launch_nt<WM, WN, false, 3>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, stream);
-    else launch_nt<WM, WN, false, 2>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, stream);
+    if (ns != 2 && NtCfg<WM, WN, false>::lds_bytes(K, 3) <= L) launch_nt<WM, WN, false, 3, GATHER>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stream);
+    else launch_nt<WM, WN, false, 2, GATHER>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stream);
   }
 }
 
 // --------------------------------------------------------------------------
 // gemm_tn: W[N, K] += G[M, N]^T . X[M, K]
 // --------------------------------------------------------------------------
-template <int WN, int WK, int NS_ = 2>
+// WS waves split the 64*WS pixel rows of a stage for the same output tile;
+// their partial sums are combined through LDS before the atomics.
+template <int WN, int WK, int WS, int NS_>
 struct TnCfg {
-  static constexpr int NW = WN * WK;
+  static constexpr int NW = WN * WK * WS;
   static constexpr int THREADS = 64 * NW;
   static constexpr int BN = 64 * WN;                 // output rows (G columns)
   static constexpr int BK = 64 * WK;                 // output cols (X columns)
+  static constexpr int ROWS = 64 * WS;               // pixel rows per stage
   static constexpr int GROW = BN * 2;                // bytes per staged G row
   static constexpr int XROW = BK * 2;
-  static constexpr int GBYTES = 64 * GROW;           // 64 pixel rows per stage
-  static constexpr int STAGE = 64 * (GROW + XROW);
+  static constexpr int GBYTES = ROWS * GROW;
+  static constexpr int STAGE = ROWS * (GROW + XROW);
   static constexpr int NS = NS_;                     // LDS stages (3: two slices in flight)
   static constexpr int LDS = NS * STAGE;
   static constexpr int GINSTS = GBYTES / 1024;
   static constexpr int INSTS = STAGE / 1024;
   static_assert(INSTS % NW == 0, "stage split");
   static constexpr int LPW = INSTS / NW;
+  static_assert(LPW <= 40, "wait_vmcnt range");
+  static_assert((WS - 1) * WN * WK * 16384 <= LDS, "reduction scratch");
 };
+
+// a / d for small a (< 2^22): float reciprocal, one correction step
+__device__ __forceinline__ uint32_t udiv_small(uint32_t a, uint32_t d, float rcp) {
+  uint32_t q = (uint32_t)((float)a * rcp);
+  const int32_t r = (int32_t)(a - q * d);
+  if (r < 0) --q;
+  else if (r >= (int32_t)d) ++q;
+  return q;
+}
 
 // LDS image of a [64 rows][RB bytes] tile for transposed reads: 16-byte chunk
 // c of row r is stored at chunk c ^ tr_swz(r).  A ds_read_b64_tr_b16 half-wave
@@ -306,44 +408,90 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* tile, int r0, int c0, int 
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-template <int WN, int WK, int NS>
-__global__ void __launch_bounds__(64 * WN * WK) __attribute__((amdgpu_waves_per_eu(2)))
+template <int WN, int WK, int WS, int NS, bool GATHER>
+__global__ void __launch_bounds__(64 * WN * WK * WS) __attribute__((amdgpu_waves_per_eu(2)))
 gemm_tn_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __restrict__ X, int64_t ldx,
-               float* __restrict__ W, int64_t ldw, int64_t M, int64_t rows_per_split) {
-  using Cfg = TnCfg<WN, WK, NS>;
+               float* __restrict__ W, int64_t ldw, int64_t M, int64_t rows_per_split, ConvGeo geo) {
+  using Cfg = TnCfg<WN, WK, WS, NS>;
+  constexpr int LPW = Cfg::LPW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int wn = wave / WK, wk = wave % WK;
+  const int wk = wave % WK, wn = (wave / WK) % WN, ws = wave / (WK * WN);
   const int n0 = blockIdx.x * Cfg::BN;
   const int c0 = blockIdx.y * Cfg::BK;
   const int64_t mbeg = (int64_t)blockIdx.z * rows_per_split;
   int64_t mend = mbeg + rows_per_split;
   if (mend > M) mend = M;
   if (mbeg >= mend) return;
-  const int T = (int)((mend - mbeg + 63) >> 6);
+  const int T = (int)((mend - mbeg + Cfg::ROWS - 1) / Cfg::ROWS);
+
+  // per-lane staging setup (constant over stages): staged row, global column offset
+  int srow[LPW];
+  int64_t scol[LPW];
+  int dkh[LPW], dkw[LPW];
+#pragma unroll
+  for (int j = 0; j < LPW; ++j) {
+    const int i = wave + j * Cfg::NW;
+    dkh[j] = dkw[j] = 0;
+    if (i < Cfg::GINSTS) {
+      constexpr int CPR = Cfg::GROW / 16;
+      const int e = i * 64 + lane;
+      srow[j] = e / CPR;
+      scol[j] = n0 + ((e % CPR) ^ tr_swz<Cfg::GROW>(srow[j])) * 8;
+    } else {
+      constexpr int CPR = Cfg::XROW / 16;
+      const int e = (i - Cfg::GINSTS) * 64 + lane;
+      srow[j] = e / CPR;
+      const int ch = (e % CPR) ^ tr_swz<Cfg::XROW>(srow[j]);
+      if (GATHER) {
+        const int k0 = c0 + (ch >> 3) * 64;          // 64-channel slice of one tap
+        const int tap = k0 / geo.C;
+        dkh[j] = tap / geo.KW;
+        dkw[j] = tap - dkh[j] * geo.KW;
+        scol[j] = (k0 - tap * geo.C) + (ch & 7) * 8;
+      } else {
+        scol[j] = c0 + ch * 8;
+      }
+    }
+  }
+  const float rcp_ow = GATHER ? 1.0f / (float)geo.OW : 0.f;
+  const float rcp_oh = GATHER ? 1.0f / (float)geo.OH : 0.f;
 
   auto stage = [&](int t) {
-    const int64_t m0 = mbeg + (int64_t)t * 64;
-    GK_LDS char* base = (GK_LDS char*)smem + (t % Cfg::NS) * Cfg::STAGE;
+    const int64_t m0 = mbeg + (int64_t)t * Cfg::ROWS;
+    GK_LDS char* base = (GK_LDS char*)smem + (t % NS) * Cfg::STAGE;
+    uint32_t n_s = 0, oh_s = 0, ow_s = 0;
+    if (GATHER) {   // pixel of the stage's first row (wave-uniform)
+      const uint32_t ohw = (uint32_t)(geo.OH * geo.OW);
+      const uint32_t mu = (uint32_t)m0;
+      n_s = mu / ohw;
+      const uint32_t rem = mu - n_s * ohw;
+      oh_s = rem / (uint32_t)geo.OW;
+      ow_s = rem - oh_s * (uint32_t)geo.OW;
+    }
 #pragma unroll
-    for (int j = 0; j < Cfg::INSTS / Cfg::NW; ++j) {
+    for (int j = 0; j < LPW; ++j) {
       const int i = wave + j * Cfg::NW;
+      int64_t gr = m0 + srow[j];
+      const bool in = gr < M;
+      gr = in ? gr : M - 1;
       const uint16_t* src;
       if (i < Cfg::GINSTS) {
-        constexpr int CPR = Cfg::GROW / 16;               // 16-byte chunks per row
-        const int e = i * 64 + lane;
-        const int r = e / CPR;
-        int64_t gr = m0 + r;
-        gr = gr < M ? gr : M - 1;
-        src = G + gr * ldg + n0 + ((e % CPR) ^ tr_swz<Cfg::GROW>(r)) * 8;
+        src = G + gr * ldg + scol[j];
+      } else if (GATHER) {
+        const uint32_t idx = ow_s + (uint32_t)srow[j];
+        const uint32_t q1 = udiv_small(idx, (uint32_t)geo.OW, rcp_ow);
+        const uint32_t ow = idx - q1 * (uint32_t)geo.OW;
+        const uint32_t t2 = oh_s + q1;
+        const uint32_t q2 = udiv_small(t2, (uint32_t)geo.OH, rcp_oh);
+        const uint32_t oh = t2 - q2 * (uint32_t)geo.OH;
+        const uint32_t n = n_s + q2;
+        const int ih = (int)oh * geo.S - geo.P + dkh[j], iw = (int)ow * geo.S - geo.P + dkw[j];
+        const bool ok = in && (unsigned)ih < (unsigned)geo.H && (unsigned)iw < (unsigned)geo.W;
+        src = ok ? X + (((int64_t)n * geo.H + ih) * geo.W + iw) * geo.C + scol[j] : geo.zero + (scol[j] & 63);
       } else {
-        constexpr int CPR = Cfg::XROW / 16;
-        const int e = (i - Cfg::GINSTS) * 64 + lane;
-        const int r = e / CPR;
-        int64_t gr = m0 + r;
-        gr = gr < M ? gr : M - 1;
-        src = X + gr * ldx + c0 + ((e % CPR) ^ tr_swz<Cfg::XROW>(r)) * 8;
+        src = X + gr * ldx + scol[j];
       }
       glds16(src, base + i * 1024);
     }
@@ -359,22 +507,22 @@ gemm_tn_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __re
   if (NS == 3 && T > 1) stage(1);
   for (int t = 0; t < T; ++t) {
     // retire slice t (with NS = 3, slice t+1 stays in flight)
-    if (NS == 3) wait_vmcnt(t + 1 < T ? Cfg::LPW : 0);
+    if (NS == 3) wait_vmcnt(t + 1 < T ? LPW : 0);
     else wait_vmcnt(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     if (t + NS - 1 < T) stage(t + NS - 1);
-    const char* Gs = smem + (t % Cfg::NS) * Cfg::STAGE;
+    const char* Gs = smem + (t % NS) * Cfg::STAGE;
     const char* Xs = Gs + Cfg::GBYTES;
-    const int64_t m0 = mbeg + (int64_t)t * 64;
+    const int64_t m0 = mbeg + (int64_t)t * Cfg::ROWS + ws * 64;
     const bool tail = m0 + 64 > mend;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8 gv[4], xv[4];
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        gv[s] = tr_frag<Cfg::GROW>(Gs, kk * 32, wn * 64 + s * 16, lane);
-        xv[s] = tr_frag<Cfg::XROW>(Xs, kk * 32, wk * 64 + s * 16, lane);
+        gv[s] = tr_frag<Cfg::GROW>(Gs, ws * 64 + kk * 32, wn * 64 + s * 16, lane);
+        xv[s] = tr_frag<Cfg::XROW>(Xs, ws * 64 + kk * 32, wk * 64 + s * 16, lane);
       }
       if (tail) {  // rows past this split's end contribute nothing
 #pragma unroll
@@ -393,6 +541,31 @@ gemm_tn_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __re
           acc[ns][ks] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gv[ns], xv[ks], acc[ns][ks], 0, 0, 0);
     }
   }
+  if (WS > 1) {   // combine the WS partial tiles through LDS
+    __syncthreads();
+    f32x4* red = reinterpret_cast<f32x4*>(smem);
+    const int slot = wn * WK + wk;
+    if (ws > 0) {
+#pragma unroll
+      for (int ns = 0; ns < 4; ++ns)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+          red[(((ws - 1) * WN * WK + slot) * 16 + ns * 4 + ks) * 64 + lane] = acc[ns][ks];
+    }
+    __syncthreads();
+    if (ws == 0) {
+#pragma unroll
+      for (int w2 = 1; w2 < WS; ++w2)
+#pragma unroll
+        for (int ns = 0; ns < 4; ++ns)
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks) {
+            const f32x4 v = red[(((w2 - 1) * WN * WK + slot) * 16 + ns * 4 + ks) * 64 + lane];
+            acc[ns][ks] += v;
+          }
+    }
+  }
+  if (ws != 0) return;
   // D[i = n][j = c]: lane holds column c = .. + (lane&15), rows n = .. + 4*(lane>>4) + r
   const int fr = lane & 15, fq = lane >> 4;
 #pragma unroll
@@ -408,35 +581,36 @@ gemm_tn_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __re
     }
 }
 
-template <int WN, int WK, int NS>
+template <int WN, int WK, int WS, int NS, bool GATHER>
 void launch_tn(const uint16_t* G, int64_t ldg, const uint16_t* X, int64_t ldx, float* W, int64_t ldw, int64_t M,
-               int N, int K, int splits, hipStream_t stream) {
-  using Cfg = TnCfg<WN, WK, NS>;
+               int N, int K, int splits, const ConvGeo& geo, hipStream_t stream) {
+  using Cfg = TnCfg<WN, WK, WS, NS>;
   const int tiles = (N / Cfg::BN) * (K / Cfg::BK);
   if (splits <= 0) {
-    const int64_t target = 1024;
+    const int64_t target = 512;
     splits = (int)((target + tiles - 1) / tiles);
   }
   int64_t rows = (M + splits - 1) / splits;
-  rows = (rows + 63) / 64 * 64;
-  if (rows < 256) rows = 256;
+  rows = (rows + Cfg::ROWS - 1) / Cfg::ROWS * Cfg::ROWS;
+  if (rows < 4 * Cfg::ROWS) rows = 4 * Cfg::ROWS;
   const int64_t nsplit = (M + rows - 1) / rows;
   dim3 grid((unsigned)(N / Cfg::BN), (unsigned)(K / Cfg::BK), (unsigned)nsplit);
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_kernel<WN, WK, NS>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_kernel<WN, WK, WS, NS, GATHER>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL((gemm_tn_kernel<WN, WK, NS>), grid, dim3(Cfg::THREADS), Cfg::LDS, stream, G, ldg, X, ldx, W, ldw,
-                     M, rows);
+  hipLaunchKernelGGL((gemm_tn_kernel<WN, WK, WS, NS, GATHER>), grid, dim3(Cfg::THREADS), Cfg::LDS, stream, G, ldg, X, ldx, W, ldw,
+                     M, rows, geo);
 }
 
 }  // namespace
 
 bool gemm_supported(int64_t N, int64_t K) { return N >= 64 && K >= 64 && N % 64 == 0 && K % 64 == 0; }
 
-void gemm_nt_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N,
-                  int K, int cfg, int max_blocks, hipStream_t stream) {
+template <bool GATHER>
+void nt_dispatch(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N,
+                 int K, int cfg, int max_blocks, const ConvGeo& geo, hipStream_t stream) {
   // cfg = tile + 10 * panel (1: resident, 2: streamed) + 100 * stages (1: two, 2: three); 0 digits = auto
   const int bres = (cfg / 10) % 10 == 0 ? -1 : ((cfg / 10) % 10 == 1 ? 1 : 0);
   const int ns = (cfg / 100) % 10 == 1 ? 2 : 3;
@@ -448,43 +622,71 @@ void gemm_nt_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* 
   static const int cfg_bn[5] = {64, 64, 128, 256, 128};
   if (cfg > 4 || N % cfg_bn[cfg] != 0) cfg = 1;   // the tile must divide N (B rows are not clamped)
   switch (cfg) {
-    case 1: launch_nt_any<4, 1>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, stream); break;   // 256 x 64
-    case 2: launch_nt_any<4, 2>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, stream); break;   // 256 x 128
-    case 3: launch_nt_any<2, 4>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, stream); break;   // 128 x 256
-    case 4: launch_nt_any<2, 2>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, stream); break;   // 128 x 128
-    default: launch_nt_any<4, 1>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, stream); break;
+    case 2: launch_nt_any<4, 2, GATHER>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stream); break;
+    case 3: launch_nt_any<2, 4, GATHER>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stream); break;
+    case 4: launch_nt_any<2, 2, GATHER>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stream); break;
+    default: launch_nt_any<4, 1, GATHER>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stream); break;
   }
 }
 
-template <int WN, int WK>
-void launch_tn_any(const uint16_t* G, int64_t ldg, const uint16_t* X, int64_t ldx, float* W, int64_t ldw, int64_t M,
-                   int N, int K, int splits, int ns, hipStream_t stream) {
-  if (ns == 3) launch_tn<WN, WK, 3>(G, ldg, X, ldx, W, ldw, M, N, K, splits, stream);
-  else launch_tn<WN, WK, 2>(G, ldg, X, ldx, W, ldw, M, N, K, splits, stream);
+void gemm_nt_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N,
+                  int K, int cfg, int max_blocks, hipStream_t stream) {
+  nt_dispatch<false>(A, lda, B, ldb, C, ldc, M, N, K, cfg, max_blocks, ConvGeo{}, stream);
 }
 
-void gemm_tn_acc_f32(const void* G, int64_t ldg, const void* X, int64_t ldx, float* W, int64_t ldw, int64_t M,
-                     int N, int K, int cfg, int splits, hipStream_t stream) {
-  const int ns = (cfg / 10) % 10 == 2 ? 3 : 2;   // cfg = tile + 10 * (1: two stages, 2: three)
+void conv_nt_bf16(const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P, int KH, int KW,
+                  const void* B, void* Y, int64_t M, int N, int cfg, int max_blocks, hipStream_t stream) {
+  ConvGeo g{static_cast<const uint16_t*>(zero), H, W, C, OH, OW, S, P, KW};
+  const int K = KH * KW * C;
+  nt_dispatch<true>(X, C, B, K, Y, N, M, N, K, cfg, max_blocks, g, stream);
+}
+
+template <int WN, int WK, int WS, bool GATHER>
+void launch_tn_any(const uint16_t* G, int64_t ldg, const uint16_t* X, int64_t ldx, float* W, int64_t ldw, int64_t M,
+                   int N, int K, int splits, int ns, const ConvGeo& geo, hipStream_t stream) {
+  if (ns == 3 && TnCfg<WN, WK, WS, 3>::LDS <= 160 * 1024)
+    launch_tn<WN, WK, WS, 3, GATHER>(G, ldg, X, ldx, W, ldw, M, N, K, splits, geo, stream);
+  else launch_tn<WN, WK, WS, 2, GATHER>(G, ldg, X, ldx, W, ldw, M, N, K, splits, geo, stream);
+}
+
+template <bool GATHER>
+void tn_dispatch(const void* G, int64_t ldg, const void* X, int64_t ldx, float* W, int64_t ldw, int64_t M, int N,
+                 int K, int cfg, int splits, const ConvGeo& geo, hipStream_t stream) {
+  // cfg = tile + 10 * (1: two stages, 2: three).  tile (WN, WK, WS):
+  // 1 (1,1,4)  2 (2,1,2)  3 (1,2,2)  4 (2,2,1)  5 (4,1,1)  6 (1,4,1)  7 (2,2,2)  8 (1,1,2)
+  const int ns = (cfg / 10) % 10 == 2 ? 3 : 2;
   cfg %= 10;
   auto g = static_cast<const uint16_t*>(G);
   auto x = static_cast<const uint16_t*>(X);
   if (cfg <= 0) {
     const bool n2 = N % 128 == 0, k2 = K % 128 == 0;
-    cfg = n2 && k2 ? 4 : (n2 ? (N % 256 == 0 ? 5 : 2) : (k2 ? (K % 256 == 0 ? 6 : 3) : 1));
+    cfg = n2 && k2 ? 7 : (n2 ? 2 : (k2 ? 3 : 1));
   }
-  static const int cfg_bn[7] = {64, 64, 128, 64, 128, 256, 64};
-  static const int cfg_bk[7] = {64, 64, 64, 128, 128, 64, 256};
-  if (cfg > 6 || N % cfg_bn[cfg] != 0 || K % cfg_bk[cfg] != 0) cfg = 1;   // tiles must divide N and K
+  static const int cfg_bn[9] = {64, 64, 128, 64, 128, 256, 64, 128, 64};
+  static const int cfg_bk[9] = {64, 64, 64, 128, 128, 64, 256, 128, 64};
+  if (cfg > 8 || N % cfg_bn[cfg] != 0 || K % cfg_bk[cfg] != 0) cfg = 1;   // tiles must divide N and K
   switch (cfg) {
-    case 1: launch_tn_any<1, 1>(g, ldg, x, ldx, W, ldw, M, N, K, splits, ns, stream); break;
-    case 2: launch_tn_any<2, 1>(g, ldg, x, ldx, W, ldw, M, N, K, splits, ns, stream); break;
-    case 3: launch_tn_any<1, 2>(g, ldg, x, ldx, W, ldw, M, N, K, splits, ns, stream); break;
-    case 4: launch_tn_any<2, 2>(g, ldg, x, ldx, W, ldw, M, N, K, splits, ns, stream); break;
-    case 5: launch_tn_any<4, 1>(g, ldg, x, ldx, W, ldw, M, N, K, splits, ns, stream); break;
-    case 6: launch_tn_any<1, 4>(g, ldg, x, ldx, W, ldw, M, N, K, splits, ns, stream); break;
-    default: launch_tn_any<1, 1>(g, ldg, x, ldx, W, ldw, M, N, K, splits, ns, stream); break;
+    case 2: launch_tn_any<2, 1, 2, GATHER>(g, ldg, x, ldx, W, ldw, M, N, K, splits, ns, geo, stream); break;
+    case 3: launch_tn_any<1, 2, 2, GATHER>(g, ldg, x, ldx, W, ldw, M, N, K, splits, ns, geo, stream); break;
+    case 4: launch_tn_any<2, 2, 1, GATHER>(g, ldg, x, ldx, W, ldw, M, N, K, splits, ns, geo, stream); break;
+    case 5: launch_tn_any<4, 1, 1, GATHER>(g, ldg, x, ldx, W, ldw, M, N, K, splits, ns, geo, stream); break;
+    case 6: launch_tn_any<1, 4, 1, GATHER>(g, ldg, x, ldx, W, ldw, M, N, K, splits, ns, geo, stream); break;
+    case 7: launch_tn_any<2, 2, 2, GATHER>(g, ldg, x, ldx, W, ldw, M, N, K, splits, ns, geo, stream); break;
+    case 8: launch_tn_any<1, 1, 2, GATHER>(g, ldg, x, ldx, W, ldw, M, N, K, splits, ns, geo, stream); break;
+    default: launch_tn_any<1, 1, 4, GATHER>(g, ldg, x, ldx, W, ldw, M, N, K, splits, ns, geo, stream); break;
   }
+}
+
+void gemm_tn_acc_f32(const void* G, int64_t ldg, const void* X, int64_t ldx, float* W, int64_t ldw, int64_t M,
+                     int N, int K, int cfg, int splits, hipStream_t stream) {
+  tn_dispatch<false>(G, ldg, X, ldx, W, ldw, M, N, K, cfg, splits, ConvGeo{}, stream);
+}
+
+void conv_tn_acc_f32(const void* G, const void* X, const void* zero, int H, int W_, int C, int OH, int OW, int S, int P,
+                     int KH, int KW, float* Wout, int64_t M, int N, int cfg, int splits, hipStream_t stream) {
+  ConvGeo g{static_cast<const uint16_t*>(zero), H, W_, C, OH, OW, S, P, KW};
+  const int K = KH * KW * C;
+  tn_dispatch<true>(G, N, X, C, Wout, K, M, N, K, cfg, splits, g, stream);
 }
 
 }  // namespace gk

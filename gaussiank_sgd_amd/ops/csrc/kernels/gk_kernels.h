@@ -218,5 +218,14 @@ void gemm_nt_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* 
                   int K, int cfg, int max_blocks, hipStream_t stream);
 void gemm_tn_acc_f32(const void* G, int64_t ldg, const void* X, int64_t ldx, float* W, int64_t ldw, int64_t M,
                      int N, int K, int cfg, int splits, hipStream_t stream);
+// Implicit-GEMM KHxKW convolution (stride S, zero padding P) over NHWC bf16:
+//   conv_nt_bf16   : Y[M = N*OH*OW, Cout] = im2col(X) . Wt[Cout, KH*KW*C]^T
+//   conv_tn_acc_f32: Wout[Cout, KH*KW*C] += G[M, Cout]^T . im2col(X)
+// Weights are channels-last ([Cout][KH][KW][C]); C % 64 == 0; `zero` points at
+// >= 64 zero bf16 (the padding row).
+void conv_nt_bf16(const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P, int KH, int KW,
+                  const void* B, void* Y, int64_t M, int N, int cfg, int max_blocks, hipStream_t stream);
+void conv_tn_acc_f32(const void* G, const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P,
+                     int KH, int KW, float* Wout, int64_t M, int N, int cfg, int splits, hipStream_t stream);
 
 }  // namespace gk

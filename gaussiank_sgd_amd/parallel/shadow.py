@@ -30,7 +30,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.bn import BNAct
-from ..ops.conv1x1 import Conv1x1
+from ..ops.conv1x1 import FastConv2d
 
 
 class _ShadowWeight(torch.autograd.Function):
@@ -80,7 +80,7 @@ def install_bf16_shadow(model: nn.Module, opt) -> int:
     names = opt._parameter_names
     count = 0
     for mod in model.modules():
-        if isinstance(mod, Conv1x1):
+        if isinstance(mod, FastConv2d):
             # its own forward reads the shadow view and (GEMM path) adds the fp32
             # weight gradient straight into the arena; other strides fall back
             # to the plain shadow conv

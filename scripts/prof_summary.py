@@ -10,6 +10,8 @@ import re
 
 
 def category(n: str) -> str:
+    if "gk::" in n and ("gemm_nt" in n or "gemm_tn" in n):
+        return "gk HIP conv GEMMs (1x1 / implicit-GEMM 3x3, MFMA)"
     if "gk::" in n:
         if "bn_" in n:
             return "gk fused BN (+ReLU/residual/pool)"

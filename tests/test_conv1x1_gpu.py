@@ -16,12 +16,32 @@ def _gpu():
     assert ops.load(), ops._load_error
 
 
-def _ref(x, w, dy):
+def _ref(x, w, dy, stride=1, padding=0):
     xr = x.detach().float().requires_grad_(True)
     wr = w.detach().to(torch.bfloat16).float().requires_grad_(True)
-    y = F.conv2d(xr, wr)
+    y = F.conv2d(xr, wr, stride=stride, padding=padding)
     y.backward(dy.float())
     return y.detach(), xr.grad, wr.grad
+
+
+@pytest.mark.parametrize("N,C,H,K,k,s", [(4, 64, 14, 64, 3, 1), (3, 128, 9, 128, 3, 2), (2, 64, 10, 256, 1, 2),
+                                         (2, 256, 7, 128, 3, 1)])
+def test_fastconv_kxk(N, C, H, K, k, s):
+    from gaussiank_sgd_amd.ops.conv1x1 import FastConv2d
+    torch.manual_seed(N * C + K + k)
+    m = FastConv2d(C, K, k, stride=s, padding=k // 2, bias=False).cuda().to(memory_format=torch.channels_last)
+    x = torch.randn(N, C, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = m(x)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    ry, rdx, rdw = _ref(x, m.weight, dy, s, k // 2)
+    assert y.shape == ry.shape
+    tol = lambda r: 1e-2 * r.abs().max().item() + 1e-3  # noqa: E731
+    assert (y.float() - ry).abs().max().item() <= tol(ry)
+    assert (x.grad.float() - rdx).abs().max().item() <= tol(rdx)
+    assert (m.weight.grad - rdw).abs().max().item() <= 2e-3 * rdw.abs().max().item() + 1e-3
 
 
 @pytest.mark.parametrize("N,C,H,K", [(4, 64, 14, 256), (3, 256, 7, 64), (2, 128, 9, 128), (8, 512, 7, 2048)])
@@ -44,7 +64,7 @@ def test_conv1x1_plain(N, C, H, K):
     assert (m.weight.grad - rdw).abs().max().item() <= 2e-3 * rdw.abs().max().item() + 1e-3
 
 
-def test_conv1x1_stride2_falls_back():
+def test_conv1x1_stride2():
     from gaussiank_sgd_amd.ops.conv1x1 import Conv1x1
     m = Conv1x1(64, 128, stride=2).cuda().to(memory_format=torch.channels_last)
     x = torch.randn(2, 64, 8, 8, device="cuda").contiguous(memory_format=torch.channels_last)

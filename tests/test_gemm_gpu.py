@@ -51,7 +51,7 @@ def test_gemm_nt_strided_rows_and_grid(g):
 
 @pytest.mark.parametrize("M,N,K", [(1000, 64, 64), (4096, 256, 64), (777, 128, 192), (2500, 512, 256),
                                    (130, 64, 128), (5000, 128, 512)])
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8, 21, 27])
 @pytest.mark.parametrize("splits", [0, 1, 7])
 def test_gemm_tn_acc(g, M, N, K, cfg, splits):
     torch.manual_seed(M * 3 + N + K)
@@ -63,3 +63,43 @@ def test_gemm_tn_acc(g, M, N, K, cfg, splits):
     ref = W0 + G.float().t() @ X.float()
     err = (W - ref).abs().max().item()
     assert err <= 1e-4 * (G.float().abs().t() @ X.float().abs()).max().item() + 1e-4, err
+
+
+def _conv_case(N, C, H, Co, k, s, p):
+    x = _rand(N, C, H, H).contiguous(memory_format=torch.channels_last)
+    w = _rand(Co, C, k, k, scale=(C * k * k) ** -0.5).contiguous(memory_format=torch.channels_last)
+    return x, w
+
+
+@pytest.mark.parametrize("N,C,H,Co,k,s,p", [(2, 64, 9, 64, 3, 1, 1), (3, 128, 7, 64, 3, 2, 1), (2, 64, 14, 128, 3, 2, 1),
+                                            (2, 128, 5, 256, 1, 1, 0), (1, 64, 11, 192, 3, 1, 1)])
+@pytest.mark.parametrize("cfg", [0, 1, 3, 22, 124])
+def test_conv_nt(g, N, C, H, Co, k, s, p, cfg):
+    import torch.nn.functional as F
+    torch.manual_seed(N + C + H + Co)
+    x, w = _conv_case(N, C, H, Co, k, s, p)
+    zero = torch.zeros(64, device="cuda", dtype=torch.bfloat16)
+    ref = F.conv2d(x.float(), w.float(), stride=s, padding=p)
+    y = torch.full(ref.shape, float("nan"), device="cuda", dtype=torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    g.conv_nt(x, w, y, zero, s, p, cfg, 0)
+    assert (y.float() - ref).abs().max().item() <= 1e-2 * ref.abs().max().item() + 1e-3
+
+
+@pytest.mark.parametrize("N,C,H,Co,k,s,p", [(2, 64, 9, 64, 3, 1, 1), (3, 128, 7, 64, 3, 2, 1), (2, 64, 14, 128, 3, 2, 1),
+                                            (2, 128, 5, 256, 1, 1, 0)])
+@pytest.mark.parametrize("cfg,splits", [(0, 0), (1, 3), (4, 0), (25, 0), (2, 7), (7, 0), (8, 2), (23, 0)])
+def test_conv_tn_acc(g, N, C, H, Co, k, s, p, cfg, splits):
+    import torch.nn.functional as F
+    torch.manual_seed(N * 7 + C + H + Co)
+    x, w = _conv_case(N, C, H, Co, k, s, p)
+    xr = x.float().requires_grad_(True)
+    wr = w.float().requires_grad_(True)
+    yr = F.conv2d(xr, wr, stride=s, padding=p)
+    dy = torch.randn_like(yr).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    yr.backward(dy.float())
+    zero = torch.zeros(64, device="cuda", dtype=torch.bfloat16)
+    out = torch.zeros(Co, C, k, k, device="cuda").contiguous(memory_format=torch.channels_last)
+    g.conv_tn_acc(dy, x, out, zero, s, p, cfg, splits)
+    err = (out - wr.grad).abs().max().item()
+    assert err <= 1e-3 * wr.grad.abs().max().item() + 1e-3, err
