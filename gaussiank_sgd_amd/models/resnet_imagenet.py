@@ -21,7 +21,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.bn import BNAct, global_avg_pool
-from ..ops.conv1x1 import Conv1x1, Conv3x3
+from ..ops.conv1x1 import Conv1x1, Conv3x3, conv_stats
 
 
 def conv3x3(inp: int, out: int, stride: int = 1, groups: int = 1, dilation: int = 1) -> nn.Conv2d:
@@ -48,8 +48,10 @@ class BasicBlock(nn.Module):
     def forward(self, x):
         x, xs = x if isinstance(x, tuple) else (x, x)   # (main, shortcut) handles, see BNAct twin
         identity = xs if self.downsample is None else self.downsample(xs)
-        out = self.bn1(self.conv1(x))
-        return self.bn2(self.conv2(out), identity)
+        y, st = conv_stats(self.conv1, x)   # BN statistics from the conv epilogue when fused
+        out = self.bn1(y, stats=st)
+        y, st = conv_stats(self.conv2, out)
+        return self.bn2(y, identity, stats=st)
 
 
 class Bottleneck(nn.Module):
@@ -69,9 +71,21 @@ class Bottleneck(nn.Module):
     def forward(self, x):
         x, xs = x if isinstance(x, tuple) else (x, x)   # (main, shortcut) handles, see BNAct twin
         identity = xs if self.downsample is None else self.downsample(xs)
-        out = self.bn1(self.conv1(x))
-        out = self.bn2(self.conv2(out))
-        return self.bn3(self.conv3(out), identity)
+        y, st = conv_stats(self.conv1, x)   # BN statistics from the conv epilogue when fused
+        out = self.bn1(y, stats=st)
+        y, st = conv_stats(self.conv2, out)
+        out = self.bn2(y, stats=st)
+        y, st = conv_stats(self.conv3, out)
+        return self.bn3(y, identity, stats=st)
+
+
+class ConvBN(nn.Sequential):
+    """``Sequential(conv, BNAct)`` (state_dict keys ``0.*``, ``1.*`` as
+    torchvision's downsample) passing the conv's fused BN statistics on."""
+
+    def forward(self, x):
+        y, st = conv_stats(self[0], x)
+        return self[1](y, stats=st)
 
 
 class ResNet(nn.Module):
@@ -117,8 +131,8 @@ class ResNet(nn.Module):
     def _make_layer(self, block, planes, blocks, stride=1):
         downsample = None
         if stride != 1 or self.inplanes != planes * block.expansion:
-            downsample = nn.Sequential(conv1x1(self.inplanes, planes * block.expansion, stride),
-                                       BNAct(planes * block.expansion))
+            downsample = ConvBN(conv1x1(self.inplanes, planes * block.expansion, stride),
+                                BNAct(planes * block.expansion))
         layers = [block(self.inplanes, planes, stride, downsample, self.groups, self.base_width)]
         self.inplanes = planes * block.expansion
         for _ in range(1, blocks):

@@ -42,7 +42,7 @@ def _grad_pair(grads, like):
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, relu, direct=None,
-                nbt=None, twin=False):
+                nbt=None, twin=False, pre=None):
         # direct = (gw_view, gb_view): weight/bias gradients are accumulated
         # straight into the optimizer's fp32 arena by the backward kernel and
         # None is returned for them, so AccumulateGrad launches nothing (its
@@ -64,8 +64,11 @@ class _BNActFn(torch.autograd.Function):
         mask = None
         if relu:
             mask = torch.empty(int(_ops().bn_mask_bytes(M, C, eb)), dtype=torch.uint8, device=x.device)
+        # pre = (partials [2, rows, C], rows): batch statistics already reduced by
+        # the producing convolution's epilogue (ops/conv1x1.py) -- no stats pass
+        pre_t, pre_rows = pre if pre is not None else (None, 0)
         _ops().bn_act_forward(x, residual, y, mask, weight, bias, running_mean, running_var, stats[0], stats[1],
-                              stats[2], stats[3], ws, float(eps), float(momentum), bool(relu), nbt)
+                              stats[2], stats[3], ws, float(eps), float(momentum), bool(relu), nbt, pre_t, pre_rows)
         ctx.relu = bool(relu)
         ctx.has_res = residual is not None
         ctx.save_for_backward(x, mask, weight, stats[0], stats[1])
@@ -76,7 +79,7 @@ class _BNActFn(torch.autograd.Function):
         x, mask, weight, mean, invstd = ctx.saved_tensors
         dy, dy2 = _grad_pair(grads, x)
         if dy is None:
-            return (None,) * 12
+            return (None,) * 13
         C = x.shape[1]
         M = x.numel() // C
         dx = torch.empty_like(x, memory_format=_CL)
@@ -87,10 +90,10 @@ class _BNActFn(torch.autograd.Function):
         gw, gb = ctx.direct if ctx.direct is not None else (None, None)
         _ops().bn_act_backward(dy, mask, x, dx, dres, weight, mean, invstd, g[0], g[1], ws, ctx.relu, gw, gb, dy2)
         if ctx.direct is not None:
-            return dx, dres, None, None, None, None, None, None, None, None, None, None
+            return dx, dres, None, None, None, None, None, None, None, None, None, None, None
         dgamma = g[0] if weight is not None and ctx.needs_input_grad[2] else None
         dbeta = g[1] if ctx.needs_input_grad[3] else None
-        return dx, dres, dgamma, dbeta, None, None, None, None, None, None, None, None
+        return dx, dres, dgamma, dbeta, None, None, None, None, None, None, None, None, None
 
 
 class _BNReLUPoolFn(torch.autograd.Function):
@@ -180,7 +183,10 @@ class BNAct(nn.BatchNorm2d):
         # both the next conv1 and the next shortcut).
         self.twin = twin
 
-    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, stats=None) -> torch.Tensor:
+        """``stats``: optional (partials, rows) of x's batch statistics reduced
+        by the producing convolution (ops/conv1x1.py conv_stats); used only on
+        the fused training path."""
         relu = self.act == "relu"
         pool = self.pool
         if self.training and self.fused and self.track_running_stats and fused_bn_available(x) and \
@@ -196,8 +202,10 @@ class BNAct(nn.BatchNorm2d):
             if pool is not None:
                 return _BNReLUPoolFn.apply(x, self.weight, self.bias, self.running_mean, self.running_var, mom,
                                            self.eps, pool, direct, nbt, self.twin)
+            if stats is not None and (stats[0].shape[2] != x.shape[1] or x.dtype != torch.bfloat16):
+                stats = None
             return _BNActFn.apply(x, residual, self.weight, self.bias, self.running_mean, self.running_var, mom,
-                                  self.eps, relu, direct, nbt, self.twin)
+                                  self.eps, relu, direct, nbt, self.twin, stats)
         out = super().forward(x)
         if residual is not None:
             out = out + residual

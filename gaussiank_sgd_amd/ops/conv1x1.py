@@ -147,22 +147,32 @@ def _geom(x_shape, w: torch.Tensor, s: int):
     return N, C, H, W, K, k, p, OH, OW
 
 
-def _fwd(x: torch.Tensor, w: torch.Tensor, s: int) -> torch.Tensor:
+def _fwd(x: torch.Tensor, w: torch.Tensor, s: int, stats_box=None) -> torch.Tensor:
+    """y = conv(x, w).  With ``stats_box`` (a list) and the HIP kernel chosen,
+    the kernel's epilogue also reduces the BatchNorm batch statistics of y
+    and ``(partials [2, rows_max, K], rows)`` is appended to the box
+    (ops/bn.py BNAct(stats=...) consumes it and skips its statistics pass)."""
     N, C, H, W, K, k, p, OH, OW = _geom(x.shape, w, s)
+    M = N * OH * OW
     y = torch.empty((N, K, OH, OW), dtype=torch.bfloat16, device=x.device, memory_format=_CL)
     g = _g()
+    st = None
+    if stats_box is not None:
+        st = torch.empty(2, min(1280, (M + 63) // 64), K, dtype=torch.float32, device=x.device)
     if k == 1 and s == 1:
         X, Y, Wm = _rows(x), _rows(y), w.reshape(K, C)
-        run = lambda c, mb: g.gemm_nt(X, Wm, Y, c, mb)  # noqa: E731
+        run = lambda c, mb: g.gemm_nt(X, Wm, Y, c, mb, st)  # noqa: E731
     else:
         z = _zero(x.device)
-        run = lambda c, mb: g.conv_nt(x, w, y, z, s, p, c, mb)  # noqa: E731
+        run = lambda c, mb: g.conv_nt(x, w, y, z, s, p, c, mb, st)  # noqa: E731
     cands = [(("hip", c, 0), (lambda c=c: run(c, 0))) for c in _NT_CFGS]
     cands.append((("miopen", 0, 0), lambda: F.conv2d(x, w, stride=s, padding=p)))
-    ch = _pick(("fwd", N, C, H, W, K, k, s), cands)
+    ch = _pick(("fwd", N, C, H, W, K, k, s, st is not None), cands)
     if ch[0] == "miopen":
         return F.conv2d(x, w, stride=s, padding=p).contiguous(memory_format=_CL)
-    run(ch[1], ch[2])
+    rows = run(ch[1], ch[2])
+    if st is not None:
+        stats_box.append((st, int(rows)))
     return y
 
 
@@ -229,13 +239,13 @@ class _FastConvFn(torch.autograd.Function):
     fp32 arena in the backward and None is returned for it."""
 
     @staticmethod
-    def forward(ctx, x, param, w_bf16, sink, stride):
+    def forward(ctx, x, param, w_bf16, sink, stride, stats_box=None):
         if x.dtype != torch.bfloat16:
             x = x.to(torch.bfloat16)
         x = x.contiguous(memory_format=_CL)
         w = w_bf16 if w_bf16 is not None else param.detach().to(torch.bfloat16)
         w = w.contiguous(memory_format=_CL)
-        y = _fwd(x, w, stride)
+        y = _fwd(x, w, stride, stats_box)
         ctx.sink = sink
         ctx.stride = stride
         ctx.param_dtype = param.dtype
@@ -262,7 +272,7 @@ class _FastConvFn(torch.autograd.Function):
                     sink(out)
                 else:
                     gparam = out.to(ctx.param_dtype)
-        return dx, gparam, None, None, None
+        return dx, gparam, None, None, None, None
 
 
 class FastConv2d(nn.Conv2d):
@@ -271,6 +281,16 @@ class FastConv2d(nn.Conv2d):
     compute, as autocast); everything else is the stock convolution."""
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self._run(x, None)
+
+    def forward_stats(self, x: torch.Tensor):
+        """(y, stats): stats = (partials, rows) of y's BatchNorm statistics
+        when the fused HIP kernel produced them, else None."""
+        box = []
+        y = self._run(x, box)
+        return y, (box[0] if box else None)
+
+    def _run(self, x: torch.Tensor, box):
         dev = x.device.type
         bf16 = x.dtype == torch.bfloat16 or (torch.is_autocast_enabled(dev) and
                                              torch.get_autocast_dtype(dev) == torch.bfloat16)
@@ -281,9 +301,16 @@ class FastConv2d(nn.Conv2d):
             w_bf16, sink = (info[0], info[1]) if use_shadow else (None, None)
             if not torch.is_grad_enabled() or not self.weight.requires_grad:
                 sink = None
-            return _FastConvFn.apply(x, self.weight, w_bf16, sink, self.stride[0])
+            return _FastConvFn.apply(x, self.weight, w_bf16, sink, self.stride[0], box)
         slow = getattr(self, "_gk_slow", None)
         return slow(x) if slow is not None else super().forward(x)
+
+
+def conv_stats(conv: nn.Module, x: torch.Tensor):
+    """(conv(x), BatchNorm partials of the output or None)."""
+    if isinstance(conv, FastConv2d):
+        return conv.forward_stats(x)
+    return conv(x), None
 
 
 class Conv1x1(FastConv2d):

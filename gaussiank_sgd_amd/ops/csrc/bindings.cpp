@@ -301,7 +301,7 @@ void bn_act_forward(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, c
                     c10::optional<at::Tensor> b, c10::optional<at::Tensor> run_mean,
                     c10::optional<at::Tensor> run_var, at::Tensor save_mean, at::Tensor save_invstd,
                     at::Tensor scale, at::Tensor shift, at::Tensor ws, double eps, double momentum, bool relu,
-                    c10::optional<at::Tensor> nbt) {
+                    c10::optional<at::Tensor> nbt, c10::optional<at::Tensor> pre, int64_t pre_rows) {
   check_cl(x, "x");
   check_cl(y, "y");
   const int64_t C = channels_of(x);
@@ -327,6 +327,19 @@ void bn_act_forward(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, c
     mp = mask->data_ptr<uint8_t>();
   }
   c10::DeviceGuard guard(x.device());
+  if (pre.has_value() && pre->defined()) {   // statistics pre-reduced by the producer (conv epilogue)
+    TORCH_CHECK(pre->is_cuda() && pre->scalar_type() == at::kFloat && pre->is_contiguous() && pre->dim() == 3 &&
+                    pre->size(0) == 2 && pre->size(2) == C && pre_rows > 0 && pre_rows <= pre->size(1),
+                "pre must be fp32 [2, rows, C] partials with 0 < pre_rows <= rows");
+    // the finalize reads rows [0, pre_rows) of each half
+    const float* ps = pre->data_ptr<float>();
+    gk::bn_act_forward_pre(x.data_ptr(), rp, y.data_ptr(), mp, M, (int)C, eb, ps, ps + pre->size(1) * C,
+                           (int)pre_rows, opt_f32(w), opt_f32(b), (float)eps, (float)momentum, opt_f32_mut(run_mean),
+                           opt_f32_mut(run_var), save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(),
+                           scale.data_ptr<float>(), shift.data_ptr<float>(), relu ? 1 : 0, opt_i64(nbt),
+                           cur_stream(x));
+    return;
+  }
   gk::bn_act_forward(x.data_ptr(), rp, y.data_ptr(), mp, M, (int)C, eb, opt_f32(w), opt_f32(b), (float)eps,
                      (float)momentum, opt_f32_mut(run_mean), opt_f32_mut(run_var), save_mean.data_ptr<float>(),
                      save_invstd.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(),
@@ -571,8 +584,23 @@ void check_rows(const at::Tensor& t, const char* name) {
   TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
 }
 
+// stats (optional): fp32 [2, rows, N] BatchNorm partials of C; returns the rows written
+float* stats_ptr(const c10::optional<at::Tensor>& st, int64_t N, int* rows) {
+  if (!st.has_value()) {
+    *rows = 0;
+    return nullptr;
+  }
+  const at::Tensor& t = *st;
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.dim() == 3 && t.size(0) == 2 &&
+                  t.size(2) == N && t.size(1) > 0,
+              "stats must be a contiguous fp32 [2, rows, N] GPU tensor");
+  *rows = (int)t.size(1);
+  return t.data_ptr<float>();
+}
+
 // C[M, N] = A[M, K] . B[N, K]^T
-void gemm_nt(at::Tensor A, at::Tensor B, at::Tensor C, int64_t cfg, int64_t max_blocks) {
+int64_t gemm_nt(at::Tensor A, at::Tensor B, at::Tensor C, int64_t cfg, int64_t max_blocks,
+                c10::optional<at::Tensor> stats) {
   check_rows(A, "A");
   check_rows(B, "B");
   check_rows(C, "C");
@@ -580,9 +608,11 @@ void gemm_nt(at::Tensor A, at::Tensor B, at::Tensor C, int64_t cfg, int64_t max_
   TORCH_CHECK(B.size(1) == K && C.size(0) == M && C.size(1) == N, "gemm_nt: shape mismatch");
   TORCH_CHECK(gk::gemm_supported(N, K), "gemm_nt: N and K must be multiples of 64");
   TORCH_CHECK(M > 0, "gemm_nt: empty M");
+  int rows = 0;
+  float* sp = stats_ptr(stats, N, &rows);
   c10::DeviceGuard guard(A.device());
-  gk::gemm_nt_bf16(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), M, (int)N,
-                   (int)K, (int)cfg, (int)max_blocks, cur_stream(A));
+  return gk::gemm_nt_bf16(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), M, (int)N,
+                          (int)K, (int)cfg, (int)max_blocks, sp, rows, cur_stream(A));
 }
 
 // W[N, K] += G[M, N]^T . X[M, K]   (fp32 W, float atomics)
@@ -614,8 +644,8 @@ void check_conv(const at::Tensor& x, const at::Tensor& w, const at::Tensor& zero
               "conv: zero must hold >= 64 bf16");
 }
 
-void conv_nt(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor zero, int64_t stride, int64_t pad, int64_t cfg,
-             int64_t max_blocks) {
+int64_t conv_nt(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor zero, int64_t stride, int64_t pad, int64_t cfg,
+                int64_t max_blocks, c10::optional<at::Tensor> stats) {
   check_conv(x, w, zero);
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
   const int64_t Co = w.size(0), KH = w.size(2), KW = w.size(3);
@@ -626,9 +656,12 @@ void conv_nt(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor zero, int64_t 
               "conv_nt: y must be channels-last bf16 [N, Cout, OH, OW]");
   const int64_t M = N * OH * OW;
   TORCH_CHECK(M > 0 && M < (int64_t(1) << 32), "conv_nt: M out of range");
+  int rows = 0;
+  float* sp = stats_ptr(stats, Co, &rows);
   c10::DeviceGuard guard(x.device());
-  gk::conv_nt_bf16(x.data_ptr(), zero.data_ptr(), (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)stride, (int)pad,
-                   (int)KH, (int)KW, w.data_ptr(), y.data_ptr(), M, (int)Co, (int)cfg, (int)max_blocks, cur_stream(x));
+  return gk::conv_nt_bf16(x.data_ptr(), zero.data_ptr(), (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)stride,
+                          (int)pad, (int)KH, (int)KW, w.data_ptr(), y.data_ptr(), M, (int)Co, (int)cfg, (int)max_blocks,
+                          sp, rows, cur_stream(x));
 }
 
 // wout: fp32 [Cout, C, KH, KW] channels-last (memory [Cout][KH][KW][C]); += dW
@@ -689,7 +722,8 @@ TORCH_LIBRARY(gksgd, m) {
   m.def(
       "bn_act_forward(Tensor x, Tensor? res, Tensor(a!) y, Tensor(i!)? mask, Tensor? w, Tensor? b, Tensor(b!)? run_mean, "
       "Tensor(c!)? run_var, Tensor(d!) save_mean, Tensor(e!) save_invstd, Tensor(f!) scale, Tensor(g!) shift, "
-      "Tensor(h!) ws, float eps, float momentum, bool relu, Tensor(j!)? nbt=None) -> ()");
+      "Tensor(h!) ws, float eps, float momentum, bool relu, Tensor(j!)? nbt=None, Tensor? pre=None, "
+      "int pre_rows=0) -> ()");
   m.def(
       "bn_relu_pool_forward(Tensor x, Tensor(a!) y, Tensor(b!) amax, Tensor? w, Tensor? b, Tensor(c!)? run_mean, "
       "Tensor(d!)? run_var, Tensor(e!) save_mean, Tensor(f!) save_invstd, Tensor(g!) scale, Tensor(h!) shift, "
@@ -709,9 +743,10 @@ TORCH_LIBRARY(gksgd, m) {
   m.def("mask_records(Tensor(a!) u, Tensor record, int k_cap) -> ()");
   m.def("cast_bf16(Tensor(a!) dst, Tensor src) -> ()");
   m.def("gemm_supported(int N, int K) -> bool", &gemm_supported);
-  m.def("gemm_nt(Tensor A, Tensor B, Tensor(a!) C, int cfg=0, int max_blocks=0) -> ()");
+  m.def("gemm_nt(Tensor A, Tensor B, Tensor(a!) C, int cfg=0, int max_blocks=0, Tensor(b!)? stats=None) -> int");
   m.def("gemm_tn_acc(Tensor G, Tensor X, Tensor(a!) W, int cfg=0, int splits=0) -> ()");
-  m.def("conv_nt(Tensor x, Tensor w, Tensor(a!) y, Tensor zero, int stride, int pad, int cfg=0, int max_blocks=0) -> ()");
+  m.def("conv_nt(Tensor x, Tensor w, Tensor(a!) y, Tensor zero, int stride, int pad, int cfg=0, int max_blocks=0, "
+        "Tensor(b!)? stats=None) -> int");
   m.def("conv_tn_acc(Tensor dy, Tensor x, Tensor(a!) wout, Tensor zero, int stride, int pad, int cfg=0, int splits=0) -> ()");
 
   m.class_<RcclEngine>("RcclEngine")

@@ -788,6 +788,32 @@ void bn_act_forward(const void* x, const void* res, void* y, uint8_t* mask, int6
                         run_var, save_mean, save_invstd, scale, shift, ws, relu, nbt, s);
 }
 
+void bn_act_forward_pre(const void* x, const void* res, void* y, uint8_t* mask, int64_t M, int C, int elem_bytes,
+                        const float* psum, const float* psq, int gy, const float* w, const float* b, float eps, float momentum,
+                        float* run_mean, float* run_var, float* save_mean, float* save_invstd, float* scale,
+                        float* shift, int relu, int64_t* nbt, hipStream_t s) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(kBlock), 0, s, psum, psq, gy, M, C, w, b, eps, momentum, run_mean, run_var, save_mean,
+                     save_invstd, scale, shift, nbt);
+#define GK_APPLY(T, R, D)                                                                                        \
+  do {                                                                                                           \
+    const Geo g = make_geo<T>(M, C, kTargetBlocks);                                                              \
+    hipLaunchKernelGGL((bn_apply_kernel<T, R, D>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, (const T*)x,            \
+                       (const T*)res, (T*)y, mask, M, C, g, scale, shift);                                       \
+  } while (0)
+#define GK_APPLY_T(T)                     \
+  if (relu && res) GK_APPLY(T, true, true);    \
+  else if (relu) GK_APPLY(T, true, false);     \
+  else if (res) GK_APPLY(T, false, true);      \
+  else GK_APPLY(T, false, false);
+  if (elem_bytes == 2) {
+    GK_APPLY_T(uint16_t)
+  } else {
+    GK_APPLY_T(float)
+  }
+#undef GK_APPLY_T
+#undef GK_APPLY
+}
+
 void bn_act_backward(const void* dy, const void* dy2, const uint8_t* mask, const void* x, void* dx, void* dres,
                      int64_t M, int C, int elem_bytes, const float* w, const float* mean, const float* invstd,
                      float* dgamma, float* dbeta, float* ws, int relu, float* gw_acc, float* gb_acc, hipStream_t s) {

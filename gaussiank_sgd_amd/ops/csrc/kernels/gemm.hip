@@ -123,7 +123,11 @@ struct NtCfg {
 template <int WM, int WN, bool BRES, int NS, bool GATHER>
 __global__ void __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(WM * WN >= 8 ? 1 : 2)))
 gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
-               uint16_t* __restrict__ C, int64_t ldc, int64_t M, int K, ConvGeo geo) {
+               uint16_t* __restrict__ C, int64_t ldc, int64_t M, int K, ConvGeo geo, float* __restrict__ stats,
+               int64_t stats_ld) {
+  // stats != nullptr: per-block BatchNorm partials of the (bf16-rounded)
+  // output, psum at stats[blockIdx.x * N + n], psq at stats[stats_ld + ...]
+  // (the [gy][C] layout bn_finalize_kernel reduces).
   using Cfg = NtCfg<WM, WN, BRES>;
   static_assert(NS == 2 || NS == 3, "stages");
   constexpr int LPW = Cfg::LPW;
@@ -137,7 +141,15 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
   // this block's work: M tiles blockIdx.x, +gridDim.x, ...; each has nk K slices
   const int64_t my_tiles = blockIdx.x < mtiles ? (mtiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
   const int T = (int)(my_tiles * nk);
-  if (T == 0) return;
+  const int Ntot = gridDim.y * Cfg::BN;
+  if (T == 0) {
+    if (stats)
+      for (int c = threadIdx.x; c < Cfg::BN; c += Cfg::THREADS) {
+        stats[(int64_t)blockIdx.x * Ntot + n0 + c] = 0.f;
+        stats[stats_ld + (int64_t)blockIdx.x * Ntot + n0 + c] = 0.f;
+      }
+    return;
+  }
   char* stage_base = smem + (BRES ? Cfg::BN * K * 2 : 0);
 
   if (BRES) {  // weight panel: slice ks at smem + ks*BSTAGE, rows swizzled as the streamed tiles
@@ -246,6 +258,11 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
   int st1 = 0, st2 = 0;
   int ks = 0;
   int buf = 0;
+  float ssum[4][4], ssq[4][4];   // BN partials: [ns][r] of this lane's column, summed over its rows
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) ssum[a][b] = ssq[a][b] = 0.f;
   int64_t mt = blockIdx.x;
   for (int t = 0; t < T; ++t) {
     // ops issued after stage(t), in order: NS=2: stores(t-1);
@@ -294,6 +311,18 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
           const f32x4 va = acc[ms][2 * pr], vb = acc[ms][2 * pr + 1];
           const uint32_t a0 = pack_bf16x2(va[0], va[1]), a1 = pack_bf16x2(va[2], va[3]);
           const uint32_t b0 = pack_bf16x2(vb[0], vb[1]), b1 = pack_bf16x2(vb[2], vb[3]);
+          if (stats && (full || m < M)) {   // statistics of the values as stored (bf16)
+            const uint32_t pk[4] = {a0, a1, b0, b1};
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+              const float lo = __uint_as_float(pk[h] << 16), hi = __uint_as_float(pk[h] & 0xffff0000u);
+              const int nsx = 2 * pr + (h >> 1), rr = (h & 1) * 2;
+              ssum[nsx][rr] += lo;
+              ssq[nsx][rr] = fmaf(lo, lo, ssq[nsx][rr]);
+              ssum[nsx][rr + 1] += hi;
+              ssq[nsx][rr + 1] = fmaf(hi, hi, ssq[nsx][rr + 1]);
+            }
+          }
           const uint32_t r0 = (uint32_t)__shfl_xor((int)(odd ? a0 : b0), 16, 64);
           const uint32_t r1 = (uint32_t)__shfl_xor((int)(odd ? a1 : b1), 16, 64);
           const uint4 v = odd ? make_uint4(r0, r1, b0, b1) : make_uint4(a0, a1, r0, r1);
@@ -307,11 +336,48 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // skipped stores: keep the counts exact
     }
   }
+  if (stats) {
+    // sum over the 16 rows (lanes fr) of each lane group, then over the WM
+    // waves sharing a column range, through LDS (every stage is consumed)
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+          ssum[a][b] += __shfl_xor(ssum[a][b], off, 64);
+          ssq[a][b] += __shfl_xor(ssq[a][b], off, 64);
+        }
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);   // [2][WM][BN]
+    if (fr == 0) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int col = wn * 64 + a * 16 + fq * 4 + b;
+          red[wm * Cfg::BN + col] = ssum[a][b];
+          red[(WM + wm) * Cfg::BN + col] = ssq[a][b];
+        }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < Cfg::BN; c += Cfg::THREADS) {
+      float sa = 0.f, sb = 0.f;
+#pragma unroll
+      for (int w2 = 0; w2 < WM; ++w2) {
+        sa += red[w2 * Cfg::BN + c];
+        sb += red[(WM + w2) * Cfg::BN + c];
+      }
+      stats[(int64_t)blockIdx.x * Ntot + n0 + c] = sa;
+      stats[stats_ld + (int64_t)blockIdx.x * Ntot + n0 + c] = sb;
+    }
+  }
 }
 
 template <int WM, int WN, bool BRES, int NS, bool GATHER>
-void launch_nt(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, uint16_t* C, int64_t ldc, int64_t M,
-               int N, int K, int max_blocks, const ConvGeo& geo, hipStream_t stream) {
+int launch_nt(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, uint16_t* C, int64_t ldc, int64_t M,
+              int N, int K, int max_blocks, const ConvGeo& geo, float* stats, int64_t stats_ld, int stats_rows,
+              hipStream_t stream) {
   using Cfg = NtCfg<WM, WN, BRES>;
   const int ntiles = N / Cfg::BN;
   const int64_t mtiles = (M + Cfg::BM - 1) / Cfg::BM;
@@ -321,6 +387,7 @@ void launch_nt(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, u
   if (max_blocks > 0) gx = max_blocks;
   if (gx < 1) gx = 1;
   if (gx > mtiles) gx = mtiles;
+  if (stats && gx > stats_rows) gx = stats_rows;   // one partial row per block
   dim3 grid((unsigned)gx, (unsigned)ntiles);
   static bool attr = [] {
     return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<WM, WN, BRES, NS, GATHER>),
@@ -328,22 +395,24 @@ void launch_nt(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, u
   }();
   (void)attr;
   hipLaunchKernelGGL((gemm_nt_kernel<WM, WN, BRES, NS, GATHER>), grid, dim3(Cfg::THREADS), lds, stream, A, lda, B,
-                     ldb, C, ldc, M, K, geo);
+                     ldb, C, ldc, M, K, geo, stats, stats_ld);
+  return (int)gx;
 }
 
 template <int WM, int WN, bool GATHER>
-void launch_nt_any(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, uint16_t* C, int64_t ldc,
-                   int64_t M, int N, int K, int max_blocks, int bres, int ns, const ConvGeo& geo, hipStream_t stream) {
+int launch_nt_any(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, uint16_t* C, int64_t ldc,
+                  int64_t M, int N, int K, int max_blocks, int bres, int ns, const ConvGeo& geo, float* stats,
+                  int64_t stats_ld, int stats_rows, hipStream_t stream) {
   // keep the weight panel resident when it fits next to the two A stages
   if (bres < 0) bres = (64 * WN) * K * 2 <= 64 * 1024;
   if (bres && NtCfg<WM, WN, true>::lds_bytes(K, 2) > 160 * 1024) bres = 0;
   constexpr int L = 160 * 1024;
   if (bres) {
-    if (ns != 2 && NtCfg<WM, WN, true>::lds_bytes(K, 3) <= L) launch_nt<WM, WN, true, 3, GATHER>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stream);
-    else launch_nt<WM, WN, true, 2, GATHER>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stream);
+    if (ns != 2 && NtCfg<WM, WN, true>::lds_bytes(K, 3) <= L) return launch_nt<WM, WN, true, 3, GATHER>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, stream);
+    else return launch_nt<WM, WN, true, 2, GATHER>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, stream);
   } else {
-    if (ns != 2 && NtCfg<WM, WN, false>::lds_bytes(K, 3) <= L) launch_nt<WM, WN, false, 3, GATHER>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stream);
-    else launch_nt<WM, WN, false, 2, GATHER>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stream);
+    if (ns != 2 && NtCfg<WM, WN, false>::lds_bytes(K, 3) <= L) return launch_nt<WM, WN, false, 3, GATHER>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, stream);
+    else return launch_nt<WM, WN, false, 2, GATHER>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, stream);
   }
 }
 
@@ -609,8 +678,9 @@ void launch_tn(const uint16_t* G, int64_t ldg, const uint16_t* X, int64_t ldx, f
 bool gemm_supported(int64_t N, int64_t K) { return N >= 64 && K >= 64 && N % 64 == 0 && K % 64 == 0; }
 
 template <bool GATHER>
-void nt_dispatch(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N,
-                 int K, int cfg, int max_blocks, const ConvGeo& geo, hipStream_t stream) {
+int nt_dispatch(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N,
+                int K, int cfg, int max_blocks, const ConvGeo& geo, float* stats, int64_t stats_ld, int stats_rows,
+                hipStream_t stream) {
   // cfg = tile + 10 * panel (1: resident, 2: streamed) + 100 * stages (1: two, 2: three); 0 digits = auto
   const int bres = (cfg / 10) % 10 == 0 ? -1 : ((cfg / 10) % 10 == 1 ? 1 : 0);
   const int ns = (cfg / 100) % 10 == 1 ? 2 : 3;
@@ -622,23 +692,26 @@ void nt_dispatch(const void* A, int64_t lda, const void* B, int64_t ldb, void* C
   static const int cfg_bn[5] = {64, 64, 128, 256, 128};
   if (cfg > 4 || N % cfg_bn[cfg] != 0) cfg = 1;   // the tile must divide N (B rows are not clamped)
   switch (cfg) {
-    case 2: launch_nt_any<4, 2, GATHER>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stream); break;
-    case 3: launch_nt_any<2, 4, GATHER>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stream); break;
-    case 4: launch_nt_any<2, 2, GATHER>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stream); break;
-    default: launch_nt_any<4, 1, GATHER>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stream); break;
+    case 2: return launch_nt_any<4, 2, GATHER>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, stream);
+    case 3: return launch_nt_any<2, 4, GATHER>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, stream);
+    case 4: return launch_nt_any<2, 2, GATHER>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, stream);
+    default: return launch_nt_any<4, 1, GATHER>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, stream);
   }
 }
 
-void gemm_nt_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N,
-                  int K, int cfg, int max_blocks, hipStream_t stream) {
-  nt_dispatch<false>(A, lda, B, ldb, C, ldc, M, N, K, cfg, max_blocks, ConvGeo{}, stream);
+int gemm_nt_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N,
+                 int K, int cfg, int max_blocks, float* stats, int stats_rows, hipStream_t stream) {
+  return nt_dispatch<false>(A, lda, B, ldb, C, ldc, M, N, K, cfg, max_blocks, ConvGeo{}, stats,
+                            (int64_t)stats_rows * N, stats_rows, stream);
 }
 
-void conv_nt_bf16(const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P, int KH, int KW,
-                  const void* B, void* Y, int64_t M, int N, int cfg, int max_blocks, hipStream_t stream) {
+int conv_nt_bf16(const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P, int KH, int KW,
+                 const void* B, void* Y, int64_t M, int N, int cfg, int max_blocks, float* stats, int stats_rows,
+                 hipStream_t stream) {
   ConvGeo g{static_cast<const uint16_t*>(zero), H, W, C, OH, OW, S, P, KW};
   const int K = KH * KW * C;
-  nt_dispatch<true>(X, C, B, K, Y, N, M, N, K, cfg, max_blocks, g, stream);
+  return nt_dispatch<true>(X, C, B, K, Y, N, M, N, K, cfg, max_blocks, g, stats, (int64_t)stats_rows * N, stats_rows,
+                           stream);
 }
 
 template <int WN, int WK, int WS, bool GATHER>

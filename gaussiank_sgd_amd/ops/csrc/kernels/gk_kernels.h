@@ -184,6 +184,13 @@ void bn_act_forward(const void* x, const void* res, void* y, uint8_t* mask, int6
                     float* save_mean, float* save_invstd, float* scale, float* shift, float* ws, int relu,
                     int64_t* nbt, hipStream_t stream);
 // dy2 (optional): a second upstream gradient of the same output, summed on load.
+// bn_act_forward with the batch statistics already reduced to per-row
+// partials (psum / psq: [gy][C] each), e.g. by the producing
+// convolution's epilogue (gemm_nt_bf16 / conv_nt_bf16 `stats`).
+void bn_act_forward_pre(const void* x, const void* res, void* y, uint8_t* mask, int64_t M, int C, int elem_bytes,
+                        const float* psum, const float* psq, int gy, const float* w, const float* b, float eps, float momentum,
+                        float* run_mean, float* run_var, float* save_mean, float* save_invstd, float* scale,
+                        float* shift, int relu, int64_t* nbt, hipStream_t stream);
 void bn_act_backward(const void* dy, const void* dy2, const uint8_t* mask, const void* x, void* dx, void* dres,
                      int64_t M, int C, int elem_bytes, const float* w, const float* mean, const float* invstd,
                      float* dgamma, float* dbeta, float* ws, int relu, float* gw_acc, float* gb_acc,
@@ -214,8 +221,11 @@ void bn_relu_pool_backward(const void* dy, const void* dy2, const uint8_t* amax,
 // pick the grid.
 // ---------------------------------------------------------------------------
 bool gemm_supported(int64_t N, int64_t K);
-void gemm_nt_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N,
-                  int K, int cfg, int max_blocks, hipStream_t stream);
+// stats (optional): [2][stats_rows][N] fp32 BatchNorm partials (sum, sum of
+// squares of the bf16 output) per workgroup row; returns the grid's row count
+// (the partial rows written, <= stats_rows) -- feed it to bn_act_forward_pre.
+int gemm_nt_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N,
+                 int K, int cfg, int max_blocks, float* stats, int stats_rows, hipStream_t stream);
 void gemm_tn_acc_f32(const void* G, int64_t ldg, const void* X, int64_t ldx, float* W, int64_t ldw, int64_t M,
                      int N, int K, int cfg, int splits, hipStream_t stream);
 // Implicit-GEMM KHxKW convolution (stride S, zero padding P) over NHWC bf16:
@@ -223,8 +233,9 @@ void gemm_tn_acc_f32(const void* G, int64_t ldg, const void* X, int64_t ldx, flo
 //   conv_tn_acc_f32: Wout[Cout, KH*KW*C] += G[M, Cout]^T . im2col(X)
 // Weights are channels-last ([Cout][KH][KW][C]); C % 64 == 0; `zero` points at
 // >= 64 zero bf16 (the padding row).
-void conv_nt_bf16(const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P, int KH, int KW,
-                  const void* B, void* Y, int64_t M, int N, int cfg, int max_blocks, hipStream_t stream);
+int conv_nt_bf16(const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P, int KH, int KW,
+                 const void* B, void* Y, int64_t M, int N, int cfg, int max_blocks, float* stats, int stats_rows,
+                 hipStream_t stream);
 void conv_tn_acc_f32(const void* G, const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P,
                      int KH, int KW, float* Wout, int64_t M, int N, int cfg, int splits, hipStream_t stream);
 

@@ -26,7 +26,7 @@ def _ref(x, w, dy, stride=1, padding=0):
 
 @pytest.mark.parametrize("N,C,H,K,k,s", [(4, 64, 14, 64, 3, 1), (3, 128, 9, 128, 3, 2), (2, 64, 10, 256, 1, 2),
                                          (2, 256, 7, 128, 3, 1)])
-def test_fastconv_kxk(N, C, H, K, k, s):
+def test_fastconv_kxk(N, C, H, K, k, s, hip_only):
     from gaussiank_sgd_amd.ops.conv1x1 import FastConv2d
     torch.manual_seed(N * C + K + k)
     m = FastConv2d(C, K, k, stride=s, padding=k // 2, bias=False).cuda().to(memory_format=torch.channels_last)
@@ -45,7 +45,7 @@ def test_fastconv_kxk(N, C, H, K, k, s):
 
 
 @pytest.mark.parametrize("N,C,H,K", [(4, 64, 14, 256), (3, 256, 7, 64), (2, 128, 9, 128), (8, 512, 7, 2048)])
-def test_conv1x1_plain(N, C, H, K):
+def test_conv1x1_plain(N, C, H, K, hip_only):
     from gaussiank_sgd_amd.ops.conv1x1 import Conv1x1
     torch.manual_seed(N * C + K)
     m = Conv1x1(C, K).cuda().to(memory_format=torch.channels_last)
@@ -102,3 +102,31 @@ def test_conv1x1_shadow_arena_grad():
         assert p.grad is not None, n
         err = (p.grad - q.grad).abs().max().item()
         assert err <= 2e-2 * q.grad.abs().max().item() + 1e-4, (n, err)
+
+
+@pytest.fixture
+def hip_only(monkeypatch):
+    """Force the HIP kernels (no autotune against MIOpen) for one test."""
+    from gaussiank_sgd_amd.ops import conv1x1
+    monkeypatch.setattr(conv1x1, "_TUNE", False)
+    monkeypatch.setattr(conv1x1, "_choices", {})
+
+
+@pytest.mark.parametrize("k,s,C,K", [(1, 1, 64, 256), (3, 1, 64, 64), (3, 2, 128, 128), (1, 2, 256, 512)])
+def test_conv_epilogue_bn_stats(k, s, C, K, hip_only):
+    """BatchNorm statistics reduced in the conv epilogue == the BN pass's own."""
+    from gaussiank_sgd_amd.ops.bn import BNAct
+    from gaussiank_sgd_amd.ops.conv1x1 import FastConv2d, conv_stats
+    torch.manual_seed(k * 100 + C)
+    conv = FastConv2d(C, K, k, stride=s, padding=k // 2, bias=False).cuda().to(memory_format=torch.channels_last)
+    bn_a = BNAct(K, act="relu").cuda()
+    bn_b = BNAct(K, act="relu").cuda()
+    x = torch.randn(4, C, 12, 12, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y, st = conv_stats(conv, x)
+        assert st is not None and st[1] > 0
+        out_a = bn_a(y, stats=st)
+        out_b = bn_b(y)
+    assert (out_a.float() - out_b.float()).abs().max().item() <= 2e-2
+    assert torch.allclose(bn_a.running_mean, bn_b.running_mean, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(bn_a.running_var, bn_b.running_var, rtol=1e-3, atol=1e-5)
