@@ -462,11 +462,14 @@ struct DyPool {
   }
 };
 
-template <typename T, typename Src>
+// WDZ: also store dz (the gated, twin-summed gradient -- the residual branch's
+// gradient) so the apply pass reads one tensor instead of dy, dy2 and the mask.
+template <typename T, typename Src, bool WDZ = false>
 __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(Src src, const T* __restrict__ x, int64_t M, int C, Geo g,
                                                                const float* __restrict__ mean,
                                                                const float* __restrict__ invstd,
-                                                               float* __restrict__ pdb, float* __restrict__ pdg) {
+                                                               float* __restrict__ pdb, float* __restrict__ pdg,
+                                                               T* __restrict__ dzo = nullptr) {
   constexpr int V = Vec<T>::N;
   const int tc = threadIdx.x % g.tpr;
   const int lane_r = threadIdx.x / g.tpr;
@@ -481,6 +484,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(Src src, const T*
     float d[V], xv[V];
     src.load(r, C, c0, d);
     Vec<T>::load(x + r * C + c0, xv);
+    if (WDZ) Vec<T>::store(dzo + r * C + c0, d);
 #pragma unroll
     for (int i = 0; i < V; ++i) {
       const float dz = d[i];
@@ -764,6 +768,25 @@ template <typename T>
 void bn_backward_t(const T* dy, const T* dy2, const uint8_t* mask, const T* x, T* dx, T* dres, int64_t M, int C,
                    const float* w, const float* mean, const float* invstd, float* dgamma, float* dbeta, float* ws,
                    int relu, float* gw_acc, float* gb_acc, hipStream_t s) {
+  if (dy2 && dres) {
+    // twin + residual (ResNet block output): the reduce pass writes dz = dres
+    // and the apply pass reads it back (one tensor instead of dy, dy2, mask)
+    const Geo g = make_geo<T>(M, C, kTargetBlocks);
+    float* pdb = ws;
+    float* pdg = ws + (int64_t)g.gy * C;
+#define GK_RED(R)                                                                                                  \
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, DyPlain<T, R, true>, true>), dim3(g.gx, g.gy), dim3(kBlock), 0, s,     \
+                     DyPlain<T, R, true>{dy, dy2, mask}, x, M, C, g, mean, invstd, pdb, pdg, dres)
+    if (relu) GK_RED(true);
+    else GK_RED(false);
+#undef GK_RED
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(kBlock), 0, s, pdb, pdg, g.gy, C,
+                       dbeta, dgamma, gb_acc, gw_acc);
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, DyPlain<T, false, false>, false>), dim3(g.gx, g.gy), dim3(kBlock), 0, s,
+                       DyPlain<T, false, false>{dres, nullptr, nullptr}, x, dx, (T*)nullptr, M, C, g, w, mean, invstd,
+                       dbeta, dgamma);
+    return;
+  }
 #define GK_BWD(R, TW)                                                                                              \
   bn_backward_src<T>(DyPlain<T, R, TW>{dy, dy2, mask}, x, dx, dres, M, C, w, mean, invstd, dgamma, dbeta, ws, gw_acc, \
                      gb_acc, s)
