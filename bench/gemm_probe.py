@@ -25,7 +25,13 @@ def main():
     K = a.K or a.C
     x = torch.randn(a.batch, a.C, a.H, a.H, device="cuda", dtype=torch.bfloat16).contiguous(
         memory_format=torch.channels_last)
-    if a.op == "conv":
+    if a.op == "wgrad3":
+        dy = torch.randn(a.batch, K, a.H, a.H, device="cuda", dtype=torch.bfloat16).contiguous(
+            memory_format=torch.channels_last)
+        out = torch.zeros(K, a.C, 3, 3, device="cuda").contiguous(memory_format=torch.channels_last)
+        z = torch.zeros(256, device="cuda", dtype=torch.bfloat16)
+        fn = lambda: g.conv_tn_acc(dy, x, out, z, 1, 1, a.cfg, 0)  # noqa: E731
+    elif a.op == "conv":
         w = torch.randn(K, a.C, 3, 3, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
         y = torch.empty(a.batch, K, a.H, a.H, device="cuda", dtype=torch.bfloat16).contiguous(
             memory_format=torch.channels_last)

@@ -38,7 +38,9 @@ _ENABLED = os.environ.get("GKSGD_FASTCONV", "1") != "0"
 _choices: Dict[tuple, tuple] = {}
 _timings: Dict[tuple, list] = {}      # key -> [(tag, ms or error)] of the search
 # candidate kernel configurations (gemm.hip: cfg digits = tile + 10*panel + 100*stages)
-_NT_CFGS = [0, 1, 2, 3, 4, 11, 13, 21, 22, 23, 24, 111, 113, 121, 122, 123, 124]
+_NT_CFGS = [1, 2, 3, 4, 11, 13, 21, 22, 23, 24, 111, 113, 121, 122, 123, 124]
+# grid override: 0 = persistent (about two blocks per CU), else a fixed block count
+_NT_GRIDS = (0, 512, 1 << 20)
 _TN_CFGS = [(c, s) for c in (1, 2, 3, 4, 5, 6, 7, 8, 21, 22, 23, 24, 27) for s in (0, 128)]
 _zeros: Dict[torch.device, torch.Tensor] = {}
 
@@ -165,7 +167,7 @@ def _fwd(x: torch.Tensor, w: torch.Tensor, s: int, stats_box=None) -> torch.Tens
     else:
         z = _zero(x.device)
         run = lambda c, mb: g.conv_nt(x, w, y, z, s, p, c, mb, st)  # noqa: E731
-    cands = [(("hip", c, 0), (lambda c=c: run(c, 0))) for c in _NT_CFGS]
+    cands = [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in _NT_CFGS for mb in _NT_GRIDS]
     cands.append((("miopen", 0, 0), lambda: F.conv2d(x, w, stride=s, padding=p)))
     ch = _pick(("fwd", N, C, H, W, K, k, s, st is not None), cands)
     if ch[0] == "miopen":
@@ -192,18 +194,18 @@ def _dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int) -> torch.Tensor:
         if k == 1:
             DY, DX = _rows(dy), _rows(dx)
             Wt = w.reshape(K, C).t().contiguous()
-            run = lambda c: g.gemm_nt(DY, Wt, DX, c, 0)  # noqa: E731
+            run = lambda c, mb: g.gemm_nt(DY, Wt, DX, c, mb)  # noqa: E731
         else:
             # dX = conv(dY, W') with W'[c][kh][kw][k] = W[k][KH-1-kh][KW-1-kw][c]
             wf = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=_CL)
             z = _zero(dy.device)
-            run = lambda c: g.conv_nt(dy, wf, dx, z, 1, p, c, 0)  # noqa: E731
-        cands = [(("hip", c, 0), (lambda c=c: run(c))) for c in _NT_CFGS]
+            run = lambda c, mb: g.conv_nt(dy, wf, dx, z, 1, p, c, mb)  # noqa: E731
+        cands = [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in _NT_CFGS for mb in _NT_GRIDS]
     cands.append((("miopen", 0, 0), miopen))
     ch = _pick(("dgrad", N, C, H, W, K, k, s), cands)
     if ch[0] == "miopen":
         return miopen().contiguous(memory_format=_CL)
-    run(ch[1])
+    run(ch[1], ch[2])
     return dx
 
 

@@ -676,6 +676,7 @@ void conv_tn_acc(at::Tensor dy, at::Tensor x, at::Tensor wout, at::Tensor zero, 
                   C % 64 == 0 && Co % 64 == 0,
               "conv_tn_acc: x must be channels-last bf16 with C, Cout % 64 == 0");
   TORCH_CHECK(zero.is_cuda() && zero.scalar_type() == at::kBFloat16 && zero.numel() >= 64, "conv_tn_acc: zero");
+  TORCH_CHECK(x.numel() < (int64_t(1) << 31), "conv_tn_acc: x too large for 32-bit gather offsets");
   const int64_t OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
   TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 &&
                   dy.is_contiguous(at::MemoryFormat::ChannelsLast) && dy.size(0) == N && dy.size(1) == Co &&

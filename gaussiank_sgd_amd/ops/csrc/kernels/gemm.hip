@@ -115,6 +115,8 @@ struct NtCfg {
   static constexpr int INSTS = STAGE / 1024;      // 1-KiB LDS-DMA instructions per stage
   static_assert(INSTS % NW == 0, "stage split");
   static constexpr int LPW = INSTS / NW;          // LDS-DMA instructions per wave per stage
+  static_assert((BM / 8) % NW == 0, "A rows split evenly over the waves");
+  static constexpr int LPWA = BRES ? LPW : (BM / 8) / NW;   // of which A-row instructions (j < LPWA)
   static constexpr int NST = 8;                   // 16-byte epilogue stores per wave per tile
   static_assert(LPW + 2 * NST <= 40, "wait_vmcnt range");
   static int lds_bytes(int K, int ns) { return ns * STAGE + (BRES ? BN * K * 2 : 0); }
@@ -173,7 +175,7 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
     const int i = wave + j * Cfg::NW;
     const int r = i * 8 + (lane >> 3);
     const int c = (lane & 7) ^ swz(r);
-    ptr[j] = (BRES || i * 8 < Cfg::BM) ? nullptr : B + (int64_t)(n0 + r - Cfg::BM) * ldb + c * 8;
+    ptr[j] = j < Cfg::LPWA ? nullptr : B + (int64_t)(n0 + r - Cfg::BM) * ldb + c * 8;
     ih0[j] = iw0[j] = 0;
   }
   auto set_rows = [&](int64_t mt) {
@@ -181,7 +183,7 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
 #pragma unroll
     for (int j = 0; j < LPW; ++j) {
       const int i = wave + j * Cfg::NW;
-      if (BRES || i * 8 < Cfg::BM) {
+      if (j < Cfg::LPWA) {
         const int r = i * 8 + (lane >> 3);
         const int c = (lane & 7) ^ swz(r);
         int64_t gr = m0 + r;
@@ -213,7 +215,7 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
     for (int j = 0; j < LPW; ++j) {
       const int i = wave + j * Cfg::NW;
       const uint16_t* src;
-      if (BRES || i * 8 < Cfg::BM) {
+      if (j < Cfg::LPWA) {
         if (GATHER) {
           const int ih = ih0[j] + s_kh, iw = iw0[j] + s_kw;
           const bool ok = (unsigned)ih < (unsigned)geo.H && (unsigned)iw < (unsigned)geo.W;
@@ -439,6 +441,8 @@ struct TnCfg {
   static_assert(INSTS % NW == 0, "stage split");
   static constexpr int LPW = INSTS / NW;
   static_assert(LPW <= 40, "wait_vmcnt range");
+  static_assert(GINSTS % NW == 0, "G rows split evenly over the waves");
+  static constexpr int LPWG = GINSTS / NW;           // G-row instructions per wave (j < LPWG)
   static_assert((WS - 1) * WN * WK * 16384 <= LDS, "reduction scratch");
 };
 
@@ -495,73 +499,86 @@ gemm_tn_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __re
   if (mbeg >= mend) return;
   const int T = (int)((mend - mbeg + Cfg::ROWS - 1) / Cfg::ROWS);
 
-  // per-lane staging setup (constant over stages): staged row, global column offset
-  int srow[LPW];
-  int64_t scol[LPW];
-  int dkh[LPW], dkw[LPW];
+  // Per-lane staging state, set up once and advanced by ROWS pixel rows per
+  // stage (no per-stage divisions or 64-bit multiplies): G / plain-X
+  // instructions keep a row pointer; gathered X instructions keep the output
+  // pixel (n, oh, ow) and their tap (dkh, dkw).
+  const uint16_t* rptr[LPW];     // current row pointer (G / plain X)
+  const uint16_t* rlast[LPW];    // row M-1 (clamp target past the end)
+  int64_t row[LPW];              // current pixel row index
+  int pn[LPW], poh[LPW], pow_[LPW], dkh[LPW], dkw[LPW], ccol[LPW];
 #pragma unroll
   for (int j = 0; j < LPW; ++j) {
     const int i = wave + j * Cfg::NW;
+    int srow, colo;
+    bool gath = false;
     dkh[j] = dkw[j] = 0;
-    if (i < Cfg::GINSTS) {
+    if (j < Cfg::LPWG) {
       constexpr int CPR = Cfg::GROW / 16;
       const int e = i * 64 + lane;
-      srow[j] = e / CPR;
-      scol[j] = n0 + ((e % CPR) ^ tr_swz<Cfg::GROW>(srow[j])) * 8;
+      srow = e / CPR;
+      colo = n0 + ((e % CPR) ^ tr_swz<Cfg::GROW>(srow)) * 8;
+      rptr[j] = G + (mbeg + srow) * ldg + colo;
+      rlast[j] = G + (M - 1) * ldg + colo;
     } else {
       constexpr int CPR = Cfg::XROW / 16;
       const int e = (i - Cfg::GINSTS) * 64 + lane;
-      srow[j] = e / CPR;
-      const int ch = (e % CPR) ^ tr_swz<Cfg::XROW>(srow[j]);
+      srow = e / CPR;
+      const int ch = (e % CPR) ^ tr_swz<Cfg::XROW>(srow);
       if (GATHER) {
         const int k0 = c0 + (ch >> 3) * 64;          // 64-channel slice of one tap
         const int tap = k0 / geo.C;
         dkh[j] = tap / geo.KW;
         dkw[j] = tap - dkh[j] * geo.KW;
-        scol[j] = (k0 - tap * geo.C) + (ch & 7) * 8;
+        colo = (k0 - tap * geo.C) + (ch & 7) * 8;
+        gath = true;
       } else {
-        scol[j] = c0 + ch * 8;
+        colo = c0 + ch * 8;
       }
+      rptr[j] = X + (mbeg + srow) * ldx + colo;
+      rlast[j] = X + (M - 1) * ldx + colo;
+    }
+    row[j] = mbeg + srow;
+    ccol[j] = colo;
+    pn[j] = poh[j] = pow_[j] = 0;
+    if (GATHER && gath) {
+      const int64_t m = mbeg + srow;
+      const int64_t ohw = (int64_t)geo.OH * geo.OW;
+      pn[j] = (int)(m / ohw);
+      const int rem = (int)(m - (int64_t)pn[j] * ohw);
+      poh[j] = rem / geo.OW;
+      pow_[j] = rem - poh[j] * geo.OW;
     }
   }
-  const float rcp_ow = GATHER ? 1.0f / (float)geo.OW : 0.f;
-  const float rcp_oh = GATHER ? 1.0f / (float)geo.OH : 0.f;
+  const int adv_q = Cfg::ROWS / (GATHER ? geo.OW : 1), adv_r = Cfg::ROWS - adv_q * (GATHER ? geo.OW : 1);
+  const int64_t gstep = (int64_t)Cfg::ROWS * ldg, xstep = (int64_t)Cfg::ROWS * ldx;
 
   auto stage = [&](int t) {
-    const int64_t m0 = mbeg + (int64_t)t * Cfg::ROWS;
     GK_LDS char* base = (GK_LDS char*)smem + (t % NS) * Cfg::STAGE;
-    uint32_t n_s = 0, oh_s = 0, ow_s = 0;
-    if (GATHER) {   // pixel of the stage's first row (wave-uniform)
-      const uint32_t ohw = (uint32_t)(geo.OH * geo.OW);
-      const uint32_t mu = (uint32_t)m0;
-      n_s = mu / ohw;
-      const uint32_t rem = mu - n_s * ohw;
-      oh_s = rem / (uint32_t)geo.OW;
-      ow_s = rem - oh_s * (uint32_t)geo.OW;
-    }
 #pragma unroll
     for (int j = 0; j < LPW; ++j) {
       const int i = wave + j * Cfg::NW;
-      int64_t gr = m0 + srow[j];
-      const bool in = gr < M;
-      gr = in ? gr : M - 1;
+      const bool in = row[j] < M;
       const uint16_t* src;
-      if (i < Cfg::GINSTS) {
-        src = G + gr * ldg + scol[j];
+      if (j < Cfg::LPWG) {
+        src = in ? rptr[j] : rlast[j];
+        rptr[j] += gstep;
       } else if (GATHER) {
-        const uint32_t idx = ow_s + (uint32_t)srow[j];
-        const uint32_t q1 = udiv_small(idx, (uint32_t)geo.OW, rcp_ow);
-        const uint32_t ow = idx - q1 * (uint32_t)geo.OW;
-        const uint32_t t2 = oh_s + q1;
-        const uint32_t q2 = udiv_small(t2, (uint32_t)geo.OH, rcp_oh);
-        const uint32_t oh = t2 - q2 * (uint32_t)geo.OH;
-        const uint32_t n = n_s + q2;
-        const int ih = (int)oh * geo.S - geo.P + dkh[j], iw = (int)ow * geo.S - geo.P + dkw[j];
+        const int ih = poh[j] * geo.S - geo.P + dkh[j], iw = pow_[j] * geo.S - geo.P + dkw[j];
         const bool ok = in && (unsigned)ih < (unsigned)geo.H && (unsigned)iw < (unsigned)geo.W;
-        src = ok ? X + (((int64_t)n * geo.H + ih) * geo.W + iw) * geo.C + scol[j] : geo.zero + (scol[j] & 63);
+        const uint32_t off = (((uint32_t)pn[j] * (uint32_t)geo.H + (uint32_t)ih) * (uint32_t)geo.W + (uint32_t)iw) *
+                                 (uint32_t)geo.C + (uint32_t)ccol[j];
+        src = ok ? X + off : geo.zero + (ccol[j] & 63);
+        // advance the pixel by ROWS
+        pow_[j] += adv_r;
+        poh[j] += adv_q;
+        if (pow_[j] >= geo.OW) { pow_[j] -= geo.OW; ++poh[j]; }
+        while (poh[j] >= geo.OH) { poh[j] -= geo.OH; ++pn[j]; }
       } else {
-        src = X + gr * ldx + scol[j];
+        src = in ? rptr[j] : rlast[j];
+        rptr[j] += xstep;
       }
+      row[j] += Cfg::ROWS;
       glds16(src, base + i * 1024);
     }
   };

@@ -16,3 +16,17 @@ for set in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
   echo "rc=$?"
   tail -2 $OUT/p$i.log
 done
+python3 - <<'PY'
+import csv, collections, glob
+for f in sorted(glob.glob("gpurun_out/ctr/p*/run_counter_collection.csv")):
+    rows = [r for r in csv.DictReader(open(f)) if "gemm_" in r["Kernel_Name"]]
+    if not rows:
+        continue
+    d = collections.defaultdict(float)
+    for r in rows:
+        d[r["Counter_Name"]] += float(r["Counter_Value"])
+    nd = len(set(r["Dispatch_Id"] for r in rows))
+    print(f, rows[0]["Kernel_Name"][:90])
+    for k, v in sorted(d.items()):
+        print("   %-28s %14.0f" % (k, v / nd))
+PY
