@@ -11,6 +11,9 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
+from ..ops.bn import BNAct
+from ..ops.conv1x1 import FastConv2d
+
 cfg = {
     "VGG11": [64, "M", 128, "M", 256, 256, "M", 512, 512, "M", 512, 512, "M"],
     "VGG13": [64, 64, "M", 128, 128, "M", 256, 256, "M", 512, 512, "M", 512, 512, "M"],
@@ -21,16 +24,25 @@ cfg = {
 
 
 def _features(spec, batch_norm: bool) -> nn.Sequential:
+    """conv -> [BN] -> ReLU [-> MaxPool], the reference's layer order and
+    state_dict indices.  MI355X: convolutions are FastConv2d (autotuned MFMA
+    implicit GEMM vs MIOpen); with batch norm, BN + ReLU (+ the following 2x2
+    max-pool) run as ONE fused BNAct pass and the ReLU / pool slots hold
+    nn.Identity (no parameters, so the indices and keys are unchanged)."""
     layers = []
     c = 3
-    for v in spec:
+    for i, v in enumerate(spec):
         if v == "M":
-            layers.append(nn.MaxPool2d(kernel_size=2, stride=2))
+            fused = batch_norm and i > 0 and spec[i - 1] != "M"
+            layers.append(nn.Identity() if fused else nn.MaxPool2d(kernel_size=2, stride=2))
         else:
-            layers.append(nn.Conv2d(c, v, kernel_size=3, padding=1))
+            layers.append(FastConv2d(c, v, kernel_size=3, padding=1))
             if batch_norm:
-                layers.append(nn.BatchNorm2d(v))
-            layers.append(nn.ReLU(inplace=True))
+                pool = (2, 2, 0) if i + 1 < len(spec) and spec[i + 1] == "M" else None
+                layers.append(BNAct(v, act="relu", pool=pool))
+                layers.append(nn.Identity())
+            else:
+                layers.append(nn.ReLU(inplace=True))
             c = v
     return nn.Sequential(*layers)
 

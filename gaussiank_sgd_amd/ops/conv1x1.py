@@ -131,7 +131,7 @@ def supported(x: torch.Tensor, conv: nn.Conv2d) -> bool:
     return (_ENABLED and x.is_cuda and x.dim() == 4 and k[0] == k[1] and k[0] in (1, 3) and
             conv.stride[0] == conv.stride[1] and conv.stride[0] in (1, 2) and
             conv.padding == (k[0] // 2, k[0] // 2) and conv.dilation == (1, 1) and conv.groups == 1 and
-            conv.bias is None and conv.padding_mode == "zeros" and x.is_contiguous(memory_format=_CL) and
+            conv.padding_mode == "zeros" and x.is_contiguous(memory_format=_CL) and
             conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0 and x.numel() > 0)
 
 
@@ -149,7 +149,7 @@ def _geom(x_shape, w: torch.Tensor, s: int):
     return N, C, H, W, K, k, p, OH, OW
 
 
-def _fwd(x: torch.Tensor, w: torch.Tensor, s: int, stats_box=None) -> torch.Tensor:
+def _fwd(x: torch.Tensor, w: torch.Tensor, s: int, stats_box=None, bias=None) -> torch.Tensor:
     """y = conv(x, w).  With ``stats_box`` (a list) and the HIP kernel chosen,
     the kernel's epilogue also reduces the BatchNorm batch statistics of y
     and ``(partials [2, rows_max, K], rows)`` is appended to the box
@@ -163,15 +163,16 @@ def _fwd(x: torch.Tensor, w: torch.Tensor, s: int, stats_box=None) -> torch.Tens
         st = torch.empty(2, min(1280, (M + 63) // 64), K, dtype=torch.float32, device=x.device)
     if k == 1 and s == 1:
         X, Y, Wm = _rows(x), _rows(y), w.reshape(K, C)
-        run = lambda c, mb: g.gemm_nt(X, Wm, Y, c, mb, st)  # noqa: E731
+        run = lambda c, mb: g.gemm_nt(X, Wm, Y, c, mb, st, bias)  # noqa: E731
     else:
         z = _zero(x.device)
-        run = lambda c, mb: g.conv_nt(x, w, y, z, s, p, c, mb, st)  # noqa: E731
+        run = lambda c, mb: g.conv_nt(x, w, y, z, s, p, c, mb, st, bias)  # noqa: E731
+    b16 = bias.to(torch.bfloat16) if bias is not None else None
     cands = [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in _NT_CFGS for mb in _NT_GRIDS]
-    cands.append((("miopen", 0, 0), lambda: F.conv2d(x, w, stride=s, padding=p)))
+    cands.append((("miopen", 0, 0), lambda: F.conv2d(x, w, b16, stride=s, padding=p)))
     ch = _pick(("fwd", N, C, H, W, K, k, s, st is not None), cands)
     if ch[0] == "miopen":
-        return F.conv2d(x, w, stride=s, padding=p).contiguous(memory_format=_CL)
+        return F.conv2d(x, w, b16, stride=s, padding=p).contiguous(memory_format=_CL)
     rows = run(ch[1], ch[2])
     if st is not None:
         stats_box.append((st, int(rows)))
@@ -241,14 +242,17 @@ class _FastConvFn(torch.autograd.Function):
     fp32 arena in the backward and None is returned for it."""
 
     @staticmethod
-    def forward(ctx, x, param, w_bf16, sink, stride, stats_box=None):
+    def forward(ctx, x, param, w_bf16, sink, stride, stats_box=None, bias=None, bias_sink=None):
         if x.dtype != torch.bfloat16:
             x = x.to(torch.bfloat16)
         x = x.contiguous(memory_format=_CL)
         w = w_bf16 if w_bf16 is not None else param.detach().to(torch.bfloat16)
         w = w.contiguous(memory_format=_CL)
-        y = _fwd(x, w, stride, stats_box)
+        b = bias.detach().float().contiguous() if bias is not None else None
+        y = _fwd(x, w, stride, stats_box, b)
         ctx.sink = sink
+        ctx.bias_sink = bias_sink
+        ctx.has_bias = bias is not None
         ctx.stride = stride
         ctx.param_dtype = param.dtype
         ctx.save_for_backward(x, w)
@@ -274,7 +278,15 @@ class _FastConvFn(torch.autograd.Function):
                     sink(out)
                 else:
                     gparam = out.to(ctx.param_dtype)
-        return dx, gparam, None, None, None, None
+        gbias = None
+        if ctx.has_bias and ctx.needs_input_grad[6]:
+            db = dy.sum(dim=(0, 2, 3), dtype=torch.float32)
+            bs = ctx.bias_sink
+            if bs is not None:
+                bs(db)          # into the optimizer's fp32 arena (shadow path)
+            else:
+                gbias = db
+        return dx, gparam, None, None, None, None, gbias, None
 
 
 class FastConv2d(nn.Conv2d):
@@ -299,11 +311,15 @@ class FastConv2d(nn.Conv2d):
         if bf16 and supported(x, self) and load():
             table = getattr(self, "_gk_shadow", None)
             info = table.get("weight") if table else None
+            binfo = table.get("bias") if table else None
             use_shadow = info is not None and torch.is_autocast_enabled(dev)
             w_bf16, sink = (info[0], info[1]) if use_shadow else (None, None)
+            bsink = binfo[1] if (use_shadow and binfo is not None) else None
             if not torch.is_grad_enabled() or not self.weight.requires_grad:
                 sink = None
-            return _FastConvFn.apply(x, self.weight, w_bf16, sink, self.stride[0], box)
+            if not torch.is_grad_enabled() or self.bias is None or not self.bias.requires_grad:
+                bsink = None
+            return _FastConvFn.apply(x, self.weight, w_bf16, sink, self.stride[0], box, self.bias, bsink)
         slow = getattr(self, "_gk_slow", None)
         return slow(x) if slow is not None else super().forward(x)
 

@@ -599,8 +599,15 @@ float* stats_ptr(const c10::optional<at::Tensor>& st, int64_t N, int* rows) {
 }
 
 // C[M, N] = A[M, K] . B[N, K]^T
+const float* bias_ptr(const c10::optional<at::Tensor>& b, int64_t N) {
+  if (!b.has_value() || !b->defined()) return nullptr;
+  TORCH_CHECK(b->is_cuda() && b->scalar_type() == at::kFloat && b->is_contiguous() && b->numel() == N,
+              "bias must be a contiguous fp32 [N] GPU tensor");
+  return b->data_ptr<float>();
+}
+
 int64_t gemm_nt(at::Tensor A, at::Tensor B, at::Tensor C, int64_t cfg, int64_t max_blocks,
-                c10::optional<at::Tensor> stats) {
+                c10::optional<at::Tensor> stats, c10::optional<at::Tensor> bias) {
   check_rows(A, "A");
   check_rows(B, "B");
   check_rows(C, "C");
@@ -612,7 +619,7 @@ int64_t gemm_nt(at::Tensor A, at::Tensor B, at::Tensor C, int64_t cfg, int64_t m
   float* sp = stats_ptr(stats, N, &rows);
   c10::DeviceGuard guard(A.device());
   return gk::gemm_nt_bf16(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), M, (int)N,
-                          (int)K, (int)cfg, (int)max_blocks, sp, rows, cur_stream(A));
+                          (int)K, (int)cfg, (int)max_blocks, sp, rows, bias_ptr(bias, N), cur_stream(A));
 }
 
 // W[N, K] += G[M, N]^T . X[M, K]   (fp32 W, float atomics)
@@ -645,7 +652,7 @@ void check_conv(const at::Tensor& x, const at::Tensor& w, const at::Tensor& zero
 }
 
 int64_t conv_nt(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor zero, int64_t stride, int64_t pad, int64_t cfg,
-                int64_t max_blocks, c10::optional<at::Tensor> stats) {
+                int64_t max_blocks, c10::optional<at::Tensor> stats, c10::optional<at::Tensor> bias) {
   check_conv(x, w, zero);
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
   const int64_t Co = w.size(0), KH = w.size(2), KW = w.size(3);
@@ -661,7 +668,7 @@ int64_t conv_nt(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor zero, int64
   c10::DeviceGuard guard(x.device());
   return gk::conv_nt_bf16(x.data_ptr(), zero.data_ptr(), (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)stride,
                           (int)pad, (int)KH, (int)KW, w.data_ptr(), y.data_ptr(), M, (int)Co, (int)cfg, (int)max_blocks,
-                          sp, rows, cur_stream(x));
+                          sp, rows, bias_ptr(bias, Co), cur_stream(x));
 }
 
 // wout: fp32 [Cout, C, KH, KW] channels-last (memory [Cout][KH][KW][C]); += dW
@@ -744,10 +751,11 @@ TORCH_LIBRARY(gksgd, m) {
   m.def("mask_records(Tensor(a!) u, Tensor record, int k_cap) -> ()");
   m.def("cast_bf16(Tensor(a!) dst, Tensor src) -> ()");
   m.def("gemm_supported(int N, int K) -> bool", &gemm_supported);
-  m.def("gemm_nt(Tensor A, Tensor B, Tensor(a!) C, int cfg=0, int max_blocks=0, Tensor(b!)? stats=None) -> int");
+  m.def("gemm_nt(Tensor A, Tensor B, Tensor(a!) C, int cfg=0, int max_blocks=0, Tensor(b!)? stats=None, "
+        "Tensor? bias=None) -> int");
   m.def("gemm_tn_acc(Tensor G, Tensor X, Tensor(a!) W, int cfg=0, int splits=0) -> ()");
   m.def("conv_nt(Tensor x, Tensor w, Tensor(a!) y, Tensor zero, int stride, int pad, int cfg=0, int max_blocks=0, "
-        "Tensor(b!)? stats=None) -> int");
+        "Tensor(b!)? stats=None, Tensor? bias=None) -> int");
   m.def("conv_tn_acc(Tensor dy, Tensor x, Tensor(a!) wout, Tensor zero, int stride, int pad, int cfg=0, int splits=0) -> ()");
 
   m.class_<RcclEngine>("RcclEngine")

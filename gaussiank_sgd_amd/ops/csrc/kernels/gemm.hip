@@ -81,6 +81,7 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 struct ConvGeo {
   const uint16_t* zero;   // >= 64 zero bf16
   int H, W, C, OH, OW, S, P, KW;
+  const float* bias;      // optional per-output-channel bias (gemm_nt / conv_nt epilogue)
 };
 
 __device__ __forceinline__ const uint16_t* conv_row(const uint16_t* X, const ConvGeo& g, int64_t m, int k0,
@@ -261,10 +262,14 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
   int ks = 0;
   int buf = 0;
   float ssum[4][4], ssq[4][4];   // BN partials: [ns][r] of this lane's column, summed over its rows
+  float bia[4][4];               // bias of this lane's columns
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) ssum[a][b] = ssq[a][b] = 0.f;
+    for (int b = 0; b < 4; ++b) {
+      ssum[a][b] = ssq[a][b] = 0.f;
+      bia[a][b] = geo.bias ? geo.bias[n0 + wn * 64 + a * 16 + fq * 4 + b] : 0.f;
+    }
   int64_t mt = blockIdx.x;
   for (int t = 0; t < T; ++t) {
     // ops issued after stage(t), in order: NS=2: stores(t-1);
@@ -311,8 +316,10 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
 #pragma unroll
         for (int pr = 0; pr < 2; ++pr) {
           const f32x4 va = acc[ms][2 * pr], vb = acc[ms][2 * pr + 1];
-          const uint32_t a0 = pack_bf16x2(va[0], va[1]), a1 = pack_bf16x2(va[2], va[3]);
-          const uint32_t b0 = pack_bf16x2(vb[0], vb[1]), b1 = pack_bf16x2(vb[2], vb[3]);
+          const float* ba = bia[2 * pr];
+          const float* bb = bia[2 * pr + 1];
+          const uint32_t a0 = pack_bf16x2(va[0] + ba[0], va[1] + ba[1]), a1 = pack_bf16x2(va[2] + ba[2], va[3] + ba[3]);
+          const uint32_t b0 = pack_bf16x2(vb[0] + bb[0], vb[1] + bb[1]), b1 = pack_bf16x2(vb[2] + bb[2], vb[3] + bb[3]);
           if (stats && (full || m < M)) {   // statistics of the values as stored (bf16)
             const uint32_t pk[4] = {a0, a1, b0, b1};
 #pragma unroll
@@ -717,15 +724,17 @@ int nt_dispatch(const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
 }
 
 int gemm_nt_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N,
-                 int K, int cfg, int max_blocks, float* stats, int stats_rows, hipStream_t stream) {
-  return nt_dispatch<false>(A, lda, B, ldb, C, ldc, M, N, K, cfg, max_blocks, ConvGeo{}, stats,
-                            (int64_t)stats_rows * N, stats_rows, stream);
+                 int K, int cfg, int max_blocks, float* stats, int stats_rows, const float* bias, hipStream_t stream) {
+  ConvGeo g{};
+  g.bias = bias;
+  return nt_dispatch<false>(A, lda, B, ldb, C, ldc, M, N, K, cfg, max_blocks, g, stats, (int64_t)stats_rows * N,
+                            stats_rows, stream);
 }
 
 int conv_nt_bf16(const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P, int KH, int KW,
                  const void* B, void* Y, int64_t M, int N, int cfg, int max_blocks, float* stats, int stats_rows,
-                 hipStream_t stream) {
-  ConvGeo g{static_cast<const uint16_t*>(zero), H, W, C, OH, OW, S, P, KW};
+                 const float* bias, hipStream_t stream) {
+  ConvGeo g{static_cast<const uint16_t*>(zero), H, W, C, OH, OW, S, P, KW, bias};
   const int K = KH * KW * C;
   return nt_dispatch<true>(X, C, B, K, Y, N, M, N, K, cfg, max_blocks, g, stats, (int64_t)stats_rows * N, stats_rows,
                            stream);
@@ -774,7 +783,7 @@ void gemm_tn_acc_f32(const void* G, int64_t ldg, const void* X, int64_t ldx, flo
 
 void conv_tn_acc_f32(const void* G, const void* X, const void* zero, int H, int W_, int C, int OH, int OW, int S, int P,
                      int KH, int KW, float* Wout, int64_t M, int N, int cfg, int splits, hipStream_t stream) {
-  ConvGeo g{static_cast<const uint16_t*>(zero), H, W_, C, OH, OW, S, P, KW};
+  ConvGeo g{static_cast<const uint16_t*>(zero), H, W_, C, OH, OW, S, P, KW, nullptr};
   const int K = KH * KW * C;
   tn_dispatch<true>(G, N, X, C, Wout, K, M, N, K, cfg, splits, g, stream);
 }

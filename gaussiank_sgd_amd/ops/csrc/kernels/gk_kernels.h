@@ -224,8 +224,9 @@ bool gemm_supported(int64_t N, int64_t K);
 // stats (optional): [2][stats_rows][N] fp32 BatchNorm partials (sum, sum of
 // squares of the bf16 output) per workgroup row; returns the grid's row count
 // (the partial rows written, <= stats_rows) -- feed it to bn_act_forward_pre.
+// bias (optional): fp32 [N] added in the epilogue (before rounding and statistics)
 int gemm_nt_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N,
-                 int K, int cfg, int max_blocks, float* stats, int stats_rows, hipStream_t stream);
+                 int K, int cfg, int max_blocks, float* stats, int stats_rows, const float* bias, hipStream_t stream);
 void gemm_tn_acc_f32(const void* G, int64_t ldg, const void* X, int64_t ldx, float* W, int64_t ldw, int64_t M,
                      int N, int K, int cfg, int splits, hipStream_t stream);
 // Implicit-GEMM KHxKW convolution (stride S, zero padding P) over NHWC bf16:
@@ -235,7 +236,7 @@ void gemm_tn_acc_f32(const void* G, int64_t ldg, const void* X, int64_t ldx, flo
 // >= 64 zero bf16 (the padding row).
 int conv_nt_bf16(const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P, int KH, int KW,
                  const void* B, void* Y, int64_t M, int N, int cfg, int max_blocks, float* stats, int stats_rows,
-                 hipStream_t stream);
+                 const float* bias, hipStream_t stream);
 void conv_tn_acc_f32(const void* G, const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P,
                      int KH, int KW, float* Wout, int64_t M, int N, int cfg, int splits, hipStream_t stream);
 

@@ -84,12 +84,16 @@ def install_bf16_shadow(model: nn.Module, opt) -> int:
             # its own forward reads the shadow view and (GEMM path) adds the fp32
             # weight gradient straight into the arena; other strides fall back
             # to the plain shadow conv
-            p = mod.weight
-            if p in names:
-                key = names[p]
-                mod._gk_shadow = {"weight": (arena.view_of(shadow, key), opt._make_sink(key))}
+            table = {}
+            for pname in ("weight", "bias"):
+                p = getattr(mod, pname, None)
+                if p is not None and p in names:
+                    key = names[p]
+                    table[pname] = (arena.view_of(shadow, key), opt._make_sink(key))
+                    count += 1
+            if table:
+                mod._gk_shadow = table
                 mod._gk_slow = types.MethodType(_conv_forward, mod)
-                count += 1
         elif isinstance(mod, (nn.Conv2d, nn.Linear)) and type(mod).forward in (nn.Conv2d.forward, nn.Linear.forward):
             table = {}
             for pname in ("weight", "bias"):

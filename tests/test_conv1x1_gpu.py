@@ -130,3 +130,26 @@ def test_conv_epilogue_bn_stats(k, s, C, K, hip_only):
     assert (out_a.float() - out_b.float()).abs().max().item() <= 2e-2
     assert torch.allclose(bn_a.running_mean, bn_b.running_mean, rtol=1e-4, atol=1e-5)
     assert torch.allclose(bn_a.running_var, bn_b.running_var, rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.parametrize("k,s", [(3, 1), (1, 1), (3, 2)])
+def test_fastconv_bias(k, s, hip_only):
+    """Conv bias added in the GEMM epilogue; its gradient = sum of dY."""
+    from gaussiank_sgd_amd.ops.conv1x1 import FastConv2d
+    torch.manual_seed(k + s)
+    m = FastConv2d(64, 128, k, stride=s, padding=k // 2, bias=True).cuda().to(memory_format=torch.channels_last)
+    torch.nn.init.uniform_(m.bias, -1.0, 1.0)
+    x = torch.randn(3, 64, 10, 10, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = m(x)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_(True)
+    wr = m.weight.detach().to(torch.bfloat16).float().requires_grad_(True)
+    br = m.bias.detach().float().requires_grad_(True)
+    yr = F.conv2d(xr, wr, br, stride=s, padding=k // 2)
+    yr.backward(dy.float())
+    assert (y.float() - yr).abs().max().item() <= 1e-2 * yr.abs().max().item() + 1e-2
+    assert (m.bias.grad - br.grad).abs().max().item() <= 1e-3 * br.grad.abs().max().item() + 1e-3
+    assert (x.grad.float() - xr.grad).abs().max().item() <= 1e-2 * xr.grad.abs().max().item() + 1e-3
