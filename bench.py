@@ -71,6 +71,8 @@ def parse():
                          "(BASELINE config: GaussianK k=0.1%% + momentum correction)")
     ap.add_argument("--no-shadow", action="store_true",
                     help="disable bf16 shadow weights / direct arena gradients (plain autocast)")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture the whole training step in a HIP graph and replay it (train/graph.py)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -141,6 +143,12 @@ def main() -> int:
             opt.clip_grad_norm_(clip)
         trainer.update_model()
 
+    if args.graph:
+        # whole-step HIP graph: capture after the eager warm-up, replay in the timed loop
+        from gaussiank_sgd_amd.train.graph import GraphedStep
+        for _ in range(args.warmup):
+            step()
+        step = GraphedStep(trainer, opt, clip)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -193,7 +201,9 @@ def main() -> int:
             "buckets": len(opt.arena.buckets),
             "exchange": opt._exchanger.kind if opt._exchanger is not None else "none",
             "momentum_correction": bool(opt._mc),
+            "hip_graph": bool(args.graph),
         },
+        "graph_captures": getattr(step, "captures", None),
         "effective_compression_ratio": round(ratio, 1),
         "selected_per_step": round(sel, 1),
         "params": nparams,

@@ -5,6 +5,12 @@ Parity: reference models/resnet.py:40-147 (option-A shortcut
 models/res_utils.py:4-13; uniform(-1/sqrt(n), 1/sqrt(n)) conv init) and
 models/preresnet.py.  ResNet-20 has 269,722 parameters in 59 tensors
 (the configuration of every published reference log).
+
+MI355X: every BatchNorm is a ``BNAct`` (ops/bn.py) -- BN + ReLU (+ the
+residual add of the block output) run as fused channels-last kernels, and a
+block output that feeds both the next block and its shortcut hands out two
+handles whose gradients are summed inside the BN backward (``twin``).  Same
+parameters and state_dict keys as nn.BatchNorm2d.
 """
 from __future__ import annotations
 
@@ -14,6 +20,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 from torch.nn import init
+
+from ..ops.bn import BNAct
 
 
 class DownsampleA(nn.Module):
@@ -35,16 +43,16 @@ class ResNetBasicblock(nn.Module):
     def __init__(self, inplanes, planes, stride=1, downsample=None):
         super().__init__()
         self.conv_a = nn.Conv2d(inplanes, planes, 3, stride=stride, padding=1, bias=False)
-        self.bn_a = nn.BatchNorm2d(planes)
+        self.bn_a = BNAct(planes, act="relu")
         self.conv_b = nn.Conv2d(planes, planes, 3, stride=1, padding=1, bias=False)
-        self.bn_b = nn.BatchNorm2d(planes)
+        self.bn_b = BNAct(planes, act="relu")       # relu(bn_b(conv_b) + residual), fused
         self.downsample = downsample
 
     def forward(self, x):
-        residual = x if self.downsample is None else self.downsample(x)
-        out = F.relu(self.bn_a(self.conv_a(x)), inplace=True)
-        out = self.bn_b(self.conv_b(out))
-        return F.relu(residual + out, inplace=True)
+        x, xs = x if isinstance(x, tuple) else (x, x)   # (main, shortcut) handles of a twin BN output
+        residual = xs if self.downsample is None else self.downsample(xs)
+        out = self.bn_a(self.conv_a(x))
+        return self.bn_b(self.conv_b(out), residual)
 
 
 class CifarResNet(nn.Module):
@@ -55,7 +63,7 @@ class CifarResNet(nn.Module):
         n = (depth - 2) // 6
         self.num_classes = num_classes
         self.conv_1_3x3 = nn.Conv2d(3, 16, 3, stride=1, padding=1, bias=False)
-        self.bn_1 = nn.BatchNorm2d(16)
+        self.bn_1 = BNAct(16, act="relu")
         self.inplanes = 16
         self.stage_1 = self._make_layer(16, n, 1)
         self.stage_2 = self._make_layer(32, n, 2)
@@ -73,6 +81,10 @@ class CifarResNet(nn.Module):
             elif isinstance(m, nn.Linear):
                 init.kaiming_normal_(m.weight)
                 m.bias.data.zero_()
+        blocks = [b for st in (self.stage_1, self.stage_2, self.stage_3) for b in st]
+        self.bn_1.twin = True
+        for b in blocks[:-1]:
+            b.bn_b.twin = True
 
     def _make_layer(self, planes, blocks, stride):
         downsample = None
@@ -85,7 +97,7 @@ class CifarResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = F.relu(self.bn_1(self.conv_1_3x3(x)), inplace=True)
+        x = self.bn_1(self.conv_1_3x3(x))
         x = self.stage_3(self.stage_2(self.stage_1(x)))
         x = self.avgpool(x)
         return self.classifier(x.reshape(x.shape[0], -1))
@@ -114,17 +126,17 @@ def resnet110(num_classes=10):
 class PreActBlock(nn.Module):
     def __init__(self, inplanes, planes, stride=1, downsample=None):
         super().__init__()
-        self.bn_a = nn.BatchNorm2d(inplanes)
+        self.bn_a = BNAct(inplanes, act="relu")
         self.conv_a = nn.Conv2d(inplanes, planes, 3, stride=stride, padding=1, bias=False)
-        self.bn_b = nn.BatchNorm2d(planes)
+        self.bn_b = BNAct(planes, act="relu")
         self.conv_b = nn.Conv2d(planes, planes, 3, padding=1, bias=False)
         self.downsample = downsample
 
     def forward(self, x):
-        out = F.relu(self.bn_a(x), inplace=False)
+        out = self.bn_a(x)
         residual = x if self.downsample is None else self.downsample(out)
         out = self.conv_a(out)
-        out = self.conv_b(F.relu(self.bn_b(out), inplace=True))
+        out = self.conv_b(self.bn_b(out))
         return out + residual
 
 
@@ -141,7 +153,7 @@ class CifarPreResNet(nn.Module):
         self.stage_1 = self._make_layer(16, n, 1)
         self.stage_2 = self._make_layer(32, n, 2)
         self.stage_3 = self._make_layer(64, n, 2)
-        self.lastact = nn.Sequential(nn.BatchNorm2d(64), nn.ReLU(inplace=True))
+        self.lastact = nn.Sequential(BNAct(64, act="relu"), nn.Identity())
         self.avgpool = nn.AvgPool2d(8)
         self.classifier = nn.Linear(64, num_classes)
         for m in self.modules():

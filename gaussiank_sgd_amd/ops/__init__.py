@@ -509,11 +509,13 @@ def cast_bf16_(dst: torch.Tensor, src: torch.Tensor) -> None:
 
 def fused_sgd_(w: torch.Tensor, m: Optional[torch.Tensor], g: torch.Tensor, chunks: torch.Tensor,
                groups: Sequence[dict], zero_grad: bool = True, grad_scale: Optional[torch.Tensor] = None,
-               w_bf16: Optional[torch.Tensor] = None) -> None:
+               w_bf16: Optional[torch.Tensor] = None, lr_mult: Optional[torch.Tensor] = None) -> None:
     """groups: dicts with lr, momentum, dampening, weight_decay, nesterov, first_step.
 
     ``w_bf16``: optional bf16 shadow arena rewritten from the new weights in
     the same pass (the compute copy used by bf16 convolutions / GEMMs).
+    ``lr_mult``: optional fp32 device scalar multiplying every lr, read by the
+    kernel (a captured HIP graph follows the host lr schedule through it).
     """
     if w.is_cuda:
         require_native(w)
@@ -522,9 +524,10 @@ def fused_sgd_(w: torch.Tensor, m: Optional[torch.Tensor], g: torch.Tensor, chun
                          [float(p.get("weight_decay", 0.0)) for p in groups],
                          [int(bool(p.get("nesterov", False))) for p in groups],
                          [int(bool(p.get("first_step", False))) for p in groups], bool(zero_grad), grad_scale,
-                         w_bf16)
+                         w_bf16, lr_mult)
         return
     gs = float(grad_scale) if grad_scale is not None else 1.0
+    lm = float(lr_mult) if lr_mult is not None else 1.0
     for start, ln, gi, _ in _decode_chunks(chunks):
         p = groups[gi]
         ws = w[start:start + ln]
@@ -540,7 +543,7 @@ def fused_sgd_(w: torch.Tensor, m: Optional[torch.Tensor], g: torch.Tensor, chun
             else:
                 ms.mul_(mom).add_(d, alpha=1 - float(p.get("dampening", 0.0)))
             d = d + mom * ms if p.get("nesterov", False) else ms
-        ws.add_(d, alpha=-float(p["lr"]))
+        ws.add_(d, alpha=-float(p["lr"]) * lm)
         if w_bf16 is not None:
             w_bf16[start:start + ln].copy_(ws)
         if zero_grad:

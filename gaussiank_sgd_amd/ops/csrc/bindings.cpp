@@ -146,7 +146,8 @@ void check_chunks(const at::Tensor& chunks) {
 void fused_sgd(at::Tensor w, c10::optional<at::Tensor> m, at::Tensor g, at::Tensor chunks, std::vector<double> lr,
                std::vector<double> momentum, std::vector<double> dampening, std::vector<double> weight_decay,
                std::vector<int64_t> nesterov, std::vector<int64_t> first_step, bool zero_grad,
-               c10::optional<at::Tensor> grad_scale, c10::optional<at::Tensor> w_bf16) {
+               c10::optional<at::Tensor> grad_scale, c10::optional<at::Tensor> w_bf16,
+               c10::optional<at::Tensor> lr_mult) {
   check_f32(w, "w");
   check_f32(g, "g");
   check_chunks(chunks);
@@ -192,6 +193,10 @@ void fused_sgd(at::Tensor w, c10::optional<at::Tensor> m, at::Tensor g, at::Tens
                     (reinterpret_cast<uintptr_t>(w_bf16->data_ptr()) & 15) == 0,
                 "w_bf16 must be a 16-byte aligned contiguous bf16 arena of w's size");
     a.w_bf16 = reinterpret_cast<uint16_t*>(w_bf16->data_ptr());
+  }
+  if (lr_mult.has_value() && lr_mult->defined()) {
+    check_f32(*lr_mult, "lr_mult");
+    a.lr_mult = lr_mult->data_ptr<float>();
   }
   c10::DeviceGuard guard(w.device());
   gk::fused_sgd(a, cur_stream(w));
@@ -717,7 +722,7 @@ TORCH_LIBRARY(gksgd, m) {
   m.def(
       "fused_sgd(Tensor(a!) w, Tensor(b!)? m, Tensor(c!) g, Tensor chunks, float[] lr, float[] momentum, "
       "float[] dampening, float[] weight_decay, int[] nesterov, int[] first_step, bool zero_grad, "
-      "Tensor? grad_scale=None, Tensor(d!)? w_bf16=None) -> ()");
+      "Tensor? grad_scale=None, Tensor(d!)? w_bf16=None, Tensor? lr_mult=None) -> ()");
   m.def("segmented_sumsq(Tensor w, Tensor g, Tensor chunks, Tensor(a!) out) -> ()");
   m.def(
       "fused_lars(Tensor(a!) w, Tensor(b!) m, Tensor g, Tensor chunks, Tensor seg_sumsq, float[] lr, "

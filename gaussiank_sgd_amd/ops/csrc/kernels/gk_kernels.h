@@ -127,6 +127,7 @@ struct SgdArgs {
   int zero_grad = 1;
   const float* grad_scale = nullptr;  // optional device scalar (clip coefficient)
   uint16_t* w_bf16 = nullptr;         // optional bf16 shadow of w written in the same pass
+  const float* lr_mult = nullptr;     // optional device scalar multiplying every group's lr (graph replay)
 };
 void fused_sgd(const SgdArgs& a, hipStream_t stream);
 

@@ -42,7 +42,8 @@ __device__ __forceinline__ float sgd_elem(float w, float& m, float g, const SgdG
 
 __global__ __launch_bounds__(kBlock) void fused_sgd_kernel(SgdArgs a) {
   const Chunk c = a.chunks[blockIdx.x];
-  const SgdGroup p = a.groups[c.group];
+  SgdGroup p = a.groups[c.group];
+  if (a.lr_mult) p.lr *= *a.lr_mult;   // lr schedule of a captured graph, read at replay time
   const float gs = a.grad_scale ? *a.grad_scale : 1.f;
   float* w = a.w + c.start;
   float* m = a.m ? a.m + c.start : nullptr;

@@ -100,6 +100,9 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         # DGC momentum correction (Lin et al. 2018): momentum is accumulated
         # locally BEFORE sparsification and the global update is plain SGD.
         self._mc = bool(opts.get("momentum_correction", _env_flag("GKSGD_MOMENTUM_CORRECTION", False)))
+        # optional device scalar multiplying the lr inside the fused update
+        # (set by train/graph.py so a captured step follows the lr schedule)
+        self._lr_mult: Optional[torch.Tensor] = None
         self._mc_applied = False
         self._base_cls = opts.get("base_cls", None)
         self._state_dirty = False
@@ -646,7 +649,7 @@ class _DistributedOptimizer(torch.optim.Optimizer):
             groups = [{"lr": g["lr"], "momentum": 0.0, "dampening": 0.0, "weight_decay": 0.0, "nesterov": False,
                        "first_step": False} for g in self.param_groups]
             ops.fused_sgd_(arena.weights, None, arena.grads, self._chunks, groups, zero_grad=self._zero_grad_in_step,
-                           w_bf16=getattr(arena, "shadow", None))
+                           w_bf16=getattr(arena, "shadow", None), lr_mult=self._lr_mult)
             self._mc_applied = False
         elif self._fused_kind == "sgd":
             groups = []
@@ -655,7 +658,8 @@ class _DistributedOptimizer(torch.optim.Optimizer):
                                "weight_decay": g.get("weight_decay", 0.0), "nesterov": g.get("nesterov", False),
                                "first_step": self._group_first[gi] and g["momentum"] != 0})
             ops.fused_sgd_(arena.weights, arena.momentum, arena.grads, self._chunks, groups,
-                           zero_grad=self._zero_grad_in_step, w_bf16=getattr(arena, "shadow", None))
+                           zero_grad=self._zero_grad_in_step, w_bf16=getattr(arena, "shadow", None),
+                           lr_mult=self._lr_mult)
             if any(self._group_first):
                 self._group_first = [False] * len(self._group_first)
                 self._adopt_state()

@@ -1,0 +1,94 @@
+"""Whole-step HIP-graph capture of a training iteration.
+
+Small per-GPU batches (the reference's ResNet-20 bs32 runs,
+logs/results/SGD_32_0.0001_topk) are launch-bound on MI355X: a step is a few
+hundred short kernels.  ``GraphedStep`` captures ONE complete iteration --
+forward, backward, bucket hooks -> fused Gaussian-k compression + exchange +
+decompression on the high-priority side stream, fused SGD update -- into a
+HIP graph (``torch.cuda.CUDAGraph`` is hipGraph on ROCm) and replays it; each
+call first copies the next batch into the graph's static input buffers, so
+every replay trains on fresh data.
+
+What the graph freezes: host-side scalars read at capture time -- the
+compression density / k, momentum flags.  The learning rate is NOT frozen:
+the fused SGD kernel multiplies the captured lr by a device scalar
+(``opt._lr_mult``) that is refreshed from the host schedule before every
+replay.  ``recapture()`` rebuilds the graph when the density schedule moves
+(epoch boundary with the reference's density warm-up).
+Requirements: every op of the step is stream-ordered without host syncs
+(true for the DistributedOptimizer / fused kernels of this package) and the
+autotuned convolution choices are cached by the eager warm-up steps.
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+import torch
+
+
+class GraphedStep:
+    def __init__(self, trainer, opt, clip: Optional[float] = None, warmup: int = 3):
+        self.trainer = trainer
+        self.opt = opt
+        self.clip = clip
+        self.warmup = warmup
+        d = trainer.data_iter()
+        self.x = d[0].clone()
+        self.y = d[1].clone() if torch.is_tensor(d[1]) else d[1]
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.lr0 = None            # lr baked into the captured update
+        self.density = None
+        self.captures = 0
+        dev = self.x.device
+        self.mult = torch.ones(1, dtype=torch.float32, device=dev)
+
+    def _body(self) -> None:
+        t, opt = self.trainer, self.opt
+        opt.zero_grad()
+        t.train(1, data=(self.x, self.y))
+        if self.clip is not None:
+            opt.synchronize()
+            opt.clip_grad_norm_(self.clip)
+        t.update_model()
+
+    def _density(self):
+        f = getattr(self.opt, "get_current_density", None)
+        return f() if f is not None else None
+
+    def recapture(self) -> None:
+        self.opt._lr_mult = None             # eager warm-up steps use the plain lr
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(self.warmup):      # eager warm-up on a side stream (allocator / autotune caches)
+                self._body()
+        torch.cuda.current_stream().wait_stream(s)
+        self.mult.fill_(1.0)
+        self.opt._lr_mult = self.mult
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self._body()
+        self.lr0 = self.trainer.lr
+        self.density = self._density()
+        self.captures += 1
+
+    def __call__(self) -> None:
+        t = self.trainer
+        if t.train_iter % t.num_batches_per_epoch == 0 and t.train_iter > 0:
+            t._on_epoch_boundary()          # host-side epoch logic (density schedule, logging)
+        d = t.data_iter()
+        self.x.copy_(d[0], non_blocking=True)
+        if torch.is_tensor(self.y):
+            self.y.copy_(d[1], non_blocking=True)
+        if self.graph is None or self._density() != self.density:
+            self.recapture()
+        # lr schedule on the host -> device multiplier read by the captured update
+        t.adjust_learning_rate(t.train_epoch, t.optimizer)
+        self.mult.fill_(float(t.lr) / float(self.lr0) if self.lr0 else 1.0)   # async, stream-ordered
+        self.graph.replay()
+        t.train_iter += 1
+
+
+def graphed(trainer, opt, clip: Optional[float] = None) -> Callable[[], None]:
+    """A zero-argument callable running one captured training iteration."""
+    return GraphedStep(trainer, opt, clip)
