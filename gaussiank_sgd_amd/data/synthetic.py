@@ -97,15 +97,17 @@ class SyntheticData:
             else:
                 seq = torch.randint(0, self.vocab, (T + 1, B), generator=g)
             return seq[:-1].to(self.device), seq[1:].to(self.device)
-        # masked LM
+        # masked LM, Google-BERT pre-training format: a fixed number of masked
+        # positions per sequence (max_predictions_per_seq = 15% of T rounded up
+        # to 8: 80 at T = 512, 20 at T = 128) with their labels, so the MLM
+        # head and loss run on those rows only
         T = self.seq_len
+        P = max(8, ((int(round(0.15 * T)) + 7) // 8) * 8)
         ids = torch.randint(5, self.vocab, (B, T), generator=g)
-        labels = torch.full((B, T), -100, dtype=torch.int64)
-        mask = torch.rand((B, T), generator=g) < 0.15
-        labels[mask] = ids[mask]
-        ids = ids.clone()
-        ids[mask] = 4  # [MASK]
-        return ids.to(self.device), labels.to(self.device)
+        pos = torch.argsort(torch.rand((B, T), generator=g), dim=1)[:, :P].sort(dim=1).values
+        labels = ids.gather(1, pos)
+        ids = ids.scatter(1, pos, 4)  # [MASK]
+        return ids.to(self.device), (pos.to(self.device), labels.to(self.device))
 
     def __iter__(self):
         return self

@@ -80,7 +80,10 @@ class BertForMaskedLM(nn.Module):
             nn.init.ones_(m.weight)
             nn.init.zeros_(m.bias)
 
-    def forward(self, input_ids, token_type_ids=None, attention_mask=None):
+    def forward(self, input_ids, token_type_ids=None, attention_mask=None, masked_positions=None):
+        """Logits [B, T, V], or [B, P, V] at ``masked_positions`` ([B, P]
+        indices, the Google-BERT pre-training format): the MLM head and the
+        vocabulary projection then run on the masked rows only."""
         B, T = input_ids.shape
         pos = torch.arange(T, device=input_ids.device).unsqueeze(0)
         tt = token_type_ids if token_type_ids is not None else torch.zeros_like(input_ids)
@@ -91,6 +94,8 @@ class BertForMaskedLM(nn.Module):
             mask = attention_mask[:, None, None, :].to(torch.bool)
         for layer in self.encoder:
             x = layer(x, mask)
+        if masked_positions is not None:
+            x = x.gather(1, masked_positions.unsqueeze(-1).expand(-1, -1, x.shape[-1]))
         h = self.mlm_ln(F.gelu(self.mlm_dense(x)))
         return F.linear(h, self.word_embeddings.weight, self.mlm_bias)
 

@@ -26,6 +26,22 @@ from typing import Callable, Optional
 import torch
 
 
+def _clone(v):
+    if torch.is_tensor(v):
+        return v.clone()
+    if isinstance(v, (tuple, list)):
+        return type(v)(_clone(e) for e in v)
+    return v
+
+
+def _copy(dst, src) -> None:
+    if torch.is_tensor(dst):
+        dst.copy_(src, non_blocking=True)
+    elif isinstance(dst, (tuple, list)):
+        for a, b in zip(dst, src):
+            _copy(a, b)
+
+
 class GraphedStep:
     def __init__(self, trainer, opt, clip: Optional[float] = None, warmup: int = 3):
         self.trainer = trainer
@@ -34,7 +50,7 @@ class GraphedStep:
         self.warmup = warmup
         d = trainer.data_iter()
         self.x = d[0].clone()
-        self.y = d[1].clone() if torch.is_tensor(d[1]) else d[1]
+        self.y = _clone(d[1])
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.lr0 = None            # lr baked into the captured update
         self.density = None
@@ -68,6 +84,7 @@ class GraphedStep:
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self._body()
+        self.trainer.train_iter -= 1          # capture records the step; it did not run it
         self.lr0 = self.trainer.lr
         self.density = self._density()
         self.captures += 1
@@ -78,8 +95,7 @@ class GraphedStep:
             t._on_epoch_boundary()          # host-side epoch logic (density schedule, logging)
         d = t.data_iter()
         self.x.copy_(d[0], non_blocking=True)
-        if torch.is_tensor(self.y):
-            self.y.copy_(d[1], non_blocking=True)
+        _copy(self.y, d[1])
         if self.graph is None or self._density() != self.density:
             self.recapture()
         # lr schedule on the host -> device multiplier read by the captured update

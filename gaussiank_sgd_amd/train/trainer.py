@@ -235,8 +235,12 @@ class DLTrainer:
                 outputs, hidden = self.net(inputs, hidden)
                 loss = self.criterion(outputs.reshape(-1, self.net.vocab_size).float(), labels.reshape(-1))
             elif self.dnn.startswith("bert"):
-                outputs = self.net(inputs)
-                loss = self.criterion(outputs, labels)
+                if isinstance(labels, (tuple, list)):     # (masked positions, labels)
+                    outputs = self.net(inputs, masked_positions=labels[0])
+                    loss = self.criterion(outputs, labels[1])
+                else:                                     # dense [B, T] labels, -100 = unmasked
+                    outputs = self.net(inputs)
+                    loss = self.criterion(outputs, labels)
             elif self.dnn == "lstman4":
                 targets, tgt_lens, in_lens = labels
                 outputs, out_lens = self.net(inputs, in_lens)
