@@ -15,6 +15,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.ln import add_layernorm
+
 
 @dataclass
 class BertConfig:
@@ -48,9 +50,10 @@ class BertLayer(nn.Module):
         q, k, v = qkv[0], qkv[1], qkv[2]
         a = F.scaled_dot_product_attention(q, k, v, attn_mask=attn_mask, dropout_p=self.p if self.training else 0.0)
         a = a.transpose(1, 2).reshape(B, T, H)
-        x = self.ln1(x + self.drop(self.attn_out(a)))
+        # ln(x + drop(y)) as one fused HIP pass each way on the GPU (ops/ln.py)
+        x = add_layernorm(self.attn_out(a), x, self.ln1, self.p, self.training)
         h = self.ffn_out(F.gelu(self.ffn_in(x)))
-        return self.ln2(x + self.drop(h))
+        return add_layernorm(h, x, self.ln2, self.p, self.training)
 
 
 class BertForMaskedLM(nn.Module):

@@ -35,6 +35,7 @@ HIP_SOURCES = [
     "kernels/optim.hip",
     "kernels/bn_act.hip",
     "kernels/gemm.hip",
+    "kernels/ln.hip",
 ]
 CXX_SOURCES = [
     "comm/rccl_engine.cpp",

@@ -703,6 +703,50 @@ void conv_tn_acc(at::Tensor dy, at::Tensor x, at::Tensor wout, at::Tensor zero, 
                       (int)splits, cur_stream(x));
 }
 
+// fused residual add (+ dropout) + LayerNorm (ln.hip)
+bool add_ln_supported(int64_t H) { return gk::add_ln_supported((int)H); }
+int64_t add_ln_ws_floats(int64_t R, int64_t H) { return 2 * gk::add_ln_partial_rows(R) * H; }
+
+void check_rows_bf16(const at::Tensor& t, const char* name, int64_t R, int64_t H) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.is_contiguous() && t.numel() == R * H,
+              name, " must be a contiguous bf16 GPU tensor of R*H elements");
+}
+
+void add_ln_forward(at::Tensor a, at::Tensor x, c10::optional<at::Tensor> gamma, c10::optional<at::Tensor> beta,
+                    at::Tensor y, at::Tensor h, at::Tensor mean, at::Tensor rstd, double eps, double p, int64_t seed) {
+  const int64_t H = x.size(-1), R = x.numel() / H;
+  TORCH_CHECK(gk::add_ln_supported((int)H), "add_ln: unsupported hidden size");
+  for (auto* t : {&a, &x, &y, &h}) check_rows_bf16(*t, "add_ln tensor", R, H);
+  TORCH_CHECK(mean.numel() >= R && rstd.numel() >= R && mean.scalar_type() == at::kFloat &&
+                  rstd.scalar_type() == at::kFloat, "mean/rstd: fp32 [R]");
+  const float* gp = gamma.has_value() && gamma->defined() ? gamma->data_ptr<float>() : nullptr;
+  const float* bp = beta.has_value() && beta->defined() ? beta->data_ptr<float>() : nullptr;
+  if (gp) TORCH_CHECK(gamma->numel() == H && gamma->is_contiguous(), "gamma: fp32 [H]");
+  if (bp) TORCH_CHECK(beta->numel() == H && beta->is_contiguous(), "beta: fp32 [H]");
+  c10::DeviceGuard guard(x.device());
+  gk::add_ln_forward(a.data_ptr(), x.data_ptr(), gp, bp, y.data_ptr(), h.data_ptr(), mean.data_ptr<float>(),
+                     rstd.data_ptr<float>(), R, (int)H, (float)eps, (float)p, (uint32_t)seed, cur_stream(x));
+}
+
+void add_ln_backward(at::Tensor dy, at::Tensor h, at::Tensor mean, at::Tensor rstd, c10::optional<at::Tensor> gamma,
+                     at::Tensor dx, c10::optional<at::Tensor> da, c10::optional<at::Tensor> dgamma,
+                     c10::optional<at::Tensor> dbeta, bool accumulate, at::Tensor ws, double p, int64_t seed) {
+  const int64_t H = h.size(-1), R = h.numel() / H;
+  for (auto* t : {&dy, &h, &dx}) check_rows_bf16(*t, "add_ln tensor", R, H);
+  if (da.has_value() && da->defined()) check_rows_bf16(*da, "da", R, H);
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() >= 2 * gk::add_ln_partial_rows(R) * H, "ws too small");
+  auto f32 = [&](const c10::optional<at::Tensor>& t) -> float* {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->numel() == H && t->is_contiguous(), "fp32 [H] expected");
+    return t->data_ptr<float>();
+  };
+  c10::DeviceGuard guard(h.device());
+  gk::add_ln_backward(dy.data_ptr(), h.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(), f32(gamma),
+                      dx.data_ptr(), da.has_value() && da->defined() ? da->data_ptr() : nullptr, f32(dgamma),
+                      f32(dbeta), accumulate ? 1 : 0, ws.data_ptr<float>(), R, (int)H, (float)p, (uint32_t)seed,
+                      cur_stream(h));
+}
+
 }  // namespace
 
 
@@ -761,6 +805,12 @@ TORCH_LIBRARY(gksgd, m) {
   m.def("gemm_tn_acc(Tensor G, Tensor X, Tensor(a!) W, int cfg=0, int splits=0) -> ()");
   m.def("conv_nt(Tensor x, Tensor w, Tensor(a!) y, Tensor zero, int stride, int pad, int cfg=0, int max_blocks=0, "
         "Tensor(b!)? stats=None, Tensor? bias=None) -> int");
+  m.def("add_ln_supported(int H) -> bool", &add_ln_supported);
+  m.def("add_ln_ws_floats(int R, int H) -> int", &add_ln_ws_floats);
+  m.def("add_ln_forward(Tensor a, Tensor x, Tensor? gamma, Tensor? beta, Tensor(a!) y, Tensor(b!) h, "
+        "Tensor(c!) mean, Tensor(d!) rstd, float eps, float p, int seed) -> ()");
+  m.def("add_ln_backward(Tensor dy, Tensor h, Tensor mean, Tensor rstd, Tensor? gamma, Tensor(a!) dx, "
+        "Tensor(b!)? da, Tensor(c!)? dgamma, Tensor(d!)? dbeta, bool accumulate, Tensor(e!) ws, float p, int seed) -> ()");
   m.def("conv_tn_acc(Tensor dy, Tensor x, Tensor(a!) wout, Tensor zero, int stride, int pad, int cfg=0, int splits=0) -> ()");
 
   m.class_<RcclEngine>("RcclEngine")
@@ -800,4 +850,6 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("gemm_tn_acc", &gemm_tn_acc);
   m.impl("conv_nt", &conv_nt);
   m.impl("conv_tn_acc", &conv_tn_acc);
+  m.impl("add_ln_forward", &add_ln_forward);
+  m.impl("add_ln_backward", &add_ln_backward);
 }

@@ -241,4 +241,22 @@ int conv_nt_bf16(const void* X, const void* zero, int H, int W, int C, int OH, i
 void conv_tn_acc_f32(const void* G, const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P,
                      int KH, int KW, float* Wout, int64_t M, int N, int cfg, int splits, hipStream_t stream);
 
+// ---------------------------------------------------------------------------
+// Fused residual add (+ dropout) + LayerNorm over rows of H bf16 (ln.hip).
+// forward : h = x + dropout_p(a), y = LN(h) * gamma + beta; saves h (bf16),
+//           mean, rstd (fp32 per row).  The dropout mask is a hash of
+//           (seed, row, column) -- recomputed in the backward, never stored.
+// backward: dx = dLN/dh (residual branch), da = dx * mask / (1 - p) (null da:
+//           no second output), dgamma / dbeta (+)= column sums; ws needs
+//           2 * add_ln_partial_rows(R) * H floats.
+// ---------------------------------------------------------------------------
+bool add_ln_supported(int H);
+int64_t add_ln_partial_rows(int64_t R);
+void add_ln_forward(const void* a, const void* x, const float* gamma, const float* beta, void* y, void* hsave,
+                    float* mean, float* rstd, int64_t R, int H, float eps, float p, uint32_t seed,
+                    hipStream_t stream);
+void add_ln_backward(const void* dy, const void* hsave, const float* mean, const float* rstd, const float* gamma,
+                     void* dx, void* da, float* dgamma, float* dbeta, int accumulate, float* ws, int64_t R, int H,
+                     float p, uint32_t seed, hipStream_t stream);
+
 }  // namespace gk
