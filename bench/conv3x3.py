@@ -25,7 +25,7 @@ HBM = 6.3e12
 # (Cin=Cout, H_in, stride, count) of ResNet-50's 3x3 convolutions
 SHAPES = [(64, 56, 1, 3), (128, 56, 2, 1), (128, 28, 1, 3), (256, 28, 2, 1), (256, 14, 1, 5), (512, 14, 2, 1),
           (512, 7, 1, 2)]
-NT_CFGS = [1, 2, 3, 4, 21, 22, 23, 24, 121, 122, 123, 124]
+NT_CFGS = [1, 2, 3, 4, 21, 22, 23, 24, 121, 122, 123, 124, 25, 26, 27, 125, 126, 127]
 TN_CFGS = [(c, sp) for c in (1, 2, 3, 4, 5, 6, 7, 8, 21, 22, 23, 24, 27) for sp in (0, 128)]
 
 

@@ -38,7 +38,7 @@ _ENABLED = os.environ.get("GKSGD_FASTCONV", "1") != "0"
 _choices: Dict[tuple, tuple] = {}
 _timings: Dict[tuple, list] = {}      # key -> [(tag, ms or error)] of the search
 # candidate kernel configurations (gemm.hip: cfg digits = tile + 10*panel + 100*stages)
-_NT_CFGS = [1, 2, 3, 4, 11, 13, 21, 22, 23, 24, 111, 113, 121, 122, 123, 124]
+_NT_CFGS = [1, 2, 3, 4, 11, 13, 21, 22, 23, 24, 111, 113, 121, 122, 123, 124, 25, 26, 27, 125, 126, 127]
 # grid override: 0 = persistent (about two blocks per CU), else a fixed block count
 _NT_GRIDS = (0, 512, 1 << 20)
 _TN_CFGS = [(c, s) for c in (1, 2, 3, 4, 5, 6, 7, 8, 21, 22, 23, 24, 27) for s in (0, 128)]
@@ -69,21 +69,28 @@ def _time(fn: Callable[[], None], reps: int = 5) -> float:
 
 
 def _pick(key: tuple, cands: List[Tuple[tuple, Callable[[], None]]]) -> tuple:
-    """Fastest candidate for ``key`` (timed once per process, then cached)."""
+    """Fastest candidate for ``key`` (timed once per process, then cached):
+    a 3-repetition screen of every candidate, then the best four re-timed
+    with 12 repetitions (one noisy sample must not decide)."""
     got = _choices.get(key)
     if got is not None:
         return got
     if not _TUNE or len(cands) == 1:
         _choices[key] = cands[0][0]
         return cands[0][0]
-    best, best_t = cands[-1][0], float("inf")
     log = _timings.setdefault(key, [])
+    screened = []
     for tag, fn in cands:
         try:
-            t = _time(fn)
+            t = _time(fn, reps=3)
         except RuntimeError as e:
             log.append((tag, "error: %s" % str(e).splitlines()[0][:200]))
             continue
+        screened.append((t, tag, fn))
+    screened.sort(key=lambda e: e[0])
+    best, best_t = cands[-1][0], float("inf")
+    for _, tag, fn in screened[:4]:
+        t = _time(fn, reps=12)
         log.append((tag, round(t, 4)))
         if t < best_t:
             best, best_t = tag, t

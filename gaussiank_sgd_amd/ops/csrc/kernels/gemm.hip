@@ -67,7 +67,9 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
     GK_VMW(10) GK_VMW(11) GK_VMW(12) GK_VMW(13) GK_VMW(14) GK_VMW(15) GK_VMW(16) GK_VMW(17) GK_VMW(18)
     GK_VMW(19) GK_VMW(20) GK_VMW(21) GK_VMW(22) GK_VMW(23) GK_VMW(24) GK_VMW(25) GK_VMW(26) GK_VMW(27)
     GK_VMW(28) GK_VMW(29) GK_VMW(30) GK_VMW(31) GK_VMW(32) GK_VMW(33) GK_VMW(34) GK_VMW(35) GK_VMW(36)
-    GK_VMW(37) GK_VMW(38) GK_VMW(39) GK_VMW(40)
+    GK_VMW(37) GK_VMW(38) GK_VMW(39) GK_VMW(40) GK_VMW(41) GK_VMW(42) GK_VMW(43) GK_VMW(44) GK_VMW(45)
+    GK_VMW(46) GK_VMW(47) GK_VMW(48) GK_VMW(49) GK_VMW(50) GK_VMW(51) GK_VMW(52) GK_VMW(53) GK_VMW(54)
+    GK_VMW(55) GK_VMW(56) GK_VMW(57) GK_VMW(58) GK_VMW(59) GK_VMW(60) GK_VMW(61) GK_VMW(62) GK_VMW(63)
     default: vmcnt_le<0>(); break;
   }
 #undef GK_VMW
@@ -104,11 +106,14 @@ __device__ __forceinline__ const uint16_t* conv_row(const uint16_t* X, const Con
 // the same for every M tile of the persistent loop); only A is streamed.
 // NS: LDS stages; NS = 3 keeps two K slices in flight behind the one being
 // multiplied.
-template <int WM, int WN, bool BRES>
+// MSB: 16-row MFMA subtiles per wave along M (4: 64x64 wave tile, 8: 128x64 --
+// fewer LDS reads per MFMA for the compute-bound shapes).
+template <int WM, int WN, bool BRES, int MSB = 4>
 struct NtCfg {
   static constexpr int NW = WM * WN;
   static constexpr int THREADS = 64 * NW;
-  static constexpr int BM = 64 * WM;
+  static constexpr int WTM = 16 * MSB;            // wave tile rows
+  static constexpr int BM = WTM * WM;
   static constexpr int BN = 64 * WN;
   static constexpr int ASTAGE = BM * 128;         // bytes: BM rows x 64 bf16
   static constexpr int BSTAGE = BN * 128;
@@ -118,12 +123,12 @@ struct NtCfg {
   static constexpr int LPW = INSTS / NW;          // LDS-DMA instructions per wave per stage
   static_assert((BM / 8) % NW == 0, "A rows split evenly over the waves");
   static constexpr int LPWA = BRES ? LPW : (BM / 8) / NW;   // of which A-row instructions (j < LPWA)
-  static constexpr int NST = 8;                   // 16-byte epilogue stores per wave per tile
-  static_assert(LPW + 2 * NST <= 40, "wait_vmcnt range");
+  static constexpr int NST = 2 * MSB;             // 16-byte epilogue stores per wave per tile
+  static_assert(LPW + 2 * NST <= 63, "wait_vmcnt range (vmcnt is 6 bits)");
   static int lds_bytes(int K, int ns) { return ns * STAGE + (BRES ? BN * K * 2 : 0); }
 };
 
-template <int WM, int WN, bool BRES, int NS, bool GATHER>
+template <int WM, int WN, bool BRES, int NS, bool GATHER, int MSB = 4>
 __global__ void __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(WM * WN >= 8 ? 1 : 2)))
 gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
                uint16_t* __restrict__ C, int64_t ldc, int64_t M, int K, ConvGeo geo, float* __restrict__ stats,
@@ -131,7 +136,7 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
   // stats != nullptr: per-block BatchNorm partials of the (bf16-rounded)
   // output, psum at stats[blockIdx.x * N + n], psq at stats[stats_ld + ...]
   // (the [gy][C] layout bn_finalize_kernel reduces).
-  using Cfg = NtCfg<WM, WN, BRES>;
+  using Cfg = NtCfg<WM, WN, BRES, MSB>;
   static_assert(NS == 2 || NS == 3, "stages");
   constexpr int LPW = Cfg::LPW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -247,9 +252,9 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
     }
   };
 
-  f32x4 acc[4][4];
+  f32x4 acc[MSB][4];
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int a = 0; a < MSB; ++a)
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -285,16 +290,19 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int c = kk * 4 + fq;
-      bf16x8 av[4], bv[4];
+      bf16x8 av[MSB], bv[4];
+#pragma unroll
+      for (int s = 0; s < MSB; ++s) {
+        const int ra = wm * Cfg::WTM + s * 16 + fr;
+        av[s] = *reinterpret_cast<const bf16x8*>(As + ra * 128 + ((c ^ swz(ra)) << 4));
+      }
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        const int ra = wm * 64 + s * 16 + fr;
-        av[s] = *reinterpret_cast<const bf16x8*>(As + ra * 128 + ((c ^ swz(ra)) << 4));
         const int rb = wn * 64 + s * 16 + fr;
         bv[s] = *reinterpret_cast<const bf16x8*>(Bs + rb * 128 + ((c ^ swz(rb)) << 4));
       }
 #pragma unroll
-      for (int ms = 0; ms < 4; ++ms)
+      for (int ms = 0; ms < MSB; ++ms)
 #pragma unroll
         for (int ns = 0; ns < 4; ++ns)
           acc[ms][ns] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv[ns], av[ms], acc[ms][ns], 0, 0, 0);
@@ -311,8 +319,8 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
       const bool full = mbase + Cfg::BM <= M;
       const bool odd = fq & 1;
 #pragma unroll
-      for (int ms = 0; ms < 4; ++ms) {
-        const int64_t m = mbase + wm * 64 + ms * 16 + fr;
+      for (int ms = 0; ms < MSB; ++ms) {
+        const int64_t m = mbase + wm * Cfg::WTM + ms * 16 + fr;
 #pragma unroll
         for (int pr = 0; pr < 2; ++pr) {
           const f32x4 va = acc[ms][2 * pr], vb = acc[ms][2 * pr + 1];
@@ -383,11 +391,11 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
   }
 }
 
-template <int WM, int WN, bool BRES, int NS, bool GATHER>
+template <int WM, int WN, bool BRES, int NS, bool GATHER, int MSB = 4>
 int launch_nt(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, uint16_t* C, int64_t ldc, int64_t M,
               int N, int K, int max_blocks, const ConvGeo& geo, float* stats, int64_t stats_ld, int stats_rows,
               hipStream_t stream) {
-  using Cfg = NtCfg<WM, WN, BRES>;
+  using Cfg = NtCfg<WM, WN, BRES, MSB>;
   const int ntiles = N / Cfg::BN;
   const int64_t mtiles = (M + Cfg::BM - 1) / Cfg::BM;
   const int lds = Cfg::lds_bytes(K, NS);
@@ -399,29 +407,29 @@ int launch_nt(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, ui
   if (stats && gx > stats_rows) gx = stats_rows;   // one partial row per block
   dim3 grid((unsigned)gx, (unsigned)ntiles);
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<WM, WN, BRES, NS, GATHER>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<WM, WN, BRES, NS, GATHER, MSB>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL((gemm_nt_kernel<WM, WN, BRES, NS, GATHER>), grid, dim3(Cfg::THREADS), lds, stream, A, lda, B,
+  hipLaunchKernelGGL((gemm_nt_kernel<WM, WN, BRES, NS, GATHER, MSB>), grid, dim3(Cfg::THREADS), lds, stream, A, lda, B,
                      ldb, C, ldc, M, K, geo, stats, stats_ld);
   return (int)gx;
 }
 
-template <int WM, int WN, bool GATHER>
+template <int WM, int WN, bool GATHER, int MSB = 4>
 int launch_nt_any(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, uint16_t* C, int64_t ldc,
                   int64_t M, int N, int K, int max_blocks, int bres, int ns, const ConvGeo& geo, float* stats,
                   int64_t stats_ld, int stats_rows, hipStream_t stream) {
   // keep the weight panel resident when it fits next to the two A stages
   if (bres < 0) bres = (64 * WN) * K * 2 <= 64 * 1024;
-  if (bres && NtCfg<WM, WN, true>::lds_bytes(K, 2) > 160 * 1024) bres = 0;
+  if (bres && NtCfg<WM, WN, true, MSB>::lds_bytes(K, 2) > 160 * 1024) bres = 0;
   constexpr int L = 160 * 1024;
   if (bres) {
-    if (ns != 2 && NtCfg<WM, WN, true>::lds_bytes(K, 3) <= L) return launch_nt<WM, WN, true, 3, GATHER>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, stream);
-    else return launch_nt<WM, WN, true, 2, GATHER>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, stream);
+    if (ns != 2 && NtCfg<WM, WN, true, MSB>::lds_bytes(K, 3) <= L) return launch_nt<WM, WN, true, 3, GATHER, MSB>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, stream);
+    else return launch_nt<WM, WN, true, 2, GATHER, MSB>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, stream);
   } else {
-    if (ns != 2 && NtCfg<WM, WN, false>::lds_bytes(K, 3) <= L) return launch_nt<WM, WN, false, 3, GATHER>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, stream);
-    else return launch_nt<WM, WN, false, 2, GATHER>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, stream);
+    if (ns != 2 && NtCfg<WM, WN, false, MSB>::lds_bytes(K, 3) <= L) return launch_nt<WM, WN, false, 3, GATHER, MSB>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, stream);
+    else return launch_nt<WM, WN, false, 2, GATHER, MSB>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, stream);
   }
 }
 
@@ -447,7 +455,7 @@ struct TnCfg {
   static constexpr int INSTS = STAGE / 1024;
   static_assert(INSTS % NW == 0, "stage split");
   static constexpr int LPW = INSTS / NW;
-  static_assert(LPW <= 40, "wait_vmcnt range");
+  static_assert(LPW <= 63, "wait_vmcnt range");
   static_assert(GINSTS % NW == 0, "G rows split evenly over the waves");
   static constexpr int LPWG = GINSTS / NW;           // G-row instructions per wave (j < LPWG)
   static_assert((WS - 1) * WN * WK * 16384 <= LDS, "reduction scratch");
@@ -713,12 +721,17 @@ int nt_dispatch(const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
   auto b = static_cast<const uint16_t*>(B);
   auto c = static_cast<uint16_t*>(C);
   if (cfg <= 0) cfg = N % 256 == 0 ? 3 : (N % 128 == 0 ? 2 : 1);
-  static const int cfg_bn[5] = {64, 64, 128, 256, 128};
-  if (cfg > 4 || N % cfg_bn[cfg] != 0) cfg = 1;   // the tile must divide N (B rows are not clamped)
+  // tiles (BM x BN, waves): 1 256x64 (4)  2 256x128 (8)  3 128x256 (8)  4 128x128 (4)
+  //                         5 256x256 (8, 128x64 per wave)  6 256x128 (4, 128x64)  7 128x256 (4, 128x64)
+  static const int cfg_bn[8] = {64, 64, 128, 256, 128, 256, 128, 256};
+  if (cfg > 7 || N % cfg_bn[cfg] != 0) cfg = 1;   // the tile must divide N (B rows are not clamped)
   switch (cfg) {
     case 2: return launch_nt_any<4, 2, GATHER>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, stream);
     case 3: return launch_nt_any<2, 4, GATHER>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, stream);
     case 4: return launch_nt_any<2, 2, GATHER>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, stream);
+    case 5: return launch_nt_any<2, 4, GATHER, 8>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, stream);
+    case 6: return launch_nt_any<2, 2, GATHER, 8>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, stream);
+    case 7: return launch_nt_any<1, 4, GATHER, 8>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, stream);
     default: return launch_nt_any<4, 1, GATHER>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, stream);
   }
 }

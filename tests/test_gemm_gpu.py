@@ -22,7 +22,7 @@ def _rand(*shape, scale=1.0):
 
 @pytest.mark.parametrize("M,N,K", [(1000, 64, 64), (4096, 256, 64), (777, 128, 192), (2048, 512, 128),
                                    (513, 192, 320), (300, 256, 1024)])
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 11, 21, 13, 23])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 11, 21, 13, 23, 5, 6, 7, 125, 126, 127, 15])
 def test_gemm_nt(g, M, N, K, cfg):
     torch.manual_seed(M + N + K)
     A = _rand(M, K)
@@ -73,7 +73,7 @@ def _conv_case(N, C, H, Co, k, s, p):
 
 @pytest.mark.parametrize("N,C,H,Co,k,s,p", [(2, 64, 9, 64, 3, 1, 1), (3, 128, 7, 64, 3, 2, 1), (2, 64, 14, 128, 3, 2, 1),
                                             (2, 128, 5, 256, 1, 1, 0), (1, 64, 11, 192, 3, 1, 1)])
-@pytest.mark.parametrize("cfg", [0, 1, 3, 22, 124])
+@pytest.mark.parametrize("cfg", [0, 1, 3, 22, 124, 5, 126, 7])
 def test_conv_nt(g, N, C, H, Co, k, s, p, cfg):
     import torch.nn.functional as F
     torch.manual_seed(N + C + H + Co)
