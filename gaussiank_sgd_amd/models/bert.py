@@ -3,7 +3,9 @@
 Standard BERT-base: vocab 30522, hidden 768, 12 layers, 12 heads, FFN 3072,
 512 positions, GELU, post-LN, MLM head tied to the word embeddings
 (~110M parameters).  Attention uses ``F.scaled_dot_product_attention`` (the
-ROCm flash-attention path); run under bf16 autocast.  Gradients stay fp32 in
+ROCm flash-attention path); run under bf16 autocast.  Every encoder / MLM-head
+linear is a ``FastLinear`` (ops/linear.py: autotuned MFMA GEMMs, GELU backward
+and bias gradient in one fused pass into the fp32 gradient arena).  Gradients stay fp32 in
 the flat arena, so compression is unaffected by the compute dtype.
 """
 from __future__ import annotations
@@ -15,6 +17,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.linear import FastLinear
 from ..ops.ln import add_layernorm
 
 
@@ -31,28 +34,55 @@ class BertConfig:
     ln_eps: float = 1e-12
 
 
+class _SplitHeads(torch.autograd.Function):
+    """[B, T, 3*H] projection -> q, k, v as [B, heads, T, d] strided views (no
+    copy).  The backward writes dq, dk, dv straight into ONE [B, T, 3, heads, d]
+    gradient -- three strided copies, instead of autograd's stack of the three
+    (a 75 MB CatArrayBatchedCopy per BERT-base layer at ~1.5 TB/s) followed by
+    the permute's reshape copy."""
+
+    @staticmethod
+    def forward(ctx, y, heads):
+        B, T, H3 = y.shape
+        d = H3 // (3 * heads)
+        ctx.dims = (B, T, heads, d)
+        v5 = y.view(B, T, 3, heads, d)
+        return v5[:, :, 0].transpose(1, 2), v5[:, :, 1].transpose(1, 2), v5[:, :, 2].transpose(1, 2)
+
+    @staticmethod
+    def backward(ctx, dq, dk, dv):
+        B, T, h, d = ctx.dims
+        ref = next(g for g in (dq, dk, dv) if g is not None)
+        g5 = torch.empty(B, T, 3, h, d, dtype=ref.dtype, device=ref.device)
+        for i, gi in enumerate((dq, dk, dv)):
+            if gi is None:
+                g5[:, :, i].zero_()
+            else:
+                g5[:, :, i].copy_(gi.transpose(1, 2))
+        return g5.view(B, T, 3 * h * d), None
+
+
 class BertLayer(nn.Module):
     def __init__(self, c: BertConfig):
         super().__init__()
         self.heads = c.heads
-        self.qkv = nn.Linear(c.hidden, 3 * c.hidden)
-        self.attn_out = nn.Linear(c.hidden, c.hidden)
+        self.qkv = FastLinear(c.hidden, 3 * c.hidden)
+        self.attn_out = FastLinear(c.hidden, c.hidden)
         self.ln1 = nn.LayerNorm(c.hidden, eps=c.ln_eps)
-        self.ffn_in = nn.Linear(c.hidden, c.intermediate)
-        self.ffn_out = nn.Linear(c.intermediate, c.hidden)
+        self.ffn_in = FastLinear(c.hidden, c.intermediate)
+        self.ffn_out = FastLinear(c.intermediate, c.hidden)
         self.ln2 = nn.LayerNorm(c.hidden, eps=c.ln_eps)
         self.drop = nn.Dropout(c.dropout)
         self.p = c.dropout
 
     def forward(self, x, attn_mask=None):
         B, T, H = x.shape
-        qkv = self.qkv(x).view(B, T, 3, self.heads, H // self.heads).permute(2, 0, 3, 1, 4)
-        q, k, v = qkv[0], qkv[1], qkv[2]
+        q, k, v = _SplitHeads.apply(self.qkv(x), self.heads)
         a = F.scaled_dot_product_attention(q, k, v, attn_mask=attn_mask, dropout_p=self.p if self.training else 0.0)
         a = a.transpose(1, 2).reshape(B, T, H)
         # ln(x + drop(y)) as one fused HIP pass each way on the GPU (ops/ln.py)
         x = add_layernorm(self.attn_out(a), x, self.ln1, self.p, self.training)
-        h = self.ffn_out(F.gelu(self.ffn_in(x)))
+        h = self.ffn_out(self.ffn_in(x, act="gelu"))
         return add_layernorm(h, x, self.ln2, self.p, self.training)
 
 
@@ -67,7 +97,7 @@ class BertForMaskedLM(nn.Module):
         self.emb_ln = nn.LayerNorm(c.hidden, eps=c.ln_eps)
         self.emb_drop = nn.Dropout(c.dropout)
         self.encoder = nn.ModuleList([BertLayer(c) for _ in range(c.layers)])
-        self.mlm_dense = nn.Linear(c.hidden, c.hidden)
+        self.mlm_dense = FastLinear(c.hidden, c.hidden)
         self.mlm_ln = nn.LayerNorm(c.hidden, eps=c.ln_eps)
         self.mlm_bias = nn.Parameter(torch.zeros(c.vocab_size))
         self.name = "bert"
@@ -99,7 +129,7 @@ class BertForMaskedLM(nn.Module):
             x = layer(x, mask)
         if masked_positions is not None:
             x = x.gather(1, masked_positions.unsqueeze(-1).expand(-1, -1, x.shape[-1]))
-        h = self.mlm_ln(F.gelu(self.mlm_dense(x)))
+        h = self.mlm_ln(self.mlm_dense(x, act="gelu"))
         return F.linear(h, self.word_embeddings.weight, self.mlm_bias)
 
 

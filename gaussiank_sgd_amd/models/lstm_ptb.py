@@ -11,6 +11,8 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
+from ..ops.linear import FastLinear
+
 
 class PTBLSTM(nn.Module):
     def __init__(self, vocab_size: int = 10000, embedding_dim: int = 1500, num_steps: int = 35,
@@ -26,7 +28,7 @@ class PTBLSTM(nn.Module):
         self.word_embeddings = nn.Embedding(vocab_size, embedding_dim)
         self.lstm = nn.LSTM(input_size=embedding_dim, hidden_size=embedding_dim, num_layers=num_layers,
                             dropout=1 - dp_keep_prob)
-        self.sm_fc = nn.Linear(embedding_dim, vocab_size)
+        self.sm_fc = FastLinear(embedding_dim, vocab_size)   # fused bias-gradient pass on the GPU
         self.name = "lstm"
         self.init_weights()
 

@@ -36,6 +36,7 @@ HIP_SOURCES = [
     "kernels/bn_act.hip",
     "kernels/gemm.hip",
     "kernels/ln.hip",
+    "kernels/linear.hip",
 ]
 CXX_SOURCES = [
     "comm/rccl_engine.cpp",

@@ -747,6 +747,38 @@ void add_ln_backward(at::Tensor dy, at::Tensor h, at::Tensor mean, at::Tensor rs
                       cur_stream(h));
 }
 
+// linear-layer column passes (linear.hip): bias gradient / fused GELU backward
+void check_bf16_2d(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 2 && t.is_contiguous() &&
+                  t.size(1) % 8 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+              name, " must be a contiguous 16-byte aligned bf16 [M, N] GPU tensor with N % 8 == 0");
+}
+
+float* colsum_db(const c10::optional<at::Tensor>& db, int64_t N) {
+  if (!db.has_value() || !db->defined()) return nullptr;
+  TORCH_CHECK(db->is_cuda() && db->scalar_type() == at::kFloat && db->is_contiguous() && db->numel() == N,
+              "db must be a contiguous fp32 [N] GPU tensor");
+  return db->data_ptr<float>();
+}
+
+void colsum_acc(at::Tensor dy, at::Tensor db) {
+  check_bf16_2d(dy, "dy");
+  float* d = colsum_db(db, dy.size(1));
+  c10::DeviceGuard guard(dy.device());
+  gk::colsum_acc_bf16(static_cast<const uint16_t*>(dy.data_ptr()), d, dy.size(0), (int)dy.size(1), cur_stream(dy));
+}
+
+void gelu_bwd_colsum(at::Tensor dy, at::Tensor pre, at::Tensor dpre, c10::optional<at::Tensor> db) {
+  check_bf16_2d(dy, "dy");
+  check_bf16_2d(pre, "pre");
+  check_bf16_2d(dpre, "dpre");
+  TORCH_CHECK(pre.sizes() == dy.sizes() && dpre.sizes() == dy.sizes(), "gelu_bwd_colsum: shape mismatch");
+  float* d = colsum_db(db, dy.size(1));
+  c10::DeviceGuard guard(dy.device());
+  gk::gelu_bwd_colsum_bf16(static_cast<const uint16_t*>(dy.data_ptr()), static_cast<const uint16_t*>(pre.data_ptr()),
+                           static_cast<uint16_t*>(dpre.data_ptr()), d, dy.size(0), (int)dy.size(1), cur_stream(dy));
+}
+
 }  // namespace
 
 
@@ -812,6 +844,8 @@ TORCH_LIBRARY(gksgd, m) {
   m.def("add_ln_backward(Tensor dy, Tensor h, Tensor mean, Tensor rstd, Tensor? gamma, Tensor(a!) dx, "
         "Tensor(b!)? da, Tensor(c!)? dgamma, Tensor(d!)? dbeta, bool accumulate, Tensor(e!) ws, float p, int seed) -> ()");
   m.def("conv_tn_acc(Tensor dy, Tensor x, Tensor(a!) wout, Tensor zero, int stride, int pad, int cfg=0, int splits=0) -> ()");
+  m.def("colsum_acc(Tensor dy, Tensor(a!) db) -> ()");
+  m.def("gelu_bwd_colsum(Tensor dy, Tensor pre, Tensor(a!) dpre, Tensor(b!)? db=None) -> ()");
 
   m.class_<RcclEngine>("RcclEngine")
       .def(torch::init<>())
@@ -852,4 +886,6 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("conv_tn_acc", &conv_tn_acc);
   m.impl("add_ln_forward", &add_ln_forward);
   m.impl("add_ln_backward", &add_ln_backward);
+  m.impl("colsum_acc", &colsum_acc);
+  m.impl("gelu_bwd_colsum", &gelu_bwd_colsum);
 }

@@ -259,4 +259,15 @@ void add_ln_backward(const void* dy, const void* hsave, const float* mean, const
                      void* dx, void* da, float* dgamma, float* dbeta, int accumulate, float* ws, int64_t R, int H,
                      float p, uint32_t seed, hipStream_t stream);
 
+// ---------------------------------------------------------------------------
+// Linear-layer column passes over bf16 [M, N] row-major gradients (linear.hip);
+// N % 8 == 0, rows 16-byte aligned; db: fp32 [N], accumulated with float atomics.
+//   colsum_acc_bf16     : db[n] += sum_m dy[m, n]                   (bias gradient)
+//   gelu_bwd_colsum_bf16: dpre = dy * gelu'(pre) (erf GELU, bf16 RNE) and, when db
+//                         is non-null, db[n] += sum_m dpre[m, n]
+// ---------------------------------------------------------------------------
+void colsum_acc_bf16(const uint16_t* dy, float* db, int64_t M, int N, hipStream_t stream);
+void gelu_bwd_colsum_bf16(const uint16_t* dy, const uint16_t* pre, uint16_t* dpre, float* db, int64_t M, int N,
+                          hipStream_t stream);
+
 }  // namespace gk

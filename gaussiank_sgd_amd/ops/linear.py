@@ -1,0 +1,258 @@
+"""Linear layers on bf16 activations through the MFMA GEMMs of
+``csrc/kernels/gemm.hip`` (autotuned per shape against hipBLASLt), with the
+bias gradient -- and, for ``act="gelu"``, the GELU backward -- in ONE fused
+HIP column pass (``csrc/kernels/linear.hip``) that adds straight into the
+optimizer's fp32 gradient arena.
+
+A linear layer over the M = prod(x.shape[:-1]) rows is the GEMM of a 1x1
+convolution over NHWC pixel rows (ops/conv1x1.py):
+
+  forward      y[M, N]  = x[M, K] . W[N, K]^T (+ b in the epilogue)   gemm_nt
+  grad-input   dx[M, K] = dy[M, N] . Wt[K, N]^T                       gemm_nt (Wt = W^T)
+  grad-weight  dW[N, K] += dy[M, N]^T . x[M, K]  (fp32 atomics)       gemm_tn_acc
+  grad-bias    db[N]   += sum_m dy[m, :]                             colsum_acc
+
+Each (direction, M, K, N) times the HIP kernel configurations and
+``torch.addmm`` / ``torch.mm`` (hipBLASLt) once per process and keeps the
+fastest (cache and switches shared with the convolutions: ``GKSGD_GEMM_TUNE``,
+``tuning/gemm_choices.json``; ``GKSGD_FASTLINEAR=0`` disables the path).
+Dimensions that are not multiples of 64 (the LSTM's 1500 -> 10000 softmax
+layer) keep hipBLASLt for the GEMMs and still get the fused bias gradient.
+``FastLinear`` is a drop-in ``nn.Linear`` (same parameters and state_dict
+keys); off the GPU or outside bf16 it is the stock layer (+ ``F.gelu``).
+
+Reference parity: the reference's models use ``nn.Linear`` (models/fcn.py,
+models/lstm.py:29); BERT is not in the reference (BASELINE config 5).
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import accum_grad_, load, require_native
+from . import conv1x1 as _cv
+
+_ENABLED = os.environ.get("GKSGD_FASTLINEAR", "1") != "0"
+
+
+def _g():
+    return torch.ops.gksgd
+
+
+def _colsum_ok(t: torch.Tensor) -> bool:
+    return (t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2 and t.is_contiguous() and
+            t.shape[1] % 8 == 0 and t.data_ptr() % 16 == 0)
+
+
+def bias_grad_acc_(db: torch.Tensor, dy: torch.Tensor) -> None:
+    """db (fp32 [N]) += dy.sum(0) for a 2-D [M, N] gradient."""
+    if _colsum_ok(dy) and db.dtype == torch.float32 and db.is_contiguous():
+        require_native(dy)
+        _g().colsum_acc(dy, db)
+    else:
+        db.add_(dy.float().sum(0))
+
+
+def gelu_backward_(dy: torch.Tensor, pre: torch.Tensor, db: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dpre = dy * gelu'(pre) (erf GELU) in pre's dtype; with ``db`` (fp32 [N])
+    also db += dpre.sum(0) -- one pass on the GPU."""
+    if _colsum_ok(dy) and _colsum_ok(pre) and dy.shape == pre.shape and \
+            (db is None or (db.dtype == torch.float32 and db.is_contiguous())):
+        require_native(dy)
+        dpre = torch.empty_like(pre)
+        _g().gelu_bwd_colsum(dy, pre, dpre, db)
+        return dpre
+    dpre = torch.ops.aten.gelu_backward(dy.float(), pre.float()).to(pre.dtype)
+    if db is not None:
+        db.add_(dpre.float().sum(0))
+    return dpre
+
+
+def _hip_gemm_ok(K: int, N: int) -> bool:
+    return K % 64 == 0 and N % 64 == 0
+
+
+def _fwd(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor]) -> torch.Tensor:
+    """y = x2 . w^T (+ bias), bf16 out."""
+    M, K = x2.shape
+    N = w.shape[0]
+    b16 = bias.to(torch.bfloat16) if bias is not None else None
+
+    def blas():
+        return torch.addmm(b16, x2, w.t()) if b16 is not None else torch.mm(x2, w.t())
+    if not _hip_gemm_ok(K, N):
+        return blas()
+    g = _g()
+    y = torch.empty(M, N, dtype=torch.bfloat16, device=x2.device)
+    cands = [(("hip", c, mb), (lambda c=c, mb=mb: g.gemm_nt(x2, w, y, c, mb, None, bias)))
+             for c in _cv._NT_CFGS for mb in _cv._NT_GRIDS]
+    cands.append((("blas", 0, 0), blas))
+    ch = _cv._pick(("lin_fwd", M, K, N, bias is not None), cands)
+    if ch[0] == "blas":
+        return blas()
+    g.gemm_nt(x2, w, y, ch[1], ch[2], None, bias)
+    return y
+
+
+def _dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """dx = dy2 . w, bf16 out."""
+    M, N = dy2.shape
+    K = w.shape[1]
+    key = ("lin_dgrad", M, K, N)
+    got = _cv._choices.get(key)
+    if not _hip_gemm_ok(K, N) or (got is not None and got[0] == "blas"):
+        return torch.mm(dy2, w)
+    g = _g()
+    dx = torch.empty(M, K, dtype=torch.bfloat16, device=dy2.device)
+    wt = w.t().contiguous()
+    cands = [(("hip", c, mb), (lambda c=c, mb=mb: g.gemm_nt(dy2, wt, dx, c, mb)))
+             for c in _cv._NT_CFGS for mb in _cv._NT_GRIDS]
+    cands.append((("blas", 0, 0), lambda: torch.mm(dy2, w)))
+    ch = _cv._pick(key, cands)
+    if ch[0] == "blas":
+        return torch.mm(dy2, w)
+    g.gemm_nt(dy2, wt, dx, ch[1], ch[2])
+    return dx
+
+
+def _wgrad_into(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor) -> None:
+    """out (fp32 [N, K]) += dy2^T . x2."""
+    M, N = dy2.shape
+    K = x2.shape[1]
+
+    def blas(o):
+        accum_grad_(o, torch.mm(dy2.t(), x2))
+    if not _hip_gemm_ok(K, N):
+        blas(out)
+        return
+    g = _g()
+    key = ("lin_wgrad", M, K, N)
+    scratch = torch.zeros_like(out) if key not in _cv._choices else None
+    cands = [(("hip", c, sp), (lambda c=c, sp=sp: g.gemm_tn_acc(dy2, x2, scratch, c, sp)))
+             for c, sp in _cv._TN_CFGS]
+    cands.append((("blas", 0, 0), lambda: blas(scratch)))
+    ch = _cv._pick(key, cands)
+    if ch[0] == "blas":
+        blas(out)
+    else:
+        g.gemm_tn_acc(dy2, x2, out, ch[1], ch[2])
+
+
+def _target(sink) -> Optional[torch.Tensor]:
+    """The fp32 arena gradient view a shadow sink accumulates into (None: no direct path)."""
+    if sink is None:
+        return None
+    gv = getattr(sink, "grad_view", None)
+    if gv is None or not gv.is_contiguous():
+        return None
+    sink.check()
+    return gv
+
+
+class _LinearFn(torch.autograd.Function):
+    """y = act(x . W^T + b) with bf16 operands.  ``weight`` / ``bias`` are the
+    fp32 master parameters; with sinks (bf16-shadow path, parallel/shadow.py)
+    their gradients are added into the optimizer's fp32 arena in the backward
+    and None is returned for them, so AccumulateGrad launches nothing (its
+    post-accumulate hook still reports the parameter ready)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, w_bf16, wsink, bias, bsink, gelu):
+        shape = x.shape
+        K = shape[-1]
+        x2 = x.reshape(-1, K)
+        if x2.dtype != torch.bfloat16:
+            x2 = x2.to(torch.bfloat16)
+        x2 = x2.contiguous()
+        w = w_bf16 if w_bf16 is not None else weight.detach().to(torch.bfloat16)
+        w = w.contiguous()
+        b = bias.detach().float().contiguous() if bias is not None else None
+        y = _fwd(x2, w, b)
+        pre = None
+        if gelu:
+            pre, y = y, F.gelu(y)
+        ctx.save_for_backward(x2, w, pre)
+        ctx.wsink, ctx.bsink, ctx.gelu = wsink, bsink, gelu
+        ctx.has_bias = bias is not None
+        ctx.in_shape = shape
+        ctx.wdtype = weight.dtype
+        ctx.bdtype = bias.dtype if bias is not None else None
+        return y.view(*shape[:-1], y.shape[-1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, pre = ctx.saved_tensors
+        N, K = w.shape
+        dy2 = dy.reshape(-1, N)
+        if dy2.dtype != torch.bfloat16:
+            dy2 = dy2.to(torch.bfloat16)
+        dy2 = dy2.contiguous()
+        db = gbias = None
+        if ctx.has_bias and ctx.needs_input_grad[4]:
+            db = _target(ctx.bsink)
+            if db is None:
+                db = gbias = torch.zeros(N, dtype=torch.float32, device=dy2.device)
+        if ctx.gelu:
+            dpre = gelu_backward_(dy2, pre, db)
+        else:
+            dpre = dy2
+            if db is not None:
+                bias_grad_acc_(db, dpre)
+        dx = _dgrad(dpre, w).view(ctx.in_shape) if ctx.needs_input_grad[0] else None
+        gweight = None
+        if ctx.needs_input_grad[1]:
+            gw = _target(ctx.wsink)
+            if gw is not None:
+                _wgrad_into(dpre, x2, gw)
+            else:
+                gw = torch.zeros(N, K, dtype=torch.float32, device=dy2.device)
+                _wgrad_into(dpre, x2, gw)
+                if ctx.wsink is not None:
+                    ctx.wsink(gw)
+                else:
+                    gweight = gw.to(ctx.wdtype)
+        if gbias is not None:
+            if ctx.bsink is not None:
+                ctx.bsink(gbias)
+                gbias = None
+            else:
+                gbias = gbias.to(ctx.bdtype)
+        return dx, gweight, None, None, gbias, None, None
+
+
+def _supported(x: torch.Tensor, mod: nn.Linear) -> bool:
+    return (_ENABLED and x.is_cuda and x.dim() >= 1 and x.shape[-1] == mod.in_features and x.numel() > 0 and
+            mod.weight.dtype == torch.float32 and mod.in_features % 8 == 0 and mod.out_features % 8 == 0)
+
+
+class FastLinear(nn.Linear):
+    """``nn.Linear`` whose bf16 training path on a GPU runs the autotuned MFMA
+    kernels and the fused bias-gradient pass; ``forward(x, act="gelu")``
+    applies GELU with its backward fused into that pass.  Everywhere else it
+    is the stock layer (+ ``F.gelu``)."""
+
+    def forward(self, x: torch.Tensor, act: Optional[str] = None) -> torch.Tensor:
+        if act not in (None, "gelu"):
+            raise ValueError("FastLinear act must be None or 'gelu', got %r" % (act,))
+        dev = x.device.type
+        bf16 = x.dtype == torch.bfloat16 or (torch.is_autocast_enabled(dev) and
+                                             torch.get_autocast_dtype(dev) == torch.bfloat16)
+        if bf16 and _supported(x, self) and load():
+            table = getattr(self, "_gk_shadow", None)
+            winfo = table.get("weight") if table else None
+            binfo = table.get("bias") if table else None
+            use_shadow = winfo is not None and torch.is_autocast_enabled(dev)
+            w_bf16, wsink = (winfo[0], winfo[1]) if use_shadow else (None, None)
+            bsink = binfo[1] if (use_shadow and binfo is not None) else None
+            if not torch.is_grad_enabled() or not self.weight.requires_grad:
+                wsink = None
+            if not torch.is_grad_enabled() or self.bias is None or not self.bias.requires_grad:
+                bsink = None
+            return _LinearFn.apply(x, self.weight, w_bf16, wsink, self.bias, bsink, act == "gelu")
+        slow = getattr(self, "_gk_slow", None)
+        y = slow(x) if slow is not None else super().forward(x)
+        return F.gelu(y) if act == "gelu" else y

@@ -31,6 +31,7 @@ import torch.nn.functional as F
 
 from ..ops.bn import BNAct
 from ..ops.conv1x1 import FastConv2d
+from ..ops.linear import FastLinear
 
 
 class _ShadowWeight(torch.autograd.Function):
@@ -80,10 +81,10 @@ def install_bf16_shadow(model: nn.Module, opt) -> int:
     names = opt._parameter_names
     count = 0
     for mod in model.modules():
-        if isinstance(mod, FastConv2d):
+        if isinstance(mod, (FastConv2d, FastLinear)):
             # its own forward reads the shadow view and (GEMM path) adds the fp32
-            # weight gradient straight into the arena; other strides fall back
-            # to the plain shadow conv
+            # weight / bias gradients straight into the arena; unsupported
+            # shapes fall back to the plain shadow conv / linear
             table = {}
             for pname in ("weight", "bias"):
                 p = getattr(mod, pname, None)
@@ -93,7 +94,8 @@ def install_bf16_shadow(model: nn.Module, opt) -> int:
                     count += 1
             if table:
                 mod._gk_shadow = table
-                mod._gk_slow = types.MethodType(_conv_forward, mod)
+                mod._gk_slow = types.MethodType(_conv_forward if isinstance(mod, FastConv2d) else _linear_forward,
+                                                mod)
         elif isinstance(mod, (nn.Conv2d, nn.Linear)) and type(mod).forward in (nn.Conv2d.forward, nn.Linear.forward):
             table = {}
             for pname in ("weight", "bias"):
