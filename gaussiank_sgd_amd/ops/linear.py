@@ -126,18 +126,23 @@ def _wgrad_into(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor) -> None:
 
     def blas(o):
         accum_grad_(o, torch.mm(dy2.t(), x2))
-    if not _hip_gemm_ok(K, N):
-        blas(out)
-        return
+
+    def blas32(o):   # hipBLASLt bf16 x bf16 -> fp32 with beta = 1, straight into the arena view
+        torch.addmm(o, dy2.t(), x2, out_dtype=torch.float32, out=o)
     g = _g()
     key = ("lin_wgrad", M, K, N)
     scratch = torch.zeros_like(out) if key not in _cv._choices else None
-    cands = [(("hip", c, sp), (lambda c=c, sp=sp: g.gemm_tn_acc(dy2, x2, scratch, c, sp)))
-             for c, sp in _cv._TN_CFGS]
+    cands = []
+    if _hip_gemm_ok(K, N):
+        cands = [(("hip", c, sp), (lambda c=c, sp=sp: g.gemm_tn_acc(dy2, x2, scratch, c, sp)))
+                 for c, sp in _cv._TN_CFGS]
+    cands.append((("blas32", 0, 0), lambda: blas32(scratch)))
     cands.append((("blas", 0, 0), lambda: blas(scratch)))
     ch = _cv._pick(key, cands)
     if ch[0] == "blas":
         blas(out)
+    elif ch[0] == "blas32":
+        blas32(out)
     else:
         g.gemm_tn_acc(dy2, x2, out, ch[1], ch[2])
 

@@ -26,7 +26,10 @@ def _ops():
 
 class _AddLNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, a, x, gamma, beta, eps, p, seed):
+    def forward(ctx, a, x, gamma, beta, eps, p, seed, direct=None):
+        # direct = (dgamma_view, dbeta_view): fp32 gradient-arena views the
+        # backward kernel accumulates into (bf16-shadow path); None is then
+        # returned for gamma / beta, so AccumulateGrad launches nothing
         H = x.shape[-1]
         a = a.to(torch.bfloat16).contiguous()
         x = x.to(torch.bfloat16).contiguous()
@@ -42,6 +45,7 @@ class _AddLNFn(torch.autograd.Function):
         ctx.p, ctx.seed = float(p), int(seed)
         ctx.has_g, ctx.has_b = gamma is not None, beta is not None
         ctx.gdtype = gamma.dtype if gamma is not None else torch.float32
+        ctx.direct = direct
         return y
 
     @staticmethod
@@ -52,15 +56,21 @@ class _AddLNFn(torch.autograd.Function):
         dy = dy.to(torch.bfloat16).contiguous()
         dx = torch.empty_like(h)
         da = torch.empty_like(h) if ctx.p > 0 else None
-        dg = torch.empty(H, dtype=torch.float32, device=h.device) if ctx.has_g and ctx.needs_input_grad[2] else None
-        db = torch.empty(H, dtype=torch.float32, device=h.device) if ctx.has_b and ctx.needs_input_grad[3] else None
+        direct = ctx.direct
+        if direct is not None:
+            dg, db = direct
+        else:
+            dg = torch.empty(H, dtype=torch.float32, device=h.device) if ctx.has_g and ctx.needs_input_grad[2] else None
+            db = torch.empty(H, dtype=torch.float32, device=h.device) if ctx.has_b and ctx.needs_input_grad[3] else None
         ws = torch.empty(int(_ops().add_ln_ws_floats(R, H)), dtype=torch.float32, device=h.device)
-        _ops().add_ln_backward(dy, h, mean, rstd, g if ctx.has_g else None, dx, da, dg, db, False, ws, ctx.p,
-                               ctx.seed)
+        _ops().add_ln_backward(dy, h, mean, rstd, g if ctx.has_g else None, dx, da, dg, db, direct is not None, ws,
+                               ctx.p, ctx.seed)
         if da is None:
             da = dx
+        if direct is not None:
+            return da, dx, None, None, None, None, None, None
         return (da, dx, dg.to(ctx.gdtype) if dg is not None else None,
-                db.to(ctx.gdtype) if db is not None else None, None, None, None)
+                db.to(ctx.gdtype) if db is not None else None, None, None, None, None)
 
 
 def fused_available(x: torch.Tensor) -> bool:
@@ -79,5 +89,8 @@ def add_layernorm(a: torch.Tensor, x: torch.Tensor, ln: nn.LayerNorm, p: float =
     if (fused_available(x) and ln.elementwise_affine and len(ln.normalized_shape) == 1 and
             a.shape == x.shape):
         seed = int(torch.randint(0, 2 ** 31 - 1, (1,), generator=_seed_gen)) if p > 0 else 0
-        return _AddLNFn.apply(a, x, ln.weight, ln.bias, ln.eps, p, seed)
+        direct = getattr(ln, "_gk_direct", None)
+        if direct is not None and not (torch.is_grad_enabled() and ln.weight.requires_grad and ln.bias.requires_grad):
+            direct = None
+        return _AddLNFn.apply(a, x, ln.weight, ln.bias, ln.eps, p, seed, direct)
     return ln(x + F.dropout(a, p, training=p > 0))

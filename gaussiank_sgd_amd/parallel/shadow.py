@@ -16,7 +16,8 @@ MI355X (profiles/r01_resnet50_bs256_fusedbn_kernel_stats.csv).
     post-accumulate hook still fires afterwards and reports the parameter
     ready to the bucket engine exactly as on the plain path;
   * ``BNAct`` modules get the same direct path for gamma/beta: the BN backward
-    kernel adds them into the arena.
+    kernel adds them into the arena; so do LayerNorms used through
+    ``ops/ln.py add_layernorm`` (the fused add+LN backward accumulates them).
 Outside bf16 autocast modules fall back to their fp32 parameters, so the
 model stays usable for fp32 evaluation.  (CPU autocast works too -- the ops
 have PyTorch fallbacks -- which is how the CPU tests check the wiring.)
@@ -108,6 +109,12 @@ def install_bf16_shadow(model: nn.Module, opt) -> int:
             if table:
                 mod._gk_shadow = table
                 mod.forward = types.MethodType(_conv_forward if isinstance(mod, nn.Conv2d) else _linear_forward, mod)
+        elif isinstance(mod, nn.LayerNorm) and mod.elementwise_affine and mod.bias is not None:
+            # ops/ln.py add_layernorm: the fused backward accumulates dgamma /
+            # dbeta straight into the arena (plain ln(x) calls ignore this)
+            if mod.weight in names and mod.bias in names:
+                mod._gk_direct = (arena.grad_views[names[mod.weight]], arena.grad_views[names[mod.bias]])
+                count += 2
         elif isinstance(mod, BNAct) and mod.affine:
             if mod.weight in names and mod.bias in names:
                 kw, kb = names[mod.weight], names[mod.bias]

@@ -58,3 +58,44 @@ def test_add_ln_dropout_statistics_and_consistency():
     kept = ~dropped
     ratio = (a.grad.float()[kept] / x.grad.float()[kept]).median().item()
     assert abs(ratio - 1 / (1 - p)) < 0.02
+
+
+def test_add_ln_direct_arena_grads():
+    """bf16-shadow path: dgamma / dbeta accumulated by the fused backward
+    straight into the optimizer's fp32 arena == the autograd path."""
+    import copy
+    from gaussiank_sgd_amd.compression import compressors
+    from gaussiank_sgd_amd.ops.linear import FastLinear
+    from gaussiank_sgd_amd.ops.ln import add_layernorm
+    from gaussiank_sgd_amd.parallel import comm, install_bf16_shadow
+    from gaussiank_sgd_amd.parallel.distributed_optimizer import DistributedOptimizer
+
+    class Blk(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.lin = FastLinear(128, 128)
+            self.ln = torch.nn.LayerNorm(128)
+
+        def forward(self, x):
+            return add_layernorm(self.lin(x), x, self.ln, 0.1, True)
+    comm.init()
+    torch.manual_seed(3)
+    net = Blk().cuda()
+    torch.nn.init.uniform_(net.ln.weight, 0.5, 1.5)
+    ref = copy.deepcopy(net)
+    opt = DistributedOptimizer(torch.optim.SGD(net.parameters(), lr=0.1), named_parameters=net.named_parameters(),
+                               compression=compressors["none"], is_sparse=False, density=1.0)
+    install_bf16_shadow(net, opt)
+    assert getattr(net.ln, "_gk_direct", None) is not None
+    x = torch.randn(300, 128, device="cuda")
+    for model in (net, ref):
+        import gaussiank_sgd_amd.ops.ln as lnmod
+        lnmod._seed_gen.manual_seed(7)          # same dropout mask in both runs
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = model(x)
+        y.float().square().mean().backward()
+    torch.cuda.synchronize()
+    for (n, p), (_, q) in zip(net.named_parameters(), ref.named_parameters()):
+        assert p.grad is not None, n
+        err = (p.grad - q.grad).abs().max().item()
+        assert err <= 2e-2 * q.grad.abs().max().item() + 1e-4, (n, err)
