@@ -231,7 +231,7 @@ class _LinearFn(torch.autograd.Function):
 
 def _supported(x: torch.Tensor, mod: nn.Linear) -> bool:
     return (_ENABLED and x.is_cuda and x.dim() >= 1 and x.shape[-1] == mod.in_features and x.numel() > 0 and
-            mod.weight.dtype == torch.float32 and mod.in_features % 8 == 0 and mod.out_features % 8 == 0)
+            mod.weight.dtype == torch.float32 and mod.out_features % 8 == 0)
 
 
 class FastLinear(nn.Linear):

@@ -309,6 +309,20 @@ class RcclCommunicator:
         uid_list = broadcast_object(uid.tolist() if uid is not None else None, 0)
         uid_t = torch.tensor(uid_list, dtype=torch.uint8)
         self.engine.init(uid_t, self.rank, self.world, self.device.index or 0)
+        self.self_test()
+
+    def self_test(self) -> None:
+        """One all-gather of the rank ids on the current stream, checked on the
+        host once at start-up: a mis-bootstrapped communicator fails here
+        (and the Exchanger falls back to torch.distributed on every rank)
+        instead of corrupting gradients later."""
+        inp = torch.full((4,), self.rank, dtype=torch.int32, device=self.device)
+        out = torch.full((4 * self.world,), -1, dtype=torch.int32, device=self.device)
+        self.engine.allgather(inp, out)
+        got = out.view(self.world, 4).cpu()
+        want = torch.arange(self.world, dtype=torch.int32)[:, None].expand(self.world, 4)
+        if not torch.equal(got, want):
+            raise RuntimeError("native RCCL all-gather self-test failed: %s" % got[:, 0].tolist())
 
     def allgather_(self, out: torch.Tensor, inp: torch.Tensor) -> None:
         self.engine.allgather(inp, out)
@@ -339,12 +353,21 @@ class Exchanger:
         if self.P > 1:
             self.kind = "torch"
             if prefer_native and self.device.type == "cuda" and os.environ.get("GKSGD_NATIVE_RCCL", "1") == "1":
+                ok = 1
                 try:
                     self.native = RcclCommunicator(self.device)
-                    self.kind = "rccl-native"
                 except Exception as e:  # pragma: no cover - GPU only
                     from ..settings import logger
                     logger.warning("native RCCL engine unavailable (%s); using torch.distributed", e)
+                    ok = 0
+                # every rank takes the same path: one failed self-test sends all to torch.distributed
+                flag = torch.tensor([ok], dtype=torch.int32,
+                                    device=self.device if backend() == "nccl" else "cpu")
+                dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+                if int(flag) == 1:
+                    self.kind = "rccl-native"
+                elif self.native is not None:
+                    self.native.destroy()
                     self.native = None
 
     def allgather_(self, out: torch.Tensor, inp: torch.Tensor) -> None:

@@ -363,3 +363,13 @@ def test_momentum_correct_and_mask(cuda):
     ops.mask_records_(u, rec.to(cuda), k_cap)
     uc[idx.long()] = 0
     assert torch.equal(u.cpu(), uc)
+
+
+def test_rccl_communicator_self_test_world1(cuda):
+    """RcclCommunicator bootstrap + its start-up all-gather self-test."""
+    from gaussiank_sgd_amd.parallel import comm
+    comm.init()
+    c = comm.RcclCommunicator(cuda)
+    c.self_test()
+    torch.cuda.synchronize()
+    c.destroy()
