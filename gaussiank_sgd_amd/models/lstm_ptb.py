@@ -3,8 +3,10 @@
 Parity: reference models/lstm.py:5-47 -- embedding 1500, 2 x LSTM(1500),
 35 unrolled steps, dropout 1 - 0.35 = 0.65, vocab 10k, uniform(-0.1, 0.1)
 init of embedding and softmax weights; 66,034,000 parameters in 11 tensors.
-``forward(inputs[T,B], hidden) -> (logits[T,B,V], hidden)``.  On ROCm the
-LSTM runs on MIOpen's fused RNN kernels.
+``forward(inputs[T,B], hidden) -> (logits[T,B,V], hidden)``.  The LSTM is
+``ops/lstm.py GkLSTM`` (same parameters as ``nn.LSTM``): bf16 hipBLASLt GEMMs
+and one fused HIP cell kernel per step -- nn.LSTM on ROCm (MIOpen) would
+compute in fp16 under bf16 autocast.
 """
 from __future__ import annotations
 
@@ -12,6 +14,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.linear import FastLinear
+from ..ops.lstm import GkLSTM
 
 
 class PTBLSTM(nn.Module):
@@ -26,8 +29,9 @@ class PTBLSTM(nn.Module):
         self.num_layers = num_layers
         self.dropout = nn.Dropout(1 - dp_keep_prob)
         self.word_embeddings = nn.Embedding(vocab_size, embedding_dim)
-        self.lstm = nn.LSTM(input_size=embedding_dim, hidden_size=embedding_dim, num_layers=num_layers,
-                            dropout=1 - dp_keep_prob)
+        # drop-in nn.LSTM (same parameter names): bf16 GEMMs + fused HIP cells (ops/lstm.py)
+        self.lstm = GkLSTM(input_size=embedding_dim, hidden_size=embedding_dim, num_layers=num_layers,
+                           dropout=1 - dp_keep_prob)
         self.sm_fc = FastLinear(embedding_dim, vocab_size)   # fused bias-gradient pass on the GPU
         self.name = "lstm"
         self.init_weights()

@@ -37,6 +37,7 @@ HIP_SOURCES = [
     "kernels/gemm.hip",
     "kernels/ln.hip",
     "kernels/linear.hip",
+    "kernels/lstm.hip",
 ]
 CXX_SOURCES = [
     "comm/rccl_engine.cpp",

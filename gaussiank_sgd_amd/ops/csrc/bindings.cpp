@@ -779,6 +779,56 @@ void gelu_bwd_colsum(at::Tensor dy, at::Tensor pre, at::Tensor dpre, c10::option
                            static_cast<uint16_t*>(dpre.data_ptr()), d, dy.size(0), (int)dy.size(1), cur_stream(dy));
 }
 
+// LSTM cell (lstm.hip)
+void check_lstm(const at::Tensor& t, at::ScalarType dt, int64_t numel, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == dt && t.is_contiguous() && t.numel() == numel, name,
+              " must be a contiguous ", at::toString(dt), " GPU tensor of ", numel, " elements");
+}
+
+void lstm_cell_fwd(at::Tensor xg, at::Tensor hg, at::Tensor c_prev, at::Tensor c, at::Tensor h, at::Tensor gates) {
+  TORCH_CHECK(xg.dim() == 2 && xg.size(1) % 4 == 0, "xg must be [B, 4H]");
+  const int64_t B = xg.size(0), H = xg.size(1) / 4;
+  check_lstm(xg, at::kBFloat16, B * 4 * H, "xg");
+  check_lstm(hg, at::kBFloat16, B * 4 * H, "hg");
+  check_lstm(c_prev, at::kFloat, B * H, "c_prev");
+  check_lstm(c, at::kFloat, B * H, "c");
+  check_lstm(h, at::kBFloat16, B * H, "h");
+  check_lstm(gates, at::kFloat, B * 4 * H, "gates");
+  c10::DeviceGuard guard(xg.device());
+  gk::lstm_cell_fwd(static_cast<const uint16_t*>(xg.data_ptr()), static_cast<const uint16_t*>(hg.data_ptr()),
+                    c_prev.data_ptr<float>(), c.data_ptr<float>(), static_cast<uint16_t*>(h.data_ptr()),
+                    gates.data_ptr<float>(), (int)B, (int)H, cur_stream(xg));
+}
+
+void lstm_cell_bwd(c10::optional<at::Tensor> dout, c10::optional<at::Tensor> dh_rec, c10::optional<at::Tensor> dc_next,
+                   at::Tensor gates, at::Tensor c, at::Tensor c_prev, at::Tensor dG, at::Tensor dc_prev) {
+  TORCH_CHECK(gates.dim() == 2 && gates.size(1) % 4 == 0, "gates must be [B, 4H]");
+  const int64_t B = gates.size(0), H = gates.size(1) / 4;
+  check_lstm(gates, at::kFloat, B * 4 * H, "gates");
+  check_lstm(c, at::kFloat, B * H, "c");
+  check_lstm(c_prev, at::kFloat, B * H, "c_prev");
+  check_lstm(dG, at::kBFloat16, B * 4 * H, "dG");
+  check_lstm(dc_prev, at::kFloat, B * H, "dc_prev");
+  const uint16_t* po = nullptr;
+  const uint16_t* pr = nullptr;
+  const float* pc = nullptr;
+  if (dout.has_value() && dout->defined()) {
+    check_lstm(*dout, at::kBFloat16, B * H, "dout");
+    po = static_cast<const uint16_t*>(dout->data_ptr());
+  }
+  if (dh_rec.has_value() && dh_rec->defined()) {
+    check_lstm(*dh_rec, at::kBFloat16, B * H, "dh_rec");
+    pr = static_cast<const uint16_t*>(dh_rec->data_ptr());
+  }
+  if (dc_next.has_value() && dc_next->defined()) {
+    check_lstm(*dc_next, at::kFloat, B * H, "dc_next");
+    pc = dc_next->data_ptr<float>();
+  }
+  c10::DeviceGuard guard(gates.device());
+  gk::lstm_cell_bwd(po, pr, pc, gates.data_ptr<float>(), c.data_ptr<float>(), c_prev.data_ptr<float>(),
+                    static_cast<uint16_t*>(dG.data_ptr()), dc_prev.data_ptr<float>(), (int)B, (int)H, cur_stream(gates));
+}
+
 }  // namespace
 
 
@@ -846,6 +896,9 @@ TORCH_LIBRARY(gksgd, m) {
   m.def("conv_tn_acc(Tensor dy, Tensor x, Tensor(a!) wout, Tensor zero, int stride, int pad, int cfg=0, int splits=0) -> ()");
   m.def("colsum_acc(Tensor dy, Tensor(a!) db) -> ()");
   m.def("gelu_bwd_colsum(Tensor dy, Tensor pre, Tensor(a!) dpre, Tensor(b!)? db=None) -> ()");
+  m.def("lstm_cell_fwd(Tensor xg, Tensor hg, Tensor c_prev, Tensor(a!) c, Tensor(b!) h, Tensor(c!) gates) -> ()");
+  m.def("lstm_cell_bwd(Tensor? dout, Tensor? dh_rec, Tensor? dc_next, Tensor gates, Tensor c, Tensor c_prev, "
+        "Tensor(a!) dG, Tensor(b!) dc_prev) -> ()");
 
   m.class_<RcclEngine>("RcclEngine")
       .def(torch::init<>())
@@ -888,4 +941,6 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("add_ln_backward", &add_ln_backward);
   m.impl("colsum_acc", &colsum_acc);
   m.impl("gelu_bwd_colsum", &gelu_bwd_colsum);
+  m.impl("lstm_cell_fwd", &lstm_cell_fwd);
+  m.impl("lstm_cell_bwd", &lstm_cell_bwd);
 }

@@ -270,4 +270,16 @@ void colsum_acc_bf16(const uint16_t* dy, float* db, int64_t M, int N, hipStream_
 void gelu_bwd_colsum_bf16(const uint16_t* dy, const uint16_t* pre, uint16_t* dpre, float* db, int64_t M, int N,
                           hipStream_t stream);
 
+// ---------------------------------------------------------------------------
+// LSTM cell (lstm.hip), PyTorch gate order i, f, g, o; rows [B][4H] / [B][H].
+//   fwd: G = xg + hg (bf16 pre-activations) -> c (fp32), h (bf16), gates (fp32)
+//   bwd: dh = dout + dh_rec (bf16, either may be null), dc_next (fp32, may be
+//        null) -> dG (bf16 [B][4H]), dc_prev (fp32)
+// ---------------------------------------------------------------------------
+void lstm_cell_fwd(const uint16_t* xg, const uint16_t* hg, const float* c_prev, float* c, uint16_t* h, float* gates,
+                   int B, int H, hipStream_t stream);
+void lstm_cell_bwd(const uint16_t* dout, const uint16_t* dh_rec, const float* dc_next, const float* gates,
+                   const float* c, const float* c_prev, uint16_t* dG, float* dc_prev, int B, int H,
+                   hipStream_t stream);
+
 }  // namespace gk

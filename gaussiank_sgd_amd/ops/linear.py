@@ -129,6 +129,9 @@ def _wgrad_into(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor) -> None:
 
     def blas32(o):   # hipBLASLt bf16 x bf16 -> fp32 with beta = 1, straight into the arena view
         torch.addmm(o, dy2.t(), x2, out_dtype=torch.float32, out=o)
+    if not dy2.is_cuda:
+        blas(out)
+        return
     g = _g()
     key = ("lin_wgrad", M, K, N)
     scratch = torch.zeros_like(out) if key not in _cv._choices else None

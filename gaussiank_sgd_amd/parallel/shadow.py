@@ -33,6 +33,7 @@ import torch.nn.functional as F
 from ..ops.bn import BNAct
 from ..ops.conv1x1 import FastConv2d
 from ..ops.linear import FastLinear
+from ..ops.lstm import GkLSTM
 
 
 class _ShadowWeight(torch.autograd.Function):
@@ -109,6 +110,17 @@ def install_bf16_shadow(model: nn.Module, opt) -> int:
             if table:
                 mod._gk_shadow = table
                 mod.forward = types.MethodType(_conv_forward if isinstance(mod, nn.Conv2d) else _linear_forward, mod)
+        elif isinstance(mod, GkLSTM):
+            # bf16 weight views for its GEMMs; its backward adds every weight /
+            # bias gradient straight into the arena
+            table = {}
+            for pname, p in mod.named_parameters(recurse=False):
+                if p in names:
+                    key = names[p]
+                    table[pname] = (arena.view_of(shadow, key), opt._make_sink(key))
+                    count += 1
+            if table:
+                mod._gk_shadow = table
         elif isinstance(mod, nn.LayerNorm) and mod.elementwise_affine and mod.bias is not None:
             # ops/ln.py add_layernorm: the fused backward accumulates dgamma /
             # dbeta straight into the arena (plain ln(x) calls ignore this)
