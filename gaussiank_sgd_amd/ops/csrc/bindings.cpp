@@ -785,23 +785,65 @@ void check_lstm(const at::Tensor& t, at::ScalarType dt, int64_t numel, const cha
               " must be a contiguous ", at::toString(dt), " GPU tensor of ", numel, " elements");
 }
 
-void lstm_cell_fwd(at::Tensor xg, at::Tensor hg, at::Tensor c_prev, at::Tensor c, at::Tensor h, at::Tensor gates) {
+// P: fp32 [S][B][N] K-slice partials of the step GEMM (N = 4Hp forward, Hp backward)
+int64_t lstm_partials(const c10::optional<at::Tensor>& P, int64_t S, int64_t B, int64_t H, int64_t gates_mult,
+                      const float** out) {
+  *out = nullptr;
+  if (!(P.has_value() && P->defined())) return 0;
+  TORCH_CHECK(P->is_cuda() && P->scalar_type() == at::kFloat && P->is_contiguous() && P->dim() == 3 &&
+                  P->size(0) >= S && S >= 1 && P->size(1) == B && P->size(2) % (64 * gates_mult) == 0 &&
+                  P->size(2) / gates_mult >= H,
+              "P must be a contiguous fp32 [>=S, B, ", gates_mult, "*Hp] tensor, Hp a multiple of 64 >= H");
+  *out = P->data_ptr<float>();
+  return P->size(2) / gates_mult;
+}
+
+uint16_t* lstm_pad(const c10::optional<at::Tensor>& t, int64_t rows, int64_t cols, const char* name) {
+  if (!(t.has_value() && t->defined())) return nullptr;
+  check_lstm(*t, at::kBFloat16, rows * cols, name);
+  return static_cast<uint16_t*>(t->data_ptr());
+}
+
+// Split-K recurrent GEMM: P[s] = A[:, slice s] B[:, slice s]^T, A [M, K], B [N, K] (bf16, row-major)
+void lstm_rec_gemm(at::Tensor A, at::Tensor Bm, at::Tensor P, int64_t S) {
+  TORCH_CHECK(A.dim() == 2 && Bm.dim() == 2 && A.size(1) == Bm.size(1), "A [M, K] and B [N, K] expected");
+  const int64_t M = A.size(0), K = A.size(1), N = Bm.size(0);
+  TORCH_CHECK(S >= 1 && K % (64 * S) == 0 && N % 64 == 0, "lstm_rec_gemm: K % (64 S) and N % 64 must be 0");
+  TORCH_CHECK(A.is_cuda() && A.scalar_type() == at::kBFloat16 && A.stride(1) == 1 && A.stride(0) % 8 == 0 &&
+                  Bm.is_cuda() && Bm.scalar_type() == at::kBFloat16 && Bm.stride(1) == 1 && Bm.stride(0) % 8 == 0,
+              "lstm_rec_gemm: bf16 GPU operands with unit column stride and 16-byte aligned rows");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(Bm.data_ptr()) % 16 == 0,
+              "lstm_rec_gemm: 16-byte aligned operands");
+  check_lstm(P, at::kFloat, S * M * N, "P");
+  c10::DeviceGuard guard(A.device());
+  gk::lstm_rec_gemm(static_cast<const uint16_t*>(A.data_ptr()), A.stride(0), static_cast<const uint16_t*>(Bm.data_ptr()),
+                    Bm.stride(0), P.data_ptr<float>(), (int)M, (int)N, (int)K, (int)S, cur_stream(A));
+}
+
+void lstm_cell_fwd(at::Tensor xg, c10::optional<at::Tensor> hg, c10::optional<at::Tensor> P, int64_t S, at::Tensor c_prev, at::Tensor c,
+                   at::Tensor h, c10::optional<at::Tensor> h_pad, at::Tensor gates) {
   TORCH_CHECK(xg.dim() == 2 && xg.size(1) % 4 == 0, "xg must be [B, 4H]");
   const int64_t B = xg.size(0), H = xg.size(1) / 4;
   check_lstm(xg, at::kBFloat16, B * 4 * H, "xg");
-  check_lstm(hg, at::kBFloat16, B * 4 * H, "hg");
   check_lstm(c_prev, at::kFloat, B * H, "c_prev");
   check_lstm(c, at::kFloat, B * H, "c");
   check_lstm(h, at::kBFloat16, B * H, "h");
   check_lstm(gates, at::kFloat, B * 4 * H, "gates");
+  const float* pp = nullptr;
+  int64_t Hp = lstm_partials(P, S, B, H, 4, &pp);
+  if (!pp) S = 0, Hp = (H + 63) / 64 * 64;
+  uint16_t* hp = lstm_pad(h_pad, B, Hp, "h_pad");
+  const uint16_t* ph = lstm_pad(hg, B, 4 * H, "hg");
   c10::DeviceGuard guard(xg.device());
-  gk::lstm_cell_fwd(static_cast<const uint16_t*>(xg.data_ptr()), static_cast<const uint16_t*>(hg.data_ptr()),
-                    c_prev.data_ptr<float>(), c.data_ptr<float>(), static_cast<uint16_t*>(h.data_ptr()),
-                    gates.data_ptr<float>(), (int)B, (int)H, cur_stream(xg));
+  gk::lstm_cell_fwd(static_cast<const uint16_t*>(xg.data_ptr()), ph, pp, (int)S, c_prev.data_ptr<float>(),
+                    c.data_ptr<float>(), static_cast<uint16_t*>(h.data_ptr()), hp, gates.data_ptr<float>(), (int)B,
+                    (int)H, (int)Hp, cur_stream(xg));
 }
 
-void lstm_cell_bwd(c10::optional<at::Tensor> dout, c10::optional<at::Tensor> dh_rec, c10::optional<at::Tensor> dc_next,
-                   at::Tensor gates, at::Tensor c, at::Tensor c_prev, at::Tensor dG, at::Tensor dc_prev) {
+void lstm_cell_bwd(c10::optional<at::Tensor> dout, c10::optional<at::Tensor> dh_rec, c10::optional<at::Tensor> P,
+                   int64_t S,
+                   c10::optional<at::Tensor> dc_next, at::Tensor gates, at::Tensor c, at::Tensor c_prev, at::Tensor dG,
+                   c10::optional<at::Tensor> dG_pad, at::Tensor dc_prev) {
   TORCH_CHECK(gates.dim() == 2 && gates.size(1) % 4 == 0, "gates must be [B, 4H]");
   const int64_t B = gates.size(0), H = gates.size(1) / 4;
   check_lstm(gates, at::kFloat, B * 4 * H, "gates");
@@ -810,23 +852,24 @@ void lstm_cell_bwd(c10::optional<at::Tensor> dout, c10::optional<at::Tensor> dh_
   check_lstm(dG, at::kBFloat16, B * 4 * H, "dG");
   check_lstm(dc_prev, at::kFloat, B * H, "dc_prev");
   const uint16_t* po = nullptr;
-  const uint16_t* pr = nullptr;
   const float* pc = nullptr;
   if (dout.has_value() && dout->defined()) {
     check_lstm(*dout, at::kBFloat16, B * H, "dout");
     po = static_cast<const uint16_t*>(dout->data_ptr());
   }
-  if (dh_rec.has_value() && dh_rec->defined()) {
-    check_lstm(*dh_rec, at::kBFloat16, B * H, "dh_rec");
-    pr = static_cast<const uint16_t*>(dh_rec->data_ptr());
-  }
   if (dc_next.has_value() && dc_next->defined()) {
     check_lstm(*dc_next, at::kFloat, B * H, "dc_next");
     pc = dc_next->data_ptr<float>();
   }
+  const float* pp = nullptr;
+  int64_t Hp = lstm_partials(P, S, B, H, 1, &pp);
+  if (!pp) S = 0, Hp = (H + 63) / 64 * 64;
+  uint16_t* gp = lstm_pad(dG_pad, B, 4 * Hp, "dG_pad");
+  const uint16_t* pr = lstm_pad(dh_rec, B, H, "dh_rec");
   c10::DeviceGuard guard(gates.device());
-  gk::lstm_cell_bwd(po, pr, pc, gates.data_ptr<float>(), c.data_ptr<float>(), c_prev.data_ptr<float>(),
-                    static_cast<uint16_t*>(dG.data_ptr()), dc_prev.data_ptr<float>(), (int)B, (int)H, cur_stream(gates));
+  gk::lstm_cell_bwd(po, pr, pp, (int)S, pc, gates.data_ptr<float>(), c.data_ptr<float>(), c_prev.data_ptr<float>(),
+                    static_cast<uint16_t*>(dG.data_ptr()), gp, dc_prev.data_ptr<float>(), (int)B, (int)H, (int)Hp,
+                    cur_stream(gates));
 }
 
 }  // namespace
@@ -896,9 +939,11 @@ TORCH_LIBRARY(gksgd, m) {
   m.def("conv_tn_acc(Tensor dy, Tensor x, Tensor(a!) wout, Tensor zero, int stride, int pad, int cfg=0, int splits=0) -> ()");
   m.def("colsum_acc(Tensor dy, Tensor(a!) db) -> ()");
   m.def("gelu_bwd_colsum(Tensor dy, Tensor pre, Tensor(a!) dpre, Tensor(b!)? db=None) -> ()");
-  m.def("lstm_cell_fwd(Tensor xg, Tensor hg, Tensor c_prev, Tensor(a!) c, Tensor(b!) h, Tensor(c!) gates) -> ()");
-  m.def("lstm_cell_bwd(Tensor? dout, Tensor? dh_rec, Tensor? dc_next, Tensor gates, Tensor c, Tensor c_prev, "
-        "Tensor(a!) dG, Tensor(b!) dc_prev) -> ()");
+  m.def("lstm_rec_gemm(Tensor A, Tensor B, Tensor(a!) P, int S) -> ()");
+  m.def("lstm_cell_fwd(Tensor xg, Tensor? hg, Tensor? P, int S, Tensor c_prev, Tensor(a!) c, Tensor(b!) h, Tensor(c!)? h_pad, "
+        "Tensor(d!) gates) -> ()");
+  m.def("lstm_cell_bwd(Tensor? dout, Tensor? dh_rec, Tensor? P, int S, Tensor? dc_next, Tensor gates, Tensor c, Tensor c_prev, "
+        "Tensor(a!) dG, Tensor(b!)? dG_pad, Tensor(c!) dc_prev) -> ()");
 
   m.class_<RcclEngine>("RcclEngine")
       .def(torch::init<>())
@@ -941,6 +986,7 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("add_ln_backward", &add_ln_backward);
   m.impl("colsum_acc", &colsum_acc);
   m.impl("gelu_bwd_colsum", &gelu_bwd_colsum);
+  m.impl("lstm_rec_gemm", &lstm_rec_gemm);
   m.impl("lstm_cell_fwd", &lstm_cell_fwd);
   m.impl("lstm_cell_bwd", &lstm_cell_bwd);
 }

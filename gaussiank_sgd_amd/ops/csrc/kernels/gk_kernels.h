@@ -271,15 +271,22 @@ void gelu_bwd_colsum_bf16(const uint16_t* dy, const uint16_t* pre, uint16_t* dpr
                           hipStream_t stream);
 
 // ---------------------------------------------------------------------------
-// LSTM cell (lstm.hip), PyTorch gate order i, f, g, o; rows [B][4H] / [B][H].
-//   fwd: G = xg + hg (bf16 pre-activations) -> c (fp32), h (bf16), gates (fp32)
-//   bwd: dh = dout + dh_rec (bf16, either may be null), dc_next (fp32, may be
-//        null) -> dG (bf16 [B][4H]), dc_prev (fp32)
+// LSTM (lstm.hip), PyTorch gate order i, f, g, o.  Hp = H rounded up to 64.
+//   lstm_rec_gemm: P[s][m][n] = sum_{k in slice s} A[m][k] B[n][k] (fp32 K-slice
+//                  partials, S slices; K % (64 S) == 0, N % 64 == 0)
+//   lstm_cell_fwd: G = xg [B][4H] (bf16) + hg [B][4H] (bf16, may be null)
+//                  + sum_s P[s] [B][4Hp] (may be null) -> c (fp32),
+//                  h (bf16 [B][H]; also into h_pad [B][Hp] when non-null), gates (fp32)
+//   lstm_cell_bwd: dh = dout + dh_rec (bf16, may be null) + sum_s P[s] [B][Hp] (may be null),
+//                  dc_next (fp32, may be null) -> dG (bf16 [B][4H]; also into
+//                  dG_pad [B][4Hp] when non-null), dc_prev (fp32)
 // ---------------------------------------------------------------------------
-void lstm_cell_fwd(const uint16_t* xg, const uint16_t* hg, const float* c_prev, float* c, uint16_t* h, float* gates,
-                   int B, int H, hipStream_t stream);
-void lstm_cell_bwd(const uint16_t* dout, const uint16_t* dh_rec, const float* dc_next, const float* gates,
-                   const float* c, const float* c_prev, uint16_t* dG, float* dc_prev, int B, int H,
-                   hipStream_t stream);
+void lstm_rec_gemm(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, float* P, int M, int N, int K,
+                   int S, hipStream_t stream);
+void lstm_cell_fwd(const uint16_t* xg, const uint16_t* hg, const float* P, int S, const float* c_prev, float* c, uint16_t* h,
+                   uint16_t* h_pad, float* gates, int B, int H, int Hp, hipStream_t stream);
+void lstm_cell_bwd(const uint16_t* dout, const uint16_t* dh_rec, const float* P, int S, const float* dc_next, const float* gates,
+                   const float* c, const float* c_prev, uint16_t* dG, uint16_t* dG_pad, float* dc_prev, int B, int H,
+                   int Hp, hipStream_t stream);
 
 }  // namespace gk

@@ -6,7 +6,7 @@
 // is one GEMM plus ONE of these element-wise kernels.
 //
 //   fwd: G = xg[t] + hg  (xg = x W_ih^T + b_ih + b_hh for every t, one GEMM;
-//        hg = h_{t-1} W_hh^T, the step's GEMM);  i, f, o = sigmoid, g = tanh
+//        hg = h_{t-1} W_hh^T, the step's split-K GEMM);  i, f, o = sigmoid, g = tanh
 //        (PyTorch gate order i, f, g, o: gate k of unit j is column k*H + j);
 //        c = f c_prev + i g;  h = o tanh(c).
 //        Writes h (bf16: the layer output and the next step's GEMM operand),
@@ -17,7 +17,9 @@
 //        (bf16: the operand of the dh_rec and weight-gradient GEMMs),
 //        dc_prev = dc f (fp32 carry).
 // One thread per (row, unit) owns its four gates; consecutive threads take
-// consecutive units, so every gate row is read coalesced.
+// consecutive units, so every gate row is read coalesced.  The step GEMMs run
+// split-K on rec_gemm_kernel below over 64-padded operands (h_pad, dG_pad and
+// padded copies of W_hh); the cell kernels sum its fp32 K-slices on load.
 #include "common.h"
 #include "gk_kernels.h"
 
@@ -35,22 +37,111 @@ __device__ __forceinline__ uint16_t f2bf16(float f) {  // round-to-nearest-even,
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
 
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Split-K recurrent GEMM  P[s][m][n] = sum_{k in slice s} A[m][k] B[n][k]
+// (fp32 partial slabs; the cell kernel that consumes them sums the S slices,
+// so there are no atomics and no inter-block hand-off).  The per-step LSTM
+// GEMM has M = batch (<= 128 per tile), N = 4H, K = H: as one GEMM it is
+// latency-bound on its K loop (~20 us for H = 1500 with hipBLASLt or the
+// gemm_nt kernel, bench/lstm_gemm_probe.py); split over S K-slices every
+// block runs only kslice / 32 MFMA steps.  Block = 4 waves; wave w owns rows
+// m0 + 32w .. +31 (two 16-row MFMA subtiles) x 64 columns (four subtiles).
+// Fragments load straight from global into registers, up to eight 32-deep K
+// steps in flight (A rows are L2-resident, each B row is read by one block per
+// slice).
+// Requirements (checked on the host): K % (64 S) == 0, N % 64 == 0, rows
+// 16-byte aligned.
+template <int D>
+__global__ __launch_bounds__(kBlock) void rec_gemm_kernel(const uint16_t* __restrict__ A, int64_t lda,
+                                                          const uint16_t* __restrict__ B, int64_t ldb,
+                                                          float* __restrict__ P, int M, int N, int kslice) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int n0 = blockIdx.x * 64;
+  const int s = blockIdx.y;
+  const int m0 = blockIdx.z * 128 + w * 32;
+  if (m0 >= M) return;  // no LDS / barriers: a wave past the last row just leaves
+  const int64_t kb = (int64_t)s * kslice + fq * 8;
+  const uint16_t* ap[2];
+  const uint16_t* bp[4];
+#pragma unroll
+  for (int ms = 0; ms < 2; ++ms) {
+    int r = m0 + ms * 16 + fr;
+    r = r < M ? r : M - 1;
+    ap[ms] = A + (int64_t)r * lda + kb;
+  }
+#pragma unroll
+  for (int ns = 0; ns < 4; ++ns) bp[ns] = B + (int64_t)(n0 + ns * 16 + fr) * ldb + kb;
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+    for (int ns = 0; ns < 4; ++ns) acc[ms][ns] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // D 32-deep K steps per batch: all 6 D fragment loads are issued before the
+  // first MFMA, so each wave keeps 6 D KB in flight (the kernel is bound by
+  // load latency, not by MFMA issue)
+  for (int k = 0; k < kslice; k += 32 * D) {
+    bf16x8 a[D][2], b[D][4];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+#pragma unroll
+      for (int ns = 0; ns < 4; ++ns) b[d][ns] = *reinterpret_cast<const bf16x8*>(bp[ns] + k + 32 * d);
+#pragma unroll
+      for (int ms = 0; ms < 2; ++ms) a[d][ms] = *reinterpret_cast<const bf16x8*>(ap[ms] + k + 32 * d);
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+      for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+        for (int ns = 0; ns < 4; ++ns)
+          acc[ms][ns] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[d][ms], b[d][ns], acc[ms][ns], 0, 0, 0);
+  }
+  // D[row = 4 fq + r][col = fr] of every 16x16 subtile
+  float* Ps = P + (int64_t)s * M * N;
+#pragma unroll
+  for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + ms * 16 + fq * 4 + r;
+      if (m < M) {
+#pragma unroll
+        for (int ns = 0; ns < 4; ++ns) Ps[(int64_t)m * N + n0 + ns * 16 + fr] = acc[ms][ns][r];
+      }
+    }
+}
+
+// Cell kernels.  Gate k of unit j: column k*H + j of the [B][4H] rows (xg,
+// gates, dG), column k*Hp + j of the 64-padded [B][4Hp] rows (P, dG_pad).
 __global__ __launch_bounds__(kBlock) void lstm_fwd_kernel(const uint16_t* __restrict__ xg,
                                                           const uint16_t* __restrict__ hg,
+                                                          const float* __restrict__ P, int S,
                                                           const float* __restrict__ c_prev, float* __restrict__ c,
-                                                          uint16_t* __restrict__ h, float* __restrict__ gates, int B,
-                                                          int H) {
+                                                          uint16_t* __restrict__ h, uint16_t* __restrict__ h_pad,
+                                                          float* __restrict__ gates, int B, int H, int Hp) {
   const int64_t idx = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (idx >= (int64_t)B * H) return;
   const int b = (int)(idx / H), j = (int)(idx - (int64_t)b * H);
   const int64_t g0 = (int64_t)b * 4 * H + j;
+  const int64_t p0 = (int64_t)b * 4 * Hp + j;
+  const int64_t slab = (int64_t)B * 4 * Hp;
   float a[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) a[k] = bf2f(xg[g0 + k * H]) + bf2f(hg[g0 + k * H]);
+  for (int k = 0; k < 4; ++k) a[k] = bf2f(xg[g0 + k * H]);
+  if (hg)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) a[k] += bf2f(hg[g0 + k * H]);
+  for (int s = 0; s < S; ++s)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) a[k] += P[s * slab + p0 + k * Hp];
   const float i = sigm(a[0]), f = sigm(a[1]), g = tanhf(a[2]), o = sigm(a[3]);
   const float cn = fmaf(f, c_prev[idx], i * g);
   c[idx] = cn;
-  h[idx] = f2bf16(o * tanhf(cn));
+  const uint16_t hv = f2bf16(o * tanhf(cn));
+  h[idx] = hv;
+  if (h_pad) h_pad[(int64_t)b * Hp + j] = hv;
   gates[g0] = i;
   gates[g0 + H] = f;
   gates[g0 + 2 * H] = g;
@@ -59,45 +150,67 @@ __global__ __launch_bounds__(kBlock) void lstm_fwd_kernel(const uint16_t* __rest
 
 __global__ __launch_bounds__(kBlock) void lstm_bwd_kernel(const uint16_t* __restrict__ dout,
                                                           const uint16_t* __restrict__ dh_rec,
+                                                          const float* __restrict__ P, int S,
                                                           const float* __restrict__ dc_next,
                                                           const float* __restrict__ gates,
                                                           const float* __restrict__ c, const float* __restrict__ c_prev,
-                                                          uint16_t* __restrict__ dG, float* __restrict__ dc_prev, int B,
-                                                          int H) {
+                                                          uint16_t* __restrict__ dG, uint16_t* __restrict__ dG_pad,
+                                                          float* __restrict__ dc_prev, int B, int H, int Hp) {
   const int64_t idx = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (idx >= (int64_t)B * H) return;
   const int b = (int)(idx / H), j = (int)(idx - (int64_t)b * H);
   const int64_t g0 = (int64_t)b * 4 * H + j;
   const float i = gates[g0], f = gates[g0 + H], g = gates[g0 + 2 * H], o = gates[g0 + 3 * H];
-  float dh = 0.f;
-  if (dout) dh += bf2f(dout[idx]);
+  float dh = dout ? bf2f(dout[idx]) : 0.f;
   if (dh_rec) dh += bf2f(dh_rec[idx]);
+  if (P) {
+    const int64_t p0 = (int64_t)b * Hp + j, slab = (int64_t)B * Hp;
+    for (int s = 0; s < S; ++s) dh += P[s * slab + p0];
+  }
   const float tc = tanhf(c[idx]);
   const float dc = (dc_next ? dc_next[idx] : 0.f) + dh * o * (1.f - tc * tc);
-  dG[g0] = f2bf16(dc * g * i * (1.f - i));
-  dG[g0 + H] = f2bf16(dc * c_prev[idx] * f * (1.f - f));
-  dG[g0 + 2 * H] = f2bf16(dc * i * (1.f - g * g));
-  dG[g0 + 3 * H] = f2bf16(dh * tc * o * (1.f - o));
+  const uint16_t d[4] = {f2bf16(dc * g * i * (1.f - i)), f2bf16(dc * c_prev[idx] * f * (1.f - f)),
+                         f2bf16(dc * i * (1.f - g * g)), f2bf16(dh * tc * o * (1.f - o))};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) dG[g0 + k * H] = d[k];
+  if (dG_pad) {
+    const int64_t q0 = (int64_t)b * 4 * Hp + j;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dG_pad[q0 + k * Hp] = d[k];
+  }
   dc_prev[idx] = dc * f;
 }
 
 }  // namespace
 
-void lstm_cell_fwd(const uint16_t* xg, const uint16_t* hg, const float* c_prev, float* c, uint16_t* h, float* gates,
-                   int B, int H, hipStream_t stream) {
-  const int64_t n = (int64_t)B * H;
-  if (n <= 0) return;
-  hipLaunchKernelGGL(lstm_fwd_kernel, dim3((unsigned)ceil_div(n, (int64_t)kBlock)), dim3(kBlock), 0, stream, xg, hg,
-                     c_prev, c, h, gates, B, H);
+void lstm_rec_gemm(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, float* P, int M, int N, int K,
+                   int S, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || S <= 0) return;
+  dim3 grid((unsigned)(N / 64), (unsigned)S, (unsigned)ceil_div(M, 128));
+  const int ks = K / S;
+  if (ks % 256 == 0)
+    hipLaunchKernelGGL(rec_gemm_kernel<8>, grid, dim3(kBlock), 0, stream, A, lda, B, ldb, P, M, N, ks);
+  else if (ks % 128 == 0)
+    hipLaunchKernelGGL(rec_gemm_kernel<4>, grid, dim3(kBlock), 0, stream, A, lda, B, ldb, P, M, N, ks);
+  else
+    hipLaunchKernelGGL(rec_gemm_kernel<2>, grid, dim3(kBlock), 0, stream, A, lda, B, ldb, P, M, N, ks);
 }
 
-void lstm_cell_bwd(const uint16_t* dout, const uint16_t* dh_rec, const float* dc_next, const float* gates,
-                   const float* c, const float* c_prev, uint16_t* dG, float* dc_prev, int B, int H,
-                   hipStream_t stream) {
+void lstm_cell_fwd(const uint16_t* xg, const uint16_t* hg, const float* P, int S, const float* c_prev, float* c, uint16_t* h,
+                   uint16_t* h_pad, float* gates, int B, int H, int Hp, hipStream_t stream) {
+  const int64_t n = (int64_t)B * H;
+  if (n <= 0) return;
+  hipLaunchKernelGGL(lstm_fwd_kernel, dim3((unsigned)ceil_div(n, (int64_t)kBlock)), dim3(kBlock), 0, stream, xg, hg, P, S,
+                     c_prev, c, h, h_pad, gates, B, H, Hp);
+}
+
+void lstm_cell_bwd(const uint16_t* dout, const uint16_t* dh_rec, const float* P, int S, const float* dc_next, const float* gates,
+                   const float* c, const float* c_prev, uint16_t* dG, uint16_t* dG_pad, float* dc_prev, int B, int H,
+                   int Hp, hipStream_t stream) {
   const int64_t n = (int64_t)B * H;
   if (n <= 0) return;
   hipLaunchKernelGGL(lstm_bwd_kernel, dim3((unsigned)ceil_div(n, (int64_t)kBlock)), dim3(kBlock), 0, stream, dout,
-                     dh_rec, dc_next, gates, c, c_prev, dG, dc_prev, B, H);
+                     dh_rec, P, S, dc_next, gates, c, c_prev, dG, dG_pad, dc_prev, B, H, Hp);
 }
 
 }  // namespace gk

@@ -1,4 +1,4 @@
-"""bf16 LSTM layers: hipBLASLt GEMMs + one fused HIP cell kernel per step.
+"""bf16 LSTM layers: a split-K MFMA step GEMM + one fused HIP cell kernel per step.
 
 ``GkLSTM`` is a drop-in ``nn.LSTM`` (sequence-first, same parameter names
 ``weight_ih_l{k}`` / ``weight_hh_l{k}`` / ``bias_ih_l{k}`` / ``bias_hh_l{k}``,
@@ -9,21 +9,29 @@ bf16 autocast and runs each step as a poorly tiled GEMM plus two hidden-update
 kernels (profiles/r01_lstm_kernel_stats.csv).  Per layer this module runs
 
   forward : xg = x W_ih^T + (b_ih + b_hh)          one GEMM over all T steps
-            per step: hg = h W_hh^T (GEMM); lstm_cell_fwd(xg[t], hg, c) -> h, c, gates
-  backward: per step: lstm_cell_bwd(dout[t], dh_rec, dc) -> dG[t], dc;
-                      dh_rec = dG[t] W_hh (GEMM)
+            per step: P = h W_hh^T (lstm_rec_gemm, fp32 K-slice partials);
+                      lstm_cell_fwd(xg[t], P, c) -> h, c, gates
+  backward: per step: lstm_cell_bwd(dout[t], P, dc) -> dG[t], dc;
+                      P = dG[t] W_hh (lstm_rec_gemm)
             dW_ih += dG^T x, dW_hh += dG^T h_prev, db += colsum(dG), dx = dG W_ih
             -- four GEMMs over all T steps; with the bf16 shadow
             (parallel/shadow.py) the weight / bias gradients go straight into
             the optimizer's fp32 arena (fp32-output GEMM, fused column pass).
 
-in bf16 with fp32 cell state.  Off the GPU (or outside bf16 autocast) the
+in bf16 with fp32 cell state.  The step GEMM is tiny (M = batch, K = H) and
+latency-bound as one GEMM (~20-35 us for H = 1500 on hipBLASLt,
+bench/lstm_gemm_probe.py); split over S K-slices into a few hundred
+workgroups it runs a handful of MFMA steps per wave, and the cell kernel sums
+the fp32 slices on load (no atomics, no extra reduction launch).  Its
+operands are 64-padded (h_pad / dG_pad written by the cell kernels, W_hh
+padded once per forward).  Off the GPU (or outside bf16 autocast) the
 same recurrence runs in fp32 with PyTorch ops, so CPU tests compare it with
 ``nn.LSTM`` exactly.
 """
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional, Tuple
 
 import torch
@@ -64,6 +72,42 @@ def _cell_bwd_ref(dout, dh_rec, dc_next, gates, c, c_prev, dG_out, dc_prev_out):
     dc_prev_out.copy_(dc * f)
 
 
+def _pad64(n: int) -> int:
+    return (n + 63) // 64 * 64
+
+
+def _cdiv(a: int, b: int) -> int:
+    return (a + b - 1) // b
+
+
+# Largest batch per direction that runs the step GEMM split-K (else one
+# hipBLASLt GEMM with a bf16 output read by the cell kernel).  Measured on
+# MI355X (bench/lstm_gemm_probe.py, H = 1500): B = 20 -> 5 us split-K vs 19 us
+# hipBLASLt both ways; B = 128 -> forward 19.5 (+12 MB of fp32 slices for the
+# cell to read) vs 20.7 us, backward 20 vs 31 us.  Override with
+# GKSGD_LSTM_SPLITK="fwd:<maxB>,bwd:<maxB>".
+SPLITK_MAX_BATCH = {"fwd": 64, "bwd": 1 << 30}
+for _kv in os.environ.get("GKSGD_LSTM_SPLITK", "").split(","):
+    if ":" in _kv:
+        _k, _v = _kv.split(":", 1)
+        SPLITK_MAX_BATCH[_k.strip()] = int(_v)
+
+
+def _splitk(direction: str, batch: int) -> bool:
+    return batch <= SPLITK_MAX_BATCH[direction]
+
+
+def _splits(kblocks: int, nblocks: int, target: int = 512) -> int:
+    """K-slice count S for the split-K step GEMM: the largest divisor of the
+    64-deep K-block count keeping S * nblocks <= target workgroups (two per
+    CU) and every slice >= two K-blocks deep."""
+    best = 1
+    for d in range(2, kblocks + 1):
+        if kblocks % d == 0 and d * nblocks <= target and kblocks // d >= 2:
+            best = d
+    return best
+
+
 class _LSTMLayerFn(torch.autograd.Function):
     """One LSTM layer over a whole sequence (one autograd node: the step loop
     lives inside forward / backward)."""
@@ -85,15 +129,29 @@ class _LSTMLayerFn(torch.autograd.Function):
         gates = torch.empty(T, B, 4 * H, dtype=torch.float32, device=dev)
         h = h0.to(cd).contiguous()
         h0c = h
-        ops = _g() if fast else None
-        whh_t = whh.t()
-        for t in range(T):
-            hg = torch.mm(h, whh_t)
-            if fast:
-                ops.lstm_cell_fwd(xg[t], hg, c_all[t], c_all[t + 1], out[t], gates[t])
-            else:
-                _cell_fwd_ref(xg[t], hg, c_all[t], c_all[t + 1], out[t], gates[t])
-            h = out[t]
+        if fast and _splitk("fwd", B):
+            # split-K step GEMM over 64-padded operands (lstm.hip rec_gemm_kernel)
+            ops = _g()
+            Hp = _pad64(H)
+            wpf = torch.zeros(4, Hp, Hp, dtype=cd, device=dev)
+            wpf[:, :H, :H] = whh.view(4, H, H)
+            wpf = wpf.view(4 * Hp, Hp)
+            S = _splits(Hp // 64, (4 * Hp // 64) * _cdiv(B, 128))
+            P = torch.empty(S, B, 4 * Hp, dtype=torch.float32, device=dev)
+            h_pad = torch.zeros(B, Hp, dtype=cd, device=dev)
+            h_pad[:, :H] = h
+            for t in range(T):
+                ops.lstm_rec_gemm(h_pad, wpf, P, S)
+                ops.lstm_cell_fwd(xg[t], None, P, S, c_all[t], c_all[t + 1], out[t], h_pad, gates[t])
+        else:
+            whh_t = whh.t()
+            for t in range(T):
+                if fast:
+                    _g().lstm_cell_fwd(xg[t], torch.mm(h, whh_t), None, 0, c_all[t], c_all[t + 1], out[t], None,
+                                       gates[t])
+                else:
+                    _cell_fwd_ref(xg[t], torch.mm(h, whh_t), c_all[t], c_all[t + 1], out[t], gates[t])
+                h = out[t]
         ctx.save_for_backward(x2, h0c, out, c_all, gates, wih, whh)
         ctx.sinks, ctx.fast, ctx.cd = sinks, fast, cd
         ctx.dtypes = (x.dtype, h0.dtype, c0.dtype, w_ih.dtype)
@@ -106,26 +164,49 @@ class _LSTMLayerFn(torch.autograd.Function):
         T, B, H = out.shape
         cd, fast = ctx.cd, ctx.fast
         dev = out.device
-        ops = _g() if fast else None
         dG = torch.empty(T, B, 4 * H, dtype=cd, device=dev)
         if dout is not None:
             dout = dout.to(cd).contiguous()
-        dh_rec = dh_n.to(cd).contiguous() if dh_n is not None else None
         dc = dc_n.float().contiguous() if dc_n is not None else None
         bufs = [torch.empty(B, H, dtype=torch.float32, device=dev) for _ in range(2)]
-        for t in range(T - 1, -1, -1):
-            dc_prev = bufs[t & 1]
-            do_t = dout[t] if dout is not None else None
-            if fast:
-                ops.lstm_cell_bwd(do_t, dh_rec, dc, gates[t], c_all[t + 1], c_all[t], dG[t], dc_prev)
-            else:
-                _cell_bwd_ref(do_t, dh_rec, dc, gates[t], c_all[t + 1], c_all[t], dG[t], dc_prev)
-            dc = dc_prev
-            dh_rec = torch.mm(dG[t], whh)
+        need_dh0 = ctx.needs_input_grad[1]
+        if fast and _splitk("bwd", B):
+            ops = _g()
+            Hp = _pad64(H)
+            # wpb[j'][k Hp + j] = W_hh[k H + j][j']: dh = dG_pad wpb^T
+            wpb = torch.zeros(Hp, 4, Hp, dtype=cd, device=dev)
+            wpb[:H, :, :H] = whh.view(4, H, H).permute(2, 0, 1)
+            wpb = wpb.view(Hp, 4 * Hp)
+            S = _splits(4 * Hp // 64, (Hp // 64) * _cdiv(B, 128), target=256)
+            P = torch.empty(S, B, Hp, dtype=torch.float32, device=dev)
+            dG_pad = torch.zeros(B, 4 * Hp, dtype=cd, device=dev)
+            for t in range(T - 1, -1, -1):
+                dc_prev = bufs[t & 1]
+                do_t = dout[t] if dout is not None else None
+                if t == T - 1 and dh_n is not None:
+                    do_t = (dh_n.float() if do_t is None else do_t.float() + dh_n.float()).to(cd)
+                ops.lstm_cell_bwd(do_t, None, P if t < T - 1 else None, S, dc, gates[t], c_all[t + 1], c_all[t],
+                                  dG[t], dG_pad, dc_prev)
+                dc = dc_prev
+                if t > 0 or need_dh0:
+                    ops.lstm_rec_gemm(dG_pad, wpb, P, S)
+            dh_rec = P.sum(0)[:, :H] if need_dh0 else None
+        else:
+            dh_rec = dh_n.to(cd).contiguous() if dh_n is not None else None
+            for t in range(T - 1, -1, -1):
+                dc_prev = bufs[t & 1]
+                do_t = dout[t] if dout is not None else None
+                if fast:
+                    _g().lstm_cell_bwd(do_t, dh_rec, None, 0, dc, gates[t], c_all[t + 1], c_all[t], dG[t], None,
+                                       dc_prev)
+                else:
+                    _cell_bwd_ref(do_t, dh_rec, dc, gates[t], c_all[t + 1], c_all[t], dG[t], dc_prev)
+                dc = dc_prev
+                dh_rec = torch.mm(dG[t], whh)
         dG2 = dG.view(T * B, 4 * H)
         xdt, hdt, cdt, wdt = ctx.dtypes
         dx = torch.mm(dG2, wih).view(ctx.in_shape) if ctx.needs_input_grad[0] else None
-        dh0 = dh_rec if ctx.needs_input_grad[1] else None
+        dh0 = dh_rec.to(hdt) if need_dh0 else None
         dc0 = dc if ctx.needs_input_grad[2] else None
         grads: List[Optional[torch.Tensor]] = [None, None, None, None]
         wsinks = ctx.sinks

@@ -24,14 +24,23 @@ def test_lstm_cells_vs_reference(B, H):
     torch.manual_seed(B + H)
     xg = (torch.randn(B, 4 * H, device="cuda") * 2).to(torch.bfloat16)
     hg = torch.randn(B, 4 * H, device="cuda").to(torch.bfloat16)
+    Hp = (H + 63) // 64 * 64
+    # two fp32 K-slice partials whose sum is hg, laid out in 64-padded gate columns
+    P = torch.zeros(2, B, 4, Hp, device="cuda")
+    P[0, :, :, :H] = hg.float().view(B, 4, H) * 0.25
+    P[1, :, :, :H] = hg.float().view(B, 4, H) * 0.75
+    P = P.view(2, B, 4 * Hp)
+    h_pad = torch.full((B, Hp), 7.0, device="cuda", dtype=torch.bfloat16)
     cp = torch.randn(B, H, device="cuda")
     outs = [torch.empty(B, H, device="cuda"), torch.empty(B, H, device="cuda", dtype=torch.bfloat16),
             torch.empty(B, 4 * H, device="cuda")]
     refs = [torch.empty_like(o, dtype=torch.float32) for o in outs]
-    g.lstm_cell_fwd(xg, hg, cp, *outs)
+    g.lstm_cell_fwd(xg, None, P, 2, cp, outs[0], outs[1], h_pad, outs[2])
     _cell_fwd_ref(xg, hg, cp, *refs)
     for o, r in zip(outs, refs):
         assert (o.float() - r).abs().max().item() <= 1e-2 * r.abs().max().item() + 1e-5
+    assert torch.equal(h_pad[:, :H], outs[1])
+    assert (h_pad[:, H:].float() == 7.0).all()
     c, _, gates = refs
     dout = torch.randn(B, H, device="cuda").to(torch.bfloat16)
     dh = torch.randn(B, H, device="cuda").to(torch.bfloat16)
@@ -40,39 +49,82 @@ def test_lstm_cells_vs_reference(B, H):
     dcp = torch.empty(B, H, device="cuda")
     rG = torch.empty(B, 4 * H, device="cuda")
     rcp = torch.empty(B, H, device="cuda")
-    g.lstm_cell_bwd(dout, dh, dcn, gates, c, cp, dG, dcp)
+    Pb = torch.zeros(3, B, Hp, device="cuda")
+    for s in range(3):
+        Pb[s, :, :H] = dh.float() / 3
+    dG_pad = torch.zeros(B, 4 * Hp, device="cuda", dtype=torch.bfloat16)
+    g.lstm_cell_bwd(dout, None, Pb, 3, dcn, gates, c, cp, dG, dG_pad, dcp)
     _cell_bwd_ref(dout, dh, dcn, gates, c, cp, rG, rcp)
     assert (dG.float() - rG).abs().max().item() <= 1e-2 * rG.abs().max().item()
     assert (dcp - rcp).abs().max().item() <= 1e-5 * rcp.abs().max().item() + 1e-6
-    g.lstm_cell_bwd(None, None, None, gates, c, cp, dG, dcp)
+    assert torch.equal(dG_pad.view(B, 4, Hp)[:, :, :H], dG.view(B, 4, H))
+    assert (dG_pad.view(B, 4, Hp)[:, :, H:] == 0).all()
+    g.lstm_cell_bwd(None, None, None, 1, None, gates, c, cp, dG, None, dcp)
+    assert dG.float().abs().max().item() == 0.0
+    # bf16 hg / dh_rec inputs (the hipBLASLt step-GEMM path)
+    outs2 = [torch.empty_like(o) for o in outs]
+    g.lstm_cell_fwd(xg, hg, None, 0, cp, outs2[0], outs2[1], None, outs2[2])
+    for o, r in zip(outs2, refs):
+        assert (o.float() - r).abs().max().item() <= 1e-2 * r.abs().max().item() + 1e-5
+    g.lstm_cell_bwd(dout, dh, None, 0, dcn, gates, c, cp, dG, None, dcp)
+    assert (dG.float() - rG).abs().max().item() <= 1e-2 * rG.abs().max().item()
+    assert (dcp - rcp).abs().max().item() <= 1e-5 * rcp.abs().max().item() + 1e-6
+    g.lstm_cell_bwd(None, None, None, 0, None, gates, c, cp, dG, None, dcp)
     assert dG.float().abs().max().item() == 0.0
 
 
-def test_gklstm_bf16_vs_fp32_nn_lstm():
+@pytest.mark.parametrize("M,N,K,S", [(128, 6144, 1536, 4), (20, 1536, 6144, 16), (3, 256, 64, 1), (200, 128, 256, 2)])
+def test_lstm_rec_gemm_vs_fp32(M, N, K, S):
+    g = torch.ops.gksgd
+    torch.manual_seed(M + N + K)
+    A = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    Bm = torch.randn(N, K, device="cuda").to(torch.bfloat16)
+    P = torch.full((S, M, N), float("nan"), device="cuda")
+    g.lstm_rec_gemm(A, Bm, P, S)
+    ref = A.float() @ Bm.float().t()
+    got = P.sum(0)
+    assert (got - ref).abs().max().item() <= 1e-4 * ref.abs().max().item() + 1e-3
+    # every slice is its own K range
+    ks = K // S
+    ref0 = A[:, :ks].float() @ Bm[:, :ks].float().t()
+    assert (P[0] - ref0).abs().max().item() <= 1e-4 * ref0.abs().max().item() + 1e-3
+
+
+@pytest.mark.parametrize("fwd_max,bwd_max", [(1 << 30, 1 << 30), (0, 0), (0, 1 << 30)],
+                         ids=["splitk", "hipblaslt", "mixed"])
+def test_gklstm_bf16_vs_fp32_nn_lstm(monkeypatch, fwd_max, bwd_max):
+    from gaussiank_sgd_amd.ops import lstm as L_
     from gaussiank_sgd_amd.ops.lstm import GkLSTM
+    monkeypatch.setitem(L_.SPLITK_MAX_BATCH, "fwd", fwd_max)
+    monkeypatch.setitem(L_.SPLITK_MAX_BATCH, "bwd", bwd_max)
     torch.manual_seed(0)
     T, B, I, H, L = 35, 16, 256, 320, 2
     ref = torch.nn.LSTM(I, H, num_layers=L).cuda()
     m = GkLSTM(I, H, num_layers=L).cuda()
     m.load_state_dict(ref.state_dict())
     x = torch.randn(T, B, I, device="cuda")
-    xa = x.clone().requires_grad_(True)
+    h0 = torch.randn(L, B, H, device="cuda") * 0.5
+    c0 = torch.randn(L, B, H, device="cuda") * 0.5
+    xa, ha, ca = (t.clone().requires_grad_(True) for t in (x, h0, c0))
     with torch.autocast("cuda", dtype=torch.bfloat16):
-        y, (hn, cn) = m(xa)
+        y, (hn, cn) = m(xa, (ha, ca))
     assert y.dtype == torch.bfloat16
-    xr = x.clone().requires_grad_(True)
+    xr, hr, cr = (t.clone().requires_grad_(True) for t in (x, h0, c0))
     torch.backends.cudnn.enabled = False     # fp32 native LSTM as the reference
     try:
-        yr, (hnr, cnr) = ref(xr)
+        yr, (hnr, cnr) = ref(xr, (hr, cr))
     finally:
         torch.backends.cudnn.enabled = True
     gy = torch.randn_like(yr)
-    (y.float() * gy).sum().backward()
-    (yr * gy).sum().backward()
+    ghn = torch.randn_like(hnr)
+    (y.float() * gy).sum().add_((hn.float() * ghn).sum()).backward()
+    (yr * gy).sum().add_((hnr * ghn).sum()).backward()
     tol = lambda r: 3e-2 * r.abs().max().item() + 1e-3  # noqa: E731
     assert (y.float() - yr).abs().max().item() <= tol(yr)
     assert (cn.float() - cnr).abs().max().item() <= tol(cnr)
     assert (xa.grad - xr.grad).abs().max().item() <= tol(xr.grad)
+    assert (ha.grad - hr.grad).abs().max().item() <= tol(hr.grad)
+    assert (ca.grad - cr.grad).abs().max().item() <= tol(cr.grad)
     for (n, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
         assert (p.grad - q.grad).abs().max().item() <= tol(q.grad), n
 
