@@ -12,6 +12,8 @@ import re
 def category(n: str) -> str:
     if "gk::" in n and ("add_ln" in n or "ln_param" in n):
         return "gk fused add+LayerNorm"
+    if "gk::" in n and ("rec_gemm" in n or "lstm_" in n):
+        return "gk LSTM (split-K step GEMM + fused cells)"
     if "gk::" in n and ("gemm_nt" in n or "gemm_tn" in n):
         return "gk HIP conv GEMMs (1x1 / implicit-GEMM 3x3, MFMA)"
     if "gk::" in n:
