@@ -19,13 +19,86 @@ from __future__ import annotations
 
 import datetime
 import os
-from typing import Any, Dict, List, Optional
+import threading
+from typing import Any, Callable, Dict, List, Optional
 
 import torch
 import torch.distributed as dist
 
 _state: Dict[str, Any] = {"initialized": False, "rank": 0, "size": 1, "local_rank": 0, "local_size": 1,
                           "backend": None, "owns_pg": False}
+# per-thread world state of a loopback (in-process fake) world; see loopback_world()
+_tls = threading.local()
+
+
+def _S() -> Dict[str, Any]:
+    st = getattr(_tls, "state", None)
+    return st if st is not None else _state
+
+
+class _LoopbackWorld:
+    """P virtual ranks = P threads of one process.  Every collective is an
+    exchange: each rank deposits its payload, all meet at a barrier, every
+    rank reads all P payloads in rank order (so reductions are deterministic
+    and identical on every rank), and a second barrier frees the slots."""
+
+    def __init__(self, P: int, timeout_s: float):
+        self.P = P
+        self.slots: List[Any] = [None] * P
+        self.barrier = threading.Barrier(P, timeout=timeout_s)
+
+    def exchange(self, rank: int, payload: Any) -> List[Any]:
+        self.slots[rank] = payload
+        self.barrier.wait()
+        got = list(self.slots)
+        self.barrier.wait()
+        return got
+
+
+def loopback_world(P: int, fn: Callable[[int], Any], timeout_s: float = 120.0) -> List[Any]:
+    """Run ``fn(rank)`` on P virtual ranks (threads) whose comm calls --
+    ``size/rank``, all-reduce, all-gather, broadcast, barrier, the hot-path
+    ``Exchanger`` -- go through an in-process loopback world with the real
+    collective semantics.  Unit-tests the whole hook -> bucket -> compress ->
+    exchange -> decompress -> step path of ``DistributedOptimizer`` for any P
+    without processes.  Returns fn's results in rank
+    order; an exception on any rank breaks the barrier for the others and is
+    re-raised here."""
+    world = _LoopbackWorld(P, timeout_s)
+    results: List[Any] = [None] * P
+    errors: List[Optional[BaseException]] = [None] * P
+
+    def run(r: int) -> None:
+        _tls.state = {"initialized": True, "rank": r, "size": P, "local_rank": r, "local_size": P,
+                      "backend": "loopback", "owns_pg": False, "world": world}
+        try:
+            results[r] = fn(r)
+        except BaseException as e:  # noqa: BLE001 - re-raised on the caller's thread
+            errors[r] = e
+            world.barrier.abort()
+        finally:
+            _tls.state = None
+
+    threads = [threading.Thread(target=run, args=(r,), name="loopback-rank%d" % r) for r in range(P)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    first = next((e for e in errors if e is not None and not isinstance(e, threading.BrokenBarrierError)), None)
+    if first is None:
+        first = next((e for e in errors if e is not None), None)
+    if first is not None:
+        raise first
+    return results
+
+
+def _loopback() -> Optional[_LoopbackWorld]:
+    st = getattr(_tls, "state", None)
+    return st["world"] if st is not None else None
+
+
+def _lb_exchange(payload: Any) -> List[Any]:
+    return _loopback().exchange(rank(), payload)
 
 
 def _env_int(*names: str, default: int) -> int:
@@ -38,7 +111,7 @@ def _env_int(*names: str, default: int) -> int:
 
 def init(backend: Optional[str] = None, timeout_s: Optional[float] = None, device: Optional[str] = None) -> None:
     """Initialise the world (idempotent).  Equivalent of ``hvd.init()``."""
-    if _state["initialized"]:
+    if _S()["initialized"]:  # (always true on a loopback rank)
         return
     rank = _env_int("RANK", "OMPI_COMM_WORLD_RANK", "PMI_RANK", default=0)
     size = _env_int("WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE", default=1)
@@ -46,7 +119,7 @@ def init(backend: Optional[str] = None, timeout_s: Optional[float] = None, devic
     local_size = _env_int("LOCAL_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_SIZE", default=size)
     if dist.is_available() and dist.is_initialized():
         rank, size = dist.get_rank(), dist.get_world_size()
-        _state["backend"] = dist.get_backend()
+        _S()["backend"] = dist.get_backend()
     elif size > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
@@ -63,43 +136,45 @@ def init(backend: Optional[str] = None, timeout_s: Optional[float] = None, devic
         if backend == "nccl":
             kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
         dist.init_process_group(backend=backend, **kw)
-        _state["backend"] = backend
-        _state["owns_pg"] = True
-    _state.update(initialized=True, rank=rank, size=size, local_rank=local_rank, local_size=local_size)
+        _S()["backend"] = backend
+        _S()["owns_pg"] = True
+    _S().update(initialized=True, rank=rank, size=size, local_rank=local_rank, local_size=local_size)
 
 
 def shutdown() -> None:
-    if _state["owns_pg"] and dist.is_initialized():
+    if _loopback() is not None:
+        return
+    if _S()["owns_pg"] and dist.is_initialized():
         dist.destroy_process_group()
-    _state.update(initialized=False, rank=0, size=1, local_rank=0, local_size=1, backend=None, owns_pg=False)
+    _S().update(initialized=False, rank=0, size=1, local_rank=0, local_size=1, backend=None, owns_pg=False)
 
 
 def is_initialized() -> bool:
-    return _state["initialized"]
+    return _S()["initialized"]
 
 
 def size() -> int:
-    return _state["size"]
+    return _S()["size"]
 
 
 def rank() -> int:
-    return _state["rank"]
+    return _S()["rank"]
 
 
 def local_rank() -> int:
-    return _state["local_rank"]
+    return _S()["local_rank"]
 
 
 def local_size() -> int:
-    return _state["local_size"]
+    return _S()["local_size"]
 
 
 def backend() -> Optional[str]:
-    return _state["backend"]
+    return _S()["backend"]
 
 
 def _distributed() -> bool:
-    return _state["size"] > 1 and dist.is_initialized()
+    return _S()["size"] > 1 and dist.is_initialized() and _loopback() is None
 
 
 class Handle:
@@ -124,7 +199,9 @@ def synchronize(handle: Handle) -> torch.Tensor:
 
 
 def barrier() -> None:
-    if _distributed():
+    if _loopback() is not None:
+        _loopback().barrier.wait()
+    elif _distributed():
         if backend() == "nccl":
             dist.barrier(device_ids=[torch.cuda.current_device()])
         else:
@@ -135,6 +212,13 @@ def barrier() -> None:
 # collectives
 # ----------------------------------------------------------------------------
 def allreduce_async_(tensor: torch.Tensor, average: bool = True, name: Optional[str] = None) -> Handle:
+    if _loopback() is not None:
+        parts = _lb_exchange(tensor.detach().clone())
+        acc = parts[0].clone()
+        for p in parts[1:]:
+            acc.add_(p)
+        tensor.copy_(acc.div_(len(parts)) if average else acc)
+        return Handle(None, tensor)
     if not _distributed():
         return Handle(None, tensor)
     if average and backend() == "nccl":
@@ -157,6 +241,10 @@ def allreduce(tensor: torch.Tensor, average: bool = True, name: Optional[str] = 
 
 def allgather_into_(out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
     """Fixed-size all-gather: out = concat over ranks of inp (out numel = P * inp numel)."""
+    if _loopback() is not None:
+        parts = _lb_exchange(inp.detach().reshape(-1).clone())
+        out.view(-1).copy_(torch.cat(parts))
+        return None
     if not _distributed():
         out.view(-1)[: inp.numel()].copy_(inp.view(-1))
         return None
@@ -168,6 +256,8 @@ def allgather_into_(out: torch.Tensor, inp: torch.Tensor, async_op: bool = False
 
 def allgather_async(tensor: torch.Tensor, name: Optional[str] = None) -> Handle:
     """Horovod semantics: first dimension may differ per rank; result is the concat."""
+    if _loopback() is not None:
+        return Handle(None, torch.cat(_lb_exchange(tensor.detach().clone()), 0))
     if not _distributed():
         return Handle(None, tensor.clone())
     t = tensor.contiguous()
@@ -195,6 +285,11 @@ def allgather(tensor: torch.Tensor, name: Optional[str] = None) -> torch.Tensor:
 
 
 def broadcast_async_(tensor: torch.Tensor, root_rank: int, name: Optional[str] = None) -> Handle:
+    if _loopback() is not None:
+        src = _lb_exchange(tensor.detach().clone() if rank() == root_rank else None)[root_rank]
+        if rank() != root_rank:
+            tensor.copy_(src)
+        return Handle(None, tensor)
     if not _distributed():
         return Handle(None, tensor)
     work = dist.broadcast(tensor, src=root_rank, async_op=True)
@@ -211,6 +306,9 @@ def broadcast(tensor: torch.Tensor, root_rank: int, name: Optional[str] = None) 
 
 def broadcast_object(obj: Any, root: int = 0) -> Any:
     """Replacement for mpi4py ``COMM_WORLD.bcast`` (dist_trainer.py:40)."""
+    if _loopback() is not None:
+        import copy
+        return copy.deepcopy(_lb_exchange(obj if rank() == root else None)[root])
     if not _distributed():
         return obj
     lst = [obj]
@@ -239,7 +337,7 @@ def broadcast_parameters(params, root_rank: int = 0) -> None:
         items = params
     else:
         raise ValueError("invalid params of type: %s" % type(params))
-    if not _distributed():
+    if not _distributed() and _loopback() is None:
         return
     seen = set()
     handles: List[Handle] = []
@@ -269,7 +367,7 @@ def broadcast_parameters(params, root_rank: int = 0) -> None:
 
 def broadcast_optimizer_state(optimizer: torch.optim.Optimizer, root_rank: int = 0) -> None:
     """Broadcast optimizer hyper-parameters and state from root (distributed_optimizer.py:620-736)."""
-    if not _distributed():
+    if not _distributed() and _loopback() is None:
         return
     sd = optimizer.state_dict()
     scalars = {"param_groups": [{k: v for k, v in g.items() if k != "params"} for g in sd["param_groups"]]}
@@ -341,7 +439,8 @@ class Exchanger:
     """Stream-ordered fixed-size collectives used by the hot path.
 
     backend 'rccl-native' -> RcclCommunicator, 'torch' -> torch.distributed,
-    'local' -> world of one (copies).  All calls are issued on the current
+    'loopback' -> in-process virtual ranks (loopback_world), 'local' -> world
+    of one (copies).  All calls are issued on the current
     stream and return without blocking the host.
     """
 
@@ -350,7 +449,9 @@ class Exchanger:
         self.P = size()
         self.native: Optional[RcclCommunicator] = None
         self.kind = "local"
-        if self.P > 1:
+        if self.P > 1 and _loopback() is not None:
+            self.kind = "loopback"          # module collectives take the loopback branch
+        elif self.P > 1:
             self.kind = "torch"
             if prefer_native and self.device.type == "cuda" and os.environ.get("GKSGD_NATIVE_RCCL", "1") == "1":
                 ok = 1
