@@ -17,6 +17,7 @@ process group at all.
 """
 from __future__ import annotations
 
+import contextlib
 import datetime
 import os
 import threading
@@ -98,7 +99,18 @@ def _loopback() -> Optional[_LoopbackWorld]:
 
 
 def _lb_exchange(payload: Any) -> List[Any]:
+    # GPU payloads: the producing stream finishes before another rank (thread,
+    # own current / comm stream) may read the tensor
+    if torch.is_tensor(payload) and payload.is_cuda:
+        torch.cuda.current_stream(payload.device).synchronize()
     return _loopback().exchange(rank(), payload)
+
+
+def _lb_settle(t: torch.Tensor) -> None:
+    # the other ranks' payloads were allocated on THEIR streams: finish reading
+    # them before they are released to (and reused by) those streams
+    if t.is_cuda:
+        torch.cuda.current_stream(t.device).synchronize()
 
 
 def _env_int(*names: str, default: int) -> int:
@@ -218,6 +230,7 @@ def allreduce_async_(tensor: torch.Tensor, average: bool = True, name: Optional[
         for p in parts[1:]:
             acc.add_(p)
         tensor.copy_(acc.div_(len(parts)) if average else acc)
+        _lb_settle(tensor)
         return Handle(None, tensor)
     if not _distributed():
         return Handle(None, tensor)
@@ -244,6 +257,7 @@ def allgather_into_(out: torch.Tensor, inp: torch.Tensor, async_op: bool = False
     if _loopback() is not None:
         parts = _lb_exchange(inp.detach().reshape(-1).clone())
         out.view(-1).copy_(torch.cat(parts))
+        _lb_settle(out)
         return None
     if not _distributed():
         out.view(-1)[: inp.numel()].copy_(inp.view(-1))
@@ -257,7 +271,9 @@ def allgather_into_(out: torch.Tensor, inp: torch.Tensor, async_op: bool = False
 def allgather_async(tensor: torch.Tensor, name: Optional[str] = None) -> Handle:
     """Horovod semantics: first dimension may differ per rank; result is the concat."""
     if _loopback() is not None:
-        return Handle(None, torch.cat(_lb_exchange(tensor.detach().clone()), 0))
+        res = torch.cat(_lb_exchange(tensor.detach().clone()), 0)
+        _lb_settle(res)
+        return Handle(None, res)
     if not _distributed():
         return Handle(None, tensor.clone())
     t = tensor.contiguous()
@@ -289,6 +305,7 @@ def broadcast_async_(tensor: torch.Tensor, root_rank: int, name: Optional[str] =
         src = _lb_exchange(tensor.detach().clone() if rank() == root_rank else None)[root_rank]
         if rank() != root_rank:
             tensor.copy_(src)
+            _lb_settle(tensor)
         return Handle(None, tensor)
     if not _distributed():
         return Handle(None, tensor)
@@ -449,6 +466,7 @@ class Exchanger:
         self.P = size()
         self.native: Optional[RcclCommunicator] = None
         self.kind = "local"
+        self._lb_state = getattr(_tls, "state", None)
         if self.P > 1 and _loopback() is not None:
             self.kind = "loopback"          # module collectives take the loopback branch
         elif self.P > 1:
@@ -471,6 +489,17 @@ class Exchanger:
                     self.native.destroy()
                     self.native = None
 
+    @contextlib.contextmanager
+    def _bound(self):
+        # a loopback rank's collectives may be issued from another thread
+        prev = getattr(_tls, "state", None)
+        if self.kind == "loopback":
+            _tls.state = self._lb_state
+        try:
+            yield
+        finally:
+            _tls.state = prev
+
     def allgather_(self, out: torch.Tensor, inp: torch.Tensor) -> None:
         if self.kind == "local":
             if out.data_ptr() != inp.data_ptr():
@@ -478,7 +507,8 @@ class Exchanger:
         elif self.native is not None:
             self.native.allgather_(out, inp)
         else:
-            allgather_into_(out, inp, async_op=False)
+            with self._bound():
+                allgather_into_(out, inp, async_op=False)
 
     def allreduce_(self, t: torch.Tensor, average: bool = True) -> None:
         if self.kind == "local":
@@ -486,7 +516,8 @@ class Exchanger:
         if self.native is not None:
             self.native.allreduce_(t, average)
         else:
-            allreduce_(t, average)
+            with self._bound():
+                allreduce_(t, average)
 
     def broadcast_(self, t: torch.Tensor, root: int = 0) -> None:
         if self.kind == "local":
@@ -494,7 +525,8 @@ class Exchanger:
         if self.native is not None:
             self.native.broadcast_(t, root)
         else:
-            broadcast_(t, root)
+            with self._bound():
+                broadcast_(t, root)
 
     def close(self) -> None:
         """Release the native communicator (after the device is idle)."""

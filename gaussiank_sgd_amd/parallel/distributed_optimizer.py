@@ -95,6 +95,10 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         self._fused_optim = bool(opts.get("fused_optimizer", _env_flag("GKSGD_FUSED_OPTIM", True)))
         self._zero_grad_in_step = bool(opts.get("zero_grad_in_step", True))
         self._overlap = bool(opts.get("overlap", _env_flag("GKSGD_OVERLAP", True)))
+        if comm.backend() == "loopback":
+            # autograd runs GPU backward (and so the grad hooks) on one shared
+            # device thread, not on the virtual rank's thread: exchange in step()
+            self._overlap = False
         self._prefer_native_rccl = bool(opts.get("native_rccl", True))
         self._planner_preset = opts.get("planner_preset", "mi355x")
         # DGC momentum correction (Lin et al. 2018): momentum is accumulated
@@ -408,8 +412,13 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         else:
             gathered = rec
         t2 = self._timer()
+        # Rank-ordered (deterministic) scatter for P > 2: with three or more
+        # contributions to one index, fp32 atomics sum in a run-dependent order,
+        # and the model replicas would drift apart by rounding (the reference's
+        # Python loop adds ranks in order, distributed_optimizer.py:468-482).
+        # With P <= 2 the atomic sum 0 + a + b is order-independent.
         ops.scatter_add_records_(g, gathered, max(self._world, 1), k_cap, 1.0 / max(self._world, 1),
-                                 self._deterministic)
+                                 self._deterministic or self._world > 2)
         self._log_selected(b.bufs.record[1:2])
         if settings.LOGGING_GRADIENTS and self._rank == 0 and self._gradient_path and \
                 self.train_iter % max(1, settings.DUMP_GRAD_EVERY) == 0:
