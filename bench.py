@@ -16,6 +16,12 @@ random init.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch-size B]
        [--compressor gaussian] [--density 0.001] [--model resnet50]
+
+N > 1: after the timed loop every rank digests its fp32 weight arena (fp64
+sum + 64-bit content hash, one HIP reduction) and the digests are all-gathered:
+``replicas_consistent`` in the JSON line says whether all replicas are still
+bit-identical.  ``GKSGD_DIST_BACKEND=gloo`` (with ``--no-native-rccl``) runs
+the multi-rank path with several ranks on one GPU (tests/test_bench_gpu.py).
 """
 from __future__ import annotations
 
@@ -77,6 +83,55 @@ def parse():
     return ap.parse_args()
 
 
+def probe_collectives(ex, P: int, dev, rec_bytes: int, dense_bytes: int, iters: int = 10):
+    """Short alpha-beta probe of this node's fabric through the bench's own
+    exchanger (after the timed loop): the packed-record all-gather at several
+    per-rank sizes around the real record, and the dense all-reduce the
+    sparse exchange replaces (up to the full fp32 gradient).  Times are the MAX
+    over ranks; fits t = alpha + beta * bytes_per_rank (utils/perf_model.py)."""
+    from gaussiank_sgd_amd.parallel import comm
+    from gaussiank_sgd_amd.utils import perf_model
+
+    def timed(fn):
+        for _ in range(3):
+            fn()
+        comm.barrier()
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(iters):
+            fn()
+        b.record()
+        torch.cuda.synchronize()
+        t = torch.tensor([a.elapsed_time(b) / iters * 1e-3], dtype=torch.float64, device="cuda")
+        if comm.backend() == "nccl":
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        return float(t)
+
+    out = {}
+    pts = []
+    for nb in sorted({4096, 65536, rec_bytes, 4 * rec_bytes, 1 << 22}):
+        words = max(nb // 4, 1)
+        inp = torch.zeros(words, dtype=torch.int32, device=dev)
+        o = torch.zeros(P * words, dtype=torch.int32, device=dev)
+        pts.append((words * 4, timed(lambda: ex.allgather_(o, inp))))
+    a, b = perf_model.fit_alpha_beta([x for x, _ in pts], [t for _, t in pts])
+    out["allgather"] = {"alpha_us": round(a * 1e6, 2), "beta_GBps": round(1e-9 / b, 1) if b > 0 else None,
+                        "points_bytes_us": [[x, round(t * 1e6, 1)] for x, t in pts],
+                        "record_us": round(dict(pts)[(rec_bytes // 4) * 4] * 1e6, 1) if rec_bytes else None}
+    pts = []
+    for nb in sorted({1 << 16, 1 << 20, 1 << 24, dense_bytes}):
+        t = torch.zeros(max(nb // 4, 1), dtype=torch.float32, device=dev)
+        pts.append((t.numel() * 4, timed(lambda t=t: ex.allreduce_(t, average=True))))
+        del t
+    a2, b2 = perf_model.fit_alpha_beta([x for x, _ in pts], [t for _, t in pts])
+    out["allreduce"] = {"alpha_us": round(a2 * 1e6, 2), "beta_GBps": round(1e-9 / b2, 1) if b2 > 0 else None,
+                        "points_bytes_us": [[x, round(t * 1e6, 1)] for x, t in pts],
+                        "dense_grad_us": round(pts[-1][1] * 1e6, 1)}
+    out["_fit"] = {"allgather": (a, b), "allreduce": (a2, b2)}
+    return out
+
+
 def main() -> int:
     args = parse()
     from gaussiank_sgd_amd import ops
@@ -98,8 +153,9 @@ def main() -> int:
     if not torch.cuda.is_available():
         print("bench.py needs a GPU", file=sys.stderr)
         return 2
-    torch.cuda.set_device(local_rank)
-    comm.init()
+    # several ranks may share a device (gloo rehearsal of the multi-rank path on one GPU)
+    torch.cuda.set_device(local_rank % torch.cuda.device_count())
+    comm.init(backend=os.environ.get("GKSGD_DIST_BACKEND") or None)
     P = comm.size()
     rank = comm.rank()
     if not ops.load():
@@ -168,10 +224,46 @@ def main() -> int:
     loss = trainer.current_loss()
     counts = opt._collect_selected()
     sel = (sum(counts) / max(1, args.steps)) if counts else 0.0
-    if is_sparse and sel > 0:
-        ratio = (nparams * 4.0) / (sel * 8.0)
-    else:
-        ratio = 1.0
+    # What goes on the wire per rank and step: one fixed-size record per
+    # bucket, (4 header + k_cap indices + k_cap values) int32 words.
+    comp = compressors[comp_name]
+    k_total, wire_bytes = 0, 0
+    for b in opt.arena.buckets:
+        if is_sparse:
+            kb = comp.k_of(b.numel, args.density)
+            k_total += kb
+            wire_bytes += (ops.REC_HDR + 2 * comp.k_cap_for(kb, b.numel)) * 4
+        else:
+            wire_bytes += b.numel * 4
+    ratio = (nparams * 4.0) / wire_bytes if wire_bytes else 1.0
+    replicas = None
+    if P > 1:
+        # bit-identical replicas: all-gather a digest of every rank's weight arena
+        torch.cuda.synchronize()
+        d = ops.arena_digest(opt.arena.weights)
+        mine = torch.tensor([x - (1 << 64) if x >= (1 << 63) else x for x in d], dtype=torch.int64,
+                            device="cuda" if comm.backend() == "nccl" else "cpu")
+        allv = [torch.zeros_like(mine) for _ in range(P)]
+        torch.distributed.all_gather(allv, mine)
+        replicas = all(torch.equal(allv[0], v) for v in allv[1:])
+    collectives = None
+    if P > 1 and opt._exchanger is not None and os.environ.get("GKSGD_BENCH_PROBE", "1") == "1":
+        timed_loop = opt._exchanger.stats()     # event-timed collectives of the timed loop (native engine)
+        collectives = probe_collectives(opt._exchanger, P, torch.device("cuda", torch.cuda.current_device()),
+                                        wire_bytes // max(1, len(opt.arena.buckets)) if is_sparse else 4096,
+                                        nparams * 4)
+        fit = collectives.pop("_fit")
+        if timed_loop:
+            collectives["timed_loop"] = timed_loop
+        out_path = os.environ.get("GKSGD_PERF_MODEL_OUT")
+        if out_path and rank == 0:
+            from gaussiank_sgd_amd.utils import perf_model
+            for op in ("allgather", "allreduce"):
+                perf_model.update(out_path, op, {
+                    "alpha_s": fit[op][0], "beta_s_per_byte": fit[op][1], "measured": True,
+                    "source": "bench.py probe, %d x %s, exchanger %s, points %s" % (
+                        P, torch.cuda.get_device_name(), opt._exchanger.kind, collectives[op]["points_bytes_us"])},
+                    key=str(P))
     ms = elapsed / args.steps * 1e3
     imgs = P * args.batch_size * tok_per_sample * args.steps / elapsed
     metric = METRIC if args.model == "resnet50" else "%s (whole node) %s k=%g%% on MI355X" % (
@@ -204,8 +296,15 @@ def main() -> int:
             "hip_graph": bool(args.graph),
         },
         "graph_captures": getattr(step, "captures", None),
+        "world": P,
+        "exchange": opt._exchanger.kind if opt._exchanger is not None else "none",
+        "replicas_consistent": replicas,
+        "collectives": collectives,
         "effective_compression_ratio": round(ratio, 1),
+        "wire_bytes_per_rank_step": wire_bytes,
         "selected_per_step": round(sel, 1),
+        "k_per_step": k_total if is_sparse else None,
+        "selected_over_k": round(sel / k_total, 4) if is_sparse and k_total else None,
         "params": nparams,
         "final_loss": round(loss, 4) if loss == loss else None,
     }
@@ -227,6 +326,9 @@ def main() -> int:
     if opt._exchanger is not None:
         opt._exchanger.close()
     comm.shutdown()
+    if replicas is False:
+        print("bench.py: replicas diverged", file=sys.stderr)
+        return 3
     return 0
 
 

@@ -18,7 +18,17 @@ Deliberate deviations:
     101st element of argsort(|x|) -- available as ``topk_legacy``.
   * ``none`` returns a 3-tuple (the reference's 2-tuple crashes its own caller).
   * variable-count selectors send at most ``k_cap`` entries per bucket; the
-    rest stays in the residual (no gradient mass is dropped).
+    rest stays in the residual (no gradient mass is dropped).  Gaussian-k and
+    DGC select at most ~4k/3 by construction, so their record holds
+    ``ceil(4k/3)`` entries; RedSync (k < nnz < 2k) 2k.
+  * ``gaussian_cal`` (new, opt-in): calibrated Gaussian-k -- the one-pass
+    count evaluates 16 thresholds around a per-bucket adaptive centre and
+    picks the count closest to k inside [2k/3, 4k/3], falling back to the
+    exact radix key when none qualifies.  ``gaussian`` stays bit-faithful to
+    the reference's <=3-loop tree (compression.py:372-381).
+  * random-k seeds are a pure function of (iteration, bucket, rank) -- the
+    reference's class-level counter (compression.py:439-553) would be shared
+    by every virtual rank of an in-process world.
 """
 from __future__ import annotations
 
@@ -38,7 +48,7 @@ class _SparseCompressor:
     ec = True
     loops = 3
     exact_k = False          # record capacity k (True) or ceil(kcap_factor * k)
-    kcap_factor = 2.0
+    kcap_factor = 4.0 / 3.0
     dense = False
     fused = True             # drives the fused HIP pipeline
     same_seed = False        # random-k: identical indices on every rank
@@ -68,10 +78,20 @@ class _SparseCompressor:
 
     @classmethod
     def next_seed(cls, rank: int = 0) -> int:
+        """Seed for the per-tensor class API (reference-style call counter)."""
         cls.counter += 1
-        if cls.same_seed:
-            return cls.counter & 0xFFFFFFFF
-        return (cls.counter * 1000003 + rank * 7919 + 17) & 0xFFFFFFFF
+        return cls.seed_for(cls.counter, 0, rank)
+
+    @classmethod
+    def seed_for(cls, step: int, bucket: int, rank: int = 0) -> int:
+        """Stateless seed: identical on every rank for the *same* variants."""
+        h = (int(step) * 1000003 + int(bucket) * 2654435761 + 17) & 0xFFFFFFFF
+        if not cls.same_seed:
+            h = (h + int(rank) * 7919 * 40503) & 0xFFFFFFFF
+        h ^= h >> 16
+        h = (h * 0x7FEB352D) & 0xFFFFFFFF
+        h ^= h >> 15
+        return h
 
     @classmethod
     def get_residuals(cls, name, like_tensor):
@@ -80,7 +100,7 @@ class _SparseCompressor:
         return cls.residuals[name]
 
     @classmethod
-    def compress(cls, tensor: torch.Tensor, name=None, sigma_scale=3, ratio=0.05):
+    def compress(cls, tensor: torch.Tensor, name=None, sigma_scale=3, ratio=0.05, seed=None):
         with torch.no_grad():
             flat = tensor.data.view(-1)
             numel = flat.numel()
@@ -93,7 +113,7 @@ class _SparseCompressor:
             if bufs is None or bufs.k_cap != k_cap or bufs.device != flat.device:
                 bufs = ops.CompressBuffers(k_cap, flat.device)
                 cls._bufs[name] = bufs
-            seed = cls.next_seed()
+            seed = cls.next_seed() if seed is None else int(seed)
             ops.compress_(flat, res, bufs, cls.mode, ec=False, zero_g=False, loops=cls.loops,
                           z=cls.z_for(ratio), k=k, k_cap=k_cap, seed=seed, sample_p=cls.sample_p)
             sent = int(bufs.record[0])
@@ -112,6 +132,16 @@ class GaussianCompressor(_SparseCompressor):
     mode = ops.MODE_GAUSSIAN
     ec = True
     loops = 3
+
+
+class GaussianCalCompressor(GaussianCompressor):
+    """Calibrated Gaussian-k (new): 16-candidate adaptive ladder, exact fallback."""
+    name = "gaussian_cal"
+    mode = ops.MODE_GAUSSIAN_CAL
+
+    @classmethod
+    def z_for(cls, ratio: float) -> float:
+        return gaussian_z(ratio)
 
 
 class GaussianCompressor2(GaussianCompressor):
@@ -188,6 +218,7 @@ class RedSyncCompressor(_SparseCompressor):
     name = "redsync"
     mode = ops.MODE_REDSYNC
     ec = True
+    kcap_factor = 2.0          # stops once k < nnz < 2k (compression.py:653-672)
 
 
 class RedSyncTrimCompressor(_SparseCompressor):
@@ -270,6 +301,7 @@ compressors = {
     "bucket": BucketCompressor,
     "gaussian": GaussianCompressor,
     "gaussian2": GaussianCompressor2,
+    "gaussian_cal": GaussianCalCompressor,
     "randomk": RandomKCompressor,
     "randomkec": RandomKECCompressor,
     "randomksame": RandomKSameCompressor,

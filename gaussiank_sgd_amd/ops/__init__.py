@@ -33,6 +33,9 @@ MODE_TOPK = 3
 MODE_RANDOMK = 4
 MODE_THRESHOLD = 5
 MODE_DGC = 6
+MODE_GAUSSIAN_CAL = 7
+
+CAL_FALLBACK = 16   # record header `chosen` when the calibrated mode used the exact radix key
 
 MAX_CAND = 16
 CHUNK_ELEMS = 16384
@@ -98,6 +101,8 @@ class CompressBuffers:
         self.ws = torch.zeros((ws_b + 255) // 256 * 64, dtype=torch.float32, device=device)
         self.record = torch.zeros(REC_HDR + 2 * self.k_cap, dtype=torch.int32, device=device)
         self.stats = torch.zeros(4, dtype=torch.float32, device=device)
+        # calibrated Gaussian-k state of the CPU mirror (on GPU it lives in ctrl)
+        self.cal = {"c": 0.0, "step": 0.0, "k": 0}
 
     def header(self) -> torch.Tensor:
         return self.record[:REC_HDR]
@@ -129,6 +134,31 @@ def hash_u32(idx: torch.Tensor, seed: int) -> torch.Tensor:
     h = (h * 0xC2B2AE35) & _M32
     h = h ^ (h >> 16)
     return h
+
+
+def hash_key(idx: torch.Tensor, seed: int, valid: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Random-k key of gk::key_of<kKeyHash>: hash in [1, 2^32-2], 0 for invalid (padding) slots."""
+    keys = hash_u32(idx, seed)
+    keys = torch.where(keys == 0xFFFFFFFF, torch.full_like(keys, 0xFFFFFFFE), keys)
+    keys = torch.where(keys == 0, torch.ones_like(keys), keys)
+    if valid is not None:
+        i = idx.to(torch.int64)
+        words = valid.to(torch.int64) & 0xFFFFFFFF
+        bit = (words[i >> 5] >> (i & 31)) & 1
+        keys = torch.where(bit == 1, keys, torch.zeros_like(keys))
+    return keys
+
+
+def valid_bitmask(layout: Sequence[Tuple[int, int]], n: int, device) -> torch.Tensor:
+    """int32 bitmask over n slots with bit i set for the real elements:
+    ``layout`` = (offset, numel) per tensor (the rest is arena padding)."""
+    bits = torch.zeros(((n + 31) // 32) * 32, dtype=torch.bool)
+    for off, ln in layout:
+        bits[off:off + ln] = True
+    w = bits.view(-1, 32).to(torch.int64)
+    words = (w << torch.arange(32, dtype=torch.int64)).sum(1)
+    words = torch.where(words >= 2 ** 31, words - 2 ** 32, words)
+    return words.to(torch.int32).to(device)
 
 
 def abs_key(x: torch.Tensor) -> torch.Tensor:
@@ -250,10 +280,54 @@ def _radix_topk_mask(keys: torch.Tensor, eligible: torch.Tensor, k: int) -> Tupl
     return mask, K, quota
 
 
+def _cal_decide(bufs: CompressBuffers, k: int, thr: List[float], counts: Sequence[int], std: float) -> Tuple[int, bool]:
+    """Mirror of decide_kernel's calibrated branch: (chosen, fallback); updates bufs.cal."""
+    import math
+    kd = float(k)
+    best, closest, bestd, closed = -1, 0, 1e300, 1e300
+    for j, c in enumerate(counts):
+        d = abs(math.log((c if c > 0 else 0.5) / kd))
+        if d < closed:
+            closed, closest = d, j
+        if 2.0 * kd / 3.0 <= c <= 4.0 * kd / 3.0 and d < bestd:
+            bestd, best = d, j
+    jc = best if best >= 0 else closest
+    nc = len(counts)
+    step = bufs.cal["step"]
+    if best < 0 and (jc == 0 or jc == nc - 1):
+        step *= 2.0
+    elif 0 < jc < nc - 1 and counts[jc + 1] > 0:
+        R = counts[jc - 1] / counts[jc + 1]
+        if R > 1.0001:
+            step *= min(max(math.log(1.7) / math.log(R), 0.5), 2.0)
+        else:
+            step *= 2.0
+    bufs.cal["step"] = min(max(step, 0.002), 1.0)
+    if std > 0.0 and thr[jc] > 0.0:
+        bufs.cal["c"] = thr[jc] / std
+    return jc, best < 0
+
+
+def _cal_ladder(bufs: CompressBuffers, k: int, z: float, mean: float, std: float) -> List[float]:
+    import math
+    st = bufs.cal
+    if st["k"] != k or not st["c"] > 0.0 or not st["step"] > 0.0:
+        t0 = mean + z * std
+        st["c"] = t0 / std if std > 0.0 and t0 > 0.0 else (z if z > 0.0 else 1.0)
+        st["step"] = 0.105
+        st["k"] = k
+    tc = st["c"] * std
+    return [tc * math.exp(st["step"] * (j - 7)) for j in range(MAX_CAND)]
+
+
 def compress_cpu_(g: torch.Tensor, r: torch.Tensor, bufs: CompressBuffers, mode: int, ec: bool, zero_g: bool,
                   loops: int, z: float, k: int, k_cap: int, seed: int = 0, fixed_thr: float = 0.0,
-                  sample_p: float = 0.01, n_stats: int = 0) -> None:
-    """Pure-torch mirror of gk::compress (same record layout and semantics)."""
+                  sample_p: float = 0.01, n_stats: int = 0, valid: Optional[torch.Tensor] = None,
+                  u: Optional[torch.Tensor] = None) -> None:
+    """Pure-torch mirror of gk::compress (same record layout and semantics).
+
+    ``u``: DGC velocity (momentum correction already applied to g by the
+    caller); sent indices are zeroed in it (momentum factor masking)."""
     with torch.no_grad():
         acc = g + r if ec else g.clone()
         r.copy_(acc)
@@ -273,7 +347,20 @@ def compress_cpu_(g: torch.Tensor, r: torch.Tensor, bufs: CompressBuffers, mode:
         stats = (mean, std, meanabs, maxabs)
         bufs.stats.copy_(torch.tensor(stats, dtype=torch.float32))
         k = max(int(k), 1)
-        if mode in (MODE_GAUSSIAN, MODE_REDSYNC, MODE_REDSYNCTRIM, MODE_THRESHOLD):
+        if mode == MODE_GAUSSIAN_CAL:
+            thr = _cal_ladder(bufs, k, z, mean, std)
+            keys = abs_key(acc)
+            bounds = [_bound_from_threshold(t) for t in thr]
+            counts = [int((keys >= b).sum()) for b in bounds]
+            chosen, fallback = _cal_decide(bufs, k, thr, counts, std)
+            if fallback:
+                mask, K, _ = _radix_topk_mask(keys, torch.ones(n, dtype=torch.bool), k)
+                chosen = CAL_FALLBACK
+                thr_chosen = float(torch.tensor([K & 0x7FFFFFFF], dtype=torch.int32).view(torch.float32))
+            else:
+                mask = keys >= bounds[chosen]
+                thr_chosen = thr[chosen]
+        elif mode in (MODE_GAUSSIAN, MODE_REDSYNC, MODE_REDSYNCTRIM, MODE_THRESHOLD):
             thr = _candidates(mode, loops, z, fixed_thr, stats)
             keys = abs_key(acc)
             bounds = [_bound_from_threshold(t) for t in thr]
@@ -284,8 +371,7 @@ def compress_cpu_(g: torch.Tensor, r: torch.Tensor, bufs: CompressBuffers, mode:
         elif mode in (MODE_TOPK, MODE_RANDOMK):
             idx = torch.arange(n, dtype=torch.int64)
             if mode == MODE_RANDOMK:
-                keys = hash_u32(idx, seed)
-                keys = torch.where(keys == 0xFFFFFFFF, torch.full_like(keys, 0xFFFFFFFE), keys)
+                keys = hash_key(idx, seed, valid)
             else:
                 keys = abs_key(acc)
             mask, K, _ = _radix_topk_mask(keys, torch.ones(n, dtype=torch.bool), k)
@@ -323,24 +409,54 @@ def compress_cpu_(g: torch.Tensor, r: torch.Tensor, bufs: CompressBuffers, mode:
         rec[REC_HDR:REC_HDR + sent] = sel.to(torch.int32)
         rec[REC_HDR + k_cap:REC_HDR + k_cap + sent] = acc[sel].view(torch.int32)
         r[sel] = 0.0
+        if u is not None:
+            u[sel] = 0.0
 
 
 def compress_(g: torch.Tensor, r: torch.Tensor, bufs: CompressBuffers, mode: int, ec: bool = True,
               zero_g: bool = True, loops: int = 3, z: float = 0.0, k: int = 1, k_cap: Optional[int] = None,
-              seed: int = 0, fixed_thr: float = 0.0, sample_p: float = 0.01, n_stats: int = 0) -> None:
+              seed: int = 0, fixed_thr: float = 0.0, sample_p: float = 0.01, n_stats: int = 0,
+              valid: Optional[torch.Tensor] = None, mc: Optional[dict] = None) -> None:
     """Sparsify ``g`` (+ residual ``r``) into ``bufs.record``.  Async on GPU.
 
     ``n_stats``: element count used for mean/std (the real, unpadded bucket
     size; padding elements are zeros and do not change the sums).
+    ``valid``: int32 bitmask of the real elements (``valid_bitmask``); random-k
+    never picks padding slots.
+    ``mc``: DGC momentum correction fused into the statistics pass -- dict with
+    ``u`` and ``w`` (bucket slices of the velocity / weight arenas), ``chunks``
+    (chunk table), ``begin``/``count`` (this bucket's rows), ``base`` (bucket
+    arena offset), ``groups`` (param-group dicts with momentum/weight_decay),
+    and optionally ``chunk_list`` (decoded rows, CPU path).  The sent indices
+    are zeroed in ``u`` (momentum factor masking).
     """
     k_cap = bufs.k_cap if k_cap is None else int(k_cap)
     if g.is_cuda:
         require_native(g)
+        kw = {}
+        if valid is not None:
+            kw["valid"] = valid
+        if mc is not None:
+            if not zero_g:
+                raise ValueError("momentum-corrected compress zeroes g")
+            kw.update(u=mc["u"], w=mc["w"], chunks=mc["chunks"], chunk_begin=int(mc["begin"]),
+                      chunk_count=int(mc["count"]), chunk_base=int(mc["base"]),
+                      mc_mu=[float(p["momentum"]) for p in mc["groups"]],
+                      mc_wd=[float(p.get("weight_decay", 0.0)) for p in mc["groups"]])
         _ops().compress(g, r, bufs.ctrl, bufs.ws, bufs.record, int(mode), bool(ec), bool(zero_g), int(loops),
                         float(z), float(fixed_thr), float(sample_p), int(k), int(k_cap), int(seed) & 0xFFFFFFFF,
-                        int(n_stats), bufs.stats)
+                        int(n_stats), bufs.stats, **kw)
     else:
-        compress_cpu_(g, r, bufs, mode, ec, zero_g, loops, z, k, k_cap, seed, fixed_thr, sample_p, n_stats)
+        u = None
+        if mc is not None:
+            base = int(mc["base"])
+            cl = mc.get("chunk_list")
+            cl = cl if cl is not None else _decode_chunks(mc["chunks"])
+            rows = [(st - base, ln, gi, sg) for st, ln, gi, sg in cl[int(mc["begin"]):int(mc["begin"]) + int(mc["count"])]]
+            momentum_correct_(mc["u"], g, mc["w"], None, 0, len(rows), mc["groups"], rows)
+            u = mc["u"]
+        compress_cpu_(g, r, bufs, mode, ec, zero_g, loops, z, k, k_cap, seed, fixed_thr, sample_p, n_stats,
+                      valid, u)
 
 
 def ctrl_fields(bufs: CompressBuffers) -> dict:
@@ -367,11 +483,72 @@ def scatter_add_records_(dst: torch.Tensor, records: torch.Tensor, P: int, k_cap
         _ops().scatter_add_records(dst, records.contiguous(), int(P), int(k_cap), float(scale), bool(deterministic))
         return
     rec = records.view(P, REC_HDR + 2 * k_cap)
+    if P == 1:
+        cnt = min(int(rec[0, 0]), k_cap)
+        idx = rec[0, REC_HDR:REC_HDR + cnt].long()
+        val = rec[0, REC_HDR + k_cap:REC_HDR + k_cap + cnt].view(torch.float32)
+        dst.index_add_(0, idx, val * scale)
+        return
+    idx, s = _rank_ordered_sum(rec, P, k_cap, dst.numel())
+    dst[idx] += s * torch.tensor(scale, dtype=torch.float32)   # fp32 scale, as the kernel
+
+
+def _rank_ordered_sum(rec: torch.Tensor, P: int, k_cap: int, n: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(unique indices, fp32 sums in rank order) of P packed records -- the
+    arithmetic of reduce_records_kernel: s = ((0 + v_0) + v_1) + ..."""
+    acc = torch.zeros(n, dtype=torch.float32)
+    seen = torch.zeros(n, dtype=torch.bool)
     for r in range(P):
-        cnt = int(rec[r, 0])
+        cnt = min(int(rec[r, 0]), k_cap)
         idx = rec[r, REC_HDR:REC_HDR + cnt].long()
         val = rec[r, REC_HDR + k_cap:REC_HDR + k_cap + cnt].view(torch.float32)
-        dst.index_add_(0, idx, val * scale)
+        acc.index_add_(0, idx, val)   # unique within one record: one fp32 add per index
+        seen[idx] = True
+    idx = torch.nonzero(seen).view(-1)
+    return idx, acc[idx]
+
+
+def apply_records_sgd_(w: torch.Tensor, w_bf16: Optional[torch.Tensor], records: torch.Tensor, P: int, k_cap: int,
+                       scale: float, lr: float, lr_mult: Optional[torch.Tensor] = None) -> None:
+    """Sparse SGD from the packed records: w[i] -= lr * scale * sum_r val_r[i]."""
+    if w.is_cuda:
+        require_native(w)
+        _ops().apply_records_sgd(w, w_bf16, records.contiguous(), int(P), int(k_cap), float(scale), float(lr), lr_mult)
+        return
+    rec = records.view(P, REC_HDR + 2 * k_cap)
+    idx, s = _rank_ordered_sum(rec, P, k_cap, w.numel())
+    lr_eff = torch.tensor(lr, dtype=torch.float32)
+    if lr_mult is not None:
+        lr_eff = lr_eff * lr_mult.float().cpu().view(())
+    w[idx] = w[idx] - lr_eff * (s * torch.tensor(scale, dtype=torch.float32))
+    if w_bf16 is not None:
+        w_bf16[idx] = w[idx].to(torch.bfloat16)
+
+
+def arena_digest(x: torch.Tensor) -> Tuple[int, int]:
+    """(fp64 sum bits, 64-bit content hash) of a flat fp32 arena -- equal digests on
+    two replicas mean bit-identical weights (up to a 2^-64 hash collision)."""
+    if x.is_cuda:
+        require_native(x)
+        out = torch.zeros(2, dtype=torch.int64, device=x.device)
+        ws = torch.zeros(2048, dtype=torch.int64, device=x.device)
+        _ops().arena_digest(x, out, ws)
+        a, b = out.cpu().tolist()
+        return int(a) & 0xFFFFFFFFFFFFFFFF, int(b) & 0xFFFFFFFFFFFFFFFF
+    import struct
+
+    import numpy as np
+    xs = x.detach().contiguous().view(-1)
+    s = float(xs.double().sum())
+    b = xs.view(torch.int32).numpy().view(np.uint32).astype(np.uint64)
+    i = np.arange(xs.numel(), dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = (b << np.uint64(32)) ^ (i * np.uint64(0x9E3779B97F4A7C15))
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+        tot = int(z.sum(dtype=np.uint64))
+    return struct.unpack("<Q", struct.pack("<d", s))[0], tot
 
 
 def fill_zero_(dst: torch.Tensor) -> None:

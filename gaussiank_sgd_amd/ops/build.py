@@ -44,6 +44,9 @@ CXX_SOURCES = [
     "bindings.cpp",
 ]
 HEADERS = ["kernels/common.h", "kernels/gk_kernels.h", "comm/rccl_engine.h"]
+# per-file extra flags: the sparse aggregation must round product and sum
+# separately (bit-identical to the reference arithmetic and the CPU mirror)
+EXTRA_FLAGS = {"kernels/scatter.hip": ["-ffp-contract=off"]}
 
 
 def _torch_dirs():
@@ -109,6 +112,7 @@ def _compile(src_rel: str, kind: str, verbose: bool) -> Path:
         cc, flags = _hipcc(), _hip_flags()
     else:
         cc, flags = os.environ.get("CXX", "g++"), _cxx_flags()
+    flags = flags + EXTRA_FLAGS.get(src_rel, [])
     obj = BUILD / (src_rel.replace("/", "_") + "." + _digest(src, flags) + ".o")
     if obj.exists():
         return obj

@@ -38,7 +38,10 @@ int64_t workspace_bytes() { return (int64_t)gk::compress_workspace_bytes(0); }
 
 void compress(at::Tensor g, at::Tensor r, at::Tensor ctrl, at::Tensor ws, at::Tensor record, int64_t mode, bool ec,
               bool zero_g, int64_t loops, double z, double fixed_thr, double sample_p, int64_t k, int64_t k_cap,
-              int64_t seed, int64_t n_stats, c10::optional<at::Tensor> stats_out) {
+              int64_t seed, int64_t n_stats, c10::optional<at::Tensor> stats_out, c10::optional<at::Tensor> valid,
+              c10::optional<at::Tensor> u, c10::optional<at::Tensor> w, c10::optional<at::Tensor> chunks,
+              int64_t chunk_begin, int64_t chunk_count, int64_t chunk_base, std::vector<double> mc_mu,
+              std::vector<double> mc_wd) {
   check_f32(g, "g");
   check_f32(r, "r");
   check_dev(ctrl, "ctrl");
@@ -50,7 +53,7 @@ void compress(at::Tensor g, at::Tensor r, at::Tensor ctrl, at::Tensor ws, at::Te
   TORCH_CHECK(record.scalar_type() == at::kInt, "record must be int32");
   TORCH_CHECK(k_cap >= 1 && record.numel() >= 4 + 2 * k_cap, "record must hold 4 + 2*k_cap int32");
   TORCH_CHECK(g.numel() < (int64_t)0x7fffffff, "bucket too large for int32 indices");
-  TORCH_CHECK(mode >= 0 && mode <= 6, "bad mode");
+  TORCH_CHECK(mode >= 0 && mode <= 7, "bad mode");
   TORCH_CHECK(loops >= 1 && loops * (loops + 1) / 2 <= gk::kMaxCand, "loops out of range");
   TORCH_CHECK((reinterpret_cast<uintptr_t>(ctrl.data_ptr()) & 7) == 0, "ctrl must be 8-byte aligned");
   TORCH_CHECK((reinterpret_cast<uintptr_t>(ws.data_ptr()) & 255) == 0, "ws must be 256-byte aligned");
@@ -79,7 +82,72 @@ void compress(at::Tensor g, at::Tensor r, at::Tensor ctrl, at::Tensor ws, at::Te
     TORCH_CHECK(stats_out->numel() >= 4, "stats_out needs 4 floats");
     a.stats_out = stats_out->data_ptr<float>();
   }
+  if (valid.has_value() && valid->defined()) {
+    check_dev(*valid, "valid");
+    TORCH_CHECK(valid->scalar_type() == at::kInt && valid->numel() * 32 >= g.numel(),
+                "valid must be an int32 bitmask of >= n bits");
+    a.valid = reinterpret_cast<const uint32_t*>(valid->data_ptr<int32_t>());
+  }
+  if (u.has_value() && u->defined()) {
+    TORCH_CHECK(w.has_value() && w->defined() && chunks.has_value() && chunks->defined(),
+                "momentum-corrected compress needs u, w and the chunk table");
+    check_f32(*u, "u");
+    check_f32(*w, "w");
+    check_dev(*chunks, "chunks");
+    TORCH_CHECK(chunks->scalar_type() == at::kLong, "chunks must be int64");
+    TORCH_CHECK(u->numel() == g.numel() && w->numel() == g.numel(), "u / w must be bucket slices like g");
+    TORCH_CHECK(zero_g, "momentum-corrected compress always zeroes g");
+    TORCH_CHECK(chunk_begin >= 0 && chunk_count >= 1 && (chunk_begin + chunk_count) * 2 <= chunks->numel(),
+                "chunk range out of bounds");
+    TORCH_CHECK(mc_mu.size() >= 1 && mc_mu.size() <= 8 && mc_wd.size() == mc_mu.size(), "1..8 param groups");
+    TORCH_CHECK(((reinterpret_cast<uintptr_t>(u->data_ptr()) | reinterpret_cast<uintptr_t>(w->data_ptr()) |
+                  reinterpret_cast<uintptr_t>(g.data_ptr()) | reinterpret_cast<uintptr_t>(r.data_ptr())) & 15) == 0,
+                "u / w / g / r must be 16-byte aligned");
+    a.u = u->data_ptr<float>();
+    a.w = w->data_ptr<float>();
+    a.chunks = reinterpret_cast<const gk::Chunk*>(chunks->data_ptr<int64_t>());
+    a.chunk_begin = (int)chunk_begin;
+    a.chunk_count = (int)chunk_count;
+    a.chunk_base = chunk_base;
+    for (size_t i = 0; i < mc_mu.size(); ++i) {
+      a.mc_mu[i] = (float)mc_mu[i];
+      a.mc_wd[i] = (float)mc_wd[i];
+    }
+  }
   gk::compress(a, cur_stream(g));
+}
+
+void apply_records_sgd(at::Tensor w, c10::optional<at::Tensor> w_bf16, at::Tensor records, int64_t P, int64_t k_cap,
+                       double scale, double lr, c10::optional<at::Tensor> lr_mult) {
+  check_f32(w, "w");
+  check_dev(records, "records");
+  TORCH_CHECK(records.scalar_type() == at::kInt, "records must be int32");
+  TORCH_CHECK(P >= 1 && records.numel() >= P * (4 + 2 * k_cap), "records too small for P x (4 + 2 k_cap)");
+  uint16_t* sh = nullptr;
+  if (w_bf16.has_value() && w_bf16->defined()) {
+    TORCH_CHECK(w_bf16->scalar_type() == at::kBFloat16 && w_bf16->numel() == w.numel() && w_bf16->is_contiguous(),
+                "w_bf16 must be a contiguous bf16 tensor of w's size");
+    sh = reinterpret_cast<uint16_t*>(w_bf16->data_ptr());
+  }
+  const float* lm = nullptr;
+  if (lr_mult.has_value() && lr_mult->defined()) {
+    check_f32(*lr_mult, "lr_mult");
+    lm = lr_mult->data_ptr<float>();
+  }
+  c10::DeviceGuard guard(w.device());
+  gk::apply_records_sgd(w.data_ptr<float>(), sh, w.numel(), records.data_ptr<int32_t>(), (int)P, k_cap, (float)scale,
+                        (float)lr, lm, cur_stream(w));
+}
+
+void arena_digest(at::Tensor x, at::Tensor out, at::Tensor ws) {
+  check_f32(x, "x");
+  check_dev(out, "out");
+  check_dev(ws, "ws");
+  TORCH_CHECK(out.scalar_type() == at::kLong && out.numel() >= 2, "out must be int64[2]");
+  TORCH_CHECK(ws.scalar_type() == at::kLong && ws.numel() >= 2048, "ws must be int64[>=2048]");
+  c10::DeviceGuard guard(x.device());
+  gk::arena_digest(x.data_ptr<float>(), x.numel(), reinterpret_cast<uint64_t*>(out.data_ptr<int64_t>()),
+                   reinterpret_cast<uint64_t*>(ws.data_ptr<int64_t>()), cur_stream(x));
 }
 
 void tensor_stats(at::Tensor x, at::Tensor ctrl, at::Tensor ws) {
@@ -571,11 +639,45 @@ struct RcclEngine : torch::CustomClassHolder {
     comm.broadcast(t.data_ptr(), (size_t)t.numel(), to_nccl(t.scalar_type()), (int)root, cur_stream(t));
   }
 
+  void allgather_many(std::vector<at::Tensor> sends, std::vector<at::Tensor> recvs) {
+    TORCH_CHECK(sends.size() == recvs.size() && !sends.empty(), "allgather_many: matching non-empty lists");
+    std::vector<const void*> sp;
+    std::vector<void*> rp;
+    std::vector<size_t> nb;
+    for (size_t i = 0; i < sends.size(); ++i) {
+      check_dev(sends[i], "send");
+      check_dev(recvs[i], "recv");
+      TORCH_CHECK(sends[i].device() == sends[0].device() && recvs[i].device() == sends[0].device(),
+                  "allgather_many: one device");
+      TORCH_CHECK(recvs[i].nbytes() == sends[i].nbytes() * (size_t)comm.world(), "recv must be world x send bytes");
+      sp.push_back(sends[i].data_ptr());
+      rp.push_back(recvs[i].data_ptr());
+      nb.push_back(sends[i].nbytes());
+    }
+    c10::DeviceGuard guard(sends[0].device());
+    comm.allgather_many(sp, rp, nb, cur_stream(sends[0]));
+  }
+
   void group_start() { comm.group_start(); }
   void group_end() { comm.group_end(); }
   void destroy() { comm.destroy(); }
   int64_t rank() const { return comm.rank(); }
   int64_t world() const { return comm.world(); }
+
+  void set_tracking(bool on) { comm.set_tracking(on); }
+  void start_watchdog(double timeout_s, double poll_ms) { comm.start_watchdog(timeout_s, poll_ms); }
+  void stop_watchdog() { comm.stop_watchdog(); }
+  int64_t poll() { return comm.poll(); }
+  bool failed() const { return comm.failed(); }
+  std::string error() const { return comm.error(); }
+  void check() const { comm.check(); }
+  int64_t in_flight() const { return comm.in_flight(); }
+  void reset_stats() { comm.reset_stats(); }
+  // [calls, bytes, ms_total, ms_max] of op 0 all-gather, 1 all-reduce, 2 broadcast, 3 grouped all-gather
+  std::vector<double> stats(int64_t op) const {
+    gk::OpStats st = comm.stats((int)op);
+    return {(double)st.calls, (double)st.bytes, st.ms_total, st.ms_max};
+  }
 };
 
 // ---------------------------------------------------------------------------
@@ -881,7 +983,12 @@ TORCH_LIBRARY(gksgd, m) {
   m.def(
       "compress(Tensor(a!) g, Tensor(b!) r, Tensor(c!) ctrl, Tensor(d!) ws, Tensor(e!) record, int mode, bool ec, "
       "bool zero_g, int loops, float z, float fixed_thr, float sample_p, int k, int k_cap, int seed, "
-      "int n_stats, Tensor(f!)? stats_out=None) -> ()");
+      "int n_stats, Tensor(f!)? stats_out=None, Tensor? valid=None, Tensor(g!)? u=None, Tensor? w=None, "
+      "Tensor? chunks=None, int chunk_begin=0, int chunk_count=0, int chunk_base=0, float[] mc_mu=[], "
+      "float[] mc_wd=[]) -> ()");
+  m.def("apply_records_sgd(Tensor(a!) w, Tensor(b!)? w_bf16, Tensor records, int P, int k_cap, float scale, float lr, "
+        "Tensor? lr_mult=None) -> ()");
+  m.def("arena_digest(Tensor x, Tensor(a!) out, Tensor(b!) ws) -> ()");
   m.def("tensor_stats(Tensor x, Tensor(a!) ctrl, Tensor(b!) ws) -> ()");
   m.def("scatter_add_records(Tensor(a!) dst, Tensor records, int P, int k_cap, float scale, bool deterministic) -> ()");
   m.def("fill_zero(Tensor(a!) dst) -> ()");
@@ -952,6 +1059,17 @@ TORCH_LIBRARY(gksgd, m) {
       .def("allgather", &RcclEngine::allgather)
       .def("allreduce", &RcclEngine::allreduce)
       .def("broadcast", &RcclEngine::broadcast)
+      .def("allgather_many", &RcclEngine::allgather_many)
+      .def("set_tracking", &RcclEngine::set_tracking)
+      .def("start_watchdog", &RcclEngine::start_watchdog)
+      .def("stop_watchdog", &RcclEngine::stop_watchdog)
+      .def("poll", &RcclEngine::poll)
+      .def("failed", &RcclEngine::failed)
+      .def("error", &RcclEngine::error)
+      .def("check", &RcclEngine::check)
+      .def("in_flight", &RcclEngine::in_flight)
+      .def("reset_stats", &RcclEngine::reset_stats)
+      .def("stats", &RcclEngine::stats)
       .def("group_start", &RcclEngine::group_start)
       .def("group_end", &RcclEngine::group_end)
       .def("destroy", &RcclEngine::destroy)
@@ -963,6 +1081,8 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("compress", &compress);
   m.impl("tensor_stats", &tensor_stats);
   m.impl("scatter_add_records", &scatter_add_records);
+  m.impl("apply_records_sgd", &apply_records_sgd);
+  m.impl("arena_digest", &arena_digest);
   m.impl("fill_zero", &fill_zero);
   m.impl("sign_bucket_compress", &sign_bucket_compress);
   m.impl("sign_bucket_decompress", &sign_bucket_decompress);

@@ -1,5 +1,6 @@
 #include "rccl_engine.h"
 
+#include <cstdio>
 #include <cstring>
 #include <stdexcept>
 
@@ -14,8 +15,20 @@ std::string rccl_error_string(ncclResult_t r) { return std::string(ncclGetErrorS
       throw std::runtime_error(std::string("RCCL error at " #expr ": ") + rccl_error_string(_r)); \
   } while (0)
 
+namespace {
+const char* op_name(int op) {
+  switch (op) {
+    case kOpAllGather: return "all-gather";
+    case kOpAllReduce: return "all-reduce";
+    case kOpBroadcast: return "broadcast";
+    default: return "grouped all-gather";
+  }
+}
+}  // namespace
+
 RcclComm::~RcclComm() {
   // Never abort from a destructor; communicator teardown is explicit.
+  stop_watchdog();
   if (comm_ != nullptr) {
     ncclCommDestroy(comm_);
     comm_ = nullptr;
@@ -39,28 +52,229 @@ void RcclComm::init(const std::vector<uint8_t>& uid, int rank, int world, int de
   GK_NCCL_CHECK(ncclCommInitRank(&comm_, world, id, rank));
   rank_ = rank;
   world_ = world;
+  device_ = device;
 }
 
 void RcclComm::destroy() {
+  stop_watchdog();
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!failed_.load()) {
+      // in-flight collectives finish before their events are released
+      for (auto& p : pending_) hipEventSynchronize(p.end);
+    }
+    retire_locked(false);
+    for (auto& p : pending_) {
+      hipEventDestroy(p.start);
+      hipEventDestroy(p.end);
+    }
+    pending_.clear();
+    for (hipEvent_t e : pool_) hipEventDestroy(e);
+    pool_.clear();
+  }
   if (comm_ != nullptr) {
-    GK_NCCL_CHECK(ncclCommDestroy(comm_));
+    ncclComm_t c = comm_;
+    comm_ = nullptr;
+    GK_NCCL_CHECK(ncclCommDestroy(c));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// completion tracking
+// ---------------------------------------------------------------------------
+hipEvent_t RcclComm::take_event() {
+  if (!pool_.empty()) {
+    hipEvent_t e = pool_.back();
+    pool_.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  if (hipEventCreate(&e) != hipSuccess) throw std::runtime_error("hipEventCreate failed");
+  return e;
+}
+
+void RcclComm::begin_op(hipStream_t s, hipEvent_t* start) {
+  check();
+  if (comm_ == nullptr) throw std::runtime_error("RcclComm not initialised");
+  *start = nullptr;
+  if (!tracking_) return;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return;  // graph capture
+  std::lock_guard<std::mutex> lk(mu_);
+  *start = take_event();
+  hipEventRecord(*start, s);
+}
+
+void RcclComm::end_op(hipStream_t s, hipEvent_t start, int op, size_t bytes) {
+  if (start == nullptr) return;
+  std::lock_guard<std::mutex> lk(mu_);
+  Pending p;
+  p.start = start;
+  p.end = take_event();
+  p.op = op;
+  p.bytes = bytes;
+  p.t_enq = std::chrono::steady_clock::now();
+  hipEventRecord(p.end, s);
+  pending_.push_back(p);
+}
+
+int RcclComm::retire_locked(bool check_timeout) {
+  while (!pending_.empty()) {
+    Pending& p = pending_.front();
+    const hipError_t q = hipEventQuery(p.end);
+    if (q == hipErrorNotReady) {
+      if (check_timeout && timeout_s_ > 0.0) {
+        const double waited =
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - p.t_enq).count();
+        if (waited > timeout_s_) {
+          char buf[256];
+          std::snprintf(buf, sizeof(buf), "rank %d: %s of %zu bytes not complete after %.1f s (world %d)", rank_,
+                        op_name(p.op), p.bytes, waited, world_);
+          fail(buf);
+          return (int)pending_.size();
+        }
+      }
+      break;
+    }
+    if (q == hipSuccess) {
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, p.start, p.end) == hipSuccess) {
+        OpStats& st = stats_[p.op];
+        st.calls += 1;
+        st.bytes += p.bytes;
+        st.ms_total += ms;
+        if (ms > st.ms_max) st.ms_max = ms;
+      }
+    }
+    pool_.push_back(p.start);
+    pool_.push_back(p.end);
+    pending_.pop_front();
+  }
+  return (int)pending_.size();
+}
+
+void RcclComm::fail(const std::string& why) {
+  bool expected = false;
+  if (!failed_.compare_exchange_strong(expected, true)) return;
+  error_ = why;
+  std::fprintf(stderr, "[gk::RcclComm] %s -- aborting the communicator\n", why.c_str());
+  if (comm_ != nullptr) {
+    ncclCommAbort(comm_);   // releases RCCL kernels spinning on a dead peer
     comm_ = nullptr;
   }
 }
 
+int RcclComm::poll() {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (comm_ != nullptr && !failed_.load()) {
+    ncclResult_t st = ncclSuccess;
+    if (ncclCommGetAsyncError(comm_, &st) == ncclSuccess && st != ncclSuccess && st != ncclInProgress)
+      fail(std::string("asynchronous RCCL error: ") + rccl_error_string(st));
+  }
+  return retire_locked(true);
+}
+
+void RcclComm::watchdog_loop() {
+  hipSetDevice(device_);
+  while (!stop_.load()) {
+    std::this_thread::sleep_for(std::chrono::microseconds((int64_t)(poll_ms_ * 1000.0)));
+    poll();
+    if (failed_.load()) break;
+  }
+}
+
+void RcclComm::start_watchdog(double timeout_s, double poll_ms) {
+  stop_watchdog();
+  timeout_s_ = timeout_s;
+  poll_ms_ = poll_ms > 0.1 ? poll_ms : 0.1;
+  stop_.store(false);
+  watchdog_ = std::thread([this] { watchdog_loop(); });
+}
+
+void RcclComm::stop_watchdog() {
+  if (watchdog_.joinable()) {
+    stop_.store(true);
+    watchdog_.join();
+  }
+}
+
+std::string RcclComm::error() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return error_;
+}
+
+void RcclComm::check() const {
+  if (failed_.load()) throw std::runtime_error("RCCL engine failed: " + error());
+}
+
+OpStats RcclComm::stats(int op) const {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (op < 0 || op >= kNumOps) return OpStats();
+  return stats_[op];
+}
+
+void RcclComm::reset_stats() {
+  std::lock_guard<std::mutex> lk(mu_);
+  for (auto& s : stats_) s = OpStats();
+}
+
+int RcclComm::in_flight() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return (int)pending_.size();
+}
+
+// ---------------------------------------------------------------------------
+// collectives
+// ---------------------------------------------------------------------------
 void RcclComm::allgather_bytes(const void* send, void* recv, size_t bytes, hipStream_t s) {
+  hipEvent_t st;
+  begin_op(s, &st);
   GK_NCCL_CHECK(ncclAllGather(send, recv, bytes, ncclUint8, comm_, s));
+  end_op(s, st, kOpAllGather, bytes);
+}
+
+void RcclComm::allgather_many(const std::vector<const void*>& sends, const std::vector<void*>& recvs,
+                              const std::vector<size_t>& bytes, hipStream_t s) {
+  if (sends.size() != recvs.size() || sends.size() != bytes.size())
+    throw std::invalid_argument("allgather_many: list lengths differ");
+  if (sends.empty()) return;
+  hipEvent_t st;
+  begin_op(s, &st);
+  size_t total = 0;
+  GK_NCCL_CHECK(ncclGroupStart());
+  for (size_t i = 0; i < sends.size(); ++i) {
+    const ncclResult_t r = ncclAllGather(sends[i], recvs[i], bytes[i], ncclUint8, comm_, s);
+    if (r != ncclSuccess) {
+      ncclGroupEnd();
+      throw std::runtime_error(std::string("RCCL error in grouped all-gather: ") + rccl_error_string(r));
+    }
+    total += bytes[i];
+  }
+  GK_NCCL_CHECK(ncclGroupEnd());
+  end_op(s, st, kOpGroup, total);
 }
 
 void RcclComm::allreduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s) {
+  hipEvent_t st;
+  begin_op(s, &st);
   GK_NCCL_CHECK(ncclAllReduce(buf, buf, count, dt, op, comm_, s));
+  size_t esz = (dt == ncclFloat64 || dt == ncclInt64 || dt == ncclUint64) ? 8
+               : (dt == ncclFloat16 || dt == ncclBfloat16) ? 2
+               : (dt == ncclInt8 || dt == ncclUint8) ? 1 : 4;
+  end_op(s, st, kOpAllReduce, count * esz);
 }
 
 void RcclComm::broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t s) {
+  hipEvent_t st;
+  begin_op(s, &st);
   GK_NCCL_CHECK(ncclBroadcast(buf, buf, count, dt, root, comm_, s));
+  end_op(s, st, kOpBroadcast, count);
 }
 
-void RcclComm::group_start() { GK_NCCL_CHECK(ncclGroupStart()); }
+void RcclComm::group_start() {
+  check();
+  GK_NCCL_CHECK(ncclGroupStart());
+}
 void RcclComm::group_end() { GK_NCCL_CHECK(ncclGroupEnd()); }
 
 }  // namespace gk

@@ -7,16 +7,43 @@
 // rank calls ncclCommInitRank.  Collectives run on the CALLER's current HIP
 // stream, so compress -> all-gather -> scatter is one stream-ordered chain
 // (no host sync, no ProcessGroup bookkeeping, capturable in a hipGraph).
+//
+// What the engine adds over a bare communicator:
+//   * grouped launches: several buckets' record all-gathers in ONE
+//     ncclGroupStart/End (one kernel launch, all xGMI links busy at once);
+//   * completion tracking: every collective is bracketed by two HIP events
+//     (pooled); a background watchdog thread retires them, keeps per-op
+//     latency / byte statistics (the measured alpha-beta of this node's
+//     xGMI fabric, fed to the bucket planners) and
+//   * failure detection: if a collective has not completed after the
+//     timeout, or RCCL reports an asynchronous error, the watchdog aborts
+//     the communicator (ncclCommAbort releases the spinning RCCL kernels, so
+//     the GPU does not hang) and flags the engine; the next call on any
+//     thread throws with the reason instead of deadlocking.
 #pragma once
 
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
+#include <chrono>
 #include <cstdint>
+#include <deque>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace gk {
+
+enum CommOp : int { kOpAllGather = 0, kOpAllReduce = 1, kOpBroadcast = 2, kOpGroup = 3, kNumOps = 4 };
+
+struct OpStats {
+  uint64_t calls = 0;
+  uint64_t bytes = 0;       // payload bytes per rank (send side)
+  double ms_total = 0.0;    // sum of event-timed GPU durations
+  double ms_max = 0.0;
+};
 
 class RcclComm {
  public:
@@ -34,15 +61,57 @@ class RcclComm {
 
   // bytes-level all-gather: recv holds world * bytes
   void allgather_bytes(const void* send, void* recv, size_t bytes, hipStream_t s);
+  // several all-gathers in one RCCL group (one launch)
+  void allgather_many(const std::vector<const void*>& sends, const std::vector<void*>& recvs,
+                      const std::vector<size_t>& bytes, hipStream_t s);
   void allreduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s);
   void broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t s);
   void group_start();
   void group_end();
 
+  // completion tracking / failure detection
+  void set_tracking(bool on) { tracking_ = on; }
+  void start_watchdog(double timeout_s, double poll_ms);
+  void stop_watchdog();
+  // retire completed collectives on the calling thread (no watchdog running);
+  // returns the number still in flight
+  int poll();
+  bool failed() const { return failed_.load(); }
+  std::string error() const;
+  void check() const;   // throws std::runtime_error(reason) once failed
+  OpStats stats(int op) const;
+  void reset_stats();
+  int in_flight() const;
+
  private:
+  struct Pending {
+    hipEvent_t start, end;
+    int op;
+    size_t bytes;
+    std::chrono::steady_clock::time_point t_enq;
+  };
+  hipEvent_t take_event();
+  void begin_op(hipStream_t s, hipEvent_t* start);
+  void end_op(hipStream_t s, hipEvent_t start, int op, size_t bytes);
+  int retire_locked(bool check_timeout);
+  void fail(const std::string& why);
+  void watchdog_loop();
+
   ncclComm_t comm_ = nullptr;
   int rank_ = 0;
   int world_ = 1;
+  int device_ = 0;
+  bool tracking_ = true;
+  mutable std::mutex mu_;
+  std::deque<Pending> pending_;
+  std::vector<hipEvent_t> pool_;
+  OpStats stats_[kNumOps];
+  std::atomic<bool> failed_{false};
+  std::string error_;
+  double timeout_s_ = 0.0;
+  double poll_ms_ = 5.0;
+  std::atomic<bool> stop_{false};
+  std::thread watchdog_;
 };
 
 std::string rccl_error_string(ncclResult_t r);

@@ -136,11 +136,15 @@ __device__ __forceinline__ uint32_t bound_from_threshold(float t) {
   return (__float_as_uint(t) & 0x7fffffffu) + 1u;
 }
 
+// Hash keys rank a uniformly random subset (random-k: the k LARGEST keys are
+// taken).  Arena padding slots (valid bit 0) get key 0 and are never picked
+// while enough real elements exist.
 template <int KEYKIND>
-__device__ __forceinline__ uint32_t key_of(int64_t i, float x, uint32_t seed) {
+__device__ __forceinline__ uint32_t key_of(int64_t i, float x, uint32_t seed, const uint32_t* valid) {
   if (KEYKIND == kKeyHash) {
+    if (valid != nullptr && !((valid[i >> 5] >> (i & 31)) & 1u)) return 0u;
     uint32_t h = hash_u32((uint32_t)i, seed);
-    return h == 0xffffffffu ? 0xfffffffeu : h;
+    return h == 0xffffffffu ? 0xfffffffeu : (h == 0u ? 1u : h);
   }
   return abs_key(x);
 }
@@ -213,6 +217,68 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(float* __restrict__ g, fl
   }
 }
 
+// DGC momentum correction fused into K1+K2: one pass reads u, g, w, r and
+// writes u, r, g:  u = mu*u + (g + wd*w);  acc = u (+ r);  r = acc;  g = 0,
+// with the moments of acc.  Replaces momentum_correct (u, g, w -> u, g) plus
+// stats (g, r -> r, g): 9 -> 7 arena streams.  Per-chunk hyper-parameters
+// (param groups); chunks are 64-element aligned, so every access is a float4.
+struct McHyper {
+  float mu[8];
+  float wd[8];
+};
+
+template <bool EC>
+__global__ __launch_bounds__(kBlock) void mc_stats_kernel(float* __restrict__ g, float* __restrict__ r,
+                                                          float* __restrict__ u, const float* __restrict__ w,
+                                                          const Chunk* __restrict__ chunks, int nchunks,
+                                                          int64_t base, McHyper hp, double* __restrict__ partials) {
+  float s = 0.f, ss = 0.f, sa = 0.f, mx = 0.f;
+  for (int ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
+    const Chunk c = chunks[ci];
+    const float mu = hp.mu[c.group], wd = hp.wd[c.group];
+    const int64_t off = c.start - base;
+    float4* g4 = reinterpret_cast<float4*>(g + off);
+    float4* r4 = reinterpret_cast<float4*>(r + off);
+    float4* u4 = reinterpret_cast<float4*>(u + off);
+    const float4* w4 = reinterpret_cast<const float4*>(w + off);
+    const int n4 = c.len >> 2;
+    for (int i = threadIdx.x; i < n4; i += kBlock) {
+      float4 uv = u4[i];
+      const float4 gv = g4[i];
+      const float4 wv = w4[i];
+      uv.x = fmaf(mu, uv.x, fmaf(wd, wv.x, gv.x));
+      uv.y = fmaf(mu, uv.y, fmaf(wd, wv.y, gv.y));
+      uv.z = fmaf(mu, uv.z, fmaf(wd, wv.z, gv.z));
+      uv.w = fmaf(mu, uv.w, fmaf(wd, wv.w, gv.w));
+      u4[i] = uv;
+      float4 a = uv;
+      if (EC) {
+        const float4 rv = r4[i];
+        a.x += rv.x; a.y += rv.y; a.z += rv.z; a.w += rv.w;
+      }
+      r4[i] = a;
+      g4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      s += (a.x + a.y) + (a.z + a.w);
+      ss += (a.x * a.x + a.y * a.y) + (a.z * a.z + a.w * a.w);
+      const float ax = fabsf(a.x), ay = fabsf(a.y), az = fabsf(a.z), aw = fabsf(a.w);
+      sa += (ax + ay) + (az + aw);
+      mx = fmaxf(mx, fmaxf(fmaxf(ax, ay), fmaxf(az, aw)));
+    }
+  }
+  __shared__ double sh[kWavesPerBlock];
+  __shared__ float shf[kWavesPerBlock];
+  const double bs = block_sum((double)s, sh);
+  const double bss = block_sum((double)ss, sh);
+  const double bsa = block_sum((double)sa, sh);
+  const float bmx = block_max(mx, shf);
+  if (threadIdx.x == 0) {
+    partials[blockIdx.x * 4 + 0] = bs;
+    partials[blockIdx.x * 4 + 1] = bss;
+    partials[blockIdx.x * 4 + 2] = bsa;
+    partials[blockIdx.x * 4 + 3] = (double)bmx;
+  }
+}
+
 // --------------------------------------------------------------------------
 // radix histogram passes
 // --------------------------------------------------------------------------
@@ -225,10 +291,13 @@ __device__ __forceinline__ uint32_t radix_digit(uint32_t key) {
 
 template <int PASS, int KEYKIND, bool VEC>
 __global__ __launch_bounds__(kBlock) void radix_hist_kernel(const float* __restrict__ x, int64_t n, uint32_t seed,
-                                                            uint32_t sample_thr, int64_t k, uint32_t* hist_set) {
+                                                            uint32_t sample_thr, int64_t k, uint32_t* hist_set,
+                                                            const uint32_t* __restrict__ valid,
+                                                            const GkCtrl* __restrict__ cond) {
   constexpr int NB = PASS == 0 ? kRadixBins0 : (PASS == 1 ? kRadixBins1 : kRadixBins2);
   __shared__ uint32_t sh_hist[kWavesPerBlock][NB];
   __shared__ uint64_t sh_scan[kWavesPerBlock];
+  if (cond != nullptr && cond->fallback == 0) return;   // conditional pass (calibrated mode), grid-uniform
   uint32_t* hist0 = hist_set;
   uint32_t* hist1 = hist_set + kRadixBins0;
   uint32_t* hist2 = hist1 + kRadixBins1;
@@ -269,7 +338,7 @@ __global__ __launch_bounds__(kBlock) void radix_hist_kernel(const float* __restr
         if (hash_u32((uint32_t)idx, seed) >= sample_thr) continue;
         key = abs_key(v[q]) + 1u;
       } else {
-        key = key_of<KEYKIND>(idx, v[q], seed);
+        key = key_of<KEYKIND>(idx, v[q], seed, valid);
       }
       bool elig = true;
       if (PASS == 1) elig = (key >> 21) == prefix;
@@ -394,6 +463,24 @@ __global__ __launch_bounds__(kBlock) void finalize_kernel(GkCtrl* __restrict__ c
       }
       nc = kMaxCand;
     }
+  } else if (mode == kModeGaussianCal) {
+    // 16 thresholds t_c * exp(step * (j - 7)), ascending in j.  The centre
+    // t_c = cal_c * sigma and the spacing persist per bucket (decide_kernel
+    // re-centres on the best candidate and adapts the spacing to the local
+    // slope of the count curve); first call / new k: the Gaussian estimate.
+    if (ctrl->cal_k != k || !(ctrl->cal_c > 0.0) || !(ctrl->cal_step > 0.0)) {
+      const double t0 = mean + z * stdev;
+      ctrl->cal_c = stdev > 0.0 && t0 > 0.0 ? t0 / stdev : (z > 0.0 ? z : 1.0);
+      ctrl->cal_step = 0.105;   // ~ln(1.11): neighbours ~1.3x apart in count on a Gaussian at 3.3 sigma
+      ctrl->cal_k = k;
+    }
+    const double tc = ctrl->cal_c * stdev;
+    for (int j = 0; j < kMaxCand; ++j) {
+      const double t = tc * exp(ctrl->cal_step * (double)(j - 7));
+      ctrl->bound[j] = bound_from_threshold((float)t);
+      ctrl->cand_thr[j] = t;
+    }
+    nc = kMaxCand;
   } else if (mode == kModeThreshold) {
     ctrl->bound[0] = bound_from_threshold((float)fixed_thr);
     ctrl->cand_thr[0] = fixed_thr;
@@ -416,6 +503,28 @@ __global__ __launch_bounds__(kBlock) void finalize_kernel(GkCtrl* __restrict__ c
   ctrl->radix_key[0] = rkey[0]; ctrl->radix_key[1] = rkey[1];
   ctrl->radix_kremain[0] = rkrem[0]; ctrl->radix_kremain[1] = rkrem[1];
   ctrl->k_eff = rkeff[1];
+  ctrl->fallback = 0;
+}
+
+// Calibrated mode, no candidate in [2k/3, 4k/3]: resolve the exact radix key
+// (k-th largest |x|) from the conditional histogram passes; the second count /
+// decide / select then run exactly as in top-k mode.
+__global__ __launch_bounds__(kBlock) void cal_fallback_kernel(GkCtrl* __restrict__ ctrl, const uint32_t* hist_exact,
+                                                              int64_t k) {
+  if (ctrl->fallback == 0) return;
+  __shared__ uint64_t sh_scan[kWavesPerBlock];
+  uint32_t key;
+  int64_t krem, keff;
+  radix_resolve(hist_exact, k, sh_scan, &key, &krem, &keff);
+  if (threadIdx.x != 0) return;
+  for (int j = 0; j < kMaxCand; ++j) ctrl->bound[j] = 0xffffffffu;
+  ctrl->bound[0] = key + 1u;  // key > K
+  ctrl->bound[1] = key;       // key >= K
+  ctrl->ncand = 2;
+  ctrl->radix_key[1] = key;
+  ctrl->radix_kremain[1] = krem;
+  ctrl->k_eff = keff;
+  ctrl->cand_thr[0] = (double)__uint_as_float(key & 0x7fffffffu);
 }
 
 // --------------------------------------------------------------------------
@@ -424,7 +533,9 @@ __global__ __launch_bounds__(kBlock) void finalize_kernel(GkCtrl* __restrict__ c
 template <int KEYKIND, bool VEC>
 __global__ __launch_bounds__(kBlock) void count_kernel(const float* __restrict__ x, int64_t n, uint32_t seed,
                                                        const GkCtrl* __restrict__ ctrl, int64_t chunk_tiles,
-                                                       uint32_t* __restrict__ blockcnt) {
+                                                       uint32_t* __restrict__ blockcnt,
+                                                       const uint32_t* __restrict__ valid, int cond) {
+  if (cond && ctrl->fallback == 0) return;
   uint32_t bnd[kMaxCand];
 #pragma unroll
   for (int j = 0; j < kMaxCand; ++j) bnd[j] = __builtin_amdgcn_readfirstlane(ctrl->bound[j]);
@@ -443,10 +554,10 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const float* __restrict__
       if (KEYKIND != kKeyHash) load4<VEC>(x, e, n, v);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const bool valid = e + q < n;
-        const uint32_t key = key_of<KEYKIND>(e + q, v[q], seed);
+        const bool inb = e + q < n;
+        const uint32_t key = inb ? key_of<KEYKIND>(e + q, v[q], seed, valid) : 0u;
 #pragma unroll
-        for (int j = 0; j < kMaxCand; ++j) cnt[j] += (valid && key >= bnd[j]) ? 1u : 0u;
+        for (int j = 0; j < kMaxCand; ++j) cnt[j] += (inb && key >= bnd[j]) ? 1u : 0u;
       }
     }
   }
@@ -469,11 +580,16 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const float* __restrict__
 __global__ __launch_bounds__(kBlock) void decide_kernel(GkCtrl* __restrict__ ctrl, const uint32_t* __restrict__ blockcnt,
                                                         int G, int mode, int loops, int64_t k, int64_t k_cap,
                                                         int64_t* __restrict__ offsets, int64_t* __restrict__ eqtake,
-                                                        int64_t* __restrict__ blocksel, int32_t* __restrict__ hdr) {
+                                                        int64_t* __restrict__ blocksel, int32_t* __restrict__ hdr,
+                                                        int cond, uint32_t* __restrict__ hist_reset) {
   __shared__ uint64_t sh_tot[kWavesPerBlock][kMaxCand];
   __shared__ uint64_t sh_scan[kWavesPerBlock];
-  __shared__ int s_chosen, s_gt, s_ge;
+  __shared__ int s_chosen, s_gt, s_ge, s_stop;
   __shared__ int64_t s_quota;
+  if (cond) {
+    if (ctrl->fallback == 0) return;
+    mode = kModeTopK;   // second decide of a calibrated fallback: exact top-k on the radix key
+  }
   const int nc = ctrl->ncand;
   // totals per candidate
   uint64_t loc[kMaxCand];
@@ -490,6 +606,7 @@ __global__ __launch_bounds__(kBlock) void decide_kernel(GkCtrl* __restrict__ ctr
   }
   __syncthreads();
   if (threadIdx.x == 0) {
+    s_stop = 0;
     int64_t tot[kMaxCand];
     for (int j = 0; j < kMaxCand; ++j)
       tot[j] = (int64_t)(sh_tot[0][j] + sh_tot[1][j] + sh_tot[2][j] + sh_tot[3][j]);
@@ -518,6 +635,43 @@ __global__ __launch_bounds__(kBlock) void decide_kernel(GkCtrl* __restrict__ ctr
     } else if (mode == kModeRedSyncTrim) {
       chosen = nc - 1;
       for (int j = 0; j < nc; ++j) if (tot[j] >= k) { chosen = j; break; }
+    } else if (mode == kModeGaussianCal) {
+      // counts are non-increasing in j.  Pick the count closest to k (log
+      // distance) among those in [2k/3, 4k/3]; re-centre the ladder on the
+      // closest candidate overall and adapt its spacing so that neighbours
+      // two steps apart differ ~1.7x in count (a candidate then always lands
+      // in the 2x-wide window).
+      int best = -1, closest = 0;
+      double bestd = 1e300, closed = 1e300;
+      for (int j = 0; j < nc; ++j) {
+        const double c = (double)tot[j];
+        const double d = fabs(log((c > 0.0 ? c : 0.5) / kd));
+        if (d < closed) { closed = d; closest = j; }
+        if (c >= 2.0 * kd / 3.0 && c <= 4.0 * kd / 3.0 && d < bestd) { bestd = d; best = j; }
+      }
+      const int jc = best >= 0 ? best : closest;
+      double step = ctrl->cal_step;
+      if (best < 0 && (jc == 0 || jc == nc - 1)) {
+        step = step * 2.0;                                  // target beyond the ladder: widen
+      } else if (jc > 0 && jc < nc - 1 && tot[jc + 1] > 0) {
+        const double R = (double)tot[jc - 1] / (double)tot[jc + 1];
+        if (R > 1.0001) {
+          double f = log(1.7) / log(R);
+          f = f < 0.5 ? 0.5 : (f > 2.0 ? 2.0 : f);
+          step = step * f;
+        } else {
+          step = step * 2.0;
+        }
+      }
+      step = step < 0.002 ? 0.002 : (step > 1.0 ? 1.0 : step);
+      const double sd = ctrl->stdev;
+      if (sd > 0.0 && ctrl->cand_thr[jc] > 0.0) ctrl->cal_c = ctrl->cand_thr[jc] / sd;
+      ctrl->cal_step = step;
+      chosen = jc;
+      if (best < 0) {
+        s_stop = 1;
+        ctrl->fallback = 1;
+      }
     } else if (mode == kModeThreshold) {
       chosen = 0;
     } else if (mode == kModeTopK || mode == kModeRandomK) {
@@ -527,14 +681,21 @@ __global__ __launch_bounds__(kBlock) void decide_kernel(GkCtrl* __restrict__ ctr
       else chosen = 0;
     }
     if (ge < 0) gt = chosen;
-    s_chosen = chosen; s_gt = gt; s_ge = ge; s_quota = quota;
-    ctrl->chosen = chosen;
+    s_chosen = cond ? kCalFallback : chosen; s_gt = gt; s_ge = ge; s_quota = quota;
+    ctrl->chosen = s_chosen;
     ctrl->sel_bound = ctrl->bound[gt];
     ctrl->eq_key = ge >= 0 ? ctrl->bound[ge] : 0xffffffffu;
     ctrl->eq_quota = ge >= 0 ? quota : 0;
     ctrl->thr = (float)ctrl->cand_thr[chosen];
   }
   __syncthreads();
+  if (s_stop) {
+    // calibrated mode without a candidate in range: clear the exact-key
+    // histograms for the conditional radix passes; offsets come from the
+    // second (conditional) count / decide
+    for (int i = threadIdx.x; i < kHistSet; i += kBlock) hist_reset[i] = 0u;
+    return;
+  }
   const int gt = s_gt, ge = s_ge;
   const int64_t quota = s_quota;
   // each thread owns up to 4 consecutive blocks
@@ -596,7 +757,8 @@ __global__ __launch_bounds__(kBlock) void select_kernel(float* __restrict__ r, i
                                                         const int64_t* __restrict__ offsets,
                                                         const int64_t* __restrict__ eqtake,
                                                         const int64_t* __restrict__ blocksel, int64_t k_cap,
-                                                        int32_t* __restrict__ out_idx, float* __restrict__ out_val) {
+                                                        int32_t* __restrict__ out_idx, float* __restrict__ out_val,
+                                                        const uint32_t* __restrict__ valid, float* __restrict__ u) {
   const int64_t my_sel = blocksel[blockIdx.x];
   int64_t running = offsets[blockIdx.x];
   if (my_sel == 0 || running >= k_cap) return;  // block-uniform
@@ -621,10 +783,10 @@ __global__ __launch_bounds__(kBlock) void select_kernel(float* __restrict__ r, i
       selm[j4] = 0; eqm[j4] = 0;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const bool valid = e + q < n;
-        const uint32_t key = key_of<KEYKIND>(e + q, v[j4][q], seed);
-        if (valid && key >= bound) selm[j4] |= 1u << q;
-        if (valid && my_eq > 0 && key == eqkey) eqm[j4] |= 1u << q;
+        const bool inb = e + q < n;
+        const uint32_t key = inb ? key_of<KEYKIND>(e + q, v[j4][q], seed, valid) : 0u;
+        if (inb && key >= bound) selm[j4] |= 1u << q;
+        if (inb && my_eq > 0 && key == eqkey) eqm[j4] |= 1u << q;
       }
     }
     // ties (radix modes): take the first `my_eq` key==eqkey elements of this block
@@ -683,6 +845,7 @@ __global__ __launch_bounds__(kBlock) void select_kernel(float* __restrict__ r, i
               out_idx[pos] = (int32_t)(e + q);
               out_val[pos] = v[j4][q];
               r[e + q] = 0.f;
+              if (u != nullptr) u[e + q] = 0.f;   // momentum factor masking (DGC)
             }
             ++pos;
           }
@@ -695,27 +858,32 @@ __global__ __launch_bounds__(kBlock) void select_kernel(float* __restrict__ r, i
 }
 
 template <int KEYKIND>
-void launch_count_select(const CompressArgs& a, const Ws& w, bool vec, int G, int64_t chunk_tiles, GkCtrl* ctrl,
-                         int32_t* out_idx, float* out_val, hipStream_t s) {
+void launch_count(const CompressArgs& a, const Ws& w, bool vec, int G, int64_t chunk_tiles, GkCtrl* ctrl, int cond,
+                  hipStream_t s) {
   if (vec)
     hipLaunchKernelGGL((count_kernel<KEYKIND, true>), dim3(G), dim3(kBlock), 0, s, a.r, a.n, a.seed, ctrl,
-                       chunk_tiles, w.blockcnt);
+                       chunk_tiles, w.blockcnt, a.valid, cond);
   else
     hipLaunchKernelGGL((count_kernel<KEYKIND, false>), dim3(G), dim3(kBlock), 0, s, a.r, a.n, a.seed, ctrl,
-                       chunk_tiles, w.blockcnt);
+                       chunk_tiles, w.blockcnt, a.valid, cond);
   hipLaunchKernelGGL(decide_kernel, dim3(1), dim3(kBlock), 0, s, ctrl, w.blockcnt, G, a.mode, a.loops, a.k,
-                     a.k_cap, w.offsets, w.eqtake, w.blocksel, a.record);
+                     a.k_cap, w.offsets, w.eqtake, w.blocksel, a.record, cond, w.hist);
+}
+
+template <int KEYKIND>
+void launch_select(const CompressArgs& a, const Ws& w, bool vec, int G, int64_t chunk_tiles, GkCtrl* ctrl,
+                   int32_t* out_idx, float* out_val, hipStream_t s) {
   if (vec)
     hipLaunchKernelGGL((select_kernel<KEYKIND, true>), dim3(G), dim3(kBlock), 0, s, a.r, a.n, a.seed, ctrl,
-                       chunk_tiles, w.offsets, w.eqtake, w.blocksel, a.k_cap, out_idx, out_val);
+                       chunk_tiles, w.offsets, w.eqtake, w.blocksel, a.k_cap, out_idx, out_val, a.valid, a.u);
   else
     hipLaunchKernelGGL((select_kernel<KEYKIND, false>), dim3(G), dim3(kBlock), 0, s, a.r, a.n, a.seed, ctrl,
-                       chunk_tiles, w.offsets, w.eqtake, w.blocksel, a.k_cap, out_idx, out_val);
+                       chunk_tiles, w.offsets, w.eqtake, w.blocksel, a.k_cap, out_idx, out_val, a.valid, a.u);
 }
 
 template <int KEYKIND>
 void launch_radix(const float* x, int64_t n, uint32_t seed, uint32_t sample_thr, int64_t k, uint32_t* set, bool vec,
-                  hipStream_t s) {
+                  const uint32_t* valid, const GkCtrl* cond, hipStream_t s) {
   const int64_t n4 = (n + 3) / 4;
   int Gh = (int)ceil_div(n4, (int64_t)kBlock * 8);
   if (Gh < 1) Gh = 1;
@@ -723,10 +891,10 @@ void launch_radix(const float* x, int64_t n, uint32_t seed, uint32_t sample_thr,
 #define GK_RADIX_PASS(P)                                                                                         \
   if (vec)                                                                                                       \
     hipLaunchKernelGGL((radix_hist_kernel<P, KEYKIND, true>), dim3(Gh), dim3(kBlock), 0, s, x, n, seed, sample_thr, \
-                       k, set);                                                                                  \
+                       k, set, valid, cond);                                                                     \
   else                                                                                                           \
     hipLaunchKernelGGL((radix_hist_kernel<P, KEYKIND, false>), dim3(Gh), dim3(kBlock), 0, s, x, n, seed,          \
-                       sample_thr, k, set);
+                       sample_thr, k, set, valid, cond);
   GK_RADIX_PASS(0)
   GK_RADIX_PASS(1)
   GK_RADIX_PASS(2)
@@ -749,20 +917,36 @@ void compress(const CompressArgs& a, hipStream_t s) {
   const bool vec_gr = ((reinterpret_cast<uintptr_t>(a.g) | reinterpret_cast<uintptr_t>(a.r)) & 15) == 0 && (a.n % 4) == 0;
   const bool vec_r = (reinterpret_cast<uintptr_t>(a.r) & 15) == 0 && (a.n % 4) == 0;
 
-  // 1. stats (+ residual add, residual write, gradient zeroing)
-  int Gs = (int)ceil_div(a.n, (int64_t)kBlock * 16);
-  if (Gs < 1) Gs = 1;
-  if (Gs > kMaxStatsBlocks) Gs = kMaxStatsBlocks;
+  // 1. stats (+ residual add, residual write, gradient zeroing; + DGC momentum
+  //    correction when a chunk table is given)
+  int Gs;
+  if (a.u != nullptr && a.chunks != nullptr) {
+    Gs = a.chunk_count < kMaxStatsBlocks ? a.chunk_count : kMaxStatsBlocks;
+    if (Gs < 1) Gs = 1;
+    McHyper hp;
+    for (int i = 0; i < 8; ++i) { hp.mu[i] = a.mc_mu[i]; hp.wd[i] = a.mc_wd[i]; }
+    const Chunk* ch = a.chunks + a.chunk_begin;
+    if (a.ec)
+      hipLaunchKernelGGL((mc_stats_kernel<true>), dim3(Gs), dim3(kBlock), 0, s, a.g, a.r, a.u, a.w, ch,
+                         a.chunk_count, a.chunk_base, hp, w.partials);
+    else
+      hipLaunchKernelGGL((mc_stats_kernel<false>), dim3(Gs), dim3(kBlock), 0, s, a.g, a.r, a.u, a.w, ch,
+                         a.chunk_count, a.chunk_base, hp, w.partials);
+  } else {
+    Gs = (int)ceil_div(a.n, (int64_t)kBlock * 16);
+    if (Gs < 1) Gs = 1;
+    if (Gs > kMaxStatsBlocks) Gs = kMaxStatsBlocks;
 #define GK_STATS(VEC, EC, ZG)                                                                                     \
   hipLaunchKernelGGL((stats_kernel<VEC, EC, true, ZG>), dim3(Gs), dim3(kBlock), 0, s, a.g, a.r, a.n, w.partials);
-  if (vec_gr) {
-    if (a.ec) { if (a.zero_g) { GK_STATS(true, true, true) } else { GK_STATS(true, true, false) } }
-    else { if (a.zero_g) { GK_STATS(true, false, true) } else { GK_STATS(true, false, false) } }
-  } else {
-    if (a.ec) { if (a.zero_g) { GK_STATS(false, true, true) } else { GK_STATS(false, true, false) } }
-    else { if (a.zero_g) { GK_STATS(false, false, true) } else { GK_STATS(false, false, false) } }
-  }
+    if (vec_gr) {
+      if (a.ec) { if (a.zero_g) { GK_STATS(true, true, true) } else { GK_STATS(true, true, false) } }
+      else { if (a.zero_g) { GK_STATS(true, false, true) } else { GK_STATS(true, false, false) } }
+    } else {
+      if (a.ec) { if (a.zero_g) { GK_STATS(false, true, true) } else { GK_STATS(false, true, false) } }
+      else { if (a.zero_g) { GK_STATS(false, false, true) } else { GK_STATS(false, false, false) } }
+    }
 #undef GK_STATS
+  }
 
   // 2. radix histograms (exact / hash / sample)
   uint32_t* hist_exact = w.hist;
@@ -770,12 +954,12 @@ void compress(const CompressArgs& a, hipStream_t s) {
   const int64_t keff = a.k < a.n ? a.k : a.n;
   if (a.mode == kModeTopK || a.mode == kModeRandomK || a.mode == kModeDGC) {
     hipMemsetAsync(w.hist, 0, sizeof(uint32_t) * 2 * kHistSet, s);
-    if (a.mode == kModeRandomK) launch_radix<kKeyHash>(a.r, a.n, a.seed, 0u, keff, hist_exact, vec_r, s);
-    else launch_radix<kKeyAbs>(a.r, a.n, a.seed, 0u, keff, hist_exact, vec_r, s);
+    if (a.mode == kModeRandomK) launch_radix<kKeyHash>(a.r, a.n, a.seed, 0u, keff, hist_exact, vec_r, a.valid, nullptr, s);
+    else launch_radix<kKeyAbs>(a.r, a.n, a.seed, 0u, keff, hist_exact, vec_r, nullptr, nullptr, s);
     if (a.mode == kModeDGC) {
       double p = a.sample_p * 4294967296.0;
       uint32_t thr = p >= 4294967295.0 ? 0xffffffffu : (uint32_t)p;
-      launch_radix<kKeySample>(a.r, a.n, a.seed, thr, a.k, hist_sample, vec_r, s);
+      launch_radix<kKeySample>(a.r, a.n, a.seed, thr, a.k, hist_sample, vec_r, nullptr, nullptr, s);
     }
   }
 
@@ -789,10 +973,20 @@ void compress(const CompressArgs& a, hipStream_t s) {
   int G = (int)(ntiles < kMaxCountBlocks ? ntiles : kMaxCountBlocks);
   const int64_t chunk_tiles = ceil_div(ntiles, (int64_t)G);
   G = (int)ceil_div(ntiles, chunk_tiles);
-  if (a.mode == kModeRandomK)
-    launch_count_select<kKeyHash>(a, w, vec_r, G, chunk_tiles, ctrl, out_idx, out_val, s);
-  else
-    launch_count_select<kKeyAbs>(a, w, vec_r, G, chunk_tiles, ctrl, out_idx, out_val, s);
+  if (a.mode == kModeRandomK) {
+    launch_count<kKeyHash>(a, w, vec_r, G, chunk_tiles, ctrl, 0, s);
+    launch_select<kKeyHash>(a, w, vec_r, G, chunk_tiles, ctrl, out_idx, out_val, s);
+  } else {
+    launch_count<kKeyAbs>(a, w, vec_r, G, chunk_tiles, ctrl, 0, s);
+    if (a.mode == kModeGaussianCal) {
+      // conditional exact-top-k fallback: every kernel below exits at once
+      // unless the decide above found no candidate in [2k/3, 4k/3]
+      launch_radix<kKeyAbs>(a.r, a.n, a.seed, 0u, keff, hist_exact, vec_r, nullptr, ctrl, s);
+      hipLaunchKernelGGL(cal_fallback_kernel, dim3(1), dim3(kBlock), 0, s, ctrl, hist_exact, keff);
+      launch_count<kKeyAbs>(a, w, vec_r, G, chunk_tiles, ctrl, 1, s);
+    }
+    launch_select<kKeyAbs>(a, w, vec_r, G, chunk_tiles, ctrl, out_idx, out_val, s);
+  }
 }
 
 void tensor_stats(const float* x, int64_t n, void* ctrl, void* ws, hipStream_t s) {

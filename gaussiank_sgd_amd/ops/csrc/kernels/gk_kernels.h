@@ -22,7 +22,13 @@ enum Mode : int {
   kModeRandomK = 4,       // k smallest hashes: a uniformly random k-subset
   kModeThreshold = 5,     // fixed threshold |x| > t
   kModeDGC = 6,           // 1% sample threshold, exact top-k when > 4k/3 (compression.py:555-620)
+  kModeGaussianCal = 7,   // calibrated Gaussian-k: 16-candidate ladder around a per-bucket adaptive
+                          // centre, closest count to k in [2k/3, 4k/3], exact radix top-k otherwise
 };
+
+// Fallback marker written to the record header's `chosen` word when the
+// calibrated mode found no candidate in range and used the exact radix key.
+constexpr int kCalFallback = 16;
 
 constexpr int kMaxCand = 16;
 constexpr int kRecHdr = 4;   // packed record header words: sent, total, chosen, thr
@@ -51,7 +57,15 @@ struct GkCtrl {
   uint32_t radix_key[2];      // [0] sampled (DGC), [1] exact
   int64_t radix_kremain[2];
   double cand_thr[kMaxCand];  // candidate thresholds in |x| units (logging/tests)
+  // calibrated Gaussian-k state, persistent across calls on one bucket
+  double cal_c;         // ladder centre / sigma
+  double cal_step;      // log spacing of the ladder
+  int64_t cal_k;        // k the state was calibrated for (re-initialised when k changes)
+  int32_t fallback;     // this call fell back to the exact radix key
+  int32_t pad1;
 };
+
+struct Chunk;
 
 struct CompressArgs {
   float* g = nullptr;          // raw gradient bucket; zeroed when zero_g
@@ -72,6 +86,21 @@ struct CompressArgs {
   void* ws = nullptr;          // gk_compress_workspace_bytes(n)
   int32_t* record = nullptr;   // [4 + 2*k_cap] int32: hdr | idx | val(fp32 bits)
   float* stats_out = nullptr;  // optional [4] copy of mean, std, meanabs, maxabs (fp32)
+  // optional validity bitmask over the n elements (bit i = 1: real element,
+  // 0: arena padding); hash-key modes (random-k) never pick invalid slots
+  const uint32_t* valid = nullptr;
+  // optional DGC momentum correction fused into the statistics pass:
+  //   u = mu * u + g + wd * w;  acc = u (+ r);  ...  and u[idx] = 0 for every
+  // sent index (momentum factor masking) in the select pass.  The chunk table
+  // rows [chunk_begin, chunk_begin + chunk_count) tile this bucket; their
+  // `start` is an arena offset, `chunk_base` the bucket's arena offset.
+  float* u = nullptr;
+  const float* w = nullptr;
+  const Chunk* chunks = nullptr;
+  int chunk_begin = 0, chunk_count = 0;
+  int64_t chunk_base = 0;
+  float mc_mu[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float mc_wd[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 };
 
 size_t compress_workspace_bytes(int64_t n);
@@ -86,6 +115,15 @@ void tensor_stats(const float* x, int64_t n, void* ctrl, void* ws, hipStream_t s
 // ---------------------------------------------------------------------------
 void scatter_add_records(float* dst, int64_t n, const int32_t* records, int P, int64_t k_cap,
                          float scale, int deterministic, hipStream_t stream);
+// Sparse SGD apply straight from the records (DGC momentum correction: the
+// global update is plain SGD on the aggregate):  w[i] -= lr * (sum_r val_r[i]) * scale
+// for every index in any record, sums in rank order; w_bf16 (optional) is
+// refreshed at the same indices; lr_mult (optional device scalar) multiplies lr.
+void apply_records_sgd(float* w, uint16_t* w_bf16, int64_t n, const int32_t* records, int P, int64_t k_cap,
+                       float scale, float lr, const float* lr_mult, hipStream_t stream);
+// 16-byte digest of a flat fp32 arena (replica consistency checks):
+// out[0] = fp64 sum (bits), out[1] = order-independent 64-bit hash of the bits.
+void arena_digest(const float* x, int64_t n, uint64_t* out, uint64_t* ws, hipStream_t stream);
 void fill_zero(float* dst, int64_t n, hipStream_t stream);
 
 // ---------------------------------------------------------------------------

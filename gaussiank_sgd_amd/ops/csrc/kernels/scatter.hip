@@ -1,17 +1,142 @@
 // Sparse aggregation (K11) and the sign-bucket-mean compressor (K9).
 //
 // Reference aggregation (distributed_optimizer.py:468-482) loops over ranks in
-// Python and index_puts half-chunks, which is wrong for unequal counts (SURVEY
-// 2.3).  Here every rank's packed record {sent, total, chosen, thr | idx[k_cap]
-// | val[k_cap]} is scattered in ONE launch with hardware fp32 atomics
-// (global_atomic_add_f32), the 1/P average folded in; the deterministic mode
-// applies the ranks in order with plain read-modify-writes (indices inside one
-// record are unique, so one launch per rank is race-free and reproducible).
+// Python, index_puts half-chunks (wrong for unequal counts), then
+// divides the sum by P.  Here the P packed records {sent, total, chosen, thr |
+// idx[k_cap] | val[k_cap]} are reduced in ONE launch:
+//
+//   reduce_records (default): every index is owned by the first rank whose
+//     record holds it; the owner sums the P contributions IN RANK ORDER
+//     (fp32, like the reference loop) and applies the 1/P average once to the
+//     sum.  No atomics, so every replica computes bit-identical gradients for
+//     any P and any duplicate pattern.  Records are sorted (the compressor
+//     emits ascending indices): a workgroup takes 1024 consecutive entries of
+//     one rank, finds the matching index window of every other rank with two
+//     binary searches, stages those windows in LDS and resolves each entry
+//     with LDS binary searches.
+//   APPLY variant (DGC momentum correction, where the global update is plain
+//     SGD on the aggregate): w[idx] -= lr * avg and the bf16 shadow weight is
+//     refreshed at idx -- the dense gradient pass of the optimizer disappears.
+//   scatter_atomic: hardware fp32 atomics (global_atomic_add_f32), for the
+//     explicit non-deterministic request only.
 #include "common.h"
 #include "gk_kernels.h"
 
 namespace gk {
 namespace {
+
+constexpr int kRedPer = 4;                       // entries per thread
+constexpr int kRedTile = kBlock * kRedPer;       // entries of the owner rank per workgroup
+constexpr int kRedWin = 1024;                    // LDS window per other rank (int32 indices)
+constexpr int kRedMaxP = 16;                     // ranks staged in LDS; more go through global memory
+
+__device__ __forceinline__ int lower_bound_i32(const int32_t* a, int lo, int hi, int32_t key) {
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (a[mid] < key) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ uint16_t f2bf_rne(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+template <bool APPLY>
+__global__ __launch_bounds__(kBlock) void reduce_records_kernel(float* __restrict__ dst, int64_t n,
+                                                                const int32_t* __restrict__ records, int P,
+                                                                int64_t k_cap, int64_t rec_words, float scale,
+                                                                const float* __restrict__ lr_ptr, float lr,
+                                                                uint16_t* __restrict__ shadow) {
+  // two roundings (product, then sum) exactly as the reference / CPU mirror:
+  // this file is compiled with -ffp-contract=off (ops/build.py), hipcc's
+  // default would fuse them into one FMA
+  __shared__ int32_t win[kRedMaxP][kRedWin];
+  __shared__ int s_lo[kRedMaxP], s_len[kRedMaxP];
+  const int r = blockIdx.y;
+  const int32_t* rec = records + (int64_t)r * rec_words;
+  int64_t cnt = rec[0];
+  if (cnt > k_cap) cnt = k_cap;
+  const int64_t t0 = (int64_t)blockIdx.x * kRedTile;
+  if (t0 >= cnt) return;                                       // block-uniform
+  const int64_t t1 = t0 + kRedTile < cnt ? t0 + kRedTile : cnt;
+  const int32_t* idx = rec + kRecHdr;
+  const float* val = reinterpret_cast<const float*>(rec + kRecHdr + k_cap);
+  const int32_t key_lo = idx[t0], key_hi = idx[t1 - 1];
+  // window [lo, lo+len) of every other rank holding keys in [key_lo, key_hi]
+  if (threadIdx.x < P && threadIdx.x < kRedMaxP) {
+    const int q = threadIdx.x;
+    const int32_t* rq = records + (int64_t)q * rec_words;
+    int cq = rq[0];
+    if (cq > k_cap) cq = (int)k_cap;
+    const int lo = lower_bound_i32(rq + kRecHdr, 0, cq, key_lo);
+    const int hi = lower_bound_i32(rq + kRecHdr, lo, cq, key_hi + 1);
+    s_lo[q] = lo;
+    s_len[q] = hi - lo;
+  }
+  __syncthreads();
+  const int Ps = P < kRedMaxP ? P : kRedMaxP;
+  for (int q = 0; q < Ps; ++q) {
+    if (q == r || s_len[q] > kRedWin) continue;
+    const int32_t* src = records + (int64_t)q * rec_words + kRecHdr + s_lo[q];
+    for (int i = threadIdx.x; i < s_len[q]; i += kBlock) win[q][i] = src[i];
+  }
+  __syncthreads();
+  const float lr_eff = APPLY ? (lr_ptr ? lr * *lr_ptr : lr) : 0.f;
+#pragma unroll
+  for (int e = 0; e < kRedPer; ++e) {
+    const int64_t j = t0 + (int64_t)e * kBlock + threadIdx.x;
+    if (j >= t1) continue;
+    const int32_t key = idx[j];
+    bool owner = true;
+    float s = 0.f;
+    for (int q = 0; q < P && owner; ++q) {
+      float v = 0.f;
+      if (q == r) {
+        v = val[j];
+      } else {
+        const int32_t* rq = records + (int64_t)q * rec_words;
+        int pos, len, lo;
+        bool hit;
+        if (q < kRedMaxP) {
+          lo = s_lo[q];
+          len = s_len[q];
+          if (len <= kRedWin) {
+            pos = lower_bound_i32(win[q], 0, len, key);
+            hit = pos < len && win[q][pos] == key;
+          } else {
+            pos = lower_bound_i32(rq + kRecHdr + lo, 0, len, key);
+            hit = pos < len && rq[kRecHdr + lo + pos] == key;
+          }
+        } else {
+          int cq = rq[0];
+          if (cq > k_cap) cq = (int)k_cap;
+          lo = 0;
+          len = cq;
+          pos = lower_bound_i32(rq + kRecHdr, 0, len, key);
+          hit = pos < len && rq[kRecHdr + pos] == key;
+        }
+        if (hit) {
+          if (q < r) owner = false;                      // an earlier rank owns this index
+          else v = reinterpret_cast<const float*>(rq + kRecHdr + k_cap)[lo + pos];
+        }
+      }
+      s = s + v;                                         // rank order: ((0 + v0) + v1) + ...
+    }
+    if (!owner || key < 0 || key >= n) continue;
+    const float avg = s * scale;
+    if (APPLY) {
+      const float wn = dst[key] - lr_eff * avg;
+      dst[key] = wn;
+      if (shadow) shadow[key] = f2bf_rne(wn);
+    } else {
+      dst[key] = dst[key] + avg;
+    }
+  }
+}
 
 __global__ __launch_bounds__(kBlock) void scatter_atomic_kernel(float* __restrict__ dst, int64_t n,
                                                                 const int32_t* __restrict__ records, int64_t k_cap,
@@ -113,6 +238,53 @@ __global__ __launch_bounds__(kBlock) void sign_apply_kernel(float* __restrict__ 
   }
 }
 
+// ---- replica digest ----------------------------------------------------------
+// fp64 sum (fixed reduction tree -> reproducible) and a wrapping 64-bit sum of
+// a position-keyed mix of every element's bits (order-independent, so exact).
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(kBlock) void digest_partial_kernel(const float* __restrict__ x, int64_t n,
+                                                                uint64_t* __restrict__ part) {
+  double s = 0.0;
+  uint64_t h = 0;
+  const int64_t tid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = tid; i < n; i += stride) {
+    const float v = x[i];
+    s += (double)v;
+    h += mix64(((uint64_t)__float_as_uint(v) << 32) ^ (uint64_t)i * 0x9e3779b97f4a7c15ull);
+  }
+  __shared__ double sh[kWavesPerBlock];
+  __shared__ uint64_t shh[kWavesPerBlock];
+  s = block_sum(s, sh);
+  h = wave_sum(h);
+  if (lane_id() == 0) shh[wave_id()] = h;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (int w = 0; w < kWavesPerBlock; ++w) t += shh[w];
+    part[2 * blockIdx.x] = (uint64_t)__double_as_longlong(s);
+    part[2 * blockIdx.x + 1] = t;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void digest_final_kernel(const uint64_t* __restrict__ part, int G,
+                                                              uint64_t* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  double s = 0.0;
+  uint64_t h = 0;
+  for (int b = 0; b < G; ++b) {
+    s += __longlong_as_double((long long)part[2 * b]);
+    h += part[2 * b + 1];
+  }
+  out[0] = (uint64_t)__double_as_longlong(s);
+  out[1] = h;
+}
+
 int grid_for(int64_t n, int cap) {
   int64_t g = ceil_div(n, (int64_t)kBlock * 8);
   if (g < 1) g = 1;
@@ -125,17 +297,36 @@ int grid_for(int64_t n, int cap) {
 void scatter_add_records(float* dst, int64_t n, const int32_t* records, int P, int64_t k_cap, float scale,
                          int deterministic, hipStream_t s) {
   const int64_t rec_words = 4 + 2 * k_cap;
-  int gx = (int)ceil_div(k_cap, (int64_t)kBlock);
-  if (gx < 1) gx = 1;
-  if (gx > 1024) gx = 1024;
-  if (deterministic) {
-    for (int r = 0; r < P; ++r)
-      hipLaunchKernelGGL(scatter_rank_kernel, dim3(gx), dim3(kBlock), 0, s, dst, n, records + (int64_t)r * rec_words,
-                         k_cap, scale);
+  if (P == 1) {  // one record: indices are unique, a plain scatter is already deterministic
+    int gx = (int)ceil_div(k_cap, (int64_t)kBlock);
+    if (gx < 1) gx = 1;
+    if (gx > 1024) gx = 1024;
+    hipLaunchKernelGGL(scatter_rank_kernel, dim3(gx), dim3(kBlock), 0, s, dst, n, records, k_cap, scale);
+  } else if (deterministic) {
+    const int gx = (int)ceil_div(k_cap, (int64_t)kRedTile);
+    hipLaunchKernelGGL((reduce_records_kernel<false>), dim3(gx < 1 ? 1 : gx, P), dim3(kBlock), 0, s, dst, n, records,
+                       P, k_cap, rec_words, scale, (const float*)nullptr, 0.f, (uint16_t*)nullptr);
   } else {
+    int gx = (int)ceil_div(k_cap, (int64_t)kBlock);
+    if (gx < 1) gx = 1;
+    if (gx > 1024) gx = 1024;
     hipLaunchKernelGGL(scatter_atomic_kernel, dim3(gx, P), dim3(kBlock), 0, s, dst, n, records, k_cap, rec_words,
                        scale);
   }
+}
+
+void apply_records_sgd(float* w, uint16_t* w_bf16, int64_t n, const int32_t* records, int P, int64_t k_cap,
+                       float scale, float lr, const float* lr_mult, hipStream_t s) {
+  const int64_t rec_words = 4 + 2 * k_cap;
+  const int gx = (int)ceil_div(k_cap, (int64_t)kRedTile);
+  hipLaunchKernelGGL((reduce_records_kernel<true>), dim3(gx < 1 ? 1 : gx, P), dim3(kBlock), 0, s, w, n, records, P,
+                     k_cap, rec_words, scale, lr_mult, lr, w_bf16);
+}
+
+void arena_digest(const float* x, int64_t n, uint64_t* out, uint64_t* ws, hipStream_t s) {
+  const int G = grid_for(n, 1024);
+  hipLaunchKernelGGL(digest_partial_kernel, dim3(G), dim3(kBlock), 0, s, x, n, ws);
+  hipLaunchKernelGGL(digest_final_kernel, dim3(1), dim3(64), 0, s, ws, G, out);
 }
 
 void fill_zero(float* dst, int64_t n, hipStream_t s) {

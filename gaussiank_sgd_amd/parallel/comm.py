@@ -334,12 +334,32 @@ def broadcast_object(obj: Any, root: int = 0) -> Any:
 
 
 # storage data_ptr -> callbacks run after a broadcast overwrote that storage
-# (the bf16 shadow arena re-casts itself from the fp32 weight arena).
+# (the bf16 shadow arena re-casts itself from the fp32 weight arena).  Bound
+# methods are held weakly: a registered optimizer (and its arenas) can still be
+# garbage-collected.
 _storage_listeners: Dict[int, List] = {}
 
 
 def on_storage_overwritten(ptr: int, fn) -> None:
-    _storage_listeners.setdefault(int(ptr), []).append(fn)
+    import weakref
+    ref = weakref.WeakMethod(fn) if hasattr(fn, "__self__") else (lambda f=fn: f)
+    lst = [r for r in _storage_listeners.get(int(ptr), []) if r() is not None]
+    lst.append(ref)
+    _storage_listeners[int(ptr)] = lst
+
+
+def _notify_storage(ptr: int) -> None:
+    live = []
+    for ref in _storage_listeners.get(ptr, ()):
+        fn = ref()
+        if fn is not None:
+            fn()
+            live.append(ref)
+    if ptr in _storage_listeners:
+        if live:
+            _storage_listeners[ptr] = live
+        else:
+            del _storage_listeners[ptr]
 
 
 def broadcast_parameters(params, root_rank: int = 0) -> None:
@@ -378,8 +398,7 @@ def broadcast_parameters(params, root_rank: int = 0) -> None:
     for h in handles:
         synchronize(h)
     for ptr, _ in seen:
-        for fn in _storage_listeners.get(ptr, ()):
-            fn()
+        _notify_storage(ptr)
 
 
 def broadcast_optimizer_state(optimizer: torch.optim.Optimizer, root_rank: int = 0) -> None:
@@ -425,6 +444,11 @@ class RcclCommunicator:
         uid_t = torch.tensor(uid_list, dtype=torch.uint8)
         self.engine.init(uid_t, self.rank, self.world, self.device.index or 0)
         self.self_test()
+        # hang / async-error watchdog: aborts the communicator instead of
+        # letting a dead peer hang the GPU; the next hot-path call raises
+        wd = float(os.environ.get("GKSGD_RCCL_WATCHDOG_S", "600"))
+        if wd > 0:
+            self.engine.start_watchdog(wd, 5.0)
 
     def self_test(self) -> None:
         """One all-gather of the rank ids on the current stream, checked on the
@@ -442,6 +466,23 @@ class RcclCommunicator:
     def allgather_(self, out: torch.Tensor, inp: torch.Tensor) -> None:
         self.engine.allgather(inp, out)
 
+    def allgather_many_(self, outs: List[torch.Tensor], inps: List[torch.Tensor]) -> None:
+        self.engine.allgather_many(inps, outs)
+
+    def check(self) -> None:
+        self.engine.check()
+
+    def stats(self) -> Dict[str, Dict[str, float]]:
+        """Event-timed per-op statistics of the completed collectives."""
+        self.engine.poll()
+        out = {}
+        for i, name in enumerate(("allgather", "allreduce", "broadcast", "allgather_grouped")):
+            calls, nbytes, ms, mx = self.engine.stats(i)
+            if calls:
+                out[name] = {"calls": int(calls), "bytes_per_call": nbytes / calls, "us_mean": 1e3 * ms / calls,
+                             "us_max": 1e3 * mx}
+        return out
+
     def allreduce_(self, t: torch.Tensor, average: bool = True) -> None:
         self.engine.allreduce(t, 1 if average else 0)
 
@@ -449,6 +490,7 @@ class RcclCommunicator:
         self.engine.broadcast(t, root)
 
     def destroy(self) -> None:
+        self.engine.stop_watchdog()
         self.engine.destroy()
 
 
@@ -509,6 +551,21 @@ class Exchanger:
         else:
             with self._bound():
                 allgather_into_(out, inp, async_op=False)
+
+    def allgather_many_(self, outs: List[torch.Tensor], inps: List[torch.Tensor]) -> None:
+        """Several fixed-size all-gathers; one grouped RCCL launch on the native engine."""
+        if self.native is not None:
+            self.native.allgather_many_(outs, inps)
+        else:
+            for o, i in zip(outs, inps):
+                self.allgather_(o, i)
+
+    def check(self) -> None:
+        if self.native is not None:
+            self.native.check()
+
+    def stats(self) -> Dict[str, Dict[str, float]]:
+        return self.native.stats() if self.native is not None else {}
 
     def allreduce_(self, t: torch.Tensor, average: bool = True) -> None:
         if self.kind == "local":

@@ -31,6 +31,7 @@ MI355X execution model (what is different, and why):
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 import time
@@ -42,6 +43,7 @@ import torch
 from .. import ops, settings
 from ..settings import logger
 from ..utils import stats as perf
+from ..utils import trace
 from . import comm
 from .buckets import GradArena, group_with_threshold
 from .comm import (allgather, allgather_async, allreduce, allreduce_, allreduce_async_, barrier,  # noqa: F401
@@ -108,6 +110,12 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         # (set by train/graph.py so a captured step follows the lr schedule)
         self._lr_mult: Optional[torch.Tensor] = None
         self._mc_applied = False
+        # Under momentum correction the global update is plain SGD on the
+        # aggregate: apply it straight from the gathered records (no dense
+        # gradient scatter, no dense optimizer pass) unless something needs the
+        # dense aggregate (clip_grad_norm_, aggregated_grads()).
+        self._sparse_apply_opt = bool(opts.get("sparse_apply", _env_flag("GKSGD_SPARSE_APPLY", True)))
+        self._pending_apply = False
         self._base_cls = opts.get("base_cls", None)
         self._state_dirty = False
 
@@ -234,11 +242,16 @@ class _DistributedOptimizer(torch.optim.Optimizer):
                 kcap_max = comp.k_cap_for(kmax, b.numel)
                 b.bufs = ops.CompressBuffers(kcap_max, dev)
                 b.gathered = torch.zeros(P * (ops.REC_HDR + 2 * kcap_max), dtype=torch.int32, device=dev)
+                if getattr(comp, "mode", None) == ops.MODE_RANDOMK:
+                    # random-k must never pick the arena's padding slots
+                    layout = [(o, self._named_parameters[k].numel()) for k, o in zip(b.keys, b.offsets)]
+                    b.extra["valid"] = ops.valid_bitmask(layout, b.span, dev)
             elif getattr(comp, "name", None) == "bucket":
                 b.extra["mask"] = torch.zeros(b.span, dtype=torch.uint8, device=dev)
                 b.extra["means"] = torch.zeros(2, dtype=torch.float32, device=dev)
                 b.extra["ws"] = ops.sign_bucket_ws(dev)
         self._sel_dev = torch.zeros(8192, dtype=torch.int32, device=dev)
+        self._sel_host: List[int] = []
 
     # ------------------------------------------------------------------
     # hooks
@@ -319,9 +332,10 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         self._selected_num_gradients = []
 
     def _collect_selected(self) -> List[int]:
-        n = min(self._sel_n, self._sel_dev.numel())
+        n = self._sel_n
         out = [int(x) for x in self._sel_dev[:n].cpu().tolist()] if n else []
-        out = self._selected_num_gradients + out
+        out = self._selected_num_gradients + self._sel_host + out
+        self._sel_host = []
         self._sel_n = 0
         return out
 
@@ -346,16 +360,17 @@ class _DistributedOptimizer(torch.optim.Optimizer):
     # ------------------------------------------------------------------
     def _launch_bucket(self, b):
         b.launched = True
-        if self._comm_stream is not None:
-            cur = torch.cuda.current_stream(self._device)
-            ev = b.extra["ready_event"]
-            ev.record(cur)
-            self._comm_stream.wait_event(ev)
-            with torch.cuda.stream(self._comm_stream):
+        with trace.range("gk/b%d/launch" % b.index):
+            if self._comm_stream is not None:
+                cur = torch.cuda.current_stream(self._device)
+                ev = b.extra["ready_event"]
+                ev.record(cur)
+                self._comm_stream.wait_event(ev)
+                with torch.cuda.stream(self._comm_stream):
+                    self._process_bucket(b)
+                    b.done_event.record(self._comm_stream)
+            else:
                 self._process_bucket(b)
-                b.done_event.record(self._comm_stream)
-        else:
-            self._process_bucket(b)
 
     def _timer(self):
         if not self._profiling:
@@ -388,51 +403,103 @@ class _DistributedOptimizer(torch.optim.Optimizer):
             self._dense(b, g, t0)
 
     def _sparse_fused(self, b, g, density, t0):
-        comp = self._compression
-        k = comp.k_of(b.numel, density)
-        k_cap = min(comp.k_cap_for(k, b.numel), b.bufs.k_cap)
-        r = b.slice(self._arena.residuals)
-        seed = comp.next_seed(self._rank)
-        arena = self._arena
-        if self._mc:
-            begin, count = self._bucket_chunks[b.index]
-            ops.momentum_correct_(arena.velocity, arena.grads, arena.weights, self._chunks, begin, count,
-                                  self.param_groups, self._chunk_list)
-            self._mc_applied = True
-        ops.compress_(g, r, b.bufs, comp.mode, ec=comp.ec, zero_g=True, loops=comp.loops, z=comp.z_for(density),
-                      k=k, k_cap=k_cap, seed=seed, sample_p=getattr(comp, "sample_p", 0.01), n_stats=b.numel)
-        rec_words = ops.REC_HDR + 2 * k_cap
-        rec = b.bufs.record[:rec_words]
-        if self._mc:
-            ops.mask_records_(b.slice(arena.velocity), rec, k_cap)  # momentum factor masking
+        rec, k_cap = self._compress_bucket(b, g, density)
         t1 = self._timer()
-        if self._world > 1:
-            gathered = b.gathered[: self._world * rec_words]
-            self._exchanger.allgather_(gathered, rec)
-        else:
-            gathered = rec
+        gathered = self._exchange_records([b], [rec], [k_cap])[0]
         t2 = self._timer()
-        # Rank-ordered (deterministic) scatter for P > 2: with three or more
-        # contributions to one index, fp32 atomics sum in a run-dependent order,
-        # and the model replicas would drift apart by rounding (the reference's
-        # Python loop adds ranks in order, distributed_optimizer.py:468-482).
-        # With P <= 2 the atomic sum 0 + a + b is order-independent.
-        ops.scatter_add_records_(g, gathered, max(self._world, 1), k_cap, 1.0 / max(self._world, 1),
-                                 self._deterministic or self._world > 2)
-        self._log_selected(b.bufs.record[1:2])
-        if settings.LOGGING_GRADIENTS and self._rank == 0 and self._gradient_path and \
-                self.train_iter % max(1, settings.DUMP_GRAD_EVERY) == 0:
-            self._queue_dump(b, r, rec, k_cap)
+        self._finish_bucket(b, g, gathered, rec, k_cap)
         t3 = self._timer()
         if self._profiling:
             self._pending_timers = getattr(self, "_pending_timers", [])
             self._pending_timers.append((b.name, t0, t1, t2, t3))
 
+    def _compress_bucket(self, b, g, density):
+        """Fused HIP compression of one bucket into its fixed-size send record."""
+        comp = self._compression
+        k = comp.k_of(b.numel, density)
+        k_cap = min(comp.k_cap_for(k, b.numel), b.bufs.k_cap)
+        r = b.slice(self._arena.residuals)
+        # stateless seed: (iteration, bucket, rank) -- identical across ranks for *same* variants
+        seed = comp.seed_for(self.train_iter, b.index, self._rank)
+        arena = self._arena
+        mc = None
+        if self._mc:
+            # DGC momentum correction fused into the compressor's statistics pass;
+            # momentum factor masking happens in its select pass
+            begin, count = self._bucket_chunks[b.index]
+            mc = {"u": b.slice(arena.velocity), "w": b.slice(arena.weights), "chunks": self._chunks, "begin": begin,
+                  "count": count, "base": b.start, "groups": self.param_groups, "chunk_list": self._chunk_list}
+            self._mc_applied = True
+        with trace.range("gk/b%d/compress" % b.index):
+            ops.compress_(g, r, b.bufs, comp.mode, ec=comp.ec, zero_g=True, loops=comp.loops,
+                          z=comp.z_for(density), k=k, k_cap=k_cap, seed=seed, sample_p=getattr(comp, "sample_p", 0.01),
+                          n_stats=b.numel, valid=b.extra.get("valid"), mc=mc)
+        rec_words = ops.REC_HDR + 2 * k_cap
+        return b.bufs.record[:rec_words], k_cap
+
+    def _exchange_records(self, bs, recs, k_caps):
+        """All-gather the records of one or more buckets (one grouped RCCL launch)."""
+        if self._world <= 1:
+            return list(recs)
+        outs = [b.gathered[: self._world * (ops.REC_HDR + 2 * kc)] for b, kc in zip(bs, k_caps)]
+        with trace.range("gk/allgather/%s" % ",".join("b%d" % b.index for b in bs)):
+            if len(bs) == 1:
+                self._exchanger.allgather_(outs[0], recs[0])
+            else:
+                self._exchanger.allgather_many_(outs, list(recs))
+        return outs
+
+    def _finish_bucket(self, b, g, gathered, rec, k_cap):
+        b.extra["agg"] = (gathered, max(self._world, 1), k_cap)
+        if self._mc and self._sparse_apply_ok():
+            # the update is applied from the records in step() (after backward:
+            # the weights it writes are still read by the rest of backward)
+            self._pending_apply = True
+        else:
+            # One deterministic launch: every index is summed over ranks in rank
+            # order and averaged once (reference loop + division,
+            # distributed_optimizer.py:468-482), so all replicas compute
+            # bit-identical aggregates for any P.
+            with trace.range("gk/b%d/decompress" % b.index):
+                ops.scatter_add_records_(g, gathered, max(self._world, 1), k_cap, 1.0 / max(self._world, 1), True)
+            b.extra["agg_done"] = True
+        self._log_selected(b.bufs.record[1:2])
+        if settings.LOGGING_GRADIENTS and self._rank == 0 and self._gradient_path and \
+                self.train_iter % max(1, settings.DUMP_GRAD_EVERY) == 0:
+            self._queue_dump(b, b.slice(self._arena.residuals), rec, k_cap)
+
+    def _launch_group(self, bs):
+        """Several due buckets at once (synchronize() without overlap): compress
+        each, ONE grouped all-gather of all records, then finish each -- one
+        collective launch instead of len(bs)."""
+        for b in bs:
+            b.launched = True
+        cur = torch.cuda.current_stream(self._device) if self._comm_stream is not None else None
+        ctx = torch.cuda.stream(self._comm_stream) if self._comm_stream is not None else contextlib.nullcontext()
+        if cur is not None:
+            ev = bs[0].extra["ready_event"]
+            ev.record(cur)
+            self._comm_stream.wait_event(ev)
+        with ctx, trace.range("gk/group/%d" % len(bs)):
+            parts = []
+            for b in bs:
+                g = b.slice(self._arena.grads)
+                rec, kc = self._compress_bucket(b, g, self.get_current_density(b.name))
+                parts.append((b, g, rec, kc))
+            outs = self._exchange_records([p[0] for p in parts], [p[2] for p in parts], [p[3] for p in parts])
+            for (b, g, rec, kc), out in zip(parts, outs):
+                self._finish_bucket(b, g, out, rec, kc)
+            if self._comm_stream is not None:
+                for b in bs:
+                    b.done_event.record(self._comm_stream)
+
     def _sparse_generic(self, b, g, density, t0):
         """Reference-semantics path for compressors without a fused spec (host syncs)."""
         comp = self._compression
         flat = g
-        tensor, ctx, values = comp.compress(flat, b.name, ratio=density)
+        # residuals are per rank: qualify the group name so the virtual ranks of
+        # an in-process world never share (and corrupt) one residual
+        tensor, ctx, values = comp.compress(flat, "%s@rank%d" % (b.name, self._rank), ratio=density)
         self._selected_num_gradients.append(int(ctx.numel()))
         if settings.LOGGING_GRADIENTS and self._rank == 0 and self._gradient_path:
             np.save("%s/r%d_gradients_iter_%d" % (self._gradient_path, self._rank, self.train_iter),
@@ -440,9 +507,18 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         t1 = self._timer()
         all_vals = allgather(values)
         all_idx = allgather(ctx.int())
+        counts = allgather(torch.tensor([int(ctx.numel())], dtype=torch.int64, device=flat.device))
         t2 = self._timer()
         flat.zero_()
-        flat.index_add_(0, all_idx.long(), all_vals)
+        # rank order, then one division (reference :468-482): fp32 atomics from
+        # several ranks would let the replicas drift apart
+        # (indices are unique inside one rank's chunk: one add per index per launch)
+        pos = 0
+        for c in counts.view(-1).tolist():
+            c = int(c)
+            if c:
+                flat.index_add_(0, all_idx[pos:pos + c].long(), all_vals[pos:pos + c])
+            pos += c
         flat.div_(max(self._world, 1))
         t3 = self._timer()
         if self._profiling:
@@ -477,8 +553,12 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         self._exchanger.allreduce_(t, average=True)
 
     def _log_selected(self, hdr_total: torch.Tensor):
-        i = self._sel_n % self._sel_dev.numel()
-        self._sel_dev[i:i + 1].copy_(hdr_total, non_blocking=True)
+        if self._sel_n == self._sel_dev.numel():
+            # ring full (long epochs x many buckets): flush to the host -- one
+            # sync per 8192 bucket-steps, nothing is overwritten
+            self._sel_host.extend(int(x) for x in self._sel_dev.cpu().tolist())
+            self._sel_n = 0
+        self._sel_dev[self._sel_n:self._sel_n + 1].copy_(hdr_total, non_blocking=True)
         self._sel_n += 1
 
     def _queue_dump(self, b, r, rec, k_cap):
@@ -515,13 +595,20 @@ class _DistributedOptimizer(torch.optim.Optimizer):
     # synchronize / step
     # ------------------------------------------------------------------
     def synchronize(self):
+        with trace.range("gk/synchronize"):
+            self._synchronize()
+
+    def _synchronize(self):
         if self._hooks_on:
             any_ready = False
-            for b in self._arena.buckets:
-                if not b.launched and b.ready > 0:
+            due = [b for b in self._arena.buckets if not b.launched and b.ready > 0]
+            if len(due) > 1 and self._fused_sparse and self._sparse and not self._profiling and \
+                    all(self.get_current_density(b.name) < 1 for b in due):
+                self._launch_group(due)
+            else:
+                for b in due:
                     self._launch_bucket(b)
-                if b.launched:
-                    any_ready = True
+            any_ready = any(b.launched for b in self._arena.buckets)
             if self._comm_stream is not None and any_ready:
                 cur = torch.cuda.current_stream(self._device)
                 for b in self._arena.buckets:
@@ -530,6 +617,7 @@ class _DistributedOptimizer(torch.optim.Optimizer):
             for b in self._arena.buckets:
                 b.ready = 0
                 b.launched = False
+                b.extra["agg_done"] = False if self._pending_apply else True
             if any_ready:
                 self.train_iter += 1
             self._flush_dumps()
@@ -560,7 +648,35 @@ class _DistributedOptimizer(torch.optim.Optimizer):
 
     def clip_grad_norm_(self, max_norm: float) -> torch.Tensor:
         """Global-norm clip over the gradient arena on device (no host sync)."""
+        self._materialize()
         return ops.clip_grad_norm_(self._arena.grads, max_norm)
+
+    def aggregated_grads(self) -> torch.Tensor:
+        """The averaged gradient arena (``p.grad`` views) after ``synchronize()``.
+
+        Under momentum correction with sparse apply the aggregate normally
+        stays in the gathered records; this scatters it into the arena (and
+        the following ``step()`` then runs the dense update)."""
+        self._materialize()
+        return self._arena.grads
+
+    def _sparse_apply_ok(self) -> bool:
+        if not (self._sparse_apply_opt and self._fused_kind == "sgd"):
+            return False
+        lrs = {float(g["lr"]) for g in self.param_groups}
+        return len(lrs) == 1
+
+    def _materialize(self) -> None:
+        if not self._pending_apply:
+            return
+        with torch.no_grad():
+            for b in self._arena.buckets:
+                agg = b.extra.get("agg")
+                if agg is not None and not b.extra.get("agg_done", False):
+                    gathered, P, k_cap = agg
+                    ops.scatter_add_records_(b.slice(self._arena.grads), gathered, P, k_cap, 1.0 / P, True)
+                    b.extra["agg_done"] = True
+        self._pending_apply = False
 
     def _setup_fused_update(self):
         self._fused_kind = None
@@ -653,7 +769,24 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         if not self._mc_applied and (self._state_dirty or arena.momentum is None):
             self._adopt_state()
         arena.reattach()
-        if self._fused_kind == "sgd" and self._mc_applied:
+        if self._fused_kind == "sgd" and self._mc_applied and self._pending_apply:
+            # momentum + weight decay were applied locally before sparsification
+            # and the aggregate is still in the records: sparse SGD straight from
+            # them (w[idx] -= lr * avg; bf16 shadow refreshed at idx).  The
+            # gradient arena was zeroed by the compressor and stays zero.
+            lr = float(self.param_groups[0]["lr"])
+            shadow = getattr(arena, "shadow", None)
+            for b in arena.buckets:
+                agg = b.extra.get("agg")
+                if agg is None or b.extra.get("agg_done", False):
+                    continue
+                gathered, P, k_cap = agg
+                ops.apply_records_sgd_(b.slice(arena.weights), b.slice(shadow) if shadow is not None else None,
+                                       gathered, P, k_cap, 1.0 / P, lr, self._lr_mult)
+                b.extra["agg_done"] = True
+            self._pending_apply = False
+            self._mc_applied = False
+        elif self._fused_kind == "sgd" and self._mc_applied:
             # momentum + weight decay were applied locally before sparsification
             groups = [{"lr": g["lr"], "momentum": 0.0, "dampening": 0.0, "weight_decay": 0.0, "nesterov": False,
                        "first_step": False} for g in self.param_groups]
@@ -695,6 +828,8 @@ class _DistributedOptimizer(torch.optim.Optimizer):
     def step(self, closure=None):
         if self._watchdog is not None:
             self._watchdog.kick()
+        if self._exchanger is not None:
+            self._exchanger.check()   # native engine: raise if its watchdog aborted a hung collective
         if not self.local:
             self.synchronize()
         if self._fused_kind is not None:
@@ -702,7 +837,7 @@ class _DistributedOptimizer(torch.optim.Optimizer):
             if closure is not None:
                 with torch.enable_grad():
                     loss = closure()
-            with torch.no_grad():
+            with torch.no_grad(), trace.range("gk/update"):
                 self._fused_step()
             return loss
         self._grads_zero = False

@@ -160,6 +160,7 @@ def models_for(P: int, density: float, preset: str = "mi355x"):
         alpha, beta = REFERENCE_ALPHA_BETA[k]
         return ((lambda b: perf.predict_allreduce_time_with_size(alpha, beta, b, P)), alpha,
                 (lambda n: perf.topk_perf_model(n)), (lambda n: perf.allgather_perf_model(n, max(P, 2), density)))
-    a = perf._nearest(perf.XGMI_ALLREDUCE, P)[0]
+    from ..utils import perf_model
+    a = perf_model.collective_ab("allreduce", max(P, 2))[0]
     return ((lambda b: perf.allreduce_perf_model_xgmi(b, P)), a, (lambda n: perf.compress_perf_model_mi355x(n)),
             (lambda n: perf.allgather_perf_model_xgmi(n, P, density)))

@@ -32,6 +32,7 @@ from ..data import DATASETS, SyntheticData
 from ..models import MaskedLMLoss, create_net, repackage_hidden
 from ..optim import sgd_param_groups
 from ..settings import logger
+from ..utils import trace
 from . import schedules
 
 _support_datasets = ["imagenet", "cifar10", "an4", "ptb", "mnist", "mnist32", "wikipedia"]
@@ -294,10 +295,12 @@ class DLTrainer:
                 labels = labels.to(self.device, non_blocking=True) if torch.is_tensor(labels) else labels
             self.iotime += time.time() - ss
             sf = time.time()
-            outputs, loss, hidden = self.forward_loss(inputs, labels, hidden)
+            with trace.range("gk/forward"):
+                outputs, loss, hidden = self.forward_loss(inputs, labels, hidden)
             self.forwardtime += time.time() - sf
             sb = time.time()
-            loss.backward()
+            with trace.range("gk/backward"):
+                loss.backward()
             self.backwardtime += time.time() - sb
             ld = loss.detach()
             loss_sum = ld if loss_sum is None else loss_sum + ld
@@ -385,11 +388,12 @@ class DLTrainer:
 
     def save_epoch_checkpoint(self):
         from ..utils.checkpoint import save_checkpoint
-        has_residuals = "compression" in self.checkpoint_state() and self.size > 1
+        # residuals / velocities are per rank: every rank saves when it has them
+        has_residuals = hasattr(self.optimizer, "compression_state") and self.size > 1
         if self.rank != 0 and not has_residuals:
             return None
         fn = os.path.join(self.checkpoint_dir(), "%s-rank%d-epoch%d.pth" % (self.dnn, self.rank, self.train_epoch))
-        save_checkpoint(self.checkpoint_state(), fn)
+        save_checkpoint(self.checkpoint_state(), fn)   # one D2H of the state
         return fn
 
     def save_checkpoint(self, state, filename):

@@ -9,7 +9,9 @@ a HIP event on the current stream instead (no device-wide sync inside
 backward), and the event deltas are read once after the pass.
 
 ``PhaseTimer`` measures named phases with HIP events (GPU) or wall clock
-(CPU) and emits roctx ranges (visible in rocprofv3 / omnitrace traces).
+(CPU) and emits roctx ranges through ``utils/trace.py`` (visible in
+rocprofv3 --marker-trace / omnitrace); the trainer times forward / backward /
+update with it when ``DLTrainer(phase_timer=True)``.
 """
 from __future__ import annotations
 
@@ -20,6 +22,8 @@ from typing import Dict, List, Tuple
 
 import numpy as np
 import torch
+
+from . import trace
 
 
 class Profiling:
@@ -122,15 +126,15 @@ class PhaseTimer:
 
     def __init__(self, cuda: bool = True, roctx: bool = True):
         self.cuda = cuda and torch.cuda.is_available()
-        self.roctx = roctx and self.cuda
+        if roctx:
+            trace.enable(True)
         self._pending: List[Tuple[str, object, object]] = []
         self.totals: Dict[str, float] = defaultdict(float)
         self.counts: Dict[str, int] = defaultdict(int)
 
     @contextlib.contextmanager
     def __call__(self, name: str):
-        if self.roctx:
-            torch.cuda.nvtx.range_push(name)
+        trace.push(name)
         if self.cuda:
             a = torch.cuda.Event(enable_timing=True)
             a.record()
@@ -146,8 +150,7 @@ class PhaseTimer:
             else:
                 self.totals[name] += time.time() - a
                 self.counts[name] += 1
-            if self.roctx:
-                torch.cuda.nvtx.range_pop()
+            trace.pop()
 
     def flush(self) -> Dict[str, float]:
         if self._pending:

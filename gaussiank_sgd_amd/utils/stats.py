@@ -104,14 +104,9 @@ GbE_multi_p_ab_small = {2: (1.6e-3, 1.0e-8), 4: (2.7e-3, 1.3e-8), 8: (4.0e-3, 1.
 GbE_multi_p_ab_large = {2: (4.4e-3, 5.8e-9), 4: (5.6e-3, 7.4e-9), 8: (7.68e-3, 8.2e-9), 16: (2.1e-3, 1.7e-8)}
 tenGbE_multi_p_ab = {2: (1.5e-5, 5.7e-11), 4: (3.6e-5, 1.1e-10), 8: (8.5e-5, 1.4e-10), 16: (1.4e-4, 2.0e-10)}
 
-# MI355X defaults (fitted from measurements; override with GKSGD_PERF_MODEL=<json>)
-# compress: t = c0 + c1*n   (HIP stats/count/select pipeline, HBM-bound)
-MI355X_COMPRESS = (12e-6, 1.0e-12 * 4 * 5)       # ~5 passes over n fp32 at ~5 TB/s
-# xGMI all-gather / all-reduce alpha-beta per world size (latency, s/byte)
-XGMI_ALLGATHER = {1: (0.0, 0.0), 2: (15e-6, 1 / 100e9), 4: (20e-6, 1 / 100e9), 8: (25e-6, 1 / 100e9)}
-XGMI_ALLREDUCE = {1: (0.0, 0.0), 2: (20e-6, 2 / 130e9), 4: (30e-6, 2 / 130e9), 8: (40e-6, 2 / 130e9)}
-
-
+# MI355X models: constants with provenance live in tuning/perf_model_mi355x.json
+# (utils/perf_model.py; measured entries are flagged, unmeasured ones are
+# labelled as defaults there).  Kept as functions so a re-fit file is picked up.
 def _nearest(table: Dict[int, Tuple[float, float]], P: int) -> Tuple[float, float]:
     if P in table:
         return table[P]
@@ -140,24 +135,30 @@ def allgather_perf_model(x: float, P: int, density: float = 0.001, eth: str = "G
 
 
 def compress_perf_model_mi355x(x: float) -> float:
+    """Fused compression pipeline time for a bucket of x gradients."""
     if x == 0:
         return 0.0
-    c0, c1 = MI355X_COMPRESS
+    from . import perf_model
+    c0, c1 = perf_model.compress_coeffs()
     return c0 + c1 * x
 
 
-def allgather_perf_model_xgmi(x: float, P: int, density: float = 0.001) -> float:
-    if x == 0:
+def allgather_perf_model_xgmi(x: float, P: int, density: float = 0.001, kcap_factor: float = 4.0 / 3.0) -> float:
+    """All-gather of one bucket's packed record: (4 + 2 k_cap) int32 words per rank."""
+    if x == 0 or P <= 1:
         return 0.0
-    a, b = _nearest(XGMI_ALLGATHER, P)
-    return a + b * (x * P * 8 * density)
+    from . import perf_model
+    a, b = perf_model.collective_ab("allgather", P)
+    rec_bytes = (4 + 2 * kcap_factor * max(x * density, 1.0)) * 4
+    return a + b * rec_bytes
 
 
 def allreduce_perf_model_xgmi(nbytes: float, P: int) -> float:
-    if nbytes == 0:
+    if nbytes == 0 or P <= 1:
         return 0.0
-    a, b = _nearest(XGMI_ALLREDUCE, P)
-    return a + b * nbytes * (P - 1) / max(P, 1)
+    from . import perf_model
+    a, b = perf_model.collective_ab("allreduce", P)
+    return a + b * nbytes
 
 
 def predict_density_with_size_and_computation(m, comp_time, P):

@@ -1,0 +1,31 @@
+#!/bin/bash
+# Round-2 GPU session: new-kernel tests first, then the whole GPU suite, the
+# smoke test and the 1-GPU headline bench.  Every GPU step has its own time
+# limit; the script stops at the first crash / abort / timeout.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/r2
+mkdir -p $OUT
+step() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"
+  tail -4 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for s in ${STEPS:-new all smoke bench}; do
+  case $s in
+    new) step new_tests 600 python -u -m pytest ${NEW_TESTS:-tests/test_kernels2_gpu.py tests/test_bench_gpu.py} -x -v \
+           --timeout 300 --timeout-method thread ;;
+    all) step all_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench1 600 python bench.py --steps 20 --warmup 10 --json-out $OUT/bench1.json ;;
+    fp32) step bench_fp32 600 python bench.py --steps 10 --warmup 5 --amp none --json-out $OUT/bench_fp32.json ;;
+    prof) step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
+           python3 bench.py ${PROF_ARGS:---steps 5 --warmup 3} ;;
+  esac
+done

@@ -1,0 +1,64 @@
+"""bench.py's own multi-rank path, rehearsed on ONE GPU.
+
+The driver's scaling run launches ``bench.py --gpus N`` under
+torch.distributed.run with one rank per GPU over RCCL.  RCCL refuses two ranks
+on one device, so here two ranks share cuda:0 over gloo
+(``GKSGD_DIST_BACKEND=gloo``, ``--no-native-rccl``) and everything else is the
+real thing: the self-launch of torch.distributed.run as a child, comm.init,
+the coalesced parameter broadcast, barriers, the MAX-over-ranks elapsed time,
+the packed all-gather + rank-ordered decompress, the selected-count
+collection, the replica digest and Exchanger.close().
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _bench(*extra, gpus=2, timeout=480, probe=False):
+    env = dict(os.environ, GKSGD_DIST_BACKEND="gloo", MASTER_PORT=str(_free_port()), HSA_ENABLE_IPC_MODE_LEGACY="0",
+               GKSGD_BENCH_PROBE="1" if probe else "0")
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    env.pop("LOCAL_RANK", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--no-native-rccl"] + list(extra)
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, "bench.py failed (%d):\n%s\n%s" % (p.returncode, p.stdout[-3000:], p.stderr[-3000:])
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-3000:]     # rank 0 prints exactly one JSON line
+    return json.loads(lines[0])
+
+
+def test_bench_resnet50_two_ranks_one_gpu(cuda):
+    out = _bench("--steps", "3", "--warmup", "2", "--batch-size", "16")
+    assert out["n_gpus"] == 2 and out["world"] == 2
+    assert out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 32
+    assert out["exchange"] == "torch"
+    assert out["replicas_consistent"] is True
+    assert out["value"] > 0 and out["ms_per_step"] > 0
+    assert out["selected_over_k"] > 0        # reference <=3-loop tree: anywhere around k
+    # wire ratio: dense fp32 bytes / fixed record bytes, k_cap = ceil(4k/3)
+    assert 300 <= out["effective_compression_ratio"] <= 400
+
+
+def test_bench_dense_two_ranks_one_gpu(cuda):
+    out = _bench("--model", "resnet20", "--steps", "3", "--warmup", "1", "--batch-size", "64", "--dense", probe=True)
+    assert out["replicas_consistent"] is True and out["config"]["compressor"] == "none"
+    # the post-run fabric probe (alpha-beta of all-gather / all-reduce through the bench's exchanger)
+    c = out["collectives"]
+    assert c["allgather"]["points_bytes_us"] and c["allreduce"]["dense_grad_us"] > 0

@@ -46,10 +46,11 @@ def test_loopback_error_propagates():
         comm.loopback_world(2, body, timeout_s=30)
 
 
-def _train(P, comp, density, steps):
+def _train(P, comp, density, steps, **opt_kw):
     from gaussiank_sgd_amd.compression import compressors
     from gaussiank_sgd_amd.parallel import distributed_optimizer as hvd
     from gaussiank_sgd_amd.train import DLTrainer
+    compressors[comp].clear()   # class-level residual state (reference API) starts empty
     trainers = []
     for r in range(P):          # built serially: model init draws from the global RNG
         torch.manual_seed(0)
@@ -60,15 +61,22 @@ def _train(P, comp, density, steps):
         t = trainers[r]
         opt = hvd.DistributedOptimizer(t.optimizer, named_parameters=t.net.named_parameters(),
                                        compression=compressors[comp], is_sparse=comp not in ("none", "bucket"),
-                                       density=density, density_warmup=False)
+                                       density=density, density_warmup=False, **opt_kw)
         hvd.broadcast_parameters(t.net.state_dict(), root_rank=0)
         t.update_optimizer(opt)
         t.base_lr = 0.5
+        sent = []
         for _ in range(steps):
             opt.zero_grad()
             t.train(1)
             t.update_model()
-        return {k: v.detach().clone() for k, v in t.net.state_dict().items()}
+            b = opt.arena.buckets[0]
+            if b.bufs is not None:
+                rec = b.bufs.record
+                sent.append(rec[4:4 + int(rec[0])].clone())
+        st = {k: v.detach().clone() for k, v in t.net.state_dict().items()}
+        st["__sent__"] = sent
+        return st
 
     return comm.loopback_world(P, body)
 
@@ -80,6 +88,8 @@ def test_loopback_optimizer_matches_reference_aggregation(comp, density):
     aggregation g = 1/P sum_r scatter(idx_r, val_r))."""
     from test_dist_gloo import STEPS, _loopback
     states = _train(2, comp, density, STEPS)
+    for s in states:
+        s.pop("__sent__")
     for k in states[0]:
         assert torch.equal(states[0][k], states[1][k]), "ranks diverged at %s" % k
     ref = _loopback(comp, density)
@@ -92,53 +102,53 @@ def test_loopback_world_ranks_agree(P):
     states = _train(P, "gaussian", 0.01, 3)
     for s in states[1:]:
         for k in s:
-            assert torch.equal(s[k], states[0][k]), k
+            if k != "__sent__":
+                assert torch.equal(s[k], states[0][k]), k
 
 
-@pytest.mark.gpu
-def test_loopback_world4_on_one_gpu():
-    """Four virtual ranks sharing one MI355X: the HIP compress / scatter-add /
-    fused-SGD path with a real P = 4 aggregation, ranks bit-identical, and
-    equal (to fp32 rounding) to the same world on the CPU mirror ops."""
-    if not torch.cuda.is_available():
-        pytest.skip("needs a GPU")
-    from gaussiank_sgd_amd import ops
-    assert ops.load(), ops._load_error
-    from gaussiank_sgd_amd.compression import compressors
-    from gaussiank_sgd_amd.parallel import distributed_optimizer as hvd
-    from gaussiank_sgd_amd.train import DLTrainer
-
-    def run(device):
-        trainers = []
-        for r in range(4):
-            torch.manual_seed(0)
-            trainers.append(DLTrainer(r, 4, dnn="fcn5net", dataset="mnist", batch_size=32, lr=0.5, nworkers=4,
-                                      device=device, learnable_data=True, seed=r))
-
-        def body(r):
-            if device == "cuda":
-                torch.cuda.set_device(0)
-            t = trainers[r]
-            opt = hvd.DistributedOptimizer(t.optimizer, named_parameters=t.net.named_parameters(),
-                                           compression=compressors["gaussian"], is_sparse=True, density=0.01,
-                                           density_warmup=False)
-            hvd.broadcast_parameters(t.net.state_dict(), root_rank=0)
-            t.update_optimizer(opt)
-            t.base_lr = 0.5
-            for _ in range(3):
-                opt.zero_grad()
-                t.train(1)
-                t.update_model()
-            if device == "cuda":
-                torch.cuda.synchronize()
-            return {k: v.detach().cpu().clone() for k, v in t.net.state_dict().items()}
-
-        return comm.loopback_world(4, body)
-
-    g = run("cuda")
-    for s in g[1:]:
+@pytest.mark.parametrize("comp", ["randomksame", "randomksameec"])
+def test_loopback_randomksame_ranks_pick_same_indices(comp):
+    """*same variants: every rank sends the SAME index set each step (seed is a
+    function of the iteration and bucket, not of a shared class counter)."""
+    states = _train(4, comp, 0.01, 3)
+    for s in states[1:]:
+        for a, b in zip(s["__sent__"], states[0]["__sent__"]):
+            assert torch.equal(a, b)
         for k in s:
-            assert torch.equal(s[k], g[0][k]), k
-    c = run("cpu")
-    for k in g[0]:
-        assert torch.allclose(g[0][k], c[0][k], atol=1e-5, rtol=1e-4), k
+            if k != "__sent__":
+                assert torch.equal(s[k], states[0][k]), k
+    # and different indices in different steps
+    assert not torch.equal(states[0]["__sent__"][0], states[0]["__sent__"][1])
+
+
+@pytest.mark.parametrize("comp", ["randomk", "dgcsampling", "topk_legacy", "gaussian_cal"])
+def test_loopback_reproducible_and_ranks_agree(comp):
+    """Rank-dependent selectors: replicas agree, and two runs give the same result
+    (no seed or residual state leaks between the virtual ranks)."""
+    a = _train(3, comp, 0.01, 3)
+    b = _train(3, comp, 0.01, 3)
+    for s in a[1:]:
+        for k in s:
+            if k != "__sent__":
+                assert torch.equal(s[k], a[0][k]), (comp, k)
+    for k in a[0]:
+        if k != "__sent__":
+            assert torch.equal(a[0][k], b[0][k]), (comp, k)
+    if comp == "randomk":       # independent draws per rank
+        assert not torch.equal(a[0]["__sent__"][0], a[1]["__sent__"][0])
+
+
+def test_loopback_momentum_correction_sparse_apply_matches_dense():
+    """DGC momentum correction: the sparse SGD apply straight from the gathered
+    records == scatter into the gradient arena + dense fused SGD."""
+    sp = _train(4, "gaussian", 0.01, 4, momentum_correction=True, sparse_apply=True)
+    dn = _train(4, "gaussian", 0.01, 4, momentum_correction=True, sparse_apply=False)
+    for s in sp[1:]:
+        for k in s:
+            if k != "__sent__":
+                assert torch.equal(s[k], sp[0][k]), k
+    for k in sp[0]:
+        if k != "__sent__":
+            assert torch.allclose(sp[0][k], dn[0][k], atol=1e-6, rtol=1e-5), k
+
+
