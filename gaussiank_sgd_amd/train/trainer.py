@@ -47,6 +47,8 @@ class DLTrainer:
                  sparsity=0.95, pretrain=None, num_steps=35, tb_writer=None, amp_handle=None, device=None,
                  amp: Optional[str] = None, channels_last: bool = False, learnable_data: bool = False,
                  seed: int = 0, data_pool: int = 4, weights_dir: str = "./weights", seq_len: Optional[int] = None):
+        # data_dir: real datasets (data/real.py: CIFAR-10 binary, MNIST idx, PTB text, .npz / .npy
+        # arrays), sharded by (rank, nworkers); absent or unrecognised -> synthetic, shape-exact
         self.size = size
         self.rank = rank
         self.pretrain = pretrain
@@ -149,11 +151,29 @@ class DLTrainer:
         if self.dnn == "bert_tiny":
             vocab = 1024
             seq_len = seq_len or 128
-        self.data = SyntheticData(ds, self.batch_size, self.device, seed=self.seed * 1000 + self.rank, pool=pool,
-                                  learnable=learnable, seq_len=(self.num_steps if ds == "ptb" else seq_len),
-                                  channels_last=self.channels_last and self.is_cuda, vocab_size=vocab)
+        self.test_data = None
+        real = None
+        if self.data_dir and os.path.isdir(self.data_dir) and not learnable:
+            from ..data.real import open_dataset
+            real = open_dataset(ds, self.data_dir, self.batch_size, self.device, self.rank, self.nworkers,
+                                seed=self.seed, channels_last=self.channels_last and self.is_cuda,
+                                num_steps=self.num_steps)
+            if real is not None:
+                self.test_data = open_dataset(ds, self.data_dir, self.batch_size, self.device, 0, 1, seed=self.seed,
+                                              channels_last=self.channels_last and self.is_cuda,
+                                              num_steps=self.num_steps, train=False)
+                logger.info("real data: %s from %s, %d samples, rank %d of %d shards", ds, self.data_dir,
+                            real.num_samples(), self.rank, self.nworkers)
+            else:
+                logger.info("no %s files under %s: synthetic data", ds, self.data_dir)
+        if real is not None:
+            self.data = real
+        else:
+            self.data = SyntheticData(ds, self.batch_size, self.device, seed=self.seed * 1000 + self.rank, pool=pool,
+                                      learnable=learnable, seq_len=(self.num_steps if ds == "ptb" else seq_len),
+                                      channels_last=self.channels_last and self.is_cuda, vocab_size=vocab)
         self.trainset_len = self.data.num_samples()
-        self._input_shape = (self.batch_size,) + tuple(self.data.spec.shape)
+        self._input_shape = (self.batch_size,) + tuple(DATASETS[ds].shape)
         self._output_shape = (self.batch_size, self.num_classes)
         self.num_batches_per_epoch = (self.trainset_len + self.batch_size * self.nworkers - 1) // (
             self.batch_size * self.nworkers)
@@ -333,7 +353,8 @@ class DLTrainer:
         self.net.eval()
         top1, top5, losses = [], [], []
         costs, steps = 0.0, 0
-        for inputs, labels in self.data.test_batches(num_batches):
+        src = self.test_data if getattr(self, "test_data", None) is not None else self.data
+        for inputs, labels in src.test_batches(num_batches):
             outputs, loss, _ = self.forward_loss(inputs, labels, None)
             losses.append(float(loss))
             if self.dnn == "lstm":
