@@ -21,7 +21,8 @@ from typing import List, Optional, Sequence, Tuple
 
 import torch
 
-_LIB = Path(__file__).resolve().parents[1] / "_C.so"
+# GKSGD_EXT overrides the library (e.g. build/asan/_C.so, the host-sanitizer build)
+_LIB = Path(os.environ.get("GKSGD_EXT") or (Path(__file__).resolve().parents[1] / "_C.so"))
 _lock = threading.Lock()
 _loaded = False
 _load_error: Optional[BaseException] = None

@@ -26,6 +26,14 @@ REPO = PKG.parent
 CSRC = PKG / "ops" / "csrc"
 BUILD = REPO / "build" / "gksgd_ext"
 TARGET = PKG / "_C.so"
+# host-sanitizer variant (python -m gaussiank_sgd_amd.ops.build --asan): the C++
+# bindings / RCCL engine and the host side of every .hip file are built with
+# AddressSanitizer + UBSan; device code is unchanged (GPU ASan is not used)
+ASAN = os.environ.get("GKSGD_ASAN", "0") == "1"
+if ASAN:
+    BUILD = REPO / "build" / "gksgd_ext_asan"
+    TARGET = REPO / "build" / "asan" / "_C.so"
+SAN_HOST = ["-fsanitize=address", "-fsanitize=undefined"]
 ARCH = os.environ.get("GKSGD_OFFLOAD_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
@@ -61,7 +69,12 @@ def _hipcc() -> str:
 
 
 def _hip_flags() -> List[str]:
-    return [
+    san = []
+    if ASAN:
+        for f in SAN_HOST:
+            san += ["-Xarch_host", f]
+        san += ["-Xarch_host", "-fno-omit-frame-pointer"]
+    return san + [
         "--offload-arch=" + ARCH,
         "-O3",
         "-fPIC",
@@ -77,7 +90,7 @@ def _cxx_flags() -> List[str]:
     inc, api_inc, _ = _torch_dirs()
     import torch
     abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
-    return [
+    return (SAN_HOST + ["-fno-omit-frame-pointer", "-g"] if ASAN else []) + [
         "-O2",
         "-fPIC",
         "-std=c++17",
@@ -139,7 +152,9 @@ def build(verbose: bool = False, force: bool = False, jobs: int = 4) -> Path:
     stamp = BUILD / ("link." + link_key)
     if TARGET.exists() and stamp.exists() and not force:
         return TARGET
-    cmd = [os.environ.get("CXX", "g++"), "-shared", "-o", str(TARGET) + ".tmp"] + [str(o) for o in objs] + [
+    TARGET.parent.mkdir(parents=True, exist_ok=True)
+    cmd = [os.environ.get("CXX", "g++"), "-shared", "-o", str(TARGET) + ".tmp"] + (SAN_HOST if ASAN else []) + \
+        [str(o) for o in objs] + [
         "-L" + str(tlib),
         "-Wl,-rpath," + str(tlib),
         "-L" + os.path.join(ROCM, "lib"),
@@ -168,7 +183,12 @@ def main(argv=None) -> int:
     ap.add_argument("-v", "--verbose", action="store_true")
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=4)
+    ap.add_argument("--asan", action="store_true", help="host ASan+UBSan variant under build/asan/ (re-execs)")
     args = ap.parse_args(argv)
+    if args.asan and not ASAN:
+        env = dict(os.environ, GKSGD_ASAN="1")
+        return subprocess.call([sys.executable, "-m", "gaussiank_sgd_amd.ops.build"] +
+                               [a for a in (argv if argv is not None else sys.argv[1:]) if a != "--asan"], env=env)
     out = build(verbose=args.verbose, force=args.force, jobs=args.jobs)
     print(out)
     return 0

@@ -25,6 +25,8 @@ for s in ${STEPS:-new all smoke bench}; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench1 600 python bench.py --steps 20 --warmup 10 --json-out $OUT/bench1.json ;;
     fp32) step bench_fp32 600 python bench.py --steps 10 --warmup 5 --amp none --json-out $OUT/bench_fp32.json ;;
+    kern) step kernels 600 python bench/kernels.py --only round2,fit --fit-out $OUT/perf_model_mi355x.json \
+           --json-out $OUT/kernels.json ;;
     prof) step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
            python3 bench.py ${PROF_ARGS:---steps 5 --warmup 3} ;;
   esac
