@@ -68,6 +68,11 @@ def parse():
     ap.add_argument("--compressor", default="gaussian")
     ap.add_argument("--density", type=float, default=0.001)
     ap.add_argument("--threshold", type=int, default=524288000, help="bucket threshold (elements), reference default")
+    ap.add_argument("--planner", default="threshold", choices=["threshold", "mgs", "mgwfbp"],
+                    help="bucket planner: reference threshold grouping, or MGS / MG-WFBP on measured layer-wise "
+                         "backward times (utils/profiler.benchmark) and the perf models (utils/perf_model.py)")
+    ap.add_argument("--plan-world", type=int, default=None,
+                    help="world size the planner's cost models assume (default: this world)")
     ap.add_argument("--amp", default="bf16", choices=["bf16", "none"])
     ap.add_argument("--no-channels-last", action="store_true")
     ap.add_argument("--dense", action="store_true", help="dense RCCL all-reduce comparator (compressor none)")
@@ -172,10 +177,17 @@ def main() -> int:
                         channels_last=not args.no_channels_last, seed=0)
     comp_name = "none" if args.dense else args.compressor
     is_sparse = not args.dense and comp_name not in ("none", "bucket")
+    seq_names = layer_times = None
+    if args.planner != "threshold":
+        # reference dist_trainer.py:38-47: layer-wise backward profile, shared from rank 0
+        from gaussiank_sgd_amd.utils.profiler import benchmark
+        seq_names, layer_times, _ = benchmark(trainer, warmup=3, iterations=10)
+        layer_times = comm.broadcast_object(list(layer_times), 0)
     opt = DistributedOptimizer(trainer.optimizer, named_parameters=trainer.net.named_parameters(),
                                compression=compressors[comp_name], is_sparse=is_sparse, density=args.density,
                                threshold=args.threshold, compress_single_rank=True, density_warmup=False,
-                               native_rccl=not args.no_native_rccl,
+                               native_rccl=not args.no_native_rccl, seq_layernames=seq_names,
+                               layerwise_times=layer_times, planner=args.planner, planner_world=args.plan_world,
                                momentum_correction=is_sparse and not args.no_momentum_correction)
     comm.broadcast_parameters(trainer.net.state_dict(), root_rank=0)
     if args.amp == "bf16" and not args.no_shadow:
@@ -291,6 +303,7 @@ def main() -> int:
             "compressor": comp_name,
             "density": args.density if is_sparse else 1.0,
             "buckets": len(opt.arena.buckets),
+            "planner": args.planner if args.planner == "threshold" else "%s@P=%s" % (args.planner, args.plan_world or P),
             "exchange": opt._exchanger.kind if opt._exchanger is not None else "none",
             "momentum_correction": bool(opt._mc),
             "hip_graph": bool(args.graph),

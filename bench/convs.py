@@ -70,6 +70,9 @@ def main() -> int:
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--gemm", action="store_true",
                     help="also time the stride-1 1x1 convs as plain torch.mm (hipBLASLt) GEMMs")
+    ap.add_argument("--ours", action="store_true",
+                    help="time the production path (ops/conv1x1.py: autotuned MFMA kernels vs MIOpen, "
+                         "tuning/gemm_choices.json) and report which implementation each direction uses")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     rows = []
@@ -90,6 +93,20 @@ def main() -> int:
             "dgrad": (lambda: torch.autograd.grad(yg, xg, dy, retain_graph=True), by + bw + bx),
             "wgrad": (lambda: torch.autograd.grad(yg, wg, dy, retain_graph=True), by + bx + bw),
         }
+        impl = {}
+        if args.ours and C % 64 == 0 and K % 64 == 0:
+            from gaussiank_sgd_amd.ops import conv1x1 as cv
+            wo = torch.zeros(K, C, k, k, device=dev, dtype=torch.float32).contiguous(memory_format=torch.channels_last)
+            cases = {
+                "fwd": (lambda: cv._fwd(x, w, s), bx + bw + by),
+                "dgrad": (lambda: cv._dgrad(dy, w, x.shape, s), by + bw + bx),
+                "wgrad": (lambda: cv._wgrad_into(dy, x, w, s, wo), by + bx + bw),
+            }
+            for name, (fn, _) in cases.items():
+                fn()
+            geo = (N, C, H, W, K, k, s)
+            impl = {"fwd": cv._choices.get(("fwd",) + geo + (False,)), "dgrad": cv._choices.get(("dgrad",) + geo),
+                    "wgrad": cv._choices.get(("wgrad",) + geo)}
         if C == 3:
             del cases["dgrad"]   # the stem's input (the image batch) needs no gradient in training
         for name, (fn, nbytes) in cases.items():
@@ -100,6 +117,8 @@ def main() -> int:
             r = dict(op=name, N=N, Cin=C, H=H, W=W, Cout=K, k=k, stride=s, count=mult, us=round(t * 1e6, 1),
                      roofline_us=round(roof * 1e6, 1), eff=round(roof / t, 3),
                      tflops=round(flops / t / 1e12, 1), bound="compute" if flops / PEAK > nbytes / HBM else "memory")
+            if impl.get(name) is not None:
+                r["impl"] = list(impl[name])
             rows.append(r)
             print(json.dumps(r), flush=True)
         if args.gemm and k == 1 and s == 1:

@@ -37,6 +37,7 @@ MODE_DGC = 6
 MODE_GAUSSIAN_CAL = 7
 
 CAL_FALLBACK = 16   # record header `chosen` when the calibrated mode used the exact radix key
+CAL_CAND = 8        # calibrated ladder size (gk::kCalCand)
 
 MAX_CAND = 16
 CHUNK_ELEMS = 16384
@@ -318,7 +319,7 @@ def _cal_ladder(bufs: CompressBuffers, k: int, z: float, mean: float, std: float
         st["step"] = 0.105
         st["k"] = k
     tc = st["c"] * std
-    return [tc * math.exp(st["step"] * (j - 7)) for j in range(MAX_CAND)]
+    return [tc * math.exp(st["step"] * (j - 0.5 * (CAL_CAND - 1))) for j in range(CAL_CAND)]
 
 
 def compress_cpu_(g: torch.Tensor, r: torch.Tensor, bufs: CompressBuffers, mode: int, ec: bool, zero_g: bool,

@@ -22,6 +22,8 @@
 //   redsync   :623-691, redsynctrim :694-738, dgcsampling :555-620
 // Deviation (documented in SURVEY 2.3/7.4): the record holds at most k_cap
 // entries; selected elements beyond k_cap stay in the residual.
+#include <cstdlib>
+
 #include "common.h"
 #include "gk_kernels.h"
 
@@ -30,6 +32,10 @@ namespace {
 
 constexpr int kTileElems = kBlock * 16;  // 4 float4 per thread per tile
 constexpr int kKeyAbs = 0, kKeyHash = 1, kKeySample = 2;
+// calibrated Gaussian-k ladder size: the ladder re-centres every call, so 8
+// candidates (the count pass tests each element against every candidate) keep
+// the count pass as cheap as the reference ladder's 6
+constexpr int kCalCand = 8;
 constexpr int kHistSet = kRadixBins0 + kRadixBins1 + kRadixBins2;
 
 struct Ws {
@@ -464,7 +470,7 @@ __global__ __launch_bounds__(kBlock) void finalize_kernel(GkCtrl* __restrict__ c
       nc = kMaxCand;
     }
   } else if (mode == kModeGaussianCal) {
-    // 16 thresholds t_c * exp(step * (j - 7)), ascending in j.  The centre
+    // kCalCand thresholds t_c * exp(step * (j - 3.5)), ascending in j.  The centre
     // t_c = cal_c * sigma and the spacing persist per bucket (decide_kernel
     // re-centres on the best candidate and adapts the spacing to the local
     // slope of the count curve); first call / new k: the Gaussian estimate.
@@ -475,12 +481,12 @@ __global__ __launch_bounds__(kBlock) void finalize_kernel(GkCtrl* __restrict__ c
       ctrl->cal_k = k;
     }
     const double tc = ctrl->cal_c * stdev;
-    for (int j = 0; j < kMaxCand; ++j) {
-      const double t = tc * exp(ctrl->cal_step * (double)(j - 7));
+    for (int j = 0; j < kCalCand; ++j) {
+      const double t = tc * exp(ctrl->cal_step * ((double)j - 0.5 * (kCalCand - 1)));
       ctrl->bound[j] = bound_from_threshold((float)t);
       ctrl->cand_thr[j] = t;
     }
-    nc = kMaxCand;
+    nc = kCalCand;
   } else if (mode == kModeThreshold) {
     ctrl->bound[0] = bound_from_threshold((float)fixed_thr);
     ctrl->cand_thr[0] = fixed_thr;
@@ -536,6 +542,12 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const float* __restrict__
                                                        uint32_t* __restrict__ blockcnt,
                                                        const uint32_t* __restrict__ valid, int cond) {
   if (cond && ctrl->fallback == 0) return;
+  // Wave-uniform counters: every (element, candidate) test is ONE v_cmp whose
+  // 64-bit lane mask is popcounted and accumulated on the SCALAR unit
+  // (s_bcnt1 + s_add), instead of a compare + conditional add per lane --
+  // half the VALU work, and no cross-lane reduction at the end.  Only the
+  // ncand live candidates are tested (uniform loop bound).
+  const int nc = __builtin_amdgcn_readfirstlane(ctrl->ncand);
   uint32_t bnd[kMaxCand];
 #pragma unroll
   for (int j = 0; j < kMaxCand; ++j) bnd[j] = __builtin_amdgcn_readfirstlane(ctrl->bound[j]);
@@ -557,15 +569,15 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const float* __restrict__
         const bool inb = e + q < n;
         const uint32_t key = inb ? key_of<KEYKIND>(e + q, v[q], seed, valid) : 0u;
 #pragma unroll
-        for (int j = 0; j < kMaxCand; ++j) cnt[j] += (inb && key >= bnd[j]) ? 1u : 0u;
+        for (int j = 0; j < kMaxCand; ++j)
+          if (j < nc) cnt[j] += (uint32_t)__popcll(__ballot(inb && key >= bnd[j]));
       }
     }
   }
   __shared__ uint32_t sh[kWavesPerBlock][kMaxCand];
+  if (lane_id() == 0) {
 #pragma unroll
-  for (int j = 0; j < kMaxCand; ++j) {
-    const uint32_t w = wave_sum(cnt[j]);
-    if (lane_id() == 0) sh[wave_id()][j] = w;
+    for (int j = 0; j < kMaxCand; ++j) sh[wave_id()][j] = j < nc ? cnt[j] : 0u;
   }
   __syncthreads();
   if (threadIdx.x < kMaxCand) {
@@ -978,7 +990,11 @@ void compress(const CompressArgs& a, hipStream_t s) {
     launch_select<kKeyHash>(a, w, vec_r, G, chunk_tiles, ctrl, out_idx, out_val, s);
   } else {
     launch_count<kKeyAbs>(a, w, vec_r, G, chunk_tiles, ctrl, 0, s);
-    if (a.mode == kModeGaussianCal) {
+    static const bool cal_fallback = [] {
+      const char* e = getenv("GKSGD_CAL_FALLBACK");   // "0": measure the pipeline without the exact fallback
+      return e == nullptr || e[0] != '0';
+    }();
+    if (a.mode == kModeGaussianCal && cal_fallback) {
       // conditional exact-top-k fallback: every kernel below exits at once
       // unless the decide above found no candidate in [2k/3, 4k/3]
       launch_radix<kKeyAbs>(a.r, a.n, a.seed, 0u, keff, hist_exact, vec_r, nullptr, ctrl, s);

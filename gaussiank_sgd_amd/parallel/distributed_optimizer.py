@@ -103,6 +103,12 @@ class _DistributedOptimizer(torch.optim.Optimizer):
             self._overlap = False
         self._prefer_native_rccl = bool(opts.get("native_rccl", True))
         self._planner_preset = opts.get("planner_preset", "mi355x")
+        # planner: "threshold" (reference default), "mgs" / "mgwfbp" (use the
+        # layer-wise times even without settings.ADAPTIVE_MERGE), "auto"
+        # (settings.ADAPTIVE_MERGE decides, reference behaviour); planner_world:
+        # world size the cost models are evaluated at (default: this world)
+        self._planner = opts.get("planner", "auto")
+        self._planner_world = opts.get("planner_world")
         # DGC momentum correction (Lin et al. 2018): momentum is accumulated
         # locally BEFORE sparsification and the global update is plain SGD.
         self._mc = bool(opts.get("momentum_correction", _env_flag("GKSGD_MOMENTUM_CORRECTION", False)))
@@ -175,22 +181,23 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         return groups, key_map
 
     def _generate_groups_mgwfbp(self):
-        P = size()
+        P = int(self._planner_world or size())
         ar, alpha, _, _ = models_for(P, self._density, self._planner_preset)
         sizes = [self._named_parameters[k].numel() for k in self._seq_layernames]
         self._sizes = sizes
         return plan_mgwfbp(self._seq_layernames, self._layerwise_times, sizes, ar, alpha)
 
     def _generate_groups_mgs(self):
-        P = size()
+        P = int(self._planner_world or size())
         _, _, ct, ag = models_for(P, self._density, self._planner_preset)
         sizes = [self._named_parameters[k].numel() for k in self._seq_layernames]
         self._sizes = sizes
         return plan_mgs(self._seq_layernames, self._layerwise_times, sizes, ct, ag)
 
     def _generate_merged_parameters(self):
-        if settings.ADAPTIVE_MERGE and self._layerwise_times is not None and self._seq_layernames is not None:
-            if self._density < 1:
+        adaptive = settings.ADAPTIVE_MERGE if self._planner == "auto" else self._planner in ("mgs", "mgwfbp")
+        if adaptive and self._layerwise_times is not None and self._seq_layernames is not None:
+            if (self._density < 1 and self._planner != "mgwfbp") or self._planner == "mgs":
                 groups, key_map = self._generate_groups_mgs()
             else:
                 groups, key_map = self._generate_groups_mgwfbp()

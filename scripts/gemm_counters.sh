@@ -3,7 +3,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/ctr
+OUT=${CTR_OUT:-gpurun_out/ctr}
 mkdir -p $OUT
 ARGS=${PROBE_ARGS:---op conv --cfg 124}
 timeout -s KILL 60 rocprofv3 -L > $OUT/avail.txt 2>&1 || true
@@ -16,9 +16,10 @@ for set in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
   echo "rc=$?"
   tail -2 $OUT/p$i.log
 done
-python3 - <<'PY'
+CTR_OUT=$OUT python3 - <<'PY'
 import csv, collections, glob
-for f in sorted(glob.glob("gpurun_out/ctr/p*/run_counter_collection.csv")):
+import os
+for f in sorted(glob.glob(os.environ.get("CTR_OUT", "gpurun_out/ctr") + "/p*/run_counter_collection.csv")):
     rows = [r for r in csv.DictReader(open(f)) if "gemm_" in r["Kernel_Name"]]
     if not rows:
         continue

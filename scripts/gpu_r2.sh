@@ -25,7 +25,14 @@ for s in ${STEPS:-new all smoke bench}; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench1 600 python bench.py --steps 20 --warmup 10 --json-out $OUT/bench1.json ;;
     fp32) step bench_fp32 600 python bench.py --steps 10 --warmup 5 --amp none --json-out $OUT/bench_fp32.json ;;
-    kern) step kernels 600 python bench/kernels.py --only round2,fit --fit-out $OUT/perf_model_mi355x.json \
+    sweep) for spec in ${SWEEP:-bert:524288000 bert:56000000 bert:28000000 bert:14000000 vgg16:524288000 vgg16:7400000 vgg16:3700000}; do
+             m=${spec%%:*}; th=${spec##*:}
+             step sweep_${m}_${th} 400 python bench.py --model $m --steps 20 --warmup 10 --threshold $th \
+               --json-out $OUT/sweep_${m}_${th}.json
+           done ;;
+    marker) export GKSGD_ROCTX=1; step marker 600 rocprofv3 --marker-trace --kernel-trace --stats --output-format csv -d $OUT/marker -o run -- \
+           python3 bench.py ${MARKER_ARGS:---model bert --steps 4 --warmup 4 --threshold 28000000}; unset GKSGD_ROCTX ;;
+    kern) step kernels 600 python bench/kernels.py --only ${KERN_ONLY:-round2,fit} --fit-out $OUT/perf_model_mi355x.json \
            --json-out $OUT/kernels.json ;;
     prof) step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
            python3 bench.py ${PROF_ARGS:---steps 5 --warmup 3} ;;
