@@ -29,25 +29,24 @@ HBM = 6.3e12
 
 
 def resnet50_convs(batch: int):
-    """(N, Cin, H, W, Cout, k, stride, pad) with multiplicity."""
-    from gaussiank_sgd_amd.models import resnet50
-    net = resnet50(num_classes=1000)
+    """(N, Cin, H, W, Cout, k, stride, pad) with multiplicity -- ResNet-50 v1.5
+    (stride on the 3x3; models/resnet_imagenet.py), enumerated from the
+    architecture (the fused blocks call their convolutions through
+    forward_stats, which bypasses module forward hooks)."""
     shapes = Counter()
-    hooks = []
-
-    def mk(mod):
-        def h(m, inp, out):
-            x = inp[0]
-            shapes[(batch, x.shape[1], x.shape[2], x.shape[3], m.out_channels, m.kernel_size[0], m.stride[0],
-                    m.padding[0])] += 1
-        return h
-    for m in net.modules():
-        if isinstance(m, torch.nn.Conv2d):
-            hooks.append(m.register_forward_hook(mk(m)))
-    with torch.no_grad():
-        net.eval()(torch.zeros(1, 3, 224, 224))
-    for h in hooks:
-        h.remove()
+    shapes[(batch, 3, 224, 224, 64, 7, 2, 3)] += 1
+    cin, H = 64, 56
+    for planes, blocks, stride in ((64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2)):
+        out = planes * 4
+        for b in range(blocks):
+            s = stride if b == 0 else 1
+            shapes[(batch, cin, H, H, planes, 1, 1, 0)] += 1
+            shapes[(batch, planes, H, H, planes, 3, s, 1)] += 1
+            Ho = H // s
+            shapes[(batch, planes, Ho, Ho, out, 1, 1, 0)] += 1
+            if b == 0:
+                shapes[(batch, cin, H, H, out, 1, s, 0)] += 1
+            cin, H = out, Ho
     return shapes
 
 
@@ -138,7 +137,7 @@ def main() -> int:
         del x, w, y, dy, xg, wg, yg
     for name, (t, roof) in tot.items():
         print("TOTAL %-5s %.2f ms per step (roofline %.2f ms, efficiency %.0f%%)" % (name, t * 1e3, roof * 1e3,
-                                                                                   100 * roof / t))
+                                                                                   100 * roof / max(t, 1e-12)))
     if args.json_out:
         with open(args.json_out, "w") as f:
             json.dump({"rows": rows, "totals_ms": {k: [v[0] * 1e3, v[1] * 1e3] for k, v in tot.items()}}, f,

@@ -25,7 +25,13 @@ def main():
     K = a.K or a.C
     x = torch.randn(a.batch, a.C, a.H, a.H, device="cuda", dtype=torch.bfloat16).contiguous(
         memory_format=torch.channels_last)
-    if a.op == "wgrad3":
+    if a.op == "lwgrad":   # linear grad-weight (BERT ffn): W[N, K] += G[M, N]^T X[M, K]
+        M = a.batch * a.H
+        G = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+        X = torch.randn(M, a.C, device="cuda", dtype=torch.bfloat16)
+        out = torch.zeros(K, a.C, device="cuda")
+        fn = lambda: g.gemm_tn_acc(G, X, out, a.cfg, 0)  # noqa: E731
+    elif a.op == "wgrad3":
         dy = torch.randn(a.batch, K, a.H, a.H, device="cuda", dtype=torch.bfloat16).contiguous(
             memory_format=torch.channels_last)
         out = torch.zeros(K, a.C, 3, 3, device="cuda").contiguous(memory_format=torch.channels_last)

@@ -483,6 +483,20 @@ __device__ __forceinline__ int tr_swz(int r) {
 // Transposed fragment: lane l (group g = l>>4, li = l&15) gets rows
 // r0 + 8g + 0..7 of column c0 + li of the swizzled [rows][RB] bf16 image, as
 // the 8 k-elements of a 16x16x32 MFMA operand.  c0 is a multiple of 16.
+// The transposed LDS read is issued as inline asm: with the builtin, the
+// compiler's wait-count pass cannot tell the read apart from the LDS-DMA
+// writes of the NEXT stage issued just before it and inserts
+// `s_waitcnt vmcnt(0)` -- which serialises the whole global->LDS pipeline
+// (each stage would wait for the loads it has just started).  The asm reads
+// carry no such dependence; tr_sync() below waits for them (lgkmcnt) and ties
+// the fragments to that wait so no MFMA can be scheduled before it.
+__device__ __forceinline__ bf16x4 ds_read_tr(const char* p) {
+  bf16x4 v;
+  const uint32_t a = (uint32_t)(uintptr_t)(GK_LDS char*)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a));
+  return v;
+}
+
 template <int RB>
 __device__ __forceinline__ bf16x8 tr_frag(const char* tile, int r0, int c0, int lane) {
   const int g = lane >> 4, li = lane & 15;
@@ -491,9 +505,30 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* tile, int r0, int c0, int 
   const int ra = r0 + 8 * g + q, rb = ra + 4;
   const char* a0 = tile + ra * RB + ((((col >> 3) ^ tr_swz<RB>(ra)) << 4) | ((col & 7) << 1));
   const char* a1 = tile + rb * RB + ((((col >> 3) ^ tr_swz<RB>(rb)) << 4) | ((col & 7) << 1));
-  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((GK_LDS bf16x4*)(GK_LDS char*)a0);
-  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((GK_LDS bf16x4*)(GK_LDS char*)a1);
+  bf16x4 lo = ds_read_tr(a0);
+  bf16x4 hi = ds_read_tr(a1);
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// the two halves of a transposed fragment at precomputed LDS addresses, k-step
+// kk adding the immediate kk * KSTEP bytes
+template <int KSTEP>
+__device__ __forceinline__ bf16x8 tr_pair(uint32_t a0, uint32_t a1, int kk) {
+  bf16x4 lo, hi;
+  if (kk == 0) {
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a0));
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(a1));
+  } else {
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo) : "v"(a0), "i"(KSTEP));
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(a1), "i"(KSTEP));
+  }
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// lgkmcnt(0) tied to the 8 fragments of one k-step
+__device__ __forceinline__ void tr_sync(bf16x8* a, bf16x8* b) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]));
 }
 
 template <int WN, int WK, int WS, int NS, bool GATHER>
@@ -604,6 +639,27 @@ gemm_tn_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __re
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // Per-lane LDS byte offsets of the 16 transposed reads of a k-step, set up
+  // once: the swizzle depends on row bits 0, 1 and 3 only, so the second
+  // k-step (rows + 32) is the same addresses + 32 rows -- an immediate offset
+  // -- and a new stage only adds its (uniform) base: 16 adds per stage instead
+  // of the full address arithmetic per read.
+  uint32_t goff[4][2], xoff[4][2];
+  {
+    const int g = lane >> 4, li = lane & 15;
+    const int q = li >> 2, p = li & 3;
+    const int ra = ws * 64 + 8 * g + q, rb = ra + 4;
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const int gc = wn * 64 + s2 * 16 + 4 * p, xc = wk * 64 + s2 * 16 + 4 * p;
+      goff[s2][0] = ra * Cfg::GROW + ((((gc >> 3) ^ tr_swz<Cfg::GROW>(ra)) << 4) | ((gc & 7) << 1));
+      goff[s2][1] = rb * Cfg::GROW + ((((gc >> 3) ^ tr_swz<Cfg::GROW>(rb)) << 4) | ((gc & 7) << 1));
+      xoff[s2][0] = Cfg::GBYTES + ra * Cfg::XROW + ((((xc >> 3) ^ tr_swz<Cfg::XROW>(ra)) << 4) | ((xc & 7) << 1));
+      xoff[s2][1] = Cfg::GBYTES + rb * Cfg::XROW + ((((xc >> 3) ^ tr_swz<Cfg::XROW>(rb)) << 4) | ((xc & 7) << 1));
+    }
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(GK_LDS char*)smem;
+
   stage(0);
   if (NS == 3 && T > 1) stage(1);
   for (int t = 0; t < T; ++t) {
@@ -613,25 +669,33 @@ gemm_tn_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __re
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     if (t + NS - 1 < T) stage(t + NS - 1);
-    const char* Gs = smem + (t % NS) * Cfg::STAGE;
-    const char* Xs = Gs + Cfg::GBYTES;
+    const uint32_t sb = lds0 + (uint32_t)((t % NS) * Cfg::STAGE);
+    uint32_t ga[4][2], xa[4][2];
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        ga[s2][h] = sb + goff[s2][h];
+        xa[s2][h] = sb + xoff[s2][h];
+      }
     const int64_t m0 = mbeg + (int64_t)t * Cfg::ROWS + ws * 64;
     const bool tail = m0 + 64 > mend;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8 gv[4], xv[4];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        gv[s] = tr_frag<Cfg::GROW>(Gs, ws * 64 + kk * 32, wn * 64 + s * 16, lane);
-        xv[s] = tr_frag<Cfg::XROW>(Xs, ws * 64 + kk * 32, wk * 64 + s * 16, lane);
+      for (int s2 = 0; s2 < 4; ++s2) {
+        gv[s2] = tr_pair<32 * Cfg::GROW>(ga[s2][0], ga[s2][1], kk);
+        xv[s2] = tr_pair<32 * Cfg::XROW>(xa[s2][0], xa[s2][1], kk);
       }
+      tr_sync(gv, xv);
       if (tail) {  // rows past this split's end contribute nothing
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int64_t m = m0 + kk * 32 + 8 * (lane >> 4) + j;
           if (m >= mend) {
 #pragma unroll
-            for (int s = 0; s < 4; ++s) gv[s][j] = 0;
+            for (int s2 = 0; s2 < 4; ++s2) gv[s2][j] = 0;
           }
         }
       }
@@ -688,8 +752,18 @@ void launch_tn(const uint16_t* G, int64_t ldg, const uint16_t* X, int64_t ldx, f
   using Cfg = TnCfg<WN, WK, WS, NS>;
   const int tiles = (N / Cfg::BN) * (K / Cfg::BK);
   if (splits <= 0) {
-    const int64_t target = 512;
-    splits = (int)((target + tiles - 1) / tiles);
+    // Whole rounds of the chip: one 8-wave block per CU at 2 waves / SIMD
+    // (the 16-wave tile: one per CU too), two rounds -- a 2.1-round grid
+    // would leave the third round almost empty (a 33% tail).
+    static const int cus = [] {
+      int d = 0, n = 0;
+      hipGetDevice(&d);
+      return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && n > 0 ? n : 256;
+    }();
+    const int64_t bpc = Cfg::NW >= 8 ? 1 : 8 / Cfg::NW;
+    const int64_t slots = (int64_t)cus * bpc;
+    splits = (int)(2 * slots / tiles);
+    if (splits < 1) splits = 1;
   }
   int64_t rows = (M + splits - 1) / splits;
   rows = (rows + Cfg::ROWS - 1) / Cfg::ROWS * Cfg::ROWS;
@@ -764,20 +838,26 @@ void launch_tn_any(const uint16_t* G, int64_t ldg, const uint16_t* X, int64_t ld
 template <bool GATHER>
 void tn_dispatch(const void* G, int64_t ldg, const void* X, int64_t ldx, float* W, int64_t ldw, int64_t M, int N,
                  int K, int cfg, int splits, const ConvGeo& geo, hipStream_t stream) {
-  // cfg = tile + 10 * (1: two stages, 2: three).  tile (WN, WK, WS):
+  // cfg = tile digit + 10 * (1: two stages, 2: three) + 100 * tile group.
+  // tile = cfg % 10 + 10 * (cfg / 100), (WN, WK, WS), 64x64 per wave:
   // 1 (1,1,4)  2 (2,1,2)  3 (1,2,2)  4 (2,2,1)  5 (4,1,1)  6 (1,4,1)  7 (2,2,2)  8 (1,1,2)
+  // 9 (4,2,1) 256x128  11 (2,4,1) 128x256  12 (4,4,1) 256x256 (16 waves): the large output
+  // tiles halve the LDS-DMA / L2 traffic per MFMA of the compute-bound (long-K) grad-weights
   const int ns = (cfg / 10) % 10 == 2 ? 3 : 2;
-  cfg %= 10;
+  cfg = cfg % 10 + 10 * ((cfg / 100) % 10);
   auto g = static_cast<const uint16_t*>(G);
   auto x = static_cast<const uint16_t*>(X);
   if (cfg <= 0) {
     const bool n2 = N % 128 == 0, k2 = K % 128 == 0;
     cfg = n2 && k2 ? 7 : (n2 ? 2 : (k2 ? 3 : 1));
   }
-  static const int cfg_bn[9] = {64, 64, 128, 64, 128, 256, 64, 128, 64};
-  static const int cfg_bk[9] = {64, 64, 64, 128, 128, 64, 256, 128, 64};
-  if (cfg > 8 || N % cfg_bn[cfg] != 0 || K % cfg_bk[cfg] != 0) cfg = 1;   // tiles must divide N and K
+  static const int cfg_bn[13] = {64, 64, 128, 64, 128, 256, 64, 128, 64, 256, 64, 128, 256};
+  static const int cfg_bk[13] = {64, 64, 64, 128, 128, 64, 256, 128, 64, 128, 64, 256, 256};
+  if (cfg > 12 || cfg == 10 || N % cfg_bn[cfg] != 0 || K % cfg_bk[cfg] != 0) cfg = 1;   // tiles must divide N and K
   switch (cfg) {
+    case 9: launch_tn_any<4, 2, 1, GATHER>(g, ldg, x, ldx, W, ldw, M, N, K, splits, ns, geo, stream); break;
+    case 11: launch_tn_any<2, 4, 1, GATHER>(g, ldg, x, ldx, W, ldw, M, N, K, splits, ns, geo, stream); break;
+    case 12: launch_tn_any<4, 4, 1, GATHER>(g, ldg, x, ldx, W, ldw, M, N, K, splits, ns, geo, stream); break;
     case 2: launch_tn_any<2, 1, 2, GATHER>(g, ldg, x, ldx, W, ldw, M, N, K, splits, ns, geo, stream); break;
     case 3: launch_tn_any<1, 2, 2, GATHER>(g, ldg, x, ldx, W, ldw, M, N, K, splits, ns, geo, stream); break;
     case 4: launch_tn_any<2, 2, 1, GATHER>(g, ldg, x, ldx, W, ldw, M, N, K, splits, ns, geo, stream); break;

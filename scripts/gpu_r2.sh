@@ -32,6 +32,27 @@ for s in ${STEPS:-new all smoke bench}; do
            done ;;
     marker) export GKSGD_ROCTX=1; step marker 600 rocprofv3 --marker-trace --kernel-trace --stats --output-format csv -d $OUT/marker -o run -- \
            python3 bench.py ${MARKER_ARGS:---model bert --steps 4 --warmup 4 --threshold 28000000}; unset GKSGD_ROCTX ;;
+    convs) step convs_ours 900 python bench/convs.py --ours --json-out $OUT/convs_ours.json ;;
+    ctr) CTR_OUT=$OUT/ctr_wgrad3 PROBE_ARGS="--op wgrad3 --cfg ${TN_CFG:-27} --C 256 --H 14" bash scripts/gemm_counters.sh \
+           > $OUT/ctr_wgrad3.log 2>&1; tail -40 $OUT/ctr_wgrad3.log
+         CTR_OUT=$OUT/ctr_conv3 PROBE_ARGS="--op conv --cfg ${NT_CFG:-124} --C 256 --H 14" bash scripts/gemm_counters.sh \
+           > $OUT/ctr_conv3.log 2>&1; tail -40 $OUT/ctr_conv3.log ;;
+    plan) step plan_bert 600 python bench.py --model bert --steps 20 --warmup 10 --planner mgs --plan-world 8 \
+           --json-out $OUT/plan_bert.json
+          step bert16 400 python bench.py --model bert --steps 20 --warmup 10 --threshold 7000000 \
+           --json-out $OUT/bert16.json ;;
+    allbench) for spec in ${ALLBENCH:-"resnet50" "vgg16" "lstm" "bert" "fcn5net" "resnet20 --batch-size 1024" \
+                  "resnet20 --batch-size 32" "resnet50 --compressor gaussian_cal" "vgg16 --compressor gaussian_cal" \
+                  "bert --compressor gaussian_cal" "lstm --compressor gaussian_cal" "bert --threshold 7000000" \
+                  "resnet50 --dense"}; do
+             tag=$(echo $spec | tr ' ' '_' | tr -d '-')
+             step ab_$tag 400 python bench.py --model $spec --steps 20 --warmup 10 --json-out $OUT/ab_$tag.json
+           done ;;
+    retune) for m in ${RETUNE_MODELS:-resnet50 bert vgg16 resnet20 lstm}; do
+              export GKSGD_GEMM_RETUNE=1 GKSGD_GEMM_SAVE=$OUT/choices_$m.json
+              step retune_$m 600 python bench.py --model $m --steps 20 --warmup 10 --json-out $OUT/retune_$m.json
+              unset GKSGD_GEMM_RETUNE GKSGD_GEMM_SAVE
+            done ;;
     kern) step kernels 600 python bench/kernels.py --only ${KERN_ONLY:-round2,fit} --fit-out $OUT/perf_model_mi355x.json \
            --json-out $OUT/kernels.json ;;
     prof) step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \

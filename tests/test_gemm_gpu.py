@@ -50,8 +50,8 @@ def test_gemm_nt_strided_rows_and_grid(g):
 
 
 @pytest.mark.parametrize("M,N,K", [(1000, 64, 64), (4096, 256, 64), (777, 128, 192), (2500, 512, 256),
-                                   (130, 64, 128), (5000, 128, 512)])
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8, 21, 27])
+                                   (130, 64, 128), (5000, 128, 512), (3001, 256, 256)])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8, 21, 27, 9, 29, 101, 121, 102, 122])
 @pytest.mark.parametrize("splits", [0, 1, 7])
 def test_gemm_tn_acc(g, M, N, K, cfg, splits):
     torch.manual_seed(M * 3 + N + K)
@@ -88,7 +88,8 @@ def test_conv_nt(g, N, C, H, Co, k, s, p, cfg):
 
 @pytest.mark.parametrize("N,C,H,Co,k,s,p", [(2, 64, 9, 64, 3, 1, 1), (3, 128, 7, 64, 3, 2, 1), (2, 64, 14, 128, 3, 2, 1),
                                             (2, 128, 5, 256, 1, 1, 0)])
-@pytest.mark.parametrize("cfg,splits", [(0, 0), (1, 3), (4, 0), (25, 0), (2, 7), (7, 0), (8, 2), (23, 0)])
+@pytest.mark.parametrize("cfg,splits", [(0, 0), (1, 3), (4, 0), (25, 0), (2, 7), (7, 0), (8, 2), (23, 0), (29, 0),
+                                        (121, 3), (102, 0)])
 def test_conv_tn_acc(g, N, C, H, Co, k, s, p, cfg, splits):
     import torch.nn.functional as F
     torch.manual_seed(N * 7 + C + H + Co)
