@@ -438,11 +438,14 @@ int launch_nt_any(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb
 // --------------------------------------------------------------------------
 // WS waves split the 64*WS pixel rows of a stage for the same output tile;
 // their partial sums are combined through LDS before the atomics.
-template <int WN, int WK, int WS, int NS_>
+// MSN: 64-row groups of the wave tile along N (1: 64x64 per wave, 2: 128x64 --
+// 25% fewer LDS reads per MFMA and twice the work per staged G row)
+template <int WN, int WK, int WS, int NS_, int MSN = 1>
 struct TnCfg {
   static constexpr int NW = WN * WK * WS;
   static constexpr int THREADS = 64 * NW;
-  static constexpr int BN = 64 * WN;                 // output rows (G columns)
+  static constexpr int WTN = 64 * MSN;               // wave tile rows (G columns)
+  static constexpr int BN = WTN * WN;                // output rows (G columns)
   static constexpr int BK = 64 * WK;                 // output cols (X columns)
   static constexpr int ROWS = 64 * WS;               // pixel rows per stage
   static constexpr int GROW = BN * 2;                // bytes per staged G row
@@ -458,7 +461,7 @@ struct TnCfg {
   static_assert(LPW <= 63, "wait_vmcnt range");
   static_assert(GINSTS % NW == 0, "G rows split evenly over the waves");
   static constexpr int LPWG = GINSTS / NW;           // G-row instructions per wave (j < LPWG)
-  static_assert((WS - 1) * WN * WK * 16384 <= LDS, "reduction scratch");
+  static_assert((WS - 1) * WN * WK * MSN * 16384 <= LDS, "reduction scratch");
 };
 
 // a / d for small a (< 2^22): float reciprocal, one correction step
@@ -525,17 +528,25 @@ __device__ __forceinline__ bf16x8 tr_pair(uint32_t a0, uint32_t a1, int kk) {
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-// lgkmcnt(0) tied to the 8 fragments of one k-step
+// lgkmcnt(0) tied to the fragments of one k-step
+template <int MSN>
 __device__ __forceinline__ void tr_sync(bf16x8* a, bf16x8* b) {
-  asm volatile("s_waitcnt lgkmcnt(0)"
-               : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]));
+  if (MSN == 1) {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]));
+  } else {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7]),
+                   "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]));
+  }
 }
 
-template <int WN, int WK, int WS, int NS, bool GATHER>
-__global__ void __launch_bounds__(64 * WN * WK * WS) __attribute__((amdgpu_waves_per_eu(2)))
+template <int WN, int WK, int WS, int NS, bool GATHER, int MSN = 1>
+__global__ void __launch_bounds__(64 * WN * WK * WS) __attribute__((amdgpu_waves_per_eu(MSN > 1 ? 1 : 2)))
 gemm_tn_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __restrict__ X, int64_t ldx,
                float* __restrict__ W, int64_t ldw, int64_t M, int64_t rows_per_split, ConvGeo geo) {
-  using Cfg = TnCfg<WN, WK, WS, NS>;
+  using Cfg = TnCfg<WN, WK, WS, NS, MSN>;
+  constexpr int NF = 4 * MSN;                        // G fragments (16 rows each) per wave
   constexpr int LPW = Cfg::LPW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
@@ -633,9 +644,9 @@ gemm_tn_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __re
     }
   };
 
-  f32x4 acc[4][4];
+  f32x4 acc[NF][4];
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int a = 0; a < NF; ++a)
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -644,16 +655,20 @@ gemm_tn_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __re
   // k-step (rows + 32) is the same addresses + 32 rows -- an immediate offset
   // -- and a new stage only adds its (uniform) base: 16 adds per stage instead
   // of the full address arithmetic per read.
-  uint32_t goff[4][2], xoff[4][2];
+  uint32_t goff[NF][2], xoff[4][2];
   {
     const int g = lane >> 4, li = lane & 15;
     const int q = li >> 2, p = li & 3;
     const int ra = ws * 64 + 8 * g + q, rb = ra + 4;
 #pragma unroll
-    for (int s2 = 0; s2 < 4; ++s2) {
-      const int gc = wn * 64 + s2 * 16 + 4 * p, xc = wk * 64 + s2 * 16 + 4 * p;
+    for (int s2 = 0; s2 < NF; ++s2) {
+      const int gc = wn * Cfg::WTN + s2 * 16 + 4 * p;
       goff[s2][0] = ra * Cfg::GROW + ((((gc >> 3) ^ tr_swz<Cfg::GROW>(ra)) << 4) | ((gc & 7) << 1));
       goff[s2][1] = rb * Cfg::GROW + ((((gc >> 3) ^ tr_swz<Cfg::GROW>(rb)) << 4) | ((gc & 7) << 1));
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const int xc = wk * 64 + s2 * 16 + 4 * p;
       xoff[s2][0] = Cfg::GBYTES + ra * Cfg::XROW + ((((xc >> 3) ^ tr_swz<Cfg::XROW>(ra)) << 4) | ((xc & 7) << 1));
       xoff[s2][1] = Cfg::GBYTES + rb * Cfg::XROW + ((((xc >> 3) ^ tr_swz<Cfg::XROW>(rb)) << 4) | ((xc & 7) << 1));
     }
@@ -670,37 +685,37 @@ gemm_tn_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __re
     __builtin_amdgcn_sched_barrier(0);
     if (t + NS - 1 < T) stage(t + NS - 1);
     const uint32_t sb = lds0 + (uint32_t)((t % NS) * Cfg::STAGE);
-    uint32_t ga[4][2], xa[4][2];
+    uint32_t ga[NF][2], xa[4][2];
+#pragma unroll
+    for (int s2 = 0; s2 < NF; ++s2)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) ga[s2][h] = sb + goff[s2][h];
 #pragma unroll
     for (int s2 = 0; s2 < 4; ++s2)
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        ga[s2][h] = sb + goff[s2][h];
-        xa[s2][h] = sb + xoff[s2][h];
-      }
+      for (int h = 0; h < 2; ++h) xa[s2][h] = sb + xoff[s2][h];
     const int64_t m0 = mbeg + (int64_t)t * Cfg::ROWS + ws * 64;
     const bool tail = m0 + 64 > mend;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 gv[4], xv[4];
+      bf16x8 gv[NF], xv[4];
 #pragma unroll
-      for (int s2 = 0; s2 < 4; ++s2) {
-        gv[s2] = tr_pair<32 * Cfg::GROW>(ga[s2][0], ga[s2][1], kk);
-        xv[s2] = tr_pair<32 * Cfg::XROW>(xa[s2][0], xa[s2][1], kk);
-      }
-      tr_sync(gv, xv);
+      for (int s2 = 0; s2 < NF; ++s2) gv[s2] = tr_pair<32 * Cfg::GROW>(ga[s2][0], ga[s2][1], kk);
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) xv[s2] = tr_pair<32 * Cfg::XROW>(xa[s2][0], xa[s2][1], kk);
+      tr_sync<MSN>(gv, xv);
       if (tail) {  // rows past this split's end contribute nothing
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int64_t m = m0 + kk * 32 + 8 * (lane >> 4) + j;
           if (m >= mend) {
 #pragma unroll
-            for (int s2 = 0; s2 < 4; ++s2) gv[s2][j] = 0;
+            for (int s2 = 0; s2 < NF; ++s2) gv[s2][j] = 0;
           }
         }
       }
 #pragma unroll
-      for (int ns = 0; ns < 4; ++ns)
+      for (int ns = 0; ns < NF; ++ns)
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks)
           acc[ns][ks] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gv[ns], xv[ks], acc[ns][ks], 0, 0, 0);
@@ -712,20 +727,20 @@ gemm_tn_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __re
     const int slot = wn * WK + wk;
     if (ws > 0) {
 #pragma unroll
-      for (int ns = 0; ns < 4; ++ns)
+      for (int ns = 0; ns < NF; ++ns)
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks)
-          red[(((ws - 1) * WN * WK + slot) * 16 + ns * 4 + ks) * 64 + lane] = acc[ns][ks];
+          red[(((ws - 1) * WN * WK + slot) * 4 * NF + ns * 4 + ks) * 64 + lane] = acc[ns][ks];
     }
     __syncthreads();
     if (ws == 0) {
 #pragma unroll
       for (int w2 = 1; w2 < WS; ++w2)
 #pragma unroll
-        for (int ns = 0; ns < 4; ++ns)
+        for (int ns = 0; ns < NF; ++ns)
 #pragma unroll
           for (int ks = 0; ks < 4; ++ks) {
-            const f32x4 v = red[(((w2 - 1) * WN * WK + slot) * 16 + ns * 4 + ks) * 64 + lane];
+            const f32x4 v = red[(((w2 - 1) * WN * WK + slot) * 4 * NF + ns * 4 + ks) * 64 + lane];
             acc[ns][ks] += v;
           }
     }
@@ -734,22 +749,22 @@ gemm_tn_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __re
   // D[i = n][j = c]: lane holds column c = .. + (lane&15), rows n = .. + 4*(lane>>4) + r
   const int fr = lane & 15, fq = lane >> 4;
 #pragma unroll
-  for (int ns = 0; ns < 4; ++ns)
+  for (int ns = 0; ns < NF; ++ns)
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       const int c = c0 + wk * 64 + ks * 16 + fr;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int n = n0 + wn * 64 + ns * 16 + fq * 4 + r;
+        const int n = n0 + wn * Cfg::WTN + ns * 16 + fq * 4 + r;
         atomicAdd(W + (int64_t)n * ldw + c, acc[ns][ks][r]);
       }
     }
 }
 
-template <int WN, int WK, int WS, int NS, bool GATHER>
+template <int WN, int WK, int WS, int NS, bool GATHER, int MSN = 1>
 void launch_tn(const uint16_t* G, int64_t ldg, const uint16_t* X, int64_t ldx, float* W, int64_t ldw, int64_t M,
                int N, int K, int splits, const ConvGeo& geo, hipStream_t stream) {
-  using Cfg = TnCfg<WN, WK, WS, NS>;
+  using Cfg = TnCfg<WN, WK, WS, NS, MSN>;
   const int tiles = (N / Cfg::BN) * (K / Cfg::BK);
   if (splits <= 0) {
     // Whole rounds of the chip: one 8-wave block per CU at 2 waves / SIMD
@@ -771,11 +786,11 @@ void launch_tn(const uint16_t* G, int64_t ldg, const uint16_t* X, int64_t ldx, f
   const int64_t nsplit = (M + rows - 1) / rows;
   dim3 grid((unsigned)(N / Cfg::BN), (unsigned)(K / Cfg::BK), (unsigned)nsplit);
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_kernel<WN, WK, WS, NS, GATHER>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_kernel<WN, WK, WS, NS, GATHER, MSN>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL((gemm_tn_kernel<WN, WK, WS, NS, GATHER>), grid, dim3(Cfg::THREADS), Cfg::LDS, stream, G, ldg, X, ldx, W, ldw,
+  hipLaunchKernelGGL((gemm_tn_kernel<WN, WK, WS, NS, GATHER, MSN>), grid, dim3(Cfg::THREADS), Cfg::LDS, stream, G, ldg, X, ldx, W, ldw,
                      M, rows, geo);
 }
 
@@ -827,12 +842,12 @@ int conv_nt_bf16(const void* X, const void* zero, int H, int W, int C, int OH, i
                            stream);
 }
 
-template <int WN, int WK, int WS, bool GATHER>
+template <int WN, int WK, int WS, bool GATHER, int MSN = 1>
 void launch_tn_any(const uint16_t* G, int64_t ldg, const uint16_t* X, int64_t ldx, float* W, int64_t ldw, int64_t M,
                    int N, int K, int splits, int ns, const ConvGeo& geo, hipStream_t stream) {
-  if (ns == 3 && TnCfg<WN, WK, WS, 3>::LDS <= 160 * 1024)
-    launch_tn<WN, WK, WS, 3, GATHER>(G, ldg, X, ldx, W, ldw, M, N, K, splits, geo, stream);
-  else launch_tn<WN, WK, WS, 2, GATHER>(G, ldg, X, ldx, W, ldw, M, N, K, splits, geo, stream);
+  if (ns == 3 && TnCfg<WN, WK, WS, 3, MSN>::LDS <= 160 * 1024)
+    launch_tn<WN, WK, WS, 3, GATHER, MSN>(G, ldg, X, ldx, W, ldw, M, N, K, splits, geo, stream);
+  else launch_tn<WN, WK, WS, 2, GATHER, MSN>(G, ldg, X, ldx, W, ldw, M, N, K, splits, geo, stream);
 }
 
 template <bool GATHER>
@@ -843,6 +858,9 @@ void tn_dispatch(const void* G, int64_t ldg, const void* X, int64_t ldx, float* 
   // 1 (1,1,4)  2 (2,1,2)  3 (1,2,2)  4 (2,2,1)  5 (4,1,1)  6 (1,4,1)  7 (2,2,2)  8 (1,1,2)
   // 9 (4,2,1) 256x128  11 (2,4,1) 128x256  12 (4,4,1) 256x256 (16 waves): the large output
   // tiles halve the LDS-DMA / L2 traffic per MFMA of the compute-bound (long-K) grad-weights
+  // 128x64 per wave (MSN 2, one wave per SIMD to fit 340-460 VGPRs) measured 1.3-3x slower than
+  // the 64x64 tiles on every BERT / ResNet-50 grad-weight shape (profiles/r02_tn_probe.json), so
+  // no tile instantiates it; the template parameter stays for future occupancy experiments.
   const int ns = (cfg / 10) % 10 == 2 ? 3 : 2;
   cfg = cfg % 10 + 10 * ((cfg / 100) % 10);
   auto g = static_cast<const uint16_t*>(G);
