@@ -121,6 +121,19 @@ class ResNet(nn.Module):
         self.bn1.twin = True
         for b in blocks[:-1]:
             (b.bn3 if isinstance(b, Bottleneck) else b.bn2).twin = True
+        # Backward fusion (ops/bn.py BnLink): a BN whose output has exactly one
+        # convolution consumer lets that conv's grad-input GEMM produce the
+        # ReLU-masked gradient and the BN's reduction partials.  Inside a block
+        # that is bn1 -> conv2 (and bn2 -> conv3); a block output feeds the next
+        # block's conv1 and, through the shortcut, the next block's last BN, which
+        # hands its residual gradient over -- not a downsample conv, whose
+        # gradient would only arrive after conv1's backward.
+        for i, b in enumerate(blocks):
+            b.bn1.bwd_link = True
+            if isinstance(b, Bottleneck):
+                b.bn2.bwd_link = True
+            if i + 1 < len(blocks) and blocks[i + 1].downsample is None:
+                (b.bn3 if isinstance(b, Bottleneck) else b.bn2).bwd_link = True
         if zero_init_residual:
             for m in self.modules():
                 if isinstance(m, Bottleneck):

@@ -39,10 +39,38 @@ def _grad_pair(grads, like):
     return (out + [None, None])[:2]
 
 
+class BnLink:
+    """Hand-off between a fused BN and the convolution that consumes its output
+    (its only consumer, guaranteed by the model wiring, ``BNAct.bwd_link``).
+
+    The consumer's grad-input GEMM runs the BN-backward epilogue
+    (csrc/kernels/gemm.hip ``BnBwd``): it writes ``dz`` = ReLU-masked
+    (dy + dy2) instead of dy and the per-channel partials of sum(dz) and
+    sum(dz * h), so the BN backward skips its reduction pass and only
+    finalizes + applies (``bn_act_backward_pre``).  For a twin output (ResNet
+    block output: next conv1 + shortcut) the shortcut's gradient dy2 must be
+    known when the conv1 grad-input runs: the residual consumer (the next
+    block's last BN, which runs its backward first) stores it here.
+    """
+
+    __slots__ = ("h", "mask", "twin", "dy2", "dz", "part")
+
+    def __init__(self):
+        self.h = self.mask = self.dy2 = self.dz = self.part = None
+        self.twin = False
+
+    def ready(self) -> bool:
+        """Can the consumer's grad-input fuse the BN-backward reduction now?"""
+        return self.h is not None and (not self.twin or self.dy2 is not None)
+
+    def clear(self) -> None:
+        self.h = self.mask = self.dy2 = self.dz = self.part = None
+
+
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, relu, direct=None,
-                nbt=None, twin=False, pre=None):
+                nbt=None, twin=False, pre=None, link=None, res_link=None):
         # direct = (gw_view, gb_view): weight/bias gradients are accumulated
         # straight into the optimizer's fp32 arena by the backward kernel and
         # None is returned for them, so AccumulateGrad launches nothing (its
@@ -72,14 +100,45 @@ class _BNActFn(torch.autograd.Function):
         ctx.relu = bool(relu)
         ctx.has_res = residual is not None
         ctx.save_for_backward(x, mask, weight, stats[0], stats[1])
+        # link: this BN's output feeds one conv that may fuse our backward
+        # reduction; res_link: our residual came from a linked twin BN, which
+        # needs our residual gradient before its consumer's grad-input runs
+        ctx.link = link
+        ctx.res_link = res_link
+        if link is not None and x.dtype == torch.bfloat16:
+            link.h, link.mask, link.twin = x, mask, bool(twin)
         return (y, y.view_as(y)) if twin else y
 
     @staticmethod
     def backward(ctx, *grads):
         x, mask, weight, mean, invstd = ctx.saved_tensors
+        link, res_link = ctx.link, ctx.res_link
+        ctx.link = ctx.res_link = None
+        gw, gb = ctx.direct if ctx.direct is not None else (None, None)
+        if link is not None and link.part is not None:
+            # the consumer conv's grad-input epilogue produced dz (masked, twin-summed)
+            # and its reduction partials: finalize + apply only
+            dz = grads[0]
+            if dz is None or dz.data_ptr() != link.dz.data_ptr():
+                raise RuntimeError("BNAct bwd_link: the linked output had another consumer")
+            part, rows = link.part
+            link.clear()
+            dx = torch.empty_like(x, memory_format=_CL)
+            g = torch.empty(2, x.shape[1], dtype=torch.float32, device=x.device)
+            _ops().bn_act_backward_pre(dz, x, dx, weight, mean, invstd, g[0], g[1], part, rows, gw, gb)
+            dres = dz if ctx.has_res and ctx.needs_input_grad[1] else None
+            if res_link is not None and dres is not None:
+                res_link.dy2 = dres
+            if ctx.direct is not None:
+                return (dx, dres) + (None,) * 13
+            dgamma = g[0] if weight is not None and ctx.needs_input_grad[2] else None
+            dbeta = g[1] if ctx.needs_input_grad[3] else None
+            return (dx, dres, dgamma, dbeta) + (None,) * 11
+        if link is not None:
+            link.clear()
         dy, dy2 = _grad_pair(grads, x)
         if dy is None:
-            return (None,) * 13
+            return (None,) * 15
         C = x.shape[1]
         M = x.numel() // C
         dx = torch.empty_like(x, memory_format=_CL)
@@ -87,13 +146,14 @@ class _BNActFn(torch.autograd.Function):
         g = torch.empty(2, C, dtype=torch.float32, device=x.device)
         ws = torch.empty(int(_ops().bn_workspace_floats(M, C, x.element_size())), dtype=torch.float32,
                          device=x.device)
-        gw, gb = ctx.direct if ctx.direct is not None else (None, None)
         _ops().bn_act_backward(dy, mask, x, dx, dres, weight, mean, invstd, g[0], g[1], ws, ctx.relu, gw, gb, dy2)
+        if res_link is not None and dres is not None:
+            res_link.dy2 = dres
         if ctx.direct is not None:
-            return dx, dres, None, None, None, None, None, None, None, None, None, None, None
+            return (dx, dres) + (None,) * 13
         dgamma = g[0] if weight is not None and ctx.needs_input_grad[2] else None
         dbeta = g[1] if ctx.needs_input_grad[3] else None
-        return dx, dres, dgamma, dbeta, None, None, None, None, None, None, None, None, None
+        return (dx, dres, dgamma, dbeta) + (None,) * 11
 
 
 class _BNReLUPoolFn(torch.autograd.Function):
@@ -170,7 +230,7 @@ class BNAct(nn.BatchNorm2d):
 
     def __init__(self, num_features: int, act: Optional[str] = None, eps: float = 1e-5, momentum: float = 0.1,
                  affine: bool = True, track_running_stats: bool = True, fused: bool = True,
-                 pool: Optional[tuple] = None, twin: bool = False):
+                 pool: Optional[tuple] = None, twin: bool = False, bwd_link: bool = False):
         super().__init__(num_features, eps=eps, momentum=momentum, affine=affine,
                          track_running_stats=track_running_stats)
         assert act in (None, "relu")
@@ -182,6 +242,10 @@ class BNAct(nn.BatchNorm2d):
         # gradients the fused backward sums on load (ResNet block outputs feed
         # both the next conv1 and the next shortcut).
         self.twin = twin
+        # bwd_link: the (main) output is consumed by exactly one FastConv2d, which
+        # may fuse this BN's backward reduction into its grad-input GEMM (BnLink);
+        # set by model code that guarantees the single consumer.
+        self.bwd_link = bwd_link
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, stats=None) -> torch.Tensor:
         """``stats``: optional (partials, rows) of x's batch statistics reduced
@@ -204,8 +268,16 @@ class BNAct(nn.BatchNorm2d):
                                            self.eps, pool, direct, nbt, self.twin)
             if stats is not None and (stats[0].shape[2] != x.shape[1] or x.dtype != torch.bfloat16):
                 stats = None
-            return _BNActFn.apply(x, residual, self.weight, self.bias, self.running_mean, self.running_var, mom,
-                                  self.eps, relu, direct, nbt, self.twin, stats)
+            link = BnLink() if self.bwd_link and torch.is_grad_enabled() and x.dtype == torch.bfloat16 else None
+            res_link = getattr(residual, "_gk_res_link", None) if residual is not None else None
+            out = _BNActFn.apply(x, residual, self.weight, self.bias, self.running_mean, self.running_var, mom,
+                                 self.eps, relu, direct, nbt, self.twin, stats, link, res_link)
+            if link is not None:
+                main = out[0] if self.twin else out
+                main._gk_bn_link = link
+                if self.twin:
+                    out[1]._gk_res_link = link
+            return out
         out = super().forward(x)
         if residual is not None:
             out = out + residual

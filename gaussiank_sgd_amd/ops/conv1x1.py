@@ -217,6 +217,46 @@ def _dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int) -> torch.Tensor:
     return dx
 
 
+def _dgrad_bn(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, link) -> torch.Tensor:
+    """Grad-input with the producing BatchNorm's backward reduction fused into
+    the epilogue (gemm.hip BnBwd; ops/bn.py BnLink): returns dz = ReLU-masked
+    (dX + dy2) and leaves the partials in ``link.part``.  Stride 1 only; the
+    caller checks ``link.ready()``."""
+    N, C, H, W, K, k, p, OH, OW = _geom(x_shape, w, s)
+    g = _g()
+    M = N * H * W
+    dz = torch.empty(x_shape, dtype=torch.bfloat16, device=dy.device, memory_format=_CL)
+    st = torch.empty(2, min(1280, (M + 63) // 64), C, dtype=torch.float32, device=dy.device)
+    h, mask, dy2 = link.h, link.mask, link.dy2
+    if k == 1:
+        DY, DZ = _rows(dy), _rows(dz)
+        Wt = w.reshape(K, C).t().contiguous()
+        H2 = _rows(h)
+        D2 = _rows(dy2) if dy2 is not None else None
+        run = lambda c, mb: g.gemm_nt(DY, Wt, DZ, c, mb, st, None, H2, D2, mask)  # noqa: E731
+    else:
+        wf = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=_CL)
+        z = _zero(dy.device)
+        run = lambda c, mb: g.conv_nt(dy, wf, dz, z, 1, p, c, mb, st, None, h, dy2, mask)  # noqa: E731
+    # 64x64-per-wave tiles (cfg digit 1-4) carry the BN-backward epilogue
+    cands = [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in _NT_CFGS if c % 10 <= 4 for mb in _NT_GRIDS]
+    ch = _pick(("dgrad_bn", N, C, H, W, K, k, s, dy2 is not None), cands)
+    rows = run(ch[1], ch[2])
+    link.part = (st, int(rows))
+    link.dz = dz
+    return dz
+
+
+def _bn_fusable(link, s: int, dgrad_key: tuple) -> bool:
+    """Fuse the producing BN's backward reduction into this grad-input?  Only
+    when its inputs are ready and the tuned plain grad-input is the HIP kernel
+    (a MIOpen choice means the HIP GEMM is the slower one for this shape)."""
+    if link is None or s != 1 or os.environ.get("GKSGD_BN_LINK", "1") == "0" or not link.ready():
+        return False
+    ch = _choices.get(dgrad_key)
+    return ch is None or ch[0] == "hip"
+
+
 def _wgrad_into(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, s: int, out_f32: torch.Tensor) -> None:
     """out_f32 ([K, C, k, k] channels-last fp32) += dW."""
     N, C, H, W, K, k, p, OH, OW = _geom(x.shape, w, s)
@@ -249,7 +289,7 @@ class _FastConvFn(torch.autograd.Function):
     fp32 arena in the backward and None is returned for it."""
 
     @staticmethod
-    def forward(ctx, x, param, w_bf16, sink, stride, stats_box=None, bias=None, bias_sink=None):
+    def forward(ctx, x, param, w_bf16, sink, stride, stats_box=None, bias=None, bias_sink=None, link=None):
         if x.dtype != torch.bfloat16:
             x = x.to(torch.bfloat16)
         x = x.contiguous(memory_format=_CL)
@@ -262,6 +302,7 @@ class _FastConvFn(torch.autograd.Function):
         ctx.has_bias = bias is not None
         ctx.stride = stride
         ctx.param_dtype = param.dtype
+        ctx.link = link
         ctx.save_for_backward(x, w)
         return y
 
@@ -270,7 +311,15 @@ class _FastConvFn(torch.autograd.Function):
         x, w = ctx.saved_tensors
         s = ctx.stride
         dy = dy.to(torch.bfloat16).contiguous(memory_format=_CL)
-        dx = _dgrad(dy, w, x.shape, s) if ctx.needs_input_grad[0] else None
+        link, ctx.link = ctx.link, None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            N, C, H, W = x.shape
+            key = ("dgrad", N, C, H, W, w.shape[0], w.shape[2], s)
+            if _bn_fusable(link, s, key):
+                dx = _dgrad_bn(dy, w, x.shape, s, link)
+            else:
+                dx = _dgrad(dy, w, x.shape, s)
         gparam = None
         if ctx.needs_input_grad[1]:
             sink = ctx.sink
@@ -293,7 +342,7 @@ class _FastConvFn(torch.autograd.Function):
                 bs(db)          # into the optimizer's fp32 arena (shadow path)
             else:
                 gbias = db
-        return dx, gparam, None, None, None, None, gbias, None
+        return dx, gparam, None, None, None, None, gbias, None, None
 
 
 class FastConv2d(nn.Conv2d):
@@ -326,7 +375,8 @@ class FastConv2d(nn.Conv2d):
                 sink = None
             if not torch.is_grad_enabled() or self.bias is None or not self.bias.requires_grad:
                 bsink = None
-            return _FastConvFn.apply(x, self.weight, w_bf16, sink, self.stride[0], box, self.bias, bsink)
+            link = getattr(x, "_gk_bn_link", None)
+            return _FastConvFn.apply(x, self.weight, w_bf16, sink, self.stride[0], box, self.bias, bsink, link)
         slow = getattr(self, "_gk_slow", None)
         return slow(x) if slow is not None else super().forward(x)
 

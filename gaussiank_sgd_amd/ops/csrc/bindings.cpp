@@ -453,6 +453,30 @@ void bn_act_backward(at::Tensor dy, c10::optional<at::Tensor> mask, at::Tensor x
                       opt_f32_mut(gb_acc), cur_stream(x));
 }
 
+void bn_act_backward_pre(at::Tensor dz, at::Tensor x, at::Tensor dx, c10::optional<at::Tensor> w, at::Tensor mean,
+                         at::Tensor invstd, at::Tensor dgamma, at::Tensor dbeta, at::Tensor part, int64_t rows,
+                         c10::optional<at::Tensor> gw_acc, c10::optional<at::Tensor> gb_acc) {
+  check_cl(dz, "dz");
+  check_cl(x, "x");
+  check_cl(dx, "dx");
+  const int64_t C = channels_of(x);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && dz.scalar_type() == at::kBFloat16 &&
+                  dx.scalar_type() == at::kBFloat16 && dz.numel() == x.numel() && dx.numel() == x.numel(),
+              "bn_act_backward_pre: bf16 dz / x / dx of one shape");
+  TORCH_CHECK(gk::bn_supported((int)C, 2), "channel count not supported by the fused kernel");
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() == 3 &&
+                  part.size(0) == 2 && part.size(2) == C && rows > 0 && rows <= part.size(1),
+              "part must be fp32 [2, rows, C] partials with 0 < rows <= part.size(1)");
+  for (const at::Tensor* t : {&mean, &invstd, &dgamma, &dbeta})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->numel() >= C, "per-channel buffers: fp32[C]");
+  c10::DeviceGuard guard(x.device());
+  const float* ps = part.data_ptr<float>();
+  gk::bn_act_backward_pre(dz.data_ptr(), x.data_ptr(), dx.data_ptr(), M, (int)C, opt_f32(w), mean.data_ptr<float>(),
+                          invstd.data_ptr<float>(), dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), ps,
+                          ps + part.size(1) * C, (int)rows, opt_f32_mut(gw_acc), opt_f32_mut(gb_acc), cur_stream(x));
+}
+
 gk::PoolGeo pool_geo(const at::Tensor& x, const at::Tensor& y, int64_t k, int64_t st, int64_t pad) {
   TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && x.size(0) == y.size(0) && x.size(1) == y.size(1), "pool shapes");
   gk::PoolGeo pg;
@@ -713,8 +737,37 @@ const float* bias_ptr(const c10::optional<at::Tensor>& b, int64_t N) {
   return b->data_ptr<float>();
 }
 
+// BatchNorm-backward epilogue operands (gemm.hip BnBwd): all-or-nothing on h
+bool bn_bwd_args(const c10::optional<at::Tensor>& h, const c10::optional<at::Tensor>& dy2,
+                 const c10::optional<at::Tensor>& mask, int64_t M, int64_t N,
+                 int64_t ldc, bool has_stats, gk::BnBwdArgs* out) {
+  if (!h.has_value() || !h->defined()) return false;
+  TORCH_CHECK(has_stats, "BN-backward epilogue needs the stats partials buffer");
+  auto rows_ok = [&](const at::Tensor& t, const char* what) {
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.numel() == M * N &&
+                    (t.dim() == 2 ? t.stride(0) == ldc && t.stride(1) == 1
+                                  : t.is_contiguous(at::MemoryFormat::ChannelsLast) && ldc == N),
+                what, " must be bf16 with C's shape and row stride");
+  };
+  rows_ok(*h, "bn h");
+  out->h = static_cast<const uint16_t*>(h->data_ptr());
+  out->dy2 = nullptr;
+  if (dy2.has_value() && dy2->defined()) {
+    rows_ok(*dy2, "bn dy2");
+    out->dy2 = static_cast<const uint16_t*>(dy2->data_ptr());
+  }
+  out->mask = nullptr;
+  if (mask.has_value() && mask->defined()) {
+    TORCH_CHECK(mask->is_cuda() && mask->scalar_type() == at::kByte && mask->numel() >= M * (N / 8),
+                "bn mask must hold M * N / 8 bytes");
+    out->mask = mask->data_ptr<uint8_t>();
+  }
+  return true;
+}
+
 int64_t gemm_nt(at::Tensor A, at::Tensor B, at::Tensor C, int64_t cfg, int64_t max_blocks,
-                c10::optional<at::Tensor> stats, c10::optional<at::Tensor> bias) {
+                c10::optional<at::Tensor> stats, c10::optional<at::Tensor> bias, c10::optional<at::Tensor> bn_h,
+                c10::optional<at::Tensor> bn_dy2, c10::optional<at::Tensor> bn_mask) {
   check_rows(A, "A");
   check_rows(B, "B");
   check_rows(C, "C");
@@ -724,9 +777,13 @@ int64_t gemm_nt(at::Tensor A, at::Tensor B, at::Tensor C, int64_t cfg, int64_t m
   TORCH_CHECK(M > 0, "gemm_nt: empty M");
   int rows = 0;
   float* sp = stats_ptr(stats, N, &rows);
+  gk::BnBwdArgs bn{};
+  const bool has_bn = bn_bwd_args(bn_h, bn_dy2, bn_mask, M, N, C.stride(0), sp != nullptr, &bn);
+  TORCH_CHECK(!has_bn || !bias.has_value() || !bias->defined(), "gemm_nt: bias and BN epilogue are exclusive");
   c10::DeviceGuard guard(A.device());
   return gk::gemm_nt_bf16(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), M, (int)N,
-                          (int)K, (int)cfg, (int)max_blocks, sp, rows, bias_ptr(bias, N), cur_stream(A));
+                          (int)K, (int)cfg, (int)max_blocks, sp, rows, bias_ptr(bias, N), has_bn ? &bn : nullptr,
+                          cur_stream(A));
 }
 
 // W[N, K] += G[M, N]^T . X[M, K]   (fp32 W, float atomics)
@@ -759,7 +816,8 @@ void check_conv(const at::Tensor& x, const at::Tensor& w, const at::Tensor& zero
 }
 
 int64_t conv_nt(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor zero, int64_t stride, int64_t pad, int64_t cfg,
-                int64_t max_blocks, c10::optional<at::Tensor> stats, c10::optional<at::Tensor> bias) {
+                int64_t max_blocks, c10::optional<at::Tensor> stats, c10::optional<at::Tensor> bias,
+                c10::optional<at::Tensor> bn_h, c10::optional<at::Tensor> bn_dy2, c10::optional<at::Tensor> bn_mask) {
   check_conv(x, w, zero);
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
   const int64_t Co = w.size(0), KH = w.size(2), KW = w.size(3);
@@ -772,10 +830,13 @@ int64_t conv_nt(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor zero, int64
   TORCH_CHECK(M > 0 && M < (int64_t(1) << 32), "conv_nt: M out of range");
   int rows = 0;
   float* sp = stats_ptr(stats, Co, &rows);
+  gk::BnBwdArgs bn{};
+  const bool has_bn = bn_bwd_args(bn_h, bn_dy2, bn_mask, M, Co, Co, sp != nullptr, &bn);
+  TORCH_CHECK(!has_bn || !bias.has_value() || !bias->defined(), "conv_nt: bias and BN epilogue are exclusive");
   c10::DeviceGuard guard(x.device());
   return gk::conv_nt_bf16(x.data_ptr(), zero.data_ptr(), (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)stride,
                           (int)pad, (int)KH, (int)KW, w.data_ptr(), y.data_ptr(), M, (int)Co, (int)cfg, (int)max_blocks,
-                          sp, rows, bias_ptr(bias, Co), cur_stream(x));
+                          sp, rows, bias_ptr(bias, Co), has_bn ? &bn : nullptr, cur_stream(x));
 }
 
 // wout: fp32 [Cout, C, KH, KW] channels-last (memory [Cout][KH][KW][C]); += dW
@@ -1033,10 +1094,14 @@ TORCH_LIBRARY(gksgd, m) {
   m.def("cast_bf16(Tensor(a!) dst, Tensor src) -> ()");
   m.def("gemm_supported(int N, int K) -> bool", &gemm_supported);
   m.def("gemm_nt(Tensor A, Tensor B, Tensor(a!) C, int cfg=0, int max_blocks=0, Tensor(b!)? stats=None, "
-        "Tensor? bias=None) -> int");
+        "Tensor? bias=None, Tensor? bn_h=None, Tensor? bn_dy2=None, Tensor? bn_mask=None) -> int");
   m.def("gemm_tn_acc(Tensor G, Tensor X, Tensor(a!) W, int cfg=0, int splits=0) -> ()");
   m.def("conv_nt(Tensor x, Tensor w, Tensor(a!) y, Tensor zero, int stride, int pad, int cfg=0, int max_blocks=0, "
-        "Tensor(b!)? stats=None, Tensor? bias=None) -> int");
+        "Tensor(b!)? stats=None, Tensor? bias=None, Tensor? bn_h=None, Tensor? bn_dy2=None, Tensor? bn_mask=None) "
+        "-> int");
+  m.def("bn_act_backward_pre(Tensor dz, Tensor x, Tensor(a!) dx, Tensor? w, Tensor mean, Tensor invstd, "
+        "Tensor(b!) dgamma, Tensor(c!) dbeta, Tensor part, int rows, Tensor(d!)? gw_acc=None, "
+        "Tensor(e!)? gb_acc=None) -> ()");
   m.def("add_ln_supported(int H) -> bool", &add_ln_supported);
   m.def("add_ln_ws_floats(int R, int H) -> int", &add_ln_ws_floats);
   m.def("add_ln_forward(Tensor a, Tensor x, Tensor? gamma, Tensor? beta, Tensor(a!) y, Tensor(b!) h, "
@@ -1092,6 +1157,7 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("clip_grad_norm", &clip_grad_norm);
   m.impl("bn_act_forward", &bn_act_forward);
   m.impl("bn_act_backward", &bn_act_backward);
+  m.impl("bn_act_backward_pre", &bn_act_backward_pre);
   m.impl("bn_relu_pool_forward", &bn_relu_pool_forward);
   m.impl("bn_relu_pool_backward", &bn_relu_pool_backward);
   m.impl("accum_grad", &accum_grad);

@@ -516,12 +516,16 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_finalize_kernel(const float* __
                                                                  const float* __restrict__ pdg, int gy, int C,
                                                                  float* __restrict__ dbeta, float* __restrict__ dgamma,
                                                                  float* __restrict__ gb_acc,
-                                                                 float* __restrict__ gw_acc) {
+                                                                 float* __restrict__ gw_acc,
+                                                                 const float* __restrict__ cmean = nullptr,
+                                                                 const float* __restrict__ cinvstd = nullptr) {
   double a = 0.0, b = 0.0;
   bool owner;
   int c;
   reduce_partials2(pdb, pdg, gy, C, &a, &b, &owner, &c);
   if (!owner) return;
+  // partials of sum(dz * x) from a GEMM epilogue: sum(dz * xhat) = invstd * (sum(dz x) - mean sum(dz))
+  if (cmean) b = (double)cinvstd[c] * (b - (double)cmean[c] * a);
   dbeta[c] = (float)a;
   dgamma[c] = (float)b;
   // direct-to-arena parameter gradients (AccumulateGrad semantics)
@@ -846,6 +850,21 @@ void bn_act_backward(const void* dy, const void* dy2, const uint8_t* mask, const
   else
     bn_backward_t<float>((const float*)dy, (const float*)dy2, mask, (const float*)x, (float*)dx, (float*)dres, M, C, w,
                          mean, invstd, dgamma, dbeta, ws, relu, gw_acc, gb_acc, s);
+}
+
+// dz (already gated and twin-summed) and its partials sum(dz), sum(dz*(x-mean))
+// [2][gy][C] from the consuming convolution's grad-input epilogue (gemm.hip
+// BnBwd): no reduction pass, only finalize + apply.
+void bn_act_backward_pre(const void* dz, const void* x, void* dx, int64_t M, int C, const float* w,
+                         const float* mean, const float* invstd, float* dgamma, float* dbeta, const float* pdb,
+                         const float* pdg, int gy, float* gw_acc, float* gb_acc, hipStream_t s) {
+  using T = uint16_t;
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(kBlock), 0, s, pdb, pdg, gy, C,
+                     dbeta, dgamma, gb_acc, gw_acc, mean, invstd);
+  const Geo g = make_geo<T>(M, C, kTargetBlocks);
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, DyPlain<T, false, false>, false>), dim3(g.gx, g.gy), dim3(kBlock), 0, s,
+                     DyPlain<T, false, false>{(const T*)dz, nullptr, nullptr}, (const T*)x, (T*)dx, (T*)nullptr, M, C,
+                     g, w, mean, invstd, dbeta, dgamma);
 }
 
 // ---------------------------------------------------------------------------

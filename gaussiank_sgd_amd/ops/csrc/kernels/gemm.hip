@@ -86,6 +86,20 @@ struct ConvGeo {
   const float* bias;      // optional per-output-channel bias (gemm_nt / conv_nt epilogue)
 };
 
+// BatchNorm-backward epilogue (grad-input GEMM of the convolution that consumes
+// a fused BN + ReLU [+ residual] output): instead of the plain gradient dy the
+// kernel stores dz = relu_mask ? bf16(dy) + dy2 : 0 (dy2: the BN output's second
+// consumer's gradient, ResNet shortcut) and reduces per-channel partials
+// sum(dz) and sum(dz * h) (h: the BN input) into `stats`, which is what the BN
+// backward's separate reduction pass would read dy, dy2, h and the mask for.
+// The operands are loaded per output row in the epilogue (transient registers:
+// the main loop's register budget is unchanged).
+struct BnBwd {
+  const uint16_t* h;      // BN input [M, N] (same ld as C); nullptr: plain epilogue
+  const uint16_t* dy2;    // optional second gradient [M, N]
+  const uint8_t* mask;    // optional 1-bit ReLU mask, byte (m, n / 8) at m * (N / 8) + n / 8
+};
+
 __device__ __forceinline__ const uint16_t* conv_row(const uint16_t* X, const ConvGeo& g, int64_t m, int k0,
                                                     int chunk) {
   const int tap = k0 / g.C, c0 = k0 - tap * g.C;
@@ -128,15 +142,20 @@ struct NtCfg {
   static int lds_bytes(int K, int ns) { return ns * STAGE + (BRES ? BN * K * 2 : 0); }
 };
 
-template <int WM, int WN, bool BRES, int NS, bool GATHER, int MSB = 4>
+template <int WM, int WN, bool BRES, int NS, bool GATHER, int MSB = 4, bool BNB = false>
 __global__ void __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(WM * WN >= 8 ? 1 : 2)))
 gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
                uint16_t* __restrict__ C, int64_t ldc, int64_t M, int K, ConvGeo geo, float* __restrict__ stats,
-               int64_t stats_ld) {
+               int64_t stats_ld, BnBwd bb) {
   // stats != nullptr: per-block BatchNorm partials of the (bf16-rounded)
   // output, psum at stats[blockIdx.x * N + n], psq at stats[stats_ld + ...]
-  // (the [gy][C] layout bn_finalize_kernel reduces).
+  // (the [gy][C] layout bn_finalize_kernel reduces).  With bb.h (BN-backward
+  // epilogue, MSB == 4 tiles only) the partials are sum(dz), sum(dz*h); the
+  // finalize centres the second with the mean.
   using Cfg = NtCfg<WM, WN, BRES, MSB>;
+  static_assert(!BNB || MSB == 4, "BN-backward epilogue: 64x64 wave tiles");
+  constexpr bool BNB_OK = BNB;
+  constexpr bool bnb = BNB;
   static_assert(NS == 2 || NS == 3, "stages");
   constexpr int LPW = Cfg::LPW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -275,6 +294,10 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
       ssum[a][b] = ssq[a][b] = 0.f;
       bia[a][b] = geo.bias ? geo.bias[n0 + wn * 64 + a * 16 + fq * 4 + b] : 0.f;
     }
+  // BN-backward epilogue: in the store layout every lane owns 8 consecutive
+  // channels per column pair pr (the same channels for every tile): offset
+  // cofs within the pair's 32 columns
+  const int cofs = (fq & 1) ? 16 + 4 * (fq - 1) : 4 * fq;
   int64_t mt = blockIdx.x;
   for (int t = 0; t < T; ++t) {
     // ops issued after stage(t), in order: NS=2: stores(t-1);
@@ -321,6 +344,21 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
 #pragma unroll
       for (int ms = 0; ms < MSB; ++ms) {
         const int64_t m = mbase + wm * Cfg::WTM + ms * 16 + fr;
+        uint4 eh[2], ed[2];   // BN-backward operands of this row: h, dy2 and the mask byte per pair
+        uint32_t em[2];
+        if (BNB_OK && bnb) {
+#pragma unroll
+          for (int pr = 0; pr < 2; ++pr) {
+            const int n = n0 + wn * 64 + pr * 32 + cofs;
+            eh[pr] = ed[pr] = make_uint4(0u, 0u, 0u, 0u);
+            em[pr] = 0u;
+            if (full || m < M) {
+              eh[pr] = *reinterpret_cast<const uint4*>(bb.h + m * ldc + n);
+              if (bb.dy2) ed[pr] = *reinterpret_cast<const uint4*>(bb.dy2 + m * ldc + n);
+              em[pr] = bb.mask ? (uint32_t)bb.mask[m * (Ntot >> 3) + (n >> 3)] : 0xffu;
+            }
+          }
+        }
 #pragma unroll
         for (int pr = 0; pr < 2; ++pr) {
           const f32x4 va = acc[ms][2 * pr], vb = acc[ms][2 * pr + 1];
@@ -328,7 +366,7 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
           const float* bb = bia[2 * pr + 1];
           const uint32_t a0 = pack_bf16x2(va[0] + ba[0], va[1] + ba[1]), a1 = pack_bf16x2(va[2] + ba[2], va[3] + ba[3]);
           const uint32_t b0 = pack_bf16x2(vb[0] + bb[0], vb[1] + bb[1]), b1 = pack_bf16x2(vb[2] + bb[2], vb[3] + bb[3]);
-          if (stats && (full || m < M)) {   // statistics of the values as stored (bf16)
+          if (stats && !bnb && (full || m < M)) {   // statistics of the values as stored (bf16)
             const uint32_t pk[4] = {a0, a1, b0, b1};
 #pragma unroll
             for (int h = 0; h < 4; ++h) {
@@ -342,8 +380,32 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
           }
           const uint32_t r0 = (uint32_t)__shfl_xor((int)(odd ? a0 : b0), 16, 64);
           const uint32_t r1 = (uint32_t)__shfl_xor((int)(odd ? a1 : b1), 16, 64);
-          const uint4 v = odd ? make_uint4(r0, r1, b0, b1) : make_uint4(a0, a1, r0, r1);
-          const int n = n0 + wn * 64 + pr * 32 + (odd ? 16 + 4 * (fq - 1) : 4 * fq);
+          uint4 v = odd ? make_uint4(r0, r1, b0, b1) : make_uint4(a0, a1, r0, r1);
+          const int n = n0 + wn * 64 + pr * 32 + cofs;
+          if (BNB_OK && bnb) {
+            const uint32_t dv[4] = {v.x, v.y, v.z, v.w};
+            const uint4 e2 = ed[pr], eh4 = eh[pr];
+            const uint32_t d2[4] = {e2.x, e2.y, e2.z, e2.w};
+            const uint32_t hh[4] = {eh4.x, eh4.y, eh4.z, eh4.w};
+            const uint32_t bits = em[pr];
+            uint32_t o[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              float lo = __uint_as_float(dv[i] << 16) + __uint_as_float(d2[i] << 16);
+              float hi = __uint_as_float(dv[i] & 0xffff0000u) + __uint_as_float(d2[i] & 0xffff0000u);
+              lo = (bits >> (2 * i)) & 1u ? lo : 0.f;
+              hi = (bits >> (2 * i + 1)) & 1u ? hi : 0.f;
+              o[i] = pack_bf16x2(lo, hi);
+              const float hl = __uint_as_float(hh[i] << 16);
+              const float hu = __uint_as_float(hh[i] & 0xffff0000u);
+              const int a = 2 * pr + (i >> 1), b = (i & 1) * 2;
+              ssum[a][b] += lo;
+              ssq[a][b] = fmaf(lo, hl, ssq[a][b]);
+              ssum[a][b + 1] += hi;
+              ssq[a][b + 1] = fmaf(hi, hu, ssq[a][b + 1]);
+            }
+            v = make_uint4(o[0], o[1], o[2], o[3]);
+          }
           if (full || m < M) *reinterpret_cast<uint4*>(C + m * ldc + n) = v;
         }
 #pragma unroll
@@ -372,7 +434,9 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
       for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
-          const int col = wn * 64 + a * 16 + fq * 4 + b;
+          // forward: [subtile a][row b] of 4fq..; BN-backward: store-layout channel
+          // cofs + 4 * (a & 1) + b of column pair a / 2
+          const int col = bnb ? wn * 64 + (a >> 1) * 32 + cofs + (a & 1) * 4 + b : wn * 64 + a * 16 + fq * 4 + b;
           red[wm * Cfg::BN + col] = ssum[a][b];
           red[(WM + wm) * Cfg::BN + col] = ssq[a][b];
         }
@@ -391,10 +455,10 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
   }
 }
 
-template <int WM, int WN, bool BRES, int NS, bool GATHER, int MSB = 4>
+template <int WM, int WN, bool BRES, int NS, bool GATHER, int MSB = 4, bool BNB = false>
 int launch_nt(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, uint16_t* C, int64_t ldc, int64_t M,
               int N, int K, int max_blocks, const ConvGeo& geo, float* stats, int64_t stats_ld, int stats_rows,
-              hipStream_t stream) {
+              const BnBwd& bb, hipStream_t stream) {
   using Cfg = NtCfg<WM, WN, BRES, MSB>;
   const int ntiles = N / Cfg::BN;
   const int64_t mtiles = (M + Cfg::BM - 1) / Cfg::BM;
@@ -407,29 +471,29 @@ int launch_nt(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, ui
   if (stats && gx > stats_rows) gx = stats_rows;   // one partial row per block
   dim3 grid((unsigned)gx, (unsigned)ntiles);
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<WM, WN, BRES, NS, GATHER, MSB>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<WM, WN, BRES, NS, GATHER, MSB, BNB>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL((gemm_nt_kernel<WM, WN, BRES, NS, GATHER, MSB>), grid, dim3(Cfg::THREADS), lds, stream, A, lda, B,
-                     ldb, C, ldc, M, K, geo, stats, stats_ld);
+  hipLaunchKernelGGL((gemm_nt_kernel<WM, WN, BRES, NS, GATHER, MSB, BNB>), grid, dim3(Cfg::THREADS), lds, stream, A, lda, B,
+                     ldb, C, ldc, M, K, geo, stats, stats_ld, bb);
   return (int)gx;
 }
 
-template <int WM, int WN, bool GATHER, int MSB = 4>
+template <int WM, int WN, bool GATHER, int MSB = 4, bool BNB = false>
 int launch_nt_any(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, uint16_t* C, int64_t ldc,
                   int64_t M, int N, int K, int max_blocks, int bres, int ns, const ConvGeo& geo, float* stats,
-                  int64_t stats_ld, int stats_rows, hipStream_t stream) {
+                  int64_t stats_ld, int stats_rows, const BnBwd& bb, hipStream_t stream) {
   // keep the weight panel resident when it fits next to the two A stages
   if (bres < 0) bres = (64 * WN) * K * 2 <= 64 * 1024;
   if (bres && NtCfg<WM, WN, true, MSB>::lds_bytes(K, 2) > 160 * 1024) bres = 0;
   constexpr int L = 160 * 1024;
   if (bres) {
-    if (ns != 2 && NtCfg<WM, WN, true, MSB>::lds_bytes(K, 3) <= L) return launch_nt<WM, WN, true, 3, GATHER, MSB>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, stream);
-    else return launch_nt<WM, WN, true, 2, GATHER, MSB>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, stream);
+    if (ns != 2 && NtCfg<WM, WN, true, MSB>::lds_bytes(K, 3) <= L) return launch_nt<WM, WN, true, 3, GATHER, MSB, BNB>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, bb, stream);
+    else return launch_nt<WM, WN, true, 2, GATHER, MSB, BNB>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, bb, stream);
   } else {
-    if (ns != 2 && NtCfg<WM, WN, false, MSB>::lds_bytes(K, 3) <= L) return launch_nt<WM, WN, false, 3, GATHER, MSB>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, stream);
-    else return launch_nt<WM, WN, false, 2, GATHER, MSB>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, stream);
+    if (ns != 2 && NtCfg<WM, WN, false, MSB>::lds_bytes(K, 3) <= L) return launch_nt<WM, WN, false, 3, GATHER, MSB, BNB>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, bb, stream);
+    else return launch_nt<WM, WN, false, 2, GATHER, MSB, BNB>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, bb, stream);
   }
 }
 
@@ -801,7 +865,7 @@ bool gemm_supported(int64_t N, int64_t K) { return N >= 64 && K >= 64 && N % 64 
 template <bool GATHER>
 int nt_dispatch(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N,
                 int K, int cfg, int max_blocks, const ConvGeo& geo, float* stats, int64_t stats_ld, int stats_rows,
-                hipStream_t stream) {
+                const BnBwd& bb, hipStream_t stream) {
   // cfg = tile + 10 * panel (1: resident, 2: streamed) + 100 * stages (1: two, 2: three); 0 digits = auto
   const int bres = (cfg / 10) % 10 == 0 ? -1 : ((cfg / 10) % 10 == 1 ? 1 : 0);
   const int ns = (cfg / 100) % 10 == 1 ? 2 : 3;
@@ -814,32 +878,43 @@ int nt_dispatch(const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
   //                         5 256x256 (8, 128x64 per wave)  6 256x128 (4, 128x64)  7 128x256 (4, 128x64)
   static const int cfg_bn[8] = {64, 64, 128, 256, 128, 256, 128, 256};
   if (cfg > 7 || N % cfg_bn[cfg] != 0) cfg = 1;   // the tile must divide N (B rows are not clamped)
+  if (bb.h) {   // BN-backward epilogue: 64x64 wave tiles only
+    switch (cfg) {
+      case 2: return launch_nt_any<4, 2, GATHER, 4, true>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, bb, stream);
+      case 3: case 5: case 7: return launch_nt_any<2, 4, GATHER, 4, true>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, bb, stream);
+      case 4: case 6: return launch_nt_any<2, 2, GATHER, 4, true>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, bb, stream);
+      default: return launch_nt_any<4, 1, GATHER, 4, true>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, bb, stream);
+    }
+  }
   switch (cfg) {
-    case 2: return launch_nt_any<4, 2, GATHER>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, stream);
-    case 3: return launch_nt_any<2, 4, GATHER>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, stream);
-    case 4: return launch_nt_any<2, 2, GATHER>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, stream);
-    case 5: return launch_nt_any<2, 4, GATHER, 8>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, stream);
-    case 6: return launch_nt_any<2, 2, GATHER, 8>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, stream);
-    case 7: return launch_nt_any<1, 4, GATHER, 8>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, stream);
-    default: return launch_nt_any<4, 1, GATHER>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, stream);
+    case 2: return launch_nt_any<4, 2, GATHER>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, bb, stream);
+    case 3: return launch_nt_any<2, 4, GATHER>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, bb, stream);
+    case 4: return launch_nt_any<2, 2, GATHER>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, bb, stream);
+    case 5: return launch_nt_any<2, 4, GATHER, 8>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, bb, stream);
+    case 6: return launch_nt_any<2, 2, GATHER, 8>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, bb, stream);
+    case 7: return launch_nt_any<1, 4, GATHER, 8>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, bb, stream);
+    default: return launch_nt_any<4, 1, GATHER>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, bb, stream);
   }
 }
 
 int gemm_nt_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N,
-                 int K, int cfg, int max_blocks, float* stats, int stats_rows, const float* bias, hipStream_t stream) {
+                 int K, int cfg, int max_blocks, float* stats, int stats_rows, const float* bias, const BnBwdArgs* bn,
+                 hipStream_t stream) {
   ConvGeo g{};
   g.bias = bias;
+  const BnBwd bb = bn ? BnBwd{bn->h, bn->dy2, bn->mask} : BnBwd{};
   return nt_dispatch<false>(A, lda, B, ldb, C, ldc, M, N, K, cfg, max_blocks, g, stats, (int64_t)stats_rows * N,
-                            stats_rows, stream);
+                            stats_rows, bb, stream);
 }
 
 int conv_nt_bf16(const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P, int KH, int KW,
                  const void* B, void* Y, int64_t M, int N, int cfg, int max_blocks, float* stats, int stats_rows,
-                 const float* bias, hipStream_t stream) {
+                 const float* bias, const BnBwdArgs* bn, hipStream_t stream) {
   ConvGeo g{static_cast<const uint16_t*>(zero), H, W, C, OH, OW, S, P, KW, bias};
   const int K = KH * KW * C;
+  const BnBwd bb = bn ? BnBwd{bn->h, bn->dy2, bn->mask} : BnBwd{};
   return nt_dispatch<true>(X, C, B, K, Y, N, M, N, K, cfg, max_blocks, g, stats, (int64_t)stats_rows * N, stats_rows,
-                           stream);
+                           bb, stream);
 }
 
 template <int WN, int WK, int WS, bool GATHER, int MSN = 1>

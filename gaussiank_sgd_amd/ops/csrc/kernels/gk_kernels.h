@@ -230,6 +230,12 @@ void bn_act_forward_pre(const void* x, const void* res, void* y, uint8_t* mask, 
                         const float* psum, const float* psq, int gy, const float* w, const float* b, float eps, float momentum,
                         float* run_mean, float* run_var, float* save_mean, float* save_invstd, float* scale,
                         float* shift, int relu, int64_t* nbt, hipStream_t stream);
+// bf16 only: dz and its [2][gy][C] partials sum(dz), sum(dz * x) come from a
+// grad-input GEMM's BatchNorm-backward epilogue (BnBwdArgs below); finalize
+// (centring with the mean) + apply only.
+void bn_act_backward_pre(const void* dz, const void* x, void* dx, int64_t M, int C, const float* w,
+                         const float* mean, const float* invstd, float* dgamma, float* dbeta, const float* pdb,
+                         const float* pdg, int gy, float* gw_acc, float* gb_acc, hipStream_t stream);
 void bn_act_backward(const void* dy, const void* dy2, const uint8_t* mask, const void* x, void* dx, void* dres,
                      int64_t M, int C, int elem_bytes, const float* w, const float* mean, const float* invstd,
                      float* dgamma, float* dbeta, float* ws, int relu, float* gw_acc, float* gb_acc,
@@ -260,12 +266,22 @@ void bn_relu_pool_backward(const void* dy, const void* dy2, const uint8_t* amax,
 // pick the grid.
 // ---------------------------------------------------------------------------
 bool gemm_supported(int64_t N, int64_t K);
+// BatchNorm-backward epilogue of a grad-input GEMM (bn != nullptr): C receives
+// dz = mask ? bf16(dy) + dy2 : 0 instead of dy, and `stats` the per-workgroup
+// partials sum(dz), sum(dz * h) -- feed them to bn_act_backward_pre.  h / dy2
+// share C's row stride; mask is the BN forward's 1-bit ReLU mask.
+struct BnBwdArgs {
+  const uint16_t* h;
+  const uint16_t* dy2;
+  const uint8_t* mask;
+};
 // stats (optional): [2][stats_rows][N] fp32 BatchNorm partials (sum, sum of
 // squares of the bf16 output) per workgroup row; returns the grid's row count
 // (the partial rows written, <= stats_rows) -- feed it to bn_act_forward_pre.
 // bias (optional): fp32 [N] added in the epilogue (before rounding and statistics)
 int gemm_nt_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N,
-                 int K, int cfg, int max_blocks, float* stats, int stats_rows, const float* bias, hipStream_t stream);
+                 int K, int cfg, int max_blocks, float* stats, int stats_rows, const float* bias, const BnBwdArgs* bn,
+                 hipStream_t stream);
 void gemm_tn_acc_f32(const void* G, int64_t ldg, const void* X, int64_t ldx, float* W, int64_t ldw, int64_t M,
                      int N, int K, int cfg, int splits, hipStream_t stream);
 // Implicit-GEMM KHxKW convolution (stride S, zero padding P) over NHWC bf16:
@@ -275,7 +291,7 @@ void gemm_tn_acc_f32(const void* G, int64_t ldg, const void* X, int64_t ldx, flo
 // >= 64 zero bf16 (the padding row).
 int conv_nt_bf16(const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P, int KH, int KW,
                  const void* B, void* Y, int64_t M, int N, int cfg, int max_blocks, float* stats, int stats_rows,
-                 const float* bias, hipStream_t stream);
+                 const float* bias, const BnBwdArgs* bn, hipStream_t stream);
 void conv_tn_acc_f32(const void* G, const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P,
                      int KH, int KW, float* Wout, int64_t M, int N, int cfg, int splits, hipStream_t stream);
 

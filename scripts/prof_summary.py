@@ -14,6 +14,8 @@ def category(n: str) -> str:
         return "gk fused add+LayerNorm"
     if "gk::" in n and ("rec_gemm" in n or "lstm_" in n):
         return "gk LSTM (split-K step GEMM + fused cells)"
+    if "gk::" in n and "colsum" in n:
+        return "gk linear bias-grad column sums"
     if "gk::" in n and ("gemm_nt" in n or "gemm_tn" in n):
         return "gk HIP conv GEMMs (1x1 / implicit-GEMM 3x3, MFMA)"
     if "gk::" in n:
@@ -26,6 +28,8 @@ def category(n: str) -> str:
         return "MIOpen conv bwd-data"
     if "igemm_wrw" in n or "bwd_weight" in n:
         return "MIOpen conv bwd-weight"
+    if "attn_fwd" in n or "bwd_kernel_d" in n or "bwd_preprocess" in n:
+        return "attention (torch SDPA flash kernels)"
     if "batched_gemm" in n or "Cijk" in n:
         return "GEMM (CK / hipBLASLt)"
     if "SubTensor" in n or "fillBuffer" in n:
