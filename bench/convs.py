@@ -97,14 +97,14 @@ def main() -> int:
             from gaussiank_sgd_amd.ops import conv1x1 as cv
             wo = torch.zeros(K, C, k, k, device=dev, dtype=torch.float32).contiguous(memory_format=torch.channels_last)
             cases = {
-                "fwd": (lambda: cv._fwd(x, w, s), bx + bw + by),
+                "fwd": (lambda: cv._fwd(x, w, s, []), bx + bw + by),   # production: BN stats epilogue
                 "dgrad": (lambda: cv._dgrad(dy, w, x.shape, s), by + bw + bx),
                 "wgrad": (lambda: cv._wgrad_into(dy, x, w, s, wo), by + bx + bw),
             }
             for name, (fn, _) in cases.items():
                 fn()
             geo = (N, C, H, W, K, k, s)
-            impl = {"fwd": cv._choices.get(("fwd",) + geo + (False,)), "dgrad": cv._choices.get(("dgrad",) + geo),
+            impl = {"fwd": cv._choices.get(("fwd",) + geo + (True,)), "dgrad": cv._choices.get(("dgrad",) + geo),
                     "wgrad": cv._choices.get(("wgrad",) + geo)}
         if C == 3:
             del cases["dgrad"]   # the stem's input (the image batch) needs no gradient in training

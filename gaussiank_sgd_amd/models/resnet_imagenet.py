@@ -22,6 +22,7 @@ import torch.nn as nn
 
 from ..ops.bn import BNAct, global_avg_pool
 from ..ops.conv1x1 import Conv1x1, Conv3x3, conv_stats
+from ..ops.stem import StemConv
 
 
 def conv3x3(inp: int, out: int, stride: int = 1, groups: int = 1, dilation: int = 1) -> nn.Conv2d:
@@ -96,7 +97,8 @@ class ResNet(nn.Module):
         self.inplanes = 64
         self.groups = groups
         self.base_width = width_per_group
-        self.conv1 = nn.Conv2d(3, 64, kernel_size=7, stride=2, padding=3, bias=False)
+        # nn.Conv2d(3, 64, 7, 2, 3, bias=False) running the gfx950 stem kernels (ops/stem.py)
+        self.conv1 = StemConv(3, 64)
         # stem BN + ReLU + 3x3/s2 max-pool run as one fused kernel pass (BNAct pool=...);
         # ``maxpool`` stays as an attribute (no parameters) for module-path compatibility.
         self.bn1 = BNAct(64, act="relu", pool=(3, 2, 1))
@@ -153,7 +155,8 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(self.bn1(self.conv1(x)))
+        y, st = conv_stats(self.conv1, x)   # BN statistics from the stem kernel's epilogue
+        x = self.maxpool(self.bn1(y, stats=st))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         return self.fc(global_avg_pool(x))   # == flatten(avgpool(x)), channels-last backward
 

@@ -161,7 +161,7 @@ class _BNReLUPoolFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, pool, direct=None, nbt=None,
-                twin=False):
+                twin=False, pre=None):
         ctx.set_materialize_grads(False)
         k, st, pad = pool
         N, C, H, W = x.shape
@@ -173,8 +173,11 @@ class _BNReLUPoolFn(torch.autograd.Function):
         M = N * H * W
         ws = torch.empty(int(_ops().bn_workspace_floats(M, C, x.element_size())), dtype=torch.float32,
                          device=x.device)
+        # pre = (partials [2, rows, C], rows): statistics from the stem conv's epilogue
+        pre_t, pre_rows = pre if pre is not None else (None, 0)
         _ops().bn_relu_pool_forward(x, y, amax, weight, bias, running_mean, running_var, stats[0], stats[1],
-                                    stats[2], stats[3], ws, float(eps), float(momentum), k, st, pad, nbt)
+                                    stats[2], stats[3], ws, float(eps), float(momentum), k, st, pad, nbt, pre_t,
+                                    pre_rows)
         ctx.pool = (k, st, pad)
         ctx.direct = direct
         ctx.save_for_backward(x, amax, weight, stats[0], stats[1])
@@ -185,7 +188,7 @@ class _BNReLUPoolFn(torch.autograd.Function):
         x, amax, weight, mean, invstd = ctx.saved_tensors
         dy, dy2 = _grad_pair(grads, x)
         if dy is None:
-            return (None,) * 11
+            return (None,) * 12
         k, st, pad = ctx.pool
         C = x.shape[1]
         M = x.numel() // C
@@ -196,10 +199,10 @@ class _BNReLUPoolFn(torch.autograd.Function):
         gw, gb = ctx.direct if ctx.direct is not None else (None, None)
         _ops().bn_relu_pool_backward(dy, amax, x, dx, weight, mean, invstd, g[0], g[1], ws, k, st, pad, gw, gb, dy2)
         if ctx.direct is not None:
-            return (dx,) + (None,) * 10
+            return (dx,) + (None,) * 11
         dgamma = g[0] if weight is not None and ctx.needs_input_grad[1] else None
         dbeta = g[1] if ctx.needs_input_grad[2] else None
-        return (dx, dgamma, dbeta) + (None,) * 8
+        return (dx, dgamma, dbeta) + (None,) * 9
 
 
 _supported_cache = {}
@@ -264,8 +267,10 @@ class BNAct(nn.BatchNorm2d):
                 mom = self.momentum     # the finalize kernel increments num_batches_tracked
             direct = getattr(self, "_gk_direct", None)
             if pool is not None:
+                pre = stats if (stats is not None and stats[0].shape[2] == x.shape[1] and
+                                x.dtype == torch.bfloat16) else None
                 return _BNReLUPoolFn.apply(x, self.weight, self.bias, self.running_mean, self.running_var, mom,
-                                           self.eps, pool, direct, nbt, self.twin)
+                                           self.eps, pool, direct, nbt, self.twin, pre)
             if stats is not None and (stats[0].shape[2] != x.shape[1] or x.dtype != torch.bfloat16):
                 stats = None
             link = BnLink() if self.bwd_link and torch.is_grad_enabled() and x.dtype == torch.bfloat16 else None

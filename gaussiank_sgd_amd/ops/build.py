@@ -46,6 +46,7 @@ HIP_SOURCES = [
     "kernels/ln.hip",
     "kernels/linear.hip",
     "kernels/lstm.hip",
+    "kernels/stem.hip",
 ]
 CXX_SOURCES = [
     "comm/rccl_engine.cpp",

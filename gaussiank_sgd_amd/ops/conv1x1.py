@@ -382,9 +382,11 @@ class FastConv2d(nn.Conv2d):
 
 
 def conv_stats(conv: nn.Module, x: torch.Tensor):
-    """(conv(x), BatchNorm partials of the output or None)."""
-    if isinstance(conv, FastConv2d):
-        return conv.forward_stats(x)
+    """(conv(x), BatchNorm partials of the output or None) -- FastConv2d and
+    the stem conv (ops/stem.py) reduce them in their GEMM epilogue."""
+    fs = getattr(conv, "forward_stats", None)
+    if fs is not None:
+        return fs(x)
     return conv(x), None
 
 

@@ -498,7 +498,8 @@ void bn_relu_pool_forward(at::Tensor x, at::Tensor y, at::Tensor amax, c10::opti
                           c10::optional<at::Tensor> b, c10::optional<at::Tensor> run_mean,
                           c10::optional<at::Tensor> run_var, at::Tensor save_mean, at::Tensor save_invstd,
                           at::Tensor scale, at::Tensor shift, at::Tensor ws, double eps, double momentum, int64_t k,
-                          int64_t st, int64_t pad, c10::optional<at::Tensor> nbt) {
+                          int64_t st, int64_t pad, c10::optional<at::Tensor> nbt, c10::optional<at::Tensor> pre,
+                          int64_t pre_rows) {
   check_cl(x, "x");
   check_cl(y, "y");
   TORCH_CHECK(x.dim() == 4 && y.scalar_type() == x.scalar_type(), "y must be 4-D with x's dtype");
@@ -513,6 +514,19 @@ void bn_relu_pool_forward(at::Tensor x, at::Tensor y, at::Tensor amax, c10::opti
   TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() >= (int64_t)gk::bn_workspace_floats(M, (int)C, eb),
               "workspace too small");
   c10::DeviceGuard guard(x.device());
+  if (pre.has_value() && pre->defined()) {   // statistics pre-reduced by the producer (stem conv epilogue)
+    TORCH_CHECK(eb == 2 && pre->is_cuda() && pre->scalar_type() == at::kFloat && pre->is_contiguous() &&
+                    pre->dim() == 3 && pre->size(0) == 2 && pre->size(2) == C && pre_rows > 0 &&
+                    pre_rows <= pre->size(1),
+                "pre must be fp32 [2, rows, C] partials (bf16 x) with 0 < pre_rows <= rows");
+    const float* ps = pre->data_ptr<float>();
+    gk::bn_relu_pool_forward_pre(x.data_ptr(), y.data_ptr(), amax.data_ptr<uint8_t>(), x.size(0), (int)C, pg, ps,
+                                 ps + pre->size(1) * C, (int)pre_rows, opt_f32(w), opt_f32(b), (float)eps,
+                                 (float)momentum, opt_f32_mut(run_mean), opt_f32_mut(run_var),
+                                 save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(), scale.data_ptr<float>(),
+                                 shift.data_ptr<float>(), opt_i64(nbt), cur_stream(x));
+    return;
+  }
   gk::bn_relu_pool_forward(x.data_ptr(), y.data_ptr(), amax.data_ptr<uint8_t>(), x.size(0), (int)C, pg, eb,
                            opt_f32(w), opt_f32(b), (float)eps, (float)momentum, opt_f32_mut(run_mean),
                            opt_f32_mut(run_var), save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(),
@@ -727,6 +741,68 @@ float* stats_ptr(const c10::optional<at::Tensor>& st, int64_t N, int* rows) {
               "stats must be a contiguous fp32 [2, rows, N] GPU tensor");
   *rows = (int)t.size(1);
   return t.data_ptr<float>();
+}
+
+// ---- ResNet stem (stem.hip) ----
+void check_stem_x(const at::Tensor& x) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.size(1) == 3 &&
+                  (x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16) &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "stem: x must be a channels-last fp32 / bf16 [N, 3, H, W] GPU tensor");
+  TORCH_CHECK(gk::stem_supported((int)x.size(2), (int)x.size(3)), "stem: unsupported image size");
+  TORCH_CHECK(x.size(0) * x.size(2) * x.size(3) < (int64_t(1) << 31), "stem: batch too large");
+}
+
+void stem_pack(at::Tensor w, at::Tensor wp) {
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.dim() == 4 && w.size(0) == 64 && w.size(1) == 3 &&
+                  w.size(2) == 7 && w.size(3) == 7,
+              "stem_pack: w must be fp32 [64, 3, 7, 7]");
+  TORCH_CHECK(wp.is_cuda() && wp.scalar_type() == at::kBFloat16 && wp.is_contiguous() && wp.numel() == 64 * 224,
+              "stem_pack: wp must be contiguous bf16 [64, 224]");
+  c10::DeviceGuard guard(w.device());
+  gk::stem_pack_weight(w.data_ptr<float>(), w.stride(0), w.stride(1), w.stride(2), w.stride(3),
+                       static_cast<uint16_t*>(wp.data_ptr()), cur_stream(w));
+}
+
+int64_t stem_fwd(at::Tensor x, at::Tensor wp, at::Tensor y, c10::optional<at::Tensor> stats) {
+  check_stem_x(x);
+  const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
+  const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  TORCH_CHECK(wp.is_cuda() && wp.scalar_type() == at::kBFloat16 && wp.is_contiguous() && wp.numel() == 64 * 224,
+              "stem_fwd: wp must be the packed bf16 [64, 224] weights");
+  TORCH_CHECK(y.is_cuda() && y.scalar_type() == at::kBFloat16 && y.dim() == 4 && y.size(0) == N && y.size(1) == 64 &&
+                  y.size(2) == OH && y.size(3) == OW && y.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "stem_fwd: y must be channels-last bf16 [N, 64, OH, OW]");
+  int rows = 0;
+  float* sp = stats_ptr(stats, 64, &rows);
+  c10::DeviceGuard guard(x.device());
+  return gk::stem_forward(x.data_ptr(), x.scalar_type() == at::kFloat, (int)N, (int)H, (int)W,
+                          static_cast<const uint16_t*>(wp.data_ptr()), static_cast<uint16_t*>(y.data_ptr()), sp, rows,
+                          cur_stream(x));
+}
+
+int64_t stem_wgrad_ws(int64_t N, int64_t H, int64_t W) {
+  return (int64_t)gk::stem_wgrad_blocks((int)N, (int)H, (int)W) * 64 * 224;
+}
+
+void stem_wgrad(at::Tensor x, at::Tensor dy, at::Tensor out, at::Tensor part) {
+  check_stem_x(x);
+  const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
+  const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 && dy.size(0) == N &&
+                  dy.size(1) == 64 && dy.size(2) == OH && dy.size(3) == OW &&
+                  dy.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "stem_wgrad: dy must be channels-last bf16 [N, 64, OH, OW]");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.dim() == 4 && out.size(0) == 64 &&
+                  out.size(1) == 3 && out.size(2) == 7 && out.size(3) == 7,
+              "stem_wgrad: out must be fp32 [64, 3, 7, 7]");
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() &&
+                  part.numel() >= stem_wgrad_ws(N, H, W),
+              "stem_wgrad: part must hold stem_wgrad_ws(N, H, W) floats");
+  c10::DeviceGuard guard(x.device());
+  gk::stem_wgrad(x.data_ptr(), x.scalar_type() == at::kFloat, (int)N, (int)H, (int)W,
+                 static_cast<const uint16_t*>(dy.data_ptr()), part.data_ptr<float>(), out.data_ptr<float>(),
+                 out.stride(0), out.stride(1), out.stride(2), out.stride(3), cur_stream(x));
 }
 
 // C[M, N] = A[M, K] . B[N, K]^T
@@ -1077,7 +1153,8 @@ TORCH_LIBRARY(gksgd, m) {
   m.def(
       "bn_relu_pool_forward(Tensor x, Tensor(a!) y, Tensor(b!) amax, Tensor? w, Tensor? b, Tensor(c!)? run_mean, "
       "Tensor(d!)? run_var, Tensor(e!) save_mean, Tensor(f!) save_invstd, Tensor(g!) scale, Tensor(h!) shift, "
-      "Tensor(i!) ws, float eps, float momentum, int k, int s, int p, Tensor(j!)? nbt=None) -> ()");
+      "Tensor(i!) ws, float eps, float momentum, int k, int s, int p, Tensor(j!)? nbt=None, Tensor? pre=None, "
+      "int pre_rows=0) -> ()");
   m.def(
       "bn_relu_pool_backward(Tensor dy, Tensor amax, Tensor x, Tensor(a!) dx, Tensor? w, Tensor mean, "
       "Tensor invstd, Tensor(b!) dgamma, Tensor(c!) dbeta, Tensor(d!) ws, int k, int s, int p, "
@@ -1099,6 +1176,11 @@ TORCH_LIBRARY(gksgd, m) {
   m.def("conv_nt(Tensor x, Tensor w, Tensor(a!) y, Tensor zero, int stride, int pad, int cfg=0, int max_blocks=0, "
         "Tensor(b!)? stats=None, Tensor? bias=None, Tensor? bn_h=None, Tensor? bn_dy2=None, Tensor? bn_mask=None) "
         "-> int");
+  m.def("stem_supported(int H, int W) -> bool", [](int64_t H, int64_t W) { return gk::stem_supported((int)H, (int)W); });
+  m.def("stem_wgrad_ws(int N, int H, int W) -> int", &stem_wgrad_ws);
+  m.def("stem_pack(Tensor w, Tensor(a!) wp) -> ()");
+  m.def("stem_fwd(Tensor x, Tensor wp, Tensor(a!) y, Tensor(b!)? stats=None) -> int");
+  m.def("stem_wgrad(Tensor x, Tensor dy, Tensor(a!) out, Tensor(b!) part) -> ()");
   m.def("bn_act_backward_pre(Tensor dz, Tensor x, Tensor(a!) dx, Tensor? w, Tensor mean, Tensor invstd, "
         "Tensor(b!) dgamma, Tensor(c!) dbeta, Tensor part, int rows, Tensor(d!)? gw_acc=None, "
         "Tensor(e!)? gb_acc=None) -> ()");
@@ -1158,6 +1240,9 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("bn_act_forward", &bn_act_forward);
   m.impl("bn_act_backward", &bn_act_backward);
   m.impl("bn_act_backward_pre", &bn_act_backward_pre);
+  m.impl("stem_pack", &stem_pack);
+  m.impl("stem_fwd", &stem_fwd);
+  m.impl("stem_wgrad", &stem_wgrad);
   m.impl("bn_relu_pool_forward", &bn_relu_pool_forward);
   m.impl("bn_relu_pool_backward", &bn_relu_pool_backward);
   m.impl("accum_grad", &accum_grad);

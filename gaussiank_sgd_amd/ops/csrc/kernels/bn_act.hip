@@ -892,6 +892,21 @@ void bn_relu_pool_forward(const void* x, void* y, uint8_t* amax, int64_t N, int 
   }
 }
 
+// statistics pre-reduced by the producing convolution (stem.hip epilogue):
+// finalize + the fused BN / ReLU / max-pool pass only (bf16)
+void bn_relu_pool_forward_pre(const void* x, void* y, uint8_t* amax, int64_t N, int C, PoolGeo pg, const float* psum,
+                              const float* psq, int gy, const float* w, const float* b, float eps, float momentum,
+                              float* run_mean, float* run_var, float* save_mean, float* save_invstd, float* scale,
+                              float* shift, int64_t* nbt, hipStream_t s) {
+  const int64_t M = N * pg.H * pg.W;
+  const int64_t P = N * pg.OH * pg.OW;
+  const int64_t threads = P * (C / 8);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(kBlock), 0, s, psum, psq, gy, M, C, w, b,
+                     eps, momentum, run_mean, run_var, save_mean, save_invstd, scale, shift, nbt);
+  hipLaunchKernelGGL(bn_relu_pool_kernel<uint16_t>, dim3((unsigned)((threads + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                     s, (const uint16_t*)x, (uint16_t*)y, amax, P, C, pg, scale, shift);
+}
+
 template <typename T, bool TWIN>
 void bn_pool_backward_tw(const T* dy, const T* dy2, const uint8_t* amax, const T* x, T* dx, int64_t M, int C,
                          PoolGeo pg, const float* w, const float* mean, const float* invstd, float* dgamma,

@@ -30,26 +30,10 @@
 
 #include "common.h"
 #include "gk_kernels.h"
+#include "mfma_util.h"
 
 namespace gk {
 namespace {
-
-typedef short bf16x8 __attribute__((ext_vector_type(8)));
-typedef short bf16x4 __attribute__((ext_vector_type(4)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-#define GK_LDS __attribute__((address_space(3)))
-
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-
-// two fp32 -> packed bf16x2, round-to-nearest-even (one v_cvt_pk_bf16_f32)
-__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{lo, hi}, bf16x2_t));
-}
-
-__device__ __forceinline__ void glds16(const void* src, GK_LDS void* dst) {
-  __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
-}
 
 __device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
 
@@ -537,33 +521,16 @@ __device__ __forceinline__ uint32_t udiv_small(uint32_t a, uint32_t d, float rcp
   return q;
 }
 
-// LDS image of a [64 rows][RB bytes] tile for transposed reads: 16-byte chunk
-// c of row r is stored at chunk c ^ tr_swz(r).  A ds_read_b64_tr_b16 half-wave
-// touches rows {R..R+3, R+8..R+11} x 32 bytes; the XOR spreads those 16
-// (row, chunk) pairs over 16 distinct 16-byte bank slots.
-template <int RB>
-__device__ __forceinline__ int tr_swz(int r) {
-  if (RB == 128) return 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1));
-  return 2 * ((r & 3) | (((r >> 3) & 1) << 2));
-}
-
 // Transposed fragment: lane l (group g = l>>4, li = l&15) gets rows
 // r0 + 8g + 0..7 of column c0 + li of the swizzled [rows][RB] bf16 image, as
 // the 8 k-elements of a 16x16x32 MFMA operand.  c0 is a multiple of 16.
-// The transposed LDS read is issued as inline asm: with the builtin, the
-// compiler's wait-count pass cannot tell the read apart from the LDS-DMA
-// writes of the NEXT stage issued just before it and inserts
+// The transposed LDS read is issued as inline asm (mfma_util.h ds_read_tr):
+// with the builtin, the compiler's wait-count pass cannot tell the read apart
+// from the LDS-DMA writes of the NEXT stage issued just before it and inserts
 // `s_waitcnt vmcnt(0)` -- which serialises the whole global->LDS pipeline
 // (each stage would wait for the loads it has just started).  The asm reads
 // carry no such dependence; tr_sync() below waits for them (lgkmcnt) and ties
 // the fragments to that wait so no MFMA can be scheduled before it.
-__device__ __forceinline__ bf16x4 ds_read_tr(const char* p) {
-  bf16x4 v;
-  const uint32_t a = (uint32_t)(uintptr_t)(GK_LDS char*)p;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a));
-  return v;
-}
-
 template <int RB>
 __device__ __forceinline__ bf16x8 tr_frag(const char* tile, int r0, int c0, int lane) {
   const int g = lane >> 4, li = lane & 15;

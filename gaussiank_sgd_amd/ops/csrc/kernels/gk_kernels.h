@@ -249,6 +249,10 @@ void bn_act_backward(const void* dy, const void* dy2, const uint8_t* mask, const
 struct PoolGeo {
   int H, W, OH, OW, k, s, p;
 };
+void bn_relu_pool_forward_pre(const void* x, void* y, uint8_t* amax, int64_t N, int C, PoolGeo pg, const float* psum,
+                              const float* psq, int gy, const float* w, const float* b, float eps, float momentum,
+                              float* run_mean, float* run_var, float* save_mean, float* save_invstd, float* scale,
+                              float* shift, int64_t* nbt, hipStream_t stream);
 void bn_relu_pool_forward(const void* x, void* y, uint8_t* amax, int64_t N, int C, PoolGeo pg, int elem_bytes,
                           const float* w, const float* b, float eps, float momentum, float* run_mean, float* run_var,
                           float* save_mean, float* save_invstd, float* scale, float* shift, float* ws, int64_t* nbt,
@@ -294,6 +298,25 @@ int conv_nt_bf16(const void* X, const void* zero, int H, int W, int C, int OH, i
                  const float* bias, const BnBwdArgs* bn, hipStream_t stream);
 void conv_tn_acc_f32(const void* G, const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P,
                      int KH, int KW, float* Wout, int64_t M, int N, int cfg, int splits, hipStream_t stream);
+
+// ---------------------------------------------------------------------------
+// ImageNet-ResNet stem: 7x7 / stride 2 / pad 3 convolution, 3 -> 64 channels
+// (stem.hip).  x: NHWC [N, H, W, 3] fp32 or bf16; y: NHWC bf16 [N, OH, OW, 64];
+// weights packed once per step into bf16 [64][224] (k = kh*32 + kw*4 + c) by
+// stem_pack_weight from [64][3][7][7] fp32 with element strides s0..s3.
+// stem_forward: optional per-block BatchNorm partials (sum, sum of squares)
+// [2][stats_rows][64]; returns the rows written.  stem_wgrad: out (fp32,
+// strides s0..s3) += dW, via per-block partials part[stem_wgrad_blocks * 64 * 224]
+// summed in a fixed order.
+// ---------------------------------------------------------------------------
+bool stem_supported(int H, int W);
+void stem_pack_weight(const float* w, int64_t s0, int64_t s1, int64_t s2, int64_t s3, uint16_t* wp,
+                      hipStream_t stream);
+int stem_forward(const void* x, bool x_f32, int N, int H, int W, const uint16_t* wp, uint16_t* y, float* stats,
+                 int stats_rows, hipStream_t stream);
+int stem_wgrad_blocks(int N, int H, int W);
+void stem_wgrad(const void* x, bool x_f32, int N, int H, int W, const uint16_t* dy, float* part, float* out,
+                int64_t s0, int64_t s1, int64_t s2, int64_t s3, hipStream_t stream);
 
 // ---------------------------------------------------------------------------
 // Fused residual add (+ dropout) + LayerNorm over rows of H bf16 (ln.hip).

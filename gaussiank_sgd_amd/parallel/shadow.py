@@ -34,6 +34,7 @@ from ..ops.bn import BNAct
 from ..ops.conv1x1 import FastConv2d
 from ..ops.linear import FastLinear
 from ..ops.lstm import GkLSTM
+from ..ops.stem import StemConv
 
 
 class _ShadowWeight(torch.autograd.Function):
@@ -83,7 +84,7 @@ def install_bf16_shadow(model: nn.Module, opt) -> int:
     names = opt._parameter_names
     count = 0
     for mod in model.modules():
-        if isinstance(mod, (FastConv2d, FastLinear)):
+        if isinstance(mod, (FastConv2d, FastLinear, StemConv)):
             # its own forward reads the shadow view and (GEMM path) adds the fp32
             # weight / bias gradients straight into the arena; unsupported
             # shapes fall back to the plain shadow conv / linear
@@ -96,7 +97,7 @@ def install_bf16_shadow(model: nn.Module, opt) -> int:
                     count += 1
             if table:
                 mod._gk_shadow = table
-                mod._gk_slow = types.MethodType(_conv_forward if isinstance(mod, FastConv2d) else _linear_forward,
+                mod._gk_slow = types.MethodType(_conv_forward if isinstance(mod, nn.Conv2d) else _linear_forward,
                                                 mod)
         elif isinstance(mod, (nn.Conv2d, nn.Linear)) and type(mod).forward in (nn.Conv2d.forward, nn.Linear.forward):
             table = {}

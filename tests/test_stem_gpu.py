@@ -1,0 +1,110 @@
+"""ResNet stem convolution (7x7 / s2 / p3, 3 -> 64) on the gfx950 kernels of
+csrc/kernels/stem.hip vs an fp32 PyTorch reference: forward (+ the BatchNorm
+statistics of its epilogue), grad-weight, and the StemConv module under bf16
+autocast (weight gradient into a fresh tensor and through the shadow arena)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+CL = torch.channels_last
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    from gaussiank_sgd_amd import ops
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    assert ops.load(), ops._load_error
+
+
+def _inputs(N, H, W, dtype, seed):
+    torch.manual_seed(seed)
+    x = torch.randn(N, 3, H, W, device="cuda").to(dtype).contiguous(memory_format=CL)
+    w = torch.randn(64, 3, 7, 7, device="cuda") * 0.1
+    return x, w
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("N,H,W", [(2, 224, 224), (3, 64, 64), (5, 32, 48), (1, 96, 80)])
+def test_stem_forward_and_stats(dtype, N, H, W):
+    g = torch.ops.gksgd
+    x, w = _inputs(N, H, W, dtype, N + H)
+    assert g.stem_supported(H, W)
+    wp = torch.empty(64, 224, dtype=torch.bfloat16, device="cuda")
+    g.stem_pack(w, wp)
+    OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    y = torch.empty(N, 64, OH, OW, dtype=torch.bfloat16, device="cuda").contiguous(memory_format=CL)
+    st = torch.full((2, 256, 64), float("nan"), device="cuda")
+    rows = g.stem_fwd(x, wp, y, st)
+    torch.cuda.synchronize()
+    ref = F.conv2d(x.to(torch.bfloat16).float(), w.to(torch.bfloat16).float(), stride=2, padding=3)
+    err = (y.float() - ref).abs().max().item()
+    assert err <= 1e-2 * ref.abs().max().item(), err
+    yf = y.float()
+    s1 = st[0, :rows].double().sum(0)
+    s2 = st[1, :rows].double().sum(0)
+    r1 = yf.double().sum((0, 2, 3))
+    r2 = yf.double().square().sum((0, 2, 3))
+    assert torch.allclose(s1, r1, rtol=1e-4, atol=1e-2 * yf.abs().max().item())
+    assert torch.allclose(s2, r2, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("N,H,W,cl_out", [(2, 224, 224, True), (3, 64, 64, False), (4, 32, 48, True)])
+def test_stem_wgrad(dtype, N, H, W, cl_out):
+    g = torch.ops.gksgd
+    x, _ = _inputs(N, H, W, dtype, 7 * N + W)
+    OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    dy = torch.randn(N, 64, OH, OW, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    out = torch.full((64, 3, 7, 7), 0.5, device="cuda")
+    if cl_out:
+        out = out.contiguous(memory_format=CL)
+    part = torch.empty(int(g.stem_wgrad_ws(N, H, W)), device="cuda")
+    g.stem_wgrad(x, dy, out, part)
+    torch.cuda.synchronize()
+    xr = x.to(torch.bfloat16).float()
+    wr = torch.zeros(64, 3, 7, 7, device="cuda", requires_grad=True)
+    F.conv2d(xr, wr, stride=2, padding=3).backward(dy.float())
+    ref = wr.grad + 0.5
+    err = (out - ref).abs().max().item()
+    assert err <= 2e-3 * wr.grad.abs().max().item() + 1e-3, err
+
+
+def test_stemconv_module_autocast():
+    from gaussiank_sgd_amd.ops.stem import StemConv
+    torch.manual_seed(3)
+    m = StemConv().cuda().to(memory_format=CL)
+    x = torch.randn(4, 3, 64, 64, device="cuda").contiguous(memory_format=CL)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y, st = m.forward_stats(x)
+    assert st is not None and y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=CL)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr = x.to(torch.bfloat16).float()
+    wr = m.weight.detach().to(torch.bfloat16).float().requires_grad_(True)
+    yr = F.conv2d(xr, wr, stride=2, padding=3)
+    yr.backward(dy.float())
+    assert (y.float() - yr).abs().max().item() <= 1e-2 * yr.abs().max().item()
+    assert (m.weight.grad - wr.grad).abs().max().item() <= 2e-3 * wr.grad.abs().max().item() + 1e-3
+
+
+def test_resnet50_stem_bn_stats_match_pass():
+    """Stem + fused BN/ReLU/max-pool with the epilogue statistics == with its own
+    statistics pass (GKSGD_STEM=0 falls back to MIOpen + the BN stats pass)."""
+    from gaussiank_sgd_amd.ops import stem
+    from gaussiank_sgd_amd.ops.bn import BNAct
+    torch.manual_seed(5)
+    conv = stem.StemConv().cuda().to(memory_format=CL)
+    bn_a = BNAct(64, act="relu", pool=(3, 2, 1)).cuda()
+    bn_b = BNAct(64, act="relu", pool=(3, 2, 1)).cuda()
+    x = torch.randn(4, 3, 96, 96, device="cuda").contiguous(memory_format=CL)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y, st = conv.forward_stats(x)
+        assert st is not None
+        out_a = bn_a(y, stats=st)
+        out_b = bn_b(y)
+    assert (out_a.float() - out_b.float()).abs().max().item() <= 2e-2
+    assert torch.allclose(bn_a.running_mean, bn_b.running_mean, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(bn_a.running_var, bn_b.running_var, rtol=1e-3, atol=1e-5)
