@@ -74,6 +74,9 @@ def main() -> int:
                          "tuning/gemm_choices.json) and report which implementation each direction uses")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
+    if args.ours:
+        from gaussiank_sgd_amd import ops
+        assert ops.load(), "native extension not built"
     rows = []
     tot = {"fwd": [0.0, 0.0], "dgrad": [0.0, 0.0], "wgrad": [0.0, 0.0]}
     for (N, C, H, W, K, k, s, p), mult in sorted(resnet50_convs(args.batch).items()):

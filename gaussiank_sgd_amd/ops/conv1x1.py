@@ -197,6 +197,12 @@ def _dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int) -> torch.Tensor:
                                                    [True, False, False])[0]
     cands = []
     dx = None
+    if s == 2:
+        # stride 2: the four parity classes of dX as stride-1 implicit GEMMs over dY
+        dx = xs
+        z = _zero(dy.device)
+        run = lambda c, mb: g.conv_dgrad_s2(dy, w, dx, z, c, mb)  # noqa: E731
+        cands = [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in _NT_CFGS for mb in _NT_GRIDS]
     if s == 1:
         dx = xs
         if k == 1:

@@ -915,6 +915,57 @@ int64_t conv_nt(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor zero, int64
                           sp, rows, bias_ptr(bias, Co), has_bn ? &bn : nullptr, cur_stream(x));
 }
 
+// grad-input of a stride-2 convolution (1x1 / pad 0 or 3x3 / pad 1) through the
+// stride-1 MFMA kernels: dX = conv_transpose(dY, W) splits into the four
+// (row, column) parity classes of dX; class (a, b) is a stride-1 KH'xKW' conv
+// over dY (taps kh with kh = a + 1 mod 2: {1} for even rows, {2, 0} for odd)
+// whose output lands on the class's pixels (gemm.hip ConvGeo remap).
+// dy: [N, K, OH, OW] channels-last bf16; w: [K, C, k, k] channels-last bf16;
+// dx: [N, C, H, W] channels-last bf16 (every pixel written).
+void conv_dgrad_s2(at::Tensor dy, at::Tensor w, at::Tensor dx, at::Tensor zero, int64_t cfg, int64_t max_blocks) {
+  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 &&
+                  dy.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv_dgrad_s2: dy must be channels-last bf16");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(0) == dy.size(1) &&
+                  w.size(2) == w.size(3) && (w.size(2) == 1 || w.size(2) == 3),
+              "conv_dgrad_s2: w must be bf16 [K, C, k, k], k in {1, 3}");
+  TORCH_CHECK(dx.is_cuda() && dx.scalar_type() == at::kBFloat16 && dx.dim() == 4 && dx.size(0) == dy.size(0) &&
+                  dx.size(1) == w.size(1) && dx.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv_dgrad_s2: dx must be channels-last bf16 [N, C, H, W]");
+  const int64_t N = dy.size(0), K = dy.size(1), OHd = dy.size(2), OWd = dy.size(3);
+  const int64_t C = w.size(1), k = w.size(2), H = dx.size(2), W = dx.size(3);
+  const int64_t p = k / 2;
+  TORCH_CHECK((H + 2 * p - k) / 2 + 1 == OHd && (W + 2 * p - k) / 2 + 1 == OWd, "conv_dgrad_s2: shape mismatch");
+  TORCH_CHECK(K % 64 == 0 && C % 64 == 0, "conv_dgrad_s2: channels must be multiples of 64");
+  TORCH_CHECK(zero.is_cuda() && zero.scalar_type() == at::kBFloat16 && zero.numel() >= 64, "zero: >= 64 bf16");
+  TORCH_CHECK(N * H * W < (int64_t(1) << 31), "conv_dgrad_s2: too many pixels");
+  c10::DeviceGuard guard(dy.device());
+  const hipStream_t st = cur_stream(dy);
+  if (k == 1) {   // one class (even, even), zeros elsewhere; B = W^T [C][K]
+    const at::Tensor wt = w.reshape({K, C}).t().contiguous();
+    gk::conv_nt_remap_bf16(dy.data_ptr(), K, zero.data_ptr(), (int)OHd, (int)OWd, (int)K, (int)OHd, (int)OWd, 1, 1,
+                           wt.data_ptr(), dx.data_ptr(), N * OHd * OWd, (int)C, (int)H, (int)W, 0, 0, 1, (int)cfg,
+                           (int)max_blocks, st);
+    return;
+  }
+  // [C][kh][kw][K] = W[K][C][kh][kw]
+  const at::Tensor wt = w.permute({1, 2, 3, 0}).contiguous();
+  for (int a = 0; a < 2; ++a) {
+    for (int b = 0; b < 2; ++b) {
+      const int64_t OHc = (H - a + 1) / 2, OWc = (W - b + 1) / 2;
+      if (OHc <= 0 || OWc <= 0) continue;
+      // class-conv tap j reads dY row oh + j: j = 0 <-> kh = 2 - a ... (a = 0: kh = 1; a = 1: kh = 2, 0)
+      // taps as device-side slices (no index upload): {1} or {2, 0}
+      at::Tensor wc = a == 0 ? wt.slice(1, 1, 2) : wt.slice(1, 0, 3, 2).flip({1});
+      wc = b == 0 ? wc.slice(2, 1, 2) : wc.slice(2, 0, 3, 2).flip({2});
+      wc = wc.contiguous();
+      gk::conv_nt_remap_bf16(dy.data_ptr(), K, zero.data_ptr(), (int)OHd, (int)OWd, (int)K, (int)OHc, (int)OWc,
+                             a == 0 ? 1 : 2, b == 0 ? 1 : 2, wc.data_ptr(), dx.data_ptr(), N * OHc * OWc, (int)C,
+                             (int)H, (int)W, a, b, 0, (int)cfg, (int)max_blocks, st);
+    }
+  }
+}
+
 // wout: fp32 [Cout, C, KH, KW] channels-last (memory [Cout][KH][KW][C]); += dW
 void conv_tn_acc(at::Tensor dy, at::Tensor x, at::Tensor wout, at::Tensor zero, int64_t stride, int64_t pad,
                  int64_t cfg, int64_t splits) {
@@ -1181,6 +1232,7 @@ TORCH_LIBRARY(gksgd, m) {
   m.def("stem_pack(Tensor w, Tensor(a!) wp) -> ()");
   m.def("stem_fwd(Tensor x, Tensor wp, Tensor(a!) y, Tensor(b!)? stats=None) -> int");
   m.def("stem_wgrad(Tensor x, Tensor dy, Tensor(a!) out, Tensor(b!) part) -> ()");
+  m.def("conv_dgrad_s2(Tensor dy, Tensor w, Tensor(a!) dx, Tensor zero, int cfg=0, int max_blocks=0) -> ()");
   m.def("bn_act_backward_pre(Tensor dz, Tensor x, Tensor(a!) dx, Tensor? w, Tensor mean, Tensor invstd, "
         "Tensor(b!) dgamma, Tensor(c!) dbeta, Tensor part, int rows, Tensor(d!)? gw_acc=None, "
         "Tensor(e!)? gb_acc=None) -> ()");
@@ -1241,6 +1293,7 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("bn_act_backward", &bn_act_backward);
   m.impl("bn_act_backward_pre", &bn_act_backward_pre);
   m.impl("stem_pack", &stem_pack);
+  m.impl("conv_dgrad_s2", &conv_dgrad_s2);
   m.impl("stem_fwd", &stem_fwd);
   m.impl("stem_wgrad", &stem_wgrad);
   m.impl("bn_relu_pool_forward", &bn_relu_pool_forward);

@@ -68,6 +68,11 @@ struct ConvGeo {
   const uint16_t* zero;   // >= 64 zero bf16
   int H, W, C, OH, OW, S, P, KW;
   const float* bias;      // optional per-output-channel bias (gemm_nt / conv_nt epilogue)
+  // gemm_nt output row remap (stride-2 grad-input parity classes): RH > 0 stores
+  // row m = (n, oh, ow) of the OH x OW class grid at image row
+  // (n * RH + 2 oh + RA) * RW + 2 ow + RB of the RH x RW output; RZ also writes
+  // zeros to the three other parity positions (1x1 stride-2: those get no tap)
+  int RH, RW, RA, RB, RZ;
 };
 
 // BatchNorm-backward epilogue (grad-input GEMM of the convolution that consumes
@@ -328,6 +333,17 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
 #pragma unroll
       for (int ms = 0; ms < MSB; ++ms) {
         const int64_t m = mbase + wm * Cfg::WTM + ms * 16 + fr;
+        int64_t orow = m;     // output row (remapped for stride-2 grad-input classes)
+        int zr = 0, zc = 0;   // RZ: sibling row / column inside the image
+        if (geo.RH) {
+          const uint32_t ohw = (uint32_t)(geo.OH * geo.OW);
+          const uint32_t mu = (uint32_t)(m < M ? m : M - 1);
+          const uint32_t ni = mu / ohw, rem = mu - ni * ohw;
+          const uint32_t oh = rem / (uint32_t)geo.OW, ow = rem - oh * (uint32_t)geo.OW;
+          orow = ((int64_t)ni * geo.RH + 2 * oh + geo.RA) * geo.RW + 2 * ow + geo.RB;
+          zr = (int)(2 * oh + 1) < geo.RH;
+          zc = (int)(2 * ow + 1) < geo.RW;
+        }
         uint4 eh[2], ed[2];   // BN-backward operands of this row: h, dy2 and the mask byte per pair
         uint32_t em[2];
         if (BNB_OK && bnb) {
@@ -390,13 +406,21 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
             }
             v = make_uint4(o[0], o[1], o[2], o[3]);
           }
-          if (full || m < M) *reinterpret_cast<uint4*>(C + m * ldc + n) = v;
+          if (full || m < M) {
+            *reinterpret_cast<uint4*>(C + orow * ldc + n) = v;
+            if (geo.RZ) {
+              const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+              if (zc) *reinterpret_cast<uint4*>(C + (orow + 1) * ldc + n) = z;
+              if (zr) *reinterpret_cast<uint4*>(C + (orow + geo.RW) * ldc + n) = z;
+              if (zr && zc) *reinterpret_cast<uint4*>(C + (orow + geo.RW + 1) * ldc + n) = z;
+            }
+          }
         }
 #pragma unroll
         for (int ns = 0; ns < 4; ++ns) acc[ms][ns] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
-      if (full) st1 = Cfg::NST;
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // skipped stores: keep the counts exact
+      if (full && !geo.RZ) st1 = Cfg::NST;
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // skipped / extra stores: keep the counts exact
     }
   }
   if (stats) {
@@ -882,6 +906,16 @@ int conv_nt_bf16(const void* X, const void* zero, int H, int W, int C, int OH, i
   const BnBwd bb = bn ? BnBwd{bn->h, bn->dy2, bn->mask} : BnBwd{};
   return nt_dispatch<true>(X, C, B, K, Y, N, M, N, K, cfg, max_blocks, g, stats, (int64_t)stats_rows * N, stats_rows,
                            bb, stream);
+}
+
+int conv_nt_remap_bf16(const void* X, int64_t ldx, const void* zero, int H, int W, int C, int OH, int OW, int KH,
+                       int KW, const void* B, void* Y, int64_t M, int N, int RH, int RW, int RA, int RB, int RZ,
+                       int cfg, int max_blocks, hipStream_t stream) {
+  ConvGeo g{static_cast<const uint16_t*>(zero), H, W, C, OH, OW, 1, 0, KW, nullptr, RH, RW, RA, RB, RZ};
+  const int K = KH * KW * C;
+  if (KH * KW == 1)   // one tap at the class pixel itself: the plain row GEMM
+    return nt_dispatch<false>(X, ldx, B, K, Y, N, M, N, K, cfg, max_blocks, g, nullptr, 0, 0, BnBwd{}, stream);
+  return nt_dispatch<true>(X, C, B, K, Y, N, M, N, K, cfg, max_blocks, g, nullptr, 0, 0, BnBwd{}, stream);
 }
 
 template <int WN, int WK, int WS, bool GATHER, int MSN = 1>

@@ -296,6 +296,14 @@ void gemm_tn_acc_f32(const void* G, int64_t ldg, const void* X, int64_t ldx, flo
 int conv_nt_bf16(const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P, int KH, int KW,
                  const void* B, void* Y, int64_t M, int N, int cfg, int max_blocks, float* stats, int stats_rows,
                  const float* bias, const BnBwdArgs* bn, hipStream_t stream);
+// One parity class (RA, RB) of a stride-2 convolution's grad-input as a stride-1,
+// padding-0 KHxKW implicit GEMM over dY (H x W x C, the forward output) whose
+// OH x OW output grid is stored at rows (n*RH + 2 oh + RA) * RW + 2 ow + RB of
+// the RH x RW grad-input (RZ: zeros at the other three parities); KH = KW = 1
+// runs the plain row GEMM over X = dY rows (row stride ldx).
+int conv_nt_remap_bf16(const void* X, int64_t ldx, const void* zero, int H, int W, int C, int OH, int OW, int KH,
+                       int KW, const void* B, void* Y, int64_t M, int N, int RH, int RW, int RA, int RB, int RZ,
+                       int cfg, int max_blocks, hipStream_t stream);
 void conv_tn_acc_f32(const void* G, const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P,
                      int KH, int KW, float* Wout, int64_t M, int N, int cfg, int splits, hipStream_t stream);
 

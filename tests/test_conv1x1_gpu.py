@@ -153,3 +153,25 @@ def test_fastconv_bias(k, s, hip_only):
     assert (y.float() - yr).abs().max().item() <= 1e-2 * yr.abs().max().item() + 1e-2
     assert (m.bias.grad - br.grad).abs().max().item() <= 1e-3 * br.grad.abs().max().item() + 1e-3
     assert (x.grad.float() - xr.grad).abs().max().item() <= 1e-2 * xr.grad.abs().max().item() + 1e-3
+
+
+@pytest.mark.parametrize("cfg", [1, 4, 124, 125])
+@pytest.mark.parametrize("N,C,H,W,K,k", [(2, 64, 10, 10, 128, 3), (3, 128, 9, 7, 64, 3), (2, 64, 12, 12, 256, 1),
+                                         (2, 128, 9, 11, 128, 1)])
+def test_conv_dgrad_s2_parity_classes(cfg, N, C, H, W, K, k):
+    """Stride-2 grad-input as four stride-1 parity-class GEMMs (remapped
+    epilogue; 1x1: zeros on the untouched parities) == conv_transpose."""
+    g = torch.ops.gksgd
+    torch.manual_seed(cfg + C + k)
+    p = k // 2
+    OH, OW = (H + 2 * p - k) // 2 + 1, (W + 2 * p - k) // 2 + 1
+    dy = torch.randn(N, K, OH, OW, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, k, k, device="cuda") * 0.1).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dx = torch.full((N, C, H, W), float("nan"), device="cuda").to(torch.bfloat16)
+    dx = dx.contiguous(memory_format=torch.channels_last)
+    z = torch.zeros(256, dtype=torch.bfloat16, device="cuda")
+    g.conv_dgrad_s2(dy, w, dx, z, cfg, 0)
+    torch.cuda.synchronize()
+    ref = torch.nn.grad.conv2d_input((N, C, H, W), w.float(), dy.float(), stride=2, padding=p)
+    assert not torch.isnan(dx.float()).any()
+    assert (dx.float() - ref).abs().max().item() <= 1e-2 * ref.abs().max().item() + 1e-3
