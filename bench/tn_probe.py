@@ -84,10 +84,14 @@ def main():
                 res["hip %d/%d" % (c, sp)] = timeit(fn)
             except RuntimeError:
                 res["hip %d/%d" % (c, sp)] = None
+        if k == 3 and s == 1 and g.wgrad3_supported(H, H, C, K):
+            part = torch.empty(int(g.wgrad3_ws(N, H, H, C, K)), device=dev)
+            res["w3 tap-parallel"] = timeit(lambda: g.conv3_wgrad(dy, x, out, part))
         res["miopen"] = timeit(lambda: torch.ops.aten.convolution_backward(
             dy, x, w, None, [s, s], [k // 2, k // 2], [1, 1], False, [0, 0], 1, [False, True, False]))
         best = min((t, kk) for kk, t in res.items() if t)
         r = {"shape": "conv wgrad N=%d C=%d H=%d K=%d k=%d s=%d" % (N, C, H, K, k, s), "best": best[1],
+             "w3_us": round(res["w3 tap-parallel"] * 1e6, 1) if "w3 tap-parallel" in res else None,
              "best_us": round(best[0] * 1e6, 1), "best_pct_peak": round(100 * flops / best[0] / PEAK, 1),
              "miopen_us": round(res["miopen"] * 1e6, 1),
              "all_us": {kk: (round(t * 1e6, 1) if t else None) for kk, t in res.items()}}

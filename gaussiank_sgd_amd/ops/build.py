@@ -47,6 +47,7 @@ HIP_SOURCES = [
     "kernels/linear.hip",
     "kernels/lstm.hip",
     "kernels/stem.hip",
+    "kernels/wgrad3.hip",
 ]
 CXX_SOURCES = [
     "comm/rccl_engine.cpp",

@@ -280,11 +280,21 @@ def _wgrad_into(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, s: int, out_
         z = _zero(x.device)
         run = lambda o, c, sp: g.conv_tn_acc(dy, x, o, z, s, p, c, sp)  # noqa: E731
     cands = [(("hip", c, sp), (lambda c=c, sp=sp: run(scratch, c, sp))) for c, sp in _TN_CFGS]
+    w3 = None
+    if k == 3 and s == 1 and g.wgrad3_supported(H, W, C, K):
+        # tap-parallel kernel (wgrad3.hip): dY and X staged once per band for all 9 taps
+        def w3(o):
+            part = torch.empty(int(g.wgrad3_ws(N, H, W, C, K)), dtype=torch.float32, device=x.device)
+            g.conv3_wgrad(dy, x, o, part)
+        cands.append((("w3", 0, 0), lambda: w3(scratch)))
     cands.append((("miopen", 0, 0), miopen))
     ch = _pick(key, cands)
     if ch[0] == "miopen":
         from . import accum_grad_
         accum_grad_(out_f32, miopen().contiguous(memory_format=_CL))
+        return
+    if ch[0] == "w3" and w3 is not None:
+        w3(out_f32)
         return
     run(out_f32, ch[1], ch[2])
 

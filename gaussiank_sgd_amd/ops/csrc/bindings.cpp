@@ -966,6 +966,33 @@ void conv_dgrad_s2(at::Tensor dy, at::Tensor w, at::Tensor dx, at::Tensor zero, 
   }
 }
 
+// tap-parallel 3x3 stride-1 grad-weight (wgrad3.hip): out (fp32 [K, C, 3, 3]) += dW
+int64_t wgrad3_ws(int64_t N, int64_t H, int64_t W, int64_t C, int64_t K) {
+  return gk::wgrad3_ws_floats((int)N, (int)H, (int)W, (int)C, (int)K);
+}
+
+void conv3_wgrad(at::Tensor dy, at::Tensor x, at::Tensor out, at::Tensor part) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv3_wgrad: x must be channels-last bf16 [N, C, H, W]");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 && dy.size(0) == N &&
+                  dy.size(2) == H && dy.size(3) == W && dy.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv3_wgrad: dy must be channels-last bf16 [N, K, H, W]");
+  const int64_t K = dy.size(1);
+  TORCH_CHECK(gk::wgrad3_supported((int)H, (int)W, (int)C, (int)K), "conv3_wgrad: unsupported shape");
+  TORCH_CHECK(N * H * W < (int64_t(1) << 31), "conv3_wgrad: too many pixels");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.dim() == 4 && out.size(0) == K &&
+                  out.size(1) == C && out.size(2) == 3 && out.size(3) == 3,
+              "conv3_wgrad: out must be fp32 [K, C, 3, 3]");
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() &&
+                  part.numel() >= wgrad3_ws(N, H, W, C, K),
+              "conv3_wgrad: part must hold wgrad3_ws floats");
+  c10::DeviceGuard guard(x.device());
+  gk::wgrad3_acc(dy.data_ptr(), x.data_ptr(), (int)N, (int)H, (int)W, (int)C, (int)K, part.data_ptr<float>(),
+                 out.data_ptr<float>(), out.stride(0), out.stride(1), out.stride(2), out.stride(3), cur_stream(x));
+}
+
 // wout: fp32 [Cout, C, KH, KW] channels-last (memory [Cout][KH][KW][C]); += dW
 void conv_tn_acc(at::Tensor dy, at::Tensor x, at::Tensor wout, at::Tensor zero, int64_t stride, int64_t pad,
                  int64_t cfg, int64_t splits) {
@@ -1232,6 +1259,11 @@ TORCH_LIBRARY(gksgd, m) {
   m.def("stem_pack(Tensor w, Tensor(a!) wp) -> ()");
   m.def("stem_fwd(Tensor x, Tensor wp, Tensor(a!) y, Tensor(b!)? stats=None) -> int");
   m.def("stem_wgrad(Tensor x, Tensor dy, Tensor(a!) out, Tensor(b!) part) -> ()");
+  m.def("wgrad3_supported(int H, int W, int C, int K) -> bool", [](int64_t H, int64_t W, int64_t C, int64_t K) {
+    return gk::wgrad3_supported((int)H, (int)W, (int)C, (int)K);
+  });
+  m.def("wgrad3_ws(int N, int H, int W, int C, int K) -> int", &wgrad3_ws);
+  m.def("conv3_wgrad(Tensor dy, Tensor x, Tensor(a!) out, Tensor(b!) part) -> ()");
   m.def("conv_dgrad_s2(Tensor dy, Tensor w, Tensor(a!) dx, Tensor zero, int cfg=0, int max_blocks=0) -> ()");
   m.def("bn_act_backward_pre(Tensor dz, Tensor x, Tensor(a!) dx, Tensor? w, Tensor mean, Tensor invstd, "
         "Tensor(b!) dgamma, Tensor(c!) dbeta, Tensor part, int rows, Tensor(d!)? gw_acc=None, "
@@ -1294,6 +1326,7 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("bn_act_backward_pre", &bn_act_backward_pre);
   m.impl("stem_pack", &stem_pack);
   m.impl("conv_dgrad_s2", &conv_dgrad_s2);
+  m.impl("conv3_wgrad", &conv3_wgrad);
   m.impl("stem_fwd", &stem_fwd);
   m.impl("stem_wgrad", &stem_wgrad);
   m.impl("bn_relu_pool_forward", &bn_relu_pool_forward);

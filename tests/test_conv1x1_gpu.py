@@ -175,3 +175,24 @@ def test_conv_dgrad_s2_parity_classes(cfg, N, C, H, W, K, k):
     ref = torch.nn.grad.conv2d_input((N, C, H, W), w.float(), dy.float(), stride=2, padding=p)
     assert not torch.isnan(dx.float()).any()
     assert (dx.float() - ref).abs().max().item() <= 1e-2 * ref.abs().max().item() + 1e-3
+
+
+@pytest.mark.parametrize("N,C,H,W,K", [(2, 64, 10, 10, 64), (3, 128, 7, 9, 64), (2, 64, 14, 14, 192),
+                                       (1, 64, 30, 12, 128), (2, 128, 5, 40, 128)])
+def test_conv3_wgrad_tap_parallel(N, C, H, W, K):
+    """Tap-parallel 3x3 grad-weight (wgrad3.hip) == PyTorch's, accumulated into
+    a pre-filled fp32 output in either memory format."""
+    g = torch.ops.gksgd
+    torch.manual_seed(N + C + H + K)
+    x = torch.randn(N, C, H, W, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(N, K, H, W, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    for cl in (True, False):
+        out = torch.full((K, C, 3, 3), 0.25, device="cuda")
+        if cl:
+            out = out.contiguous(memory_format=torch.channels_last)
+        part = torch.empty(int(g.wgrad3_ws(N, H, W, C, K)), device="cuda")
+        g.conv3_wgrad(dy, x, out, part)
+        torch.cuda.synchronize()
+        ref = torch.nn.grad.conv2d_weight(x.float(), (K, C, 3, 3), dy.float(), padding=1) + 0.25
+        err = (out - ref).abs().max().item()
+        assert err <= 2e-3 * (ref - 0.25).abs().max().item() + 1e-3, (cl, err)
