@@ -86,7 +86,7 @@ def main():
                 res["hip %d/%d" % (c, sp)] = None
         if k == 3 and s == 1 and g.wgrad3_supported(H, H, C, K):
             part = torch.empty(int(g.wgrad3_ws(N, H, H, C, K)), device=dev)
-            res["w3 tap-parallel"] = timeit(lambda: g.conv3_wgrad(dy, x, out, part))
+            res["w3 tap-parallel"] = timeit(lambda: g.conv3_wgrad(dy, x, out, part, torch.zeros(256, dtype=torch.bfloat16, device=x.device)))
         res["miopen"] = timeit(lambda: torch.ops.aten.convolution_backward(
             dy, x, w, None, [s, s], [k // 2, k // 2], [1, 1], False, [0, 0], 1, [False, True, False]))
         best = min((t, kk) for kk, t in res.items() if t)

@@ -43,7 +43,7 @@ def main():
         dy = torch.randn(N, K, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         out = torch.zeros(K, C, 3, 3, device="cuda").contiguous(memory_format=torch.channels_last)
         part = torch.empty(int(g.wgrad3_ws(N, H, H, C, K)), device="cuda")
-        t = timeit(lambda: g.conv3_wgrad(dy, x, out, part))
+        t = timeit(lambda: g.conv3_wgrad(dy, x, out, part, torch.zeros(256, dtype=torch.bfloat16, device=x.device)))
         flops = 2.0 * N * H * H * C * K * 9
         r = {"shape": "N=%d C=%d H=%d K=%d" % (N, C, H, K), "us": round(t * 1e6, 1),
              "pct_peak": round(100 * flops / t / 2.5e15, 1)}

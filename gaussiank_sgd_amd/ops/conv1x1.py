@@ -285,7 +285,7 @@ def _wgrad_into(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, s: int, out_
         # tap-parallel kernel (wgrad3.hip): dY and X staged once per band for all 9 taps
         def w3(o):
             part = torch.empty(int(g.wgrad3_ws(N, H, W, C, K)), dtype=torch.float32, device=x.device)
-            g.conv3_wgrad(dy, x, o, part)
+            g.conv3_wgrad(dy, x, o, part, _zero(x.device))
         cands.append((("w3", 0, 0), lambda: w3(scratch)))
     cands.append((("miopen", 0, 0), miopen))
     ch = _pick(key, cands)

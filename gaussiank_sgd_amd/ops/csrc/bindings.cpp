@@ -971,7 +971,7 @@ int64_t wgrad3_ws(int64_t N, int64_t H, int64_t W, int64_t C, int64_t K) {
   return gk::wgrad3_ws_floats((int)N, (int)H, (int)W, (int)C, (int)K);
 }
 
-void conv3_wgrad(at::Tensor dy, at::Tensor x, at::Tensor out, at::Tensor part) {
+void conv3_wgrad(at::Tensor dy, at::Tensor x, at::Tensor out, at::Tensor part, at::Tensor zero) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast),
               "conv3_wgrad: x must be channels-last bf16 [N, C, H, W]");
@@ -989,7 +989,9 @@ void conv3_wgrad(at::Tensor dy, at::Tensor x, at::Tensor out, at::Tensor part) {
                   part.numel() >= wgrad3_ws(N, H, W, C, K),
               "conv3_wgrad: part must hold wgrad3_ws floats");
   c10::DeviceGuard guard(x.device());
-  gk::wgrad3_acc(dy.data_ptr(), x.data_ptr(), (int)N, (int)H, (int)W, (int)C, (int)K, part.data_ptr<float>(),
+  TORCH_CHECK(zero.is_cuda() && zero.scalar_type() == at::kBFloat16 && zero.numel() >= 64, "zero: >= 64 bf16");
+  gk::wgrad3_acc(dy.data_ptr(), x.data_ptr(), zero.data_ptr(), (int)N, (int)H, (int)W, (int)C, (int)K,
+                 part.data_ptr<float>(),
                  out.data_ptr<float>(), out.stride(0), out.stride(1), out.stride(2), out.stride(3), cur_stream(x));
 }
 
@@ -1263,7 +1265,7 @@ TORCH_LIBRARY(gksgd, m) {
     return gk::wgrad3_supported((int)H, (int)W, (int)C, (int)K);
   });
   m.def("wgrad3_ws(int N, int H, int W, int C, int K) -> int", &wgrad3_ws);
-  m.def("conv3_wgrad(Tensor dy, Tensor x, Tensor(a!) out, Tensor(b!) part) -> ()");
+  m.def("conv3_wgrad(Tensor dy, Tensor x, Tensor(a!) out, Tensor(b!) part, Tensor zero) -> ()");
   m.def("conv_dgrad_s2(Tensor dy, Tensor w, Tensor(a!) dx, Tensor zero, int cfg=0, int max_blocks=0) -> ()");
   m.def("bn_act_backward_pre(Tensor dz, Tensor x, Tensor(a!) dx, Tensor? w, Tensor mean, Tensor invstd, "
         "Tensor(b!) dgamma, Tensor(c!) dbeta, Tensor part, int rows, Tensor(d!)? gw_acc=None, "

@@ -330,12 +330,12 @@ void stem_wgrad(const void* x, bool x_f32, int N, int H, int W, const uint16_t* 
 // 3x3 / stride-1 / pad-1 convolution grad-weight, tap-parallel (wgrad3.hip):
 // dy [N, H, W, K], x [N, H, W, C] channels-last bf16; out (fp32 [K][C][3][3]
 // with element strides s0..s3) += dW via per-block partials
-// part[wgrad3_ws_floats] summed in a fixed order.
+// part[wgrad3_ws_floats] summed in a fixed order; zero: >= 64 zero bf16.
 // ---------------------------------------------------------------------------
 bool wgrad3_supported(int H, int W, int C, int K);
 int64_t wgrad3_ws_floats(int N, int H, int W, int C, int K);
-void wgrad3_acc(const void* dy, const void* x, int N, int H, int W, int C, int K, float* part, float* out, int64_t s0,
-                int64_t s1, int64_t s2, int64_t s3, hipStream_t stream);
+void wgrad3_acc(const void* dy, const void* x, const void* zero, int N, int H, int W, int C, int K, float* part,
+                float* out, int64_t s0, int64_t s1, int64_t s2, int64_t s3, hipStream_t stream);
 
 // ---------------------------------------------------------------------------
 // Fused residual add (+ dropout) + LayerNorm over rows of H bf16 (ln.hip).

@@ -191,7 +191,7 @@ def test_conv3_wgrad_tap_parallel(N, C, H, W, K):
         if cl:
             out = out.contiguous(memory_format=torch.channels_last)
         part = torch.empty(int(g.wgrad3_ws(N, H, W, C, K)), device="cuda")
-        g.conv3_wgrad(dy, x, out, part)
+        g.conv3_wgrad(dy, x, out, part, torch.zeros(256, dtype=torch.bfloat16, device=x.device))
         torch.cuda.synchronize()
         ref = torch.nn.grad.conv2d_weight(x.float(), (K, C, 3, 3), dy.float(), padding=1) + 0.25
         err = (out - ref).abs().max().item()
