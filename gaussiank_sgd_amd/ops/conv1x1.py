@@ -38,7 +38,8 @@ _ENABLED = os.environ.get("GKSGD_FASTCONV", "1") != "0"
 _choices: Dict[tuple, tuple] = {}
 _timings: Dict[tuple, list] = {}      # key -> [(tag, ms or error)] of the search
 # candidate kernel configurations (gemm.hip: cfg digits = tile + 10*panel + 100*stages)
-_NT_CFGS = [1, 2, 3, 4, 11, 13, 21, 22, 23, 24, 111, 113, 121, 122, 123, 124, 25, 26, 27, 125, 126, 127]
+_NT_CFGS = [1, 2, 3, 4, 11, 13, 21, 22, 23, 24, 111, 113, 121, 122, 123, 124, 25, 26, 27, 125, 126, 127,
+            211, 212, 213, 214, 221, 222, 223, 224]   # 2xx: four LDS stages (more bytes in flight)
 # grid override: 0 = persistent (about two blocks per CU), else a fixed block count
 _NT_GRIDS = (0, 512, 1 << 20)
 _TN_CFGS = [(c, s) for c in (1, 2, 3, 4, 5, 6, 7, 8, 21, 22, 23, 24, 27, 9, 29, 101, 121, 102, 122) for s in (0, 128)]

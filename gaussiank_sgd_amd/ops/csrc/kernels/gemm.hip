@@ -128,6 +128,7 @@ struct NtCfg {
   static constexpr int LPWA = BRES ? LPW : (BM / 8) / NW;   // of which A-row instructions (j < LPWA)
   static constexpr int NST = 2 * MSB;             // 16-byte epilogue stores per wave per tile
   static_assert(LPW + 2 * NST <= 63, "wait_vmcnt range (vmcnt is 6 bits)");
+  static constexpr bool NS4_OK = 2 * LPW + 3 * NST <= 63;   // four stages: 2 stages + 3 tiles of stores in flight
   static int lds_bytes(int K, int ns) { return ns * STAGE + (BRES ? BN * K * 2 : 0); }
 };
 
@@ -145,7 +146,7 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
   static_assert(!BNB || MSB == 4, "BN-backward epilogue: 64x64 wave tiles");
   constexpr bool BNB_OK = BNB;
   constexpr bool bnb = BNB;
-  static_assert(NS == 2 || NS == 3, "stages");
+  static_assert(NS >= 2 && NS <= 4, "stages");
   constexpr int LPW = Cfg::LPW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
@@ -267,11 +268,12 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
     for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   stage();
-  if (NS == 3 && T > 1) stage();
+  if (NS >= 3 && T > 1) stage();
+  if (NS == 4 && T > 2) stage();
   const int fr = lane & 15, fq = lane >> 4;
   // stores issued by the last two steps (0 when none, or when a partial tile
   // drained its stores with vmcnt(0) right away)
-  int st1 = 0, st2 = 0;
+  int st1 = 0, st2 = 0, st3 = 0;
   int ks = 0;
   int buf = 0;
   float ssum[4][4], ssq[4][4];   // BN partials: [ns][r] of this lane's column, summed over its rows
@@ -291,8 +293,10 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
   for (int t = 0; t < T; ++t) {
     // ops issued after stage(t), in order: NS=2: stores(t-1);
     // NS=3: stores(t-2), stage(t+1), stores(t-1).  Retire stage(t) only.
+    // after stage(t): stores(t-NS+1..t-1) and the stages t+1 .. t+NS-2 issued since
     if (NS == 2) wait_vmcnt(st1);
-    else wait_vmcnt(st2 + (t + 1 < T ? LPW : 0) + st1);
+    else if (NS == 3) wait_vmcnt(st2 + (t + 1 < T ? LPW : 0) + st1);
+    else wait_vmcnt(st3 + st2 + st1 + ((t + 1 < T) + (t + 2 < T)) * LPW);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     if (s_t < T) stage();
@@ -319,6 +323,7 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
         for (int ns = 0; ns < 4; ++ns)
           acc[ms][ns] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv[ns], av[ms], acc[ms][ns], 0, 0, 0);
     }
+    st3 = st2;
     st2 = st1;
     st1 = 0;
     if (++ks == nk) {
@@ -496,6 +501,10 @@ int launch_nt_any(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb
   if (bres < 0) bres = (64 * WN) * K * 2 <= 64 * 1024;
   if (bres && NtCfg<WM, WN, true, MSB>::lds_bytes(K, 2) > 160 * 1024) bres = 0;
   constexpr int L = 160 * 1024;
+  if (ns == 4 && bres && NtCfg<WM, WN, true, MSB>::NS4_OK && NtCfg<WM, WN, true, MSB>::lds_bytes(K, 4) <= L)
+    return launch_nt<WM, WN, true, 4, GATHER, MSB, BNB>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, bb, stream);
+  if (ns == 4 && !bres && NtCfg<WM, WN, false, MSB>::NS4_OK && NtCfg<WM, WN, false, MSB>::lds_bytes(K, 4) <= L)
+    return launch_nt<WM, WN, false, 4, GATHER, MSB, BNB>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, bb, stream);
   if (bres) {
     if (ns != 2 && NtCfg<WM, WN, true, MSB>::lds_bytes(K, 3) <= L) return launch_nt<WM, WN, true, 3, GATHER, MSB, BNB>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, bb, stream);
     else return launch_nt<WM, WN, true, 2, GATHER, MSB, BNB>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, bb, stream);
@@ -857,9 +866,10 @@ template <bool GATHER>
 int nt_dispatch(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N,
                 int K, int cfg, int max_blocks, const ConvGeo& geo, float* stats, int64_t stats_ld, int stats_rows,
                 const BnBwd& bb, hipStream_t stream) {
-  // cfg = tile + 10 * panel (1: resident, 2: streamed) + 100 * stages (1: two, 2: three); 0 digits = auto
+  // cfg = tile + 10 * panel (1: resident, 2: streamed) + 100 * stages (0: three, 1: two, 2: four; a
+  // four-stage request falls back to three where the counts or the LDS do not fit)
   const int bres = (cfg / 10) % 10 == 0 ? -1 : ((cfg / 10) % 10 == 1 ? 1 : 0);
-  const int ns = (cfg / 100) % 10 == 1 ? 2 : 3;
+  const int ns = (cfg / 100) % 10 == 1 ? 2 : ((cfg / 100) % 10 == 2 ? 4 : 3);
   cfg %= 10;
   auto a = static_cast<const uint16_t*>(A);
   auto b = static_cast<const uint16_t*>(B);

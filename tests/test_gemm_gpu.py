@@ -22,7 +22,7 @@ def _rand(*shape, scale=1.0):
 
 @pytest.mark.parametrize("M,N,K", [(1000, 64, 64), (4096, 256, 64), (777, 128, 192), (2048, 512, 128),
                                    (513, 192, 320), (300, 256, 1024)])
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 11, 21, 13, 23, 5, 6, 7, 125, 126, 127, 15])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 11, 21, 13, 23, 5, 6, 7, 125, 126, 127, 15, 211, 213, 222, 224])
 def test_gemm_nt(g, M, N, K, cfg):
     torch.manual_seed(M + N + K)
     A = _rand(M, K)
@@ -73,7 +73,7 @@ def _conv_case(N, C, H, Co, k, s, p):
 
 @pytest.mark.parametrize("N,C,H,Co,k,s,p", [(2, 64, 9, 64, 3, 1, 1), (3, 128, 7, 64, 3, 2, 1), (2, 64, 14, 128, 3, 2, 1),
                                             (2, 128, 5, 256, 1, 1, 0), (1, 64, 11, 192, 3, 1, 1)])
-@pytest.mark.parametrize("cfg", [0, 1, 3, 22, 124, 5, 126, 7])
+@pytest.mark.parametrize("cfg", [0, 1, 3, 22, 124, 5, 126, 7, 214, 221])
 def test_conv_nt(g, N, C, H, Co, k, s, p, cfg):
     import torch.nn.functional as F
     torch.manual_seed(N + C + H + Co)
@@ -104,3 +104,18 @@ def test_conv_tn_acc(g, N, C, H, Co, k, s, p, cfg, splits):
     g.conv_tn_acc(dy, x, out, zero, s, p, cfg, splits)
     err = (out - wr.grad).abs().max().item()
     assert err <= 1e-3 * wr.grad.abs().max().item() + 1e-3, err
+
+
+@pytest.mark.parametrize("cfg", [211, 213, 222, 224, 13, 124])
+@pytest.mark.parametrize("mb", [1, 3, 7])
+def test_gemm_nt_deep_pipeline_few_blocks(g, cfg, mb):
+    """Few persistent blocks walking many tiles: every LDS stage of the 3- and
+    4-stage pipelines is reused many times (partial last tile included)."""
+    torch.manual_seed(cfg + mb)
+    M, N, K = 5000 + 37, 256, 128
+    A = _rand(M, K)
+    B = _rand(N, K, scale=K ** -0.5)
+    C = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
+    g.gemm_nt(A, B, C, cfg, mb)
+    ref = A.float() @ B.float().t()
+    assert (C.float() - ref).abs().max().item() <= 1e-2 * ref.abs().max().item() + 1e-3
