@@ -2,8 +2,10 @@
 
 Standard BERT-base: vocab 30522, hidden 768, 12 layers, 12 heads, FFN 3072,
 512 positions, GELU, post-LN, MLM head tied to the word embeddings
-(~110M parameters).  Attention uses ``F.scaled_dot_product_attention`` (the
-ROCm flash-attention path); run under bf16 autocast.  Every encoder / MLM-head
+(~110M parameters).  On the GPU, attention is the flash-style HIP kernel of
+ops/attention.py on the packed QKV projection (no head split / merge copies);
+with an attention mask or on the CPU it is ``F.scaled_dot_product_attention``.
+Run under bf16 autocast.  Every encoder / MLM-head
 linear is a ``FastLinear`` (ops/linear.py: autotuned MFMA GEMMs, GELU backward
 and bias gradient in one fused pass into the fp32 gradient arena).  Gradients stay fp32 in
 the flat arena, so compression is unaffected by the compute dtype.
@@ -17,6 +19,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops import attention
 from ..ops.linear import FastLinear
 from ..ops.ln import add_layernorm
 
@@ -77,9 +80,15 @@ class BertLayer(nn.Module):
 
     def forward(self, x, attn_mask=None):
         B, T, H = x.shape
-        q, k, v = _SplitHeads.apply(self.qkv(x), self.heads)
-        a = F.scaled_dot_product_attention(q, k, v, attn_mask=attn_mask, dropout_p=self.p if self.training else 0.0)
-        a = a.transpose(1, 2).reshape(B, T, H)
+        y = self.qkv(x)
+        if attn_mask is None and attention.fused_available(y, self.heads):
+            # flash-style HIP attention straight on the packed projection (ops/attention.py)
+            a = attention.self_attention(y, self.heads, self.p, self.training)
+        else:
+            q, k, v = _SplitHeads.apply(y, self.heads)
+            a = F.scaled_dot_product_attention(q, k, v, attn_mask=attn_mask,
+                                               dropout_p=self.p if self.training else 0.0)
+            a = a.transpose(1, 2).reshape(B, T, H)
         # ln(x + drop(y)) as one fused HIP pass each way on the GPU (ops/ln.py)
         x = add_layernorm(self.attn_out(a), x, self.ln1, self.p, self.training)
         h = self.ffn_out(self.ffn_in(x, act="gelu"))

@@ -48,12 +48,13 @@ HIP_SOURCES = [
     "kernels/lstm.hip",
     "kernels/stem.hip",
     "kernels/wgrad3.hip",
+    "kernels/attn.hip",
 ]
 CXX_SOURCES = [
     "comm/rccl_engine.cpp",
     "bindings.cpp",
 ]
-HEADERS = ["kernels/common.h", "kernels/gk_kernels.h", "comm/rccl_engine.h"]
+HEADERS = ["kernels/common.h", "kernels/gk_kernels.h", "kernels/mfma_util.h", "comm/rccl_engine.h"]
 # per-file extra flags: the sparse aggregation must round product and sum
 # separately (bit-identical to the reference arithmetic and the CPU mirror)
 EXTRA_FLAGS = {"kernels/scatter.hip": ["-ffp-contract=off"]}

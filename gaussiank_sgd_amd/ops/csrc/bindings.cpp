@@ -1066,6 +1066,55 @@ void add_ln_backward(at::Tensor dy, at::Tensor h, at::Tensor mean, at::Tensor rs
                       cur_stream(h));
 }
 
+// fused self-attention (attn.hip)
+void check_attn(const at::Tensor& t, const char* name, int64_t rows, int64_t cols) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.is_contiguous() && t.numel() == rows * cols &&
+                  reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+              name, " must be a contiguous 16-byte aligned bf16 GPU tensor of ", rows, " x ", cols, " elements");
+}
+
+void check_attn_f32(const at::Tensor& t, const char* name, int64_t n) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == n,
+              name, " must be a contiguous fp32 GPU tensor of ", n, " elements");
+}
+
+void attn_fwd(at::Tensor qkv, at::Tensor out, at::Tensor lse, int64_t heads, double p, int64_t seed) {
+  TORCH_CHECK(qkv.dim() == 3 && qkv.size(2) == 3 * heads * 64, "qkv: [B, T, 3 * heads * 64]");
+  const int64_t B = qkv.size(0), T = qkv.size(1);
+  TORCH_CHECK(gk::attn_supported((int)T, 64), "attn: T must be a multiple of 128");
+  check_attn(qkv, "qkv", B * T, 3 * heads * 64);
+  check_attn(out, "out", B * T, heads * 64);
+  check_attn_f32(lse, "lse", B * heads * T);
+  TORCH_CHECK(p >= 0.0 && p < 1.0, "attn: dropout p in [0, 1)");
+  c10::DeviceGuard guard(qkv.device());
+  gk::attn_fwd(qkv.data_ptr(), out.data_ptr(), lse.data_ptr<float>(), (int)B, (int)T, (int)heads, (float)p,
+               (uint32_t)seed, cur_stream(qkv));
+}
+
+void attn_bwd(at::Tensor qkv, at::Tensor out, at::Tensor dout, at::Tensor lse, at::Tensor delta, at::Tensor dqkv,
+              int64_t heads, double p, int64_t seed) {
+  TORCH_CHECK(qkv.dim() == 3 && qkv.size(2) == 3 * heads * 64, "qkv: [B, T, 3 * heads * 64]");
+  const int64_t B = qkv.size(0), T = qkv.size(1);
+  TORCH_CHECK(gk::attn_supported((int)T, 64), "attn: T must be a multiple of 128");
+  check_attn(qkv, "qkv", B * T, 3 * heads * 64);
+  check_attn(dqkv, "dqkv", B * T, 3 * heads * 64);
+  check_attn(out, "out", B * T, heads * 64);
+  check_attn(dout, "dout", B * T, heads * 64);
+  check_attn_f32(lse, "lse", B * heads * T);
+  check_attn_f32(delta, "delta", B * heads * T);
+  c10::DeviceGuard guard(qkv.device());
+  gk::attn_bwd(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
+               dqkv.data_ptr(), (int)B, (int)T, (int)heads, (float)p, (uint32_t)seed, cur_stream(qkv));
+}
+
+void attn_dropout_mask(at::Tensor mask, int64_t B, int64_t heads, int64_t T, double p, int64_t seed) {
+  TORCH_CHECK(mask.is_cuda() && mask.scalar_type() == at::kByte && mask.is_contiguous() &&
+                  mask.numel() == B * heads * T * T, "mask: contiguous uint8 [B, heads, T, T]");
+  c10::DeviceGuard guard(mask.device());
+  gk::attn_dropout_mask(mask.data_ptr<uint8_t>(), (int)B, (int)heads, (int)T, (float)p, (uint32_t)seed,
+                        cur_stream(mask));
+}
+
 // linear-layer column passes (linear.hip): bias gradient / fused GELU backward
 void check_bf16_2d(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 2 && t.is_contiguous() &&
@@ -1270,6 +1319,12 @@ TORCH_LIBRARY(gksgd, m) {
   m.def("bn_act_backward_pre(Tensor dz, Tensor x, Tensor(a!) dx, Tensor? w, Tensor mean, Tensor invstd, "
         "Tensor(b!) dgamma, Tensor(c!) dbeta, Tensor part, int rows, Tensor(d!)? gw_acc=None, "
         "Tensor(e!)? gb_acc=None) -> ()");
+  m.def("attn_supported(int T, int D) -> bool",
+        [](int64_t T, int64_t D) { return gk::attn_supported((int)T, (int)D); });
+  m.def("attn_fwd(Tensor qkv, Tensor(a!) out, Tensor(b!) lse, int heads, float p, int seed) -> ()");
+  m.def("attn_bwd(Tensor qkv, Tensor out, Tensor dout, Tensor lse, Tensor(a!) delta, Tensor(b!) dqkv, int heads, "
+        "float p, int seed) -> ()");
+  m.def("attn_dropout_mask(Tensor(a!) mask, int B, int heads, int T, float p, int seed) -> ()");
   m.def("add_ln_supported(int H) -> bool", &add_ln_supported);
   m.def("add_ln_ws_floats(int R, int H) -> int", &add_ln_ws_floats);
   m.def("add_ln_forward(Tensor a, Tensor x, Tensor? gamma, Tensor? beta, Tensor(a!) y, Tensor(b!) h, "
@@ -1341,6 +1396,9 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("gemm_tn_acc", &gemm_tn_acc);
   m.impl("conv_nt", &conv_nt);
   m.impl("conv_tn_acc", &conv_tn_acc);
+  m.impl("attn_fwd", &attn_fwd);
+  m.impl("attn_bwd", &attn_bwd);
+  m.impl("attn_dropout_mask", &attn_dropout_mask);
   m.impl("add_ln_forward", &add_ln_forward);
   m.impl("add_ln_backward", &add_ln_backward);
   m.impl("colsum_acc", &colsum_acc);

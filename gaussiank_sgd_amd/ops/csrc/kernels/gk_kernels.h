@@ -338,6 +338,19 @@ void wgrad3_acc(const void* dy, const void* x, const void* zero, int N, int H, i
                 float* out, int64_t s0, int64_t s1, int64_t s2, int64_t s3, hipStream_t stream);
 
 // ---------------------------------------------------------------------------
+// Fused multi-head self-attention, head dim 64 (attn.hip).  qkv / dqkv:
+// [B, T, 3, H, 64] bf16; out / dout: [B, T, H, 64] bf16; lse / delta: fp32
+// [B, H, T].  Dropout p on the attention probabilities with a hash mask
+// (seed); attn_dropout_mask materialises the same mask as [B, H, T, T] bytes.
+// ---------------------------------------------------------------------------
+bool attn_supported(int T, int D);
+void attn_fwd(const void* qkv, void* out, float* lse, int B, int T, int H, float p, uint32_t seed,
+              hipStream_t stream);
+void attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* delta, void* dqkv, int B,
+              int T, int H, float p, uint32_t seed, hipStream_t stream);
+void attn_dropout_mask(uint8_t* mask, int B, int H, int T, float p, uint32_t seed, hipStream_t stream);
+
+// ---------------------------------------------------------------------------
 // Fused residual add (+ dropout) + LayerNorm over rows of H bf16 (ln.hip).
 // forward : h = x + dropout_p(a), y = LN(h) * gamma + beta; saves h (bf16),
 //           mean, rstd (fp32 per row).  The dropout mask is a hash of
