@@ -50,9 +50,10 @@ def dropout_mask(B: int, heads: int, T: int, p: float, seed: int, device) -> tor
         m = torch.empty(B, heads, T, T, dtype=torch.uint8, device=device)
         _ops().attn_dropout_mask(m, B, heads, T, float(p), int(seed))
         return m.bool()
-    idx = torch.arange(B * heads * T * T, dtype=torch.int64)
-    keep = (hash_u32(idx, int(seed) & 0xFFFFFFFF) >> 16) >= drop_threshold(p)
-    return keep.view(B, heads, T, T)
+    # one 32-bit hash per pair of keys: low half -> even key, high half -> odd key
+    h = hash_u32(torch.arange(B * heads * T * T // 2, dtype=torch.int64), int(seed) & 0xFFFFFFFF)
+    u = torch.stack([h & 0xFFFF, h >> 16], dim=1)
+    return (u >= drop_threshold(p)).view(B, heads, T, T)
 
 
 def reference_attention(qkv: torch.Tensor, heads: int, p: float = 0.0, seed: int = 0) -> torch.Tensor:
