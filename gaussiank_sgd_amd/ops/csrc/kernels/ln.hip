@@ -21,7 +21,8 @@ namespace gk {
 namespace {
 
 constexpr int kLnMaxChunks = 8;          // per lane: H <= 64 * 8 * 8 = 4096
-constexpr int kLnRowsPerWave = 8;        // backward: rows per wave before column partials are flushed
+constexpr int kLnRowsPerWave = 4;        // backward: rows per wave (RPW at a time)
+constexpr int kLnRowsPerBlock = kLnRowsPerWave * kWavesPerBlock;   // backward: one partial row per block
 
 __device__ __forceinline__ void load8(const uint16_t* p, float* v) {
   const uint4 u = *reinterpret_cast<const uint4*>(p);
@@ -31,6 +32,12 @@ __device__ __forceinline__ void load8(const uint16_t* p, float* v) {
     v[2 * i] = __uint_as_float(w[i] << 16);
     v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
   }
+}
+
+__device__ __forceinline__ void load8f(const float* p, float* v) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
 __device__ __forceinline__ uint32_t bf16r(float f) {
@@ -52,7 +59,19 @@ __device__ __forceinline__ bool keep(uint32_t seed, int64_t row, int col, uint32
   return hash_u32((uint32_t)(row * 8191 + col), seed ^ (uint32_t)(row >> 19)) < thr;
 }
 
-template <int CH>
+// sum over the L lanes of one row (L = 64 / rows-per-wave, a power of two)
+template <int L>
+__device__ __forceinline__ float row_sum(float v) {
+#pragma unroll
+  for (int off = L / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// RPW rows per wave, L = 64 / RPW lanes per row; lane sl owns 16-byte chunks
+// sl + L j (j < CH) of its row.  BERT's H = 768 is 96 chunks: 2 rows per wave
+// x 32 lanes x 3 chunks, every lane busy (one row per wave left half the
+// lanes idle on the second chunk)
+template <int CH, int RPW>
 __global__ __launch_bounds__(kBlock) void add_ln_fwd_kernel(const uint16_t* __restrict__ a,
                                                             const uint16_t* __restrict__ x,
                                                             const float* __restrict__ gamma,
@@ -60,16 +79,21 @@ __global__ __launch_bounds__(kBlock) void add_ln_fwd_kernel(const uint16_t* __re
                                                             uint16_t* __restrict__ hsave, float* __restrict__ mean,
                                                             float* __restrict__ rstd, int64_t R, int H, float eps,
                                                             uint32_t seed, uint32_t thr, float scale) {
-  const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-  if (row >= R) return;
+  constexpr int L = 64 / RPW;
+  const int lane = threadIdx.x & 63, sl = lane % L;
+  const int64_t row0 = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * RPW;
+  if (row0 >= R) return;
+  const int64_t row = row0 + lane / L;
+  const bool rv = row < R;
   const int nc = H >> 3;
   float h[CH][8];
   float s = 0.f;
 #pragma unroll
   for (int j = 0; j < CH; ++j) {
-    const int c = lane + j * 64;
-    if (c < nc) {
+    const int c = sl + j * L;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[j][i] = 0.f;
+    if (rv && c < nc) {
       float av[8], xv[8];
       load8(a + row * H + c * 8, av);
       load8(x + row * H + c * 8, xv);
@@ -81,71 +105,77 @@ __global__ __launch_bounds__(kBlock) void add_ln_fwd_kernel(const uint16_t* __re
       }
     }
   }
-  const float mu = wave_sum(s) / (float)H;
+  const float mu = row_sum<L>(s) / (float)H;
   float q = 0.f;
 #pragma unroll
   for (int j = 0; j < CH; ++j)
-    if (lane + j * 64 < nc)
+    if (rv && sl + j * L < nc)
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const float d = h[j][i] - mu;
         q = fmaf(d, d, q);
       }
-  const float rs = rsqrtf(wave_sum(q) / (float)H + eps);
+  const float rs = rsqrtf(row_sum<L>(q) / (float)H + eps);
 #pragma unroll
   for (int j = 0; j < CH; ++j) {
-    const int c = lane + j * 64;
-    if (c < nc) {
-      float o[8];
+    const int c = sl + j * L;
+    if (rv && c < nc) {
+      float gv[8], bv[8], o[8];
+      if (gamma) load8f(gamma + c * 8, gv);
+      if (beta) load8f(beta + c * 8, bv);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int col = c * 8 + i;
-        o[i] = (h[j][i] - mu) * rs * (gamma ? gamma[col] : 1.f) + (beta ? beta[col] : 0.f);
-      }
+      for (int i = 0; i < 8; ++i) o[i] = (h[j][i] - mu) * rs * (gamma ? gv[i] : 1.f) + (beta ? bv[i] : 0.f);
       store8(y + row * H + c * 8, o);
       store8(hsave + row * H + c * 8, h[j]);
     }
   }
-  if (lane == 0) {
+  if (rv && sl == 0) {
     mean[row] = mu;
     rstd[row] = rs;
   }
 }
 
-// one wave walks kLnRowsPerWave rows; lane owns columns (lane + 64 j)*8 .. +7
-// and accumulates dgamma / dbeta partials for them in registers
-template <int CH>
+// A block walks kLnRowsPerBlock rows (each wave kLnRowsPerWave, RPW at a
+// time); lanes accumulate dgamma / dbeta partials of their columns in
+// registers, the block adds its waves' partials in a fixed order through LDS
+// and writes ONE partial row (deterministic, no atomics).
+template <int CH, int RPW>
 __global__ __launch_bounds__(kBlock) void add_ln_bwd_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ hsave, const float* __restrict__ mean,
     const float* __restrict__ rstd, const float* __restrict__ gamma, uint16_t* __restrict__ dx,
     uint16_t* __restrict__ da, float* __restrict__ pg, float* __restrict__ pb, int64_t R, int H, uint32_t seed,
     uint32_t thr, float scale) {
-  const int lane = threadIdx.x & 63;
-  const int64_t wave_g = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  constexpr int L = 64 / RPW;
+  __shared__ float red[2][64 * 8 * kLnMaxChunks];
+  const int lane = threadIdx.x & 63, sl = lane % L, wave = threadIdx.x >> 6;
   const int nc = H >> 3;
   float accg[CH][8], accb[CH][8];
 #pragma unroll
   for (int j = 0; j < CH; ++j)
 #pragma unroll
     for (int i = 0; i < 8; ++i) accg[j][i] = accb[j][i] = 0.f;
-  for (int rr = 0; rr < kLnRowsPerWave; ++rr) {
-    const int64_t row = wave_g * kLnRowsPerWave + rr;
-    if (row >= R) break;
-    const float mu = mean[row], rs = rstd[row];
+  const int64_t wrow = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * kLnRowsPerWave;
+#pragma unroll 1
+  for (int rr = 0; rr < kLnRowsPerWave; rr += RPW) {
+    const int64_t row = wrow + rr + lane / L;
+    const bool rv = row < R;
+    const float mu = rv ? mean[row] : 0.f, rs = rv ? rstd[row] : 0.f;
     float g[CH][8], xh[CH][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
-      const int c = lane + j * 64;
-      if (c < nc) {
-        float dv[8], hv[8];
+      const int c = sl + j * L;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g[j][i] = xh[j][i] = 0.f;
+      if (rv && c < nc) {
+        float dv[8], hv[8], gv[8];
         load8(dy + row * H + c * 8, dv);
         load8(hsave + row * H + c * 8, hv);
+        if (gamma) load8f(gamma + c * 8, gv);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          const int col = c * 8 + i;
           xh[j][i] = (hv[i] - mu) * rs;
-          g[j][i] = dv[i] * (gamma ? gamma[col] : 1.f);
+          g[j][i] = gamma ? dv[i] * gv[i] : dv[i];
           s1 += g[j][i];
           s2 = fmaf(g[j][i], xh[j][i], s2);
           accg[j][i] = fmaf(dv[i], xh[j][i], accg[j][i]);
@@ -153,11 +183,11 @@ __global__ __launch_bounds__(kBlock) void add_ln_bwd_kernel(
         }
       }
     }
-    const float m1 = wave_sum(s1) / (float)H, m2 = wave_sum(s2) / (float)H;
+    const float m1 = row_sum<L>(s1) / (float)H, m2 = row_sum<L>(s2) / (float)H;
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
-      const int c = lane + j * 64;
-      if (c < nc) {
+      const int c = sl + j * L;
+      if (rv && c < nc) {
         float o[8], od[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -169,52 +199,70 @@ __global__ __launch_bounds__(kBlock) void add_ln_bwd_kernel(
       }
     }
   }
-  // per-wave column partials: row wave_g of [nwaves][H]
+  // the row halves of a wave own the same columns: fold them first
+  if (RPW == 2) {
 #pragma unroll
-  for (int j = 0; j < CH; ++j) {
-    const int c = lane + j * 64;
-    if (c < nc) {
+    for (int j = 0; j < CH; ++j)
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        pg[wave_g * H + c * 8 + i] = accg[j][i];
-        pb[wave_g * H + c * 8 + i] = accb[j][i];
+        accg[j][i] += __shfl_xor(accg[j][i], 32, 64);
+        accb[j][i] += __shfl_xor(accb[j][i], 32, 64);
+      }
+  }
+  // waves 0, 1, 2, 3 in turn into the block's LDS row (fixed order)
+  for (int w = 0; w < kWavesPerBlock; ++w) {
+    if (wave == w && lane < L) {
+#pragma unroll
+      for (int j = 0; j < CH; ++j) {
+        const int c = sl + j * L;
+        if (c < nc)
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            red[0][c * 8 + i] = w ? red[0][c * 8 + i] + accg[j][i] : accg[j][i];
+            red[1][c * 8 + i] = w ? red[1][c * 8 + i] + accb[j][i] : accb[j][i];
+          }
       }
     }
+    __syncthreads();
+  }
+  for (int c4 = threadIdx.x; c4 < (H >> 2); c4 += kBlock) {
+    reinterpret_cast<float4*>(pg + (int64_t)blockIdx.x * H)[c4] = reinterpret_cast<const float4*>(red[0])[c4];
+    reinterpret_cast<float4*>(pb + (int64_t)blockIdx.x * H)[c4] = reinterpret_cast<const float4*>(red[1])[c4];
   }
 }
 
-// dgamma / dbeta (+)= column sums of the [P][H] partials.  A workgroup owns
-// kFinCols columns; its threads split the P rows kFinParts ways with 8 loads
-// in flight each (the partials are L2-resident: an un-pipelined loop is
-// latency-bound), then combine in fp64 through LDS.
-constexpr int kFinCols = 16;
-constexpr int kFinParts = kBlock / kFinCols;
+// dgamma / dbeta (+)= column sums of the [P][H] partials, in two levels so
+// the 6 MB of BERT partials stream at full width: level 1 (grid: 64-column
+// slabs x kFinSplits row ranges) writes [kFinSplits][H] sums, level 2 adds
+// those kFinSplits rows in order (fp64 within each level, deterministic).
+constexpr int kFinSplits = 32;
+constexpr int kFinParts = kBlock / 64;   // row interleave inside a level-1 block
 
-__global__ __launch_bounds__(kBlock) void ln_param_finalize_kernel(const float* __restrict__ pg,
-                                                                   const float* __restrict__ pb, int64_t P, int H,
-                                                                   float* __restrict__ dgamma,
-                                                                   float* __restrict__ dbeta, int accumulate) {
-  __shared__ double sh[2][kFinParts][kFinCols];
-  const int cl = threadIdx.x % kFinCols;
-  const int part = threadIdx.x / kFinCols;
-  const int col = blockIdx.x * kFinCols + cl;
+__global__ __launch_bounds__(kBlock) void ln_param_partial_kernel(const float* __restrict__ pg,
+                                                                  const float* __restrict__ pb, int64_t P, int H,
+                                                                  float* __restrict__ q) {
+  __shared__ double sh[2][kFinParts][64];
+  const int cl = threadIdx.x & 63, part = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + cl;
+  const int64_t per = (P + kFinSplits - 1) / kFinSplits;
+  const int64_t r0 = blockIdx.y * per, r1 = r0 + per < P ? r0 + per : P;
   double sg = 0.0, sb = 0.0;
   if (col < H) {
-    int64_t r = part;
-    for (; r + 7 * kFinParts < P; r += 8 * kFinParts) {
-      float vg[8], vb[8];
+    int64_t r = r0 + part;
+    for (; r + 3 * kFinParts < r1; r += 4 * kFinParts) {
+      float vg[4], vb[4];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < 4; ++u) {
         vg[u] = pg[(r + u * kFinParts) * H + col];
         vb[u] = pb[(r + u * kFinParts) * H + col];
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < 4; ++u) {
         sg += vg[u];
         sb += vb[u];
       }
     }
-    for (; r < P; r += kFinParts) {
+    for (; r < r1; r += kFinParts) {
       sg += pg[r * H + col];
       sb += pb[r * H + col];
     }
@@ -225,13 +273,42 @@ __global__ __launch_bounds__(kBlock) void ln_param_finalize_kernel(const float* 
   if (part == 0 && col < H) {
     double tg = 0.0, tb = 0.0;
 #pragma unroll
-    for (int q = 0; q < kFinParts; ++q) {
-      tg += sh[0][q][cl];
-      tb += sh[1][q][cl];
+    for (int k = 0; k < kFinParts; ++k) {
+      tg += sh[0][k][cl];
+      tb += sh[1][k][cl];
     }
-    if (dgamma) dgamma[col] = (accumulate ? dgamma[col] : 0.f) + (float)tg;
-    if (dbeta) dbeta[col] = (accumulate ? dbeta[col] : 0.f) + (float)tb;
+    q[(int64_t)blockIdx.y * H + col] = (float)tg;
+    q[(int64_t)(kFinSplits + blockIdx.y) * H + col] = (float)tb;
   }
+}
+
+__global__ __launch_bounds__(kBlock) void ln_param_finalize_kernel(const float* __restrict__ q, int H,
+                                                                   float* __restrict__ dgamma,
+                                                                   float* __restrict__ dbeta, int accumulate) {
+  const int col = blockIdx.x * kBlock + threadIdx.x;
+  if (col >= H) return;
+  double tg = 0.0, tb = 0.0;
+#pragma unroll 8
+  for (int k = 0; k < kFinSplits; ++k) {
+    tg += q[(int64_t)k * H + col];
+    tb += q[(int64_t)(kFinSplits + k) * H + col];
+  }
+  if (dgamma) dgamma[col] = (accumulate ? dgamma[col] : 0.f) + (float)tg;
+  if (dbeta) dbeta[col] = (accumulate ? dbeta[col] : 0.f) + (float)tb;
+}
+
+// (CH, RPW) for a row of nc 16-byte chunks: two rows per wave up to 256
+// chunks (H <= 2048), the fewest chunks per lane that cover the row
+template <template <int, int> class Launch>
+void ln_dispatch(int nc, Launch<1, 2> l12, Launch<2, 2> l22, Launch<3, 2> l32, Launch<4, 2> l42, Launch<6, 2> l62,
+                 Launch<8, 2> l82, Launch<8, 1> l81) {
+  if (nc <= 32) l12();
+  else if (nc <= 64) l22();
+  else if (nc <= 96) l32();
+  else if (nc <= 128) l42();
+  else if (nc <= 192) l62();
+  else if (nc <= 256) l82();
+  else l81();
 }
 
 }  // namespace
@@ -239,26 +316,66 @@ __global__ __launch_bounds__(kBlock) void ln_param_finalize_kernel(const float* 
 bool add_ln_supported(int H) { return H % 8 == 0 && H >= 8 && H <= 64 * 8 * kLnMaxChunks; }
 
 int64_t add_ln_partial_rows(int64_t R) {
-  const int64_t waves = (R + kLnRowsPerWave - 1) / kLnRowsPerWave;
-  return (waves + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock;
+  // per-block partial rows + the [2][kFinSplits] level-1 sums (in rows of H)
+  return (R + kLnRowsPerBlock - 1) / kLnRowsPerBlock + kFinSplits;
 }
+
+namespace {
+struct LnFwdArgs {
+  const uint16_t *a, *x;
+  const float *gamma, *beta;
+  uint16_t *y, *hsave;
+  float *mean, *rstd;
+  int64_t R;
+  int H;
+  float eps;
+  uint32_t seed, thr;
+  float scale;
+  hipStream_t stream;
+};
+
+template <int CH, int RPW>
+struct LnFwdLaunch {
+  const LnFwdArgs* p;
+  void operator()() const {
+    const int64_t waves = (p->R + RPW - 1) / RPW;
+    const unsigned grid = (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
+    hipLaunchKernelGGL((add_ln_fwd_kernel<CH, RPW>), dim3(grid), dim3(kBlock), 0, p->stream, p->a, p->x, p->gamma,
+                       p->beta, p->y, p->hsave, p->mean, p->rstd, p->R, p->H, p->eps, p->seed, p->thr, p->scale);
+  }
+};
+
+struct LnBwdArgs {
+  const uint16_t *dy, *hsave;
+  const float *mean, *rstd, *gamma;
+  uint16_t *dx, *da;
+  float *pg, *pb;
+  int64_t R;
+  int H;
+  uint32_t seed, thr;
+  float scale;
+  hipStream_t stream;
+};
+
+template <int CH, int RPW>
+struct LnBwdLaunch {
+  const LnBwdArgs* p;
+  void operator()() const {
+    hipLaunchKernelGGL((add_ln_bwd_kernel<CH, RPW>), dim3((unsigned)((p->R + kLnRowsPerBlock - 1) / kLnRowsPerBlock)), dim3(kBlock), 0,
+                       p->stream, p->dy, p->hsave, p->mean, p->rstd, p->gamma, p->dx, p->da, p->pg, p->pb, p->R, p->H,
+                       p->seed, p->thr, p->scale);
+  }
+};
+}  // namespace
 
 void add_ln_forward(const void* a, const void* x, const float* gamma, const float* beta, void* y, void* hsave,
                     float* mean, float* rstd, int64_t R, int H, float eps, float p, uint32_t seed,
                     hipStream_t stream) {
   const uint32_t thr = p > 0.f ? (uint32_t)((1.0 - (double)p) * 4294967295.0) : 0u;
   const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  const unsigned grid = (unsigned)((R + kWavesPerBlock - 1) / kWavesPerBlock);
-#define GK_LNF(CH)                                                                                                 \
-  hipLaunchKernelGGL(add_ln_fwd_kernel<CH>, dim3(grid), dim3(kBlock), 0, stream, (const uint16_t*)a,              \
-                     (const uint16_t*)x, gamma, beta, (uint16_t*)y, (uint16_t*)hsave, mean, rstd, R, H, eps, seed, \
-                     thr, scale)
-  const int ch = ((H >> 3) + 63) / 64;
-  if (ch <= 1) GK_LNF(1);
-  else if (ch <= 2) GK_LNF(2);
-  else if (ch <= 4) GK_LNF(4);
-  else GK_LNF(8);
-#undef GK_LNF
+  const LnFwdArgs args{(const uint16_t*)a, (const uint16_t*)x, gamma, beta, (uint16_t*)y, (uint16_t*)hsave, mean,
+                       rstd, R, H, eps, seed, thr, scale, stream};
+  ln_dispatch<LnFwdLaunch>(H >> 3, {&args}, {&args}, {&args}, {&args}, {&args}, {&args}, {&args});
 }
 
 void add_ln_backward(const void* dy, const void* hsave, const float* mean, const float* rstd, const float* gamma,
@@ -266,23 +383,19 @@ void add_ln_backward(const void* dy, const void* hsave, const float* mean, const
                      float p, uint32_t seed, hipStream_t stream) {
   const uint32_t thr = p > 0.f ? (uint32_t)((1.0 - (double)p) * 4294967295.0) : 0u;
   const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  const int64_t P = add_ln_partial_rows(R);
+  const int64_t P = (R + kLnRowsPerBlock - 1) / kLnRowsPerBlock;
   float* pg = ws;
   float* pb = ws + P * H;
-  const unsigned grid = (unsigned)(P / kWavesPerBlock);
-#define GK_LNB(CH)                                                                                                  \
-  hipLaunchKernelGGL(add_ln_bwd_kernel<CH>, dim3(grid), dim3(kBlock), 0, stream, (const uint16_t*)dy,               \
-                     (const uint16_t*)hsave, mean, rstd, gamma, (uint16_t*)dx, (uint16_t*)da, pg, pb, R, H, seed, \
-                     thr, scale)
-  const int ch = ((H >> 3) + 63) / 64;
-  if (ch <= 1) GK_LNB(1);
-  else if (ch <= 2) GK_LNB(2);
-  else if (ch <= 4) GK_LNB(4);
-  else GK_LNB(8);
-#undef GK_LNB
-  if (dgamma || dbeta)
-    hipLaunchKernelGGL(ln_param_finalize_kernel, dim3((H + kFinCols - 1) / kFinCols), dim3(kBlock), 0, stream, pg,
-                       pb, P, H, dgamma, dbeta, accumulate);
+  float* q = ws + 2 * P * H;   // [2][kFinSplits][H]: fits the 2 * add_ln_partial_rows(R) * H of the workspace
+  const LnBwdArgs args{(const uint16_t*)dy, (const uint16_t*)hsave, mean, rstd, gamma, (uint16_t*)dx,
+                       (uint16_t*)da, pg, pb, R, H, seed, thr, scale, stream};
+  ln_dispatch<LnBwdLaunch>(H >> 3, {&args}, {&args}, {&args}, {&args}, {&args}, {&args}, {&args});
+  if (dgamma || dbeta) {
+    hipLaunchKernelGGL(ln_param_partial_kernel, dim3((H + 63) / 64, kFinSplits), dim3(kBlock), 0, stream, pg, pb, P, H,
+                       q);
+    hipLaunchKernelGGL(ln_param_finalize_kernel, dim3((H + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, q, H,
+                       dgamma, dbeta, accumulate);
+  }
 }
 
 }  // namespace gk
