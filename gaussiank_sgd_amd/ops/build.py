@@ -34,6 +34,14 @@ if ASAN:
     BUILD = REPO / "build" / "gksgd_ext_asan"
     TARGET = REPO / "build" / "asan" / "_C.so"
 SAN_HOST = ["-fsanitize=address", "-fsanitize=undefined"]
+# A/B variants: GKSGD_VARIANT=<name> builds variants/<name>/_C.so with the extra
+# hipcc flags of GKSGD_VARIANT_FLAGS (e.g. "-DGK_BN_UNROLL=1"); load it with
+# GKSGD_EXT=variants/<name>/_C.so (under variants/: build/ is not sent to the GPU box)
+VARIANT = os.environ.get("GKSGD_VARIANT", "")
+VARIANT_FLAGS = os.environ.get("GKSGD_VARIANT_FLAGS", "").split()
+if VARIANT and not ASAN:
+    BUILD = REPO / "build" / ("gksgd_ext_" + VARIANT)
+    TARGET = REPO / "variants" / VARIANT / "_C.so"
 ARCH = os.environ.get("GKSGD_OFFLOAD_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
@@ -77,7 +85,7 @@ def _hip_flags() -> List[str]:
         for f in SAN_HOST:
             san += ["-Xarch_host", f]
         san += ["-Xarch_host", "-fno-omit-frame-pointer"]
-    return san + [
+    return san + VARIANT_FLAGS + [
         "--offload-arch=" + ARCH,
         "-O3",
         "-fPIC",

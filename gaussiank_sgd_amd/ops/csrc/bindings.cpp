@@ -898,6 +898,7 @@ int64_t conv_nt(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor zero, int64
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
   const int64_t Co = w.size(0), KH = w.size(2), KW = w.size(3);
   const int64_t OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
+  TORCH_CHECK(KH <= 4 && KW <= 4, "conv_nt: kernels up to 4x4 (gemm.hip kMaxTaps)");
   TORCH_CHECK(y.is_cuda() && y.scalar_type() == at::kBFloat16 && y.dim() == 4 &&
                   y.is_contiguous(at::MemoryFormat::ChannelsLast) && y.size(0) == N && y.size(1) == Co &&
                   y.size(2) == OH && y.size(3) == OW,
@@ -1273,6 +1274,7 @@ TORCH_LIBRARY(gksgd, m) {
 
   m.def("bn_workspace_floats(int M, int C, int elem_bytes) -> int", &bn_workspace_floats);
   m.def("bn_supported(int C, int elem_bytes) -> bool", &bn_supported);
+  m.def("bn_set_blocks(int blocks) -> ()", [](int64_t b) { gk::bn_set_blocks((int)b); });
   m.def("bn_mask_bytes(int M, int C, int elem_bytes) -> int", &bn_mask_bytes);
   m.def(
       "bn_act_forward(Tensor x, Tensor? res, Tensor(a!) y, Tensor(i!)? mask, Tensor? w, Tensor? b, Tensor(b!)? run_mean, "

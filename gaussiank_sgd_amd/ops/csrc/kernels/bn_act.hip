@@ -52,9 +52,12 @@ struct Vec<uint16_t> {  // bf16
     }
   }
   __device__ static void store(uint16_t* p, const float* v) {
+    // v_cvt_pk_bf16_f32: round-to-nearest-even, NaN stays NaN (same values as f32_to_bf16)
     uint32_t w[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f32_to_bf16(v[2 * i]) | ((uint32_t)f32_to_bf16(v[2 * i + 1]) << 16);
+    for (int i = 0; i < 4; ++i)
+      w[i] = __builtin_bit_cast(uint32_t, __builtin_convertvector(
+                 (float __attribute__((ext_vector_type(2)))){v[2 * i], v[2 * i + 1]}, __bf16 __attribute__((ext_vector_type(2)))));
     *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
   }
 };
@@ -70,6 +73,34 @@ struct Vec<float> {
     *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
   }
 };
+
+// Streaming row loop of the BN passes: a thread walks rows r, r + rl, ... < r1
+// of its 16-byte channel vector; U rows are loaded before any is used.
+// Measured (bench/bn_probe.py, profiles/r02_bn_probe_unroll.txt): U = 4 and
+// 2048-4096 workgroups are SLOWER than U = 1 at 1024 workgroups on every
+// ResNet-50 shape (block-output backward 1151 -> 1285 us at 56x56x256), so the
+// passes run U = 1; all of them sit at 4.5-5.8 TB/s either way.
+template <int U, typename Row, typename L, typename F>
+__device__ __forceinline__ void stream_rows(int64_t r, int64_t r1, int rl, L&& load, F&& use) {
+  for (; r + (int64_t)(U - 1) * rl < r1; r += (int64_t)U * rl) {
+    Row v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) load(v[u], r + (int64_t)u * rl);
+#pragma unroll
+    for (int u = 0; u < U; ++u) use(v[u], r + (int64_t)u * rl);
+  }
+  for (; r < r1; r += rl) {
+    Row v;
+    load(v, r);
+    use(v, r);
+  }
+}
+
+// rows in flight per thread in the streaming passes (stream_rows)
+#ifndef GK_BN_UNROLL
+#define GK_BN_UNROLL 1
+#endif
+constexpr int kBnUnroll = GK_BN_UNROLL;
 
 struct Geo {
   int tpr;      // threads across the channel tile
@@ -102,7 +133,7 @@ Geo make_geo(int64_t M, int C, int target_blocks) {
 // ---------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------
-template <typename T>
+template <typename T, int U = kBnUnroll>
 __global__ __launch_bounds__(kBlock) void bn_stats_kernel(const T* __restrict__ x, int64_t M, int C, Geo g,
                                                           float* __restrict__ psum, float* __restrict__ psq) {
   constexpr int V = Vec<T>::N;
@@ -115,15 +146,16 @@ __global__ __launch_bounds__(kBlock) void bn_stats_kernel(const T* __restrict__ 
   float s[V], q[V];
 #pragma unroll
   for (int i = 0; i < V; ++i) s[i] = q[i] = 0.f;
-  for (int64_t r = (lane_r < g.rl ? r0 + lane_r : r1); r < r1; r += g.rl) {
-    float v[V];
-    Vec<T>::load(x + r * C + c0, v);
+  struct Row { float v[V]; };
+  stream_rows<U, Row>(
+      lane_r < g.rl ? r0 + lane_r : r1, r1, g.rl, [&](Row& w, int64_t r) { Vec<T>::load(x + r * C + c0, w.v); },
+      [&](const Row& w, int64_t) {
 #pragma unroll
-    for (int i = 0; i < V; ++i) {
-      s[i] += v[i];
-      q[i] = fmaf(v[i], v[i], q[i]);
-    }
-  }
+        for (int i = 0; i < V; ++i) {
+          s[i] += w.v[i];
+          q[i] = fmaf(w.v[i], w.v[i], q[i]);
+        }
+      });
   __shared__ float sh[2][kBlock * 8];
 #pragma unroll
   for (int i = 0; i < V; ++i) {
@@ -226,7 +258,7 @@ __global__ __launch_bounds__(kBlock) void bn_finalize_kernel(const float* __rest
   }
 }
 
-template <typename T, bool RELU, bool RES>
+template <typename T, bool RELU, bool RES, int U = kBnUnroll>
 __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res,
                                                           T* __restrict__ y, uint8_t* __restrict__ mask, int64_t M,
                                                           int C, Geo g, const float* __restrict__ scale,
@@ -241,25 +273,29 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const T* __restrict__ 
   const int64_t r0 = (int64_t)blockIdx.y * g.rows_per_block;
   int64_t r1 = r0 + g.rows_per_block;
   if (r1 > M) r1 = M;
-  for (int64_t r = (lane_r < g.rl ? r0 + lane_r : r1); r < r1; r += g.rl) {
-    float v[V];
-    Vec<T>::load(x + r * C + c0, v);
-    float rv[V];
-    if (RES) Vec<T>::load(res + r * C + c0, rv);
-    uint32_t bits = 0;
+  struct Row { float v[V], rv[RES ? V : 1]; };
+  stream_rows<U, Row>(
+      lane_r < g.rl ? r0 + lane_r : r1, r1, g.rl,
+      [&](Row& w, int64_t r) {
+        Vec<T>::load(x + r * C + c0, w.v);
+        if (RES) Vec<T>::load(res + r * C + c0, w.rv);
+      },
+      [&](const Row& w, int64_t r) {
+        float o[V];
+        uint32_t bits = 0;
 #pragma unroll
-    for (int i = 0; i < V; ++i) {
-      float o = fmaf(v[i], sc[i], sf[i]);
-      if (RES) o += rv[i];
-      if (RELU) {
-        bits |= (o > 0.f ? 1u : 0u) << i;
-        o = fmaxf(o, 0.f);
-      }
-      v[i] = o;
-    }
-    Vec<T>::store(y + r * C + c0, v);
-    if (RELU) mask[r * (C / V) + c0 / V] = (uint8_t)bits;
-  }
+        for (int i = 0; i < V; ++i) {
+          float t = fmaf(w.v[i], sc[i], sf[i]);
+          if (RES) t += w.rv[i];
+          if (RELU) {
+            bits |= (t > 0.f ? 1u : 0u) << i;
+            t = fmaxf(t, 0.f);
+          }
+          o[i] = t;
+        }
+        Vec<T>::store(y + r * C + c0, o);
+        if (RELU) mask[r * (C / V) + c0 / V] = (uint8_t)bits;
+      });
 }
 
 __device__ __forceinline__ float round_bf16(float f) { return __uint_as_float((uint32_t)f32_to_bf16(f) << 16); }
@@ -272,7 +308,10 @@ __device__ __forceinline__ float round_bf16(float f) { return __uint_as_float((u
 // (0xff when the max is <= 0, i.e. the ReLU blocks the gradient).  The
 // full-resolution BN output is never written.  Window scan order and the
 // strict '>' (first max wins, NaN propagates) match at::max_pool2d.
-template <typename T>
+// KK > 0: compile-time k x k window whose KK*KK loads are all issued before
+// any is used (out-of-image taps read the always-valid window centre and are
+// skipped); the runtime loop waits for each tap's load in turn.
+template <typename T, int KK = 0>
 __global__ __launch_bounds__(kBlock) void bn_relu_pool_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                               uint8_t* __restrict__ amax, int64_t P, int C, PoolGeo pg,
                                                               const float* __restrict__ scale,
@@ -296,22 +335,47 @@ __global__ __launch_bounds__(kBlock) void bn_relu_pool_kernel(const T* __restric
     m[i] = -INFINITY;
     idx[i] = 0xffu;
   }
-  for (int kh = 0; kh < pg.k; ++kh) {
-    const int ih = oh * pg.s - pg.p + kh;
-    if (ih < 0 || ih >= pg.H) continue;
-    for (int kw = 0; kw < pg.k; ++kw) {
-      const int iw = ow * pg.s - pg.p + kw;
-      if (iw < 0 || iw >= pg.W) continue;
-      float v[V];
-      Vec<T>::load(x + ((n * pg.H + ih) * pg.W + iw) * C + c0, v);
-      const uint32_t pos = (uint32_t)(kh * pg.k + kw);
+  if constexpr (KK > 0) {
+    const int hc = oh * pg.s - pg.p + KK / 2, wc = ow * pg.s - pg.p + KK / 2;   // centre (requires p == KK / 2)
+    float v[KK * KK][V];
+    bool ok[KK * KK];
+#pragma unroll
+    for (int q = 0; q < KK * KK; ++q) {
+      const int ih = hc - KK / 2 + q / KK, iw = wc - KK / 2 + q % KK;
+      ok[q] = ih >= 0 && ih < pg.H && iw >= 0 && iw < pg.W;
+      Vec<T>::load(x + ((n * pg.H + (ok[q] ? ih : hc)) * pg.W + (ok[q] ? iw : wc)) * C + c0, v[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < KK * KK; ++q) {
+      if (!ok[q]) continue;
 #pragma unroll
       for (int i = 0; i < V; ++i) {
-        float z = fmaf(v[i], sc[i], sf[i]);
+        float z = fmaf(v[q][i], sc[i], sf[i]);
         if (sizeof(T) == 2) z = round_bf16(z);
         if (z > m[i] || z != z) {
           m[i] = z;
-          idx[i] = pos;
+          idx[i] = (uint32_t)q;
+        }
+      }
+    }
+  } else {
+    for (int kh = 0; kh < pg.k; ++kh) {
+      const int ih = oh * pg.s - pg.p + kh;
+      if (ih < 0 || ih >= pg.H) continue;
+      for (int kw = 0; kw < pg.k; ++kw) {
+        const int iw = ow * pg.s - pg.p + kw;
+        if (iw < 0 || iw >= pg.W) continue;
+        float v[V];
+        Vec<T>::load(x + ((n * pg.H + ih) * pg.W + iw) * C + c0, v);
+        const uint32_t pos = (uint32_t)(kh * pg.k + kw);
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+          float z = fmaf(v[i], sc[i], sf[i]);
+          if (sizeof(T) == 2) z = round_bf16(z);
+          if (z > m[i] || z != z) {
+            m[i] = z;
+            idx[i] = pos;
+          }
         }
       }
     }
@@ -464,7 +528,7 @@ struct DyPool {
 
 // WDZ: also store dz (the gated, twin-summed gradient -- the residual branch's
 // gradient) so the apply pass reads one tensor instead of dy, dy2 and the mask.
-template <typename T, typename Src, bool WDZ = false>
+template <typename T, typename Src, bool WDZ = false, int U = kBnUnroll>
 __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(Src src, const T* __restrict__ x, int64_t M, int C, Geo g,
                                                                const float* __restrict__ mean,
                                                                const float* __restrict__ invstd,
@@ -480,18 +544,22 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(Src src, const T*
   const int64_t r0 = (int64_t)blockIdx.y * g.rows_per_block;
   int64_t r1 = r0 + g.rows_per_block;
   if (r1 > M) r1 = M;
-  for (int64_t r = (lane_r < g.rl ? r0 + lane_r : r1); r < r1; r += g.rl) {
-    float d[V], xv[V];
-    src.load(r, C, c0, d);
-    Vec<T>::load(x + r * C + c0, xv);
-    if (WDZ) Vec<T>::store(dzo + r * C + c0, d);
+  struct Row { float d[V], xv[V]; };
+  stream_rows<U, Row>(
+      lane_r < g.rl ? r0 + lane_r : r1, r1, g.rl,
+      [&](Row& w, int64_t r) {
+        src.load(r, C, c0, w.d);
+        Vec<T>::load(x + r * C + c0, w.xv);
+      },
+      [&](const Row& w, int64_t r) {
+        if (WDZ) Vec<T>::store(dzo + r * C + c0, w.d);
 #pragma unroll
-    for (int i = 0; i < V; ++i) {
-      const float dz = d[i];
-      sb[i] += dz;
-      sg[i] = fmaf(dz, (xv[i] - mu[i]) * is[i], sg[i]);
-    }
-  }
+        for (int i = 0; i < V; ++i) {
+          const float dz = w.d[i];
+          sb[i] += dz;
+          sg[i] = fmaf(dz, (w.xv[i] - mu[i]) * is[i], sg[i]);
+        }
+      });
   __shared__ float sh[2][kBlock * 8];
 #pragma unroll
   for (int i = 0; i < V; ++i) {
@@ -533,7 +601,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_finalize_kernel(const float* __
   if (gw_acc) gw_acc[c] += (float)b;
 }
 
-template <typename T, typename Src, bool DRES>
+template <typename T, typename Src, bool DRES, int U = kBnUnroll>
 __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(Src src, const T* __restrict__ x, T* __restrict__ dx,
                                                               T* __restrict__ dres, int64_t M, int C, Geo g,
                                                               const float* __restrict__ w,
@@ -560,19 +628,23 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(Src src, const T* 
   const int64_t r0 = (int64_t)blockIdx.y * g.rows_per_block;
   int64_t r1 = r0 + g.rows_per_block;
   if (r1 > M) r1 = M;
-  for (int64_t r = (lane_r < g.rl ? r0 + lane_r : r1); r < r1; r += g.rl) {
-    float d[V], xv[V], o[V];
-    src.load(r, C, c0, d);
-    Vec<T>::load(x + r * C + c0, xv);
+  struct Row { float d[V], xv[V]; };
+  stream_rows<U, Row>(
+      lane_r < g.rl ? r0 + lane_r : r1, r1, g.rl,
+      [&](Row& w, int64_t r) {
+        src.load(r, C, c0, w.d);
+        Vec<T>::load(x + r * C + c0, w.xv);
+      },
+      [&](const Row& w, int64_t r) {
+        float o[V];
 #pragma unroll
-    for (int i = 0; i < V; ++i) {
-      const float dz = d[i];
-      const float xh = (xv[i] - mu[i]) * is[i];
-      o[i] = k1[i] * (dz - k2[i] - xh * k3[i]);
-    }
-    Vec<T>::store(dx + r * C + c0, o);
-    if (DRES) Vec<T>::store(dres + r * C + c0, d);
-  }
+        for (int i = 0; i < V; ++i) {
+          const float xh = (w.xv[i] - mu[i]) * is[i];
+          o[i] = k1[i] * (w.d[i] - k2[i] - xh * k3[i]);
+        }
+        Vec<T>::store(dx + r * C + c0, o);
+        if (DRES) Vec<T>::store(dres + r * C + c0, w.d);
+      });
 }
 
 // Tile-ordered pool backward (k <= 2s, s == 2: the 3x3/s2 stem pool).  The
@@ -622,6 +694,23 @@ __global__ __launch_bounds__(kBlock) void bn_pool_tile_kernel(const T* __restric
     const int64_t n = t / tplane;
     const int rem = (int)(t - n * tplane);
     const int th = rem / TW, tw = rem - (rem / TW) * TW;
+    // the s*s input pixels of the tile (issued first: independent of the windows;
+    // out-of-image pixels read the tile's first in-image pixel and are skipped)
+    float xv[S * S][V];
+    bool okq[S * S];
+    int64_t xo[S * S];
+    {
+      const int ihb = th * S - pg.p, iwb = tw * S - pg.p;
+      const int ihs = ihb < 0 ? 0 : (ihb < pg.H ? ihb : pg.H - 1);   // an in-image pixel (clamped)
+      const int iws = iwb < 0 ? 0 : (iwb < pg.W ? iwb : pg.W - 1);
+#pragma unroll
+      for (int q = 0; q < S * S; ++q) {
+        const int ih = ihb + q / S, iw = iwb + q % S;
+        okq[q] = ih >= 0 && ih < pg.H && iw >= 0 && iw < pg.W;
+        xo[q] = ((n * pg.H + (okq[q] ? ih : ihs)) * pg.W + (okq[q] ? iw : iws)) * C + c0;
+        Vec<T>::load(x + xo[q], xv[q]);
+      }
+    }
     // the <= 4 windows that reach this tile
     uint32_t a[4][2];
     float gv[4][V];
@@ -652,7 +741,7 @@ __global__ __launch_bounds__(kBlock) void bn_pool_tile_kernel(const T* __restric
 #pragma unroll
     for (int q = 0; q < S * S; ++q) {
       const int ih = th * S - pg.p + (q / S), iw = tw * S - pg.p + (q % S);
-      if (ih < 0 || ih >= pg.H || iw < 0 || iw >= pg.W) continue;
+      if (!okq[q]) continue;
       float d[V];
 #pragma unroll
       for (int i = 0; i < V; ++i) d[i] = 0.f;
@@ -666,19 +755,16 @@ __global__ __launch_bounds__(kBlock) void bn_pool_tile_kernel(const T* __restric
         for (int i = 0; i < V; ++i)
           if (((a[j][i / 4] >> (8 * (i % 4))) & 0xffu) == pos) d[i] += gv[j][i];
       }
-      const int64_t xo = ((n * pg.H + ih) * pg.W + iw) * C + c0;
-      float xv[V];
-      Vec<T>::load(x + xo, xv);
       if (APPLY) {
         float o[V];
 #pragma unroll
-        for (int i = 0; i < V; ++i) o[i] = k1[i] * (d[i] - k2[i] - (xv[i] - mu[i]) * is[i] * k3[i]);
-        Vec<T>::store(dx + xo, o);
+        for (int i = 0; i < V; ++i) o[i] = k1[i] * (d[i] - k2[i] - (xv[q][i] - mu[i]) * is[i] * k3[i]);
+        Vec<T>::store(dx + xo[q], o);
       } else {
 #pragma unroll
         for (int i = 0; i < V; ++i) {
           sb[i] += d[i];
-          sg[i] = fmaf(d[i], (xv[i] - mu[i]) * is[i], sg[i]);
+          sg[i] = fmaf(d[i], (xv[q][i] - mu[i]) * is[i], sg[i]);
         }
       }
     }
@@ -704,8 +790,10 @@ __global__ __launch_bounds__(kBlock) void bn_pool_tile_kernel(const T* __restric
   }
 }
 
-constexpr int kTargetBlocks = 1024;
 constexpr int kPoolTargetBlocks = 4096;
+// blocks per streaming pass (<= kPoolTargetBlocks: the workspace is sized for that)
+int g_bn_blocks = 1024;
+#define kTargetBlocks g_bn_blocks
 
 }  // namespace
 
@@ -715,6 +803,8 @@ size_t bn_workspace_floats(int64_t M, int C, int elem_bytes) {
       elem_bytes == 2 ? make_geo<uint16_t>(M, C, kPoolTargetBlocks) : make_geo<float>(M, C, kPoolTargetBlocks);
   return (size_t)2 * g.gy * C;
 }
+
+void bn_set_blocks(int blocks) { g_bn_blocks = blocks < 64 ? 64 : blocks > kPoolTargetBlocks ? kPoolTargetBlocks : blocks; }
 
 bool bn_supported(int C, int elem_bytes) {
   const int V = elem_bytes == 2 ? 8 : 4;
@@ -882,8 +972,12 @@ void bn_relu_pool_forward(const void* x, void* y, uint8_t* amax, int64_t N, int 
   if (elem_bytes == 2) {
     bn_stats_t<uint16_t>((const uint16_t*)x, M, C, w, b, eps, momentum, run_mean, run_var, save_mean, save_invstd,
                          scale, shift, ws, nbt, s);
-    hipLaunchKernelGGL(bn_relu_pool_kernel<uint16_t>, grid, dim3(kBlock), 0, s, (const uint16_t*)x, (uint16_t*)y, amax,
-                       P, C, pg, scale, shift);
+    if (pg.k == 3 && pg.p == 1)
+      hipLaunchKernelGGL((bn_relu_pool_kernel<uint16_t, 3>), grid, dim3(kBlock), 0, s, (const uint16_t*)x, (uint16_t*)y,
+                         amax, P, C, pg, scale, shift);
+    else
+      hipLaunchKernelGGL(bn_relu_pool_kernel<uint16_t>, grid, dim3(kBlock), 0, s, (const uint16_t*)x, (uint16_t*)y, amax,
+                         P, C, pg, scale, shift);
   } else {
     bn_stats_t<float>((const float*)x, M, C, w, b, eps, momentum, run_mean, run_var, save_mean, save_invstd, scale,
                        shift, ws, nbt, s);
@@ -903,8 +997,13 @@ void bn_relu_pool_forward_pre(const void* x, void* y, uint8_t* amax, int64_t N, 
   const int64_t threads = P * (C / 8);
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(kBlock), 0, s, psum, psq, gy, M, C, w, b,
                      eps, momentum, run_mean, run_var, save_mean, save_invstd, scale, shift, nbt);
-  hipLaunchKernelGGL(bn_relu_pool_kernel<uint16_t>, dim3((unsigned)((threads + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                     s, (const uint16_t*)x, (uint16_t*)y, amax, P, C, pg, scale, shift);
+  const dim3 grid((unsigned)((threads + kBlock - 1) / kBlock));
+  if (pg.k == 3 && pg.p == 1)
+    hipLaunchKernelGGL((bn_relu_pool_kernel<uint16_t, 3>), grid, dim3(kBlock), 0, s, (const uint16_t*)x, (uint16_t*)y,
+                       amax, P, C, pg, scale, shift);
+  else
+    hipLaunchKernelGGL(bn_relu_pool_kernel<uint16_t>, grid, dim3(kBlock), 0, s, (const uint16_t*)x, (uint16_t*)y, amax,
+                       P, C, pg, scale, shift);
 }
 
 template <typename T, bool TWIN>

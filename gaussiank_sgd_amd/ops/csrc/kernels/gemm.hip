@@ -59,11 +59,22 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 #undef GK_VMW
 }
 
+// wait_vmcnt with the loop's steady-state count as a compile-time fast path:
+// the generic switch compiles to a compare-and-branch chain (~15 scalar
+// instructions per K step); the steady state is one compare.
+template <int COMMON>
+__device__ __forceinline__ void wait_vmcnt_fast(int n) {
+  if (n == COMMON) vmcnt_le<COMMON>();
+  else wait_vmcnt(n);
+}
+
 // Implicit-GEMM convolution: row m of the A operand is output pixel
 // (n, oh, ow) and K slice k0 (64 channels) is tap (kh, kw) of input channels
 // c0..c0+63 (K = KH*KW*C, tap-major, matching a channels-last [Cout][KH][KW][C]
 // weight).  Out-of-image taps read a zero row (padding) -- LDS-DMA cannot write
 // zeros itself.
+constexpr int kMaxTaps = 4;   // gemm_nt gather: at most 4 taps per kernel dimension
+
 struct ConvGeo {
   const uint16_t* zero;   // >= 64 zero bf16
   int H, W, C, OH, OW, S, P, KW;
@@ -150,7 +161,7 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
   constexpr int LPW = Cfg::LPW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: LDS-DMA M0 and fragment bases in SGPRs
   const int wm = wave / WN, wn = wave % WN;
   const int n0 = blockIdx.y * Cfg::BN;
   const int64_t mtiles = (M + Cfg::BM - 1) / Cfg::BM;
@@ -184,14 +195,19 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
   // Instruction j of this wave fills staged rows i*8 .. i*8+7, i = wave + j*NW:
   // A rows while i*8 < BM, B rows after (streamed panel only).
   const uint16_t* ptr[LPW];   // A: row (or gathered pixel) base + chunk; B: row base + chunk
-  int ih0[LPW], iw0[LPW];     // gather: input position of tap (0, 0)
+  // gather: bit kh of okh / bit kw of okw set when tap row kh / column kw of
+  // this lane's output pixel lies inside the image (set once per M tile; a K
+  // step tests two bits instead of recomputing and comparing the position)
+  uint32_t okh[LPW], okw[LPW];
+  const uint16_t* zrow[LPW];  // gather: this lane's chunk of the zero row (padding taps)
 #pragma unroll
   for (int j = 0; j < LPW; ++j) {
     const int i = wave + j * Cfg::NW;
     const int r = i * 8 + (lane >> 3);
     const int c = (lane & 7) ^ swz(r);
     ptr[j] = j < Cfg::LPWA ? nullptr : B + (int64_t)(n0 + r - Cfg::BM) * ldb + c * 8;
-    ih0[j] = iw0[j] = 0;
+    okh[j] = okw[j] = 0u;
+    zrow[j] = GATHER ? geo.zero + c * 8 : nullptr;
   }
   auto set_rows = [&](int64_t mt) {
     const int64_t m0 = mt * Cfg::BM;
@@ -208,9 +224,17 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
           const uint32_t mu = (uint32_t)gr;
           const uint32_t n = mu / ohw, rem = mu - n * ohw;
           const uint32_t oh = rem / (uint32_t)geo.OW, ow = rem - oh * (uint32_t)geo.OW;
-          ih0[j] = (int)oh * geo.S - geo.P;
-          iw0[j] = (int)ow * geo.S - geo.P;
-          ptr[j] = A + (((int64_t)n * geo.H + ih0[j]) * geo.W + iw0[j]) * geo.C + c * 8;
+          const int ih0 = (int)oh * geo.S - geo.P;
+          const int iw0 = (int)ow * geo.S - geo.P;
+          uint32_t bh = 0u, bw = 0u;
+#pragma unroll
+          for (int q = 0; q < kMaxTaps; ++q) {   // host: KH, KW <= kMaxTaps
+            bh |= (uint32_t)((unsigned)(ih0 + q) < (unsigned)geo.H) << q;
+            bw |= (uint32_t)((unsigned)(iw0 + q) < (unsigned)geo.W) << q;
+          }
+          okh[j] = bh;
+          okw[j] = bw;
+          ptr[j] = A + (((int64_t)n * geo.H + ih0) * geo.W + iw0) * geo.C + c * 8;
         } else {
           ptr[j] = A + gr * lda + c * 8;
         }
@@ -226,16 +250,15 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
   auto stage = [&]() {
     GK_LDS char* base = (GK_LDS char*)stage_base + s_buf * Cfg::STAGE;
     const int k0 = s_ks << 6;
+    const int64_t toff = GATHER ? (int64_t)(s_kh * geo.W + s_kw) * geo.C + s_c0 : 0;   // wave-uniform
 #pragma unroll
     for (int j = 0; j < LPW; ++j) {
       const int i = wave + j * Cfg::NW;
       const uint16_t* src;
       if (j < Cfg::LPWA) {
         if (GATHER) {
-          const int ih = ih0[j] + s_kh, iw = iw0[j] + s_kw;
-          const bool ok = (unsigned)ih < (unsigned)geo.H && (unsigned)iw < (unsigned)geo.W;
-          const int c = (lane & 7) ^ swz(i * 8 + (lane >> 3));
-          src = ok ? ptr[j] + (int64_t)(s_kh * geo.W + s_kw) * geo.C + s_c0 : geo.zero + c * 8;
+          const bool ok = ((okh[j] >> s_kh) & (okw[j] >> s_kw) & 1u) != 0u;
+          src = ok ? ptr[j] + toff : zrow[j];
         } else {
           src = ptr[j] + k0;
         }
@@ -294,9 +317,9 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
     // ops issued after stage(t), in order: NS=2: stores(t-1);
     // NS=3: stores(t-2), stage(t+1), stores(t-1).  Retire stage(t) only.
     // after stage(t): stores(t-NS+1..t-1) and the stages t+1 .. t+NS-2 issued since
-    if (NS == 2) wait_vmcnt(st1);
-    else if (NS == 3) wait_vmcnt(st2 + (t + 1 < T ? LPW : 0) + st1);
-    else wait_vmcnt(st3 + st2 + st1 + ((t + 1 < T) + (t + 2 < T)) * LPW);
+    if (NS == 2) wait_vmcnt_fast<0>(st1);
+    else if (NS == 3) wait_vmcnt_fast<LPW>(st2 + (t + 1 < T ? LPW : 0) + st1);
+    else wait_vmcnt_fast<2 * LPW>(st3 + st2 + st1 + ((t + 1 < T) + (t + 2 < T)) * LPW);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     if (s_t < T) stage();
@@ -743,7 +766,7 @@ gemm_tn_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __re
   if (NS == 3 && T > 1) stage(1);
   for (int t = 0; t < T; ++t) {
     // retire slice t (with NS = 3, slice t+1 stays in flight)
-    if (NS == 3) wait_vmcnt(t + 1 < T ? LPW : 0);
+    if (NS == 3) wait_vmcnt_fast<LPW>(t + 1 < T ? LPW : 0);
     else wait_vmcnt(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);

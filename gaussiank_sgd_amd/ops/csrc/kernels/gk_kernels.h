@@ -217,6 +217,8 @@ void clip_grad_norm(float* g, int64_t n, float max_norm, double* ws, float* coef
 // ---------------------------------------------------------------------------
 size_t bn_workspace_floats(int64_t M, int C, int elem_bytes);
 bool bn_supported(int C, int elem_bytes);
+// workgroups per streaming BN pass (default 1024, clamped to [64, 4096]; bench/bn_probe.py)
+void bn_set_blocks(int blocks);
 size_t bn_mask_bytes(int64_t M, int C, int elem_bytes);
 void bn_act_forward(const void* x, const void* res, void* y, uint8_t* mask, int64_t M, int C, int elem_bytes,
                     const float* w, const float* b, float eps, float momentum, float* run_mean, float* run_var,
