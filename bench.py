@@ -211,6 +211,8 @@ def main() -> int:
             opt.clip_grad_norm_(clip)
         trainer.update_model()
 
+    if args.graph and args.model == "lstm":
+        raise SystemExit("bench.py --graph: the LSTM carries hidden state across steps; not graph-capturable")
     if args.graph:
         # whole-step HIP graph: capture after the eager warm-up, replay in the timed loop
         from gaussiank_sgd_amd.train.graph import GraphedStep

@@ -154,6 +154,7 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         self._grads_zero = True
         self._pending_dumps: List[tuple] = []
         self._sel_dev: Optional[torch.Tensor] = None
+        self._graph_sel: List[torch.Tensor] = []   # per-bucket selected-count slots of a captured step
         self._sel_n = 0
         self._setup_exchange()
         self._setup_fused_update()
@@ -234,7 +235,9 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         self._is_cuda = dev.type == "cuda"
         self._exchanger = comm.Exchanger(dev, prefer_native=self._prefer_native_rccl) if self._hooks_on else None
         self._comm_stream = None
-        if self._is_cuda and self._hooks_on:
+        # GKSGD_COMM_STREAM=0: compression / exchange inline on the compute stream
+        # (no overlap; a single-stream step, e.g. for whole-step graph capture)
+        if self._is_cuda and self._hooks_on and os.environ.get("GKSGD_COMM_STREAM", "1") != "0":
             self._comm_stream = torch.cuda.Stream(device=dev, priority=-1)
         comp = self._compression
         self._fused_sparse = self._sparse and getattr(comp, "fused", False) and not getattr(comp, "dense", False)
@@ -560,6 +563,13 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         self._exchanger.allreduce_(t, average=True)
 
     def _log_selected(self, hdr_total: torch.Tensor):
+        if self._is_cuda and torch.cuda.is_current_stream_capturing():
+            # whole-step graph capture: the replayed copy lands in a slot of its
+            # own; train/graph.py logs the slots after every replay
+            slot = torch.zeros(1, dtype=torch.int32, device=hdr_total.device)
+            slot.copy_(hdr_total.view(-1)[:1], non_blocking=True)
+            self._graph_sel.append(slot)
+            return
         if self._sel_n == self._sel_dev.numel():
             # ring full (long epochs x many buckets): flush to the host -- one
             # sync per 8192 bucket-steps, nothing is overwritten

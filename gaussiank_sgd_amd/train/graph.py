@@ -15,12 +15,22 @@ the fused SGD kernel multiplies the captured lr by a device scalar
 (``opt._lr_mult``) that is refreshed from the host schedule before every
 replay.  ``recapture()`` rebuilds the graph when the density schedule moves
 (epoch boundary with the reference's density warm-up).
+Single stream: the optimizer's side (compression / exchange) stream is
+dropped for the captured step -- a hipGraph with cross-stream branches
+replays on ROCm 7 at ~10 ms per ResNet-20 bs32 step (the runtime resolves
+the branch edges from the host), the same step captured on one stream at
+1.43 ms (eager: 4.9 ms; scripts/graph_probe.sh, profiles/r02_graph_probe.txt).
+Overlap buys nothing in a replay whose launches are already on the device.
+``GKSGD_GRAPH_COMM_STREAM=1`` keeps the side stream.
+Not for recurrent models that carry hidden state across steps (bench.py
+refuses ``--graph`` for the LSTM).
 Requirements: every op of the step is stream-ordered without host syncs
 (true for the DistributedOptimizer / fused kernels of this package) and the
 autotuned convolution choices are cached by the eager warm-up steps.
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, Optional
 
 import torch
@@ -57,6 +67,10 @@ class GraphedStep:
         self.captures = 0
         dev = self.x.device
         self.mult = torch.ones(1, dtype=torch.float32, device=dev)
+        cs = getattr(opt, "_comm_stream", None)
+        if cs is not None and os.environ.get("GKSGD_GRAPH_COMM_STREAM", "0") != "1":
+            torch.cuda.current_stream(dev).wait_stream(cs)   # drain the side stream, then go single-stream
+            opt._comm_stream = None
 
     def _body(self) -> None:
         t, opt = self.trainer, self.opt
@@ -82,6 +96,7 @@ class GraphedStep:
         self.mult.fill_(1.0)
         self.opt._lr_mult = self.mult
         self.graph = torch.cuda.CUDAGraph()
+        self.opt._graph_sel = []
         with torch.cuda.graph(self.graph):
             self._body()
         self.trainer.train_iter -= 1          # capture records the step; it did not run it
@@ -102,6 +117,8 @@ class GraphedStep:
         t.adjust_learning_rate(t.train_epoch, t.optimizer)
         self.mult.fill_(float(t.lr) / float(self.lr0) if self.lr0 else 1.0)   # async, stream-ordered
         self.graph.replay()
+        for slot in getattr(self.opt, "_graph_sel", ()):   # selected counts of this replay (stream-ordered copies)
+            self.opt._log_selected(slot)
         t.train_iter += 1
 
 
