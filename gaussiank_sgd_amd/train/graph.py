@@ -87,12 +87,19 @@ class GraphedStep:
 
     def recapture(self) -> None:
         self.opt._lr_mult = None             # eager warm-up steps use the plain lr
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(self.warmup):      # eager warm-up on a side stream (allocator / autotune caches)
+        # warm-up on the current stream by default: MIOpen picked naive fallback
+        # solvers on a fresh side stream (ResNet-20 bs1024: 16.8 ms/step replayed
+        # vs 5.9 ms with this warm-up; eager 4.8-5.1 ms, profiles/r02_graph_probe.txt)
+        if os.environ.get("GKSGD_GRAPH_WARMUP_SIDE", "0") == "1":
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(self.warmup):      # eager warm-up on a side stream (allocator / autotune caches)
+                    self._body()
+            torch.cuda.current_stream().wait_stream(s)
+        else:
+            for _ in range(self.warmup):
                 self._body()
-        torch.cuda.current_stream().wait_stream(s)
         self.mult.fill_(1.0)
         self.opt._lr_mult = self.mult
         self.graph = torch.cuda.CUDAGraph()
