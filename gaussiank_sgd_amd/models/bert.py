@@ -20,6 +20,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import attention
+from ..ops.embedding import bert_embeddings
 from ..ops.linear import FastLinear
 from ..ops.ln import add_layernorm
 
@@ -126,10 +127,9 @@ class BertForMaskedLM(nn.Module):
         """Logits [B, T, V], or [B, P, V] at ``masked_positions`` ([B, P]
         indices, the Google-BERT pre-training format): the MLM head and the
         vocabulary projection then run on the masked rows only."""
-        B, T = input_ids.shape
-        pos = torch.arange(T, device=input_ids.device).unsqueeze(0)
-        tt = token_type_ids if token_type_ids is not None else torch.zeros_like(input_ids)
-        x = self.word_embeddings(input_ids) + self.position_embeddings(pos) + self.token_type_embeddings(tt)
+        # word + position + token-type lookups: one fused HIP pass each way on the GPU (ops/embedding.py)
+        x = bert_embeddings(input_ids, token_type_ids, self.word_embeddings, self.position_embeddings,
+                            self.token_type_embeddings)
         x = self.emb_drop(self.emb_ln(x))
         mask = None
         if attention_mask is not None:

@@ -57,6 +57,7 @@ HIP_SOURCES = [
     "kernels/stem.hip",
     "kernels/wgrad3.hip",
     "kernels/attn.hip",
+    "kernels/embed.hip",
 ]
 CXX_SOURCES = [
     "comm/rccl_engine.cpp",

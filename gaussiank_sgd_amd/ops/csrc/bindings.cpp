@@ -1067,6 +1067,58 @@ void add_ln_backward(at::Tensor dy, at::Tensor h, at::Tensor mean, at::Tensor rs
                       cur_stream(h));
 }
 
+// fused BERT input embedding (embed.hip)
+bool emb_supported(int64_t H, int64_t NT) { return gk::emb_supported((int)H, (int)NT); }
+int64_t emb_part_floats(int64_t H) { return (int64_t)gk::emb_type_parts() * 2 * H; }
+
+void emb_forward(at::Tensor ids, c10::optional<at::Tensor> tt, at::Tensor Ww, at::Tensor Wp, at::Tensor Wt,
+                 at::Tensor out) {
+  const int64_t B = ids.size(0), T = ids.size(1), M = B * T, H = Ww.size(1);
+  TORCH_CHECK(ids.is_cuda() && ids.scalar_type() == at::kLong && ids.dim() == 2 && ids.is_contiguous(),
+              "emb: ids must be contiguous int64 [B, T]");
+  const int64_t* tp = nullptr;
+  if (tt.has_value() && tt->defined()) {
+    TORCH_CHECK(tt->scalar_type() == at::kLong && tt->numel() == M && tt->is_contiguous(), "emb: tt int64 [B, T]");
+    tp = tt->data_ptr<int64_t>();
+  }
+  for (const at::Tensor* t : {&Ww, &Wp, &Wt})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->dim() == 2 && t->size(1) == H && t->is_contiguous(),
+                "emb: tables must be contiguous fp32 [*, H]");
+  TORCH_CHECK(gk::emb_supported((int)H, (int)Wt.size(0)) && T <= Wp.size(0), "emb: unsupported shape");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.numel() == M * H && out.is_contiguous(),
+              "emb: out fp32 [B, T, H]");
+  c10::DeviceGuard guard(ids.device());
+  gk::emb_forward(ids.data_ptr<int64_t>(), tp, Ww.data_ptr<float>(), Wp.data_ptr<float>(), Wt.data_ptr<float>(),
+                  out.data_ptr<float>(), M, (int)T, (int)H, cur_stream(ids));
+}
+
+void emb_backward(at::Tensor ids, c10::optional<at::Tensor> tt, at::Tensor dx, c10::optional<at::Tensor> dWw,
+                  c10::optional<at::Tensor> dWp, c10::optional<at::Tensor> dWt, at::Tensor part) {
+  const int64_t B = ids.size(0), T = ids.size(1), M = B * T, H = dx.size(-1);
+  TORCH_CHECK(ids.is_cuda() && ids.scalar_type() == at::kLong && ids.dim() == 2 && ids.is_contiguous(),
+              "emb: ids must be contiguous int64 [B, T]");
+  TORCH_CHECK(dx.is_cuda() && dx.scalar_type() == at::kFloat && dx.numel() == M * H && dx.is_contiguous(),
+              "emb: dx fp32 [B, T, H]");
+  const int64_t* tp = nullptr;
+  if (tt.has_value() && tt->defined()) {
+    TORCH_CHECK(tt->scalar_type() == at::kLong && tt->numel() == M && tt->is_contiguous(), "emb: tt int64 [B, T]");
+    tp = tt->data_ptr<int64_t>();
+  }
+  auto g = [&](const c10::optional<at::Tensor>& t) -> float* {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->dim() == 2 && t->size(1) == H &&
+                    t->is_contiguous(), "emb: gradient tables must be contiguous fp32 [*, H]");
+    return t->data_ptr<float>();
+  };
+  const int64_t P = dWp.has_value() && dWp->defined() ? dWp->size(0) : T;
+  const int64_t NT = dWt.has_value() && dWt->defined() ? dWt->size(0) : 1;
+  TORCH_CHECK(gk::emb_supported((int)H, (int)NT) && T <= P, "emb: unsupported shape");
+  TORCH_CHECK(part.scalar_type() == at::kFloat && part.numel() >= emb_part_floats(H), "emb: part too small");
+  c10::DeviceGuard guard(ids.device());
+  gk::emb_backward(ids.data_ptr<int64_t>(), tp, dx.data_ptr<float>(), g(dWw), g(dWp), g(dWt), part.data_ptr<float>(),
+                   M, (int)B, (int)T, (int)P, (int)NT, (int)H, cur_stream(ids));
+}
+
 // fused self-attention (attn.hip)
 void check_attn(const at::Tensor& t, const char* name, int64_t rows, int64_t cols) {
   TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.is_contiguous() && t.numel() == rows * cols &&
@@ -1329,6 +1381,11 @@ TORCH_LIBRARY(gksgd, m) {
   m.def("attn_dropout_mask(Tensor(a!) mask, int B, int heads, int T, float p, int seed) -> ()");
   m.def("add_ln_supported(int H) -> bool", &add_ln_supported);
   m.def("add_ln_ws_floats(int R, int H) -> int", &add_ln_ws_floats);
+  m.def("emb_supported(int H, int NT) -> bool", &emb_supported);
+  m.def("emb_part_floats(int H) -> int", &emb_part_floats);
+  m.def("emb_forward(Tensor ids, Tensor? tt, Tensor Ww, Tensor Wp, Tensor Wt, Tensor(a!) out) -> ()");
+  m.def("emb_backward(Tensor ids, Tensor? tt, Tensor dx, Tensor(a!)? dWw, Tensor(b!)? dWp, Tensor(c!)? dWt, "
+        "Tensor(d!) part) -> ()");
   m.def("add_ln_forward(Tensor a, Tensor x, Tensor? gamma, Tensor? beta, Tensor(a!) y, Tensor(b!) h, "
         "Tensor(c!) mean, Tensor(d!) rstd, float eps, float p, int seed) -> ()");
   m.def("add_ln_backward(Tensor dy, Tensor h, Tensor mean, Tensor rstd, Tensor? gamma, Tensor(a!) dx, "
@@ -1402,6 +1459,8 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("attn_bwd", &attn_bwd);
   m.impl("attn_dropout_mask", &attn_dropout_mask);
   m.impl("add_ln_forward", &add_ln_forward);
+  m.impl("emb_forward", &emb_forward);
+  m.impl("emb_backward", &emb_backward);
   m.impl("add_ln_backward", &add_ln_backward);
   m.impl("colsum_acc", &colsum_acc);
   m.impl("gelu_bwd_colsum", &gelu_bwd_colsum);

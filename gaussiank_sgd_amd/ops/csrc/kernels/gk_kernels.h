@@ -353,6 +353,18 @@ void attn_bwd(const void* qkv, const void* out, const void* dout, const float* l
 void attn_dropout_mask(uint8_t* mask, int B, int H, int T, float p, uint32_t seed, hipStream_t stream);
 
 // ---------------------------------------------------------------------------
+// Fused BERT input embedding (embed.hip): out[m] = Ww[ids[m]] + Wp[m % T] + Wt[tt[m]]
+// (fp32 [*, H], H % 4 == 0; tt may be null = type 0).  Backward: dWw (zeroed by
+// the caller) += scatter of dx rows (fp32 atomics), dWp = sum over the batch
+// (written, rows >= T zero), dWt = per-type sums through part
+// (emb_type_parts() * 2 * H floats); any of the three may be null.
+int emb_type_parts();
+bool emb_supported(int H, int NT);
+void emb_forward(const int64_t* ids, const int64_t* tt, const float* Ww, const float* Wp, const float* Wt, float* out,
+                 int64_t M, int T, int H, hipStream_t s);
+void emb_backward(const int64_t* ids, const int64_t* tt, const float* dx, float* dWw, float* dWp, float* dWt,
+                  float* part, int64_t M, int B, int T, int P, int NT, int H, hipStream_t s);
+
 // Fused residual add (+ dropout) + LayerNorm over rows of H bf16 (ln.hip).
 // forward : h = x + dropout_p(a), y = LN(h) * gamma + beta; saves h (bf16),
 //           mean, rstd (fp32 per row).  The dropout mask is a hash of
