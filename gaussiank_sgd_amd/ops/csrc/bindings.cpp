@@ -1092,8 +1092,12 @@ void emb_forward(at::Tensor ids, c10::optional<at::Tensor> tt, at::Tensor Ww, at
                   out.data_ptr<float>(), M, (int)T, (int)H, cur_stream(ids));
 }
 
+int64_t emb_word_ws_ints(int64_t V, int64_t M) { return gk::emb_word_ws_ints(V, M); }
+int64_t emb_word_part_floats(int64_t M, int64_t H) { return gk::emb_word_maxc(M) * H; }
+
 void emb_backward(at::Tensor ids, c10::optional<at::Tensor> tt, at::Tensor dx, c10::optional<at::Tensor> dWw,
-                  c10::optional<at::Tensor> dWp, c10::optional<at::Tensor> dWt, at::Tensor part) {
+                  c10::optional<at::Tensor> dWp, c10::optional<at::Tensor> dWt, at::Tensor part, at::Tensor sid,
+                  at::Tensor order, at::Tensor wws, at::Tensor wpart) {
   const int64_t B = ids.size(0), T = ids.size(1), M = B * T, H = dx.size(-1);
   TORCH_CHECK(ids.is_cuda() && ids.scalar_type() == at::kLong && ids.dim() == 2 && ids.is_contiguous(),
               "emb: ids must be contiguous int64 [B, T]");
@@ -1114,9 +1118,22 @@ void emb_backward(at::Tensor ids, c10::optional<at::Tensor> tt, at::Tensor dx, c
   const int64_t NT = dWt.has_value() && dWt->defined() ? dWt->size(0) : 1;
   TORCH_CHECK(gk::emb_supported((int)H, (int)NT) && T <= P, "emb: unsupported shape");
   TORCH_CHECK(part.scalar_type() == at::kFloat && part.numel() >= emb_part_floats(H), "emb: part too small");
+  const int64_t V = dWw.has_value() && dWw->defined() ? dWw->size(0) : 0;
+  if (V > 0) {
+    TORCH_CHECK(sid.is_cuda() && sid.scalar_type() == at::kLong && sid.numel() == M && sid.is_contiguous() &&
+                    order.is_cuda() && order.scalar_type() == at::kLong && order.numel() == M && order.is_contiguous(),
+                "emb: sid / order must be the stable sort of ids (int64 [M])");
+    TORCH_CHECK(wws.is_cuda() && wws.scalar_type() == at::kInt && wws.numel() >= gk::emb_word_ws_ints(V, M),
+                "emb: word workspace int32 [emb_word_ws_ints(V, M)]");
+    TORCH_CHECK(wpart.is_cuda() && wpart.scalar_type() == at::kFloat && wpart.numel() >= gk::emb_word_maxc(M) * H,
+                "emb: word partials fp32 [emb_word_part_floats(M, H)]");
+    TORCH_CHECK(V < (1ll << 31) && M < (1ll << 31), "emb: sizes must fit int32");
+  }
   c10::DeviceGuard guard(ids.device());
   gk::emb_backward(ids.data_ptr<int64_t>(), tp, dx.data_ptr<float>(), g(dWw), g(dWp), g(dWt), part.data_ptr<float>(),
-                   M, (int)B, (int)T, (int)P, (int)NT, (int)H, cur_stream(ids));
+                   V > 0 ? sid.data_ptr<int64_t>() : nullptr, V > 0 ? order.data_ptr<int64_t>() : nullptr,
+                   V > 0 ? wws.data_ptr<int>() : nullptr, V > 0 ? wpart.data_ptr<float>() : nullptr, V, M, (int)B,
+                   (int)T, (int)P, (int)NT, (int)H, cur_stream(ids));
 }
 
 // fused self-attention (attn.hip)
@@ -1384,8 +1401,10 @@ TORCH_LIBRARY(gksgd, m) {
   m.def("emb_supported(int H, int NT) -> bool", &emb_supported);
   m.def("emb_part_floats(int H) -> int", &emb_part_floats);
   m.def("emb_forward(Tensor ids, Tensor? tt, Tensor Ww, Tensor Wp, Tensor Wt, Tensor(a!) out) -> ()");
+  m.def("emb_word_ws_ints(int V, int M) -> int", &emb_word_ws_ints);
+  m.def("emb_word_part_floats(int M, int H) -> int", &emb_word_part_floats);
   m.def("emb_backward(Tensor ids, Tensor? tt, Tensor dx, Tensor(a!)? dWw, Tensor(b!)? dWp, Tensor(c!)? dWt, "
-        "Tensor(d!) part) -> ()");
+        "Tensor(d!) part, Tensor sid, Tensor order, Tensor(e!) wws, Tensor(f!) wpart) -> ()");
   m.def("add_ln_forward(Tensor a, Tensor x, Tensor? gamma, Tensor? beta, Tensor(a!) y, Tensor(b!) h, "
         "Tensor(c!) mean, Tensor(d!) rstd, float eps, float p, int seed) -> ()");
   m.def("add_ln_backward(Tensor dy, Tensor h, Tensor mean, Tensor rstd, Tensor? gamma, Tensor(a!) dx, "

@@ -362,8 +362,15 @@ int emb_type_parts();
 bool emb_supported(int H, int NT);
 void emb_forward(const int64_t* ids, const int64_t* tt, const float* Ww, const float* Wp, const float* Wt, float* out,
                  int64_t M, int T, int H, hipStream_t s);
+// sid / order: the ids stably sorted and their token positions; with them
+// (and wws: emb_word_ws_ints(V, M) ints, wpart: emb_word_maxc(M) * H floats)
+// dWw is WRITTEN row by row, deterministically; sid == nullptr: dWw zeroed by
+// the caller and accumulated with fp32 atomics.
+int64_t emb_word_maxc(int64_t M);
+int64_t emb_word_ws_ints(int64_t V, int64_t M);
 void emb_backward(const int64_t* ids, const int64_t* tt, const float* dx, float* dWw, float* dWp, float* dWt,
-                  float* part, int64_t M, int B, int T, int P, int NT, int H, hipStream_t s);
+                  float* part, const int64_t* sid, const int64_t* order, int* wws, float* wpart, int64_t V,
+                  int64_t M, int B, int T, int P, int NT, int H, hipStream_t s);
 
 // Fused residual add (+ dropout) + LayerNorm over rows of H bf16 (ln.hip).
 // forward : h = x + dropout_p(a), y = LN(h) * gamma + beta; saves h (bf16),

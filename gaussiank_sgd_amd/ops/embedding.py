@@ -2,12 +2,14 @@
 
 ``bert_embeddings(ids, tt, word, pos, ttype)`` = ``word(ids) + pos(arange(T))
 + ttype(tt)`` -- the three ``nn.Embedding`` lookups of the BERT input layer
-(fp32 [B, T, H]).  On the GPU it is one HIP pass forward and, backward, an
-atomic row scatter (word table), a batch sum (positions) and a fixed-order
+(fp32 [B, T, H]).  On the GPU it is one HIP pass forward and, backward, a
+bucketed row gather (word table), a batch sum (positions) and a fixed-order
 per-type reduction (token types) instead of PyTorch's three sort-based
-``embedding_dense_backward`` passes.  The word-table gradient is summed with
-fp32 atomics (order not fixed); ``torch.use_deterministic_algorithms(True)``
-or ``GKSGD_FUSED_EMB=0`` keeps the PyTorch path.  Elsewhere (CPU, no
+``embedding_dense_backward`` passes.  The word-table gradient is a stable
+sort of the ids plus gather-sums (64-token chunks for frequent ids, then one
+wave per vocabulary row), in ascending token order: deterministic;
+``torch.use_deterministic_algorithms(True)`` or ``GKSGD_FUSED_EMB=0`` keeps
+the PyTorch path.  Elsewhere (CPU, no
 extension, non-fp32 tables, padding_idx / max_norm) it is the plain
 composition.  The ``nn.Embedding`` modules and their state_dict keys are
 untouched.
@@ -47,11 +49,19 @@ class _EmbFn(torch.autograd.Function):
         sw, sp, st = ctx.shapes
         dev = dx.device
         dx = dx.float().contiguous()
-        dWw = torch.zeros(sw, dtype=torch.float32, device=dev) if ctx.needs_input_grad[2] else None
+        # every row of dWw is written by the counting-sort gather (no zero fill)
+        dWw = torch.empty(sw, dtype=torch.float32, device=dev) if ctx.needs_input_grad[2] else None
         dWp = torch.empty(sp, dtype=torch.float32, device=dev) if ctx.needs_input_grad[3] else None
         dWt = torch.empty(st, dtype=torch.float32, device=dev) if ctx.needs_input_grad[4] else None
         part = torch.empty(_ops().emb_part_floats(sw[1]), dtype=torch.float32, device=dev)
-        _ops().emb_backward(ids, tt, dx, dWw, dWp, dWt, part)
+        M = ids.numel()
+        if dWw is not None:
+            sid, order = torch.sort(ids.reshape(-1), stable=True)   # rocprim radix sort: ids bucketed, positions ascending
+        else:
+            sid = order = ids.reshape(-1)
+        wws = torch.empty(_ops().emb_word_ws_ints(sw[0], M), dtype=torch.int32, device=dev)
+        wpart = torch.empty(_ops().emb_word_part_floats(M, sw[1]), dtype=torch.float32, device=dev)
+        _ops().emb_backward(ids, tt, dx, dWw, dWp, dWt, part, sid, order, wws, wpart)
         return None, None, dWw, dWp, dWt
 
 

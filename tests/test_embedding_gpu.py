@@ -23,7 +23,9 @@ def _grads(mods):
 def test_fused_embedding_matches_torch(cuda, B, T, V, P, H, with_tt):
     mods = _mods(V, P, 2, H, cuda)
     ids = torch.randint(0, V, (B, T), device=cuda)
-    ids[0, :3] = 5                      # repeated ids: several atomic adds into one row
+    ids[0, :3] = 5                      # an id seen a few times: ranked (ascending token) sum
+    if T >= 100:
+        ids[:, :100] = 7                    # an id seen > 64 times: slot-order sum
     tt = torch.randint(0, 2, (B, T), device=cuda) if with_tt else None
     assert emb.fused_available(ids, *mods)
     dy = torch.randn(B, T, H, device=cuda)
@@ -56,3 +58,22 @@ def test_fused_embedding_bert_autocast(cuda):
     g = m.word_embeddings.weight.grad
     assert g is not None and torch.isfinite(g).all() and g.abs().sum() > 0
     assert m.position_embeddings.weight.grad[64:].abs().sum() == 0     # rows past T get no gradient
+
+
+def test_fused_embedding_backward_deterministic(cuda):
+    B, T, V, P, H = 8, 512, 30522, 512, 768
+    mods = _mods(V, P, 2, H, cuda)
+    ids = torch.randint(5, V, (B, T), device=cuda)
+    ids[:, ::7] = 4                     # a [MASK]-like id: 586 tokens, ten 64-token chunks
+    tt = torch.randint(0, 2, (B, T), device=cuda)
+    dy = torch.randn(B, T, H, device=cuda)
+    runs = []
+    for _ in range(2):
+        for m in mods:
+            m.weight.grad = None
+        emb.bert_embeddings(ids, tt, *mods).backward(dy)
+        runs.append(_grads(mods))
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
+    ref = torch.zeros(V, H, device=cuda, dtype=torch.float64).index_add_(0, ids.view(-1), dy.view(-1, H).double())
+    torch.testing.assert_close(runs[0][0].double(), ref, rtol=1e-5, atol=1e-4)
