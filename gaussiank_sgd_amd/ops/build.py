@@ -58,6 +58,7 @@ HIP_SOURCES = [
     "kernels/wgrad3.hip",
     "kernels/attn.hip",
     "kernels/embed.hip",
+    "kernels/xent.hip",
 ]
 CXX_SOURCES = [
     "comm/rccl_engine.cpp",

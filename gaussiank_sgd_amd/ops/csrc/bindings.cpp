@@ -1067,6 +1067,39 @@ void add_ln_backward(at::Tensor dy, at::Tensor h, at::Tensor mean, at::Tensor rs
                       cur_stream(h));
 }
 
+// fused softmax cross-entropy (xent.hip)
+bool xent_supported(int64_t V) { return gk::xent_supported((int)V); }
+
+void xent_forward(at::Tensor logits, at::Tensor labels, at::Tensor lse, at::Tensor loss, int64_t ignore) {
+  TORCH_CHECK(logits.is_cuda() && logits.scalar_type() == at::kBFloat16 && logits.dim() == 2 && logits.is_contiguous(),
+              "xent: logits must be contiguous bf16 [R, V]");
+  const int64_t R = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(gk::xent_supported((int)V), "xent: V must be even");
+  TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kLong && labels.numel() == R && labels.is_contiguous(),
+              "xent: labels int64 [R]");
+  for (const at::Tensor* t : {&lse, &loss})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->numel() == R && t->is_contiguous(), "xent: fp32 [R]");
+  c10::DeviceGuard guard(logits.device());
+  gk::xent_forward(logits.data_ptr(), labels.data_ptr<int64_t>(), lse.data_ptr<float>(), loss.data_ptr<float>(), R,
+                   (int)V, ignore, cur_stream(logits));
+}
+
+void xent_backward(at::Tensor logits, at::Tensor labels, at::Tensor lse, at::Tensor scale, at::Tensor grad,
+                   int64_t ignore) {
+  TORCH_CHECK(logits.is_cuda() && logits.scalar_type() == at::kBFloat16 && logits.dim() == 2 && logits.is_contiguous(),
+              "xent: logits must be contiguous bf16 [R, V]");
+  const int64_t R = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(gk::xent_supported((int)V), "xent: V must be even");
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.numel() == R && labels.is_contiguous(), "xent: labels int64 [R]");
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.numel() == R && scale.scalar_type() == at::kFloat &&
+                  scale.numel() == 1 && scale.is_cuda(), "xent: lse fp32 [R], scale fp32 [1]");
+  TORCH_CHECK(grad.scalar_type() == at::kBFloat16 && grad.sizes() == logits.sizes() && grad.is_contiguous(),
+              "xent: grad bf16 like logits");
+  c10::DeviceGuard guard(logits.device());
+  gk::xent_backward(logits.data_ptr(), labels.data_ptr<int64_t>(), lse.data_ptr<float>(), scale.data_ptr<float>(),
+                    grad.data_ptr(), R, (int)V, ignore, cur_stream(logits));
+}
+
 // fused BERT input embedding (embed.hip)
 bool emb_supported(int64_t H, int64_t NT) { return gk::emb_supported((int)H, (int)NT); }
 int64_t emb_part_floats(int64_t H) { return (int64_t)gk::emb_type_parts() * 2 * H; }
@@ -1398,6 +1431,9 @@ TORCH_LIBRARY(gksgd, m) {
   m.def("attn_dropout_mask(Tensor(a!) mask, int B, int heads, int T, float p, int seed) -> ()");
   m.def("add_ln_supported(int H) -> bool", &add_ln_supported);
   m.def("add_ln_ws_floats(int R, int H) -> int", &add_ln_ws_floats);
+  m.def("xent_supported(int V) -> bool", &xent_supported);
+  m.def("xent_forward(Tensor logits, Tensor labels, Tensor(a!) lse, Tensor(b!) loss, int ignore) -> ()");
+  m.def("xent_backward(Tensor logits, Tensor labels, Tensor lse, Tensor scale, Tensor(a!) grad, int ignore) -> ()");
   m.def("emb_supported(int H, int NT) -> bool", &emb_supported);
   m.def("emb_part_floats(int H) -> int", &emb_part_floats);
   m.def("emb_forward(Tensor ids, Tensor? tt, Tensor Ww, Tensor Wp, Tensor Wt, Tensor(a!) out) -> ()");
@@ -1478,6 +1514,8 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("attn_bwd", &attn_bwd);
   m.impl("attn_dropout_mask", &attn_dropout_mask);
   m.impl("add_ln_forward", &add_ln_forward);
+  m.impl("xent_forward", &xent_forward);
+  m.impl("xent_backward", &xent_backward);
   m.impl("emb_forward", &emb_forward);
   m.impl("emb_backward", &emb_backward);
   m.impl("add_ln_backward", &add_ln_backward);

@@ -372,6 +372,15 @@ void emb_backward(const int64_t* ids, const int64_t* tt, const float* dx, float*
                   float* part, const int64_t* sid, const int64_t* order, int* wws, float* wpart, int64_t V,
                   int64_t M, int B, int T, int P, int NT, int H, hipStream_t s);
 
+// Fused softmax cross-entropy over bf16 logit rows (xent.hip), V even:
+// forward writes lse[R] and loss[R] (0 for label == ignore); backward writes
+// bf16 dlogits = (softmax - onehot) * (*scale) (0 rows for ignored labels).
+bool xent_supported(int V);
+void xent_forward(const void* logits, const int64_t* labels, float* lse, float* loss, int64_t R, int V, int64_t ignore,
+                  hipStream_t s);
+void xent_backward(const void* logits, const int64_t* labels, const float* lse, const float* scale, void* grad,
+                   int64_t R, int V, int64_t ignore, hipStream_t s);
+
 // Fused residual add (+ dropout) + LayerNorm over rows of H bf16 (ln.hip).
 // forward : h = x + dropout_p(a), y = LN(h) * gamma + beta; saves h (bf16),
 //           mean, rstd (fp32 per row).  The dropout mask is a hash of

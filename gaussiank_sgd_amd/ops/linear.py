@@ -76,11 +76,14 @@ def _hip_gemm_ok(K: int, N: int) -> bool:
     return K % 64 == 0 and N % 64 == 0
 
 
-def _fwd(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor]) -> torch.Tensor:
-    """y = x2 . w^T (+ bias), bf16 out."""
+def _fwd(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor],
+         b16: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = x2 . w^T (+ bias), bf16 out.  ``b16``: the bias already in bf16 (the
+    shadow arena's view) -- hipBLASLt then needs no per-call cast."""
     M, K = x2.shape
     N = w.shape[0]
-    b16 = bias.to(torch.bfloat16) if bias is not None else None
+    if b16 is None and bias is not None:
+        b16 = bias.to(torch.bfloat16)
 
     def blas():
         return torch.addmm(b16, x2, w.t()) if b16 is not None else torch.mm(x2, w.t())
@@ -169,7 +172,7 @@ class _LinearFn(torch.autograd.Function):
     post-accumulate hook still reports the parameter ready)."""
 
     @staticmethod
-    def forward(ctx, x, weight, w_bf16, wsink, bias, bsink, gelu):
+    def forward(ctx, x, weight, w_bf16, wsink, bias, bsink, gelu, b_bf16=None):
         shape = x.shape
         K = shape[-1]
         x2 = x.reshape(-1, K)
@@ -179,7 +182,7 @@ class _LinearFn(torch.autograd.Function):
         w = w_bf16 if w_bf16 is not None else weight.detach().to(torch.bfloat16)
         w = w.contiguous()
         b = bias.detach().float().contiguous() if bias is not None else None
-        y = _fwd(x2, w, b)
+        y = _fwd(x2, w, b, b_bf16)
         pre = None
         if gelu:
             pre, y = y, F.gelu(y)
@@ -229,7 +232,7 @@ class _LinearFn(torch.autograd.Function):
                 gbias = None
             else:
                 gbias = gbias.to(ctx.bdtype)
-        return dx, gweight, None, None, gbias, None, None
+        return dx, gweight, None, None, gbias, None, None, None
 
 
 def _supported(x: torch.Tensor, mod: nn.Linear) -> bool:
@@ -256,11 +259,12 @@ class FastLinear(nn.Linear):
             use_shadow = winfo is not None and torch.is_autocast_enabled(dev)
             w_bf16, wsink = (winfo[0], winfo[1]) if use_shadow else (None, None)
             bsink = binfo[1] if (use_shadow and binfo is not None) else None
+            b_bf16 = binfo[0] if (use_shadow and binfo is not None) else None
             if not torch.is_grad_enabled() or not self.weight.requires_grad:
                 wsink = None
             if not torch.is_grad_enabled() or self.bias is None or not self.bias.requires_grad:
                 bsink = None
-            return _LinearFn.apply(x, self.weight, w_bf16, wsink, self.bias, bsink, act == "gelu")
+            return _LinearFn.apply(x, self.weight, w_bf16, wsink, self.bias, bsink, act == "gelu", b_bf16)
         slow = getattr(self, "_gk_slow", None)
         y = slow(x) if slow is not None else super().forward(x)
         return F.gelu(y) if act == "gelu" else y
