@@ -30,6 +30,7 @@ import torch.nn as nn
 from .. import settings
 from ..data import DATASETS, SyntheticData
 from ..models import MaskedLMLoss, create_net, repackage_hidden
+from ..ops import xent
 from ..optim import sgd_param_groups
 from ..settings import logger
 from ..utils import trace
@@ -254,7 +255,14 @@ class DLTrainer:
             if self.dnn == "lstm":
                 hidden = repackage_hidden(hidden) if hidden is not None else self.net.init_hidden(inputs.shape[1])
                 outputs, hidden = self.net(inputs, hidden)
-                loss = self.criterion(outputs.reshape(-1, self.net.vocab_size).float(), labels.reshape(-1))
+                c = self.criterion
+                if (isinstance(c, nn.CrossEntropyLoss) and c.reduction == "mean" and c.weight is None and
+                        c.label_smoothing == 0.0):
+                    # fused softmax cross-entropy on the bf16 logits on the GPU (ops/xent.py)
+                    loss = xent.cross_entropy(outputs.reshape(-1, self.net.vocab_size), labels.reshape(-1),
+                                              ignore_index=self.criterion.ignore_index)
+                else:
+                    loss = self.criterion(outputs.reshape(-1, self.net.vocab_size).float(), labels.reshape(-1))
             elif self.dnn.startswith("bert"):
                 if isinstance(labels, (tuple, list)):     # (masked positions, labels)
                     outputs = self.net(inputs, masked_positions=labels[0])
