@@ -195,21 +195,19 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
   // Instruction j of this wave fills staged rows i*8 .. i*8+7, i = wave + j*NW:
   // A rows while i*8 < BM, B rows after (streamed panel only).
   const uint16_t* ptr[LPW];   // A: row (or gathered pixel) base + chunk; B: row base + chunk
-  // gather: bit kh (bits 0-3) / bit 8 + kw (bits 8-11) of okb set when tap row
-  // kh / column kw of this lane's output pixel lies inside the image (set once
-  // per M tile; a K step tests two bits instead of recomputing and comparing
-  // the position).  Padding taps read the zero row: any 16-byte chunk of it
-  // will do, so one per-lane chunk (lane & 7, eight distinct chunks per eight
-  // lanes as for a data row) serves every instruction.
-  uint32_t okb[LPW];
-  const uint16_t* zsrc = GATHER ? geo.zero + (lane & 7) * 8 : nullptr;
+  // gather: bit kh of okh / bit kw of okw set when tap row kh / column kw of
+  // this lane's output pixel lies inside the image (set once per M tile; a K
+  // step tests two bits instead of recomputing and comparing the position)
+  uint32_t okh[LPW], okw[LPW];
+  const uint16_t* zrow[LPW];  // gather: this lane's chunk of the zero row (padding taps)
 #pragma unroll
   for (int j = 0; j < LPW; ++j) {
     const int i = wave + j * Cfg::NW;
     const int r = i * 8 + (lane >> 3);
     const int c = (lane & 7) ^ swz(r);
     ptr[j] = j < Cfg::LPWA ? nullptr : B + (int64_t)(n0 + r - Cfg::BM) * ldb + c * 8;
-    okb[j] = 0u;
+    okh[j] = okw[j] = 0u;
+    zrow[j] = GATHER ? geo.zero + c * 8 : nullptr;
   }
   auto set_rows = [&](int64_t mt) {
     const int64_t m0 = mt * Cfg::BM;
@@ -234,7 +232,8 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
             bh |= (uint32_t)((unsigned)(ih0 + q) < (unsigned)geo.H) << q;
             bw |= (uint32_t)((unsigned)(iw0 + q) < (unsigned)geo.W) << q;
           }
-          okb[j] = bh | (bw << 8);
+          okh[j] = bh;
+          okw[j] = bw;
           ptr[j] = A + (((int64_t)n * geo.H + ih0) * geo.W + iw0) * geo.C + c * 8;
         } else {
           ptr[j] = A + gr * lda + c * 8;
@@ -258,8 +257,8 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
       const uint16_t* src;
       if (j < Cfg::LPWA) {
         if (GATHER) {
-          const bool ok = ((okb[j] >> s_kh) & (okb[j] >> (8 + s_kw)) & 1u) != 0u;
-          src = ok ? ptr[j] + toff : zsrc;
+          const bool ok = ((okh[j] >> s_kh) & (okw[j] >> s_kw) & 1u) != 0u;
+          src = ok ? ptr[j] + toff : zrow[j];
         } else {
           src = ptr[j] + k0;
         }
@@ -301,10 +300,14 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
   int ks = 0;
   int buf = 0;
   float ssum[4][4], ssq[4][4];   // BN partials: [ns][r] of this lane's column, summed over its rows
+  float bia[4][4];               // bias of this lane's columns
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) ssum[a][b] = ssq[a][b] = 0.f;
+    for (int b = 0; b < 4; ++b) {
+      ssum[a][b] = ssq[a][b] = 0.f;
+      bia[a][b] = geo.bias ? geo.bias[n0 + wn * 64 + a * 16 + fq * 4 + b] : 0.f;
+    }
   // BN-backward epilogue: in the store layout every lane owns 8 consecutive
   // channels per column pair pr (the same channels for every tile): offset
   // cofs within the pair's 32 columns
@@ -387,15 +390,8 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
 #pragma unroll
         for (int pr = 0; pr < 2; ++pr) {
           const f32x4 va = acc[ms][2 * pr], vb = acc[ms][2 * pr + 1];
-          // bias of this lane's columns, loaded per tile (L1-resident) rather than held
-          // in 16 registers through the main loop
-          float ba[4] = {0.f, 0.f, 0.f, 0.f}, bb[4] = {0.f, 0.f, 0.f, 0.f};
-          if (geo.bias) {
-            const float4 x0 = *reinterpret_cast<const float4*>(geo.bias + n0 + wn * 64 + 2 * pr * 16 + fq * 4);
-            const float4 x1 = *reinterpret_cast<const float4*>(geo.bias + n0 + wn * 64 + (2 * pr + 1) * 16 + fq * 4);
-            ba[0] = x0.x; ba[1] = x0.y; ba[2] = x0.z; ba[3] = x0.w;
-            bb[0] = x1.x; bb[1] = x1.y; bb[2] = x1.z; bb[3] = x1.w;
-          }
+          const float* ba = bia[2 * pr];
+          const float* bb = bia[2 * pr + 1];
           const uint32_t a0 = pack_bf16x2(va[0] + ba[0], va[1] + ba[1]), a1 = pack_bf16x2(va[2] + ba[2], va[3] + ba[3]);
           const uint32_t b0 = pack_bf16x2(vb[0] + bb[0], vb[1] + bb[1]), b1 = pack_bf16x2(vb[2] + bb[2], vb[3] + bb[3]);
           if (stats && !bnb && (full || m < M)) {   // statistics of the values as stored (bf16)
