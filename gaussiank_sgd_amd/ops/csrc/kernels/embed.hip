@@ -48,21 +48,6 @@ __global__ __launch_bounds__(kBlock) void emb_fwd_kernel(const int64_t* __restri
   reinterpret_cast<float4*>(out)[i] = make_float4(a.x + b.x + c.x, a.y + b.y + c.y, a.z + b.z + c.z, a.w + b.w + c.w);
 }
 
-__global__ __launch_bounds__(kBlock) void emb_word_bwd_kernel(const int64_t* __restrict__ ids,
-                                                              const float* __restrict__ dx, float* __restrict__ dWw,
-                                                              int64_t M, int H4) {
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= M * H4) return;
-  const int64_t m = i / H4;
-  const int h = (int)(i - m * H4);
-  const float4 g = reinterpret_cast<const float4*>(dx)[i];
-  float* dst = dWw + ids[m] * (int64_t)H4 * 4 + h * 4;
-  atomicAdd(dst + 0, g.x);
-  atomicAdd(dst + 1, g.y);
-  atomicAdd(dst + 2, g.z);
-  atomicAdd(dst + 3, g.w);
-}
-
 // dWp[t] = sum_b dx[b * T + t] for t < T; rows T..P-1 are zero
 __global__ __launch_bounds__(kBlock) void emb_pos_bwd_kernel(const float* __restrict__ dx, float* __restrict__ dWp,
                                                              int B, int T, int P, int H4) {
@@ -293,8 +278,8 @@ void emb_forward(const int64_t* ids, const int64_t* tt, const float* Ww, const f
 void emb_backward(const int64_t* ids, const int64_t* tt, const float* dx, float* dWw, float* dWp, float* dWt,
                   float* part, const int64_t* sid, const int64_t* order, int* wws, float* wpart, int64_t V,
                   int64_t M, int B, int T, int P, int NT, int H, hipStream_t s) {
+  (void)ids;
   const int H4 = H / 4;
-  const int64_t n = M * H4;
   if (dWw && sid) {   // stable-sort buckets + gathers: every row of dWw written (no zero fill)
     int* rstart = wws;
     int* rend = wws + V;
@@ -313,9 +298,6 @@ void emb_backward(const int64_t* ids, const int64_t* tt, const float* dx, float*
                        order, rstart, rend, cbase, chunk_row, counter, dx, wpart, maxc, H4);
     hipLaunchKernelGGL(emb_word_gather_kernel, dim3((unsigned)((V + kBlock / 64 - 1) / (kBlock / 64))), dim3(kBlock), 0,
                        s, order, rstart, rend, cbase, dx, wpart, dWw, (int)V, H4);
-  } else if (dWw) {   // zeroed by the caller: fp32 atomics
-    hipLaunchKernelGGL(emb_word_bwd_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, ids, dx,
-                       dWw, M, H4);
   }
   if (dWp)
     hipLaunchKernelGGL(emb_pos_bwd_kernel, dim3((unsigned)(((int64_t)P * H4 + kBlock - 1) / kBlock)), dim3(kBlock), 0,

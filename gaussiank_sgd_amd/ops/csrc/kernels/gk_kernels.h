@@ -364,8 +364,7 @@ void emb_forward(const int64_t* ids, const int64_t* tt, const float* Ww, const f
                  int64_t M, int T, int H, hipStream_t s);
 // sid / order: the ids stably sorted and their token positions; with them
 // (and wws: emb_word_ws_ints(V, M) ints, wpart: emb_word_maxc(M) * H floats)
-// dWw is WRITTEN row by row, deterministically; sid == nullptr: dWw zeroed by
-// the caller and accumulated with fp32 atomics.
+// dWw is WRITTEN row by row, deterministically (dWw requires sid / order).
 int64_t emb_word_maxc(int64_t M);
 int64_t emb_word_ws_ints(int64_t V, int64_t M);
 void emb_backward(const int64_t* ids, const int64_t* tt, const float* dx, float* dWw, float* dWp, float* dWt,
