@@ -6,13 +6,28 @@ Metric (BASELINE.json): "images/sec (whole node) ResNet-50 k=0.1% at 1/2/4/8
 MI355X; effective grad compression ratio".  One process per GPU; launched
 by ``torch.distributed.run`` for N > 1 (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*).
 
-Each timed step is the FULL training step: zero_grad, forward (bf16
-autocast, channels_last), backward, per-bucket fused Gaussian-k compression
-with error feedback, packed all-gather over RCCL, scatter-add average, fused
+Each timed step is the FULL training step: zero_grad, forward
+(channels_last), backward, per-bucket fused Gaussian-k compression with error
+feedback, packed all-gather over RCCL, scatter-add average, fused
 momentum-SGD update of every parameter.  The compressor also runs at N = 1
 (world of one) so the per-GPU work is identical at every N (weak scaling).
 Data: synthetic ImageNet-shaped batches generated on the device; weights:
 random init.
+
+Precision: the headline is fp32 compute (fp32 weights, activations and
+gradients -- the reference trained in fp32, settings.py:28 USE_FP16=False),
+on the hand-written fp32-MFMA convolutions (ops/conv1x1.py); a second timed
+phase in the same process measures the bf16-autocast step and reports it as
+``bf16_value`` / ``bf16_ms_per_step`` (``--no-bf16-phase`` skips it;
+``--amp bf16`` makes bf16 the headline).
+
+N > 1 also times, after the sparse loop, a dense comparator: the same model
+with a bucketed (``--dense-bucket-mb``, 25 MB), backward-overlapped RCCL
+all-reduce of fp32 gradients and no compression -- ``dense_ms_per_step`` /
+``speedup_vs_dense`` answer whether sparsification pays on xGMI.
+``exposed_comm_ms`` is the mean time, per timed step, from the end of the
+backward pass on the compute stream to the end of the update (event pair):
+the communication + decompression + update that the backward did not hide.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch-size B]
        [--compressor gaussian] [--density 0.001] [--model resnet50]
@@ -73,7 +88,13 @@ def parse():
                          "backward times (utils/profiler.benchmark) and the perf models (utils/perf_model.py)")
     ap.add_argument("--plan-world", type=int, default=None,
                     help="world size the planner's cost models assume (default: this world)")
-    ap.add_argument("--amp", default="bf16", choices=["bf16", "none"])
+    ap.add_argument("--amp", default="none", choices=["bf16", "none"],
+                    help="headline compute precision: none = fp32 (the reference's), bf16 = bf16 autocast")
+    ap.add_argument("--no-bf16-phase", action="store_true",
+                    help="skip the secondary bf16 phase of an fp32 headline run")
+    ap.add_argument("--no-dense-phase", action="store_true", help="skip the dense comparator at N > 1")
+    ap.add_argument("--dense-bucket-mb", type=float, default=25.0,
+                    help="bucket size of the dense comparator's overlapped all-reduce (MB of fp32 gradients)")
     ap.add_argument("--no-channels-last", action="store_true")
     ap.add_argument("--dense", action="store_true", help="dense RCCL all-reduce comparator (compressor none)")
     ap.add_argument("--no-native-rccl", action="store_true")
@@ -137,20 +158,135 @@ def probe_collectives(ex, P: int, dev, rec_bytes: int, dense_bytes: int, iters: 
     return out
 
 
-def main() -> int:
-    args = parse()
-    from gaussiank_sgd_amd import ops
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def build(args, amp: str, dense: bool, threshold: int, P: int, rank: int):
+    """Trainer + DistributedOptimizer of one timed phase.  amp: "fp32" / "bf16"."""
     from gaussiank_sgd_amd.compression import compressors
     from gaussiank_sgd_amd.parallel import comm
     from gaussiank_sgd_amd.parallel.distributed_optimizer import DistributedOptimizer
     from gaussiank_sgd_amd.train import DLTrainer
 
+    dataset, _, _, _, _ = MODELS[args.model]
+    trainer = DLTrainer(rank, P, dnn=args.model, dataset=dataset, batch_size=args.batch_size,
+                        lr=0.1, nworkers=P, device="cuda", amp="bf16" if amp == "bf16" else None,
+                        channels_last=not args.no_channels_last, seed=0)
+    comp_name = "none" if dense else args.compressor
+    is_sparse = not dense and comp_name not in ("none", "bucket")
+    seq_names = layer_times = None
+    if args.planner != "threshold" and not dense:
+        # reference dist_trainer.py:38-47: layer-wise backward profile, shared from rank 0
+        from gaussiank_sgd_amd.utils.profiler import benchmark
+        seq_names, layer_times, _ = benchmark(trainer, warmup=3, iterations=10)
+        layer_times = comm.broadcast_object(list(layer_times), 0)
+    opt = DistributedOptimizer(trainer.optimizer, named_parameters=trainer.net.named_parameters(),
+                               compression=compressors[comp_name], is_sparse=is_sparse, density=args.density,
+                               threshold=threshold, compress_single_rank=True, density_warmup=False,
+                               native_rccl=not args.no_native_rccl, seq_layernames=seq_names,
+                               layerwise_times=layer_times, planner=args.planner if not dense else "threshold",
+                               planner_world=args.plan_world,
+                               momentum_correction=is_sparse and not args.no_momentum_correction)
+    comm.broadcast_parameters(trainer.net.state_dict(), root_rank=0)
+    if not args.no_shadow:
+        from gaussiank_sgd_amd.parallel import install_bf16_shadow, install_direct_grads
+        if amp == "bf16":
+            install_bf16_shadow(trainer.net, opt)
+        else:
+            install_direct_grads(trainer.net, opt)
+    trainer.update_optimizer(opt)
+    trainer.display = 10 ** 9  # no host-syncing log lines inside the timed loop
+    return trainer, opt, comp_name, is_sparse
+
+
+def run_phase(args, trainer, opt, steps: int, warmup: int, P: int):
+    """W untimed warm-up steps, then EXACTLY K steps bracketed by a barrier +
+    synchronize on both sides; returns (elapsed seconds, max over ranks;
+    exposed-comm ms per step, max over ranks; the step callable)."""
+    from gaussiank_sgd_amd.parallel import comm
+
+    state = {"hidden": None}
+    clip = 0.25 if args.model == "lstm" else None  # reference dist_trainer.py:80-85
+    marks = []   # (end of backward, end of update) event pairs of the timed steps
+
+    def step():
+        opt.zero_grad()
+        if args.model == "lstm":
+            _, state["hidden"] = trainer.train(1, hidden=state["hidden"])
+        else:
+            trainer.train(1)
+        ev = None
+        if state.get("mark"):
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+        if clip is not None:
+            opt.synchronize()
+            opt.clip_grad_norm_(clip)
+        trainer.update_model()
+        if ev is not None:
+            e2 = torch.cuda.Event(enable_timing=True)
+            e2.record()
+            marks.append((ev, e2))
+
+    if args.graph and args.model == "lstm":
+        raise SystemExit("bench.py --graph: the LSTM carries hidden state across steps; not graph-capturable")
+    run = step
+    if args.graph:
+        # whole-step HIP graph: capture after the eager warm-up, replay in the timed loop
+        from gaussiank_sgd_amd.train.graph import GraphedStep
+        for _ in range(warmup):
+            step()
+        run = GraphedStep(trainer, opt, clip)
+    for _ in range(warmup):
+        run()
+    torch.cuda.synchronize()
+    opt._collect_selected()  # drop warm-up counts
+    state["mark"] = not args.graph
+    comm.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        run()
+    comm.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    state["mark"] = False
+    exposed = sum(a.elapsed_time(b) for a, b in marks) / len(marks) if marks else float("nan")
+    t = torch.tensor([elapsed, exposed], dtype=torch.float64, device="cuda")
+    if P > 1:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return float(t[0]), float(t[1]), run
+
+
+def release(trainer, opt) -> None:
+    import gc
+    if opt._exchanger is not None:
+        opt._exchanger.close()
+        opt._exchanger = None
+    del trainer, opt
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+
+
+def main() -> int:
+    args = parse()
+    from gaussiank_sgd_amd import ops
+    from gaussiank_sgd_amd.compression import compressors
+    from gaussiank_sgd_amd.parallel import comm
+
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus > 1 and world_env == 1:
-        # self-launch: start torch.distributed.run as a child (never exec after touching the GPU)
+        # self-launch: start torch.distributed.run as a child (never exec after touching the GPU);
+        # a free port unless MASTER_PORT pins one (a busy fixed port would fail the whole run)
         import subprocess
+        port = os.environ.get("MASTER_PORT") or str(free_port())
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
-               "--master-addr", "127.0.0.1", "--master-port", os.environ.get("MASTER_PORT", "29533"),
+               "--master-addr", "127.0.0.1", "--master-port", port,
                os.path.abspath(__file__)] + sys.argv[1:]
         return subprocess.call(cmd)
 
@@ -172,83 +308,19 @@ def main() -> int:
     dataset, default_bs, unit, tok_per_sample, data_desc = MODELS[args.model]
     if args.batch_size is None:
         args.batch_size = int(os.environ.get("GKSGD_BENCH_BS", default_bs)) if args.model == "resnet50" else default_bs
-    trainer = DLTrainer(rank, P, dnn=args.model, dataset=dataset, batch_size=args.batch_size,
-                        lr=0.1, nworkers=P, device="cuda", amp=None if args.amp == "none" else "bf16",
-                        channels_last=not args.no_channels_last, seed=0)
-    comp_name = "none" if args.dense else args.compressor
-    is_sparse = not args.dense and comp_name not in ("none", "bucket")
-    seq_names = layer_times = None
-    if args.planner != "threshold":
-        # reference dist_trainer.py:38-47: layer-wise backward profile, shared from rank 0
-        from gaussiank_sgd_amd.utils.profiler import benchmark
-        seq_names, layer_times, _ = benchmark(trainer, warmup=3, iterations=10)
-        layer_times = comm.broadcast_object(list(layer_times), 0)
-    opt = DistributedOptimizer(trainer.optimizer, named_parameters=trainer.net.named_parameters(),
-                               compression=compressors[comp_name], is_sparse=is_sparse, density=args.density,
-                               threshold=args.threshold, compress_single_rank=True, density_warmup=False,
-                               native_rccl=not args.no_native_rccl, seq_layernames=seq_names,
-                               layerwise_times=layer_times, planner=args.planner, planner_world=args.plan_world,
-                               momentum_correction=is_sparse and not args.no_momentum_correction)
-    comm.broadcast_parameters(trainer.net.state_dict(), root_rank=0)
-    if args.amp == "bf16" and not args.no_shadow:
-        from gaussiank_sgd_amd.parallel import install_bf16_shadow
-        install_bf16_shadow(trainer.net, opt)
-    trainer.update_optimizer(opt)
-    trainer.display = 10 ** 9  # no host-syncing log lines inside the timed loop
+    amp = "bf16" if args.amp == "bf16" else "fp32"
+    trainer, opt, comp_name, is_sparse = build(args, amp, args.dense, args.threshold, P, rank)
     nparams = sum(p.numel() for p in trainer.net.parameters() if p.requires_grad)
-
-    state = {"hidden": None}
-    clip = 0.25 if args.model == "lstm" else None  # reference dist_trainer.py:80-85
-
-    def step():
-        opt.zero_grad()
-        if args.model == "lstm":
-            _, state["hidden"] = trainer.train(1, hidden=state["hidden"])
-        else:
-            trainer.train(1)
-        if clip is not None:
-            opt.synchronize()
-            opt.clip_grad_norm_(clip)
-        trainer.update_model()
-
-    if args.graph and args.model == "lstm":
-        raise SystemExit("bench.py --graph: the LSTM carries hidden state across steps; not graph-capturable")
-    if args.graph:
-        # whole-step HIP graph: capture after the eager warm-up, replay in the timed loop
-        from gaussiank_sgd_amd.train.graph import GraphedStep
-        for _ in range(args.warmup):
-            step()
-        step = GraphedStep(trainer, opt, clip)
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    opt._collect_selected()  # drop warm-up counts
-    comm.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    comm.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if P > 1:
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    elapsed = float(t)
+    elapsed, exposed, step = run_phase(args, trainer, opt, args.steps, args.warmup, P)
     loss = trainer.current_loss()
-    counts = opt._collect_selected()
-    sel = (sum(counts) / max(1, args.steps)) if counts else 0.0
+    pairs = opt._collect_selected(with_totals=True)
+    sent = sum(p[0] for p in pairs) / max(1, args.steps)
+    total = sum(p[1] for p in pairs) / max(1, args.steps)
     # What goes on the wire per rank and step: one fixed-size record per
     # bucket, (4 header + k_cap indices + k_cap values) int32 words.
     comp = compressors[comp_name]
-    k_total, wire_bytes = 0, 0
-    for b in opt.arena.buckets:
-        if is_sparse:
-            kb = comp.k_of(b.numel, args.density)
-            k_total += kb
-            wire_bytes += (ops.REC_HDR + 2 * comp.k_cap_for(kb, b.numel)) * 4
-        else:
-            wire_bytes += b.numel * 4
+    k_total = sum(comp.k_of(b.numel, args.density) for b in opt.arena.buckets) if is_sparse else 0
+    wire_bytes = opt.wire_bytes_per_step(args.density if is_sparse else 1.0)
     ratio = (nparams * 4.0) / wire_bytes if wire_bytes else 1.0
     replicas = None
     if P > 1:
@@ -293,7 +365,7 @@ def main() -> int:
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16" if args.amp == "bf16" else "fp32",
+        "dtype": amp,
         "data": data_desc + ", random-init weights",
         "config": {
             "model": args.model,
@@ -314,12 +386,16 @@ def main() -> int:
         "world": P,
         "exchange": opt._exchanger.kind if opt._exchanger is not None else "none",
         "replicas_consistent": replicas,
+        "exposed_comm_ms": round(exposed, 3) if exposed == exposed else None,
         "collectives": collectives,
         "effective_compression_ratio": round(ratio, 1),
         "wire_bytes_per_rank_step": wire_bytes,
-        "selected_per_step": round(sel, 1),
+        # sent: entries actually in the records (<= k_cap per bucket); total:
+        # entries that passed the threshold before the k_cap overflow cut
+        "selected_per_step": round(sent, 1),
+        "candidates_per_step": round(total, 1),
         "k_per_step": k_total if is_sparse else None,
-        "selected_over_k": round(sel / k_total, 4) if is_sparse and k_total else None,
+        "selected_over_k": round(sent / k_total, 4) if is_sparse and k_total else None,
         "params": nparams,
         "final_loss": round(loss, 4) if loss == loss else None,
     }
@@ -332,14 +408,37 @@ def main() -> int:
         with open(os.environ["GKSGD_GEMM_DUMP"], "w") as f:
             json.dump([[list(k), list(v), [[list(t), r] for t, r in log.get(k, [])]]
                        for k, v in tuned_choices().items()], f)
+    release(trainer, opt)
+
+    # ---- dense comparator (N > 1): bucketed, backward-overlapped RCCL all-reduce
+    if P > 1 and not args.dense and not args.no_dense_phase:
+        bucket_elems = max(1, int(args.dense_bucket_mb * 1e6 / 4))
+        dtr, dopt, _, _ = build(args, amp, True, bucket_elems, P, rank)
+        dsteps = max(5, min(args.steps, 10))
+        d_el, d_exp, _ = run_phase(args, dtr, dopt, dsteps, max(3, min(args.warmup, 5)), P)
+        dms = d_el / dsteps * 1e3
+        out["dense_ms_per_step"] = round(dms, 3)
+        out["dense_value"] = round(P * args.batch_size * tok_per_sample * dsteps / d_el, 2)
+        out["dense_buckets"] = len(dopt.arena.buckets)
+        out["dense_exposed_comm_ms"] = round(d_exp, 3) if d_exp == d_exp else None
+        out["speedup_vs_dense"] = round(dms / ms, 4)
+        release(dtr, dopt)
+
+    # ---- secondary bf16 phase of an fp32 headline
+    if amp == "fp32" and not args.no_bf16_phase:
+        btr, bopt, _, _ = build(args, "bf16", args.dense, args.threshold, P, rank)
+        b_el, b_exp, _ = run_phase(args, btr, bopt, args.steps, args.warmup, P)
+        out["bf16_ms_per_step"] = round(b_el / args.steps * 1e3, 3)
+        out["bf16_value"] = round(P * args.batch_size * tok_per_sample * args.steps / b_el, 2)
+        out["bf16_exposed_comm_ms"] = round(b_exp, 3) if b_exp == b_exp else None
+        release(btr, bopt)
+
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
-    if opt._exchanger is not None:
-        opt._exchanger.close()
     comm.shutdown()
     if replicas is False:
         print("bench.py: replicas diverged", file=sys.stderr)

@@ -105,7 +105,7 @@ class _BNActFn(torch.autograd.Function):
         # needs our residual gradient before its consumer's grad-input runs
         ctx.link = link
         ctx.res_link = res_link
-        if link is not None and x.dtype == torch.bfloat16:
+        if link is not None:
             link.h, link.mask, link.twin = x, mask, bool(twin)
         return (y, y.view_as(y)) if twin else y
 
@@ -267,13 +267,12 @@ class BNAct(nn.BatchNorm2d):
                 mom = self.momentum     # the finalize kernel increments num_batches_tracked
             direct = getattr(self, "_gk_direct", None)
             if pool is not None:
-                pre = stats if (stats is not None and stats[0].shape[2] == x.shape[1] and
-                                x.dtype == torch.bfloat16) else None
+                pre = stats if (stats is not None and stats[0].shape[2] == x.shape[1]) else None
                 return _BNReLUPoolFn.apply(x, self.weight, self.bias, self.running_mean, self.running_var, mom,
                                            self.eps, pool, direct, nbt, self.twin, pre)
-            if stats is not None and (stats[0].shape[2] != x.shape[1] or x.dtype != torch.bfloat16):
+            if stats is not None and stats[0].shape[2] != x.shape[1]:
                 stats = None
-            link = BnLink() if self.bwd_link and torch.is_grad_enabled() and x.dtype == torch.bfloat16 else None
+            link = BnLink() if self.bwd_link and torch.is_grad_enabled() else None
             res_link = getattr(residual, "_gk_res_link", None) if residual is not None else None
             out = _BNActFn.apply(x, residual, self.weight, self.bias, self.running_mean, self.running_var, mom,
                                  self.eps, relu, direct, nbt, self.twin, stats, link, res_link)

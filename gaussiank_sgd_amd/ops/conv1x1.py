@@ -1,5 +1,10 @@
-"""Convolutions on channels-last bf16 activations through the MFMA GEMMs of
+"""Convolutions on channels-last activations through the MFMA GEMMs of
 ``csrc/kernels/gemm.hip``, autotuned per shape against MIOpen.
+
+Two compute precisions share the kernels: bf16 (under bf16 autocast,
+v_mfma_f32_16x16x32_bf16) and fp32 (fp32 inputs without autocast -- the
+reference's precision, settings.py:28 USE_FP16=False -- on
+v_mfma_f32_16x16x4_f32: exact fp32 products, fp32 accumulation).
 
 * 1x1, stride 1: a plain GEMM over the ``M = N*H*W`` pixel rows (forward
   ``Y = X W^T``, grad-input ``dX = dY W``, grad-weight ``dW += dY^T X``).
@@ -43,6 +48,19 @@ _NT_CFGS = [1, 2, 3, 4, 11, 13, 21, 22, 23, 24, 111, 113, 121, 122, 123, 124, 25
 # grid override: 0 = persistent (about two blocks per CU), else a fixed block count
 _NT_GRIDS = (0, 512, 1 << 20)
 _TN_CFGS = [(c, s) for c in (1, 2, 3, 4, 5, 6, 7, 8, 21, 22, 23, 24, 27, 9, 29, 101, 121, 102, 122) for s in (0, 128)]
+# fp32: 64x64 wave tiles only (gemm.hip maps NT tiles 5-7 onto them); TN cfg = tile + 10 * (1: two stages)
+_NT_CFGS_F32 = [1, 2, 3, 4, 7, 11, 12, 13, 14, 21, 22, 23, 24, 101, 102, 103, 104, 201, 202, 203, 204]
+_TN_CFGS_F32 = [(c, s) for c in (1, 2, 3, 4, 5, 6, 7, 8, 9, 11, 12, 13, 14, 15, 16) for s in (0, 64)]
+
+
+def _nt_cfgs(dt: torch.dtype) -> List[int]:
+    return _NT_CFGS_F32 if dt == torch.float32 else _NT_CFGS
+
+
+def _dkey(dt: torch.dtype) -> tuple:
+    """Autotune key suffix: fp32 keys are tagged, bf16 keys keep their
+    round-2 form so the shipped tuning cache stays valid."""
+    return ("f32",) if dt == torch.float32 else ()
 _zeros: Dict[torch.device, torch.Tensor] = {}
 
 
@@ -135,6 +153,7 @@ def tuned_choices() -> Dict[tuple, tuple]:
 
 
 def supported(x: torch.Tensor, conv: nn.Conv2d) -> bool:
+    """Shapes the HIP kernels take (either precision)."""
     k = conv.kernel_size
     return (_ENABLED and x.is_cuda and x.dim() == 4 and k[0] == k[1] and k[0] in (1, 3) and
             conv.stride[0] == conv.stride[1] and conv.stride[0] in (1, 2) and
@@ -164,7 +183,8 @@ def _fwd(x: torch.Tensor, w: torch.Tensor, s: int, stats_box=None, bias=None) ->
     (ops/bn.py BNAct(stats=...) consumes it and skips its statistics pass)."""
     N, C, H, W, K, k, p, OH, OW = _geom(x.shape, w, s)
     M = N * OH * OW
-    y = torch.empty((N, K, OH, OW), dtype=torch.bfloat16, device=x.device, memory_format=_CL)
+    dt = x.dtype
+    y = torch.empty((N, K, OH, OW), dtype=dt, device=x.device, memory_format=_CL)
     g = _g()
     st = None
     if stats_box is not None:
@@ -175,10 +195,10 @@ def _fwd(x: torch.Tensor, w: torch.Tensor, s: int, stats_box=None, bias=None) ->
     else:
         z = _zero(x.device)
         run = lambda c, mb: g.conv_nt(x, w, y, z, s, p, c, mb, st, bias)  # noqa: E731
-    b16 = bias.to(torch.bfloat16) if bias is not None else None
-    cands = [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in _NT_CFGS for mb in _NT_GRIDS]
+    b16 = bias.to(dt) if bias is not None else None
+    cands = [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in _nt_cfgs(dt) for mb in _NT_GRIDS]
     cands.append((("miopen", 0, 0), lambda: F.conv2d(x, w, b16, stride=s, padding=p)))
-    ch = _pick(("fwd", N, C, H, W, K, k, s, st is not None), cands)
+    ch = _pick(("fwd", N, C, H, W, K, k, s, st is not None) + _dkey(dt), cands)
     if ch[0] == "miopen":
         return F.conv2d(x, w, b16, stride=s, padding=p).contiguous(memory_format=_CL)
     rows = run(ch[1], ch[2])
@@ -190,8 +210,8 @@ def _fwd(x: torch.Tensor, w: torch.Tensor, s: int, stats_box=None, bias=None) ->
 def _dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int) -> torch.Tensor:
     N, C, H, W, K, k, p, OH, OW = _geom(x_shape, w, s)
     g = _g()
-
-    xs = torch.empty(x_shape, dtype=torch.bfloat16, device=dy.device, memory_format=_CL)   # shape only
+    dt = dy.dtype
+    xs = torch.empty(x_shape, dtype=dt, device=dy.device, memory_format=_CL)   # shape only
 
     def miopen():
         return torch.ops.aten.convolution_backward(dy, xs, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
@@ -203,7 +223,7 @@ def _dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int) -> torch.Tensor:
         dx = xs
         z = _zero(dy.device)
         run = lambda c, mb: g.conv_dgrad_s2(dy, w, dx, z, c, mb)  # noqa: E731
-        cands = [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in _NT_CFGS for mb in _NT_GRIDS]
+        cands = [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in _nt_cfgs(dt) for mb in _NT_GRIDS]
     if s == 1:
         dx = xs
         if k == 1:
@@ -215,9 +235,9 @@ def _dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int) -> torch.Tensor:
             wf = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=_CL)
             z = _zero(dy.device)
             run = lambda c, mb: g.conv_nt(dy, wf, dx, z, 1, p, c, mb)  # noqa: E731
-        cands = [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in _NT_CFGS for mb in _NT_GRIDS]
+        cands = [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in _nt_cfgs(dt) for mb in _NT_GRIDS]
     cands.append((("miopen", 0, 0), miopen))
-    ch = _pick(("dgrad", N, C, H, W, K, k, s), cands)
+    ch = _pick(("dgrad", N, C, H, W, K, k, s) + _dkey(dt), cands)
     if ch[0] == "miopen":
         return miopen().contiguous(memory_format=_CL)
     run(ch[1], ch[2])
@@ -232,7 +252,8 @@ def _dgrad_bn(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, link) -> torch
     N, C, H, W, K, k, p, OH, OW = _geom(x_shape, w, s)
     g = _g()
     M = N * H * W
-    dz = torch.empty(x_shape, dtype=torch.bfloat16, device=dy.device, memory_format=_CL)
+    dt = dy.dtype
+    dz = torch.empty(x_shape, dtype=dt, device=dy.device, memory_format=_CL)
     st = torch.empty(2, min(1280, (M + 63) // 64), C, dtype=torch.float32, device=dy.device)
     h, mask, dy2 = link.h, link.mask, link.dy2
     if k == 1:
@@ -246,8 +267,9 @@ def _dgrad_bn(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, link) -> torch
         z = _zero(dy.device)
         run = lambda c, mb: g.conv_nt(dy, wf, dz, z, 1, p, c, mb, st, None, h, dy2, mask)  # noqa: E731
     # 64x64-per-wave tiles (cfg digit 1-4) carry the BN-backward epilogue
-    cands = [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in _NT_CFGS if c % 10 <= 4 for mb in _NT_GRIDS]
-    ch = _pick(("dgrad_bn", N, C, H, W, K, k, s, dy2 is not None), cands)
+    cands = [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in _nt_cfgs(dt) if c % 10 <= 4
+             for mb in _NT_GRIDS]
+    ch = _pick(("dgrad_bn", N, C, H, W, K, k, s, dy2 is not None) + _dkey(dt), cands)
     rows = run(ch[1], ch[2])
     link.part = (st, int(rows))
     link.dz = dz
@@ -260,15 +282,22 @@ def _bn_fusable(link, s: int, dgrad_key: tuple) -> bool:
     (a MIOpen choice means the HIP GEMM is the slower one for this shape)."""
     if link is None or s != 1 or os.environ.get("GKSGD_BN_LINK", "1") == "0" or not link.ready():
         return False
+    if link.h.dtype != dgrad_key_dtype(dgrad_key):
+        return False
     ch = _choices.get(dgrad_key)
     return ch is None or ch[0] == "hip"
+
+
+def dgrad_key_dtype(key: tuple) -> torch.dtype:
+    return torch.float32 if key[-1] == "f32" else torch.bfloat16
 
 
 def _wgrad_into(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, s: int, out_f32: torch.Tensor) -> None:
     """out_f32 ([K, C, k, k] channels-last fp32) += dW."""
     N, C, H, W, K, k, p, OH, OW = _geom(x.shape, w, s)
     g = _g()
-    key = ("wgrad", N, C, H, W, K, k, s)
+    dt = x.dtype
+    key = ("wgrad", N, C, H, W, K, k, s) + _dkey(dt)
     scratch = torch.zeros_like(out_f32) if key not in _choices else None
 
     def miopen():
@@ -280,9 +309,10 @@ def _wgrad_into(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, s: int, out_
     else:
         z = _zero(x.device)
         run = lambda o, c, sp: g.conv_tn_acc(dy, x, o, z, s, p, c, sp)  # noqa: E731
-    cands = [(("hip", c, sp), (lambda c=c, sp=sp: run(scratch, c, sp))) for c, sp in _TN_CFGS]
+    cands = [(("hip", c, sp), (lambda c=c, sp=sp: run(scratch, c, sp)))
+             for c, sp in (_TN_CFGS_F32 if dt == torch.float32 else _TN_CFGS)]
     w3 = None
-    if k == 3 and s == 1 and g.wgrad3_supported(H, W, C, K):
+    if k == 3 and s == 1 and dt == torch.bfloat16 and g.wgrad3_supported(H, W, C, K):
         # tap-parallel kernel (wgrad3.hip): dY and X staged once per band for all 9 taps
         def w3(o):
             part = torch.empty(int(g.wgrad3_ws(N, H, W, C, K)), dtype=torch.float32, device=x.device)
@@ -301,16 +331,22 @@ def _wgrad_into(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, s: int, out_
 
 
 class _FastConvFn(torch.autograd.Function):
-    """y = conv(x, w_bf16).  ``param`` is the fp32 master weight; with a
-    ``sink`` (bf16-shadow path) its gradient is added into the optimizer's
-    fp32 arena in the backward and None is returned for it."""
+    """y = conv(x, w) in the compute dtype ``dt`` (bf16 or fp32).  ``param``
+    is the fp32 master weight; ``w_bf16`` its bf16-shadow view (bf16 path);
+    with a ``sink`` (the optimizer's gradient arena: bf16-shadow or fp32
+    direct-gradient path) the weight gradient is added into the arena in the
+    backward and None is returned for it."""
 
     @staticmethod
-    def forward(ctx, x, param, w_bf16, sink, stride, stats_box=None, bias=None, bias_sink=None, link=None):
-        if x.dtype != torch.bfloat16:
-            x = x.to(torch.bfloat16)
+    def forward(ctx, x, param, w_bf16, sink, stride, stats_box=None, bias=None, bias_sink=None, link=None,
+                dt=torch.bfloat16):
+        if x.dtype != dt:
+            x = x.to(dt)
         x = x.contiguous(memory_format=_CL)
-        w = w_bf16 if w_bf16 is not None else param.detach().to(torch.bfloat16)
+        if dt == torch.bfloat16:
+            w = w_bf16 if w_bf16 is not None else param.detach().to(torch.bfloat16)
+        else:
+            w = param.detach()
         w = w.contiguous(memory_format=_CL)
         b = bias.detach().float().contiguous() if bias is not None else None
         y = _fwd(x, w, stride, stats_box, b)
@@ -320,6 +356,7 @@ class _FastConvFn(torch.autograd.Function):
         ctx.stride = stride
         ctx.param_dtype = param.dtype
         ctx.link = link
+        ctx.dt = dt
         ctx.save_for_backward(x, w)
         return y
 
@@ -327,12 +364,12 @@ class _FastConvFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
         s = ctx.stride
-        dy = dy.to(torch.bfloat16).contiguous(memory_format=_CL)
+        dy = dy.to(ctx.dt).contiguous(memory_format=_CL)
         link, ctx.link = ctx.link, None
         dx = None
         if ctx.needs_input_grad[0]:
             N, C, H, W = x.shape
-            key = ("dgrad", N, C, H, W, w.shape[0], w.shape[2], s)
+            key = ("dgrad", N, C, H, W, w.shape[0], w.shape[2], s) + _dkey(ctx.dt)
             if _bn_fusable(link, s, key):
                 dx = _dgrad_bn(dy, w, x.shape, s, link)
             else:
@@ -359,13 +396,14 @@ class _FastConvFn(torch.autograd.Function):
                 bs(db)          # into the optimizer's fp32 arena (shadow path)
             else:
                 gbias = db
-        return dx, gparam, None, None, None, None, gbias, None, None
+        return dx, gparam, None, None, None, None, gbias, None, None, None
 
 
 class FastConv2d(nn.Conv2d):
-    """``nn.Conv2d`` whose bias-free 1x1 / 3x3 (stride 1 or 2, 'same'
-    padding) training path on a GPU runs the autotuned MFMA kernels (bf16
-    compute, as autocast); everything else is the stock convolution."""
+    """``nn.Conv2d`` whose 1x1 / 3x3 (stride 1 or 2, 'same' padding)
+    training path on a GPU runs the autotuned MFMA kernels: bf16 compute
+    under bf16 autocast, fp32 compute for fp32 inputs without autocast;
+    everything else is the stock convolution."""
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         return self._run(x, None)
@@ -379,21 +417,29 @@ class FastConv2d(nn.Conv2d):
 
     def _run(self, x: torch.Tensor, box):
         dev = x.device.type
-        bf16 = x.dtype == torch.bfloat16 or (torch.is_autocast_enabled(dev) and
-                                             torch.get_autocast_dtype(dev) == torch.bfloat16)
-        if bf16 and supported(x, self) and load():
-            table = getattr(self, "_gk_shadow", None)
-            info = table.get("weight") if table else None
-            binfo = table.get("bias") if table else None
-            use_shadow = info is not None and torch.is_autocast_enabled(dev)
-            w_bf16, sink = (info[0], info[1]) if use_shadow else (None, None)
-            bsink = binfo[1] if (use_shadow and binfo is not None) else None
+        autocast = torch.is_autocast_enabled(dev)
+        bf16 = x.dtype == torch.bfloat16 or (autocast and torch.get_autocast_dtype(dev) == torch.bfloat16)
+        f32 = not autocast and x.dtype == torch.float32 and self.weight.dtype == torch.float32 and \
+            os.environ.get("GKSGD_FASTCONV_F32", "1") != "0"
+        if (bf16 or f32) and supported(x, self) and load():
+            if bf16:
+                table = getattr(self, "_gk_shadow", None)
+                info = table.get("weight") if table else None
+                binfo = table.get("bias") if table else None
+                use_shadow = info is not None and autocast
+                w_bf16, sink = (info[0], info[1]) if use_shadow else (None, None)
+                bsink = binfo[1] if (use_shadow and binfo is not None) else None
+            else:
+                # fp32 direct-gradient path (parallel/shadow.py install_direct_grads)
+                table = getattr(self, "_gk_direct_grads", None) or {}
+                w_bf16, sink, bsink = None, table.get("weight"), table.get("bias")
             if not torch.is_grad_enabled() or not self.weight.requires_grad:
                 sink = None
             if not torch.is_grad_enabled() or self.bias is None or not self.bias.requires_grad:
                 bsink = None
             link = getattr(x, "_gk_bn_link", None)
-            return _FastConvFn.apply(x, self.weight, w_bf16, sink, self.stride[0], box, self.bias, bsink, link)
+            return _FastConvFn.apply(x, self.weight, w_bf16, sink, self.stride[0], box, self.bias, bsink, link,
+                                     torch.bfloat16 if bf16 else torch.float32)
         slow = getattr(self, "_gk_slow", None)
         return slow(x) if slow is not None else super().forward(x)
 

@@ -461,10 +461,12 @@ void bn_act_backward_pre(at::Tensor dz, at::Tensor x, at::Tensor dx, c10::option
   check_cl(dx, "dx");
   const int64_t C = channels_of(x);
   const int64_t M = x.numel() / C;
-  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && dz.scalar_type() == at::kBFloat16 &&
-                  dx.scalar_type() == at::kBFloat16 && dz.numel() == x.numel() && dx.numel() == x.numel(),
-              "bn_act_backward_pre: bf16 dz / x / dx of one shape");
-  TORCH_CHECK(gk::bn_supported((int)C, 2), "channel count not supported by the fused kernel");
+  TORCH_CHECK((x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat) &&
+                  dz.scalar_type() == x.scalar_type() && dx.scalar_type() == x.scalar_type() &&
+                  dz.numel() == x.numel() && dx.numel() == x.numel(),
+              "bn_act_backward_pre: dz / x / dx of one shape and dtype (bf16 or fp32)");
+  const int eb = (int)x.element_size();
+  TORCH_CHECK(gk::bn_supported((int)C, eb), "channel count not supported by the fused kernel");
   TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() == 3 &&
                   part.size(0) == 2 && part.size(2) == C && rows > 0 && rows <= part.size(1),
               "part must be fp32 [2, rows, C] partials with 0 < rows <= part.size(1)");
@@ -472,7 +474,7 @@ void bn_act_backward_pre(at::Tensor dz, at::Tensor x, at::Tensor dx, c10::option
     TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->numel() >= C, "per-channel buffers: fp32[C]");
   c10::DeviceGuard guard(x.device());
   const float* ps = part.data_ptr<float>();
-  gk::bn_act_backward_pre(dz.data_ptr(), x.data_ptr(), dx.data_ptr(), M, (int)C, opt_f32(w), mean.data_ptr<float>(),
+  gk::bn_act_backward_pre(dz.data_ptr(), x.data_ptr(), dx.data_ptr(), M, (int)C, eb, opt_f32(w), mean.data_ptr<float>(),
                           invstd.data_ptr<float>(), dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), ps,
                           ps + part.size(1) * C, (int)rows, opt_f32_mut(gw_acc), opt_f32_mut(gb_acc), cur_stream(x));
 }
@@ -723,9 +725,14 @@ struct RcclEngine : torch::CustomClassHolder {
 // ---------------------------------------------------------------------------
 bool gemm_supported(int64_t N, int64_t K) { return gk::gemm_supported(N, K); }
 
-void check_rows(const at::Tensor& t, const char* name) {
-  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 2, name, " must be a 2-D bf16 GPU tensor");
-  TORCH_CHECK(t.stride(1) == 1 && t.stride(0) % 8 == 0, name, " rows must be contiguous, 16-byte aligned");
+// GEMM operand: 2-D bf16 or fp32 rows (one dtype per call: `like`)
+bool is_gemm_dtype(const at::Tensor& t) { return t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kFloat; }
+
+void check_rows(const at::Tensor& t, const char* name, const at::Tensor& like) {
+  TORCH_CHECK(t.is_cuda() && is_gemm_dtype(t) && t.scalar_type() == like.scalar_type() && t.dim() == 2, name,
+              " must be a 2-D bf16 or fp32 GPU tensor (all operands one dtype)");
+  TORCH_CHECK(t.stride(1) == 1 && (t.stride(0) * t.element_size()) % 16 == 0, name,
+              " rows must be contiguous, 16-byte aligned");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
 }
 
@@ -816,26 +823,27 @@ const float* bias_ptr(const c10::optional<at::Tensor>& b, int64_t N) {
 // BatchNorm-backward epilogue operands (gemm.hip BnBwd): all-or-nothing on h
 bool bn_bwd_args(const c10::optional<at::Tensor>& h, const c10::optional<at::Tensor>& dy2,
                  const c10::optional<at::Tensor>& mask, int64_t M, int64_t N,
-                 int64_t ldc, bool has_stats, gk::BnBwdArgs* out) {
+                 int64_t ldc, bool has_stats, at::ScalarType dt, gk::BnBwdArgs* out) {
   if (!h.has_value() || !h->defined()) return false;
   TORCH_CHECK(has_stats, "BN-backward epilogue needs the stats partials buffer");
   auto rows_ok = [&](const at::Tensor& t, const char* what) {
-    TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.numel() == M * N &&
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == dt && t.numel() == M * N &&
                     (t.dim() == 2 ? t.stride(0) == ldc && t.stride(1) == 1
                                   : t.is_contiguous(at::MemoryFormat::ChannelsLast) && ldc == N),
-                what, " must be bf16 with C's shape and row stride");
+                what, " must have C's dtype, shape and row stride");
   };
   rows_ok(*h, "bn h");
-  out->h = static_cast<const uint16_t*>(h->data_ptr());
+  out->h = h->data_ptr();
   out->dy2 = nullptr;
   if (dy2.has_value() && dy2->defined()) {
     rows_ok(*dy2, "bn dy2");
-    out->dy2 = static_cast<const uint16_t*>(dy2->data_ptr());
+    out->dy2 = dy2->data_ptr();
   }
   out->mask = nullptr;
   if (mask.has_value() && mask->defined()) {
-    TORCH_CHECK(mask->is_cuda() && mask->scalar_type() == at::kByte && mask->numel() >= M * (N / 8),
-                "bn mask must hold M * N / 8 bytes");
+    const int64_t V = dt == at::kFloat ? 4 : 8;   // channels per mask byte (bn_act.hip)
+    TORCH_CHECK(mask->is_cuda() && mask->scalar_type() == at::kByte && mask->numel() >= M * (N / V),
+                "bn mask must hold M * N / V bytes");
     out->mask = mask->data_ptr<uint8_t>();
   }
   return true;
@@ -844,9 +852,9 @@ bool bn_bwd_args(const c10::optional<at::Tensor>& h, const c10::optional<at::Ten
 int64_t gemm_nt(at::Tensor A, at::Tensor B, at::Tensor C, int64_t cfg, int64_t max_blocks,
                 c10::optional<at::Tensor> stats, c10::optional<at::Tensor> bias, c10::optional<at::Tensor> bn_h,
                 c10::optional<at::Tensor> bn_dy2, c10::optional<at::Tensor> bn_mask) {
-  check_rows(A, "A");
-  check_rows(B, "B");
-  check_rows(C, "C");
+  check_rows(A, "A", A);
+  check_rows(B, "B", A);
+  check_rows(C, "C", A);
   const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
   TORCH_CHECK(B.size(1) == K && C.size(0) == M && C.size(1) == N, "gemm_nt: shape mismatch");
   TORCH_CHECK(gk::gemm_supported(N, K), "gemm_nt: N and K must be multiples of 64");
@@ -854,18 +862,18 @@ int64_t gemm_nt(at::Tensor A, at::Tensor B, at::Tensor C, int64_t cfg, int64_t m
   int rows = 0;
   float* sp = stats_ptr(stats, N, &rows);
   gk::BnBwdArgs bn{};
-  const bool has_bn = bn_bwd_args(bn_h, bn_dy2, bn_mask, M, N, C.stride(0), sp != nullptr, &bn);
+  const bool has_bn = bn_bwd_args(bn_h, bn_dy2, bn_mask, M, N, C.stride(0), sp != nullptr, C.scalar_type(), &bn);
   TORCH_CHECK(!has_bn || !bias.has_value() || !bias->defined(), "gemm_nt: bias and BN epilogue are exclusive");
   c10::DeviceGuard guard(A.device());
-  return gk::gemm_nt_bf16(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), M, (int)N,
-                          (int)K, (int)cfg, (int)max_blocks, sp, rows, bias_ptr(bias, N), has_bn ? &bn : nullptr,
-                          cur_stream(A));
+  return gk::gemm_nt(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), M, (int)N,
+                     (int)K, A.scalar_type() == at::kFloat, (int)cfg, (int)max_blocks, sp, rows, bias_ptr(bias, N),
+                     has_bn ? &bn : nullptr, cur_stream(A));
 }
 
 // W[N, K] += G[M, N]^T . X[M, K]   (fp32 W, float atomics)
 void gemm_tn_acc(at::Tensor G, at::Tensor X, at::Tensor W, int64_t cfg, int64_t splits) {
-  check_rows(G, "G");
-  check_rows(X, "X");
+  check_rows(G, "G", G);
+  check_rows(X, "X", G);
   TORCH_CHECK(W.is_cuda() && W.scalar_type() == at::kFloat && W.dim() == 2 && W.stride(1) == 1,
               "W must be a 2-D fp32 GPU tensor with contiguous rows");
   const int64_t M = G.size(0), N = G.size(1), K = X.size(1);
@@ -873,22 +881,26 @@ void gemm_tn_acc(at::Tensor G, at::Tensor X, at::Tensor W, int64_t cfg, int64_t 
   TORCH_CHECK(gk::gemm_supported(N, K), "gemm_tn_acc: N and K must be multiples of 64");
   if (M == 0) return;
   c10::DeviceGuard guard(G.device());
-  gk::gemm_tn_acc_f32(G.data_ptr(), G.stride(0), X.data_ptr(), X.stride(0), W.data_ptr<float>(), W.stride(0), M,
-                      (int)N, (int)K, (int)cfg, (int)splits, cur_stream(G));
+  gk::gemm_tn_acc(G.data_ptr(), G.stride(0), X.data_ptr(), X.stride(0), W.data_ptr<float>(), W.stride(0), M, (int)N,
+                  (int)K, G.scalar_type() == at::kFloat, (int)cfg, (int)splits, cur_stream(G));
 }
 
 // implicit-GEMM convolution over NHWC bf16 (x: [N, C, H, W] channels-last,
 // w: [Cout, C, KH, KW] channels-last, y: [N, Cout, OH, OW] channels-last)
+// the padding row: >= 128 zero bytes (one K slice of either dtype)
+void check_zero(const at::Tensor& zero) {
+  TORCH_CHECK(zero.is_cuda() && zero.is_contiguous() && zero.numel() * zero.element_size() >= 128,
+              "zero must hold >= 128 zero bytes");
+}
+
 void check_conv(const at::Tensor& x, const at::Tensor& w, const at::Tensor& zero) {
-  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
-                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
-              "conv: x must be a channels-last bf16 GPU tensor");
-  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 &&
+  TORCH_CHECK(x.is_cuda() && is_gemm_dtype(x) && x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv: x must be a channels-last bf16 or fp32 GPU tensor");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == x.scalar_type() && w.dim() == 4 &&
                   w.is_contiguous(at::MemoryFormat::ChannelsLast) && w.size(1) == x.size(1),
-              "conv: w must be a channels-last bf16 [Cout, C, KH, KW] GPU tensor");
+              "conv: w must be a channels-last [Cout, C, KH, KW] GPU tensor of x's dtype");
   TORCH_CHECK(x.size(1) % 64 == 0 && w.size(0) % 64 == 0, "conv: C and Cout must be multiples of 64");
-  TORCH_CHECK(zero.is_cuda() && zero.scalar_type() == at::kBFloat16 && zero.numel() >= 64 && zero.is_contiguous(),
-              "conv: zero must hold >= 64 bf16");
+  check_zero(zero);
 }
 
 int64_t conv_nt(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor zero, int64_t stride, int64_t pad, int64_t cfg,
@@ -899,21 +911,21 @@ int64_t conv_nt(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor zero, int64
   const int64_t Co = w.size(0), KH = w.size(2), KW = w.size(3);
   const int64_t OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
   TORCH_CHECK(KH <= 4 && KW <= 4, "conv_nt: kernels up to 4x4 (gemm.hip kMaxTaps)");
-  TORCH_CHECK(y.is_cuda() && y.scalar_type() == at::kBFloat16 && y.dim() == 4 &&
+  TORCH_CHECK(y.is_cuda() && y.scalar_type() == x.scalar_type() && y.dim() == 4 &&
                   y.is_contiguous(at::MemoryFormat::ChannelsLast) && y.size(0) == N && y.size(1) == Co &&
                   y.size(2) == OH && y.size(3) == OW,
-              "conv_nt: y must be channels-last bf16 [N, Cout, OH, OW]");
+              "conv_nt: y must be channels-last [N, Cout, OH, OW] of x's dtype");
   const int64_t M = N * OH * OW;
   TORCH_CHECK(M > 0 && M < (int64_t(1) << 32), "conv_nt: M out of range");
   int rows = 0;
   float* sp = stats_ptr(stats, Co, &rows);
   gk::BnBwdArgs bn{};
-  const bool has_bn = bn_bwd_args(bn_h, bn_dy2, bn_mask, M, Co, Co, sp != nullptr, &bn);
+  const bool has_bn = bn_bwd_args(bn_h, bn_dy2, bn_mask, M, Co, Co, sp != nullptr, y.scalar_type(), &bn);
   TORCH_CHECK(!has_bn || !bias.has_value() || !bias->defined(), "conv_nt: bias and BN epilogue are exclusive");
   c10::DeviceGuard guard(x.device());
-  return gk::conv_nt_bf16(x.data_ptr(), zero.data_ptr(), (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)stride,
-                          (int)pad, (int)KH, (int)KW, w.data_ptr(), y.data_ptr(), M, (int)Co, (int)cfg, (int)max_blocks,
-                          sp, rows, bias_ptr(bias, Co), has_bn ? &bn : nullptr, cur_stream(x));
+  return gk::conv_nt(x.data_ptr(), zero.data_ptr(), (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)stride, (int)pad,
+                     (int)KH, (int)KW, w.data_ptr(), y.data_ptr(), M, (int)Co, x.scalar_type() == at::kFloat, (int)cfg,
+                     (int)max_blocks, sp, rows, bias_ptr(bias, Co), has_bn ? &bn : nullptr, cur_stream(x));
 }
 
 // grad-input of a stride-2 convolution (1x1 / pad 0 or 3x3 / pad 1) through the
@@ -924,29 +936,29 @@ int64_t conv_nt(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor zero, int64
 // dy: [N, K, OH, OW] channels-last bf16; w: [K, C, k, k] channels-last bf16;
 // dx: [N, C, H, W] channels-last bf16 (every pixel written).
 void conv_dgrad_s2(at::Tensor dy, at::Tensor w, at::Tensor dx, at::Tensor zero, int64_t cfg, int64_t max_blocks) {
-  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 &&
-                  dy.is_contiguous(at::MemoryFormat::ChannelsLast),
-              "conv_dgrad_s2: dy must be channels-last bf16");
-  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(0) == dy.size(1) &&
+  TORCH_CHECK(dy.is_cuda() && is_gemm_dtype(dy) && dy.dim() == 4 && dy.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv_dgrad_s2: dy must be channels-last bf16 or fp32");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == dy.scalar_type() && w.dim() == 4 && w.size(0) == dy.size(1) &&
                   w.size(2) == w.size(3) && (w.size(2) == 1 || w.size(2) == 3),
-              "conv_dgrad_s2: w must be bf16 [K, C, k, k], k in {1, 3}");
-  TORCH_CHECK(dx.is_cuda() && dx.scalar_type() == at::kBFloat16 && dx.dim() == 4 && dx.size(0) == dy.size(0) &&
+              "conv_dgrad_s2: w must be [K, C, k, k] of dy's dtype, k in {1, 3}");
+  TORCH_CHECK(dx.is_cuda() && dx.scalar_type() == dy.scalar_type() && dx.dim() == 4 && dx.size(0) == dy.size(0) &&
                   dx.size(1) == w.size(1) && dx.is_contiguous(at::MemoryFormat::ChannelsLast),
-              "conv_dgrad_s2: dx must be channels-last bf16 [N, C, H, W]");
+              "conv_dgrad_s2: dx must be channels-last [N, C, H, W] of dy's dtype");
+  const bool f32 = dy.scalar_type() == at::kFloat;
   const int64_t N = dy.size(0), K = dy.size(1), OHd = dy.size(2), OWd = dy.size(3);
   const int64_t C = w.size(1), k = w.size(2), H = dx.size(2), W = dx.size(3);
   const int64_t p = k / 2;
   TORCH_CHECK((H + 2 * p - k) / 2 + 1 == OHd && (W + 2 * p - k) / 2 + 1 == OWd, "conv_dgrad_s2: shape mismatch");
   TORCH_CHECK(K % 64 == 0 && C % 64 == 0, "conv_dgrad_s2: channels must be multiples of 64");
-  TORCH_CHECK(zero.is_cuda() && zero.scalar_type() == at::kBFloat16 && zero.numel() >= 64, "zero: >= 64 bf16");
+  check_zero(zero);
   TORCH_CHECK(N * H * W < (int64_t(1) << 31), "conv_dgrad_s2: too many pixels");
   c10::DeviceGuard guard(dy.device());
   const hipStream_t st = cur_stream(dy);
   if (k == 1) {   // one class (even, even), zeros elsewhere; B = W^T [C][K]
     const at::Tensor wt = w.reshape({K, C}).t().contiguous();
-    gk::conv_nt_remap_bf16(dy.data_ptr(), K, zero.data_ptr(), (int)OHd, (int)OWd, (int)K, (int)OHd, (int)OWd, 1, 1,
-                           wt.data_ptr(), dx.data_ptr(), N * OHd * OWd, (int)C, (int)H, (int)W, 0, 0, 1, (int)cfg,
-                           (int)max_blocks, st);
+    gk::conv_nt_remap(dy.data_ptr(), K, zero.data_ptr(), (int)OHd, (int)OWd, (int)K, (int)OHd, (int)OWd, 1, 1,
+                      wt.data_ptr(), dx.data_ptr(), N * OHd * OWd, (int)C, (int)H, (int)W, 0, 0, 1, f32, (int)cfg,
+                      (int)max_blocks, st);
     return;
   }
   // [C][kh][kw][K] = W[K][C][kh][kw]
@@ -960,9 +972,9 @@ void conv_dgrad_s2(at::Tensor dy, at::Tensor w, at::Tensor dx, at::Tensor zero, 
       at::Tensor wc = a == 0 ? wt.slice(1, 1, 2) : wt.slice(1, 0, 3, 2).flip({1});
       wc = b == 0 ? wc.slice(2, 1, 2) : wc.slice(2, 0, 3, 2).flip({2});
       wc = wc.contiguous();
-      gk::conv_nt_remap_bf16(dy.data_ptr(), K, zero.data_ptr(), (int)OHd, (int)OWd, (int)K, (int)OHc, (int)OWc,
-                             a == 0 ? 1 : 2, b == 0 ? 1 : 2, wc.data_ptr(), dx.data_ptr(), N * OHc * OWc, (int)C,
-                             (int)H, (int)W, a, b, 0, (int)cfg, (int)max_blocks, st);
+      gk::conv_nt_remap(dy.data_ptr(), K, zero.data_ptr(), (int)OHd, (int)OWd, (int)K, (int)OHc, (int)OWc,
+                        a == 0 ? 1 : 2, b == 0 ? 1 : 2, wc.data_ptr(), dx.data_ptr(), N * OHc * OWc, (int)C, (int)H,
+                        (int)W, a, b, 0, f32, (int)cfg, (int)max_blocks, st);
     }
   }
 }
@@ -1004,23 +1016,23 @@ void conv_tn_acc(at::Tensor dy, at::Tensor x, at::Tensor wout, at::Tensor zero, 
               "conv_tn_acc: wout must be a channels-last fp32 [Cout, C, KH, KW] tensor");
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
   const int64_t Co = wout.size(0), KH = wout.size(2), KW = wout.size(3);
-  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous(at::MemoryFormat::ChannelsLast) &&
-                  C % 64 == 0 && Co % 64 == 0,
-              "conv_tn_acc: x must be channels-last bf16 with C, Cout % 64 == 0");
-  TORCH_CHECK(zero.is_cuda() && zero.scalar_type() == at::kBFloat16 && zero.numel() >= 64, "conv_tn_acc: zero");
+  TORCH_CHECK(x.is_cuda() && is_gemm_dtype(x) && x.is_contiguous(at::MemoryFormat::ChannelsLast) && C % 64 == 0 &&
+                  Co % 64 == 0,
+              "conv_tn_acc: x must be channels-last bf16 or fp32 with C, Cout % 64 == 0");
+  check_zero(zero);
   TORCH_CHECK(x.numel() < (int64_t(1) << 31), "conv_tn_acc: x too large for 32-bit gather offsets");
   const int64_t OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
-  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 &&
+  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == x.scalar_type() && dy.dim() == 4 &&
                   dy.is_contiguous(at::MemoryFormat::ChannelsLast) && dy.size(0) == N && dy.size(1) == Co &&
                   dy.size(2) == OH && dy.size(3) == OW,
-              "conv_tn_acc: dy must be channels-last bf16 [N, Cout, OH, OW]");
+              "conv_tn_acc: dy must be channels-last [N, Cout, OH, OW] of x's dtype");
   const int64_t M = N * OH * OW;
   TORCH_CHECK(M < (int64_t(1) << 32), "conv_tn_acc: M out of range");
   if (M == 0) return;
   c10::DeviceGuard guard(x.device());
-  gk::conv_tn_acc_f32(dy.data_ptr(), x.data_ptr(), zero.data_ptr(), (int)H, (int)W, (int)C, (int)OH, (int)OW,
-                      (int)stride, (int)pad, (int)KH, (int)KW, wout.data_ptr<float>(), M, (int)Co, (int)cfg,
-                      (int)splits, cur_stream(x));
+  gk::conv_tn_acc(dy.data_ptr(), x.data_ptr(), zero.data_ptr(), (int)H, (int)W, (int)C, (int)OH, (int)OW,
+                  (int)stride, (int)pad, (int)KH, (int)KW, wout.data_ptr<float>(), M, (int)Co,
+                  x.scalar_type() == at::kFloat, (int)cfg, (int)splits, cur_stream(x));
 }
 
 // fused residual add (+ dropout) + LayerNorm (ln.hip)

@@ -945,16 +945,25 @@ void bn_act_backward(const void* dy, const void* dy2, const uint8_t* mask, const
 // dz (already gated and twin-summed) and its partials sum(dz), sum(dz*(x-mean))
 // [2][gy][C] from the consuming convolution's grad-input epilogue (gemm.hip
 // BnBwd): no reduction pass, only finalize + apply.
-void bn_act_backward_pre(const void* dz, const void* x, void* dx, int64_t M, int C, const float* w,
-                         const float* mean, const float* invstd, float* dgamma, float* dbeta, const float* pdb,
-                         const float* pdg, int gy, float* gw_acc, float* gb_acc, hipStream_t s) {
-  using T = uint16_t;
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(kBlock), 0, s, pdb, pdg, gy, C,
-                     dbeta, dgamma, gb_acc, gw_acc, mean, invstd);
+template <typename T>
+void bn_bwd_apply_pre_t(const T* dz, const T* x, T* dx, int64_t M, int C, const float* w, const float* mean,
+                        const float* invstd, float* dgamma, float* dbeta, hipStream_t s) {
   const Geo g = make_geo<T>(M, C, kTargetBlocks);
   hipLaunchKernelGGL((bn_bwd_apply_kernel<T, DyPlain<T, false, false>, false>), dim3(g.gx, g.gy), dim3(kBlock), 0, s,
-                     DyPlain<T, false, false>{(const T*)dz, nullptr, nullptr}, (const T*)x, (T*)dx, (T*)nullptr, M, C,
-                     g, w, mean, invstd, dbeta, dgamma);
+                     DyPlain<T, false, false>{dz, nullptr, nullptr}, x, dx, (T*)nullptr, M, C, g, w, mean, invstd,
+                     dbeta, dgamma);
+}
+
+void bn_act_backward_pre(const void* dz, const void* x, void* dx, int64_t M, int C, int elem_bytes, const float* w,
+                         const float* mean, const float* invstd, float* dgamma, float* dbeta, const float* pdb,
+                         const float* pdg, int gy, float* gw_acc, float* gb_acc, hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(kBlock), 0, s, pdb, pdg, gy, C,
+                     dbeta, dgamma, gb_acc, gw_acc, mean, invstd);
+  if (elem_bytes == 2)
+    bn_bwd_apply_pre_t<uint16_t>((const uint16_t*)dz, (const uint16_t*)x, (uint16_t*)dx, M, C, w, mean, invstd, dgamma,
+                                 dbeta, s);
+  else
+    bn_bwd_apply_pre_t<float>((const float*)dz, (const float*)x, (float*)dx, M, C, w, mean, invstd, dgamma, dbeta, s);
 }
 
 // ---------------------------------------------------------------------------

@@ -76,7 +76,7 @@ __device__ __forceinline__ void wait_vmcnt_fast(int n) {
 constexpr int kMaxTaps = 4;   // gemm_nt gather: at most 4 taps per kernel dimension
 
 struct ConvGeo {
-  const uint16_t* zero;   // >= 64 zero bf16
+  const void* zero;       // >= 128 zero bytes (one K slice row of either element type)
   int H, W, C, OH, OW, S, P, KW;
   const float* bias;      // optional per-output-channel bias (gemm_nt / conv_nt epilogue)
   // gemm_nt output row remap (stride-2 grad-input parity classes): RH > 0 stores
@@ -95,23 +95,11 @@ struct ConvGeo {
 // The operands are loaded per output row in the epilogue (transient registers:
 // the main loop's register budget is unchanged).
 struct BnBwd {
-  const uint16_t* h;      // BN input [M, N] (same ld as C); nullptr: plain epilogue
-  const uint16_t* dy2;    // optional second gradient [M, N]
-  const uint8_t* mask;    // optional 1-bit ReLU mask, byte (m, n / 8) at m * (N / 8) + n / 8
+  const void* h;          // BN input [M, N] (same ld and element type as C); nullptr: plain epilogue
+  const void* dy2;        // optional second gradient [M, N]
+  const uint8_t* mask;    // optional 1-bit ReLU mask, one byte per 16-byte vector: (m, n / V) at
+                          // m * (N / V) + n / V, V = 8 (bf16) or 4 (fp32) -- bn_act.hip's layout
 };
-
-__device__ __forceinline__ const uint16_t* conv_row(const uint16_t* X, const ConvGeo& g, int64_t m, int k0,
-                                                    int chunk) {
-  const int tap = k0 / g.C, c0 = k0 - tap * g.C;
-  const int kh = tap / g.KW, kw = tap - kh * g.KW;
-  const uint32_t ohw = (uint32_t)(g.OH * g.OW);
-  const uint32_t mu = (uint32_t)m;
-  const uint32_t n = mu / ohw, rem = mu - n * ohw;
-  const uint32_t oh = rem / (uint32_t)g.OW, ow = rem - oh * (uint32_t)g.OW;
-  const int ih = (int)oh * g.S - g.P + kh, iw = (int)ow * g.S - g.P + kw;
-  if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W) return g.zero + chunk * 8;
-  return X + (((int64_t)n * g.H + ih) * g.W + iw) * g.C + c0 + chunk * 8;
-}
 
 // --------------------------------------------------------------------------
 // gemm_nt
@@ -121,15 +109,29 @@ __device__ __forceinline__ const uint16_t* conv_row(const uint16_t* X, const Con
 // NS: LDS stages; NS = 3 keeps two K slices in flight behind the one being
 // multiplied.
 // MSB: 16-row MFMA subtiles per wave along M (4: 64x64 wave tile, 8: 128x64 --
-// fewer LDS reads per MFMA for the compute-bound shapes).
-template <int WM, int WN, bool BRES, int MSB = 4>
+// fewer LDS reads per MFMA for the compute-bound shapes; bf16 only).
+// T: element type, uint16_t (bf16 bits) or float.  A K slice is always one
+// 128-byte LDS row per staged row -- 64 bf16 or 32 fp32 -- so staging,
+// swizzle and fragment addressing are shared; a 16-byte fragment feeds one
+// v_mfma_f32_16x16x32_bf16 (bf16) or four v_mfma_f32_16x16x4_f32 (fp32, exact
+// fp32 products and sums: the reference's precision, no bf16 splitting).
+template <typename T>
+struct Elem {
+  static constexpr bool F32 = sizeof(T) == 4;
+  static constexpr int EPC = 16 / (int)sizeof(T);   // elements per 16-byte chunk
+  static constexpr int KS = 8 * EPC;                // K elements per 128-byte slice row
+  // 16-byte epilogue stores per 16-row subtile per wave (64 output columns)
+  static constexpr int ST_PER_SUB = F32 ? 4 : 2;
+};
+
+template <int WM, int WN, bool BRES, int MSB = 4, typename T = uint16_t>
 struct NtCfg {
   static constexpr int NW = WM * WN;
   static constexpr int THREADS = 64 * NW;
   static constexpr int WTM = 16 * MSB;            // wave tile rows
   static constexpr int BM = WTM * WM;
   static constexpr int BN = 64 * WN;
-  static constexpr int ASTAGE = BM * 128;         // bytes: BM rows x 64 bf16
+  static constexpr int ASTAGE = BM * 128;         // bytes: BM rows x one K slice
   static constexpr int BSTAGE = BN * 128;
   static constexpr int STAGE = BRES ? ASTAGE : ASTAGE + BSTAGE;
   static constexpr int INSTS = STAGE / 1024;      // 1-KiB LDS-DMA instructions per stage
@@ -137,25 +139,29 @@ struct NtCfg {
   static constexpr int LPW = INSTS / NW;          // LDS-DMA instructions per wave per stage
   static_assert((BM / 8) % NW == 0, "A rows split evenly over the waves");
   static constexpr int LPWA = BRES ? LPW : (BM / 8) / NW;   // of which A-row instructions (j < LPWA)
-  static constexpr int NST = 2 * MSB;             // 16-byte epilogue stores per wave per tile
+  static constexpr int NST = Elem<T>::ST_PER_SUB * MSB;     // 16-byte epilogue stores per wave per tile
   static_assert(LPW + 2 * NST <= 63, "wait_vmcnt range (vmcnt is 6 bits)");
   static constexpr bool NS4_OK = 2 * LPW + 3 * NST <= 63;   // four stages: 2 stages + 3 tiles of stores in flight
-  static int lds_bytes(int K, int ns) { return ns * STAGE + (BRES ? BN * K * 2 : 0); }
+  static int lds_bytes(int K, int ns) { return ns * STAGE + (BRES ? BN * K * (int)sizeof(T) : 0); }
 };
 
-template <int WM, int WN, bool BRES, int NS, bool GATHER, int MSB = 4, bool BNB = false>
+template <int WM, int WN, bool BRES, int NS, bool GATHER, int MSB = 4, bool BNB = false, typename T = uint16_t>
 __global__ void __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(WM * WN >= 8 ? 1 : 2)))
-gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
-               uint16_t* __restrict__ C, int64_t ldc, int64_t M, int K, ConvGeo geo, float* __restrict__ stats,
+gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
+               T* __restrict__ C, int64_t ldc, int64_t M, int K, ConvGeo geo, float* __restrict__ stats,
                int64_t stats_ld, BnBwd bb) {
-  // stats != nullptr: per-block BatchNorm partials of the (bf16-rounded)
+  // stats != nullptr: per-block BatchNorm partials of the (dtype-rounded)
   // output, psum at stats[blockIdx.x * N + n], psq at stats[stats_ld + ...]
   // (the [gy][C] layout bn_finalize_kernel reduces).  With bb.h (BN-backward
   // epilogue, MSB == 4 tiles only) the partials are sum(dz), sum(dz*h); the
   // finalize centres the second with the mean.
-  using Cfg = NtCfg<WM, WN, BRES, MSB>;
+  using Cfg = NtCfg<WM, WN, BRES, MSB, T>;
+  using E = Elem<T>;
+  constexpr bool F32 = E::F32;
+  constexpr int EPC = E::EPC;
+  constexpr int KS = E::KS;
   static_assert(!BNB || MSB == 4, "BN-backward epilogue: 64x64 wave tiles");
-  constexpr bool BNB_OK = BNB;
+  static_assert(!F32 || MSB == 4, "fp32: 64x64 wave tiles");
   constexpr bool bnb = BNB;
   static_assert(NS >= 2 && NS <= 4, "stages");
   constexpr int LPW = Cfg::LPW;
@@ -165,12 +171,12 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
   const int wm = wave / WN, wn = wave % WN;
   const int n0 = blockIdx.y * Cfg::BN;
   const int64_t mtiles = (M + Cfg::BM - 1) / Cfg::BM;
-  const int nk = K >> 6;
+  const int nk = K / KS;
   // this block's work: M tiles blockIdx.x, +gridDim.x, ...; each has nk K slices
   const int64_t my_tiles = blockIdx.x < mtiles ? (mtiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
-  const int T = (int)(my_tiles * nk);
+  const int T_ = (int)(my_tiles * nk);
   const int Ntot = gridDim.y * Cfg::BN;
-  if (T == 0) {
+  if (T_ == 0) {
     if (stats)
       for (int c = threadIdx.x; c < Cfg::BN; c += Cfg::THREADS) {
         stats[(int64_t)blockIdx.x * Ntot + n0 + c] = 0.f;
@@ -178,7 +184,7 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
       }
     return;
   }
-  char* stage_base = smem + (BRES ? Cfg::BN * K * 2 : 0);
+  char* stage_base = smem + (BRES ? Cfg::BN * K * (int)sizeof(T) : 0);
 
   if (BRES) {  // weight panel: slice ks at smem + ks*BSTAGE, rows swizzled as the streamed tiles
     const int per = Cfg::BN / 8;
@@ -186,7 +192,7 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
       const int ks = i / per, ri = i % per;
       const int r = ri * 8 + (lane >> 3);
       const int c = (lane & 7) ^ swz(r);
-      glds16(B + (int64_t)(n0 + r) * ldb + ks * 64 + c * 8, (GK_LDS char*)smem + ks * Cfg::BSTAGE + ri * 1024);
+      glds16(B + (int64_t)(n0 + r) * ldb + ks * KS + c * EPC, (GK_LDS char*)smem + ks * Cfg::BSTAGE + ri * 1024);
     }
   }
 
@@ -194,20 +200,20 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
   // rows) or once per kernel (B rows); a K step only adds the slice offset.
   // Instruction j of this wave fills staged rows i*8 .. i*8+7, i = wave + j*NW:
   // A rows while i*8 < BM, B rows after (streamed panel only).
-  const uint16_t* ptr[LPW];   // A: row (or gathered pixel) base + chunk; B: row base + chunk
+  const T* ptr[LPW];          // A: row (or gathered pixel) base + chunk; B: row base + chunk
   // gather: bit kh of okh / bit kw of okw set when tap row kh / column kw of
   // this lane's output pixel lies inside the image (set once per M tile; a K
   // step tests two bits instead of recomputing and comparing the position)
   uint32_t okh[LPW], okw[LPW];
-  const uint16_t* zrow[LPW];  // gather: this lane's chunk of the zero row (padding taps)
+  const T* zrow[LPW];         // gather: this lane's chunk of the zero row (padding taps)
 #pragma unroll
   for (int j = 0; j < LPW; ++j) {
     const int i = wave + j * Cfg::NW;
     const int r = i * 8 + (lane >> 3);
     const int c = (lane & 7) ^ swz(r);
-    ptr[j] = j < Cfg::LPWA ? nullptr : B + (int64_t)(n0 + r - Cfg::BM) * ldb + c * 8;
+    ptr[j] = j < Cfg::LPWA ? nullptr : B + (int64_t)(n0 + r - Cfg::BM) * ldb + c * EPC;
     okh[j] = okw[j] = 0u;
-    zrow[j] = GATHER ? geo.zero + c * 8 : nullptr;
+    zrow[j] = GATHER ? static_cast<const T*>(geo.zero) + c * EPC : nullptr;
   }
   auto set_rows = [&](int64_t mt) {
     const int64_t m0 = mt * Cfg::BM;
@@ -234,9 +240,9 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
           }
           okh[j] = bh;
           okw[j] = bw;
-          ptr[j] = A + (((int64_t)n * geo.H + ih0) * geo.W + iw0) * geo.C + c * 8;
+          ptr[j] = A + (((int64_t)n * geo.H + ih0) * geo.W + iw0) * geo.C + c * EPC;
         } else {
-          ptr[j] = A + gr * lda + c * 8;
+          ptr[j] = A + gr * lda + c * EPC;
         }
       }
     }
@@ -249,12 +255,12 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
   set_rows(s_mt);
   auto stage = [&]() {
     GK_LDS char* base = (GK_LDS char*)stage_base + s_buf * Cfg::STAGE;
-    const int k0 = s_ks << 6;
+    const int k0 = s_ks * KS;
     const int64_t toff = GATHER ? (int64_t)(s_kh * geo.W + s_kw) * geo.C + s_c0 : 0;   // wave-uniform
 #pragma unroll
     for (int j = 0; j < LPW; ++j) {
       const int i = wave + j * Cfg::NW;
-      const uint16_t* src;
+      const T* src;
       if (j < Cfg::LPWA) {
         if (GATHER) {
           const bool ok = ((okh[j] >> s_kh) & (okw[j] >> s_kw) & 1u) != 0u;
@@ -270,7 +276,7 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
     ++s_t;
     s_buf = s_buf + 1 == NS ? 0 : s_buf + 1;
     if (GATHER) {
-      s_c0 += 64;
+      s_c0 += KS;
       if (s_c0 == geo.C) {
         s_c0 = 0;
         if (++s_kw == geo.KW) { s_kw = 0; ++s_kh; }
@@ -280,7 +286,7 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
       s_ks = 0;
       s_kh = s_kw = s_c0 = 0;
       s_mt += gridDim.x;
-      if (s_t < T) set_rows(s_mt);
+      if (s_t < T_) set_rows(s_mt);
     }
   };
 
@@ -291,8 +297,8 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
     for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   stage();
-  if (NS >= 3 && T > 1) stage();
-  if (NS == 4 && T > 2) stage();
+  if (NS >= 3 && T_ > 1) stage();
+  if (NS == 4 && T_ > 2) stage();
   const int fr = lane & 15, fq = lane >> 4;
   // stores issued by the last two steps (0 when none, or when a partial tile
   // drained its stores with vmcnt(0) right away)
@@ -308,52 +314,74 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
       ssum[a][b] = ssq[a][b] = 0.f;
       bia[a][b] = geo.bias ? geo.bias[n0 + wn * 64 + a * 16 + fq * 4 + b] : 0.f;
     }
-  // BN-backward epilogue: in the store layout every lane owns 8 consecutive
+  // bf16 BN-backward epilogue: in the store layout every lane owns 8 consecutive
   // channels per column pair pr (the same channels for every tile): offset
   // cofs within the pair's 32 columns
   const int cofs = (fq & 1) ? 16 + 4 * (fq - 1) : 4 * fq;
   int64_t mt = blockIdx.x;
-  for (int t = 0; t < T; ++t) {
+  for (int t = 0; t < T_; ++t) {
     // ops issued after stage(t), in order: NS=2: stores(t-1);
     // NS=3: stores(t-2), stage(t+1), stores(t-1).  Retire stage(t) only.
     // after stage(t): stores(t-NS+1..t-1) and the stages t+1 .. t+NS-2 issued since
     if (NS == 2) wait_vmcnt_fast<0>(st1);
-    else if (NS == 3) wait_vmcnt_fast<LPW>(st2 + (t + 1 < T ? LPW : 0) + st1);
-    else wait_vmcnt_fast<2 * LPW>(st3 + st2 + st1 + ((t + 1 < T) + (t + 2 < T)) * LPW);
+    else if (NS == 3) wait_vmcnt_fast<LPW>(st2 + (t + 1 < T_ ? LPW : 0) + st1);
+    else wait_vmcnt_fast<2 * LPW>(st3 + st2 + st1 + ((t + 1 < T_) + (t + 2 < T_)) * LPW);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (s_t < T) stage();
+    if (s_t < T_) stage();
     const char* As = stage_base + buf * Cfg::STAGE;
     buf = buf + 1 == NS ? 0 : buf + 1;
     const char* Bs = BRES ? smem + ks * Cfg::BSTAGE : As + Cfg::ASTAGE;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int c = kk * 4 + fq;
-      bf16x8 av[MSB], bv[4];
+      if constexpr (F32) {
+        // lane (fr, fq) holds K elements 16 kk + 4 fq + 0..3 of its row; MFMA j
+        // contracts element j of every lane group (the same K permutation on
+        // both operands, so the sum is the GEMM's)
+        f32x4 av[MSB], bv[4];
 #pragma unroll
-      for (int s = 0; s < MSB; ++s) {
-        const int ra = wm * Cfg::WTM + s * 16 + fr;
-        av[s] = *reinterpret_cast<const bf16x8*>(As + ra * 128 + ((c ^ swz(ra)) << 4));
+        for (int s = 0; s < MSB; ++s) {
+          const int ra = wm * Cfg::WTM + s * 16 + fr;
+          av[s] = *reinterpret_cast<const f32x4*>(As + ra * 128 + ((c ^ swz(ra)) << 4));
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int rb = wn * 64 + s * 16 + fr;
+          bv[s] = *reinterpret_cast<const f32x4*>(Bs + rb * 128 + ((c ^ swz(rb)) << 4));
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int ms = 0; ms < MSB; ++ms)
+#pragma unroll
+            for (int ns = 0; ns < 4; ++ns)
+              acc[ms][ns] = __builtin_amdgcn_mfma_f32_16x16x4f32(bv[ns][j], av[ms][j], acc[ms][ns], 0, 0, 0);
+      } else {
+        bf16x8 av[MSB], bv[4];
+#pragma unroll
+        for (int s = 0; s < MSB; ++s) {
+          const int ra = wm * Cfg::WTM + s * 16 + fr;
+          av[s] = *reinterpret_cast<const bf16x8*>(As + ra * 128 + ((c ^ swz(ra)) << 4));
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int rb = wn * 64 + s * 16 + fr;
+          bv[s] = *reinterpret_cast<const bf16x8*>(Bs + rb * 128 + ((c ^ swz(rb)) << 4));
+        }
+#pragma unroll
+        for (int ms = 0; ms < MSB; ++ms)
+#pragma unroll
+          for (int ns = 0; ns < 4; ++ns)
+            acc[ms][ns] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv[ns], av[ms], acc[ms][ns], 0, 0, 0);
       }
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int rb = wn * 64 + s * 16 + fr;
-        bv[s] = *reinterpret_cast<const bf16x8*>(Bs + rb * 128 + ((c ^ swz(rb)) << 4));
-      }
-#pragma unroll
-      for (int ms = 0; ms < MSB; ++ms)
-#pragma unroll
-        for (int ns = 0; ns < 4; ++ns)
-          acc[ms][ns] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv[ns], av[ms], acc[ms][ns], 0, 0, 0);
     }
     st3 = st2;
     st2 = st1;
     st1 = 0;
     if (++ks == nk) {
       ks = 0;
-      // lane holds C[m = fr][n = 4*fq + r] of every 16x16 subtile.  Lanes fq and
-      // fq^1 swap halves of the subtile pair (2p, 2p+1) so each lane owns 8
-      // consecutive channels: one 16-byte store per lane per pair.
+      // lane holds C[m = fr][n = 4*fq + r] of every 16x16 subtile.
       const int64_t mbase = mt * Cfg::BM;
       mt += gridDim.x;
       const bool full = mbase + Cfg::BM <= M;
@@ -361,6 +389,7 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
 #pragma unroll
       for (int ms = 0; ms < MSB; ++ms) {
         const int64_t m = mbase + wm * Cfg::WTM + ms * 16 + fr;
+        const bool live = full || m < M;
         int64_t orow = m;     // output row (remapped for stride-2 grad-input classes)
         int zr = 0, zc = 0;   // RZ: sibling row / column inside the image
         if (geo.RH) {
@@ -372,75 +401,121 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
           zr = (int)(2 * oh + 1) < geo.RH;
           zc = (int)(2 * ow + 1) < geo.RW;
         }
-        uint4 eh[2], ed[2];   // BN-backward operands of this row: h, dy2 and the mask byte per pair
-        uint32_t em[2];
-        if (BNB_OK && bnb) {
+        if constexpr (F32) {
+          // fp32: lane owns 4 consecutive channels of every subtile -- one
+          // 16-byte store per subtile, no shuffle
+#pragma unroll
+          for (int ns = 0; ns < 4; ++ns) {
+            const int n = n0 + wn * 64 + ns * 16 + fq * 4;
+            f32x4 v = acc[ms][ns];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += bia[ns][r];
+            if (bnb) {
+              // dz = mask ? dy + dy2 : 0; partials sum(dz), sum(dz * h)
+              f32x4 hv = f32x4{0.f, 0.f, 0.f, 0.f}, d2 = f32x4{0.f, 0.f, 0.f, 0.f};
+              uint32_t bits = 0u;
+              if (live) {
+                hv = *reinterpret_cast<const f32x4*>(static_cast<const float*>(bb.h) + m * ldc + n);
+                if (bb.dy2) d2 = *reinterpret_cast<const f32x4*>(static_cast<const float*>(bb.dy2) + m * ldc + n);
+                bits = bb.mask ? (uint32_t)bb.mask[m * (Ntot >> 2) + (n >> 2)] : 0xfu;
+              }
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float dz = (bits >> r) & 1u ? v[r] + d2[r] : 0.f;
+                v[r] = dz;
+                ssum[ns][r] += dz;
+                ssq[ns][r] = fmaf(dz, hv[r], ssq[ns][r]);
+              }
+            } else if (stats && live) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                ssum[ns][r] += v[r];
+                ssq[ns][r] = fmaf(v[r], v[r], ssq[ns][r]);
+              }
+            }
+            if (live) {
+              *reinterpret_cast<f32x4*>(C + orow * ldc + n) = v;
+              if (geo.RZ) {
+                const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+                if (zc) *reinterpret_cast<f32x4*>(C + (orow + 1) * ldc + n) = z;
+                if (zr) *reinterpret_cast<f32x4*>(C + (orow + geo.RW) * ldc + n) = z;
+                if (zr && zc) *reinterpret_cast<f32x4*>(C + (orow + geo.RW + 1) * ldc + n) = z;
+              }
+            }
+          }
+        } else {
+          // bf16: lanes fq and fq^1 swap halves of the subtile pair (2p, 2p+1) so
+          // each lane owns 8 consecutive channels: one 16-byte store per lane per pair.
+          uint4 eh[2], ed[2];   // BN-backward operands of this row: h, dy2 and the mask byte per pair
+          uint32_t em[2];
+          if (bnb) {
+#pragma unroll
+            for (int pr = 0; pr < 2; ++pr) {
+              const int n = n0 + wn * 64 + pr * 32 + cofs;
+              eh[pr] = ed[pr] = make_uint4(0u, 0u, 0u, 0u);
+              em[pr] = 0u;
+              if (live) {
+                eh[pr] = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(bb.h) + m * ldc + n);
+                if (bb.dy2) ed[pr] = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(bb.dy2) + m * ldc + n);
+                em[pr] = bb.mask ? (uint32_t)bb.mask[m * (Ntot >> 3) + (n >> 3)] : 0xffu;
+              }
+            }
+          }
 #pragma unroll
           for (int pr = 0; pr < 2; ++pr) {
+            const f32x4 va = acc[ms][2 * pr], vb = acc[ms][2 * pr + 1];
+            const float* ba = bia[2 * pr];
+            const float* bb2 = bia[2 * pr + 1];
+            const uint32_t a0 = pack_bf16x2(va[0] + ba[0], va[1] + ba[1]), a1 = pack_bf16x2(va[2] + ba[2], va[3] + ba[3]);
+            const uint32_t b0 = pack_bf16x2(vb[0] + bb2[0], vb[1] + bb2[1]), b1 = pack_bf16x2(vb[2] + bb2[2], vb[3] + bb2[3]);
+            if (stats && !bnb && live) {   // statistics of the values as stored (bf16)
+              const uint32_t pk[4] = {a0, a1, b0, b1};
+#pragma unroll
+              for (int h = 0; h < 4; ++h) {
+                const float lo = __uint_as_float(pk[h] << 16), hi = __uint_as_float(pk[h] & 0xffff0000u);
+                const int nsx = 2 * pr + (h >> 1), rr = (h & 1) * 2;
+                ssum[nsx][rr] += lo;
+                ssq[nsx][rr] = fmaf(lo, lo, ssq[nsx][rr]);
+                ssum[nsx][rr + 1] += hi;
+                ssq[nsx][rr + 1] = fmaf(hi, hi, ssq[nsx][rr + 1]);
+              }
+            }
+            const uint32_t r0 = (uint32_t)__shfl_xor((int)(odd ? a0 : b0), 16, 64);
+            const uint32_t r1 = (uint32_t)__shfl_xor((int)(odd ? a1 : b1), 16, 64);
+            uint4 v = odd ? make_uint4(r0, r1, b0, b1) : make_uint4(a0, a1, r0, r1);
             const int n = n0 + wn * 64 + pr * 32 + cofs;
-            eh[pr] = ed[pr] = make_uint4(0u, 0u, 0u, 0u);
-            em[pr] = 0u;
-            if (full || m < M) {
-              eh[pr] = *reinterpret_cast<const uint4*>(bb.h + m * ldc + n);
-              if (bb.dy2) ed[pr] = *reinterpret_cast<const uint4*>(bb.dy2 + m * ldc + n);
-              em[pr] = bb.mask ? (uint32_t)bb.mask[m * (Ntot >> 3) + (n >> 3)] : 0xffu;
-            }
-          }
-        }
+            if (bnb) {
+              const uint32_t dv[4] = {v.x, v.y, v.z, v.w};
+              const uint4 e2 = ed[pr], eh4 = eh[pr];
+              const uint32_t d2[4] = {e2.x, e2.y, e2.z, e2.w};
+              const uint32_t hh[4] = {eh4.x, eh4.y, eh4.z, eh4.w};
+              const uint32_t bits = em[pr];
+              uint32_t o[4];
 #pragma unroll
-        for (int pr = 0; pr < 2; ++pr) {
-          const f32x4 va = acc[ms][2 * pr], vb = acc[ms][2 * pr + 1];
-          const float* ba = bia[2 * pr];
-          const float* bb = bia[2 * pr + 1];
-          const uint32_t a0 = pack_bf16x2(va[0] + ba[0], va[1] + ba[1]), a1 = pack_bf16x2(va[2] + ba[2], va[3] + ba[3]);
-          const uint32_t b0 = pack_bf16x2(vb[0] + bb[0], vb[1] + bb[1]), b1 = pack_bf16x2(vb[2] + bb[2], vb[3] + bb[3]);
-          if (stats && !bnb && (full || m < M)) {   // statistics of the values as stored (bf16)
-            const uint32_t pk[4] = {a0, a1, b0, b1};
-#pragma unroll
-            for (int h = 0; h < 4; ++h) {
-              const float lo = __uint_as_float(pk[h] << 16), hi = __uint_as_float(pk[h] & 0xffff0000u);
-              const int nsx = 2 * pr + (h >> 1), rr = (h & 1) * 2;
-              ssum[nsx][rr] += lo;
-              ssq[nsx][rr] = fmaf(lo, lo, ssq[nsx][rr]);
-              ssum[nsx][rr + 1] += hi;
-              ssq[nsx][rr + 1] = fmaf(hi, hi, ssq[nsx][rr + 1]);
+              for (int i = 0; i < 4; ++i) {
+                float lo = __uint_as_float(dv[i] << 16) + __uint_as_float(d2[i] << 16);
+                float hi = __uint_as_float(dv[i] & 0xffff0000u) + __uint_as_float(d2[i] & 0xffff0000u);
+                lo = (bits >> (2 * i)) & 1u ? lo : 0.f;
+                hi = (bits >> (2 * i + 1)) & 1u ? hi : 0.f;
+                o[i] = pack_bf16x2(lo, hi);
+                const float hl = __uint_as_float(hh[i] << 16);
+                const float hu = __uint_as_float(hh[i] & 0xffff0000u);
+                const int a = 2 * pr + (i >> 1), b = (i & 1) * 2;
+                ssum[a][b] += lo;
+                ssq[a][b] = fmaf(lo, hl, ssq[a][b]);
+                ssum[a][b + 1] += hi;
+                ssq[a][b + 1] = fmaf(hi, hu, ssq[a][b + 1]);
+              }
+              v = make_uint4(o[0], o[1], o[2], o[3]);
             }
-          }
-          const uint32_t r0 = (uint32_t)__shfl_xor((int)(odd ? a0 : b0), 16, 64);
-          const uint32_t r1 = (uint32_t)__shfl_xor((int)(odd ? a1 : b1), 16, 64);
-          uint4 v = odd ? make_uint4(r0, r1, b0, b1) : make_uint4(a0, a1, r0, r1);
-          const int n = n0 + wn * 64 + pr * 32 + cofs;
-          if (BNB_OK && bnb) {
-            const uint32_t dv[4] = {v.x, v.y, v.z, v.w};
-            const uint4 e2 = ed[pr], eh4 = eh[pr];
-            const uint32_t d2[4] = {e2.x, e2.y, e2.z, e2.w};
-            const uint32_t hh[4] = {eh4.x, eh4.y, eh4.z, eh4.w};
-            const uint32_t bits = em[pr];
-            uint32_t o[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              float lo = __uint_as_float(dv[i] << 16) + __uint_as_float(d2[i] << 16);
-              float hi = __uint_as_float(dv[i] & 0xffff0000u) + __uint_as_float(d2[i] & 0xffff0000u);
-              lo = (bits >> (2 * i)) & 1u ? lo : 0.f;
-              hi = (bits >> (2 * i + 1)) & 1u ? hi : 0.f;
-              o[i] = pack_bf16x2(lo, hi);
-              const float hl = __uint_as_float(hh[i] << 16);
-              const float hu = __uint_as_float(hh[i] & 0xffff0000u);
-              const int a = 2 * pr + (i >> 1), b = (i & 1) * 2;
-              ssum[a][b] += lo;
-              ssq[a][b] = fmaf(lo, hl, ssq[a][b]);
-              ssum[a][b + 1] += hi;
-              ssq[a][b + 1] = fmaf(hi, hu, ssq[a][b + 1]);
-            }
-            v = make_uint4(o[0], o[1], o[2], o[3]);
-          }
-          if (full || m < M) {
-            *reinterpret_cast<uint4*>(C + orow * ldc + n) = v;
-            if (geo.RZ) {
-              const uint4 z = make_uint4(0u, 0u, 0u, 0u);
-              if (zc) *reinterpret_cast<uint4*>(C + (orow + 1) * ldc + n) = z;
-              if (zr) *reinterpret_cast<uint4*>(C + (orow + geo.RW) * ldc + n) = z;
-              if (zr && zc) *reinterpret_cast<uint4*>(C + (orow + geo.RW + 1) * ldc + n) = z;
+            if (live) {
+              *reinterpret_cast<uint4*>(C + orow * ldc + n) = v;
+              if (geo.RZ) {
+                const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+                if (zc) *reinterpret_cast<uint4*>(C + (orow + 1) * ldc + n) = z;
+                if (zr) *reinterpret_cast<uint4*>(C + (orow + geo.RW) * ldc + n) = z;
+                if (zr && zc) *reinterpret_cast<uint4*>(C + (orow + geo.RW + 1) * ldc + n) = z;
+              }
             }
           }
         }
@@ -470,9 +545,10 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
       for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
-          // forward: [subtile a][row b] of 4fq..; BN-backward: store-layout channel
-          // cofs + 4 * (a & 1) + b of column pair a / 2
-          const int col = bnb ? wn * 64 + (a >> 1) * 32 + cofs + (a & 1) * 4 + b : wn * 64 + a * 16 + fq * 4 + b;
+          // forward and fp32: [subtile a][row b] of 4fq..; bf16 BN-backward:
+          // store-layout channel cofs + 4 * (a & 1) + b of column pair a / 2
+          const int col = (bnb && !F32) ? wn * 64 + (a >> 1) * 32 + cofs + (a & 1) * 4 + b
+                                        : wn * 64 + a * 16 + fq * 4 + b;
           red[wm * Cfg::BN + col] = ssum[a][b];
           red[(WM + wm) * Cfg::BN + col] = ssq[a][b];
         }
@@ -491,11 +567,11 @@ gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
   }
 }
 
-template <int WM, int WN, bool BRES, int NS, bool GATHER, int MSB = 4, bool BNB = false>
-int launch_nt(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, uint16_t* C, int64_t ldc, int64_t M,
+template <int WM, int WN, bool BRES, int NS, bool GATHER, int MSB = 4, bool BNB = false, typename T = uint16_t>
+int launch_nt(const T* A, int64_t lda, const T* B, int64_t ldb, T* C, int64_t ldc, int64_t M,
               int N, int K, int max_blocks, const ConvGeo& geo, float* stats, int64_t stats_ld, int stats_rows,
               const BnBwd& bb, hipStream_t stream) {
-  using Cfg = NtCfg<WM, WN, BRES, MSB>;
+  using Cfg = NtCfg<WM, WN, BRES, MSB, T>;
   const int ntiles = N / Cfg::BN;
   const int64_t mtiles = (M + Cfg::BM - 1) / Cfg::BM;
   const int lds = Cfg::lds_bytes(K, NS);
@@ -507,34 +583,36 @@ int launch_nt(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, ui
   if (stats && gx > stats_rows) gx = stats_rows;   // one partial row per block
   dim3 grid((unsigned)gx, (unsigned)ntiles);
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<WM, WN, BRES, NS, GATHER, MSB, BNB>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<WM, WN, BRES, NS, GATHER, MSB, BNB, T>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL((gemm_nt_kernel<WM, WN, BRES, NS, GATHER, MSB, BNB>), grid, dim3(Cfg::THREADS), lds, stream, A, lda, B,
-                     ldb, C, ldc, M, K, geo, stats, stats_ld, bb);
+  hipLaunchKernelGGL((gemm_nt_kernel<WM, WN, BRES, NS, GATHER, MSB, BNB, T>), grid, dim3(Cfg::THREADS), lds, stream, A,
+                     lda, B, ldb, C, ldc, M, K, geo, stats, stats_ld, bb);
   return (int)gx;
 }
 
-template <int WM, int WN, bool GATHER, int MSB = 4, bool BNB = false>
-int launch_nt_any(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, uint16_t* C, int64_t ldc,
+template <int WM, int WN, bool GATHER, int MSB = 4, bool BNB = false, typename T = uint16_t>
+int launch_nt_any(const T* A, int64_t lda, const T* B, int64_t ldb, T* C, int64_t ldc,
                   int64_t M, int N, int K, int max_blocks, int bres, int ns, const ConvGeo& geo, float* stats,
                   int64_t stats_ld, int stats_rows, const BnBwd& bb, hipStream_t stream) {
+  using CR = NtCfg<WM, WN, true, MSB, T>;
+  using CS = NtCfg<WM, WN, false, MSB, T>;
   // keep the weight panel resident when it fits next to the two A stages
-  if (bres < 0) bres = (64 * WN) * K * 2 <= 64 * 1024;
-  if (bres && NtCfg<WM, WN, true, MSB>::lds_bytes(K, 2) > 160 * 1024) bres = 0;
+  if (bres < 0) bres = (64 * WN) * K * (int)sizeof(T) <= 64 * 1024;
+  if (bres && CR::lds_bytes(K, 2) > 160 * 1024) bres = 0;
   constexpr int L = 160 * 1024;
-  if (ns == 4 && bres && NtCfg<WM, WN, true, MSB>::NS4_OK && NtCfg<WM, WN, true, MSB>::lds_bytes(K, 4) <= L)
-    return launch_nt<WM, WN, true, 4, GATHER, MSB, BNB>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, bb, stream);
-  if (ns == 4 && !bres && NtCfg<WM, WN, false, MSB>::NS4_OK && NtCfg<WM, WN, false, MSB>::lds_bytes(K, 4) <= L)
-    return launch_nt<WM, WN, false, 4, GATHER, MSB, BNB>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, bb, stream);
+#define GK_NT(BR, S) \
+  launch_nt<WM, WN, BR, S, GATHER, MSB, BNB, T>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, bb, stream)
+  if (ns == 4 && bres && CR::NS4_OK && CR::lds_bytes(K, 4) <= L) return GK_NT(true, 4);
+  if (ns == 4 && !bres && CS::NS4_OK && CS::lds_bytes(K, 4) <= L) return GK_NT(false, 4);
   if (bres) {
-    if (ns != 2 && NtCfg<WM, WN, true, MSB>::lds_bytes(K, 3) <= L) return launch_nt<WM, WN, true, 3, GATHER, MSB, BNB>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, bb, stream);
-    else return launch_nt<WM, WN, true, 2, GATHER, MSB, BNB>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, bb, stream);
-  } else {
-    if (ns != 2 && NtCfg<WM, WN, false, MSB>::lds_bytes(K, 3) <= L) return launch_nt<WM, WN, false, 3, GATHER, MSB, BNB>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, bb, stream);
-    else return launch_nt<WM, WN, false, 2, GATHER, MSB, BNB>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, bb, stream);
+    if (ns != 2 && CR::lds_bytes(K, 3) <= L) return GK_NT(true, 3);
+    return GK_NT(true, 2);
   }
+  if (ns != 2 && CS::lds_bytes(K, 3) <= L) return GK_NT(false, 3);
+  return GK_NT(false, 2);
+#undef GK_NT
 }
 
 // --------------------------------------------------------------------------
@@ -716,7 +794,7 @@ gemm_tn_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __re
         const bool ok = in && (unsigned)ih < (unsigned)geo.H && (unsigned)iw < (unsigned)geo.W;
         const uint32_t off = (((uint32_t)pn[j] * (uint32_t)geo.H + (uint32_t)ih) * (uint32_t)geo.W + (uint32_t)iw) *
                                  (uint32_t)geo.C + (uint32_t)ccol[j];
-        src = ok ? X + off : geo.zero + (ccol[j] & 63);
+        src = ok ? X + off : static_cast<const uint16_t*>(geo.zero) + (ccol[j] & 63);
         // advance the pixel by ROWS
         pow_[j] += adv_r;
         poh[j] += adv_q;
@@ -881,11 +959,279 @@ void launch_tn(const uint16_t* G, int64_t ldg, const uint16_t* X, int64_t ldx, f
                      M, rows, geo);
 }
 
+// --------------------------------------------------------------------------
+// gemm_tn, fp32 operands: W[N, K] += G[M, N]^T . X[M, K] on v_mfma_f32_16x16x4_f32
+// --------------------------------------------------------------------------
+// Both operands are M-major (pixel rows), the contraction runs over M, so an
+// MFMA operand wants one column of 4 consecutive staged rows per lane.  fp32
+// has no transposed LDS read; fp32 MFMA is 16x slower than bf16 per FLOP, so
+// 4 ds_read_b32 per 4 MFMAs (128 cycles) cost nothing that matters: lane
+// (i = l % 16, g = l / 16) reads rows kb + 4g + j (j = 0..3) of column i and
+// MFMA j contracts rows {kb + j, kb + 4 + j, kb + 8 + j, kb + 12 + j} -- the
+// same row permutation on both operands.  The 16-byte chunk index of a staged
+// row is XOR-ed with bit 2 of the row, which puts the two half-waves of every
+// ds_read_b32 (rows 4 apart) on disjoint banks.  Rows past this block's split
+// (and padding taps) load from a zero vector, so the tail needs no masking.
+// Each wave owns a 64x64 output tile; WN x WK waves per block, ROWS = 32
+// pixel rows (two 16-row k-groups, 128 MFMAs per wave) per LDS stage.
+__device__ __attribute__((aligned(16))) float g_tn_zero[32];
+
+template <int WN, int WK, int NS_>
+struct TnF32Cfg {
+  static constexpr int NW = WN * WK;
+  static constexpr int THREADS = 64 * NW;
+  static constexpr int BN = 64 * WN;
+  static constexpr int BK = 64 * WK;
+  static constexpr int ROWS = 32;
+  static constexpr int GROW = BN * 4;
+  static constexpr int XROW = BK * 4;
+  static constexpr int GBYTES = ROWS * GROW;
+  static constexpr int STAGE = ROWS * (GROW + XROW);
+  static constexpr int NS = NS_;
+  static constexpr int LDS = NS * STAGE;
+  static constexpr int GINSTS = GBYTES / 1024;
+  static constexpr int INSTS = STAGE / 1024;
+  static_assert(INSTS % NW == 0 && GINSTS % NW == 0, "stage split");
+  static constexpr int LPW = INSTS / NW;
+  static constexpr int LPWG = GINSTS / NW;
+  static_assert(LPW <= 63, "wait_vmcnt range");
+};
+
+__device__ __forceinline__ int swz4(int r) { return r & 4; }
+
+template <int WN, int WK, int NS, bool GATHER>
+__global__ void __launch_bounds__(64 * WN * WK) __attribute__((amdgpu_waves_per_eu(1)))
+gemm_tn_f32_kernel(const float* __restrict__ G, int64_t ldg, const float* __restrict__ X, int64_t ldx,
+                   float* __restrict__ W, int64_t ldw, int64_t M, int64_t rows_per_split, ConvGeo geo) {
+  using Cfg = TnF32Cfg<WN, WK, NS>;
+  constexpr int LPW = Cfg::LPW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wk = wave % WK, wn = wave / WK;
+  const int n0 = blockIdx.x * Cfg::BN;
+  const int c0 = blockIdx.y * Cfg::BK;
+  const int64_t mbeg = (int64_t)blockIdx.z * rows_per_split;
+  int64_t mend = mbeg + rows_per_split;
+  if (mend > M) mend = M;
+  if (mbeg >= mend) return;
+  const int T = (int)((mend - mbeg + Cfg::ROWS - 1) / Cfg::ROWS);
+
+  // per-lane staging state (set once, advanced by ROWS rows per stage)
+  const float* rptr[LPW];
+  int64_t row[LPW];
+  int pn[LPW], poh[LPW], pow_[LPW], dkh[LPW], dkw[LPW], ccol[LPW];
+#pragma unroll
+  for (int j = 0; j < LPW; ++j) {
+    const int i = wave + j * Cfg::NW;
+    int srow, colo;
+    bool gath = false;
+    dkh[j] = dkw[j] = 0;
+    if (j < Cfg::LPWG) {
+      constexpr int CPR = Cfg::GROW / 16;
+      const int e = i * 64 + lane;
+      srow = e / CPR;
+      colo = n0 + ((e % CPR) ^ swz4(srow)) * 4;
+      rptr[j] = G + (mbeg + srow) * ldg + colo;
+    } else {
+      constexpr int CPR = Cfg::XROW / 16;
+      const int e = (i - Cfg::GINSTS) * 64 + lane;
+      srow = e / CPR;
+      const int kcol = c0 + ((e % CPR) ^ swz4(srow)) * 4;
+      if (GATHER) {
+        const int tap = kcol / geo.C;
+        dkh[j] = tap / geo.KW;
+        dkw[j] = tap - dkh[j] * geo.KW;
+        colo = kcol - tap * geo.C;
+        gath = true;
+      } else {
+        colo = kcol;
+      }
+      rptr[j] = X + (mbeg + srow) * ldx + colo;
+    }
+    row[j] = mbeg + srow;
+    ccol[j] = colo;
+    pn[j] = poh[j] = pow_[j] = 0;
+    if (GATHER && gath) {
+      const int64_t m = mbeg + srow;
+      const int64_t ohw = (int64_t)geo.OH * geo.OW;
+      pn[j] = (int)(m / ohw);
+      const int rem = (int)(m - (int64_t)pn[j] * ohw);
+      poh[j] = rem / geo.OW;
+      pow_[j] = rem - poh[j] * geo.OW;
+    }
+  }
+  const int adv_q = Cfg::ROWS / (GATHER ? geo.OW : 1), adv_r = Cfg::ROWS - adv_q * (GATHER ? geo.OW : 1);
+  const int64_t gstep = (int64_t)Cfg::ROWS * ldg, xstep = (int64_t)Cfg::ROWS * ldx;
+
+  auto stage = [&](int t) {
+    GK_LDS char* base = (GK_LDS char*)smem + (t % NS) * Cfg::STAGE;
+#pragma unroll
+    for (int j = 0; j < LPW; ++j) {
+      const int i = wave + j * Cfg::NW;
+      const bool in = row[j] < mend;
+      const float* src;
+      if (j < Cfg::LPWG) {
+        src = in ? rptr[j] : g_tn_zero;
+        rptr[j] += gstep;
+      } else if (GATHER) {
+        const int ih = poh[j] * geo.S - geo.P + dkh[j], iw = pow_[j] * geo.S - geo.P + dkw[j];
+        const bool ok = in && (unsigned)ih < (unsigned)geo.H && (unsigned)iw < (unsigned)geo.W;
+        const uint32_t off = (((uint32_t)pn[j] * (uint32_t)geo.H + (uint32_t)ih) * (uint32_t)geo.W + (uint32_t)iw) *
+                                 (uint32_t)geo.C + (uint32_t)ccol[j];
+        src = ok ? X + off : g_tn_zero;
+        pow_[j] += adv_r;
+        poh[j] += adv_q;
+        if (pow_[j] >= geo.OW) { pow_[j] -= geo.OW; ++poh[j]; }
+        while (poh[j] >= geo.OH) { poh[j] -= geo.OH; ++pn[j]; }
+      } else {
+        src = in ? rptr[j] : g_tn_zero;
+        rptr[j] += xstep;
+      }
+      row[j] += Cfg::ROWS;
+      glds16(src, base + i * 1024);
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // per-lane byte offsets of row 4g (+ j + 16 kg: immediates) of this lane's
+  // column in each 16-column fragment
+  const int fi = lane & 15, fg = lane >> 4;
+  int goff[4], xoff[4];
+#pragma unroll
+  for (int s2 = 0; s2 < 4; ++s2) {
+    const int gc = wn * 64 + s2 * 16 + fi;
+    const int xc = wk * 64 + s2 * 16 + fi;
+    const int r = 4 * fg;
+    goff[s2] = r * Cfg::GROW + ((((gc >> 2) ^ swz4(r)) << 4) | ((gc & 3) << 2));
+    xoff[s2] = Cfg::GBYTES + r * Cfg::XROW + ((((xc >> 2) ^ swz4(r)) << 4) | ((xc & 3) << 2));
+  }
+
+  stage(0);
+  if (NS >= 3 && T > 1) stage(1);
+  for (int t = 0; t < T; ++t) {
+    if (NS == 3) wait_vmcnt_fast<LPW>(t + 1 < T ? LPW : 0);
+    else wait_vmcnt(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + NS - 1 < T) stage(t + NS - 1);
+    const char* sb = smem + (t % NS) * Cfg::STAGE;
+    // fragments of k-group kg: [j][s2] (32 values); the next group's reads are
+    // issued before this group's 64 MFMAs so only one LDS latency per stage shows
+    float gv[2][4][4], xv[2][4][4];
+    auto load = [&](int kg, float (&g)[4][4], float (&x)[4][4]) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int rr = kg * 16 + j;   // row offset of MFMA j's k-slot 0
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+          g[j][s2] = *reinterpret_cast<const float*>(sb + goff[s2] + rr * Cfg::GROW);
+          x[j][s2] = *reinterpret_cast<const float*>(sb + xoff[s2] + rr * Cfg::XROW);
+        }
+      }
+    };
+    load(0, gv[0], xv[0]);
+#pragma unroll
+    for (int kg = 0; kg < Cfg::ROWS / 16; ++kg) {
+      if (kg + 1 < Cfg::ROWS / 16) load(kg + 1, gv[(kg + 1) & 1], xv[(kg + 1) & 1]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int ns = 0; ns < 4; ++ns)
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks)
+            acc[ns][ks] = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[kg & 1][j][ns], xv[kg & 1][j][ks], acc[ns][ks], 0, 0, 0);
+    }
+  }
+  // D[i = n][j = c]: lane holds column c = .. + (lane & 15), rows n = .. + 4 (lane >> 4) + r
+#pragma unroll
+  for (int ns = 0; ns < 4; ++ns)
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int c = c0 + wk * 64 + ks * 16 + fi;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wn * 64 + ns * 16 + fg * 4 + r;
+        atomicAdd(W + (int64_t)n * ldw + c, acc[ns][ks][r]);
+      }
+    }
+}
+
+template <int WN, int WK, int NS, bool GATHER>
+void launch_tn_f32(const float* G, int64_t ldg, const float* X, int64_t ldx, float* W, int64_t ldw, int64_t M, int N,
+                   int K, int splits, const ConvGeo& geo, hipStream_t stream) {
+  using Cfg = TnF32Cfg<WN, WK, NS>;
+  const int tiles = (N / Cfg::BN) * (K / Cfg::BK);
+  if (splits <= 0) {
+    // two rounds of the chip's block slots (LDS-limited blocks per CU)
+    static const int cus = [] {
+      int d = 0, n = 0;
+      hipGetDevice(&d);
+      return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && n > 0 ? n : 256;
+    }();
+    int bpc = (160 * 1024) / Cfg::LDS;
+    const int by_waves = 16 / Cfg::NW;
+    if (bpc > by_waves) bpc = by_waves;
+    if (bpc < 1) bpc = 1;
+    splits = (int)(2 * (int64_t)cus * bpc / tiles);
+    if (splits < 1) splits = 1;
+  }
+  int64_t rows = (M + splits - 1) / splits;
+  rows = (rows + Cfg::ROWS - 1) / Cfg::ROWS * Cfg::ROWS;
+  if (rows < 4 * Cfg::ROWS) rows = 4 * Cfg::ROWS;
+  const int64_t nsplit = (M + rows - 1) / rows;
+  dim3 grid((unsigned)(N / Cfg::BN), (unsigned)(K / Cfg::BK), (unsigned)nsplit);
+  static bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_f32_kernel<WN, WK, NS, GATHER>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS) == hipSuccess;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL((gemm_tn_f32_kernel<WN, WK, NS, GATHER>), grid, dim3(Cfg::THREADS), Cfg::LDS, stream, G, ldg, X,
+                     ldx, W, ldw, M, rows, geo);
+}
+
+template <bool GATHER>
+void tn_f32_dispatch(const float* G, int64_t ldg, const float* X, int64_t ldx, float* W, int64_t ldw, int64_t M, int N,
+                     int K, int cfg, int splits, const ConvGeo& geo, hipStream_t stream) {
+  // cfg = tile + 10 * stages (0/2: three, 1: two).  tiles (WN, WK), 64x64 per wave:
+  // 1 (1,1)  2 (2,1)  3 (1,2)  4 (2,2)  5 (4,1)  6 (1,4)  7 (4,2)  8 (2,4)  9 (4,4, two stages)
+  const bool ns3 = (cfg / 10) % 10 != 1;
+  cfg %= 10;
+  if (cfg <= 0) cfg = (N % 128 == 0 && K % 128 == 0) ? 4 : (N % 128 == 0 ? 2 : (K % 128 == 0 ? 3 : 1));
+  static const int cfg_bn[10] = {64, 64, 128, 64, 128, 256, 64, 256, 128, 256};
+  static const int cfg_bk[10] = {64, 64, 64, 128, 128, 64, 256, 128, 256, 256};
+  if (N % cfg_bn[cfg] != 0 || K % cfg_bk[cfg] != 0) cfg = 1;
+#define GK_TNF(WN_, WK_)                                                                                   \
+  do {                                                                                                     \
+    if (ns3 && TnF32Cfg<WN_, WK_, 3>::LDS <= 160 * 1024)                                                   \
+      launch_tn_f32<WN_, WK_, 3, GATHER>(G, ldg, X, ldx, W, ldw, M, N, K, splits, geo, stream);            \
+    else                                                                                                   \
+      launch_tn_f32<WN_, WK_, 2, GATHER>(G, ldg, X, ldx, W, ldw, M, N, K, splits, geo, stream);            \
+  } while (0)
+  switch (cfg) {
+    case 2: GK_TNF(2, 1); break;
+    case 3: GK_TNF(1, 2); break;
+    case 4: GK_TNF(2, 2); break;
+    case 5: GK_TNF(4, 1); break;
+    case 6: GK_TNF(1, 4); break;
+    case 7: GK_TNF(4, 2); break;
+    case 8: GK_TNF(2, 4); break;
+    case 9: GK_TNF(4, 4); break;
+    default: GK_TNF(1, 1); break;
+  }
+#undef GK_TNF
+}
+
 }  // namespace
 
 bool gemm_supported(int64_t N, int64_t K) { return N >= 64 && K >= 64 && N % 64 == 0 && K % 64 == 0; }
 
-template <bool GATHER>
+template <bool GATHER, typename T>
 int nt_dispatch(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N,
                 int K, int cfg, int max_blocks, const ConvGeo& geo, float* stats, int64_t stats_ld, int stats_rows,
                 const BnBwd& bb, hipStream_t stream) {
@@ -894,61 +1240,80 @@ int nt_dispatch(const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
   const int bres = (cfg / 10) % 10 == 0 ? -1 : ((cfg / 10) % 10 == 1 ? 1 : 0);
   const int ns = (cfg / 100) % 10 == 1 ? 2 : ((cfg / 100) % 10 == 2 ? 4 : 3);
   cfg %= 10;
-  auto a = static_cast<const uint16_t*>(A);
-  auto b = static_cast<const uint16_t*>(B);
-  auto c = static_cast<uint16_t*>(C);
+  auto a = static_cast<const T*>(A);
+  auto b = static_cast<const T*>(B);
+  auto c = static_cast<T*>(C);
   if (cfg <= 0) cfg = N % 256 == 0 ? 3 : (N % 128 == 0 ? 2 : 1);
   // tiles (BM x BN, waves): 1 256x64 (4)  2 256x128 (8)  3 128x256 (8)  4 128x128 (4)
   //                         5 256x256 (8, 128x64 per wave)  6 256x128 (4, 128x64)  7 128x256 (4, 128x64)
+  // fp32 runs 64x64 wave tiles only (5-7 map to the 64x64 tile of the same block width)
   static const int cfg_bn[8] = {64, 64, 128, 256, 128, 256, 128, 256};
   if (cfg > 7 || N % cfg_bn[cfg] != 0) cfg = 1;   // the tile must divide N (B rows are not clamped)
+#define GK_NTA(WM_, WN_, MSB_, BNB_) \
+  return launch_nt_any<WM_, WN_, GATHER, MSB_, BNB_, T>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, bb, stream)
   if (bb.h) {   // BN-backward epilogue: 64x64 wave tiles only
     switch (cfg) {
-      case 2: return launch_nt_any<4, 2, GATHER, 4, true>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, bb, stream);
-      case 3: case 5: case 7: return launch_nt_any<2, 4, GATHER, 4, true>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, bb, stream);
-      case 4: case 6: return launch_nt_any<2, 2, GATHER, 4, true>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, bb, stream);
-      default: return launch_nt_any<4, 1, GATHER, 4, true>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, bb, stream);
+      case 2: GK_NTA(4, 2, 4, true);
+      case 3: case 5: case 7: GK_NTA(2, 4, 4, true);
+      case 4: case 6: GK_NTA(2, 2, 4, true);
+      default: GK_NTA(4, 1, 4, true);
     }
   }
-  switch (cfg) {
-    case 2: return launch_nt_any<4, 2, GATHER>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, bb, stream);
-    case 3: return launch_nt_any<2, 4, GATHER>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, bb, stream);
-    case 4: return launch_nt_any<2, 2, GATHER>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, bb, stream);
-    case 5: return launch_nt_any<2, 4, GATHER, 8>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, bb, stream);
-    case 6: return launch_nt_any<2, 2, GATHER, 8>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, bb, stream);
-    case 7: return launch_nt_any<1, 4, GATHER, 8>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, bb, stream);
-    default: return launch_nt_any<4, 1, GATHER>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, bb, stream);
+  if constexpr (sizeof(T) == 4) {
+    switch (cfg) {
+      case 2: GK_NTA(4, 2, 4, false);
+      case 3: case 5: GK_NTA(2, 4, 4, false);
+      case 7: GK_NTA(1, 4, 4, false);
+      case 4: case 6: GK_NTA(2, 2, 4, false);
+      default: GK_NTA(4, 1, 4, false);
+    }
+  } else {
+    switch (cfg) {
+      case 2: GK_NTA(4, 2, 4, false);
+      case 3: GK_NTA(2, 4, 4, false);
+      case 4: GK_NTA(2, 2, 4, false);
+      case 5: GK_NTA(2, 4, 8, false);
+      case 6: GK_NTA(2, 2, 8, false);
+      case 7: GK_NTA(1, 4, 8, false);
+      default: GK_NTA(4, 1, 4, false);
+    }
   }
+#undef GK_NTA
 }
 
-int gemm_nt_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N,
-                 int K, int cfg, int max_blocks, float* stats, int stats_rows, const float* bias, const BnBwdArgs* bn,
-                 hipStream_t stream) {
+int gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N, int K,
+            bool f32, int cfg, int max_blocks, float* stats, int stats_rows, const float* bias, const BnBwdArgs* bn,
+            hipStream_t stream) {
   ConvGeo g{};
   g.bias = bias;
   const BnBwd bb = bn ? BnBwd{bn->h, bn->dy2, bn->mask} : BnBwd{};
-  return nt_dispatch<false>(A, lda, B, ldb, C, ldc, M, N, K, cfg, max_blocks, g, stats, (int64_t)stats_rows * N,
-                            stats_rows, bb, stream);
+  const int64_t sld = (int64_t)stats_rows * N;
+  return f32 ? nt_dispatch<false, float>(A, lda, B, ldb, C, ldc, M, N, K, cfg, max_blocks, g, stats, sld, stats_rows, bb, stream)
+             : nt_dispatch<false, uint16_t>(A, lda, B, ldb, C, ldc, M, N, K, cfg, max_blocks, g, stats, sld, stats_rows, bb, stream);
 }
 
-int conv_nt_bf16(const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P, int KH, int KW,
-                 const void* B, void* Y, int64_t M, int N, int cfg, int max_blocks, float* stats, int stats_rows,
-                 const float* bias, const BnBwdArgs* bn, hipStream_t stream) {
-  ConvGeo g{static_cast<const uint16_t*>(zero), H, W, C, OH, OW, S, P, KW, bias};
+int conv_nt(const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P, int KH, int KW,
+            const void* B, void* Y, int64_t M, int N, bool f32, int cfg, int max_blocks, float* stats, int stats_rows,
+            const float* bias, const BnBwdArgs* bn, hipStream_t stream) {
+  ConvGeo g{zero, H, W, C, OH, OW, S, P, KW, bias};
   const int K = KH * KW * C;
   const BnBwd bb = bn ? BnBwd{bn->h, bn->dy2, bn->mask} : BnBwd{};
-  return nt_dispatch<true>(X, C, B, K, Y, N, M, N, K, cfg, max_blocks, g, stats, (int64_t)stats_rows * N, stats_rows,
-                           bb, stream);
+  const int64_t sld = (int64_t)stats_rows * N;
+  return f32 ? nt_dispatch<true, float>(X, C, B, K, Y, N, M, N, K, cfg, max_blocks, g, stats, sld, stats_rows, bb, stream)
+             : nt_dispatch<true, uint16_t>(X, C, B, K, Y, N, M, N, K, cfg, max_blocks, g, stats, sld, stats_rows, bb, stream);
 }
 
-int conv_nt_remap_bf16(const void* X, int64_t ldx, const void* zero, int H, int W, int C, int OH, int OW, int KH,
-                       int KW, const void* B, void* Y, int64_t M, int N, int RH, int RW, int RA, int RB, int RZ,
-                       int cfg, int max_blocks, hipStream_t stream) {
-  ConvGeo g{static_cast<const uint16_t*>(zero), H, W, C, OH, OW, 1, 0, KW, nullptr, RH, RW, RA, RB, RZ};
+int conv_nt_remap(const void* X, int64_t ldx, const void* zero, int H, int W, int C, int OH, int OW, int KH, int KW,
+                  const void* B, void* Y, int64_t M, int N, int RH, int RW, int RA, int RB, int RZ, bool f32, int cfg,
+                  int max_blocks, hipStream_t stream) {
+  ConvGeo g{zero, H, W, C, OH, OW, 1, 0, KW, nullptr, RH, RW, RA, RB, RZ};
   const int K = KH * KW * C;
-  if (KH * KW == 1)   // one tap at the class pixel itself: the plain row GEMM
-    return nt_dispatch<false>(X, ldx, B, K, Y, N, M, N, K, cfg, max_blocks, g, nullptr, 0, 0, BnBwd{}, stream);
-  return nt_dispatch<true>(X, C, B, K, Y, N, M, N, K, cfg, max_blocks, g, nullptr, 0, 0, BnBwd{}, stream);
+  if (KH * KW == 1) {   // one tap at the class pixel itself: the plain row GEMM
+    return f32 ? nt_dispatch<false, float>(X, ldx, B, K, Y, N, M, N, K, cfg, max_blocks, g, nullptr, 0, 0, BnBwd{}, stream)
+               : nt_dispatch<false, uint16_t>(X, ldx, B, K, Y, N, M, N, K, cfg, max_blocks, g, nullptr, 0, 0, BnBwd{}, stream);
+  }
+  return f32 ? nt_dispatch<true, float>(X, C, B, K, Y, N, M, N, K, cfg, max_blocks, g, nullptr, 0, 0, BnBwd{}, stream)
+             : nt_dispatch<true, uint16_t>(X, C, B, K, Y, N, M, N, K, cfg, max_blocks, g, nullptr, 0, 0, BnBwd{}, stream);
 }
 
 template <int WN, int WK, int WS, bool GATHER, int MSN = 1>
@@ -996,16 +1361,24 @@ void tn_dispatch(const void* G, int64_t ldg, const void* X, int64_t ldx, float* 
   }
 }
 
-void gemm_tn_acc_f32(const void* G, int64_t ldg, const void* X, int64_t ldx, float* W, int64_t ldw, int64_t M,
-                     int N, int K, int cfg, int splits, hipStream_t stream) {
-  tn_dispatch<false>(G, ldg, X, ldx, W, ldw, M, N, K, cfg, splits, ConvGeo{}, stream);
+void gemm_tn_acc(const void* G, int64_t ldg, const void* X, int64_t ldx, float* W, int64_t ldw, int64_t M, int N,
+                 int K, bool f32, int cfg, int splits, hipStream_t stream) {
+  if (f32)
+    tn_f32_dispatch<false>(static_cast<const float*>(G), ldg, static_cast<const float*>(X), ldx, W, ldw, M, N, K, cfg,
+                           splits, ConvGeo{}, stream);
+  else
+    tn_dispatch<false>(G, ldg, X, ldx, W, ldw, M, N, K, cfg, splits, ConvGeo{}, stream);
 }
 
-void conv_tn_acc_f32(const void* G, const void* X, const void* zero, int H, int W_, int C, int OH, int OW, int S, int P,
-                     int KH, int KW, float* Wout, int64_t M, int N, int cfg, int splits, hipStream_t stream) {
-  ConvGeo g{static_cast<const uint16_t*>(zero), H, W_, C, OH, OW, S, P, KW, nullptr};
+void conv_tn_acc(const void* G, const void* X, const void* zero, int H, int W_, int C, int OH, int OW, int S, int P,
+                 int KH, int KW, float* Wout, int64_t M, int N, bool f32, int cfg, int splits, hipStream_t stream) {
+  ConvGeo g{zero, H, W_, C, OH, OW, S, P, KW, nullptr};
   const int K = KH * KW * C;
-  tn_dispatch<true>(G, N, X, C, Wout, K, M, N, K, cfg, splits, g, stream);
+  if (f32)
+    tn_f32_dispatch<true>(static_cast<const float*>(G), N, static_cast<const float*>(X), C, Wout, K, M, N, K, cfg,
+                          splits, g, stream);
+  else
+    tn_dispatch<true>(G, N, X, C, Wout, K, M, N, K, cfg, splits, g, stream);
 }
 
 }  // namespace gk

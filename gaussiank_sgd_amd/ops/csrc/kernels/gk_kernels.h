@@ -227,15 +227,15 @@ void bn_act_forward(const void* x, const void* res, void* y, uint8_t* mask, int6
 // dy2 (optional): a second upstream gradient of the same output, summed on load.
 // bn_act_forward with the batch statistics already reduced to per-row
 // partials (psum / psq: [gy][C] each), e.g. by the producing
-// convolution's epilogue (gemm_nt_bf16 / conv_nt_bf16 `stats`).
+// convolution's epilogue (gemm_nt / conv_nt `stats`).
 void bn_act_forward_pre(const void* x, const void* res, void* y, uint8_t* mask, int64_t M, int C, int elem_bytes,
                         const float* psum, const float* psq, int gy, const float* w, const float* b, float eps, float momentum,
                         float* run_mean, float* run_var, float* save_mean, float* save_invstd, float* scale,
                         float* shift, int relu, int64_t* nbt, hipStream_t stream);
-// bf16 only: dz and its [2][gy][C] partials sum(dz), sum(dz * x) come from a
-// grad-input GEMM's BatchNorm-backward epilogue (BnBwdArgs below); finalize
-// (centring with the mean) + apply only.
-void bn_act_backward_pre(const void* dz, const void* x, void* dx, int64_t M, int C, const float* w,
+// dz and its [2][gy][C] partials sum(dz), sum(dz * x) come from a grad-input
+// GEMM's BatchNorm-backward epilogue (BnBwdArgs below); finalize (centring
+// with the mean) + apply only.  bf16 (elem_bytes 2) or fp32 (4).
+void bn_act_backward_pre(const void* dz, const void* x, void* dx, int64_t M, int C, int elem_bytes, const float* w,
                          const float* mean, const float* invstd, float* dgamma, float* dbeta, const float* pdb,
                          const float* pdg, int gy, float* gw_acc, float* gb_acc, hipStream_t stream);
 void bn_act_backward(const void* dy, const void* dy2, const uint8_t* mask, const void* x, void* dx, void* dres,
@@ -264,50 +264,53 @@ void bn_relu_pool_backward(const void* dy, const void* dy2, const uint8_t* amax,
                            float* dgamma, float* dbeta, float* ws, float* gw_acc, float* gb_acc, hipStream_t stream);
 
 // ---------------------------------------------------------------------------
-// MFMA GEMMs for 1x1 convolutions over channels-last activations (gemm.hip).
-// bf16 operands, fp32 accumulation.  N, K multiples of 64 (gemm_supported).
-//   gemm_nt_bf16   : C[M, N] (bf16)  = A[M, K] . B[N, K]^T
-//   gemm_tn_acc_f32: W[N, K] (fp32) += G[M, N]^T . X[M, K]   (float atomics)
+// MFMA GEMMs and implicit-GEMM convolutions over channels-last activations
+// (gemm.hip).  Operands bf16 (v_mfma_f32_16x16x32_bf16) or, with f32 = true,
+// fp32 (v_mfma_f32_16x16x4_f32: exact fp32 products, fp32 accumulation).
+// N, K multiples of 64 (gemm_supported).
+//   gemm_nt    : C[M, N] (operand dtype) = A[M, K] . B[N, K]^T
+//   gemm_tn_acc: W[N, K] (fp32) += G[M, N]^T . X[M, K]   (float atomics)
 // cfg <= 0 picks the tile shape from N (and K); max_blocks / splits <= 0
 // pick the grid.
 // ---------------------------------------------------------------------------
 bool gemm_supported(int64_t N, int64_t K);
 // BatchNorm-backward epilogue of a grad-input GEMM (bn != nullptr): C receives
-// dz = mask ? bf16(dy) + dy2 : 0 instead of dy, and `stats` the per-workgroup
-// partials sum(dz), sum(dz * h) -- feed them to bn_act_backward_pre.  h / dy2
-// share C's row stride; mask is the BN forward's 1-bit ReLU mask.
+// dz = mask ? dy + dy2 : 0 instead of dy (dy rounded to the operand dtype), and
+// `stats` the per-workgroup partials sum(dz), sum(dz * h) -- feed them to
+// bn_act_backward_pre.  h / dy2 share C's row stride and dtype; mask is the BN
+// forward's 1-bit ReLU mask (bn_act.hip layout).
 struct BnBwdArgs {
-  const uint16_t* h;
-  const uint16_t* dy2;
+  const void* h;
+  const void* dy2;
   const uint8_t* mask;
 };
 // stats (optional): [2][stats_rows][N] fp32 BatchNorm partials (sum, sum of
-// squares of the bf16 output) per workgroup row; returns the grid's row count
+// squares of the stored output) per workgroup row; returns the grid's row count
 // (the partial rows written, <= stats_rows) -- feed it to bn_act_forward_pre.
 // bias (optional): fp32 [N] added in the epilogue (before rounding and statistics)
-int gemm_nt_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N,
-                 int K, int cfg, int max_blocks, float* stats, int stats_rows, const float* bias, const BnBwdArgs* bn,
-                 hipStream_t stream);
-void gemm_tn_acc_f32(const void* G, int64_t ldg, const void* X, int64_t ldx, float* W, int64_t ldw, int64_t M,
-                     int N, int K, int cfg, int splits, hipStream_t stream);
-// Implicit-GEMM KHxKW convolution (stride S, zero padding P) over NHWC bf16:
-//   conv_nt_bf16   : Y[M = N*OH*OW, Cout] = im2col(X) . Wt[Cout, KH*KW*C]^T
-//   conv_tn_acc_f32: Wout[Cout, KH*KW*C] += G[M, Cout]^T . im2col(X)
+int gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N, int K,
+            bool f32, int cfg, int max_blocks, float* stats, int stats_rows, const float* bias, const BnBwdArgs* bn,
+            hipStream_t stream);
+void gemm_tn_acc(const void* G, int64_t ldg, const void* X, int64_t ldx, float* W, int64_t ldw, int64_t M, int N,
+                 int K, bool f32, int cfg, int splits, hipStream_t stream);
+// Implicit-GEMM KHxKW convolution (stride S, zero padding P) over NHWC:
+//   conv_nt    : Y[M = N*OH*OW, Cout] = im2col(X) . Wt[Cout, KH*KW*C]^T
+//   conv_tn_acc: Wout[Cout, KH*KW*C] += G[M, Cout]^T . im2col(X)
 // Weights are channels-last ([Cout][KH][KW][C]); C % 64 == 0; `zero` points at
-// >= 64 zero bf16 (the padding row).
-int conv_nt_bf16(const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P, int KH, int KW,
-                 const void* B, void* Y, int64_t M, int N, int cfg, int max_blocks, float* stats, int stats_rows,
-                 const float* bias, const BnBwdArgs* bn, hipStream_t stream);
+// >= 128 zero bytes (the padding row).
+int conv_nt(const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P, int KH, int KW,
+            const void* B, void* Y, int64_t M, int N, bool f32, int cfg, int max_blocks, float* stats, int stats_rows,
+            const float* bias, const BnBwdArgs* bn, hipStream_t stream);
 // One parity class (RA, RB) of a stride-2 convolution's grad-input as a stride-1,
 // padding-0 KHxKW implicit GEMM over dY (H x W x C, the forward output) whose
 // OH x OW output grid is stored at rows (n*RH + 2 oh + RA) * RW + 2 ow + RB of
 // the RH x RW grad-input (RZ: zeros at the other three parities); KH = KW = 1
 // runs the plain row GEMM over X = dY rows (row stride ldx).
-int conv_nt_remap_bf16(const void* X, int64_t ldx, const void* zero, int H, int W, int C, int OH, int OW, int KH,
-                       int KW, const void* B, void* Y, int64_t M, int N, int RH, int RW, int RA, int RB, int RZ,
-                       int cfg, int max_blocks, hipStream_t stream);
-void conv_tn_acc_f32(const void* G, const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P,
-                     int KH, int KW, float* Wout, int64_t M, int N, int cfg, int splits, hipStream_t stream);
+int conv_nt_remap(const void* X, int64_t ldx, const void* zero, int H, int W, int C, int OH, int OW, int KH, int KW,
+                  const void* B, void* Y, int64_t M, int N, int RH, int RW, int RA, int RB, int RZ, bool f32, int cfg,
+                  int max_blocks, hipStream_t stream);
+void conv_tn_acc(const void* G, const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P,
+                 int KH, int KW, float* Wout, int64_t M, int N, bool f32, int cfg, int splits, hipStream_t stream);
 
 // ---------------------------------------------------------------------------
 // ImageNet-ResNet stem: 7x7 / stride 2 / pad 3 convolution, 3 -> 64 channels

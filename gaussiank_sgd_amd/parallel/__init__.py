@@ -4,6 +4,6 @@ DistributedOptimizer."""
 from . import comm
 from .buckets import GradArena, group_with_threshold
 from .distributed_optimizer import DistributedOptimizer
-from .shadow import install_bf16_shadow
+from .shadow import install_bf16_shadow, install_direct_grads
 
-__all__ = ["comm", "GradArena", "group_with_threshold", "DistributedOptimizer", "install_bf16_shadow"]
+__all__ = ["comm", "GradArena", "group_with_threshold", "DistributedOptimizer", "install_bf16_shadow", "install_direct_grads"]

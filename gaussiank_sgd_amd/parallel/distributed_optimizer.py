@@ -90,7 +90,13 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         dw = opts.get("density_warmup", True)
         self._dynamic_densities = list(DEFAULT_DYNAMIC_DENSITIES) if dw is True else (list(dw) if dw else None)
         logger.info("_dynamic_densities: %s", self._dynamic_densities)
+        # entries SENT per bucket-step this epoch (reference :420,136-144 keep the
+        # per-call counts and average them at the epoch boundary); with the
+        # fused k_cap record these are min(total, k_cap) -- _epoch_sel keeps the
+        # (sent, total-above-threshold) pairs
         self._selected_num_gradients: List[int] = []
+        self._epoch_sel: List[tuple] = []
+        self._sel_generic: List[tuple] = []
 
         self._compress_single = bool(opts.get("compress_single_rank", _env_flag("GKSGD_COMPRESS_SINGLE", False)))
         self._deterministic = bool(opts.get("deterministic", settings.DETERMINISTIC))
@@ -260,8 +266,8 @@ class _DistributedOptimizer(torch.optim.Optimizer):
                 b.extra["mask"] = torch.zeros(b.span, dtype=torch.uint8, device=dev)
                 b.extra["means"] = torch.zeros(2, dtype=torch.float32, device=dev)
                 b.extra["ws"] = ops.sign_bucket_ws(dev)
-        self._sel_dev = torch.zeros(8192, dtype=torch.int32, device=dev)
-        self._sel_host: List[int] = []
+        self._sel_dev = torch.zeros(8192, 2, dtype=torch.int32, device=dev)   # (sent, total) per bucket-step
+        self._sel_host: List[tuple] = []
 
     # ------------------------------------------------------------------
     # hooks
@@ -327,27 +333,68 @@ class _DistributedOptimizer(torch.optim.Optimizer):
     # density schedule / logging (reference :136-160)
     # ------------------------------------------------------------------
     def increase_one_epoch(self):
+        # the epoch's counts are those of the density in force during it (logged
+        # before the schedule moves on)
+        self._drain_selected()
+        density = self.get_current_density()
         self.train_epoch += 1
-        counts = self._collect_selected()
+        counts = self._selected_num_gradients
         if rank() == 0:
-            density = self.get_current_density()
             sz = int(np.sum(self._sizes))
             k = max(int(sz * density), 1)
             mean = float(np.mean(counts)) if counts else 0.0
             logger.info("Average number of selected gradients: %f, exact k: %d", mean, k)
             logger.info("The number of selected gradients: %s", counts)
+            totals = [t for _, t in self._epoch_sel]
+            if totals and sum(totals) != sum(counts):
+                logger.info("Average number above the threshold (before the k_cap cut): %f", float(np.mean(totals)))
             if counts:
-                per_iter = mean * len(self._arena.buckets)
-                logger.info("Effective compression ratio: %.1fx", perf.effective_compression_ratio(sz, per_iter))
+                logger.info("Effective compression ratio: %.1fx", self.wire_compression_ratio(density))
         self._selected_num_gradients = []
+        self._epoch_sel = []
 
-    def _collect_selected(self) -> List[int]:
+    def _drain_selected(self) -> List[tuple]:
+        """(sent, total) per bucket-step logged since the last drain (one D2H
+        copy); also appended to the epoch's lists."""
         n = self._sel_n
-        out = [int(x) for x in self._sel_dev[:n].cpu().tolist()] if n else []
-        out = self._selected_num_gradients + self._sel_host + out
+        dev = [tuple(int(v) for v in x) for x in self._sel_dev[:n].cpu().tolist()] if n else []
+        out = self._sel_generic + self._sel_host + dev
+        self._sel_generic = []
         self._sel_host = []
         self._sel_n = 0
+        self._epoch_sel.extend(out)
+        self._selected_num_gradients.extend(s for s, _ in out)
         return out
+
+    def _collect_selected(self, with_totals: bool = False) -> list:
+        """Counts of the bucket-steps since the last call (a display window):
+        entries sent, or (sent, total) pairs with ``with_totals``.  The epoch
+        summary (increase_one_epoch) still sees every window."""
+        pairs = self._drain_selected()
+        return pairs if with_totals else [s for s, _ in pairs]
+
+    def wire_bytes_per_step(self, density: Optional[float] = None) -> int:
+        """Bytes one rank puts on the wire per step: the fixed-size record of
+        every sparse bucket ((4 + 2 k_cap) int32 words), the dense fp32 bucket
+        otherwise (the sign-bucket compressor: two fp32 means)."""
+        comp = self._compression
+        name = getattr(comp, "name", "none")
+        total = 0
+        for b in self._arena.buckets:
+            d = self.get_current_density(b.name) if density is None else density
+            if self._sparse and d < 1 and hasattr(comp, "k_of"):
+                total += (ops.REC_HDR + 2 * comp.k_cap_for(comp.k_of(b.numel, d), b.numel)) * 4
+            elif name == "bucket":
+                total += 8
+            else:
+                total += b.numel * 4
+        return total
+
+    def wire_compression_ratio(self, density: Optional[float] = None) -> float:
+        """Dense fp32 gradient bytes / bytes actually exchanged per rank and step."""
+        sz = int(np.sum(self._sizes))
+        wb = self.wire_bytes_per_step(density)
+        return (sz * 4.0) / wb if wb else 1.0
 
     def get_current_density(self, name=None):
         density = self._density
@@ -473,7 +520,7 @@ class _DistributedOptimizer(torch.optim.Optimizer):
             with trace.range("gk/b%d/decompress" % b.index):
                 ops.scatter_add_records_(g, gathered, max(self._world, 1), k_cap, 1.0 / max(self._world, 1), True)
             b.extra["agg_done"] = True
-        self._log_selected(b.bufs.record[1:2])
+        self._log_selected(b.bufs.record[0:2])
         if settings.LOGGING_GRADIENTS and self._rank == 0 and self._gradient_path and \
                 self.train_iter % max(1, settings.DUMP_GRAD_EVERY) == 0:
             self._queue_dump(b, b.slice(self._arena.residuals), rec, k_cap)
@@ -510,7 +557,7 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         # residuals are per rank: qualify the group name so the virtual ranks of
         # an in-process world never share (and corrupt) one residual
         tensor, ctx, values = comp.compress(flat, "%s@rank%d" % (b.name, self._rank), ratio=density)
-        self._selected_num_gradients.append(int(ctx.numel()))
+        self._sel_generic.append((int(ctx.numel()), int(ctx.numel())))
         if settings.LOGGING_GRADIENTS and self._rank == 0 and self._gradient_path:
             np.save("%s/r%d_gradients_iter_%d" % (self._gradient_path, self._rank, self.train_iter),
                     tensor.detach().cpu().numpy())
@@ -562,20 +609,21 @@ class _DistributedOptimizer(torch.optim.Optimizer):
             return
         self._exchanger.allreduce_(t, average=True)
 
-    def _log_selected(self, hdr_total: torch.Tensor):
+    def _log_selected(self, hdr: torch.Tensor):
+        """Queue a record header's (sent, total) words (device copy, no sync)."""
         if self._is_cuda and torch.cuda.is_current_stream_capturing():
             # whole-step graph capture: the replayed copy lands in a slot of its
             # own; train/graph.py logs the slots after every replay
-            slot = torch.zeros(1, dtype=torch.int32, device=hdr_total.device)
-            slot.copy_(hdr_total.view(-1)[:1], non_blocking=True)
+            slot = torch.zeros(2, dtype=torch.int32, device=hdr.device)
+            slot.copy_(hdr.view(-1)[:2], non_blocking=True)
             self._graph_sel.append(slot)
             return
-        if self._sel_n == self._sel_dev.numel():
+        if self._sel_n == self._sel_dev.shape[0]:
             # ring full (long epochs x many buckets): flush to the host -- one
             # sync per 8192 bucket-steps, nothing is overwritten
-            self._sel_host.extend(int(x) for x in self._sel_dev.cpu().tolist())
+            self._sel_host.extend(tuple(int(v) for v in x) for x in self._sel_dev.cpu().tolist())
             self._sel_n = 0
-        self._sel_dev[self._sel_n:self._sel_n + 1].copy_(hdr_total, non_blocking=True)
+        self._sel_dev[self._sel_n].copy_(hdr.view(-1)[:2], non_blocking=True)
         self._sel_n += 1
 
     def _queue_dump(self, b, r, rec, k_cap):
@@ -632,9 +680,15 @@ class _DistributedOptimizer(torch.optim.Optimizer):
                     if b.launched:
                         cur.wait_event(b.done_event)
             for b in self._arena.buckets:
+                if b.launched:
+                    b.extra["agg_done"] = False if self._pending_apply else True
+                else:
+                    # no gradients reached this bucket this step: its gathered
+                    # records are from an earlier step and must not be re-applied
+                    b.extra["agg"] = None
+                    b.extra["agg_done"] = True
                 b.ready = 0
                 b.launched = False
-                b.extra["agg_done"] = False if self._pending_apply else True
             if any_ready:
                 self.train_iter += 1
             self._flush_dumps()

@@ -139,3 +139,31 @@ def install_bf16_shadow(model: nn.Module, opt) -> int:
         model.register_load_state_dict_post_hook(lambda m, keys: opt.refresh_shadow())
         model._gk_shadow_hooked = True
     return count
+
+
+def install_direct_grads(model: nn.Module, opt) -> int:
+    """fp32 counterpart of ``install_bf16_shadow`` (the reference's precision:
+    fp32 weights, activations and gradients, settings.py:28): no shadow
+    weights, but the hand-written kernels add their weight gradients straight
+    into the optimizer's fp32 gradient arena -- FastConv2d's grad-weight GEMM
+    (ops/conv1x1.py fp32 path) and BNAct's backward (gamma / beta) -- so
+    AccumulateGrad launches nothing for them.  Returns the number of
+    parameters on the direct path."""
+    arena = opt.arena
+    names = opt._parameter_names
+    count = 0
+    for mod in model.modules():
+        if isinstance(mod, FastConv2d) and not isinstance(mod, StemConv):
+            table = {}
+            for pname in ("weight", "bias"):
+                p = getattr(mod, pname, None)
+                if p is not None and p in names:
+                    table[pname] = opt._make_sink(names[p])
+                    count += 1
+            if table:
+                mod._gk_direct_grads = table
+        elif isinstance(mod, BNAct) and mod.affine:
+            if mod.weight in names and mod.bias in names:
+                mod._gk_direct = (arena.grad_views[names[mod.weight]], arena.grad_views[names[mod.bias]])
+                count += 2
+    return count

@@ -125,14 +125,15 @@ def ssgd(dnn, dataset, data_dir, nworkers, lr, batch_size, nsteps_update, max_ep
                 speed = batch_size * nsteps_update / time_per_iter
                 logger.warning("Time per iteration including communication: %f, Speed: %f images/s", time_per_iter,
                                speed)
+                # this window's counts (the optimizer keeps every window for the epoch summary)
                 sel = optimizer._collect_selected() if hasattr(optimizer, "_collect_selected") else []
-                optimizer._selected_num_gradients = list(sel)  # keep for the epoch summary
                 per_iter_sel = float(np.mean(sel)) * len(optimizer.arena.buckets) if sel else 0.0
+                ratio = optimizer.wire_compression_ratio() if hasattr(optimizer, "wire_compression_ratio") else 1.0
                 metrics.write(iter=int(trainer.get_train_iter()), epoch=epoch, rank=rank, time_per_iter=time_per_iter,
                               samples_per_s=speed, samples_per_s_node=speed * nworkers,
                               density=optimizer.get_current_density(),
                               selected_per_iter=per_iter_sel,
-                              compression_ratio=(nparams * 4.0 / (per_iter_sel * 8.0)) if per_iter_sel else 1.0,
+                              compression_ratio=ratio,
                               loss=float(trainer.current_loss()),
                               hbm_gb=(torch.cuda.max_memory_allocated() / 2 ** 30) if trainer.is_cuda else 0.0)
                 times = []
