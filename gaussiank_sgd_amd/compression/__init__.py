@@ -18,11 +18,16 @@ Deliberate deviations:
     101st element of argsort(|x|) -- available as ``topk_legacy``.
   * ``none`` returns a 3-tuple (the reference's 2-tuple crashes its own caller).
   * variable-count selectors send at most ``k_cap`` entries per bucket; the
-    rest stays in the residual (no gradient mass is dropped).  Gaussian-k and
-    DGC select at most ~4k/3 by construction, so their record holds
-    ``ceil(4k/3)`` entries; RedSync (k < nnz < 2k) 2k.
+    rest stays in the residual (no gradient mass is dropped).  The record
+    holds ``ceil(4k/3)`` entries for Gaussian-k and DGC,
+    2k for RedSync (k < nnz < 2k).  When the reference rule's threshold
+    passes more than k_cap entries (heavy-tailed buckets: the reference's
+    <=3-loop tree stops at up to 18x k), the pipeline re-selects by
+    magnitude -- the evaluated candidate threshold with the largest count
+    in [2k/3, k_cap], else the exact radix key at k_cap -- so the record always holds
+    the LARGEST entries; the header's ``total`` keeps the reference count.
   * ``gaussian_cal`` (new, opt-in): calibrated Gaussian-k -- the one-pass
-    count evaluates 16 thresholds around a per-bucket adaptive centre and
+    count evaluates 8 thresholds around a per-bucket adaptive centre and
     picks the count closest to k inside [2k/3, 4k/3], falling back to the
     exact radix key when none qualifies.  ``gaussian`` stays bit-faithful to
     the reference's <=3-loop tree (compression.py:372-381).
@@ -135,7 +140,7 @@ class GaussianCompressor(_SparseCompressor):
 
 
 class GaussianCalCompressor(GaussianCompressor):
-    """Calibrated Gaussian-k (new): 16-candidate adaptive ladder, exact fallback."""
+    """Calibrated Gaussian-k (new): 8-candidate adaptive ladder, exact fallback."""
     name = "gaussian_cal"
     mode = ops.MODE_GAUSSIAN_CAL
 

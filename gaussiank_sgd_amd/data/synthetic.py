@@ -129,43 +129,5 @@ class SyntheticData:
         return [self._batches[i % len(self._batches)] for i in range(n)]
 
 
-class NpzDataset:
-    """Real data from ``<path>`` holding ``x`` and ``y`` arrays (numpy, no pickle)."""
-
-    def __init__(self, path: str, batch_size: int, device="cpu", rank: int = 0, world: int = 1, seed: int = 0):
-        d = np.load(path, allow_pickle=False)
-        self.x = torch.from_numpy(d["x"])
-        self.y = torch.from_numpy(d["y"]).long()
-        self.batch_size = batch_size
-        self.device = torch.device(device)
-        self.rank, self.world = rank, world
-        self.epoch = 0
-        self.seed = seed
-        self._order = None
-        self._pos = 0
-        self._reshuffle()
-
-    def _reshuffle(self):
-        g = torch.Generator()
-        g.manual_seed(self.seed + self.epoch)
-        perm = torch.randperm(self.x.shape[0], generator=g)
-        self._order = perm[self.rank::self.world]
-        self._pos = 0
-
-    def num_samples(self) -> int:
-        return int(self.x.shape[0])
-
-    def __iter__(self):
-        return self
-
-    def __next__(self):
-        if self._pos + self.batch_size > self._order.numel():
-            self.epoch += 1
-            self._reshuffle()
-        idx = self._order[self._pos:self._pos + self.batch_size]
-        self._pos += self.batch_size
-        return self.x[idx].to(self.device, non_blocking=True), self.y[idx].to(self.device, non_blocking=True)
-
-
 def make_data(dataset: str, batch_size: int, device="cpu", **kw) -> SyntheticData:
     return SyntheticData(dataset, batch_size, device, **kw)

@@ -37,6 +37,7 @@ MODE_DGC = 6
 MODE_GAUSSIAN_CAL = 7
 
 CAL_FALLBACK = 16   # record header `chosen` when the calibrated mode used the exact radix key
+OVERFLOW_EXACT = 17  # ... when a threshold mode overflowed k_cap with every candidate (exact top-k_cap)
 CAL_CAND = 8        # calibrated ladder size (gk::kCalCand)
 
 MAX_CAND = 16
@@ -310,6 +311,20 @@ def _cal_decide(bufs: CompressBuffers, k: int, thr: List[float], counts: Sequenc
     return jc, best < 0
 
 
+def _overflow_alt(counts: Sequence[int], k: int, k_cap: int) -> int:
+    """decide_kernel's magnitude-correct overflow rule: the candidate with the
+    largest count in [2k/3, k_cap] (first on ties), -1 when none lands there."""
+    alt, bc = -1, -1
+    for j, c in enumerate(counts):
+        if c <= k_cap and 3 * c >= 2 * k and c > bc:
+            alt, bc = j, c
+    return alt
+
+
+def _key_thr(K: int) -> float:
+    return float(torch.tensor([K & 0x7FFFFFFF], dtype=torch.int32).view(torch.float32))
+
+
 def _cal_ladder(bufs: CompressBuffers, k: int, z: float, mean: float, std: float) -> List[float]:
     import math
     st = bufs.cal
@@ -349,6 +364,17 @@ def compress_cpu_(g: torch.Tensor, r: torch.Tensor, bufs: CompressBuffers, mode:
         stats = (mean, std, meanabs, maxabs)
         bufs.stats.copy_(torch.tensor(stats, dtype=torch.float32))
         k = max(int(k), 1)
+        ref_total = None   # the reference rule's count when it overflowed k_cap
+        allm = torch.ones(n, dtype=torch.bool)
+
+        def reselect(keys, bounds, thr, counts, chosen):
+            # magnitude-correct overflow (decide_kernel): tighter candidate or exact top-k_cap
+            alt = _overflow_alt(counts, k, k_cap)
+            if alt >= 0:
+                return keys >= bounds[alt], alt, thr[alt]
+            m, K, _ = _radix_topk_mask(keys, allm, min(k_cap, n))
+            return m, OVERFLOW_EXACT, _key_thr(K)
+
         if mode == MODE_GAUSSIAN_CAL:
             thr = _cal_ladder(bufs, k, z, mean, std)
             keys = abs_key(acc)
@@ -356,9 +382,12 @@ def compress_cpu_(g: torch.Tensor, r: torch.Tensor, bufs: CompressBuffers, mode:
             counts = [int((keys >= b).sum()) for b in bounds]
             chosen, fallback = _cal_decide(bufs, k, thr, counts, std)
             if fallback:
-                mask, K, _ = _radix_topk_mask(keys, torch.ones(n, dtype=torch.bool), k)
+                mask, K, _ = _radix_topk_mask(keys, allm, k)
                 chosen = CAL_FALLBACK
-                thr_chosen = float(torch.tensor([K & 0x7FFFFFFF], dtype=torch.int32).view(torch.float32))
+                thr_chosen = _key_thr(K)
+            elif counts[chosen] > k_cap:
+                ref_total = counts[chosen]
+                mask, chosen, thr_chosen = reselect(keys, bounds, thr, counts, chosen)
             else:
                 mask = keys >= bounds[chosen]
                 thr_chosen = thr[chosen]
@@ -368,8 +397,12 @@ def compress_cpu_(g: torch.Tensor, r: torch.Tensor, bufs: CompressBuffers, mode:
             bounds = [_bound_from_threshold(t) for t in thr]
             counts = [int((keys >= b).sum()) for b in bounds]
             chosen = _decide(mode, loops, k, counts)
-            mask = keys >= bounds[chosen]
-            thr_chosen = thr[chosen]
+            if counts[chosen] > k_cap:
+                ref_total = counts[chosen]
+                mask, chosen, thr_chosen = reselect(keys, bounds, thr, counts, chosen)
+            else:
+                mask = keys >= bounds[chosen]
+                thr_chosen = thr[chosen]
         elif mode in (MODE_TOPK, MODE_RANDOMK):
             idx = torch.arange(n, dtype=torch.int64)
             if mode == MODE_RANDOMK:
@@ -388,10 +421,20 @@ def compress_cpu_(g: torch.Tensor, r: torch.Tensor, bufs: CompressBuffers, mode:
             skeys = torch.where(sampled, keys + 1, torch.zeros_like(keys))
             smask, Ks, _ = _radix_topk_mask(skeys, sampled, k)
             cand0 = keys >= Ks
-            if int(cand0.sum()) > 4 * k / 3:
-                mask, K, _ = _radix_topk_mask(keys, torch.ones(n, dtype=torch.bool), k)
+            c0 = int(cand0.sum())
+            if c0 > 4 * k / 3:
+                mask, K, _ = _radix_topk_mask(keys, allm, k)
                 chosen = 1
                 thr_chosen = float(torch.tensor([K], dtype=torch.int32).view(torch.float32))
+            elif c0 > k_cap:
+                # only when k_cap < 4k/3: the three evaluated candidates of the GPU ladder
+                _, K, _ = _radix_topk_mask(keys, allm, k)
+                bounds = [Ks, K + 1, K]
+                thr = [float(torch.tensor([max(Ks - 1, 0)], dtype=torch.int32).view(torch.float32)),
+                       _key_thr(K), _key_thr(K)]
+                counts = [int((keys >= b).sum()) for b in bounds]
+                ref_total = c0
+                mask, chosen, thr_chosen = reselect(keys, bounds, thr, counts, 0)
             else:
                 mask = cand0
                 chosen = 0
@@ -405,7 +448,7 @@ def compress_cpu_(g: torch.Tensor, r: torch.Tensor, bufs: CompressBuffers, mode:
         rec = bufs.record
         rec.zero_()
         rec[0] = sent
-        rec[1] = min(total, 0x7FFFFFFF)
+        rec[1] = min(total if ref_total is None else ref_total, 0x7FFFFFFF)
         rec[2] = chosen
         rec[3] = torch.tensor([thr_chosen], dtype=torch.float32).view(torch.int32)[0]
         rec[REC_HDR:REC_HDR + sent] = sel.to(torch.int32)

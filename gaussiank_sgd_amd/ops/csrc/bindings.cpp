@@ -698,8 +698,7 @@ struct RcclEngine : torch::CustomClassHolder {
     comm.allgather_many(sp, rp, nb, cur_stream(sends[0]));
   }
 
-  void group_start() { comm.group_start(); }
-  void group_end() { comm.group_end(); }
+  void inject_failure(std::string why) { comm.inject_failure(why); }
   void destroy() { comm.destroy(); }
   int64_t rank() const { return comm.rank(); }
   int64_t world() const { return comm.world(); }
@@ -1484,8 +1483,7 @@ TORCH_LIBRARY(gksgd, m) {
       .def("in_flight", &RcclEngine::in_flight)
       .def("reset_stats", &RcclEngine::reset_stats)
       .def("stats", &RcclEngine::stats)
-      .def("group_start", &RcclEngine::group_start)
-      .def("group_end", &RcclEngine::group_end)
+      .def("inject_failure", &RcclEngine::inject_failure)
       .def("destroy", &RcclEngine::destroy)
       .def("rank", &RcclEngine::rank)
       .def("world", &RcclEngine::world);

@@ -30,7 +30,7 @@ RcclComm::~RcclComm() {
   // Never abort from a destructor; communicator teardown is explicit.
   stop_watchdog();
   if (comm_ != nullptr) {
-    ncclCommDestroy(comm_);
+    if (!aborted_.load()) ncclCommDestroy(comm_);   // an aborted communicator is already freed
     comm_ = nullptr;
   }
 }
@@ -72,10 +72,11 @@ void RcclComm::destroy() {
     for (hipEvent_t e : pool_) hipEventDestroy(e);
     pool_.clear();
   }
+  std::lock_guard<std::mutex> ek(enq_mu_);
   if (comm_ != nullptr) {
     ncclComm_t c = comm_;
     comm_ = nullptr;
-    GK_NCCL_CHECK(ncclCommDestroy(c));
+    if (!aborted_.load()) GK_NCCL_CHECK(ncclCommDestroy(c));
   }
 }
 
@@ -153,25 +154,58 @@ int RcclComm::retire_locked(bool check_timeout) {
   return (int)pending_.size();
 }
 
+// Failure protocol (watchdog thread vs the owning thread's enqueues):
+//  * fail() only marks the failure (under mu_); it never touches comm_.
+//  * every collective is enqueued under enq_mu_ after check(), so once
+//    failed_ is set no NEW enqueue reads comm_;
+//  * abort_comm() -- outside mu_ -- waits (bounded) for an enqueue already
+//    past its check() to leave enq_mu_, then aborts.  If that enqueue is
+//    itself stuck inside RCCL (a dead peer during lazy connection setup) the
+//    grace period ends and the abort runs concurrently with it, which is what
+//    ncclCommAbort exists for (it releases blocked calls and spinning kernels).
+//  * comm_ stays a valid handle value; only the owner's destroy() clears it,
+//    and an aborted communicator is never destroyed again.
 void RcclComm::fail(const std::string& why) {
   bool expected = false;
   if (!failed_.compare_exchange_strong(expected, true)) return;
   error_ = why;
   std::fprintf(stderr, "[gk::RcclComm] %s -- aborting the communicator\n", why.c_str());
-  if (comm_ != nullptr) {
-    ncclCommAbort(comm_);   // releases RCCL kernels spinning on a dead peer
-    comm_ = nullptr;
+}
+
+void RcclComm::abort_comm() {
+  if (!failed_.load() || aborted_.load()) return;
+  std::unique_lock<std::mutex> ek(enq_mu_, std::defer_lock);
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(abort_grace_ms_);
+  while (!ek.try_lock()) {
+    if (std::chrono::steady_clock::now() >= deadline) break;
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
   }
+  bool expected = false;
+  if (comm_ != nullptr && aborted_.compare_exchange_strong(expected, true))
+    ncclCommAbort(comm_);   // releases RCCL kernels spinning on a dead peer
+}
+
+void RcclComm::inject_failure(const std::string& why) {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    fail(why);
+  }
+  abort_comm();
 }
 
 int RcclComm::poll() {
-  std::lock_guard<std::mutex> lk(mu_);
-  if (comm_ != nullptr && !failed_.load()) {
-    ncclResult_t st = ncclSuccess;
-    if (ncclCommGetAsyncError(comm_, &st) == ncclSuccess && st != ncclSuccess && st != ncclInProgress)
-      fail(std::string("asynchronous RCCL error: ") + rccl_error_string(st));
+  int left;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (comm_ != nullptr && !failed_.load()) {
+      ncclResult_t st = ncclSuccess;
+      if (ncclCommGetAsyncError(comm_, &st) == ncclSuccess && st != ncclSuccess && st != ncclInProgress)
+        fail(std::string("asynchronous RCCL error: ") + rccl_error_string(st));
+    }
+    left = retire_locked(true);
   }
-  return retire_locked(true);
+  abort_comm();   // no-op unless this poll (or an earlier one) failed the communicator
+  return left;
 }
 
 void RcclComm::watchdog_loop() {
@@ -227,6 +261,7 @@ int RcclComm::in_flight() const {
 // collectives
 // ---------------------------------------------------------------------------
 void RcclComm::allgather_bytes(const void* send, void* recv, size_t bytes, hipStream_t s) {
+  std::lock_guard<std::mutex> ek(enq_mu_);   // see the failure protocol above fail()
   hipEvent_t st;
   begin_op(s, &st);
   GK_NCCL_CHECK(ncclAllGather(send, recv, bytes, ncclUint8, comm_, s));
@@ -238,6 +273,7 @@ void RcclComm::allgather_many(const std::vector<const void*>& sends, const std::
   if (sends.size() != recvs.size() || sends.size() != bytes.size())
     throw std::invalid_argument("allgather_many: list lengths differ");
   if (sends.empty()) return;
+  std::lock_guard<std::mutex> ek(enq_mu_);
   hipEvent_t st;
   begin_op(s, &st);
   size_t total = 0;
@@ -255,6 +291,7 @@ void RcclComm::allgather_many(const std::vector<const void*>& sends, const std::
 }
 
 void RcclComm::allreduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s) {
+  std::lock_guard<std::mutex> ek(enq_mu_);
   hipEvent_t st;
   begin_op(s, &st);
   GK_NCCL_CHECK(ncclAllReduce(buf, buf, count, dt, op, comm_, s));
@@ -265,16 +302,11 @@ void RcclComm::allreduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t
 }
 
 void RcclComm::broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t s) {
+  std::lock_guard<std::mutex> ek(enq_mu_);
   hipEvent_t st;
   begin_op(s, &st);
   GK_NCCL_CHECK(ncclBroadcast(buf, buf, count, dt, root, comm_, s));
   end_op(s, st, kOpBroadcast, count);
 }
-
-void RcclComm::group_start() {
-  check();
-  GK_NCCL_CHECK(ncclGroupStart());
-}
-void RcclComm::group_end() { GK_NCCL_CHECK(ncclGroupEnd()); }
 
 }  // namespace gk

@@ -66,8 +66,6 @@ class RcclComm {
                       const std::vector<size_t>& bytes, hipStream_t s);
   void allreduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s);
   void broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t s);
-  void group_start();
-  void group_end();
 
   // completion tracking / failure detection
   void set_tracking(bool on) { tracking_ = on; }
@@ -82,6 +80,9 @@ class RcclComm {
   OpStats stats(int op) const;
   void reset_stats();
   int in_flight() const;
+  // test hook: fail + abort as the watchdog would, from the calling thread
+  void inject_failure(const std::string& why);
+  void set_abort_grace_ms(int ms) { abort_grace_ms_ = ms < 0 ? 0 : ms; }
 
  private:
   struct Pending {
@@ -94,7 +95,8 @@ class RcclComm {
   void begin_op(hipStream_t s, hipEvent_t* start);
   void end_op(hipStream_t s, hipEvent_t start, int op, size_t bytes);
   int retire_locked(bool check_timeout);
-  void fail(const std::string& why);
+  void fail(const std::string& why);   // caller holds mu_; marks only
+  void abort_comm();                    // caller holds neither lock
   void watchdog_loop();
 
   ncclComm_t comm_ = nullptr;
@@ -107,6 +109,9 @@ class RcclComm {
   std::vector<hipEvent_t> pool_;
   OpStats stats_[kNumOps];
   std::atomic<bool> failed_{false};
+  std::atomic<bool> aborted_{false};
+  std::mutex enq_mu_;   // held for each collective enqueue (check + RCCL call)
+  int abort_grace_ms_ = 2000;
   std::string error_;
   double timeout_s_ = 0.0;
   double poll_ms_ = 5.0;

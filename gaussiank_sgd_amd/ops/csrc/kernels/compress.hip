@@ -21,7 +21,13 @@
 //   gaussian2 :405-435  same, <=5 loops, no residual add
 //   redsync   :623-691, redsynctrim :694-738, dgcsampling :555-620
 // Deviation (documented in SURVEY 2.3/7.4): the record holds at most k_cap
-// entries; selected elements beyond k_cap stay in the residual.
+// entries.  When the reference rule's threshold passes more than k_cap
+// entries, decide re-selects by magnitude: the tightest-fitting evaluated
+// candidate (the largest count in [2k/3, k_cap] -- a higher threshold, so a
+// subset of the largest |x|), or, when no candidate lands there, the exact
+// radix key at k_cap (top-k_cap, conditional passes).  The record therefore always
+// holds the largest entries; everything unsent stays in the residual, and the
+// header's `total` keeps the reference rule's count.
 #include <cstdlib>
 
 #include "common.h"
@@ -510,10 +516,13 @@ __global__ __launch_bounds__(kBlock) void finalize_kernel(GkCtrl* __restrict__ c
   ctrl->radix_kremain[0] = rkrem[0]; ctrl->radix_kremain[1] = rkrem[1];
   ctrl->k_eff = rkeff[1];
   ctrl->fallback = 0;
+  ctrl->ref_total = -1;
 }
 
-// Calibrated mode, no candidate in [2k/3, 4k/3]: resolve the exact radix key
-// (k-th largest |x|) from the conditional histogram passes; the second count /
+// Calibrated mode with no candidate in [2k/3, 4k/3] (k = k_eff), or a
+// threshold mode whose every candidate overflows k_cap (k = k_cap): resolve
+// the exact radix key (k-th largest |x|) from the conditional histogram
+// passes; the second count /
 // decide / select then run exactly as in top-k mode.
 __global__ __launch_bounds__(kBlock) void cal_fallback_kernel(GkCtrl* __restrict__ ctrl, const uint32_t* hist_exact,
                                                               int64_t k) {
@@ -600,7 +609,7 @@ __global__ __launch_bounds__(kBlock) void decide_kernel(GkCtrl* __restrict__ ctr
   __shared__ int64_t s_quota;
   if (cond) {
     if (ctrl->fallback == 0) return;
-    mode = kModeTopK;   // second decide of a calibrated fallback: exact top-k on the radix key
+    mode = kModeTopK;   // second decide of a fallback: exact top-k (or top-k_cap) on the radix key
   }
   const int nc = ctrl->ncand;
   // totals per candidate
@@ -692,8 +701,26 @@ __global__ __launch_bounds__(kBlock) void decide_kernel(GkCtrl* __restrict__ ctr
       if ((double)tot[0] > 4.0 * kd / 3.0) { chosen = 1; gt = 1; ge = 2; quota = ctrl->radix_kremain[1]; }
       else chosen = 0;
     }
+    // magnitude-correct overflow: the threshold choice passes more than k_cap
+    // entries -> the evaluated candidate with the largest count in
+    // [2k/3, k_cap] (a higher threshold: the largest entries), else the exact
+    // key at k_cap
+    if (!cond && ge < 0 && !s_stop && tot[chosen] > k_cap) {
+      ctrl->ref_total = tot[chosen];
+      int alt = -1;
+      int64_t bc = -1;
+      for (int j = 0; j < nc; ++j)
+        if (tot[j] <= k_cap && 3 * tot[j] >= 2 * k && tot[j] > bc) { bc = tot[j]; alt = j; }
+      if (alt >= 0) {
+        chosen = alt;
+      } else {
+        s_stop = 1;
+        ctrl->fallback = 2;
+      }
+    }
     if (ge < 0) gt = chosen;
-    s_chosen = cond ? kCalFallback : chosen; s_gt = gt; s_ge = ge; s_quota = quota;
+    s_chosen = cond ? (ctrl->fallback == 2 ? kOverflowExact : kCalFallback) : chosen;
+    s_gt = gt; s_ge = ge; s_quota = quota;
     ctrl->chosen = s_chosen;
     ctrl->sel_bound = ctrl->bound[gt];
     ctrl->eq_key = ge >= 0 ? ctrl->bound[ge] : 0xffffffffu;
@@ -702,9 +729,9 @@ __global__ __launch_bounds__(kBlock) void decide_kernel(GkCtrl* __restrict__ ctr
   }
   __syncthreads();
   if (s_stop) {
-    // calibrated mode without a candidate in range: clear the exact-key
-    // histograms for the conditional radix passes; offsets come from the
-    // second (conditional) count / decide
+    // fallback to the exact key: clear the exact-key histograms for the
+    // conditional radix passes; offsets and header come from the second
+    // (conditional) count / decide
     for (int i = threadIdx.x; i < kHistSet; i += kBlock) hist_reset[i] = 0u;
     return;
   }
@@ -753,8 +780,9 @@ __global__ __launch_bounds__(kBlock) void decide_kernel(GkCtrl* __restrict__ ctr
     const int64_t sent = total < k_cap ? total : k_cap;
     ctrl->total = total;
     ctrl->sent = sent;
+    const int64_t rt = ctrl->ref_total >= 0 ? ctrl->ref_total : total;
     hdr[0] = (int32_t)sent;
-    hdr[1] = (int32_t)(total > 0x7fffffff ? 0x7fffffff : total);
+    hdr[1] = (int32_t)(rt > 0x7fffffff ? 0x7fffffff : rt);
     hdr[2] = s_chosen;
     hdr[3] = __float_as_int(ctrl->thr);
   }
@@ -990,15 +1018,14 @@ void compress(const CompressArgs& a, hipStream_t s) {
     launch_select<kKeyHash>(a, w, vec_r, G, chunk_tiles, ctrl, out_idx, out_val, s);
   } else {
     launch_count<kKeyAbs>(a, w, vec_r, G, chunk_tiles, ctrl, 0, s);
-    static const bool cal_fallback = [] {
-      const char* e = getenv("GKSGD_CAL_FALLBACK");   // "0": measure the pipeline without the exact fallback
-      return e == nullptr || e[0] != '0';
-    }();
-    if (a.mode == kModeGaussianCal && cal_fallback) {
-      // conditional exact-top-k fallback: every kernel below exits at once
-      // unless the decide above found no candidate in [2k/3, 4k/3]
-      launch_radix<kKeyAbs>(a.r, a.n, a.seed, 0u, keff, hist_exact, vec_r, nullptr, ctrl, s);
-      hipLaunchKernelGGL(cal_fallback_kernel, dim3(1), dim3(kBlock), 0, s, ctrl, hist_exact, keff);
+    if (a.mode != kModeTopK) {
+      // conditional exact fallback: every kernel below exits at once unless
+      // the decide above set ctrl->fallback -- calibrated mode without a
+      // candidate in [2k/3, 4k/3] (top-k), or a threshold mode whose every
+      // candidate overflows k_cap (top-k_cap)
+      const int64_t kfb = a.mode == kModeGaussianCal ? keff : (a.k_cap < a.n ? a.k_cap : a.n);
+      launch_radix<kKeyAbs>(a.r, a.n, a.seed, 0u, kfb, hist_exact, vec_r, nullptr, ctrl, s);
+      hipLaunchKernelGGL(cal_fallback_kernel, dim3(1), dim3(kBlock), 0, s, ctrl, hist_exact, kfb);
       launch_count<kKeyAbs>(a, w, vec_r, G, chunk_tiles, ctrl, 1, s);
     }
     launch_select<kKeyAbs>(a, w, vec_r, G, chunk_tiles, ctrl, out_idx, out_val, s);

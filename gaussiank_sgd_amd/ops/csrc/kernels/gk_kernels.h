@@ -22,13 +22,16 @@ enum Mode : int {
   kModeRandomK = 4,       // k smallest hashes: a uniformly random k-subset
   kModeThreshold = 5,     // fixed threshold |x| > t
   kModeDGC = 6,           // 1% sample threshold, exact top-k when > 4k/3 (compression.py:555-620)
-  kModeGaussianCal = 7,   // calibrated Gaussian-k: 16-candidate ladder around a per-bucket adaptive
-                          // centre, closest count to k in [2k/3, 4k/3], exact radix top-k otherwise
+  kModeGaussianCal = 7,   // calibrated Gaussian-k: 8-candidate ladder (kCalCand) around a per-bucket
+                          // adaptive centre, closest count to k in [2k/3, 4k/3], exact radix top-k otherwise
 };
 
-// Fallback marker written to the record header's `chosen` word when the
-// calibrated mode found no candidate in range and used the exact radix key.
+// Fallback markers written to the record header's `chosen` word: the
+// calibrated mode found no candidate in range and used the exact radix key
+// (top-k); a threshold mode's choice exceeded k_cap and no evaluated
+// candidate fitted, so the exact radix key at k_cap was used (top-k_cap).
 constexpr int kCalFallback = 16;
+constexpr int kOverflowExact = 17;
 
 constexpr int kMaxCand = 16;
 constexpr int kRecHdr = 4;   // packed record header words: sent, total, chosen, thr
@@ -61,8 +64,12 @@ struct GkCtrl {
   double cal_c;         // ladder centre / sigma
   double cal_step;      // log spacing of the ladder
   int64_t cal_k;        // k the state was calibrated for (re-initialised when k changes)
-  int32_t fallback;     // this call fell back to the exact radix key
+  int32_t fallback;     // this call fell back to the exact radix key (1: top-k, 2: top-k_cap)
   int32_t pad1;
+  // entries above the reference rule's threshold when that exceeded k_cap and
+  // the selection moved to a tighter candidate / the exact key (header word
+  // `total`); -1 when the reference choice fitted
+  int64_t ref_total;
 };
 
 struct Chunk;

@@ -1,4 +1,4 @@
-"""Layer-wise backward profiler and phase timers.
+"""Layer-wise backward profiler.
 
 Parity: reference profiling.py:13-148 -- ``benchmark(trainer)`` runs
 5 warm-up + 50 measured forward/backward passes, timestamps every
@@ -8,10 +8,9 @@ calls ``torch.cuda.synchronize()`` inside every hook; here each hook records
 a HIP event on the current stream instead (no device-wide sync inside
 backward), and the event deltas are read once after the pass.
 
-``PhaseTimer`` measures named phases with HIP events (GPU) or wall clock
-(CPU) and emits roctx ranges through ``utils/trace.py`` (visible in
-rocprofv3 --marker-trace / omnitrace); the trainer times forward / backward /
-update with it when ``DLTrainer(phase_timer=True)``.
+Phase ranges (forward / backward / compress / exchange / update) are roctx
+ranges emitted by ``utils/trace.py`` (rocprofv3 --marker-trace); the
+optimizer's per-bucket timers are ``DistributedOptimizer(profiling=True)``.
 """
 from __future__ import annotations
 
@@ -119,44 +118,3 @@ def benchmark(trainer, warmup: int = 5, iterations: int = 50):
     sizes = p.get_backward_key_sizes()
     p.remove()
     return keys[::-1], list(times[::-1]), sizes[::-1]
-
-
-class PhaseTimer:
-    """Accumulates named phase durations; ``with timer('compress'):`` ..."""
-
-    def __init__(self, cuda: bool = True, roctx: bool = True):
-        self.cuda = cuda and torch.cuda.is_available()
-        if roctx:
-            trace.enable(True)
-        self._pending: List[Tuple[str, object, object]] = []
-        self.totals: Dict[str, float] = defaultdict(float)
-        self.counts: Dict[str, int] = defaultdict(int)
-
-    @contextlib.contextmanager
-    def __call__(self, name: str):
-        trace.push(name)
-        if self.cuda:
-            a = torch.cuda.Event(enable_timing=True)
-            a.record()
-        else:
-            a = time.time()
-        try:
-            yield
-        finally:
-            if self.cuda:
-                b = torch.cuda.Event(enable_timing=True)
-                b.record()
-                self._pending.append((name, a, b))
-            else:
-                self.totals[name] += time.time() - a
-                self.counts[name] += 1
-            trace.pop()
-
-    def flush(self) -> Dict[str, float]:
-        if self._pending:
-            torch.cuda.synchronize()
-            for name, a, b in self._pending:
-                self.totals[name] += a.elapsed_time(b) / 1e3
-                self.counts[name] += 1
-            self._pending = []
-        return {k: self.totals[k] / max(1, self.counts[k]) for k in self.totals}

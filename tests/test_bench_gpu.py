@@ -51,13 +51,23 @@ def test_bench_resnet50_two_ranks_one_gpu(cuda):
     assert out["exchange"] == "torch"
     assert out["replicas_consistent"] is True
     assert out["value"] > 0 and out["ms_per_step"] > 0
-    assert out["selected_over_k"] > 0        # reference <=3-loop tree: anywhere around k
+    # headline precision is the reference's fp32; the bf16 phase is a second timed loop
+    assert out["dtype"] == "fp32"
+    assert out["bf16_value"] > 0 and out["bf16_ms_per_step"] > 0
+    # sent <= k_cap per bucket; the header's total keeps the reference rule's count
+    assert 0 < out["selected_over_k"] <= 4.0 / 3.0 + 1e-3
+    assert out["candidates_per_step"] >= out["selected_per_step"]
     # wire ratio: dense fp32 bytes / fixed record bytes, k_cap = ceil(4k/3)
     assert 300 <= out["effective_compression_ratio"] <= 400
+    assert out["exposed_comm_ms"] is not None and out["exposed_comm_ms"] >= 0
+    # dense comparator: bucketed (25 MB), backward-overlapped all-reduce after the sparse loop
+    assert out["dense_ms_per_step"] > 0 and out["dense_buckets"] > 1
+    assert out["speedup_vs_dense"] == pytest.approx(out["dense_ms_per_step"] / out["ms_per_step"], rel=1e-2)
 
 
 def test_bench_dense_two_ranks_one_gpu(cuda):
-    out = _bench("--model", "resnet20", "--steps", "3", "--warmup", "1", "--batch-size", "64", "--dense", probe=True)
+    out = _bench("--model", "resnet20", "--steps", "3", "--warmup", "1", "--batch-size", "64", "--dense",
+                 "--no-bf16-phase", probe=True)
     assert out["replicas_consistent"] is True and out["config"]["compressor"] == "none"
     # the post-run fabric probe (alpha-beta of all-gather / all-reduce through the bench's exchanger)
     c = out["collectives"]

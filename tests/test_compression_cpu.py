@@ -98,6 +98,40 @@ def test_conservation_and_cap():
     rebuilt = rr.clone()
     rebuilt[idx] += val
     assert torch.equal(rebuilt, acc)
+    # overflow is cut by magnitude (exact top-k_cap), not by index order
+    assert int(rec[2]) == ops.OVERFLOW_EXACT
+    assert set(idx.tolist()) == set(torch.topk(acc.abs(), k_cap).indices.tolist())
+
+
+@pytest.mark.parametrize("k_cap_mult", [4.0 / 3.0, 1.0, 3.0])
+def test_gaussian_overflow_sends_largest(k_cap_mult):
+    """Heavy-tailed bucket: the reference tree stops far above k (the VGG /
+    multi-bucket case).  The record must hold <= k_cap entries that are the
+    LARGEST |x| (every sent magnitude >= every unsent one), the header keeps
+    the reference rule's count, and nothing is lost (conservation)."""
+    g = torch.Generator().manual_seed(11)
+    n = 200_000
+    x = torch.randn(n, generator=g) * 1e-4
+    x[torch.randperm(n, generator=g)[: n // 2]] = 0.0      # heavy-zero gradient (ReLU nets)
+    hot = torch.randperm(n, generator=g)[: n // 50]         # 2% outliers dominate sigma
+    x[hot] = (1.0 + torch.rand(hot.numel(), generator=g)) * torch.sign(torch.randn(hot.numel(), generator=g))
+    r = torch.zeros(n)
+    ratio = 0.001
+    k = int(n * ratio)
+    k_cap = max(1, math.ceil(k * k_cap_mult))
+    _, rr, rec, idx, val, _ = _mirror(x, r, ops.MODE_GAUSSIAN, k, k_cap, z=gaussian_z(ratio))
+    acc = x + r
+    ref_total = int(reference.gaussian(x, r, ratio, loops=3, ec=True)[1].numel())
+    assert int(rec[1]) == ref_total and ref_total > k_cap        # the reference overflows
+    sent = int(rec[0])
+    assert 0 < sent <= k_cap
+    unsent = torch.ones(n, dtype=torch.bool)
+    unsent[idx] = False
+    assert float(val.abs().min()) >= float(acc.abs()[unsent].max())
+    assert bool((idx[1:] > idx[:-1]).all())
+    rebuilt = rr.clone()
+    rebuilt[idx] += val
+    assert torch.equal(rebuilt, acc)
 
 
 def test_dgc_mirror_semantics():

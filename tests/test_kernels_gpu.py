@@ -59,10 +59,17 @@ def test_gaussian_pipeline(cuda, n, loops, ec):
     assert float(xg.abs().sum()) == 0.0
     sent, total, idx, val = _sel(recg, k_cap)
     thr = float(recg[3:4].view(torch.float32))
-    mask = acc.abs() > thr
-    expect = mask.nonzero().view(-1)
-    assert total == int(mask.sum())
-    assert torch.equal(idx, expect[:sent])
+    if int(recg[2]) == ops.OVERFLOW_EXACT:
+        # the reference threshold passed > k_cap: exact top-k_cap by magnitude
+        assert sent == k_cap and total > k_cap
+        unsent = torch.ones(n, dtype=torch.bool)
+        unsent[idx] = False
+        assert float(val.abs().min()) >= float(acc.abs()[unsent].max())
+    else:
+        mask = acc.abs() > thr
+        expect = mask.nonzero().view(-1)
+        assert total == int(mask.sum()) and sent == total
+        assert torch.equal(idx, expect)
     assert torch.equal(val, acc[idx])
     res_expect = acc.clone()
     res_expect[idx] = 0
@@ -146,6 +153,9 @@ def test_threshold_modes_vs_mirror(cuda, mode):
 
 
 def test_kcap_overflow_stays_in_residual(cuda):
+    """Overflow past k_cap: the record holds the k_cap LARGEST entries (exact
+    radix key at k_cap), the header the reference count, the rest stays in
+    the residual (conservation)."""
     n = 1 << 16
     x, r = _pair(n, seed=13)
     k_cap = 10
@@ -153,15 +163,42 @@ def test_kcap_overflow_stays_in_residual(cuda):
     xg, rg = x.clone().to(cuda), r.clone().to(cuda)
     ops.compress_(xg, rg, bufs, ops.MODE_THRESHOLD, ec=True, zero_g=True, k=5, k_cap=k_cap, fixed_thr=0.0)
     torch.cuda.synchronize()
-    sent, total, idx, val = _sel(bufs.record.cpu(), k_cap)
+    rec = bufs.record.cpu()
+    sent, total, idx, val = _sel(rec, k_cap)
     acc = x + r
     nz = (acc.abs() > 0).nonzero().view(-1)
     assert sent == k_cap and total == nz.numel()
-    assert torch.equal(idx, nz[:k_cap])
+    assert int(rec[2]) == ops.OVERFLOW_EXACT
+    assert set(idx.tolist()) == set(torch.topk(acc.abs(), k_cap).indices.tolist())
+    assert bool((idx[1:] > idx[:-1]).all())
     # conservation: acc == scatter(sent) + residual
     rebuilt = rg.cpu().clone()
     rebuilt[idx] += val
     assert torch.equal(rebuilt, acc)
+
+
+@pytest.mark.parametrize("k_cap_mult", [4.0 / 3.0, 1.0, 3.0])
+def test_gaussian_overflow_gpu_matches_mirror(cuda, k_cap_mult):
+    """Heavy-tailed bucket whose reference threshold passes >> k_cap: the GPU
+    record equals the CPU mirror's (exact top-k_cap) and holds the largest
+    |x| -- every sent magnitude >= every unsent one."""
+    n = 200_000
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(n, generator=g) * 1e-4
+    hot = torch.randperm(n, generator=g)[: n // 50]
+    x[hot] = (1.0 + torch.rand(hot.numel(), generator=g)) * torch.sign(torch.randn(hot.numel(), generator=g))
+    r = torch.zeros(n)
+    k = 200
+    k_cap = max(1, math.ceil(k * k_cap_mult))
+    (xg, rg, recg, _), (xc, rc, recc, _) = _run_both(x, r, ops.MODE_GAUSSIAN, k, k_cap, True, 3,
+                                                     gaussian_z(0.001), device=cuda)
+    assert int(recg[1]) > k_cap and int(recg[2]) == ops.OVERFLOW_EXACT
+    assert torch.equal(recg, recc)
+    assert torch.equal(rg, rc)
+    sent, total, idx, val = _sel(recg, k_cap)
+    unsent = torch.ones(n, dtype=torch.bool)
+    unsent[idx] = False
+    assert sent == k_cap and float(val.abs().min()) >= float((x + r).abs()[unsent].max())
 
 
 @pytest.mark.parametrize("deterministic", [False, True])
@@ -373,3 +410,49 @@ def test_rccl_communicator_self_test_world1(cuda):
     c.self_test()
     torch.cuda.synchronize()
     c.destroy()
+
+
+def test_rccl_engine_failure_races_enqueue(cuda):
+    """The watchdog's failure path (inject_failure = fail + abort, what the
+    timeout / async-error poll runs) fired from another thread while the
+    owning thread keeps enqueuing collectives: every enqueue either completes
+    or raises the failure -- none touches the aborted communicator -- and the
+    engine tears down cleanly afterwards (rccl_engine.cpp failure protocol)."""
+    import threading
+    import time
+    cls = ops.rccl_engine_class()
+    e = cls()
+    e.init(cls.unique_id(), 0, 1, 0)
+    e.start_watchdog(600.0, 1.0)
+    t = torch.arange(1 << 16, dtype=torch.float32, device=cuda)
+    out = torch.zeros_like(t)
+    fire = threading.Event()
+
+    def killer():
+        fire.wait()
+        time.sleep(0.002)
+        e.inject_failure("test: injected failure")
+
+    th = threading.Thread(target=killer)
+    th.start()
+    raised = None
+    ok = 0
+    for i in range(20000):
+        if i == 50:
+            fire.set()
+        try:
+            e.allgather(t, out)
+            e.allreduce(t, 1)
+            ok += 1
+        except RuntimeError as err:
+            raised = str(err)
+            break
+    th.join()
+    torch.cuda.synchronize()
+    assert ok >= 50
+    assert raised is not None and "injected failure" in raised, raised
+    assert e.failed() and "injected failure" in e.error()
+    with pytest.raises(RuntimeError):
+        e.allgather(t, out)
+    e.stop_watchdog()
+    e.destroy()
