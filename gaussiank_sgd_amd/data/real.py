@@ -17,7 +17,14 @@ MI355X design:
     background thread into pinned memory, copies it to the GPU on a side
     stream (non_blocking) and runs normalisation / augmentation ON THE GPU
     (random crop + flip + normalise as one batched op), so the training
-    stream never waits for the host.
+    stream never waits for the host;
+  * ImageNet as an image folder (``<root>/train/<class>/*.JPEG``, torchvision
+    ImageFolder layout; the reference's HDF5 reader is broken):
+    ``ImageFolderRows`` decodes with PIL in a thread pool inside the
+    loader's gather thread and applies the reference's host transform --
+    ``RandomResizedCrop(224)`` + horizontal flip for training, ``Resize(256)``
+    + ``CenterCrop(224)`` for evaluation (dl_trainer.py:305-313) -- to uint8;
+    the normalisation runs on the GPU.
 """
 from __future__ import annotations
 
@@ -110,6 +117,113 @@ class _MmapRows:
 def _read_words(path: str) -> List[str]:
     with open(path, "r") as f:
         return f.read().replace("\n", "<eos>").split()
+
+
+IMAGE_EXTS = (".jpg", ".jpeg", ".png", ".bmp", ".ppm", ".webp")
+
+
+def find_image_folder(root: str, train: bool = True) -> Optional[str]:
+    """``root/train`` (``root/val``) when present, else ``root`` itself, if it
+    holds class sub-directories with images."""
+    for cand in ([os.path.join(root, "train")] if train else [os.path.join(root, "val"), os.path.join(root, "test")]) + [root]:
+        if os.path.isdir(cand):
+            subs = [d for d in sorted(os.listdir(cand)) if os.path.isdir(os.path.join(cand, d))]
+            if subs and any(f.lower().endswith(IMAGE_EXTS) for f in os.listdir(os.path.join(cand, subs[0]))):
+                return cand
+    return None
+
+
+def scan_image_folder(folder: str) -> Tuple[List[str], torch.Tensor, List[str]]:
+    """(files, labels, classes): classes = sorted sub-directory names, label =
+    class index (torchvision ImageFolder convention)."""
+    classes = sorted(d for d in os.listdir(folder) if os.path.isdir(os.path.join(folder, d)))
+    files, labels = [], []
+    for ci, c in enumerate(classes):
+        cdir = os.path.join(folder, c)
+        for f in sorted(os.listdir(cdir)):
+            if f.lower().endswith(IMAGE_EXTS):
+                files.append(os.path.join(cdir, f))
+                labels.append(ci)
+    return files, torch.tensor(labels, dtype=torch.int64), classes
+
+
+def random_resized_crop_box(W: int, H: int, rng: np.random.Generator, scale=(0.08, 1.0),
+                            ratio=(3.0 / 4.0, 4.0 / 3.0)) -> Tuple[int, int, int, int]:
+    """torchvision RandomResizedCrop.get_params: (left, top, width, height)."""
+    import math
+    area = H * W
+    log_r = (math.log(ratio[0]), math.log(ratio[1]))
+    for _ in range(10):
+        target = area * rng.uniform(scale[0], scale[1])
+        ar = math.exp(rng.uniform(log_r[0], log_r[1]))
+        w = int(round(math.sqrt(target * ar)))
+        h = int(round(math.sqrt(target / ar)))
+        if 0 < w <= W and 0 < h <= H:
+            top = int(rng.integers(0, H - h + 1))
+            left = int(rng.integers(0, W - w + 1))
+            return left, top, w, h
+    in_ratio = float(W) / float(H)   # fallback: centre crop at the clamped ratio
+    if in_ratio < min(ratio):
+        w, h = W, int(round(W / min(ratio)))
+    elif in_ratio > max(ratio):
+        h, w = H, int(round(H * max(ratio)))
+    else:
+        w, h = W, H
+    return (W - w) // 2, (H - h) // 2, w, h
+
+
+class ImageFolderRows:
+    """An image folder as rows of uint8 [3, size, size] images, decoded on
+    demand (``gather``) with the reference's train / eval host transforms.
+    Randomness is a pure function of (seed, epoch, sample index), so every
+    rank's crops are reproducible and independent of the thread schedule."""
+
+    def __init__(self, folder: str, size: int = 224, train: bool = True, seed: int = 0, workers: int = 8):
+        self.files, self.labels, self.classes = scan_image_folder(folder)
+        if not self.files:
+            raise OSError("no images under %s" % folder)
+        self.size, self.train, self.seed = int(size), bool(train), int(seed)
+        self.shape = (len(self.files), 3, self.size, self.size)
+        self.dtype = torch.uint8
+        self.epoch = 0
+        self._pool = None
+        self._workers = max(1, int(workers))
+
+    def __len__(self) -> int:
+        return len(self.files)
+
+    def load(self, i: int) -> np.ndarray:
+        from PIL import Image
+        with Image.open(self.files[i]) as im:
+            im = im.convert("RGB")
+            S = self.size
+            if self.train:
+                rng = np.random.default_rng((self.seed, self.epoch, int(i)))
+                left, top, w, h = random_resized_crop_box(im.width, im.height, rng)
+                im = im.resize((S, S), Image.BILINEAR, box=(left, top, left + w, top + h))
+                if rng.random() < 0.5:
+                    im = im.transpose(Image.FLIP_LEFT_RIGHT)
+            else:
+                short = int(round(S * 256 / 224))          # Resize(256) for 224 crops
+                if im.width <= im.height:
+                    nw, nh = short, int(short * im.height / im.width)
+                else:
+                    nw, nh = int(short * im.width / im.height), short
+                im = im.resize((nw, nh), Image.BILINEAR)
+                left, top = int(round((nw - S) / 2.0)), int(round((nh - S) / 2.0))
+                im = im.crop((left, top, left + S, top + S))
+            return np.asarray(im, dtype=np.uint8).transpose(2, 0, 1)
+
+    def gather(self, idx: torch.Tensor, out: torch.Tensor) -> None:
+        import concurrent.futures as cf
+        if self._pool is None:
+            self._pool = cf.ThreadPoolExecutor(max_workers=self._workers, thread_name_prefix="gk-decode")
+        ids = [int(i) for i in idx.tolist()]
+        for b, arr in enumerate(self._pool.map(self.load, ids)):
+            out[b].copy_(torch.from_numpy(arr))
+
+    def set_epoch(self, epoch: int) -> None:
+        self.epoch = int(epoch)
 
 
 def ptb_raw_data(data_path: str, prefix: str = "ptb"):
@@ -246,8 +360,7 @@ class DeviceLoader:
                  shuffle: bool = True, seq_first: bool = False):
         self.x, self.y = x, y
         self.device = torch.device(device)
-        self.sampler = ShardedSampler(len(x) if not torch.is_tensor(x) else x.shape[0], batch_size, rank, world,
-                                      seed, shuffle)
+        self.sampler = ShardedSampler(x.shape[0], batch_size, rank, world, seed, shuffle)
         self.transform = transform
         self.train = train
         self.seq_first = seq_first
@@ -269,7 +382,7 @@ class DeviceLoader:
     def _gather(self, idx: torch.Tensor):
         xs = (self.batch_size,) + tuple(self.x.shape[1:])
         xb = torch.empty(xs, dtype=self.x.dtype, pin_memory=self._pin)
-        if isinstance(self.x, _MmapRows):
+        if isinstance(self.x, (_MmapRows, ImageFolderRows)):   # memory-mapped arrays, decoded image folders
             self.x.gather(idx, xb)
         else:
             torch.index_select(self.x, 0, idx, out=xb)
@@ -286,6 +399,8 @@ class DeviceLoader:
                     self._q.put(self._gather(idx))
                 self.epoch += 1
                 self.sampler.set_epoch(self.epoch)
+                if isinstance(self.x, ImageFolderRows):
+                    self.x.set_epoch(self.epoch)
         except BaseException as e:  # noqa: BLE001 - surfaced on the consumer side
             self._q.put(e)
 
@@ -352,6 +467,11 @@ def open_dataset(dataset: str, data_dir: str, batch_size: int, device, rank: int
             x, y = read_mnist_idx(data_dir, train)
         except OSError:
             return None
+    elif dataset == "imagenet" and find_image_folder(data_dir, train) is not None:
+        # image folder: host decode + the reference's crop / flip, GPU normalise
+        rows = ImageFolderRows(find_image_folder(data_dir, train), image_size or 224, train, seed + 7919 * rank)
+        return DeviceLoader(rows, rows.labels, batch_size, device, rank, world, seed,
+                            normalize_transform(IMAGENET_MEAN, IMAGENET_STD, channels_last), train, shuffle=train)
     elif dataset == "ptb":
         if not os.path.isfile(os.path.join(data_dir, "ptb.train.txt")):
             return None

@@ -127,6 +127,47 @@ def record_views(rec: torch.Tensor, k_cap: int) -> Tuple[torch.Tensor, torch.Ten
 _M32 = 0xFFFFFFFF
 
 
+# ---------------------------------------------------------------------------
+# dropout / sampling seeds
+# ---------------------------------------------------------------------------
+_graph_words: dict = {}
+
+
+def graph_seed_word(device) -> torch.Tensor:
+    """The per-device int32 word that captured dropout kernels mix into their
+    seed at run time (train/graph.py writes a new value before every replay)."""
+    device = torch.device(device)
+    w = _graph_words.get(device)
+    if w is None:
+        w = _graph_words[device] = torch.zeros(1, dtype=torch.int32, device=device)
+    return w
+
+
+def set_graph_seed(device, value: int) -> None:
+    """Stream-ordered write of the replay word (before a graph replay)."""
+    v = int(value) & 0xFFFFFFFF
+    graph_seed_word(device).fill_(v - (1 << 32) if v >= (1 << 31) else v)
+
+
+def capture_seed_word(device) -> Optional[torch.Tensor]:
+    """The replay word when the current stream is being captured, else None."""
+    if torch.device(device).type == "cuda" and torch.cuda.is_current_stream_capturing():
+        return graph_seed_word(device)
+    return None
+
+
+def seed_generator() -> torch.Generator:
+    """Host generator of the dropout seeds: derived from the process's torch
+    seed (DLTrainer seeds it) and the rank, so ranks draw different masks and
+    ``--seed`` changes them."""
+    g = getattr(seed_generator, "_g", None)
+    if g is None:
+        import os
+        base = (int(torch.initial_seed()) * 0x9E3779B97F4A7C15 + int(os.environ.get("RANK", "0")) * 7919) & (2 ** 63 - 1)
+        g = seed_generator._g = torch.Generator().manual_seed(base)
+    return g
+
+
 def hash_u32(idx: torch.Tensor, seed: int) -> torch.Tensor:
     """Bit-exact mirror of gk::hash_u32 (murmur3 fmix32 of a Weyl sequence)."""
     i = idx.to(torch.int64) & _M32
@@ -461,8 +502,13 @@ def compress_cpu_(g: torch.Tensor, r: torch.Tensor, bufs: CompressBuffers, mode:
 def compress_(g: torch.Tensor, r: torch.Tensor, bufs: CompressBuffers, mode: int, ec: bool = True,
               zero_g: bool = True, loops: int = 3, z: float = 0.0, k: int = 1, k_cap: Optional[int] = None,
               seed: int = 0, fixed_thr: float = 0.0, sample_p: float = 0.01, n_stats: int = 0,
-              valid: Optional[torch.Tensor] = None, mc: Optional[dict] = None) -> None:
+              valid: Optional[torch.Tensor] = None, mc: Optional[dict] = None,
+              seed_dev: Optional[torch.Tensor] = None) -> None:
     """Sparsify ``g`` (+ residual ``r``) into ``bufs.record``.  Async on GPU.
+
+    ``seed_dev``: optional int32 device word holding the seed (read by the
+    kernels at run time instead of ``seed``): a captured hipGraph replays with
+    whatever the host wrote there before the replay.
 
     ``n_stats``: element count used for mean/std (the real, unpadded bucket
     size; padding elements are zeros and do not change the sums).
@@ -481,6 +527,8 @@ def compress_(g: torch.Tensor, r: torch.Tensor, bufs: CompressBuffers, mode: int
         kw = {}
         if valid is not None:
             kw["valid"] = valid
+        if seed_dev is not None:
+            kw["seed_dev"] = seed_dev
         if mc is not None:
             if not zero_g:
                 raise ValueError("momentum-corrected compress zeroes g")
@@ -492,6 +540,8 @@ def compress_(g: torch.Tensor, r: torch.Tensor, bufs: CompressBuffers, mode: int
                         float(z), float(fixed_thr), float(sample_p), int(k), int(k_cap), int(seed) & 0xFFFFFFFF,
                         int(n_stats), bufs.stats, **kw)
     else:
+        if seed_dev is not None:
+            seed = int(seed_dev.view(-1)[0]) & 0xFFFFFFFF
         u = None
         if mc is not None:
             base = int(mc["base"])

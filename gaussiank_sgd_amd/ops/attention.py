@@ -20,9 +20,8 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
-from . import hash_u32, load
+from . import capture_seed_word, hash_u32, load, seed_generator
 
-_seed_gen = torch.Generator().manual_seed(0xA77E)
 HEAD_DIM = 64
 
 
@@ -42,13 +41,14 @@ def drop_scale(p: float) -> float:
     return 65536.0 / (65536 - thr) if thr else 1.0
 
 
-def dropout_mask(B: int, heads: int, T: int, p: float, seed: int, device) -> torch.Tensor:
-    """The kernels' keep mask as bool [B, heads, T, T] (tests / CPU mirror)."""
+def dropout_mask(B: int, heads: int, T: int, p: float, seed: int, device, seed_dev=None) -> torch.Tensor:
+    """The kernels' keep mask as bool [B, heads, T, T] (tests / CPU mirror);
+    ``seed_dev``: the replay word the captured kernels mixed in."""
     device = torch.device(device)
     if device.type == "cuda":
         load()
         m = torch.empty(B, heads, T, T, dtype=torch.uint8, device=device)
-        _ops().attn_dropout_mask(m, B, heads, T, float(p), int(seed))
+        _ops().attn_dropout_mask(m, B, heads, T, float(p), int(seed), seed_dev)
         return m.bool()
     # one 32-bit hash per pair of keys: low half -> even key, high half -> odd key
     h = hash_u32(torch.arange(B * heads * T * T // 2, dtype=torch.int64), int(seed) & 0xFFFFFFFF)
@@ -73,13 +73,15 @@ def reference_attention(qkv: torch.Tensor, heads: int, p: float = 0.0, seed: int
 
 class _FlashAttnFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, heads, p, seed):
+    def forward(ctx, qkv, heads, p, seed, seed_dev=None):
+        # seed_dev: the graph replay word (ops.graph_seed_word) under capture --
+        # forward and backward of one replay read the same word
         B, T, _ = qkv.shape
         out = torch.empty(B, T, heads * HEAD_DIM, dtype=torch.bfloat16, device=qkv.device)
         lse = torch.empty(B * heads * T, dtype=torch.float32, device=qkv.device)
-        _ops().attn_fwd(qkv, out, lse, int(heads), float(p), int(seed))
+        _ops().attn_fwd(qkv, out, lse, int(heads), float(p), int(seed), seed_dev)
         ctx.save_for_backward(qkv, out, lse)
-        ctx.heads, ctx.p, ctx.seed = int(heads), float(p), int(seed)
+        ctx.heads, ctx.p, ctx.seed, ctx.seed_dev = int(heads), float(p), int(seed), seed_dev
         return out
 
     @staticmethod
@@ -88,8 +90,8 @@ class _FlashAttnFn(torch.autograd.Function):
         dout = dout.to(torch.bfloat16).contiguous()
         delta = torch.empty_like(lse)
         dqkv = torch.empty_like(qkv)
-        _ops().attn_bwd(qkv, out, dout, lse, delta, dqkv, ctx.heads, ctx.p, ctx.seed)
-        return dqkv, None, None, None
+        _ops().attn_bwd(qkv, out, dout, lse, delta, dqkv, ctx.heads, ctx.p, ctx.seed, ctx.seed_dev)
+        return dqkv, None, None, None, None
 
 
 def fused_available(qkv: torch.Tensor, heads: int) -> bool:
@@ -115,6 +117,7 @@ def self_attention(qkv: torch.Tensor, heads: int, p: float = 0.0, training: bool
     p = float(p) if training else 0.0
     if attn_mask is None and fused_available(qkv, heads):
         if seed is None:
-            seed = int(torch.randint(0, 2 ** 31 - 1, (1,), generator=_seed_gen)) if p > 0 else 0
-        return _FlashAttnFn.apply(qkv.to(torch.bfloat16).contiguous(), heads, p, seed)
+            seed = int(torch.randint(0, 2 ** 31 - 1, (1,), generator=seed_generator())) if p > 0 else 0
+        seed_dev = capture_seed_word(qkv.device) if p > 0 else None
+        return _FlashAttnFn.apply(qkv.to(torch.bfloat16).contiguous(), heads, p, seed, seed_dev)
     return _sdpa(qkv, heads, p, attn_mask)

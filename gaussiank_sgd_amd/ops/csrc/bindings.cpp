@@ -41,7 +41,7 @@ void compress(at::Tensor g, at::Tensor r, at::Tensor ctrl, at::Tensor ws, at::Te
               int64_t seed, int64_t n_stats, c10::optional<at::Tensor> stats_out, c10::optional<at::Tensor> valid,
               c10::optional<at::Tensor> u, c10::optional<at::Tensor> w, c10::optional<at::Tensor> chunks,
               int64_t chunk_begin, int64_t chunk_count, int64_t chunk_base, std::vector<double> mc_mu,
-              std::vector<double> mc_wd) {
+              std::vector<double> mc_wd, c10::optional<at::Tensor> seed_dev) {
   check_f32(g, "g");
   check_f32(r, "r");
   check_dev(ctrl, "ctrl");
@@ -73,6 +73,12 @@ void compress(at::Tensor g, at::Tensor r, at::Tensor ctrl, at::Tensor ws, at::Te
   a.k = k < 1 ? 1 : k;
   a.k_cap = k_cap;
   a.seed = (uint32_t)(seed & 0xffffffff);
+  if (seed_dev.has_value() && seed_dev->defined()) {
+    // graph replays: the seed word is refreshed in device memory before each replay
+    check_dev(*seed_dev, "seed_dev");
+    TORCH_CHECK(seed_dev->scalar_type() == at::kInt && seed_dev->numel() >= 1, "seed_dev must be int32[>=1]");
+    a.seed_dev = reinterpret_cast<const uint32_t*>(seed_dev->data_ptr<int32_t>());
+  }
   a.ctrl = ctrl.data_ptr();
   a.ws = ws.data_ptr();
   a.record = record.data_ptr<int32_t>();
@@ -811,6 +817,13 @@ void stem_wgrad(at::Tensor x, at::Tensor dy, at::Tensor out, at::Tensor part) {
                  out.stride(0), out.stride(1), out.stride(2), out.stride(3), cur_stream(x));
 }
 
+// optional device seed word (graph replays): int32[>=1] on the GPU
+const uint32_t* seed_word(const c10::optional<at::Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kInt && t->numel() >= 1, "seed_dev must be a GPU int32[>=1]");
+  return reinterpret_cast<const uint32_t*>(t->data_ptr<int32_t>());
+}
+
 // C[M, N] = A[M, K] . B[N, K]^T
 const float* bias_ptr(const c10::optional<at::Tensor>& b, int64_t N) {
   if (!b.has_value() || !b->defined()) return nullptr;
@@ -1044,7 +1057,8 @@ void check_rows_bf16(const at::Tensor& t, const char* name, int64_t R, int64_t H
 }
 
 void add_ln_forward(at::Tensor a, at::Tensor x, c10::optional<at::Tensor> gamma, c10::optional<at::Tensor> beta,
-                    at::Tensor y, at::Tensor h, at::Tensor mean, at::Tensor rstd, double eps, double p, int64_t seed) {
+                    at::Tensor y, at::Tensor h, at::Tensor mean, at::Tensor rstd, double eps, double p, int64_t seed,
+                    c10::optional<at::Tensor> seed_dev) {
   const int64_t H = x.size(-1), R = x.numel() / H;
   TORCH_CHECK(gk::add_ln_supported((int)H), "add_ln: unsupported hidden size");
   for (auto* t : {&a, &x, &y, &h}) check_rows_bf16(*t, "add_ln tensor", R, H);
@@ -1056,12 +1070,14 @@ void add_ln_forward(at::Tensor a, at::Tensor x, c10::optional<at::Tensor> gamma,
   if (bp) TORCH_CHECK(beta->numel() == H && beta->is_contiguous(), "beta: fp32 [H]");
   c10::DeviceGuard guard(x.device());
   gk::add_ln_forward(a.data_ptr(), x.data_ptr(), gp, bp, y.data_ptr(), h.data_ptr(), mean.data_ptr<float>(),
-                     rstd.data_ptr<float>(), R, (int)H, (float)eps, (float)p, (uint32_t)seed, cur_stream(x));
+                     rstd.data_ptr<float>(), R, (int)H, (float)eps, (float)p, (uint32_t)seed, seed_word(seed_dev),
+                     cur_stream(x));
 }
 
 void add_ln_backward(at::Tensor dy, at::Tensor h, at::Tensor mean, at::Tensor rstd, c10::optional<at::Tensor> gamma,
                      at::Tensor dx, c10::optional<at::Tensor> da, c10::optional<at::Tensor> dgamma,
-                     c10::optional<at::Tensor> dbeta, bool accumulate, at::Tensor ws, double p, int64_t seed) {
+                     c10::optional<at::Tensor> dbeta, bool accumulate, at::Tensor ws, double p, int64_t seed,
+                     c10::optional<at::Tensor> seed_dev) {
   const int64_t H = h.size(-1), R = h.numel() / H;
   for (auto* t : {&dy, &h, &dx}) check_rows_bf16(*t, "add_ln tensor", R, H);
   if (da.has_value() && da->defined()) check_rows_bf16(*da, "da", R, H);
@@ -1075,7 +1091,7 @@ void add_ln_backward(at::Tensor dy, at::Tensor h, at::Tensor mean, at::Tensor rs
   gk::add_ln_backward(dy.data_ptr(), h.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(), f32(gamma),
                       dx.data_ptr(), da.has_value() && da->defined() ? da->data_ptr() : nullptr, f32(dgamma),
                       f32(dbeta), accumulate ? 1 : 0, ws.data_ptr<float>(), R, (int)H, (float)p, (uint32_t)seed,
-                      cur_stream(h));
+                      seed_word(seed_dev), cur_stream(h));
 }
 
 // fused softmax cross-entropy (xent.hip)
@@ -1192,7 +1208,8 @@ void check_attn_f32(const at::Tensor& t, const char* name, int64_t n) {
               name, " must be a contiguous fp32 GPU tensor of ", n, " elements");
 }
 
-void attn_fwd(at::Tensor qkv, at::Tensor out, at::Tensor lse, int64_t heads, double p, int64_t seed) {
+void attn_fwd(at::Tensor qkv, at::Tensor out, at::Tensor lse, int64_t heads, double p, int64_t seed,
+              c10::optional<at::Tensor> seed_dev) {
   TORCH_CHECK(qkv.dim() == 3 && qkv.size(2) == 3 * heads * 64, "qkv: [B, T, 3 * heads * 64]");
   const int64_t B = qkv.size(0), T = qkv.size(1);
   TORCH_CHECK(gk::attn_supported((int)T, 64), "attn: T must be a multiple of 128");
@@ -1202,11 +1219,11 @@ void attn_fwd(at::Tensor qkv, at::Tensor out, at::Tensor lse, int64_t heads, dou
   TORCH_CHECK(p >= 0.0 && p < 1.0, "attn: dropout p in [0, 1)");
   c10::DeviceGuard guard(qkv.device());
   gk::attn_fwd(qkv.data_ptr(), out.data_ptr(), lse.data_ptr<float>(), (int)B, (int)T, (int)heads, (float)p,
-               (uint32_t)seed, cur_stream(qkv));
+               (uint32_t)seed, seed_word(seed_dev), cur_stream(qkv));
 }
 
 void attn_bwd(at::Tensor qkv, at::Tensor out, at::Tensor dout, at::Tensor lse, at::Tensor delta, at::Tensor dqkv,
-              int64_t heads, double p, int64_t seed) {
+              int64_t heads, double p, int64_t seed, c10::optional<at::Tensor> seed_dev) {
   TORCH_CHECK(qkv.dim() == 3 && qkv.size(2) == 3 * heads * 64, "qkv: [B, T, 3 * heads * 64]");
   const int64_t B = qkv.size(0), T = qkv.size(1);
   TORCH_CHECK(gk::attn_supported((int)T, 64), "attn: T must be a multiple of 128");
@@ -1218,15 +1235,17 @@ void attn_bwd(at::Tensor qkv, at::Tensor out, at::Tensor dout, at::Tensor lse, a
   check_attn_f32(delta, "delta", B * heads * T);
   c10::DeviceGuard guard(qkv.device());
   gk::attn_bwd(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
-               dqkv.data_ptr(), (int)B, (int)T, (int)heads, (float)p, (uint32_t)seed, cur_stream(qkv));
+               dqkv.data_ptr(), (int)B, (int)T, (int)heads, (float)p, (uint32_t)seed, seed_word(seed_dev),
+               cur_stream(qkv));
 }
 
-void attn_dropout_mask(at::Tensor mask, int64_t B, int64_t heads, int64_t T, double p, int64_t seed) {
+void attn_dropout_mask(at::Tensor mask, int64_t B, int64_t heads, int64_t T, double p, int64_t seed,
+                       c10::optional<at::Tensor> seed_dev) {
   TORCH_CHECK(mask.is_cuda() && mask.scalar_type() == at::kByte && mask.is_contiguous() &&
                   mask.numel() == B * heads * T * T, "mask: contiguous uint8 [B, heads, T, T]");
   c10::DeviceGuard guard(mask.device());
   gk::attn_dropout_mask(mask.data_ptr<uint8_t>(), (int)B, (int)heads, (int)T, (float)p, (uint32_t)seed,
-                        cur_stream(mask));
+                        seed_word(seed_dev), cur_stream(mask));
 }
 
 // linear-layer column passes (linear.hip): bias gradient / fused GELU backward
@@ -1365,7 +1384,7 @@ TORCH_LIBRARY(gksgd, m) {
       "bool zero_g, int loops, float z, float fixed_thr, float sample_p, int k, int k_cap, int seed, "
       "int n_stats, Tensor(f!)? stats_out=None, Tensor? valid=None, Tensor(g!)? u=None, Tensor? w=None, "
       "Tensor? chunks=None, int chunk_begin=0, int chunk_count=0, int chunk_base=0, float[] mc_mu=[], "
-      "float[] mc_wd=[]) -> ()");
+      "float[] mc_wd=[], Tensor? seed_dev=None) -> ()");
   m.def("apply_records_sgd(Tensor(a!) w, Tensor(b!)? w_bf16, Tensor records, int P, int k_cap, float scale, float lr, "
         "Tensor? lr_mult=None) -> ()");
   m.def("arena_digest(Tensor x, Tensor(a!) out, Tensor(b!) ws) -> ()");
@@ -1436,10 +1455,10 @@ TORCH_LIBRARY(gksgd, m) {
         "Tensor(e!)? gb_acc=None) -> ()");
   m.def("attn_supported(int T, int D) -> bool",
         [](int64_t T, int64_t D) { return gk::attn_supported((int)T, (int)D); });
-  m.def("attn_fwd(Tensor qkv, Tensor(a!) out, Tensor(b!) lse, int heads, float p, int seed) -> ()");
+  m.def("attn_fwd(Tensor qkv, Tensor(a!) out, Tensor(b!) lse, int heads, float p, int seed, Tensor? seed_dev=None) -> ()");
   m.def("attn_bwd(Tensor qkv, Tensor out, Tensor dout, Tensor lse, Tensor(a!) delta, Tensor(b!) dqkv, int heads, "
-        "float p, int seed) -> ()");
-  m.def("attn_dropout_mask(Tensor(a!) mask, int B, int heads, int T, float p, int seed) -> ()");
+        "float p, int seed, Tensor? seed_dev=None) -> ()");
+  m.def("attn_dropout_mask(Tensor(a!) mask, int B, int heads, int T, float p, int seed, Tensor? seed_dev=None) -> ()");
   m.def("add_ln_supported(int H) -> bool", &add_ln_supported);
   m.def("add_ln_ws_floats(int R, int H) -> int", &add_ln_ws_floats);
   m.def("xent_supported(int V) -> bool", &xent_supported);
@@ -1453,9 +1472,10 @@ TORCH_LIBRARY(gksgd, m) {
   m.def("emb_backward(Tensor ids, Tensor? tt, Tensor dx, Tensor(a!)? dWw, Tensor(b!)? dWp, Tensor(c!)? dWt, "
         "Tensor(d!) part, Tensor sid, Tensor order, Tensor(e!) wws, Tensor(f!) wpart) -> ()");
   m.def("add_ln_forward(Tensor a, Tensor x, Tensor? gamma, Tensor? beta, Tensor(a!) y, Tensor(b!) h, "
-        "Tensor(c!) mean, Tensor(d!) rstd, float eps, float p, int seed) -> ()");
+        "Tensor(c!) mean, Tensor(d!) rstd, float eps, float p, int seed, Tensor? seed_dev=None) -> ()");
   m.def("add_ln_backward(Tensor dy, Tensor h, Tensor mean, Tensor rstd, Tensor? gamma, Tensor(a!) dx, "
-        "Tensor(b!)? da, Tensor(c!)? dgamma, Tensor(d!)? dbeta, bool accumulate, Tensor(e!) ws, float p, int seed) -> ()");
+        "Tensor(b!)? da, Tensor(c!)? dgamma, Tensor(d!)? dbeta, bool accumulate, Tensor(e!) ws, float p, int seed, "
+        "Tensor? seed_dev=None) -> ()");
   m.def("conv_tn_acc(Tensor dy, Tensor x, Tensor(a!) wout, Tensor zero, int stride, int pad, int cfg=0, int splits=0) -> ()");
   m.def("colsum_acc(Tensor dy, Tensor(a!) db) -> ()");
   m.def("gelu_bwd_colsum(Tensor dy, Tensor pre, Tensor(a!) dpre, Tensor(b!)? db=None) -> ()");

@@ -181,7 +181,16 @@ struct AttnArgs {
   float dscale;       // 1 / (1 - p_effective)
   uint32_t thr;       // drop threshold on 16 hash bits
   uint32_t seed;
+  // optional replay word (graph capture): the effective seed mixes it in, so
+  // a replayed step draws a fresh mask while forward and backward of one
+  // replay read the same word
+  const uint32_t* seed_dev;
 };
+
+__device__ __forceinline__ uint32_t eff_seed(const AttnArgs& a) {
+  if (a.seed_dev == nullptr) return a.seed;
+  return hash_u32(__builtin_amdgcn_readfirstlane(*a.seed_dev), a.seed);
+}
 
 // ---------------------------------------------------------------------------
 // forward: one workgroup = 4 waves x 32 queries of one (batch, head); K/V
@@ -190,6 +199,7 @@ struct AttnArgs {
 template <bool DROP>
 __global__ void __launch_bounds__(64 * kAW, 2) attn_fwd_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[kStages * 2 * kTileB];
+  const uint32_t seed = DROP ? eff_seed(a) : 0u;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, g = lane >> 4;
   const int T = a.T, H = a.H;
   const int nqb = T / kRows;
@@ -274,8 +284,8 @@ __global__ void __launch_bounds__(64 * kAW, 2) attn_fwd_kernel(AttnArgs a) {
         uint32_t hh[2];
         if (DROP) {
           const uint32_t pi = hrow[qt] + t * (kKT / 2) + 8 * kt;
-          hh[0] = pair_hash(a.seed, pi);
-          hh[1] = pair_hash(a.seed, pi + 1);
+          hh[0] = pair_hash(seed, pi);
+          hh[1] = pair_hash(seed, pi + 1);
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -339,6 +349,7 @@ __global__ void __launch_bounds__(64 * kAW, 2) attn_fwd_kernel(AttnArgs a) {
 template <bool DROP>
 __global__ void __launch_bounds__(64 * kAW, 2) attn_bwd_dq_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[kStages * 2 * kTileB];
+  const uint32_t seed = DROP ? eff_seed(a) : 0u;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, g = lane >> 4;
   const int T = a.T, H = a.H;
   const int nqb = T / kRows;
@@ -430,8 +441,8 @@ __global__ void __launch_bounds__(64 * kAW, 2) attn_bwd_dq_kernel(AttnArgs a) {
         uint32_t hh[2];
         if (DROP) {
           const uint32_t pi = hrow[qt] + t * (kKT / 2) + 8 * kt;
-          hh[0] = pair_hash(a.seed, pi);
-          hh[1] = pair_hash(a.seed, pi + 1);
+          hh[0] = pair_hash(seed, pi);
+          hh[1] = pair_hash(seed, pi + 1);
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -492,6 +503,7 @@ constexpr int kKvBuf = 2 * kTileB + 512;   // Q tile, dO tile, lse[64], delta[64
 template <bool DROP>
 __global__ void __launch_bounds__(64 * kAW, 2) attn_bwd_kv_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[kStages * kKvBuf];
+  const uint32_t seed = DROP ? eff_seed(a) : 0u;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, g = lane >> 4;
   const int T = a.T, H = a.H;
   const int nkb = T / kRows;
@@ -588,7 +600,7 @@ __global__ void __launch_bounds__(64 * kAW, 2) attn_bwd_kv_kernel(AttnArgs a) {
           uint32_t hq[4];
           if (DROP) {
             const uint32_t pi = hkey + (uint32_t)(t * kKT + qr + rown) * (uint32_t)(T >> 1) + 8 * kt;
-            const uint32_t m0 = pair_hash(a.seed, pi), m1 = pair_hash(a.seed, pi + (uint32_t)(T >> 1));
+            const uint32_t m0 = pair_hash(seed, pi), m1 = pair_hash(seed, pi + (uint32_t)(T >> 1));
             const uint32_t o0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)m0, 0xB1, 0xF, 0xF, false);
             const uint32_t o1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)m1, 0xB1, 0xF, 0xF, false);
             const bool odd = li & 1;
@@ -659,8 +671,9 @@ __global__ void __launch_bounds__(64 * kAW, 2) attn_bwd_kv_kernel(AttnArgs a) {
 }
 
 // keep mask [B*H][T][T] as bytes, from the same pair hashes
-__global__ void attn_dropout_mask_kernel(uint8_t* __restrict__ mask, int64_t npairs, uint32_t seed, uint32_t thr) {
+__global__ void attn_dropout_mask_kernel(uint8_t* __restrict__ mask, int64_t npairs, AttnArgs a, uint32_t thr) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t seed = eff_seed(a);
   if (i < npairs) {
     const uint32_t hv = pair_hash(seed, (uint32_t)i);
     mask[2 * i] = (hv & 0xffffu) >= thr ? 1 : 0;
@@ -668,8 +681,9 @@ __global__ void attn_dropout_mask_kernel(uint8_t* __restrict__ mask, int64_t npa
   }
 }
 
-AttnArgs make_args(int T, int H, float p, uint32_t seed) {
+AttnArgs make_args(int T, int H, float p, uint32_t seed, const uint32_t* seed_dev) {
   AttnArgs a{};
+  a.seed_dev = seed_dev;
   a.T = T;
   a.H = H;
   a.qscale = 0.125f;                       // 1 / sqrt(64)
@@ -687,8 +701,8 @@ AttnArgs make_args(int T, int H, float p, uint32_t seed) {
 bool attn_supported(int T, int D) { return D == kHD && T >= kRows && T % kRows == 0; }
 
 void attn_fwd(const void* qkv, void* out, float* lse, int B, int T, int H, float p, uint32_t seed,
-              hipStream_t stream) {
-  AttnArgs a = make_args(T, H, p, seed);
+              const uint32_t* seed_dev, hipStream_t stream) {
+  AttnArgs a = make_args(T, H, p, seed, seed_dev);
   a.qkv = static_cast<const uint16_t*>(qkv);
   a.o = static_cast<uint16_t*>(out);
   a.lse = lse;
@@ -698,8 +712,8 @@ void attn_fwd(const void* qkv, void* out, float* lse, int B, int T, int H, float
 }
 
 void attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* delta, void* dqkv, int B,
-              int T, int H, float p, uint32_t seed, hipStream_t stream) {
-  AttnArgs a = make_args(T, H, p, seed);
+              int T, int H, float p, uint32_t seed, const uint32_t* seed_dev, hipStream_t stream) {
+  AttnArgs a = make_args(T, H, p, seed, seed_dev);
   a.qkv = static_cast<const uint16_t*>(qkv);
   a.out = static_cast<const uint16_t*>(out);
   a.dout = static_cast<const uint16_t*>(dout);
@@ -716,11 +730,12 @@ void attn_bwd(const void* qkv, const void* out, const void* dout, const float* l
   }
 }
 
-void attn_dropout_mask(uint8_t* mask, int B, int H, int T, float p, uint32_t seed, hipStream_t stream) {
-  const AttnArgs a = make_args(T, H, p, seed);
+void attn_dropout_mask(uint8_t* mask, int B, int H, int T, float p, uint32_t seed, const uint32_t* seed_dev,
+                       hipStream_t stream) {
+  const AttnArgs a = make_args(T, H, p, seed, seed_dev);
   const int64_t npairs = (int64_t)B * H * T * T / 2;
   hipLaunchKernelGGL(attn_dropout_mask_kernel, dim3((unsigned)((npairs + 255) / 256)), dim3(256), 0, stream, mask,
-                     npairs, seed, a.thr);
+                     npairs, a, a.thr);
 }
 
 }  // namespace gk

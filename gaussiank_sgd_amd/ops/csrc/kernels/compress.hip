@@ -305,11 +305,13 @@ template <int PASS, int KEYKIND, bool VEC>
 __global__ __launch_bounds__(kBlock) void radix_hist_kernel(const float* __restrict__ x, int64_t n, uint32_t seed,
                                                             uint32_t sample_thr, int64_t k, uint32_t* hist_set,
                                                             const uint32_t* __restrict__ valid,
-                                                            const GkCtrl* __restrict__ cond) {
+                                                            const GkCtrl* __restrict__ cond,
+                                                            const uint32_t* __restrict__ seed_dev) {
   constexpr int NB = PASS == 0 ? kRadixBins0 : (PASS == 1 ? kRadixBins1 : kRadixBins2);
   __shared__ uint32_t sh_hist[kWavesPerBlock][NB];
   __shared__ uint64_t sh_scan[kWavesPerBlock];
   if (cond != nullptr && cond->fallback == 0) return;   // conditional pass (calibrated mode), grid-uniform
+  if (seed_dev != nullptr) seed = __builtin_amdgcn_readfirstlane(*seed_dev);
   uint32_t* hist0 = hist_set;
   uint32_t* hist1 = hist_set + kRadixBins0;
   uint32_t* hist2 = hist1 + kRadixBins1;
@@ -549,8 +551,10 @@ template <int KEYKIND, bool VEC>
 __global__ __launch_bounds__(kBlock) void count_kernel(const float* __restrict__ x, int64_t n, uint32_t seed,
                                                        const GkCtrl* __restrict__ ctrl, int64_t chunk_tiles,
                                                        uint32_t* __restrict__ blockcnt,
-                                                       const uint32_t* __restrict__ valid, int cond) {
+                                                       const uint32_t* __restrict__ valid, int cond,
+                                                       const uint32_t* __restrict__ seed_dev) {
   if (cond && ctrl->fallback == 0) return;
+  if (seed_dev != nullptr) seed = __builtin_amdgcn_readfirstlane(*seed_dev);
   // Wave-uniform counters: every (element, candidate) test is ONE v_cmp whose
   // 64-bit lane mask is popcounted and accumulated on the SCALAR unit
   // (s_bcnt1 + s_add), instead of a compare + conditional add per lane --
@@ -798,8 +802,10 @@ __global__ __launch_bounds__(kBlock) void select_kernel(float* __restrict__ r, i
                                                         const int64_t* __restrict__ eqtake,
                                                         const int64_t* __restrict__ blocksel, int64_t k_cap,
                                                         int32_t* __restrict__ out_idx, float* __restrict__ out_val,
-                                                        const uint32_t* __restrict__ valid, float* __restrict__ u) {
+                                                        const uint32_t* __restrict__ valid, float* __restrict__ u,
+                                                        const uint32_t* __restrict__ seed_dev) {
   const int64_t my_sel = blocksel[blockIdx.x];
+  if (seed_dev != nullptr) seed = __builtin_amdgcn_readfirstlane(*seed_dev);
   int64_t running = offsets[blockIdx.x];
   if (my_sel == 0 || running >= k_cap) return;  // block-uniform
   const uint32_t bound = __builtin_amdgcn_readfirstlane(ctrl->sel_bound);
@@ -902,10 +908,10 @@ void launch_count(const CompressArgs& a, const Ws& w, bool vec, int G, int64_t c
                   hipStream_t s) {
   if (vec)
     hipLaunchKernelGGL((count_kernel<KEYKIND, true>), dim3(G), dim3(kBlock), 0, s, a.r, a.n, a.seed, ctrl,
-                       chunk_tiles, w.blockcnt, a.valid, cond);
+                       chunk_tiles, w.blockcnt, a.valid, cond, a.seed_dev);
   else
     hipLaunchKernelGGL((count_kernel<KEYKIND, false>), dim3(G), dim3(kBlock), 0, s, a.r, a.n, a.seed, ctrl,
-                       chunk_tiles, w.blockcnt, a.valid, cond);
+                       chunk_tiles, w.blockcnt, a.valid, cond, a.seed_dev);
   hipLaunchKernelGGL(decide_kernel, dim3(1), dim3(kBlock), 0, s, ctrl, w.blockcnt, G, a.mode, a.loops, a.k,
                      a.k_cap, w.offsets, w.eqtake, w.blocksel, a.record, cond, w.hist);
 }
@@ -915,15 +921,17 @@ void launch_select(const CompressArgs& a, const Ws& w, bool vec, int G, int64_t 
                    int32_t* out_idx, float* out_val, hipStream_t s) {
   if (vec)
     hipLaunchKernelGGL((select_kernel<KEYKIND, true>), dim3(G), dim3(kBlock), 0, s, a.r, a.n, a.seed, ctrl,
-                       chunk_tiles, w.offsets, w.eqtake, w.blocksel, a.k_cap, out_idx, out_val, a.valid, a.u);
+                       chunk_tiles, w.offsets, w.eqtake, w.blocksel, a.k_cap, out_idx, out_val, a.valid, a.u,
+                       a.seed_dev);
   else
     hipLaunchKernelGGL((select_kernel<KEYKIND, false>), dim3(G), dim3(kBlock), 0, s, a.r, a.n, a.seed, ctrl,
-                       chunk_tiles, w.offsets, w.eqtake, w.blocksel, a.k_cap, out_idx, out_val, a.valid, a.u);
+                       chunk_tiles, w.offsets, w.eqtake, w.blocksel, a.k_cap, out_idx, out_val, a.valid, a.u,
+                       a.seed_dev);
 }
 
 template <int KEYKIND>
 void launch_radix(const float* x, int64_t n, uint32_t seed, uint32_t sample_thr, int64_t k, uint32_t* set, bool vec,
-                  const uint32_t* valid, const GkCtrl* cond, hipStream_t s) {
+                  const uint32_t* valid, const GkCtrl* cond, const uint32_t* seed_dev, hipStream_t s) {
   const int64_t n4 = (n + 3) / 4;
   int Gh = (int)ceil_div(n4, (int64_t)kBlock * 8);
   if (Gh < 1) Gh = 1;
@@ -931,10 +939,10 @@ void launch_radix(const float* x, int64_t n, uint32_t seed, uint32_t sample_thr,
 #define GK_RADIX_PASS(P)                                                                                         \
   if (vec)                                                                                                       \
     hipLaunchKernelGGL((radix_hist_kernel<P, KEYKIND, true>), dim3(Gh), dim3(kBlock), 0, s, x, n, seed, sample_thr, \
-                       k, set, valid, cond);                                                                     \
+                       k, set, valid, cond, seed_dev);                                                           \
   else                                                                                                           \
     hipLaunchKernelGGL((radix_hist_kernel<P, KEYKIND, false>), dim3(Gh), dim3(kBlock), 0, s, x, n, seed,          \
-                       sample_thr, k, set, valid, cond);
+                       sample_thr, k, set, valid, cond, seed_dev);
   GK_RADIX_PASS(0)
   GK_RADIX_PASS(1)
   GK_RADIX_PASS(2)
@@ -994,12 +1002,14 @@ void compress(const CompressArgs& a, hipStream_t s) {
   const int64_t keff = a.k < a.n ? a.k : a.n;
   if (a.mode == kModeTopK || a.mode == kModeRandomK || a.mode == kModeDGC) {
     hipMemsetAsync(w.hist, 0, sizeof(uint32_t) * 2 * kHistSet, s);
-    if (a.mode == kModeRandomK) launch_radix<kKeyHash>(a.r, a.n, a.seed, 0u, keff, hist_exact, vec_r, a.valid, nullptr, s);
-    else launch_radix<kKeyAbs>(a.r, a.n, a.seed, 0u, keff, hist_exact, vec_r, nullptr, nullptr, s);
+    if (a.mode == kModeRandomK)
+      launch_radix<kKeyHash>(a.r, a.n, a.seed, 0u, keff, hist_exact, vec_r, a.valid, nullptr, a.seed_dev, s);
+    else
+      launch_radix<kKeyAbs>(a.r, a.n, a.seed, 0u, keff, hist_exact, vec_r, nullptr, nullptr, a.seed_dev, s);
     if (a.mode == kModeDGC) {
       double p = a.sample_p * 4294967296.0;
       uint32_t thr = p >= 4294967295.0 ? 0xffffffffu : (uint32_t)p;
-      launch_radix<kKeySample>(a.r, a.n, a.seed, thr, a.k, hist_sample, vec_r, nullptr, nullptr, s);
+      launch_radix<kKeySample>(a.r, a.n, a.seed, thr, a.k, hist_sample, vec_r, nullptr, nullptr, a.seed_dev, s);
     }
   }
 
@@ -1024,7 +1034,7 @@ void compress(const CompressArgs& a, hipStream_t s) {
       // candidate in [2k/3, 4k/3] (top-k), or a threshold mode whose every
       // candidate overflows k_cap (top-k_cap)
       const int64_t kfb = a.mode == kModeGaussianCal ? keff : (a.k_cap < a.n ? a.k_cap : a.n);
-      launch_radix<kKeyAbs>(a.r, a.n, a.seed, 0u, kfb, hist_exact, vec_r, nullptr, ctrl, s);
+      launch_radix<kKeyAbs>(a.r, a.n, a.seed, 0u, kfb, hist_exact, vec_r, nullptr, ctrl, a.seed_dev, s);
       hipLaunchKernelGGL(cal_fallback_kernel, dim3(1), dim3(kBlock), 0, s, ctrl, hist_exact, kfb);
       launch_count<kKeyAbs>(a, w, vec_r, G, chunk_tiles, ctrl, 1, s);
     }

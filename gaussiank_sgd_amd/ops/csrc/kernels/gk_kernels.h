@@ -89,6 +89,7 @@ struct CompressArgs {
   int64_t k = 1;
   int64_t k_cap = 1;
   uint32_t seed = 0;
+  const uint32_t* seed_dev = nullptr;   // optional: seed read from device memory (graph replays)
   void* ctrl = nullptr;        // GkCtrl
   void* ws = nullptr;          // gk_compress_workspace_bytes(n)
   int32_t* record = nullptr;   // [4 + 2*k_cap] int32: hdr | idx | val(fp32 bits)
@@ -354,13 +355,16 @@ void wgrad3_acc(const void* dy, const void* x, const void* zero, int N, int H, i
 // [B, T, 3, H, 64] bf16; out / dout: [B, T, H, 64] bf16; lse / delta: fp32
 // [B, H, T].  Dropout p on the attention probabilities with a hash mask
 // (seed); attn_dropout_mask materialises the same mask as [B, H, T, T] bytes.
+// seed_dev (optional): a device word mixed into the seed at run time
+// (hash(*seed_dev, seed)) -- a captured graph draws a new mask every replay.
 // ---------------------------------------------------------------------------
 bool attn_supported(int T, int D);
 void attn_fwd(const void* qkv, void* out, float* lse, int B, int T, int H, float p, uint32_t seed,
-              hipStream_t stream);
+              const uint32_t* seed_dev, hipStream_t stream);
 void attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* delta, void* dqkv, int B,
-              int T, int H, float p, uint32_t seed, hipStream_t stream);
-void attn_dropout_mask(uint8_t* mask, int B, int H, int T, float p, uint32_t seed, hipStream_t stream);
+              int T, int H, float p, uint32_t seed, const uint32_t* seed_dev, hipStream_t stream);
+void attn_dropout_mask(uint8_t* mask, int B, int H, int T, float p, uint32_t seed, const uint32_t* seed_dev,
+                       hipStream_t stream);
 
 // ---------------------------------------------------------------------------
 // Fused BERT input embedding (embed.hip): out[m] = Ww[ids[m]] + Wp[m % T] + Wt[tt[m]]
@@ -400,12 +404,13 @@ void xent_backward(const void* logits, const int64_t* labels, const float* lse, 
 // ---------------------------------------------------------------------------
 bool add_ln_supported(int H);
 int64_t add_ln_partial_rows(int64_t R);
+// seed_dev (optional): device word mixed into the dropout seed (graph replays)
 void add_ln_forward(const void* a, const void* x, const float* gamma, const float* beta, void* y, void* hsave,
                     float* mean, float* rstd, int64_t R, int H, float eps, float p, uint32_t seed,
-                    hipStream_t stream);
+                    const uint32_t* seed_dev, hipStream_t stream);
 void add_ln_backward(const void* dy, const void* hsave, const float* mean, const float* rstd, const float* gamma,
                      void* dx, void* da, float* dgamma, float* dbeta, int accumulate, float* ws, int64_t R, int H,
-                     float p, uint32_t seed, hipStream_t stream);
+                     float p, uint32_t seed, const uint32_t* seed_dev, hipStream_t stream);
 
 // ---------------------------------------------------------------------------
 // Linear-layer column passes over bf16 [M, N] row-major gradients (linear.hip);

@@ -78,7 +78,9 @@ __global__ __launch_bounds__(kBlock) void add_ln_fwd_kernel(const uint16_t* __re
                                                             const float* __restrict__ beta, uint16_t* __restrict__ y,
                                                             uint16_t* __restrict__ hsave, float* __restrict__ mean,
                                                             float* __restrict__ rstd, int64_t R, int H, float eps,
-                                                            uint32_t seed, uint32_t thr, float scale) {
+                                                            uint32_t seed, uint32_t thr, float scale,
+                                                            const uint32_t* __restrict__ seed_dev) {
+  if (seed_dev != nullptr) seed = hash_u32(__builtin_amdgcn_readfirstlane(*seed_dev), seed);
   constexpr int L = 64 / RPW;
   const int lane = threadIdx.x & 63, sl = lane % L;
   const int64_t row0 = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * RPW;
@@ -144,7 +146,8 @@ __global__ __launch_bounds__(kBlock) void add_ln_bwd_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ hsave, const float* __restrict__ mean,
     const float* __restrict__ rstd, const float* __restrict__ gamma, uint16_t* __restrict__ dx,
     uint16_t* __restrict__ da, float* __restrict__ pg, float* __restrict__ pb, int64_t R, int H, uint32_t seed,
-    uint32_t thr, float scale) {
+    uint32_t thr, float scale, const uint32_t* __restrict__ seed_dev) {
+  if (seed_dev != nullptr) seed = hash_u32(__builtin_amdgcn_readfirstlane(*seed_dev), seed);
   constexpr int L = 64 / RPW;
   __shared__ float red[2][64 * 8 * kLnMaxChunks];
   const int lane = threadIdx.x & 63, sl = lane % L, wave = threadIdx.x >> 6;
@@ -331,6 +334,7 @@ struct LnFwdArgs {
   float eps;
   uint32_t seed, thr;
   float scale;
+  const uint32_t* seed_dev;
   hipStream_t stream;
 };
 
@@ -341,7 +345,8 @@ struct LnFwdLaunch {
     const int64_t waves = (p->R + RPW - 1) / RPW;
     const unsigned grid = (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
     hipLaunchKernelGGL((add_ln_fwd_kernel<CH, RPW>), dim3(grid), dim3(kBlock), 0, p->stream, p->a, p->x, p->gamma,
-                       p->beta, p->y, p->hsave, p->mean, p->rstd, p->R, p->H, p->eps, p->seed, p->thr, p->scale);
+                       p->beta, p->y, p->hsave, p->mean, p->rstd, p->R, p->H, p->eps, p->seed, p->thr, p->scale,
+                       p->seed_dev);
   }
 };
 
@@ -354,6 +359,7 @@ struct LnBwdArgs {
   int H;
   uint32_t seed, thr;
   float scale;
+  const uint32_t* seed_dev;
   hipStream_t stream;
 };
 
@@ -363,24 +369,24 @@ struct LnBwdLaunch {
   void operator()() const {
     hipLaunchKernelGGL((add_ln_bwd_kernel<CH, RPW>), dim3((unsigned)((p->R + kLnRowsPerBlock - 1) / kLnRowsPerBlock)), dim3(kBlock), 0,
                        p->stream, p->dy, p->hsave, p->mean, p->rstd, p->gamma, p->dx, p->da, p->pg, p->pb, p->R, p->H,
-                       p->seed, p->thr, p->scale);
+                       p->seed, p->thr, p->scale, p->seed_dev);
   }
 };
 }  // namespace
 
 void add_ln_forward(const void* a, const void* x, const float* gamma, const float* beta, void* y, void* hsave,
                     float* mean, float* rstd, int64_t R, int H, float eps, float p, uint32_t seed,
-                    hipStream_t stream) {
+                    const uint32_t* seed_dev, hipStream_t stream) {
   const uint32_t thr = p > 0.f ? (uint32_t)((1.0 - (double)p) * 4294967295.0) : 0u;
   const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
   const LnFwdArgs args{(const uint16_t*)a, (const uint16_t*)x, gamma, beta, (uint16_t*)y, (uint16_t*)hsave, mean,
-                       rstd, R, H, eps, seed, thr, scale, stream};
+                       rstd, R, H, eps, seed, thr, scale, seed_dev, stream};
   ln_dispatch<LnFwdLaunch>(H >> 3, {&args}, {&args}, {&args}, {&args}, {&args}, {&args}, {&args});
 }
 
 void add_ln_backward(const void* dy, const void* hsave, const float* mean, const float* rstd, const float* gamma,
                      void* dx, void* da, float* dgamma, float* dbeta, int accumulate, float* ws, int64_t R, int H,
-                     float p, uint32_t seed, hipStream_t stream) {
+                     float p, uint32_t seed, const uint32_t* seed_dev, hipStream_t stream) {
   const uint32_t thr = p > 0.f ? (uint32_t)((1.0 - (double)p) * 4294967295.0) : 0u;
   const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
   const int64_t P = (R + kLnRowsPerBlock - 1) / kLnRowsPerBlock;
@@ -388,7 +394,7 @@ void add_ln_backward(const void* dy, const void* hsave, const float* mean, const
   float* pb = ws + P * H;
   float* q = ws + 2 * P * H;   // [2][kFinSplits][H]: fits the 2 * add_ln_partial_rows(R) * H of the workspace
   const LnBwdArgs args{(const uint16_t*)dy, (const uint16_t*)hsave, mean, rstd, gamma, (uint16_t*)dx,
-                       (uint16_t*)da, pg, pb, R, H, seed, thr, scale, stream};
+                       (uint16_t*)da, pg, pb, R, H, seed, thr, scale, seed_dev, stream};
   ln_dispatch<LnBwdLaunch>(H >> 3, {&args}, {&args}, {&args}, {&args}, {&args}, {&args}, {&args});
   if (dgamma || dbeta) {
     hipLaunchKernelGGL(ln_param_partial_kernel, dim3((H + 63) / 64, kFinSplits), dim3(kBlock), 0, stream, pg, pb, P, H,

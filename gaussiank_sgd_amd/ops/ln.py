@@ -15,9 +15,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from . import load
-
-_seed_gen = torch.Generator().manual_seed(0x5eed)
+from . import capture_seed_word, load, seed_generator
 
 
 def _ops():
@@ -26,7 +24,7 @@ def _ops():
 
 class _AddLNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, a, x, gamma, beta, eps, p, seed, direct=None):
+    def forward(ctx, a, x, gamma, beta, eps, p, seed, direct=None, seed_dev=None):
         # direct = (dgamma_view, dbeta_view): fp32 gradient-arena views the
         # backward kernel accumulates into (bf16-shadow path); None is then
         # returned for gamma / beta, so AccumulateGrad launches nothing
@@ -40,9 +38,9 @@ class _AddLNFn(torch.autograd.Function):
         rstd = torch.empty(R, dtype=torch.float32, device=x.device)
         g = gamma.detach().float().contiguous() if gamma is not None else None
         b = beta.detach().float().contiguous() if beta is not None else None
-        _ops().add_ln_forward(a, x, g, b, y, h, mean, rstd, float(eps), float(p), int(seed))
+        _ops().add_ln_forward(a, x, g, b, y, h, mean, rstd, float(eps), float(p), int(seed), seed_dev)
         ctx.save_for_backward(h, mean, rstd, g if g is not None else torch.empty(0, device=x.device))
-        ctx.p, ctx.seed = float(p), int(seed)
+        ctx.p, ctx.seed, ctx.seed_dev = float(p), int(seed), seed_dev
         ctx.has_g, ctx.has_b = gamma is not None, beta is not None
         ctx.gdtype = gamma.dtype if gamma is not None else torch.float32
         ctx.direct = direct
@@ -64,13 +62,13 @@ class _AddLNFn(torch.autograd.Function):
             db = torch.empty(H, dtype=torch.float32, device=h.device) if ctx.has_b and ctx.needs_input_grad[3] else None
         ws = torch.empty(int(_ops().add_ln_ws_floats(R, H)), dtype=torch.float32, device=h.device)
         _ops().add_ln_backward(dy, h, mean, rstd, g if ctx.has_g else None, dx, da, dg, db, direct is not None, ws,
-                               ctx.p, ctx.seed)
+                               ctx.p, ctx.seed, ctx.seed_dev)
         if da is None:
             da = dx
         if direct is not None:
-            return da, dx, None, None, None, None, None, None
+            return da, dx, None, None, None, None, None, None, None
         return (da, dx, dg.to(ctx.gdtype) if dg is not None else None,
-                db.to(ctx.gdtype) if db is not None else None, None, None, None, None)
+                db.to(ctx.gdtype) if db is not None else None, None, None, None, None, None)
 
 
 def fused_available(x: torch.Tensor) -> bool:
@@ -88,9 +86,10 @@ def add_layernorm(a: torch.Tensor, x: torch.Tensor, ln: nn.LayerNorm, p: float =
     p = float(p) if training else 0.0
     if (fused_available(x) and ln.elementwise_affine and len(ln.normalized_shape) == 1 and
             a.shape == x.shape):
-        seed = int(torch.randint(0, 2 ** 31 - 1, (1,), generator=_seed_gen)) if p > 0 else 0
+        seed = int(torch.randint(0, 2 ** 31 - 1, (1,), generator=seed_generator())) if p > 0 else 0
         direct = getattr(ln, "_gk_direct", None)
         if direct is not None and not (torch.is_grad_enabled() and ln.weight.requires_grad and ln.bias.requires_grad):
             direct = None
-        return _AddLNFn.apply(a, x, ln.weight, ln.bias, ln.eps, p, seed, direct)
+        return _AddLNFn.apply(a, x, ln.weight, ln.bias, ln.eps, p, seed, direct,
+                              capture_seed_word(x.device) if p > 0 else None)
     return ln(x + F.dropout(a, p, training=p > 0))

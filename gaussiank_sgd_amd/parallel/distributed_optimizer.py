@@ -121,6 +121,10 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         # optional device scalar multiplying the lr inside the fused update
         # (set by train/graph.py so a captured step follows the lr schedule)
         self._lr_mult: Optional[torch.Tensor] = None
+        # optional int32 device words, one per bucket, holding the compressor
+        # seeds (train/graph.py: a captured step reads them at replay time, so
+        # random-k / DGC sampling draw new indices every replay)
+        self._seed_dev: Optional[torch.Tensor] = None
         self._mc_applied = False
         # Under momentum correction the global update is plain SGD on the
         # aggregate: apply it straight from the gathered records (no dense
@@ -373,6 +377,26 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         pairs = self._drain_selected()
         return pairs if with_totals else [s for s, _ in pairs]
 
+    def enable_device_seeds(self) -> torch.Tensor:
+        """Switch the compressors to seeds read from device memory (one int32
+        word per bucket); ``refresh_device_seeds`` writes the step's seeds."""
+        if self._seed_dev is None:
+            self._seed_dev = torch.zeros(len(self._arena.buckets), dtype=torch.int32, device=self._device)
+        self.refresh_device_seeds()
+        return self._seed_dev
+
+    def refresh_device_seeds(self, step: Optional[int] = None) -> None:
+        """Write seed_for(step, bucket, rank) of every bucket into the device
+        words (one stream-ordered H2D copy; what a graph replay will read)."""
+        if self._seed_dev is None:
+            return
+        comp = self._compression
+        it = self.train_iter if step is None else int(step)
+        fn = getattr(comp, "seed_for", None)
+        vals = [fn(it, b.index, self._rank) if fn is not None else 0 for b in self._arena.buckets]
+        host = torch.tensor([v - (1 << 32) if v >= (1 << 31) else v for v in vals], dtype=torch.int32)
+        self._seed_dev.copy_(host, non_blocking=True)
+
     def wire_bytes_per_step(self, density: Optional[float] = None) -> int:
         """Bytes one rank puts on the wire per step: the fixed-size record of
         every sparse bucket ((4 + 2 k_cap) int32 words), the dense fp32 bucket
@@ -478,6 +502,7 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         r = b.slice(self._arena.residuals)
         # stateless seed: (iteration, bucket, rank) -- identical across ranks for *same* variants
         seed = comp.seed_for(self.train_iter, b.index, self._rank)
+        seed_dev = self._seed_dev[b.index:b.index + 1] if self._seed_dev is not None else None
         arena = self._arena
         mc = None
         if self._mc:
@@ -490,7 +515,7 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         with trace.range("gk/b%d/compress" % b.index):
             ops.compress_(g, r, b.bufs, comp.mode, ec=comp.ec, zero_g=True, loops=comp.loops,
                           z=comp.z_for(density), k=k, k_cap=k_cap, seed=seed, sample_p=getattr(comp, "sample_p", 0.01),
-                          n_stats=b.numel, valid=b.extra.get("valid"), mc=mc)
+                          n_stats=b.numel, valid=b.extra.get("valid"), mc=mc, seed_dev=seed_dev)
         rec_words = ops.REC_HDR + 2 * k_cap
         return b.bufs.record[:rec_words], k_cap
 

@@ -10,10 +10,13 @@ call first copies the next batch into the graph's static input buffers, so
 every replay trains on fresh data.
 
 What the graph freezes: host-side scalars read at capture time -- the
-compression density / k, momentum flags.  The learning rate is NOT frozen:
-the fused SGD kernel multiplies the captured lr by a device scalar
-(``opt._lr_mult``) that is refreshed from the host schedule before every
-replay.  ``recapture()`` rebuilds the graph when the density schedule moves
+compression density / k, momentum flags.  NOT frozen: the learning rate (the
+fused SGD kernel multiplies the captured lr by a device scalar,
+``opt._lr_mult``, refreshed from the host schedule before every replay), the
+compressor seeds (random-k / DGC sampling read one int32 device word per
+bucket, ``opt.refresh_device_seeds``, so every replay draws new indices) and
+the dropout masks (the attention / add+LayerNorm kernels mix a per-device
+replay word, ``ops.graph_seed_word``, into their seed).  ``recapture()`` rebuilds the graph when the density schedule moves
 (epoch boundary with the reference's density warm-up).
 Single stream: the optimizer's side (compression / exchange) stream is
 dropped for the captured step -- a hipGraph with cross-stream branches
@@ -65,6 +68,7 @@ class GraphedStep:
         self.lr0 = None            # lr baked into the captured update
         self.density = None
         self.captures = 0
+        self.replays = 0
         dev = self.x.device
         self.mult = torch.ones(1, dtype=torch.float32, device=dev)
         cs = getattr(opt, "_comm_stream", None)
@@ -102,11 +106,20 @@ class GraphedStep:
                 self._body()
         self.mult.fill_(1.0)
         self.opt._lr_mult = self.mult
+        # compressor seeds and dropout masks: device words the captured kernels
+        # read at replay time (refreshed before every replay below)
+        if hasattr(self.opt, "enable_device_seeds"):
+            self.opt.enable_device_seeds()
+        from .. import ops
+        ops.graph_seed_word(self.x.device)
         self.graph = torch.cuda.CUDAGraph()
         self.opt._graph_sel = []
+        it0 = getattr(self.opt, "train_iter", None)
         with torch.cuda.graph(self.graph):
             self._body()
         self.trainer.train_iter -= 1          # capture records the step; it did not run it
+        if it0 is not None:
+            self.opt.train_iter = it0         # (the captured synchronize() advanced it on the host)
         self.lr0 = self.trainer.lr
         self.density = self._density()
         self.captures += 1
@@ -123,10 +136,19 @@ class GraphedStep:
         # lr schedule on the host -> device multiplier read by the captured update
         t.adjust_learning_rate(t.train_epoch, t.optimizer)
         self.mult.fill_(float(t.lr) / float(self.lr0) if self.lr0 else 1.0)   # async, stream-ordered
+        # fresh random-k / DGC sample seeds (this iteration's seed_for) and a new
+        # dropout replay word: nothing random is frozen into the graph
+        if hasattr(self.opt, "refresh_device_seeds"):
+            self.opt.refresh_device_seeds()
+        from .. import ops
+        self.replays += 1
+        ops.set_graph_seed(self.x.device, self.replays * 0x9E3779B1 + 1)
         self.graph.replay()
         for slot in getattr(self.opt, "_graph_sel", ()):   # selected counts of this replay (stream-ordered copies)
             self.opt._log_selected(slot)
         t.train_iter += 1
+        if hasattr(self.opt, "train_iter"):
+            self.opt.train_iter += 1
 
 
 def graphed(trainer, opt, clip: Optional[float] = None) -> Callable[[], None]:

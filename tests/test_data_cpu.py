@@ -92,3 +92,50 @@ def test_trainer_uses_real_data(tmp_path):
     assert isinstance(t.data, real.DeviceLoader) and t.trainset_len == 100
     t.train(1)
     t.data.close()
+
+
+def _jpeg_tree(root, classes=3, per_class=5):
+    from PIL import Image
+    rng = np.random.default_rng(0)
+    for split in ("train", "val"):
+        for c in range(classes):
+            d = root / split / ("n%08d" % c)
+            d.mkdir(parents=True)
+            for i in range(per_class):
+                w, h = int(rng.integers(40, 90)), int(rng.integers(40, 90))
+                arr = rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
+                Image.fromarray(arr).save(str(d / ("img_%d.JPEG" % i)), quality=90)
+
+
+def test_imagenet_image_folder_loader(tmp_path):
+    """ImageNet image-folder reader: class labels from sorted sub-directories,
+    RandomResizedCrop + flip on the host (train) / Resize + CenterCrop (eval),
+    rank sharding with DistributedSampler semantics, GPU-side normalisation
+    (here: CPU), reproducible crops."""
+    _jpeg_tree(tmp_path)
+    S = 32
+    loaders = [real.open_dataset("imagenet", str(tmp_path), 4, "cpu", rank=r, world=2, seed=3, image_size=S)
+               for r in range(2)]
+    for ld in loaders:
+        assert ld is not None and ld.num_samples() == 15
+        assert ld.sampler.per_rank == 8 and ld.batches_per_epoch() == 2
+        x, y = next(ld)
+        assert x.shape == (4, 3, S, S) and x.dtype == torch.float32
+        assert y.dtype == torch.int64 and int(y.min()) >= 0 and int(y.max()) <= 2
+        assert float(x.abs().max()) < 3.0 / 0.224          # normalised
+        ld.close()
+    # the two ranks see disjoint sample sets in an epoch (15 samples padded to 16)
+    idx = [set(real.ShardedSampler(15, 4, r, 2, seed=3).indices().tolist()) for r in range(2)]
+    assert len(idx[0] | idx[1]) == 15
+    # crops are a pure function of (seed, epoch, index)
+    rows = real.ImageFolderRows(real.find_image_folder(str(tmp_path), True), S, True, seed=5)
+    a, b = rows.load(3), rows.load(3)
+    assert a.shape == (3, S, S) and np.array_equal(a, b)
+    rows.set_epoch(1)
+    assert not np.array_equal(rows.load(3), a)
+    ev = real.open_dataset("imagenet", str(tmp_path), 5, "cpu", train=False, image_size=S)
+    xe, ye = next(ev)
+    assert xe.shape == (5, 3, S, S) and ye.tolist() == [0, 0, 0, 0, 0]     # eval: not shuffled
+    ev.close()
+    l, t, w, h = real.random_resized_crop_box(100, 60, np.random.default_rng(1))
+    assert 0 <= l and l + w <= 100 and 0 <= t and t + h <= 60

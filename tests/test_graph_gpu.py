@@ -61,3 +61,70 @@ def test_graph_lr_multiplier_scales_update():
     step.graph.replay()
     torch.cuda.synchronize()
     assert torch.equal(opt.arena.weights, w0)
+
+
+def test_graph_randomk_indices_change_per_replay():
+    """random-k under whole-step capture: the compressor seed is read from a
+    device word refreshed before every replay, so two replays send different
+    index sets (a seed baked in at capture would repeat them)."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from gaussiank_sgd_amd.compression import compressors
+    from gaussiank_sgd_amd.parallel import comm
+    from gaussiank_sgd_amd.parallel.distributed_optimizer import DistributedOptimizer
+    from gaussiank_sgd_amd.train import DLTrainer
+    from gaussiank_sgd_amd.train.graph import GraphedStep
+    from gaussiank_sgd_amd import ops
+    comm.init()
+    t = DLTrainer(0, 1, dnn="resnet20", dataset="cifar10", batch_size=16, lr=0.05, device="cuda",
+                  channels_last=True, data_pool=1, seed=0)
+    opt = DistributedOptimizer(t.optimizer, named_parameters=t.net.named_parameters(),
+                               compression=compressors["randomkec"], is_sparse=True, density=0.01,
+                               compress_single_rank=True, density_warmup=False)
+    t.update_optimizer(opt)
+    t.display = 10 ** 9
+    step = GraphedStep(t, opt)
+    step()
+    sets = []
+    for _ in range(3):
+        step()
+        torch.cuda.synchronize()
+        b = opt.arena.buckets[0]
+        rec = b.bufs.record.cpu()
+        sent = int(rec[0])
+        assert sent > 0
+        sets.append(frozenset(rec[ops.REC_HDR:ops.REC_HDR + sent].tolist()))
+    assert step.captures == 1
+    assert sets[0] != sets[1] and sets[1] != sets[2]
+
+
+def test_graph_attention_dropout_changes_per_replay():
+    """The fused attention's dropout mask under capture: the kernels mix the
+    per-device replay word into their seed, so one input replayed twice gives
+    two different outputs; without dropout the replays agree bit for bit."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from gaussiank_sgd_amd import ops
+    from gaussiank_sgd_amd.ops.attention import fused_available, self_attention
+    qkv = (torch.randn(2, 128, 3 * 2 * 64, device="cuda") * 0.5).to(torch.bfloat16)
+    if not fused_available(qkv, 2):
+        pytest.skip("fused attention unavailable")
+    outs = {}
+    for p in (0.0, 0.1):
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self_attention(qkv, 2, p)          # warm-up outside the capture
+        torch.cuda.current_stream().wait_stream(s)
+        with torch.cuda.graph(g):
+            o = self_attention(qkv, 2, p)
+        res = []
+        for r in range(2):
+            ops.set_graph_seed(qkv.device, 1000 + r)
+            g.replay()
+            torch.cuda.synchronize()
+            res.append(o.clone())
+        outs[p] = res
+    assert torch.equal(outs[0.0][0], outs[0.0][1])
+    assert not torch.equal(outs[0.1][0], outs[0.1][1])
