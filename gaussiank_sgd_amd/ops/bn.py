@@ -67,10 +67,57 @@ class BnLink:
         self.h = self.mask = self.dy2 = self.dz = self.part = None
 
 
+class ProducerLink:
+    """Hand-off between a fused BN and the convolution that PRODUCED its input
+    (fp32 path; ops/conv1x1.py attaches one to its output).
+
+    Lazy BN backward: instead of materialising dx = dL/d(conv output) with an
+    apply pass, the BN backward stores dz (ReLU-masked, twin-summed gradient),
+    its input x and the per-channel coefficients here, and returns dz itself
+    to autograd; the producer's grad-input and grad-weight GEMMs recognise it
+    (same storage) and compute dx = k1 ((dz - k2) - (x - mu) k4) on the fly
+    (gemm.hip LazyA).  ``materialize()`` runs the apply kernel for a consumer
+    without the lazy path (MIOpen choice, bf16).
+    """
+
+    __slots__ = ("lazy", "dx")
+
+    def __init__(self):
+        self.lazy = None    # (dz, x, coef, padz, padx)
+        self.dx = None      # materialised dx (cached: grad-input and grad-weight may both ask)
+
+    def matches(self, dy: torch.Tensor) -> bool:
+        return self.lazy is not None and dy.data_ptr() == self.lazy[0].data_ptr() and dy.shape == self.lazy[0].shape
+
+    def materialize(self) -> torch.Tensor:
+        if self.dx is None:
+            dz, x, coef, _, _ = self.lazy
+            self.dx = torch.empty_like(x, memory_format=_CL)
+            _ops().bn_lazy_apply(dz, x, self.dx, coef)
+        return self.dx
+
+    def clear(self) -> None:
+        self.lazy = self.dx = None
+
+
+def _lazy_buffers(x: torch.Tensor):
+    C = x.shape[1]
+    coef = torch.empty(C, 4, dtype=torch.float32, device=x.device)
+    padz = torch.empty(C, dtype=x.dtype, device=x.device)
+    padx = torch.empty(C, dtype=x.dtype, device=x.device)
+    return coef, padz, padx
+
+
+def _lazy_ok(x: torch.Tensor, plink) -> bool:
+    import os
+    return (plink is not None and x.dtype == torch.float32 and x.shape[1] % 64 == 0 and
+            os.environ.get("GKSGD_BN_LAZY", "1") != "0")
+
+
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, relu, direct=None,
-                nbt=None, twin=False, pre=None, link=None, res_link=None):
+                nbt=None, twin=False, pre=None, link=None, res_link=None, plink=None):
         # direct = (gw_view, gb_view): weight/bias gradients are accumulated
         # straight into the optimizer's fp32 arena by the backward kernel and
         # None is returned for them, so AccumulateGrad launches nothing (its
@@ -105,6 +152,7 @@ class _BNActFn(torch.autograd.Function):
         # needs our residual gradient before its consumer's grad-input runs
         ctx.link = link
         ctx.res_link = res_link
+        ctx.plink = plink
         if link is not None:
             link.h, link.mask, link.twin = x, mask, bool(twin)
         return (y, y.view_as(y)) if twin else y
@@ -112,9 +160,10 @@ class _BNActFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, *grads):
         x, mask, weight, mean, invstd = ctx.saved_tensors
-        link, res_link = ctx.link, ctx.res_link
-        ctx.link = ctx.res_link = None
+        link, res_link, plink = ctx.link, ctx.res_link, ctx.plink
+        ctx.link = ctx.res_link = ctx.plink = None
         gw, gb = ctx.direct if ctx.direct is not None else (None, None)
+        lazy = _lazy_ok(x, plink) and ctx.needs_input_grad[0]
         if link is not None and link.part is not None:
             # the consumer conv's grad-input epilogue produced dz (masked, twin-summed)
             # and its reduction partials: finalize + apply only
@@ -123,37 +172,55 @@ class _BNActFn(torch.autograd.Function):
                 raise RuntimeError("BNAct bwd_link: the linked output had another consumer")
             part, rows = link.part
             link.clear()
-            dx = torch.empty_like(x, memory_format=_CL)
             g = torch.empty(2, x.shape[1], dtype=torch.float32, device=x.device)
-            _ops().bn_act_backward_pre(dz, x, dx, weight, mean, invstd, g[0], g[1], part, rows, gw, gb)
+            if lazy:
+                # finalize only; the producing conv's GEMMs apply the BN backward themselves
+                coef, padz, padx = _lazy_buffers(x)
+                _ops().bn_bwd_lazy_pre(x, part, rows, weight, mean, invstd, g[0], g[1], coef, padz, padx, gw, gb)
+                plink.lazy = (dz, x, coef, padz, padx)
+                dx = dz
+            else:
+                dx = torch.empty_like(x, memory_format=_CL)
+                _ops().bn_act_backward_pre(dz, x, dx, weight, mean, invstd, g[0], g[1], part, rows, gw, gb)
             dres = dz if ctx.has_res and ctx.needs_input_grad[1] else None
             if res_link is not None and dres is not None:
                 res_link.dy2 = dres
             if ctx.direct is not None:
-                return (dx, dres) + (None,) * 13
+                return (dx, dres) + (None,) * 14
             dgamma = g[0] if weight is not None and ctx.needs_input_grad[2] else None
             dbeta = g[1] if ctx.needs_input_grad[3] else None
-            return (dx, dres, dgamma, dbeta) + (None,) * 11
+            return (dx, dres, dgamma, dbeta) + (None,) * 12
         if link is not None:
             link.clear()
         dy, dy2 = _grad_pair(grads, x)
         if dy is None:
-            return (None,) * 15
+            return (None,) * 16
         C = x.shape[1]
         M = x.numel() // C
-        dx = torch.empty_like(x, memory_format=_CL)
-        dres = torch.empty_like(x, memory_format=_CL) if ctx.has_res and ctx.needs_input_grad[1] else None
         g = torch.empty(2, C, dtype=torch.float32, device=x.device)
         ws = torch.empty(int(_ops().bn_workspace_floats(M, C, x.element_size())), dtype=torch.float32,
                          device=x.device)
-        _ops().bn_act_backward(dy, mask, x, dx, dres, weight, mean, invstd, g[0], g[1], ws, ctx.relu, gw, gb, dy2)
+        if lazy:
+            # the reduce pass writes dz (= the residual gradient); no apply pass
+            dz = torch.empty_like(x, memory_format=_CL)
+            coef, padz, padx = _lazy_buffers(x)
+            _ops().bn_act_backward_lazy(dy, dy2, mask, x, dz, weight, mean, invstd, g[0], g[1], ws, ctx.relu, coef,
+                                        padz, padx, gw, gb)
+            plink.lazy = (dz, x, coef, padz, padx)
+            dx = dz
+            dres = dz if ctx.has_res and ctx.needs_input_grad[1] else None
+        else:
+            dx = torch.empty_like(x, memory_format=_CL)
+            dres = torch.empty_like(x, memory_format=_CL) if ctx.has_res and ctx.needs_input_grad[1] else None
+            _ops().bn_act_backward(dy, mask, x, dx, dres, weight, mean, invstd, g[0], g[1], ws, ctx.relu, gw, gb,
+                                   dy2)
         if res_link is not None and dres is not None:
             res_link.dy2 = dres
         if ctx.direct is not None:
-            return (dx, dres) + (None,) * 13
+            return (dx, dres) + (None,) * 14
         dgamma = g[0] if weight is not None and ctx.needs_input_grad[2] else None
         dbeta = g[1] if ctx.needs_input_grad[3] else None
-        return (dx, dres, dgamma, dbeta) + (None,) * 11
+        return (dx, dres, dgamma, dbeta) + (None,) * 12
 
 
 class _BNReLUPoolFn(torch.autograd.Function):
@@ -274,8 +341,9 @@ class BNAct(nn.BatchNorm2d):
                 stats = None
             link = BnLink() if self.bwd_link and torch.is_grad_enabled() else None
             res_link = getattr(residual, "_gk_res_link", None) if residual is not None else None
+            plink = getattr(x, "_gk_plink", None) if torch.is_grad_enabled() else None
             out = _BNActFn.apply(x, residual, self.weight, self.bias, self.running_mean, self.running_var, mom,
-                                 self.eps, relu, direct, nbt, self.twin, stats, link, res_link)
+                                 self.eps, relu, direct, nbt, self.twin, stats, link, res_link, plink)
             if link is not None:
                 main = out[0] if self.twin else out
                 main._gk_bn_link = link

@@ -207,11 +207,23 @@ def _fwd(x: torch.Tensor, w: torch.Tensor, s: int, stats_box=None, bias=None) ->
     return y
 
 
-def _dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int) -> torch.Tensor:
+def _lz_kw(lz, rows: bool = False) -> dict:
+    """Kernel keywords of a lazy BN-backward operand (ops/bn.py ProducerLink):
+    the dz operand is the tensor passed in place of dy; x (the BN input) has
+    its layout (``rows``: as an [M, C] row view)."""
+    _, x, coef, padz, padx = lz
+    return dict(lz_x=_rows(x) if rows else x, lz_coef=coef, lz_padz=padz, lz_padx=padx)
+
+
+def _dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, lz=None, plink=None) -> torch.Tensor:
+    """Grad-input.  ``lz``: dy is the dz of a lazy BN backward (the kernels
+    compute dx from dz and the BN input themselves); the "mat" candidate
+    materialises dx (``plink.materialize()``) and runs the plain path."""
     N, C, H, W, K, k, p, OH, OW = _geom(x_shape, w, s)
     g = _g()
     dt = dy.dtype
     xs = torch.empty(x_shape, dtype=dt, device=dy.device, memory_format=_CL)   # shape only
+    kw = _lz_kw(lz, rows=(s == 1 and k == 1)) if lz is not None else {}
 
     def miopen():
         return torch.ops.aten.convolution_backward(dy, xs, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
@@ -222,20 +234,27 @@ def _dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int) -> torch.Tensor:
         # stride 2: the four parity classes of dX as stride-1 implicit GEMMs over dY
         dx = xs
         z = _zero(dy.device)
-        run = lambda c, mb: g.conv_dgrad_s2(dy, w, dx, z, c, mb)  # noqa: E731
+        run = lambda c, mb: g.conv_dgrad_s2(dy, w, dx, z, c, mb, **kw)  # noqa: E731
         cands = [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in _nt_cfgs(dt) for mb in _NT_GRIDS]
     if s == 1:
         dx = xs
         if k == 1:
             DY, DX = _rows(dy), _rows(dx)
             Wt = w.reshape(K, C).t().contiguous()
-            run = lambda c, mb: g.gemm_nt(DY, Wt, DX, c, mb)  # noqa: E731
+            run = lambda c, mb: g.gemm_nt(DY, Wt, DX, c, mb, **kw)  # noqa: E731
         else:
             # dX = conv(dY, W') with W'[c][kh][kw][k] = W[k][KH-1-kh][KW-1-kw][c]
             wf = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=_CL)
             z = _zero(dy.device)
-            run = lambda c, mb: g.conv_nt(dy, wf, dx, z, 1, p, c, mb)  # noqa: E731
+            run = lambda c, mb: g.conv_nt(dy, wf, dx, z, 1, p, c, mb, **kw)  # noqa: E731
         cands = [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in _nt_cfgs(dt) for mb in _NT_GRIDS]
+    if lz is not None:
+        cands.append((("mat", 0, 0), lambda: _dgrad(plink.materialize(), w, x_shape, s)))
+        ch = _pick(("dgrad", N, C, H, W, K, k, s) + _dkey(dt) + ("lz",), cands)
+        if ch[0] == "mat":
+            return _dgrad(plink.materialize(), w, x_shape, s)
+        run(ch[1], ch[2])
+        return dx
     cands.append((("miopen", 0, 0), miopen))
     ch = _pick(("dgrad", N, C, H, W, K, k, s) + _dkey(dt), cands)
     if ch[0] == "miopen":
@@ -244,12 +263,14 @@ def _dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int) -> torch.Tensor:
     return dx
 
 
-def _dgrad_bn(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, link) -> torch.Tensor:
+def _dgrad_bn(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, link, lz=None, plink=None) -> torch.Tensor:
     """Grad-input with the producing BatchNorm's backward reduction fused into
     the epilogue (gemm.hip BnBwd; ops/bn.py BnLink): returns dz = ReLU-masked
     (dX + dy2) and leaves the partials in ``link.part``.  Stride 1 only; the
-    caller checks ``link.ready()``."""
+    caller checks ``link.ready()``.  ``lz``: dy is a lazy BN-backward dz (see
+    _dgrad)."""
     N, C, H, W, K, k, p, OH, OW = _geom(x_shape, w, s)
+    kw = _lz_kw(lz, rows=(k == 1)) if lz is not None else {}
     g = _g()
     M = N * H * W
     dt = dy.dtype
@@ -261,15 +282,22 @@ def _dgrad_bn(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, link) -> torch
         Wt = w.reshape(K, C).t().contiguous()
         H2 = _rows(h)
         D2 = _rows(dy2) if dy2 is not None else None
-        run = lambda c, mb: g.gemm_nt(DY, Wt, DZ, c, mb, st, None, H2, D2, mask)  # noqa: E731
+        run = lambda c, mb: g.gemm_nt(DY, Wt, DZ, c, mb, st, None, H2, D2, mask, **kw)  # noqa: E731
     else:
         wf = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=_CL)
         z = _zero(dy.device)
-        run = lambda c, mb: g.conv_nt(dy, wf, dz, z, 1, p, c, mb, st, None, h, dy2, mask)  # noqa: E731
+        run = lambda c, mb: g.conv_nt(dy, wf, dz, z, 1, p, c, mb, st, None, h, dy2, mask, **kw)  # noqa: E731
     # 64x64-per-wave tiles (cfg digit 1-4) carry the BN-backward epilogue
     cands = [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in _nt_cfgs(dt) if c % 10 <= 4
              for mb in _NT_GRIDS]
-    ch = _pick(("dgrad_bn", N, C, H, W, K, k, s, dy2 is not None) + _dkey(dt), cands)
+    key = ("dgrad_bn", N, C, H, W, K, k, s, dy2 is not None) + _dkey(dt)
+    if lz is not None:
+        cands.append((("mat", 0, 0), lambda: _dgrad_bn(plink.materialize(), w, x_shape, s, link)))
+        ch = _pick(key + ("lz",), cands)
+        if ch[0] == "mat":
+            return _dgrad_bn(plink.materialize(), w, x_shape, s, link)
+    else:
+        ch = _pick(key, cands)
     rows = run(ch[1], ch[2])
     link.part = (st, int(rows))
     link.dz = dz
@@ -292,25 +320,36 @@ def dgrad_key_dtype(key: tuple) -> torch.dtype:
     return torch.float32 if key[-1] == "f32" else torch.bfloat16
 
 
-def _wgrad_into(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, s: int, out_f32: torch.Tensor) -> None:
-    """out_f32 ([K, C, k, k] channels-last fp32) += dW."""
+def _wgrad_into(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, s: int, out_f32: torch.Tensor, lz=None,
+                plink=None) -> None:
+    """out_f32 ([K, C, k, k] channels-last fp32) += dW.  ``lz``: dy is a lazy
+    BN-backward dz (see _dgrad)."""
     N, C, H, W, K, k, p, OH, OW = _geom(x.shape, w, s)
     g = _g()
     dt = x.dtype
-    key = ("wgrad", N, C, H, W, K, k, s) + _dkey(dt)
+    key = ("wgrad", N, C, H, W, K, k, s) + _dkey(dt) + (("lz",) if lz is not None else ())
     scratch = torch.zeros_like(out_f32) if key not in _choices else None
+    kw = _lz_kw(lz, rows=(k == 1 and s == 1)) if lz is not None else {}
 
     def miopen():
         return torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
                                                    [False, True, False])[1]
     if k == 1 and s == 1:
         DY, X = _rows(dy), _rows(x)
-        run = lambda o, c, sp: g.gemm_tn_acc(DY, X, o.view(K, C), c, sp)  # noqa: E731
+        run = lambda o, c, sp: g.gemm_tn_acc(DY, X, o.view(K, C), c, sp, **kw)  # noqa: E731
     else:
         z = _zero(x.device)
-        run = lambda o, c, sp: g.conv_tn_acc(dy, x, o, z, s, p, c, sp)  # noqa: E731
+        run = lambda o, c, sp: g.conv_tn_acc(dy, x, o, z, s, p, c, sp, **kw)  # noqa: E731
     cands = [(("hip", c, sp), (lambda c=c, sp=sp: run(scratch, c, sp)))
              for c, sp in (_TN_CFGS_F32 if dt == torch.float32 else _TN_CFGS)]
+    if lz is not None:
+        cands.append((("mat", 0, 0), lambda: _wgrad_into(plink.materialize(), x, w, s, scratch)))
+        ch = _pick(key, cands)
+        if ch[0] == "mat":
+            _wgrad_into(plink.materialize(), x, w, s, out_f32)
+        else:
+            run(out_f32, ch[1], ch[2])
+        return
     w3 = None
     if k == 3 and s == 1 and dt == torch.bfloat16 and g.wgrad3_supported(H, W, C, K):
         # tap-parallel kernel (wgrad3.hip): dY and X staged once per band for all 9 taps
@@ -339,7 +378,7 @@ class _FastConvFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, param, w_bf16, sink, stride, stats_box=None, bias=None, bias_sink=None, link=None,
-                dt=torch.bfloat16):
+                dt=torch.bfloat16, plink=None):
         if x.dtype != dt:
             x = x.to(dt)
         x = x.contiguous(memory_format=_CL)
@@ -357,6 +396,7 @@ class _FastConvFn(torch.autograd.Function):
         ctx.param_dtype = param.dtype
         ctx.link = link
         ctx.dt = dt
+        ctx.plink = plink       # the consuming BN may hand back a lazy dz (ops/bn.py ProducerLink)
         ctx.save_for_backward(x, w)
         return y
 
@@ -366,37 +406,46 @@ class _FastConvFn(torch.autograd.Function):
         s = ctx.stride
         dy = dy.to(ctx.dt).contiguous(memory_format=_CL)
         link, ctx.link = ctx.link, None
+        plink, ctx.plink = ctx.plink, None
+        # lazy BN backward: dy is the consuming BN's dz; dx is formed inside the GEMMs
+        lz = plink.lazy if plink is not None and plink.matches(dy) else None
+        if plink is not None and plink.lazy is not None and lz is None:
+            # autograd summed the BN's dz with another consumer's gradient: the sum is not dx
+            raise RuntimeError("FastConv2d: lazy BN gradient mixed with another consumer of the conv output; "
+                               "set GKSGD_BN_LAZY=0 for this model")
         dx = None
         if ctx.needs_input_grad[0]:
             N, C, H, W = x.shape
             key = ("dgrad", N, C, H, W, w.shape[0], w.shape[2], s) + _dkey(ctx.dt)
             if _bn_fusable(link, s, key):
-                dx = _dgrad_bn(dy, w, x.shape, s, link)
+                dx = _dgrad_bn(dy, w, x.shape, s, link, lz, plink)
             else:
-                dx = _dgrad(dy, w, x.shape, s)
+                dx = _dgrad(dy, w, x.shape, s, lz, plink)
         gparam = None
         if ctx.needs_input_grad[1]:
             sink = ctx.sink
             if sink is not None and getattr(sink, "grad_view", None) is not None and \
                     sink.grad_view.is_contiguous(memory_format=_CL):
                 sink.check()
-                _wgrad_into(dy, x, w, s, sink.grad_view)
+                _wgrad_into(dy, x, w, s, sink.grad_view, lz, plink)
             else:
                 out = torch.zeros(w.shape, dtype=torch.float32, device=x.device).contiguous(memory_format=_CL)
-                _wgrad_into(dy, x, w, s, out)
+                _wgrad_into(dy, x, w, s, out, lz, plink)
                 if sink is not None:
                     sink(out)
                 else:
                     gparam = out.to(ctx.param_dtype)
         gbias = None
         if ctx.has_bias and ctx.needs_input_grad[6]:
-            db = dy.sum(dim=(0, 2, 3), dtype=torch.float32)
+            db = (plink.materialize() if lz is not None else dy).sum(dim=(0, 2, 3), dtype=torch.float32)
             bs = ctx.bias_sink
             if bs is not None:
                 bs(db)          # into the optimizer's fp32 arena (shadow path)
             else:
                 gbias = db
-        return dx, gparam, None, None, None, None, gbias, None, None, None
+        if plink is not None:
+            plink.clear()
+        return dx, gparam, None, None, None, None, gbias, None, None, None, None
 
 
 class FastConv2d(nn.Conv2d):
@@ -438,8 +487,15 @@ class FastConv2d(nn.Conv2d):
             if not torch.is_grad_enabled() or self.bias is None or not self.bias.requires_grad:
                 bsink = None
             link = getattr(x, "_gk_bn_link", None)
-            return _FastConvFn.apply(x, self.weight, w_bf16, sink, self.stride[0], box, self.bias, bsink, link,
-                                     torch.bfloat16 if bf16 else torch.float32)
+            plink = None
+            if f32 and not bf16 and torch.is_grad_enabled():
+                from .bn import ProducerLink
+                plink = ProducerLink()
+            y = _FastConvFn.apply(x, self.weight, w_bf16, sink, self.stride[0], box, self.bias, bsink, link,
+                                  torch.bfloat16 if bf16 else torch.float32, plink)
+            if plink is not None:
+                y._gk_plink = plink
+            return y
         slow = getattr(self, "_gk_slow", None)
         return slow(x) if slow is not None else super().forward(x)
 

@@ -485,6 +485,84 @@ void bn_act_backward_pre(at::Tensor dz, at::Tensor x, at::Tensor dx, c10::option
                           ps + part.size(1) * C, (int)rows, opt_f32_mut(gw_acc), opt_f32_mut(gb_acc), cur_stream(x));
 }
 
+// ---- lazy BN backward (bn_act.hip bn_bwd_finalize_lazy): no apply pass ----
+void check_lazy_out(const at::Tensor& x, int64_t C, const at::Tensor& coef, const at::Tensor& padz,
+                    const at::Tensor& padx) {
+  TORCH_CHECK(coef.is_cuda() && coef.scalar_type() == at::kFloat && coef.is_contiguous() && coef.numel() >= 4 * C,
+              "coef must be a contiguous fp32 [C, 4] GPU tensor");
+  for (const at::Tensor* t : {&padz, &padx})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == x.scalar_type() && t->is_contiguous() && t->numel() >= C,
+                "padz / padx must be contiguous [C] GPU tensors of x's dtype");
+}
+
+void bn_bwd_lazy_pre(at::Tensor x, at::Tensor part, int64_t rows, c10::optional<at::Tensor> w, at::Tensor mean,
+                     at::Tensor invstd, at::Tensor dgamma, at::Tensor dbeta, at::Tensor coef, at::Tensor padz,
+                     at::Tensor padx, c10::optional<at::Tensor> gw_acc, c10::optional<at::Tensor> gb_acc) {
+  check_cl(x, "x");
+  const int64_t C = channels_of(x);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() == 3 &&
+                  part.size(0) == 2 && part.size(2) == C && rows > 0 && rows <= part.size(1),
+              "part must be fp32 [2, rows, C] partials with 0 < rows <= part.size(1)");
+  for (const at::Tensor* t : {&mean, &invstd, &dgamma, &dbeta})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->numel() >= C, "per-channel buffers: fp32[C]");
+  check_lazy_out(x, C, coef, padz, padx);
+  c10::DeviceGuard guard(x.device());
+  const float* ps = part.data_ptr<float>();
+  gk::bn_bwd_finalize_lazy(ps, ps + part.size(1) * C, (int)rows, M, (int)C, (int)x.element_size(), 1, opt_f32(w),
+                           mean.data_ptr<float>(), invstd.data_ptr<float>(), dgamma.data_ptr<float>(),
+                           dbeta.data_ptr<float>(), opt_f32_mut(gw_acc), opt_f32_mut(gb_acc), coef.data_ptr<float>(),
+                           padz.data_ptr(), padx.data_ptr(), cur_stream(x));
+}
+
+void bn_act_backward_lazy(at::Tensor dy, c10::optional<at::Tensor> dy2, c10::optional<at::Tensor> mask, at::Tensor x,
+                          at::Tensor dz, c10::optional<at::Tensor> w, at::Tensor mean, at::Tensor invstd,
+                          at::Tensor dgamma, at::Tensor dbeta, at::Tensor ws, bool relu, at::Tensor coef,
+                          at::Tensor padz, at::Tensor padx, c10::optional<at::Tensor> gw_acc,
+                          c10::optional<at::Tensor> gb_acc) {
+  check_cl(dy, "dy");
+  check_cl(x, "x");
+  check_cl(dz, "dz");
+  const int64_t C = channels_of(x);
+  const int64_t M = x.numel() / C;
+  const int eb = x.element_size();
+  TORCH_CHECK(dy.scalar_type() == x.scalar_type() && dz.scalar_type() == x.scalar_type() && dz.numel() == x.numel(),
+              "dtype / shape mismatch");
+  TORCH_CHECK(gk::bn_supported((int)C, eb), "channel count not supported by the fused kernel");
+  const uint8_t* mp = nullptr;
+  if (relu) {
+    TORCH_CHECK(mask.has_value() && mask->defined() && mask->scalar_type() == at::kByte &&
+                    mask->numel() >= (int64_t)gk::bn_mask_bytes(M, (int)C, eb),
+                "relu backward needs the forward's mask");
+    mp = mask->data_ptr<uint8_t>();
+  }
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() >= (int64_t)gk::bn_workspace_floats(M, (int)C, eb),
+              "workspace too small");
+  check_lazy_out(x, C, coef, padz, padx);
+  c10::DeviceGuard guard(x.device());
+  const void* d2 = opt_like(dy2, dy, "dy2");
+  gk::bn_act_backward_lazy(dy.data_ptr(), d2, mp, x.data_ptr(), dz.data_ptr(), M, (int)C, eb, opt_f32(w),
+                           mean.data_ptr<float>(), invstd.data_ptr<float>(), dgamma.data_ptr<float>(),
+                           dbeta.data_ptr<float>(), ws.data_ptr<float>(), relu ? 1 : 0, opt_f32_mut(gw_acc),
+                           opt_f32_mut(gb_acc), coef.data_ptr<float>(), padz.data_ptr(), padx.data_ptr(),
+                           cur_stream(x));
+}
+
+void bn_lazy_apply(at::Tensor dz, at::Tensor x, at::Tensor dx, at::Tensor coef) {
+  check_cl(dz, "dz");
+  check_cl(x, "x");
+  check_cl(dx, "dx");
+  const int64_t C = channels_of(x);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(dz.scalar_type() == x.scalar_type() && dx.scalar_type() == x.scalar_type() &&
+                  dz.numel() == x.numel() && dx.numel() == x.numel(), "dz / x / dx of one shape and dtype");
+  TORCH_CHECK(gk::bn_supported((int)C, (int)x.element_size()), "channel count not supported by the fused kernel");
+  TORCH_CHECK(coef.is_cuda() && coef.scalar_type() == at::kFloat && coef.numel() >= 4 * C, "coef: fp32 [C, 4]");
+  c10::DeviceGuard guard(x.device());
+  gk::bn_lazy_apply(dz.data_ptr(), x.data_ptr(), dx.data_ptr(), M, (int)C, (int)x.element_size(),
+                    coef.data_ptr<float>(), cur_stream(x));
+}
+
 gk::PoolGeo pool_geo(const at::Tensor& x, const at::Tensor& y, int64_t k, int64_t st, int64_t pad) {
   TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && x.size(0) == y.size(0) && x.size(1) == y.size(1), "pool shapes");
   gk::PoolGeo pg;
@@ -861,9 +939,36 @@ bool bn_bwd_args(const c10::optional<at::Tensor>& h, const c10::optional<at::Ten
   return true;
 }
 
+// lazy BN-backward operand (gemm.hip LazyA): x like dz (the operand), fp32
+// coef [C][4], padz / padx [C]; all four or none
+bool lazy_args(const c10::optional<at::Tensor>& x, const c10::optional<at::Tensor>& coef,
+               const c10::optional<at::Tensor>& padz, const c10::optional<at::Tensor>& padx, const at::Tensor& dz,
+               int64_t C, gk::LazyArgs* out) {
+  if (!x.has_value() || !x->defined()) return false;
+  TORCH_CHECK(dz.scalar_type() == at::kFloat, "lazy BN operand: fp32 kernels only");
+  TORCH_CHECK(x->is_cuda() && x->scalar_type() == dz.scalar_type() && x->sizes() == dz.sizes() &&
+                  x->strides() == dz.strides(),
+              "lz_x must match the dz operand's dtype, shape and strides");
+  TORCH_CHECK(coef.has_value() && coef->defined() && coef->is_cuda() && coef->scalar_type() == at::kFloat &&
+                  coef->is_contiguous() && coef->numel() >= 4 * C,
+              "lz_coef must be a contiguous fp32 [C, 4] GPU tensor");
+  for (const c10::optional<at::Tensor>* t : {&padz, &padx})
+    TORCH_CHECK(t->has_value() && (*t)->defined() && (*t)->is_cuda() && (*t)->scalar_type() == dz.scalar_type() &&
+                    (*t)->is_contiguous() && (*t)->numel() >= C,
+                "lz_padz / lz_padx must be contiguous [C] GPU tensors of dz's dtype");
+  TORCH_CHECK(C > 0 && C % 64 == 0, "lazy BN operand: channels must be a multiple of 64");
+  out->x = x->data_ptr();
+  out->coef = coef->data_ptr<float>();
+  out->padz = padz->data_ptr();
+  out->padx = padx->data_ptr();
+  out->C = (int)C;
+  return true;
+}
+
 int64_t gemm_nt(at::Tensor A, at::Tensor B, at::Tensor C, int64_t cfg, int64_t max_blocks,
                 c10::optional<at::Tensor> stats, c10::optional<at::Tensor> bias, c10::optional<at::Tensor> bn_h,
-                c10::optional<at::Tensor> bn_dy2, c10::optional<at::Tensor> bn_mask) {
+                c10::optional<at::Tensor> bn_dy2, c10::optional<at::Tensor> bn_mask, c10::optional<at::Tensor> lz_x, c10::optional<at::Tensor> lz_coef,
+                c10::optional<at::Tensor> lz_padz, c10::optional<at::Tensor> lz_padx) {
   check_rows(A, "A", A);
   check_rows(B, "B", A);
   check_rows(C, "C", A);
@@ -876,14 +981,19 @@ int64_t gemm_nt(at::Tensor A, at::Tensor B, at::Tensor C, int64_t cfg, int64_t m
   gk::BnBwdArgs bn{};
   const bool has_bn = bn_bwd_args(bn_h, bn_dy2, bn_mask, M, N, C.stride(0), sp != nullptr, C.scalar_type(), &bn);
   TORCH_CHECK(!has_bn || !bias.has_value() || !bias->defined(), "gemm_nt: bias and BN epilogue are exclusive");
+  gk::LazyArgs lz{};
+  const bool has_lz = lazy_args(lz_x, lz_coef, lz_padz, lz_padx, A, K, &lz);
   c10::DeviceGuard guard(A.device());
-  return gk::gemm_nt(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), M, (int)N,
-                     (int)K, A.scalar_type() == at::kFloat, (int)cfg, (int)max_blocks, sp, rows, bias_ptr(bias, N),
-                     has_bn ? &bn : nullptr, cur_stream(A));
+  const int r = gk::gemm_nt(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), M, (int)N,
+                            (int)K, A.scalar_type() == at::kFloat, (int)cfg, (int)max_blocks, sp, rows,
+                            bias_ptr(bias, N), has_bn ? &bn : nullptr, has_lz ? &lz : nullptr, cur_stream(A));
+  TORCH_CHECK(r >= 0, "gemm_nt: the lazy operand's coefficient table does not fit this tile configuration");
+  return r;
 }
 
 // W[N, K] += G[M, N]^T . X[M, K]   (fp32 W, float atomics)
-void gemm_tn_acc(at::Tensor G, at::Tensor X, at::Tensor W, int64_t cfg, int64_t splits) {
+void gemm_tn_acc(at::Tensor G, at::Tensor X, at::Tensor W, int64_t cfg, int64_t splits, c10::optional<at::Tensor> lz_x, c10::optional<at::Tensor> lz_coef,
+                c10::optional<at::Tensor> lz_padz, c10::optional<at::Tensor> lz_padx) {
   check_rows(G, "G", G);
   check_rows(X, "X", G);
   TORCH_CHECK(W.is_cuda() && W.scalar_type() == at::kFloat && W.dim() == 2 && W.stride(1) == 1,
@@ -892,9 +1002,11 @@ void gemm_tn_acc(at::Tensor G, at::Tensor X, at::Tensor W, int64_t cfg, int64_t 
   TORCH_CHECK(X.size(0) == M && W.size(0) == N && W.size(1) == K, "gemm_tn_acc: shape mismatch");
   TORCH_CHECK(gk::gemm_supported(N, K), "gemm_tn_acc: N and K must be multiples of 64");
   if (M == 0) return;
+  gk::LazyArgs lz{};
+  const bool has_lz = lazy_args(lz_x, lz_coef, lz_padz, lz_padx, G, N, &lz);
   c10::DeviceGuard guard(G.device());
   gk::gemm_tn_acc(G.data_ptr(), G.stride(0), X.data_ptr(), X.stride(0), W.data_ptr<float>(), W.stride(0), M, (int)N,
-                  (int)K, G.scalar_type() == at::kFloat, (int)cfg, (int)splits, cur_stream(G));
+                  (int)K, G.scalar_type() == at::kFloat, (int)cfg, (int)splits, has_lz ? &lz : nullptr, cur_stream(G));
 }
 
 // implicit-GEMM convolution over NHWC bf16 (x: [N, C, H, W] channels-last,
@@ -917,7 +1029,9 @@ void check_conv(const at::Tensor& x, const at::Tensor& w, const at::Tensor& zero
 
 int64_t conv_nt(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor zero, int64_t stride, int64_t pad, int64_t cfg,
                 int64_t max_blocks, c10::optional<at::Tensor> stats, c10::optional<at::Tensor> bias,
-                c10::optional<at::Tensor> bn_h, c10::optional<at::Tensor> bn_dy2, c10::optional<at::Tensor> bn_mask) {
+                c10::optional<at::Tensor> bn_h, c10::optional<at::Tensor> bn_dy2, c10::optional<at::Tensor> bn_mask,
+                c10::optional<at::Tensor> lz_x, c10::optional<at::Tensor> lz_coef,
+                c10::optional<at::Tensor> lz_padz, c10::optional<at::Tensor> lz_padx) {
   check_conv(x, w, zero);
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
   const int64_t Co = w.size(0), KH = w.size(2), KW = w.size(3);
@@ -934,10 +1048,15 @@ int64_t conv_nt(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor zero, int64
   gk::BnBwdArgs bn{};
   const bool has_bn = bn_bwd_args(bn_h, bn_dy2, bn_mask, M, Co, Co, sp != nullptr, y.scalar_type(), &bn);
   TORCH_CHECK(!has_bn || !bias.has_value() || !bias->defined(), "conv_nt: bias and BN epilogue are exclusive");
+  gk::LazyArgs lz{};
+  const bool has_lz = lazy_args(lz_x, lz_coef, lz_padz, lz_padx, x, C, &lz);
   c10::DeviceGuard guard(x.device());
-  return gk::conv_nt(x.data_ptr(), zero.data_ptr(), (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)stride, (int)pad,
-                     (int)KH, (int)KW, w.data_ptr(), y.data_ptr(), M, (int)Co, x.scalar_type() == at::kFloat, (int)cfg,
-                     (int)max_blocks, sp, rows, bias_ptr(bias, Co), has_bn ? &bn : nullptr, cur_stream(x));
+  const int r = gk::conv_nt(x.data_ptr(), zero.data_ptr(), (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)stride,
+                            (int)pad, (int)KH, (int)KW, w.data_ptr(), y.data_ptr(), M, (int)Co,
+                            x.scalar_type() == at::kFloat, (int)cfg, (int)max_blocks, sp, rows, bias_ptr(bias, Co),
+                            has_bn ? &bn : nullptr, has_lz ? &lz : nullptr, cur_stream(x));
+  TORCH_CHECK(r >= 0, "conv_nt: the lazy operand's coefficient table does not fit this tile configuration");
+  return r;
 }
 
 // grad-input of a stride-2 convolution (1x1 / pad 0 or 3x3 / pad 1) through the
@@ -947,7 +1066,9 @@ int64_t conv_nt(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor zero, int64
 // whose output lands on the class's pixels (gemm.hip ConvGeo remap).
 // dy: [N, K, OH, OW] channels-last bf16; w: [K, C, k, k] channels-last bf16;
 // dx: [N, C, H, W] channels-last bf16 (every pixel written).
-void conv_dgrad_s2(at::Tensor dy, at::Tensor w, at::Tensor dx, at::Tensor zero, int64_t cfg, int64_t max_blocks) {
+void conv_dgrad_s2(at::Tensor dy, at::Tensor w, at::Tensor dx, at::Tensor zero, int64_t cfg, int64_t max_blocks,
+                   c10::optional<at::Tensor> lz_x, c10::optional<at::Tensor> lz_coef,
+                c10::optional<at::Tensor> lz_padz, c10::optional<at::Tensor> lz_padx) {
   TORCH_CHECK(dy.is_cuda() && is_gemm_dtype(dy) && dy.dim() == 4 && dy.is_contiguous(at::MemoryFormat::ChannelsLast),
               "conv_dgrad_s2: dy must be channels-last bf16 or fp32");
   TORCH_CHECK(w.is_cuda() && w.scalar_type() == dy.scalar_type() && w.dim() == 4 && w.size(0) == dy.size(1) &&
@@ -964,13 +1085,15 @@ void conv_dgrad_s2(at::Tensor dy, at::Tensor w, at::Tensor dx, at::Tensor zero, 
   TORCH_CHECK(K % 64 == 0 && C % 64 == 0, "conv_dgrad_s2: channels must be multiples of 64");
   check_zero(zero);
   TORCH_CHECK(N * H * W < (int64_t(1) << 31), "conv_dgrad_s2: too many pixels");
+  gk::LazyArgs lzv{};
+  const gk::LazyArgs* lz = lazy_args(lz_x, lz_coef, lz_padz, lz_padx, dy, K, &lzv) ? &lzv : nullptr;
   c10::DeviceGuard guard(dy.device());
   const hipStream_t st = cur_stream(dy);
   if (k == 1) {   // one class (even, even), zeros elsewhere; B = W^T [C][K]
     const at::Tensor wt = w.reshape({K, C}).t().contiguous();
     gk::conv_nt_remap(dy.data_ptr(), K, zero.data_ptr(), (int)OHd, (int)OWd, (int)K, (int)OHd, (int)OWd, 1, 1,
                       wt.data_ptr(), dx.data_ptr(), N * OHd * OWd, (int)C, (int)H, (int)W, 0, 0, 1, f32, (int)cfg,
-                      (int)max_blocks, st);
+                      (int)max_blocks, lz, st);
     return;
   }
   // [C][kh][kw][K] = W[K][C][kh][kw]
@@ -986,7 +1109,7 @@ void conv_dgrad_s2(at::Tensor dy, at::Tensor w, at::Tensor dx, at::Tensor zero, 
       wc = wc.contiguous();
       gk::conv_nt_remap(dy.data_ptr(), K, zero.data_ptr(), (int)OHd, (int)OWd, (int)K, (int)OHc, (int)OWc,
                         a == 0 ? 1 : 2, b == 0 ? 1 : 2, wc.data_ptr(), dx.data_ptr(), N * OHc * OWc, (int)C, (int)H,
-                        (int)W, a, b, 0, f32, (int)cfg, (int)max_blocks, st);
+                        (int)W, a, b, 0, f32, (int)cfg, (int)max_blocks, lz, st);
     }
   }
 }
@@ -1022,7 +1145,8 @@ void conv3_wgrad(at::Tensor dy, at::Tensor x, at::Tensor out, at::Tensor part, a
 
 // wout: fp32 [Cout, C, KH, KW] channels-last (memory [Cout][KH][KW][C]); += dW
 void conv_tn_acc(at::Tensor dy, at::Tensor x, at::Tensor wout, at::Tensor zero, int64_t stride, int64_t pad,
-                 int64_t cfg, int64_t splits) {
+                 int64_t cfg, int64_t splits, c10::optional<at::Tensor> lz_x, c10::optional<at::Tensor> lz_coef,
+                c10::optional<at::Tensor> lz_padz, c10::optional<at::Tensor> lz_padx) {
   TORCH_CHECK(wout.is_cuda() && wout.scalar_type() == at::kFloat && wout.dim() == 4 &&
                   wout.is_contiguous(at::MemoryFormat::ChannelsLast) && wout.size(1) == x.size(1),
               "conv_tn_acc: wout must be a channels-last fp32 [Cout, C, KH, KW] tensor");
@@ -1041,10 +1165,12 @@ void conv_tn_acc(at::Tensor dy, at::Tensor x, at::Tensor wout, at::Tensor zero, 
   const int64_t M = N * OH * OW;
   TORCH_CHECK(M < (int64_t(1) << 32), "conv_tn_acc: M out of range");
   if (M == 0) return;
+  gk::LazyArgs lz{};
+  const bool has_lz = lazy_args(lz_x, lz_coef, lz_padz, lz_padx, dy, Co, &lz);
   c10::DeviceGuard guard(x.device());
   gk::conv_tn_acc(dy.data_ptr(), x.data_ptr(), zero.data_ptr(), (int)H, (int)W, (int)C, (int)OH, (int)OW,
                   (int)stride, (int)pad, (int)KH, (int)KW, wout.data_ptr<float>(), M, (int)Co,
-                  x.scalar_type() == at::kFloat, (int)cfg, (int)splits, cur_stream(x));
+                  x.scalar_type() == at::kFloat, (int)cfg, (int)splits, has_lz ? &lz : nullptr, cur_stream(x));
 }
 
 // fused residual add (+ dropout) + LayerNorm (ln.hip)
@@ -1434,11 +1560,11 @@ TORCH_LIBRARY(gksgd, m) {
   m.def("cast_bf16(Tensor(a!) dst, Tensor src) -> ()");
   m.def("gemm_supported(int N, int K) -> bool", &gemm_supported);
   m.def("gemm_nt(Tensor A, Tensor B, Tensor(a!) C, int cfg=0, int max_blocks=0, Tensor(b!)? stats=None, "
-        "Tensor? bias=None, Tensor? bn_h=None, Tensor? bn_dy2=None, Tensor? bn_mask=None) -> int");
-  m.def("gemm_tn_acc(Tensor G, Tensor X, Tensor(a!) W, int cfg=0, int splits=0) -> ()");
+        "Tensor? bias=None, Tensor? bn_h=None, Tensor? bn_dy2=None, Tensor? bn_mask=None, Tensor? lz_x=None, Tensor? lz_coef=None, Tensor? lz_padz=None, Tensor? lz_padx=None) -> int");
+  m.def("gemm_tn_acc(Tensor G, Tensor X, Tensor(a!) W, int cfg=0, int splits=0, Tensor? lz_x=None, Tensor? lz_coef=None, Tensor? lz_padz=None, Tensor? lz_padx=None) -> ()");
   m.def("conv_nt(Tensor x, Tensor w, Tensor(a!) y, Tensor zero, int stride, int pad, int cfg=0, int max_blocks=0, "
-        "Tensor(b!)? stats=None, Tensor? bias=None, Tensor? bn_h=None, Tensor? bn_dy2=None, Tensor? bn_mask=None) "
-        "-> int");
+        "Tensor(b!)? stats=None, Tensor? bias=None, Tensor? bn_h=None, Tensor? bn_dy2=None, Tensor? bn_mask=None, "
+        "Tensor? lz_x=None, Tensor? lz_coef=None, Tensor? lz_padz=None, Tensor? lz_padx=None) -> int");
   m.def("stem_supported(int H, int W) -> bool", [](int64_t H, int64_t W) { return gk::stem_supported((int)H, (int)W); });
   m.def("stem_wgrad_ws(int N, int H, int W) -> int", &stem_wgrad_ws);
   m.def("stem_pack(Tensor w, Tensor(a!) wp) -> ()");
@@ -1449,7 +1575,15 @@ TORCH_LIBRARY(gksgd, m) {
   });
   m.def("wgrad3_ws(int N, int H, int W, int C, int K) -> int", &wgrad3_ws);
   m.def("conv3_wgrad(Tensor dy, Tensor x, Tensor(a!) out, Tensor(b!) part, Tensor zero) -> ()");
-  m.def("conv_dgrad_s2(Tensor dy, Tensor w, Tensor(a!) dx, Tensor zero, int cfg=0, int max_blocks=0) -> ()");
+  m.def("conv_dgrad_s2(Tensor dy, Tensor w, Tensor(a!) dx, Tensor zero, int cfg=0, int max_blocks=0, "
+        "Tensor? lz_x=None, Tensor? lz_coef=None, Tensor? lz_padz=None, Tensor? lz_padx=None) -> ()");
+  m.def("bn_bwd_lazy_pre(Tensor x, Tensor part, int rows, Tensor? w, Tensor mean, Tensor invstd, "
+        "Tensor(a!) dgamma, Tensor(b!) dbeta, Tensor(c!) coef, Tensor(d!) padz, Tensor(e!) padx, "
+        "Tensor(f!)? gw_acc=None, Tensor(g!)? gb_acc=None) -> ()");
+  m.def("bn_act_backward_lazy(Tensor dy, Tensor? dy2, Tensor? mask, Tensor x, Tensor(a!) dz, Tensor? w, "
+        "Tensor mean, Tensor invstd, Tensor(b!) dgamma, Tensor(c!) dbeta, Tensor(d!) ws, bool relu, "
+        "Tensor(e!) coef, Tensor(f!) padz, Tensor(g!) padx, Tensor(h!)? gw_acc=None, Tensor(i!)? gb_acc=None) -> ()");
+  m.def("bn_lazy_apply(Tensor dz, Tensor x, Tensor(a!) dx, Tensor coef) -> ()");
   m.def("bn_act_backward_pre(Tensor dz, Tensor x, Tensor(a!) dx, Tensor? w, Tensor mean, Tensor invstd, "
         "Tensor(b!) dgamma, Tensor(c!) dbeta, Tensor part, int rows, Tensor(d!)? gw_acc=None, "
         "Tensor(e!)? gb_acc=None) -> ()");
@@ -1476,7 +1610,8 @@ TORCH_LIBRARY(gksgd, m) {
   m.def("add_ln_backward(Tensor dy, Tensor h, Tensor mean, Tensor rstd, Tensor? gamma, Tensor(a!) dx, "
         "Tensor(b!)? da, Tensor(c!)? dgamma, Tensor(d!)? dbeta, bool accumulate, Tensor(e!) ws, float p, int seed, "
         "Tensor? seed_dev=None) -> ()");
-  m.def("conv_tn_acc(Tensor dy, Tensor x, Tensor(a!) wout, Tensor zero, int stride, int pad, int cfg=0, int splits=0) -> ()");
+  m.def("conv_tn_acc(Tensor dy, Tensor x, Tensor(a!) wout, Tensor zero, int stride, int pad, int cfg=0, int splits=0, "
+        "Tensor? lz_x=None, Tensor? lz_coef=None, Tensor? lz_padz=None, Tensor? lz_padx=None) -> ()");
   m.def("colsum_acc(Tensor dy, Tensor(a!) db) -> ()");
   m.def("gelu_bwd_colsum(Tensor dy, Tensor pre, Tensor(a!) dpre, Tensor(b!)? db=None) -> ()");
   m.def("lstm_rec_gemm(Tensor A, Tensor B, Tensor(a!) P, int S) -> ()");
@@ -1525,6 +1660,9 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("bn_act_forward", &bn_act_forward);
   m.impl("bn_act_backward", &bn_act_backward);
   m.impl("bn_act_backward_pre", &bn_act_backward_pre);
+  m.impl("bn_bwd_lazy_pre", &bn_bwd_lazy_pre);
+  m.impl("bn_act_backward_lazy", &bn_act_backward_lazy);
+  m.impl("bn_lazy_apply", &bn_lazy_apply);
   m.impl("stem_pack", &stem_pack);
   m.impl("conv_dgrad_s2", &conv_dgrad_s2);
   m.impl("conv3_wgrad", &conv3_wgrad);

@@ -27,6 +27,10 @@ namespace gk {
 namespace {
 
 __device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+__device__ __forceinline__ uint16_t f32_to_bf16(float f);
+__device__ __forceinline__ float round_to_bf16(float f) { return bf16_to_f32(f32_to_bf16(f)); }
+__device__ __forceinline__ void store_elem(float* p, float v) { *p = v; }
+__device__ __forceinline__ void store_elem(uint16_t* p, float v) { *p = f32_to_bf16(v); }
 
 __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
   uint32_t u = __float_as_uint(f);
@@ -601,6 +605,47 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_finalize_kernel(const float* __
   if (gw_acc) gw_acc[c] += (float)b;
 }
 
+// Lazy backward apply (the consumer kernels compute dx themselves): finalize as
+// above and emit, per channel, the coefficients of
+//   dx = k1 * ((dz - k2) - (x - mu) * k4),  k1 = gamma invstd, k2 = mean(dz),
+//   k4 = invstd^2 mean(dz (x - mu)) ... = invstd * mean(dz * xhat)
+// as coef[c] = {k1, k2, mu, k4}, plus the two padding rows padz = k2 and
+// padx = mu in the activation dtype: a padding tap that loads them yields
+// exactly dx = 0 (gemm.hip LazyA / LazyG).  center: the dgamma partials are
+// sum(dz * x) (GEMM epilogue) rather than sum(dz * xhat) (reduce pass).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void bn_bwd_finalize_lazy_kernel(
+    const float* __restrict__ pdb, const float* __restrict__ pdg, int gy, int C, int64_t M, int center,
+    const float* __restrict__ w, const float* __restrict__ mean, const float* __restrict__ invstd,
+    float* __restrict__ dbeta, float* __restrict__ dgamma, float* __restrict__ gb_acc, float* __restrict__ gw_acc,
+    float4* __restrict__ coef, T* __restrict__ padz, T* __restrict__ padx) {
+  double a = 0.0, b = 0.0;
+  bool owner;
+  int c;
+  reduce_partials2(pdb, pdg, gy, C, &a, &b, &owner, &c);
+  if (!owner) return;
+  const float is = invstd[c];
+  if (center) b = (double)is * (b - (double)mean[c] * a);
+  dbeta[c] = (float)a;
+  dgamma[c] = (float)b;
+  if (gb_acc) gb_acc[c] += (float)a;
+  if (gw_acc) gw_acc[c] += (float)b;
+  const float invM = 1.f / (float)M;
+  const float gam = w ? w[c] : 1.f;
+  const float k1 = gam * is;
+  const float k2 = (float)a * invM;
+  const float k4 = is * ((float)b * invM);
+  float mu = mean[c];
+  float k2r = k2;
+  if (sizeof(T) == 2) {   // bf16 padding rows: the transform subtracts the same rounded values
+    k2r = round_to_bf16(k2);
+    mu = round_to_bf16(mu);
+  }
+  coef[c] = make_float4(k1, k2r, mu, k4);
+  store_elem(padz + c, k2r);
+  store_elem(padx + c, mu);
+}
+
 template <typename T, typename Src, bool DRES, int U = kBnUnroll>
 __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(Src src, const T* __restrict__ x, T* __restrict__ dx,
                                                               T* __restrict__ dres, int64_t M, int C, Geo g,
@@ -952,6 +997,93 @@ void bn_bwd_apply_pre_t(const T* dz, const T* x, T* dx, int64_t M, int C, const 
   hipLaunchKernelGGL((bn_bwd_apply_kernel<T, DyPlain<T, false, false>, false>), dim3(g.gx, g.gy), dim3(kBlock), 0, s,
                      DyPlain<T, false, false>{dz, nullptr, nullptr}, x, dx, (T*)nullptr, M, C, g, w, mean, invstd,
                      dbeta, dgamma);
+}
+
+void bn_bwd_finalize_lazy(const float* pdb, const float* pdg, int gy, int64_t M, int C, int elem_bytes, int center,
+                          const float* w, const float* mean, const float* invstd, float* dgamma, float* dbeta,
+                          float* gw_acc, float* gb_acc, float* coef, void* padz, void* padx, hipStream_t s) {
+  const dim3 grid((C + kFinC - 1) / kFinC);
+  if (elem_bytes == 2)
+    hipLaunchKernelGGL(bn_bwd_finalize_lazy_kernel<uint16_t>, grid, dim3(kBlock), 0, s, pdb, pdg, gy, C, M, center, w,
+                       mean, invstd, dbeta, dgamma, gb_acc, gw_acc, reinterpret_cast<float4*>(coef),
+                       static_cast<uint16_t*>(padz), static_cast<uint16_t*>(padx));
+  else
+    hipLaunchKernelGGL(bn_bwd_finalize_lazy_kernel<float>, grid, dim3(kBlock), 0, s, pdb, pdg, gy, C, M, center, w,
+                       mean, invstd, dbeta, dgamma, gb_acc, gw_acc, reinterpret_cast<float4*>(coef),
+                       static_cast<float*>(padz), static_cast<float*>(padx));
+}
+
+// Full (unlinked) backward without the apply pass: the reduce pass writes dz
+// (ReLU-masked, twin-summed dy) and the partials; the finalize emits the lazy
+// coefficients.  dz doubles as the residual gradient.
+template <typename T>
+void bn_backward_lazy_t(const T* dy, const T* dy2, const uint8_t* mask, const T* x, T* dz, int64_t M, int C,
+                        const float* w, const float* mean, const float* invstd, float* dgamma, float* dbeta, float* ws,
+                        int relu, float* gw_acc, float* gb_acc, float* coef, void* padz, void* padx, hipStream_t s) {
+  const Geo g = make_geo<T>(M, C, kTargetBlocks);
+  float* pdb = ws;
+  float* pdg = ws + (int64_t)g.gy * C;
+#define GK_RED(R, TW)                                                                                              \
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, DyPlain<T, R, TW>, true>), dim3(g.gx, g.gy), dim3(kBlock), 0, s,      \
+                     DyPlain<T, R, TW>{dy, dy2, mask}, x, M, C, g, mean, invstd, pdb, pdg, dz)
+  if (relu && dy2) GK_RED(true, true);
+  else if (relu) GK_RED(true, false);
+  else if (dy2) GK_RED(false, true);
+  else GK_RED(false, false);
+#undef GK_RED
+  bn_bwd_finalize_lazy(pdb, pdg, g.gy, M, C, sizeof(T), 0, w, mean, invstd, dgamma, dbeta, gw_acc, gb_acc, coef,
+                       padz, padx, s);
+}
+
+void bn_act_backward_lazy(const void* dy, const void* dy2, const uint8_t* mask, const void* x, void* dz, int64_t M,
+                          int C, int elem_bytes, const float* w, const float* mean, const float* invstd,
+                          float* dgamma, float* dbeta, float* ws, int relu, float* gw_acc, float* gb_acc, float* coef,
+                          void* padz, void* padx, hipStream_t s) {
+  if (elem_bytes == 2)
+    bn_backward_lazy_t<uint16_t>((const uint16_t*)dy, (const uint16_t*)dy2, mask, (const uint16_t*)x, (uint16_t*)dz,
+                                 M, C, w, mean, invstd, dgamma, dbeta, ws, relu, gw_acc, gb_acc, coef, padz, padx, s);
+  else
+    bn_backward_lazy_t<float>((const float*)dy, (const float*)dy2, mask, (const float*)x, (float*)dz, M, C, w, mean,
+                              invstd, dgamma, dbeta, ws, relu, gw_acc, gb_acc, coef, padz, padx, s);
+}
+
+// Materialise a lazy dx (a consumer that cannot take the lazy operand):
+// dx = k1 * ((dz - k2) - (x - mu) * k4) from the coefficient table.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void bn_lazy_apply_kernel(const T* __restrict__ dz, const T* __restrict__ x,
+                                                               T* __restrict__ dx, int64_t M, int C, Geo g,
+                                                               const float4* __restrict__ coef) {
+  constexpr int V = Vec<T>::N;
+  const int tc = threadIdx.x % g.tpr;
+  const int lane_r = threadIdx.x / g.tpr;
+  const int c0 = blockIdx.x * g.ct + tc * V;
+  float4 cf[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) cf[i] = coef[c0 + i];
+  const int64_t r0 = (int64_t)blockIdx.y * g.rows_per_block;
+  int64_t r1 = r0 + g.rows_per_block;
+  if (r1 > M) r1 = M;
+  for (int64_t r = lane_r < g.rl ? r0 + lane_r : r1; r < r1; r += g.rl) {
+    float d[V], xv[V], o[V];
+    Vec<T>::load(dz + r * C + c0, d);
+    Vec<T>::load(x + r * C + c0, xv);
+#pragma unroll
+    for (int i = 0; i < V; ++i) o[i] = cf[i].x * ((d[i] - cf[i].y) - (xv[i] - cf[i].z) * cf[i].w);
+    Vec<T>::store(dx + r * C + c0, o);
+  }
+}
+
+void bn_lazy_apply(const void* dz, const void* x, void* dx, int64_t M, int C, int elem_bytes, const float* coef,
+                   hipStream_t s) {
+  if (elem_bytes == 2) {
+    const Geo g = make_geo<uint16_t>(M, C, kTargetBlocks);
+    hipLaunchKernelGGL(bn_lazy_apply_kernel<uint16_t>, dim3(g.gx, g.gy), dim3(kBlock), 0, s, (const uint16_t*)dz,
+                       (const uint16_t*)x, (uint16_t*)dx, M, C, g, reinterpret_cast<const float4*>(coef));
+  } else {
+    const Geo g = make_geo<float>(M, C, kTargetBlocks);
+    hipLaunchKernelGGL(bn_lazy_apply_kernel<float>, dim3(g.gx, g.gy), dim3(kBlock), 0, s, (const float*)dz,
+                       (const float*)x, (float*)dx, M, C, g, reinterpret_cast<const float4*>(coef));
+  }
 }
 
 void bn_act_backward_pre(const void* dz, const void* x, void* dx, int64_t M, int C, int elem_bytes, const float* w,

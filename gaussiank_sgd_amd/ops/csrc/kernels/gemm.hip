@@ -101,6 +101,22 @@ struct BnBwd {
                           // m * (N / V) + n / V, V = 8 (bf16) or 4 (fp32) -- bn_act.hip's layout
 };
 
+// Lazy BatchNorm-backward operand (fp32): the A operand (NT) / G operand (TN)
+// is the gradient of a BN input, dx = k1 ((dz - k2) - (x - mu) k4), which is
+// never materialised -- the kernel stages dz AND x tiles and applies the
+// per-channel affine map after its LDS reads (bn_act.hip bn_bwd_finalize_lazy
+// makes coef[c] = {k1, k2, mu, k4}).  Padding taps load the rows padz = k2 and
+// padx = mu, so they contribute exactly 0.  The BN's apply pass (read dz and
+// x, write dx) disappears; the two consumers (grad-input and grad-weight of
+// the producing convolution) read dz and x instead of dx.
+struct LazyA {
+  const void* x;          // BN input, same layout / strides as the dz operand
+  const float* coef;      // [C] x {k1, k2, mu, k4}
+  const void* padz;       // [C] padding row of dz (k2)
+  const void* padx;       // [C] padding row of x (mu)
+  int C;                  // channels of dz (coefficient table length)
+};
+
 // --------------------------------------------------------------------------
 // gemm_nt
 // --------------------------------------------------------------------------
@@ -124,7 +140,7 @@ struct Elem {
   static constexpr int ST_PER_SUB = F32 ? 4 : 2;
 };
 
-template <int WM, int WN, bool BRES, int MSB = 4, typename T = uint16_t>
+template <int WM, int WN, bool BRES, int MSB = 4, typename T = uint16_t, bool LZ = false>
 struct NtCfg {
   static constexpr int NW = WM * WN;
   static constexpr int THREADS = 64 * NW;
@@ -132,32 +148,40 @@ struct NtCfg {
   static constexpr int BM = WTM * WM;
   static constexpr int BN = 64 * WN;
   static constexpr int ASTAGE = BM * 128;         // bytes: BM rows x one K slice
+  static constexpr int NACOPY = LZ ? 2 : 1;       // lazy BN operand: dz and x tiles
+  static constexpr int ASTAGES = NACOPY * ASTAGE;
   static constexpr int BSTAGE = BN * 128;
-  static constexpr int STAGE = BRES ? ASTAGE : ASTAGE + BSTAGE;
+  static constexpr int STAGE = BRES ? ASTAGES : ASTAGES + BSTAGE;
   static constexpr int INSTS = STAGE / 1024;      // 1-KiB LDS-DMA instructions per stage
   static_assert(INSTS % NW == 0, "stage split");
   static constexpr int LPW = INSTS / NW;          // LDS-DMA instructions per wave per stage
   static_assert((BM / 8) % NW == 0, "A rows split evenly over the waves");
-  static constexpr int LPWA = BRES ? LPW : (BM / 8) / NW;   // of which A-row instructions (j < LPWA)
+  static constexpr int LPWA = BRES ? LPW : NACOPY * (BM / 8) / NW;   // of which A-row instructions (j < LPWA)
   static constexpr int NST = Elem<T>::ST_PER_SUB * MSB;     // 16-byte epilogue stores per wave per tile
   static_assert(LPW + 2 * NST <= 63, "wait_vmcnt range (vmcnt is 6 bits)");
   static constexpr bool NS4_OK = 2 * LPW + 3 * NST <= 63;   // four stages: 2 stages + 3 tiles of stores in flight
-  static int lds_bytes(int K, int ns) { return ns * STAGE + (BRES ? BN * K * (int)sizeof(T) : 0); }
+  // LDS: [lazy coefficient table][resident weight panel][stages]
+  __host__ __device__ static int coef_bytes(int C) { return LZ ? ((C * 16 + 1023) / 1024) * 1024 : 0; }
+  static int lds_bytes(int K, int ns, int C = 0) {
+    return ns * STAGE + (BRES ? BN * K * (int)sizeof(T) : 0) + coef_bytes(C);
+  }
 };
 
-template <int WM, int WN, bool BRES, int NS, bool GATHER, int MSB = 4, bool BNB = false, typename T = uint16_t>
+template <int WM, int WN, bool BRES, int NS, bool GATHER, int MSB = 4, bool BNB = false, typename T = uint16_t,
+          bool LZ = false>
 __global__ void __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(WM * WN >= 8 ? 1 : 2)))
 gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
                T* __restrict__ C, int64_t ldc, int64_t M, int K, ConvGeo geo, float* __restrict__ stats,
-               int64_t stats_ld, BnBwd bb) {
+               int64_t stats_ld, BnBwd bb, LazyA lz) {
   // stats != nullptr: per-block BatchNorm partials of the (dtype-rounded)
   // output, psum at stats[blockIdx.x * N + n], psq at stats[stats_ld + ...]
   // (the [gy][C] layout bn_finalize_kernel reduces).  With bb.h (BN-backward
   // epilogue, MSB == 4 tiles only) the partials are sum(dz), sum(dz*h); the
   // finalize centres the second with the mean.
-  using Cfg = NtCfg<WM, WN, BRES, MSB, T>;
+  using Cfg = NtCfg<WM, WN, BRES, MSB, T, LZ>;
   using E = Elem<T>;
   constexpr bool F32 = E::F32;
+  static_assert(!LZ || F32, "lazy BN operand: fp32 kernels");
   constexpr int EPC = E::EPC;
   constexpr int KS = E::KS;
   static_assert(!BNB || MSB == 4, "BN-backward epilogue: 64x64 wave tiles");
@@ -184,15 +208,25 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
       }
     return;
   }
-  char* stage_base = smem + (BRES ? Cfg::BN * K * (int)sizeof(T) : 0);
+  const int coefb = Cfg::coef_bytes(lz.C);
+  char* panel = smem + coefb;
+  char* stage_base = panel + (BRES ? Cfg::BN * K * (int)sizeof(T) : 0);
+  if (LZ) {
+    // lazy BN coefficients -> LDS (read back per fragment); drained before any
+    // stage is issued, so the pipeline's vmcnt bookkeeping is untouched
+    float4* ct = reinterpret_cast<float4*>(smem);
+    const float4* cg = reinterpret_cast<const float4*>(lz.coef);
+    for (int c = threadIdx.x; c < lz.C; c += Cfg::THREADS) ct[c] = cg[c];
+    __syncthreads();
+  }
 
-  if (BRES) {  // weight panel: slice ks at smem + ks*BSTAGE, rows swizzled as the streamed tiles
+  if (BRES) {  // weight panel: slice ks at panel + ks*BSTAGE, rows swizzled as the streamed tiles
     const int per = Cfg::BN / 8;
     for (int i = wave; i < nk * per; i += Cfg::NW) {
       const int ks = i / per, ri = i % per;
       const int r = ri * 8 + (lane >> 3);
       const int c = (lane & 7) ^ swz(r);
-      glds16(B + (int64_t)(n0 + r) * ldb + ks * KS + c * EPC, (GK_LDS char*)smem + ks * Cfg::BSTAGE + ri * 1024);
+      glds16(B + (int64_t)(n0 + r) * ldb + ks * KS + c * EPC, (GK_LDS char*)panel + ks * Cfg::BSTAGE + ri * 1024);
     }
   }
 
@@ -206,14 +240,20 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
   // step tests two bits instead of recomputing and comparing the position)
   uint32_t okh[LPW], okw[LPW];
   const T* zrow[LPW];         // gather: this lane's chunk of the zero row (padding taps)
+  // lazy operand: instructions i in [BM/8, 2 BM/8) stage the x tile; its
+  // rows are the dz rows at a fixed element offset (same layout)
+  const int64_t xoff = LZ ? static_cast<const T*>(lz.x) - A : 0;
 #pragma unroll
   for (int j = 0; j < LPW; ++j) {
     const int i = wave + j * Cfg::NW;
     const int r = i * 8 + (lane >> 3);
     const int c = (lane & 7) ^ swz(r);
-    ptr[j] = j < Cfg::LPWA ? nullptr : B + (int64_t)(n0 + r - Cfg::BM) * ldb + c * EPC;
+    const bool isx = LZ && i >= Cfg::BM / 8 && j < Cfg::LPWA;
+    ptr[j] = j < Cfg::LPWA ? nullptr : B + (int64_t)(n0 + r - Cfg::NACOPY * Cfg::BM) * ldb + c * EPC;
     okh[j] = okw[j] = 0u;
-    zrow[j] = GATHER ? static_cast<const T*>(geo.zero) + c * EPC : nullptr;
+    zrow[j] = !GATHER ? nullptr
+              : LZ ? static_cast<const T*>(isx ? lz.padx : lz.padz) + c * EPC
+                   : static_cast<const T*>(geo.zero) + c * EPC;
   }
   auto set_rows = [&](int64_t mt) {
     const int64_t m0 = mt * Cfg::BM;
@@ -221,7 +261,9 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
     for (int j = 0; j < LPW; ++j) {
       const int i = wave + j * Cfg::NW;
       if (j < Cfg::LPWA) {
-        const int r = i * 8 + (lane >> 3);
+        const int ia = (LZ && i >= Cfg::BM / 8) ? i - Cfg::BM / 8 : i;   // row group within its A copy
+        const int64_t xo = (LZ && i >= Cfg::BM / 8) ? xoff : 0;
+        const int r = ia * 8 + (lane >> 3);
         const int c = (lane & 7) ^ swz(r);
         int64_t gr = m0 + r;
         gr = gr < M ? gr : M - 1;
@@ -240,9 +282,9 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
           }
           okh[j] = bh;
           okw[j] = bw;
-          ptr[j] = A + (((int64_t)n * geo.H + ih0) * geo.W + iw0) * geo.C + c * EPC;
+          ptr[j] = A + xo + (((int64_t)n * geo.H + ih0) * geo.W + iw0) * geo.C + c * EPC;
         } else {
-          ptr[j] = A + gr * lda + c * EPC;
+          ptr[j] = A + xo + gr * lda + c * EPC;
         }
       }
     }
@@ -264,7 +306,7 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
       if (j < Cfg::LPWA) {
         if (GATHER) {
           const bool ok = ((okh[j] >> s_kh) & (okw[j] >> s_kw) & 1u) != 0u;
-          src = ok ? ptr[j] + toff : zrow[j];
+          src = ok ? ptr[j] + toff : zrow[j] + (LZ ? s_c0 : 0);   // lazy: per-channel padding rows
         } else {
           src = ptr[j] + k0;
         }
@@ -331,7 +373,9 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
     if (s_t < T_) stage();
     const char* As = stage_base + buf * Cfg::STAGE;
     buf = buf + 1 == NS ? 0 : buf + 1;
-    const char* Bs = BRES ? smem + ks * Cfg::BSTAGE : As + Cfg::ASTAGE;
+    const char* Bs = BRES ? panel + ks * Cfg::BSTAGE : As + Cfg::ASTAGES;
+    // lazy operand: channel of element 0 of this slice (K = taps x C, tap-major)
+    const int cbase = LZ ? (ks * KS) % lz.C : 0;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int c = kk * 4 + fq;
@@ -349,6 +393,20 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
         for (int s = 0; s < 4; ++s) {
           const int rb = wn * 64 + s * 16 + fr;
           bv[s] = *reinterpret_cast<const f32x4*>(Bs + rb * 128 + ((c ^ swz(rb)) << 4));
+        }
+        if constexpr (LZ) {
+          // dx = k1 ((dz - k2) - (x - mu) k4) for channels cbase + 4c .. +3
+          const float4* ct = reinterpret_cast<const float4*>(smem) + cbase + 4 * c;
+          float4 cf[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) cf[e] = ct[e];
+#pragma unroll
+          for (int s = 0; s < MSB; ++s) {
+            const int ra = wm * Cfg::WTM + s * 16 + fr;
+            const f32x4 xv = *reinterpret_cast<const f32x4*>(As + Cfg::ASTAGE + ra * 128 + ((c ^ swz(ra)) << 4));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) av[s][e] = cf[e].x * ((av[s][e] - cf[e].y) - (xv[e] - cf[e].z) * cf[e].w);
+          }
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -567,14 +625,15 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
   }
 }
 
-template <int WM, int WN, bool BRES, int NS, bool GATHER, int MSB = 4, bool BNB = false, typename T = uint16_t>
+template <int WM, int WN, bool BRES, int NS, bool GATHER, int MSB = 4, bool BNB = false, typename T = uint16_t,
+          bool LZ = false>
 int launch_nt(const T* A, int64_t lda, const T* B, int64_t ldb, T* C, int64_t ldc, int64_t M,
               int N, int K, int max_blocks, const ConvGeo& geo, float* stats, int64_t stats_ld, int stats_rows,
-              const BnBwd& bb, hipStream_t stream) {
-  using Cfg = NtCfg<WM, WN, BRES, MSB, T>;
+              const BnBwd& bb, const LazyA& lz, hipStream_t stream) {
+  using Cfg = NtCfg<WM, WN, BRES, MSB, T, LZ>;
   const int ntiles = N / Cfg::BN;
   const int64_t mtiles = (M + Cfg::BM - 1) / Cfg::BM;
-  const int lds = Cfg::lds_bytes(K, NS);
+  const int lds = Cfg::lds_bytes(K, NS, lz.C);
   const int per_cu = (160 * 1024) / lds > 0 ? (160 * 1024) / lds : 1;
   int64_t gx = ((int64_t)256 * per_cu + ntiles - 1) / ntiles;
   if (max_blocks > 0) gx = max_blocks;
@@ -583,34 +642,36 @@ int launch_nt(const T* A, int64_t lda, const T* B, int64_t ldb, T* C, int64_t ld
   if (stats && gx > stats_rows) gx = stats_rows;   // one partial row per block
   dim3 grid((unsigned)gx, (unsigned)ntiles);
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<WM, WN, BRES, NS, GATHER, MSB, BNB, T>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<WM, WN, BRES, NS, GATHER, MSB, BNB, T, LZ>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL((gemm_nt_kernel<WM, WN, BRES, NS, GATHER, MSB, BNB, T>), grid, dim3(Cfg::THREADS), lds, stream, A,
-                     lda, B, ldb, C, ldc, M, K, geo, stats, stats_ld, bb);
+  hipLaunchKernelGGL((gemm_nt_kernel<WM, WN, BRES, NS, GATHER, MSB, BNB, T, LZ>), grid, dim3(Cfg::THREADS), lds, stream,
+                     A, lda, B, ldb, C, ldc, M, K, geo, stats, stats_ld, bb, lz);
   return (int)gx;
 }
 
-template <int WM, int WN, bool GATHER, int MSB = 4, bool BNB = false, typename T = uint16_t>
+template <int WM, int WN, bool GATHER, int MSB = 4, bool BNB = false, typename T = uint16_t, bool LZ = false>
 int launch_nt_any(const T* A, int64_t lda, const T* B, int64_t ldb, T* C, int64_t ldc,
                   int64_t M, int N, int K, int max_blocks, int bres, int ns, const ConvGeo& geo, float* stats,
-                  int64_t stats_ld, int stats_rows, const BnBwd& bb, hipStream_t stream) {
-  using CR = NtCfg<WM, WN, true, MSB, T>;
-  using CS = NtCfg<WM, WN, false, MSB, T>;
+                  int64_t stats_ld, int stats_rows, const BnBwd& bb, const LazyA& lz, hipStream_t stream) {
+  using CR = NtCfg<WM, WN, true, MSB, T, LZ>;
+  using CS = NtCfg<WM, WN, false, MSB, T, LZ>;
+  const int cc = lz.C;
   // keep the weight panel resident when it fits next to the two A stages
   if (bres < 0) bres = (64 * WN) * K * (int)sizeof(T) <= 64 * 1024;
-  if (bres && CR::lds_bytes(K, 2) > 160 * 1024) bres = 0;
+  if (bres && CR::lds_bytes(K, 2, cc) > 160 * 1024) bres = 0;
   constexpr int L = 160 * 1024;
 #define GK_NT(BR, S) \
-  launch_nt<WM, WN, BR, S, GATHER, MSB, BNB, T>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, bb, stream)
-  if (ns == 4 && bres && CR::NS4_OK && CR::lds_bytes(K, 4) <= L) return GK_NT(true, 4);
-  if (ns == 4 && !bres && CS::NS4_OK && CS::lds_bytes(K, 4) <= L) return GK_NT(false, 4);
+  launch_nt<WM, WN, BR, S, GATHER, MSB, BNB, T, LZ>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, bb, lz, stream)
+  if (ns == 4 && bres && CR::NS4_OK && CR::lds_bytes(K, 4, cc) <= L) return GK_NT(true, 4);
+  if (ns == 4 && !bres && CS::NS4_OK && CS::lds_bytes(K, 4, cc) <= L) return GK_NT(false, 4);
   if (bres) {
-    if (ns != 2 && CR::lds_bytes(K, 3) <= L) return GK_NT(true, 3);
+    if (ns != 2 && CR::lds_bytes(K, 3, cc) <= L) return GK_NT(true, 3);
     return GK_NT(true, 2);
   }
-  if (ns != 2 && CS::lds_bytes(K, 3) <= L) return GK_NT(false, 3);
+  if (ns != 2 && CS::lds_bytes(K, 3, cc) <= L) return GK_NT(false, 3);
+  if (CS::lds_bytes(K, 2, cc) > L) return -1;   // does not fit (lazy coefficient table too large)
   return GK_NT(false, 2);
 #undef GK_NT
 }
@@ -976,7 +1037,7 @@ void launch_tn(const uint16_t* G, int64_t ldg, const uint16_t* X, int64_t ldx, f
 // pixel rows (two 16-row k-groups, 128 MFMAs per wave) per LDS stage.
 __device__ __attribute__((aligned(16))) float g_tn_zero[32];
 
-template <int WN, int WK, int NS_>
+template <int WN, int WK, int NS_, bool LZ = false>
 struct TnF32Cfg {
   static constexpr int NW = WN * WK;
   static constexpr int THREADS = 64 * NW;
@@ -985,11 +1046,14 @@ struct TnF32Cfg {
   static constexpr int ROWS = 32;
   static constexpr int GROW = BN * 4;
   static constexpr int XROW = BK * 4;
-  static constexpr int GBYTES = ROWS * GROW;
-  static constexpr int STAGE = ROWS * (GROW + XROW);
+  static constexpr int NGCOPY = LZ ? 2 : 1;        // lazy BN operand: dz and x tiles of G
+  static constexpr int GBYTES = ROWS * GROW;       // one G copy
+  static constexpr int GBYTES_ALL = NGCOPY * GBYTES;
+  static constexpr int STAGE = ROWS * (NGCOPY * GROW + XROW);
   static constexpr int NS = NS_;
   static constexpr int LDS = NS * STAGE;
-  static constexpr int GINSTS = GBYTES / 1024;
+  static constexpr int GINSTS1 = GBYTES / 1024;
+  static constexpr int GINSTS = GBYTES_ALL / 1024;
   static constexpr int INSTS = STAGE / 1024;
   static_assert(INSTS % NW == 0 && GINSTS % NW == 0, "stage split");
   static constexpr int LPW = INSTS / NW;
@@ -999,11 +1063,11 @@ struct TnF32Cfg {
 
 __device__ __forceinline__ int swz4(int r) { return r & 4; }
 
-template <int WN, int WK, int NS, bool GATHER>
+template <int WN, int WK, int NS, bool GATHER, bool LZ = false>
 __global__ void __launch_bounds__(64 * WN * WK) __attribute__((amdgpu_waves_per_eu(1)))
 gemm_tn_f32_kernel(const float* __restrict__ G, int64_t ldg, const float* __restrict__ X, int64_t ldx,
-                   float* __restrict__ W, int64_t ldw, int64_t M, int64_t rows_per_split, ConvGeo geo) {
-  using Cfg = TnF32Cfg<WN, WK, NS>;
+                   float* __restrict__ W, int64_t ldw, int64_t M, int64_t rows_per_split, ConvGeo geo, LazyA lz) {
+  using Cfg = TnF32Cfg<WN, WK, NS, LZ>;
   constexpr int LPW = Cfg::LPW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
@@ -1029,10 +1093,11 @@ gemm_tn_f32_kernel(const float* __restrict__ G, int64_t ldg, const float* __rest
     dkh[j] = dkw[j] = 0;
     if (j < Cfg::LPWG) {
       constexpr int CPR = Cfg::GROW / 16;
-      const int e = i * 64 + lane;
+      const bool isx = LZ && i >= Cfg::GINSTS1;    // lazy: second G copy = the BN input x
+      const int e = (isx ? i - Cfg::GINSTS1 : i) * 64 + lane;
       srow = e / CPR;
       colo = n0 + ((e % CPR) ^ swz4(srow)) * 4;
-      rptr[j] = G + (mbeg + srow) * ldg + colo;
+      rptr[j] = (isx ? static_cast<const float*>(lz.x) : G) + (mbeg + srow) * ldg + colo;
     } else {
       constexpr int CPR = Cfg::XROW / 16;
       const int e = (i - Cfg::GINSTS) * 64 + lane;
@@ -1109,8 +1174,13 @@ gemm_tn_f32_kernel(const float* __restrict__ G, int64_t ldg, const float* __rest
     const int xc = wk * 64 + s2 * 16 + fi;
     const int r = 4 * fg;
     goff[s2] = r * Cfg::GROW + ((((gc >> 2) ^ swz4(r)) << 4) | ((gc & 3) << 2));
-    xoff[s2] = Cfg::GBYTES + r * Cfg::XROW + ((((xc >> 2) ^ swz4(r)) << 4) | ((xc & 3) << 2));
+    xoff[s2] = Cfg::GBYTES_ALL + r * Cfg::XROW + ((((xc >> 2) ^ swz4(r)) << 4) | ((xc & 3) << 2));
   }
+  // lazy operand: coefficients of this lane's four G columns (fixed for the block)
+  float4 cf[4];
+#pragma unroll
+  for (int s2 = 0; s2 < 4; ++s2)
+    cf[s2] = LZ ? reinterpret_cast<const float4*>(lz.coef)[n0 + wn * 64 + s2 * 16 + fi] : make_float4(0.f, 0.f, 0.f, 0.f);
 
   stage(0);
   if (NS >= 3 && T > 1) stage(1);
@@ -1121,6 +1191,8 @@ gemm_tn_f32_kernel(const float* __restrict__ G, int64_t ldg, const float* __rest
     __builtin_amdgcn_sched_barrier(0);
     if (t + NS - 1 < T) stage(t + NS - 1);
     const char* sb = smem + (t % NS) * Cfg::STAGE;
+    const int64_t mst = mbeg + (int64_t)t * Cfg::ROWS;   // first row of this stage
+    const bool tail = LZ && mst + Cfg::ROWS > mend;      // lazy: rows past the split must give 0, not k1(-k2 + mu k4)
     // fragments of k-group kg: [j][s2] (32 values); the next group's reads are
     // issued before this group's 64 MFMAs so only one LDS latency per stage shows
     float gv[2][4][4], xv[2][4][4];
@@ -1132,6 +1204,15 @@ gemm_tn_f32_kernel(const float* __restrict__ G, int64_t ldg, const float* __rest
         for (int s2 = 0; s2 < 4; ++s2) {
           g[j][s2] = *reinterpret_cast<const float*>(sb + goff[s2] + rr * Cfg::GROW);
           x[j][s2] = *reinterpret_cast<const float*>(sb + xoff[s2] + rr * Cfg::XROW);
+        }
+        if constexpr (LZ) {
+          const bool live = !tail || mst + rr + 4 * fg < mend;
+#pragma unroll
+          for (int s2 = 0; s2 < 4; ++s2) {
+            const float xz = *reinterpret_cast<const float*>(sb + Cfg::GBYTES + goff[s2] + rr * Cfg::GROW);
+            const float d = cf[s2].x * ((g[j][s2] - cf[s2].y) - (xz - cf[s2].z) * cf[s2].w);
+            g[j][s2] = live ? d : 0.f;
+          }
         }
       }
     };
@@ -1162,10 +1243,10 @@ gemm_tn_f32_kernel(const float* __restrict__ G, int64_t ldg, const float* __rest
     }
 }
 
-template <int WN, int WK, int NS, bool GATHER>
+template <int WN, int WK, int NS, bool GATHER, bool LZ = false>
 void launch_tn_f32(const float* G, int64_t ldg, const float* X, int64_t ldx, float* W, int64_t ldw, int64_t M, int N,
-                   int K, int splits, const ConvGeo& geo, hipStream_t stream) {
-  using Cfg = TnF32Cfg<WN, WK, NS>;
+                   int K, int splits, const ConvGeo& geo, const LazyA& lz, hipStream_t stream) {
+  using Cfg = TnF32Cfg<WN, WK, NS, LZ>;
   const int tiles = (N / Cfg::BN) * (K / Cfg::BK);
   if (splits <= 0) {
     // two rounds of the chip's block slots (LDS-limited blocks per CU)
@@ -1187,17 +1268,17 @@ void launch_tn_f32(const float* G, int64_t ldg, const float* X, int64_t ldx, flo
   const int64_t nsplit = (M + rows - 1) / rows;
   dim3 grid((unsigned)(N / Cfg::BN), (unsigned)(K / Cfg::BK), (unsigned)nsplit);
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_f32_kernel<WN, WK, NS, GATHER>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_f32_kernel<WN, WK, NS, GATHER, LZ>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL((gemm_tn_f32_kernel<WN, WK, NS, GATHER>), grid, dim3(Cfg::THREADS), Cfg::LDS, stream, G, ldg, X,
-                     ldx, W, ldw, M, rows, geo);
+  hipLaunchKernelGGL((gemm_tn_f32_kernel<WN, WK, NS, GATHER, LZ>), grid, dim3(Cfg::THREADS), Cfg::LDS, stream, G, ldg,
+                     X, ldx, W, ldw, M, rows, geo, lz);
 }
 
 template <bool GATHER>
 void tn_f32_dispatch(const float* G, int64_t ldg, const float* X, int64_t ldx, float* W, int64_t ldw, int64_t M, int N,
-                     int K, int cfg, int splits, const ConvGeo& geo, hipStream_t stream) {
+                     int K, int cfg, int splits, const ConvGeo& geo, const LazyArgs* lza, hipStream_t stream) {
   // cfg = tile + 10 * stages (0/2: three, 1: two).  tiles (WN, WK), 64x64 per wave:
   // 1 (1,1)  2 (2,1)  3 (1,2)  4 (2,2)  5 (4,1)  6 (1,4)  7 (4,2)  8 (2,4)  9 (4,4, two stages)
   const bool ns3 = (cfg / 10) % 10 != 1;
@@ -1206,12 +1287,18 @@ void tn_f32_dispatch(const float* G, int64_t ldg, const float* X, int64_t ldx, f
   static const int cfg_bn[10] = {64, 64, 128, 64, 128, 256, 64, 256, 128, 256};
   static const int cfg_bk[10] = {64, 64, 64, 128, 128, 64, 256, 128, 256, 256};
   if (N % cfg_bn[cfg] != 0 || K % cfg_bk[cfg] != 0) cfg = 1;
-#define GK_TNF(WN_, WK_)                                                                                   \
-  do {                                                                                                     \
-    if (ns3 && TnF32Cfg<WN_, WK_, 3>::LDS <= 160 * 1024)                                                   \
-      launch_tn_f32<WN_, WK_, 3, GATHER>(G, ldg, X, ldx, W, ldw, M, N, K, splits, geo, stream);            \
-    else                                                                                                   \
-      launch_tn_f32<WN_, WK_, 2, GATHER>(G, ldg, X, ldx, W, ldw, M, N, K, splits, geo, stream);            \
+  const LazyA lz = lza ? LazyA{lza->x, lza->coef, lza->padz, lza->padx, lza->C} : LazyA{};
+#define GK_TNF(WN_, WK_)                                                                                      \
+  do {                                                                                                        \
+    if (lza) {                                                                                                \
+      if (ns3 && TnF32Cfg<WN_, WK_, 3, true>::LDS <= 160 * 1024)                                              \
+        launch_tn_f32<WN_, WK_, 3, GATHER, true>(G, ldg, X, ldx, W, ldw, M, N, K, splits, geo, lz, stream);   \
+      else                                                                                                    \
+        launch_tn_f32<WN_, WK_, 2, GATHER, true>(G, ldg, X, ldx, W, ldw, M, N, K, splits, geo, lz, stream);   \
+    } else if (ns3 && TnF32Cfg<WN_, WK_, 3>::LDS <= 160 * 1024)                                               \
+      launch_tn_f32<WN_, WK_, 3, GATHER>(G, ldg, X, ldx, W, ldw, M, N, K, splits, geo, lz, stream);           \
+    else                                                                                                      \
+      launch_tn_f32<WN_, WK_, 2, GATHER>(G, ldg, X, ldx, W, ldw, M, N, K, splits, geo, lz, stream);           \
   } while (0)
   switch (cfg) {
     case 2: GK_TNF(2, 1); break;
@@ -1221,7 +1308,15 @@ void tn_f32_dispatch(const float* G, int64_t ldg, const float* X, int64_t ldx, f
     case 6: GK_TNF(1, 4); break;
     case 7: GK_TNF(4, 2); break;
     case 8: GK_TNF(2, 4); break;
-    case 9: GK_TNF(4, 4); break;
+    case 9:
+      if (lza) {
+        GK_TNF(2, 4);   // the lazy 256x256 tile does not fit in LDS
+      } else if (ns3 && TnF32Cfg<4, 4, 3>::LDS <= 160 * 1024) {
+        launch_tn_f32<4, 4, 3, GATHER>(G, ldg, X, ldx, W, ldw, M, N, K, splits, geo, lz, stream);
+      } else {
+        launch_tn_f32<4, 4, 2, GATHER>(G, ldg, X, ldx, W, ldw, M, N, K, splits, geo, lz, stream);
+      }
+      break;
     default: GK_TNF(1, 1); break;
   }
 #undef GK_TNF
@@ -1234,7 +1329,7 @@ bool gemm_supported(int64_t N, int64_t K) { return N >= 64 && K >= 64 && N % 64 
 template <bool GATHER, typename T>
 int nt_dispatch(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N,
                 int K, int cfg, int max_blocks, const ConvGeo& geo, float* stats, int64_t stats_ld, int stats_rows,
-                const BnBwd& bb, hipStream_t stream) {
+                const BnBwd& bb, const LazyArgs* lza, hipStream_t stream) {
   // cfg = tile + 10 * panel (1: resident, 2: streamed) + 100 * stages (0: three, 1: two, 2: four; a
   // four-stage request falls back to three where the counts or the LDS do not fit)
   const int bres = (cfg / 10) % 10 == 0 ? -1 : ((cfg / 10) % 10 == 1 ? 1 : 0);
@@ -1249,33 +1344,52 @@ int nt_dispatch(const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
   // fp32 runs 64x64 wave tiles only (5-7 map to the 64x64 tile of the same block width)
   static const int cfg_bn[8] = {64, 64, 128, 256, 128, 256, 128, 256};
   if (cfg > 7 || N % cfg_bn[cfg] != 0) cfg = 1;   // the tile must divide N (B rows are not clamped)
-#define GK_NTA(WM_, WN_, MSB_, BNB_) \
-  return launch_nt_any<WM_, WN_, GATHER, MSB_, BNB_, T>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, bb, stream)
+  const LazyA lz = lza ? LazyA{lza->x, lza->coef, lza->padz, lza->padx, lza->C} : LazyA{};
+#define GK_NTA(WM_, WN_, MSB_, BNB_, LZ_) \
+  return launch_nt_any<WM_, WN_, GATHER, MSB_, BNB_, T, LZ_>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, bb, lz, stream)
+  if constexpr (sizeof(T) == 4) {
+    if (lza) {   // lazy BN-backward A operand (fp32)
+      if (bb.h) {
+        switch (cfg) {
+          case 2: GK_NTA(4, 2, 4, true, true);
+          case 3: case 5: case 7: GK_NTA(2, 4, 4, true, true);
+          case 4: case 6: GK_NTA(2, 2, 4, true, true);
+          default: GK_NTA(4, 1, 4, true, true);
+        }
+      }
+      switch (cfg) {
+        case 2: GK_NTA(4, 2, 4, false, true);
+        case 3: case 5: case 7: GK_NTA(2, 4, 4, false, true);
+        case 4: case 6: GK_NTA(2, 2, 4, false, true);
+        default: GK_NTA(4, 1, 4, false, true);
+      }
+    }
+  }
   if (bb.h) {   // BN-backward epilogue: 64x64 wave tiles only
     switch (cfg) {
-      case 2: GK_NTA(4, 2, 4, true);
-      case 3: case 5: case 7: GK_NTA(2, 4, 4, true);
-      case 4: case 6: GK_NTA(2, 2, 4, true);
-      default: GK_NTA(4, 1, 4, true);
+      case 2: GK_NTA(4, 2, 4, true, false);
+      case 3: case 5: case 7: GK_NTA(2, 4, 4, true, false);
+      case 4: case 6: GK_NTA(2, 2, 4, true, false);
+      default: GK_NTA(4, 1, 4, true, false);
     }
   }
   if constexpr (sizeof(T) == 4) {
     switch (cfg) {
-      case 2: GK_NTA(4, 2, 4, false);
-      case 3: case 5: GK_NTA(2, 4, 4, false);
-      case 7: GK_NTA(1, 4, 4, false);
-      case 4: case 6: GK_NTA(2, 2, 4, false);
-      default: GK_NTA(4, 1, 4, false);
+      case 2: GK_NTA(4, 2, 4, false, false);
+      case 3: case 5: GK_NTA(2, 4, 4, false, false);
+      case 7: GK_NTA(1, 4, 4, false, false);
+      case 4: case 6: GK_NTA(2, 2, 4, false, false);
+      default: GK_NTA(4, 1, 4, false, false);
     }
   } else {
     switch (cfg) {
-      case 2: GK_NTA(4, 2, 4, false);
-      case 3: GK_NTA(2, 4, 4, false);
-      case 4: GK_NTA(2, 2, 4, false);
-      case 5: GK_NTA(2, 4, 8, false);
-      case 6: GK_NTA(2, 2, 8, false);
-      case 7: GK_NTA(1, 4, 8, false);
-      default: GK_NTA(4, 1, 4, false);
+      case 2: GK_NTA(4, 2, 4, false, false);
+      case 3: GK_NTA(2, 4, 4, false, false);
+      case 4: GK_NTA(2, 2, 4, false, false);
+      case 5: GK_NTA(2, 4, 8, false, false);
+      case 6: GK_NTA(2, 2, 8, false, false);
+      case 7: GK_NTA(1, 4, 8, false, false);
+      default: GK_NTA(4, 1, 4, false, false);
     }
   }
 #undef GK_NTA
@@ -1283,37 +1397,37 @@ int nt_dispatch(const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
 
 int gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N, int K,
             bool f32, int cfg, int max_blocks, float* stats, int stats_rows, const float* bias, const BnBwdArgs* bn,
-            hipStream_t stream) {
+            const LazyArgs* lazy, hipStream_t stream) {
   ConvGeo g{};
   g.bias = bias;
   const BnBwd bb = bn ? BnBwd{bn->h, bn->dy2, bn->mask} : BnBwd{};
   const int64_t sld = (int64_t)stats_rows * N;
-  return f32 ? nt_dispatch<false, float>(A, lda, B, ldb, C, ldc, M, N, K, cfg, max_blocks, g, stats, sld, stats_rows, bb, stream)
-             : nt_dispatch<false, uint16_t>(A, lda, B, ldb, C, ldc, M, N, K, cfg, max_blocks, g, stats, sld, stats_rows, bb, stream);
+  return f32 ? nt_dispatch<false, float>(A, lda, B, ldb, C, ldc, M, N, K, cfg, max_blocks, g, stats, sld, stats_rows, bb, lazy, stream)
+             : nt_dispatch<false, uint16_t>(A, lda, B, ldb, C, ldc, M, N, K, cfg, max_blocks, g, stats, sld, stats_rows, bb, nullptr, stream);
 }
 
 int conv_nt(const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P, int KH, int KW,
             const void* B, void* Y, int64_t M, int N, bool f32, int cfg, int max_blocks, float* stats, int stats_rows,
-            const float* bias, const BnBwdArgs* bn, hipStream_t stream) {
+            const float* bias, const BnBwdArgs* bn, const LazyArgs* lazy, hipStream_t stream) {
   ConvGeo g{zero, H, W, C, OH, OW, S, P, KW, bias};
   const int K = KH * KW * C;
   const BnBwd bb = bn ? BnBwd{bn->h, bn->dy2, bn->mask} : BnBwd{};
   const int64_t sld = (int64_t)stats_rows * N;
-  return f32 ? nt_dispatch<true, float>(X, C, B, K, Y, N, M, N, K, cfg, max_blocks, g, stats, sld, stats_rows, bb, stream)
-             : nt_dispatch<true, uint16_t>(X, C, B, K, Y, N, M, N, K, cfg, max_blocks, g, stats, sld, stats_rows, bb, stream);
+  return f32 ? nt_dispatch<true, float>(X, C, B, K, Y, N, M, N, K, cfg, max_blocks, g, stats, sld, stats_rows, bb, lazy, stream)
+             : nt_dispatch<true, uint16_t>(X, C, B, K, Y, N, M, N, K, cfg, max_blocks, g, stats, sld, stats_rows, bb, nullptr, stream);
 }
 
 int conv_nt_remap(const void* X, int64_t ldx, const void* zero, int H, int W, int C, int OH, int OW, int KH, int KW,
                   const void* B, void* Y, int64_t M, int N, int RH, int RW, int RA, int RB, int RZ, bool f32, int cfg,
-                  int max_blocks, hipStream_t stream) {
+                  int max_blocks, const LazyArgs* lazy, hipStream_t stream) {
   ConvGeo g{zero, H, W, C, OH, OW, 1, 0, KW, nullptr, RH, RW, RA, RB, RZ};
   const int K = KH * KW * C;
   if (KH * KW == 1) {   // one tap at the class pixel itself: the plain row GEMM
-    return f32 ? nt_dispatch<false, float>(X, ldx, B, K, Y, N, M, N, K, cfg, max_blocks, g, nullptr, 0, 0, BnBwd{}, stream)
-               : nt_dispatch<false, uint16_t>(X, ldx, B, K, Y, N, M, N, K, cfg, max_blocks, g, nullptr, 0, 0, BnBwd{}, stream);
+    return f32 ? nt_dispatch<false, float>(X, ldx, B, K, Y, N, M, N, K, cfg, max_blocks, g, nullptr, 0, 0, BnBwd{}, lazy, stream)
+               : nt_dispatch<false, uint16_t>(X, ldx, B, K, Y, N, M, N, K, cfg, max_blocks, g, nullptr, 0, 0, BnBwd{}, nullptr, stream);
   }
-  return f32 ? nt_dispatch<true, float>(X, C, B, K, Y, N, M, N, K, cfg, max_blocks, g, nullptr, 0, 0, BnBwd{}, stream)
-             : nt_dispatch<true, uint16_t>(X, C, B, K, Y, N, M, N, K, cfg, max_blocks, g, nullptr, 0, 0, BnBwd{}, stream);
+  return f32 ? nt_dispatch<true, float>(X, C, B, K, Y, N, M, N, K, cfg, max_blocks, g, nullptr, 0, 0, BnBwd{}, lazy, stream)
+             : nt_dispatch<true, uint16_t>(X, C, B, K, Y, N, M, N, K, cfg, max_blocks, g, nullptr, 0, 0, BnBwd{}, nullptr, stream);
 }
 
 template <int WN, int WK, int WS, bool GATHER, int MSN = 1>
@@ -1362,21 +1476,22 @@ void tn_dispatch(const void* G, int64_t ldg, const void* X, int64_t ldx, float* 
 }
 
 void gemm_tn_acc(const void* G, int64_t ldg, const void* X, int64_t ldx, float* W, int64_t ldw, int64_t M, int N,
-                 int K, bool f32, int cfg, int splits, hipStream_t stream) {
+                 int K, bool f32, int cfg, int splits, const LazyArgs* lazy, hipStream_t stream) {
   if (f32)
     tn_f32_dispatch<false>(static_cast<const float*>(G), ldg, static_cast<const float*>(X), ldx, W, ldw, M, N, K, cfg,
-                           splits, ConvGeo{}, stream);
+                           splits, ConvGeo{}, lazy, stream);
   else
     tn_dispatch<false>(G, ldg, X, ldx, W, ldw, M, N, K, cfg, splits, ConvGeo{}, stream);
 }
 
 void conv_tn_acc(const void* G, const void* X, const void* zero, int H, int W_, int C, int OH, int OW, int S, int P,
-                 int KH, int KW, float* Wout, int64_t M, int N, bool f32, int cfg, int splits, hipStream_t stream) {
+                 int KH, int KW, float* Wout, int64_t M, int N, bool f32, int cfg, int splits, const LazyArgs* lazy,
+                 hipStream_t stream) {
   ConvGeo g{zero, H, W_, C, OH, OW, S, P, KW, nullptr};
   const int K = KH * KW * C;
   if (f32)
     tn_f32_dispatch<true>(static_cast<const float*>(G), N, static_cast<const float*>(X), C, Wout, K, M, N, K, cfg,
-                          splits, g, stream);
+                          splits, g, lazy, stream);
   else
     tn_dispatch<true>(G, N, X, C, Wout, K, M, N, K, cfg, splits, g, stream);
 }

@@ -243,6 +243,22 @@ void bn_act_forward_pre(const void* x, const void* res, void* y, uint8_t* mask, 
 // dz and its [2][gy][C] partials sum(dz), sum(dz * x) come from a grad-input
 // GEMM's BatchNorm-backward epilogue (BnBwdArgs below); finalize (centring
 // with the mean) + apply only.  bf16 (elem_bytes 2) or fp32 (4).
+// Lazy BN backward (no apply pass): dx = k1 * ((dz - k2) - (x - mu) * k4) is
+// computed by the consumer GEMMs (gemm.hip LazyA / LazyG) from dz, x and
+// coef[C] = {k1, k2, mu, k4}; padz / padx ([C], activation dtype) are the
+// padding rows that make a padded tap contribute exactly 0.
+//   bn_bwd_finalize_lazy: from [2][gy][C] partials (center: sum(dz*x) form)
+//   bn_act_backward_lazy: full path, the reduce pass writes dz
+//   bn_lazy_apply       : materialise dx (for a consumer without the lazy path)
+void bn_bwd_finalize_lazy(const float* pdb, const float* pdg, int gy, int64_t M, int C, int elem_bytes, int center,
+                          const float* w, const float* mean, const float* invstd, float* dgamma, float* dbeta,
+                          float* gw_acc, float* gb_acc, float* coef, void* padz, void* padx, hipStream_t stream);
+void bn_act_backward_lazy(const void* dy, const void* dy2, const uint8_t* mask, const void* x, void* dz, int64_t M,
+                          int C, int elem_bytes, const float* w, const float* mean, const float* invstd,
+                          float* dgamma, float* dbeta, float* ws, int relu, float* gw_acc, float* gb_acc, float* coef,
+                          void* padz, void* padx, hipStream_t stream);
+void bn_lazy_apply(const void* dz, const void* x, void* dx, int64_t M, int C, int elem_bytes, const float* coef,
+                   hipStream_t stream);
 void bn_act_backward_pre(const void* dz, const void* x, void* dx, int64_t M, int C, int elem_bytes, const float* w,
                          const float* mean, const float* invstd, float* dgamma, float* dbeta, const float* pdb,
                          const float* pdg, int gy, float* gw_acc, float* gb_acc, hipStream_t stream);
@@ -292,15 +308,27 @@ struct BnBwdArgs {
   const void* dy2;
   const uint8_t* mask;
 };
+// Lazy BN-backward operand (fp32; bn_bwd_finalize_lazy): the A operand of
+// gemm_nt / conv_nt / conv_nt_remap (or G of the grad-weight) is
+// dx = k1 ((dz - k2) - (x - mu) k4) computed in-kernel from dz (the operand
+// pointer) and x (same layout); returns -1 when the coefficient table does not
+// fit next to the tiles in LDS.
+struct LazyArgs {
+  const void* x;
+  const float* coef;   // [C][4]
+  const void* padz;    // [C]
+  const void* padx;    // [C]
+  int C;
+};
 // stats (optional): [2][stats_rows][N] fp32 BatchNorm partials (sum, sum of
 // squares of the stored output) per workgroup row; returns the grid's row count
 // (the partial rows written, <= stats_rows) -- feed it to bn_act_forward_pre.
 // bias (optional): fp32 [N] added in the epilogue (before rounding and statistics)
 int gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N, int K,
             bool f32, int cfg, int max_blocks, float* stats, int stats_rows, const float* bias, const BnBwdArgs* bn,
-            hipStream_t stream);
+            const LazyArgs* lazy, hipStream_t stream);
 void gemm_tn_acc(const void* G, int64_t ldg, const void* X, int64_t ldx, float* W, int64_t ldw, int64_t M, int N,
-                 int K, bool f32, int cfg, int splits, hipStream_t stream);
+                 int K, bool f32, int cfg, int splits, const LazyArgs* lazy, hipStream_t stream);
 // Implicit-GEMM KHxKW convolution (stride S, zero padding P) over NHWC:
 //   conv_nt    : Y[M = N*OH*OW, Cout] = im2col(X) . Wt[Cout, KH*KW*C]^T
 //   conv_tn_acc: Wout[Cout, KH*KW*C] += G[M, Cout]^T . im2col(X)
@@ -308,7 +336,7 @@ void gemm_tn_acc(const void* G, int64_t ldg, const void* X, int64_t ldx, float* 
 // >= 128 zero bytes (the padding row).
 int conv_nt(const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P, int KH, int KW,
             const void* B, void* Y, int64_t M, int N, bool f32, int cfg, int max_blocks, float* stats, int stats_rows,
-            const float* bias, const BnBwdArgs* bn, hipStream_t stream);
+            const float* bias, const BnBwdArgs* bn, const LazyArgs* lazy, hipStream_t stream);
 // One parity class (RA, RB) of a stride-2 convolution's grad-input as a stride-1,
 // padding-0 KHxKW implicit GEMM over dY (H x W x C, the forward output) whose
 // OH x OW output grid is stored at rows (n*RH + 2 oh + RA) * RW + 2 ow + RB of
@@ -316,9 +344,10 @@ int conv_nt(const void* X, const void* zero, int H, int W, int C, int OH, int OW
 // runs the plain row GEMM over X = dY rows (row stride ldx).
 int conv_nt_remap(const void* X, int64_t ldx, const void* zero, int H, int W, int C, int OH, int OW, int KH, int KW,
                   const void* B, void* Y, int64_t M, int N, int RH, int RW, int RA, int RB, int RZ, bool f32, int cfg,
-                  int max_blocks, hipStream_t stream);
+                  int max_blocks, const LazyArgs* lazy, hipStream_t stream);
 void conv_tn_acc(const void* G, const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P,
-                 int KH, int KW, float* Wout, int64_t M, int N, bool f32, int cfg, int splits, hipStream_t stream);
+                 int KH, int KW, float* Wout, int64_t M, int N, bool f32, int cfg, int splits, const LazyArgs* lazy,
+                 hipStream_t stream);
 
 // ---------------------------------------------------------------------------
 // ImageNet-ResNet stem: 7x7 / stride 2 / pad 3 convolution, 3 -> 64 channels

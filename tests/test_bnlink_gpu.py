@@ -113,6 +113,9 @@ def test_resnet50_bn_link_matches_unfused(monkeypatch):
     m = resnet50(num_classes=16).cuda().to(memory_format=CL)
     x = torch.randn(4, 3, 64, 64, device="cuda").contiguous(memory_format=CL)
     ref = _step(m, x, amp=False)
+    # the fp32 reference step runs the fp32 MFMA kernels, BN-backward fusion included
+    assert len(calls) == 13 + 16 + 12, len(calls)
+    calls.clear()
     monkeypatch.setenv("GKSGD_BN_LINK", "0")
     g0 = _step(m, x)
     assert not calls
