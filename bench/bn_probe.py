@@ -3,11 +3,12 @@ bs512 activation shapes: microseconds and achieved HBM bandwidth of
 
   fwd      stats + finalize + apply(+residual)(+ReLU mask)   (bn_act_forward)
   fwd_pre  finalize + apply from producer partials            (epilogue statistics)
+  fwd_res_pre  the same + residual add (block output BN)
   bwd_pre  finalize + apply from the grad-input epilogue's partials
   bwd      reduce + finalize + apply (twin + residual: block output)
 
 for each workgroup count in --blocks (bn_set_blocks), so the streaming grid can
-be picked from measurements.  Bytes: the tensors each pass must move (bf16),
+be picked from measurements.  Bytes: the tensors each pass must move (--dtype bf16 | f32),
 the mask / partials ignored.
 
     python bench/bn_probe.py [--batch 512] [--blocks 1024,2048,4096]
@@ -44,27 +45,30 @@ def main():
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--blocks", default="1024,2048,4096")
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     a = ap.parse_args()
+    dt = torch.float32 if a.dtype == "f32" else torch.bfloat16
+    eb = 4 if a.dtype == "f32" else 2
     assert ops.load(), ops._load_error
     g = torch.ops.gksgd
     dev = torch.device("cuda", 0)
-    out = {"batch": a.batch, "rows": []}
+    out = {"batch": a.batch, "dtype": a.dtype, "rows": []}
     for H, C in SHAPES:
         M = a.batch * H * H
-        x = torch.randn(M, C, device=dev).to(torch.bfloat16)
-        res = torch.randn(M, C, device=dev).to(torch.bfloat16)
+        x = torch.randn(M, C, device=dev).to(dt)
+        res = torch.randn(M, C, device=dev).to(dt)
         y = torch.empty_like(x)
-        dz = torch.randn(M, C, device=dev).to(torch.bfloat16)
+        dz = torch.randn(M, C, device=dev).to(dt)
         dx = torch.empty_like(x)
         dres = torch.empty_like(x)
-        mask = torch.empty(g.bn_mask_bytes(M, C, 2), dtype=torch.uint8, device=dev)
-        ws = torch.empty(g.bn_workspace_floats(M, C, 2), dtype=torch.float32, device=dev)
+        mask = torch.empty(g.bn_mask_bytes(M, C, eb), dtype=torch.uint8, device=dev)
+        ws = torch.empty(g.bn_workspace_floats(M, C, eb), dtype=torch.float32, device=dev)
         w = torch.ones(C, device=dev)
         b = torch.zeros(C, device=dev)
         st = [torch.zeros(C, device=dev) for _ in range(4)]
         gg = [torch.zeros(C, device=dev) for _ in range(2)]
         part = torch.randn(2, 256, C, device=dev)
-        mb = M * C * 2 / 1e6
+        mb = M * C * eb / 1e6
         for nb in [int(v) for v in a.blocks.split(",")]:
             g.bn_set_blocks(nb)
 
@@ -73,6 +77,10 @@ def main():
 
             def fwd_pre():
                 g.bn_act_forward(x, None, y, mask, w, b, None, None, st[0], st[1], st[2], st[3], ws, 1e-5, 0.1, True,
+                                 None, part, 256)
+
+            def fwd_res_pre():
+                g.bn_act_forward(x, res, y, mask, w, b, None, None, st[0], st[1], st[2], st[3], ws, 1e-5, 0.1, True,
                                  None, part, 256)
 
             def bwd_pre():
@@ -86,7 +94,7 @@ def main():
             # tensor passes: fwd reads x twice (stats, apply) + res, writes y: 4;
             # fwd_pre 2; bwd_pre reads dz, x, writes dx: 3; bwd reduce reads dy, dy2, x,
             # writes dz; apply reads dz, x, writes dx: 7
-            for name, fn, passes in (("fwd", fwd, 4), ("fwd_pre", fwd_pre, 2), ("bwd_pre", bwd_pre, 3), ("bwd", bwd, 7)):
+            for name, fn, passes in (("fwd", fwd, 4), ("fwd_pre", fwd_pre, 2), ("fwd_res_pre", fwd_res_pre, 3), ("bwd_pre", bwd_pre, 3), ("bwd", bwd, 7)):
                 us = timeit(fn)
                 row[name + "_us"] = round(us, 1)
                 row[name + "_TBs"] = round(passes * mb / us, 3)

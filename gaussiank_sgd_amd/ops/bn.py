@@ -78,6 +78,16 @@ class ProducerLink:
     (same storage) and compute dx = k1 ((dz - k2) - (x - mu) k4) on the fly
     (gemm.hip LazyA).  ``materialize()`` runs the apply kernel for a consumer
     without the lazy path (MIOpen choice, bf16).
+
+    Opt-in (``GKSGD_BN_LAZY=1``).  Measured on MI355X at ResNet-50 bs512 fp32
+    (gpurun_out tune dump summarised in profiles/r03_bn_lazy_tuning.txt): the
+    lazy NT / TN GEMMs run 1.3-2.4x the time of the plain GEMM on every shape
+    -- the dz and x tiles double the A-side LDS-DMA stages and the coefficient
+    reads double the fragment reads, which costs the deep stage pipeline the
+    fp32 kernels rely on at one wave per SIMD -- so the autotuner picks
+    "materialise + plain GEMM" everywhere and the step is 1 ms slower (148.4
+    vs 147.4 ms).  The kernels stay tested (tests/test_bn_lazy_gpu.py) for
+    the cases where the GEMM is not the bound.
     """
 
     __slots__ = ("lazy", "dx")
@@ -111,7 +121,7 @@ def _lazy_buffers(x: torch.Tensor):
 def _lazy_ok(x: torch.Tensor, plink) -> bool:
     import os
     return (plink is not None and x.dtype == torch.float32 and x.shape[1] % 64 == 0 and
-            os.environ.get("GKSGD_BN_LAZY", "1") != "0")
+            os.environ.get("GKSGD_BN_LAZY", "0") != "0")
 
 
 class _BNActFn(torch.autograd.Function):

@@ -36,6 +36,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import load
+from . import streams
 
 _CL = torch.channels_last
 _TUNE = os.environ.get("GKSGD_GEMM_TUNE", "1") != "0"
@@ -94,9 +95,19 @@ def _pick(key: tuple, cands: List[Tuple[tuple, Callable[[], None]]]) -> tuple:
     got = _choices.get(key)
     if got is not None:
         return got
-    if not _TUNE or len(cands) == 1:
+    if len(cands) == 1:
         _choices[key] = cands[0][0]
         return cands[0][0]
+    if not _TUNE:
+        # untuned: the first candidate that runs (a lazy-operand tile may refuse its LDS budget)
+        for tag, fn in cands:
+            try:
+                fn()
+            except RuntimeError:
+                continue
+            _choices[key] = tag
+            return tag
+        raise RuntimeError("no candidate ran for %s" % (key,))
     log = _timings.setdefault(key, [])
     screened = []
     for tag, fn in cands:
@@ -320,6 +331,11 @@ def dgrad_key_dtype(key: tuple) -> torch.dtype:
     return torch.float32 if key[-1] == "f32" else torch.bfloat16
 
 
+def _wgrad_key(x: torch.Tensor, w: torch.Tensor, s: int, lz=None) -> tuple:
+    N, C, H, W, K, k, p, OH, OW = _geom(x.shape, w, s)
+    return ("wgrad", N, C, H, W, K, k, s) + _dkey(x.dtype) + (("lz",) if lz is not None else ())
+
+
 def _wgrad_into(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, s: int, out_f32: torch.Tensor, lz=None,
                 plink=None) -> None:
     """out_f32 ([K, C, k, k] channels-last fp32) += dW.  ``lz``: dy is a lazy
@@ -327,7 +343,7 @@ def _wgrad_into(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, s: int, out_
     N, C, H, W, K, k, p, OH, OW = _geom(x.shape, w, s)
     g = _g()
     dt = x.dtype
-    key = ("wgrad", N, C, H, W, K, k, s) + _dkey(dt) + (("lz",) if lz is not None else ())
+    key = _wgrad_key(x, w, s, lz)
     scratch = torch.zeros_like(out_f32) if key not in _choices else None
     kw = _lz_kw(lz, rows=(k == 1 and s == 1)) if lz is not None else {}
 
@@ -413,6 +429,24 @@ class _FastConvFn(torch.autograd.Function):
             # autograd summed the BN's dz with another consumer's gradient: the sum is not dx
             raise RuntimeError("FastConv2d: lazy BN gradient mixed with another consumer of the conv output; "
                                "set GKSGD_BN_LAZY=0 for this model")
+        # grad-weight into the optimizer's arena: off the critical path on the side
+        # stream (ops/streams.py), issued first so it overlaps the grad-input GEMM and
+        # the BatchNorm passes that follow it; tuned shapes whose choice is a HIP kernel
+        # only (the search times candidates on the current stream; MIOpen calls stay
+        # on the stream its handle and workspace were set up for)
+        sink = ctx.sink if ctx.needs_input_grad[1] else None
+        direct = sink is not None and getattr(sink, "grad_view", None) is not None and \
+            sink.grad_view.is_contiguous(memory_format=_CL)
+        wgrad_done = False
+        if direct and lz is None and streams.enabled(x.device) and \
+                _choices.get(_wgrad_key(x, w, s), ("",))[0] in ("hip", "w3"):
+            sink.check()
+            side = streams.fork(x.device)
+            with torch.cuda.stream(side):
+                _wgrad_into(dy, x, w, s, sink.grad_view)
+            for t in (dy, x, w):
+                t.record_stream(side)
+            wgrad_done = True
         dx = None
         if ctx.needs_input_grad[0]:
             N, C, H, W = x.shape
@@ -422,10 +456,8 @@ class _FastConvFn(torch.autograd.Function):
             else:
                 dx = _dgrad(dy, w, x.shape, s, lz, plink)
         gparam = None
-        if ctx.needs_input_grad[1]:
-            sink = ctx.sink
-            if sink is not None and getattr(sink, "grad_view", None) is not None and \
-                    sink.grad_view.is_contiguous(memory_format=_CL):
+        if ctx.needs_input_grad[1] and not wgrad_done:
+            if direct:
                 sink.check()
                 _wgrad_into(dy, x, w, s, sink.grad_view, lz, plink)
             else:

@@ -1091,9 +1091,10 @@ void conv_dgrad_s2(at::Tensor dy, at::Tensor w, at::Tensor dx, at::Tensor zero, 
   const hipStream_t st = cur_stream(dy);
   if (k == 1) {   // one class (even, even), zeros elsewhere; B = W^T [C][K]
     const at::Tensor wt = w.reshape({K, C}).t().contiguous();
-    gk::conv_nt_remap(dy.data_ptr(), K, zero.data_ptr(), (int)OHd, (int)OWd, (int)K, (int)OHd, (int)OWd, 1, 1,
-                      wt.data_ptr(), dx.data_ptr(), N * OHd * OWd, (int)C, (int)H, (int)W, 0, 0, 1, f32, (int)cfg,
-                      (int)max_blocks, lz, st);
+    const int r = gk::conv_nt_remap(dy.data_ptr(), K, zero.data_ptr(), (int)OHd, (int)OWd, (int)K, (int)OHd,
+                                    (int)OWd, 1, 1, wt.data_ptr(), dx.data_ptr(), N * OHd * OWd, (int)C, (int)H, (int)W,
+                                    0, 0, 1, f32, (int)cfg, (int)max_blocks, lz, st);
+    TORCH_CHECK(r >= 0, "conv_dgrad_s2: the lazy operand's coefficient table does not fit this tile configuration");
     return;
   }
   // [C][kh][kw][K] = W[K][C][kh][kw]
@@ -1107,9 +1108,12 @@ void conv_dgrad_s2(at::Tensor dy, at::Tensor w, at::Tensor dx, at::Tensor zero, 
       at::Tensor wc = a == 0 ? wt.slice(1, 1, 2) : wt.slice(1, 0, 3, 2).flip({1});
       wc = b == 0 ? wc.slice(2, 1, 2) : wc.slice(2, 0, 3, 2).flip({2});
       wc = wc.contiguous();
-      gk::conv_nt_remap(dy.data_ptr(), K, zero.data_ptr(), (int)OHd, (int)OWd, (int)K, (int)OHc, (int)OWc,
-                        a == 0 ? 1 : 2, b == 0 ? 1 : 2, wc.data_ptr(), dx.data_ptr(), N * OHc * OWc, (int)C, (int)H,
-                        (int)W, a, b, 0, f32, (int)cfg, (int)max_blocks, lz, st);
+      // a refused tile (lazy operand too large) must fail loudly: its class's pixels would stay unwritten
+      const int r = gk::conv_nt_remap(dy.data_ptr(), K, zero.data_ptr(), (int)OHd, (int)OWd, (int)K, (int)OHc,
+                                      (int)OWc, a == 0 ? 1 : 2, b == 0 ? 1 : 2, wc.data_ptr(), dx.data_ptr(),
+                                      N * OHc * OWc, (int)C, (int)H, (int)W, a, b, 0, f32, (int)cfg, (int)max_blocks,
+                                      lz, st);
+      TORCH_CHECK(r >= 0, "conv_dgrad_s2: the lazy operand's coefficient table does not fit this tile configuration");
     }
   }
 }

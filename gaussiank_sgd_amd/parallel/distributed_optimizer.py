@@ -41,6 +41,7 @@ import numpy as np
 import torch
 
 from .. import ops, settings
+from ..ops import streams
 from ..settings import logger
 from ..utils import stats as perf
 from ..utils import trace
@@ -447,10 +448,13 @@ class _DistributedOptimizer(torch.optim.Optimizer):
                 ev = b.extra["ready_event"]
                 ev.record(cur)
                 self._comm_stream.wait_event(ev)
+                # grad-weight GEMMs still running on the side stream (ops/streams.py)
+                streams.join(self._device, self._comm_stream)
                 with torch.cuda.stream(self._comm_stream):
                     self._process_bucket(b)
                     b.done_event.record(self._comm_stream)
             else:
+                streams.join(self._device)
                 self._process_bucket(b)
 
     def _timer(self):
@@ -562,6 +566,9 @@ class _DistributedOptimizer(torch.optim.Optimizer):
             ev = bs[0].extra["ready_event"]
             ev.record(cur)
             self._comm_stream.wait_event(ev)
+            streams.join(self._device, self._comm_stream)
+        else:
+            streams.join(self._device)
         with ctx, trace.range("gk/group/%d" % len(bs)):
             parts = []
             for b in bs:
@@ -689,6 +696,8 @@ class _DistributedOptimizer(torch.optim.Optimizer):
             self._synchronize()
 
     def _synchronize(self):
+        if self._is_cuda:
+            streams.join(self._device)   # normally done by the end-of-backward callback already
         if self._hooks_on:
             any_ready = False
             due = [b for b in self._arena.buckets if not b.launched and b.ready > 0]

@@ -1,7 +1,7 @@
 #!/bin/bash
 set -u
 mkdir -p gpurun_out/r3d
-timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_bn_lazy_gpu.py -k "resnet50 or bnact" \
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_bn_lazy_gpu.py \
   > gpurun_out/r3d/lazy.log 2>&1
 rc=$?; echo lazy_rc=$rc; tail -30 gpurun_out/r3d/lazy.log
 [ $rc -ne 0 ] && exit $rc

@@ -94,3 +94,42 @@ def test_overlap_on_off_bitwise_deterministic(cuda, comp):
         torch.cuda.synchronize()
         results.append(opt.arena.weights.clone())
     assert torch.equal(results[0], results[1])
+
+
+@pytest.mark.parametrize("amp", ["none", "bf16"])
+def test_wgrad_side_stream_matches_inline(cuda, monkeypatch, amp):
+    """Grad-weight GEMMs on the side HIP stream (ops/streams.py), joined by the
+    bucket launches on the comm stream and the end-of-backward callback, give
+    the same weights as the inline single-stream backward (up to the fp32
+    atomic-accumulation order of the grad-weight kernels)."""
+    from gaussiank_sgd_amd.ops import streams
+    results = []
+    for side in ("1", "0"):   # opt-in (ops/streams.py: no measured gain at bs512)
+        monkeypatch.setenv("GKSGD_WGRAD_STREAM", side)
+        torch.manual_seed(0)
+        comm.init()
+        t = DLTrainer(0, 1, dnn="resnet50", dataset="imagenet", batch_size=8, lr=0.05, device="cuda",
+                      amp=amp, channels_last=True, data_pool=1)
+        opt = DistributedOptimizer(t.optimizer, named_parameters=t.net.named_parameters(),
+                                   compression=compressors["gaussian"], is_sparse=True, density=0.01,
+                                   compress_single_rank=True, density_warmup=False, threshold=2_000_000)
+        from gaussiank_sgd_amd.parallel import install_bf16_shadow, install_direct_grads
+        (install_bf16_shadow if amp == "bf16" else install_direct_grads)(t.net, opt)   # grad-weight sinks
+        t.update_optimizer(opt)
+        assert len(opt.arena.buckets) > 1
+        g = torch.Generator(device="cuda").manual_seed(5)
+        forked = False
+        for _ in range(3):
+            x = torch.randn(8, 3, 224, 224, device="cuda", generator=g).contiguous(memory_format=torch.channels_last)
+            y = torch.randint(0, 1000, (8,), device="cuda", generator=g)
+            opt.zero_grad()
+            t.train(1, data=(x, y))
+            forked = forked or bool(streams._side)
+            assert not streams.pending("cuda")       # joined at the end of backward
+            t.update_model()
+        torch.cuda.synchronize()
+        if side == "1":
+            assert forked, "side stream never used"
+        results.append(opt.arena.weights.clone())
+    err = (results[0] - results[1]).abs().max().item()
+    assert err <= 1e-3 * results[1].abs().max().item(), err
