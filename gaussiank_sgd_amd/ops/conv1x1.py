@@ -208,7 +208,18 @@ def _fwd(x: torch.Tensor, w: torch.Tensor, s: int, stats_box=None, bias=None) ->
         run = lambda c, mb: g.conv_nt(x, w, y, z, s, p, c, mb, st, bias)  # noqa: E731
     b16 = bias.to(dt) if bias is not None else None
     cands = [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in _nt_cfgs(dt) for mb in _NT_GRIDS]
-    cands.append((("miopen", 0, 0), lambda: F.conv2d(x, w, b16, stride=s, padding=p)))
+
+    def miopen():
+        out = F.conv2d(x, w, b16, stride=s, padding=p)
+        if st is not None and ws is not None:
+            # a MIOpen output leaves the consuming BN its statistics pass: time it too
+            g.bn_stats_partials(out.contiguous(memory_format=_CL), ws)
+        return out
+    ws = None
+    if st is not None and (("fwd", N, C, H, W, K, k, s, True) + _dkey(dt)) not in _choices and \
+            g.bn_supported(K, x.element_size()):
+        ws = torch.empty(int(g.bn_workspace_floats(M, K, x.element_size())), dtype=torch.float32, device=x.device)
+    cands.append((("miopen", 0, 0), miopen))
     ch = _pick(("fwd", N, C, H, W, K, k, s, st is not None) + _dkey(dt), cands)
     if ch[0] == "miopen":
         return F.conv2d(x, w, b16, stride=s, padding=p).contiguous(memory_format=_CL)

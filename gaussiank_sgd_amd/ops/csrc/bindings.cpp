@@ -548,6 +548,18 @@ void bn_act_backward_lazy(at::Tensor dy, c10::optional<at::Tensor> dy2, c10::opt
                            cur_stream(x));
 }
 
+void bn_stats_partials(at::Tensor x, at::Tensor ws) {
+  check_cl(x, "x");
+  const int64_t C = channels_of(x);
+  const int64_t M = x.numel() / C;
+  const int eb = (int)x.element_size();
+  TORCH_CHECK(gk::bn_supported((int)C, eb), "channel count not supported by the fused kernel");
+  TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == at::kFloat && ws.numel() >= (int64_t)gk::bn_workspace_floats(M, (int)C, eb),
+              "workspace too small");
+  c10::DeviceGuard guard(x.device());
+  gk::bn_stats_partials(x.data_ptr(), M, (int)C, eb, ws.data_ptr<float>(), cur_stream(x));
+}
+
 void bn_lazy_apply(at::Tensor dz, at::Tensor x, at::Tensor dx, at::Tensor coef) {
   check_cl(dz, "dz");
   check_cl(x, "x");
@@ -1588,6 +1600,7 @@ TORCH_LIBRARY(gksgd, m) {
         "Tensor mean, Tensor invstd, Tensor(b!) dgamma, Tensor(c!) dbeta, Tensor(d!) ws, bool relu, "
         "Tensor(e!) coef, Tensor(f!) padz, Tensor(g!) padx, Tensor(h!)? gw_acc=None, Tensor(i!)? gb_acc=None) -> ()");
   m.def("bn_lazy_apply(Tensor dz, Tensor x, Tensor(a!) dx, Tensor coef) -> ()");
+  m.def("bn_stats_partials(Tensor x, Tensor(a!) ws) -> ()");
   m.def("bn_act_backward_pre(Tensor dz, Tensor x, Tensor(a!) dx, Tensor? w, Tensor mean, Tensor invstd, "
         "Tensor(b!) dgamma, Tensor(c!) dbeta, Tensor part, int rows, Tensor(d!)? gw_acc=None, "
         "Tensor(e!)? gb_acc=None) -> ()");
@@ -1667,6 +1680,7 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("bn_bwd_lazy_pre", &bn_bwd_lazy_pre);
   m.impl("bn_act_backward_lazy", &bn_act_backward_lazy);
   m.impl("bn_lazy_apply", &bn_lazy_apply);
+  m.impl("bn_stats_partials", &bn_stats_partials);
   m.impl("stem_pack", &stem_pack);
   m.impl("conv_dgrad_s2", &conv_dgrad_s2);
   m.impl("conv3_wgrad", &conv3_wgrad);

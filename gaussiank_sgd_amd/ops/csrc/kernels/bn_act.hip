@@ -39,6 +39,29 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
   return (uint16_t)(u >> 16);
 }
 
+// Streaming 16-byte accesses of the BN passes.  The activations (up to 1.6 GB
+// per tensor at ResNet-50 bs512 fp32) are touched once per pass and never fit
+// the 4 MB L2 / 256 MB MALL, so GK_BN_NT_LD / GK_BN_NT_ST (A/B variants, see
+// ops/build.py GKSGD_VARIANT) mark them non-temporal.
+#ifndef GK_BN_NT_LD
+#define GK_BN_NT_LD 0
+#endif
+#ifndef GK_BN_NT_ST
+#define GK_BN_NT_ST 0
+#endif
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld16(const uint4* p) {
+  if (GK_BN_NT_LD) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v[0], v[1], v[2], v[3]);
+  }
+  return *p;
+}
+__device__ __forceinline__ void st16(uint4* p, uint4 v) {
+  if (GK_BN_NT_ST) __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4*>(p));
+  else *p = v;
+}
+
 // 16-byte vector of VEC elements of T, converted to/from fp32.
 template <typename T>
 struct Vec;
@@ -47,7 +70,7 @@ template <>
 struct Vec<uint16_t> {  // bf16
   static constexpr int N = 8;
   __device__ static void load(const uint16_t* p, float* v) {
-    const uint4 u = *reinterpret_cast<const uint4*>(p);
+    const uint4 u = ld16(reinterpret_cast<const uint4*>(p));
     const uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -62,7 +85,7 @@ struct Vec<uint16_t> {  // bf16
     for (int i = 0; i < 4; ++i)
       w[i] = __builtin_bit_cast(uint32_t, __builtin_convertvector(
                  (float __attribute__((ext_vector_type(2)))){v[2 * i], v[2 * i + 1]}, __bf16 __attribute__((ext_vector_type(2)))));
-    *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+    st16(reinterpret_cast<uint4*>(p), make_uint4(w[0], w[1], w[2], w[3]));
   }
 };
 
@@ -70,11 +93,12 @@ template <>
 struct Vec<float> {
   static constexpr int N = 4;
   __device__ static void load(const float* p, float* v) {
-    const float4 f = *reinterpret_cast<const float4*>(p);
-    v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+    const uint4 u = ld16(reinterpret_cast<const uint4*>(p));
+    v[0] = __uint_as_float(u.x); v[1] = __uint_as_float(u.y); v[2] = __uint_as_float(u.z); v[3] = __uint_as_float(u.w);
   }
   __device__ static void store(float* p, const float* v) {
-    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    st16(reinterpret_cast<uint4*>(p), make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                                                 __float_as_uint(v[3])));
   }
 };
 
@@ -937,6 +961,18 @@ void bn_backward_t(const T* dy, const T* dy2, const uint8_t* mask, const T* x, T
 }
 
 size_t bn_mask_bytes(int64_t M, int C, int elem_bytes) { return (size_t)M * (size_t)(C / (elem_bytes == 2 ? 8 : 4)); }
+
+void bn_stats_partials(const void* x, int64_t M, int C, int elem_bytes, float* ws, hipStream_t s) {
+  if (elem_bytes == 2) {
+    const Geo g = make_geo<uint16_t>(M, C, kTargetBlocks);
+    hipLaunchKernelGGL(bn_stats_kernel<uint16_t>, dim3(g.gx, g.gy), dim3(kBlock), 0, s, static_cast<const uint16_t*>(x), M,
+                       C, g, ws, ws + (int64_t)g.gy * C);
+  } else {
+    const Geo g = make_geo<float>(M, C, kTargetBlocks);
+    hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(g.gx, g.gy), dim3(kBlock), 0, s, static_cast<const float*>(x), M, C,
+                       g, ws, ws + (int64_t)g.gy * C);
+  }
+}
 
 void bn_act_forward(const void* x, const void* res, void* y, uint8_t* mask, int64_t M, int C, int elem_bytes,
                     const float* w, const float* b, float eps, float momentum, float* run_mean, float* run_var,

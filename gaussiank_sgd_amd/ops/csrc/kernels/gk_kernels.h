@@ -228,6 +228,10 @@ bool bn_supported(int C, int elem_bytes);
 // workgroups per streaming BN pass (default 1024, clamped to [64, 4096]; bench/bn_probe.py)
 void bn_set_blocks(int blocks);
 size_t bn_mask_bytes(int64_t M, int C, int elem_bytes);
+// the statistics pass of bn_act_forward alone (per-block sum / sum-of-squares
+// partials into ws): what a convolution without the statistics epilogue costs
+// the BN that consumes it (the autotuner times MIOpen candidates with it)
+void bn_stats_partials(const void* x, int64_t M, int C, int elem_bytes, float* ws, hipStream_t s);
 void bn_act_forward(const void* x, const void* res, void* y, uint8_t* mask, int64_t M, int C, int elem_bytes,
                     const float* w, const float* b, float eps, float momentum, float* run_mean, float* run_var,
                     float* save_mean, float* save_invstd, float* scale, float* shift, float* ws, int relu,
