@@ -40,14 +40,17 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
 }
 
 // Streaming 16-byte accesses of the BN passes.  The activations (up to 1.6 GB
-// per tensor at ResNet-50 bs512 fp32) are touched once per pass and never fit
-// the 4 MB L2 / 256 MB MALL, so GK_BN_NT_LD / GK_BN_NT_ST (A/B variants, see
-// ops/build.py GKSGD_VARIANT) mark them non-temporal.
+// per tensor at ResNet-50 bs512 fp32) are touched once per pass and do not fit
+// the 4 MB L2 / 256 MB MALL, so loads and stores are non-temporal.  Measured
+// (bench/bn_probe.py, every ResNet-50 bs512 BN shape and pass summed,
+// profiles/r03_bn_nontemporal.txt): fp32 14.24 -> 13.63 ms, bf16 7.67 -> 7.32
+// ms (stores only: 13.93 / 7.30).  -DGK_BN_NT_LD=0 / -DGK_BN_NT_ST=0 restore
+// plain accesses (ops/build.py GKSGD_VARIANT A/B builds).
 #ifndef GK_BN_NT_LD
-#define GK_BN_NT_LD 0
+#define GK_BN_NT_LD 1
 #endif
 #ifndef GK_BN_NT_ST
-#define GK_BN_NT_ST 0
+#define GK_BN_NT_ST 1
 #endif
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint4 ld16(const uint4* p) {
