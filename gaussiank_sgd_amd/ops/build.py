@@ -59,6 +59,7 @@ HIP_SOURCES = [
     "kernels/attn.hip",
     "kernels/embed.hip",
     "kernels/xent.hip",
+    "kernels/winograd.hip",
 ]
 CXX_SOURCES = [
     "comm/rccl_engine.cpp",

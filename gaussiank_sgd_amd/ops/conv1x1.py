@@ -47,9 +47,16 @@ _choices: Dict[tuple, tuple] = {}
 # of its time (GKSGD_GK_MARGIN, default 5%: the fp32 implicit-GEMM kernels
 # trail MIOpen's by 1-5% on some 3x3 shapes -- kept, so the fp32 step runs on
 # code this package owns; 0 = fastest wins)
-_OWN = ("hip", "w3", "mat")
+_OWN = ("hip", "w3", "mat", "wino")
 _GK_MARGIN = float(os.environ.get("GKSGD_GK_MARGIN", "0.05"))
 _timings: Dict[tuple, list] = {}      # key -> [(tag, ms or error)] of the search
+# fp32 3x3 stride-1 forward / grad-input: Winograd F(2x2, 3x3) candidates
+# (winograd.hip, 2.25x fewer MFMA FLOPs); GKSGD_WINO=0 leaves them out.  Their
+# autotune keys carry a "wino" tag so choices cached before they existed are
+# searched again.  _FORCE (GKSGD_CONV_FORCE=wino, tests) keeps only them.
+_WINO = os.environ.get("GKSGD_WINO", "1") != "0"
+_FORCE = os.environ.get("GKSGD_CONV_FORCE", "")
+_WINO_GRIDS = (0, 1 << 20)
 # candidate kernel configurations (gemm.hip: cfg digits = tile + 10*panel + 100*stages)
 _NT_CFGS = [1, 2, 3, 4, 11, 13, 21, 22, 23, 24, 111, 113, 121, 122, 123, 124, 25, 26, 27, 125, 126, 127,
             211, 212, 213, 214, 221, 222, 223, 224]   # 2xx: four LDS stages (more bytes in flight)
@@ -202,6 +209,35 @@ def _geom(x_shape, w: torch.Tensor, s: int):
     return N, C, H, W, K, k, p, OH, OW
 
 
+def _wino_ok(dt: torch.dtype, k: int, s: int, C: int, K: int) -> bool:
+    return _WINO and dt == torch.float32 and k == 3 and s == 1 and C % 8 == 0 and K % 64 == 0
+
+
+def _wino_fits(*ts: torch.Tensor) -> bool:
+    # the kernels address their inputs through 32-bit buffer descriptors
+    return all(t.numel() * 4 < (1 << 31) for t in ts)
+
+
+def _wino_cands(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, flip: bool, st=None, bn=()) -> list:
+    """Winograd candidates: filter transform (per call: the weights change
+    every step) + wino_conv; ``bn`` = (h, dy2, mask) of the BN-backward epilogue."""
+    g = _g()
+    u = torch.empty(16 * w.shape[0] * w.shape[1], dtype=torch.float32, device=x.device)
+
+    def run(mb):
+        g.wino_weights(w, u, flip)
+        return g.wino_conv(x, u, out, mb, st, *bn)
+    return [(("wino", 0, mb), (lambda mb=mb: run(mb))) for mb in _WINO_GRIDS]
+
+
+def _forced(cands: list) -> list:
+    if _FORCE:
+        sel = [c for c in cands if c[0][0] == _FORCE]
+        if sel:
+            return sel
+    return cands
+
+
 def _fwd(x: torch.Tensor, w: torch.Tensor, s: int, stats_box=None, bias=None) -> torch.Tensor:
     """y = conv(x, w).  With ``stats_box`` (a list) and the HIP kernel chosen,
     the kernel's epilogue also reduces the BatchNorm batch statistics of y
@@ -223,6 +259,9 @@ def _fwd(x: torch.Tensor, w: torch.Tensor, s: int, stats_box=None, bias=None) ->
         run = lambda c, mb: g.conv_nt(x, w, y, z, s, p, c, mb, st, bias)  # noqa: E731
     b16 = bias.to(dt) if bias is not None else None
     cands = [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in _nt_cfgs(dt) for mb in _NT_GRIDS]
+    wino = bias is None and _wino_ok(dt, k, s, C, K) and _wino_fits(x)
+    if wino:
+        cands += _wino_cands(x, w, y, False, st)
 
     def miopen():
         out = F.conv2d(x, w, b16, stride=s, padding=p)
@@ -235,10 +274,14 @@ def _fwd(x: torch.Tensor, w: torch.Tensor, s: int, stats_box=None, bias=None) ->
             g.bn_supported(K, x.element_size()):
         ws = torch.empty(int(g.bn_workspace_floats(M, K, x.element_size())), dtype=torch.float32, device=x.device)
     cands.append((("miopen", 0, 0), miopen))
-    ch = _pick(("fwd", N, C, H, W, K, k, s, st is not None) + _dkey(dt), cands)
+    ch = _pick(("fwd", N, C, H, W, K, k, s, st is not None) + _dkey(dt) + (("wino",) if wino else ()),
+               _forced(cands))
     if ch[0] == "miopen":
         return F.conv2d(x, w, b16, stride=s, padding=p).contiguous(memory_format=_CL)
-    rows = run(ch[1], ch[2])
+    if ch[0] == "wino":
+        rows = dict(cands)[ch]()
+    else:
+        rows = run(ch[1], ch[2])
     if st is not None:
         stats_box.append((st, int(rows)))
     return y
@@ -292,12 +335,23 @@ def _dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, lz=None, plink=No
             return _dgrad(plink.materialize(), w, x_shape, s)
         run(ch[1], ch[2])
         return dx
+    wino = _wino_ok(dt, k, s, K, C) and _wino_fits(dy)
+    if wino:
+        cands += _wino_cands(dy, w, dx, True)
     cands.append((("miopen", 0, 0), miopen))
-    ch = _pick(("dgrad", N, C, H, W, K, k, s) + _dkey(dt), cands)
+    ch = _pick(_dgrad_key(N, C, H, W, K, k, s, dt), _forced(cands))
     if ch[0] == "miopen":
         return miopen().contiguous(memory_format=_CL)
+    if ch[0] == "wino":
+        dict(cands)[ch]()
+        return dx
     run(ch[1], ch[2])
     return dx
+
+
+def _dgrad_key(N, C, H, W, K, k, s, dt) -> tuple:
+    wino = _wino_ok(dt, k, s, K, C) and N * H * W * max(C, K) * 4 < (1 << 31)
+    return ("dgrad", N, C, H, W, K, k, s) + _dkey(dt) + (("wino",) if wino else ())
 
 
 def _dgrad_bn(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, link, lz=None, plink=None) -> torch.Tensor:
@@ -334,8 +388,14 @@ def _dgrad_bn(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, link, lz=None,
         if ch[0] == "mat":
             return _dgrad_bn(plink.materialize(), w, x_shape, s, link)
     else:
-        ch = _pick(key, cands)
-    rows = run(ch[1], ch[2])
+        if _wino_ok(dt, k, s, K, C) and _wino_fits(dy):
+            cands += _wino_cands(dy, w, dz, True, st, (h, dy2, mask))
+            key = key + ("wino",)
+        ch = _pick(key, _forced(cands))
+    if ch[0] == "wino":
+        rows = dict(cands)[ch]()
+    else:
+        rows = run(ch[1], ch[2])
     link.part = (st, int(rows))
     link.dz = dz
     return dz
@@ -350,16 +410,18 @@ def _bn_fusable(link, s: int, dgrad_key: tuple) -> bool:
     if link.h.dtype != dgrad_key_dtype(dgrad_key):
         return False
     ch = _choices.get(dgrad_key)
-    return ch is None or ch[0] == "hip"
+    return ch is None or ch[0] in ("hip", "wino")
 
 
 def dgrad_key_dtype(key: tuple) -> torch.dtype:
-    return torch.float32 if key[-1] == "f32" else torch.bfloat16
+    return torch.float32 if "f32" in key[8:] else torch.bfloat16
 
 
 def _wgrad_key(x: torch.Tensor, w: torch.Tensor, s: int, lz=None) -> tuple:
     N, C, H, W, K, k, p, OH, OW = _geom(x.shape, w, s)
-    return ("wgrad", N, C, H, W, K, k, s) + _dkey(x.dtype) + (("lz",) if lz is not None else ())
+    wino = lz is None and _wino_ok(x.dtype, k, s, C, K) and C % 64 == 0 and N * H * W * max(C, K) * 4 < (1 << 31)
+    return ("wgrad", N, C, H, W, K, k, s) + _dkey(x.dtype) + (("lz",) if lz is not None else ()) + \
+        (("wino",) if wino else ())
 
 
 def _wgrad_into(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, s: int, out_f32: torch.Tensor, lz=None,
@@ -392,6 +454,13 @@ def _wgrad_into(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, s: int, out_
         else:
             run(out_f32, ch[1], ch[2])
         return
+    if key[-1] == "wino":
+        # Winograd F(2x2, 3x3) grad-weight (winograd.hip): per-split dU partials + finalize
+        def wino_w(o, sp):
+            part = torch.empty(int(g.wino_wgrad_ws(N, H, W, C, K, sp)), dtype=torch.float32, device=x.device)
+            g.wino_wgrad(x, dy, o, part, sp)
+        for sp in (0, 512):
+            cands.append((("wino", 0, sp), (lambda sp=sp: wino_w(scratch, sp))))
     w3 = None
     if k == 3 and s == 1 and dt == torch.bfloat16 and g.wgrad3_supported(H, W, C, K):
         # tap-parallel kernel (wgrad3.hip): dY and X staged once per band for all 9 taps
@@ -406,9 +475,12 @@ def _wgrad_into(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, s: int, out_
         from . import accum_grad_
         accum_grad_(o, miopen().contiguous(memory_format=_CL))
     cands.append((("miopen", 0, 0), lambda: miopen_acc(scratch)))
-    ch = _pick(key, cands)
+    ch = _pick(key, _forced(cands))
     if ch[0] == "miopen":
         miopen_acc(out_f32)
+        return
+    if ch[0] == "wino":
+        wino_w(out_f32, ch[2])
         return
     if ch[0] == "w3" and w3 is not None:
         w3(out_f32)
@@ -481,7 +553,7 @@ class _FastConvFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             N, C, H, W = x.shape
-            key = ("dgrad", N, C, H, W, w.shape[0], w.shape[2], s) + _dkey(ctx.dt)
+            key = _dgrad_key(N, C, H, W, w.shape[0], w.shape[2], s, ctx.dt)
             if _bn_fusable(link, s, key):
                 dx = _dgrad_bn(dy, w, x.shape, s, link, lz, plink)
             else:

@@ -1071,6 +1071,80 @@ int64_t conv_nt(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor zero, int64
   return r;
 }
 
+// Winograd F(2x2, 3x3) fp32 convolution (winograd.hip).  w: forward weight
+// [K, C, 3, 3] channels-last fp32; flip = false: u = transform of w for the
+// forward (Ci = C, Co = K); flip = true: of the grad-input filter (Ci = K,
+// Co = C).  u: contiguous fp32 with 16 * K * C elements.
+void wino_weights(at::Tensor w, at::Tensor u, bool flip) {
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3 &&
+                  w.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "wino_weights: w must be a channels-last fp32 [K, C, 3, 3] GPU tensor");
+  const int64_t K = w.size(0), C = w.size(1);
+  const int64_t Co = flip ? C : K, Ci = flip ? K : C;
+  TORCH_CHECK(Ci % 8 == 0 && Co % 64 == 0, "wino_weights: input channels % 8 and output channels % 64");
+  TORCH_CHECK(u.is_cuda() && u.scalar_type() == at::kFloat && u.is_contiguous() && u.numel() == 16 * K * C,
+              "wino_weights: u must be a contiguous fp32 tensor of 16 * K * C elements");
+  c10::DeviceGuard guard(w.device());
+  gk::wino_weights(w.data_ptr<float>(), u.data_ptr<float>(), (int)Co, (int)Ci, flip ? 1 : 0, cur_stream(w));
+}
+
+// y = conv3x3(x) (stride 1, padding 1) from the transformed filter u;
+// x: [N, Ci, H, W], y: [N, Co, H, W], both channels-last fp32.  Optional
+// BatchNorm statistics partials / BN-backward epilogue as conv_nt.
+int64_t wino_conv(at::Tensor x, at::Tensor u, at::Tensor y, int64_t max_blocks, c10::optional<at::Tensor> stats,
+                  c10::optional<at::Tensor> bn_h, c10::optional<at::Tensor> bn_dy2, c10::optional<at::Tensor> bn_mask) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.dim() == 4 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "wino_conv: x must be a channels-last fp32 GPU tensor");
+  const int64_t N = x.size(0), Ci = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(y.is_cuda() && y.scalar_type() == at::kFloat && y.dim() == 4 &&
+                  y.is_contiguous(at::MemoryFormat::ChannelsLast) && y.size(0) == N && y.size(2) == H &&
+                  y.size(3) == W,
+              "wino_conv: y must be a channels-last fp32 [N, Co, H, W] GPU tensor");
+  const int64_t Co = y.size(1);
+  TORCH_CHECK(Ci % 8 == 0 && Co % 64 == 0, "wino_conv: Ci % 8 == 0 and Co % 64 == 0");
+  TORCH_CHECK(u.is_cuda() && u.scalar_type() == at::kFloat && u.is_contiguous() && u.numel() == 16 * Ci * Co,
+              "wino_conv: u must hold 16 * Ci * Co fp32 (wino_weights)");
+  TORCH_CHECK(N * ((H + 1) / 2) * ((W + 1) / 2) < (int64_t(1) << 31) && x.numel() > 0 &&
+                  x.numel() * 4 < (int64_t(1) << 31),
+              "wino_conv: size out of range (input bytes < 2^31: buffer-descriptor addressing)");
+  int rows = 0;
+  float* sp = stats_ptr(stats, Co, &rows);
+  gk::BnBwdArgs bn{};
+  const bool has_bn = bn_bwd_args(bn_h, bn_dy2, bn_mask, N * H * W, Co, Co, sp != nullptr, at::kFloat, &bn);
+  c10::DeviceGuard guard(x.device());
+  return gk::wino_conv(x.data_ptr<float>(), u.data_ptr<float>(), y.data_ptr<float>(), (int)N, (int)H, (int)W, (int)Ci,
+                       (int)Co, (int)max_blocks, sp, rows, has_bn ? &bn : nullptr, cur_stream(x));
+}
+
+// out ([K, C, 3, 3] channels-last fp32) += dW of the 3x3 stride-1 convolution
+// x [N, C, H, W] -> dy [N, K, H, W] (channels-last fp32), Winograd F(2x2, 3x3);
+// part: >= wino_wgrad_ws(...) fp32 workspace
+int64_t wino_wgrad_ws(int64_t N, int64_t H, int64_t W, int64_t C, int64_t K, int64_t splits) {
+  return (int64_t)gk::wino_wgrad_splits((int)N, (int)H, (int)W, (int)C, (int)K, (int)splits) * 16 * K * C;
+}
+
+void wino_wgrad(at::Tensor x, at::Tensor dy, at::Tensor out, at::Tensor part, int64_t splits) {
+  auto cl = [](const at::Tensor& t) {
+    return t.is_cuda() && t.scalar_type() == at::kFloat && t.dim() == 4 && t.is_contiguous(at::MemoryFormat::ChannelsLast);
+  };
+  TORCH_CHECK(cl(x) && cl(dy) && cl(out), "wino_wgrad: x, dy, out must be channels-last fp32 GPU tensors");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), K = dy.size(1);
+  TORCH_CHECK(dy.size(0) == N && dy.size(2) == H && dy.size(3) == W, "wino_wgrad: dy must be [N, K, H, W]");
+  TORCH_CHECK(out.size(0) == K && out.size(1) == C && out.size(2) == 3 && out.size(3) == 3,
+              "wino_wgrad: out must be [K, C, 3, 3]");
+  TORCH_CHECK(C % 64 == 0 && K % 64 == 0, "wino_wgrad: C and K must be multiples of 64");
+  TORCH_CHECK(N * ((H + 1) / 2) * ((W + 1) / 2) < (int64_t(1) << 31) && x.numel() * 4 < (int64_t(1) << 31) &&
+                  dy.numel() * 4 < (int64_t(1) << 31),
+              "wino_wgrad: size out of range (x, dy bytes < 2^31: buffer-descriptor addressing)");
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() &&
+                  part.numel() >= wino_wgrad_ws(N, H, W, C, K, splits),
+              "wino_wgrad: workspace too small (wino_wgrad_ws)");
+  c10::DeviceGuard guard(x.device());
+  gk::wino_wgrad(x.data_ptr<float>(), dy.data_ptr<float>(), part.data_ptr<float>(), out.data_ptr<float>(), (int)N,
+                 (int)H, (int)W, (int)C, (int)K, (int)splits, cur_stream(x));
+}
+
 // grad-input of a stride-2 convolution (1x1 / pad 0 or 3x3 / pad 1) through the
 // stride-1 MFMA kernels: dX = conv_transpose(dY, W) splits into the four
 // (row, column) parity classes of dX; class (a, b) is a stride-1 KH'xKW' conv
@@ -1591,6 +1665,11 @@ TORCH_LIBRARY(gksgd, m) {
   });
   m.def("wgrad3_ws(int N, int H, int W, int C, int K) -> int", &wgrad3_ws);
   m.def("conv3_wgrad(Tensor dy, Tensor x, Tensor(a!) out, Tensor(b!) part, Tensor zero) -> ()");
+  m.def("wino_weights(Tensor w, Tensor(a!) u, bool flip) -> ()");
+  m.def("wino_wgrad_ws(int N, int H, int W, int C, int K, int splits=0) -> int", &wino_wgrad_ws);
+  m.def("wino_wgrad(Tensor x, Tensor dy, Tensor(a!) out, Tensor(b!) part, int splits=0) -> ()");
+  m.def("wino_conv(Tensor x, Tensor u, Tensor(a!) y, int max_blocks=0, Tensor(b!)? stats=None, Tensor? bn_h=None, "
+        "Tensor? bn_dy2=None, Tensor? bn_mask=None) -> int");
   m.def("conv_dgrad_s2(Tensor dy, Tensor w, Tensor(a!) dx, Tensor zero, int cfg=0, int max_blocks=0, "
         "Tensor? lz_x=None, Tensor? lz_coef=None, Tensor? lz_padz=None, Tensor? lz_padx=None) -> ()");
   m.def("bn_bwd_lazy_pre(Tensor x, Tensor part, int rows, Tensor? w, Tensor mean, Tensor invstd, "
@@ -1695,6 +1774,9 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("gemm_nt", &gemm_nt);
   m.impl("gemm_tn_acc", &gemm_tn_acc);
   m.impl("conv_nt", &conv_nt);
+  m.impl("wino_weights", &wino_weights);
+  m.impl("wino_conv", &wino_conv);
+  m.impl("wino_wgrad", &wino_wgrad);
   m.impl("conv_tn_acc", &conv_tn_acc);
   m.impl("attn_fwd", &attn_fwd);
   m.impl("attn_bwd", &attn_bwd);

@@ -352,6 +352,24 @@ int conv_nt_remap(const void* X, int64_t ldx, const void* zero, int H, int W, in
 void conv_tn_acc(const void* G, const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P,
                  int KH, int KW, float* Wout, int64_t M, int N, bool f32, int cfg, int splits, const LazyArgs* lazy,
                  hipStream_t stream);
+// Winograd F(2x2, 3x3) fp32 convolution, stride 1, padding 1 (winograd.hip).
+//   wino_weights: filter transform of w ([Co][3][3][Ci] channels-last fp32;
+//                 flip = 1: of the grad-input filter W'[c][kh][kw][k] =
+//                 W[k][2-kh][2-kw][c], w then being the forward [K][3][3][C])
+//                 into u = [Ci/8][16][Co][8]
+//   wino_conv   : y[N, H, W, Co] = conv3x3(x[N, H, W, Ci]) from u; Ci % 8 == 0,
+//                 Co % 64 == 0; optional BatchNorm statistics / BN-backward
+//                 epilogue (as conv_nt); returns the partial rows written.
+void wino_weights(const float* w, float* u, int Co, int Ci, int flip, hipStream_t stream);
+int wino_conv(const float* x, const float* u, float* y, int N, int H, int W, int Ci, int Co, int max_blocks,
+              float* stats, int stats_rows, const BnBwdArgs* bn, hipStream_t stream);
+//   wino_wgrad  : out[K][3][3][C] (fp32, channels-last) += dW of the 3x3 stride-1
+//                 convolution x[N, H, W, C] -> dy[N, H, W, K] (C, K % 64 == 0);
+//                 part: wino_wgrad_splits(...) * 16 * K * C fp32 workspace
+//                 (per-split partials, summed in a fixed order: deterministic)
+int wino_wgrad_splits(int N, int H, int W, int C, int K, int splits);
+void wino_wgrad(const float* x, const float* dy, float* part, float* out, int N, int H, int W, int C, int K,
+                int splits, hipStream_t stream);
 
 // ---------------------------------------------------------------------------
 // ImageNet-ResNet stem: 7x7 / stride 2 / pad 3 convolution, 3 -> 64 channels

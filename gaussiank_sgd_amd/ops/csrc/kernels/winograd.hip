@@ -1,0 +1,627 @@
+// Winograd F(2x2, 3x3) convolution in fp32 on v_mfma_f32_16x16x4_f32 (gfx950).
+//
+// Why: at the reference's precision (fp32, settings.py:28) the 3x3 stride-1
+// convolutions of a ResNet are bound by the fp32 MFMA rate (64 FLOP/clk/SIMD,
+// 1/16 of bf16), not by memory.  F(2x2, 3x3) computes each 2x2 output tile
+// from a 4x4 input patch with 16 element-wise products per (tile, Cin, Cout)
+// instead of 36: 2.25x fewer MFMA FLOPs.  The transforms are exact-weight
+// additions (+-1 for the data, 1/2 for the filter), so the result is a
+// rearranged fp32 sum of the same products with a few extra roundings --
+// same precision class as the direct convolution (tests vs fp64).
+//
+//   V[xi][t][c]  = (B^T d_t,c B)[xi]            input transform (in-kernel)
+//   U[xi][c][k]  = (G g_k,c G^T)[xi]            filter transform (wino_wt)
+//   M[xi][t][k]  = sum_c V[xi][t][c] U[xi][c][k]   16 GEMMs on MFMA
+//   Y_t,k        = A^T M[.][t][k] A             output transform (epilogue)
+//
+// Grad-input of the same convolution is the forward convolution of dY with the
+// flipped, transposed filter: the same kernel with U built from W'[c][kh][kw][k]
+// = W[k][2-kh][2-kw][c] (wino_wt flip = 1).
+//
+// (GK_WINO_PROBE_* macros: timing-only A/B builds of bench/wino_probe.hip that
+// drop the loads / LDS stores / epilogue stores / barriers; never defined in
+// the extension build.)
+//
+// Kernel layout.  512 threads = 8 waves (two per SIMD); a block owns 64 tiles
+// x 64 output channels for ALL 16 xi, each wave 32 tiles x 16 channels x 16 xi
+// (128 fp32 accumulators per lane).  Keeping every xi of a (tile, channel) in
+// one lane makes the output transform a register-only epilogue.
+// Input channels stream in stages of 8: per stage every thread loads one
+// tile's 4x4 patch for one channel (16 loads, zero padding in registers),
+// transforms it and writes 16 V values; U arrives pre-chunked
+// ([Cin/8][16][Cout][8]) so a block's stage slice is 16 contiguous 2-KiB rows.
+// Two LDS stages (64 KiB each): the next stage's global loads are issued
+// before this stage's 128 MFMAs per wave and land in LDS after them (one
+// barrier per stage), pipelined across tile-block boundaries of the
+// persistent loop.  Operand reads are ds_read_b64: lane (i, q) reads channels
+// 2q, 2q+1 of row i and MFMA j contracts channels {2q + j} -- the same
+// permutation on both operands.  The MFMA is issued with U as the A operand
+// so a lane ends with 4 consecutive output channels of one tile: 16-byte
+// stores.  (One wave per SIMD with 32x32 wave tiles -- 256 accumulators per
+// lane -- spills even with all 512 VGPR + AGPR registers.)
+//
+// Grid: (tile blocks, Cout / 64) persistent along tiles with the x extent a
+// multiple of 8, so all Cout blocks of a tile block run on one XCD (blocks
+// are dealt round-robin to the 8 XCDs) and share the input patches in its L2.
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+#include "gk_kernels.h"
+#include "mfma_util.h"
+
+namespace gk {
+namespace {
+
+constexpr int WBT = 64;                 // tiles per block
+constexpr int WBK = 64;                 // output channels per block
+constexpr int WCK = 8;                  // input channels per stage
+constexpr int WVS = 16 * WBT * WCK;     // floats of one V stage
+constexpr int WUS = 16 * WBK * WCK;     // floats of one U stage
+constexpr int WSTAGE = WVS + WUS;       // 16384 floats = 64 KiB
+constexpr int WLDS = 2 * WSTAGE * 4;    // bytes
+
+struct WinoGeo {
+  int H, W, Ci, Co, TH, TW, ntiles;
+  uint32_t xbytes;   // bytes of the input tensor (< 2^31: buffer-descriptor range check)
+};
+
+struct WBnb {                // BN-backward epilogue operands (gemm.hip BnBwd, fp32)
+  const float* h;            // BN input [M, Co]; nullptr: plain epilogue
+  const float* dy2;          // optional second gradient [M, Co]
+  const uint8_t* mask;       // optional ReLU mask, one byte per 4 channels (bit r: channel 4j + r)
+};
+
+// filter transform: one thread per (co, ci) of the convolution being run;
+// u = [Ci/8][16][Co][8]
+__global__ void __launch_bounds__(256) wino_wt_kernel(const float* __restrict__ w, float* __restrict__ u, int Co, int Ci,
+                                                      int flip) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (int64_t)Co * Ci) return;
+  const int co = (int)(idx / Ci), ci = (int)(idx - (int64_t)co * Ci);
+  float g[3][3];
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw)
+      g[kh][kw] = flip ? w[((int64_t)ci * 9 + (2 - kh) * 3 + (2 - kw)) * Co + co]    // W[k = ci][.][.][c = co]
+                       : w[((int64_t)co * 9 + kh * 3 + kw) * Ci + ci];               // W[co][kh][kw][ci]
+  float t[4][3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    t[0][j] = g[0][j];
+    t[1][j] = 0.5f * (g[0][j] + g[1][j] + g[2][j]);
+    t[2][j] = 0.5f * (g[0][j] - g[1][j] + g[2][j]);
+    t[3][j] = g[2][j];
+  }
+  float* dst = u + ((int64_t)(ci >> 3) * 16 * Co + co) * 8 + (ci & 7);
+  const int64_t xs = (int64_t)Co * 8;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    dst[(4 * i + 0) * xs] = t[i][0];
+    dst[(4 * i + 1) * xs] = 0.5f * (t[i][0] + t[i][1] + t[i][2]);
+    dst[(4 * i + 2) * xs] = 0.5f * (t[i][0] - t[i][1] + t[i][2]);
+    dst[(4 * i + 3) * xs] = t[i][2];
+  }
+}
+
+template <bool STATS, bool BNB>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
+wino_f23_kernel(const float* __restrict__ x, const float* __restrict__ u, float* __restrict__ y, WinoGeo g,
+                float* __restrict__ stats, int64_t stats_ld, WBnb bb) {
+  extern __shared__ __attribute__((aligned(16))) float wlds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wt = wave >> 2, wk = wave & 3;
+  const int fi = lane & 15, fq = lane >> 4;
+  const int k0 = blockIdx.y * WBK;
+  const int ntb = (g.ntiles + WBT - 1) / WBT;
+  const int nst = g.Ci / WCK;
+  const int my_tb = (int)blockIdx.x < ntb ? (ntb - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int total = my_tb * nst;
+  const int THW = g.TH * g.TW;
+  // loader role: tile ltile of the block's 64, channel lc of the stage's 8
+  const int ltile = tid >> 3, lc = tid & 7;
+
+  f32x4 acc[16][2];     // [xi][tile subtile]
+#pragma unroll
+  for (int xi = 0; xi < 16; ++xi)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[xi][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float ssum[4], ssq[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) ssum[r] = ssq[r] = 0.f;
+
+  // x through a buffer descriptor: a patch pixel outside the image gets the
+  // byte offset 0x80000000 (past num_records), which the hardware range check
+  // turns into a zero load -- no branches, no per-load address arithmetic
+  // (the stage's channel offset is the scalar soffset).
+  const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), (short)0, (int)g.xbytes, 0x00020000);
+  uint32_t voff[16];
+  auto set_tile = [&](int tb) {
+    const int tt = tb * WBT + ltile;
+    const bool tv = tt < g.ntiles;
+    const int ttc = tv ? tt : 0;
+    const int n = ttc / THW, r = ttc - n * THW, th = r / g.TW, tw = r - th * g.TW;
+    const int ih0 = 2 * th - 1, iw0 = 2 * tw - 1;
+    // modulo-2^32 byte offset of pixel (ih0, iw0) (may wrap for ih0 = -1; valid taps land in range)
+    const uint32_t base = (uint32_t)((((int64_t)n * g.H + ih0) * g.W + iw0) * g.Ci + lc) * 4u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool v = tv && (unsigned)(ih0 + i) < (unsigned)g.H && (unsigned)(iw0 + j) < (unsigned)g.W;
+        voff[4 * i + j] = v ? base + (uint32_t)((i * g.W + j) * g.Ci) * 4u : 0x80000000u;
+      }
+  };
+
+  float dv[16];
+  // stage s into LDS buffer b: the patch loads (registers, transformed later
+  // by lstore) and U's 32 KiB slice by LDS-DMA, 4 x 1 KiB per wave
+  auto gload = [&](int s, int b) {
+#pragma unroll
+    for (int p = 0; p < 16; ++p) {
+#ifdef GK_WINO_PROBE_NOLOAD
+      dv[p] = (float)(voff[p] & 7);
+#else
+      dv[p] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)voff[p], s * WCK * 4, 0));
+#endif
+    }
+#ifndef GK_WINO_PROBE_NOLOAD
+    GK_LDS char* ub = (GK_LDS char*)wlds + (b * WSTAGE + WVS) * 4;
+    const float* us = u + ((int64_t)s * 16 * g.Co + k0) * 8;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = wave * 4 + i, xi = q >> 1, half = q & 1;
+      glds16(us + (int64_t)xi * g.Co * 8 + half * 256 + lane * 4, ub + q * 1024);
+    }
+#endif
+  };
+  auto lstore = [&](int b) {
+    float* V = wlds + b * WSTAGE;
+    float t[16];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {   // B^T d
+      t[0 + j] = dv[0 + j] - dv[8 + j];
+      t[4 + j] = dv[4 + j] + dv[8 + j];
+      t[8 + j] = dv[8 + j] - dv[4 + j];
+      t[12 + j] = dv[4 + j] - dv[12 + j];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {   // (.) B
+      V[((4 * i + 0) * WBT + ltile) * WCK + lc] = t[4 * i + 0] - t[4 * i + 2];
+      V[((4 * i + 1) * WBT + ltile) * WCK + lc] = t[4 * i + 1] + t[4 * i + 2];
+      V[((4 * i + 2) * WBT + ltile) * WCK + lc] = t[4 * i + 2] - t[4 * i + 1];
+      V[((4 * i + 3) * WBT + ltile) * WCK + lc] = t[4 * i + 1] - t[4 * i + 3];
+    }
+  };
+  // half h of the 16 xi of LDS buffer b
+  auto compute = [&](int b, int h) {
+    const float* V = wlds + b * WSTAGE;
+    const float* U = V + WVS;
+#pragma unroll
+    for (int x8 = 0; x8 < 8; ++x8) {
+      const int xi = h * 8 + x8;
+      f32x2 bv[2];
+      const f32x2 a = *reinterpret_cast<const f32x2*>(U + (xi * WBK + wk * 16 + fi) * WCK + 2 * fq);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        bv[s2] = *reinterpret_cast<const f32x2*>(V + (xi * WBT + wt * 32 + s2 * 16 + fi) * WCK + 2 * fq);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ts = 0; ts < 2; ++ts)
+          acc[xi][ts] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], bv[ts][j], acc[xi][ts], 0, 0, 0);
+    }
+  };
+  auto epilogue = [&](int tb) {
+#pragma unroll
+    for (int ts = 0; ts < 2; ++ts) {
+      const int tt = tb * WBT + wt * 32 + ts * 16 + fi;
+      const bool tv = tt < g.ntiles;
+      const int ttc = tv ? tt : 0;
+      const int n = ttc / THW, rr = ttc - n * THW, th = rr / g.TW, tw = rr - th * g.TW;
+      {
+        const int kk = k0 + wk * 16 + 4 * fq;
+        f32x4 o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {   // A^T M A
+          float s0[4], s1[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            s0[j] = acc[j][ts][r] + acc[4 + j][ts][r] + acc[8 + j][ts][r];
+            s1[j] = acc[4 + j][ts][r] - acc[8 + j][ts][r] - acc[12 + j][ts][r];
+          }
+          o[0][r] = s0[0] + s0[1] + s0[2];
+          o[1][r] = s0[1] - s0[2] - s0[3];
+          o[2][r] = s1[0] + s1[1] + s1[2];
+          o[3][r] = s1[1] - s1[2] - s1[3];
+        }
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const int oh = 2 * th + (p >> 1), ow = 2 * tw + (p & 1);
+          if (!tv || oh >= g.H || ow >= g.W) continue;
+          const int64_t row = ((int64_t)n * g.H + oh) * g.W + ow;
+          f32x4 v = o[p];
+          if constexpr (BNB) {
+            const f32x4 hv = *reinterpret_cast<const f32x4*>(bb.h + row * g.Co + kk);
+            const f32x4 d2 = bb.dy2 ? *reinterpret_cast<const f32x4*>(bb.dy2 + row * g.Co + kk) : f32x4{0.f, 0.f, 0.f, 0.f};
+            const uint32_t bits = bb.mask ? (uint32_t)bb.mask[row * (g.Co >> 2) + (kk >> 2)] : 0xfu;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float dz = (bits >> r) & 1u ? v[r] + d2[r] : 0.f;
+              v[r] = dz;
+              ssum[r] += dz;
+              ssq[r] = fmaf(dz, hv[r], ssq[r]);
+            }
+          } else if constexpr (STATS) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              ssum[r] += v[r];
+              ssq[r] = fmaf(v[r], v[r], ssq[r]);
+            }
+          }
+#ifdef GK_WINO_PROBE_NOEPI
+          if (g.H < 0)
+#endif
+          *reinterpret_cast<f32x4*>(y + row * g.Co + kk) = v;
+        }
+#pragma unroll
+        for (int xi = 0; xi < 16; ++xi) acc[xi][ts] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+
+  if (total > 0) {
+    int tb = blockIdx.x, s = 0;
+    set_tile(tb);
+    gload(0, 0);
+    lstore(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // U's LDS-DMA
+    __syncthreads();
+    for (int it = 0; it < total; ++it) {
+      int ntb_ = tb, ns_ = s + 1;
+      if (ns_ == nst) {
+        ns_ = 0;
+        ntb_ = tb + gridDim.x;
+      }
+      const bool more = it + 1 < total;
+      const int cur = it & 1, nxt = cur ^ 1;
+      if (more) {
+        if (ns_ == 0) set_tile(ntb_);
+        gload(ns_, nxt);
+      }
+      compute(cur, 0);
+      // the next stage's transform between the two MFMA halves: its VALU and
+      // LDS writes issue while MFMAs are in flight
+#ifndef GK_WINO_PROBE_NOLSTORE
+      if (more) lstore(nxt);
+#endif
+      compute(cur, 1);
+      if (s == nst - 1) epilogue(tb);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // U's LDS-DMA (and the epilogue stores)
+#ifndef GK_WINO_PROBE_NOBAR
+      __syncthreads();
+#endif
+      tb = ntb_;
+      s = ns_;
+    }
+  }
+
+  if constexpr (STATS || BNB) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) {
+        ssum[r] += __shfl_xor(ssum[r], off, 64);
+        ssq[r] += __shfl_xor(ssq[r], off, 64);
+      }
+    __syncthreads();
+    float* red = wlds;   // [sum | sq][wt][64]
+    if (fi == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = wk * 16 + 4 * fq + r;
+        red[wt * WBK + col] = ssum[r];
+        red[(2 + wt) * WBK + col] = ssq[r];
+      }
+    }
+    __syncthreads();
+    if (tid < WBK) {
+      stats[(int64_t)blockIdx.x * g.Co + k0 + tid] = red[tid] + red[WBK + tid];
+      stats[stats_ld + (int64_t)blockIdx.x * g.Co + k0 + tid] = red[2 * WBK + tid] + red[3 * WBK + tid];
+    }
+  }
+}
+
+template <bool STATS, bool BNB>
+int launch_wino(const float* x, const float* u, float* y, const WinoGeo& g, int max_blocks, float* stats,
+                int stats_rows, const WBnb& bb, hipStream_t stream) {
+  const int ntb = (g.ntiles + WBT - 1) / WBT;
+  const int nkb = g.Co / WBK;
+  // persistent along tiles, about one block per CU (128 KiB of LDS), x extent a multiple of 8
+  int gx = max_blocks > 0 ? max_blocks : ((256 + nkb - 1) / nkb + 7) / 8 * 8;
+  if (gx > ntb) gx = ntb;
+  if ((STATS || BNB) && gx > stats_rows) gx = stats_rows;   // one partial row per block
+  if (gx < 1) gx = 1;
+  static bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&wino_f23_kernel<STATS, BNB>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, WLDS) == hipSuccess;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL((wino_f23_kernel<STATS, BNB>), dim3((unsigned)gx, (unsigned)nkb), dim3(512), WLDS, stream, x, u,
+                     y, g, stats, (int64_t)stats_rows * g.Co, bb);
+  return gx;
+}
+
+// --------------------------------------------------------------------------
+// Grad-weight.  Differentiating the forward tile formula w.r.t. the filter:
+//   dU[xi][c][k] = sum_t V[xi][t][c] dM[xi][t][k],  dM_t = A dY_t A^T (4x4)
+//   dW[k][c]     = G^T dU[.][c][k] G                (3x3)
+// -- 16 GEMMs reduced over the tiles (2.25x fewer MFMA FLOPs than the 9-tap
+// direct grad-weight).  Block = 64 input x 64 output channels x all 16 xi for
+// one contiguous range of tiles (a split); 8 waves, each 32 c x 16 k x 16 xi
+// (128 accumulators per lane; lane ends with 4 consecutive c of one k).
+// Stages of 8 tiles: thread (tile, channel) loads the tile's 4x4 input patch
+// of channel c (16 loads, 64 lanes = 256 contiguous bytes per pixel) and its
+// 2x2 dY block of channel k, transforms both and writes V / dM rows
+// [xi][channel][tile] (row stride 10 floats: 2-way write conflicts, aligned
+// 8-byte operand reads).  Two stages of 80 KiB fill the 160 KiB LDS.  Each
+// block writes its dU partial (plain stores, no atomics: deterministic); the
+// finalize kernel sums the splits, applies G^T . G and adds into the fp32
+// gradient (channels-last [K][3][3][C]).  Blocks are remapped so the Cout /
+// Cin blocks of one split sit on one XCD and share its patches in L2.
+constexpr int WGT = 8;                      // tiles per stage
+constexpr int WGRS = 10;                    // LDS row stride (floats)
+constexpr int WGHALF = 16 * 64 * WGRS;      // floats of one operand stage
+constexpr int WGSTAGE = 2 * WGHALF;         // V + dM
+constexpr int WGLDS = 2 * WGSTAGE * 4;      // 163840 bytes
+
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
+wino_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ part, WinoGeo g,
+                  int splits, int tps) {
+  // g.Ci = C (input channels), g.Co = K (output channels)
+  extern __shared__ __attribute__((aligned(16))) float wlds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wave >> 2, wk = wave & 3;
+  const int fi = lane & 15, fq = lane >> 4;
+  const int ncb = g.Ci / 64, nkb = g.Co / 64;
+  const int nb = ncb * nkb * splits;
+  // XCD-aware remap (nb % 8 == 0): hardware block b runs on XCD b % 8
+  const int bid = blockIdx.x;
+  const int logical = (bid & 7) * (nb >> 3) + (bid >> 3);
+  const int split = logical / (ncb * nkb), rem = logical - split * ncb * nkb;
+  const int c0 = (rem / nkb) * 64, k0 = (rem % nkb) * 64;
+  const int t_begin = split * tps;
+  int t_end = t_begin + tps;
+  if (t_end > g.ntiles) t_end = g.ntiles;
+  const int nst = t_end > t_begin ? (t_end - t_begin + WGT - 1) / WGT : 0;
+  const int THW = g.TH * g.TW;
+  const int lt = tid >> 6, lch = tid & 63;   // loader: tile lt of the stage, channel lch
+
+  f32x4 acc[16][2];   // [xi][c subtile]
+#pragma unroll
+  for (int xi = 0; xi < 16; ++xi)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[xi][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // x and dy through buffer descriptors (out-of-image taps: offset past the
+  // range, loaded as zero); the loader's tile advances by 8 per stage, its
+  // (n, th, tw) is stepped incrementally (no per-stage division)
+  const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), (short)0, (int)g.xbytes, 0x00020000);
+  const auto gr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dy), (short)0,
+                                                    (int)(g.xbytes / g.Ci * g.Co), 0x00020000);
+  int ct = t_begin + lt, cn = 0, cth = 0, ctw = 0;
+  {
+    const int t0 = ct < g.ntiles ? ct : 0;
+    cn = t0 / THW;
+    const int r = t0 - cn * THW;
+    cth = r / g.TW;
+    ctw = r - cth * g.TW;
+  }
+  float dv[16], gv[4];
+  auto gload = [&](int st) {
+    const bool tv = ct < t_end;
+    const int ih0 = 2 * cth - 1, iw0 = 2 * ctw - 1;
+    const uint32_t xb = (uint32_t)((((int64_t)cn * g.H + ih0) * g.W + iw0) * g.Ci + c0 + lch) * 4u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool v = tv && (unsigned)(ih0 + i) < (unsigned)g.H && (unsigned)(iw0 + j) < (unsigned)g.W;
+        const uint32_t o = v ? xb + (uint32_t)((i * g.W + j) * g.Ci) * 4u : 0x80000000u;
+#ifdef GK_WINO_PROBE_NOLOAD
+        dv[4 * i + j] = (float)(o & 7);
+#else
+        dv[4 * i + j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)o, 0, 0));
+#endif
+      }
+    const uint32_t gb = (uint32_t)((((int64_t)cn * g.H + 2 * cth) * g.W + 2 * ctw) * g.Co + k0 + lch) * 4u;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const bool v = tv && 2 * cth + a < g.H && 2 * ctw + b < g.W;
+        const uint32_t o = v ? gb + (uint32_t)((a * g.W + b) * g.Co) * 4u : 0x80000000u;
+#ifdef GK_WINO_PROBE_NOLOAD
+        gv[2 * a + b] = (float)(o & 7);
+#else
+        gv[2 * a + b] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(gr, (int)o, 0, 0));
+#endif
+      }
+    // next stage's tile: +WGT
+    ct += WGT;
+    ctw += WGT;
+    while (ctw >= g.TW) {
+      ctw -= g.TW;
+      if (++cth == g.TH) {
+        cth = 0;
+        ++cn;
+      }
+    }
+    (void)st;
+  };
+  auto lstore = [&](int buf) {
+    float* V = wlds + buf * WGSTAGE;
+    float* D = V + WGHALF;
+    float t[16];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {   // B^T d
+      t[0 + j] = dv[0 + j] - dv[8 + j];
+      t[4 + j] = dv[4 + j] + dv[8 + j];
+      t[8 + j] = dv[8 + j] - dv[4 + j];
+      t[12 + j] = dv[4 + j] - dv[12 + j];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {   // (.) B
+      V[((4 * i + 0) * 64 + lch) * WGRS + lt] = t[4 * i + 0] - t[4 * i + 2];
+      V[((4 * i + 1) * 64 + lch) * WGRS + lt] = t[4 * i + 1] + t[4 * i + 2];
+      V[((4 * i + 2) * 64 + lch) * WGRS + lt] = t[4 * i + 2] - t[4 * i + 1];
+      V[((4 * i + 3) * 64 + lch) * WGRS + lt] = t[4 * i + 1] - t[4 * i + 3];
+    }
+    // dM = A dY A^T, A = [[1,0],[1,1],[1,-1],[0,-1]]: rows (p, p+q, p-q, -q) of each column
+    float m[4][2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const float p = gv[b], q = gv[2 + b];
+      m[0][b] = p;
+      m[1][b] = p + q;
+      m[2][b] = p - q;
+      m[3][b] = -q;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float p = m[i][0], q = m[i][1];
+      D[((4 * i + 0) * 64 + lch) * WGRS + lt] = p;
+      D[((4 * i + 1) * 64 + lch) * WGRS + lt] = p + q;
+      D[((4 * i + 2) * 64 + lch) * WGRS + lt] = p - q;
+      D[((4 * i + 3) * 64 + lch) * WGRS + lt] = -q;
+    }
+  };
+  auto compute = [&](int buf, int h) {
+    const float* V = wlds + buf * WGSTAGE;
+    const float* D = V + WGHALF;
+#pragma unroll
+    for (int x8 = 0; x8 < 8; ++x8) {
+      const int xi = h * 8 + x8;
+      f32x2 a[2];
+#pragma unroll
+      for (int cs = 0; cs < 2; ++cs)
+        a[cs] = *reinterpret_cast<const f32x2*>(V + ((xi * 64) + wc * 32 + cs * 16 + fi) * WGRS + 2 * fq);
+      const f32x2 b = *reinterpret_cast<const f32x2*>(D + ((xi * 64) + wk * 16 + fi) * WGRS + 2 * fq);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int cs = 0; cs < 2; ++cs)
+          acc[xi][cs] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cs][j], b[j], acc[xi][cs], 0, 0, 0);
+    }
+  };
+
+  if (nst > 0) {
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    for (int st = 0; st < nst; ++st) {
+      const bool more = st + 1 < nst;
+      if (more) gload(st + 1);
+      compute(st & 1, 0);
+#ifndef GK_WINO_PROBE_NOLSTORE
+      if (more) lstore((st + 1) & 1);
+#endif
+      compute(st & 1, 1);
+#ifndef GK_WINO_PROBE_NOBAR
+      __syncthreads();
+#endif
+    }
+  }
+  // dU partial of this split: part[split][xi][k][c], 4 consecutive c per lane
+  const int k = k0 + wk * 16 + fi;
+#pragma unroll
+  for (int xi = 0; xi < 16; ++xi)
+#pragma unroll
+    for (int cs = 0; cs < 2; ++cs) {
+      const int c = c0 + wc * 32 + cs * 16 + 4 * fq;
+      *reinterpret_cast<f32x4*>(part + (((int64_t)split * 16 + xi) * g.Co + k) * g.Ci + c) = acc[xi][cs];
+    }
+}
+
+// out[k][kh][kw][c] += G^T (sum_s part[s][.][k][c]) G; one thread per (k, c)
+__global__ void __launch_bounds__(256) wino_wgrad_finalize_kernel(const float* __restrict__ part, float* __restrict__ out,
+                                                                  int K, int C, int splits) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (int64_t)K * C) return;
+  const int k = (int)(idx / C), c = (int)(idx - (int64_t)k * C);
+  float du[16];
+#pragma unroll
+  for (int xi = 0; xi < 16; ++xi) du[xi] = 0.f;
+  for (int sp = 0; sp < splits; ++sp) {
+    const float* p = part + ((int64_t)sp * 16 * K + k) * C + c;
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi) du[xi] += p[(int64_t)xi * K * C];
+  }
+  float t[3][4];   // G^T dU
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float a = du[j], b = du[4 + j], c2 = du[8 + j], d = du[12 + j];
+    t[0][j] = a + 0.5f * (b + c2);
+    t[1][j] = 0.5f * (b - c2);
+    t[2][j] = 0.5f * (b + c2) + d;
+  }
+  float* o = out + (int64_t)k * 9 * C + c;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    o[(3 * i + 0) * C] += t[i][0] + 0.5f * (t[i][1] + t[i][2]);
+    o[(3 * i + 1) * C] += 0.5f * (t[i][1] - t[i][2]);
+    o[(3 * i + 2) * C] += 0.5f * (t[i][1] + t[i][2]) + t[i][3];
+  }
+}
+
+}  // namespace
+
+void wino_weights(const float* w, float* u, int Co, int Ci, int flip, hipStream_t stream) {
+  const int64_t n = (int64_t)Co * Ci;
+  hipLaunchKernelGGL(wino_wt_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, w, u, Co, Ci, flip);
+}
+
+int wino_conv(const float* x, const float* u, float* y, int N, int H, int W, int Ci, int Co, int max_blocks,
+              float* stats, int stats_rows, const BnBwdArgs* bn, hipStream_t stream) {
+  WinoGeo g{H, W, Ci, Co, (H + 1) / 2, (W + 1) / 2, 0, 0};
+  g.ntiles = N * g.TH * g.TW;
+  g.xbytes = (uint32_t)((int64_t)N * H * W * Ci * 4);
+  const WBnb bb = bn ? WBnb{static_cast<const float*>(bn->h), static_cast<const float*>(bn->dy2), bn->mask} : WBnb{};
+  if (bn) return launch_wino<false, true>(x, u, y, g, max_blocks, stats, stats_rows, bb, stream);
+  if (stats) return launch_wino<true, false>(x, u, y, g, max_blocks, stats, stats_rows, bb, stream);
+  return launch_wino<false, false>(x, u, y, g, max_blocks, nullptr, 0, bb, stream);
+}
+
+int wino_wgrad_splits(int N, int H, int W, int C, int K, int splits) {
+  const int ntiles = N * ((H + 1) / 2) * ((W + 1) / 2);
+  const int cells = (C / 64) * (K / 64);
+  if (splits <= 0) splits = (256 + cells - 1) / cells;     // about one block per CU
+  splits = (splits + 7) / 8 * 8;                            // XCD remap: block count % 8 == 0
+  const int maxs = (ntiles + WGT - 1) / WGT;
+  if (splits > maxs) splits = (maxs + 7) / 8 * 8;
+  return splits;
+}
+
+void wino_wgrad(const float* x, const float* dy, float* part, float* out, int N, int H, int W, int C, int K,
+                int splits, hipStream_t stream) {
+  WinoGeo g{H, W, C, K, (H + 1) / 2, (W + 1) / 2, 0, 0};
+  g.ntiles = N * g.TH * g.TW;
+  g.xbytes = (uint32_t)((int64_t)N * H * W * C * 4);
+  splits = wino_wgrad_splits(N, H, W, C, K, splits);
+  int tps = (g.ntiles + splits - 1) / splits;
+  tps = (tps + WGT - 1) / WGT * WGT;
+  const int nb = (C / 64) * (K / 64) * splits;
+  static bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&wino_wgrad_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, WGLDS) == hipSuccess;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL(wino_wgrad_kernel, dim3((unsigned)nb), dim3(512), WGLDS, stream, x, dy, part, g, splits, tps);
+  const int64_t n = (int64_t)K * C;
+  hipLaunchKernelGGL(wino_wgrad_finalize_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, part, out, K,
+                     C, splits);
+}
+
+}  // namespace gk

@@ -16,8 +16,8 @@ def category(n: str) -> str:
         return "gk LSTM (split-K step GEMM + fused cells)"
     if "gk::" in n and "colsum" in n:
         return "gk linear bias-grad column sums"
-    if "gk::" in n and ("gemm_nt" in n or "gemm_tn" in n or "stem_" in n or "wgrad3" in n):
-        return "gk HIP conv GEMMs (1x1 / implicit-GEMM 3x3, MFMA)"
+    if "gk::" in n and ("gemm_nt" in n or "gemm_tn" in n or "stem_" in n or "wgrad3" in n or "wino_" in n):
+        return "gk HIP conv GEMMs (1x1 / implicit-GEMM 3x3 / Winograd, MFMA)"
     if "gk::" in n and "attn_" in n:
         return "gk fused attention (flash fwd / dQ / dK-dV, MFMA)"
     if "gk::" in n:

@@ -221,6 +221,9 @@ def test_resnet50_step_lazy_matches_plain(monkeypatch):
     small-batch BatchNorms, so both are compared against fp64, not each
     other)."""
     from gaussiank_sgd_amd.models.resnet_imagenet import resnet50
+    from gaussiank_sgd_amd.ops import conv1x1
+    # the lazy operands ride on the direct kernels; compare like with like
+    monkeypatch.setattr(conv1x1, "_WINO", False)
     torch.manual_seed(0)
     m0 = resnet50(num_classes=10)
     x = torch.randn(8, 3, 96, 96)
