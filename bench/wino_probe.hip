@@ -34,11 +34,14 @@ int main(int argc, char** argv) {
   const int N = argc > 1 ? atoi(argv[1]) : 512;
   const int iters = argc > 2 ? atoi(argv[2]) : 20;
   const char* tag = argc > 3 ? argv[3] : "base";
+  const int only_c = argc > 4 ? atoi(argv[4]) : 0;     // run one channel count only (0: all)
+  const int only_op = argc > 5 ? atoi(argv[5]) : -1;   // 0 fwd, 1 fwd_stats, 2 wgrad (-1: all)
   struct S { int C, H; } shapes[] = {{64, 56}, {128, 28}, {256, 14}, {512, 7}};
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
   for (auto sh : shapes) {
+    if (only_c && sh.C != only_c) continue;
     const int C = sh.C, K = sh.C, H = sh.H, W = sh.H;
     const int64_t nx = (int64_t)N * H * W * C;
     float* x = dalloc(nx, 1);
@@ -51,6 +54,7 @@ int main(int argc, char** argv) {
     float* part = dalloc((int64_t)splits * 16 * K * C, 7);
     const double flops = 2.0 * N * H * W * (double)C * K * 9;
     for (int op = 0; op < 3; ++op) {
+      if (only_op >= 0 && op != only_op) continue;
       auto run = [&]() {
         if (op == 0) gk::wino_conv(x, u, y, N, H, W, C, K, 0, nullptr, 0, nullptr, 0);
         else if (op == 1) gk::wino_conv(x, u, y, N, H, W, C, K, 0, st, 1280, nullptr, 0);

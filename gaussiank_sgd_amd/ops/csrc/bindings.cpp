@@ -1106,8 +1106,8 @@ int64_t wino_conv(at::Tensor x, at::Tensor u, at::Tensor y, int64_t max_blocks, 
   TORCH_CHECK(u.is_cuda() && u.scalar_type() == at::kFloat && u.is_contiguous() && u.numel() == 16 * Ci * Co,
               "wino_conv: u must hold 16 * Ci * Co fp32 (wino_weights)");
   TORCH_CHECK(N * ((H + 1) / 2) * ((W + 1) / 2) < (int64_t(1) << 31) && x.numel() > 0 &&
-                  x.numel() * 4 < (int64_t(1) << 31),
-              "wino_conv: size out of range (input bytes < 2^31: buffer-descriptor addressing)");
+                  x.numel() * 4 < (int64_t(1) << 31) && y.numel() * 4 < (int64_t(1) << 31),
+              "wino_conv: size out of range (input / output bytes < 2^31: buffer-descriptor addressing)");
   int rows = 0;
   float* sp = stats_ptr(stats, Co, &rows);
   gk::BnBwdArgs bn{};

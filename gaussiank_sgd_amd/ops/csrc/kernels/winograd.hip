@@ -45,6 +45,8 @@
 // are dealt round-robin to the 8 XCDs) and share the input patches in its L2.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "common.h"
 #include "gk_kernels.h"
 #include "mfma_util.h"
@@ -63,6 +65,7 @@ constexpr int WLDS = 2 * WSTAGE * 4;    // bytes
 struct WinoGeo {
   int H, W, Ci, Co, TH, TW, ntiles;
   uint32_t xbytes;   // bytes of the input tensor (< 2^31: buffer-descriptor range check)
+  uint32_t ybytes;   // bytes of the output tensor (< 2^31; BN-backward operands have its shape)
 };
 
 struct WBnb {                // BN-backward epilogue operands (gemm.hip BnBwd, fp32)
@@ -71,8 +74,16 @@ struct WBnb {                // BN-backward epilogue operands (gemm.hip BnBwd, f
   const uint8_t* mask;       // optional ReLU mask, one byte per 4 channels (bit r: channel 4j + r)
 };
 
+// LDS bank swizzle of the forward kernel's operand rows (8 floats = four
+// 8-byte slots per row): slot q of row r lives at q ^ wsw(r).  An MFMA operand
+// read has 16 lanes on rows r..r+15 at one slot; without the swizzle rows 4
+// apart share banks (4-way conflicts, measured 0.59 conflict cycles per LDS
+// cycle); with it the 16 rows cover all 32 banks.  U is stored pre-swizzled
+// by the filter transform, so its LDS-DMA copy lands swizzled.
+__host__ __device__ __forceinline__ int wsw(int r) { return (r >> 2) & 3; }
+
 // filter transform: one thread per (co, ci) of the convolution being run;
-// u = [Ci/8][16][Co][8]
+// u = [Ci/8][16][Co][8] (slots swizzled by wsw(co))
 __global__ void __launch_bounds__(256) wino_wt_kernel(const float* __restrict__ w, float* __restrict__ u, int Co, int Ci,
                                                       int flip) {
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -93,7 +104,8 @@ __global__ void __launch_bounds__(256) wino_wt_kernel(const float* __restrict__ 
     t[2][j] = 0.5f * (g[0][j] - g[1][j] + g[2][j]);
     t[3][j] = g[2][j];
   }
-  float* dst = u + ((int64_t)(ci >> 3) * 16 * Co + co) * 8 + (ci & 7);
+  // 8-byte slot (ci & 7) >> 1 of row co stored at slot ^ wsw(co) (see wsw)
+  float* dst = u + ((int64_t)(ci >> 3) * 16 * Co + co) * 8 + ((((ci & 7) >> 1) ^ wsw(co)) << 1) + (ci & 1);
   const int64_t xs = (int64_t)Co * 8;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -135,9 +147,8 @@ wino_f23_kernel(const float* __restrict__ x, const float* __restrict__ u, float*
   // byte offset 0x80000000 (past num_records), which the hardware range check
   // turns into a zero load -- no branches, no per-load address arithmetic
   // (the stage's channel offset is the scalar soffset).
-  const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), (short)0, (int)g.xbytes, 0x00020000);
   uint32_t voff[16];
-  auto set_tile = [&](int tb) {
+  auto set_tile = [&](int tb) __attribute__((always_inline)) {
     const int tt = tb * WBT + ltile;
     const bool tv = tt < g.ntiles;
     const int ttc = tv ? tt : 0;
@@ -154,18 +165,44 @@ wino_f23_kernel(const float* __restrict__ x, const float* __restrict__ u, float*
       }
   };
 
-  float dv[16];
-  // stage s into LDS buffer b: the patch loads (registers, transformed later
-  // by lstore) and U's 32 KiB slice by LDS-DMA, 4 x 1 KiB per wave
-  auto gload = [&](int s, int b) {
+  // patch values of two stages in flight (ring of two register sets): stage
+  // s + 2 is loaded while stage s is multiplied and stage s + 1 transformed
+  float dv[2][16];
+  // Issued as inline asm: the compiler's wait-count pass, unable to order the
+  // ring's loads against the LDS-DMA and epilogue stores across the loop
+  // back-edge, would wait vmcnt(0) before the transform (draining the
+  // stage-(s + 2) prefetch it just issued).  The transform waits itself
+  // (vwait, tied to the registers).
+  // the descriptor as four readfirstlane'd words: provably uniform, so the
+  // "s" asm operand gets SGPRs
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const uint64_t xa = (uint64_t)(uintptr_t)x;
+  const u32x4 xrs = u32x4{(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)xa),
+                          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(xa >> 32)),
+                          (uint32_t)__builtin_amdgcn_readfirstlane((int)g.xbytes), 0x00020000u};
+  auto gload_v = [&](int s, int r) __attribute__((always_inline)) {
+    const int so = __builtin_amdgcn_readfirstlane(s * WCK * 4);
 #pragma unroll
     for (int p = 0; p < 16; ++p) {
 #ifdef GK_WINO_PROBE_NOLOAD
-      dv[p] = (float)(voff[p] & 7);
+      dv[r][p] = (float)(voff[p] & 7);
 #else
-      dv[p] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)voff[p], s * WCK * 4, 0));
+      asm volatile("buffer_load_dword %0, %1, %2, %3 offen" : "=v"(dv[r][p]) : "v"(voff[p]), "s"(xrs), "s"(so));
 #endif
     }
+  };
+  // at most N vector-memory ops outstanding; the ring's registers tied to the wait
+  auto vwait = [&](auto NC, int r) __attribute__((always_inline)) {
+    constexpr int N = decltype(NC)::value;
+    float* d = dv[r];
+    asm volatile("s_waitcnt vmcnt(%16)"
+                 : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3]), "+v"(d[4]), "+v"(d[5]), "+v"(d[6]), "+v"(d[7]),
+                   "+v"(d[8]), "+v"(d[9]), "+v"(d[10]), "+v"(d[11]), "+v"(d[12]), "+v"(d[13]), "+v"(d[14]), "+v"(d[15])
+                 : "n"(N)
+                 : "memory");
+  };
+  // U's 32 KiB slice of stage s into LDS buffer b by LDS-DMA, 4 x 1 KiB per wave
+  auto gload_u = [&](int s, int b) __attribute__((always_inline)) {
 #ifndef GK_WINO_PROBE_NOLOAD
     GK_LDS char* ub = (GK_LDS char*)wlds + (b * WSTAGE + WVS) * 4;
     const float* us = u + ((int64_t)s * 16 * g.Co + k0) * 8;
@@ -176,36 +213,41 @@ wino_f23_kernel(const float* __restrict__ x, const float* __restrict__ u, float*
     }
 #endif
   };
-  auto lstore = [&](int b) {
+  auto lstore = [&](int b, int r) __attribute__((always_inline)) {
     float* V = wlds + b * WSTAGE;
+    const float* d = dv[r];
     float t[16];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {   // B^T d
-      t[0 + j] = dv[0 + j] - dv[8 + j];
-      t[4 + j] = dv[4 + j] + dv[8 + j];
-      t[8 + j] = dv[8 + j] - dv[4 + j];
-      t[12 + j] = dv[4 + j] - dv[12 + j];
+      t[0 + j] = d[0 + j] - d[8 + j];
+      t[4 + j] = d[4 + j] + d[8 + j];
+      t[8 + j] = d[8 + j] - d[4 + j];
+      t[12 + j] = d[4 + j] - d[12 + j];
     }
+    const int col = ((((lc >> 1) ^ wsw(ltile)) << 1) | (lc & 1));
 #pragma unroll
     for (int i = 0; i < 4; ++i) {   // (.) B
-      V[((4 * i + 0) * WBT + ltile) * WCK + lc] = t[4 * i + 0] - t[4 * i + 2];
-      V[((4 * i + 1) * WBT + ltile) * WCK + lc] = t[4 * i + 1] + t[4 * i + 2];
-      V[((4 * i + 2) * WBT + ltile) * WCK + lc] = t[4 * i + 2] - t[4 * i + 1];
-      V[((4 * i + 3) * WBT + ltile) * WCK + lc] = t[4 * i + 1] - t[4 * i + 3];
+      V[((4 * i + 0) * WBT + ltile) * WCK + col] = t[4 * i + 0] - t[4 * i + 2];
+      V[((4 * i + 1) * WBT + ltile) * WCK + col] = t[4 * i + 1] + t[4 * i + 2];
+      V[((4 * i + 2) * WBT + ltile) * WCK + col] = t[4 * i + 2] - t[4 * i + 1];
+      V[((4 * i + 3) * WBT + ltile) * WCK + col] = t[4 * i + 1] - t[4 * i + 3];
     }
   };
-  // half h of the 16 xi of LDS buffer b
-  auto compute = [&](int b, int h) {
+  // half h of the 16 xi of LDS buffer b.  (Reading the operands of xi + 2
+  // ahead through a 3-deep register ring measured 7% slower: the compiler
+  // drops the paired ds_read2st64 and adds address arithmetic.)
+  const int rcol = (fq ^ wsw(fi)) << 1;   // swizzled slot of this lane's operand rows (rows = 16-multiple + fi)
+  auto compute = [&](int b, int h) __attribute__((always_inline)) {
     const float* V = wlds + b * WSTAGE;
     const float* U = V + WVS;
 #pragma unroll
     for (int x8 = 0; x8 < 8; ++x8) {
       const int xi = h * 8 + x8;
       f32x2 bv[2];
-      const f32x2 a = *reinterpret_cast<const f32x2*>(U + (xi * WBK + wk * 16 + fi) * WCK + 2 * fq);
+      const f32x2 a = *reinterpret_cast<const f32x2*>(U + (xi * WBK + wk * 16 + fi) * WCK + rcol);
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
-        bv[s2] = *reinterpret_cast<const f32x2*>(V + (xi * WBT + wt * 32 + s2 * 16 + fi) * WCK + 2 * fq);
+        bv[s2] = *reinterpret_cast<const f32x2*>(V + (xi * WBT + wt * 32 + s2 * 16 + fi) * WCK + rcol);
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -213,97 +255,158 @@ wino_f23_kernel(const float* __restrict__ x, const float* __restrict__ u, float*
           acc[xi][ts] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], bv[ts][j], acc[xi][ts], 0, 0, 0);
     }
   };
-  auto epilogue = [&](int tb) {
+  // BN-backward epilogue operands through buffer descriptors (an invalid
+  // pixel's offset is past the range and loads zero): all loads of a 16-tile
+  // subtile's four pixels are issued before any is used, one exposed latency
+  // per subtile instead of one per pixel
+  const auto hr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(bb.h), (short)0, (int)g.ybytes, 0x00020000);
+  const auto dr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(bb.dy2), (short)0, bb.dy2 ? (int)g.ybytes : 0,
+                                                    0x00020000);
+  const auto mr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(bb.mask), (short)0,
+                                                    bb.mask ? (int)(g.ybytes / 16) : 0, 0x00020000);
+  auto epilogue = [&](int tb) __attribute__((always_inline)) {
 #pragma unroll
     for (int ts = 0; ts < 2; ++ts) {
       const int tt = tb * WBT + wt * 32 + ts * 16 + fi;
       const bool tv = tt < g.ntiles;
       const int ttc = tv ? tt : 0;
       const int n = ttc / THW, rr = ttc - n * THW, th = rr / g.TW, tw = rr - th * g.TW;
-      {
-        const int kk = k0 + wk * 16 + 4 * fq;
-        f32x4 o[4];
+      const int kk = k0 + wk * 16 + 4 * fq;
+      bool pv[4];
+      int64_t row[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {   // A^T M A
-          float s0[4], s1[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            s0[j] = acc[j][ts][r] + acc[4 + j][ts][r] + acc[8 + j][ts][r];
-            s1[j] = acc[4 + j][ts][r] - acc[8 + j][ts][r] - acc[12 + j][ts][r];
-          }
-          o[0][r] = s0[0] + s0[1] + s0[2];
-          o[1][r] = s0[1] - s0[2] - s0[3];
-          o[2][r] = s1[0] + s1[1] + s1[2];
-          o[3][r] = s1[1] - s1[2] - s1[3];
-        }
+      for (int p = 0; p < 4; ++p) {
+        const int oh = 2 * th + (p >> 1), ow = 2 * tw + (p & 1);
+        pv[p] = tv && oh < g.H && ow < g.W;
+        row[p] = ((int64_t)n * g.H + oh) * g.W + ow;
+      }
+      f32x4 hv[4], d2[4];
+      uint32_t bits[4];
+      if constexpr (BNB) {
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
-          const int oh = 2 * th + (p >> 1), ow = 2 * tw + (p & 1);
-          if (!tv || oh >= g.H || ow >= g.W) continue;
-          const int64_t row = ((int64_t)n * g.H + oh) * g.W + ow;
-          f32x4 v = o[p];
-          if constexpr (BNB) {
-            const f32x4 hv = *reinterpret_cast<const f32x4*>(bb.h + row * g.Co + kk);
-            const f32x4 d2 = bb.dy2 ? *reinterpret_cast<const f32x4*>(bb.dy2 + row * g.Co + kk) : f32x4{0.f, 0.f, 0.f, 0.f};
-            const uint32_t bits = bb.mask ? (uint32_t)bb.mask[row * (g.Co >> 2) + (kk >> 2)] : 0xfu;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float dz = (bits >> r) & 1u ? v[r] + d2[r] : 0.f;
-              v[r] = dz;
-              ssum[r] += dz;
-              ssq[r] = fmaf(dz, hv[r], ssq[r]);
-            }
-          } else if constexpr (STATS) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              ssum[r] += v[r];
-              ssq[r] = fmaf(v[r], v[r], ssq[r]);
-            }
-          }
-#ifdef GK_WINO_PROBE_NOEPI
-          if (g.H < 0)
-#endif
-          *reinterpret_cast<f32x4*>(y + row * g.Co + kk) = v;
+          const uint32_t off = pv[p] ? (uint32_t)(row[p] * g.Co + kk) * 4u : 0x80000000u;
+          hv[p] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(hr, (int)off, 0, 0));
+          d2[p] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(dr, (int)off, 0, 0));
+          const uint32_t moff = pv[p] ? (uint32_t)(row[p] * (g.Co >> 2) + (kk >> 2)) : 0x80000000u;
+          bits[p] = bb.mask ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(mr, (int)moff, 0, 0) : 0xfu;
         }
+      }
+      f32x4 o[4];
 #pragma unroll
-        for (int xi = 0; xi < 16; ++xi) acc[xi][ts] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int r = 0; r < 4; ++r) {   // A^T M A
+        float s0[4], s1[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          s0[j] = acc[j][ts][r] + acc[4 + j][ts][r] + acc[8 + j][ts][r];
+          s1[j] = acc[4 + j][ts][r] - acc[8 + j][ts][r] - acc[12 + j][ts][r];
+        }
+        o[0][r] = s0[0] + s0[1] + s0[2];
+        o[1][r] = s0[1] - s0[2] - s0[3];
+        o[2][r] = s1[0] + s1[1] + s1[2];
+        o[3][r] = s1[1] - s1[2] - s1[3];
+      }
+#pragma unroll
+      for (int xi = 0; xi < 16; ++xi) acc[xi][ts] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        f32x4 v = o[p];
+        if constexpr (BNB) {
+          // invalid pixels: bits = 0 -> dz = 0, no contribution
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float dz = (bits[p] >> r) & 1u ? v[r] + d2[p][r] : 0.f;
+            v[r] = dz;
+            ssum[r] += dz;
+            ssq[r] = fmaf(dz, hv[p][r], ssq[r]);
+          }
+        } else if constexpr (STATS) {
+          const float m = pv[p] ? 1.f : 0.f;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            ssum[r] = fmaf(m, v[r], ssum[r]);
+            ssq[r] = fmaf(m * v[r], v[r], ssq[r]);
+          }
+        }
+#ifdef GK_WINO_PROBE_NOEPI
+        if (g.H < 0)
+#endif
+        if (pv[p]) *reinterpret_cast<f32x4*>(y + row[p] * g.Co + kk) = v;
       }
     }
   };
 
   if (total > 0) {
-    int tb = blockIdx.x, s = 0;
-    set_tile(tb);
-    gload(0, 0);
-    lstore(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // U's LDS-DMA
-    __syncthreads();
-    for (int it = 0; it < total; ++it) {
-      int ntb_ = tb, ns_ = s + 1;
-      if (ns_ == nst) {
-        ns_ = 0;
-        ntb_ = tb + gridDim.x;
+    int tb = blockIdx.x, s = 0;   // compute cursor (tile block, stage)
+    int lb = blockIdx.x, ls = 0;  // load cursor, one stage ahead of the transform
+    auto adv = [&](int& t, int& st) __attribute__((always_inline)) {
+      if (++st == nst) {
+        st = 0;
+        t += gridDim.x;
       }
-      const bool more = it + 1 < total;
-      const int cur = it & 1, nxt = cur ^ 1;
-      if (more) {
-        if (ns_ == 0) set_tile(ntb_);
-        gload(ns_, nxt);
+    };
+    set_tile(lb);
+    gload_u(0, 0);
+    gload_v(0, 0);
+    if (total > 1) {
+      adv(lb, ls);
+      if (ls == 0) set_tile(lb);
+      gload_v(ls, 1);
+    }
+    vwait(std::integral_constant<int, 0>{}, 0);   // everything, U's LDS-DMA included
+    vwait(std::integral_constant<int, 0>{}, 1);
+    lstore(0, 0);
+    __syncthreads();
+    // the register ring index must be a compile-time constant (a runtime one
+    // becomes s_set_gpr_idx moves with a vmcnt(0) after every load): the
+    // loop body is instantiated for cur = 0 and 1 and the loop runs in pairs
+    int it = 0;
+    auto step = [&](auto CUR) __attribute__((always_inline)) {
+      constexpr int cur = decltype(CUR)::value, nxt = cur ^ 1;
+      const bool more = it + 1 < total, pf = it + 2 < total;
+      // U of stage it + 1 (LDS-DMA, oldest), then the patches of stage it + 2
+      if (more) gload_u(ls, nxt);
+      if (pf) {
+        adv(lb, ls);
+        if (ls == 0) set_tile(lb);
+        gload_v(ls, cur);
       }
       compute(cur, 0);
-      // the next stage's transform between the two MFMA halves: its VALU and
-      // LDS writes issue while MFMAs are in flight
+      // stage it + 1's transform (loaded one iteration ago) between the two
+      // MFMA halves: its VALU and LDS writes issue while MFMAs are in flight.
+      // Its 16 loads retired once at most the 20 (4 DMA + 16 patch) or 4 ops
+      // issued this iteration are outstanding (loads retire in order).
+      if (more) {
+        if (pf) vwait(std::integral_constant<int, 20>{}, nxt);
+        else vwait(std::integral_constant<int, 4>{}, nxt);
 #ifndef GK_WINO_PROBE_NOLSTORE
-      if (more) lstore(nxt);
+        lstore(nxt, nxt);
 #endif
+      }
       compute(cur, 1);
-      if (s == nst - 1) epilogue(tb);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // U's LDS-DMA (and the epilogue stores)
+      const bool epi = s == nst - 1;
+      if (epi) epilogue(tb);
+      // Barrier without __syncthreads()' release fence (which waits for
+      // vmcnt(0) and would drain the stage-(it + 2) prefetch): U's LDS-DMA
+      // (issued before the 16 patch loads, and loads retire in order) and
+      // this wave's LDS writes must be done; the patch loads stay in flight.
+      // One asm statement with a memory clobber so no LDS access moves across.
+      if (pf) {
 #ifndef GK_WINO_PROBE_NOBAR
-      __syncthreads();
+        asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#else
+        asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
 #endif
-      tb = ntb_;
-      s = ns_;
+      } else {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      }
+      (void)epi;
+      adv(tb, s);
+      ++it;
+    };
+    while (it < total) {
+      step(std::integral_constant<int, 0>{});
+      if (it < total) step(std::integral_constant<int, 1>{});
     }
   }
 
@@ -420,7 +523,7 @@ wino_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, flo
     ctw = r - cth * g.TW;
   }
   float dv[16], gv[4];
-  auto gload = [&](int st) {
+  auto gload = [&](int st) __attribute__((always_inline)) {
     const bool tv = ct < t_end;
     const int ih0 = 2 * cth - 1, iw0 = 2 * ctw - 1;
     const uint32_t xb = (uint32_t)((((int64_t)cn * g.H + ih0) * g.W + iw0) * g.Ci + c0 + lch) * 4u;
@@ -461,7 +564,7 @@ wino_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, flo
     }
     (void)st;
   };
-  auto lstore = [&](int buf) {
+  auto lstore = [&](int buf) __attribute__((always_inline)) {
     float* V = wlds + buf * WGSTAGE;
     float* D = V + WGHALF;
     float t[16];
@@ -498,7 +601,7 @@ wino_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, flo
       D[((4 * i + 3) * 64 + lch) * WGRS + lt] = -q;
     }
   };
-  auto compute = [&](int buf, int h) {
+  auto compute = [&](int buf, int h) __attribute__((always_inline)) {
     const float* V = wlds + buf * WGSTAGE;
     const float* D = V + WGHALF;
 #pragma unroll
@@ -585,9 +688,10 @@ void wino_weights(const float* w, float* u, int Co, int Ci, int flip, hipStream_
 
 int wino_conv(const float* x, const float* u, float* y, int N, int H, int W, int Ci, int Co, int max_blocks,
               float* stats, int stats_rows, const BnBwdArgs* bn, hipStream_t stream) {
-  WinoGeo g{H, W, Ci, Co, (H + 1) / 2, (W + 1) / 2, 0, 0};
+  WinoGeo g{H, W, Ci, Co, (H + 1) / 2, (W + 1) / 2, 0, 0, 0};
   g.ntiles = N * g.TH * g.TW;
   g.xbytes = (uint32_t)((int64_t)N * H * W * Ci * 4);
+  g.ybytes = (uint32_t)((int64_t)N * H * W * Co * 4);
   const WBnb bb = bn ? WBnb{static_cast<const float*>(bn->h), static_cast<const float*>(bn->dy2), bn->mask} : WBnb{};
   if (bn) return launch_wino<false, true>(x, u, y, g, max_blocks, stats, stats_rows, bb, stream);
   if (stats) return launch_wino<true, false>(x, u, y, g, max_blocks, stats, stats_rows, bb, stream);
@@ -606,7 +710,7 @@ int wino_wgrad_splits(int N, int H, int W, int C, int K, int splits) {
 
 void wino_wgrad(const float* x, const float* dy, float* part, float* out, int N, int H, int W, int C, int K,
                 int splits, hipStream_t stream) {
-  WinoGeo g{H, W, C, K, (H + 1) / 2, (W + 1) / 2, 0, 0};
+  WinoGeo g{H, W, C, K, (H + 1) / 2, (W + 1) / 2, 0, 0, 0};
   g.ntiles = N * g.TH * g.TW;
   g.xbytes = (uint32_t)((int64_t)N * H * W * C * 4);
   splits = wino_wgrad_splits(N, H, W, C, K, splits);
