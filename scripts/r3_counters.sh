@@ -2,7 +2,7 @@
 # PMC counters of the production GEMM kernels (fp32 headline + bf16), two passes
 # per probe (scripts/gemm_counters.sh), summarised by scripts/ctr_table.py.
 set -u
-D=gpurun_out/r3ctr
+D=${CTR_D:-gpurun_out/r3ctr}/ctr
 mkdir -p $D
 probe() {
   local name=$1 kf=$2; shift 2

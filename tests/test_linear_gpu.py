@@ -152,5 +152,8 @@ def test_bert_tiny_step_bf16(cuda):
         t.update_model()
         losses.append(t.current_loss())
     assert all(v == v for v in losses)
-    assert int(opt.arena.buckets[0].bufs.record[0]) > 0
+    # the reference's Gaussian-k may select nothing from a tiny bucket on a given
+    # step (a 128-element LayerNorm bucket at density 0.01 has k = 2): check
+    # that the step as a whole sent gradients
+    assert sum(int(b.bufs.record[0]) for b in opt.arena.buckets) > 0
     assert min(losses[-5:]) < losses[0]
