@@ -461,7 +461,27 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
         }
         if constexpr (F32) {
           // fp32: lane owns 4 consecutive channels of every subtile -- one
-          // 16-byte store per subtile, no shuffle
+          // 16-byte store per subtile, no shuffle.  BN-backward operands of the
+          // row's four subtiles are all loaded before the first is used (one
+          // exposed latency per row instead of one per subtile).
+          f32x4 ehv[4], ed2[4];
+          uint32_t ebits[4];
+          if (bnb) {
+#pragma unroll
+            for (int ns = 0; ns < 4; ++ns) {
+              ehv[ns] = ed2[ns] = f32x4{0.f, 0.f, 0.f, 0.f};
+              ebits[ns] = 0u;
+            }
+            if (live) {
+#pragma unroll
+              for (int ns = 0; ns < 4; ++ns) {
+                const int n = n0 + wn * 64 + ns * 16 + fq * 4;
+                ehv[ns] = *reinterpret_cast<const f32x4*>(static_cast<const float*>(bb.h) + m * ldc + n);
+                if (bb.dy2) ed2[ns] = *reinterpret_cast<const f32x4*>(static_cast<const float*>(bb.dy2) + m * ldc + n);
+                ebits[ns] = bb.mask ? (uint32_t)bb.mask[m * (Ntot >> 2) + (n >> 2)] : 0xfu;
+              }
+            }
+          }
 #pragma unroll
           for (int ns = 0; ns < 4; ++ns) {
             const int n = n0 + wn * 64 + ns * 16 + fq * 4;
@@ -470,13 +490,8 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
             for (int r = 0; r < 4; ++r) v[r] += bia[ns][r];
             if (bnb) {
               // dz = mask ? dy + dy2 : 0; partials sum(dz), sum(dz * h)
-              f32x4 hv = f32x4{0.f, 0.f, 0.f, 0.f}, d2 = f32x4{0.f, 0.f, 0.f, 0.f};
-              uint32_t bits = 0u;
-              if (live) {
-                hv = *reinterpret_cast<const f32x4*>(static_cast<const float*>(bb.h) + m * ldc + n);
-                if (bb.dy2) d2 = *reinterpret_cast<const f32x4*>(static_cast<const float*>(bb.dy2) + m * ldc + n);
-                bits = bb.mask ? (uint32_t)bb.mask[m * (Ntot >> 2) + (n >> 2)] : 0xfu;
-              }
+              const f32x4 hv = ehv[ns], d2 = ed2[ns];
+              const uint32_t bits = ebits[ns];
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
                 const float dz = (bits >> r) & 1u ? v[r] + d2[r] : 0.f;
