@@ -60,7 +60,6 @@ HIP_SOURCES = [
     "kernels/embed.hip",
     "kernels/xent.hip",
     "kernels/winograd.hip",
-    "kernels/gemm_big.hip",
 ]
 CXX_SOURCES = [
     "comm/rccl_engine.cpp",

@@ -47,7 +47,7 @@ _choices: Dict[tuple, tuple] = {}
 # of its time (GKSGD_GK_MARGIN, default 5%: the fp32 implicit-GEMM kernels
 # trail MIOpen's by 1-5% on some 3x3 shapes -- kept, so the fp32 step runs on
 # code this package owns; 0 = fastest wins)
-_OWN = ("hip", "w3", "mat", "wino", "big")
+_OWN = ("hip", "w3", "mat", "wino")
 _GK_MARGIN = float(os.environ.get("GKSGD_GK_MARGIN", "0.05"))
 _timings: Dict[tuple, list] = {}      # key -> [(tag, ms or error)] of the search
 # fp32 3x3 stride-1 forward / grad-input: Winograd F(2x2, 3x3) candidates

@@ -1003,20 +1003,6 @@ int64_t gemm_nt(at::Tensor A, at::Tensor B, at::Tensor C, int64_t cfg, int64_t m
   return r;
 }
 
-// large-tile bf16 GEMM (gemm_big.hip): C = A . B^T (+ bias); false: shape not tiled by cfg
-bool gemm_big(at::Tensor A, at::Tensor B, at::Tensor C, int64_t cfg, c10::optional<at::Tensor> bias) {
-  check_rows(A, "A", A);
-  check_rows(B, "B", A);
-  check_rows(C, "C", A);
-  TORCH_CHECK(A.scalar_type() == at::kBFloat16, "gemm_big: bf16 operands");
-  const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
-  TORCH_CHECK(B.size(1) == K && C.size(0) == M && C.size(1) == N, "gemm_big: shape mismatch");
-  if (!gk::gemm_big_supported(M, N, K, (int)cfg)) return false;
-  c10::DeviceGuard guard(A.device());
-  return gk::gemm_big_nt(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), M, (int)N,
-                         (int)K, (int)cfg, bias_ptr(bias, N), cur_stream(A));
-}
-
 // W[N, K] += G[M, N]^T . X[M, K]   (fp32 W, float atomics)
 void gemm_tn_acc(at::Tensor G, at::Tensor X, at::Tensor W, int64_t cfg, int64_t splits, c10::optional<at::Tensor> lz_x, c10::optional<at::Tensor> lz_coef,
                 c10::optional<at::Tensor> lz_padz, c10::optional<at::Tensor> lz_padx) {
@@ -1665,9 +1651,6 @@ TORCH_LIBRARY(gksgd, m) {
   m.def("gemm_supported(int N, int K) -> bool", &gemm_supported);
   m.def("gemm_nt(Tensor A, Tensor B, Tensor(a!) C, int cfg=0, int max_blocks=0, Tensor(b!)? stats=None, "
         "Tensor? bias=None, Tensor? bn_h=None, Tensor? bn_dy2=None, Tensor? bn_mask=None, Tensor? lz_x=None, Tensor? lz_coef=None, Tensor? lz_padz=None, Tensor? lz_padx=None) -> int");
-  m.def("gemm_big(Tensor A, Tensor B, Tensor(a!) C, int cfg=0, Tensor? bias=None) -> bool");
-  m.def("gemm_big_supported(int M, int N, int K, int cfg=0) -> bool",
-        [](int64_t M, int64_t N, int64_t K, int64_t cfg) { return gk::gemm_big_supported(M, N, K, (int)cfg); });
   m.def("gemm_tn_acc(Tensor G, Tensor X, Tensor(a!) W, int cfg=0, int splits=0, Tensor? lz_x=None, Tensor? lz_coef=None, Tensor? lz_padz=None, Tensor? lz_padx=None) -> ()");
   m.def("conv_nt(Tensor x, Tensor w, Tensor(a!) y, Tensor zero, int stride, int pad, int cfg=0, int max_blocks=0, "
         "Tensor(b!)? stats=None, Tensor? bias=None, Tensor? bn_h=None, Tensor? bn_dy2=None, Tensor? bn_mask=None, "
@@ -1789,7 +1772,6 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("mask_records", &mask_records);
   m.impl("cast_bf16", &cast_bf16);
   m.impl("gemm_nt", &gemm_nt);
-  m.impl("gemm_big", &gemm_big);
   m.impl("gemm_tn_acc", &gemm_tn_acc);
   m.impl("conv_nt", &conv_nt);
   m.impl("wino_weights", &wino_weights);

@@ -302,12 +302,6 @@ void bn_relu_pool_backward(const void* dy, const void* dy2, const uint8_t* amax,
 // pick the grid.
 // ---------------------------------------------------------------------------
 bool gemm_supported(int64_t N, int64_t K);
-// Large-tile bf16 NT GEMM (gemm_big.hip): C[M, N] = A[M, K] . B[N, K]^T (+ fp32
-// bias), bf16 in / out; cfg 0: 256x256 block tiles, 1: 128x256, 2: 256x128.
-// Returns false (nothing launched) when M, N do not divide into the tile.
-bool gemm_big_supported(int64_t M, int64_t N, int64_t K, int cfg);
-bool gemm_big_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N, int K,
-                 int cfg, const float* bias, hipStream_t stream);
 // BatchNorm-backward epilogue of a grad-input GEMM (bn != nullptr): C receives
 // dz = mask ? dy + dy2 : 0 instead of dy (dy rounded to the operand dtype), and
 // `stats` the per-workgroup partials sum(dz), sum(dz * h) -- feed them to

@@ -93,34 +93,19 @@ def _fwd(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor],
     y = torch.empty(M, N, dtype=torch.bfloat16, device=x2.device)
     cands = [(("hip", c, mb), (lambda c=c, mb=mb: g.gemm_nt(x2, w, y, c, mb, None, bias)))
              for c in _cv._NT_CFGS for mb in _cv._NT_GRIDS]
-    big = _big_cfgs(M, N, K)
-    cands += [(("big", c, 0), (lambda c=c: g.gemm_big(x2, w, y, c, bias))) for c in big]
     cands.append((("blas", 0, 0), blas))
-    ch = _cv._pick(("lin_fwd", M, K, N, bias is not None) + (("big",) if big else ()), cands)
+    ch = _cv._pick(("lin_fwd", M, K, N, bias is not None), cands)
     if ch[0] == "blas":
         return blas()
-    if ch[0] == "big":
-        g.gemm_big(x2, w, y, ch[1], bias)
-        return y
     g.gemm_nt(x2, w, y, ch[1], ch[2], None, bias)
     return y
-
-
-def _big_cfgs(M: int, N: int, K: int) -> list:
-    """Large-tile kernel configurations (csrc/kernels/gemm_big.hip) whose tile
-    divides the [M, N] output (GKSGD_GEMM_BIG=0: none)."""
-    if os.environ.get("GKSGD_GEMM_BIG", "1") == "0":
-        return []
-    g = _g()
-    return [c for c in (0, 1, 2) if g.gemm_big_supported(M, N, K, c)]
 
 
 def _dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """dx = dy2 . w, bf16 out."""
     M, N = dy2.shape
     K = w.shape[1]
-    big = _big_cfgs(M, K, N) if _hip_gemm_ok(K, N) else []
-    key = ("lin_dgrad", M, K, N) + (("big",) if big else ())
+    key = ("lin_dgrad", M, K, N)
     got = _cv._choices.get(key)
     if not _hip_gemm_ok(K, N) or (got is not None and got[0] == "blas"):
         return torch.mm(dy2, w)
@@ -129,14 +114,10 @@ def _dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     wt = w.t().contiguous()
     cands = [(("hip", c, mb), (lambda c=c, mb=mb: g.gemm_nt(dy2, wt, dx, c, mb)))
              for c in _cv._NT_CFGS for mb in _cv._NT_GRIDS]
-    cands += [(("big", c, 0), (lambda c=c: g.gemm_big(dy2, wt, dx, c))) for c in big]
     cands.append((("blas", 0, 0), lambda: torch.mm(dy2, w)))
     ch = _cv._pick(key, cands)
     if ch[0] == "blas":
         return torch.mm(dy2, w)
-    if ch[0] == "big":
-        g.gemm_big(dy2, wt, dx, ch[1])
-        return dx
     g.gemm_nt(dy2, wt, dx, ch[1], ch[2])
     return dx
 
