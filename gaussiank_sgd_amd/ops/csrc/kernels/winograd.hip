@@ -165,9 +165,7 @@ wino_f23_kernel(const float* __restrict__ x, const float* __restrict__ u, float*
       }
   };
 
-  // patch values of two stages in flight (ring of two register sets): stage
-  // s + 2 is loaded while stage s is multiplied and stage s + 1 transformed
-  float dv[2][16];
+  float dv[1][16];
   // Issued as inline asm: the compiler's wait-count pass, unable to order the
   // ring's loads against the LDS-DMA and epilogue stores across the loop
   // back-edge, would wait vmcnt(0) before the transform (draining the
@@ -233,26 +231,36 @@ wino_f23_kernel(const float* __restrict__ x, const float* __restrict__ u, float*
       V[((4 * i + 3) * WBT + ltile) * WCK + col] = t[4 * i + 1] - t[4 * i + 3];
     }
   };
-  // half h of the 16 xi of LDS buffer b.  (Reading the operands of xi + 2
-  // ahead through a 3-deep register ring measured 7% slower: the compiler
-  // drops the paired ds_read2st64 and adds address arithmetic.)
+  // All 16 xi of LDS buffer b, the operands of xi + 1 read (into the other
+  // register set) before the MFMAs of xi are issued, so the LDS latency hides
+  // behind them; mid() runs between xi = 7 and xi = 8 (the next stage's
+  // transform: its VALU and LDS writes issue while MFMAs are in flight).
+  // Offsets are lane constants plus compile-time xi strides: the reads are
+  // one base register and immediate offsets.
   const int rcol = (fq ^ wsw(fi)) << 1;   // swizzled slot of this lane's operand rows (rows = 16-multiple + fi)
-  auto compute = [&](int b, int h) __attribute__((always_inline)) {
+  const int aoff = (wk * 16 + fi) * WCK + rcol;
+  const int boff = (wt * 32 + fi) * WCK + rcol;
+  auto compute = [&](int b, auto mid) __attribute__((always_inline)) {
     const float* V = wlds + b * WSTAGE;
     const float* U = V + WVS;
+    f32x2 fa[2], fb[2][2];
+    auto rd = [&](int xi, int sl) __attribute__((always_inline)) {
+      fa[sl] = *reinterpret_cast<const f32x2*>(U + xi * (WBK * WCK) + aoff);
+      fb[sl][0] = *reinterpret_cast<const f32x2*>(V + xi * (WBT * WCK) + boff);
+      fb[sl][1] = *reinterpret_cast<const f32x2*>(V + xi * (WBT * WCK) + boff + 16 * WCK);
+    };
+    rd(0, 0);
 #pragma unroll
-    for (int x8 = 0; x8 < 8; ++x8) {
-      const int xi = h * 8 + x8;
-      f32x2 bv[2];
-      const f32x2 a = *reinterpret_cast<const f32x2*>(U + (xi * WBK + wk * 16 + fi) * WCK + rcol);
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-        bv[s2] = *reinterpret_cast<const f32x2*>(V + (xi * WBT + wt * 32 + s2 * 16 + fi) * WCK + rcol);
+    for (int xi = 0; xi < 16; ++xi) {
+      const int sl = xi & 1;
+      if (xi + 1 < 16) rd(xi + 1, sl ^ 1);
+      if (xi == 8) mid();
+      __builtin_amdgcn_sched_barrier(0);   // keep the reads of xi + 1 ahead of the MFMAs of xi
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int ts = 0; ts < 2; ++ts)
-          acc[xi][ts] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], bv[ts][j], acc[xi][ts], 0, 0, 0);
+          acc[xi][ts] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[sl][j], fb[sl][ts][j], acc[xi][ts], 0, 0, 0);
     }
   };
   // BN-backward epilogue operands through buffer descriptors (an invalid
@@ -282,16 +290,19 @@ wino_f23_kernel(const float* __restrict__ x, const float* __restrict__ u, float*
       }
       f32x4 hv[4], d2[4];
       uint32_t bits[4];
-      if constexpr (BNB) {
+      // BN operands of pixels [p0, p0 + 2): two pixels per batch keeps the
+      // epilogue inside the register budget of the pipelined main loop
+      auto bnload = [&](int p0) __attribute__((always_inline)) {
 #pragma unroll
-        for (int p = 0; p < 4; ++p) {
+        for (int p = p0; p < p0 + 2; ++p) {
           const uint32_t off = pv[p] ? (uint32_t)(row[p] * g.Co + kk) * 4u : 0x80000000u;
           hv[p] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(hr, (int)off, 0, 0));
           d2[p] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(dr, (int)off, 0, 0));
           const uint32_t moff = pv[p] ? (uint32_t)(row[p] * (g.Co >> 2) + (kk >> 2)) : 0x80000000u;
           bits[p] = bb.mask ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(mr, (int)moff, 0, 0) : 0xfu;
         }
-      }
+      };
+      if constexpr (BNB) bnload(0);
       f32x4 o[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {   // A^T M A
@@ -310,6 +321,9 @@ wino_f23_kernel(const float* __restrict__ x, const float* __restrict__ u, float*
       for (int xi = 0; xi < 16; ++xi) acc[xi][ts] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
+        if constexpr (BNB) {
+          if (p == 2) bnload(2);
+        }
         f32x4 v = o[p];
         if constexpr (BNB) {
           // invalid pixels: bits = 0 -> dz = 0, no contribution
@@ -338,7 +352,7 @@ wino_f23_kernel(const float* __restrict__ x, const float* __restrict__ u, float*
 
   if (total > 0) {
     int tb = blockIdx.x, s = 0;   // compute cursor (tile block, stage)
-    int lb = blockIdx.x, ls = 0;  // load cursor, one stage ahead of the transform
+    int lb = blockIdx.x, ls = 0;  // load cursor, one stage ahead
     auto adv = [&](int& t, int& st) __attribute__((always_inline)) {
       if (++st == nst) {
         st = 0;
@@ -348,59 +362,41 @@ wino_f23_kernel(const float* __restrict__ x, const float* __restrict__ u, float*
     set_tile(lb);
     gload_u(0, 0);
     gload_v(0, 0);
-    if (total > 1) {
-      adv(lb, ls);
-      if (ls == 0) set_tile(lb);
-      gload_v(ls, 1);
-    }
     vwait(std::integral_constant<int, 0>{}, 0);   // everything, U's LDS-DMA included
-    vwait(std::integral_constant<int, 0>{}, 1);
     lstore(0, 0);
     __syncthreads();
-    // the register ring index must be a compile-time constant (a runtime one
-    // becomes s_set_gpr_idx moves with a vmcnt(0) after every load): the
-    // loop body is instantiated for cur = 0 and 1 and the loop runs in pairs
+    // One stage of patches in flight: stage it + 1's loads are issued at the
+    // top of iteration it (after its U LDS-DMA) and transformed in the middle
+    // of the iteration's MFMAs.  (Two stages in flight measured the same and
+    // cost 16 registers the BN epilogues spill without.)
     int it = 0;
     auto step = [&](auto CUR) __attribute__((always_inline)) {
       constexpr int cur = decltype(CUR)::value, nxt = cur ^ 1;
-      const bool more = it + 1 < total, pf = it + 2 < total;
-      // U of stage it + 1 (LDS-DMA, oldest), then the patches of stage it + 2
-      if (more) gload_u(ls, nxt);
-      if (pf) {
+      const bool more = it + 1 < total;
+      if (more) {
         adv(lb, ls);
         if (ls == 0) set_tile(lb);
-        gload_v(ls, cur);
+        gload_u(ls, nxt);
+        gload_v(ls, 0);
       }
-      compute(cur, 0);
-      // stage it + 1's transform (loaded one iteration ago) between the two
-      // MFMA halves: its VALU and LDS writes issue while MFMAs are in flight.
-      // Its 16 loads retired once at most the 20 (4 DMA + 16 patch) or 4 ops
-      // issued this iteration are outstanding (loads retire in order).
-      if (more) {
-        if (pf) vwait(std::integral_constant<int, 20>{}, nxt);
-        else vwait(std::integral_constant<int, 4>{}, nxt);
+      compute(cur, [&]() __attribute__((always_inline)) {
+        if (more) {
+          vwait(std::integral_constant<int, 0>{}, 0);   // the patch loads are the youngest ops
 #ifndef GK_WINO_PROBE_NOLSTORE
-        lstore(nxt, nxt);
+          lstore(nxt, 0);
 #endif
-      }
-      compute(cur, 1);
-      const bool epi = s == nst - 1;
-      if (epi) epilogue(tb);
-      // Barrier without __syncthreads()' release fence (which waits for
-      // vmcnt(0) and would drain the stage-(it + 2) prefetch): U's LDS-DMA
-      // (issued before the 16 patch loads, and loads retire in order) and
-      // this wave's LDS writes must be done; the patch loads stay in flight.
-      // One asm statement with a memory clobber so no LDS access moves across.
-      if (pf) {
+        }
+      });
+      if (s == nst - 1) epilogue(tb);
+      // Barrier without __syncthreads()' release fence (the epilogue's global
+      // stores need no ordering here): U's LDS-DMA and this wave's LDS writes
+      // are done.  One asm statement with a memory clobber so no LDS access
+      // moves across it.
 #ifndef GK_WINO_PROBE_NOBAR
-        asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #else
-        asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 #endif
-      } else {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      }
-      (void)epi;
       adv(tb, s);
       ++it;
     };
@@ -601,22 +597,30 @@ wino_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, flo
       D[((4 * i + 3) * 64 + lch) * WGRS + lt] = -q;
     }
   };
-  auto compute = [&](int buf, int h) __attribute__((always_inline)) {
+  // all 16 xi of buffer buf, the operands of xi + 1 read before the MFMAs of
+  // xi (forward kernel's scheme); mid() between xi = 7 and 8
+  auto compute = [&](int buf, auto mid) __attribute__((always_inline)) {
     const float* V = wlds + buf * WGSTAGE;
     const float* D = V + WGHALF;
-#pragma unroll
-    for (int x8 = 0; x8 < 8; ++x8) {
-      const int xi = h * 8 + x8;
-      f32x2 a[2];
+    f32x2 fa[2][2], fb[2];
+    auto rd = [&](int xi, int sl) __attribute__((always_inline)) {
 #pragma unroll
       for (int cs = 0; cs < 2; ++cs)
-        a[cs] = *reinterpret_cast<const f32x2*>(V + ((xi * 64) + wc * 32 + cs * 16 + fi) * WGRS + 2 * fq);
-      const f32x2 b = *reinterpret_cast<const f32x2*>(D + ((xi * 64) + wk * 16 + fi) * WGRS + 2 * fq);
+        fa[sl][cs] = *reinterpret_cast<const f32x2*>(V + ((xi * 64) + wc * 32 + cs * 16 + fi) * WGRS + 2 * fq);
+      fb[sl] = *reinterpret_cast<const f32x2*>(D + ((xi * 64) + wk * 16 + fi) * WGRS + 2 * fq);
+    };
+    rd(0, 0);
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi) {
+      const int sl = xi & 1;
+      if (xi + 1 < 16) rd(xi + 1, sl ^ 1);
+      if (xi == 8) mid();
+      __builtin_amdgcn_sched_barrier(0);   // keep the reads of xi + 1 ahead of the MFMAs of xi
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int cs = 0; cs < 2; ++cs)
-          acc[xi][cs] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cs][j], b[j], acc[xi][cs], 0, 0, 0);
+          acc[xi][cs] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[sl][cs][j], fb[sl][j], acc[xi][cs], 0, 0, 0);
     }
   };
 
@@ -627,11 +631,11 @@ wino_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, flo
     for (int st = 0; st < nst; ++st) {
       const bool more = st + 1 < nst;
       if (more) gload(st + 1);
-      compute(st & 1, 0);
+      compute(st & 1, [&]() __attribute__((always_inline)) {
 #ifndef GK_WINO_PROBE_NOLSTORE
-      if (more) lstore((st + 1) & 1);
+        if (more) lstore((st + 1) & 1);
 #endif
-      compute(st & 1, 1);
+      });
 #ifndef GK_WINO_PROBE_NOBAR
       __syncthreads();
 #endif
