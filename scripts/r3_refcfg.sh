@@ -3,7 +3,7 @@
 # fp32 headline phase + bf16 phase per run, eager and whole-step hipGraph, plus
 # a 2-rank gloo rehearsal of the multi-rank path on one GPU.
 set -u
-D=gpurun_out/r3j
+D=${REFCFG_D:-gpurun_out/r3j}
 mkdir -p $D
 run() {
   local name=$1; shift
