@@ -60,6 +60,7 @@ HIP_SOURCES = [
     "kernels/embed.hip",
     "kernels/xent.hip",
     "kernels/winograd.hip",
+    "kernels/stem_f32.hip",
 ]
 CXX_SOURCES = [
     "comm/rccl_engine.cpp",

@@ -613,12 +613,11 @@ void bn_relu_pool_forward(at::Tensor x, at::Tensor y, at::Tensor amax, c10::opti
               "workspace too small");
   c10::DeviceGuard guard(x.device());
   if (pre.has_value() && pre->defined()) {   // statistics pre-reduced by the producer (stem conv epilogue)
-    TORCH_CHECK(eb == 2 && pre->is_cuda() && pre->scalar_type() == at::kFloat && pre->is_contiguous() &&
-                    pre->dim() == 3 && pre->size(0) == 2 && pre->size(2) == C && pre_rows > 0 &&
-                    pre_rows <= pre->size(1),
-                "pre must be fp32 [2, rows, C] partials (bf16 x) with 0 < pre_rows <= rows");
+    TORCH_CHECK(pre->is_cuda() && pre->scalar_type() == at::kFloat && pre->is_contiguous() && pre->dim() == 3 &&
+                    pre->size(0) == 2 && pre->size(2) == C && pre_rows > 0 && pre_rows <= pre->size(1),
+                "pre must be fp32 [2, rows, C] partials with 0 < pre_rows <= rows");
     const float* ps = pre->data_ptr<float>();
-    gk::bn_relu_pool_forward_pre(x.data_ptr(), y.data_ptr(), amax.data_ptr<uint8_t>(), x.size(0), (int)C, pg, ps,
+    gk::bn_relu_pool_forward_pre(x.data_ptr(), y.data_ptr(), amax.data_ptr<uint8_t>(), x.size(0), (int)C, pg, eb, ps,
                                  ps + pre->size(1) * C, (int)pre_rows, opt_f32(w), opt_f32(b), (float)eps,
                                  (float)momentum, opt_f32_mut(run_mean), opt_f32_mut(run_var),
                                  save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(), scale.data_ptr<float>(),
@@ -905,6 +904,47 @@ void stem_wgrad(at::Tensor x, at::Tensor dy, at::Tensor out, at::Tensor part) {
   gk::stem_wgrad(x.data_ptr(), x.scalar_type() == at::kFloat, (int)N, (int)H, (int)W,
                  static_cast<const uint16_t*>(dy.data_ptr()), part.data_ptr<float>(), out.data_ptr<float>(),
                  out.stride(0), out.stride(1), out.stride(2), out.stride(3), cur_stream(x));
+}
+
+// fp32 stem (stem_f32.hip): x [N, 3, 224, 224] channels-last fp32, w [64, 3, 7, 7] fp32,
+// y [N, 64, 112, 112] channels-last fp32
+int64_t stem_f32_fwd(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tensor> stats) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.dim() == 4 && x.size(1) == 3 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast) && gk::stem_f32_supported((int)x.size(2), (int)x.size(3)),
+              "stem_f32_fwd: x must be a channels-last fp32 [N, 3, 224, 224] GPU tensor");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.dim() == 4 && w.size(0) == 64 && w.size(1) == 3 &&
+                  w.size(2) == 7 && w.size(3) == 7, "stem_f32_fwd: w must be fp32 [64, 3, 7, 7]");
+  const int64_t N = x.size(0);
+  TORCH_CHECK(y.is_cuda() && y.scalar_type() == at::kFloat && y.dim() == 4 && y.size(0) == N && y.size(1) == 64 &&
+                  y.size(2) == 112 && y.size(3) == 112 && y.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "stem_f32_fwd: y must be a channels-last fp32 [N, 64, 112, 112] GPU tensor");
+  int rows = 0;
+  float* sp = stats_ptr(stats, 64, &rows);
+  c10::DeviceGuard guard(x.device());
+  return gk::stem_f32_forward(x.data_ptr<float>(), (int)N, (int)x.size(2), (int)x.size(3), w.data_ptr<float>(),
+                              w.stride(0), w.stride(1), w.stride(2), w.stride(3), y.data_ptr<float>(), sp, rows,
+                              cur_stream(x));
+}
+
+int64_t stem_f32_wgrad_ws(int64_t N) { return (int64_t)gk::stem_f32_wgrad_blocks((int)N) * 64 * 148; }
+
+void stem_f32_wgrad(at::Tensor x, at::Tensor dy, at::Tensor out, at::Tensor part) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.dim() == 4 && x.size(1) == 3 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast) && gk::stem_f32_supported((int)x.size(2), (int)x.size(3)),
+              "stem_f32_wgrad: x must be a channels-last fp32 [N, 3, 224, 224] GPU tensor");
+  const int64_t N = x.size(0);
+  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kFloat && dy.dim() == 4 && dy.size(0) == N &&
+                  dy.size(1) == 64 && dy.size(2) == 112 && dy.size(3) == 112 &&
+                  dy.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "stem_f32_wgrad: dy must be a channels-last fp32 [N, 64, 112, 112] GPU tensor");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.dim() == 4 && out.size(0) == 64 &&
+                  out.size(1) == 3 && out.size(2) == 7 && out.size(3) == 7, "stem_f32_wgrad: out must be fp32 [64, 3, 7, 7]");
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() &&
+                  part.numel() >= stem_f32_wgrad_ws(N), "stem_f32_wgrad: part must hold stem_f32_wgrad_ws(N) floats");
+  c10::DeviceGuard guard(x.device());
+  gk::stem_f32_wgrad(x.data_ptr<float>(), dy.data_ptr<float>(), (int)N, (int)x.size(2), (int)x.size(3),
+                     part.data_ptr<float>(), out.data_ptr<float>(), out.stride(0), out.stride(1), out.stride(2),
+                     out.stride(3), cur_stream(x));
 }
 
 // optional device seed word (graph replays): int32[>=1] on the GPU
@@ -1660,6 +1700,10 @@ TORCH_LIBRARY(gksgd, m) {
   m.def("stem_pack(Tensor w, Tensor(a!) wp) -> ()");
   m.def("stem_fwd(Tensor x, Tensor wp, Tensor(a!) y, Tensor(b!)? stats=None) -> int");
   m.def("stem_wgrad(Tensor x, Tensor dy, Tensor(a!) out, Tensor(b!) part) -> ()");
+  m.def("stem_f32_supported(int H, int W) -> bool", [](int64_t H, int64_t W) { return gk::stem_f32_supported((int)H, (int)W); });
+  m.def("stem_f32_fwd(Tensor x, Tensor w, Tensor(a!) y, Tensor(b!)? stats=None) -> int");
+  m.def("stem_f32_wgrad_ws(int N) -> int", &stem_f32_wgrad_ws);
+  m.def("stem_f32_wgrad(Tensor x, Tensor dy, Tensor(a!) out, Tensor(b!) part) -> ()");
   m.def("wgrad3_supported(int H, int W, int C, int K) -> bool", [](int64_t H, int64_t W, int64_t C, int64_t K) {
     return gk::wgrad3_supported((int)H, (int)W, (int)C, (int)K);
   });
@@ -1765,6 +1809,8 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("conv3_wgrad", &conv3_wgrad);
   m.impl("stem_fwd", &stem_fwd);
   m.impl("stem_wgrad", &stem_wgrad);
+  m.impl("stem_f32_fwd", &stem_f32_fwd);
+  m.impl("stem_f32_wgrad", &stem_f32_wgrad);
   m.impl("bn_relu_pool_forward", &bn_relu_pool_forward);
   m.impl("bn_relu_pool_backward", &bn_relu_pool_backward);
   m.impl("accum_grad", &accum_grad);

@@ -1166,19 +1166,22 @@ void bn_relu_pool_forward(const void* x, void* y, uint8_t* amax, int64_t N, int 
   }
 }
 
-// statistics pre-reduced by the producing convolution (stem.hip epilogue):
-// finalize + the fused BN / ReLU / max-pool pass only (bf16)
-void bn_relu_pool_forward_pre(const void* x, void* y, uint8_t* amax, int64_t N, int C, PoolGeo pg, const float* psum,
-                              const float* psq, int gy, const float* w, const float* b, float eps, float momentum,
-                              float* run_mean, float* run_var, float* save_mean, float* save_invstd, float* scale,
-                              float* shift, int64_t* nbt, hipStream_t s) {
+// statistics pre-reduced by the producing convolution (stem.hip / stem_f32.hip
+// epilogues): finalize + the fused BN / ReLU / max-pool pass only
+void bn_relu_pool_forward_pre(const void* x, void* y, uint8_t* amax, int64_t N, int C, PoolGeo pg, int elem_bytes,
+                              const float* psum, const float* psq, int gy, const float* w, const float* b, float eps,
+                              float momentum, float* run_mean, float* run_var, float* save_mean, float* save_invstd,
+                              float* scale, float* shift, int64_t* nbt, hipStream_t s) {
   const int64_t M = N * pg.H * pg.W;
   const int64_t P = N * pg.OH * pg.OW;
-  const int64_t threads = P * (C / 8);
+  const int64_t threads = P * (C / (elem_bytes == 2 ? 8 : 4));
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(kBlock), 0, s, psum, psq, gy, M, C, w, b,
                      eps, momentum, run_mean, run_var, save_mean, save_invstd, scale, shift, nbt);
   const dim3 grid((unsigned)((threads + kBlock - 1) / kBlock));
-  if (pg.k == 3 && pg.p == 1)
+  if (elem_bytes == 4)
+    hipLaunchKernelGGL(bn_relu_pool_kernel<float>, grid, dim3(kBlock), 0, s, (const float*)x, (float*)y, amax, P, C, pg,
+                       scale, shift);
+  else if (pg.k == 3 && pg.p == 1)
     hipLaunchKernelGGL((bn_relu_pool_kernel<uint16_t, 3>), grid, dim3(kBlock), 0, s, (const uint16_t*)x, (uint16_t*)y,
                        amax, P, C, pg, scale, shift);
   else

@@ -279,7 +279,8 @@ void bn_act_backward(const void* dy, const void* dy2, const uint8_t* mask, const
 struct PoolGeo {
   int H, W, OH, OW, k, s, p;
 };
-void bn_relu_pool_forward_pre(const void* x, void* y, uint8_t* amax, int64_t N, int C, PoolGeo pg, const float* psum,
+void bn_relu_pool_forward_pre(const void* x, void* y, uint8_t* amax, int64_t N, int C, PoolGeo pg, int elem_bytes,
+                              const float* psum,
                               const float* psq, int gy, const float* w, const float* b, float eps, float momentum,
                               float* run_mean, float* run_var, float* save_mean, float* save_invstd, float* scale,
                               float* shift, int64_t* nbt, hipStream_t stream);
@@ -360,6 +361,16 @@ void conv_tn_acc(const void* G, const void* X, const void* zero, int H, int W, i
 //   wino_conv   : y[N, H, W, Co] = conv3x3(x[N, H, W, Ci]) from u; Ci % 8 == 0,
 //                 Co % 64 == 0; optional BatchNorm statistics / BN-backward
 //                 epilogue (as conv_nt); returns the partial rows written.
+// fp32 ResNet stem (stem_f32.hip): x NHWC fp32 [N, 224, 224, 3], w [64][3][7][7]
+// fp32 with element strides s0..s3, y NHWC fp32 [N, 112, 112, 64]; forward
+// returns the BatchNorm partial rows written; grad-weight adds into out
+// (strided like w) through per-block partials (stem_f32_wgrad_blocks(N) x 64 x 148).
+bool stem_f32_supported(int H, int W);
+int stem_f32_wgrad_blocks(int N);
+int stem_f32_forward(const float* x, int N, int H, int W, const float* w, int64_t s0, int64_t s1, int64_t s2,
+                     int64_t s3, float* y, float* stats, int stats_rows, hipStream_t stream);
+void stem_f32_wgrad(const float* x, const float* dy, int N, int H, int W, float* part, float* out, int64_t s0,
+                    int64_t s1, int64_t s2, int64_t s3, hipStream_t stream);
 void wino_weights(const float* w, float* u, int Co, int Ci, int flip, hipStream_t stream);
 int wino_conv(const float* x, const float* u, float* y, int N, int H, int W, int Ci, int Co, int max_blocks,
               float* stats, int stats_rows, const BnBwdArgs* bn, hipStream_t stream);

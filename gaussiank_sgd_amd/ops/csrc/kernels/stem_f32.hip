@@ -1,0 +1,295 @@
+// The ImageNet-ResNet stem convolution (7x7, stride 2, padding 3, 3 -> 64
+// channels) at fp32 -- the reference's precision -- on v_mfma_f32_16x16x4_f32.
+// stem.hip is the bf16 path (bf16 MFMA on packed 4-channel pixels); at fp32
+// MIOpen was the fallback, 1.4 ms forward + 2.2 ms grad-weight per bs512 step
+// (profiles/r03_resnet50_bs512_fp32_kernel_stats.csv, igemm_fwd / igemm_wrw
+// rows): its implicit GEMM handles the 3-channel input badly.
+//
+// K = 7 x 7 x 3 = 147 taps, ordered (kh, kw, c) like the NHWC input, padded to
+// 148; a tap's offset inside an LDS input band is koff(k) = (kh * PW + kw) * 3
+// + c (koff table in LDS), so an MFMA operand element is one ds_read_b32 at
+// pixel_base + koff.
+//
+// forward: a persistent block walks bands of 4 output rows of one image; the
+//   band's 13 input rows (zero padding materialised, 230 pixels x 3 channels)
+//   and the whole [64][148] weight matrix sit in LDS.  Wave w owns output row
+//   w of the band: 7 16-pixel subtiles x 4 16-channel subtiles (112 fp32
+//   accumulators), 37 k-steps of 4 taps, weights as the MFMA A operand so a
+//   lane ends with 4 consecutive channels of one pixel (16-byte stores); the
+//   epilogue reduces the following BatchNorm's batch statistics per block
+//   (stats row = block, as gemm.hip's conv epilogue).
+// grad-weight: dW[n][k] = sum_px dY[px][n] A[px][k], contraction over pixels
+//   4 at a time: dY fragments straight from global (lane = channel, coalesced),
+//   A fragments gathered from the LDS band; each wave accumulates 64 x 160
+//   (4 x 10 subtiles, 160 registers) over its rows of every band of the
+//   block; the 4 waves are summed through LDS and every block writes one
+//   partial; stem_f32_wgrad_reduce sums the partials in block order
+//   (deterministic) into the (arena) gradient.
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+#include "gk_kernels.h"
+#include "mfma_util.h"
+
+namespace gk {
+namespace {
+
+constexpr int kFR = 4;                    // output rows per band (one per wave)
+constexpr int kFIn = 2 * kFR + 5;         // input rows per band
+constexpr int kFK = 147, kFKP = 148;      // taps, padded
+constexpr int kFOW = 112;                 // output width the kernels are built for (224 input)
+constexpr int kFPW = 2 * kFOW + 6;        // padded input band width (pixels)
+constexpr int kFBand = kFIn * kFPW * 3;   // floats of one input band
+constexpr int kFWg = 64 * kFKP;           // floats of the weight matrix
+constexpr int kFKS = 10;                  // grad-weight k subtiles (160 >= 148)
+
+struct StemF32Geo {
+  int N, H, W, OH, OW, nbands;   // nbands = N * OH / kFR
+};
+
+__device__ __forceinline__ void koff_table(int* kt) {
+  for (int k = threadIdx.x; k < 16 * kFKS; k += blockDim.x) {
+    int v = 0;
+    if (k < kFK) {
+      const int kh = k / 21, r = k - kh * 21, kw = r / 3, c = r - kw * 3;
+      v = (kh * kFPW + kw) * 3 + c;
+    }
+    kt[k] = v;   // padded taps read any in-band value: their weight is 0 / their gradient is dropped
+  }
+}
+
+// input rows 2 orow0 - 3 .. + 12 of image n, columns -3 .. 226, zero outside
+__device__ __forceinline__ void load_band(float* band, const float* __restrict__ x, const StemF32Geo& g, int n,
+                                          int orow0) {
+  const int ih0 = 2 * orow0 - 3;
+  for (int i = threadIdx.x; i < kFBand; i += blockDim.x) {
+    const int rr = i / (kFPW * 3), rem = i - rr * (kFPW * 3);
+    const int pc = rem / 3, c = rem - pc * 3;
+    const int ih = ih0 + rr, iw = pc - 3;
+    float v = 0.f;
+    if ((unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W) v = x[(((int64_t)n * g.H + ih) * g.W + iw) * 3 + c];
+    band[i] = v;
+  }
+}
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+stem_f32_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w, int64_t s0, int64_t s1, int64_t s2,
+                    int64_t s3, float* __restrict__ y, StemF32Geo g, float* __restrict__ stats, int64_t stats_ld) {
+  extern __shared__ __attribute__((aligned(16))) float fl[];
+  float* band = fl;
+  float* wl = fl + kFBand;
+  int* kt = reinterpret_cast<int*>(wl + kFWg);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fi = lane & 15, fq = lane >> 4;
+  // weights [n][k], k = (kh * 7 + kw) * 3 + c, k = 147 zero
+  for (int i = threadIdx.x; i < kFWg; i += blockDim.x) {
+    const int n = i / kFKP, k = i - n * kFKP;
+    float v = 0.f;
+    if (k < kFK) {
+      const int kh = k / 21, r = k - kh * 21, kw = r / 3, c = r - kw * 3;
+      v = w[n * s0 + c * s1 + kh * s2 + kw * s3];
+    }
+    wl[i] = v;
+  }
+  koff_table(kt);
+  float ssum[4][4], ssq[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ssum[a][r] = ssq[a][r] = 0.f;
+  const int bpi = g.OH / kFR;   // bands per image
+  for (int b = blockIdx.x; b < g.nbands; b += gridDim.x) {
+    const int n = b / bpi, orow0 = (b - n * bpi) * kFR;
+    __syncthreads();   // the previous band's reads are done
+    load_band(band, x, g, n, orow0);
+    __syncthreads();
+    f32x4 acc[7][4];
+#pragma unroll
+    for (int t = 0; t < 7; ++t)
+#pragma unroll
+      for (int a = 0; a < 4; ++a) acc[t][a] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int pb[7];
+#pragma unroll
+    for (int t = 0; t < 7; ++t) pb[t] = (2 * wave * kFPW + 2 * (t * 16 + fi)) * 3;
+    for (int s = 0; s < kFKP / 4; ++s) {
+      const int ko = kt[4 * s + fq];
+      float bw[4], ax[7];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) bw[a] = wl[(a * 16 + fi) * kFKP + 4 * s + fq];
+#pragma unroll
+      for (int t = 0; t < 7; ++t) ax[t] = band[pb[t] + ko];
+#pragma unroll
+      for (int t = 0; t < 7; ++t)
+#pragma unroll
+        for (int a = 0; a < 4; ++a) acc[t][a] = __builtin_amdgcn_mfma_f32_16x16x4f32(bw[a], ax[t], acc[t][a], 0, 0, 0);
+    }
+    // lane: channels a * 16 + 4 fq + r of pixel t * 16 + fi of output row orow0 + wave
+    const int orow = orow0 + wave;
+#pragma unroll
+    for (int t = 0; t < 7; ++t) {
+      const int ocol = t * 16 + fi;
+      float* yp = y + (((int64_t)n * g.OH + orow) * g.OW + ocol) * 64;
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const f32x4 v = acc[t][a];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          ssum[a][r] += v[r];
+          ssq[a][r] = fmaf(v[r], v[r], ssq[a][r]);
+        }
+        *reinterpret_cast<f32x4*>(yp + a * 16 + 4 * fq) = v;
+      }
+    }
+  }
+  if (stats) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+          ssum[a][r] += __shfl_xor(ssum[a][r], off, 64);
+          ssq[a][r] += __shfl_xor(ssq[a][r], off, 64);
+        }
+    __syncthreads();
+    float* red = fl;   // [sum | sq][wave][64]
+    if (fi == 0) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          red[wave * 64 + a * 16 + 4 * fq + r] = ssum[a][r];
+          red[(4 + wave) * 64 + a * 16 + 4 * fq + r] = ssq[a][r];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      float sa = 0.f, sb = 0.f;
+#pragma unroll
+      for (int w2 = 0; w2 < 4; ++w2) {
+        sa += red[w2 * 64 + threadIdx.x];
+        sb += red[(4 + w2) * 64 + threadIdx.x];
+      }
+      stats[(int64_t)blockIdx.x * 64 + threadIdx.x] = sa;
+      stats[stats_ld + (int64_t)blockIdx.x * 64 + threadIdx.x] = sb;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+stem_f32_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ part,
+                      StemF32Geo g) {
+  extern __shared__ __attribute__((aligned(16))) float fl[];
+  float* band = fl;                                  // also the cross-wave reduction area [64][160]
+  int* kt = reinterpret_cast<int*>(fl + (kFBand > 64 * 160 ? kFBand : 64 * 160));
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fi = lane & 15, fq = lane >> 4;
+  koff_table(kt);
+  __syncthreads();
+  int ko[kFKS];
+#pragma unroll
+  for (int ks = 0; ks < kFKS; ++ks) ko[ks] = kt[ks * 16 + fi];
+  f32x4 acc[4][kFKS];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int ks = 0; ks < kFKS; ++ks) acc[a][ks] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int bpi = g.OH / kFR;
+  for (int b = blockIdx.x; b < g.nbands; b += gridDim.x) {
+    const int n = b / bpi, orow0 = (b - n * bpi) * kFR;
+    __syncthreads();
+    load_band(band, x, g, n, orow0);
+    __syncthreads();
+    const int orow = orow0 + wave;
+    const float* dyr = dy + (((int64_t)n * g.OH + orow) * g.OW) * 64;
+    for (int s = 0; s < kFOW / 4; ++s) {
+      const int ocol = 4 * s + fq;   // the pixel this lane's contraction slot holds
+      float ga[4], xb[kFKS];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) ga[a] = dyr[(int64_t)ocol * 64 + a * 16 + fi];
+      const int pb = (2 * wave * kFPW + 2 * ocol) * 3;
+#pragma unroll
+      for (int ks = 0; ks < kFKS; ++ks) xb[ks] = band[pb + ko[ks]];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int ks = 0; ks < kFKS; ++ks)
+          acc[a][ks] = __builtin_amdgcn_mfma_f32_16x16x4f32(ga[a], xb[ks], acc[a][ks], 0, 0, 0);
+    }
+  }
+  // lane: dW[n = a * 16 + 4 fq + r][k = ks * 16 + fi]; sum the 4 waves in order through LDS
+  float* red = fl;
+  for (int w2 = 0; w2 < 4; ++w2) {
+    __syncthreads();
+    if (wave == w2) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int ks = 0; ks < kFKS; ++ks)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float* p = red + (a * 16 + 4 * fq + r) * 160 + ks * 16 + fi;
+            *p = (w2 == 0 ? 0.f : *p) + acc[a][ks][r];
+          }
+    }
+  }
+  __syncthreads();
+  float* dst = part + (int64_t)blockIdx.x * 64 * kFKP;
+  for (int i = threadIdx.x; i < 64 * kFKP; i += blockDim.x) {
+    const int nn = i / kFKP, k = i - nn * kFKP;
+    dst[i] = red[nn * 160 + k];
+  }
+}
+
+// out[n][c][kh][kw] (strided fp32, the (arena) gradient) += sum over blocks
+__global__ void __launch_bounds__(256) stem_f32_wgrad_reduce_kernel(const float* __restrict__ part, int blocks,
+                                                                    float* __restrict__ out, int64_t s0, int64_t s1,
+                                                                    int64_t s2, int64_t s3) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= 64 * kFK) return;
+  const int n = i / kFK, k = i - n * kFK;
+  float s = 0.f;
+  for (int b = 0; b < blocks; ++b) s += part[((int64_t)b * 64 + n) * kFKP + k];
+  const int kh = k / 21, r = k - kh * 21, kw = r / 3, c = r - kw * 3;
+  out[n * s0 + c * s1 + kh * s2 + kw * s3] += s;
+}
+
+constexpr int kFFwdLds = (kFBand + kFWg) * 4 + 160 * 4;
+constexpr int kFWgLds = (kFBand > 64 * 160 ? kFBand : 64 * 160) * 4 + 160 * 4;
+
+}  // namespace
+
+bool stem_f32_supported(int H, int W) { return H == 224 && W == 224; }
+
+int stem_f32_wgrad_blocks(int N) { return N * (kFOW / kFR) < 512 ? N * (kFOW / kFR) : 512; }
+
+int stem_f32_forward(const float* x, int N, int H, int W, const float* w, int64_t s0, int64_t s1, int64_t s2,
+                     int64_t s3, float* y, float* stats, int stats_rows, hipStream_t stream) {
+  StemF32Geo g{N, H, W, kFOW, kFOW, N * (kFOW / kFR)};
+  int grid = g.nbands < 512 ? g.nbands : 512;
+  if (stats && grid > stats_rows) grid = stats_rows;
+  static bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_f32_fwd_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, kFFwdLds) == hipSuccess;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL(stem_f32_fwd_kernel, dim3((unsigned)grid), dim3(256), kFFwdLds, stream, x, w, s0, s1, s2, s3, y, g,
+                     stats, (int64_t)stats_rows * 64);
+  return grid;
+}
+
+void stem_f32_wgrad(const float* x, const float* dy, int N, int H, int W, float* part, float* out, int64_t s0,
+                    int64_t s1, int64_t s2, int64_t s3, hipStream_t stream) {
+  StemF32Geo g{N, H, W, kFOW, kFOW, N * (kFOW / kFR)};
+  const int grid = stem_f32_wgrad_blocks(N);
+  static bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_f32_wgrad_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, kFWgLds) == hipSuccess;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL(stem_f32_wgrad_kernel, dim3((unsigned)grid), dim3(256), kFWgLds, stream, x, dy, part, g);
+  hipLaunchKernelGGL(stem_f32_wgrad_reduce_kernel, dim3((64 * kFK + 255) / 256), dim3(256), 0, stream, part, grid, out,
+                     s0, s1, s2, s3);
+}
+
+}  // namespace gk

@@ -11,6 +11,9 @@ fp32 / bf16 image batch and bf16 autocast it runs:
 * backward: grad-weight only (the image needs no gradient) -- added into the
   optimizer's fp32 gradient arena on the bf16-shadow path, like FastConv2d.
 
+Without autocast (fp32 compute, the reference's precision) the fp32 kernels of
+``csrc/kernels/stem_f32.hip`` run instead (fp32 output and statistics).
+
 MIOpen's implicit GEMM handles the 3-channel input badly (0.7 ms per
 direction at bs512, profiles/r01_resnet50_conv_roofline_bs512.txt).
 Reference parity: the reference's ResNet-50 is torchvision's
@@ -28,6 +31,7 @@ from . import load
 
 _CL = torch.channels_last
 _ENABLED = os.environ.get("GKSGD_STEM", "1") != "0"
+_F32 = os.environ.get("GKSGD_STEM_F32", "1") != "0"   # fp32 stem kernels (else MIOpen at fp32)
 
 
 def _g():
@@ -77,6 +81,48 @@ class _StemFn(torch.autograd.Function):
         return None, gparam, None, None
 
 
+class _StemF32Fn(torch.autograd.Function):
+    """fp32 stem (csrc/kernels/stem_f32.hip): fp32 products and sums, the
+    reference's precision; grad-weight into the fp32 direct-gradient arena
+    when the model is on that path (parallel/shadow.py install_direct_grads)."""
+
+    @staticmethod
+    def forward(ctx, x, param, sink, stats_box):
+        g = _g()
+        N = x.shape[0]
+        y = torch.empty((N, 64, 112, 112), dtype=torch.float32, device=x.device, memory_format=_CL)
+        st = None
+        if stats_box is not None:
+            st = torch.empty(2, 512, 64, dtype=torch.float32, device=x.device)
+        rows = g.stem_f32_fwd(x, param.detach(), y, st)
+        if st is not None:
+            stats_box.append((st, int(rows)))
+        ctx.sink = sink
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        g = _g()
+        dy = dy.float().contiguous(memory_format=_CL)
+        gparam = None
+        if ctx.needs_input_grad[1]:
+            part = torch.empty(int(g.stem_f32_wgrad_ws(x.shape[0])), dtype=torch.float32, device=x.device)
+            sink = ctx.sink
+            if sink is not None and getattr(sink, "grad_view", None) is not None:
+                sink.check()
+                g.stem_f32_wgrad(x, dy, sink.grad_view, part)
+            else:
+                out = torch.zeros(64, 3, 7, 7, dtype=torch.float32, device=x.device)
+                g.stem_f32_wgrad(x, dy, out, part)
+                if sink is not None:
+                    sink(out)
+                else:
+                    gparam = out
+        return None, gparam, None, None
+
+
 class StemConv(nn.Conv2d):
     """``nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)`` with the
     gfx950 stem kernels on the training path."""
@@ -92,7 +138,21 @@ class StemConv(nn.Conv2d):
                 not (torch.is_grad_enabled() and x.requires_grad) and load() and
                 bool(_g().stem_supported(x.shape[2], x.shape[3])))
 
+    def _fast_f32(self, x: torch.Tensor) -> bool:
+        dev = x.device.type
+        return (_ENABLED and _F32 and x.is_cuda and x.dim() == 4 and x.shape[1] == 3 and self.out_channels == 64 and
+                x.dtype == torch.float32 and self.weight.dtype == torch.float32 and
+                x.is_contiguous(memory_format=_CL) and not torch.is_autocast_enabled(dev) and
+                not (torch.is_grad_enabled() and x.requires_grad) and load() and
+                bool(_g().stem_f32_supported(x.shape[2], x.shape[3])))
+
     def _run(self, x: torch.Tensor, box):
+        if self._fast_f32(x):
+            table = getattr(self, "_gk_direct_grads", None) or {}
+            sink = table.get("weight")
+            if not torch.is_grad_enabled() or not self.weight.requires_grad:
+                sink = None
+            return _StemF32Fn.apply(x, self.weight, sink, box)
         if self._fast(x):
             table = getattr(self, "_gk_shadow", None)
             info = table.get("weight") if table else None

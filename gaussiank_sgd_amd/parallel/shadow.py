@@ -146,14 +146,15 @@ def install_direct_grads(model: nn.Module, opt) -> int:
     fp32 weights, activations and gradients, settings.py:28): no shadow
     weights, but the hand-written kernels add their weight gradients straight
     into the optimizer's fp32 gradient arena -- FastConv2d's grad-weight GEMM
-    (ops/conv1x1.py fp32 path) and BNAct's backward (gamma / beta) -- so
+    (ops/conv1x1.py fp32 path), the fp32 stem (ops/stem.py) and BNAct's
+    backward (gamma / beta) -- so
     AccumulateGrad launches nothing for them.  Returns the number of
     parameters on the direct path."""
     arena = opt.arena
     names = opt._parameter_names
     count = 0
     for mod in model.modules():
-        if isinstance(mod, FastConv2d) and not isinstance(mod, StemConv):
+        if isinstance(mod, (FastConv2d, StemConv)):
             table = {}
             for pname in ("weight", "bias"):
                 p = getattr(mod, pname, None)

@@ -108,3 +108,76 @@ def test_resnet50_stem_bn_stats_match_pass():
     assert (out_a.float() - out_b.float()).abs().max().item() <= 2e-2
     assert torch.allclose(bn_a.running_mean, bn_b.running_mean, rtol=1e-4, atol=1e-5)
     assert torch.allclose(bn_a.running_var, bn_b.running_var, rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.parametrize("N", [1, 3])
+def test_stem_f32_fwd_stats_wgrad(N):
+    """fp32 stem kernels (stem_f32.hip) vs fp64 torch: output, BatchNorm
+    statistics partials, grad-weight accumulated into a strided target."""
+    import torch.nn.functional as F
+    from gaussiank_sgd_amd import ops
+    assert ops.load()
+    g = torch.ops.gksgd
+    torch.manual_seed(N)
+    CL = torch.channels_last
+    x = torch.randn(N, 3, 224, 224, device="cuda").contiguous(memory_format=CL)
+    w = torch.randn(64, 3, 7, 7, device="cuda") * 0.1
+    y = torch.full((N, 64, 112, 112), float("nan"), device="cuda").contiguous(memory_format=CL)
+    st = torch.full((2, 512, 64), float("nan"), device="cuda")
+    rows = g.stem_f32_fwd(x, w, y, st)
+    ref = F.conv2d(x.double(), w.double(), stride=2, padding=3)
+    bound = F.conv2d(x.double().abs(), w.double().abs(), stride=2, padding=3)
+    assert (y.double() - ref).abs().max().item() <= 2e-6 * bound.max().item() + 1e-6
+    s = st[:, :rows].double().sum(1)
+    yd = ref.permute(0, 2, 3, 1).reshape(-1, 64)
+    assert torch.allclose(s[0], yd.sum(0), rtol=1e-5, atol=1e-3)
+    assert torch.allclose(s[1], (yd * yd).sum(0), rtol=1e-5, atol=1e-3)
+    dy = torch.randn(N, 64, 112, 112, device="cuda").contiguous(memory_format=CL)
+    out0 = torch.randn(64, 3, 7, 7, device="cuda").contiguous(memory_format=CL)
+    out = out0.clone()
+    part = torch.empty(int(g.stem_f32_wgrad_ws(N)), device="cuda")
+    g.stem_f32_wgrad(x, dy, out, part)
+    gw = torch.ops.aten.convolution_backward(dy.double(), x.double(), w.double(), None, [2, 2], [3, 3], [1, 1], False,
+                                             [0, 0], 1, [False, True, False])[1]
+    gb = torch.ops.aten.convolution_backward(dy.double().abs(), x.double().abs(), w.double(), None, [2, 2], [3, 3],
+                                             [1, 1], False, [0, 0], 1, [False, True, False])[1]
+    assert (out.double() - out0.double() - gw).abs().max().item() <= 2e-6 * gb.max().item() + 1e-5
+
+
+def test_stem_conv_f32_autograd():
+    """StemConv at fp32 (no autocast) runs stem_f32 and matches fp64 torch."""
+    import torch.nn.functional as F
+    from gaussiank_sgd_amd.ops.stem import StemConv
+    torch.manual_seed(3)
+    CL = torch.channels_last
+    conv = StemConv().cuda()
+    x = torch.randn(2, 3, 224, 224, device="cuda").contiguous(memory_format=CL)
+    assert conv._fast_f32(x)
+    y = conv(x)
+    assert y.dtype == torch.float32
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    wd = conv.weight.detach().double().requires_grad_(True)
+    yd = F.conv2d(x.double(), wd, stride=2, padding=3)
+    yd.backward(dy.double())
+    assert (y.double() - yd).abs().max().item() <= 1e-5 * yd.abs().max().item() + 1e-5
+    assert (conv.weight.grad.double() - wd.grad).abs().max().item() <= 1e-5 * wd.grad.abs().max().item() + 1e-5
+
+
+def test_resnet50_stem_f32_bn_stats_match_pass():
+    """fp32 stem + fused BN/ReLU/max-pool fed by the stem's epilogue statistics
+    == the same BN running its own statistics pass."""
+    from gaussiank_sgd_amd.ops import stem
+    from gaussiank_sgd_amd.ops.bn import BNAct
+    torch.manual_seed(6)
+    conv = stem.StemConv().cuda().to(memory_format=CL)
+    bn_a = BNAct(64, act="relu", pool=(3, 2, 1)).cuda()
+    bn_b = BNAct(64, act="relu", pool=(3, 2, 1)).cuda()
+    x = torch.randn(2, 3, 224, 224, device="cuda").contiguous(memory_format=CL)
+    y, st = conv.forward_stats(x)
+    assert st is not None and y.dtype == torch.float32
+    out_a = bn_a(y, stats=st)
+    out_b = bn_b(y)
+    assert (out_a - out_b).abs().max().item() <= 1e-4
+    assert torch.allclose(bn_a.running_mean, bn_b.running_mean, rtol=1e-5, atol=1e-6)
+    assert torch.allclose(bn_a.running_var, bn_b.running_var, rtol=1e-5, atol=1e-6)
