@@ -43,6 +43,7 @@ constexpr int kKeyAbs = 0, kKeyHash = 1, kKeySample = 2;
 // the count pass as cheap as the reference ladder's 6
 constexpr int kCalCand = 8;
 constexpr int kHistSet = kRadixBins0 + kRadixBins1 + kRadixBins2;
+constexpr int kSyncCounters = 4;   // stats->finalize, count->decide, radix2->fallback key, cond count->decide
 
 struct Ws {
   double* partials;   // kMaxStatsBlocks * 4
@@ -51,9 +52,20 @@ struct Ws {
   int64_t* eqtake;    // kMaxCountBlocks
   int64_t* blocksel;  // kMaxCountBlocks
   uint32_t* hist;     // 2 * kHistSet (set 0: exact/hash, set 1: DGC sample)
+  uint32_t* sync;     // kSyncCounters arrival counters (last-block hand-off), zero between kernels
 };
 
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Partials handed from every block to a last-block reduction go through
+// device-coherent (agent-scope) accesses: they bypass the per-XCD L2s, so no
+// L2 write-back / invalidate fence is needed around the hand-off.
+template <typename T>
+__device__ __forceinline__ void st_dev(T* p, T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+template <typename T>
+__device__ __forceinline__ T ld_dev(const T* p) {
+  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 __host__ __device__ inline Ws carve(void* base) {
   char* p = reinterpret_cast<char*>(base);
@@ -64,7 +76,8 @@ __host__ __device__ inline Ws carve(void* base) {
   w.offsets = reinterpret_cast<int64_t*>(p + o); o = align_up(o + sizeof(int64_t) * kMaxCountBlocks, 256);
   w.eqtake = reinterpret_cast<int64_t*>(p + o); o = align_up(o + sizeof(int64_t) * kMaxCountBlocks, 256);
   w.blocksel = reinterpret_cast<int64_t*>(p + o); o = align_up(o + sizeof(int64_t) * kMaxCountBlocks, 256);
-  w.hist = reinterpret_cast<uint32_t*>(p + o);
+  w.hist = reinterpret_cast<uint32_t*>(p + o); o = align_up(o + sizeof(uint32_t) * 2 * kHistSet, 256);
+  w.sync = reinterpret_cast<uint32_t*>(p + o);
   return w;
 }
 
@@ -75,7 +88,8 @@ size_t ws_bytes() {
   o = align_up(o + sizeof(int64_t) * kMaxCountBlocks, 256) * 1;
   o = align_up(o + sizeof(int64_t) * kMaxCountBlocks, 256);
   o = align_up(o + sizeof(int64_t) * kMaxCountBlocks, 256);
-  o += sizeof(uint32_t) * 2 * kHistSet;
+  o = align_up(o + sizeof(uint32_t) * 2 * kHistSet, 256);
+  o += sizeof(uint32_t) * kSyncCounters;
   return align_up(o, 256);
 }
 
@@ -117,7 +131,7 @@ __device__ void radix_find(const uint32_t* hist, int nbins, int64_t kr, uint64_t
   const int t = threadIdx.x;
   const int hi = nbins - t * per;
   uint64_t ls = 0;
-  for (int q = 0; q < per; ++q) ls += hist[hi - 1 - q];
+  for (int q = 0; q < per; ++q) ls += ld_dev(&hist[hi - 1 - q]);
   uint64_t tot;
   const uint64_t before = block_excl_scan_u64(ls, sh, &tot);
   __shared__ int s_digit;
@@ -128,7 +142,7 @@ __device__ void radix_find(const uint32_t* hist, int nbins, int64_t kr, uint64_t
     int64_t cum = (int64_t)before;
     for (int q = 0; q < per; ++q) {
       const int d = hi - 1 - q;
-      const int64_t h = hist[d];
+      const int64_t h = ld_dev(&hist[d]);
       if (cum + h >= kr) { s_digit = d; s_kr = kr - cum; break; }
       cum += h;
     }
@@ -177,11 +191,71 @@ __device__ __forceinline__ void load4(const float* __restrict__ p, int64_t e, in
 }
 
 // --------------------------------------------------------------------------
-// K1+K2: residual add + moments
+// Last-block hand-off: every block publishes its partials, then counts itself
+// in; the block that arrives last runs the 1-workgroup reduction (finalize /
+// decide / fallback key) in place of a separate launch.  No block waits on
+// another (no spin), so there is no co-residency requirement.  The counter
+// is reset by the last block, ready for the next kernel that uses it.
 // --------------------------------------------------------------------------
-template <bool VEC, bool EC, bool WRITE_R, bool ZERO_G>
-__global__ __launch_bounds__(kBlock) void stats_kernel(float* __restrict__ g, float* __restrict__ r, int64_t n,
-                                                       double* __restrict__ partials) {
+// The partials are written with st_dev (device-coherent) and read with
+// ld_dev; each writer waits for its stores to complete before the block
+// counts itself in, so the last block reads every block's values.  (An
+// agent-scope release / acquire fence would instead write back / invalidate
+// the whole L2 of the XCD -- per block, that costs more than the launch it
+// saves.)
+__device__ __forceinline__ bool last_block(uint32_t* counter) {
+  __shared__ uint32_t s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's st_dev / atomics completed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = prev == gridDim.x - 1;
+    if (last) st_dev(counter, 0u);
+    s_last = last ? 1u : 0u;
+  }
+  __syncthreads();
+  return s_last != 0u;
+}
+
+struct FinArgs {   // finalize_body arguments (stats -> finalize hand-off)
+  GkCtrl* ctrl;
+  int64_t n;
+  int mode, loops;
+  double z, fixed_thr;
+  int64_t k;
+  float* stats_out;
+  uint32_t* counter;
+};
+
+struct DecArgs {   // decide_body arguments (count -> decide hand-off)
+  GkCtrl* ctrl;
+  int mode, loops;
+  int64_t k, k_cap;
+  int64_t* offsets;
+  int64_t* eqtake;
+  int64_t* blocksel;
+  int32_t* hdr;
+  uint32_t* hist_reset;
+  uint32_t* counter;
+};
+
+__device__ __forceinline__ void finalize_body(GkCtrl* __restrict__ ctrl, const double* __restrict__ partials, int nparts, int64_t n,
+                              int mode, int loops, double z, double fixed_thr, int64_t k, const uint32_t* hist_exact,
+                              const uint32_t* hist_sample, float* stats_out);
+__device__ __forceinline__ void decide_body(GkCtrl* __restrict__ ctrl, const uint32_t* __restrict__ blockcnt, int G, int mode,
+                            int loops, int64_t k, int64_t k_cap, int64_t* __restrict__ offsets,
+                            int64_t* __restrict__ eqtake, int64_t* __restrict__ blocksel, int32_t* __restrict__ hdr,
+                            int cond, uint32_t* __restrict__ hist_reset);
+__device__ __forceinline__ void cal_fallback_body(GkCtrl* __restrict__ ctrl, const uint32_t* hist_exact, int64_t k);
+
+// --------------------------------------------------------------------------
+// K1+K2: residual add + moments (FIN: + finalize in the last block)
+// --------------------------------------------------------------------------
+// (8 waves per SIMD: the rarely-run finalize call must not set the register
+// budget of this streaming kernel)
+template <bool VEC, bool EC, bool WRITE_R, bool ZERO_G, bool FIN>
+__global__ __launch_bounds__(kBlock, 8) void stats_kernel(float* __restrict__ g, float* __restrict__ r, int64_t n,
+                                                       double* __restrict__ partials, FinArgs fa) {
   float s = 0.f, ss = 0.f, sa = 0.f, mx = 0.f;
   const int64_t tid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * kBlock;
@@ -222,11 +296,14 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(float* __restrict__ g, fl
   const double bsa = block_sum((double)sa, sh);
   const float bmx = block_max(mx, shf);
   if (threadIdx.x == 0) {
-    partials[blockIdx.x * 4 + 0] = bs;
-    partials[blockIdx.x * 4 + 1] = bss;
-    partials[blockIdx.x * 4 + 2] = bsa;
-    partials[blockIdx.x * 4 + 3] = (double)bmx;
+    st_dev(&partials[blockIdx.x * 4 + 0], bs);
+    st_dev(&partials[blockIdx.x * 4 + 1], bss);
+    st_dev(&partials[blockIdx.x * 4 + 2], bsa);
+    st_dev(&partials[blockIdx.x * 4 + 3], (double)bmx);
   }
+  if (FIN && last_block(fa.counter))
+    finalize_body(fa.ctrl, partials, (int)gridDim.x, fa.n, fa.mode, fa.loops, fa.z, fa.fixed_thr, fa.k, nullptr,
+                  nullptr, fa.stats_out);
 }
 
 // DGC momentum correction fused into K1+K2: one pass reads u, g, w, r and
@@ -239,11 +316,12 @@ struct McHyper {
   float wd[8];
 };
 
-template <bool EC>
-__global__ __launch_bounds__(kBlock) void mc_stats_kernel(float* __restrict__ g, float* __restrict__ r,
+template <bool EC, bool FIN>
+__global__ __launch_bounds__(kBlock, 8) void mc_stats_kernel(float* __restrict__ g, float* __restrict__ r,
                                                           float* __restrict__ u, const float* __restrict__ w,
                                                           const Chunk* __restrict__ chunks, int nchunks,
-                                                          int64_t base, McHyper hp, double* __restrict__ partials) {
+                                                          int64_t base, McHyper hp, double* __restrict__ partials,
+                                                          FinArgs fa) {
   float s = 0.f, ss = 0.f, sa = 0.f, mx = 0.f;
   for (int ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
     const Chunk c = chunks[ci];
@@ -284,11 +362,14 @@ __global__ __launch_bounds__(kBlock) void mc_stats_kernel(float* __restrict__ g,
   const double bsa = block_sum((double)sa, sh);
   const float bmx = block_max(mx, shf);
   if (threadIdx.x == 0) {
-    partials[blockIdx.x * 4 + 0] = bs;
-    partials[blockIdx.x * 4 + 1] = bss;
-    partials[blockIdx.x * 4 + 2] = bsa;
-    partials[blockIdx.x * 4 + 3] = (double)bmx;
+    st_dev(&partials[blockIdx.x * 4 + 0], bs);
+    st_dev(&partials[blockIdx.x * 4 + 1], bss);
+    st_dev(&partials[blockIdx.x * 4 + 2], bsa);
+    st_dev(&partials[blockIdx.x * 4 + 3], (double)bmx);
   }
+  if (FIN && last_block(fa.counter))
+    finalize_body(fa.ctrl, partials, (int)gridDim.x, fa.n, fa.mode, fa.loops, fa.z, fa.fixed_thr, fa.k, nullptr,
+                  nullptr, fa.stats_out);
 }
 
 // --------------------------------------------------------------------------
@@ -301,12 +382,13 @@ __device__ __forceinline__ uint32_t radix_digit(uint32_t key) {
   return key & 0x3ffu;
 }
 
-template <int PASS, int KEYKIND, bool VEC>
+template <int PASS, int KEYKIND, bool VEC, bool FB = false>
 __global__ __launch_bounds__(kBlock) void radix_hist_kernel(const float* __restrict__ x, int64_t n, uint32_t seed,
                                                             uint32_t sample_thr, int64_t k, uint32_t* hist_set,
                                                             const uint32_t* __restrict__ valid,
-                                                            const GkCtrl* __restrict__ cond,
-                                                            const uint32_t* __restrict__ seed_dev) {
+                                                            GkCtrl* __restrict__ cond,
+                                                            const uint32_t* __restrict__ seed_dev,
+                                                            uint32_t* __restrict__ fb_counter = nullptr) {
   constexpr int NB = PASS == 0 ? kRadixBins0 : (PASS == 1 ? kRadixBins1 : kRadixBins2);
   __shared__ uint32_t sh_hist[kWavesPerBlock][NB];
   __shared__ uint64_t sh_scan[kWavesPerBlock];
@@ -319,7 +401,7 @@ __global__ __launch_bounds__(kBlock) void radix_hist_kernel(const float* __restr
   if (PASS >= 1) {
     // eligible total (DGC sample size) and k_eff
     uint64_t loc = 0;
-    for (int b = threadIdx.x; b < kRadixBins0; b += kBlock) loc += hist0[b];
+    for (int b = threadIdx.x; b < kRadixBins0; b += kBlock) loc += ld_dev(&hist0[b]);
     uint64_t tot;
     (void)block_excl_scan_u64(loc, sh_scan, &tot);
     int64_t kr = k < (int64_t)tot ? k : (int64_t)tot;
@@ -366,6 +448,8 @@ __global__ __launch_bounds__(kBlock) void radix_hist_kernel(const float* __restr
     const uint32_t c = sh_hist[0][b] + sh_hist[1][b] + sh_hist[2][b] + sh_hist[3][b];
     if (c) atomicAdd(&out[b], c);
   }
+  // conditional chain: the last block of pass 2 resolves the fallback key
+  if (FB && PASS == 2 && last_block(fb_counter)) cal_fallback_body(cond, hist_set, k);
 }
 
 // Derive the final key (k-th largest) and the tie quota from three hists.
@@ -375,7 +459,7 @@ __device__ void radix_resolve(const uint32_t* hist_set, int64_t k, uint64_t* sh,
   const uint32_t* hist1 = hist_set + kRadixBins0;
   const uint32_t* hist2 = hist1 + kRadixBins1;
   uint64_t loc = 0;
-  for (int b = threadIdx.x; b < kRadixBins0; b += kBlock) loc += hist0[b];
+  for (int b = threadIdx.x; b < kRadixBins0; b += kBlock) loc += ld_dev(&hist0[b]);
   uint64_t tot;
   (void)block_excl_scan_u64(loc, sh, &tot);
   int64_t keff = k < (int64_t)tot ? k : (int64_t)tot;
@@ -393,20 +477,19 @@ __device__ void radix_resolve(const uint32_t* hist_set, int64_t k, uint64_t* sh,
 // --------------------------------------------------------------------------
 // finalize: statistics + candidate ladder (1 workgroup)
 // --------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void finalize_kernel(GkCtrl* __restrict__ ctrl, const double* __restrict__ partials,
-                                                          int nparts, int64_t n, int mode, int loops, double z,
-                                                          double fixed_thr, int64_t k, const uint32_t* hist_exact,
-                                                          const uint32_t* hist_sample, float* stats_out) {
+__device__ __forceinline__ void finalize_body(GkCtrl* __restrict__ ctrl, const double* __restrict__ partials, int nparts, int64_t n,
+                              int mode, int loops, double z, double fixed_thr, int64_t k, const uint32_t* hist_exact,
+                              const uint32_t* hist_sample, float* stats_out) {
   __shared__ double sh[kWavesPerBlock];
   __shared__ float shf[kWavesPerBlock];
   __shared__ uint64_t sh_scan[kWavesPerBlock];
   double s = 0, ss = 0, sa = 0;
   float mx = 0.f;
   for (int b = threadIdx.x; b < nparts; b += kBlock) {
-    s += partials[b * 4 + 0];
-    ss += partials[b * 4 + 1];
-    sa += partials[b * 4 + 2];
-    mx = fmaxf(mx, (float)partials[b * 4 + 3]);
+    s += ld_dev(&partials[b * 4 + 0]);
+    ss += ld_dev(&partials[b * 4 + 1]);
+    sa += ld_dev(&partials[b * 4 + 2]);
+    mx = fmaxf(mx, (float)ld_dev(&partials[b * 4 + 3]));
   }
   s = block_sum(s, sh);
   ss = block_sum(ss, sh);
@@ -521,13 +604,19 @@ __global__ __launch_bounds__(kBlock) void finalize_kernel(GkCtrl* __restrict__ c
   ctrl->ref_total = -1;
 }
 
+__global__ __launch_bounds__(kBlock) void finalize_kernel(GkCtrl* __restrict__ ctrl, const double* __restrict__ partials,
+                                                          int nparts, int64_t n, int mode, int loops, double z,
+                                                          double fixed_thr, int64_t k, const uint32_t* hist_exact,
+                                                          const uint32_t* hist_sample, float* stats_out) {
+  finalize_body(ctrl, partials, nparts, n, mode, loops, z, fixed_thr, k, hist_exact, hist_sample, stats_out);
+}
+
 // Calibrated mode with no candidate in [2k/3, 4k/3] (k = k_eff), or a
 // threshold mode whose every candidate overflows k_cap (k = k_cap): resolve
 // the exact radix key (k-th largest |x|) from the conditional histogram
 // passes; the second count /
 // decide / select then run exactly as in top-k mode.
-__global__ __launch_bounds__(kBlock) void cal_fallback_kernel(GkCtrl* __restrict__ ctrl, const uint32_t* hist_exact,
-                                                              int64_t k) {
+__device__ __forceinline__ void cal_fallback_body(GkCtrl* __restrict__ ctrl, const uint32_t* hist_exact, int64_t k) {
   if (ctrl->fallback == 0) return;
   __shared__ uint64_t sh_scan[kWavesPerBlock];
   uint32_t key;
@@ -547,66 +636,126 @@ __global__ __launch_bounds__(kBlock) void cal_fallback_kernel(GkCtrl* __restrict
 // --------------------------------------------------------------------------
 // K4: one-pass multi-threshold count (counters in registers)
 // --------------------------------------------------------------------------
-template <int KEYKIND, bool VEC>
+template <int KEYKIND, bool VEC, int NC>
 __global__ __launch_bounds__(kBlock) void count_kernel(const float* __restrict__ x, int64_t n, uint32_t seed,
-                                                       const GkCtrl* __restrict__ ctrl, int64_t chunk_tiles,
+                                                       GkCtrl* __restrict__ ctrl, int64_t chunk_tiles,
                                                        uint32_t* __restrict__ blockcnt,
                                                        const uint32_t* __restrict__ valid, int cond,
-                                                       const uint32_t* __restrict__ seed_dev) {
+                                                       const uint32_t* __restrict__ seed_dev, DecArgs da) {
   if (cond && ctrl->fallback == 0) return;
   if (seed_dev != nullptr) seed = __builtin_amdgcn_readfirstlane(*seed_dev);
   // Wave-uniform counters: every (element, candidate) test is ONE v_cmp whose
   // 64-bit lane mask is popcounted and accumulated on the SCALAR unit
   // (s_bcnt1 + s_add), instead of a compare + conditional add per lane --
-  // half the VALU work, and no cross-lane reduction at the end.  Only the
-  // ncand live candidates are tested (uniform loop bound).
-  const int nc = __builtin_amdgcn_readfirstlane(ctrl->ncand);
-  uint32_t bnd[kMaxCand];
+  // no cross-lane reduction at the end.  NC (>= the live candidate count,
+  // chosen by the host from the mode) is a compile-time bound: no per-test
+  // branch; dead candidates carry bound 0xffffffff and count nothing.
+  uint32_t bnd[NC];
 #pragma unroll
-  for (int j = 0; j < kMaxCand; ++j) bnd[j] = __builtin_amdgcn_readfirstlane(ctrl->bound[j]);
-  uint32_t cnt[kMaxCand];
+  for (int j = 0; j < NC; ++j) bnd[j] = __builtin_amdgcn_readfirstlane(ctrl->bound[j]);
+  uint32_t cnt[NC];
 #pragma unroll
-  for (int j = 0; j < kMaxCand; ++j) cnt[j] = 0u;
+  for (int j = 0; j < NC; ++j) cnt[j] = 0u;
   const int64_t ntiles = (n + kTileElems - 1) / kTileElems;
   const int64_t t0 = (int64_t)blockIdx.x * chunk_tiles;
   const int64_t t1 = t0 + chunk_tiles < ntiles ? t0 + chunk_tiles : ntiles;
-  for (int64_t tile = t0; tile < t1; ++tile) {
-    const int64_t base = tile * kTileElems;
+  int64_t tile = t0;
+  if (VEC && KEYKIND != kKeyHash) {
+    // full tiles, next tile's four float4 in flight while this one is tested
+    const int64_t nfull = n / kTileElems;
+    const int64_t tf = t1 < nfull ? t1 : nfull;
+    if (tile < tf) {
+      const float4* p = reinterpret_cast<const float4*>(x) + threadIdx.x;
+      float4 nx[4];
 #pragma unroll
-    for (int j4 = 0; j4 < 4; ++j4) {
-      const int64_t e = base + j4 * (kBlock * 4) + threadIdx.x * 4;
-      float v[4] = {0.f, 0.f, 0.f, 0.f};
-      if (KEYKIND != kKeyHash) load4<VEC>(x, e, n, v);
+      for (int j4 = 0; j4 < 4; ++j4) nx[j4] = p[tile * (kTileElems / 4) + j4 * kBlock];
+      for (; tile < tf; ++tile) {
+        float4 cu[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const bool inb = e + q < n;
-        const uint32_t key = inb ? key_of<KEYKIND>(e + q, v[q], seed, valid) : 0u;
+        for (int j4 = 0; j4 < 4; ++j4) cu[j4] = nx[j4];
+        if (tile + 1 < tf) {
 #pragma unroll
-        for (int j = 0; j < kMaxCand; ++j)
-          if (j < nc) cnt[j] += (uint32_t)__popcll(__ballot(inb && key >= bnd[j]));
+          for (int j4 = 0; j4 < 4; ++j4) nx[j4] = p[(tile + 1) * (kTileElems / 4) + j4 * kBlock];
+        }
+#pragma unroll
+        for (int j4 = 0; j4 < 4; ++j4) {
+          const uint32_t k4[4] = {abs_key(cu[j4].x), abs_key(cu[j4].y), abs_key(cu[j4].z), abs_key(cu[j4].w)};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+#pragma unroll
+            for (int j = 0; j < NC; ++j) cnt[j] += (uint32_t)__popcll(__ballot(k4[q] >= bnd[j]));
+            __builtin_amdgcn_sched_barrier(0);   // accumulate per element: no SGPR spills
+          }
+        }
       }
     }
   }
-  __shared__ uint32_t sh[kWavesPerBlock][kMaxCand];
+  for (; tile < t1; ++tile) {
+    const int64_t base = tile * kTileElems;
+    uint32_t key[16];
+    uint32_t inb = 0xffffu;         // in-range bits of this thread's 16 elements
+    if (base + kTileElems <= n) {   // full tile (block-uniform): no bounds tests
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4) {
+        const int64_t e = base + j4 * (kBlock * 4) + threadIdx.x * 4;
+        float v[4] = {0.f, 0.f, 0.f, 0.f};
+        if (KEYKIND != kKeyHash) {
+          if (VEC) {
+            const float4 f = *reinterpret_cast<const float4*>(x + e);
+            v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+          } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = x[e + q];
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) key[j4 * 4 + q] = key_of<KEYKIND>(e + q, v[q], seed, valid);
+      }
+    } else {
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4) {
+        const int64_t e = base + j4 * (kBlock * 4) + threadIdx.x * 4;
+        float v[4] = {0.f, 0.f, 0.f, 0.f};
+        if (KEYKIND != kKeyHash) load4<VEC>(x, e, n, v);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const bool in = e + q < n;
+          key[j4 * 4 + q] = in ? key_of<KEYKIND>(e + q, v[q], seed, valid) : 0u;
+          if (!in) inb &= ~(1u << (j4 * 4 + q));
+        }
+      }
+    }
+    // no lane-divergent branch around the ballots: the counters are wave-uniform
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const bool in = (inb >> q) & 1u;
+#pragma unroll
+      for (int j = 0; j < NC; ++j) cnt[j] += (uint32_t)__popcll(__ballot(in && key[q] >= bnd[j]));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  __shared__ uint32_t sh[kWavesPerBlock][NC];
   if (lane_id() == 0) {
 #pragma unroll
-    for (int j = 0; j < kMaxCand; ++j) sh[wave_id()][j] = j < nc ? cnt[j] : 0u;
+    for (int j = 0; j < NC; ++j) sh[wave_id()][j] = cnt[j];
   }
   __syncthreads();
   if (threadIdx.x < kMaxCand) {
     const int j = threadIdx.x;
-    blockcnt[blockIdx.x * kMaxCand + j] = sh[0][j] + sh[1][j] + sh[2][j] + sh[3][j];
+    st_dev(&blockcnt[blockIdx.x * kMaxCand + j], j < NC ? sh[0][j] + sh[1][j] + sh[2][j] + sh[3][j] : 0u);
   }
+  if (last_block(da.counter))   // decide on the totals in the last block
+    decide_body(ctrl, blockcnt, (int)gridDim.x, da.mode, da.loops, da.k, da.k_cap, da.offsets, da.eqtake, da.blocksel,
+                da.hdr, cond, da.hist_reset);
 }
 
 // --------------------------------------------------------------------------
 // decide: replay the reference decision tree, offsets per block (1 WG)
 // --------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void decide_kernel(GkCtrl* __restrict__ ctrl, const uint32_t* __restrict__ blockcnt,
-                                                        int G, int mode, int loops, int64_t k, int64_t k_cap,
-                                                        int64_t* __restrict__ offsets, int64_t* __restrict__ eqtake,
-                                                        int64_t* __restrict__ blocksel, int32_t* __restrict__ hdr,
-                                                        int cond, uint32_t* __restrict__ hist_reset) {
+__device__ __forceinline__ void decide_body(GkCtrl* __restrict__ ctrl, const uint32_t* __restrict__ blockcnt, int G, int mode,
+                            int loops, int64_t k, int64_t k_cap, int64_t* __restrict__ offsets,
+                            int64_t* __restrict__ eqtake, int64_t* __restrict__ blocksel, int32_t* __restrict__ hdr,
+                            int cond, uint32_t* __restrict__ hist_reset) {
   __shared__ uint64_t sh_tot[kWavesPerBlock][kMaxCand];
   __shared__ uint64_t sh_scan[kWavesPerBlock];
   __shared__ int s_chosen, s_gt, s_ge, s_stop;
@@ -622,7 +771,7 @@ __global__ __launch_bounds__(kBlock) void decide_kernel(GkCtrl* __restrict__ ctr
   for (int j = 0; j < kMaxCand; ++j) loc[j] = 0;
   for (int b = threadIdx.x; b < G; b += kBlock) {
 #pragma unroll
-    for (int j = 0; j < kMaxCand; ++j) loc[j] += blockcnt[b * kMaxCand + j];
+    for (int j = 0; j < kMaxCand; ++j) loc[j] += ld_dev(&blockcnt[b * kMaxCand + j]);
   }
 #pragma unroll
   for (int j = 0; j < kMaxCand; ++j) {
@@ -750,8 +899,8 @@ __global__ __launch_bounds__(kBlock) void decide_kernel(GkCtrl* __restrict__ ctr
     const int b = threadIdx.x * kPer + q;
     gtc[q] = 0; eqc[q] = 0;
     if (b < G) {
-      gtc[q] = blockcnt[b * kMaxCand + gt];
-      if (ge >= 0) eqc[q] = (int64_t)blockcnt[b * kMaxCand + ge] - gtc[q];
+      gtc[q] = ld_dev(&blockcnt[b * kMaxCand + gt]);
+      if (ge >= 0) eqc[q] = (int64_t)ld_dev(&blockcnt[b * kMaxCand + ge]) - gtc[q];
     }
     eq_loc += eqc[q];
   }
@@ -903,17 +1052,46 @@ __global__ __launch_bounds__(kBlock) void select_kernel(float* __restrict__ r, i
   }
 }
 
+// live candidates of a count pass (finalize_kernel / cal_fallback_kernel ladders)
+int count_cands(const CompressArgs& a, int cond) {
+  if (cond) return 2;
+  switch (a.mode) {
+    case kModeGaussian: { const int l = a.loops < 1 ? 1 : a.loops; const int c = l * (l + 1) / 2;
+                          return c < kMaxCand ? c : kMaxCand; }
+    case kModeRedSync: return 7;
+    case kModeGaussianCal: return kCalCand;
+    case kModeThreshold: return 1;
+    case kModeTopK: case kModeRandomK: return 2;
+    case kModeDGC: return 3;
+    default: return kMaxCand;
+  }
+}
+
 template <int KEYKIND>
 void launch_count(const CompressArgs& a, const Ws& w, bool vec, int G, int64_t chunk_tiles, GkCtrl* ctrl, int cond,
                   hipStream_t s) {
-  if (vec)
-    hipLaunchKernelGGL((count_kernel<KEYKIND, true>), dim3(G), dim3(kBlock), 0, s, a.r, a.n, a.seed, ctrl,
-                       chunk_tiles, w.blockcnt, a.valid, cond, a.seed_dev);
-  else
-    hipLaunchKernelGGL((count_kernel<KEYKIND, false>), dim3(G), dim3(kBlock), 0, s, a.r, a.n, a.seed, ctrl,
-                       chunk_tiles, w.blockcnt, a.valid, cond, a.seed_dev);
-  hipLaunchKernelGGL(decide_kernel, dim3(1), dim3(kBlock), 0, s, ctrl, w.blockcnt, G, a.mode, a.loops, a.k,
-                     a.k_cap, w.offsets, w.eqtake, w.blocksel, a.record, cond, w.hist);
+  const int nc = count_cands(a, cond);
+  DecArgs da;
+  da.ctrl = ctrl; da.mode = a.mode; da.loops = a.loops; da.k = a.k; da.k_cap = a.k_cap;
+  da.offsets = w.offsets; da.eqtake = w.eqtake; da.blocksel = w.blocksel; da.hdr = a.record;
+  da.hist_reset = w.hist; da.counter = w.sync + (cond ? 3 : 1);
+#define GK_COUNT(NC)                                                                                              \
+  if (vec)                                                                                                        \
+    hipLaunchKernelGGL((count_kernel<KEYKIND, true, NC>), dim3(G), dim3(kBlock), 0, s, a.r, a.n, a.seed, ctrl,    \
+                       chunk_tiles, w.blockcnt, a.valid, cond, a.seed_dev, da);                                   \
+  else                                                                                                            \
+    hipLaunchKernelGGL((count_kernel<KEYKIND, false, NC>), dim3(G), dim3(kBlock), 0, s, a.r, a.n, a.seed, ctrl,   \
+                       chunk_tiles, w.blockcnt, a.valid, cond, a.seed_dev, da);
+  if constexpr (KEYKIND == kKeyHash) {
+    GK_COUNT(2)
+  } else {
+    if (nc <= 2) { GK_COUNT(2) }
+    else if (nc <= 3) { GK_COUNT(3) }
+    else if (nc <= 6) { GK_COUNT(6) }
+    else if (nc <= 8) { GK_COUNT(8) }
+    else { GK_COUNT(kMaxCand) }
+  }
+#undef GK_COUNT
 }
 
 template <int KEYKIND>
@@ -929,9 +1107,12 @@ void launch_select(const CompressArgs& a, const Ws& w, bool vec, int G, int64_t 
                        a.seed_dev);
 }
 
+// fb_counter != nullptr: conditional fallback chain (cond != nullptr), pass 2
+// resolves the fallback key in its last block
 template <int KEYKIND>
 void launch_radix(const float* x, int64_t n, uint32_t seed, uint32_t sample_thr, int64_t k, uint32_t* set, bool vec,
-                  const uint32_t* valid, const GkCtrl* cond, const uint32_t* seed_dev, hipStream_t s) {
+                  const uint32_t* valid, GkCtrl* cond, const uint32_t* seed_dev, hipStream_t s,
+                  uint32_t* fb_counter = nullptr) {
   const int64_t n4 = (n + 3) / 4;
   int Gh = (int)ceil_div(n4, (int64_t)kBlock * 8);
   if (Gh < 1) Gh = 1;
@@ -945,7 +1126,16 @@ void launch_radix(const float* x, int64_t n, uint32_t seed, uint32_t sample_thr,
                        sample_thr, k, set, valid, cond, seed_dev);
   GK_RADIX_PASS(0)
   GK_RADIX_PASS(1)
-  GK_RADIX_PASS(2)
+  if (fb_counter != nullptr) {
+    if (vec)
+      hipLaunchKernelGGL((radix_hist_kernel<2, KEYKIND, true, true>), dim3(Gh), dim3(kBlock), 0, s, x, n, seed,
+                         sample_thr, k, set, valid, cond, seed_dev, fb_counter);
+    else
+      hipLaunchKernelGGL((radix_hist_kernel<2, KEYKIND, false, true>), dim3(Gh), dim3(kBlock), 0, s, x, n, seed,
+                         sample_thr, k, set, valid, cond, seed_dev, fb_counter);
+  } else {
+    GK_RADIX_PASS(2)
+  }
 #undef GK_RADIX_PASS
 }
 
@@ -966,7 +1156,14 @@ void compress(const CompressArgs& a, hipStream_t s) {
   const bool vec_r = (reinterpret_cast<uintptr_t>(a.r) & 15) == 0 && (a.n % 4) == 0;
 
   // 1. stats (+ residual add, residual write, gradient zeroing; + DGC momentum
-  //    correction when a chunk table is given)
+  //    correction when a chunk table is given); threshold modes finalize in
+  //    the last stats block (radix modes need the histograms first)
+  const bool radix_mode = a.mode == kModeTopK || a.mode == kModeRandomK || a.mode == kModeDGC;
+  const int64_t keff = a.k < a.n ? a.k : a.n;
+  const int64_t n_stats = a.n_stats > 0 ? a.n_stats : a.n;
+  FinArgs fa;
+  fa.ctrl = ctrl; fa.n = n_stats; fa.mode = a.mode; fa.loops = a.loops; fa.z = a.z; fa.fixed_thr = a.fixed_thr;
+  fa.k = keff; fa.stats_out = a.stats_out; fa.counter = w.sync + 0;
   int Gs;
   if (a.u != nullptr && a.chunks != nullptr) {
     Gs = a.chunk_count < kMaxStatsBlocks ? a.chunk_count : kMaxStatsBlocks;
@@ -974,18 +1171,21 @@ void compress(const CompressArgs& a, hipStream_t s) {
     McHyper hp;
     for (int i = 0; i < 8; ++i) { hp.mu[i] = a.mc_mu[i]; hp.wd[i] = a.mc_wd[i]; }
     const Chunk* ch = a.chunks + a.chunk_begin;
-    if (a.ec)
-      hipLaunchKernelGGL((mc_stats_kernel<true>), dim3(Gs), dim3(kBlock), 0, s, a.g, a.r, a.u, a.w, ch,
-                         a.chunk_count, a.chunk_base, hp, w.partials);
-    else
-      hipLaunchKernelGGL((mc_stats_kernel<false>), dim3(Gs), dim3(kBlock), 0, s, a.g, a.r, a.u, a.w, ch,
-                         a.chunk_count, a.chunk_base, hp, w.partials);
+#define GK_MC(EC, FIN)                                                                                            \
+  hipLaunchKernelGGL((mc_stats_kernel<EC, FIN>), dim3(Gs), dim3(kBlock), 0, s, a.g, a.r, a.u, a.w, ch,             \
+                     a.chunk_count, a.chunk_base, hp, w.partials, fa);
+    if (a.ec) { if (radix_mode) { GK_MC(true, false) } else { GK_MC(true, true) } }
+    else { if (radix_mode) { GK_MC(false, false) } else { GK_MC(false, true) } }
+#undef GK_MC
   } else {
     Gs = (int)ceil_div(a.n, (int64_t)kBlock * 16);
     if (Gs < 1) Gs = 1;
     if (Gs > kMaxStatsBlocks) Gs = kMaxStatsBlocks;
+#define GK_STATS2(VEC, EC, ZG, FIN)                                                                               \
+  hipLaunchKernelGGL((stats_kernel<VEC, EC, true, ZG, FIN>), dim3(Gs), dim3(kBlock), 0, s, a.g, a.r, a.n,          \
+                     w.partials, fa);
 #define GK_STATS(VEC, EC, ZG)                                                                                     \
-  hipLaunchKernelGGL((stats_kernel<VEC, EC, true, ZG>), dim3(Gs), dim3(kBlock), 0, s, a.g, a.r, a.n, w.partials);
+  if (radix_mode) { GK_STATS2(VEC, EC, ZG, false) } else { GK_STATS2(VEC, EC, ZG, true) }
     if (vec_gr) {
       if (a.ec) { if (a.zero_g) { GK_STATS(true, true, true) } else { GK_STATS(true, true, false) } }
       else { if (a.zero_g) { GK_STATS(true, false, true) } else { GK_STATS(true, false, false) } }
@@ -994,13 +1194,13 @@ void compress(const CompressArgs& a, hipStream_t s) {
       else { if (a.zero_g) { GK_STATS(false, false, true) } else { GK_STATS(false, false, false) } }
     }
 #undef GK_STATS
+#undef GK_STATS2
   }
 
   // 2. radix histograms (exact / hash / sample)
   uint32_t* hist_exact = w.hist;
   uint32_t* hist_sample = w.hist + kHistSet;
-  const int64_t keff = a.k < a.n ? a.k : a.n;
-  if (a.mode == kModeTopK || a.mode == kModeRandomK || a.mode == kModeDGC) {
+  if (radix_mode) {
     hipMemsetAsync(w.hist, 0, sizeof(uint32_t) * 2 * kHistSet, s);
     if (a.mode == kModeRandomK)
       launch_radix<kKeyHash>(a.r, a.n, a.seed, 0u, keff, hist_exact, vec_r, a.valid, nullptr, a.seed_dev, s);
@@ -1013,12 +1213,12 @@ void compress(const CompressArgs& a, hipStream_t s) {
     }
   }
 
-  // 3. finalize
-  const int64_t n_stats = a.n_stats > 0 ? a.n_stats : a.n;
-  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(kBlock), 0, s, ctrl, w.partials, Gs, n_stats, a.mode, a.loops, a.z,
-                     a.fixed_thr, keff, hist_exact, hist_sample, a.stats_out);
+  // 3. finalize (radix modes; the threshold modes finalized in the stats pass)
+  if (radix_mode)
+    hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(kBlock), 0, s, ctrl, w.partials, Gs, n_stats, a.mode, a.loops,
+                       a.z, a.fixed_thr, keff, hist_exact, hist_sample, a.stats_out);
 
-  // 4-6. count, decide, select
+  // 4-6. count (+ decide in its last block), select
   const int64_t ntiles = ceil_div(a.n, (int64_t)kTileElems);
   int G = (int)(ntiles < kMaxCountBlocks ? ntiles : kMaxCountBlocks);
   const int64_t chunk_tiles = ceil_div(ntiles, (int64_t)G);
@@ -1034,8 +1234,7 @@ void compress(const CompressArgs& a, hipStream_t s) {
       // candidate in [2k/3, 4k/3] (top-k), or a threshold mode whose every
       // candidate overflows k_cap (top-k_cap)
       const int64_t kfb = a.mode == kModeGaussianCal ? keff : (a.k_cap < a.n ? a.k_cap : a.n);
-      launch_radix<kKeyAbs>(a.r, a.n, a.seed, 0u, kfb, hist_exact, vec_r, nullptr, ctrl, a.seed_dev, s);
-      hipLaunchKernelGGL(cal_fallback_kernel, dim3(1), dim3(kBlock), 0, s, ctrl, hist_exact, kfb);
+      launch_radix<kKeyAbs>(a.r, a.n, a.seed, 0u, kfb, hist_exact, vec_r, nullptr, ctrl, a.seed_dev, s, w.sync + 2);
       launch_count<kKeyAbs>(a, w, vec_r, G, chunk_tiles, ctrl, 1, s);
     }
     launch_select<kKeyAbs>(a, w, vec_r, G, chunk_tiles, ctrl, out_idx, out_val, s);
@@ -1050,9 +1249,11 @@ void tensor_stats(const float* x, int64_t n, void* ctrl, void* ws, hipStream_t s
   float* xx = const_cast<float*>(x);
   const bool vec = (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (n % 4) == 0;
   if (vec)
-    hipLaunchKernelGGL((stats_kernel<true, false, false, false>), dim3(Gs), dim3(kBlock), 0, s, xx, xx, n, w.partials);
+    hipLaunchKernelGGL((stats_kernel<true, false, false, false, false>), dim3(Gs), dim3(kBlock), 0, s, xx, xx, n,
+                       w.partials, FinArgs{});
   else
-    hipLaunchKernelGGL((stats_kernel<false, false, false, false>), dim3(Gs), dim3(kBlock), 0, s, xx, xx, n, w.partials);
+    hipLaunchKernelGGL((stats_kernel<false, false, false, false, false>), dim3(Gs), dim3(kBlock), 0, s, xx, xx, n,
+                       w.partials, FinArgs{});
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(kBlock), 0, s, reinterpret_cast<GkCtrl*>(ctrl), w.partials, Gs, n,
                      (int)kModeThreshold, 1, 0.0, 0.0, (int64_t)1, w.hist, w.hist, (float*)nullptr);
 }
