@@ -910,8 +910,9 @@ void stem_wgrad(at::Tensor x, at::Tensor dy, at::Tensor out, at::Tensor part) {
 // y [N, 64, 112, 112] channels-last fp32
 int64_t stem_f32_fwd(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tensor> stats) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.dim() == 4 && x.size(1) == 3 &&
-                  x.is_contiguous(at::MemoryFormat::ChannelsLast) && gk::stem_f32_supported((int)x.size(2), (int)x.size(3)),
-              "stem_f32_fwd: x must be a channels-last fp32 [N, 3, 224, 224] GPU tensor");
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast) && gk::stem_f32_supported((int)x.size(2), (int)x.size(3)) &&
+                  reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "stem_f32_fwd: x must be a channels-last fp32 [N, 3, 224, 224] GPU tensor (16-byte aligned)");
   TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.dim() == 4 && w.size(0) == 64 && w.size(1) == 3 &&
                   w.size(2) == 7 && w.size(3) == 7, "stem_f32_fwd: w must be fp32 [64, 3, 7, 7]");
   const int64_t N = x.size(0);
@@ -930,8 +931,9 @@ int64_t stem_f32_wgrad_ws(int64_t N) { return (int64_t)gk::stem_f32_wgrad_blocks
 
 void stem_f32_wgrad(at::Tensor x, at::Tensor dy, at::Tensor out, at::Tensor part) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.dim() == 4 && x.size(1) == 3 &&
-                  x.is_contiguous(at::MemoryFormat::ChannelsLast) && gk::stem_f32_supported((int)x.size(2), (int)x.size(3)),
-              "stem_f32_wgrad: x must be a channels-last fp32 [N, 3, 224, 224] GPU tensor");
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast) && gk::stem_f32_supported((int)x.size(2), (int)x.size(3)) &&
+                  reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "stem_f32_wgrad: x must be a channels-last fp32 [N, 3, 224, 224] GPU tensor (16-byte aligned)");
   const int64_t N = x.size(0);
   TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kFloat && dy.dim() == 4 && dy.size(0) == N &&
                   dy.size(1) == 64 && dy.size(2) == 112 && dy.size(3) == 112 &&

@@ -7,8 +7,8 @@
 //
 // K = 7 x 7 x 3 = 147 taps, ordered (kh, kw, c) like the NHWC input, padded to
 // 148; a tap's offset inside an LDS input band is koff(k) = (kh * PW + kw) * 3
-// + c (koff table in LDS), so an MFMA operand element is one ds_read_b32 at
-// pixel_base + koff.
+// + c (tap_off, computed per k-step), so an MFMA operand element is one
+// ds_read_b32 at pixel_base + koff.
 //
 // forward: a persistent block walks bands of 4 output rows of one image; the
 //   band's 13 input rows (zero padding materialised, 230 pixels x 3 channels)
@@ -47,29 +47,33 @@ struct StemF32Geo {
   int N, H, W, OH, OW, nbands;   // nbands = N * OH / kFR
 };
 
-__device__ __forceinline__ void koff_table(int* kt) {
-  for (int k = threadIdx.x; k < 16 * kFKS; k += blockDim.x) {
-    int v = 0;
-    if (k < kFK) {
-      const int kh = k / 21, r = k - kh * 21, kw = r / 3, c = r - kw * 3;
-      v = (kh * kFPW + kw) * 3 + c;
-    }
-    kt[k] = v;   // padded taps read any in-band value: their weight is 0 / their gradient is dropped
+// input rows 2 orow0 - 3 .. + 12 of image n, columns -3 .. 226, zero outside.
+// An NHWC image row is 224 x 3 contiguous floats (16-byte aligned: 2688 B),
+// copied as float4; the 3-pixel borders are zero.
+__device__ __forceinline__ void load_band(float* band, const float* __restrict__ x, const StemF32Geo& g, int n,
+                                          int orow0) {
+  constexpr int RV = 2 * kFOW * 3 / 4;   // float4 per input row
+  constexpr int RW = kFPW * 3;           // floats per band row
+  const int ih0 = 2 * orow0 - 3;
+  for (int i = threadIdx.x; i < kFIn * RV; i += blockDim.x) {
+    const int rr = i / RV, j = i - rr * RV;
+    const int ih = ih0 + rr;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if ((unsigned)ih < (unsigned)g.H) v = reinterpret_cast<const float4*>(x + ((int64_t)n * g.H + ih) * g.W * 3)[j];
+    float* d = band + rr * RW + 9 + 4 * j;
+    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+  }
+  for (int i = threadIdx.x; i < kFIn * 18; i += blockDim.x) {
+    const int rr = i / 18, j = i - rr * 18;
+    band[rr * RW + (j < 9 ? j : RW - 18 + j)] = 0.f;
   }
 }
 
-// input rows 2 orow0 - 3 .. + 12 of image n, columns -3 .. 226, zero outside
-__device__ __forceinline__ void load_band(float* band, const float* __restrict__ x, const StemF32Geo& g, int n,
-                                          int orow0) {
-  const int ih0 = 2 * orow0 - 3;
-  for (int i = threadIdx.x; i < kFBand; i += blockDim.x) {
-    const int rr = i / (kFPW * 3), rem = i - rr * (kFPW * 3);
-    const int pc = rem / 3, c = rem - pc * 3;
-    const int ih = ih0 + rr, iw = pc - 3;
-    float v = 0.f;
-    if ((unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W) v = x[(((int64_t)n * g.H + ih) * g.W + iw) * 3 + c];
-    band[i] = v;
-  }
+// LDS offset of tap k inside the band (koff table, computed: one fewer LDS
+// round trip per k-step); the padded tap 147 reads offset 0 (weight 0)
+__device__ __forceinline__ int tap_off(int k) {
+  const int kh = k / 21, r = k - kh * 21, kw = r / 3, c = r - kw * 3;
+  return k < kFK ? (kh * kFPW + kw) * 3 + c : 0;
 }
 
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
@@ -78,7 +82,6 @@ stem_f32_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w, in
   extern __shared__ __attribute__((aligned(16))) float fl[];
   float* band = fl;
   float* wl = fl + kFBand;
-  int* kt = reinterpret_cast<int*>(wl + kFWg);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fi = lane & 15, fq = lane >> 4;
   // weights [n][k], k = (kh * 7 + kw) * 3 + c, k = 147 zero
@@ -91,7 +94,6 @@ stem_f32_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w, in
     }
     wl[i] = v;
   }
-  koff_table(kt);
   float ssum[4][4], ssq[4][4];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
@@ -111,17 +113,28 @@ stem_f32_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w, in
     int pb[7];
 #pragma unroll
     for (int t = 0; t < 7; ++t) pb[t] = (2 * wave * kFPW + 2 * (t * 16 + fi)) * 3;
-    for (int s = 0; s < kFKP / 4; ++s) {
-      const int ko = kt[4 * s + fq];
-      float bw[4], ax[7];
+    // operands of k-step s + 1 read while the 28 MFMAs of step s run
+    auto ldop = [&](int st, float (&bwv)[4], float (&axv)[7]) __attribute__((always_inline)) {
+      const int k = 4 * st + fq;
+      const int ko = tap_off(k);
 #pragma unroll
-      for (int a = 0; a < 4; ++a) bw[a] = wl[(a * 16 + fi) * kFKP + 4 * s + fq];
+      for (int a = 0; a < 4; ++a) bwv[a] = wl[(a * 16 + fi) * kFKP + k];
 #pragma unroll
-      for (int t = 0; t < 7; ++t) ax[t] = band[pb[t] + ko];
+      for (int t = 0; t < 7; ++t) axv[t] = band[pb[t] + ko];
+    };
+    float bw[4], ax[7];
+    ldop(0, bw, ax);
+    for (int st = 0; st < kFKP / 4; ++st) {
+      float bn[4], an[7];
+      if (st + 1 < kFKP / 4) ldop(st + 1, bn, an);
 #pragma unroll
       for (int t = 0; t < 7; ++t)
 #pragma unroll
         for (int a = 0; a < 4; ++a) acc[t][a] = __builtin_amdgcn_mfma_f32_16x16x4f32(bw[a], ax[t], acc[t][a], 0, 0, 0);
+#pragma unroll
+      for (int a = 0; a < 4; ++a) bw[a] = bn[a];
+#pragma unroll
+      for (int t = 0; t < 7; ++t) ax[t] = an[t];
     }
     // lane: channels a * 16 + 4 fq + r of pixel t * 16 + fi of output row orow0 + wave
     const int orow = orow0 + wave;
@@ -181,14 +194,11 @@ stem_f32_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy,
                       StemF32Geo g) {
   extern __shared__ __attribute__((aligned(16))) float fl[];
   float* band = fl;                                  // also the cross-wave reduction area [64][160]
-  int* kt = reinterpret_cast<int*>(fl + (kFBand > 64 * 160 ? kFBand : 64 * 160));
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fi = lane & 15, fq = lane >> 4;
-  koff_table(kt);
-  __syncthreads();
   int ko[kFKS];
 #pragma unroll
-  for (int ks = 0; ks < kFKS; ++ks) ko[ks] = kt[ks * 16 + fi];
+  for (int ks = 0; ks < kFKS; ++ks) ko[ks] = tap_off(ks * 16 + fi);   // taps >= 147: gradient dropped
   f32x4 acc[4][kFKS];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
@@ -202,19 +212,30 @@ stem_f32_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy,
     __syncthreads();
     const int orow = orow0 + wave;
     const float* dyr = dy + (((int64_t)n * g.OH + orow) * g.OW) * 64;
-    for (int s = 0; s < kFOW / 4; ++s) {
-      const int ocol = 4 * s + fq;   // the pixel this lane's contraction slot holds
-      float ga[4], xb[kFKS];
+    // dY (global) and A (LDS) fragments of pixel step s + 1 in flight while
+    // the 40 MFMAs of step s run
+    auto ldop = [&](int st, float (&gav)[4], float (&xbv)[kFKS]) __attribute__((always_inline)) {
+      const int ocol = 4 * st + fq;   // the pixel this lane's contraction slot holds
 #pragma unroll
-      for (int a = 0; a < 4; ++a) ga[a] = dyr[(int64_t)ocol * 64 + a * 16 + fi];
+      for (int a = 0; a < 4; ++a) gav[a] = dyr[(int64_t)ocol * 64 + a * 16 + fi];
       const int pb = (2 * wave * kFPW + 2 * ocol) * 3;
 #pragma unroll
-      for (int ks = 0; ks < kFKS; ++ks) xb[ks] = band[pb + ko[ks]];
+      for (int ks = 0; ks < kFKS; ++ks) xbv[ks] = band[pb + ko[ks]];
+    };
+    float ga[4], xb[kFKS];
+    ldop(0, ga, xb);
+    for (int st = 0; st < kFOW / 4; ++st) {
+      float gn[4], xn[kFKS];
+      if (st + 1 < kFOW / 4) ldop(st + 1, gn, xn);
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int ks = 0; ks < kFKS; ++ks)
           acc[a][ks] = __builtin_amdgcn_mfma_f32_16x16x4f32(ga[a], xb[ks], acc[a][ks], 0, 0, 0);
+#pragma unroll
+      for (int a = 0; a < 4; ++a) ga[a] = gn[a];
+#pragma unroll
+      for (int ks = 0; ks < kFKS; ++ks) xb[ks] = xn[ks];
     }
   }
   // lane: dW[n = a * 16 + 4 fq + r][k = ks * 16 + fi]; sum the 4 waves in order through LDS
@@ -254,8 +275,8 @@ __global__ void __launch_bounds__(256) stem_f32_wgrad_reduce_kernel(const float*
   out[n * s0 + c * s1 + kh * s2 + kw * s3] += s;
 }
 
-constexpr int kFFwdLds = (kFBand + kFWg) * 4 + 160 * 4;
-constexpr int kFWgLds = (kFBand > 64 * 160 ? kFBand : 64 * 160) * 4 + 160 * 4;
+constexpr int kFFwdLds = (kFBand + kFWg) * 4;
+constexpr int kFWgLds = (kFBand > 64 * 160 ? kFBand : 64 * 160) * 4;
 
 }  // namespace
 

@@ -142,9 +142,9 @@ class StemConv(nn.Conv2d):
         dev = x.device.type
         return (_ENABLED and _F32 and x.is_cuda and x.dim() == 4 and x.shape[1] == 3 and self.out_channels == 64 and
                 x.dtype == torch.float32 and self.weight.dtype == torch.float32 and
-                x.is_contiguous(memory_format=_CL) and not torch.is_autocast_enabled(dev) and
-                not (torch.is_grad_enabled() and x.requires_grad) and load() and
-                bool(_g().stem_f32_supported(x.shape[2], x.shape[3])))
+                x.is_contiguous(memory_format=_CL) and x.data_ptr() % 16 == 0 and
+                not torch.is_autocast_enabled(dev) and not (torch.is_grad_enabled() and x.requires_grad) and
+                load() and bool(_g().stem_f32_supported(x.shape[2], x.shape[3])))
 
     def _run(self, x: torch.Tensor, box):
         if self._fast_f32(x):
