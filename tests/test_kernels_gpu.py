@@ -456,3 +456,28 @@ def test_rccl_engine_failure_races_enqueue(cuda):
         e.allgather(t, out)
     e.stop_watchdog()
     e.destroy()
+
+
+@pytest.mark.parametrize("mode", [ops.MODE_GAUSSIAN, ops.MODE_GAUSSIAN_CAL, ops.MODE_TOPK])
+def test_compress_reused_buffers_varying_sizes(cuda, mode):
+    """One CompressBuffers pair reused across buckets of different sizes (grid
+    sizes): the last-block hand-off counters (stats -> finalize, count ->
+    decide, radix -> fallback key) must be back at zero after every call, so
+    each record equals the CPU mirror's."""
+    k_cap = 3000
+    gb, rb = ops.CompressBuffers(k_cap, cuda), ops.CompressBuffers(k_cap, "cpu")
+    for i, n in enumerate([1_200_000, 5_000, 300_007 * 4, 64, 1_200_000]):
+        x, r = _pair(n, seed=31 + i)
+        k = max(int(n * 0.001), 1)
+        xg, rg = x.clone().to(cuda), r.clone().to(cuda)
+        xc, rc = x.clone(), r.clone()
+        for g_, r_, b_ in ((xg, rg, gb), (xc, rc, rb)):
+            ops.compress_(g_, r_, b_, mode, ec=True, zero_g=True, loops=3, z=gaussian_z(0.001), k=k, k_cap=k_cap,
+                          seed=5)
+        torch.cuda.synchronize()
+        recg = gb.record.cpu()
+        sg, tg, ig, vg = _sel(recg, k_cap)
+        sc, tc, ic, vc = _sel(rb.record, k_cap)
+        assert (sg, tg) == (sc, tc), (n, mode, sg, tg, sc, tc)
+        assert torch.equal(ig, ic) and torch.equal(vg, vc)
+        assert torch.equal(rg.cpu(), rc)
