@@ -1161,8 +1161,12 @@ void bn_relu_pool_forward(const void* x, void* y, uint8_t* amax, int64_t N, int 
   } else {
     bn_stats_t<float>((const float*)x, M, C, w, b, eps, momentum, run_mean, run_var, save_mean, save_invstd, scale,
                        shift, ws, nbt, s);
-    hipLaunchKernelGGL(bn_relu_pool_kernel<float>, grid, dim3(kBlock), 0, s, (const float*)x, (float*)y, amax, P, C, pg,
-                       scale, shift);
+    if (pg.k == 3 && pg.p == 1)   // all 9 window loads in flight
+      hipLaunchKernelGGL((bn_relu_pool_kernel<float, 3>), grid, dim3(kBlock), 0, s, (const float*)x, (float*)y, amax, P,
+                         C, pg, scale, shift);
+    else
+      hipLaunchKernelGGL(bn_relu_pool_kernel<float>, grid, dim3(kBlock), 0, s, (const float*)x, (float*)y, amax, P, C,
+                         pg, scale, shift);
   }
 }
 
@@ -1178,7 +1182,10 @@ void bn_relu_pool_forward_pre(const void* x, void* y, uint8_t* amax, int64_t N, 
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(kBlock), 0, s, psum, psq, gy, M, C, w, b,
                      eps, momentum, run_mean, run_var, save_mean, save_invstd, scale, shift, nbt);
   const dim3 grid((unsigned)((threads + kBlock - 1) / kBlock));
-  if (elem_bytes == 4)
+  if (elem_bytes == 4 && pg.k == 3 && pg.p == 1)
+    hipLaunchKernelGGL((bn_relu_pool_kernel<float, 3>), grid, dim3(kBlock), 0, s, (const float*)x, (float*)y, amax, P, C,
+                       pg, scale, shift);
+  else if (elem_bytes == 4)
     hipLaunchKernelGGL(bn_relu_pool_kernel<float>, grid, dim3(kBlock), 0, s, (const float*)x, (float*)y, amax, P, C, pg,
                        scale, shift);
   else if (pg.k == 3 && pg.p == 1)
