@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Summarise scripts/wino_counters.sh passes: MFMA utilisation, VALU/LDS per
 MFMA, wait shares and LDS bank-conflict ratio per Winograd kernel.
-usage: python scripts/wino_ctr_summary.py gpurun_out/<dir>/ctr"""
+usage: python scripts/wino_ctr_summary.py gpurun_out/<dir>/ctr [kernel-substring,...]
+(any kernel using v_mfma_f32_16x16x4_f32 only: the stem_f32 kernels too)"""
 import collections
 import csv
 import glob
@@ -9,6 +10,7 @@ import os
 import sys
 
 root = sys.argv[1]
+keys = sys.argv[2].split(",") if len(sys.argv) > 2 else ["wino_f23", "wino_wgrad_kernel"]
 groups = collections.defaultdict(list)
 for f in sorted(glob.glob(os.path.join(root, "*_p[12]/run_counter_collection.csv"))):
     groups[os.path.basename(os.path.dirname(f))[:-3]].append(f)
@@ -16,7 +18,7 @@ for g, files in groups.items():
     d = collections.defaultdict(float)
     name = ""
     for f in files:
-        rows = [r for r in csv.DictReader(open(f)) if ("wino_f23" in r["Kernel_Name"] or "wino_wgrad_kernel" in r["Kernel_Name"])]
+        rows = [r for r in csv.DictReader(open(f)) if any(k in r["Kernel_Name"] for k in keys)]
         if not rows:
             continue
         name = rows[0]["Kernel_Name"][:60]
