@@ -320,13 +320,13 @@ def _dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, lz=None, plink=No
         dx = xs
         if k == 1:
             DY, DX = _rows(dy), _rows(dx)
-            Wt = w.reshape(K, C).t().contiguous()
-            run = lambda c, mb: g.gemm_nt(DY, Wt, DX, c, mb, **kw)  # noqa: E731
+            Wt = _lazy(lambda: w.reshape(K, C).t().contiguous())
+            run = lambda c, mb: g.gemm_nt(DY, Wt(), DX, c, mb, **kw)  # noqa: E731
         else:
             # dX = conv(dY, W') with W'[c][kh][kw][k] = W[k][KH-1-kh][KW-1-kw][c]
-            wf = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=_CL)
+            wf = _lazy(lambda: w.flip(2, 3).transpose(0, 1).contiguous(memory_format=_CL))
             z = _zero(dy.device)
-            run = lambda c, mb: g.conv_nt(dy, wf, dx, z, 1, p, c, mb, **kw)  # noqa: E731
+            run = lambda c, mb: g.conv_nt(dy, wf(), dx, z, 1, p, c, mb, **kw)  # noqa: E731
         cands = [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in _nt_cfgs(dt) for mb in _NT_GRIDS]
     if lz is not None:
         cands.append((("mat", 0, 0), lambda: _dgrad(plink.materialize(), w, x_shape, s)))
@@ -347,6 +347,18 @@ def _dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, lz=None, plink=No
         return dx
     run(ch[1], ch[2])
     return dx
+
+
+def _lazy(make):
+    """Memoised weight re-layout: built on first use only, so a Winograd /
+    MIOpen choice does not pay the transpose / flip copy it never reads."""
+    box = []
+
+    def get():
+        if not box:
+            box.append(make())
+        return box[0]
+    return get
 
 
 def _dgrad_key(N, C, H, W, K, k, s, dt) -> tuple:
@@ -370,14 +382,14 @@ def _dgrad_bn(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, link, lz=None,
     h, mask, dy2 = link.h, link.mask, link.dy2
     if k == 1:
         DY, DZ = _rows(dy), _rows(dz)
-        Wt = w.reshape(K, C).t().contiguous()
+        Wt = _lazy(lambda: w.reshape(K, C).t().contiguous())
         H2 = _rows(h)
         D2 = _rows(dy2) if dy2 is not None else None
-        run = lambda c, mb: g.gemm_nt(DY, Wt, DZ, c, mb, st, None, H2, D2, mask, **kw)  # noqa: E731
+        run = lambda c, mb: g.gemm_nt(DY, Wt(), DZ, c, mb, st, None, H2, D2, mask, **kw)  # noqa: E731
     else:
-        wf = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=_CL)
+        wf = _lazy(lambda: w.flip(2, 3).transpose(0, 1).contiguous(memory_format=_CL))
         z = _zero(dy.device)
-        run = lambda c, mb: g.conv_nt(dy, wf, dz, z, 1, p, c, mb, st, None, h, dy2, mask, **kw)  # noqa: E731
+        run = lambda c, mb: g.conv_nt(dy, wf(), dz, z, 1, p, c, mb, st, None, h, dy2, mask, **kw)  # noqa: E731
     # 64x64-per-wave tiles (cfg digit 1-4) carry the BN-backward epilogue
     cands = [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in _nt_cfgs(dt) if c % 10 <= 4
              for mb in _NT_GRIDS]
