@@ -16,6 +16,12 @@
 //   select  (grid)   ballot/popcount block scan, writes ascending indices +
 //                    values into the record, zeroes sent entries of r [K5]
 //
+// The 1-workgroup steps run in the LAST block of the preceding grid pass
+// (last_block(): device-coherent partials + an arrival counter, no spin):
+// finalize in the stats pass (threshold modes; radix modes keep a separate
+// finalize after the histograms), decide in the count pass, and the fallback
+// key in the conditional radix pass 2 -- 7 launches per threshold-mode call.
+//
 // Reference semantics reproduced (compression.py):
 //   gaussian  :358-389  threshold mu + |ppf(ratio/2)| * sigma, <=3 loops
 //   gaussian2 :405-435  same, <=5 loops, no residual add
