@@ -25,6 +25,19 @@ N > 1 also times, after the sparse loop, a dense comparator: the same model
 with a bucketed (``--dense-bucket-mb``, 25 MB), backward-overlapped RCCL
 all-reduce of fp32 gradients and no compression -- ``dense_ms_per_step`` /
 ``speedup_vs_dense`` answer whether sparsification pays on xGMI.
+
+At every N the same compressed step and the dense comparator are also timed
+at the reference's own per-worker batch (``REF_BATCH``: ResNet-50 32,
+/root/reference/exp_configs/resnet50.conf:2), where the exchange is a far
+larger share of the step: ``ref_bs32_value`` / ``ref_bs32_dense_value`` /
+``ref_bs32_speedup_vs_dense``.
+
+Fail-soft: only the headline phase is fatal.  Every secondary phase (fabric
+probe, dense comparator, reference-batch phases, bf16) runs under
+``optional_phase``: an exception is recorded as ``<phase>_error`` in the one
+JSON line (``GKSGD_BENCH_FAIL_PHASE=<phase>`` injects one, tests).  ``phases``
+records per phase the exchanger kind and, on the native engine, the
+event-timed collectives of its timed loop.
 ``exposed_comm_ms`` is the mean time, per timed step, from the end of the
 backward pass on the compute stream to the end of the update (event pair):
 the communication + decompression + update that the backward did not hide.
@@ -70,6 +83,16 @@ MODELS = {
     "fcn5net": ("mnist", 1024, "images/s", 1, "synthetic (MNIST-shaped 1x28x28, on-device)"),
 }
 
+# The reference's own per-worker batch (/root/reference/exp_configs/<dnn>.conf:2):
+# the "ref_bs" phases time the same step at that batch, where the exchange is a
+# larger share of the step than at the headline batch.
+REF_BATCH = {"resnet50": 32, "vgg16i": 128, "vgg16": 128, "resnet20": 32, "lstm": 20, "fcn5net": 128}
+
+# BERT (BASELINE config 5, "bucketed compression"): default bucket threshold in
+# elements (~25 MB of fp32 gradients per bucket, overlapped with the backward)
+# instead of the reference's single 524,288,000-element group.
+DEFAULT_THRESHOLD = {"bert": 6_500_000}
+
 
 def parse():
     ap = argparse.ArgumentParser()
@@ -82,7 +105,9 @@ def parse():
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--compressor", default="gaussian")
     ap.add_argument("--density", type=float, default=0.001)
-    ap.add_argument("--threshold", type=int, default=524288000, help="bucket threshold (elements), reference default")
+    ap.add_argument("--threshold", type=int, default=None,
+                    help="bucket threshold (elements); default: the reference's 524288000 (one group), "
+                         "BERT 6.5 M (~25 MB buckets, BASELINE config 5 'bucketed compression')")
     ap.add_argument("--planner", default="threshold", choices=["threshold", "mgs", "mgwfbp"],
                     help="bucket planner: reference threshold grouping, or MGS / MG-WFBP on measured layer-wise "
                          "backward times (utils/profiler.benchmark) and the perf models (utils/perf_model.py)")
@@ -93,6 +118,10 @@ def parse():
     ap.add_argument("--no-bf16-phase", action="store_true",
                     help="skip the secondary bf16 phase of an fp32 headline run")
     ap.add_argument("--no-dense-phase", action="store_true", help="skip the dense comparator at N > 1")
+    ap.add_argument("--ref-batch", type=int, default=None,
+                    help="per-GPU batch of the reference-batch phases (default: the reference's exp_configs "
+                         "batch of the model, ResNet-50 32; 0 skips them)")
+    ap.add_argument("--ref-steps", type=int, default=10, help="timed steps of each reference-batch phase")
     ap.add_argument("--dense-bucket-mb", type=float, default=25.0,
                     help="bucket size of the dense comparator's overlapped all-reduce (MB of fp32 gradients)")
     ap.add_argument("--no-channels-last", action="store_true")
@@ -165,7 +194,17 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
-def build(args, amp: str, dense: bool, threshold: int, P: int, rank: int):
+class Phase:
+    """One timed phase's objects.  ``release()`` clears every reference held
+    here (trainer, optimizer, step closure / GraphedStep with its graph pool)
+    so the next phase is timed without the previous one's memory resident."""
+
+    def __init__(self, trainer, opt, comp_name: str, is_sparse: bool, batch: int):
+        self.trainer, self.opt, self.comp_name, self.is_sparse, self.batch = trainer, opt, comp_name, is_sparse, batch
+        self.step = None
+
+
+def build(args, amp: str, dense: bool, threshold: int, P: int, rank: int, batch: int) -> Phase:
     """Trainer + DistributedOptimizer of one timed phase.  amp: "fp32" / "bf16"."""
     from gaussiank_sgd_amd.compression import compressors
     from gaussiank_sgd_amd.parallel import comm
@@ -173,7 +212,7 @@ def build(args, amp: str, dense: bool, threshold: int, P: int, rank: int):
     from gaussiank_sgd_amd.train import DLTrainer
 
     dataset, _, _, _, _ = MODELS[args.model]
-    trainer = DLTrainer(rank, P, dnn=args.model, dataset=dataset, batch_size=args.batch_size,
+    trainer = DLTrainer(rank, P, dnn=args.model, dataset=dataset, batch_size=batch,
                         lr=0.1, nworkers=P, device="cuda", amp="bf16" if amp == "bf16" else None,
                         channels_last=not args.no_channels_last, seed=0)
     comp_name = "none" if dense else args.compressor
@@ -200,15 +239,17 @@ def build(args, amp: str, dense: bool, threshold: int, P: int, rank: int):
             install_direct_grads(trainer.net, opt)
     trainer.update_optimizer(opt)
     trainer.display = 10 ** 9  # no host-syncing log lines inside the timed loop
-    return trainer, opt, comp_name, is_sparse
+    return Phase(trainer, opt, comp_name, is_sparse, batch)
 
 
-def run_phase(args, trainer, opt, steps: int, warmup: int, P: int):
+def run_phase(args, ph: Phase, steps: int, warmup: int, P: int):
     """W untimed warm-up steps, then EXACTLY K steps bracketed by a barrier +
     synchronize on both sides; returns (elapsed seconds, max over ranks;
-    exposed-comm ms per step, max over ranks; the step callable)."""
+    exposed-comm ms per step, max over ranks).  The step callable is kept
+    on ``ph``."""
     from gaussiank_sgd_amd.parallel import comm
 
+    trainer, opt = ph.trainer, ph.opt
     state = {"hidden": None}
     clip = 0.25 if args.model == "lstm" else None  # reference dist_trainer.py:80-85
     marks = []   # (end of backward, end of update) event pairs of the timed steps
@@ -241,6 +282,7 @@ def run_phase(args, trainer, opt, steps: int, warmup: int, P: int):
         for _ in range(warmup):
             step()
         run = GraphedStep(trainer, opt, clip)
+    ph.step = run
     for _ in range(warmup):
         run()
     torch.cuda.synchronize()
@@ -259,18 +301,79 @@ def run_phase(args, trainer, opt, steps: int, warmup: int, P: int):
     t = torch.tensor([elapsed, exposed], dtype=torch.float64, device="cuda")
     if P > 1:
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    return float(t[0]), float(t[1]), run
+    return float(t[0]), float(t[1])
 
 
-def release(trainer, opt) -> None:
+def phase_info(ph: Phase) -> dict:
+    """Exchanger kind and the event-timed collectives of the phase's timed
+    loop (native engine; empty for torch.distributed / local)."""
+    ex = ph.opt._exchanger if ph is not None and ph.opt is not None else None
+    info = {"exchange": ex.kind if ex is not None else "none", "buckets": len(ph.opt.arena.buckets) if ph else None}
+    if ex is not None:
+        try:
+            info["timed_loop"] = ex.stats() or None
+        except Exception as e:  # noqa: BLE001 - diagnostics only
+            info["timed_loop"] = "error: %s" % e
+    return info
+
+
+def release(ph) -> None:
     import gc
-    if opt._exchanger is not None:
-        opt._exchanger.close()
-        opt._exchanger = None
-    del trainer, opt
+    if ph is None:
+        return
+    opt = ph.opt
+    if opt is not None and opt._exchanger is not None:
+        try:
+            opt._exchanger.close()
+        finally:
+            opt._exchanger = None
+    ph.trainer = ph.opt = ph.step = None
+    del opt
     gc.collect()
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
+
+
+def _agree(ok: bool, P: int) -> bool:
+    """Every rank's verdict on a phase (MIN over ranks); False if the
+    agreement itself fails (a broken communicator ends the optional phases)."""
+    if P == 1:
+        return ok
+    from gaussiank_sgd_amd.parallel import comm
+    try:
+        dev = "cuda" if comm.backend() == "nccl" else "cpu"
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MIN)
+        return int(t) == 1
+    except Exception:  # noqa: BLE001
+        return False
+
+
+def optional_phase(name: str, out: dict, P: int, fn) -> bool:
+    """Run one secondary phase fail-soft: an exception (or the injected one,
+    ``GKSGD_BENCH_FAIL_PHASE=<name>``) is recorded as ``<name>_error`` in the
+    JSON line instead of losing the headline."""
+    holder = []
+    err = None
+    try:
+        if os.environ.get("GKSGD_BENCH_FAIL_PHASE") == name:
+            raise RuntimeError("injected failure (GKSGD_BENCH_FAIL_PHASE=%s)" % name)
+        fn(holder)
+    except Exception as e:  # noqa: BLE001 - fail-soft by design
+        msg = str(e).strip().splitlines()
+        err = "%s: %s" % (type(e).__name__, msg[0][:300] if msg else "")
+        print("bench.py: phase %s failed: %s" % (name, err), file=sys.stderr, flush=True)
+    for ph in holder:
+        try:
+            release(ph)
+        except Exception as e:  # noqa: BLE001
+            err = err or "release: %s" % e
+    ok = _agree(err is None, P)
+    if err is not None:
+        out[name + "_error"] = err
+    elif not ok:
+        out[name + "_error"] = "failed on another rank"
+    return ok
 
 
 def main() -> int:
@@ -308,10 +411,16 @@ def main() -> int:
     dataset, default_bs, unit, tok_per_sample, data_desc = MODELS[args.model]
     if args.batch_size is None:
         args.batch_size = int(os.environ.get("GKSGD_BENCH_BS", default_bs)) if args.model == "resnet50" else default_bs
+    if args.threshold is None:
+        args.threshold = DEFAULT_THRESHOLD.get(args.model, 524288000)
+    ref_bs = REF_BATCH.get(args.model) if args.ref_batch is None else args.ref_batch
     amp = "bf16" if args.amp == "bf16" else "fp32"
-    trainer, opt, comp_name, is_sparse = build(args, amp, args.dense, args.threshold, P, rank)
+
+    # ---- headline phase: any failure here is fatal (non-zero exit, no JSON line)
+    ph = build(args, amp, args.dense, args.threshold, P, rank, args.batch_size)
+    trainer, opt, comp_name, is_sparse = ph.trainer, ph.opt, ph.comp_name, ph.is_sparse
     nparams = sum(p.numel() for p in trainer.net.parameters() if p.requires_grad)
-    elapsed, exposed, step = run_phase(args, trainer, opt, args.steps, args.warmup, P)
+    elapsed, exposed = run_phase(args, ph, args.steps, args.warmup, P)
     loss = trainer.current_loss()
     pairs = opt._collect_selected(with_totals=True)
     sent = sum(p[0] for p in pairs) / max(1, args.steps)
@@ -322,6 +431,9 @@ def main() -> int:
     k_total = sum(comp.k_of(b.numel, args.density) for b in opt.arena.buckets) if is_sparse else 0
     wire_bytes = opt.wire_bytes_per_step(args.density if is_sparse else 1.0)
     ratio = (nparams * 4.0) / wire_bytes if wire_bytes else 1.0
+    n_buckets = len(opt.arena.buckets)
+    kind = opt._exchanger.kind if opt._exchanger is not None else "none"
+    phases = {"headline": phase_info(ph)}
     replicas = None
     if P > 1:
         # bit-identical replicas: all-gather a digest of every rank's weight arena
@@ -332,24 +444,6 @@ def main() -> int:
         allv = [torch.zeros_like(mine) for _ in range(P)]
         torch.distributed.all_gather(allv, mine)
         replicas = all(torch.equal(allv[0], v) for v in allv[1:])
-    collectives = None
-    if P > 1 and opt._exchanger is not None and os.environ.get("GKSGD_BENCH_PROBE", "1") == "1":
-        timed_loop = opt._exchanger.stats()     # event-timed collectives of the timed loop (native engine)
-        collectives = probe_collectives(opt._exchanger, P, torch.device("cuda", torch.cuda.current_device()),
-                                        wire_bytes // max(1, len(opt.arena.buckets)) if is_sparse else 4096,
-                                        nparams * 4)
-        fit = collectives.pop("_fit")
-        if timed_loop:
-            collectives["timed_loop"] = timed_loop
-        out_path = os.environ.get("GKSGD_PERF_MODEL_OUT")
-        if out_path and rank == 0:
-            from gaussiank_sgd_amd.utils import perf_model
-            for op in ("allgather", "allreduce"):
-                perf_model.update(out_path, op, {
-                    "alpha_s": fit[op][0], "beta_s_per_byte": fit[op][1], "measured": True,
-                    "source": "bench.py probe, %d x %s, exchanger %s, points %s" % (
-                        P, torch.cuda.get_device_name(), opt._exchanger.kind, collectives[op]["points_bytes_us"])},
-                    key=str(P))
     ms = elapsed / args.steps * 1e3
     imgs = P * args.batch_size * tok_per_sample * args.steps / elapsed
     metric = METRIC if args.model == "resnet50" else "%s (whole node) %s k=%g%% on MI355X" % (
@@ -376,18 +470,19 @@ def main() -> int:
             "parallelism": "dp%d" % P,
             "compressor": comp_name,
             "density": args.density if is_sparse else 1.0,
-            "buckets": len(opt.arena.buckets),
+            "buckets": n_buckets,
+            "threshold": args.threshold,
             "planner": args.planner if args.planner == "threshold" else "%s@P=%s" % (args.planner, args.plan_world or P),
-            "exchange": opt._exchanger.kind if opt._exchanger is not None else "none",
+            "exchange": kind,
             "momentum_correction": bool(opt._mc),
             "hip_graph": bool(args.graph),
         },
-        "graph_captures": getattr(step, "captures", None),
+        "graph_captures": getattr(ph.step, "captures", None),
         "world": P,
-        "exchange": opt._exchanger.kind if opt._exchanger is not None else "none",
+        "exchange": kind,
         "replicas_consistent": replicas,
         "exposed_comm_ms": round(exposed, 3) if exposed == exposed else None,
-        "collectives": collectives,
+        "collectives": None,
         "effective_compression_ratio": round(ratio, 1),
         "wire_bytes_per_rank_step": wire_bytes,
         # sent: entries actually in the records (<= k_cap per bucket); total:
@@ -398,48 +493,112 @@ def main() -> int:
         "selected_over_k": round(sent / k_total, 4) if is_sparse and k_total else None,
         "params": nparams,
         "final_loss": round(loss, 4) if loss == loss else None,
+        "phases": phases,
     }
-    if rank == 0 and os.environ.get("GKSGD_GEMM_SAVE"):
-        from gaussiank_sgd_amd.ops.conv1x1 import save_choices
-        save_choices(os.environ["GKSGD_GEMM_SAVE"])
+    del trainer, opt   # the Phase holder keeps the only references; release() drops them
+
+    def collectives_probe(holder):
+        # alpha-beta probe of the fabric through the headline's exchanger (N > 1)
+        ex = ph.opt._exchanger
+        if ex is None:
+            return
+        timed_loop = ex.stats()     # event-timed collectives of the timed loop (native engine)
+        col = probe_collectives(ex, P, torch.device("cuda", torch.cuda.current_device()),
+                                wire_bytes // max(1, n_buckets) if is_sparse else 4096, nparams * 4)
+        fit = col.pop("_fit")
+        if timed_loop:
+            col["timed_loop"] = timed_loop
+        out["collectives"] = col
+        out_path = os.environ.get("GKSGD_PERF_MODEL_OUT")
+        if out_path and rank == 0:
+            from gaussiank_sgd_amd.utils import perf_model
+            for op in ("allgather", "allreduce"):
+                perf_model.update(out_path, op, {
+                    "alpha_s": fit[op][0], "beta_s_per_byte": fit[op][1], "measured": True,
+                    "source": "bench.py probe, %d x %s, exchanger %s, points %s" % (
+                        P, torch.cuda.get_device_name(), ex.kind, col[op]["points_bytes_us"])},
+                    key=str(P))
+
+    alive = True
+    if P > 1 and os.environ.get("GKSGD_BENCH_PROBE", "1") == "1":
+        alive = optional_phase("collectives", out, P, collectives_probe)
     if rank == 0 and os.environ.get("GKSGD_GEMM_DUMP"):
         from gaussiank_sgd_amd.ops.conv1x1 import tuned_choices, tuning_log
         log = tuning_log()
         with open(os.environ["GKSGD_GEMM_DUMP"], "w") as f:
             json.dump([[list(k), list(v), [[list(t), r] for t, r in log.get(k, [])]]
                        for k, v in tuned_choices().items()], f)
-    release(trainer, opt)
+    release(ph)
+    ph = None
+
+    def timed(holder, name, amp_, dense, threshold, batch, steps, warmup):
+        p = build(args, amp_, dense, threshold, P, rank, batch)
+        holder.append(p)
+        el, exp_ = run_phase(args, p, steps, warmup, P)
+        info = phase_info(p)
+        info.update(ms_per_step=round(el / steps * 1e3, 3),
+                    value=round(P * batch * tok_per_sample * steps / el, 2),
+                    exposed_comm_ms=round(exp_, 3) if exp_ == exp_ else None, per_gpu_batch=batch, steps=steps)
+        phases[name] = info
+        return info
 
     # ---- dense comparator (N > 1): bucketed, backward-overlapped RCCL all-reduce
-    if P > 1 and not args.dense and not args.no_dense_phase:
-        bucket_elems = max(1, int(args.dense_bucket_mb * 1e6 / 4))
-        dtr, dopt, _, _ = build(args, amp, True, bucket_elems, P, rank)
-        dsteps = max(5, min(args.steps, 10))
-        d_el, d_exp, _ = run_phase(args, dtr, dopt, dsteps, max(3, min(args.warmup, 5)), P)
-        dms = d_el / dsteps * 1e3
-        out["dense_ms_per_step"] = round(dms, 3)
-        out["dense_value"] = round(P * args.batch_size * tok_per_sample * dsteps / d_el, 2)
-        out["dense_buckets"] = len(dopt.arena.buckets)
-        out["dense_exposed_comm_ms"] = round(d_exp, 3) if d_exp == d_exp else None
-        out["speedup_vs_dense"] = round(dms / ms, 4)
-        release(dtr, dopt)
+    dense_elems = max(1, int(args.dense_bucket_mb * 1e6 / 4))
+    if alive and P > 1 and not args.dense and not args.no_dense_phase:
+        def dense_phase(holder):
+            i = timed(holder, "dense", amp, True, dense_elems, args.batch_size, max(5, min(args.steps, 10)),
+                      max(3, min(args.warmup, 5)))
+            out["dense_ms_per_step"] = i["ms_per_step"]
+            out["dense_value"] = i["value"]
+            out["dense_buckets"] = i["buckets"]
+            out["dense_exposed_comm_ms"] = i["exposed_comm_ms"]
+            out["speedup_vs_dense"] = round(i["ms_per_step"] / ms, 4)
+        alive = optional_phase("dense", out, P, dense_phase)
+
+    # ---- reference-batch phases: the same compressed step, and the dense
+    # comparator, at the reference's per-worker batch (exp_configs/<dnn>.conf)
+    if alive and ref_bs and not args.dense:
+        tag = "ref_bs%d" % ref_bs
+        rsteps, rwarm = max(1, args.ref_steps), max(2, min(args.warmup, 5))
+
+        def ref_sparse(holder):
+            i = timed(holder, tag, amp, False, args.threshold, ref_bs, rsteps, rwarm)
+            out[tag + "_value"] = i["value"]
+            out[tag + "_ms_per_step"] = i["ms_per_step"]
+            out[tag + "_exposed_comm_ms"] = i["exposed_comm_ms"]
+
+        def ref_dense(holder):
+            i = timed(holder, tag + "_dense", amp, True, dense_elems, ref_bs, rsteps, rwarm)
+            out[tag + "_dense_value"] = i["value"]
+            out[tag + "_dense_ms_per_step"] = i["ms_per_step"]
+            if (tag + "_ms_per_step") in out:
+                out[tag + "_speedup_vs_dense"] = round(i["ms_per_step"] / out[tag + "_ms_per_step"], 4)
+        alive = optional_phase(tag, out, P, ref_sparse)
+        if alive:
+            alive = optional_phase(tag + "_dense", out, P, ref_dense)
 
     # ---- secondary bf16 phase of an fp32 headline
-    if amp == "fp32" and not args.no_bf16_phase:
-        btr, bopt, _, _ = build(args, "bf16", args.dense, args.threshold, P, rank)
-        b_el, b_exp, _ = run_phase(args, btr, bopt, args.steps, args.warmup, P)
-        out["bf16_ms_per_step"] = round(b_el / args.steps * 1e3, 3)
-        out["bf16_value"] = round(P * args.batch_size * tok_per_sample * args.steps / b_el, 2)
-        out["bf16_exposed_comm_ms"] = round(b_exp, 3) if b_exp == b_exp else None
-        release(btr, bopt)
+    if alive and amp == "fp32" and not args.no_bf16_phase:
+        def bf16_phase(holder):
+            i = timed(holder, "bf16", "bf16", args.dense, args.threshold, args.batch_size, args.steps, args.warmup)
+            out["bf16_ms_per_step"] = i["ms_per_step"]
+            out["bf16_value"] = i["value"]
+            out["bf16_exposed_comm_ms"] = i["exposed_comm_ms"]
+        alive = optional_phase("bf16", out, P, bf16_phase)
 
+    if rank == 0 and os.environ.get("GKSGD_GEMM_SAVE"):
+        from gaussiank_sgd_amd.ops.conv1x1 import save_choices
+        save_choices(os.environ["GKSGD_GEMM_SAVE"])
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
-    comm.shutdown()
+    try:
+        comm.shutdown()
+    except Exception as e:  # noqa: BLE001 - the result line is already out
+        print("bench.py: shutdown: %s" % e, file=sys.stderr)
     if replicas is False:
         print("bench.py: replicas diverged", file=sys.stderr)
         return 3

@@ -16,6 +16,8 @@ reference-compatible per-tensor API (it syncs once to size its outputs).
 Deliberate deviations:
   * ``topk`` is EXACT top-k (radix select); the shipped reference picks every
     101st element of argsort(|x|) -- available as ``topk_legacy``.
+  * ``bucketized_topk`` (torch only) is the reference's bucketized variant
+    that produced its two ``*_bucketized_topk`` logs, quirk included.
   * ``none`` returns a 3-tuple (the reference's 2-tuple crashes its own caller).
   * variable-count selectors send at most ``k_cap`` entries per bucket; the
     rest stays in the residual (no gradient mass is dropped).  The record
@@ -188,6 +190,24 @@ class TopKLegacyCompressor(_SparseCompressor):
             return tensor, idx, vals
 
 
+class BucketizedTopKCompressor(TopKLegacyCompressor):
+    """The reference's 'bucketized' topk (compression.py:60-93: per-value-bin
+    quota of the |x|-sorted positions, with its bin/index pairing quirk), EC,
+    torch only -- the selection behind the reference's
+    logs/results/{SGD,LARS}_1024_*_bucketized_topk runs."""
+    name = "bucketized_topk"
+
+    @classmethod
+    def compress(cls, tensor, name=None, sigma_scale=2.5, ratio=0.05):
+        with torch.no_grad():
+            flat = tensor.data.view(-1)
+            res = cls.get_residuals(name, flat)
+            acc, idx, vals, new_res = reference.bucketized_topk(flat, res, ratio, ec=True)
+            flat.copy_(acc)
+            res.copy_(new_res)
+            return tensor, idx, vals
+
+
 class RandomKCompressor(_SparseCompressor):
     """k uniformly random indices, no EC (compression.py:439-489)."""
     name = "randomk"
@@ -303,6 +323,7 @@ compressors = {
     "topk": TopKCompressor,
     "topk2": TopKCompressor2,
     "topk_legacy": TopKLegacyCompressor,
+    "bucketized_topk": BucketizedTopKCompressor,
     "bucket": BucketCompressor,
     "gaussian": GaussianCompressor,
     "gaussian2": GaussianCompressor2,

@@ -9,6 +9,7 @@ allocate freely: tests and parity studies only, never the hot path.
   gaussian2      compression.py:405-435   no EC, <=5 loops
   topk2          compression.py:315-334   torch.topk, no EC
   uniform topk   compression.py:96-104,180-198   argsort(|x|)[::101][-k:]
+  bucketized     compression.py:60-93    per-value-bin quota on argsort(|x|, desc)
   randomk        compression.py:461-474
   redsync        compression.py:638-679
   redsynctrim    compression.py:707-737
@@ -93,6 +94,44 @@ def uniform_abs_topk(tensor: torch.Tensor, residual: Optional[torch.Tensor], rat
     sorted_index = torch.abs(acc).argsort()
     indexes = sorted_index[::101][-k:]
     return _finish(acc, indexes)
+
+
+def bucketized_topk(tensor: torch.Tensor, residual: Optional[torch.Tensor], ratio: float,
+                    ec: bool = True) -> Result:
+    """The reference's ``TopKCompressor.bucketized_topk`` (compression.py:60-93)
+    behind the ``topk`` compressor's EC, re-stated without its per-bin Python
+    loop but with its exact semantics, quirk included:
+
+    * positions of ``argsort(|x|, descending)`` are consumed bin by bin, in the
+      ASCENDING order of the bins ``unique(int(100 x))`` -- so the chunk of
+      positions charged to a bin is NOT that bin's members (the
+      ascending bins are paired with descending-sorted indices);
+    * a bin of count c takes its first ``c`` positions when c == 1, else
+      ``round(c k / n)`` (Python's round: half to even);
+    * if fewer than k were taken, the untaken positions (in order) fill up;
+      the result is cut to k.
+
+    Ties in |x| are broken by the stable sort (the reference's unstable
+    argsort leaves them unspecified)."""
+    acc = tensor + residual if (ec and residual is not None) else tensor.clone()
+    flat = acc.reshape(-1)
+    n = flat.numel()
+    k = _k(n, ratio)
+    sorted_index = torch.argsort(torch.abs(flat), descending=True, stable=True)
+    sorted_int = (flat[sorted_index] * 100).int()          # truncation toward zero, as .int()
+    _, counts = torch.unique(sorted_int, sorted=True, return_counts=True)
+    counts = counts.to(torch.int64)
+    # round((count * k) / n): the double quotient, rounded half to even (torch.round)
+    take = torch.round((counts * k).to(torch.float64) / n).to(torch.int64)
+    take = torch.where(counts == 1, counts, take)
+    starts = torch.cumsum(counts, 0) - counts
+    pos_bin = torch.repeat_interleave(torch.arange(counts.numel(), device=flat.device), counts)
+    offset = torch.arange(n, device=flat.device) - starts[pos_bin]
+    sel = offset < take[pos_bin]
+    indexes = sorted_index[sel]
+    if indexes.numel() < k:
+        indexes = torch.cat([indexes, sorted_index[~sel][: k - indexes.numel()]])
+    return _finish(acc, indexes[:k])
 
 
 def randomk(tensor: torch.Tensor, residual: Optional[torch.Tensor], ratio: float, ec: bool = False,

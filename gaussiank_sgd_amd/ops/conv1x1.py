@@ -213,9 +213,14 @@ def _wino_ok(dt: torch.dtype, k: int, s: int, C: int, K: int) -> bool:
     return _WINO and dt == torch.float32 and k == 3 and s == 1 and C % 8 == 0 and K % 64 == 0
 
 
-def _wino_fits(*ts: torch.Tensor) -> bool:
-    # the kernels address their inputs through 32-bit buffer descriptors
-    return all(t.numel() * 4 < (1 << 31) for t in ts)
+def _wino_shape_fits(N: int, H: int, W: int, C: int, K: int) -> bool:
+    """Every operand a Winograd stride-1 3x3 kernel addresses through a 32-bit
+    buffer descriptor is < 2^31 bytes: forward x [N, C, H, W] and y
+    [N, K, H, W]; grad-input dy [N, K, H, W] and dx / the BN-backward
+    epilogue's h, dy2, mask (dx-shaped) [N, C, H, W]; grad-weight x and dy.
+    The hardware range check would silently zero loads past the limit, so
+    the candidate is refused (the bindings also refuse it loudly)."""
+    return N * H * W * max(C, K) * 4 < (1 << 31) and N * ((H + 1) // 2) * ((W + 1) // 2) < (1 << 31)
 
 
 def _wino_cands(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, flip: bool, st=None, bn=()) -> list:
@@ -259,7 +264,7 @@ def _fwd(x: torch.Tensor, w: torch.Tensor, s: int, stats_box=None, bias=None) ->
         run = lambda c, mb: g.conv_nt(x, w, y, z, s, p, c, mb, st, bias)  # noqa: E731
     b16 = bias.to(dt) if bias is not None else None
     cands = [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in _nt_cfgs(dt) for mb in _NT_GRIDS]
-    wino = bias is None and _wino_ok(dt, k, s, C, K) and _wino_fits(x)
+    wino = bias is None and _wino_ok(dt, k, s, C, K) and _wino_shape_fits(N, H, W, C, K)
     if wino:
         cands += _wino_cands(x, w, y, False, st)
 
@@ -335,7 +340,7 @@ def _dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, lz=None, plink=No
             return _dgrad(plink.materialize(), w, x_shape, s)
         run(ch[1], ch[2])
         return dx
-    wino = _wino_ok(dt, k, s, K, C) and _wino_fits(dy)
+    wino = _wino_ok(dt, k, s, K, C) and _wino_shape_fits(N, H, W, C, K)
     if wino:
         cands += _wino_cands(dy, w, dx, True)
     cands.append((("miopen", 0, 0), miopen))
@@ -362,7 +367,7 @@ def _lazy(make):
 
 
 def _dgrad_key(N, C, H, W, K, k, s, dt) -> tuple:
-    wino = _wino_ok(dt, k, s, K, C) and N * H * W * max(C, K) * 4 < (1 << 31)
+    wino = _wino_ok(dt, k, s, K, C) and _wino_shape_fits(N, H, W, C, K)
     return ("dgrad", N, C, H, W, K, k, s) + _dkey(dt) + (("wino",) if wino else ())
 
 
@@ -400,7 +405,7 @@ def _dgrad_bn(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, link, lz=None,
         if ch[0] == "mat":
             return _dgrad_bn(plink.materialize(), w, x_shape, s, link)
     else:
-        if _wino_ok(dt, k, s, K, C) and _wino_fits(dy):
+        if _wino_ok(dt, k, s, K, C) and _wino_shape_fits(N, H, W, C, K):
             cands += _wino_cands(dy, w, dz, True, st, (h, dy2, mask))
             key = key + ("wino",)
         ch = _pick(key, _forced(cands))
@@ -431,7 +436,7 @@ def dgrad_key_dtype(key: tuple) -> torch.dtype:
 
 def _wgrad_key(x: torch.Tensor, w: torch.Tensor, s: int, lz=None) -> tuple:
     N, C, H, W, K, k, p, OH, OW = _geom(x.shape, w, s)
-    wino = lz is None and _wino_ok(x.dtype, k, s, C, K) and C % 64 == 0 and N * H * W * max(C, K) * 4 < (1 << 31)
+    wino = lz is None and _wino_ok(x.dtype, k, s, C, K) and C % 64 == 0 and _wino_shape_fits(N, H, W, C, K)
     return ("wgrad", N, C, H, W, K, k, s) + _dkey(x.dtype) + (("lz",) if lz is not None else ()) + \
         (("wino",) if wino else ())
 

@@ -208,7 +208,24 @@ __device__ __forceinline__ void load4(const float* __restrict__ p, int64_t e, in
 // counts itself in, so the last block reads every block's values.  (An
 // agent-scope release / acquire fence would instead write back / invalidate
 // the whole L2 of the XCD -- per block, that costs more than the launch it
-// saves.)
+// saves: the stats pass leaves every block's slice of r dirty in L2.)
+//
+// Hardware assumption (gfx950, ROCm 7.2), stated because the C++ memory model
+// alone does not give this hand-off a happens-before edge (relaxed RMW): it is
+// the first row of the measured-valid table of MI355X_MICROARCH.md
+// "Workgroup dispatch, XCD placement & inter-workgroup visibility" --
+//   * every handed-off byte is stored `sc1` (st_dev / agent-scope atomics: the
+//     per-block partials, block counts and histogram adds) and loaded `sc1`
+//     (ld_dev) -- 4- or 8-byte accesses, hipMalloc'd workspace;
+//   * every storing wave runs `s_waitcnt vmcnt(0)` after its stores and the
+//     workgroup barrier precedes the ONE lane's agent-scope add to ONE
+//     unsharded counter;
+//   * the workgroup whose add came last (told by the value returned) loads
+//     only after its add returned, its other waves after a barrier.
+// The asm waitcnt and the barriers also keep the compiler from moving the
+// atomic loads / stores across the add.  tests/test_kernels_gpu.py
+// (test_last_block_handoff_stress) replays the hand-offs at the largest grid
+// sizes, back to back, and checks every header and record against the host.
 __device__ __forceinline__ bool last_block(uint32_t* counter) {
   __shared__ uint32_t s_last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's st_dev / atomics completed
@@ -222,6 +239,26 @@ __device__ __forceinline__ bool last_block(uint32_t* counter) {
   __syncthreads();
   return s_last != 0u;
 }
+
+// Live candidates of a mode's threshold ladder: the ONE definition both the
+// finalize step (which fills ctrl->bound[0 .. n)) and the host's choice of the
+// count kernel's compile-time candidate bound NC (count_cands) read, so a
+// ladder cannot grow on one side only (a count pass with NC below the live
+// count would report zero for the candidates past NC).
+__host__ __device__ constexpr int ladder_cands(int mode, int loops) {
+  return mode == kModeGaussian ? ((loops < 1 ? 1 : loops) * ((loops < 1 ? 1 : loops) + 1) / 2 < kMaxCand
+                                      ? (loops < 1 ? 1 : loops) * ((loops < 1 ? 1 : loops) + 1) / 2
+                                      : kMaxCand)
+         : mode == kModeRedSync ? 7
+         : mode == kModeGaussianCal ? kCalCand
+         : mode == kModeThreshold ? 1
+         : (mode == kModeTopK || mode == kModeRandomK) ? 2
+         : mode == kModeDGC ? 3
+         : kMaxCand;   // RedSyncTrim: the whole descending-ratio ladder
+}
+constexpr int kFallbackCands = 2;   // conditional exact-key pass: key > K, key >= K
+static_assert(ladder_cands(kModeGaussian, 5) == 15 && ladder_cands(kModeGaussian, 3) == 6, "gaussian ladder");
+static_assert(ladder_cands(kModeRedSync, 3) <= kMaxCand && kCalCand <= kMaxCand, "ladder sizes");
 
 struct FinArgs {   // finalize_body arguments (stats -> finalize hand-off)
   GkCtrl* ctrl;
@@ -602,7 +639,8 @@ __device__ __forceinline__ void finalize_body(GkCtrl* __restrict__ ctrl, const d
     ctrl->cand_thr[1] = (double)__uint_as_float(rkey[1] & 0x7fffffffu);
     nc = 3;
   }
-  ctrl->ncand = nc < kMaxCand ? nc : kMaxCand;
+  (void)nc;
+  ctrl->ncand = ladder_cands(mode, loops);   // == the ladder filled above (shared with count_cands)
   ctrl->radix_key[0] = rkey[0]; ctrl->radix_key[1] = rkey[1];
   ctrl->radix_kremain[0] = rkrem[0]; ctrl->radix_kremain[1] = rkrem[1];
   ctrl->k_eff = rkeff[1];
@@ -632,7 +670,7 @@ __device__ __forceinline__ void cal_fallback_body(GkCtrl* __restrict__ ctrl, con
   for (int j = 0; j < kMaxCand; ++j) ctrl->bound[j] = 0xffffffffu;
   ctrl->bound[0] = key + 1u;  // key > K
   ctrl->bound[1] = key;       // key >= K
-  ctrl->ncand = 2;
+  ctrl->ncand = kFallbackCands;
   ctrl->radix_key[1] = key;
   ctrl->radix_kremain[1] = krem;
   ctrl->k_eff = keff;
@@ -1059,19 +1097,7 @@ __global__ __launch_bounds__(kBlock) void select_kernel(float* __restrict__ r, i
 }
 
 // live candidates of a count pass (finalize_kernel / cal_fallback_kernel ladders)
-int count_cands(const CompressArgs& a, int cond) {
-  if (cond) return 2;
-  switch (a.mode) {
-    case kModeGaussian: { const int l = a.loops < 1 ? 1 : a.loops; const int c = l * (l + 1) / 2;
-                          return c < kMaxCand ? c : kMaxCand; }
-    case kModeRedSync: return 7;
-    case kModeGaussianCal: return kCalCand;
-    case kModeThreshold: return 1;
-    case kModeTopK: case kModeRandomK: return 2;
-    case kModeDGC: return 3;
-    default: return kMaxCand;
-  }
-}
+int count_cands(const CompressArgs& a, int cond) { return cond ? kFallbackCands : ladder_cands(a.mode, a.loops); }
 
 template <int KEYKIND>
 void launch_count(const CompressArgs& a, const Ws& w, bool vec, int G, int64_t chunk_tiles, GkCtrl* ctrl, int cond,

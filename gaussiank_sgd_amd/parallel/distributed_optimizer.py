@@ -506,7 +506,12 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         r = b.slice(self._arena.residuals)
         # stateless seed: (iteration, bucket, rank) -- identical across ranks for *same* variants
         seed = comp.seed_for(self.train_iter, b.index, self._rank)
-        seed_dev = self._seed_dev[b.index:b.index + 1] if self._seed_dev is not None else None
+        # device seed words only while a graph captures (every replay reads the
+        # words refresh_device_seeds wrote); an eager step -- the warm-up steps of a
+        # recapture included -- takes seed_for(train_iter) directly
+        seed_dev = None
+        if self._seed_dev is not None and self._is_cuda and torch.cuda.is_current_stream_capturing():
+            seed_dev = self._seed_dev[b.index:b.index + 1]
         arena = self._arena
         mc = None
         if self._mc:

@@ -22,7 +22,7 @@ Single stream: the optimizer's side (compression / exchange) stream is
 dropped for the captured step -- a hipGraph with cross-stream branches
 replays on ROCm 7 at ~10 ms per ResNet-20 bs32 step (the runtime resolves
 the branch edges from the host), the same step captured on one stream at
-1.43 ms (eager: 4.9 ms; scripts/graph_probe.sh, profiles/r02_graph_probe.txt).
+1.43 ms (eager: 4.9 ms; scripts/gpurun/graph_probe.sh, profiles/r02_graph_probe.txt).
 Overlap buys nothing in a replay whose launches are already on the device.
 ``GKSGD_GRAPH_COMM_STREAM=1`` keeps the side stream.
 Not for recurrent models that carry hidden state across steps (bench.py

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise scripts/ctr_top.sh counter passes into one table per kernel:
+"""Summarise scripts/gpurun/ctr_top.sh counter passes into one table per kernel:
 wall us (kernel trace), MFMA pipe utilisation (16x16x32 bf16 MFMAs x 16
 cycles / (wall x 2.1 GHz x 1024 SIMDs)), VALU and SALU instructions per MFMA,
 LDS bank-conflict cycles / LDS-active cycles, and the share of wave cycles
@@ -46,7 +46,7 @@ def main():
     ap.add_argument("root")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
-    lines = ["# rocprofv3 --pmc passes (scripts/ctr_top.sh -> scripts/gemm_counters.sh), one probe kernel each",
+    lines = ["# rocprofv3 --pmc passes (scripts/gpurun/ctr_top.sh -> scripts/gpurun/gemm_counters.sh), one probe kernel each",
              "# mfma%% = MFMA instrs x 16 cyc / (median wall x %.1f GHz x %d SIMDs); valu/mfma, salu/mfma: instruction "
              "ratios (VALU count includes the MFMAs); lds_conf = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE; wait / stall = "
              "SQ_WAIT_ANY / SQ_WAIT_INST_ANY over SQ_WAVE_CYCLES" % (CLOCK / 1e9, SIMDS),

@@ -41,7 +41,7 @@ if [ "$MODE" = sweep ]; then
   step bench_dense 600 python bench.py --steps 20 --warmup 10 --dense --json-out $OUT/bench_dense.json
 fi
 
-# find-db for additional batch sizes: FIND_BS="384 512" bash scripts/gpu_check.sh findbs
+# find-db for additional batch sizes: FIND_BS="384 512" bash scripts/gpurun/gpu_check.sh findbs
 if [ "$MODE" = findbs ]; then
   for bs in ${FIND_BS:-512}; do
     step find_bs$bs 900 python bench.py --steps 10 --warmup 5 --batch-size $bs --cudnn-benchmark --json-out $OUT/find_bs$bs.json
@@ -50,7 +50,7 @@ if [ "$MODE" = findbs ]; then
   mkdir -p $OUT/tuning && cp -r tuning/miopen $OUT/tuning/
 fi
 # targeted: GPU tests of given files + bench A/B + profile
-#   TESTS="tests/test_shadow_gpu.py" AB="--no-shadow" bash scripts/gpu_check.sh ab
+#   TESTS="tests/test_shadow_gpu.py" AB="--no-shadow" bash scripts/gpurun/gpu_check.sh ab
 if [ "$MODE" = ab ]; then
   step pytest_sel 600 python -m pytest ${TESTS:-tests/test_shadow_gpu.py} -x -q
   step bench_a 600 python bench.py --steps 20 --warmup 10 --json-out $OUT/bench_a.json

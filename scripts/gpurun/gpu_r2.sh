@@ -33,9 +33,9 @@ for s in ${STEPS:-new all smoke bench}; do
     marker) export GKSGD_ROCTX=1; step marker 600 rocprofv3 --marker-trace --kernel-trace --stats --output-format csv -d $OUT/marker -o run -- \
            python3 bench.py ${MARKER_ARGS:---model bert --steps 4 --warmup 4 --threshold 28000000}; unset GKSGD_ROCTX ;;
     convs) step convs_ours 900 python bench/convs.py --ours --json-out $OUT/convs_ours.json ;;
-    ctr) CTR_OUT=$OUT/ctr_wgrad3 PROBE_ARGS="--op wgrad3 --cfg ${TN_CFG:-27} --C 256 --H 14" bash scripts/gemm_counters.sh \
+    ctr) CTR_OUT=$OUT/ctr_wgrad3 PROBE_ARGS="--op wgrad3 --cfg ${TN_CFG:-27} --C 256 --H 14" bash scripts/gpurun/gemm_counters.sh \
            > $OUT/ctr_wgrad3.log 2>&1; tail -40 $OUT/ctr_wgrad3.log
-         CTR_OUT=$OUT/ctr_conv3 PROBE_ARGS="--op conv --cfg ${NT_CFG:-124} --C 256 --H 14" bash scripts/gemm_counters.sh \
+         CTR_OUT=$OUT/ctr_conv3 PROBE_ARGS="--op conv --cfg ${NT_CFG:-124} --C 256 --H 14" bash scripts/gpurun/gemm_counters.sh \
            > $OUT/ctr_conv3.log 2>&1; tail -40 $OUT/ctr_conv3.log ;;
     plan) step plan_bert 600 python bench.py --model bert --steps 20 --warmup 10 --planner mgs --plan-world 8 \
            --json-out $OUT/plan_bert.json

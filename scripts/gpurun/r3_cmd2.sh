@@ -20,7 +20,7 @@ $P --op cwgrad --C 256 --K 64 --H 56 --k 1 --sweep 1,2,3,4,5,6,7,8,9,11,14,16
 } > gpurun_out/r3b/sweep.jsonl 2>&1 || exit 1
 echo sweep_ok
 CTR_OUT=gpurun_out/r3b/ctr_nt PROBE_ARGS="--op conv --dtype f32 --C 64 --H 56 --k 3 --cfg 104" KFILTER=gemm_nt \
-  bash scripts/gemm_counters.sh > gpurun_out/r3b/ctr_nt.log 2>&1
+  bash scripts/gpurun/gemm_counters.sh > gpurun_out/r3b/ctr_nt.log 2>&1
 CTR_OUT=gpurun_out/r3b/ctr_tn PROBE_ARGS="--op cwgrad --dtype f32 --C 256 --H 14 --k 3 --cfg 7" KFILTER=gemm_tn \
-  bash scripts/gemm_counters.sh > gpurun_out/r3b/ctr_tn.log 2>&1
+  bash scripts/gpurun/gemm_counters.sh > gpurun_out/r3b/ctr_tn.log 2>&1
 echo ctr_done

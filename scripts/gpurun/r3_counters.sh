@@ -1,12 +1,12 @@
 #!/bin/bash
 # PMC counters of the production GEMM kernels (fp32 headline + bf16), two passes
-# per probe (scripts/gemm_counters.sh), summarised by scripts/ctr_table.py.
+# per probe (scripts/gpurun/gemm_counters.sh), summarised by scripts/ctr_table.py.
 set -u
 D=${CTR_D:-gpurun_out/r3ctr}/ctr
 mkdir -p $D
 probe() {
   local name=$1 kf=$2; shift 2
-  CTR_OUT=$D/$name PROBE_ARGS="$* --iters 10" KFILTER=$kf bash scripts/gemm_counters.sh > $D/$name.log 2>&1
+  CTR_OUT=$D/$name PROBE_ARGS="$* --iters 10" KFILTER=$kf bash scripts/gpurun/gemm_counters.sh > $D/$name.log 2>&1
   echo "$name rc=$?"
 }
 probe f32_conv3x3_fwd_c64 gemm_nt --op conv --dtype f32 --C 64 --H 56 --k 3 --cfg 104 --mb 512

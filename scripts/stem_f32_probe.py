@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Runs the fp32 stem kernels (forward with statistics, grad-weight) a few
 times at ResNet-50 bs512 shapes -- a short program for rocprofv3 --pmc passes
-(scripts/stem_counters.sh).  usage: python scripts/stem_f32_probe.py [N] [iters] [fwd|wgrad|both]"""
+(scripts/gpurun/stem_counters.sh).  usage: python scripts/stem_f32_probe.py [N] [iters] [fwd|wgrad|both]"""
 import os
 import sys
 

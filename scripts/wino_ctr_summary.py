@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise scripts/wino_counters.sh passes: MFMA utilisation, VALU/LDS per
+"""Summarise scripts/gpurun/wino_counters.sh passes: MFMA utilisation, VALU/LDS per
 MFMA, wait shares and LDS bank-conflict ratio per Winograd kernel.
 usage: python scripts/wino_ctr_summary.py gpurun_out/<dir>/ctr [kernel-substring,...]
 (any kernel using v_mfma_f32_16x16x4_f32 only: the stem_f32 kernels too)"""

@@ -1,0 +1,55 @@
+"""bench.py's fail-soft phase runner and defaults, on CPU (no GPU needed)."""
+import importlib.util
+import os
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def bench():
+    spec = importlib.util.spec_from_file_location("gk_bench", os.path.join(ROOT, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_optional_phase_records_error(bench, monkeypatch):
+    out = {}
+
+    def boom(holder):
+        raise ValueError("bad shape\nsecond line")
+    assert bench.optional_phase("dense", out, 1, boom) is False
+    assert out["dense_error"] == "ValueError: bad shape"
+
+
+def test_optional_phase_injection_and_success(bench, monkeypatch):
+    out = {}
+    ran = []
+    monkeypatch.setenv("GKSGD_BENCH_FAIL_PHASE", "bf16")
+    assert bench.optional_phase("bf16", out, 1, lambda h: ran.append(1)) is False
+    assert "injected failure" in out["bf16_error"] and not ran
+    assert bench.optional_phase("ref_bs32", out, 1, lambda h: ran.append(1)) is True
+    assert ran == [1] and "ref_bs32_error" not in out
+
+
+def test_reference_batches_and_bert_buckets(bench):
+    # the reference's per-worker batches (/root/reference/exp_configs/*.conf:2)
+    assert bench.REF_BATCH["resnet50"] == 32 and bench.REF_BATCH["vgg16"] == 128 and bench.REF_BATCH["lstm"] == 20
+    # BERT: bucketed compression (~25 MB fp32 buckets) by default
+    assert bench.DEFAULT_THRESHOLD["bert"] * 4 == pytest.approx(26e6, rel=0.1)
+
+
+def test_bert_default_threshold_gives_buckets(bench):
+    """The BERT default threshold splits the 110 M gradients into >= 4 buckets
+    (reference grouping rule: reverse registration order until >= threshold)."""
+    import torch
+    from gaussiank_sgd_amd.models.bert import bert_base
+    from gaussiank_sgd_amd.parallel.buckets import group_with_threshold
+    with torch.device("meta"):
+        net = bert_base()
+    names = [n for n, p in net.named_parameters()]
+    sizes = {n: p.numel() for n, p in net.named_parameters()}
+    groups = group_with_threshold(names, sizes, bench.DEFAULT_THRESHOLD["bert"])
+    assert len(groups) >= 4

@@ -30,9 +30,10 @@ def _free_port():
     return p
 
 
-def _bench(*extra, gpus=2, timeout=480, probe=False):
+def _bench(*extra, gpus=2, timeout=480, probe=False, env_extra=None):
     env = dict(os.environ, GKSGD_DIST_BACKEND="gloo", MASTER_PORT=str(_free_port()), HSA_ENABLE_IPC_MODE_LEGACY="0",
                GKSGD_BENCH_PROBE="1" if probe else "0")
+    env.update(env_extra or {})
     env.pop("WORLD_SIZE", None)
     env.pop("RANK", None)
     env.pop("LOCAL_RANK", None)
@@ -45,7 +46,7 @@ def _bench(*extra, gpus=2, timeout=480, probe=False):
 
 
 def test_bench_resnet50_two_ranks_one_gpu(cuda):
-    out = _bench("--steps", "3", "--warmup", "2", "--batch-size", "16")
+    out = _bench("--steps", "3", "--warmup", "2", "--batch-size", "16", "--ref-batch", "8", "--ref-steps", "2")
     assert out["n_gpus"] == 2 and out["world"] == 2
     assert out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 32
     assert out["exchange"] == "torch"
@@ -63,6 +64,28 @@ def test_bench_resnet50_two_ranks_one_gpu(cuda):
     # dense comparator: bucketed (25 MB), backward-overlapped all-reduce after the sparse loop
     assert out["dense_ms_per_step"] > 0 and out["dense_buckets"] > 1
     assert out["speedup_vs_dense"] == pytest.approx(out["dense_ms_per_step"] / out["ms_per_step"], rel=1e-2)
+    # reference-batch phases (the reference's per-worker batch; here shrunk to 8)
+    assert out["ref_bs8_value"] > 0 and out["ref_bs8_dense_value"] > 0
+    assert out["ref_bs8_speedup_vs_dense"] == pytest.approx(
+        out["ref_bs8_dense_ms_per_step"] / out["ref_bs8_ms_per_step"], rel=1e-2)
+    # per-phase exchanger kind (gloo: torch.distributed) and no recorded failure
+    ph = out["phases"]
+    assert set(ph) >= {"headline", "dense", "ref_bs8", "ref_bs8_dense", "bf16"}
+    assert all(p["exchange"] == "torch" for p in ph.values())
+    assert ph["ref_bs8"]["per_gpu_batch"] == 8 and ph["dense"]["buckets"] > 1
+    assert not [k for k in out if k.endswith("_error")]
+
+
+def test_bench_phase_failure_keeps_headline(cuda):
+    """A failing secondary phase (injected into the dense comparator) is
+    recorded as dense_error; the headline line still comes out, rc 0, and the
+    phases after it still run."""
+    out = _bench("--model", "resnet20", "--steps", "2", "--warmup", "1", "--batch-size", "32", "--ref-batch", "16",
+                 "--ref-steps", "2", env_extra={"GKSGD_BENCH_FAIL_PHASE": "dense"})
+    assert out["value"] > 0 and out["n_gpus"] == 2
+    assert "injected failure" in out["dense_error"]
+    assert "dense_ms_per_step" not in out and "speedup_vs_dense" not in out
+    assert out["ref_bs16_value"] > 0 and out["bf16_value"] > 0
 
 
 def test_bench_dense_two_ranks_one_gpu(cuda):

@@ -189,3 +189,77 @@ def test_topk_legacy_is_uniform_101():
     _, idx, _, _ = reference.uniform_abs_topk(t, None, 0.001, ec=False)
     sorted_index = t.abs().argsort()
     assert torch.equal(idx, sorted_index[::101][-20:])
+
+
+def _bin_loop_bucketized(tensor, k):
+    """Literal per-bin statement of the reference rule (compression.py:60-93),
+    independent of the vectorised oracle."""
+    import torch
+    n = tensor.numel()
+    si = torch.argsort(torch.abs(tensor), descending=True, stable=True)
+    vals = (tensor[si] * 100).int()
+    _, counts = torch.unique(vals, sorted=True, return_counts=True)
+    take, rest, start = [], [], 0
+    for c in counts.tolist():
+        e = c if c == 1 else round((c * k) / n)
+        take += si[start:start + e].tolist()
+        rest += si[start + e:start + c].tolist()
+        start += c
+    if len(take) < k:
+        take += rest[:k - len(take)]
+    return take[:k]
+
+
+def test_bucketized_topk_matches_bin_loop_and_quirk():
+    import torch
+    from gaussiank_sgd_amd.compression import compressors, reference
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(5000, generator=g) * 0.05
+    for ratio in (0.001, 0.01, 0.05):
+        k = max(int(x.numel() * ratio), 1)
+        acc, idx, vals, res = reference.bucketized_topk(x, None, ratio, ec=False)
+        assert idx.tolist() == _bin_loop_bucketized(x, k)
+        assert idx.numel() == k and torch.equal(vals, x[idx])
+        assert torch.equal(res[idx], torch.zeros(k)) and torch.equal(acc, x)
+    # the quirk: the selection is NOT the top-k by magnitude
+    k = 50
+    _, idx, _, _ = reference.bucketized_topk(x, None, k / x.numel(), ec=False)
+    top = set(torch.topk(x.abs(), k).indices.tolist())
+    assert len(top & set(idx.tolist())) < k
+    # registry: EC compressor with the reference's (tensor, indexes, values) API
+    comp = compressors["bucketized_topk"]
+    comp.clear()
+    t = x.clone()
+    out, i2, v2 = comp.compress(t, name="b", ratio=0.01)
+    assert out is t and i2.numel() == 50 and torch.equal(comp.residuals["b"][i2], torch.zeros(50))
+    assert torch.allclose(comp.residuals["b"] + torch.zeros_like(x).index_put_((i2,), v2), x)
+
+
+def test_bucketized_topk_against_reference_source():
+    """When the reference tree is present (this container), exec its own
+    bucketized_topk (function source only, nothing else of the module) and
+    compare on a fixed tensor with distinct magnitudes."""
+    import ast
+    import os
+    import pytest
+    import torch
+    path = "/root/reference/compression.py"
+    if not os.path.exists(path):
+        pytest.skip("reference tree not present")
+    tree = ast.parse(open(path).read())
+    fn = None
+    for node in ast.walk(tree):
+        if isinstance(node, ast.FunctionDef) and node.name == "bucketized_topk":
+            fn = node
+    assert fn is not None
+    fn.decorator_list = []
+    ns = {"torch": torch}
+    exec(compile(ast.Module(body=[fn], type_ignores=[]), path, "exec"), ns)
+    from gaussiank_sgd_amd.compression import reference
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(4000, generator=g) * 0.03
+    for ratio in (0.002, 0.01, 0.04):
+        k = max(int(x.numel() * ratio), 1)
+        _, ref_idx = ns["bucketized_topk"](x.clone(), k)
+        _, idx, _, _ = reference.bucketized_topk(x, None, ratio, ec=False)
+        assert idx.tolist() == ref_idx.tolist()

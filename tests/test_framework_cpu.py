@@ -340,3 +340,20 @@ def test_global_avg_pool_cl():
     (gx,) = torch.autograd.grad(y, x, g)
     (gr,) = torch.autograd.grad(ref, x, g)
     assert gx.is_contiguous(memory_format=torch.channels_last) and torch.allclose(gx, gr, atol=1e-6)
+
+
+def test_winograd_candidate_filter_checks_every_operand():
+    """Grad-input with C > K: dy [N, K, H, W] fits a 32-bit buffer descriptor
+    but dx and the BN-backward epilogue's h / dy2 / mask ([N, C, H, W]) do not;
+    the Winograd candidate must be refused (verdict r3 item 7)."""
+    import torch
+    from gaussiank_sgd_amd.ops import conv1x1 as cv
+    N, H, W, C, K = 256, 56, 56, 1024, 64
+    assert N * H * W * K * 4 < (1 << 31) <= N * H * W * C * 4
+    assert not cv._wino_shape_fits(N, H, W, C, K)
+    assert not cv._wino_shape_fits(N, H, W, K, C)      # forward / grad-weight, C < K
+    key = cv._dgrad_key(N, C, H, W, K, 3, 1, torch.float32)
+    assert "wino" not in key
+    # below the limit in every operand: offered
+    assert cv._wino_shape_fits(32, 56, 56, 256, 64)
+    assert "wino" in cv._dgrad_key(32, 64, 56, 56, 64, 3, 1, torch.float32)

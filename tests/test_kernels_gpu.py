@@ -481,3 +481,58 @@ def test_compress_reused_buffers_varying_sizes(cuda, mode):
         assert (sg, tg) == (sc, tc), (n, mode, sg, tg, sc, tc)
         assert torch.equal(ig, ic) and torch.equal(vg, vc)
         assert torch.equal(rg.cpu(), rc)
+
+
+@pytest.mark.parametrize("mode", [ops.MODE_GAUSSIAN, ops.MODE_GAUSSIAN_CAL, ops.MODE_TOPK, ops.MODE_DGC])
+def test_last_block_handoff_stress(cuda, mode):
+    """The last-block hand-offs (stats -> finalize, count -> decide, radix ->
+    fallback key; compress.hip last_block) at the LARGEST grids
+    (kMaxStatsBlocks / kMaxCountBlocks), back to back on one set of buffers,
+    with an unrelated GEMM loading the chip from a second stream (uneven
+    load, L1/L2 warm).  Every call is checked word by word: the statistics
+    against fp64 torch (stale partials would move them), the header's total
+    against the count above its own threshold (count -> decide), the record's
+    indices / values / residual against that selection (decide's offsets),
+    and for exact top-k the whole record against the CPU mirror."""
+    n = 2048 * 4096 * 2 + 4093          # > kMaxStatsBlocks full tiles: every grid at its cap
+    k = n // 1000
+    k_cap = (4 * k + 2) // 3 if mode != ops.MODE_TOPK else k
+    gb = ops.CompressBuffers(k_cap, cuda)
+    cb = ops.CompressBuffers(k_cap, "cpu")
+    side = torch.cuda.Stream()
+    a = torch.randn(4096, 4096, device=cuda)
+    z = gaussian_z(0.001)
+    for it in range(5):
+        x, r = _pair(n, seed=100 + it, dist="t" if it % 2 else "normal")
+        xg, rg = x.to(cuda), r.to(cuda)
+        with torch.cuda.stream(side):
+            for _ in range(4):
+                a = torch.tanh(a @ a * 1e-3)
+        ops.compress_(xg, rg, gb, mode, ec=True, zero_g=True, loops=3, z=z, k=k, k_cap=k_cap, seed=it)
+        torch.cuda.synchronize()
+        acc = x + r
+        recg = gb.record.cpu()
+        st = gb.stats.cpu()
+        assert abs(float(st[0]) - float(acc.double().mean())) < 1e-5 * float(acc.abs().max()), it
+        assert math.isclose(float(st[1]), float(acc.double().std()), rel_tol=1e-5), it
+        sent, total, idx, val = _sel(recg, k_cap)
+        assert 0 < sent <= k_cap and sent == min(total, k_cap), it
+        assert bool((idx[1:] > idx[:-1]).all()), it
+        assert torch.equal(val, acc[idx]), it
+        res = acc.clone()
+        res[idx] = 0
+        assert torch.equal(rg.cpu(), res), it
+        chosen = int(recg[2])
+        if mode == ops.MODE_TOPK:
+            ops.compress_(x.clone(), r.clone(), cb, mode, ec=True, zero_g=True, loops=3, z=z, k=k, k_cap=k_cap,
+                          seed=it)
+            assert torch.equal(recg, cb.record), it
+        elif chosen not in (ops.OVERFLOW_EXACT, ops.CAL_FALLBACK) and mode != ops.MODE_DGC:
+            thr = float(recg[3:4].view(torch.float32))
+            expect = (acc.abs() > thr).nonzero().view(-1)
+            assert total == expect.numel() and torch.equal(idx, expect[:sent]), it
+        else:
+            # exact-key selections: every sent magnitude >= every unsent one
+            unsent = torch.ones(n, dtype=torch.bool)
+            unsent[idx] = False
+            assert float(val.abs().min()) >= float(acc.abs()[unsent].max()), it

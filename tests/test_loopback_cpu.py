@@ -121,7 +121,7 @@ def test_loopback_randomksame_ranks_pick_same_indices(comp):
     assert not torch.equal(states[0]["__sent__"][0], states[0]["__sent__"][1])
 
 
-@pytest.mark.parametrize("comp", ["randomk", "dgcsampling", "topk_legacy", "gaussian_cal"])
+@pytest.mark.parametrize("comp", ["randomk", "dgcsampling", "topk_legacy", "bucketized_topk", "gaussian_cal"])
 def test_loopback_reproducible_and_ranks_agree(comp):
     """Rank-dependent selectors: replicas agree, and two runs give the same result
     (no seed or residual state leaks between the virtual ranks)."""

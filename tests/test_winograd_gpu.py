@@ -155,3 +155,58 @@ def test_wino_wgrad(g, N, C, H, K, splits):
                                                 [1, 1], False, [0, 0], 1, [False, True, False])[1]
     err = (out.double() - out0.double() - ref).abs().max().item()
     assert err <= _tol(bound) + 1e-6 * out0.abs().max().item(), err
+
+
+# non-square spatial sizes (H != W, odd W): the kernels take H and W separately
+# and the autotuner offers Winograd for any fp32 3x3 stride-1 shape
+RECT = [(2, 64, 7, 9, 64), (2, 64, 14, 8, 128), (1, 128, 5, 11, 64), (3, 64, 9, 4, 64)]
+
+
+def _rect(N, C, H, W, K, seed):
+    torch.manual_seed(seed)
+    x = torch.randn(N, C, H, W, device="cuda").contiguous(memory_format=CL)
+    w = (torch.randn(K, C, 3, 3, device="cuda") * (9 * C) ** -0.5).contiguous(memory_format=CL)
+    return x, w
+
+
+@pytest.mark.parametrize("N,C,H,W,K", RECT)
+@pytest.mark.parametrize("mb", [0, 3])
+def test_wino_fwd_nonsquare(g, N, C, H, W, K, mb):
+    x, w = _rect(N, C, H, W, K, N + C + H + 3 * W + K + mb)
+    u = torch.empty(16 * K * C, device="cuda")
+    g.wino_weights(w, u, False)
+    y = torch.full((N, K, H, W), float("nan"), device="cuda").contiguous(memory_format=CL)
+    g.wino_conv(x, u, y, mb)
+    ref = F.conv2d(x.double(), w.double(), padding=1)
+    bound = F.conv2d(x.double().abs(), w.double().abs(), padding=1)
+    assert (y.double() - ref).abs().max().item() <= _tol(bound)
+
+
+@pytest.mark.parametrize("N,C,H,W,K", RECT)
+def test_wino_dgrad_nonsquare(g, N, C, H, W, K):
+    x, w = _rect(N, C, H, W, K, 7 * N + C + H + W + K)
+    dy = torch.randn(N, K, H, W, device="cuda").contiguous(memory_format=CL)
+    u = torch.empty(16 * K * C, device="cuda")
+    g.wino_weights(w, u, True)
+    dx = torch.full(x.shape, float("nan"), device="cuda").contiguous(memory_format=CL)
+    g.wino_conv(dy, u, dx, 0)
+    ref = torch.ops.aten.convolution_backward(dy.double(), x.double(), w.double(), None, [1, 1], [1, 1], [1, 1],
+                                              False, [0, 0], 1, [True, False, False])[0]
+    bound = torch.ops.aten.convolution_backward(dy.double().abs(), x.double(), w.double().abs(), None, [1, 1], [1, 1],
+                                                [1, 1], False, [0, 0], 1, [True, False, False])[0]
+    assert (dx.double() - ref).abs().max().item() <= _tol(bound)
+
+
+@pytest.mark.parametrize("N,C,H,W,K", RECT)
+@pytest.mark.parametrize("splits", [0, 3])
+def test_wino_wgrad_nonsquare(g, N, C, H, W, K, splits):
+    x, w = _rect(N, C, H, W, K, 11 * N + C + H + W + K + splits)
+    dy = torch.randn(N, K, H, W, device="cuda").contiguous(memory_format=CL)
+    out = torch.zeros(K, C, 3, 3, device="cuda").contiguous(memory_format=CL)
+    part = torch.empty(int(g.wino_wgrad_ws(N, H, W, C, K, splits)), device="cuda")
+    g.wino_wgrad(x, dy, out, part, splits)
+    ref = torch.ops.aten.convolution_backward(dy.double(), x.double(), w.double(), None, [1, 1], [1, 1], [1, 1],
+                                              False, [0, 0], 1, [False, True, False])[1]
+    bound = torch.ops.aten.convolution_backward(dy.double().abs(), x.double().abs(), w.double(), None, [1, 1], [1, 1],
+                                                [1, 1], False, [0, 0], 1, [False, True, False])[1]
+    assert (out.double() - ref).abs().max().item() <= _tol(bound)
