@@ -334,25 +334,27 @@ def release(ph) -> None:
     torch.cuda.empty_cache()
 
 
-def _agree(ok: bool, P: int) -> bool:
-    """Every rank's verdict on a phase (MIN over ranks); False if the
-    agreement itself fails (a broken communicator ends the optional phases)."""
+def _agree(ok: bool, P: int):
+    """(all ranks ok, communicator alive): the MIN of every rank's verdict on
+    a phase; a failing agreement collective means the communicator is broken
+    and ends the optional phases."""
     if P == 1:
-        return ok
+        return ok, True
     from gaussiank_sgd_amd.parallel import comm
     try:
         dev = "cuda" if comm.backend() == "nccl" else "cpu"
         t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MIN)
-        return int(t) == 1
+        return int(t) == 1, True
     except Exception:  # noqa: BLE001
-        return False
+        return False, False
 
 
 def optional_phase(name: str, out: dict, P: int, fn) -> bool:
     """Run one secondary phase fail-soft: an exception (or the injected one,
     ``GKSGD_BENCH_FAIL_PHASE=<name>``) is recorded as ``<name>_error`` in the
-    JSON line instead of losing the headline."""
+    JSON line instead of losing the headline.  Returns whether the ranks
+    could still agree afterwards (False: skip the remaining phases)."""
     holder = []
     err = None
     try:
@@ -368,12 +370,12 @@ def optional_phase(name: str, out: dict, P: int, fn) -> bool:
             release(ph)
         except Exception as e:  # noqa: BLE001
             err = err or "release: %s" % e
-    ok = _agree(err is None, P)
+    ok, alive = _agree(err is None, P)
     if err is not None:
         out[name + "_error"] = err
     elif not ok:
         out[name + "_error"] = "failed on another rank"
-    return ok
+    return alive
 
 
 def main() -> int:

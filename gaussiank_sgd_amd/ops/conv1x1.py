@@ -63,8 +63,11 @@ _NT_CFGS = [1, 2, 3, 4, 11, 13, 21, 22, 23, 24, 111, 113, 121, 122, 123, 124, 25
 # grid override: 0 = persistent (about two blocks per CU), else a fixed block count
 _NT_GRIDS = (0, 512, 1 << 20)
 _TN_CFGS = [(c, s) for c in (1, 2, 3, 4, 5, 6, 7, 8, 21, 22, 23, 24, 27, 9, 29, 101, 121, 102, 122) for s in (0, 128)]
-# fp32: 64x64 wave tiles only (gemm.hip maps NT tiles 5-7 onto them); TN cfg = tile + 10 * (1: two stages)
-_NT_CFGS_F32 = [1, 2, 3, 4, 7, 11, 12, 13, 14, 21, 22, 23, 24, 101, 102, 103, 104, 201, 202, 203, 204]
+# fp32: 64x64 wave tiles (gemm.hip maps NT tiles 5-7 onto them) and, cfg + 1000, 32x64 wave tiles
+# (twice the waves: the small-M layers of small batches, e.g. the reference's bs32); TN cfg = tile +
+# 10 * (1: two stages)
+_NT_CFGS_F32 = [1, 2, 3, 4, 7, 11, 12, 13, 14, 21, 22, 23, 24, 101, 102, 103, 104, 201, 202, 203, 204,
+                1001, 1002, 1003, 1004, 1005, 1006, 1007, 1021, 1022, 1101, 1102, 1103]
 _TN_CFGS_F32 = [(c, s) for c in (1, 2, 3, 4, 5, 6, 7, 8, 9, 11, 12, 13, 14, 15, 16) for s in (0, 64)]
 
 
@@ -395,8 +398,9 @@ def _dgrad_bn(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, link, lz=None,
         wf = _lazy(lambda: w.flip(2, 3).transpose(0, 1).contiguous(memory_format=_CL))
         z = _zero(dy.device)
         run = lambda c, mb: g.conv_nt(dy, wf(), dz, z, 1, p, c, mb, st, None, h, dy2, mask, **kw)  # noqa: E731
-    # 64x64-per-wave tiles (cfg digit 1-4) carry the BN-backward epilogue
-    cands = [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in _nt_cfgs(dt) if c % 10 <= 4
+    # 64x64-per-wave tiles (cfg digit 1-4) and the fp32 32x64 family (cfg >= 1000) carry the
+    # BN-backward epilogue
+    cands = [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in _nt_cfgs(dt) if c % 10 <= 4 or c >= 1000
              for mb in _NT_GRIDS]
     key = ("dgrad_bn", N, C, H, W, K, k, s, dy2 is not None) + _dkey(dt)
     if lz is not None:

@@ -184,8 +184,8 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
   static_assert(!LZ || F32, "lazy BN operand: fp32 kernels");
   constexpr int EPC = E::EPC;
   constexpr int KS = E::KS;
-  static_assert(!BNB || MSB == 4, "BN-backward epilogue: 64x64 wave tiles");
-  static_assert(!F32 || MSB == 4, "fp32: 64x64 wave tiles");
+  static_assert(!BNB || MSB == 4 || F32, "bf16 BN-backward epilogue: 64x64 wave tiles");
+  static_assert(!F32 || MSB == 4 || MSB == 2, "fp32: 64x64 or 32x64 wave tiles");
   constexpr bool bnb = BNB;
   static_assert(NS >= 2 && NS <= 4, "stages");
   constexpr int LPW = Cfg::LPW;
@@ -1347,12 +1347,16 @@ int nt_dispatch(const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
                 const BnBwd& bb, const LazyArgs* lza, hipStream_t stream) {
   // cfg = tile + 10 * panel (1: resident, 2: streamed) + 100 * stages (0: three, 1: two, 2: four; a
   // four-stage request falls back to three where the counts or the LDS do not fit)
+  // + 1000 * family (fp32 only; 1: 32x64 wave tiles -- twice the waves of the 64x64 tiles for the
+  // small-M layers of small batches, where the 64x64 grid leaves SIMDs idle)
   const int bres = (cfg / 10) % 10 == 0 ? -1 : ((cfg / 10) % 10 == 1 ? 1 : 0);
   const int ns = (cfg / 100) % 10 == 1 ? 2 : ((cfg / 100) % 10 == 2 ? 4 : 3);
+  const int fam = (cfg / 1000) % 10;
   cfg %= 10;
   auto a = static_cast<const T*>(A);
   auto b = static_cast<const T*>(B);
   auto c = static_cast<T*>(C);
+  const int cfg_req = cfg;   // the 32x64 family checks its own tile widths
   if (cfg <= 0) cfg = N % 256 == 0 ? 3 : (N % 128 == 0 ? 2 : 1);
   // tiles (BM x BN, waves): 1 256x64 (4)  2 256x128 (8)  3 128x256 (8)  4 128x128 (4)
   //                         5 256x256 (8, 128x64 per wave)  6 256x128 (4, 128x64)  7 128x256 (4, 128x64)
@@ -1377,6 +1381,35 @@ int nt_dispatch(const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
         case 3: case 5: case 7: GK_NTA(2, 4, 4, false, true);
         case 4: case 6: GK_NTA(2, 2, 4, false, true);
         default: GK_NTA(4, 1, 4, false, true);
+      }
+    }
+  }
+  if constexpr (sizeof(T) == 4) {
+    if (fam == 1 && !lza) {
+      // 32x64 wave tiles: 1 128x64 (4 waves)  2 64x128 (4)  3 64x64 (2)  4 32x256 (4)  5 128x128 (8)
+      //                   6 64x256 (8)  7 32x128 (2)
+      static const int bn32[8] = {64, 64, 128, 64, 256, 128, 256, 128};
+      cfg = cfg_req;
+      if (cfg <= 0 || cfg > 7 || N % bn32[cfg] != 0) cfg = 1;
+      if (bb.h) {
+        switch (cfg) {
+          case 2: GK_NTA(2, 2, 2, true, false);
+          case 3: GK_NTA(2, 1, 2, true, false);
+          case 4: GK_NTA(1, 4, 2, true, false);
+          case 5: GK_NTA(4, 2, 2, true, false);
+          case 6: GK_NTA(2, 4, 2, true, false);
+          case 7: GK_NTA(1, 2, 2, true, false);
+          default: GK_NTA(4, 1, 2, true, false);
+        }
+      }
+      switch (cfg) {
+        case 2: GK_NTA(2, 2, 2, false, false);
+        case 3: GK_NTA(2, 1, 2, false, false);
+        case 4: GK_NTA(1, 4, 2, false, false);
+        case 5: GK_NTA(4, 2, 2, false, false);
+        case 6: GK_NTA(2, 4, 2, false, false);
+        case 7: GK_NTA(1, 2, 2, false, false);
+        default: GK_NTA(4, 1, 2, false, false);
       }
     }
   }

@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--top", type=int, default=60)
     ap.add_argument("--marker", default=None,
                     help="substring of a kernel launched once per step; only the last --steps steps are counted")
+    ap.add_argument("--sequence", default=None,
+                    help="also write the ordered dispatches of the LAST step (name, grid, us) to this CSV")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = c.execute("select name, start, end, grid_x, grid_y, grid_z, workgroup_x, vgpr_count, accum_vgpr_count, "
@@ -33,6 +35,14 @@ def main():
         marks = [i for i, r in enumerate(rows) if a.marker in r[0]]
         if len(marks) > a.steps:
             rows = rows[marks[-a.steps - 1] + 1:]
+    if a.sequence and a.marker:
+        marks = [i for i, r in enumerate(rows) if a.marker in r[0]]
+        last = rows[marks[-2] + 1:marks[-1] + 1] if len(marks) >= 2 else rows
+        with open(a.sequence, "w") as f:
+            f.write("i,us,grid,wg,kernel\n")
+            for i, (name, s, e, gx, gy, gz, wx, vg, ag, lds) in enumerate(last):
+                short = name.split("(")[0].replace("void ", "").replace("gk::(anonymous namespace)::", "gk::")
+                f.write('%d,%.1f,"%d,%d,%d",%d,"%s"\n' % (i, (e - s) / 1e3, gx // max(wx, 1), gy, gz, wx, short[:150]))
     per = collections.defaultdict(lambda: [0, 0.0, None])
     for name, s, e, gx, gy, gz, wx, vg, ag, lds in rows:
         p = per[name]

@@ -20,7 +20,7 @@ def test_optional_phase_records_error(bench, monkeypatch):
 
     def boom(holder):
         raise ValueError("bad shape\nsecond line")
-    assert bench.optional_phase("dense", out, 1, boom) is False
+    assert bench.optional_phase("dense", out, 1, boom) is True     # ranks can still agree: go on
     assert out["dense_error"] == "ValueError: bad shape"
 
 
@@ -28,7 +28,7 @@ def test_optional_phase_injection_and_success(bench, monkeypatch):
     out = {}
     ran = []
     monkeypatch.setenv("GKSGD_BENCH_FAIL_PHASE", "bf16")
-    assert bench.optional_phase("bf16", out, 1, lambda h: ran.append(1)) is False
+    assert bench.optional_phase("bf16", out, 1, lambda h: ran.append(1)) is True
     assert "injected failure" in out["bf16_error"] and not ran
     assert bench.optional_phase("ref_bs32", out, 1, lambda h: ran.append(1)) is True
     assert ran == [1] and "ref_bs32_error" not in out

@@ -28,7 +28,9 @@ def _tol(ref_abs):
 
 @pytest.mark.parametrize("M,N,K", [(1000, 64, 64), (4096, 256, 64), (777, 128, 192), (2048, 512, 128),
                                    (513, 192, 320), (300, 256, 1024)])
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 7, 11, 13, 22, 24, 101, 104, 201, 203])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 7, 11, 13, 22, 24, 101, 104, 201, 203,
+                                 # 32x64 wave tiles (family 1000): every tile, panels and stage counts
+                                 1001, 1002, 1003, 1004, 1005, 1006, 1007, 1011, 1022, 1103, 1205, 1217])
 def test_gemm_nt_f32(g, M, N, K, cfg):
     torch.manual_seed(M + N + K)
     A = torch.randn(M, K, device="cuda")
@@ -40,7 +42,7 @@ def test_gemm_nt_f32(g, M, N, K, cfg):
     assert err <= _tol(A.double().abs() @ B.double().abs().t()), err
 
 
-@pytest.mark.parametrize("cfg,mb", [(13, 1), (24, 3), (204, 7), (0, 5)])
+@pytest.mark.parametrize("cfg,mb", [(13, 1), (24, 3), (204, 7), (0, 5), (1001, 3), (1105, 2), (1003, 0), (1207, 9)])
 def test_gemm_nt_f32_few_blocks_bias_stats(g, cfg, mb):
     """Persistent blocks walking many tiles (partial last tile) with the bias
     and BatchNorm-statistics epilogues."""
@@ -87,7 +89,7 @@ CONV_CASES = [(2, 64, 9, 64, 3, 1, 1), (3, 128, 7, 64, 3, 2, 1), (2, 64, 14, 128
 
 
 @pytest.mark.parametrize("N,C,H,Co,k,s,p", CONV_CASES)
-@pytest.mark.parametrize("cfg", [0, 1, 3, 22, 104, 7, 204, 21])
+@pytest.mark.parametrize("cfg", [0, 1, 3, 22, 104, 7, 204, 21, 1001, 1002, 1104, 1007, 1016])
 def test_conv_nt_f32(g, N, C, H, Co, k, s, p, cfg):
     torch.manual_seed(N + C + H + Co)
     x, w = _conv_case(N, C, H, Co, k)
@@ -100,7 +102,7 @@ def test_conv_nt_f32(g, N, C, H, Co, k, s, p, cfg):
 
 
 @pytest.mark.parametrize("N,C,H,Co,k,s,p", [c for c in CONV_CASES if c[5] == 2])
-@pytest.mark.parametrize("cfg", [0, 1, 4, 13])
+@pytest.mark.parametrize("cfg", [0, 1, 4, 13, 1002, 1103])
 def test_conv_dgrad_s2_f32(g, N, C, H, Co, k, s, p, cfg):
     torch.manual_seed(N + 5 * C + H + Co)
     x, w = _conv_case(N, C, H, Co, k)
@@ -131,7 +133,8 @@ def test_conv_tn_acc_f32(g, N, C, H, Co, k, s, p, cfg, splits):
 
 @pytest.mark.parametrize("k", [1, 3])
 @pytest.mark.parametrize("twin", [False, True])
-def test_dgrad_bn_epilogue_f32(g, k, twin):
+@pytest.mark.parametrize("cfg", [4, 1002, 1003, 1105])
+def test_dgrad_bn_epilogue_f32(g, k, twin, cfg):
     """Grad-input with the BN-backward epilogue: dz = mask ? dX + dy2 : 0 and the
     partials sum(dz), sum(dz * h) -- fp32 operands, fp32 ReLU mask layout."""
     torch.manual_seed(k * 10 + twin)
@@ -155,12 +158,12 @@ def test_dgrad_bn_epilogue_f32(g, k, twin):
     zero = torch.zeros(64, device="cuda")
     if k == 1:
         rows = g.gemm_nt(dy.permute(0, 2, 3, 1).reshape(M, Co), w.reshape(Co, C).t().contiguous(),
-                         dz.permute(0, 2, 3, 1).reshape(M, C), 4, 0, st, None,
+                         dz.permute(0, 2, 3, 1).reshape(M, C), cfg, 0, st, None,
                          h.permute(0, 2, 3, 1).reshape(M, C),
                          dy2.permute(0, 2, 3, 1).reshape(M, C) if twin else None, mask)
     else:
         wf = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=CL)
-        rows = g.conv_nt(dy, wf, dz, zero, 1, p, 4, 0, st, None, h, dy2, mask)
+        rows = g.conv_nt(dy, wf, dz, zero, 1, p, cfg, 0, st, None, h, dy2, mask)
     assert (dz.double() - dz_ref).abs().max().item() <= 1e-5 * dz_ref.abs().max().item() + 1e-5
     s = st[:, :rows].double().sum(1)
     dzc = dz_ref.permute(0, 2, 3, 1).reshape(M, C)
