@@ -544,6 +544,15 @@ def main() -> int:
         phases[name] = info
         return info
 
+    # ---- secondary bf16 phase of an fp32 headline
+    if alive and amp == "fp32" and not args.no_bf16_phase:
+        def bf16_phase(holder):
+            i = timed(holder, "bf16", "bf16", args.dense, args.threshold, args.batch_size, args.steps, args.warmup)
+            out["bf16_ms_per_step"] = i["ms_per_step"]
+            out["bf16_value"] = i["value"]
+            out["bf16_exposed_comm_ms"] = i["exposed_comm_ms"]
+        alive = optional_phase("bf16", out, P, bf16_phase)
+
     # ---- dense comparator (N > 1): bucketed, backward-overlapped RCCL all-reduce
     dense_elems = max(1, int(args.dense_bucket_mb * 1e6 / 4))
     if alive and P > 1 and not args.dense and not args.no_dense_phase:
@@ -578,15 +587,6 @@ def main() -> int:
         alive = optional_phase(tag, out, P, ref_sparse)
         if alive:
             alive = optional_phase(tag + "_dense", out, P, ref_dense)
-
-    # ---- secondary bf16 phase of an fp32 headline
-    if alive and amp == "fp32" and not args.no_bf16_phase:
-        def bf16_phase(holder):
-            i = timed(holder, "bf16", "bf16", args.dense, args.threshold, args.batch_size, args.steps, args.warmup)
-            out["bf16_ms_per_step"] = i["ms_per_step"]
-            out["bf16_value"] = i["value"]
-            out["bf16_exposed_comm_ms"] = i["exposed_comm_ms"]
-        alive = optional_phase("bf16", out, P, bf16_phase)
 
     if rank == 0 and os.environ.get("GKSGD_GEMM_SAVE"):
         from gaussiank_sgd_amd.ops.conv1x1 import save_choices

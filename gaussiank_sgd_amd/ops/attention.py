@@ -4,12 +4,13 @@
 ``[B, T, 3 * heads * 64]`` (the ``[B, T, 3, heads, 64]`` layout of BERT's fused
 QKV linear) and returns ``softmax(q k^T / 8) -> dropout_p -> @ v`` merged back
 to ``[B, T, heads * 64]`` -- the input layout of the attention-output linear.
-On a GPU with bf16 activations this is one flash-style HIP kernel forward and
+On a GPU with bf16 activations (or fp32, the reference's precision:
+``csrc/kernels/attn_f32.hip`` on fp32 MFMA) this is one flash-style HIP kernel forward and
 two backward (dQ with ``delta = rowsum(dO * O)``, then dK / dV); nothing of
 size T x T is stored and there are no head split / merge copies: the kernels
 read q, k, v with the packed row stride and write ``dqkv`` in the projection's
 own layout.  The dropout mask is a hash of (seed, b*heads + h, query, key),
-regenerated in the backward.  Elsewhere (CPU, fp32, masks, other head dims)
+regenerated in the backward.  Elsewhere (CPU, masks, other head dims)
 it is ``F.scaled_dot_product_attention`` with identical semantics.
 
 Not in the reference (its model zoo has no transformer); BASELINE config 5
@@ -94,12 +95,47 @@ class _FlashAttnFn(torch.autograd.Function):
         return dqkv, None, None, None, None
 
 
+class _FlashAttnF32Fn(torch.autograd.Function):
+    """fp32 twin of _FlashAttnFn (csrc/kernels/attn_f32.hip): fp32 operands on
+    v_mfma_f32_16x16x4_f32, the same dropout hashes."""
+
+    @staticmethod
+    def forward(ctx, qkv, heads, p, seed, seed_dev=None):
+        B, T, _ = qkv.shape
+        out = torch.empty(B, T, heads * HEAD_DIM, dtype=torch.float32, device=qkv.device)
+        lse = torch.empty(B * heads * T, dtype=torch.float32, device=qkv.device)
+        _ops().attn_f32_fwd(qkv, out, lse, int(heads), float(p), int(seed), seed_dev)
+        ctx.save_for_backward(qkv, out, lse)
+        ctx.heads, ctx.p, ctx.seed, ctx.seed_dev = int(heads), float(p), int(seed), seed_dev
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, out, lse = ctx.saved_tensors
+        dout = dout.to(torch.float32).contiguous()
+        delta = torch.empty_like(lse)
+        dqkv = torch.empty_like(qkv)
+        _ops().attn_f32_bwd(qkv, out, dout, lse, delta, dqkv, ctx.heads, ctx.p, ctx.seed, ctx.seed_dev)
+        return dqkv, None, None, None, None
+
+
+def _compute_dtype(qkv: torch.Tensor):
+    if torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16:
+        return torch.bfloat16
+    return qkv.dtype if qkv.dtype in (torch.bfloat16, torch.float32) else None
+
+
 def fused_available(qkv: torch.Tensor, heads: int) -> bool:
+    """The HIP kernels take this call: bf16 (autocast or bf16 activations) or
+    fp32 (no autocast: the reference's precision), head dim 64, T % 128 == 0."""
     if not qkv.is_cuda or qkv.dim() != 3 or qkv.shape[-1] != 3 * heads * HEAD_DIM:
         return False
-    bf16 = qkv.dtype == torch.bfloat16 or (torch.is_autocast_enabled("cuda") and
-                                           torch.get_autocast_dtype("cuda") == torch.bfloat16)
-    return bf16 and load() and bool(_ops().attn_supported(qkv.shape[1], HEAD_DIM))
+    dt = _compute_dtype(qkv)
+    if dt is None or not load():
+        return False
+    if dt == torch.float32:
+        return bool(_ops().attn_f32_supported(qkv.shape[1], HEAD_DIM))
+    return bool(_ops().attn_supported(qkv.shape[1], HEAD_DIM))
 
 
 def _sdpa(qkv: torch.Tensor, heads: int, p: float, attn_mask=None) -> torch.Tensor:
@@ -119,5 +155,7 @@ def self_attention(qkv: torch.Tensor, heads: int, p: float = 0.0, training: bool
         if seed is None:
             seed = int(torch.randint(0, 2 ** 31 - 1, (1,), generator=seed_generator())) if p > 0 else 0
         seed_dev = capture_seed_word(qkv.device) if p > 0 else None
+        if _compute_dtype(qkv) == torch.float32:
+            return _FlashAttnF32Fn.apply(qkv.contiguous(), heads, p, seed, seed_dev)
         return _FlashAttnFn.apply(qkv.to(torch.bfloat16).contiguous(), heads, p, seed, seed_dev)
     return _sdpa(qkv, heads, p, attn_mask)

@@ -57,6 +57,7 @@ HIP_SOURCES = [
     "kernels/stem.hip",
     "kernels/wgrad3.hip",
     "kernels/attn.hip",
+    "kernels/attn_f32.hip",
     "kernels/embed.hip",
     "kernels/xent.hip",
     "kernels/winograd.hip",

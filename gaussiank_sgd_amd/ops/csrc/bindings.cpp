@@ -1497,6 +1497,44 @@ void attn_bwd(at::Tensor qkv, at::Tensor out, at::Tensor dout, at::Tensor lse, a
                cur_stream(qkv));
 }
 
+void check_attn32(const at::Tensor& t, const char* name, int64_t rows, int64_t cols) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == rows * cols &&
+                  reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+              name, " must be a contiguous 16-byte aligned fp32 GPU tensor of ", rows, " x ", cols, " elements");
+}
+
+void attn_f32_fwd(at::Tensor qkv, at::Tensor out, at::Tensor lse, int64_t heads, double p, int64_t seed,
+                  c10::optional<at::Tensor> seed_dev) {
+  TORCH_CHECK(qkv.dim() == 3 && qkv.size(2) == 3 * heads * 64, "qkv: [B, T, 3 * heads * 64]");
+  const int64_t B = qkv.size(0), T = qkv.size(1);
+  TORCH_CHECK(gk::attn_f32_supported((int)T, 64), "attn_f32: T must be a multiple of 128");
+  check_attn32(qkv, "qkv", B * T, 3 * heads * 64);
+  check_attn32(out, "out", B * T, heads * 64);
+  check_attn_f32(lse, "lse", B * heads * T);
+  TORCH_CHECK(p >= 0.0 && p < 1.0, "attn: dropout p in [0, 1)");
+  TORCH_CHECK(B * heads * T * (T / 2) < (int64_t(1) << 32), "attn: dropout hash index must fit 32 bits");
+  c10::DeviceGuard guard(qkv.device());
+  gk::attn_f32_fwd(qkv.data_ptr<float>(), out.data_ptr<float>(), lse.data_ptr<float>(), (int)B, (int)T, (int)heads,
+                   (float)p, (uint32_t)seed, seed_word(seed_dev), cur_stream(qkv));
+}
+
+void attn_f32_bwd(at::Tensor qkv, at::Tensor out, at::Tensor dout, at::Tensor lse, at::Tensor delta, at::Tensor dqkv,
+                  int64_t heads, double p, int64_t seed, c10::optional<at::Tensor> seed_dev) {
+  TORCH_CHECK(qkv.dim() == 3 && qkv.size(2) == 3 * heads * 64, "qkv: [B, T, 3 * heads * 64]");
+  const int64_t B = qkv.size(0), T = qkv.size(1);
+  TORCH_CHECK(gk::attn_f32_supported((int)T, 64), "attn_f32: T must be a multiple of 128");
+  check_attn32(qkv, "qkv", B * T, 3 * heads * 64);
+  check_attn32(dqkv, "dqkv", B * T, 3 * heads * 64);
+  check_attn32(out, "out", B * T, heads * 64);
+  check_attn32(dout, "dout", B * T, heads * 64);
+  check_attn_f32(lse, "lse", B * heads * T);
+  check_attn_f32(delta, "delta", B * heads * T);
+  c10::DeviceGuard guard(qkv.device());
+  gk::attn_f32_bwd(qkv.data_ptr<float>(), out.data_ptr<float>(), dout.data_ptr<float>(), lse.data_ptr<float>(),
+                   delta.data_ptr<float>(), dqkv.data_ptr<float>(), (int)B, (int)T, (int)heads, (float)p,
+                   (uint32_t)seed, seed_word(seed_dev), cur_stream(qkv));
+}
+
 void attn_dropout_mask(at::Tensor mask, int64_t B, int64_t heads, int64_t T, double p, int64_t seed,
                        c10::optional<at::Tensor> seed_dev) {
   TORCH_CHECK(mask.is_cuda() && mask.scalar_type() == at::kByte && mask.is_contiguous() &&
@@ -1507,12 +1545,6 @@ void attn_dropout_mask(at::Tensor mask, int64_t B, int64_t heads, int64_t T, dou
 }
 
 // linear-layer column passes (linear.hip): bias gradient / fused GELU backward
-void check_bf16_2d(const at::Tensor& t, const char* name) {
-  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 2 && t.is_contiguous() &&
-                  t.size(1) % 8 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
-              name, " must be a contiguous 16-byte aligned bf16 [M, N] GPU tensor with N % 8 == 0");
-}
-
 float* colsum_db(const c10::optional<at::Tensor>& db, int64_t N) {
   if (!db.has_value() || !db->defined()) return nullptr;
   TORCH_CHECK(db->is_cuda() && db->scalar_type() == at::kFloat && db->is_contiguous() && db->numel() == N,
@@ -1520,22 +1552,39 @@ float* colsum_db(const c10::optional<at::Tensor>& db, int64_t N) {
   return db->data_ptr<float>();
 }
 
+void check_col_2d(const at::Tensor& t, const char* name, at::ScalarType dt) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == dt && t.dim() == 2 && t.is_contiguous() && t.size(1) % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+              name, " must be a contiguous 16-byte aligned ", at::toString(dt),
+              " [M, N] GPU tensor with N % 8 == 0 (bf16 or fp32, all operands alike)");
+}
+
 void colsum_acc(at::Tensor dy, at::Tensor db) {
-  check_bf16_2d(dy, "dy");
+  const bool f32 = dy.scalar_type() == at::kFloat;
+  check_col_2d(dy, "dy", f32 ? at::kFloat : at::kBFloat16);
   float* d = colsum_db(db, dy.size(1));
   c10::DeviceGuard guard(dy.device());
-  gk::colsum_acc_bf16(static_cast<const uint16_t*>(dy.data_ptr()), d, dy.size(0), (int)dy.size(1), cur_stream(dy));
+  if (f32)
+    gk::colsum_acc_f32(dy.data_ptr<float>(), d, dy.size(0), (int)dy.size(1), cur_stream(dy));
+  else
+    gk::colsum_acc_bf16(static_cast<const uint16_t*>(dy.data_ptr()), d, dy.size(0), (int)dy.size(1), cur_stream(dy));
 }
 
 void gelu_bwd_colsum(at::Tensor dy, at::Tensor pre, at::Tensor dpre, c10::optional<at::Tensor> db) {
-  check_bf16_2d(dy, "dy");
-  check_bf16_2d(pre, "pre");
-  check_bf16_2d(dpre, "dpre");
+  const bool f32 = dy.scalar_type() == at::kFloat;
+  const auto dt = f32 ? at::kFloat : at::kBFloat16;
+  check_col_2d(dy, "dy", dt);
+  check_col_2d(pre, "pre", dt);
+  check_col_2d(dpre, "dpre", dt);
   TORCH_CHECK(pre.sizes() == dy.sizes() && dpre.sizes() == dy.sizes(), "gelu_bwd_colsum: shape mismatch");
   float* d = colsum_db(db, dy.size(1));
   c10::DeviceGuard guard(dy.device());
-  gk::gelu_bwd_colsum_bf16(static_cast<const uint16_t*>(dy.data_ptr()), static_cast<const uint16_t*>(pre.data_ptr()),
-                           static_cast<uint16_t*>(dpre.data_ptr()), d, dy.size(0), (int)dy.size(1), cur_stream(dy));
+  if (f32)
+    gk::gelu_bwd_colsum_f32(dy.data_ptr<float>(), pre.data_ptr<float>(), dpre.data_ptr<float>(), d, dy.size(0),
+                            (int)dy.size(1), cur_stream(dy));
+  else
+    gk::gelu_bwd_colsum_bf16(static_cast<const uint16_t*>(dy.data_ptr()), static_cast<const uint16_t*>(pre.data_ptr()),
+                             static_cast<uint16_t*>(dpre.data_ptr()), d, dy.size(0), (int)dy.size(1), cur_stream(dy));
 }
 
 // LSTM cell (lstm.hip)
@@ -1735,6 +1784,11 @@ TORCH_LIBRARY(gksgd, m) {
   m.def("attn_bwd(Tensor qkv, Tensor out, Tensor dout, Tensor lse, Tensor(a!) delta, Tensor(b!) dqkv, int heads, "
         "float p, int seed, Tensor? seed_dev=None) -> ()");
   m.def("attn_dropout_mask(Tensor(a!) mask, int B, int heads, int T, float p, int seed, Tensor? seed_dev=None) -> ()");
+  m.def("attn_f32_fwd(Tensor qkv, Tensor(a!) out, Tensor(b!) lse, int heads, float p, int seed, Tensor? seed_dev=None) -> ()");
+  m.def("attn_f32_bwd(Tensor qkv, Tensor out, Tensor dout, Tensor lse, Tensor(a!) delta, Tensor(b!) dqkv, int heads, "
+        "float p, int seed, Tensor? seed_dev=None) -> ()");
+  m.def("attn_f32_supported(int T, int D) -> bool",
+        [](int64_t T, int64_t D) { return gk::attn_f32_supported((int)T, (int)D); });
   m.def("add_ln_supported(int H) -> bool", &add_ln_supported);
   m.def("add_ln_ws_floats(int R, int H) -> int", &add_ln_ws_floats);
   m.def("xent_supported(int V) -> bool", &xent_supported);
@@ -1829,6 +1883,8 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("attn_fwd", &attn_fwd);
   m.impl("attn_bwd", &attn_bwd);
   m.impl("attn_dropout_mask", &attn_dropout_mask);
+  m.impl("attn_f32_fwd", &attn_f32_fwd);
+  m.impl("attn_f32_bwd", &attn_f32_bwd);
   m.impl("add_ln_forward", &add_ln_forward);
   m.impl("xent_forward", &xent_forward);
   m.impl("xent_backward", &xent_backward);

@@ -421,6 +421,12 @@ void wgrad3_acc(const void* dy, const void* x, const void* zero, int N, int H, i
 // (hash(*seed_dev, seed)) -- a captured graph draws a new mask every replay.
 // ---------------------------------------------------------------------------
 bool attn_supported(int T, int D);
+// fp32 variants (attn_f32.hip): same layouts, fp32 qkv / out / dout / dqkv
+bool attn_f32_supported(int T, int D);
+void attn_f32_fwd(const float* qkv, float* out, float* lse, int B, int T, int H, float p, uint32_t seed,
+                  const uint32_t* seed_dev, hipStream_t stream);
+void attn_f32_bwd(const float* qkv, const float* out, const float* dout, const float* lse, float* delta, float* dqkv,
+                  int B, int T, int H, float p, uint32_t seed, const uint32_t* seed_dev, hipStream_t stream);
 void attn_fwd(const void* qkv, void* out, float* lse, int B, int T, int H, float p, uint32_t seed,
               const uint32_t* seed_dev, hipStream_t stream);
 void attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* delta, void* dqkv, int B,
@@ -484,6 +490,9 @@ void add_ln_backward(const void* dy, const void* hsave, const float* mean, const
 void colsum_acc_bf16(const uint16_t* dy, float* db, int64_t M, int N, hipStream_t stream);
 void gelu_bwd_colsum_bf16(const uint16_t* dy, const uint16_t* pre, uint16_t* dpre, float* db, int64_t M, int N,
                           hipStream_t stream);
+void colsum_acc_f32(const float* dy, float* db, int64_t M, int N, hipStream_t stream);
+void gelu_bwd_colsum_f32(const float* dy, const float* pre, float* dpre, float* db, int64_t M, int N,
+                         hipStream_t stream);
 
 // ---------------------------------------------------------------------------
 // LSTM (lstm.hip), PyTorch gate order i, f, g, o.  Hp = H rounded up to 64.

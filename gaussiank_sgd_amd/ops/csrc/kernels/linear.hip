@@ -1,4 +1,4 @@
-// Column passes of bf16 linear layers (BERT encoder / MLM head, LSTM softmax),
+// Column passes of bf16 / fp32 linear layers (BERT encoder / MLM head, LSTM softmax),
 // accumulating straight into the optimizer's fp32 gradient arena:
 //   colsum_acc  db[n] += sum_m dy[m, n]                       (bias gradient)
 //   gelu_bwd    dpre = dy * gelu'(pre) (erf GELU, as F.gelu) and, with db,
@@ -8,9 +8,9 @@
 // (profiles/r01_bert_kernel_stats.csv: 49 calls, 1.3 ms per BERT step) plus a
 // cast-and-add into the fp32 arena; here it is a streaming pass at HBM rate.
 //
-// Layout: [M, N] row-major bf16, N % 8 == 0, rows 16-byte aligned.  Lane
+// Layout: [M, N] row-major bf16 or fp32, N % 8 == 0, rows 16-byte aligned.  Lane
 // (rl, cl) of a 256-thread block owns columns 8*cl .. 8*cl+7 of the block's
-// 256-column slab (one 16-byte load per row, kUnroll rows in flight) and rows
+// 256-column slab (one 16-byte load per row in bf16, two in fp32; kUnroll rows in flight) and rows
 // rl, rl + 8, ... of the block's row range.  The 8 row lanes' fp32 sums are
 // folded through LDS and each column receives ONE float atomic per block
 // (a wave's atomics cover 256 contiguous bytes: the full-rate shape).
@@ -41,11 +41,51 @@ __device__ __forceinline__ float gelu_grad(float x) {
   return fmaf(x, pdf, cdf);
 }
 
-template <bool GELU>
-__global__ __launch_bounds__(kBlock) void colsum_kernel(const uint16_t* __restrict__ dy,
-                                                        const uint16_t* __restrict__ pre,
-                                                        uint16_t* __restrict__ dpre, float* __restrict__ db,
-                                                        int64_t M, int N) {
+// 8 consecutive elements of a row as fp32, and back (bf16: one 16-byte
+// access, fp32: two)
+template <typename T>
+struct Row8;
+template <>
+struct Row8<uint16_t> {
+  static __device__ __forceinline__ void load(const uint16_t* p, float v[8]) {
+    const uint4 u = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      v[2 * h] = lo_bf(w[h]);
+      v[2 * h + 1] = hi_bf(w[h]);
+    }
+  }
+  // rounds v to the stored precision (the values the consumers read) and stores
+  static __device__ __forceinline__ void store(uint16_t* p, float v[8]) {
+    uint32_t w[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      w[h] = bf_bits(v[2 * h]) | (bf_bits(v[2 * h + 1]) << 16);
+      v[2 * h] = lo_bf(w[h]);
+      v[2 * h + 1] = hi_bf(w[h]);
+    }
+    *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+};
+template <>
+struct Row8<float> {
+  static __device__ __forceinline__ void load(const float* p, float v[8]) {
+    const float4 a = *reinterpret_cast<const float4*>(p);
+    const float4 b = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  static __device__ __forceinline__ void store(float* p, float v[8]) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+};
+
+template <bool GELU, typename T>
+__global__ __launch_bounds__(kBlock) void colsum_kernel(const T* __restrict__ dy, const T* __restrict__ pre,
+                                                        T* __restrict__ dpre, float* __restrict__ db, int64_t M,
+                                                        int N) {
   __shared__ float red[kRL][kCL * 8];
   const int cl = threadIdx.x % kCL, rl = threadIdx.x / kCL;
   const int c0 = (blockIdx.x * kCL + cl) * 8;
@@ -55,37 +95,28 @@ __global__ __launch_bounds__(kBlock) void colsum_kernel(const uint16_t* __restri
   if (c0 < N) {
     const int64_t step = (int64_t)gridDim.y * kRL;
     for (int64_t r = (int64_t)blockIdx.y * kRL + rl; r < M; r += kUnroll * step) {
-      uint4 u[kUnroll], p[kUnroll];
+      float u[kUnroll][8], q[kUnroll][8];
 #pragma unroll
       for (int j = 0; j < kUnroll; ++j) {
         const int64_t rr = r + j * step;
-        u[j] = make_uint4(0u, 0u, 0u, 0u);
-        p[j] = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) u[j][i] = q[j][i] = 0.f;
         if (rr < M) {
-          u[j] = *reinterpret_cast<const uint4*>(dy + rr * N + c0);
-          if (GELU) p[j] = *reinterpret_cast<const uint4*>(pre + rr * N + c0);
+          Row8<T>::load(dy + rr * N + c0, u[j]);
+          if (GELU) Row8<T>::load(pre + rr * N + c0, q[j]);
         }
       }
 #pragma unroll
       for (int j = 0; j < kUnroll; ++j) {
-        uint32_t w[4] = {u[j].x, u[j].y, u[j].z, u[j].w};
         if (GELU) {
-          const uint32_t q[4] = {p[j].x, p[j].y, p[j].z, p[j].w};
 #pragma unroll
-          for (int h = 0; h < 4; ++h) {
-            const float d0 = lo_bf(w[h]) * gelu_grad(lo_bf(q[h]));
-            const float d1 = hi_bf(w[h]) * gelu_grad(hi_bf(q[h]));
-            w[h] = bf_bits(d0) | (bf_bits(d1) << 16);
-          }
+          for (int i = 0; i < 8; ++i) u[j][i] *= gelu_grad(q[j][i]);
           const int64_t rr = r + j * step;
-          if (rr < M) *reinterpret_cast<uint4*>(dpre + rr * N + c0) = make_uint4(w[0], w[1], w[2], w[3]);
+          if (rr < M) Row8<T>::store(dpre + rr * N + c0, u[j]);   // u: now the stored values
         }
-        // sums of the values as stored (the bf16 the weight / input GEMMs consume)
+        // sums of the values as stored (what the weight / input GEMMs consume)
 #pragma unroll
-        for (int h = 0; h < 4; ++h) {
-          s[2 * h] += lo_bf(w[h]);
-          s[2 * h + 1] += hi_bf(w[h]);
-        }
+        for (int i = 0; i < 8; ++i) s[i] += u[j][i];
       }
     }
   }
@@ -102,9 +133,8 @@ __global__ __launch_bounds__(kBlock) void colsum_kernel(const uint16_t* __restri
   }
 }
 
-template <bool GELU>
-void launch_colsum(const uint16_t* dy, const uint16_t* pre, uint16_t* dpre, float* db, int64_t M, int N,
-                   hipStream_t s) {
+template <bool GELU, typename T>
+void launch_colsum(const T* dy, const T* pre, T* dpre, float* db, int64_t M, int N, hipStream_t s) {
   if (M <= 0 || N <= 0) return;
   const int gx = (int)ceil_div(N, kCL * 8);
   // >= two unrolled passes per lane; about eight blocks per CU in total
@@ -112,20 +142,30 @@ void launch_colsum(const uint16_t* dy, const uint16_t* pre, uint16_t* dpre, floa
   const int64_t cap = 2048 / gx > 0 ? 2048 / gx : 1;
   if (gy > cap) gy = cap;
   if (gy < 1) gy = 1;
-  hipLaunchKernelGGL((colsum_kernel<GELU>), dim3((unsigned)gx, (unsigned)gy), dim3(kBlock), 0, s, dy, pre, dpre, db,
-                     M, N);
+  hipLaunchKernelGGL((colsum_kernel<GELU, T>), dim3((unsigned)gx, (unsigned)gy), dim3(kBlock), 0, s, dy, pre, dpre,
+                     db, M, N);
 }
 
 }  // namespace
 
 void colsum_acc_bf16(const uint16_t* dy, float* db, int64_t M, int N, hipStream_t stream) {
   if (db == nullptr) return;
-  launch_colsum<false>(dy, nullptr, nullptr, db, M, N, stream);
+  launch_colsum<false, uint16_t>(dy, nullptr, nullptr, db, M, N, stream);
 }
 
 void gelu_bwd_colsum_bf16(const uint16_t* dy, const uint16_t* pre, uint16_t* dpre, float* db, int64_t M, int N,
                           hipStream_t stream) {
-  launch_colsum<true>(dy, pre, dpre, db, M, N, stream);
+  launch_colsum<true, uint16_t>(dy, pre, dpre, db, M, N, stream);
+}
+
+void colsum_acc_f32(const float* dy, float* db, int64_t M, int N, hipStream_t stream) {
+  if (db == nullptr) return;
+  launch_colsum<false, float>(dy, nullptr, nullptr, db, M, N, stream);
+}
+
+void gelu_bwd_colsum_f32(const float* dy, const float* pre, float* dpre, float* db, int64_t M, int N,
+                         hipStream_t stream) {
+  launch_colsum<true, float>(dy, pre, dpre, db, M, N, stream);
 }
 
 }  // namespace gk

@@ -19,7 +19,9 @@ fastest (cache and switches shared with the convolutions: ``GKSGD_GEMM_TUNE``,
 Dimensions that are not multiples of 64 (the LSTM's 1500 -> 10000 softmax
 layer) keep hipBLASLt for the GEMMs and still get the fused bias gradient.
 ``FastLinear`` is a drop-in ``nn.Linear`` (same parameters and state_dict
-keys); off the GPU or outside bf16 it is the stock layer (+ ``F.gelu``).
+keys).  fp32 inputs without autocast (the reference's precision) take the same
+path on the fp32 MFMA kernels (``v_mfma_f32_16x16x4_f32``) and the fp32 column
+pass; off the GPU it is the stock layer (+ ``F.gelu``).
 
 Reference parity: the reference's models use ``nn.Linear`` (models/fcn.py,
 models/lstm.py:29); BERT is not in the reference (BASELINE config 5).
@@ -44,7 +46,7 @@ def _g():
 
 
 def _colsum_ok(t: torch.Tensor) -> bool:
-    return (t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2 and t.is_contiguous() and
+    return (t.is_cuda and t.dtype in (torch.bfloat16, torch.float32) and t.dim() == 2 and t.is_contiguous() and
             t.shape[1] % 8 == 0 and t.data_ptr() % 16 == 0)
 
 
@@ -60,7 +62,7 @@ def bias_grad_acc_(db: torch.Tensor, dy: torch.Tensor) -> None:
 def gelu_backward_(dy: torch.Tensor, pre: torch.Tensor, db: Optional[torch.Tensor] = None) -> torch.Tensor:
     """dpre = dy * gelu'(pre) (erf GELU) in pre's dtype; with ``db`` (fp32 [N])
     also db += dpre.sum(0) -- one pass on the GPU."""
-    if _colsum_ok(dy) and _colsum_ok(pre) and dy.shape == pre.shape and \
+    if _colsum_ok(dy) and _colsum_ok(pre) and dy.shape == pre.shape and dy.dtype == pre.dtype and \
             (db is None or (db.dtype == torch.float32 and db.is_contiguous())):
         require_native(dy)
         dpre = torch.empty_like(pre)
@@ -78,23 +80,25 @@ def _hip_gemm_ok(K: int, N: int) -> bool:
 
 def _fwd(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor],
          b16: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """y = x2 . w^T (+ bias), bf16 out.  ``b16``: the bias already in bf16 (the
-    shadow arena's view) -- hipBLASLt then needs no per-call cast."""
+    """y = x2 . w^T (+ bias) in x2's dtype (bf16, or fp32: the fp32 MFMA
+    kernels).  ``b16``: the bias already in bf16 (the shadow arena's view) --
+    hipBLASLt then needs no per-call cast."""
     M, K = x2.shape
     N = w.shape[0]
+    dt = x2.dtype
     if b16 is None and bias is not None:
-        b16 = bias.to(torch.bfloat16)
+        b16 = bias.to(dt)
 
     def blas():
         return torch.addmm(b16, x2, w.t()) if b16 is not None else torch.mm(x2, w.t())
     if not _hip_gemm_ok(K, N):
         return blas()
     g = _g()
-    y = torch.empty(M, N, dtype=torch.bfloat16, device=x2.device)
+    y = torch.empty(M, N, dtype=dt, device=x2.device)
     cands = [(("hip", c, mb), (lambda c=c, mb=mb: g.gemm_nt(x2, w, y, c, mb, None, bias)))
-             for c in _cv._NT_CFGS for mb in _cv._NT_GRIDS]
+             for c in _cv._nt_cfgs(dt) for mb in _cv._NT_GRIDS]
     cands.append((("blas", 0, 0), blas))
-    ch = _cv._pick(("lin_fwd", M, K, N, bias is not None), cands)
+    ch = _cv._pick(("lin_fwd", M, K, N, bias is not None) + _cv._dkey(dt), cands)
     if ch[0] == "blas":
         return blas()
     g.gemm_nt(x2, w, y, ch[1], ch[2], None, bias)
@@ -102,18 +106,19 @@ def _fwd(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor],
 
 
 def _dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """dx = dy2 . w, bf16 out."""
+    """dx = dy2 . w in dy2's dtype."""
     M, N = dy2.shape
     K = w.shape[1]
-    key = ("lin_dgrad", M, K, N)
+    dt = dy2.dtype
+    key = ("lin_dgrad", M, K, N) + _cv._dkey(dt)
     got = _cv._choices.get(key)
     if not _hip_gemm_ok(K, N) or (got is not None and got[0] == "blas"):
         return torch.mm(dy2, w)
     g = _g()
-    dx = torch.empty(M, K, dtype=torch.bfloat16, device=dy2.device)
+    dx = torch.empty(M, K, dtype=dt, device=dy2.device)
     wt = w.t().contiguous()
     cands = [(("hip", c, mb), (lambda c=c, mb=mb: g.gemm_nt(dy2, wt, dx, c, mb)))
-             for c in _cv._NT_CFGS for mb in _cv._NT_GRIDS]
+             for c in _cv._nt_cfgs(dt) for mb in _cv._NT_GRIDS]
     cands.append((("blas", 0, 0), lambda: torch.mm(dy2, w)))
     ch = _cv._pick(key, cands)
     if ch[0] == "blas":
@@ -130,18 +135,23 @@ def _wgrad_into(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor) -> None:
     def blas(o):
         accum_grad_(o, torch.mm(dy2.t(), x2))
 
-    def blas32(o):   # hipBLASLt bf16 x bf16 -> fp32 with beta = 1, straight into the arena view
-        torch.addmm(o, dy2.t(), x2, out_dtype=torch.float32, out=o)
+    f32 = dy2.dtype == torch.float32
+
+    def blas32(o):   # hipBLASLt -> fp32 with beta = 1, straight into the arena view
+        if f32:
+            torch.addmm(o, dy2.t(), x2, out=o)
+        else:
+            torch.addmm(o, dy2.t(), x2, out_dtype=torch.float32, out=o)
     if not dy2.is_cuda:
         blas(out)
         return
     g = _g()
-    key = ("lin_wgrad", M, K, N)
+    key = ("lin_wgrad", M, K, N) + _cv._dkey(dy2.dtype)
     scratch = torch.zeros_like(out) if key not in _cv._choices else None
     cands = []
     if _hip_gemm_ok(K, N):
         cands = [(("hip", c, sp), (lambda c=c, sp=sp: g.gemm_tn_acc(dy2, x2, scratch, c, sp)))
-                 for c, sp in _cv._TN_CFGS]
+                 for c, sp in (_cv._TN_CFGS_F32 if f32 else _cv._TN_CFGS)]
     cands.append((("blas32", 0, 0), lambda: blas32(scratch)))
     cands.append((("blas", 0, 0), lambda: blas(scratch)))
     ch = _cv._pick(key, cands)
@@ -165,21 +175,23 @@ def _target(sink) -> Optional[torch.Tensor]:
 
 
 class _LinearFn(torch.autograd.Function):
-    """y = act(x . W^T + b) with bf16 operands.  ``weight`` / ``bias`` are the
-    fp32 master parameters; with sinks (bf16-shadow path, parallel/shadow.py)
-    their gradients are added into the optimizer's fp32 arena in the backward
-    and None is returned for them, so AccumulateGrad launches nothing (its
-    post-accumulate hook still reports the parameter ready)."""
+    """y = act(x . W^T + b) with bf16 operands (``dt`` bf16) or fp32 operands
+    (``dt`` fp32: the reference's precision, fp32 MFMA kernels).  ``weight`` /
+    ``bias`` are the fp32 master parameters; with sinks (bf16-shadow path or
+    fp32 direct-gradient path, parallel/shadow.py) their gradients are added
+    into the optimizer's fp32 arena in the backward and None is returned for
+    them, so AccumulateGrad launches nothing (its post-accumulate hook still
+    reports the parameter ready)."""
 
     @staticmethod
-    def forward(ctx, x, weight, w_bf16, wsink, bias, bsink, gelu, b_bf16=None):
+    def forward(ctx, x, weight, w_bf16, wsink, bias, bsink, gelu, b_bf16=None, dt=torch.bfloat16):
         shape = x.shape
         K = shape[-1]
         x2 = x.reshape(-1, K)
-        if x2.dtype != torch.bfloat16:
-            x2 = x2.to(torch.bfloat16)
+        if x2.dtype != dt:
+            x2 = x2.to(dt)
         x2 = x2.contiguous()
-        w = w_bf16 if w_bf16 is not None else weight.detach().to(torch.bfloat16)
+        w = w_bf16 if w_bf16 is not None else weight.detach().to(dt)
         w = w.contiguous()
         b = bias.detach().float().contiguous() if bias is not None else None
         y = _fwd(x2, w, b, b_bf16)
@@ -199,8 +211,8 @@ class _LinearFn(torch.autograd.Function):
         x2, w, pre = ctx.saved_tensors
         N, K = w.shape
         dy2 = dy.reshape(-1, N)
-        if dy2.dtype != torch.bfloat16:
-            dy2 = dy2.to(torch.bfloat16)
+        if dy2.dtype != x2.dtype:
+            dy2 = dy2.to(x2.dtype)
         dy2 = dy2.contiguous()
         db = gbias = None
         if ctx.has_bias and ctx.needs_input_grad[4]:
@@ -232,7 +244,7 @@ class _LinearFn(torch.autograd.Function):
                 gbias = None
             else:
                 gbias = gbias.to(ctx.bdtype)
-        return dx, gweight, None, None, gbias, None, None, None
+        return dx, gweight, None, None, gbias, None, None, None, None
 
 
 def _supported(x: torch.Tensor, mod: nn.Linear) -> bool:
@@ -250,8 +262,20 @@ class FastLinear(nn.Linear):
         if act not in (None, "gelu"):
             raise ValueError("FastLinear act must be None or 'gelu', got %r" % (act,))
         dev = x.device.type
-        bf16 = x.dtype == torch.bfloat16 or (torch.is_autocast_enabled(dev) and
-                                             torch.get_autocast_dtype(dev) == torch.bfloat16)
+        autocast = torch.is_autocast_enabled(dev)
+        bf16 = x.dtype == torch.bfloat16 or (autocast and torch.get_autocast_dtype(dev) == torch.bfloat16)
+        f32 = not autocast and x.dtype == torch.float32 and os.environ.get("GKSGD_FASTLINEAR_F32", "1") != "0"
+        if f32 and _supported(x, self) and load():
+            # fp32 (the reference's precision): fp32 MFMA GEMMs, weight / bias
+            # gradients straight into the fp32 arena (install_direct_grads)
+            table = getattr(self, "_gk_direct_grads", None) or {}
+            wsink, bsink = table.get("weight"), table.get("bias")
+            if not torch.is_grad_enabled() or not self.weight.requires_grad:
+                wsink = None
+            if not torch.is_grad_enabled() or self.bias is None or not self.bias.requires_grad:
+                bsink = None
+            return _LinearFn.apply(x, self.weight, None, wsink, self.bias, bsink, act == "gelu", None,
+                                   torch.float32)
         if bf16 and _supported(x, self) and load():
             table = getattr(self, "_gk_shadow", None)
             winfo = table.get("weight") if table else None

@@ -146,7 +146,8 @@ def install_direct_grads(model: nn.Module, opt) -> int:
     fp32 weights, activations and gradients, settings.py:28): no shadow
     weights, but the hand-written kernels add their weight gradients straight
     into the optimizer's fp32 gradient arena -- FastConv2d's grad-weight GEMM
-    (ops/conv1x1.py fp32 path), the fp32 stem (ops/stem.py) and BNAct's
+    (ops/conv1x1.py fp32 path), FastLinear's (ops/linear.py fp32 path), the
+    fp32 stem (ops/stem.py) and BNAct's
     backward (gamma / beta) -- so
     AccumulateGrad launches nothing for them.  Returns the number of
     parameters on the direct path."""
@@ -154,7 +155,7 @@ def install_direct_grads(model: nn.Module, opt) -> int:
     names = opt._parameter_names
     count = 0
     for mod in model.modules():
-        if isinstance(mod, (FastConv2d, StemConv)):
+        if isinstance(mod, (FastConv2d, StemConv, FastLinear)):
             table = {}
             for pname in ("weight", "bias"):
                 p = getattr(mod, pname, None)

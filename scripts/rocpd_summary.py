@@ -41,7 +41,7 @@ def main():
         with open(a.sequence, "w") as f:
             f.write("i,us,grid,wg,kernel\n")
             for i, (name, s, e, gx, gy, gz, wx, vg, ag, lds) in enumerate(last):
-                short = name.split("(")[0].replace("void ", "").replace("gk::(anonymous namespace)::", "gk::")
+                short = name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
                 f.write('%d,%.1f,"%d,%d,%d",%d,"%s"\n' % (i, (e - s) / 1e3, gx // max(wx, 1), gy, gz, wx, short[:150]))
     per = collections.defaultdict(lambda: [0, 0.0, None])
     for name, s, e, gx, gy, gz, wx, vg, ag, lds in rows:

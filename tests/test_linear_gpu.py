@@ -158,3 +158,98 @@ def test_bert_tiny_step_bf16(cuda):
     assert sum(int(b.bufs.record[0]) for b in opt.arena.buckets) > 0
     assert min(losses[-5:]) < losses[0]
 
+
+
+# ---- fp32 path (no autocast: the reference's precision) --------------------
+@pytest.mark.parametrize("M,N", [(1000, 264), (37, 8), (4096, 768)])
+def test_colsum_acc_f32(M, N):
+    from gaussiank_sgd_amd.ops.linear import bias_grad_acc_
+    torch.manual_seed(M + N)
+    dy = torch.randn(M, N, device="cuda")
+    db = torch.randn(N, device="cuda")
+    ref = db.double() + dy.double().sum(0)
+    bias_grad_acc_(db, dy)
+    assert (db.double() - ref).abs().max().item() <= 2e-6 * M + 1e-5
+
+
+@pytest.mark.parametrize("M,N", [(1000, 264), (512, 3072)])
+def test_gelu_backward_colsum_f32(M, N):
+    from gaussiank_sgd_amd.ops.linear import gelu_backward_
+    torch.manual_seed(M + N)
+    pre = torch.randn(M, N, device="cuda") * 2
+    dy = torch.randn(M, N, device="cuda")
+    db = torch.zeros(N, device="cuda")
+    dpre = gelu_backward_(dy, pre, db)
+    ref = torch.ops.aten.gelu_backward(dy.double(), pre.double())
+    assert dpre.dtype == torch.float32
+    assert (dpre.double() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+    assert (db.double() - ref.sum(0)).abs().max().item() <= 2e-6 * M + 1e-5
+
+
+def _check_linear_f32(M, K, N, act, bias):
+    from gaussiank_sgd_amd.ops import conv1x1
+    from gaussiank_sgd_amd.ops.linear import FastLinear
+    torch.manual_seed(M + K + N)
+    m = FastLinear(K, N, bias=bias).cuda()
+    if bias:
+        torch.nn.init.uniform_(m.bias, -1.0, 1.0)
+    x = torch.randn(3, M, K, device="cuda").requires_grad_(True)
+    y = m(x, act=act)
+    assert y.dtype == torch.float32 and y.shape == (3, M, N)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr = x.detach().double().requires_grad_(True)
+    wr = m.weight.detach().double().requires_grad_(True)
+    br = m.bias.detach().double().requires_grad_(True) if bias else None
+    yr = F.linear(xr, wr, br)
+    if act == "gelu":
+        yr = F.gelu(yr)
+    yr.backward(dy.double())
+    tol = lambda r: 1e-5 * r.abs().max().item() + 1e-5  # noqa: E731
+    assert (y.double() - yr).abs().max().item() <= tol(yr)
+    assert (x.grad.double() - xr.grad).abs().max().item() <= tol(xr.grad)
+    assert (m.weight.grad.double() - wr.grad).abs().max().item() <= tol(wr.grad)
+    if bias:
+        assert (m.bias.grad.double() - br.grad).abs().max().item() <= tol(br.grad)
+    keys = [k for k in conv1x1.tuned_choices() if k[0].startswith("lin_") and "f32" in k]
+    assert keys, "fp32 linear path not taken"
+
+
+@pytest.mark.parametrize("M,K,N,act,bias", [(300, 128, 192, None, True), (517, 64, 256, "gelu", True),
+                                            (128, 256, 64, None, False), (200, 768, 2304, None, True)])
+def test_fastlinear_f32_hip_vs_fp64(M, K, N, act, bias, hip_only):
+    _check_linear_f32(M, K, N, act, bias)
+
+
+def test_fastlinear_f32_autotuned_and_direct_arena():
+    """Autotuned fp32 linears; through DistributedOptimizer + install_direct_grads
+    the fp32 weight / bias gradients go straight into the arena."""
+    from gaussiank_sgd_amd.compression import compressors
+    from gaussiank_sgd_amd.ops.linear import FastLinear
+    from gaussiank_sgd_amd.parallel import comm, install_direct_grads
+    from gaussiank_sgd_amd.parallel.distributed_optimizer import DistributedOptimizer
+    _check_linear_f32(300, 128, 192, "gelu", True)
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = FastLinear(128, 256)
+            self.b = FastLinear(256, 64)
+
+        def forward(self, x):
+            return self.b(self.a(x, act="gelu"))
+    comm.init()
+    torch.manual_seed(0)
+    net = Net().cuda()
+    ref = copy.deepcopy(net)
+    opt = DistributedOptimizer(torch.optim.SGD(net.parameters(), lr=0.1), named_parameters=net.named_parameters(),
+                               compression=compressors["none"], is_sparse=False, density=1.0)
+    assert install_direct_grads(net, opt) == 4
+    x = torch.randn(200, 128, device="cuda")
+    for model in (net, ref):
+        model(x).square().mean().backward()
+    torch.cuda.synchronize()
+    for (n, p), (_, q) in zip(net.named_parameters(), ref.named_parameters()):
+        assert p.grad is not None, n
+        err = (p.grad - q.grad).abs().max().item()
+        assert err <= 1e-5 * q.grad.abs().max().item() + 1e-6, (n, err)
