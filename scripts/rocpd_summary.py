@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--top", type=int, default=60)
     ap.add_argument("--marker", default=None,
                     help="substring of a kernel launched once per step; only the last --steps steps are counted")
+    ap.add_argument("--marker-per-step", type=int, default=1,
+                    help="dispatches of the marker kernel per step (e.g. 12 for a per-layer BERT kernel)")
     ap.add_argument("--sequence", default=None,
                     help="also write the ordered dispatches of the LAST step (name, grid, us) to this CSV")
     a = ap.parse_args()
@@ -33,6 +35,8 @@ def main():
                      "lds_size from kernels order by start").fetchall()
     if a.marker:
         marks = [i for i, r in enumerate(rows) if a.marker in r[0]]
+        nper = max(1, a.marker_per_step)
+        marks = marks[nper - 1::nper]   # the last marker dispatch of every step
         if len(marks) > a.steps:
             rows = rows[marks[-a.steps - 1] + 1:]
     if a.sequence and a.marker:
