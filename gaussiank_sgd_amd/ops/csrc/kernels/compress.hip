@@ -688,12 +688,14 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const float* __restrict__
                                                        const uint32_t* __restrict__ seed_dev, DecArgs da) {
   if (cond && ctrl->fallback == 0) return;
   if (seed_dev != nullptr) seed = __builtin_amdgcn_readfirstlane(*seed_dev);
-  // Wave-uniform counters: every (element, candidate) test is ONE v_cmp whose
-  // 64-bit lane mask is popcounted and accumulated on the SCALAR unit
-  // (s_bcnt1 + s_add), instead of a compare + conditional add per lane --
-  // no cross-lane reduction at the end.  NC (>= the live candidate count,
-  // chosen by the host from the mode) is a compile-time bound: no per-test
-  // branch; dead candidates carry bound 0xffffffff and count nothing.
+  // Per-lane counters: every (element, candidate) test is a compare + carry-in
+  // add on the VALU (v_cmp + v_addc), summed over the wave once per block.
+  // (Round 3 accumulated ballots on the scalar unit instead -- one s_bcnt1 +
+  // s_add per test, serialised behind each v_cmp's SGPR write: 40 us for the
+  // 6-candidate Gaussian ladder on a 25.6 M bucket, half the HBM rate.)  NC
+  // (>= the live candidate count, chosen by the host from the mode) is a
+  // compile-time bound: no per-test branch; dead candidates carry bound
+  // 0xffffffff and count nothing.
   uint32_t bnd[NC];
 #pragma unroll
   for (int j = 0; j < NC; ++j) bnd[j] = __builtin_amdgcn_readfirstlane(ctrl->bound[j]);
@@ -725,11 +727,9 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const float* __restrict__
         for (int j4 = 0; j4 < 4; ++j4) {
           const uint32_t k4[4] = {abs_key(cu[j4].x), abs_key(cu[j4].y), abs_key(cu[j4].z), abs_key(cu[j4].w)};
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
+          for (int q = 0; q < 4; ++q)
 #pragma unroll
-            for (int j = 0; j < NC; ++j) cnt[j] += (uint32_t)__popcll(__ballot(k4[q] >= bnd[j]));
-            __builtin_amdgcn_sched_barrier(0);   // accumulate per element: no SGPR spills
-          }
+            for (int j = 0; j < NC; ++j) cnt[j] += k4[q] >= bnd[j] ? 1u : 0u;
         }
       }
     }
@@ -769,15 +769,16 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const float* __restrict__
         }
       }
     }
-    // no lane-divergent branch around the ballots: the counters are wave-uniform
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const bool in = (inb >> q) & 1u;
 #pragma unroll
-      for (int j = 0; j < NC; ++j) cnt[j] += (uint32_t)__popcll(__ballot(in && key[q] >= bnd[j]));
-      __builtin_amdgcn_sched_barrier(0);
+      for (int j = 0; j < NC; ++j) cnt[j] += (in && key[q] >= bnd[j]) ? 1u : 0u;
     }
   }
+  // per-lane counts -> per-wave totals (one reduction per block)
+#pragma unroll
+  for (int j = 0; j < NC; ++j) cnt[j] = wave_sum(cnt[j]);
   __shared__ uint32_t sh[kWavesPerBlock][NC];
   if (lane_id() == 0) {
 #pragma unroll

@@ -62,6 +62,24 @@ def _env_flag(name: str, default: bool) -> bool:
     return v.strip().lower() in ("1", "true", "yes", "on")
 
 
+# ONE high-priority communication stream per device, shared by every
+# DistributedOptimizer of the process.  torch.cuda.Stream(priority=-1) hands
+# out the next stream of the high-priority pool on every call, and HIP maps
+# streams onto GPU_MAX_HW_QUEUES (4) hardware queues round-robin: a process
+# that builds several optimizers (bench.py's phases, a re-created trainer)
+# ends up with a comm stream that shares the compute stream's hardware queue,
+# which measured 34-100 % slower steps afterwards (profiles/r04_phase_order.txt).
+_COMM_STREAMS: Dict[int, "torch.cuda.Stream"] = {}
+
+
+def _comm_stream_for(dev: torch.device) -> "torch.cuda.Stream":
+    i = dev.index if dev.index is not None else torch.cuda.current_device()
+    s = _COMM_STREAMS.get(i)
+    if s is None:
+        s = _COMM_STREAMS[i] = torch.cuda.Stream(device=i, priority=-1)
+    return s
+
+
 class _DistributedOptimizer(torch.optim.Optimizer):
     def __init__(self, params, named_parameters, compression, is_sparse=False, density=0.001,
                  seq_layernames=None, layerwise_times=None, norm_clip=None, threshold=0, writer=None,
@@ -249,7 +267,7 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         # GKSGD_COMM_STREAM=0: compression / exchange inline on the compute stream
         # (no overlap; a single-stream step, e.g. for whole-step graph capture)
         if self._is_cuda and self._hooks_on and os.environ.get("GKSGD_COMM_STREAM", "1") != "0":
-            self._comm_stream = torch.cuda.Stream(device=dev, priority=-1)
+            self._comm_stream = _comm_stream_for(dev)
         comp = self._compression
         self._fused_sparse = self._sparse and getattr(comp, "fused", False) and not getattr(comp, "dense", False)
         max_density = max([self._density] + (self._dynamic_densities or []))
