@@ -1606,10 +1606,11 @@ int64_t lstm_partials(const c10::optional<at::Tensor>& P, int64_t S, int64_t B, 
   return P->size(2) / gates_mult;
 }
 
-uint16_t* lstm_pad(const c10::optional<at::Tensor>& t, int64_t rows, int64_t cols, const char* name) {
+void* lstm_pad(const c10::optional<at::Tensor>& t, int64_t rows, int64_t cols, const char* name,
+               at::ScalarType dt = at::kBFloat16) {
   if (!(t.has_value() && t->defined())) return nullptr;
-  check_lstm(*t, at::kBFloat16, rows * cols, name);
-  return static_cast<uint16_t*>(t->data_ptr());
+  check_lstm(*t, dt, rows * cols, name);
+  return t->data_ptr();
 }
 
 // Split-K recurrent GEMM: P[s] = A[:, slice s] B[:, slice s]^T, A [M, K], B [N, K] (bf16, row-major)
@@ -1617,35 +1618,50 @@ void lstm_rec_gemm(at::Tensor A, at::Tensor Bm, at::Tensor P, int64_t S) {
   TORCH_CHECK(A.dim() == 2 && Bm.dim() == 2 && A.size(1) == Bm.size(1), "A [M, K] and B [N, K] expected");
   const int64_t M = A.size(0), K = A.size(1), N = Bm.size(0);
   TORCH_CHECK(S >= 1 && K % (64 * S) == 0 && N % 64 == 0, "lstm_rec_gemm: K % (64 S) and N % 64 must be 0");
-  TORCH_CHECK(A.is_cuda() && A.scalar_type() == at::kBFloat16 && A.stride(1) == 1 && A.stride(0) % 8 == 0 &&
-                  Bm.is_cuda() && Bm.scalar_type() == at::kBFloat16 && Bm.stride(1) == 1 && Bm.stride(0) % 8 == 0,
-              "lstm_rec_gemm: bf16 GPU operands with unit column stride and 16-byte aligned rows");
+  const bool f32 = A.scalar_type() == at::kFloat;
+  const auto dt = f32 ? at::kFloat : at::kBFloat16;
+  const int64_t al = f32 ? 4 : 8;   // elements per 16 bytes
+  TORCH_CHECK(A.is_cuda() && A.scalar_type() == dt && A.stride(1) == 1 && A.stride(0) % al == 0 &&
+                  Bm.is_cuda() && Bm.scalar_type() == dt && Bm.stride(1) == 1 && Bm.stride(0) % al == 0,
+              "lstm_rec_gemm: bf16 or fp32 GPU operands (both alike) with unit column stride and 16-byte aligned rows");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(Bm.data_ptr()) % 16 == 0,
               "lstm_rec_gemm: 16-byte aligned operands");
   check_lstm(P, at::kFloat, S * M * N, "P");
   c10::DeviceGuard guard(A.device());
-  gk::lstm_rec_gemm(static_cast<const uint16_t*>(A.data_ptr()), A.stride(0), static_cast<const uint16_t*>(Bm.data_ptr()),
-                    Bm.stride(0), P.data_ptr<float>(), (int)M, (int)N, (int)K, (int)S, cur_stream(A));
+  if (f32)
+    gk::lstm_rec_gemm_f32(A.data_ptr<float>(), A.stride(0), Bm.data_ptr<float>(), Bm.stride(0), P.data_ptr<float>(),
+                          (int)M, (int)N, (int)K, (int)S, cur_stream(A));
+  else
+    gk::lstm_rec_gemm(static_cast<const uint16_t*>(A.data_ptr()), A.stride(0),
+                      static_cast<const uint16_t*>(Bm.data_ptr()), Bm.stride(0), P.data_ptr<float>(), (int)M, (int)N,
+                      (int)K, (int)S, cur_stream(A));
 }
 
 void lstm_cell_fwd(at::Tensor xg, c10::optional<at::Tensor> hg, c10::optional<at::Tensor> P, int64_t S, at::Tensor c_prev, at::Tensor c,
                    at::Tensor h, c10::optional<at::Tensor> h_pad, at::Tensor gates) {
   TORCH_CHECK(xg.dim() == 2 && xg.size(1) % 4 == 0, "xg must be [B, 4H]");
   const int64_t B = xg.size(0), H = xg.size(1) / 4;
-  check_lstm(xg, at::kBFloat16, B * 4 * H, "xg");
+  const bool f32 = xg.scalar_type() == at::kFloat;
+  const auto dt = f32 ? at::kFloat : at::kBFloat16;   // xg / hg / h / h_pad storage (bf16 or fp32 alike)
+  check_lstm(xg, dt, B * 4 * H, "xg");
   check_lstm(c_prev, at::kFloat, B * H, "c_prev");
   check_lstm(c, at::kFloat, B * H, "c");
-  check_lstm(h, at::kBFloat16, B * H, "h");
+  check_lstm(h, dt, B * H, "h");
   check_lstm(gates, at::kFloat, B * 4 * H, "gates");
   const float* pp = nullptr;
   int64_t Hp = lstm_partials(P, S, B, H, 4, &pp);
   if (!pp) S = 0, Hp = (H + 63) / 64 * 64;
-  uint16_t* hp = lstm_pad(h_pad, B, Hp, "h_pad");
-  const uint16_t* ph = lstm_pad(hg, B, 4 * H, "hg");
+  void* hp = lstm_pad(h_pad, B, Hp, "h_pad", dt);
+  const void* ph = lstm_pad(hg, B, 4 * H, "hg", dt);
   c10::DeviceGuard guard(xg.device());
-  gk::lstm_cell_fwd(static_cast<const uint16_t*>(xg.data_ptr()), ph, pp, (int)S, c_prev.data_ptr<float>(),
-                    c.data_ptr<float>(), static_cast<uint16_t*>(h.data_ptr()), hp, gates.data_ptr<float>(), (int)B,
-                    (int)H, (int)Hp, cur_stream(xg));
+  if (f32)
+    gk::lstm_cell_fwd_f32(xg.data_ptr<float>(), static_cast<const float*>(ph), pp, (int)S, c_prev.data_ptr<float>(),
+                          c.data_ptr<float>(), h.data_ptr<float>(), static_cast<float*>(hp), gates.data_ptr<float>(),
+                          (int)B, (int)H, (int)Hp, cur_stream(xg));
+  else
+    gk::lstm_cell_fwd(static_cast<const uint16_t*>(xg.data_ptr()), static_cast<const uint16_t*>(ph), pp, (int)S,
+                      c_prev.data_ptr<float>(), c.data_ptr<float>(), static_cast<uint16_t*>(h.data_ptr()),
+                      static_cast<uint16_t*>(hp), gates.data_ptr<float>(), (int)B, (int)H, (int)Hp, cur_stream(xg));
 }
 
 void lstm_cell_bwd(c10::optional<at::Tensor> dout, c10::optional<at::Tensor> dh_rec, c10::optional<at::Tensor> P,
@@ -1654,16 +1670,18 @@ void lstm_cell_bwd(c10::optional<at::Tensor> dout, c10::optional<at::Tensor> dh_
                    c10::optional<at::Tensor> dG_pad, at::Tensor dc_prev) {
   TORCH_CHECK(gates.dim() == 2 && gates.size(1) % 4 == 0, "gates must be [B, 4H]");
   const int64_t B = gates.size(0), H = gates.size(1) / 4;
+  const bool f32 = dG.scalar_type() == at::kFloat;
+  const auto dt = f32 ? at::kFloat : at::kBFloat16;   // dout / dh_rec / dG / dG_pad storage
   check_lstm(gates, at::kFloat, B * 4 * H, "gates");
   check_lstm(c, at::kFloat, B * H, "c");
   check_lstm(c_prev, at::kFloat, B * H, "c_prev");
-  check_lstm(dG, at::kBFloat16, B * 4 * H, "dG");
+  check_lstm(dG, dt, B * 4 * H, "dG");
   check_lstm(dc_prev, at::kFloat, B * H, "dc_prev");
-  const uint16_t* po = nullptr;
+  const void* po = nullptr;
   const float* pc = nullptr;
   if (dout.has_value() && dout->defined()) {
-    check_lstm(*dout, at::kBFloat16, B * H, "dout");
-    po = static_cast<const uint16_t*>(dout->data_ptr());
+    check_lstm(*dout, dt, B * H, "dout");
+    po = dout->data_ptr();
   }
   if (dc_next.has_value() && dc_next->defined()) {
     check_lstm(*dc_next, at::kFloat, B * H, "dc_next");
@@ -1672,12 +1690,18 @@ void lstm_cell_bwd(c10::optional<at::Tensor> dout, c10::optional<at::Tensor> dh_
   const float* pp = nullptr;
   int64_t Hp = lstm_partials(P, S, B, H, 1, &pp);
   if (!pp) S = 0, Hp = (H + 63) / 64 * 64;
-  uint16_t* gp = lstm_pad(dG_pad, B, 4 * Hp, "dG_pad");
-  const uint16_t* pr = lstm_pad(dh_rec, B, H, "dh_rec");
+  void* gp = lstm_pad(dG_pad, B, 4 * Hp, "dG_pad", dt);
+  const void* pr = lstm_pad(dh_rec, B, H, "dh_rec", dt);
   c10::DeviceGuard guard(gates.device());
-  gk::lstm_cell_bwd(po, pr, pp, (int)S, pc, gates.data_ptr<float>(), c.data_ptr<float>(), c_prev.data_ptr<float>(),
-                    static_cast<uint16_t*>(dG.data_ptr()), gp, dc_prev.data_ptr<float>(), (int)B, (int)H, (int)Hp,
-                    cur_stream(gates));
+  if (f32)
+    gk::lstm_cell_bwd_f32(static_cast<const float*>(po), static_cast<const float*>(pr), pp, (int)S, pc,
+                          gates.data_ptr<float>(), c.data_ptr<float>(), c_prev.data_ptr<float>(), dG.data_ptr<float>(),
+                          static_cast<float*>(gp), dc_prev.data_ptr<float>(), (int)B, (int)H, (int)Hp, cur_stream(gates));
+  else
+    gk::lstm_cell_bwd(static_cast<const uint16_t*>(po), static_cast<const uint16_t*>(pr), pp, (int)S, pc,
+                      gates.data_ptr<float>(), c.data_ptr<float>(), c_prev.data_ptr<float>(),
+                      static_cast<uint16_t*>(dG.data_ptr()), static_cast<uint16_t*>(gp), dc_prev.data_ptr<float>(),
+                      (int)B, (int)H, (int)Hp, cur_stream(gates));
 }
 
 }  // namespace

@@ -512,5 +512,13 @@ void lstm_cell_fwd(const uint16_t* xg, const uint16_t* hg, const float* P, int S
 void lstm_cell_bwd(const uint16_t* dout, const uint16_t* dh_rec, const float* P, int S, const float* dc_next, const float* gates,
                    const float* c, const float* c_prev, uint16_t* dG, uint16_t* dG_pad, float* dc_prev, int B, int H,
                    int Hp, hipStream_t stream);
+// fp32 variants (the reference's precision): fp32 operands, same layouts
+void lstm_rec_gemm_f32(const float* A, int64_t lda, const float* B, int64_t ldb, float* P, int M, int N, int K, int S,
+                       hipStream_t stream);
+void lstm_cell_fwd_f32(const float* xg, const float* hg, const float* P, int S, const float* c_prev, float* c, float* h,
+                       float* h_pad, float* gates, int B, int H, int Hp, hipStream_t stream);
+void lstm_cell_bwd_f32(const float* dout, const float* dh_rec, const float* P, int S, const float* dc_next,
+                       const float* gates, const float* c, const float* c_prev, float* dG, float* dG_pad, float* dc_prev,
+                       int B, int H, int Hp, hipStream_t stream);
 
 }  // namespace gk

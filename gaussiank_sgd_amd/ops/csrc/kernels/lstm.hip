@@ -113,13 +113,81 @@ __global__ __launch_bounds__(kBlock) void rec_gemm_kernel(const uint16_t* __rest
     }
 }
 
+// fp32 twin (the reference's precision, v_mfma_f32_16x16x4_f32): lane (fr, fq)
+// loads 4 consecutive K elements of its row as one float4 and MFMA j contracts
+// element j of every lane group (the same permutation on both operands), so
+// each 16-deep K step is 4 MFMAs per 16x16 subtile; D such steps in flight.
+template <int D>
+__global__ __launch_bounds__(kBlock) void rec_gemm_f32_kernel(const float* __restrict__ A, int64_t lda,
+                                                              const float* __restrict__ B, int64_t ldb,
+                                                              float* __restrict__ P, int M, int N, int kslice) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int n0 = blockIdx.x * 64;
+  const int s = blockIdx.y;
+  const int m0 = blockIdx.z * 128 + w * 32;
+  if (m0 >= M) return;
+  const int64_t kb = (int64_t)s * kslice + fq * 4;
+  const float* ap[2];
+  const float* bp[4];
+#pragma unroll
+  for (int ms = 0; ms < 2; ++ms) {
+    int r = m0 + ms * 16 + fr;
+    r = r < M ? r : M - 1;
+    ap[ms] = A + (int64_t)r * lda + kb;
+  }
+#pragma unroll
+  for (int ns = 0; ns < 4; ++ns) bp[ns] = B + (int64_t)(n0 + ns * 16 + fr) * ldb + kb;
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+    for (int ns = 0; ns < 4; ++ns) acc[ms][ns] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < kslice; k += 16 * D) {
+    f32x4 a[D][2], b[D][4];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+#pragma unroll
+      for (int ns = 0; ns < 4; ++ns) b[d][ns] = *reinterpret_cast<const f32x4*>(bp[ns] + k + 16 * d);
+#pragma unroll
+      for (int ms = 0; ms < 2; ++ms) a[d][ms] = *reinterpret_cast<const f32x4*>(ap[ms] + k + 16 * d);
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+          for (int ns = 0; ns < 4; ++ns)
+            acc[ms][ns] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[d][ms][j], b[d][ns][j], acc[ms][ns], 0, 0, 0);
+  }
+  float* Ps = P + (int64_t)s * M * N;
+#pragma unroll
+  for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + ms * 16 + fq * 4 + r;
+      if (m < M) {
+#pragma unroll
+        for (int ns = 0; ns < 4; ++ns) Ps[(int64_t)m * N + n0 + ns * 16 + fr] = acc[ms][ns][r];
+      }
+    }
+}
+
+// element storage of the cell kernels' bf16 / fp32 operands
+__device__ __forceinline__ float ld_e(const uint16_t* p, int64_t i) { return bf2f(p[i]); }
+__device__ __forceinline__ float ld_e(const float* p, int64_t i) { return p[i]; }
+__device__ __forceinline__ uint16_t cvt_e(float v, uint16_t*) { return f2bf16(v); }
+__device__ __forceinline__ float cvt_e(float v, float*) { return v; }
+
 // Cell kernels.  Gate k of unit j: column k*H + j of the [B][4H] rows (xg,
 // gates, dG), column k*Hp + j of the 64-padded [B][4Hp] rows (P, dG_pad).
-__global__ __launch_bounds__(kBlock) void lstm_fwd_kernel(const uint16_t* __restrict__ xg,
-                                                          const uint16_t* __restrict__ hg,
+template <typename T>
+__global__ __launch_bounds__(kBlock) void lstm_fwd_kernel(const T* __restrict__ xg, const T* __restrict__ hg,
                                                           const float* __restrict__ P, int S,
                                                           const float* __restrict__ c_prev, float* __restrict__ c,
-                                                          uint16_t* __restrict__ h, uint16_t* __restrict__ h_pad,
+                                                          T* __restrict__ h, T* __restrict__ h_pad,
                                                           float* __restrict__ gates, int B, int H, int Hp) {
   const int64_t idx = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (idx >= (int64_t)B * H) return;
@@ -129,17 +197,17 @@ __global__ __launch_bounds__(kBlock) void lstm_fwd_kernel(const uint16_t* __rest
   const int64_t slab = (int64_t)B * 4 * Hp;
   float a[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) a[k] = bf2f(xg[g0 + k * H]);
+  for (int k = 0; k < 4; ++k) a[k] = ld_e(xg, g0 + k * H);
   if (hg)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) a[k] += bf2f(hg[g0 + k * H]);
+    for (int k = 0; k < 4; ++k) a[k] += ld_e(hg, g0 + k * H);
   for (int s = 0; s < S; ++s)
 #pragma unroll
     for (int k = 0; k < 4; ++k) a[k] += P[s * slab + p0 + k * Hp];
   const float i = sigm(a[0]), f = sigm(a[1]), g = tanhf(a[2]), o = sigm(a[3]);
   const float cn = fmaf(f, c_prev[idx], i * g);
   c[idx] = cn;
-  const uint16_t hv = f2bf16(o * tanhf(cn));
+  const T hv = cvt_e(o * tanhf(cn), h);
   h[idx] = hv;
   if (h_pad) h_pad[(int64_t)b * Hp + j] = hv;
   gates[g0] = i;
@@ -148,29 +216,29 @@ __global__ __launch_bounds__(kBlock) void lstm_fwd_kernel(const uint16_t* __rest
   gates[g0 + 3 * H] = o;
 }
 
-__global__ __launch_bounds__(kBlock) void lstm_bwd_kernel(const uint16_t* __restrict__ dout,
-                                                          const uint16_t* __restrict__ dh_rec,
+template <typename T>
+__global__ __launch_bounds__(kBlock) void lstm_bwd_kernel(const T* __restrict__ dout, const T* __restrict__ dh_rec,
                                                           const float* __restrict__ P, int S,
                                                           const float* __restrict__ dc_next,
                                                           const float* __restrict__ gates,
                                                           const float* __restrict__ c, const float* __restrict__ c_prev,
-                                                          uint16_t* __restrict__ dG, uint16_t* __restrict__ dG_pad,
+                                                          T* __restrict__ dG, T* __restrict__ dG_pad,
                                                           float* __restrict__ dc_prev, int B, int H, int Hp) {
   const int64_t idx = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (idx >= (int64_t)B * H) return;
   const int b = (int)(idx / H), j = (int)(idx - (int64_t)b * H);
   const int64_t g0 = (int64_t)b * 4 * H + j;
   const float i = gates[g0], f = gates[g0 + H], g = gates[g0 + 2 * H], o = gates[g0 + 3 * H];
-  float dh = dout ? bf2f(dout[idx]) : 0.f;
-  if (dh_rec) dh += bf2f(dh_rec[idx]);
+  float dh = dout ? ld_e(dout, idx) : 0.f;
+  if (dh_rec) dh += ld_e(dh_rec, idx);
   if (P) {
     const int64_t p0 = (int64_t)b * Hp + j, slab = (int64_t)B * Hp;
     for (int s = 0; s < S; ++s) dh += P[s * slab + p0];
   }
   const float tc = tanhf(c[idx]);
   const float dc = (dc_next ? dc_next[idx] : 0.f) + dh * o * (1.f - tc * tc);
-  const uint16_t d[4] = {f2bf16(dc * g * i * (1.f - i)), f2bf16(dc * c_prev[idx] * f * (1.f - f)),
-                         f2bf16(dc * i * (1.f - g * g)), f2bf16(dh * tc * o * (1.f - o))};
+  const T d[4] = {cvt_e(dc * g * i * (1.f - i), dG), cvt_e(dc * c_prev[idx] * f * (1.f - f), dG),
+                  cvt_e(dc * i * (1.f - g * g), dG), cvt_e(dh * tc * o * (1.f - o), dG)};
 #pragma unroll
   for (int k = 0; k < 4; ++k) dG[g0 + k * H] = d[k];
   if (dG_pad) {
@@ -196,21 +264,56 @@ void lstm_rec_gemm(const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ld
     hipLaunchKernelGGL(rec_gemm_kernel<2>, grid, dim3(kBlock), 0, stream, A, lda, B, ldb, P, M, N, ks);
 }
 
-void lstm_cell_fwd(const uint16_t* xg, const uint16_t* hg, const float* P, int S, const float* c_prev, float* c, uint16_t* h,
-                   uint16_t* h_pad, float* gates, int B, int H, int Hp, hipStream_t stream) {
+void lstm_rec_gemm_f32(const float* A, int64_t lda, const float* B, int64_t ldb, float* P, int M, int N, int K, int S,
+                       hipStream_t stream) {
+  if (M <= 0 || N <= 0 || S <= 0) return;
+  dim3 grid((unsigned)(N / 64), (unsigned)S, (unsigned)ceil_div(M, 128));
+  const int ks = K / S;
+  if (ks % 128 == 0)
+    hipLaunchKernelGGL(rec_gemm_f32_kernel<8>, grid, dim3(kBlock), 0, stream, A, lda, B, ldb, P, M, N, ks);
+  else
+    hipLaunchKernelGGL(rec_gemm_f32_kernel<4>, grid, dim3(kBlock), 0, stream, A, lda, B, ldb, P, M, N, ks);
+}
+
+template <typename T>
+void cell_fwd(const T* xg, const T* hg, const float* P, int S, const float* c_prev, float* c, T* h, T* h_pad,
+              float* gates, int B, int H, int Hp, hipStream_t stream) {
   const int64_t n = (int64_t)B * H;
   if (n <= 0) return;
-  hipLaunchKernelGGL(lstm_fwd_kernel, dim3((unsigned)ceil_div(n, (int64_t)kBlock)), dim3(kBlock), 0, stream, xg, hg, P, S,
-                     c_prev, c, h, h_pad, gates, B, H, Hp);
+  hipLaunchKernelGGL(lstm_fwd_kernel<T>, dim3((unsigned)ceil_div(n, (int64_t)kBlock)), dim3(kBlock), 0, stream, xg, hg,
+                     P, S, c_prev, c, h, h_pad, gates, B, H, Hp);
+}
+
+template <typename T>
+void cell_bwd(const T* dout, const T* dh_rec, const float* P, int S, const float* dc_next, const float* gates,
+              const float* c, const float* c_prev, T* dG, T* dG_pad, float* dc_prev, int B, int H, int Hp,
+              hipStream_t stream) {
+  const int64_t n = (int64_t)B * H;
+  if (n <= 0) return;
+  hipLaunchKernelGGL(lstm_bwd_kernel<T>, dim3((unsigned)ceil_div(n, (int64_t)kBlock)), dim3(kBlock), 0, stream, dout,
+                     dh_rec, P, S, dc_next, gates, c, c_prev, dG, dG_pad, dc_prev, B, H, Hp);
+}
+
+void lstm_cell_fwd(const uint16_t* xg, const uint16_t* hg, const float* P, int S, const float* c_prev, float* c, uint16_t* h,
+                   uint16_t* h_pad, float* gates, int B, int H, int Hp, hipStream_t stream) {
+  cell_fwd<uint16_t>(xg, hg, P, S, c_prev, c, h, h_pad, gates, B, H, Hp, stream);
 }
 
 void lstm_cell_bwd(const uint16_t* dout, const uint16_t* dh_rec, const float* P, int S, const float* dc_next, const float* gates,
                    const float* c, const float* c_prev, uint16_t* dG, uint16_t* dG_pad, float* dc_prev, int B, int H,
                    int Hp, hipStream_t stream) {
-  const int64_t n = (int64_t)B * H;
-  if (n <= 0) return;
-  hipLaunchKernelGGL(lstm_bwd_kernel, dim3((unsigned)ceil_div(n, (int64_t)kBlock)), dim3(kBlock), 0, stream, dout,
-                     dh_rec, P, S, dc_next, gates, c, c_prev, dG, dG_pad, dc_prev, B, H, Hp);
+  cell_bwd<uint16_t>(dout, dh_rec, P, S, dc_next, gates, c, c_prev, dG, dG_pad, dc_prev, B, H, Hp, stream);
+}
+
+void lstm_cell_fwd_f32(const float* xg, const float* hg, const float* P, int S, const float* c_prev, float* c, float* h,
+                       float* h_pad, float* gates, int B, int H, int Hp, hipStream_t stream) {
+  cell_fwd<float>(xg, hg, P, S, c_prev, c, h, h_pad, gates, B, H, Hp, stream);
+}
+
+void lstm_cell_bwd_f32(const float* dout, const float* dh_rec, const float* P, int S, const float* dc_next,
+                       const float* gates, const float* c, const float* c_prev, float* dG, float* dG_pad, float* dc_prev,
+                       int B, int H, int Hp, hipStream_t stream) {
+  cell_bwd<float>(dout, dh_rec, P, S, dc_next, gates, c, c_prev, dG, dG_pad, dc_prev, B, H, Hp, stream);
 }
 
 }  // namespace gk

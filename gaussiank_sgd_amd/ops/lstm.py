@@ -1,4 +1,5 @@
-"""bf16 LSTM layers: a split-K MFMA step GEMM + one fused HIP cell kernel per step.
+"""LSTM layers: a split-K MFMA step GEMM + one fused HIP cell kernel per step
+(bf16 under autocast, fp32 at the reference's precision).
 
 ``GkLSTM`` is a drop-in ``nn.LSTM`` (sequence-first, same parameter names
 ``weight_ih_l{k}`` / ``weight_hh_l{k}`` / ``bias_ih_l{k}`` / ``bias_hh_l{k}``,
@@ -24,9 +25,10 @@ bench/lstm_gemm_probe.py); split over S K-slices into a few hundred
 workgroups it runs a handful of MFMA steps per wave, and the cell kernel sums
 the fp32 slices on load (no atomics, no extra reduction launch).  Its
 operands are 64-padded (h_pad / dG_pad written by the cell kernels, W_hh
-padded once per forward).  Off the GPU (or outside bf16 autocast) the
-same recurrence runs in fp32 with PyTorch ops, so CPU tests compare it with
-``nn.LSTM`` exactly.
+padded once per forward).  fp32 inputs without autocast (the reference's
+precision) run the same kernels on fp32 operands (``v_mfma_f32_16x16x4_f32``
+step GEMM, fp32 h / dG).  Off the GPU the same recurrence runs in fp32 with
+PyTorch ops, so CPU tests compare it with ``nn.LSTM`` exactly.
 """
 from __future__ import annotations
 
@@ -113,10 +115,12 @@ class _LSTMLayerFn(torch.autograd.Function):
     lives inside forward / backward)."""
 
     @staticmethod
-    def forward(ctx, x, h0, c0, w_ih, w_hh, b_ih, b_hh, shadows, sinks, fast):
+    def forward(ctx, x, h0, c0, w_ih, w_hh, b_ih, b_hh, shadows, sinks, fast, cd=torch.bfloat16):
+        # fast: the HIP kernels (split-K step GEMM + fused cells) in the compute
+        # dtype cd -- bf16 under autocast, fp32 otherwise (the reference's precision)
         T, B, _ = x.shape
         H = w_hh.shape[1]
-        cd = torch.bfloat16 if fast else torch.float32
+        cd = cd if fast else torch.float32
         dev = x.device
         wih = shadows[0] if shadows[0] is not None else w_ih.detach().to(cd)
         whh = shadows[1] if shadows[1] is not None else w_hh.detach().to(cd)
@@ -233,7 +237,7 @@ class _LSTMLayerFn(torch.autograd.Function):
                     sink(tgt)
                 else:
                     grads[k] = tgt.to(wdt)
-        return (dx, dh0, dc0, grads[0], grads[1], grads[2], grads[3], None, None, None)
+        return (dx, dh0, dc0, grads[0], grads[1], grads[2], grads[3], None, None, None, None)
 
 
 class GkLSTM(nn.Module):
@@ -268,11 +272,17 @@ class GkLSTM(nn.Module):
             hx = (z, z)
         h0, c0 = hx
         dev = x.device.type
-        fast = (x.is_cuda and torch.is_autocast_enabled(dev) and torch.get_autocast_dtype(dev) == torch.bfloat16
-                and load())
+        bf16 = x.is_cuda and torch.is_autocast_enabled(dev) and torch.get_autocast_dtype(dev) == torch.bfloat16
+        # fp32 (no autocast, the reference's precision) runs the same HIP step
+        # GEMM and cell kernels on fp32 operands (GKSGD_LSTM_F32=0: PyTorch ops)
+        f32 = (x.is_cuda and not torch.is_autocast_enabled(dev) and x.dtype == torch.float32 and
+               os.environ.get("GKSGD_LSTM_F32", "1") != "0")
+        fast = (bf16 or f32) and load()
         if x.is_cuda and fast:
             require_native(x)
-        table = getattr(self, "_gk_shadow", None) if fast else None
+        cd = torch.bfloat16 if bf16 else torch.float32
+        table = getattr(self, "_gk_shadow", None) if (fast and bf16) else None
+        direct = getattr(self, "_gk_direct_grads", None) if (fast and not bf16) else None
         grad_on = torch.is_grad_enabled()
         hn, cn = [], []
         y = x
@@ -289,8 +299,12 @@ class GkLSTM(nn.Module):
                         shadows[j] = info[0]
                     if grad_on and p.requires_grad:
                         sinks[j] = info[1]
+            elif direct:
+                for j, (n, p) in enumerate(zip(names, params)):
+                    if n in direct and grad_on and p.requires_grad:
+                        sinks[j] = direct[n]
             with torch.autocast(dev, enabled=False):
-                y, h_k, c_k = _LSTMLayerFn.apply(y, h0[k], c0[k], *params, tuple(shadows), tuple(sinks), fast)
+                y, h_k, c_k = _LSTMLayerFn.apply(y, h0[k], c0[k], *params, tuple(shadows), tuple(sinks), fast, cd)
             hn.append(h_k)
             cn.append(c_k)
             if k < L - 1 and self.dropout > 0 and self.training:

@@ -168,4 +168,14 @@ def install_direct_grads(model: nn.Module, opt) -> int:
             if mod.weight in names and mod.bias in names:
                 mod._gk_direct = (arena.grad_views[names[mod.weight]], arena.grad_views[names[mod.bias]])
                 count += 2
+        elif isinstance(mod, GkLSTM):
+            # fp32 GkLSTM (ops/lstm.py): its backward adds every weight / bias
+            # gradient straight into the arena
+            table = {}
+            for pname, p in mod.named_parameters(recurse=False):
+                if p in names:
+                    table[pname] = opt._make_sink(names[p])
+                    count += 1
+            if table:
+                mod._gk_direct_grads = table
     return count

@@ -88,9 +88,14 @@ def ssgd(dnn, dataset, data_dir, nworkers, lr, batch_size, nsteps_update, max_ep
     if getattr(trainer, "_pending_compression", None):
         optimizer.load_compression_state(trainer._pending_compression)
     hvd.broadcast_parameters(trainer.net.state_dict(), root_rank=0)
-    if bf16_shadow and amp == "bf16" and trainer.is_cuda:
-        from ..parallel import install_bf16_shadow
-        install_bf16_shadow(trainer.net, optimizer)
+    if bf16_shadow and trainer.is_cuda:
+        # bf16: weight shadows + arena gradient sinks; fp32: the kernels' weight
+        # gradients straight into the arena (parallel/shadow.py)
+        from ..parallel import install_bf16_shadow, install_direct_grads
+        if amp == "bf16":
+            install_bf16_shadow(trainer.net, optimizer)
+        else:
+            install_direct_grads(trainer.net, optimizer)
     trainer.update_optimizer(optimizer)
     iters_per_epoch = max(1, trainer.get_num_of_training_samples() // (nworkers * batch_size * nsteps_update))
     from ..utils.watchdog import JsonlMetrics

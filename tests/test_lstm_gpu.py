@@ -181,3 +181,139 @@ def test_ptb_lstm_step_bf16(cuda):
     assert not torch.isnan(opt.arena.weights).any()
     # per-tensor buckets: a small bucket may legitimately send nothing in a step
     assert sum(int(b.bufs.record[0]) for b in opt.arena.buckets) > 0
+
+
+# ---- fp32 path (no autocast: the reference's precision) --------------------
+
+@pytest.mark.parametrize("B,H", [(128, 1500), (3, 40)])
+def test_lstm_cells_f32_vs_reference(B, H):
+    """fp32 cell kernels (xg / hg / h / dG in fp32) vs the fp32 PyTorch cells."""
+    from gaussiank_sgd_amd.ops.lstm import _cell_bwd_ref, _cell_fwd_ref
+    g = torch.ops.gksgd
+    torch.manual_seed(B + H + 1)
+    xg = torch.randn(B, 4 * H, device="cuda") * 2
+    hg = torch.randn(B, 4 * H, device="cuda")
+    Hp = (H + 63) // 64 * 64
+    P = torch.zeros(2, B, 4, Hp, device="cuda")
+    P[0, :, :, :H] = hg.view(B, 4, H) * 0.25
+    P[1, :, :, :H] = hg.view(B, 4, H) * 0.75
+    P = P.view(2, B, 4 * Hp)
+    h_pad = torch.full((B, Hp), 7.0, device="cuda")
+    cp = torch.randn(B, H, device="cuda")
+    outs = [torch.empty(B, H, device="cuda"), torch.empty(B, H, device="cuda"), torch.empty(B, 4 * H, device="cuda")]
+    refs = [torch.empty_like(o) for o in outs]
+    g.lstm_cell_fwd(xg, None, P, 2, cp, outs[0], outs[1], h_pad, outs[2])
+    _cell_fwd_ref(xg, hg, cp, *refs)
+    for o, r in zip(outs, refs):
+        assert (o - r).abs().max().item() <= 1e-5 * r.abs().max().item() + 1e-6
+    assert torch.equal(h_pad[:, :H], outs[1])
+    assert (h_pad[:, H:] == 7.0).all()
+    c, _, gates = refs
+    dout = torch.randn(B, H, device="cuda")
+    dh = torch.randn(B, H, device="cuda")
+    dcn = torch.randn(B, H, device="cuda")
+    dG = torch.empty(B, 4 * H, device="cuda")
+    dcp = torch.empty(B, H, device="cuda")
+    rG = torch.empty(B, 4 * H, device="cuda")
+    rcp = torch.empty(B, H, device="cuda")
+    Pb = torch.zeros(3, B, Hp, device="cuda")
+    for s in range(3):
+        Pb[s, :, :H] = dh / 3
+    dG_pad = torch.zeros(B, 4 * Hp, device="cuda")
+    g.lstm_cell_bwd(dout, None, Pb, 3, dcn, gates, c, cp, dG, dG_pad, dcp)
+    _cell_bwd_ref(dout, dh, dcn, gates, c, cp, rG, rcp)
+    assert (dG - rG).abs().max().item() <= 1e-5 * rG.abs().max().item() + 1e-6
+    assert (dcp - rcp).abs().max().item() <= 1e-5 * rcp.abs().max().item() + 1e-6
+    assert torch.equal(dG_pad.view(B, 4, Hp)[:, :, :H], dG.view(B, 4, H))
+    assert (dG_pad.view(B, 4, Hp)[:, :, H:] == 0).all()
+    # fp32 hg / dh_rec inputs (the unpadded step-GEMM path)
+    outs2 = [torch.empty_like(o) for o in outs]
+    g.lstm_cell_fwd(xg, hg, None, 0, cp, outs2[0], outs2[1], None, outs2[2])
+    for o, r in zip(outs2, refs):
+        assert (o - r).abs().max().item() <= 1e-5 * r.abs().max().item() + 1e-6
+    g.lstm_cell_bwd(dout, dh, None, 0, dcn, gates, c, cp, dG, None, dcp)
+    assert (dG - rG).abs().max().item() <= 1e-5 * rG.abs().max().item() + 1e-6
+    g.lstm_cell_bwd(None, None, None, 0, None, gates, c, cp, dG, None, dcp)
+    assert dG.abs().max().item() == 0.0
+    with pytest.raises(RuntimeError):    # mixed storage dtypes are refused
+        g.lstm_cell_fwd(xg, hg.to(torch.bfloat16), None, 0, cp, outs2[0], outs2[1], None, outs2[2])
+
+
+@pytest.mark.parametrize("M,N,K,S", [(128, 6144, 1536, 4), (20, 1536, 6144, 16), (3, 256, 64, 1), (200, 128, 256, 2)])
+def test_lstm_rec_gemm_f32_vs_fp64(M, N, K, S):
+    g = torch.ops.gksgd
+    torch.manual_seed(M + N + K + 1)
+    A = torch.randn(M, K, device="cuda")
+    Bm = torch.randn(N, K, device="cuda")
+    P = torch.full((S, M, N), float("nan"), device="cuda")
+    g.lstm_rec_gemm(A, Bm, P, S)
+    ref = A.double() @ Bm.double().t()
+    scale = (A.double().abs() @ Bm.double().abs().t()).max().item()
+    assert (P.double().sum(0) - ref).abs().max().item() <= 2e-6 * scale
+    ks = K // S
+    ref0 = A[:, :ks].double() @ Bm[:, :ks].double().t()
+    assert (P[0].double() - ref0).abs().max().item() <= 2e-6 * scale
+
+
+@pytest.mark.parametrize("fwd_max,bwd_max", [(1 << 30, 1 << 30), (0, 0), (0, 1 << 30)],
+                         ids=["splitk", "blas", "mixed"])
+def test_gklstm_f32_vs_fp64_nn_lstm(monkeypatch, fwd_max, bwd_max):
+    """fp32 GkLSTM (HIP step GEMM + fp32 cells) vs an fp64 nn.LSTM."""
+    from gaussiank_sgd_amd.ops import lstm as L_
+    from gaussiank_sgd_amd.ops.lstm import GkLSTM
+    monkeypatch.setitem(L_.SPLITK_MAX_BATCH, "fwd", fwd_max)
+    monkeypatch.setitem(L_.SPLITK_MAX_BATCH, "bwd", bwd_max)
+    torch.manual_seed(0)
+    T, B, I, H, L = 35, 16, 256, 320, 2
+    ref = torch.nn.LSTM(I, H, num_layers=L).cuda().double()
+    m = GkLSTM(I, H, num_layers=L).cuda()
+    m.load_state_dict({k: v.float() for k, v in ref.state_dict().items()})
+    x = torch.randn(T, B, I, device="cuda")
+    h0 = torch.randn(L, B, H, device="cuda") * 0.5
+    c0 = torch.randn(L, B, H, device="cuda") * 0.5
+    xa, ha, ca = (t.clone().requires_grad_(True) for t in (x, h0, c0))
+    y, (hn, cn) = m(xa, (ha, ca))
+    assert y.dtype == torch.float32
+    xr, hr, cr = (t.double().requires_grad_(True) for t in (x, h0, c0))
+    torch.backends.cudnn.enabled = False
+    try:
+        yr, (hnr, cnr) = ref(xr, (hr, cr))
+    finally:
+        torch.backends.cudnn.enabled = True
+    gy = torch.randn_like(yr)
+    ghn = torch.randn_like(hnr)
+    (y.double() * gy).sum().add_((hn.double() * ghn).sum()).backward()
+    (yr * gy).sum().add_((hnr * ghn).sum()).backward()
+    tol = lambda r: 1e-4 * r.abs().max().item() + 1e-6  # noqa: E731
+    assert (y.double() - yr).abs().max().item() <= tol(yr)
+    assert (cn.double() - cnr).abs().max().item() <= tol(cnr)
+    assert (xa.grad.double() - xr.grad).abs().max().item() <= tol(xr.grad)
+    assert (ha.grad.double() - hr.grad).abs().max().item() <= tol(hr.grad)
+    assert (ca.grad.double() - cr.grad).abs().max().item() <= tol(cr.grad)
+    for (n, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
+        assert (p.grad.double() - q.grad).abs().max().item() <= tol(q.grad), n
+
+
+def test_gklstm_f32_direct_arena_grads():
+    """install_direct_grads: the fp32 GkLSTM backward adds its weight / bias
+    gradients straight into the optimizer arena (same values as the plain path)."""
+    from gaussiank_sgd_amd.compression import compressors
+    from gaussiank_sgd_amd.ops.lstm import GkLSTM
+    from gaussiank_sgd_amd.parallel import comm, install_direct_grads
+    from gaussiank_sgd_amd.parallel.distributed_optimizer import DistributedOptimizer
+    comm.init()
+    torch.manual_seed(1)
+    net = GkLSTM(128, 192, num_layers=2).cuda()
+    ref = copy.deepcopy(net)
+    opt = DistributedOptimizer(torch.optim.SGD(net.parameters(), lr=0.1), named_parameters=net.named_parameters(),
+                               compression=compressors["none"], is_sparse=False, density=1.0)
+    assert install_direct_grads(net, opt) == 8
+    x = torch.randn(12, 8, 128, device="cuda")
+    for model in (net, ref):
+        y, _ = model(x)
+        y.square().mean().backward()
+    torch.cuda.synchronize()
+    for (n, p), (_, q) in zip(net.named_parameters(), ref.named_parameters()):
+        assert p.grad is not None, n
+        err = (p.grad - q.grad).abs().max().item()
+        assert err <= 1e-5 * q.grad.abs().max().item() + 1e-7, (n, err)
