@@ -1012,14 +1012,30 @@ __global__ __launch_bounds__(kBlock) void select_kernel(float* __restrict__ r, i
   const int64_t t0 = (int64_t)blockIdx.x * chunk_tiles;
   const int64_t t1 = t0 + chunk_tiles < ntiles ? t0 + chunk_tiles : ntiles;
   const int w = wave_id();
+  // the next tile's 16 values are in flight while this tile is tested and
+  // compacted (the two block barriers per tile otherwise expose the load
+  // latency once per tile)
+  float nv[4][4];
+  if (t0 < t1) {
+#pragma unroll
+    for (int j4 = 0; j4 < 4; ++j4) load4<VEC>(r, t0 * kTileElems + j4 * (kBlock * 4) + threadIdx.x * 4, n, nv[j4]);
+  }
   for (int64_t tile = t0; tile < t1 && running < k_cap; ++tile) {
     const int64_t base = tile * kTileElems;
     float v[4][4];
     uint32_t selm[4], eqm[4];
 #pragma unroll
+    for (int j4 = 0; j4 < 4; ++j4)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[j4][q] = nv[j4][q];
+    if (tile + 1 < t1) {
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4)
+        load4<VEC>(r, (tile + 1) * kTileElems + j4 * (kBlock * 4) + threadIdx.x * 4, n, nv[j4]);
+    }
+#pragma unroll
     for (int j4 = 0; j4 < 4; ++j4) {
       const int64_t e = base + j4 * (kBlock * 4) + threadIdx.x * 4;
-      load4<VEC>(r, e, n, v[j4]);
       selm[j4] = 0; eqm[j4] = 0;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise scripts/gpurun/r3_counters.sh output: one row per probe with wall time
+"""Summarise scripts/gpurun/r3/r3_counters.sh output: one row per probe with wall time
 (median kernel duration), MFMA busy share, instruction ratios and waits.
 
 mfma% = SQ_VALU_MFMA_BUSY_CYCLES / (median wall x 2.1 GHz x 1024 SIMDs) (the

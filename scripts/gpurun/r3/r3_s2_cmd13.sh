@@ -10,4 +10,4 @@ rc=$?; echo tests_rc=$rc; tail -2 $D/tests.log
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $D/smoke.log 2>&1
 rc=$?; echo smoke_rc=$rc; tail -1 $D/smoke.log
 [ $rc -eq 0 ] || exit $rc
-REFCFG_D=$D/refcfg bash scripts/gpurun/r3_refcfg.sh
+REFCFG_D=$D/refcfg bash scripts/gpurun/r3/r3_refcfg.sh

@@ -11,5 +11,5 @@ timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $D/prof_fp32 -o run -- pyt
 echo prof_rc=$?
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $D/prof_bf16 -o run -- python3 bench.py --amp bf16 --steps 10 --warmup 3 > $D/prof_bf16.log 2>&1
 echo prof16_rc=$?
-CTR_D=$D bash scripts/gpurun/r3_counters.sh > $D/ctr.log 2>&1
+CTR_D=$D bash scripts/gpurun/r3/r3_counters.sh > $D/ctr.log 2>&1
 echo ctr_rc=$?

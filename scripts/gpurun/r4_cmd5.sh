@@ -10,7 +10,7 @@ rc=$?; echo tests_rc=$rc; tail -4 $D/tests.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python3 bench.py --json-out $D/bench_cached.json > $D/bench_cached.log 2>&1
 rc=$?; echo bench_rc=$rc; python3 -c "import json;d=json.load(open('$D/bench_cached.json'));print('cached', d['value'], d['ms_per_step'], d.get('bf16_value'), d.get('ref_bs32_value'))"; [ $rc -eq 0 ] || exit $rc
-GKSGD_GEMM_RETUNE=1 GKSGD_GEMM_SAVE=$D/gemm_choices.json timeout -k 10 900 python3 bench.py --json-out $D/bench_retuned.json > $D/bench_retuned.log 2>&1
+GKSGD_GEMM_RETUNE=1 GKSGD_GEMM_SAVE=$D/gemm_choices.json GKSGD_GEMM_DUMP=$D/gemm_dump.json timeout -k 10 900 python3 bench.py --json-out $D/bench_retuned.json > $D/bench_retuned.log 2>&1
 rc=$?; echo bench2_rc=$rc; python3 -c "import json;d=json.load(open('$D/bench_retuned.json'));print('retuned', d['value'], d['ms_per_step'], d.get('bf16_value'), d.get('ref_bs32_value'))"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python3 scripts/debug/phase_order_probe.py --order b,s,b,d,b > $D/order.log 2>&1
 rc=$?; echo order_rc=$rc; grep phase $D/order.log
