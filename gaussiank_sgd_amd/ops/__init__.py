@@ -231,6 +231,14 @@ def _f32(x: float) -> float:
     return struct.unpack("f", struct.pack("f", x))[0]
 
 
+GAUSS_WALK = 6   # compress.hip kGaussWalk
+
+
+def _gauss_ext(loops: int) -> bool:
+    L = max(loops, 1)
+    return min(L * (L + 1) // 2, MAX_CAND) <= GAUSS_WALK
+
+
 def _candidates(mode: int, loops: int, z: float, fixed_thr: float, stats: Tuple[float, float, float, float]):
     """Candidate thresholds (|x| units) and key bounds, mirroring finalize_kernel."""
     mean, std, meanabs, maxabs = stats
@@ -245,6 +253,16 @@ def _candidates(mode: int, loops: int, z: float, fixed_thr: float, stats: Tuple[
                     t *= 1.5
                 for _ in range(a):
                     t *= 0.5
+                thr.append(_f32(t))
+        if _gauss_ext(loops):
+            # overflow extension (compress.hip ladder_cands): dead slots up to
+            # GAUSS_WALK, then t_top * 1.25^j above the walk's top node
+            thr.extend([None] * (GAUSS_WALK - len(thr)))
+            t = t0
+            for _ in range(max(loops, 1) - 1):
+                t *= 1.5
+            for _ in range(MAX_CAND - GAUSS_WALK):
+                t *= 1.25
                 thr.append(_f32(t))
     elif mode in (MODE_REDSYNC, MODE_REDSYNCTRIM):
         mv = torch.tensor(meanabs, dtype=torch.float32)
@@ -435,7 +453,8 @@ def compress_cpu_(g: torch.Tensor, r: torch.Tensor, bufs: CompressBuffers, mode:
         elif mode in (MODE_GAUSSIAN, MODE_REDSYNC, MODE_REDSYNCTRIM, MODE_THRESHOLD):
             thr = _candidates(mode, loops, z, fixed_thr, stats)
             keys = abs_key(acc)
-            bounds = [_bound_from_threshold(t) for t in thr]
+            bounds = [0xFFFFFFFF if t is None else _bound_from_threshold(t) for t in thr]
+            thr = [0.0 if t is None else t for t in thr]
             counts = [int((keys >= b).sum()) for b in bounds]
             chosen = _decide(mode, loops, k, counts)
             if counts[chosen] > k_cap:

@@ -245,10 +245,25 @@ __device__ __forceinline__ bool last_block(uint32_t* counter) {
 // count kernel's compile-time candidate bound NC (count_cands) read, so a
 // ladder cannot grow on one side only (a count pass with NC below the live
 // count would report zero for the candidates past NC).
+// Gaussian-k: the reference's refinement walk (tri(loops) nodes t0 * 1.5^b *
+// 0.5^a) plus, for loops <= 3, kGaussExt overflow-extension thresholds
+// above the walk's top node (t_top * 1.25^j, slots kGaussWalk ..): when every
+// walk node passes more than k_cap entries (heavy-tailed gradients: the walk
+// stops at 2.25 t0 with the count still above 4k/3), the decide step picks the
+// extension node with the largest count in [2k/3, k_cap] -- a magnitude-
+// correct selection from the same count pass -- instead of running the three
+// radix passes of the exact top-k_cap fallback.  The extension is tested only
+// for the rare elements above its lowest threshold (count_kernel NX).
+constexpr int kGaussWalk = 6, kGaussExt = kMaxCand - kGaussWalk;
+constexpr double kGaussExtRatio = 1.25;
+__host__ __device__ constexpr int gauss_walk(int loops) {
+  return (loops < 1 ? 1 : loops) * ((loops < 1 ? 1 : loops) + 1) / 2 < kMaxCand
+             ? (loops < 1 ? 1 : loops) * ((loops < 1 ? 1 : loops) + 1) / 2
+             : kMaxCand;
+}
+__host__ __device__ constexpr bool gauss_ext(int loops) { return gauss_walk(loops) <= kGaussWalk; }
 __host__ __device__ constexpr int ladder_cands(int mode, int loops) {
-  return mode == kModeGaussian ? ((loops < 1 ? 1 : loops) * ((loops < 1 ? 1 : loops) + 1) / 2 < kMaxCand
-                                      ? (loops < 1 ? 1 : loops) * ((loops < 1 ? 1 : loops) + 1) / 2
-                                      : kMaxCand)
+  return mode == kModeGaussian ? (gauss_ext(loops) ? kGaussWalk + kGaussExt : gauss_walk(loops))
          : mode == kModeRedSync ? 7
          : mode == kModeGaussianCal ? kCalCand
          : mode == kModeThreshold ? 1
@@ -257,7 +272,8 @@ __host__ __device__ constexpr int ladder_cands(int mode, int loops) {
          : kMaxCand;   // RedSyncTrim: the whole descending-ratio ladder
 }
 constexpr int kFallbackCands = 2;   // conditional exact-key pass: key > K, key >= K
-static_assert(ladder_cands(kModeGaussian, 5) == 15 && ladder_cands(kModeGaussian, 3) == 6, "gaussian ladder");
+static_assert(ladder_cands(kModeGaussian, 5) == 15 && ladder_cands(kModeGaussian, 3) == kMaxCand &&
+              gauss_walk(3) == kGaussWalk && kGaussExt > 0, "gaussian ladder");
 static_assert(ladder_cands(kModeRedSync, 3) <= kMaxCand && kCalCand <= kMaxCand, "ladder sizes");
 
 struct FinArgs {   // finalize_body arguments (stats -> finalize hand-off)
@@ -574,6 +590,16 @@ __device__ __forceinline__ void finalize_body(GkCtrl* __restrict__ ctrl, const d
         ++nc;
       }
     }
+    if (gauss_ext(loops)) {
+      // overflow extension (see ladder_cands); slots nc .. kGaussWalk stay dead
+      double t = t0;
+      for (int q = 0; q < (loops < 1 ? 1 : loops) - 1; ++q) t *= 1.5;
+      for (int j = 0; j < kGaussExt; ++j) {
+        t *= kGaussExtRatio;
+        ctrl->bound[kGaussWalk + j] = bound_from_threshold((float)t);
+        ctrl->cand_thr[kGaussWalk + j] = t;
+      }
+    }
   } else if (mode == kModeRedSync || mode == kModeRedSyncTrim) {
     const float mean_val = (float)meanabs;
     const float max_val = mx;
@@ -680,7 +706,7 @@ __device__ __forceinline__ void cal_fallback_body(GkCtrl* __restrict__ ctrl, con
 // --------------------------------------------------------------------------
 // K4: one-pass multi-threshold count (counters in registers)
 // --------------------------------------------------------------------------
-template <int KEYKIND, bool VEC, int NC>
+template <int KEYKIND, bool VEC, int NC, int NX = 0>
 __global__ __launch_bounds__(kBlock) void count_kernel(const float* __restrict__ x, int64_t n, uint32_t seed,
                                                        GkCtrl* __restrict__ ctrl, int64_t chunk_tiles,
                                                        uint32_t* __restrict__ blockcnt,
@@ -702,6 +728,24 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const float* __restrict__
   uint32_t cnt[NC];
 #pragma unroll
   for (int j = 0; j < NC; ++j) cnt[j] = 0u;
+  // NX ascending extension candidates (bound[NC ..]): tested only for the
+  // elements above the lowest of them (a branch that is almost never taken
+  // for a Gaussian-k overflow ladder), so they cost one compare per element
+  constexpr int NXA = NX > 0 ? NX : 1;
+  uint32_t xb[NXA], xc[NXA];
+#pragma unroll
+  for (int j = 0; j < NXA; ++j) {
+    xb[j] = NX > 0 ? __builtin_amdgcn_readfirstlane(ctrl->bound[NC + j]) : 0xffffffffu;
+    xc[j] = 0u;
+  }
+  auto test = [&](uint32_t key, bool in) {
+#pragma unroll
+    for (int j = 0; j < NC; ++j) cnt[j] += (in && key >= bnd[j]) ? 1u : 0u;
+    if (NX > 0 && in && key >= xb[0]) {
+#pragma unroll
+      for (int j = 0; j < NXA; ++j) xc[j] += key >= xb[j] ? 1u : 0u;
+    }
+  };
   const int64_t ntiles = (n + kTileElems - 1) / kTileElems;
   const int64_t t0 = (int64_t)blockIdx.x * chunk_tiles;
   const int64_t t1 = t0 + chunk_tiles < ntiles ? t0 + chunk_tiles : ntiles;
@@ -727,9 +771,7 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const float* __restrict__
         for (int j4 = 0; j4 < 4; ++j4) {
           const uint32_t k4[4] = {abs_key(cu[j4].x), abs_key(cu[j4].y), abs_key(cu[j4].z), abs_key(cu[j4].w)};
 #pragma unroll
-          for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int j = 0; j < NC; ++j) cnt[j] += k4[q] >= bnd[j] ? 1u : 0u;
+          for (int q = 0; q < 4; ++q) test(k4[q], true);
         }
       }
     }
@@ -770,24 +812,25 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const float* __restrict__
       }
     }
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const bool in = (inb >> q) & 1u;
-#pragma unroll
-      for (int j = 0; j < NC; ++j) cnt[j] += (in && key[q] >= bnd[j]) ? 1u : 0u;
-    }
+    for (int q = 0; q < 16; ++q) test(key[q], (inb >> q) & 1u);
   }
   // per-lane counts -> per-wave totals (one reduction per block)
+  static_assert(NC + NX <= kMaxCand, "candidate slots");
 #pragma unroll
   for (int j = 0; j < NC; ++j) cnt[j] = wave_sum(cnt[j]);
-  __shared__ uint32_t sh[kWavesPerBlock][NC];
+#pragma unroll
+  for (int j = 0; j < NX; ++j) xc[j] = wave_sum(xc[j]);
+  __shared__ uint32_t sh[kWavesPerBlock][NC + NXA];
   if (lane_id() == 0) {
 #pragma unroll
     for (int j = 0; j < NC; ++j) sh[wave_id()][j] = cnt[j];
+#pragma unroll
+    for (int j = 0; j < NX; ++j) sh[wave_id()][NC + j] = xc[j];
   }
   __syncthreads();
   if (threadIdx.x < kMaxCand) {
     const int j = threadIdx.x;
-    st_dev(&blockcnt[blockIdx.x * kMaxCand + j], j < NC ? sh[0][j] + sh[1][j] + sh[2][j] + sh[3][j] : 0u);
+    st_dev(&blockcnt[blockIdx.x * kMaxCand + j], j < NC + NX ? sh[0][j] + sh[1][j] + sh[2][j] + sh[3][j] : 0u);
   }
   if (last_block(da.counter))   // decide on the totals in the last block
     decide_body(ctrl, blockcnt, (int)gridDim.x, da.mode, da.loops, da.k, da.k_cap, da.offsets, da.eqtake, da.blocksel,
@@ -1124,6 +1167,13 @@ void launch_count(const CompressArgs& a, const Ws& w, bool vec, int G, int64_t c
   da.ctrl = ctrl; da.mode = a.mode; da.loops = a.loops; da.k = a.k; da.k_cap = a.k_cap;
   da.offsets = w.offsets; da.eqtake = w.eqtake; da.blocksel = w.blocksel; da.hdr = a.record;
   da.hist_reset = w.hist; da.counter = w.sync + (cond ? 3 : 1);
+#define GK_COUNT2(NC, NX)                                                                                         \
+  if (vec)                                                                                                        \
+    hipLaunchKernelGGL((count_kernel<KEYKIND, true, NC, NX>), dim3(G), dim3(kBlock), 0, s, a.r, a.n, a.seed, ctrl, \
+                       chunk_tiles, w.blockcnt, a.valid, cond, a.seed_dev, da);                                   \
+  else                                                                                                            \
+    hipLaunchKernelGGL((count_kernel<KEYKIND, false, NC, NX>), dim3(G), dim3(kBlock), 0, s, a.r, a.n, a.seed,     \
+                       ctrl, chunk_tiles, w.blockcnt, a.valid, cond, a.seed_dev, da);
 #define GK_COUNT(NC)                                                                                              \
   if (vec)                                                                                                        \
     hipLaunchKernelGGL((count_kernel<KEYKIND, true, NC>), dim3(G), dim3(kBlock), 0, s, a.r, a.n, a.seed, ctrl,    \
@@ -1134,13 +1184,15 @@ void launch_count(const CompressArgs& a, const Ws& w, bool vec, int G, int64_t c
   if constexpr (KEYKIND == kKeyHash) {
     GK_COUNT(2)
   } else {
-    if (nc <= 2) { GK_COUNT(2) }
+    if (!cond && a.mode == kModeGaussian && gauss_ext(a.loops)) { GK_COUNT2(kGaussWalk, kGaussExt) }
+    else if (nc <= 2) { GK_COUNT(2) }
     else if (nc <= 3) { GK_COUNT(3) }
     else if (nc <= 6) { GK_COUNT(6) }
     else if (nc <= 8) { GK_COUNT(8) }
     else { GK_COUNT(kMaxCand) }
   }
 #undef GK_COUNT
+#undef GK_COUNT2
 }
 
 template <int KEYKIND>

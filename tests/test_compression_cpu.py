@@ -263,3 +263,37 @@ def test_bucketized_topk_against_reference_source():
         _, ref_idx = ns["bucketized_topk"](x.clone(), k)
         _, idx, _, _ = reference.bucketized_topk(x, None, ratio, ec=False)
         assert idx.tolist() == ref_idx.tolist()
+
+
+def test_gaussian_overflow_extension_node():
+    """Power-law tail: the reference walk (t0, 1.5 t0, 2.25 t0) still passes
+    more than k_cap entries; one of the overflow-extension thresholds
+    (2.25 t0 * 1.25^j, ladder slots 6..15) lands in [2k/3, k_cap] and is chosen
+    -- a magnitude-correct selection from the same count pass, no exact
+    fallback.  The header keeps the reference rule's count."""
+    g = torch.Generator().manual_seed(21)
+    n = 400_000
+    u = torch.rand(n, generator=g).clamp_min(1e-12)
+    x = (u ** (-1.0 / 2.5) - 1.0) * 1e-3 * torch.sign(torch.randn(n, generator=g))   # Pareto(2.5) tail
+    r = torch.zeros(n)
+    ratio = 0.001
+    k = int(n * ratio)
+    k_cap = math.ceil(4 * k / 3)
+    z = gaussian_z(ratio)
+    _, rr, rec, idx, val, b = _mirror(x, r, ops.MODE_GAUSSIAN, k, k_cap, z=z)
+    ref_total = int(reference.gaussian(x, r, ratio, loops=3, ec=True)[1].numel())
+    assert ref_total > k_cap and int(rec[1]) == ref_total
+    chosen = int(rec[2])
+    assert 6 <= chosen < ops.MAX_CAND, chosen
+    sent = int(rec[0])
+    assert 2 * k <= 3 * sent <= 3 * k_cap
+    acc = x + r
+    thr = float(rec[3:4].view(torch.float32))
+    assert torch.equal(idx, (acc.abs() > thr).nonzero().view(-1))
+    # the threshold is the walk's top node times 1.25^(chosen - 5)
+    mean, std = float(acc.double().mean()), float(acc.double().std())
+    t = (mean + z * std) * 2.25 * 1.25 ** (chosen - 5)
+    assert abs(thr - t) <= 1e-6 * t
+    rebuilt = rr.clone()
+    rebuilt[idx] += val
+    assert torch.equal(rebuilt, acc)

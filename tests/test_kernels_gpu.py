@@ -536,3 +536,21 @@ def test_last_block_handoff_stress(cuda, mode):
             unsent = torch.ones(n, dtype=torch.bool)
             unsent[idx] = False
             assert float(val.abs().min()) >= float(acc.abs()[unsent].max()), it
+
+
+def test_gaussian_overflow_extension_gpu_matches_mirror(cuda):
+    """Power-law tail: an overflow-extension threshold (ladder slots 6..15,
+    counted for the rare elements above the lowest of them) resolves the k_cap
+    overflow; GPU record and residual equal the CPU mirror's."""
+    n = 400_000 + 37
+    g = torch.Generator().manual_seed(21)
+    u = torch.rand(n, generator=g).clamp_min(1e-12)
+    x = (u ** (-1.0 / 2.5) - 1.0) * 1e-3 * torch.sign(torch.randn(n, generator=g))
+    r = torch.zeros(n)
+    k = n // 1000
+    k_cap = math.ceil(4 * k / 3)
+    (xg, rg, recg, _), (xc, rc, recc, _) = _run_both(x, r, ops.MODE_GAUSSIAN, k, k_cap, True, 3,
+                                                     gaussian_z(0.001), device=cuda)
+    assert 6 <= int(recg[2]) < ops.MAX_CAND and int(recg[1]) > k_cap
+    assert torch.equal(recg, recc)
+    assert torch.equal(rg, rc)
