@@ -75,6 +75,24 @@ def _nt_cfgs(dt: torch.dtype) -> List[int]:
     return _NT_CFGS_F32 if dt == torch.float32 else _NT_CFGS
 
 
+# fp32 split-K (cfg + 10000 S: S fp32 partial planes over K slices, then one
+# reduce pass with the fused epilogue -- gemm.hip nt_splitk_reduce_kernel) for
+# row GEMMs whose output tiles cannot fill 256 CUs over a deep K: the 1x1
+# convolutions of stages 3-4 at the reference's batch 32 (M = 1568, N = 512,
+# K = 2048 is 52 tiles of 128x128).
+_SPLITK_BASE = (4, 1, 1001, 1002, 1003)
+_SPLITK_MAX_OUT = 1 << 22
+_SPLITK_GRIDS = (0, 1 << 20)
+
+
+def _splitk_cfgs(dt: torch.dtype, M: int, N: int, K: int) -> List[int]:
+    """Split-K candidate configs of an [M, K] x [N, K]^T fp32 GEMM (empty when
+    its output alone fills the chip)."""
+    if dt != torch.float32 or M * N > _SPLITK_MAX_OUT:
+        return []
+    return [c + 10000 * S for S in (2, 4, 8) if K % (64 * S) == 0 and K // S >= 128 for c in _SPLITK_BASE]
+
+
 def _dkey(dt: torch.dtype) -> tuple:
     """Autotune key suffix: fp32 keys are tagged, bf16 keys keep their
     round-2 form so the shipped tuning cache stays valid."""
@@ -259,14 +277,17 @@ def _fwd(x: torch.Tensor, w: torch.Tensor, s: int, stats_box=None, bias=None) ->
     st = None
     if stats_box is not None:
         st = torch.empty(2, min(1280, (M + 63) // 64), K, dtype=torch.float32, device=x.device)
+    split = []
     if k == 1 and s == 1:
         X, Y, Wm = _rows(x), _rows(y), w.reshape(K, C)
         run = lambda c, mb: g.gemm_nt(X, Wm, Y, c, mb, st, bias)  # noqa: E731
+        split = _splitk_cfgs(dt, M, K, C)
     else:
         z = _zero(x.device)
         run = lambda c, mb: g.conv_nt(x, w, y, z, s, p, c, mb, st, bias)  # noqa: E731
     b16 = bias.to(dt) if bias is not None else None
     cands = [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in _nt_cfgs(dt) for mb in _NT_GRIDS]
+    cands += [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in split for mb in _SPLITK_GRIDS]
     wino = bias is None and _wino_ok(dt, k, s, C, K) and _wino_shape_fits(N, H, W, C, K)
     if wino:
         cands += _wino_cands(x, w, y, False, st)
@@ -317,6 +338,7 @@ def _dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, lz=None, plink=No
         return torch.ops.aten.convolution_backward(dy, xs, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
                                                    [True, False, False])[0]
     cands = []
+    split = []
     dx = None
     if s == 2:
         # stride 2: the four parity classes of dX as stride-1 implicit GEMMs over dY
@@ -330,12 +352,15 @@ def _dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, lz=None, plink=No
             DY, DX = _rows(dy), _rows(dx)
             Wt = _lazy(lambda: w.reshape(K, C).t().contiguous())
             run = lambda c, mb: g.gemm_nt(DY, Wt(), DX, c, mb, **kw)  # noqa: E731
+            if lz is None:
+                split = _splitk_cfgs(dt, N * H * W, C, K)
         else:
             # dX = conv(dY, W') with W'[c][kh][kw][k] = W[k][KH-1-kh][KW-1-kw][c]
             wf = _lazy(lambda: w.flip(2, 3).transpose(0, 1).contiguous(memory_format=_CL))
             z = _zero(dy.device)
             run = lambda c, mb: g.conv_nt(dy, wf(), dx, z, 1, p, c, mb, **kw)  # noqa: E731
         cands = [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in _nt_cfgs(dt) for mb in _NT_GRIDS]
+        cands += [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in split for mb in _SPLITK_GRIDS]
     if lz is not None:
         cands.append((("mat", 0, 0), lambda: _dgrad(plink.materialize(), w, x_shape, s)))
         ch = _pick(("dgrad", N, C, H, W, K, k, s) + _dkey(dt) + ("lz",), cands)
@@ -394,7 +419,9 @@ def _dgrad_bn(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, link, lz=None,
         H2 = _rows(h)
         D2 = _rows(dy2) if dy2 is not None else None
         run = lambda c, mb: g.gemm_nt(DY, Wt(), DZ, c, mb, st, None, H2, D2, mask, **kw)  # noqa: E731
+        split = _splitk_cfgs(dt, M, C, K) if lz is None else []
     else:
+        split = []
         wf = _lazy(lambda: w.flip(2, 3).transpose(0, 1).contiguous(memory_format=_CL))
         z = _zero(dy.device)
         run = lambda c, mb: g.conv_nt(dy, wf(), dz, z, 1, p, c, mb, st, None, h, dy2, mask, **kw)  # noqa: E731
@@ -402,6 +429,7 @@ def _dgrad_bn(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, link, lz=None,
     # BN-backward epilogue
     cands = [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in _nt_cfgs(dt) if c % 10 <= 4 or c >= 1000
              for mb in _NT_GRIDS]
+    cands += [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in split for mb in _SPLITK_GRIDS]
     key = ("dgrad_bn", N, C, H, W, K, k, s, dy2 is not None) + _dkey(dt)
     if lz is not None:
         cands.append((("mat", 0, 0), lambda: _dgrad_bn(plink.materialize(), w, x_shape, s, link)))

@@ -1038,9 +1038,18 @@ int64_t gemm_nt(at::Tensor A, at::Tensor B, at::Tensor C, int64_t cfg, int64_t m
   gk::LazyArgs lz{};
   const bool has_lz = lazy_args(lz_x, lz_coef, lz_padz, lz_padx, A, K, &lz);
   c10::DeviceGuard guard(A.device());
+  // cfg >= 10000: split-K over S = cfg / 10000 fp32 partial planes (gemm.hip nt_splitk_reduce_kernel)
+  const int64_t S = cfg / 10000;
+  at::Tensor ws;
+  if (S > 1) {
+    TORCH_CHECK(A.scalar_type() == at::kFloat && !has_lz && S <= 16 && K % (64 * S) == 0,
+                "gemm_nt split-K: fp32, no lazy operand, S <= 16 and K % (64 S) == 0");
+    ws = at::empty({S, M, N}, A.options().dtype(at::kFloat));
+  }
   const int r = gk::gemm_nt(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), M, (int)N,
                             (int)K, A.scalar_type() == at::kFloat, (int)cfg, (int)max_blocks, sp, rows,
-                            bias_ptr(bias, N), has_bn ? &bn : nullptr, has_lz ? &lz : nullptr, cur_stream(A));
+                            bias_ptr(bias, N), has_bn ? &bn : nullptr, has_lz ? &lz : nullptr, cur_stream(A),
+                            S > 1 ? ws.data_ptr<float>() : nullptr);
   TORCH_CHECK(r >= 0, "gemm_nt: the lazy operand's coefficient table does not fit this tile configuration");
   return r;
 }

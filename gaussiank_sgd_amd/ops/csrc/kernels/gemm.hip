@@ -86,6 +86,10 @@ struct ConvGeo {
   // (n * RH + 2 oh + RA) * RW + 2 ow + RB of the RH x RW output; RZ also writes
   // zeros to the three other parity positions (1x1 stride-2: those get no tap)
   int RH, RW, RA, RB, RZ;
+  // gemm_nt split-K (row GEMMs only): KZ > 1 launches KZ planes along z, plane z
+  // multiplies K slices [z K, (z + 1) K) of A and B into its own fp32 output
+  // plane C + z M ldc (plain epilogue); nt_splitk_reduce_kernel sums the planes
+  int KZ;
 };
 
 // BatchNorm-backward epilogue (grad-input GEMM of the convolution that consumes
@@ -191,6 +195,14 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
   constexpr bool bnb = BNB;
   static_assert(NS >= 2 && NS <= 4, "stages");
   constexpr int LPW = Cfg::LPW;
+  if constexpr (!GATHER && !LZ) {
+    if (gridDim.z > 1) {   // split-K plane (ConvGeo::KZ): K is the per-plane depth
+      const int64_t z = blockIdx.z;
+      A += z * K;
+      B += z * K;
+      C += z * M * ldc;
+    }
+  }
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: LDS-DMA M0 and fragment bases in SGPRs
@@ -686,12 +698,13 @@ int launch_nt(const T* A, int64_t lda, const T* B, int64_t ldb, T* C, int64_t ld
   const int64_t mtiles = (M + Cfg::BM - 1) / Cfg::BM;
   const int lds = Cfg::lds_bytes(K, NS, lz.C);
   const int per_cu = (160 * 1024) / lds > 0 ? (160 * 1024) / lds : 1;
-  int64_t gx = ((int64_t)256 * per_cu + ntiles - 1) / ntiles;
+  const int kz = (!GATHER && !LZ && geo.KZ > 1) ? geo.KZ : 1;
+  int64_t gx = ((int64_t)256 * per_cu + ntiles * kz - 1) / (ntiles * kz);
   if (max_blocks > 0) gx = max_blocks;
   if (gx < 1) gx = 1;
   if (gx > mtiles) gx = mtiles;
   if (stats && gx > stats_rows) gx = stats_rows;   // one partial row per block
-  dim3 grid((unsigned)gx, (unsigned)ntiles);
+  dim3 grid((unsigned)gx, (unsigned)ntiles, (unsigned)kz);
   static bool attr = [] {
     return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<WM, WN, BRES, NS, GATHER, MSB, BNB, T, LZ>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
@@ -1479,13 +1492,101 @@ int nt_dispatch(const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
 #undef GK_NTA
 }
 
+// Split-K epilogue: C = sum of the KZ fp32 planes (+ bias), with the epilogue
+// of the fused kernel -- BatchNorm statistics partials of the output, or the
+// BN-backward dz = mask ? dx + dy2 : 0 with sum(dz), sum(dz * h) -- one
+// partial row per block ([gy][N] layout of bn_finalize_kernel).  Block: 64
+// column quads x 4 row lanes over a contiguous row range.
+__global__ __launch_bounds__(256) void nt_splitk_reduce_kernel(const float* __restrict__ ws, int S, int64_t M, int N,
+                                                               float* __restrict__ C, int64_t ldc,
+                                                               const float* __restrict__ bias,
+                                                               float* __restrict__ stats, int64_t stats_ld,
+                                                               int64_t rows_per_block, BnBwd bb) {
+  const int q = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int n = (blockIdx.y * 64 + q) * 4;
+  const bool colok = n < N;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = r0 + rows_per_block < M ? r0 + rows_per_block : M;
+  const int64_t plane = M * (int64_t)N;
+  const float* hp = static_cast<const float*>(bb.h);
+  const float* d2p = static_cast<const float*>(bb.dy2);
+  f32x4 b = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (bias && colok) b = *reinterpret_cast<const f32x4*>(bias + n);
+  float ps[4] = {0.f, 0.f, 0.f, 0.f}, pq[4] = {0.f, 0.f, 0.f, 0.f};
+  if (colok) {
+    for (int64_t m = r0 + rl; m < r1; m += 4) {
+      const float* src = ws + m * N + n;
+      f32x4 v = *reinterpret_cast<const f32x4*>(src);
+      for (int z = 1; z < S; ++z) v += *reinterpret_cast<const f32x4*>(src + z * plane);
+      v += b;
+      if (hp) {
+        const f32x4 hv = *reinterpret_cast<const f32x4*>(hp + m * ldc + n);
+        const f32x4 d2 = d2p ? *reinterpret_cast<const f32x4*>(d2p + m * ldc + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+        const uint32_t bits = bb.mask ? (uint32_t)bb.mask[m * (N >> 2) + (n >> 2)] : 0xfu;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float dz = (bits >> r) & 1u ? v[r] + d2[r] : 0.f;
+          v[r] = dz;
+          ps[r] += dz;
+          pq[r] = fmaf(dz, hv[r], pq[r]);
+        }
+      } else if (stats) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          ps[r] += v[r];
+          pq[r] = fmaf(v[r], v[r], pq[r]);
+        }
+      }
+      *reinterpret_cast<f32x4*>(C + m * ldc + n) = v;
+    }
+  }
+  if (!stats) return;
+  __shared__ float red[2][4][256];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    red[0][rl][q * 4 + r] = ps[r];
+    red[1][rl][q * 4 + r] = pq[r];
+  }
+  __syncthreads();
+  const int c = threadIdx.x;   // 256 columns of this block
+  const int nc = blockIdx.y * 256 + c;
+  if (nc < N) {
+    const float sa = (red[0][0][c] + red[0][1][c]) + (red[0][2][c] + red[0][3][c]);
+    const float sb = (red[1][0][c] + red[1][1][c]) + (red[1][2][c] + red[1][3][c]);
+    stats[(int64_t)blockIdx.x * N + nc] = sa;
+    stats[stats_ld + (int64_t)blockIdx.x * N + nc] = sb;
+  }
+}
+
 int gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N, int K,
             bool f32, int cfg, int max_blocks, float* stats, int stats_rows, const float* bias, const BnBwdArgs* bn,
-            const LazyArgs* lazy, hipStream_t stream) {
+            const LazyArgs* lazy, hipStream_t stream, float* splitk_ws) {
   ConvGeo g{};
   g.bias = bias;
   const BnBwd bb = bn ? BnBwd{bn->h, bn->dy2, bn->mask} : BnBwd{};
   const int64_t sld = (int64_t)stats_rows * N;
+  const int S = cfg / 10000;
+  if (S > 1) {
+    // split-K (fp32 row GEMM, host-checked: K % (64 S) == 0, no lazy operand):
+    // KZ plain partial planes into splitk_ws [S][M][N], then the reduce epilogue
+    if (!f32 || lazy || splitk_ws == nullptr || K % (64 * S) != 0) return -1;
+    ConvGeo gz{};
+    gz.KZ = S;
+    const int r = nt_dispatch<false, float>(A, lda, B, ldb, splitk_ws, N, M, N, K / S, cfg % 10000, max_blocks, gz,
+                                            nullptr, 0, 0, BnBwd{}, nullptr, stream);
+    if (r < 0) return r;
+    const int ny = (N + 255) / 256;
+    int64_t gx = 1024 / ny;
+    const int64_t rmax = (M + 3) / 4;
+    if (gx > rmax) gx = rmax;
+    if (stats && gx > stats_rows) gx = stats_rows;
+    if (gx < 1) gx = 1;
+    const int64_t rpb = (M + gx - 1) / gx;
+    gx = (M + rpb - 1) / rpb;
+    hipLaunchKernelGGL(nt_splitk_reduce_kernel, dim3((unsigned)gx, (unsigned)ny), dim3(256), 0, stream, splitk_ws, S,
+                       M, N, static_cast<float*>(C), ldc, bias, stats, sld, rpb, bb);
+    return (int)gx;
+  }
   return f32 ? nt_dispatch<false, float>(A, lda, B, ldb, C, ldc, M, N, K, cfg, max_blocks, g, stats, sld, stats_rows, bb, lazy, stream)
              : nt_dispatch<false, uint16_t>(A, lda, B, ldb, C, ldc, M, N, K, cfg, max_blocks, g, stats, sld, stats_rows, bb, nullptr, stream);
 }

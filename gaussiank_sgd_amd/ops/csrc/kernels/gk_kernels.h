@@ -331,7 +331,7 @@ struct LazyArgs {
 // bias (optional): fp32 [N] added in the epilogue (before rounding and statistics)
 int gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N, int K,
             bool f32, int cfg, int max_blocks, float* stats, int stats_rows, const float* bias, const BnBwdArgs* bn,
-            const LazyArgs* lazy, hipStream_t stream);
+            const LazyArgs* lazy, hipStream_t stream, float* splitk_ws = nullptr);
 void gemm_tn_acc(const void* G, int64_t ldg, const void* X, int64_t ldx, float* W, int64_t ldw, int64_t M, int N,
                  int K, bool f32, int cfg, int splits, const LazyArgs* lazy, hipStream_t stream);
 // Implicit-GEMM KHxKW convolution (stride S, zero padding P) over NHWC:

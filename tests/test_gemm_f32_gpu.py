@@ -131,6 +131,66 @@ def test_conv_tn_acc_f32(g, N, C, H, Co, k, s, p, cfg, splits):
     assert err <= 1e-5 * wr.grad.abs().max().item() + 1e-5, err
 
 
+@pytest.mark.parametrize("M,N,K", [(1568, 512, 2048), (6272 + 5, 256, 1024), (100, 64, 512)])
+@pytest.mark.parametrize("cfg", [20004, 40001, 81001, 21002, 41003, 80004])
+@pytest.mark.parametrize("mb", [0, 1 << 20, 3])
+def test_gemm_nt_f32_splitk_bias_stats(g, M, N, K, cfg, mb):
+    """Split-K (cfg + 10000 S): S fp32 partial planes over K slices, summed by
+    the reduce epilogue with the bias and BatchNorm-statistics partials."""
+    S = cfg // 10000
+    if K % (64 * S):
+        pytest.skip("K not divisible")
+    torch.manual_seed(M + N + cfg)
+    A = torch.randn(M, K, device="cuda")
+    B = torch.randn(N, K, device="cuda") * K ** -0.5
+    bias = torch.randn(N, device="cuda")
+    C = torch.full((M, N), float("nan"), device="cuda")
+    st = torch.full((2, min(1280, (M + 63) // 64), N), float("nan"), device="cuda")
+    rows = g.gemm_nt(A, B, C, cfg, mb, st, bias)
+    ref = A.double() @ B.double().t() + bias.double()
+    assert (C.double() - ref).abs().max().item() <= _tol(A.double().abs() @ B.double().abs().t() + 1)
+    assert 1 <= rows <= st.shape[1]
+    s = st[:, :rows].double().sum(1)
+    Cd = C.double()
+    assert torch.allclose(s[0], Cd.sum(0), rtol=1e-5, atol=1e-3)
+    assert torch.allclose(s[1], (Cd * Cd).sum(0), rtol=1e-5, atol=1e-3)
+    C2 = torch.full((M, N), float("nan"), device="cuda")
+    g.gemm_nt(A, B, C2, cfg, mb)                       # plain epilogue
+    assert (C2.double() - (ref - bias.double())).abs().max().item() <= _tol(A.double().abs() @ B.double().abs().t() + 1)
+
+
+def test_gemm_nt_f32_splitk_refuses_bad_k(g):
+    A = torch.randn(64, 192, device="cuda")
+    B = torch.randn(64, 192, device="cuda")
+    C = torch.empty(64, 64, device="cuda")
+    with pytest.raises(RuntimeError):
+        g.gemm_nt(A, B, C, 40004, 0)                    # K = 192 is not a multiple of 64 * 4
+
+
+@pytest.mark.parametrize("twin", [False, True])
+@pytest.mark.parametrize("cfg", [20004, 41002])
+def test_dgrad_bn_epilogue_f32_splitk(g, twin, cfg):
+    """Split-K grad-input with the BN-backward epilogue in the reduce pass."""
+    torch.manual_seed(7 + twin)
+    M, C, Co = 1568 + 3, 256, 1024
+    dy = torch.randn(M, Co, device="cuda")
+    w = torch.randn(Co, C, device="cuda") * Co ** -0.5
+    h = torch.randn(M, C, device="cuda")
+    dy2 = torch.randn(M, C, device="cuda") if twin else None
+    relu = torch.rand(M, C, device="cuda") > 0.4
+    bits = relu.reshape(M, C // 4, 4).to(torch.int32)
+    mask = (bits * torch.tensor([1, 2, 4, 8], device="cuda", dtype=torch.int32)).sum(-1).to(torch.uint8).reshape(-1)
+    ref = dy.double() @ w.double() + (dy2.double() if twin else 0)
+    ref = torch.where(relu, ref, torch.zeros_like(ref))
+    dz = torch.full((M, C), float("nan"), device="cuda")
+    st = torch.full((2, 64, C), float("nan"), device="cuda")
+    rows = g.gemm_nt(dy, w.t().contiguous(), dz, cfg, 0, st, None, h, dy2, mask)
+    assert (dz.double() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item() + 1e-5
+    s = st[:, :rows].double().sum(1)
+    assert torch.allclose(s[0], ref.sum(0), rtol=1e-5, atol=1e-4)
+    assert torch.allclose(s[1], (ref * h.double()).sum(0), rtol=1e-5, atol=1e-4)
+
+
 @pytest.mark.parametrize("k", [1, 3])
 @pytest.mark.parametrize("twin", [False, True])
 @pytest.mark.parametrize("cfg", [4, 1002, 1003, 1105])
