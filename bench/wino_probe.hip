@@ -12,6 +12,14 @@
 
 #include "winograd.hip"
 
+// the split-K reduce lives in gemm.hip (not linked into this probe; splits are never requested here)
+namespace gk {
+int splitk_reduce(const float*, int, int64_t, int, float*, int64_t, const float*, float*, int, const BnBwdArgs*,
+                  hipStream_t) {
+  return -1;
+}
+}  // namespace gk
+
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 
 __global__ void fill_kernel(float* p, int64_t n, uint32_t seed) {

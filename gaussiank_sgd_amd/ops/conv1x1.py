@@ -250,10 +250,17 @@ def _wino_cands(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, flip: bool,
     g = _g()
     u = torch.empty(16 * w.shape[0] * w.shape[1], dtype=torch.float32, device=x.device)
 
-    def run(mb):
+    def run(mb, sp=1):
         g.wino_weights(w, u, flip)
-        return g.wino_conv(x, u, out, mb, st, *bn)
-    return [(("wino", 0, mb), (lambda mb=mb: run(mb))) for mb in _WINO_GRIDS]
+        return g.wino_conv(x, u, out, mb, st, *bn, splits=sp)
+    cands = [(("wino", 0, mb), (lambda mb=mb: run(mb))) for mb in _WINO_GRIDS]
+    # small batches: fewer (64-tile x 64-channel) blocks than CUs -> also offer
+    # input-channel splits (fp32 partial planes + one reduce pass with the epilogue)
+    N, Ci, H, W = x.shape
+    blocks = -(-(N * ((H + 1) // 2) * ((W + 1) // 2)) // 64) * (out.shape[1] // 64)
+    if blocks < 256:
+        cands += [(("wino", sp, 0), (lambda sp=sp: run(0, sp))) for sp in (2, 4) if Ci % (8 * sp) == 0]
+    return cands
 
 
 def _forced(cands: list) -> list:

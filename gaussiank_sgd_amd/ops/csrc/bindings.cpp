@@ -1143,7 +1143,8 @@ void wino_weights(at::Tensor w, at::Tensor u, bool flip) {
 // x: [N, Ci, H, W], y: [N, Co, H, W], both channels-last fp32.  Optional
 // BatchNorm statistics partials / BN-backward epilogue as conv_nt.
 int64_t wino_conv(at::Tensor x, at::Tensor u, at::Tensor y, int64_t max_blocks, c10::optional<at::Tensor> stats,
-                  c10::optional<at::Tensor> bn_h, c10::optional<at::Tensor> bn_dy2, c10::optional<at::Tensor> bn_mask) {
+                  c10::optional<at::Tensor> bn_h, c10::optional<at::Tensor> bn_dy2, c10::optional<at::Tensor> bn_mask,
+                  int64_t splits) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.dim() == 4 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast),
               "wino_conv: x must be a channels-last fp32 GPU tensor");
@@ -1164,8 +1165,15 @@ int64_t wino_conv(at::Tensor x, at::Tensor u, at::Tensor y, int64_t max_blocks, 
   gk::BnBwdArgs bn{};
   const bool has_bn = bn_bwd_args(bn_h, bn_dy2, bn_mask, N * H * W, Co, Co, sp != nullptr, at::kFloat, &bn);
   c10::DeviceGuard guard(x.device());
-  return gk::wino_conv(x.data_ptr<float>(), u.data_ptr<float>(), y.data_ptr<float>(), (int)N, (int)H, (int)W, (int)Ci,
-                       (int)Co, (int)max_blocks, sp, rows, has_bn ? &bn : nullptr, cur_stream(x));
+  // splits > 1: input-channel split into fp32 partial planes + one reduce pass
+  TORCH_CHECK(splits >= 1 && splits <= 16 && Ci % (8 * splits) == 0, "wino_conv: splits in [1, 16] dividing Ci / 8");
+  at::Tensor ws;
+  if (splits > 1) ws = at::empty({splits, N * H * W, Co}, x.options());
+  const int r = gk::wino_conv(x.data_ptr<float>(), u.data_ptr<float>(), y.data_ptr<float>(), (int)N, (int)H, (int)W,
+                              (int)Ci, (int)Co, (int)max_blocks, sp, rows, has_bn ? &bn : nullptr, cur_stream(x),
+                              (int)splits, splits > 1 ? ws.data_ptr<float>() : nullptr);
+  TORCH_CHECK(r >= 0, "wino_conv: split configuration refused");
+  return r;
 }
 
 // out ([K, C, 3, 3] channels-last fp32) += dW of the 3x3 stride-1 convolution
@@ -1797,7 +1805,7 @@ TORCH_LIBRARY(gksgd, m) {
   m.def("wino_wgrad_ws(int N, int H, int W, int C, int K, int splits=0) -> int", &wino_wgrad_ws);
   m.def("wino_wgrad(Tensor x, Tensor dy, Tensor(a!) out, Tensor(b!) part, int splits=0) -> ()");
   m.def("wino_conv(Tensor x, Tensor u, Tensor(a!) y, int max_blocks=0, Tensor(b!)? stats=None, Tensor? bn_h=None, "
-        "Tensor? bn_dy2=None, Tensor? bn_mask=None) -> int");
+        "Tensor? bn_dy2=None, Tensor? bn_mask=None, int splits=1) -> int");
   m.def("conv_dgrad_s2(Tensor dy, Tensor w, Tensor(a!) dx, Tensor zero, int cfg=0, int max_blocks=0, "
         "Tensor? lz_x=None, Tensor? lz_coef=None, Tensor? lz_padz=None, Tensor? lz_padx=None) -> ()");
   m.def("bn_bwd_lazy_pre(Tensor x, Tensor part, int rows, Tensor? w, Tensor mean, Tensor invstd, "

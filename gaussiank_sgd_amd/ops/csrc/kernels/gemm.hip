@@ -1558,6 +1558,22 @@ __global__ __launch_bounds__(256) void nt_splitk_reduce_kernel(const float* __re
   }
 }
 
+int splitk_reduce(const float* ws, int S, int64_t M, int N, float* C, int64_t ldc, const float* bias, float* stats,
+                  int stats_rows, const BnBwdArgs* bn, hipStream_t stream) {
+  const BnBwd bb = bn ? BnBwd{bn->h, bn->dy2, bn->mask} : BnBwd{};
+  const int ny = (N + 255) / 256;
+  int64_t gx = 1024 / ny;
+  const int64_t rmax = (M + 3) / 4;
+  if (gx > rmax) gx = rmax;
+  if (stats && gx > stats_rows) gx = stats_rows;
+  if (gx < 1) gx = 1;
+  const int64_t rpb = (M + gx - 1) / gx;
+  gx = (M + rpb - 1) / rpb;
+  hipLaunchKernelGGL(nt_splitk_reduce_kernel, dim3((unsigned)gx, (unsigned)ny), dim3(256), 0, stream, ws, S, M, N, C,
+                     ldc, bias, stats, (int64_t)stats_rows * N, rpb, bb);
+  return (int)gx;
+}
+
 int gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N, int K,
             bool f32, int cfg, int max_blocks, float* stats, int stats_rows, const float* bias, const BnBwdArgs* bn,
             const LazyArgs* lazy, hipStream_t stream, float* splitk_ws) {
@@ -1575,17 +1591,7 @@ int gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int
     const int r = nt_dispatch<false, float>(A, lda, B, ldb, splitk_ws, N, M, N, K / S, cfg % 10000, max_blocks, gz,
                                             nullptr, 0, 0, BnBwd{}, nullptr, stream);
     if (r < 0) return r;
-    const int ny = (N + 255) / 256;
-    int64_t gx = 1024 / ny;
-    const int64_t rmax = (M + 3) / 4;
-    if (gx > rmax) gx = rmax;
-    if (stats && gx > stats_rows) gx = stats_rows;
-    if (gx < 1) gx = 1;
-    const int64_t rpb = (M + gx - 1) / gx;
-    gx = (M + rpb - 1) / rpb;
-    hipLaunchKernelGGL(nt_splitk_reduce_kernel, dim3((unsigned)gx, (unsigned)ny), dim3(256), 0, stream, splitk_ws, S,
-                       M, N, static_cast<float*>(C), ldc, bias, stats, sld, rpb, bb);
-    return (int)gx;
+    return splitk_reduce(splitk_ws, S, M, N, static_cast<float*>(C), ldc, bias, stats, stats_rows, bn, stream);
   }
   return f32 ? nt_dispatch<false, float>(A, lda, B, ldb, C, ldc, M, N, K, cfg, max_blocks, g, stats, sld, stats_rows, bb, lazy, stream)
              : nt_dispatch<false, uint16_t>(A, lda, B, ldb, C, ldc, M, N, K, cfg, max_blocks, g, stats, sld, stats_rows, bb, nullptr, stream);

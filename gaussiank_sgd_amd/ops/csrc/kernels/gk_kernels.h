@@ -332,6 +332,11 @@ struct LazyArgs {
 int gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N, int K,
             bool f32, int cfg, int max_blocks, float* stats, int stats_rows, const float* bias, const BnBwdArgs* bn,
             const LazyArgs* lazy, hipStream_t stream, float* splitk_ws = nullptr);
+// C[M, N] (row stride ldc) = sum of the S fp32 planes ws[S][M][N] (+ bias), with the
+// BatchNorm statistics partials (stats != nullptr) or the BN-backward epilogue (bn);
+// returns the number of partial rows written (<= stats_rows)
+int splitk_reduce(const float* ws, int S, int64_t M, int N, float* C, int64_t ldc, const float* bias, float* stats,
+                  int stats_rows, const BnBwdArgs* bn, hipStream_t stream);
 void gemm_tn_acc(const void* G, int64_t ldg, const void* X, int64_t ldx, float* W, int64_t ldw, int64_t M, int N,
                  int K, bool f32, int cfg, int splits, const LazyArgs* lazy, hipStream_t stream);
 // Implicit-GEMM KHxKW convolution (stride S, zero padding P) over NHWC:
@@ -373,7 +378,8 @@ void stem_f32_wgrad(const float* x, const float* dy, int N, int H, int W, float*
                     int64_t s1, int64_t s2, int64_t s3, hipStream_t stream);
 void wino_weights(const float* w, float* u, int Co, int Ci, int flip, hipStream_t stream);
 int wino_conv(const float* x, const float* u, float* y, int N, int H, int W, int Ci, int Co, int max_blocks,
-              float* stats, int stats_rows, const BnBwdArgs* bn, hipStream_t stream);
+              float* stats, int stats_rows, const BnBwdArgs* bn, hipStream_t stream, int splits = 1,
+              float* split_ws = nullptr);
 //   wino_wgrad  : out[K][3][3][C] (fp32, channels-last) += dW of the 3x3 stride-1
 //                 convolution x[N, H, W, C] -> dy[N, H, W, K] (C, K % 64 == 0);
 //                 part: wino_wgrad_splits(...) * 16 * K * C fp32 workspace

@@ -66,6 +66,7 @@ struct WinoGeo {
   int H, W, Ci, Co, TH, TW, ntiles;
   uint32_t xbytes;   // bytes of the input tensor (< 2^31: buffer-descriptor range check)
   uint32_t ybytes;   // bytes of the output tensor (< 2^31; BN-backward operands have its shape)
+  int64_t yplane;    // split over the input channels (grid z > 1): floats between output planes
 };
 
 struct WBnb {                // BN-backward epilogue operands (gemm.hip BnBwd, fp32)
@@ -127,7 +128,12 @@ wino_f23_kernel(const float* __restrict__ x, const float* __restrict__ u, float*
   const int fi = lane & 15, fq = lane >> 4;
   const int k0 = blockIdx.y * WBK;
   const int ntb = (g.ntiles + WBT - 1) / WBT;
-  const int nst = g.Ci / WCK;
+  // split over the input channels (small batches: too few tile blocks to fill
+  // the chip): plane z accumulates stages [sb, sb + nst) into its own output
+  // plane (plain epilogue); splitk_reduce sums the planes with the epilogue
+  const int nst = g.Ci / WCK / (int)gridDim.z;
+  const int sb = (int)blockIdx.z * nst;
+  if (!STATS && !BNB && gridDim.z > 1) y += (int64_t)blockIdx.z * g.yplane;
   const int my_tb = (int)blockIdx.x < ntb ? (ntb - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
   const int total = my_tb * nst;
   const int THW = g.TH * g.TW;
@@ -179,7 +185,7 @@ wino_f23_kernel(const float* __restrict__ x, const float* __restrict__ u, float*
                           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(xa >> 32)),
                           (uint32_t)__builtin_amdgcn_readfirstlane((int)g.xbytes), 0x00020000u};
   auto gload_v = [&](int s, int r) __attribute__((always_inline)) {
-    const int so = __builtin_amdgcn_readfirstlane(s * WCK * 4);
+    const int so = __builtin_amdgcn_readfirstlane((sb + s) * WCK * 4);
 #pragma unroll
     for (int p = 0; p < 16; ++p) {
 #ifdef GK_WINO_PROBE_NOLOAD
@@ -203,7 +209,7 @@ wino_f23_kernel(const float* __restrict__ x, const float* __restrict__ u, float*
   auto gload_u = [&](int s, int b) __attribute__((always_inline)) {
 #ifndef GK_WINO_PROBE_NOLOAD
     GK_LDS char* ub = (GK_LDS char*)wlds + (b * WSTAGE + WVS) * 4;
-    const float* us = u + ((int64_t)s * 16 * g.Co + k0) * 8;
+    const float* us = u + ((int64_t)(sb + s) * 16 * g.Co + k0) * 8;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int q = wave * 4 + i, xi = q >> 1, half = q & 1;
@@ -434,11 +440,12 @@ wino_f23_kernel(const float* __restrict__ x, const float* __restrict__ u, float*
 
 template <bool STATS, bool BNB>
 int launch_wino(const float* x, const float* u, float* y, const WinoGeo& g, int max_blocks, float* stats,
-                int stats_rows, const WBnb& bb, hipStream_t stream) {
+                int stats_rows, const WBnb& bb, hipStream_t stream, int splits = 1) {
   const int ntb = (g.ntiles + WBT - 1) / WBT;
   const int nkb = g.Co / WBK;
   // persistent along tiles, about one block per CU (128 KiB of LDS), x extent a multiple of 8
-  int gx = max_blocks > 0 ? max_blocks : ((256 + nkb - 1) / nkb + 7) / 8 * 8;
+  // (with z planes too: block id x + gx (y + ny z) keeps a tile block's planes on one XCD)
+  int gx = max_blocks > 0 ? max_blocks : ((256 + nkb * splits - 1) / (nkb * splits) + 7) / 8 * 8;
   if (gx > ntb) gx = ntb;
   if ((STATS || BNB) && gx > stats_rows) gx = stats_rows;   // one partial row per block
   if (gx < 1) gx = 1;
@@ -447,8 +454,8 @@ int launch_wino(const float* x, const float* u, float* y, const WinoGeo& g, int 
                                hipFuncAttributeMaxDynamicSharedMemorySize, WLDS) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL((wino_f23_kernel<STATS, BNB>), dim3((unsigned)gx, (unsigned)nkb), dim3(512), WLDS, stream, x, u,
-                     y, g, stats, (int64_t)stats_rows * g.Co, bb);
+  hipLaunchKernelGGL((wino_f23_kernel<STATS, BNB>), dim3((unsigned)gx, (unsigned)nkb, (unsigned)splits), dim3(512), WLDS,
+                     stream, x, u, y, g, stats, (int64_t)stats_rows * g.Co, bb);
   return gx;
 }
 
@@ -691,11 +698,19 @@ void wino_weights(const float* w, float* u, int Co, int Ci, int flip, hipStream_
 }
 
 int wino_conv(const float* x, const float* u, float* y, int N, int H, int W, int Ci, int Co, int max_blocks,
-              float* stats, int stats_rows, const BnBwdArgs* bn, hipStream_t stream) {
-  WinoGeo g{H, W, Ci, Co, (H + 1) / 2, (W + 1) / 2, 0, 0, 0};
+              float* stats, int stats_rows, const BnBwdArgs* bn, hipStream_t stream, int splits, float* split_ws) {
+  WinoGeo g{H, W, Ci, Co, (H + 1) / 2, (W + 1) / 2, 0, 0, 0, 0};
   g.ntiles = N * g.TH * g.TW;
   g.xbytes = (uint32_t)((int64_t)N * H * W * Ci * 4);
   g.ybytes = (uint32_t)((int64_t)N * H * W * Co * 4);
+  if (splits > 1) {
+    // input-channel split: plain partial planes into split_ws [splits][N H W][Co],
+    // then one reduce pass with the statistics / BN-backward epilogue
+    if (split_ws == nullptr || Ci % (WCK * splits) != 0) return -1;
+    g.yplane = (int64_t)N * H * W * Co;
+    launch_wino<false, false>(x, u, split_ws, g, max_blocks, nullptr, 0, WBnb{}, stream, splits);
+    return splitk_reduce(split_ws, splits, (int64_t)N * H * W, Co, y, Co, nullptr, stats, stats_rows, bn, stream);
+  }
   const WBnb bb = bn ? WBnb{static_cast<const float*>(bn->h), static_cast<const float*>(bn->dy2), bn->mask} : WBnb{};
   if (bn) return launch_wino<false, true>(x, u, y, g, max_blocks, stats, stats_rows, bb, stream);
   if (stats) return launch_wino<true, false>(x, u, y, g, max_blocks, stats, stats_rows, bb, stream);
@@ -714,7 +729,7 @@ int wino_wgrad_splits(int N, int H, int W, int C, int K, int splits) {
 
 void wino_wgrad(const float* x, const float* dy, float* part, float* out, int N, int H, int W, int C, int K,
                 int splits, hipStream_t stream) {
-  WinoGeo g{H, W, C, K, (H + 1) / 2, (W + 1) / 2, 0, 0, 0};
+  WinoGeo g{H, W, C, K, (H + 1) / 2, (W + 1) / 2, 0, 0, 0, 0};
   g.ntiles = N * g.TH * g.TW;
   g.xbytes = (uint32_t)((int64_t)N * H * W * C * 4);
   splits = wino_wgrad_splits(N, H, W, C, K, splits);

@@ -210,3 +210,55 @@ def test_wino_wgrad_nonsquare(g, N, C, H, W, K, splits):
     bound = torch.ops.aten.convolution_backward(dy.double().abs(), x.double().abs(), w.double(), None, [1, 1], [1, 1],
                                                 [1, 1], False, [0, 0], 1, [False, True, False])[1]
     assert (out.double() - ref).abs().max().item() <= _tol(bound)
+
+
+@pytest.mark.parametrize("N,C,H,K,splits", [(4, 512, 7, 512, 4), (2, 256, 14, 256, 2), (3, 64, 9, 128, 2),
+                                              (1, 128, 7, 64, 4)])
+@pytest.mark.parametrize("mb", [0, 3])
+def test_wino_fwd_split_stats(g, N, C, H, K, splits, mb):
+    """Input-channel split (small batches): fp32 partial planes summed by the
+    reduce pass, which also writes the BatchNorm statistics partials."""
+    x, w = _case(N, C, H, K, N + C + H + K + splits)
+    u = torch.empty(16 * K * C, device="cuda")
+    g.wino_weights(w, u, False)
+    y = torch.full((N, K, H, H), float("nan"), device="cuda").contiguous(memory_format=CL)
+    st = torch.full((2, 64, K), float("nan"), device="cuda")
+    rows = g.wino_conv(x, u, y, mb, st, splits=splits)
+    ref = F.conv2d(x.double(), w.double(), padding=1)
+    bound = F.conv2d(x.double().abs(), w.double().abs(), padding=1)
+    assert (y.double() - ref).abs().max().item() <= _tol(bound)
+    yd = y.double().permute(0, 2, 3, 1).reshape(-1, K)
+    s = st[:, :rows].double().sum(1)
+    assert torch.allclose(s[0], yd.sum(0), rtol=1e-5, atol=1e-3)
+    assert torch.allclose(s[1], (yd * yd).sum(0), rtol=1e-5, atol=1e-3)
+    y2 = torch.full_like(y, float("nan"))
+    g.wino_conv(x, u, y2, mb, splits=splits)            # plain epilogue
+    assert (y2.double() - ref).abs().max().item() <= _tol(bound)
+
+
+@pytest.mark.parametrize("twin", [False, True])
+def test_wino_dgrad_bn_epilogue_split(g, twin):
+    torch.manual_seed(31 + twin)
+    N, C, Co, H = 2, 128, 256, 7
+    dy = torch.randn(N, Co, H, H, device="cuda").contiguous(memory_format=CL)
+    w = (torch.randn(Co, C, 3, 3, device="cuda") * 0.05).contiguous(memory_format=CL)
+    h = torch.randn(N, C, H, H, device="cuda").contiguous(memory_format=CL)
+    dy2 = torch.randn(N, C, H, H, device="cuda").contiguous(memory_format=CL) if twin else None
+    relu = torch.rand(N, C, H, H, device="cuda") > 0.4
+    M = N * H * H
+    bits = relu.permute(0, 2, 3, 1).reshape(M, C // 4, 4).to(torch.int32)
+    mask = (bits * torch.tensor([1, 2, 4, 8], device="cuda", dtype=torch.int32)).sum(-1).to(torch.uint8).reshape(-1)
+    ref_dx = torch.ops.aten.convolution_backward(dy.double(), h.double(), w.double(), None, [1, 1], [1, 1], [1, 1],
+                                                 False, [0, 0], 1, [True, False, False])[0]
+    dz_ref = torch.where(relu, ref_dx + (dy2.double() if twin else 0), torch.zeros_like(ref_dx))
+    u = torch.empty(16 * Co * C, device="cuda")
+    g.wino_weights(w, u, True)
+    dz = torch.full(h.shape, float("nan"), device="cuda").contiguous(memory_format=CL)
+    st = torch.full((2, 64, C), float("nan"), device="cuda")
+    rows = g.wino_conv(dy, u, dz, 0, st, h, dy2, mask, splits=4)
+    assert (dz.double() - dz_ref).abs().max().item() <= 1e-5 * dz_ref.abs().max().item() + 1e-5
+    s = st[:, :rows].double().sum(1)
+    dzc = dz_ref.permute(0, 2, 3, 1).reshape(M, C)
+    hc = h.double().permute(0, 2, 3, 1).reshape(M, C)
+    assert torch.allclose(s[0], dzc.sum(0), rtol=1e-5, atol=1e-4)
+    assert torch.allclose(s[1], (dzc * hc).sum(0), rtol=1e-5, atol=1e-4)
