@@ -524,12 +524,6 @@ def main() -> int:
     alive = True
     if P > 1 and os.environ.get("GKSGD_BENCH_PROBE", "1") == "1":
         alive = optional_phase("collectives", out, P, collectives_probe)
-    if rank == 0 and os.environ.get("GKSGD_GEMM_DUMP"):
-        from gaussiank_sgd_amd.ops.conv1x1 import tuned_choices, tuning_log
-        log = tuning_log()
-        with open(os.environ["GKSGD_GEMM_DUMP"], "w") as f:
-            json.dump([[list(k), list(v), [[list(t), r] for t, r in log.get(k, [])]]
-                       for k, v in tuned_choices().items()], f)
     release(ph)
     ph = None
 
@@ -588,6 +582,13 @@ def main() -> int:
         if alive:
             alive = optional_phase(tag + "_dense", out, P, ref_dense)
 
+    # every phase's shapes (the reference-batch phases tune their own keys)
+    if rank == 0 and os.environ.get("GKSGD_GEMM_DUMP"):
+        from gaussiank_sgd_amd.ops.conv1x1 import tuned_choices, tuning_log
+        log = tuning_log()
+        with open(os.environ["GKSGD_GEMM_DUMP"], "w") as f:
+            json.dump([[list(k), list(v), [[list(t), r] for t, r in log.get(k, [])]]
+                       for k, v in tuned_choices().items()], f)
     if rank == 0 and os.environ.get("GKSGD_GEMM_SAVE"):
         from gaussiank_sgd_amd.ops.conv1x1 import save_choices
         save_choices(os.environ["GKSGD_GEMM_SAVE"])
