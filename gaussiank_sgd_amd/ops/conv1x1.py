@@ -93,6 +93,10 @@ def _splitk_cfgs(dt: torch.dtype, M: int, N: int, K: int) -> List[int]:
     return [c + 10000 * S for S in (2, 4, 8) if K % (64 * S) == 0 and K // S >= 128 for c in _SPLITK_BASE]
 
 
+# (the implicit-GEMM convolutions split the same way over their (tap, channel)
+# K slices: conv_nt with cfg + 10000 S)
+
+
 def _dkey(dt: torch.dtype) -> tuple:
     """Autotune key suffix: fp32 keys are tagged, bf16 keys keep their
     round-2 form so the shipped tuning cache stays valid."""
@@ -292,6 +296,7 @@ def _fwd(x: torch.Tensor, w: torch.Tensor, s: int, stats_box=None, bias=None) ->
     else:
         z = _zero(x.device)
         run = lambda c, mb: g.conv_nt(x, w, y, z, s, p, c, mb, st, bias)  # noqa: E731
+        split = _splitk_cfgs(dt, M, K, k * k * C)
     b16 = bias.to(dt) if bias is not None else None
     cands = [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in _nt_cfgs(dt) for mb in _NT_GRIDS]
     cands += [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in split for mb in _SPLITK_GRIDS]

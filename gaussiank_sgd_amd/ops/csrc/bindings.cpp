@@ -1114,10 +1114,19 @@ int64_t conv_nt(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor zero, int64
   gk::LazyArgs lz{};
   const bool has_lz = lazy_args(lz_x, lz_coef, lz_padz, lz_padx, x, C, &lz);
   c10::DeviceGuard guard(x.device());
+  // cfg >= 10000: split-K over S = cfg / 10000 fp32 partial planes of the (tap, channel) slices
+  const int64_t S = cfg / 10000;
+  at::Tensor ws;
+  if (S > 1) {
+    TORCH_CHECK(x.scalar_type() == at::kFloat && !has_lz && S <= 16 && C % 32 == 0 && (KH * KW * C / 32) % S == 0,
+                "conv_nt split-K: fp32, no lazy operand, S <= 16 dividing the K slices");
+    ws = at::empty({S, M, Co}, x.options());
+  }
   const int r = gk::conv_nt(x.data_ptr(), zero.data_ptr(), (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)stride,
                             (int)pad, (int)KH, (int)KW, w.data_ptr(), y.data_ptr(), M, (int)Co,
                             x.scalar_type() == at::kFloat, (int)cfg, (int)max_blocks, sp, rows, bias_ptr(bias, Co),
-                            has_bn ? &bn : nullptr, has_lz ? &lz : nullptr, cur_stream(x));
+                            has_bn ? &bn : nullptr, has_lz ? &lz : nullptr, cur_stream(x),
+                            S > 1 ? ws.data_ptr<float>() : nullptr);
   TORCH_CHECK(r >= 0, "conv_nt: the lazy operand's coefficient table does not fit this tile configuration");
   return r;
 }

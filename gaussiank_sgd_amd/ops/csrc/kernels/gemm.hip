@@ -195,10 +195,22 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
   constexpr bool bnb = BNB;
   static_assert(NS >= 2 && NS <= 4, "stages");
   constexpr int LPW = Cfg::LPW;
-  if constexpr (!GATHER && !LZ) {
-    if (gridDim.z > 1) {   // split-K plane (ConvGeo::KZ): K is the per-plane depth
+  // split-K plane (ConvGeo::KZ): K is the per-plane depth; a gathered A starts
+  // at the plane's first (tap, channel) slice instead of a column offset
+  int kz_kh = 0, kz_kw = 0, kz_c0 = 0;
+  if constexpr (!LZ) {
+    if (gridDim.z > 1) {
       const int64_t z = blockIdx.z;
-      A += z * K;
+      if constexpr (GATHER) {
+        const int per = geo.C / E::KS;   // K slices per tap
+        const int s0 = (int)z * (K / E::KS);
+        const int tap = s0 / per;
+        kz_c0 = (s0 - tap * per) * E::KS;
+        kz_kh = tap / geo.KW;
+        kz_kw = tap - kz_kh * geo.KW;
+      } else {
+        A += z * K;
+      }
       B += z * K;
       C += z * M * ldc;
     }
@@ -305,7 +317,7 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
   };
   int64_t s_mt = blockIdx.x;    // tile of the next stage to issue
   int s_ks = 0;                 // its K slice
-  int s_kh = 0, s_kw = 0, s_c0 = 0;   // gather: tap and channel offset of that slice
+  int s_kh = kz_kh, s_kw = kz_kw, s_c0 = kz_c0;   // gather: tap and channel offset of that slice
   int s_t = 0;
   int s_buf = 0;                // LDS stage of the next issue (s_t % NS)
   set_rows(s_mt);
@@ -350,7 +362,7 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
     }
     if (++s_ks == nk) {
       s_ks = 0;
-      s_kh = s_kw = s_c0 = 0;
+      s_kh = kz_kh; s_kw = kz_kw; s_c0 = kz_c0;
       s_mt += gridDim.x;
       if (s_t < T_) set_rows(s_mt);
     }
@@ -401,7 +413,17 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     const bool pf = s_t < T_;   // a stage to issue during this slice's MFMAs (wave-uniform)
+    // fp32 spreads the next stage's LDS-DMA over the MFMA groups (16 fp32 MFMAs
+    // per group hide each piece's issue cost); bf16 (4 MFMAs per group) issues
+    // the whole stage right after the barrier -- measured on the ResNet-50
+    // bs512 step: spreading cost bf16 ~1.4 ms (41.0 -> 42.4 ms); fp32 128.3 ms
+    // with the previous tuning choices (128.1 before), 127.0 ms after a retune
+    constexpr bool SPREAD = F32;
     if (pf) stage_prep();
+    if (!SPREAD && pf) {
+#pragma unroll
+      for (int q = 0; q < LPW; ++q) stage_issue(q);
+    }
     const char* As = stage_base + buf * Cfg::STAGE;
     buf = buf + 1 == NS ? 0 : buf + 1;
     const char* Bs = BRES ? panel + ks * Cfg::BSTAGE : As + Cfg::ASTAGES;
@@ -412,12 +434,14 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
     // the next stage is issued after group (q * NG) / LPW
     constexpr int NG = 2 * MSB;
     auto issue_group = [&](int gi) {
-      if (pf) {
+      if constexpr (SPREAD) {
+        if (pf) {
 #pragma unroll
-        for (int q = 0; q < LPW; ++q)
-          if ((q * NG) / LPW == gi) stage_issue(q);
+          for (int q = 0; q < LPW; ++q)
+            if ((q * NG) / LPW == gi) stage_issue(q);
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
-      __builtin_amdgcn_sched_barrier(0);
     };
     // Fragments: the 4 B fragments of a half are read one half ahead (both
     // halves' in flight at the slice start), the A fragment of subtile ms one
@@ -698,7 +722,7 @@ int launch_nt(const T* A, int64_t lda, const T* B, int64_t ldb, T* C, int64_t ld
   const int64_t mtiles = (M + Cfg::BM - 1) / Cfg::BM;
   const int lds = Cfg::lds_bytes(K, NS, lz.C);
   const int per_cu = (160 * 1024) / lds > 0 ? (160 * 1024) / lds : 1;
-  const int kz = (!GATHER && !LZ && geo.KZ > 1) ? geo.KZ : 1;
+  const int kz = (!LZ && geo.KZ > 1) ? geo.KZ : 1;
   int64_t gx = ((int64_t)256 * per_cu + ntiles * kz - 1) / (ntiles * kz);
   if (max_blocks > 0) gx = max_blocks;
   if (gx < 1) gx = 1;
@@ -1599,9 +1623,21 @@ int gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int
 
 int conv_nt(const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P, int KH, int KW,
             const void* B, void* Y, int64_t M, int N, bool f32, int cfg, int max_blocks, float* stats, int stats_rows,
-            const float* bias, const BnBwdArgs* bn, const LazyArgs* lazy, hipStream_t stream) {
+            const float* bias, const BnBwdArgs* bn, const LazyArgs* lazy, hipStream_t stream, float* splitk_ws) {
   ConvGeo g{zero, H, W, C, OH, OW, S, P, KW, bias};
   const int K = KH * KW * C;
+  const int SK = cfg / 10000;
+  if (SK > 1) {
+    // split-K over the (tap, channel) slices: plain partial planes, then the reduce epilogue
+    const int nks = K / 32;   // fp32 K slices
+    if (!f32 || lazy || splitk_ws == nullptr || nks % SK != 0 || C % 32 != 0) return -1;
+    ConvGeo gz{zero, H, W, C, OH, OW, S, P, KW, nullptr};
+    gz.KZ = SK;
+    const int r = nt_dispatch<true, float>(X, C, B, K, splitk_ws, N, M, N, K / SK, cfg % 10000, max_blocks, gz,
+                                           nullptr, 0, 0, BnBwd{}, nullptr, stream);
+    if (r < 0) return r;
+    return splitk_reduce(splitk_ws, SK, M, N, static_cast<float*>(Y), N, bias, stats, stats_rows, bn, stream);
+  }
   const BnBwd bb = bn ? BnBwd{bn->h, bn->dy2, bn->mask} : BnBwd{};
   const int64_t sld = (int64_t)stats_rows * N;
   return f32 ? nt_dispatch<true, float>(X, C, B, K, Y, N, M, N, K, cfg, max_blocks, g, stats, sld, stats_rows, bb, lazy, stream)

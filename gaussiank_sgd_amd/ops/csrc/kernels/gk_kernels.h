@@ -346,7 +346,8 @@ void gemm_tn_acc(const void* G, int64_t ldg, const void* X, int64_t ldx, float* 
 // >= 128 zero bytes (the padding row).
 int conv_nt(const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P, int KH, int KW,
             const void* B, void* Y, int64_t M, int N, bool f32, int cfg, int max_blocks, float* stats, int stats_rows,
-            const float* bias, const BnBwdArgs* bn, const LazyArgs* lazy, hipStream_t stream);
+            const float* bias, const BnBwdArgs* bn, const LazyArgs* lazy, hipStream_t stream,
+            float* splitk_ws = nullptr);
 // One parity class (RA, RB) of a stride-2 convolution's grad-input as a stride-1,
 // padding-0 KHxKW implicit GEMM over dY (H x W x C, the forward output) whose
 // OH x OW output grid is stored at rows (n*RH + 2 oh + RA) * RW + 2 ow + RB of

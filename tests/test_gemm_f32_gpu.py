@@ -101,6 +101,37 @@ def test_conv_nt_f32(g, N, C, H, Co, k, s, p, cfg):
     assert (y.double() - ref).abs().max().item() <= _tol(bound)
 
 
+@pytest.mark.parametrize("N,C,H,Co,k,s,p", [(4, 512, 14, 512, 3, 2, 1), (2, 256, 28, 256, 3, 2, 1),
+                                            (3, 128, 9, 64, 3, 1, 1), (4, 1024, 14, 256, 1, 2, 0)])
+@pytest.mark.parametrize("cfg", [20004, 41002, 81001, 30004])
+def test_conv_nt_f32_splitk_stats(g, N, C, H, Co, k, s, p, cfg):
+    """Implicit-GEMM split-K: each plane starts at its own (tap, channel)
+    slice (planes cross tap boundaries when the slice count per tap does not
+    divide), reduce epilogue with the bias and BatchNorm statistics."""
+    S = cfg // 10000
+    torch.manual_seed(N + C + H + Co + cfg)
+    x, w = _conv_case(N, C, H, Co, k)
+    if (k * k * C // 32) % S:
+        OH = (H + 2 * p - k) // s + 1
+        y = torch.empty(N, Co, OH, OH, device="cuda").contiguous(memory_format=CL)
+        with pytest.raises(RuntimeError):
+            g.conv_nt(x, w, y, torch.zeros(64, device="cuda"), s, p, cfg, 0)
+        return
+    bias = torch.randn(Co, device="cuda")
+    zero = torch.zeros(64, device="cuda")
+    ref = F.conv2d(x.double(), w.double(), bias.double(), stride=s, padding=p)
+    bound = F.conv2d(x.double().abs(), w.double().abs(), bias.double().abs(), stride=s, padding=p)
+    y = torch.full(ref.shape, float("nan"), device="cuda").contiguous(memory_format=CL)
+    M = ref.shape[0] * ref.shape[2] * ref.shape[3]
+    st = torch.full((2, min(1280, (M + 63) // 64), Co), float("nan"), device="cuda")
+    rows = g.conv_nt(x, w, y, zero, s, p, cfg, 0, st, bias)
+    assert (y.double() - ref).abs().max().item() <= _tol(bound)
+    yd = y.double().permute(0, 2, 3, 1).reshape(-1, Co)
+    sm = st[:, :rows].double().sum(1)
+    assert torch.allclose(sm[0], yd.sum(0), rtol=1e-5, atol=1e-3)
+    assert torch.allclose(sm[1], (yd * yd).sum(0), rtol=1e-5, atol=1e-3)
+
+
 @pytest.mark.parametrize("N,C,H,Co,k,s,p", [c for c in CONV_CASES if c[5] == 2])
 @pytest.mark.parametrize("cfg", [0, 1, 4, 13, 1002, 1103])
 def test_conv_dgrad_s2_f32(g, N, C, H, Co, k, s, p, cfg):
