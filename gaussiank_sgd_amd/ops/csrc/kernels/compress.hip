@@ -714,23 +714,28 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const float* __restrict__
                                                        const uint32_t* __restrict__ seed_dev, DecArgs da) {
   if (cond && ctrl->fallback == 0) return;
   if (seed_dev != nullptr) seed = __builtin_amdgcn_readfirstlane(*seed_dev);
-  // Per-lane counters: every (element, candidate) test is a compare + carry-in
-  // add on the VALU (v_cmp + v_addc), summed over the wave once per block.
-  // (Round 3 accumulated ballots on the scalar unit instead -- one s_bcnt1 +
-  // s_add per test, serialised behind each v_cmp's SGPR write: 40 us for the
-  // 6-candidate Gaussian ladder on a 25.6 M bucket, half the HBM rate.)  NC
+  // Per-lane counters, summed over the wave once per block.  |x| keys are
+  // < 2^31, so [key < b] is the sign bit of key - b (b <= 2^31): one v_sub +
+  // one v_lshr_add per (element, candidate), independent chains, and
+  // count(key >= b) = in-range elements - count(key < b).  (A compare +
+  // carry-in add -- v_cmp + v_addc -- chains every candidate through VCC with
+  // a wait state per pair: 45 us for the 6-candidate Gaussian ladder on a
+  // 25.6 M bucket, ~5 us per candidate; round 3's ballots on the scalar unit
+  // were 40 us.)  Hash / sample keys span 32 bits and keep the compare.  NC
   // (>= the live candidate count, chosen by the host from the mode) is a
   // compile-time bound: no per-test branch; dead candidates carry bound
   // 0xffffffff and count nothing.
+  constexpr bool SIGN = KEYKIND == kKeyAbs;
   uint32_t bnd[NC];
 #pragma unroll
   for (int j = 0; j < NC; ++j) bnd[j] = __builtin_amdgcn_readfirstlane(ctrl->bound[j]);
-  uint32_t cnt[NC];
+  uint32_t cnt[NC];   // SIGN: elements below bound j; else: elements at or above it
 #pragma unroll
   for (int j = 0; j < NC; ++j) cnt[j] = 0u;
-  // NX ascending extension candidates (bound[NC ..]): tested only for the
-  // elements above the lowest of them (a branch that is almost never taken
-  // for a Gaussian-k overflow ladder), so they cost one compare per element
+  uint32_t nin = 0u;  // SIGN: in-range elements of this lane
+  // NX ascending extension candidates (bound[NC ..]): tested only when one of
+  // a float4's elements is above the lowest of them (a branch that is almost
+  // never taken for a Gaussian-k overflow ladder)
   constexpr int NXA = NX > 0 ? NX : 1;
   uint32_t xb[NXA], xc[NXA];
 #pragma unroll
@@ -738,13 +743,20 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const float* __restrict__
     xb[j] = NX > 0 ? __builtin_amdgcn_readfirstlane(ctrl->bound[NC + j]) : 0xffffffffu;
     xc[j] = 0u;
   }
+  auto test_ext = [&](uint32_t key, bool in) {
+#pragma unroll
+    for (int j = 0; j < NXA; ++j) xc[j] += (in && key >= xb[j]) ? 1u : 0u;
+  };
   auto test = [&](uint32_t key, bool in) {
+    if constexpr (SIGN) {
+      nin += in ? 1u : 0u;
 #pragma unroll
-    for (int j = 0; j < NC; ++j) cnt[j] += (in && key >= bnd[j]) ? 1u : 0u;
-    if (NX > 0 && in && key >= xb[0]) {
+      for (int j = 0; j < NC; ++j) cnt[j] += in ? (key - bnd[j]) >> 31 : 0u;
+    } else {
 #pragma unroll
-      for (int j = 0; j < NXA; ++j) xc[j] += key >= xb[j] ? 1u : 0u;
+      for (int j = 0; j < NC; ++j) cnt[j] += (in && key >= bnd[j]) ? 1u : 0u;
     }
+    if (NX > 0 && in && key >= xb[0]) test_ext(key, true);
   };
   const int64_t ntiles = (n + kTileElems - 1) / kTileElems;
   const int64_t t0 = (int64_t)blockIdx.x * chunk_tiles;
@@ -771,8 +783,24 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const float* __restrict__
         for (int j4 = 0; j4 < 4; ++j4) {
           const uint32_t k4[4] = {abs_key(b[j4].x), abs_key(b[j4].y), abs_key(b[j4].z), abs_key(b[j4].w)};
 #pragma unroll
-          for (int q = 0; q < 4; ++q) test(k4[q], true);
+          for (int q = 0; q < 4; ++q) {
+            if constexpr (SIGN) {
+#pragma unroll
+              for (int j = 0; j < NC; ++j) cnt[j] += (k4[q] - bnd[j]) >> 31;
+            } else {
+#pragma unroll
+              for (int j = 0; j < NC; ++j) cnt[j] += k4[q] >= bnd[j] ? 1u : 0u;
+            }
+          }
+          if constexpr (NX > 0) {   // one guard per float4
+            const uint32_t m = max(max(k4[0], k4[1]), max(k4[2], k4[3]));
+            if (m >= xb[0]) {
+#pragma unroll
+              for (int q = 0; q < 4; ++q) test_ext(k4[q], true);
+            }
+          }
         }
+        nin += 16u;
       };
       ld(tile, ba);
       if (tile + 1 < tf) ld(tile + 1, bb);
@@ -824,6 +852,10 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const float* __restrict__
     }
 #pragma unroll
     for (int q = 0; q < 16; ++q) test(key[q], (inb >> q) & 1u);
+  }
+  if constexpr (SIGN) {
+#pragma unroll
+    for (int j = 0; j < NC; ++j) cnt[j] = bnd[j] == 0xffffffffu ? 0u : nin - cnt[j];
   }
   // per-lane counts -> per-wave totals (one reduction per block)
   static_assert(NC + NX <= kMaxCand, "candidate slots");

@@ -479,30 +479,47 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
         b[s] = *reinterpret_cast<const Frag*>(Bs + rb * 128 + ((c ^ swz(rb)) << 4));
       }
     };
+    if constexpr (!F32) {
+      // bf16: each half's A and B fragments read at its start, then its MFMAs
+      // (the round-3 schedule; streaming A one subtile ahead measured slower here)
 #pragma unroll
-    for (int kk = 0; kk < NBB; ++kk) ldB(kk, bv[kk]);
-    Frag an = ldA(0, 0);
+      for (int kk = 0; kk < 2; ++kk) {
+        Frag av[MSB], bh[4];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int sb = NBB == 2 ? kk : 0;
-      if (NBB == 1 && kk == 1) ldB(1, bv[0]);
+        for (int s2 = 0; s2 < MSB; ++s2) av[s2] = ldA(kk, s2);
+        ldB(kk, bh);
 #pragma unroll
-      for (int ms = 0; ms < MSB; ++ms) {
-        const Frag a = an;
-        if (ms + 1 < MSB) an = ldA(kk, ms + 1);
-        else if (kk == 0) an = ldA(1, 0);
-        if constexpr (F32) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int ns = 0; ns < 4; ++ns)
-              acc[ms][ns] = __builtin_amdgcn_mfma_f32_16x16x4f32(bv[sb][ns][j], a[j], acc[ms][ns], 0, 0, 0);
-        } else {
+        for (int ms = 0; ms < MSB; ++ms)
 #pragma unroll
           for (int ns = 0; ns < 4; ++ns)
-            acc[ms][ns] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv[sb][ns], a, acc[ms][ns], 0, 0, 0);
+            acc[ms][ns] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[ns], av[ms], acc[ms][ns], 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < NBB; ++kk) ldB(kk, bv[kk]);
+      Frag an = ldA(0, 0);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int sb = NBB == 2 ? kk : 0;
+        if (NBB == 1 && kk == 1) ldB(1, bv[0]);
+#pragma unroll
+        for (int ms = 0; ms < MSB; ++ms) {
+          const Frag a = an;
+          if (ms + 1 < MSB) an = ldA(kk, ms + 1);
+          else if (kk == 0) an = ldA(1, 0);
+          if constexpr (F32) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+              for (int ns = 0; ns < 4; ++ns)
+                acc[ms][ns] = __builtin_amdgcn_mfma_f32_16x16x4f32(bv[sb][ns][j], a[j], acc[ms][ns], 0, 0, 0);
+          } else {
+#pragma unroll
+            for (int ns = 0; ns < 4; ++ns)
+              acc[ms][ns] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv[sb][ns], a, acc[ms][ns], 0, 0, 0);
+          }
+          issue_group(kk * MSB + ms);
         }
-        issue_group(kk * MSB + ms);
       }
     }
     if (pf) stage_advance();

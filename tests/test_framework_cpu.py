@@ -357,3 +357,43 @@ def test_winograd_candidate_filter_checks_every_operand():
     # below the limit in every operand: offered
     assert cv._wino_shape_fits(32, 56, 56, 256, 64)
     assert "wino" in cv._dgrad_key(32, 64, 56, 56, 64, 3, 1, torch.float32)
+
+
+def test_splitk_candidates_only_for_underfilled_deep_gemms():
+    """fp32 split-K configs (cfg + 10000 S) are offered only when the output
+    is small (<= 4 M elements) and K splits into >= 128-deep, 64-aligned
+    planes; bf16 never gets them (partial planes are fp32)."""
+    import torch
+    from gaussiank_sgd_amd.ops import conv1x1 as cv
+    c = cv._splitk_cfgs(torch.float32, 1568, 512, 2048)          # stage-4 1x1 at bs32
+    assert c and all(x >= 20000 for x in c)
+    S = sorted({x // 10000 for x in c})
+    assert S == [2, 4, 8]
+    assert all(2048 % (64 * s) == 0 and 2048 // s >= 128 for s in S)
+    assert {x % 10000 for x in c} == set(cv._SPLITK_BASE)
+    assert cv._splitk_cfgs(torch.bfloat16, 1568, 512, 2048) == []
+    assert cv._splitk_cfgs(torch.float32, 25088 * 16, 512, 2048) == []   # bs512: the output fills the chip
+    assert {x // 10000 for x in cv._splitk_cfgs(torch.float32, 1568, 512, 256)} == {2}   # 256 / 4 < 128
+    assert cv._splitk_cfgs(torch.float32, 1568, 512, 192) == []           # 192 % 128 != 0
+    # implicit-GEMM convolutions split over their tap x channel depth (3x3 x 512)
+    assert {x // 10000 for x in cv._splitk_cfgs(torch.float32, 1568, 512, 9 * 512)} == {2, 4, 8}
+
+
+def test_winograd_split_candidates_small_grids_only():
+    """Input-channel splits of the Winograd kernel are offered when the
+    64-tile x 64-channel block grid is below one block per CU (bs32 stages
+    3-4), never for the bs512 shapes."""
+    import torch
+    from gaussiank_sgd_amd.ops import conv1x1 as cv
+
+    def tags(N, C, H, K):
+        x = torch.empty(N, C, H, H, device="meta")
+        w = torch.empty(K, C, 3, 3, device="meta")
+        y = torch.empty(N, K, H, H, device="meta")
+        return [t for t, _ in cv._wino_cands(x, w, y, False)]
+    small = tags(32, 512, 7, 512)          # 512 tiles -> 8 x 8 = 64 blocks
+    assert ("wino", 2, 0) in small and ("wino", 4, 0) in small
+    big = tags(512, 512, 7, 512)           # 8192 tiles -> 128 x 8 blocks
+    assert all(t[1] == 0 for t in big)
+    odd = tags(32, 24, 7, 64)              # Ci = 24: 8 x 3 channel stages -> no 2- or 4-way split
+    assert all(t[1] == 0 for t in odd)
