@@ -73,6 +73,26 @@ __device__ __forceinline__ T ld_dev(const T* p) {
   return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Bulk device-coherent reads for the single-workgroup hand-offs (finalize /
+// decide / fallback key).  The compiler follows every agent-scope atomic load
+// with s_waitcnt vmcnt(0), so a loop of ld_dev() is a chain of serial
+// round trips past the XCD's L2 (64 in a row for the decide's block counts:
+// most of the count pass's 41 us against select's 25 us over the same data).
+// A raw buffer load with the sc1 cache policy is the instruction the atomic
+// load becomes, but an ordinary load to the compiler: issued back to back,
+// one wait before the first use.  base: wave-uniform array base.
+constexpr int kCpolSc1 = 16;   // SC1 (LLVM CPol::SC1)
+template <typename T>
+__device__ __forceinline__ T ld_coh(const T* base, int idx) {
+  static_assert(sizeof(T) == 4 || sizeof(T) == 8, "32- or 64-bit element");
+  const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(base), (short)0, 0x7fffffff, 0x00020000);
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, idx * 4, 0, kCpolSc1));
+  } else {
+    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, idx * 8, 0, kCpolSc1));
+  }
+}
+
 __host__ __device__ inline Ws carve(void* base) {
   char* p = reinterpret_cast<char*>(base);
   Ws w;
@@ -130,14 +150,20 @@ __device__ __forceinline__ uint64_t block_excl_scan_u64(uint64_t v, uint64_t* sh
 }
 
 // Find the digit holding the kr-th largest key (1-based) in a histogram of
-// nbins (multiple of 256).  Result broadcast to every thread.
+// nbins (multiple of 256, <= 256 kRadixPer).  Result broadcast to every thread.
+constexpr int kRadixPer = (kRadixBins0 > kRadixBins1 ? kRadixBins0 : kRadixBins1) / kBlock;
+static_assert(kRadixBins2 <= kRadixBins0 && kRadixPer <= 8, "radix bins per thread");
 __device__ void radix_find(const uint32_t* hist, int nbins, int64_t kr, uint64_t* sh, int* digit_out,
                            int64_t* kr_out) {
-  const int per = nbins / kBlock;
+  const int per = nbins / kBlock;   // <= kRadixPer
   const int t = threadIdx.x;
   const int hi = nbins - t * per;
+  uint32_t hv[kRadixPer];           // this thread's bins, all loads in flight at once
+#pragma unroll
+  for (int q = 0; q < kRadixPer; ++q) hv[q] = q < per ? ld_coh(hist, hi - 1 - q) : 0u;
   uint64_t ls = 0;
-  for (int q = 0; q < per; ++q) ls += ld_dev(&hist[hi - 1 - q]);
+#pragma unroll
+  for (int q = 0; q < kRadixPer; ++q) ls += hv[q];
   uint64_t tot;
   const uint64_t before = block_excl_scan_u64(ls, sh, &tot);
   __shared__ int s_digit;
@@ -146,9 +172,11 @@ __device__ void radix_find(const uint32_t* hist, int nbins, int64_t kr, uint64_t
   __syncthreads();
   if ((int64_t)before < kr && kr <= (int64_t)(before + ls)) {
     int64_t cum = (int64_t)before;
-    for (int q = 0; q < per; ++q) {
+#pragma unroll
+    for (int q = 0; q < kRadixPer; ++q) {
+      if (q >= per) break;
       const int d = hi - 1 - q;
-      const int64_t h = ld_dev(&hist[d]);
+      const int64_t h = hv[q];
       if (cum + h >= kr) { s_digit = d; s_kr = kr - cum; break; }
       cum += h;
     }
@@ -460,7 +488,13 @@ __global__ __launch_bounds__(kBlock) void radix_hist_kernel(const float* __restr
   if (PASS >= 1) {
     // eligible total (DGC sample size) and k_eff
     uint64_t loc = 0;
-    for (int b = threadIdx.x; b < kRadixBins0; b += kBlock) loc += ld_dev(&hist0[b]);
+    {
+      uint32_t hv[kRadixBins0 / kBlock];   // all loads in flight before the adds
+#pragma unroll
+      for (int q = 0; q < kRadixBins0 / kBlock; ++q) hv[q] = ld_coh(hist0, threadIdx.x + q * kBlock);
+#pragma unroll
+      for (int q = 0; q < kRadixBins0 / kBlock; ++q) loc += hv[q];
+    }
     uint64_t tot;
     (void)block_excl_scan_u64(loc, sh_scan, &tot);
     int64_t kr = k < (int64_t)tot ? k : (int64_t)tot;
@@ -518,7 +552,13 @@ __device__ void radix_resolve(const uint32_t* hist_set, int64_t k, uint64_t* sh,
   const uint32_t* hist1 = hist_set + kRadixBins0;
   const uint32_t* hist2 = hist1 + kRadixBins1;
   uint64_t loc = 0;
-  for (int b = threadIdx.x; b < kRadixBins0; b += kBlock) loc += ld_dev(&hist0[b]);
+  {
+      uint32_t hv[kRadixBins0 / kBlock];   // all loads in flight before the adds
+#pragma unroll
+      for (int q = 0; q < kRadixBins0 / kBlock; ++q) hv[q] = ld_coh(hist0, threadIdx.x + q * kBlock);
+#pragma unroll
+      for (int q = 0; q < kRadixBins0 / kBlock; ++q) loc += hv[q];
+    }
   uint64_t tot;
   (void)block_excl_scan_u64(loc, sh, &tot);
   int64_t keff = k < (int64_t)tot ? k : (int64_t)tot;
@@ -544,11 +584,16 @@ __device__ __forceinline__ void finalize_body(GkCtrl* __restrict__ ctrl, const d
   __shared__ uint64_t sh_scan[kWavesPerBlock];
   double s = 0, ss = 0, sa = 0;
   float mx = 0.f;
+  // a partial row's four loads in flight before the adds (two rows per step
+  // spill at the stats kernel's 64-VGPR budget)
   for (int b = threadIdx.x; b < nparts; b += kBlock) {
-    s += ld_dev(&partials[b * 4 + 0]);
-    ss += ld_dev(&partials[b * 4 + 1]);
-    sa += ld_dev(&partials[b * 4 + 2]);
-    mx = fmaxf(mx, (float)ld_dev(&partials[b * 4 + 3]));
+    double v[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] = ld_coh(partials, b * 4 + c);
+    s += v[0];
+    ss += v[1];
+    sa += v[2];
+    mx = fmaxf(mx, (float)v[3]);
   }
   s = block_sum(s, sh);
   ss = block_sum(ss, sh);
@@ -901,8 +946,11 @@ __device__ __forceinline__ void decide_body(GkCtrl* __restrict__ ctrl, const uin
 #pragma unroll
   for (int j = 0; j < kMaxCand; ++j) loc[j] = 0;
   for (int b = threadIdx.x; b < G; b += kBlock) {
+    uint32_t v[kMaxCand];   // all of the row's loads in flight before the first add
 #pragma unroll
-    for (int j = 0; j < kMaxCand; ++j) loc[j] += ld_dev(&blockcnt[b * kMaxCand + j]);
+    for (int j = 0; j < kMaxCand; ++j) v[j] = ld_coh(blockcnt, b * kMaxCand + j);
+#pragma unroll
+    for (int j = 0; j < kMaxCand; ++j) loc[j] += v[j];
   }
 #pragma unroll
   for (int j = 0; j < kMaxCand; ++j) {
@@ -1030,8 +1078,8 @@ __device__ __forceinline__ void decide_body(GkCtrl* __restrict__ ctrl, const uin
     const int b = threadIdx.x * kPer + q;
     gtc[q] = 0; eqc[q] = 0;
     if (b < G) {
-      gtc[q] = ld_dev(&blockcnt[b * kMaxCand + gt]);
-      if (ge >= 0) eqc[q] = (int64_t)ld_dev(&blockcnt[b * kMaxCand + ge]) - gtc[q];
+      gtc[q] = ld_coh(blockcnt, b * kMaxCand + gt);
+      if (ge >= 0) eqc[q] = (int64_t)ld_coh(blockcnt, b * kMaxCand + ge) - gtc[q];
     }
     eq_loc += eqc[q];
   }
