@@ -69,6 +69,10 @@ _TN_CFGS = [(c, s) for c in (1, 2, 3, 4, 5, 6, 7, 8, 21, 22, 23, 24, 27, 9, 29, 
 _NT_CFGS_F32 = [1, 2, 3, 4, 7, 11, 12, 13, 14, 21, 22, 23, 24, 101, 102, 103, 104, 201, 202, 203, 204,
                 1001, 1002, 1003, 1004, 1005, 1006, 1007, 1021, 1022, 1101, 1102, 1103]
 _TN_CFGS_F32 = [(c, s) for c in (1, 2, 3, 4, 5, 6, 7, 8, 9, 11, 12, 13, 14, 15, 16) for s in (0, 64)]
+# grad-weight of small-batch layers (pixel rows <= _TN_SMALL_M, e.g. ResNet-50 bs32): the default split
+# count (two rounds of block slots) trades partial-sum atomics against idle CUs; these let the tuner pick
+_TN_SMALL_M = 1 << 17
+_TN_SMALL_F32 = [(c, s) for c in (4, 5, 11, 14, 15) for s in (16, 32, 128)]
 
 
 def _nt_cfgs(dt: torch.dtype) -> List[int]:
@@ -505,8 +509,10 @@ def _wgrad_into(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, s: int, out_
     else:
         z = _zero(x.device)
         run = lambda o, c, sp: g.conv_tn_acc(dy, x, o, z, s, p, c, sp, **kw)  # noqa: E731
-    cands = [(("hip", c, sp), (lambda c=c, sp=sp: run(scratch, c, sp)))
-             for c, sp in (_TN_CFGS_F32 if dt == torch.float32 else _TN_CFGS)]
+    tn = list(_TN_CFGS_F32 if dt == torch.float32 else _TN_CFGS)
+    if dt == torch.float32 and N * OH * OW <= _TN_SMALL_M:
+        tn += _TN_SMALL_F32   # small batches: more / fewer pixel splits than the two-rounds default
+    cands = [(("hip", c, sp), (lambda c=c, sp=sp: run(scratch, c, sp))) for c, sp in tn]
     if lz is not None:
         cands.append((("mat", 0, 0), lambda: _wgrad_into(plink.materialize(), x, w, s, scratch)))
         ch = _pick(key, cands)
