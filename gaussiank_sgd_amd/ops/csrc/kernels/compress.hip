@@ -35,6 +35,7 @@
 // holds the largest entries; everything unsent stays in the residual, and the
 // header's `total` keeps the reference rule's count.
 #include <cstdlib>
+#include <cstring>
 
 #include "common.h"
 #include "gk_kernels.h"
@@ -315,6 +316,7 @@ struct FinArgs {   // finalize_body arguments (stats -> finalize hand-off)
 };
 
 struct DecArgs {   // decide_body arguments (count -> decide hand-off)
+  int in_kernel;     // 1: decide in the count pass's last block; 0: a separate decide_kernel launch
   GkCtrl* ctrl;
   int mode, loops;
   int64_t k, k_cap;
@@ -920,9 +922,16 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const float* __restrict__
     const int j = threadIdx.x;
     st_dev(&blockcnt[blockIdx.x * kMaxCand + j], j < NC + NX ? sh[0][j] + sh[1][j] + sh[2][j] + sh[3][j] : 0u);
   }
-  if (last_block(da.counter))   // decide on the totals in the last block
+  if (da.in_kernel && last_block(da.counter))   // decide on the totals in the last block
     decide_body(ctrl, blockcnt, (int)gridDim.x, da.mode, da.loops, da.k, da.k_cap, da.offsets, da.eqtake, da.blocksel,
                 da.hdr, cond, da.hist_reset);
+}
+
+// the decide as its own 1-workgroup launch (hand-off by kernel boundary)
+__global__ __launch_bounds__(kBlock) void decide_kernel(const uint32_t* __restrict__ blockcnt, int G, int cond,
+                                                        DecArgs da) {
+  decide_body(da.ctrl, blockcnt, G, da.mode, da.loops, da.k, da.k_cap, da.offsets, da.eqtake, da.blocksel, da.hdr,
+              cond, da.hist_reset);
 }
 
 // --------------------------------------------------------------------------
@@ -1250,11 +1259,25 @@ __global__ __launch_bounds__(kBlock) void select_kernel(float* __restrict__ r, i
 // live candidates of a count pass (finalize_kernel / cal_fallback_kernel ladders)
 int count_cands(const CompressArgs& a, int cond) { return cond ? kFallbackCands : ladder_cands(a.mode, a.loops); }
 
+// Single-workgroup hand-offs: by last-block arrival counter inside the
+// producing grid, or by a separate 1-workgroup launch after it.  The counter
+// costs one agent-scope atomic per block on ONE address, and the atomics
+// serialise (~19 ns each, measured: count pass on a 4 M bucket, 1024 blocks
+// of one tile each, 32 us against select's 5.5 us over the same data); a
+// launch costs ~5 us.  Default: launches (GKSGD_HANDOFF=lastblock restores
+// the in-grid hand-off).  The conditional fallback chain keeps the in-grid
+// form: it must cost nothing extra when it does not fire.
+bool handoff_by_launch() {
+  const char* e = getenv("GKSGD_HANDOFF");
+  return !(e != nullptr && strcmp(e, "lastblock") == 0);
+}
+
 template <int KEYKIND>
 void launch_count(const CompressArgs& a, const Ws& w, bool vec, int G, int64_t chunk_tiles, GkCtrl* ctrl, int cond,
                   hipStream_t s) {
   const int nc = count_cands(a, cond);
   DecArgs da;
+  da.in_kernel = (cond || !handoff_by_launch()) ? 1 : 0;
   da.ctrl = ctrl; da.mode = a.mode; da.loops = a.loops; da.k = a.k; da.k_cap = a.k_cap;
   da.offsets = w.offsets; da.eqtake = w.eqtake; da.blocksel = w.blocksel; da.hdr = a.record;
   da.hist_reset = w.hist; da.counter = w.sync + (cond ? 3 : 1);
@@ -1284,6 +1307,8 @@ void launch_count(const CompressArgs& a, const Ws& w, bool vec, int G, int64_t c
   }
 #undef GK_COUNT
 #undef GK_COUNT2
+  if (!da.in_kernel)
+    hipLaunchKernelGGL(decide_kernel, dim3(1), dim3(kBlock), 0, s, w.blockcnt, G, cond, da);
 }
 
 template <int KEYKIND>
@@ -1351,6 +1376,7 @@ void compress(const CompressArgs& a, hipStream_t s) {
   //    correction when a chunk table is given); threshold modes finalize in
   //    the last stats block (radix modes need the histograms first)
   const bool radix_mode = a.mode == kModeTopK || a.mode == kModeRandomK || a.mode == kModeDGC;
+  const bool fin_in = !radix_mode && !handoff_by_launch();   // finalize in the stats pass's last block
   const int64_t keff = a.k < a.n ? a.k : a.n;
   const int64_t n_stats = a.n_stats > 0 ? a.n_stats : a.n;
   FinArgs fa;
@@ -1366,8 +1392,8 @@ void compress(const CompressArgs& a, hipStream_t s) {
 #define GK_MC(EC, FIN)                                                                                            \
   hipLaunchKernelGGL((mc_stats_kernel<EC, FIN>), dim3(Gs), dim3(kBlock), 0, s, a.g, a.r, a.u, a.w, ch,             \
                      a.chunk_count, a.chunk_base, hp, w.partials, fa);
-    if (a.ec) { if (radix_mode) { GK_MC(true, false) } else { GK_MC(true, true) } }
-    else { if (radix_mode) { GK_MC(false, false) } else { GK_MC(false, true) } }
+    if (a.ec) { if (!fin_in) { GK_MC(true, false) } else { GK_MC(true, true) } }
+    else { if (!fin_in) { GK_MC(false, false) } else { GK_MC(false, true) } }
 #undef GK_MC
   } else {
     Gs = (int)ceil_div(a.n, (int64_t)kBlock * 16);
@@ -1377,7 +1403,7 @@ void compress(const CompressArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((stats_kernel<VEC, EC, true, ZG, FIN>), dim3(Gs), dim3(kBlock), 0, s, a.g, a.r, a.n,          \
                      w.partials, fa);
 #define GK_STATS(VEC, EC, ZG)                                                                                     \
-  if (radix_mode) { GK_STATS2(VEC, EC, ZG, false) } else { GK_STATS2(VEC, EC, ZG, true) }
+  if (!fin_in) { GK_STATS2(VEC, EC, ZG, false) } else { GK_STATS2(VEC, EC, ZG, true) }
     if (vec_gr) {
       if (a.ec) { if (a.zero_g) { GK_STATS(true, true, true) } else { GK_STATS(true, true, false) } }
       else { if (a.zero_g) { GK_STATS(true, false, true) } else { GK_STATS(true, false, false) } }
@@ -1405,8 +1431,8 @@ void compress(const CompressArgs& a, hipStream_t s) {
     }
   }
 
-  // 3. finalize (radix modes; the threshold modes finalized in the stats pass)
-  if (radix_mode)
+  // 3. finalize (radix modes, or every mode with launch hand-offs)
+  if (!fin_in)
     hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(kBlock), 0, s, ctrl, w.partials, Gs, n_stats, a.mode, a.loops,
                        a.z, a.fixed_thr, keff, hist_exact, hist_sample, a.stats_out);
 

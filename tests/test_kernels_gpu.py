@@ -483,8 +483,9 @@ def test_compress_reused_buffers_varying_sizes(cuda, mode):
         assert torch.equal(rg.cpu(), rc)
 
 
+@pytest.mark.parametrize("handoff", ["launch", "lastblock"])
 @pytest.mark.parametrize("mode", [ops.MODE_GAUSSIAN, ops.MODE_GAUSSIAN_CAL, ops.MODE_TOPK, ops.MODE_DGC])
-def test_last_block_handoff_stress(cuda, mode):
+def test_last_block_handoff_stress(cuda, mode, handoff, monkeypatch):
     """The last-block hand-offs (stats -> finalize, count -> decide, radix ->
     fallback key; compress.hip last_block) at the LARGEST grids
     (kMaxStatsBlocks / kMaxCountBlocks), back to back on one set of buffers,
@@ -494,6 +495,7 @@ def test_last_block_handoff_stress(cuda, mode):
     against the count above its own threshold (count -> decide), the record's
     indices / values / residual against that selection (decide's offsets),
     and for exact top-k the whole record against the CPU mirror."""
+    monkeypatch.setenv("GKSGD_HANDOFF", handoff)   # compress.hip handoff_by_launch()
     n = 2048 * 4096 * 2 + 4093          # > kMaxStatsBlocks full tiles: every grid at its cap
     k = n // 1000
     k_cap = (4 * k + 2) // 3 if mode != ops.MODE_TOPK else k
