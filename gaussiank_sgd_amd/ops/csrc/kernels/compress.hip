@@ -328,10 +328,11 @@ struct DecArgs {   // decide_body arguments (count -> decide hand-off)
   uint32_t* counter;
 };
 
+template <bool BATCH = false>
 __device__ __forceinline__ void finalize_body(GkCtrl* __restrict__ ctrl, const double* __restrict__ partials, int nparts, int64_t n,
                               int mode, int loops, double z, double fixed_thr, int64_t k, const uint32_t* hist_exact,
                               const uint32_t* hist_sample, float* stats_out);
-__device__ __forceinline__ void decide_body(GkCtrl* __restrict__ ctrl, const uint32_t* __restrict__ blockcnt, int G, int mode,
+__device__ __forceinline__ void decide_body(GkCtrl* __restrict__ gctrl, const uint32_t* __restrict__ blockcnt, int G, int mode,
                             int loops, int64_t k, int64_t k_cap, int64_t* __restrict__ offsets,
                             int64_t* __restrict__ eqtake, int64_t* __restrict__ blocksel, int32_t* __restrict__ hdr,
                             int cond, uint32_t* __restrict__ hist_reset);
@@ -578,6 +579,7 @@ __device__ void radix_resolve(const uint32_t* hist_set, int64_t k, uint64_t* sh,
 // --------------------------------------------------------------------------
 // finalize: statistics + candidate ladder (1 workgroup)
 // --------------------------------------------------------------------------
+template <bool BATCH>
 __device__ __forceinline__ void finalize_body(GkCtrl* __restrict__ ctrl, const double* __restrict__ partials, int nparts, int64_t n,
                               int mode, int loops, double z, double fixed_thr, int64_t k, const uint32_t* hist_exact,
                               const uint32_t* hist_sample, float* stats_out) {
@@ -586,16 +588,36 @@ __device__ __forceinline__ void finalize_body(GkCtrl* __restrict__ ctrl, const d
   __shared__ uint64_t sh_scan[kWavesPerBlock];
   double s = 0, ss = 0, sa = 0;
   float mx = 0.f;
-  // a partial row's four loads in flight before the adds (two rows per step
-  // spill at the stats kernel's 64-VGPR budget)
-  for (int b = threadIdx.x; b < nparts; b += kBlock) {
-    double v[4];
+  if (BATCH) {
+    // finalize_kernel (its own launch, full register file): every partial row
+    // of this thread in flight at once, one round trip
+    constexpr int kRows = kMaxStatsBlocks / kBlock;
+    double v[kRows][4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) v[c] = ld_coh(partials, b * 4 + c);
-    s += v[0];
-    ss += v[1];
-    sa += v[2];
-    mx = fmaxf(mx, (float)v[3]);
+    for (int i = 0; i < kRows; ++i) {
+      const int b = threadIdx.x + i * kBlock;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[i][c] = b < nparts ? ld_coh(partials, b * 4 + c) : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < kRows; ++i) {
+      s += v[i][0];
+      ss += v[i][1];
+      sa += v[i][2];
+      mx = fmaxf(mx, (float)v[i][3]);
+    }
+  } else {
+    // in the stats pass's last block: a partial row's four loads in flight
+    // before the adds (two rows per step spill at the 64-VGPR budget)
+    for (int b = threadIdx.x; b < nparts; b += kBlock) {
+      double v[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[c] = ld_coh(partials, b * 4 + c);
+      s += v[0];
+      ss += v[1];
+      sa += v[2];
+      mx = fmaxf(mx, (float)v[3]);
+    }
   }
   s = block_sum(s, sh);
   ss = block_sum(ss, sh);
@@ -725,7 +747,7 @@ __global__ __launch_bounds__(kBlock) void finalize_kernel(GkCtrl* __restrict__ c
                                                           int nparts, int64_t n, int mode, int loops, double z,
                                                           double fixed_thr, int64_t k, const uint32_t* hist_exact,
                                                           const uint32_t* hist_sample, float* stats_out) {
-  finalize_body(ctrl, partials, nparts, n, mode, loops, z, fixed_thr, k, hist_exact, hist_sample, stats_out);
+  finalize_body<true>(ctrl, partials, nparts, n, mode, loops, z, fixed_thr, k, hist_exact, hist_sample, stats_out);
 }
 
 // Calibrated mode with no candidate in [2k/3, 4k/3] (k = k_eff), or a
@@ -753,7 +775,7 @@ __device__ __forceinline__ void cal_fallback_body(GkCtrl* __restrict__ ctrl, con
 // --------------------------------------------------------------------------
 // K4: one-pass multi-threshold count (counters in registers)
 // --------------------------------------------------------------------------
-template <int KEYKIND, bool VEC, int NC, int NX = 0>
+template <int KEYKIND, bool VEC, int NC, int NX = 0, bool DEC = true>
 __global__ __launch_bounds__(kBlock) void count_kernel(const float* __restrict__ x, int64_t n, uint32_t seed,
                                                        GkCtrl* __restrict__ ctrl, int64_t chunk_tiles,
                                                        uint32_t* __restrict__ blockcnt,
@@ -922,9 +944,11 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const float* __restrict__
     const int j = threadIdx.x;
     st_dev(&blockcnt[blockIdx.x * kMaxCand + j], j < NC + NX ? sh[0][j] + sh[1][j] + sh[2][j] + sh[3][j] : 0u);
   }
-  if (da.in_kernel && last_block(da.counter))   // decide on the totals in the last block
-    decide_body(ctrl, blockcnt, (int)gridDim.x, da.mode, da.loops, da.k, da.k_cap, da.offsets, da.eqtake, da.blocksel,
-                da.hdr, cond, da.hist_reset);
+  if constexpr (DEC) {   // decide on the totals in the last block (else: decide_kernel after this grid)
+    if (last_block(da.counter))
+      decide_body(ctrl, blockcnt, (int)gridDim.x, da.mode, da.loops, da.k, da.k_cap, da.offsets, da.eqtake,
+                  da.blocksel, da.hdr, cond, da.hist_reset);
+  }
 }
 
 // the decide as its own 1-workgroup launch (hand-off by kernel boundary)
@@ -937,7 +961,7 @@ __global__ __launch_bounds__(kBlock) void decide_kernel(const uint32_t* __restri
 // --------------------------------------------------------------------------
 // decide: replay the reference decision tree, offsets per block (1 WG)
 // --------------------------------------------------------------------------
-__device__ __forceinline__ void decide_body(GkCtrl* __restrict__ ctrl, const uint32_t* __restrict__ blockcnt, int G, int mode,
+__device__ __forceinline__ void decide_body(GkCtrl* __restrict__ gctrl, const uint32_t* __restrict__ blockcnt, int G, int mode,
                             int loops, int64_t k, int64_t k_cap, int64_t* __restrict__ offsets,
                             int64_t* __restrict__ eqtake, int64_t* __restrict__ blocksel, int32_t* __restrict__ hdr,
                             int cond, uint32_t* __restrict__ hist_reset) {
@@ -945,6 +969,27 @@ __device__ __forceinline__ void decide_body(GkCtrl* __restrict__ ctrl, const uin
   __shared__ uint64_t sh_scan[kWavesPerBlock];
   __shared__ int s_chosen, s_gt, s_ge, s_stop;
   __shared__ int64_t s_quota;
+  __shared__ __attribute__((aligned(16))) GkCtrl s_ctrl;
+  // ONE batch of loads, then no global read: the control block into an LDS
+  // snapshot (one dword per thread; every ctrl read below is an LDS read and
+  // the fields the decision writes go back to global after it) and this
+  // thread's kPer block rows of counts into registers (totals AND offsets).
+  // Loaded one dependent round trip at a time this step took 16 us on the
+  // 892-block count grid (its own launch, r4c12), ~2/3 of it waiting.
+  constexpr int kCw = (int)(sizeof(GkCtrl) / 4);
+  static_assert(sizeof(GkCtrl) % 4 == 0 && kCw <= kBlock, "ctrl snapshot: one dword per thread");
+  constexpr int kPer = kMaxCountBlocks / kBlock;   // each thread owns kPer consecutive blocks
+  const uint32_t cw = threadIdx.x < kCw ? ld_coh(reinterpret_cast<const uint32_t*>(gctrl), (int)threadIdx.x) : 0u;
+  uint32_t row[kPer][kMaxCand];
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int b = threadIdx.x * kPer + q;
+#pragma unroll
+    for (int j = 0; j < kMaxCand; ++j) row[q][j] = b < G ? ld_coh(blockcnt, b * kMaxCand + j) : 0u;
+  }
+  if (threadIdx.x < kCw) reinterpret_cast<uint32_t*>(&s_ctrl)[threadIdx.x] = cw;
+  __syncthreads();
+  GkCtrl* ctrl = &s_ctrl;
   if (cond) {
     if (ctrl->fallback == 0) return;
     mode = kModeTopK;   // second decide of a fallback: exact top-k (or top-k_cap) on the radix key
@@ -953,13 +998,10 @@ __device__ __forceinline__ void decide_body(GkCtrl* __restrict__ ctrl, const uin
   // totals per candidate
   uint64_t loc[kMaxCand];
 #pragma unroll
-  for (int j = 0; j < kMaxCand; ++j) loc[j] = 0;
-  for (int b = threadIdx.x; b < G; b += kBlock) {
-    uint32_t v[kMaxCand];   // all of the row's loads in flight before the first add
+  for (int j = 0; j < kMaxCand; ++j) {
+    loc[j] = 0;
 #pragma unroll
-    for (int j = 0; j < kMaxCand; ++j) v[j] = ld_coh(blockcnt, b * kMaxCand + j);
-#pragma unroll
-    for (int j = 0; j < kMaxCand; ++j) loc[j] += v[j];
+    for (int q = 0; q < kPer; ++q) loc[j] += row[q][j];
   }
 #pragma unroll
   for (int j = 0; j < kMaxCand; ++j) {
@@ -967,11 +1009,17 @@ __device__ __forceinline__ void decide_body(GkCtrl* __restrict__ ctrl, const uin
     if (lane_id() == 0) sh_tot[wave_id()][j] = w;
   }
   __syncthreads();
+  // per-candidate totals in LDS: the decision indexes them dynamically (a
+  // private array would live in scratch)
+  __shared__ int64_t s_tot[kMaxCand];
+  if (threadIdx.x < kMaxCand) {
+    const int j = threadIdx.x;
+    s_tot[j] = (int64_t)(sh_tot[0][j] + sh_tot[1][j] + sh_tot[2][j] + sh_tot[3][j]);
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
     s_stop = 0;
-    int64_t tot[kMaxCand];
-    for (int j = 0; j < kMaxCand; ++j)
-      tot[j] = (int64_t)(sh_tot[0][j] + sh_tot[1][j] + sh_tot[2][j] + sh_tot[3][j]);
+    const int64_t* tot = s_tot;
     int chosen = 0, gt = 0, ge = -1;
     int64_t quota = 0;
     const double kd = (double)k;
@@ -1067,6 +1115,17 @@ __device__ __forceinline__ void decide_body(GkCtrl* __restrict__ ctrl, const uin
     ctrl->eq_key = ge >= 0 ? ctrl->bound[ge] : 0xffffffffu;
     ctrl->eq_quota = ge >= 0 ? quota : 0;
     ctrl->thr = (float)ctrl->cand_thr[chosen];
+    // the decision's fields back to the control block (read by the select /
+    // conditional passes and the next call)
+    gctrl->cal_c = ctrl->cal_c;
+    gctrl->cal_step = ctrl->cal_step;
+    gctrl->fallback = ctrl->fallback;
+    gctrl->ref_total = ctrl->ref_total;
+    gctrl->chosen = ctrl->chosen;
+    gctrl->sel_bound = ctrl->sel_bound;
+    gctrl->eq_key = ctrl->eq_key;
+    gctrl->eq_quota = ctrl->eq_quota;
+    gctrl->thr = ctrl->thr;
   }
   __syncthreads();
   if (s_stop) {
@@ -1078,18 +1137,20 @@ __device__ __forceinline__ void decide_body(GkCtrl* __restrict__ ctrl, const uin
   }
   const int gt = s_gt, ge = s_ge;
   const int64_t quota = s_quota;
-  // each thread owns up to 4 consecutive blocks
-  constexpr int kPer = kMaxCountBlocks / kBlock;
   int64_t gtc[kPer], eqc[kPer];
   uint64_t eq_loc = 0;
 #pragma unroll
   for (int q = 0; q < kPer; ++q) {
-    const int b = threadIdx.x * kPer + q;
-    gtc[q] = 0; eqc[q] = 0;
-    if (b < G) {
-      gtc[q] = ld_coh(blockcnt, b * kMaxCand + gt);
-      if (ge >= 0) eqc[q] = (int64_t)ld_coh(blockcnt, b * kMaxCand + ge) - gtc[q];
+    // row[q][gt], row[q][ge] by uniform selects (no dynamic register index);
+    // rows past G were loaded as zeros
+    uint32_t vg = 0u, ve = 0u;
+#pragma unroll
+    for (int j = 0; j < kMaxCand; ++j) {
+      vg = j == gt ? row[q][j] : vg;
+      ve = j == ge ? row[q][j] : ve;
     }
+    gtc[q] = vg;
+    eqc[q] = ge >= 0 ? (int64_t)ve - (int64_t)vg : 0;
     eq_loc += eqc[q];
   }
   uint64_t eq_tot;
@@ -1119,8 +1180,8 @@ __device__ __forceinline__ void decide_body(GkCtrl* __restrict__ ctrl, const uin
   if (threadIdx.x == 0) {
     const int64_t total = (int64_t)sel_tot;
     const int64_t sent = total < k_cap ? total : k_cap;
-    ctrl->total = total;
-    ctrl->sent = sent;
+    gctrl->total = total;
+    gctrl->sent = sent;
     const int64_t rt = ctrl->ref_total >= 0 ? ctrl->ref_total : total;
     hdr[0] = (int32_t)sent;
     hdr[1] = (int32_t)(rt > 0x7fffffff ? 0x7fffffff : rt);
@@ -1281,20 +1342,15 @@ void launch_count(const CompressArgs& a, const Ws& w, bool vec, int G, int64_t c
   da.ctrl = ctrl; da.mode = a.mode; da.loops = a.loops; da.k = a.k; da.k_cap = a.k_cap;
   da.offsets = w.offsets; da.eqtake = w.eqtake; da.blocksel = w.blocksel; da.hdr = a.record;
   da.hist_reset = w.hist; da.counter = w.sync + (cond ? 3 : 1);
-#define GK_COUNT2(NC, NX)                                                                                         \
+#define GK_COUNT3(NC, NX, DEC)                                                                                    \
   if (vec)                                                                                                        \
-    hipLaunchKernelGGL((count_kernel<KEYKIND, true, NC, NX>), dim3(G), dim3(kBlock), 0, s, a.r, a.n, a.seed, ctrl, \
-                       chunk_tiles, w.blockcnt, a.valid, cond, a.seed_dev, da);                                   \
+    hipLaunchKernelGGL((count_kernel<KEYKIND, true, NC, NX, DEC>), dim3(G), dim3(kBlock), 0, s, a.r, a.n, a.seed,  \
+                       ctrl, chunk_tiles, w.blockcnt, a.valid, cond, a.seed_dev, da);                             \
   else                                                                                                            \
-    hipLaunchKernelGGL((count_kernel<KEYKIND, false, NC, NX>), dim3(G), dim3(kBlock), 0, s, a.r, a.n, a.seed,     \
+    hipLaunchKernelGGL((count_kernel<KEYKIND, false, NC, NX, DEC>), dim3(G), dim3(kBlock), 0, s, a.r, a.n, a.seed, \
                        ctrl, chunk_tiles, w.blockcnt, a.valid, cond, a.seed_dev, da);
-#define GK_COUNT(NC)                                                                                              \
-  if (vec)                                                                                                        \
-    hipLaunchKernelGGL((count_kernel<KEYKIND, true, NC>), dim3(G), dim3(kBlock), 0, s, a.r, a.n, a.seed, ctrl,    \
-                       chunk_tiles, w.blockcnt, a.valid, cond, a.seed_dev, da);                                   \
-  else                                                                                                            \
-    hipLaunchKernelGGL((count_kernel<KEYKIND, false, NC>), dim3(G), dim3(kBlock), 0, s, a.r, a.n, a.seed, ctrl,   \
-                       chunk_tiles, w.blockcnt, a.valid, cond, a.seed_dev, da);
+#define GK_COUNT2(NC, NX) if (da.in_kernel) { GK_COUNT3(NC, NX, true) } else { GK_COUNT3(NC, NX, false) }
+#define GK_COUNT(NC) GK_COUNT2(NC, 0)
   if constexpr (KEYKIND == kKeyHash) {
     GK_COUNT(2)
   } else {
@@ -1307,6 +1363,7 @@ void launch_count(const CompressArgs& a, const Ws& w, bool vec, int G, int64_t c
   }
 #undef GK_COUNT
 #undef GK_COUNT2
+#undef GK_COUNT3
   if (!da.in_kernel)
     hipLaunchKernelGGL(decide_kernel, dim3(1), dim3(kBlock), 0, s, w.blockcnt, G, cond, da);
 }
