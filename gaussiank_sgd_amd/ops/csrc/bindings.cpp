@@ -1335,9 +1335,10 @@ void conv_tn_acc(at::Tensor dy, at::Tensor x, at::Tensor wout, at::Tensor zero, 
 bool add_ln_supported(int64_t H) { return gk::add_ln_supported((int)H); }
 int64_t add_ln_ws_floats(int64_t R, int64_t H) { return 2 * gk::add_ln_partial_rows(R) * H; }
 
-void check_rows_bf16(const at::Tensor& t, const char* name, int64_t R, int64_t H) {
-  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.is_contiguous() && t.numel() == R * H,
-              name, " must be a contiguous bf16 GPU tensor of R*H elements");
+void check_rows_ln(const at::Tensor& t, const char* name, int64_t R, int64_t H, at::ScalarType dt) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == dt && t.is_contiguous() && t.numel() == R * H &&
+                  reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+              name, " must be a contiguous, 16-byte aligned GPU tensor of R*H elements (bf16 or fp32, all alike)");
 }
 
 void add_ln_forward(at::Tensor a, at::Tensor x, c10::optional<at::Tensor> gamma, c10::optional<at::Tensor> beta,
@@ -1345,7 +1346,9 @@ void add_ln_forward(at::Tensor a, at::Tensor x, c10::optional<at::Tensor> gamma,
                     c10::optional<at::Tensor> seed_dev) {
   const int64_t H = x.size(-1), R = x.numel() / H;
   TORCH_CHECK(gk::add_ln_supported((int)H), "add_ln: unsupported hidden size");
-  for (auto* t : {&a, &x, &y, &h}) check_rows_bf16(*t, "add_ln tensor", R, H);
+  const auto dt = x.scalar_type();
+  TORCH_CHECK(dt == at::kBFloat16 || dt == at::kFloat, "add_ln: bf16 or fp32 storage");
+  for (auto* t : {&a, &x, &y, &h}) check_rows_ln(*t, "add_ln tensor", R, H, dt);
   TORCH_CHECK(mean.numel() >= R && rstd.numel() >= R && mean.scalar_type() == at::kFloat &&
                   rstd.scalar_type() == at::kFloat, "mean/rstd: fp32 [R]");
   const float* gp = gamma.has_value() && gamma->defined() ? gamma->data_ptr<float>() : nullptr;
@@ -1355,7 +1358,7 @@ void add_ln_forward(at::Tensor a, at::Tensor x, c10::optional<at::Tensor> gamma,
   c10::DeviceGuard guard(x.device());
   gk::add_ln_forward(a.data_ptr(), x.data_ptr(), gp, bp, y.data_ptr(), h.data_ptr(), mean.data_ptr<float>(),
                      rstd.data_ptr<float>(), R, (int)H, (float)eps, (float)p, (uint32_t)seed, seed_word(seed_dev),
-                     cur_stream(x));
+                     cur_stream(x), dt == at::kFloat);
 }
 
 void add_ln_backward(at::Tensor dy, at::Tensor h, at::Tensor mean, at::Tensor rstd, c10::optional<at::Tensor> gamma,
@@ -1363,8 +1366,10 @@ void add_ln_backward(at::Tensor dy, at::Tensor h, at::Tensor mean, at::Tensor rs
                      c10::optional<at::Tensor> dbeta, bool accumulate, at::Tensor ws, double p, int64_t seed,
                      c10::optional<at::Tensor> seed_dev) {
   const int64_t H = h.size(-1), R = h.numel() / H;
-  for (auto* t : {&dy, &h, &dx}) check_rows_bf16(*t, "add_ln tensor", R, H);
-  if (da.has_value() && da->defined()) check_rows_bf16(*da, "da", R, H);
+  const auto dt = h.scalar_type();
+  TORCH_CHECK(dt == at::kBFloat16 || dt == at::kFloat, "add_ln: bf16 or fp32 storage");
+  for (auto* t : {&dy, &h, &dx}) check_rows_ln(*t, "add_ln tensor", R, H, dt);
+  if (da.has_value() && da->defined()) check_rows_ln(*da, "da", R, H, dt);
   TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() >= 2 * gk::add_ln_partial_rows(R) * H, "ws too small");
   auto f32 = [&](const c10::optional<at::Tensor>& t) -> float* {
     if (!t.has_value() || !t->defined()) return nullptr;
@@ -1375,7 +1380,7 @@ void add_ln_backward(at::Tensor dy, at::Tensor h, at::Tensor mean, at::Tensor rs
   gk::add_ln_backward(dy.data_ptr(), h.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(), f32(gamma),
                       dx.data_ptr(), da.has_value() && da->defined() ? da->data_ptr() : nullptr, f32(dgamma),
                       f32(dbeta), accumulate ? 1 : 0, ws.data_ptr<float>(), R, (int)H, (float)p, (uint32_t)seed,
-                      seed_word(seed_dev), cur_stream(h));
+                      seed_word(seed_dev), cur_stream(h), dt == at::kFloat);
 }
 
 // fused softmax cross-entropy (xent.hip)

@@ -482,10 +482,10 @@ int64_t add_ln_partial_rows(int64_t R);
 // seed_dev (optional): device word mixed into the dropout seed (graph replays)
 void add_ln_forward(const void* a, const void* x, const float* gamma, const float* beta, void* y, void* hsave,
                     float* mean, float* rstd, int64_t R, int H, float eps, float p, uint32_t seed,
-                    const uint32_t* seed_dev, hipStream_t stream);
+                    const uint32_t* seed_dev, hipStream_t stream, bool f32 = false);
 void add_ln_backward(const void* dy, const void* hsave, const float* mean, const float* rstd, const float* gamma,
                      void* dx, void* da, float* dgamma, float* dbeta, int accumulate, float* ws, int64_t R, int H,
-                     float p, uint32_t seed, const uint32_t* seed_dev, hipStream_t stream);
+                     float p, uint32_t seed, const uint32_t* seed_dev, hipStream_t stream, bool f32 = false);
 
 // ---------------------------------------------------------------------------
 // Linear-layer column passes over bf16 [M, N] row-major gradients (linear.hip);

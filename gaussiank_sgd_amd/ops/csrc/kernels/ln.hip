@@ -9,7 +9,8 @@
 // in the forward and the mirror image in the backward (profiles/
 // r01_bert_kernel_stats.csv).  Here each direction is one row pass (one wave
 // per row, bf16 I/O, fp32 math, 16-byte vector accesses) plus, backward, a
-// tiny column-partials finalize for dgamma / dbeta.  The dropout mask is kept
+// tiny column-partials finalize for dgamma / dbeta.  Storage bf16 (autocast)
+// or fp32 (the reference's precision), fp32 math either way.  The dropout mask is kept
 // as 1 bit per element and regenerated from nothing: it is a hash of
 // (seed, row, column), so the backward needs no mask tensor at all.
 #include <hip/hip_runtime.h>
@@ -54,6 +55,15 @@ __device__ __forceinline__ void store8(uint16_t* p, const float* v) {
   *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// 8-element chunks of either storage type: 16 bytes of bf16 or 32 of fp32
+__device__ __forceinline__ void ld8(const uint16_t* p, float* v) { load8(p, v); }
+__device__ __forceinline__ void ld8(const float* p, float* v) { load8f(p, v); }
+__device__ __forceinline__ void st8(uint16_t* p, const float* v) { store8(p, v); }
+__device__ __forceinline__ void st8(float* p, const float* v) {
+  reinterpret_cast<float4*>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
+  reinterpret_cast<float4*>(p)[1] = make_float4(v[4], v[5], v[6], v[7]);
+}
+
 // keep element (row, col) with probability 1 - p: hash < keep threshold
 __device__ __forceinline__ bool keep(uint32_t seed, int64_t row, int col, uint32_t thr) {
   return hash_u32((uint32_t)(row * 8191 + col), seed ^ (uint32_t)(row >> 19)) < thr;
@@ -71,12 +81,12 @@ __device__ __forceinline__ float row_sum(float v) {
 // sl + L j (j < CH) of its row.  BERT's H = 768 is 96 chunks: 2 rows per wave
 // x 32 lanes x 3 chunks, every lane busy (one row per wave left half the
 // lanes idle on the second chunk)
-template <int CH, int RPW>
-__global__ __launch_bounds__(kBlock) void add_ln_fwd_kernel(const uint16_t* __restrict__ a,
-                                                            const uint16_t* __restrict__ x,
+template <int CH, int RPW, typename T>
+__global__ __launch_bounds__(kBlock) void add_ln_fwd_kernel(const T* __restrict__ a,
+                                                            const T* __restrict__ x,
                                                             const float* __restrict__ gamma,
-                                                            const float* __restrict__ beta, uint16_t* __restrict__ y,
-                                                            uint16_t* __restrict__ hsave, float* __restrict__ mean,
+                                                            const float* __restrict__ beta, T* __restrict__ y,
+                                                            T* __restrict__ hsave, float* __restrict__ mean,
                                                             float* __restrict__ rstd, int64_t R, int H, float eps,
                                                             uint32_t seed, uint32_t thr, float scale,
                                                             const uint32_t* __restrict__ seed_dev) {
@@ -97,8 +107,8 @@ __global__ __launch_bounds__(kBlock) void add_ln_fwd_kernel(const uint16_t* __re
     for (int i = 0; i < 8; ++i) h[j][i] = 0.f;
     if (rv && c < nc) {
       float av[8], xv[8];
-      load8(a + row * H + c * 8, av);
-      load8(x + row * H + c * 8, xv);
+      ld8(a + row * H + c * 8, av);
+      ld8(x + row * H + c * 8, xv);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const float ad = thr ? (keep(seed, row, c * 8 + i, thr) ? av[i] * scale : 0.f) : av[i];
@@ -127,8 +137,8 @@ __global__ __launch_bounds__(kBlock) void add_ln_fwd_kernel(const uint16_t* __re
       if (beta) load8f(beta + c * 8, bv);
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] = (h[j][i] - mu) * rs * (gamma ? gv[i] : 1.f) + (beta ? bv[i] : 0.f);
-      store8(y + row * H + c * 8, o);
-      store8(hsave + row * H + c * 8, h[j]);
+      st8(y + row * H + c * 8, o);
+      st8(hsave + row * H + c * 8, h[j]);
     }
   }
   if (rv && sl == 0) {
@@ -141,11 +151,11 @@ __global__ __launch_bounds__(kBlock) void add_ln_fwd_kernel(const uint16_t* __re
 // time); lanes accumulate dgamma / dbeta partials of their columns in
 // registers, the block adds its waves' partials in a fixed order through LDS
 // and writes ONE partial row (deterministic, no atomics).
-template <int CH, int RPW>
+template <int CH, int RPW, typename T>
 __global__ __launch_bounds__(kBlock) void add_ln_bwd_kernel(
-    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ hsave, const float* __restrict__ mean,
-    const float* __restrict__ rstd, const float* __restrict__ gamma, uint16_t* __restrict__ dx,
-    uint16_t* __restrict__ da, float* __restrict__ pg, float* __restrict__ pb, int64_t R, int H, uint32_t seed,
+    const T* __restrict__ dy, const T* __restrict__ hsave, const float* __restrict__ mean,
+    const float* __restrict__ rstd, const float* __restrict__ gamma, T* __restrict__ dx,
+    T* __restrict__ da, float* __restrict__ pg, float* __restrict__ pb, int64_t R, int H, uint32_t seed,
     uint32_t thr, float scale, const uint32_t* __restrict__ seed_dev) {
   if (seed_dev != nullptr) seed = hash_u32(__builtin_amdgcn_readfirstlane(*seed_dev), seed);
   constexpr int L = 64 / RPW;
@@ -172,8 +182,8 @@ __global__ __launch_bounds__(kBlock) void add_ln_bwd_kernel(
       for (int i = 0; i < 8; ++i) g[j][i] = xh[j][i] = 0.f;
       if (rv && c < nc) {
         float dv[8], hv[8], gv[8];
-        load8(dy + row * H + c * 8, dv);
-        load8(hsave + row * H + c * 8, hv);
+        ld8(dy + row * H + c * 8, dv);
+        ld8(hsave + row * H + c * 8, hv);
         if (gamma) load8f(gamma + c * 8, gv);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -197,8 +207,8 @@ __global__ __launch_bounds__(kBlock) void add_ln_bwd_kernel(
           o[i] = rs * (g[j][i] - m1 - xh[j][i] * m2);
           if (da) od[i] = thr ? (keep(seed, row, c * 8 + i, thr) ? o[i] * scale : 0.f) : o[i];
         }
-        store8(dx + row * H + c * 8, o);
-        if (da) store8(da + row * H + c * 8, od);
+        st8(dx + row * H + c * 8, o);
+        if (da) st8(da + row * H + c * 8, od);
       }
     }
   }
@@ -325,9 +335,9 @@ int64_t add_ln_partial_rows(int64_t R) {
 
 namespace {
 struct LnFwdArgs {
-  const uint16_t *a, *x;
+  const void *a, *x;
   const float *gamma, *beta;
-  uint16_t *y, *hsave;
+  void *y, *hsave;
   float *mean, *rstd;
   int64_t R;
   int H;
@@ -336,24 +346,31 @@ struct LnFwdArgs {
   float scale;
   const uint32_t* seed_dev;
   hipStream_t stream;
+  bool f32;
 };
 
 template <int CH, int RPW>
 struct LnFwdLaunch {
   const LnFwdArgs* p;
-  void operator()() const {
+  template <typename T>
+  void go() const {
     const int64_t waves = (p->R + RPW - 1) / RPW;
     const unsigned grid = (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
-    hipLaunchKernelGGL((add_ln_fwd_kernel<CH, RPW>), dim3(grid), dim3(kBlock), 0, p->stream, p->a, p->x, p->gamma,
-                       p->beta, p->y, p->hsave, p->mean, p->rstd, p->R, p->H, p->eps, p->seed, p->thr, p->scale,
-                       p->seed_dev);
+    hipLaunchKernelGGL((add_ln_fwd_kernel<CH, RPW, T>), dim3(grid), dim3(kBlock), 0, p->stream,
+                       static_cast<const T*>(p->a), static_cast<const T*>(p->x), p->gamma, p->beta,
+                       static_cast<T*>(p->y), static_cast<T*>(p->hsave), p->mean, p->rstd, p->R, p->H, p->eps, p->seed,
+                       p->thr, p->scale, p->seed_dev);
+  }
+  void operator()() const {
+    if (p->f32) go<float>();
+    else go<uint16_t>();
   }
 };
 
 struct LnBwdArgs {
-  const uint16_t *dy, *hsave;
+  const void *dy, *hsave;
   const float *mean, *rstd, *gamma;
-  uint16_t *dx, *da;
+  void *dx, *da;
   float *pg, *pb;
   int64_t R;
   int H;
@@ -361,40 +378,45 @@ struct LnBwdArgs {
   float scale;
   const uint32_t* seed_dev;
   hipStream_t stream;
+  bool f32;
 };
 
 template <int CH, int RPW>
 struct LnBwdLaunch {
   const LnBwdArgs* p;
+  template <typename T>
+  void go() const {
+    hipLaunchKernelGGL((add_ln_bwd_kernel<CH, RPW, T>), dim3((unsigned)((p->R + kLnRowsPerBlock - 1) / kLnRowsPerBlock)),
+                       dim3(kBlock), 0, p->stream, static_cast<const T*>(p->dy), static_cast<const T*>(p->hsave),
+                       p->mean, p->rstd, p->gamma, static_cast<T*>(p->dx), static_cast<T*>(p->da), p->pg, p->pb, p->R,
+                       p->H, p->seed, p->thr, p->scale, p->seed_dev);
+  }
   void operator()() const {
-    hipLaunchKernelGGL((add_ln_bwd_kernel<CH, RPW>), dim3((unsigned)((p->R + kLnRowsPerBlock - 1) / kLnRowsPerBlock)), dim3(kBlock), 0,
-                       p->stream, p->dy, p->hsave, p->mean, p->rstd, p->gamma, p->dx, p->da, p->pg, p->pb, p->R, p->H,
-                       p->seed, p->thr, p->scale, p->seed_dev);
+    if (p->f32) go<float>();
+    else go<uint16_t>();
   }
 };
 }  // namespace
 
 void add_ln_forward(const void* a, const void* x, const float* gamma, const float* beta, void* y, void* hsave,
                     float* mean, float* rstd, int64_t R, int H, float eps, float p, uint32_t seed,
-                    const uint32_t* seed_dev, hipStream_t stream) {
+                    const uint32_t* seed_dev, hipStream_t stream, bool f32) {
   const uint32_t thr = p > 0.f ? (uint32_t)((1.0 - (double)p) * 4294967295.0) : 0u;
   const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  const LnFwdArgs args{(const uint16_t*)a, (const uint16_t*)x, gamma, beta, (uint16_t*)y, (uint16_t*)hsave, mean,
-                       rstd, R, H, eps, seed, thr, scale, seed_dev, stream};
+  const LnFwdArgs args{a, x, gamma, beta, y, hsave, mean, rstd, R, H, eps, seed, thr, scale, seed_dev, stream, f32};
   ln_dispatch<LnFwdLaunch>(H >> 3, {&args}, {&args}, {&args}, {&args}, {&args}, {&args}, {&args});
 }
 
 void add_ln_backward(const void* dy, const void* hsave, const float* mean, const float* rstd, const float* gamma,
                      void* dx, void* da, float* dgamma, float* dbeta, int accumulate, float* ws, int64_t R, int H,
-                     float p, uint32_t seed, const uint32_t* seed_dev, hipStream_t stream) {
+                     float p, uint32_t seed, const uint32_t* seed_dev, hipStream_t stream, bool f32) {
   const uint32_t thr = p > 0.f ? (uint32_t)((1.0 - (double)p) * 4294967295.0) : 0u;
   const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
   const int64_t P = (R + kLnRowsPerBlock - 1) / kLnRowsPerBlock;
   float* pg = ws;
   float* pb = ws + P * H;
   float* q = ws + 2 * P * H;   // [2][kFinSplits][H]: fits the 2 * add_ln_partial_rows(R) * H of the workspace
-  const LnBwdArgs args{(const uint16_t*)dy, (const uint16_t*)hsave, mean, rstd, gamma, (uint16_t*)dx,
-                       (uint16_t*)da, pg, pb, R, H, seed, thr, scale, seed_dev, stream};
+  const LnBwdArgs args{dy, hsave, mean, rstd, gamma, dx, da, pg, pb, R, H, seed, thr, scale, seed_dev, stream, f32};
   ln_dispatch<LnBwdLaunch>(H >> 3, {&args}, {&args}, {&args}, {&args}, {&args}, {&args}, {&args});
   if (dgamma || dbeta) {
     hipLaunchKernelGGL(ln_param_partial_kernel, dim3((H + 63) / 64, kFinSplits), dim3(kBlock), 0, stream, pg, pb, P, H,

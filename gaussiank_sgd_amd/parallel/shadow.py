@@ -147,8 +147,8 @@ def install_direct_grads(model: nn.Module, opt) -> int:
     weights, but the hand-written kernels add their weight gradients straight
     into the optimizer's fp32 gradient arena -- FastConv2d's grad-weight GEMM
     (ops/conv1x1.py fp32 path), FastLinear's (ops/linear.py fp32 path), the
-    fp32 stem (ops/stem.py) and BNAct's
-    backward (gamma / beta) -- so
+    fp32 stem (ops/stem.py), the LSTM (ops/lstm.py), the fused add + LayerNorm
+    (ops/ln.py) and BNAct's backward (gamma / beta) -- so
     AccumulateGrad launches nothing for them.  Returns the number of
     parameters on the direct path."""
     arena = opt.arena
@@ -165,6 +165,11 @@ def install_direct_grads(model: nn.Module, opt) -> int:
             if table:
                 mod._gk_direct_grads = table
         elif isinstance(mod, BNAct) and mod.affine:
+            if mod.weight in names and mod.bias in names:
+                mod._gk_direct = (arena.grad_views[names[mod.weight]], arena.grad_views[names[mod.bias]])
+                count += 2
+        elif isinstance(mod, nn.LayerNorm) and mod.elementwise_affine and mod.bias is not None:
+            # fp32 fused add + LayerNorm (ops/ln.py): dgamma / dbeta into the arena
             if mod.weight in names and mod.bias in names:
                 mod._gk_direct = (arena.grad_views[names[mod.weight]], arena.grad_views[names[mod.bias]])
                 count += 2

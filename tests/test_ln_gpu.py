@@ -99,3 +99,53 @@ def test_add_ln_direct_arena_grads():
         assert p.grad is not None, n
         err = (p.grad - q.grad).abs().max().item()
         assert err <= 2e-2 * q.grad.abs().max().item() + 1e-4, (n, err)
+
+
+@pytest.mark.parametrize("R,H", [(37, 768), (256, 64), (128, 1024), (9, 4096), (300, 136)])
+def test_add_ln_f32_vs_fp64(R, H):
+    """fp32 storage (no autocast, the reference's precision): the fused HIP
+    row passes vs an fp64 PyTorch LayerNorm, at fp32 tolerances."""
+    from gaussiank_sgd_amd.ops import ln as L_
+    from gaussiank_sgd_amd.ops.ln import add_layernorm
+    torch.manual_seed(R + H + 1)
+    ln = torch.nn.LayerNorm(H).cuda()
+    torch.nn.init.uniform_(ln.weight, 0.5, 1.5)
+    torch.nn.init.uniform_(ln.bias, -0.5, 0.5)
+    a = torch.randn(R, H, device="cuda").requires_grad_(True)
+    x = torch.randn(R, H, device="cuda").requires_grad_(True)
+    assert L_.fused_available(x)
+    y = add_layernorm(a, x, ln, 0.0, True)
+    assert y.dtype == torch.float32
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    ar = a.detach().double().requires_grad_(True)
+    xr = x.detach().double().requires_grad_(True)
+    w = ln.weight.detach().double().requires_grad_(True)
+    b = ln.bias.detach().double().requires_grad_(True)
+    yr = F.layer_norm(xr + ar, (H,), w, b, ln.eps)
+    yr.backward(dy.double())
+    tol = lambda r: 2e-5 * r.abs().max().item() + 1e-5  # noqa: E731
+    assert (y.double() - yr).abs().max().item() <= tol(yr)
+    assert (x.grad.double() - xr.grad).abs().max().item() <= tol(xr.grad)
+    assert torch.equal(a.grad, x.grad)                    # no dropout: da == dx
+    assert (ln.weight.grad.double() - w.grad).abs().max().item() <= 1e-5 * w.grad.abs().max().item() + 1e-4
+    assert (ln.bias.grad.double() - b.grad).abs().max().item() <= 1e-5 * b.grad.abs().max().item() + 1e-4
+
+
+def test_add_ln_f32_dropout_matches_bf16_mask():
+    """fp32 and bf16 storage regenerate the same hash mask for one seed."""
+    from gaussiank_sgd_amd.ops.ln import _AddLNFn
+    torch.manual_seed(3)
+    R, H, p = 64, 768, 0.1
+    ln = torch.nn.LayerNorm(H).cuda()
+    a = torch.randn(R, H, device="cuda")
+    x = torch.randn(R, H, device="cuda")
+    dyr = torch.randn(R, H, device="cuda")
+    masks = []
+    for cd in (torch.float32, torch.bfloat16):
+        aa = a.clone().requires_grad_(True)
+        y = _AddLNFn.apply(aa, x, ln.weight, ln.bias, ln.eps, p, 1234, None, None, cd)
+        (y.float() * dyr).sum().backward()
+        masks.append(aa.grad == 0)
+    assert torch.equal(masks[0], masks[1])
+    assert abs(masks[0].float().mean().item() - p) < 0.02
