@@ -10,11 +10,11 @@ rc=$?; echo tests_rc=$rc; tail -3 $D/tests.log; [ $rc -eq 0 ] || exit $rc
 cp gpurun_out/r4c8/choices_bert.json $D/choices_bert.json 2>/dev/null || true
 B="python3 bench.py --model bert --no-bf16-phase --ref-batch 0 --steps 8 --warmup 4"
 show() { python3 -c "import json;d=json.load(open('$D/$1.json'));print('$1', d['value'], d['ms_per_step'], d['config']['buckets'])"; }
-GKSGD_GEMM_CACHE=tuning/choices_bert_r4c8.json timeout -k 10 400 $B --json-out $D/bert_ln.json > $D/bert_ln.log 2>&1
+timeout -k 10 400 $B --json-out $D/bert_ln.json > $D/bert_ln.log 2>&1
 rc=$?; echo ln_rc=$rc; show bert_ln; [ $rc -eq 0 ] || exit $rc
-GKSGD_LN_F32=0 GKSGD_GEMM_CACHE=tuning/choices_bert_r4c8.json timeout -k 10 400 $B --json-out $D/bert_noln.json > $D/bert_noln.log 2>&1
+GKSGD_LN_F32=0 timeout -k 10 400 $B --json-out $D/bert_noln.json > $D/bert_noln.log 2>&1
 rc=$?; echo noln_rc=$rc; show bert_noln; [ $rc -eq 0 ] || exit $rc
-GKSGD_GEMM_CACHE=tuning/choices_bert_r4c8.json timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $D/prof -o prof -- python3 bench.py --model bert --no-bf16-phase --ref-batch 0 --steps 5 --warmup 3 > $D/prof.log 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $D/prof -o prof -- python3 bench.py --model bert --no-bf16-phase --ref-batch 0 --steps 5 --warmup 3 > $D/prof.log 2>&1
 rc=$?; echo prof_rc=$rc; [ $rc -eq 0 ] || exit $rc
 python3 scripts/rocpd_summary.py --marker attn_f32_fwd --marker-per-step 12 --steps 5 $(find $D/prof -name '*.db' | head -1) $D/bert_f32_summary.txt > $D/sum.log 2>&1; echo sum_rc=$?
 head -14 $D/bert_f32_summary.txt
