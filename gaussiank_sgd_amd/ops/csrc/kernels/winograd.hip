@@ -61,6 +61,18 @@ constexpr int WVS = 16 * WBT * WCK;     // floats of one V stage
 constexpr int WUS = 16 * WBK * WCK;     // floats of one U stage
 constexpr int WSTAGE = WVS + WUS;       // 16384 floats = 64 KiB
 constexpr int WLDS = 2 * WSTAGE * 4;    // bytes
+// xi slot at which the forward kernel waits for the next stage's patches and
+// transforms them; its 16 LDS writes then go out 16 / (16 - slot) per slot.
+// Measured on the bs512 shapes (r4c18-r4c21, bench/wino_probe.hip): one burst
+// at slot 8 (the round-3 form) 563-665 us, spread from slot 8 1-2% faster,
+// from slot 12 2-3% faster; staggering the two waves of a SIMD over different
+// slots (a wave-uniform branch per slot) was slower than either, and so was
+// deferring xi = 15's MFMAs across the stage barrier (+1-2%, r4c22).
+#ifndef GK_WINO_XFORM
+#define GK_WINO_XFORM 12
+#endif
+constexpr int kWinoXform = GK_WINO_XFORM;
+static_assert(kWinoXform == 8 || kWinoXform == 12 || kWinoXform == 14 || kWinoXform == 15, "16 - slot divides 16");
 
 struct WinoGeo {
   int H, W, Ci, Co, TH, TW, ntiles;
@@ -217,8 +229,13 @@ wino_f23_kernel(const float* __restrict__ x, const float* __restrict__ u, float*
     }
 #endif
   };
-  auto lstore = [&](int b, int r) __attribute__((always_inline)) {
-    float* V = wlds + b * WSTAGE;
+  // input transform B^T d B of the landed patch into vt[xi] (registers); its 16
+  // LDS writes are issued two per xi slot of the next compute() (lwrite), so
+  // they interleave with the operand reads instead of queueing ahead of them
+  // in one burst (measured: the burst form stalls the MFMAs behind the LDS
+  // queue, r4c18 ablation)
+  float vt[16];
+  auto ltrans = [&](int r) __attribute__((always_inline)) {
     const float* d = dv[r];
     float t[16];
 #pragma unroll
@@ -228,28 +245,45 @@ wino_f23_kernel(const float* __restrict__ x, const float* __restrict__ u, float*
       t[8 + j] = d[8 + j] - d[4 + j];
       t[12 + j] = d[4 + j] - d[12 + j];
     }
-    const int col = ((((lc >> 1) ^ wsw(ltile)) << 1) | (lc & 1));
 #pragma unroll
     for (int i = 0; i < 4; ++i) {   // (.) B
-      V[((4 * i + 0) * WBT + ltile) * WCK + col] = t[4 * i + 0] - t[4 * i + 2];
-      V[((4 * i + 1) * WBT + ltile) * WCK + col] = t[4 * i + 1] + t[4 * i + 2];
-      V[((4 * i + 2) * WBT + ltile) * WCK + col] = t[4 * i + 2] - t[4 * i + 1];
-      V[((4 * i + 3) * WBT + ltile) * WCK + col] = t[4 * i + 1] - t[4 * i + 3];
+      vt[4 * i + 0] = t[4 * i + 0] - t[4 * i + 2];
+      vt[4 * i + 1] = t[4 * i + 1] + t[4 * i + 2];
+      vt[4 * i + 2] = t[4 * i + 2] - t[4 * i + 1];
+      vt[4 * i + 3] = t[4 * i + 1] - t[4 * i + 3];
     }
+  };
+  const int lcol = ((((lc >> 1) ^ wsw(ltile)) << 1) | (lc & 1));
+  // LDS writes of vt[q0 .. q0 + NQ) into buffer b
+  auto lwrite = [&](int b, int q0, int nq) __attribute__((always_inline)) {
+    float* V = wlds + b * WSTAGE;
+#pragma unroll
+    for (int q = q0; q < q0 + nq; ++q) V[(q * WBT + ltile) * WCK + lcol] = vt[q];
+  };
+  auto lstore = [&](int b, int r) __attribute__((always_inline)) {
+    ltrans(r);
+    lwrite(b, 0, 16);
   };
   // All 16 xi of LDS buffer b, the operands of xi + 1 read (into the other
   // register set) before the MFMAs of xi are issued, so the LDS latency hides
-  // behind them; mid() runs between xi = 7 and xi = 8 (the next stage's
+  // behind them; mid(xi) runs before the MFMAs of each xi (from xi = 8: the next stage's
   // transform: its VALU and LDS writes issue while MFMAs are in flight).
   // Offsets are lane constants plus compile-time xi strides: the reads are
   // one base register and immediate offsets.
   const int rcol = (fq ^ wsw(fi)) << 1;   // swizzled slot of this lane's operand rows (rows = 16-multiple + fi)
   const int aoff = (wk * 16 + fi) * WCK + rcol;
   const int boff = (wt * 32 + fi) * WCK + rcol;
+  f32x2 fa[2], fb[2][2];   // operand register double buffer
+  auto mfma_xi = [&](int xi, int sl) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ts = 0; ts < 2; ++ts)
+        acc[xi][ts] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[sl][j], fb[sl][ts][j], acc[xi][ts], 0, 0, 0);
+  };
   auto compute = [&](int b, auto mid) __attribute__((always_inline)) {
     const float* V = wlds + b * WSTAGE;
     const float* U = V + WVS;
-    f32x2 fa[2], fb[2][2];
     auto rd = [&](int xi, int sl) __attribute__((always_inline)) {
       fa[sl] = *reinterpret_cast<const f32x2*>(U + xi * (WBK * WCK) + aoff);
       fb[sl][0] = *reinterpret_cast<const f32x2*>(V + xi * (WBT * WCK) + boff);
@@ -260,13 +294,9 @@ wino_f23_kernel(const float* __restrict__ x, const float* __restrict__ u, float*
     for (int xi = 0; xi < 16; ++xi) {
       const int sl = xi & 1;
       if (xi + 1 < 16) rd(xi + 1, sl ^ 1);
-      if (xi == 8) mid();
+      mid(xi);
       __builtin_amdgcn_sched_barrier(0);   // keep the reads of xi + 1 ahead of the MFMAs of xi
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int ts = 0; ts < 2; ++ts)
-          acc[xi][ts] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[sl][j], fb[sl][ts][j], acc[xi][ts], 0, 0, 0);
+      mfma_xi(xi, sl);
     }
   };
   // BN-backward epilogue operands through buffer descriptors (an invalid
@@ -385,11 +415,21 @@ wino_f23_kernel(const float* __restrict__ x, const float* __restrict__ u, float*
         gload_u(ls, nxt);
         gload_v(ls, 0);
       }
-      compute(cur, [&]() __attribute__((always_inline)) {
-        if (more) {
-          vwait(std::integral_constant<int, 0>{}, 0);   // the patch loads are the youngest ops
+      compute(cur, [&](int xi) __attribute__((always_inline)) {
+        constexpr int X0 = kWinoXform, PER = 16 / (16 - X0);
+        if (more && xi >= X0) {
+          if (xi == X0) {
+            vwait(std::integral_constant<int, 0>{}, 0);   // the patch loads are the youngest ops
+            ltrans(0);
+          }
 #ifndef GK_WINO_PROBE_NOLSTORE
-          lstore(nxt, 0);
+          // BN-backward epilogue variant: one burst (the spread form's live
+          // transform registers push its epilogue into spills)
+          if constexpr (BNB) {
+            if (xi == X0) lwrite(nxt, 0, 16);
+          } else {
+            lwrite(nxt, PER * (xi - X0), PER);
+          }
 #endif
         }
       });
@@ -567,9 +607,12 @@ wino_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, flo
     }
     (void)st;
   };
-  auto lstore = [&](int buf) __attribute__((always_inline)) {
-    float* V = wlds + buf * WGSTAGE;
-    float* D = V + WGHALF;
+  // transforms of the landed patch / dY block into registers (tv, td); their
+  // 32 LDS writes go out four per xi slot of the next compute() (lwrite)
+  // instead of in one burst that queued ahead of the operand reads (the burst
+  // form cost 25% of the kernel, r4c18 ablation)
+  float tv[16], td[16];
+  auto ltrans_v = [&]() __attribute__((always_inline)) {
     float t[16];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {   // B^T d
@@ -580,11 +623,13 @@ wino_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, flo
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {   // (.) B
-      V[((4 * i + 0) * 64 + lch) * WGRS + lt] = t[4 * i + 0] - t[4 * i + 2];
-      V[((4 * i + 1) * 64 + lch) * WGRS + lt] = t[4 * i + 1] + t[4 * i + 2];
-      V[((4 * i + 2) * 64 + lch) * WGRS + lt] = t[4 * i + 2] - t[4 * i + 1];
-      V[((4 * i + 3) * 64 + lch) * WGRS + lt] = t[4 * i + 1] - t[4 * i + 3];
+      tv[4 * i + 0] = t[4 * i + 0] - t[4 * i + 2];
+      tv[4 * i + 1] = t[4 * i + 1] + t[4 * i + 2];
+      tv[4 * i + 2] = t[4 * i + 2] - t[4 * i + 1];
+      tv[4 * i + 3] = t[4 * i + 1] - t[4 * i + 3];
     }
+  };
+  auto ltrans_d = [&]() __attribute__((always_inline)) {
     // dM = A dY A^T, A = [[1,0],[1,1],[1,-1],[0,-1]]: rows (p, p+q, p-q, -q) of each column
     float m[4][2];
 #pragma unroll
@@ -598,14 +643,25 @@ wino_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, flo
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float p = m[i][0], q = m[i][1];
-      D[((4 * i + 0) * 64 + lch) * WGRS + lt] = p;
-      D[((4 * i + 1) * 64 + lch) * WGRS + lt] = p + q;
-      D[((4 * i + 2) * 64 + lch) * WGRS + lt] = p - q;
-      D[((4 * i + 3) * 64 + lch) * WGRS + lt] = -q;
+      td[4 * i + 0] = p;
+      td[4 * i + 1] = p + q;
+      td[4 * i + 2] = p - q;
+      td[4 * i + 3] = -q;
     }
   };
+  // LDS writes of rows [q0, q0 + nq) of V / of dM into buffer buf
+  auto lwrite_v = [&](int buf, int q0, int nq) __attribute__((always_inline)) {
+    float* V = wlds + buf * WGSTAGE;
+#pragma unroll
+    for (int q = q0; q < q0 + nq; ++q) V[(q * 64 + lch) * WGRS + lt] = tv[q];
+  };
+  auto lwrite_d = [&](int buf, int q0, int nq) __attribute__((always_inline)) {
+    float* D = wlds + buf * WGSTAGE + WGHALF;
+#pragma unroll
+    for (int q = q0; q < q0 + nq; ++q) D[(q * 64 + lch) * WGRS + lt] = td[q];
+  };
   // all 16 xi of buffer buf, the operands of xi + 1 read before the MFMAs of
-  // xi (forward kernel's scheme); mid() between xi = 7 and 8
+  // xi (forward kernel's scheme); mid(xi) before the MFMAs of each xi
   auto compute = [&](int buf, auto mid) __attribute__((always_inline)) {
     const float* V = wlds + buf * WGSTAGE;
     const float* D = V + WGHALF;
@@ -621,7 +677,7 @@ wino_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, flo
     for (int xi = 0; xi < 16; ++xi) {
       const int sl = xi & 1;
       if (xi + 1 < 16) rd(xi + 1, sl ^ 1);
-      if (xi == 8) mid();
+      mid(xi);
       __builtin_amdgcn_sched_barrier(0);   // keep the reads of xi + 1 ahead of the MFMAs of xi
 #pragma unroll
       for (int j = 0; j < 2; ++j)
@@ -633,15 +689,26 @@ wino_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, flo
 
   if (nst > 0) {
     gload(0);
-    lstore(0);
+    ltrans_v();
+    ltrans_d();
+    lwrite_v(0, 0, 16);
+    lwrite_d(0, 0, 16);
     __syncthreads();
     for (int st = 0; st < nst; ++st) {
       const bool more = st + 1 < nst;
       if (more) gload(st + 1);
-      compute(st & 1, [&]() __attribute__((always_inline)) {
+      compute(st & 1, [&](int xi) __attribute__((always_inline)) {
+        // one burst of the 32 LDS writes at xi = 8 (spreading them over the
+        // xi slots measured 3% slower here, r4c19: the extra live transform
+        // registers push the kernel to its 256-VGPR cap)
+        if (more && xi == 8) {
+          ltrans_v();
+          ltrans_d();
 #ifndef GK_WINO_PROBE_NOLSTORE
-        if (more) lstore((st + 1) & 1);
+          lwrite_v((st + 1) & 1, 0, 16);
+          lwrite_d((st + 1) & 1, 0, 16);
 #endif
+        }
       });
 #ifndef GK_WINO_PROBE_NOBAR
       __syncthreads();
