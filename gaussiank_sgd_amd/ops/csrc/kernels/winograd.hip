@@ -509,18 +509,23 @@ int launch_wino(const float* x, const float* u, float* y, const WinoGeo& g, int 
 // (128 accumulators per lane; lane ends with 4 consecutive c of one k).
 // Stages of 8 tiles: thread (tile, channel) loads the tile's 4x4 input patch
 // of channel c (16 loads, 64 lanes = 256 contiguous bytes per pixel) and its
-// 2x2 dY block of channel k, transforms both and writes V / dM rows
+// 2x2 dY block of channel k, transforms the patch and writes V rows
 // [xi][channel][tile] (row stride 10 floats: 2-way write conflicts, aligned
-// 8-byte operand reads).  Two stages of 80 KiB fill the 160 KiB LDS.  Each
+// 8-byte operand reads) and the dY block raw ([tile][k][2x2], one 16-byte
+// write); the MFMA's dM operand is formed in registers from it (two raw
+// blocks per lane per stage: one add per xi), which halved the LDS writes
+// (grad-weight 7-8% faster than the transformed-dM layout, r4c24).  Two
+// stages of 48 KiB.  Each
 // block writes its dU partial (plain stores, no atomics: deterministic); the
 // finalize kernel sums the splits, applies G^T . G and adds into the fp32
 // gradient (channels-last [K][3][3][C]).  Blocks are remapped so the Cout /
 // Cin blocks of one split sit on one XCD and share its patches in L2.
 constexpr int WGT = 8;                      // tiles per stage
 constexpr int WGRS = 10;                    // LDS row stride (floats)
-constexpr int WGHALF = 16 * 64 * WGRS;      // floats of one operand stage
-constexpr int WGSTAGE = 2 * WGHALF;         // V + dM
-constexpr int WGLDS = 2 * WGSTAGE * 4;      // 163840 bytes
+constexpr int WGHALF = 16 * 64 * WGRS;      // floats of one V stage
+constexpr int WGD = WGT * 64 * 4;           // floats of one raw dY stage: [tile][k][2x2]
+constexpr int WGSTAGE = WGHALF + WGD;       // V + raw dY
+constexpr int WGLDS = 2 * WGSTAGE * 4;      // 98304 bytes
 
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
 wino_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ part, WinoGeo g,
@@ -607,11 +612,10 @@ wino_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, flo
     }
     (void)st;
   };
-  // transforms of the landed patch / dY block into registers (tv, td); their
-  // 32 LDS writes go out four per xi slot of the next compute() (lwrite)
-  // instead of in one burst that queued ahead of the operand reads (the burst
-  // form cost 25% of the kernel, r4c18 ablation)
-  float tv[16], td[16];
+  // input transform of the landed patch into registers (tv); its 16 LDS
+  // writes and the raw dY block's one go out together at xi = 8 of the next
+  // compute() (spreading them over the xi slots measured slower, r4c19)
+  float tv[16];
   auto ltrans_v = [&]() __attribute__((always_inline)) {
     float t[16];
 #pragma unroll
@@ -629,48 +633,54 @@ wino_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, flo
       tv[4 * i + 3] = t[4 * i + 1] - t[4 * i + 3];
     }
   };
-  auto ltrans_d = [&]() __attribute__((always_inline)) {
-    // dM = A dY A^T, A = [[1,0],[1,1],[1,-1],[0,-1]]: rows (p, p+q, p-q, -q) of each column
-    float m[4][2];
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const float p = gv[b], q = gv[2 + b];
-      m[0][b] = p;
-      m[1][b] = p + q;
-      m[2][b] = p - q;
-      m[3][b] = -q;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float p = m[i][0], q = m[i][1];
-      td[4 * i + 0] = p;
-      td[4 * i + 1] = p + q;
-      td[4 * i + 2] = p - q;
-      td[4 * i + 3] = -q;
-    }
-  };
-  // LDS writes of rows [q0, q0 + nq) of V / of dM into buffer buf
+  // LDS writes of V rows [q0, q0 + nq) into buffer buf
   auto lwrite_v = [&](int buf, int q0, int nq) __attribute__((always_inline)) {
     float* V = wlds + buf * WGSTAGE;
 #pragma unroll
     for (int q = q0; q < q0 + nq; ++q) V[(q * 64 + lch) * WGRS + lt] = tv[q];
   };
-  auto lwrite_d = [&](int buf, int q0, int nq) __attribute__((always_inline)) {
+  // the raw 2x2 dY block of (tile lt, channel k = lch): one 16-byte write
+  // ([tile][k][4]: consecutive lanes, consecutive 16 bytes); dM = A dY A^T is
+  // formed in the consumer's registers (compute), which replaces the 16
+  // transformed dM rows per thread of the round-3 layout -- half of this
+  // kernel's LDS writes, and the 16 dM operand reads per stage
+  auto lwrite_d = [&](int buf) __attribute__((always_inline)) {
     float* D = wlds + buf * WGSTAGE + WGHALF;
-#pragma unroll
-    for (int q = q0; q < q0 + nq; ++q) D[(q * 64 + lch) * WGRS + lt] = td[q];
+    *reinterpret_cast<f32x4*>(D + (lt * 64 + lch) * 4) = f32x4{gv[0], gv[1], gv[2], gv[3]};
   };
   // all 16 xi of buffer buf, the operands of xi + 1 read before the MFMAs of
   // xi (forward kernel's scheme); mid(xi) before the MFMAs of each xi
   auto compute = [&](int buf, auto mid) __attribute__((always_inline)) {
     const float* V = wlds + buf * WGSTAGE;
     const float* D = V + WGHALF;
+    // this lane's B operand rows: dM[xi][k = wk*16 + fi][tiles 2fq, 2fq + 1]
+    // from the two raw dY blocks.  Row transform once per stage (m = A dY:
+    // rows p, p + q, p - q, -q of each column); dM[4i + c] is then one add /
+    // negate of m[i][0], m[i][1] per xi (A's column combination).
+    float m[2][4][2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const f32x4 r = *reinterpret_cast<const f32x4*>(D + ((2 * fq + j) * 64 + wk * 16 + fi) * 4);
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const float p = r[b], q = r[2 + b];
+        m[j][0][b] = p;
+        m[j][1][b] = p + q;
+        m[j][2][b] = p - q;
+        m[j][3][b] = -q;
+      }
+    }
+    auto dm = [&](int j, int xi) __attribute__((always_inline)) {
+      const float p = m[j][xi >> 2][0], q = m[j][xi >> 2][1];
+      const int c = xi & 3;
+      return c == 0 ? p : c == 1 ? p + q : c == 2 ? p - q : -q;
+    };
     f32x2 fa[2][2], fb[2];
     auto rd = [&](int xi, int sl) __attribute__((always_inline)) {
 #pragma unroll
       for (int cs = 0; cs < 2; ++cs)
         fa[sl][cs] = *reinterpret_cast<const f32x2*>(V + ((xi * 64) + wc * 32 + cs * 16 + fi) * WGRS + 2 * fq);
-      fb[sl] = *reinterpret_cast<const f32x2*>(D + ((xi * 64) + wk * 16 + fi) * WGRS + 2 * fq);
+      fb[sl] = f32x2{dm(0, xi), dm(1, xi)};
     };
     rd(0, 0);
 #pragma unroll
@@ -690,23 +700,20 @@ wino_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, flo
   if (nst > 0) {
     gload(0);
     ltrans_v();
-    ltrans_d();
     lwrite_v(0, 0, 16);
-    lwrite_d(0, 0, 16);
+    lwrite_d(0);
     __syncthreads();
     for (int st = 0; st < nst; ++st) {
       const bool more = st + 1 < nst;
       if (more) gload(st + 1);
       compute(st & 1, [&](int xi) __attribute__((always_inline)) {
-        // one burst of the 32 LDS writes at xi = 8 (spreading them over the
-        // xi slots measured 3% slower here, r4c19: the extra live transform
-        // registers push the kernel to its 256-VGPR cap)
+        // one burst at xi = 8: the 16 V rows and the raw dY block (spreading
+        // the V writes over the xi slots measured 3-4% slower, r4c19 / r4c24)
         if (more && xi == 8) {
           ltrans_v();
-          ltrans_d();
 #ifndef GK_WINO_PROBE_NOLSTORE
           lwrite_v((st + 1) & 1, 0, 16);
-          lwrite_d((st + 1) & 1, 0, 16);
+          lwrite_d((st + 1) & 1);
 #endif
         }
       });
