@@ -150,6 +150,58 @@ __device__ __forceinline__ uint64_t block_excl_scan_u64(uint64_t v, uint64_t* sh
   return before + inc - v;
 }
 
+// Exclusive scan of a u32 over the 256 threads of the block, in thread order
+// (half the shuffles of the u64 form; for counts bounded by the bucket size).
+__device__ __forceinline__ uint32_t block_excl_scan_u32(uint32_t v, uint32_t* sh /*>=4*/, uint32_t* total) {
+  uint32_t inc = v;
+  const int l = lane_id();
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t o = __shfl_up(inc, off, 64);
+    if (l >= off) inc += o;
+  }
+  __syncthreads();
+  if (l == 63) sh[wave_id()] = inc;
+  __syncthreads();
+  uint32_t before = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kWavesPerBlock; ++w) {
+    const uint32_t s = sh[w];
+    if (w < wave_id()) before += s;
+    tot += s;
+  }
+  *total = tot;
+  return before + inc - v;
+}
+
+// Block totals of N (<= 16) per-thread u32 counters through one LDS
+// transpose: every thread stores its N values, then thread t sums the 16
+// values t % 16 + 16 i of counter t / 16 and the 16 partials of a
+// counter (16 consecutive lanes) meet in four shuffle steps -- instead of N
+// dependent six-step shuffle chains (wave_sum per counter: 16 x 6 ds_bpermute
+// on the decide / count tails).  out[j] (LDS) holds counter j's total on
+// return; sh holds N * kBlock words.
+template <int N>
+__device__ __forceinline__ void block_totals_u32(const uint32_t (&v)[N], uint32_t* sh, uint32_t* out) {
+  static_assert(N >= 1 && N <= kBlock / 16, "one 16-thread group per counter");
+#pragma unroll
+  for (int j = 0; j < N; ++j) sh[j * kBlock + threadIdx.x] = v[j];
+  __syncthreads();
+  const int j = threadIdx.x >> 4, part = threadIdx.x & 15;
+  uint32_t a = 0u;
+  if (j < N) {
+    // elements part, part + 16, ...: the 16 lanes of a group read 16
+    // consecutive words per step (no bank conflicts)
+    const uint32_t* p = sh + j * kBlock + part;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) a += p[16 * i];
+  }
+#pragma unroll
+  for (int off = 8; off > 0; off >>= 1) a += __shfl_xor(a, off, 16);
+  if (j < N && part == 0) out[j] = a;
+  __syncthreads();
+}
+
 // Find the digit holding the kr-th largest key (1-based) in a histogram of
 // nbins (multiple of 256, <= 256 kRadixPer).  Result broadcast to every thread.
 constexpr int kRadixPer = (kRadixBins0 > kRadixBins1 ? kRadixBins0 : kRadixBins1) / kBlock;
@@ -619,10 +671,45 @@ __device__ __forceinline__ void finalize_body(GkCtrl* __restrict__ ctrl, const d
       mx = fmaxf(mx, (float)v[3]);
     }
   }
-  s = block_sum(s, sh);
-  ss = block_sum(ss, sh);
-  sa = block_sum(sa, sh);
-  mx = block_max(mx, shf);
+  if (BATCH) {
+    // the three sums and the max through one LDS transpose (thread t reduces
+    // 16 values of quantity t / 16; 16-lane groups meet in four shuffle
+    // steps) instead of three block_sum + block_max shuffle chains
+    __shared__ __attribute__((aligned(16))) double sh_q[4 * kBlock];
+    __shared__ double s_q[4];
+    sh_q[threadIdx.x] = s;
+    sh_q[kBlock + threadIdx.x] = ss;
+    sh_q[2 * kBlock + threadIdx.x] = sa;
+    sh_q[3 * kBlock + threadIdx.x] = (double)mx;
+    __syncthreads();
+    const int qi = threadIdx.x >> 4, part = threadIdx.x & 15;
+    double a = 0.0;
+    if (qi < 4) {
+      const double* p = sh_q + qi * kBlock + part;   // elements part + 16 i: conflict-free
+      double t[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) t[i] = p[16 * i];
+      a = t[0];
+#pragma unroll
+      for (int i = 1; i < 16; ++i) a = qi == 3 ? fmax(a, t[i]) : a + t[i];
+    }
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) {
+      const double o = __shfl_xor(a, off, 16);
+      a = qi == 3 ? fmax(a, o) : a + o;
+    }
+    if (qi < 4 && part == 0) s_q[qi] = a;
+    __syncthreads();
+    s = s_q[0];
+    ss = s_q[1];
+    sa = s_q[2];
+    mx = (float)s_q[3];
+  } else {
+    s = block_sum(s, sh);
+    ss = block_sum(ss, sh);
+    sa = block_sum(sa, sh);
+    mx = block_max(mx, shf);
+  }
 
   uint32_t rkey[2] = {0u, 0u};
   int64_t rkrem[2] = {0, 0}, rkeff[2] = {0, 0};
@@ -926,23 +1013,19 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const float* __restrict__
 #pragma unroll
     for (int j = 0; j < NC; ++j) cnt[j] = bnd[j] == 0xffffffffu ? 0u : nin - cnt[j];
   }
-  // per-lane counts -> per-wave totals (one reduction per block)
+  // per-lane counts -> block totals (one LDS transpose per block)
   static_assert(NC + NX <= kMaxCand, "candidate slots");
+  uint32_t all[NC + NX];
 #pragma unroll
-  for (int j = 0; j < NC; ++j) cnt[j] = wave_sum(cnt[j]);
+  for (int j = 0; j < NC; ++j) all[j] = cnt[j];
 #pragma unroll
-  for (int j = 0; j < NX; ++j) xc[j] = wave_sum(xc[j]);
-  __shared__ uint32_t sh[kWavesPerBlock][NC + NXA];
-  if (lane_id() == 0) {
-#pragma unroll
-    for (int j = 0; j < NC; ++j) sh[wave_id()][j] = cnt[j];
-#pragma unroll
-    for (int j = 0; j < NX; ++j) sh[wave_id()][NC + j] = xc[j];
-  }
-  __syncthreads();
+  for (int j = 0; j < NX; ++j) all[NC + j] = xc[j];
+  __shared__ __attribute__((aligned(16))) uint32_t sh[(NC + NX) * kBlock];
+  __shared__ uint32_t s_bt[kMaxCand];
+  block_totals_u32<NC + NX>(all, sh, s_bt);
   if (threadIdx.x < kMaxCand) {
     const int j = threadIdx.x;
-    st_dev(&blockcnt[blockIdx.x * kMaxCand + j], j < NC + NX ? sh[0][j] + sh[1][j] + sh[2][j] + sh[3][j] : 0u);
+    st_dev(&blockcnt[blockIdx.x * kMaxCand + j], j < NC + NX ? s_bt[j] : 0u);
   }
   if constexpr (DEC) {   // decide on the totals in the last block (else: decide_kernel after this grid)
     if (last_block(da.counter))
@@ -965,7 +1048,6 @@ __device__ __forceinline__ void decide_body(GkCtrl* __restrict__ gctrl, const ui
                             int loops, int64_t k, int64_t k_cap, int64_t* __restrict__ offsets,
                             int64_t* __restrict__ eqtake, int64_t* __restrict__ blocksel, int32_t* __restrict__ hdr,
                             int cond, uint32_t* __restrict__ hist_reset) {
-  __shared__ uint64_t sh_tot[kWavesPerBlock][kMaxCand];
   __shared__ uint64_t sh_scan[kWavesPerBlock];
   __shared__ int s_chosen, s_gt, s_ge, s_stop;
   __shared__ int64_t s_quota;
@@ -995,27 +1077,22 @@ __device__ __forceinline__ void decide_body(GkCtrl* __restrict__ gctrl, const ui
     mode = kModeTopK;   // second decide of a fallback: exact top-k (or top-k_cap) on the radix key
   }
   const int nc = ctrl->ncand;
-  // totals per candidate
-  uint64_t loc[kMaxCand];
+  // totals per candidate (u32: a candidate's count is at most the bucket
+  // size, < 2^31 elements) through one LDS transpose
+  uint32_t loc[kMaxCand];
 #pragma unroll
   for (int j = 0; j < kMaxCand; ++j) {
-    loc[j] = 0;
+    loc[j] = 0u;
 #pragma unroll
     for (int q = 0; q < kPer; ++q) loc[j] += row[q][j];
   }
-#pragma unroll
-  for (int j = 0; j < kMaxCand; ++j) {
-    const uint64_t w = wave_sum(loc[j]);
-    if (lane_id() == 0) sh_tot[wave_id()][j] = w;
-  }
-  __syncthreads();
+  __shared__ __attribute__((aligned(16))) uint32_t sh_t[kMaxCand * kBlock];
+  __shared__ uint32_t s_tot32[kMaxCand];
+  block_totals_u32<kMaxCand>(loc, sh_t, s_tot32);
   // per-candidate totals in LDS: the decision indexes them dynamically (a
   // private array would live in scratch)
   __shared__ int64_t s_tot[kMaxCand];
-  if (threadIdx.x < kMaxCand) {
-    const int j = threadIdx.x;
-    s_tot[j] = (int64_t)(sh_tot[0][j] + sh_tot[1][j] + sh_tot[2][j] + sh_tot[3][j]);
-  }
+  if (threadIdx.x < kMaxCand) s_tot[threadIdx.x] = (int64_t)s_tot32[threadIdx.x];
   __syncthreads();
   if (threadIdx.x == 0) {
     s_stop = 0;
@@ -1138,7 +1215,7 @@ __device__ __forceinline__ void decide_body(GkCtrl* __restrict__ gctrl, const ui
   const int gt = s_gt, ge = s_ge;
   const int64_t quota = s_quota;
   int64_t gtc[kPer], eqc[kPer];
-  uint64_t eq_loc = 0;
+  uint32_t eq_loc = 0u;
 #pragma unroll
   for (int q = 0; q < kPer; ++q) {
     // row[q][gt], row[q][ge] by uniform selects (no dynamic register index);
@@ -1151,22 +1228,29 @@ __device__ __forceinline__ void decide_body(GkCtrl* __restrict__ gctrl, const ui
     }
     gtc[q] = vg;
     eqc[q] = ge >= 0 ? (int64_t)ve - (int64_t)vg : 0;
-    eq_loc += eqc[q];
+    eq_loc += (uint32_t)eqc[q];
   }
-  uint64_t eq_tot;
-  uint64_t eq_before = block_excl_scan_u64(eq_loc, sh_scan, &eq_tot);
+  // the equal-key quota scan only when the decision has an exact-key slot
+  // (block-uniform: ge comes from LDS)
+  uint32_t eq_before = 0u;
+  if (ge >= 0) {
+    uint32_t eq_tot;
+    eq_before = block_excl_scan_u32(eq_loc, reinterpret_cast<uint32_t*>(sh_scan), &eq_tot);
+  }
   int64_t take[kPer];
-  uint64_t sel_loc = 0;
+  uint32_t sel_loc = 0u;
+  int64_t eqb = (int64_t)eq_before;
 #pragma unroll
   for (int q = 0; q < kPer; ++q) {
-    int64_t rem = quota - (int64_t)eq_before;
+    int64_t rem = quota - eqb;
     if (rem < 0) rem = 0;
     take[q] = eqc[q] < rem ? eqc[q] : rem;
-    eq_before += eqc[q];
-    sel_loc += gtc[q] + take[q];
+    eqb += eqc[q];
+    sel_loc += (uint32_t)(gtc[q] + take[q]);
   }
-  uint64_t sel_tot;
-  uint64_t sel_before = block_excl_scan_u64(sel_loc, sh_scan, &sel_tot);
+  uint32_t sel_tot32;
+  uint64_t sel_before = block_excl_scan_u32(sel_loc, reinterpret_cast<uint32_t*>(sh_scan), &sel_tot32);
+  const uint64_t sel_tot = sel_tot32;
 #pragma unroll
   for (int q = 0; q < kPer; ++q) {
     const int b = threadIdx.x * kPer + q;
