@@ -402,6 +402,36 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
   // channels per column pair pr (the same channels for every tile): offset
   // cofs within the pair's 32 columns
   const int cofs = (fq & 1) ? 16 + 4 * (fq - 1) : 4 * fq;
+  // fp32 BN-backward epilogue operands (h, dy2, mask byte per 16-byte chunk)
+  // of a 16-row subtile row ms.  The first PMS rows of a tile are loaded at
+  // the start of its last K slice, so their latency hides under that slice's
+  // MFMAs instead of stalling the epilogue; row ms + PMS is loaded into the
+  // slot row ms frees while row ms is written.  (These loads are consumed
+  // inside the same iteration, so the stage / store vmcnt accounting below is
+  // unchanged.)
+  // (32x64 wave tiles only: the 64x64 ones have no registers for it -- one
+  // prefetched row already pushed them into 15-190 VGPRs of spills)
+  constexpr bool PRE = F32 && BNB && MSB == 2;
+  constexpr int PMS = PRE ? 2 : 1;
+  f32x4 pre_h[PMS][4], pre_d[PMS][4];
+  uint32_t pre_b[PMS][4];
+  auto bn_row_load = [&](int64_t mbase_, int ms, f32x4* hh, f32x4* dd, uint32_t* bits) {
+    const int64_t m = mbase_ + wm * Cfg::WTM + ms * 16 + fr;
+#pragma unroll
+    for (int ns = 0; ns < 4; ++ns) {
+      hh[ns] = dd[ns] = f32x4{0.f, 0.f, 0.f, 0.f};
+      bits[ns] = 0u;
+    }
+    if (m < M) {
+#pragma unroll
+      for (int ns = 0; ns < 4; ++ns) {
+        const int n = n0 + wn * 64 + ns * 16 + fq * 4;
+        hh[ns] = *reinterpret_cast<const f32x4*>(static_cast<const float*>(bb.h) + m * ldc + n);
+        if (bb.dy2) dd[ns] = *reinterpret_cast<const f32x4*>(static_cast<const float*>(bb.dy2) + m * ldc + n);
+        bits[ns] = bb.mask ? (uint32_t)bb.mask[m * (Ntot >> 2) + (n >> 2)] : 0xfu;
+      }
+    }
+  };
   int64_t mt = blockIdx.x;
   for (int t = 0; t < T_; ++t) {
     // ops issued after stage(t), in order: NS=2: stores(t-1);
@@ -420,6 +450,12 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
     // with the previous tuning choices (128.1 before), 127.0 ms after a retune
     constexpr bool SPREAD = F32;
     if (pf) stage_prep();
+    if constexpr (PRE) {
+      if (ks == nk - 1) {
+#pragma unroll
+        for (int r = 0; r < PMS; ++r) bn_row_load(mt * Cfg::BM, r, pre_h[r], pre_d[r], pre_b[r]);
+      }
+    }
     if (!SPREAD && pf) {
 #pragma unroll
       for (int q = 0; q < LPW; ++q) stage_issue(q);
@@ -551,11 +587,20 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
         if constexpr (F32) {
           // fp32: lane owns 4 consecutive channels of every subtile -- one
           // 16-byte store per subtile, no shuffle.  BN-backward operands of the
-          // row's four subtiles are all loaded before the first is used (one
-          // exposed latency per row instead of one per subtile).
+          // row's four subtiles: prefetch slots (32x64 wave tiles) or loaded
+          // here, all four before the first use.
           f32x4 ehv[4], ed2[4];
           uint32_t ebits[4];
-          if (bnb) {
+          if constexpr (PRE) {
+            const int slot = ms % PMS;
+#pragma unroll
+            for (int ns = 0; ns < 4; ++ns) {
+              ehv[ns] = pre_h[slot][ns];
+              ed2[ns] = pre_d[slot][ns];
+              ebits[ns] = pre_b[slot][ns];
+            }
+            if (ms + PMS < MSB) bn_row_load(mbase, ms + PMS, pre_h[slot], pre_d[slot], pre_b[slot]);
+          } else if (bnb) {
 #pragma unroll
             for (int ns = 0; ns < 4; ++ns) {
               ehv[ns] = ed2[ns] = f32x4{0.f, 0.f, 0.f, 0.f};
