@@ -633,7 +633,10 @@ wino_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, flo
       tv[4 * i + 3] = t[4 * i + 1] - t[4 * i + 3];
     }
   };
-  // LDS writes of V rows [q0, q0 + nq) into buffer buf
+  // LDS writes of V rows [q0, q0 + nq) into buffer buf (2-way bank conflicts:
+  // rows 32 apart share banks at the 10-word stride; storing the rows with bit
+  // 5 set tile-swapped -- conflict-free, the wc = 1 waves swapping their dM
+  // pair to match -- measured 7% slower, r4c33)
   auto lwrite_v = [&](int buf, int q0, int nq) __attribute__((always_inline)) {
     float* V = wlds + buf * WGSTAGE;
 #pragma unroll
