@@ -21,13 +21,17 @@ Contract (ops/conv1x1.py, parallel/distributed_optimizer.py):
   stream -- consumers that read gradients mid-backward (a bucket launch on the
   communication stream) call it first.
 
-Off by default (``GKSGD_WGRAD_STREAM=1`` enables it; never during HIP-graph
-capture).  Measured on MI355X, fp32 ResNet-50 bs512 (bench/stream_probe.py):
-146.0 ms/step inline vs 147.8 ms with the side stream, and 2x the reserved
-memory; bf16 41.0 vs 41.8 ms.  Most likely cause (not traced): the
-persistent GEMM grids keep the CUs' register files and LDS occupied, so a BN
-pass issued on the other stream finds few free wave slots until the GEMM
-drains and little actually runs concurrently.  MIOpen grad-weights on the side stream were
+``GKSGD_WGRAD_STREAM``: ``0`` (default) never forks, ``auto`` forks only for
+small per-GPU batches (N <= 64, e.g. the reference's bs32), ``1`` always;
+never during HIP-graph capture.  Measured on MI355X, fp32 ResNet-50 bs512
+(bench/stream_probe.py): 146.0 ms/step inline vs 147.8 ms with the side
+stream, and 2x the reserved memory; bf16 41.0 vs 41.8 ms.  Most likely cause
+(not traced): the persistent GEMM grids keep the CUs' register files and LDS
+occupied, so a BN pass issued on the other stream finds few free wave slots
+until the GEMM drains and little actually runs concurrently.  At bs32 the
+grids are small and the fork usually pays (13.38 -> 13.21 ms/step, r4c6;
+12.85 vs 13.15 / 13.06 off in an interleaved A/B, r4c34) but one of the two
+``auto`` runs of that A/B took 17.1 ms/step, so it stays opt-in.  MIOpen grad-weights on the side stream were
 worse still (532 ms/step: its handle and workspace follow the stream), so a
 fork only ever carries a HIP-kernel choice.
 """
@@ -43,9 +47,18 @@ _pending: Dict[int, bool] = {}
 _callback_queued: Dict[int, bool] = {}
 
 
-def enabled(device: torch.device) -> bool:
-    return (device.type == "cuda" and os.environ.get("GKSGD_WGRAD_STREAM", "0") != "0"
-            and not torch.cuda.is_current_stream_capturing())
+AUTO_MAX_BATCH = 64
+
+
+def enabled(device: torch.device, batch: Optional[int] = None) -> bool:
+    """Fork this convolution's grad-weight?  ``batch``: its per-GPU batch
+    (``auto`` mode forks only at batch <= AUTO_MAX_BATCH)."""
+    if device.type != "cuda" or torch.cuda.is_current_stream_capturing():
+        return False
+    mode = os.environ.get("GKSGD_WGRAD_STREAM", "0")
+    if mode == "auto":
+        return batch is not None and batch <= AUTO_MAX_BATCH
+    return mode != "0"
 
 
 def _index(device) -> int:
