@@ -86,7 +86,7 @@ MODELS = {
 # The reference's own per-worker batch (/root/reference/exp_configs/<dnn>.conf:2):
 # the "ref_bs" phases time the same step at that batch, where the exchange is a
 # larger share of the step than at the headline batch.
-REF_BATCH = {"resnet50": 32, "vgg16i": 128, "vgg16": 128, "resnet20": 32, "lstm": 20, "fcn5net": 128}
+REF_BATCH = {"resnet50": 32, "vgg16i": 128, "vgg16": 128, "resnet20": 1024, "lstm": 20, "fcn5net": 128}
 
 # BERT (BASELINE config 5, "bucketed compression"): default bucket threshold in
 # elements (~25 MB of fp32 gradients per bucket, overlapped with the backward)
@@ -287,6 +287,8 @@ def run_phase(args, ph: Phase, steps: int, warmup: int, P: int):
         run()
     torch.cuda.synchronize()
     opt._collect_selected()  # drop warm-up counts
+    if opt._exchanger is not None:
+        opt._exchanger.reset_stats()   # shared communicator: count this phase's timed loop only
     state["mark"] = not args.graph
     comm.barrier()
     torch.cuda.synchronize()
@@ -350,15 +352,70 @@ def _agree(ok: bool, P: int):
         return False, False
 
 
+_EMIT = {"json_out": None}
+
+
+def emit(out: dict) -> None:
+    """Rank 0's one JSON line (stdout, and --json-out)."""
+    line = json.dumps(out)
+    print(line, flush=True)
+    if _EMIT["json_out"]:
+        with open(_EMIT["json_out"], "w") as f:
+            f.write(line + "\n")
+
+
+def _phase_deadline(name: str, out: dict, rank: int):
+    """A secondary phase that does not finish in ``GKSGD_BENCH_PHASE_TIMEOUT_S``
+    (default 240 s) ends the process: rank 0 first prints the JSON line with
+    the headline and the phases finished so far plus ``<name>_error``.  This
+    covers the ASYMMETRIC failure the agreement collective cannot: one rank
+    raises while the others still wait inside the phase's collectives, which
+    would otherwise hang until the 1800 s collective timeout and lose the
+    line.  Every rank arms its own timer, so every rank exits."""
+    import threading
+    s = float(os.environ.get("GKSGD_BENCH_PHASE_TIMEOUT_S", "240"))
+
+    def fire():
+        out[name + "_error"] = "timeout: phase not finished after %.0f s on rank %d" % (s, rank)
+        print("bench.py: phase %s timed out after %.0f s; exiting" % (name, s), file=sys.stderr, flush=True)
+        if rank == 0:
+            try:
+                emit(out)
+            finally:
+                os._exit(0)
+        os._exit(0)
+
+    t = threading.Timer(s, fire)
+    t.daemon = True
+    t.start()
+    return t
+
+
+def _injected(name: str) -> bool:
+    """GKSGD_BENCH_FAIL_PHASE=<phase> fails that phase on every rank;
+    GKSGD_BENCH_FAIL_PHASE_RANK=<r> restricts it to rank r (asymmetric)."""
+    if os.environ.get("GKSGD_BENCH_FAIL_PHASE") != name:
+        return False
+    only = os.environ.get("GKSGD_BENCH_FAIL_PHASE_RANK")
+    if only is None or only == "":
+        return True
+    from gaussiank_sgd_amd.parallel import comm
+    return int(only) == comm.rank()
+
+
 def optional_phase(name: str, out: dict, P: int, fn) -> bool:
     """Run one secondary phase fail-soft: an exception (or the injected one,
     ``GKSGD_BENCH_FAIL_PHASE=<name>``) is recorded as ``<name>_error`` in the
-    JSON line instead of losing the headline.  Returns whether the ranks
-    could still agree afterwards (False: skip the remaining phases)."""
+    JSON line instead of losing the headline; a phase that hangs (one rank
+    failed while the others wait in its collectives) hits ``_phase_deadline``.
+    Returns whether the ranks could still agree afterwards (False: skip the
+    remaining phases)."""
+    from gaussiank_sgd_amd.parallel import comm
     holder = []
     err = None
+    timer = _phase_deadline(name, out, comm.rank()) if P > 1 else None
     try:
-        if os.environ.get("GKSGD_BENCH_FAIL_PHASE") == name:
+        if _injected(name):
             raise RuntimeError("injected failure (GKSGD_BENCH_FAIL_PHASE=%s)" % name)
         fn(holder)
     except Exception as e:  # noqa: BLE001 - fail-soft by design
@@ -371,6 +428,8 @@ def optional_phase(name: str, out: dict, P: int, fn) -> bool:
         except Exception as e:  # noqa: BLE001
             err = err or "release: %s" % e
     ok, alive = _agree(err is None, P)
+    if timer is not None:
+        timer.cancel()
     if err is not None:
         out[name + "_error"] = err
     elif not ok:
@@ -380,6 +439,7 @@ def optional_phase(name: str, out: dict, P: int, fn) -> bool:
 
 def main() -> int:
     args = parse()
+    _EMIT["json_out"] = args.json_out
     from gaussiank_sgd_amd import ops
     from gaussiank_sgd_amd.compression import compressors
     from gaussiank_sgd_amd.parallel import comm
@@ -592,12 +652,9 @@ def main() -> int:
     if rank == 0 and os.environ.get("GKSGD_GEMM_SAVE"):
         from gaussiank_sgd_amd.ops.conv1x1 import save_choices
         save_choices(os.environ["GKSGD_GEMM_SAVE"])
+    out["native_inits"] = comm.native_bootstraps()   # one per process: the communicator is shared by every phase
     if rank == 0:
-        line = json.dumps(out)
-        print(line, flush=True)
-        if args.json_out:
-            with open(args.json_out, "w") as f:
-                f.write(line + "\n")
+        emit(out)
     try:
         comm.shutdown()
     except Exception as e:  # noqa: BLE001 - the result line is already out

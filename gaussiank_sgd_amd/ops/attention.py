@@ -120,8 +120,11 @@ class _FlashAttnF32Fn(torch.autograd.Function):
 
 
 def _compute_dtype(qkv: torch.Tensor):
-    if torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16:
-        return torch.bfloat16
+    """bf16 under bf16 autocast; otherwise the storage dtype -- but an
+    autocast to any OTHER dtype (fp16) takes the SDPA composition, which
+    follows autocast (as ops/ln.py and ops/linear.py do)."""
+    if torch.is_autocast_enabled("cuda"):
+        return torch.bfloat16 if torch.get_autocast_dtype("cuda") == torch.bfloat16 else None
     return qkv.dtype if qkv.dtype in (torch.bfloat16, torch.float32) else None
 
 

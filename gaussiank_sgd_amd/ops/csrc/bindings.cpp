@@ -753,6 +753,18 @@ struct RcclEngine : torch::CustomClassHolder {
     comm.init(v, (int)rank, (int)world, (int)device);
   }
 
+  // non-blocking bootstrap (parallel/comm.py _bootstrap_native)
+  void init_async(at::Tensor uid, int64_t rank, int64_t world, int64_t device) {
+    TORCH_CHECK(!uid.is_cuda() && uid.scalar_type() == at::kByte, "uid must be a CPU uint8 tensor");
+    at::Tensor c = uid.contiguous();
+    std::vector<uint8_t> v(c.data_ptr<uint8_t>(), c.data_ptr<uint8_t>() + c.numel());
+    comm.init_async(v, (int)rank, (int)world, (int)device);
+  }
+  int64_t init_poll() { return comm.init_poll(); }
+  void init_wait(double timeout_s) { comm.init_wait(timeout_s); }
+  void abort() { comm.abort(); }
+  void set_op_timeout(double s) { comm.set_op_timeout(s); }
+
   void allgather(at::Tensor send, at::Tensor recv) {
     check_dev(send, "send");
     check_dev(recv, "recv");
@@ -1875,6 +1887,11 @@ TORCH_LIBRARY(gksgd, m) {
       .def(torch::init<>())
       .def_static("unique_id", &RcclEngine::unique_id)
       .def("init", &RcclEngine::init)
+      .def("init_async", &RcclEngine::init_async)
+      .def("init_poll", &RcclEngine::init_poll)
+      .def("init_wait", &RcclEngine::init_wait)
+      .def("abort", &RcclEngine::abort)
+      .def("set_op_timeout", &RcclEngine::set_op_timeout)
       .def("allgather", &RcclEngine::allgather)
       .def("allreduce", &RcclEngine::allreduce)
       .def("broadcast", &RcclEngine::broadcast)

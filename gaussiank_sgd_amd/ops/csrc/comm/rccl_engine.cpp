@@ -16,6 +16,13 @@ std::string rccl_error_string(ncclResult_t r) { return std::string(ncclGetErrorS
   } while (0)
 
 namespace {
+size_t dtype_bytes(ncclDataType_t dt) {
+  return (dt == ncclFloat64 || dt == ncclInt64 || dt == ncclUint64) ? 8
+         : (dt == ncclFloat16 || dt == ncclBfloat16)                 ? 2
+         : (dt == ncclInt8 || dt == ncclUint8)                       ? 1
+                                                                     : 4;
+}
+
 const char* op_name(int op) {
   switch (op) {
     case kOpAllGather: return "all-gather";
@@ -43,16 +50,113 @@ std::vector<uint8_t> RcclComm::make_unique_id() {
   return out;
 }
 
-void RcclComm::init(const std::vector<uint8_t>& uid, int rank, int world, int device) {
+void RcclComm::init(const std::vector<uint8_t>& uid, int rank, int world, int device, double timeout_s) {
+  init_async(uid, rank, world, device);
+  init_wait(timeout_s);
+}
+
+void RcclComm::init_async(const std::vector<uint8_t>& uid, int rank, int world, int device) {
   if (comm_ != nullptr) throw std::runtime_error("RcclComm already initialised");
   ncclUniqueId id;
   if (uid.size() != sizeof(id.internal)) throw std::runtime_error("bad ncclUniqueId size");
   std::memcpy(id.internal, uid.data(), sizeof(id.internal));
   if (hipSetDevice(device) != hipSuccess) throw std::runtime_error("hipSetDevice failed");
-  GK_NCCL_CHECK(ncclCommInitRank(&comm_, world, id, rank));
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;   // returns at once; progress is polled (init_poll / init_wait)
+  ncclComm_t c = nullptr;
+  const ncclResult_t r = ncclCommInitRankConfig(&c, world, id, rank, &cfg);
+  if (r != ncclSuccess && r != ncclInProgress) {
+    if (c != nullptr) ncclCommAbort(c);
+    throw std::runtime_error(std::string("ncclCommInitRankConfig: ") + rccl_error_string(r));
+  }
+  comm_ = c;
   rank_ = rank;
   world_ = world;
   device_ = device;
+  init_done_ = false;
+  aborted_.store(false);
+  failed_.store(false);
+}
+
+int RcclComm::init_poll() {
+  if (comm_ == nullptr) throw std::runtime_error("RcclComm: init_poll before init_async (or after abort)");
+  if (init_done_) return 0;
+  ncclResult_t st = ncclSuccess;
+  const ncclResult_t q = ncclCommGetAsyncError(comm_, &st);
+  if (q != ncclSuccess) st = q;
+  if (st == ncclInProgress) return 1;
+  if (st != ncclSuccess) {
+    const std::string why = std::string("RCCL communicator init failed: ") + rccl_error_string(st);
+    abort();
+    throw std::runtime_error(why);
+  }
+  init_done_ = true;
+  return 0;
+}
+
+void RcclComm::init_wait(double timeout_s) {
+  const auto t0 = std::chrono::steady_clock::now();
+  while (init_poll() != 0) {
+    const double waited = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (timeout_s > 0.0 && waited > timeout_s) {
+      char buf[160];
+      std::snprintf(buf, sizeof(buf), "rank %d: RCCL communicator init not complete after %.1f s (world %d)",
+                    rank_, waited, world_);
+      abort();
+      throw std::runtime_error(buf);
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(500));
+  }
+}
+
+// Bootstrap failure (here or on another rank): release the communicator at
+// once.  ncclCommAbort also frees a communicator whose init is still in
+// progress and releases RCCL kernels spinning on a peer that never arrived.
+void RcclComm::abort() {
+  stop_watchdog();
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!failed_.load()) fail("aborted by the bootstrap protocol");
+  }
+  std::lock_guard<std::mutex> ek(enq_mu_);
+  bool expected = false;
+  if (comm_ != nullptr && aborted_.compare_exchange_strong(expected, true)) ncclCommAbort(comm_);
+  std::lock_guard<std::mutex> lk(mu_);
+  for (auto& p : pending_) {
+    pool_.push_back(p.start);
+    pool_.push_back(p.end);
+  }
+  pending_.clear();
+  comm_ = nullptr;
+}
+
+void RcclComm::settle(ncclResult_t r, const char* what, double timeout_s) {
+  if (r == ncclSuccess) return;
+  if (r != ncclInProgress)
+    throw std::runtime_error(std::string("RCCL error at ") + what + ": " + rccl_error_string(r));
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    ncclResult_t st = ncclSuccess;
+    const ncclResult_t q = ncclCommGetAsyncError(comm_, &st);
+    if (q != ncclSuccess) st = q;
+    if (st == ncclSuccess) return;
+    if (st != ncclInProgress) {
+      const std::string why = std::string("RCCL error at ") + what + ": " + rccl_error_string(st);
+      std::lock_guard<std::mutex> lk(mu_);
+      fail(why);   // the watchdog (or destroy) aborts the communicator
+      throw std::runtime_error(why);
+    }
+    const double waited = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (timeout_s > 0.0 && waited > timeout_s) {
+      char buf[200];
+      std::snprintf(buf, sizeof(buf), "rank %d: %s still in progress after %.1f s (world %d)", rank_, what, waited,
+                    world_);
+      std::lock_guard<std::mutex> lk(mu_);
+      fail(buf);
+      throw std::runtime_error(buf);
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(100));
+  }
 }
 
 void RcclComm::destroy() {
@@ -73,11 +177,41 @@ void RcclComm::destroy() {
     pool_.clear();
   }
   std::lock_guard<std::mutex> ek(enq_mu_);
-  if (comm_ != nullptr) {
-    ncclComm_t c = comm_;
-    comm_ = nullptr;
-    if (!aborted_.load()) GK_NCCL_CHECK(ncclCommDestroy(c));
+  if (comm_ == nullptr) return;
+  ncclComm_t c = comm_;
+  comm_ = nullptr;
+  if (aborted_.load()) return;   // an aborted communicator is already freed
+  if (failed_.load() || !init_done_) {
+    aborted_.store(true);
+    ncclCommAbort(c);
+    return;
   }
+  // non-blocking teardown: finalize (flush), bounded wait, then free; a
+  // finalize that does not finish (dead peer) ends in an abort
+  ncclResult_t r = ncclCommFinalize(c);
+  const auto t0 = std::chrono::steady_clock::now();
+  while (r == ncclSuccess || r == ncclInProgress) {
+    ncclResult_t st = ncclSuccess;
+    if (ncclCommGetAsyncError(c, &st) != ncclSuccess) {
+      r = ncclInternalError;
+      break;
+    }
+    if (st != ncclInProgress) {
+      r = st;
+      break;
+    }
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > op_timeout_s_) {
+      r = ncclInProgress;
+      break;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+  if (r != ncclSuccess) {
+    aborted_.store(true);
+    ncclCommAbort(c);
+    return;
+  }
+  GK_NCCL_CHECK(ncclCommDestroy(c));
 }
 
 // ---------------------------------------------------------------------------
@@ -264,7 +398,7 @@ void RcclComm::allgather_bytes(const void* send, void* recv, size_t bytes, hipSt
   std::lock_guard<std::mutex> ek(enq_mu_);   // see the failure protocol above fail()
   hipEvent_t st;
   begin_op(s, &st);
-  GK_NCCL_CHECK(ncclAllGather(send, recv, bytes, ncclUint8, comm_, s));
+  settle(ncclAllGather(send, recv, bytes, ncclUint8, comm_, s), "ncclAllGather", op_timeout_s_);
   end_op(s, st, kOpAllGather, bytes);
 }
 
@@ -286,7 +420,7 @@ void RcclComm::allgather_many(const std::vector<const void*>& sends, const std::
     }
     total += bytes[i];
   }
-  GK_NCCL_CHECK(ncclGroupEnd());
+  settle(ncclGroupEnd(), "grouped ncclAllGather", op_timeout_s_);
   end_op(s, st, kOpGroup, total);
 }
 
@@ -294,19 +428,16 @@ void RcclComm::allreduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t
   std::lock_guard<std::mutex> ek(enq_mu_);
   hipEvent_t st;
   begin_op(s, &st);
-  GK_NCCL_CHECK(ncclAllReduce(buf, buf, count, dt, op, comm_, s));
-  size_t esz = (dt == ncclFloat64 || dt == ncclInt64 || dt == ncclUint64) ? 8
-               : (dt == ncclFloat16 || dt == ncclBfloat16) ? 2
-               : (dt == ncclInt8 || dt == ncclUint8) ? 1 : 4;
-  end_op(s, st, kOpAllReduce, count * esz);
+  settle(ncclAllReduce(buf, buf, count, dt, op, comm_, s), "ncclAllReduce", op_timeout_s_);
+  end_op(s, st, kOpAllReduce, count * dtype_bytes(dt));
 }
 
 void RcclComm::broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t s) {
   std::lock_guard<std::mutex> ek(enq_mu_);
   hipEvent_t st;
   begin_op(s, &st);
-  GK_NCCL_CHECK(ncclBroadcast(buf, buf, count, dt, root, comm_, s));
-  end_op(s, st, kOpBroadcast, count);
+  settle(ncclBroadcast(buf, buf, count, dt, root, comm_, s), "ncclBroadcast", op_timeout_s_);
+  end_op(s, st, kOpBroadcast, count * dtype_bytes(dt));   // bytes, like the other ops
 }
 
 }  // namespace gk

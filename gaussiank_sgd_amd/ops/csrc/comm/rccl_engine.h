@@ -2,9 +2,16 @@
 //
 // Replaces the reference's Horovod background thread + MPI coordinator
 // (distributed_optimizer.py:21-26, Horovod 0.19 C++ core) with a direct RCCL
-// communicator per process.  Bootstrap: rank 0 creates an ncclUniqueId, the
-// Python side ships its 128 bytes through the torch.distributed store, every
-// rank calls ncclCommInitRank.  Collectives run on the CALLER's current HIP
+// communicator per process (one per device, built once and shared by every
+// optimizer of the process, like hvd.init() at dist_trainer.py:125-126).
+// Bootstrap: rank 0 creates an ncclUniqueId, the Python side ships its 128
+// bytes through the torch.distributed store, every rank starts a NON-BLOCKING
+// ncclCommInitRankConfig (config.blocking = 0) and polls it against a
+// deadline: a peer that never arrives ends in ncclCommAbort and an exception
+// on this rank instead of a process blocked forever inside RCCL.  The Python
+// side agrees every bootstrap step over the process group (parallel/comm.py
+// _bootstrap_native), so a failure on any rank sends all ranks to the
+// torch.distributed path.  Collectives run on the CALLER's current HIP
 // stream, so compress -> all-gather -> scatter is one stream-ordered chain
 // (no host sync, no ProcessGroup bookkeeping, capturable in a hipGraph).
 //
@@ -53,7 +60,19 @@ class RcclComm {
   RcclComm& operator=(const RcclComm&) = delete;
 
   static std::vector<uint8_t> make_unique_id();
-  void init(const std::vector<uint8_t>& uid, int rank, int world, int device);
+  // blocking convenience form: init_async + init_wait(timeout_s)
+  void init(const std::vector<uint8_t>& uid, int rank, int world, int device, double timeout_s = 120.0);
+  // non-blocking bootstrap: returns once the init is started
+  void init_async(const std::vector<uint8_t>& uid, int rank, int world, int device);
+  // 0 = ready, 1 = still in progress; aborts + throws on an RCCL error
+  int init_poll();
+  // polls until ready; on the deadline aborts the communicator and throws
+  void init_wait(double timeout_s);
+  // unconditional ncclCommAbort (bootstrap failure on this or another rank)
+  void abort();
+  // bound on how long an enqueue may wait for a non-blocking communicator
+  // to leave ncclInProgress (lazy connection setup on the first collectives)
+  void set_op_timeout(double s) { op_timeout_s_ = s; }
   void destroy();
   bool initialized() const { return comm_ != nullptr; }
   int rank() const { return rank_; }
@@ -95,6 +114,9 @@ class RcclComm {
   void begin_op(hipStream_t s, hipEvent_t* start);
   void end_op(hipStream_t s, hipEvent_t start, int op, size_t bytes);
   int retire_locked(bool check_timeout);
+  // non-blocking communicator: wait (bounded) until an enqueue that returned
+  // ncclInProgress has completed; throws on error / deadline
+  void settle(ncclResult_t r, const char* what, double timeout_s);
   void fail(const std::string& why);   // caller holds mu_; marks only
   void abort_comm();                    // caller holds neither lock
   void watchdog_loop();
@@ -104,6 +126,8 @@ class RcclComm {
   int world_ = 1;
   int device_ = 0;
   bool tracking_ = true;
+  bool init_done_ = false;
+  double op_timeout_s_ = 300.0;
   mutable std::mutex mu_;
   std::deque<Pending> pending_;
   std::vector<hipEvent_t> pool_;

@@ -1050,7 +1050,8 @@ __device__ __forceinline__ void decide_body(GkCtrl* __restrict__ gctrl, const ui
                             int cond, uint32_t* __restrict__ hist_reset) {
   __shared__ uint64_t sh_scan[kWavesPerBlock];
   __shared__ int s_chosen, s_gt, s_ge, s_stop;
-  __shared__ int64_t s_quota;
+  __shared__ int64_t s_quota, s_ref_total;
+  __shared__ float s_thr;
   __shared__ __attribute__((aligned(16))) GkCtrl s_ctrl;
   // ONE batch of loads, then no global read: the control block into an LDS
   // snapshot (one dword per thread; every ctrl read below is an LDS read and
@@ -1071,7 +1072,10 @@ __device__ __forceinline__ void decide_body(GkCtrl* __restrict__ gctrl, const ui
   }
   if (threadIdx.x < kCw) reinterpret_cast<uint32_t*>(&s_ctrl)[threadIdx.x] = cw;
   __syncthreads();
-  GkCtrl* ctrl = &s_ctrl;
+  // read-only snapshot: everything the decision changes goes through `dec`
+  // and is written back to gctrl below (a write to the snapshot, which would
+  // be silently dropped, does not compile)
+  const GkCtrl* ctrl = &s_ctrl;
   if (cond) {
     if (ctrl->fallback == 0) return;
     mode = kModeTopK;   // second decide of a fallback: exact top-k (or top-k_cap) on the radix key
@@ -1096,6 +1100,11 @@ __device__ __forceinline__ void decide_body(GkCtrl* __restrict__ gctrl, const ui
   __syncthreads();
   if (threadIdx.x == 0) {
     s_stop = 0;
+    struct {
+      double cal_c, cal_step;
+      int32_t fallback;
+      int64_t ref_total;
+    } dec = {ctrl->cal_c, ctrl->cal_step, ctrl->fallback, ctrl->ref_total};
     const int64_t* tot = s_tot;
     int chosen = 0, gt = 0, ge = -1;
     int64_t quota = 0;
@@ -1137,7 +1146,7 @@ __device__ __forceinline__ void decide_body(GkCtrl* __restrict__ gctrl, const ui
         if (c >= 2.0 * kd / 3.0 && c <= 4.0 * kd / 3.0 && d < bestd) { bestd = d; best = j; }
       }
       const int jc = best >= 0 ? best : closest;
-      double step = ctrl->cal_step;
+      double step = dec.cal_step;
       if (best < 0 && (jc == 0 || jc == nc - 1)) {
         step = step * 2.0;                                  // target beyond the ladder: widen
       } else if (jc > 0 && jc < nc - 1 && tot[jc + 1] > 0) {
@@ -1152,12 +1161,12 @@ __device__ __forceinline__ void decide_body(GkCtrl* __restrict__ gctrl, const ui
       }
       step = step < 0.002 ? 0.002 : (step > 1.0 ? 1.0 : step);
       const double sd = ctrl->stdev;
-      if (sd > 0.0 && ctrl->cand_thr[jc] > 0.0) ctrl->cal_c = ctrl->cand_thr[jc] / sd;
-      ctrl->cal_step = step;
+      if (sd > 0.0 && ctrl->cand_thr[jc] > 0.0) dec.cal_c = ctrl->cand_thr[jc] / sd;
+      dec.cal_step = step;
       chosen = jc;
       if (best < 0) {
         s_stop = 1;
-        ctrl->fallback = 1;
+        dec.fallback = 1;
       }
     } else if (mode == kModeThreshold) {
       chosen = 0;
@@ -1172,7 +1181,7 @@ __device__ __forceinline__ void decide_body(GkCtrl* __restrict__ gctrl, const ui
     // [2k/3, k_cap] (a higher threshold: the largest entries), else the exact
     // key at k_cap
     if (!cond && ge < 0 && !s_stop && tot[chosen] > k_cap) {
-      ctrl->ref_total = tot[chosen];
+      dec.ref_total = tot[chosen];
       int alt = -1;
       int64_t bc = -1;
       for (int j = 0; j < nc; ++j)
@@ -1181,28 +1190,25 @@ __device__ __forceinline__ void decide_body(GkCtrl* __restrict__ gctrl, const ui
         chosen = alt;
       } else {
         s_stop = 1;
-        ctrl->fallback = 2;
+        dec.fallback = 2;
       }
     }
     if (ge < 0) gt = chosen;
-    s_chosen = cond ? (ctrl->fallback == 2 ? kOverflowExact : kCalFallback) : chosen;
+    s_chosen = cond ? (dec.fallback == 2 ? kOverflowExact : kCalFallback) : chosen;
     s_gt = gt; s_ge = ge; s_quota = quota;
-    ctrl->chosen = s_chosen;
-    ctrl->sel_bound = ctrl->bound[gt];
-    ctrl->eq_key = ge >= 0 ? ctrl->bound[ge] : 0xffffffffu;
-    ctrl->eq_quota = ge >= 0 ? quota : 0;
-    ctrl->thr = (float)ctrl->cand_thr[chosen];
-    // the decision's fields back to the control block (read by the select /
+    s_thr = (float)ctrl->cand_thr[chosen];
+    s_ref_total = dec.ref_total;
+    // the decision's fields to the control block (read by the select /
     // conditional passes and the next call)
-    gctrl->cal_c = ctrl->cal_c;
-    gctrl->cal_step = ctrl->cal_step;
-    gctrl->fallback = ctrl->fallback;
-    gctrl->ref_total = ctrl->ref_total;
-    gctrl->chosen = ctrl->chosen;
-    gctrl->sel_bound = ctrl->sel_bound;
-    gctrl->eq_key = ctrl->eq_key;
-    gctrl->eq_quota = ctrl->eq_quota;
-    gctrl->thr = ctrl->thr;
+    gctrl->cal_c = dec.cal_c;
+    gctrl->cal_step = dec.cal_step;
+    gctrl->fallback = dec.fallback;
+    gctrl->ref_total = dec.ref_total;
+    gctrl->chosen = s_chosen;
+    gctrl->sel_bound = ctrl->bound[gt];
+    gctrl->eq_key = ge >= 0 ? ctrl->bound[ge] : 0xffffffffu;
+    gctrl->eq_quota = ge >= 0 ? quota : 0;
+    gctrl->thr = s_thr;
   }
   __syncthreads();
   if (s_stop) {
@@ -1266,11 +1272,11 @@ __device__ __forceinline__ void decide_body(GkCtrl* __restrict__ gctrl, const ui
     const int64_t sent = total < k_cap ? total : k_cap;
     gctrl->total = total;
     gctrl->sent = sent;
-    const int64_t rt = ctrl->ref_total >= 0 ? ctrl->ref_total : total;
+    const int64_t rt = s_ref_total >= 0 ? s_ref_total : total;
     hdr[0] = (int32_t)sent;
     hdr[1] = (int32_t)(rt > 0x7fffffff ? 0x7fffffff : rt);
     hdr[2] = s_chosen;
-    hdr[3] = __float_as_int(ctrl->thr);
+    hdr[3] = __float_as_int(s_thr);
   }
 }
 

@@ -21,6 +21,7 @@ import contextlib
 import datetime
 import os
 import threading
+import time
 from typing import Any, Callable, Dict, List, Optional
 
 import torch
@@ -156,6 +157,7 @@ def init(backend: Optional[str] = None, timeout_s: Optional[float] = None, devic
 def shutdown() -> None:
     if _loopback() is not None:
         return
+    release_native()
     if _S()["owns_pg"] and dist.is_initialized():
         dist.destroy_process_group()
     _S().update(initialized=False, rank=0, size=1, local_rank=0, local_size=1, backend=None, owns_pg=False)
@@ -425,39 +427,54 @@ def broadcast_optimizer_state(optimizer: torch.optim.Optimizer, root_rank: int =
 # ----------------------------------------------------------------------------
 # native RCCL engine
 # ----------------------------------------------------------------------------
+def _all_ok(ok: bool) -> bool:
+    """MIN over the ranks of a per-rank verdict: every rank gets the same answer."""
+    if _loopback() is not None:
+        return all(bool(x) for x in _lb_exchange(bool(ok)))
+    if not _distributed():
+        return bool(ok)
+    dev = torch.device("cuda", torch.cuda.current_device()) if backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return int(t.item()) == 1
+
+
+def _wait_event(ev, timeout_s: float, what: str) -> None:
+    """Host wait for a recorded HIP event with a deadline (no blocking
+    synchronize: a collective whose peer never arrives must not hang us)."""
+    deadline = time.monotonic() + timeout_s
+    while not ev.query():
+        if time.monotonic() > deadline:
+            raise TimeoutError("%s not complete after %.1f s" % (what, timeout_s))
+        time.sleep(0.0005)
+
+
 class RcclCommunicator:
-    """Own RCCL communicator (C++ ``gk::RcclComm``) bootstrapped through the
-    torch.distributed store.  Collectives run on the CALLER's current stream."""
+    """Own RCCL communicator (C++ ``gk::RcclComm``), built ONCE per process and
+    device by ``native_communicator`` (the bootstrap protocol below) and shared
+    by every ``Exchanger`` / ``DistributedOptimizer`` of the process, as
+    ``hvd.init()`` is called once per process in the reference
+    (dist_trainer.py:125-126).  Collectives run on the CALLER's current stream."""
 
-    def __init__(self, device: torch.device):
-        from .. import ops
-        cls = ops.rccl_engine_class()
-        self.engine = cls()
+    def __init__(self, engine, device: torch.device, rank_: int, world: int):
+        self.engine = engine
         self.device = torch.device(device)
-        self.world = size()
-        self.rank = rank()
-        if self.rank == 0:
-            uid = cls.unique_id()
-        else:
-            uid = None
-        uid_list = broadcast_object(uid.tolist() if uid is not None else None, 0)
-        uid_t = torch.tensor(uid_list, dtype=torch.uint8)
-        self.engine.init(uid_t, self.rank, self.world, self.device.index or 0)
-        self.self_test()
-        # hang / async-error watchdog: aborts the communicator instead of
-        # letting a dead peer hang the GPU; the next hot-path call raises
-        wd = float(os.environ.get("GKSGD_RCCL_WATCHDOG_S", "600"))
-        if wd > 0:
-            self.engine.start_watchdog(wd, 5.0)
+        self.rank = rank_
+        self.world = world
+        self.users = 0          # Exchangers that attached to it (diagnostics)
 
-    def self_test(self) -> None:
+    def self_test(self, timeout_s: float = 120.0) -> None:
         """One all-gather of the rank ids on the current stream, checked on the
-        host once at start-up: a mis-bootstrapped communicator fails here
-        (and the Exchanger falls back to torch.distributed on every rank)
-        instead of corrupting gradients later."""
+        host with a deadline at start-up: a mis-bootstrapped communicator fails
+        here (and every rank falls back to torch.distributed) instead of
+        corrupting gradients later."""
         inp = torch.full((4,), self.rank, dtype=torch.int32, device=self.device)
         out = torch.full((4 * self.world,), -1, dtype=torch.int32, device=self.device)
         self.engine.allgather(inp, out)
+        if self.device.type == "cuda":
+            ev = torch.cuda.Event()
+            ev.record()
+            _wait_event(ev, timeout_s, "native RCCL all-gather self-test")
         got = out.view(self.world, 4).cpu()
         want = torch.arange(self.world, dtype=torch.int32)[:, None].expand(self.world, 4)
         if not torch.equal(got, want):
@@ -483,6 +500,10 @@ class RcclCommunicator:
                              "us_max": 1e3 * mx}
         return out
 
+    def reset_stats(self) -> None:
+        self.engine.poll()
+        self.engine.reset_stats()
+
     def allreduce_(self, t: torch.Tensor, average: bool = True) -> None:
         self.engine.allreduce(t, 1 if average else 0)
 
@@ -494,42 +515,162 @@ class RcclCommunicator:
         self.engine.destroy()
 
 
+def _bootstrap_native(device: torch.device, engine_cls=None,
+                      timeout_s: Optional[float] = None) -> Optional[RcclCommunicator]:
+    """Build the native communicator with every blocking step bounded and
+    agreed over the process group before the next one starts:
+
+    1. rank 0 makes the ncclUniqueId; it is broadcast (None if that failed)
+       and the ranks agree that the engine class loaded everywhere;
+    2. every rank starts a NON-BLOCKING ``ncclCommInitRankConfig`` and polls it
+       against ``GKSGD_RCCL_INIT_TIMEOUT_S`` (default 120 s); on the deadline the
+       communicator is aborted (ncclCommAbort);  agree;
+    3. a start-up all-gather self-test, waited for with the same deadline;
+       agree.
+
+    A failure on ANY rank at ANY step aborts the communicator on every rank
+    that built one and returns None everywhere, so all ranks take the
+    torch.distributed path together; nothing waits without a deadline except
+    the agreement collectives themselves, which every rank reaches in bounded
+    time.  ``engine_cls`` substitutes the C++ engine (fault-injection tests)."""
+    from ..settings import logger
+    _BOOTSTRAPS[0] += 1
+    r, P = rank(), size()
+    tmo = float(timeout_s if timeout_s is not None else os.environ.get("GKSGD_RCCL_INIT_TIMEOUT_S", "120"))
+    err: Optional[str] = None
+    cls = engine_cls
+    if cls is None:
+        try:
+            from .. import ops
+            cls = ops.rccl_engine_class()
+        except Exception as e:  # noqa: BLE001 - agreed below
+            err = "engine class: %s" % e
+    uid = None
+    if r == 0 and err is None:
+        try:
+            uid = [int(x) for x in cls.unique_id().tolist()]
+        except Exception as e:  # noqa: BLE001
+            err = "unique id: %s" % e
+    uid = broadcast_object(uid, 0)
+    if not _all_ok(err is None and uid is not None):
+        logger.warning("native RCCL engine not used (bootstrap step 1 on rank %d: %s)", r,
+                       err or "another rank failed")
+        return None
+
+    # step 2: non-blocking init with a deadline
+    eng = None
+    aborted = False
+    try:
+        eng = cls()
+        idx = device.index if device.index is not None else 0
+        eng.init_async(torch.tensor(uid, dtype=torch.uint8), r, P, idx)
+        deadline = time.monotonic() + tmo
+        while int(eng.init_poll()) != 0:
+            if time.monotonic() > deadline:
+                eng.abort()
+                aborted = True
+                raise TimeoutError("RCCL communicator init not complete after %.1f s" % tmo)
+            time.sleep(0.001)
+    except Exception as e:  # noqa: BLE001 - agreed below
+        err = "init: %s" % e
+        aborted = True        # init_poll / init_async abort (or never built) the communicator on error
+    if not _all_ok(err is None):
+        if eng is not None and not aborted:
+            eng.abort()
+        logger.warning("native RCCL engine not used (bootstrap step 2 on rank %d: %s)", r,
+                       err or "another rank failed")
+        return None
+
+    # step 3: start-up self-test with a deadline
+    c = RcclCommunicator(eng, device, r, P)
+    try:
+        c.self_test(tmo)
+    except Exception as e:  # noqa: BLE001
+        err = "self-test: %s" % e
+        eng.abort()           # releases RCCL kernels still spinning on a missing peer
+        aborted = True
+    if not _all_ok(err is None):
+        if not aborted:
+            eng.abort()
+        logger.warning("native RCCL engine not used (bootstrap step 3 on rank %d: %s)", r,
+                       err or "another rank failed")
+        return None
+    # hang / async-error watchdog: aborts the communicator instead of letting a
+    # dead peer hang the GPU; the next hot-path call raises
+    wd = float(os.environ.get("GKSGD_RCCL_WATCHDOG_S", "600"))
+    if wd > 0:
+        eng.start_watchdog(wd, 5.0)
+    return c
+
+
+_BOOTSTRAPS = [0]
+
+
+def native_bootstraps() -> int:
+    """How many times this process ran the native bootstrap (one per device
+    is the design: bench.py reports it as ``native_inits``)."""
+    return _BOOTSTRAPS[0]
+
+
+def native_communicator(device, engine_cls=None) -> Optional[RcclCommunicator]:
+    """The process's native communicator for ``device`` (one per device,
+    built on first use by ``_bootstrap_native`` -- a COLLECTIVE call: every
+    rank must ask for it at the same point -- and reused afterwards; None when
+    the ranks agreed to use torch.distributed).  The verdict is cached too,
+    identical on every rank, so later calls are local.  ``shutdown()`` /
+    ``release_native()`` destroy it."""
+    dev = torch.device(device)
+    if dev.type == "cuda" and dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    cache = _S().setdefault("native", {})
+    key = (str(dev), engine_cls)
+    if key not in cache:
+        cache[key] = _bootstrap_native(dev, engine_cls)
+    return cache[key]
+
+
+def release_native() -> None:
+    """Destroy the cached native communicators (after their devices are idle)."""
+    cache = _S().pop("native", None) or {}
+    for c in cache.values():
+        if c is None:
+            continue
+        if c.device.type == "cuda":
+            torch.cuda.synchronize(c.device)
+        c.destroy()
+
+
 class Exchanger:
     """Stream-ordered fixed-size collectives used by the hot path.
 
-    backend 'rccl-native' -> RcclCommunicator, 'torch' -> torch.distributed,
-    'loopback' -> in-process virtual ranks (loopback_world), 'local' -> world
-    of one (copies).  All calls are issued on the current
-    stream and return without blocking the host.
+    backend 'rccl-native' -> the process's shared RcclCommunicator,
+    'torch' -> torch.distributed, 'loopback' -> in-process virtual ranks
+    (loopback_world), 'local' -> world of one (copies).  All calls are issued
+    on the current stream and return without blocking the host.
+
+    ``force_native`` uses the native engine even in a world of one (GPU tests
+    of the shared communicator); ``engine_cls`` substitutes the C++ engine.
     """
 
-    def __init__(self, device: torch.device, prefer_native: bool = True):
+    def __init__(self, device: torch.device, prefer_native: bool = True, engine_cls=None,
+                 force_native: bool = False):
         self.device = torch.device(device)
         self.P = size()
         self.native: Optional[RcclCommunicator] = None
-        self.kind = "local"
         self._lb_state = getattr(_tls, "state", None)
-        if self.P > 1 and _loopback() is not None:
-            self.kind = "loopback"          # module collectives take the loopback branch
-        elif self.P > 1:
-            self.kind = "torch"
-            if prefer_native and self.device.type == "cuda" and os.environ.get("GKSGD_NATIVE_RCCL", "1") == "1":
-                ok = 1
-                try:
-                    self.native = RcclCommunicator(self.device)
-                except Exception as e:  # pragma: no cover - GPU only
-                    from ..settings import logger
-                    logger.warning("native RCCL engine unavailable (%s); using torch.distributed", e)
-                    ok = 0
-                # every rank takes the same path: one failed self-test sends all to torch.distributed
-                flag = torch.tensor([ok], dtype=torch.int32,
-                                    device=self.device if backend() == "nccl" else "cpu")
-                dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-                if int(flag) == 1:
-                    self.kind = "rccl-native"
-                elif self.native is not None:
-                    self.native.destroy()
-                    self.native = None
+        lb = _loopback() is not None
+        if self.P > 1:
+            self.kind = "loopback" if lb else "torch"
+        else:
+            self.kind = "local"
+        want = prefer_native and (self.P > 1 or force_native) and os.environ.get("GKSGD_NATIVE_RCCL", "1") == "1"
+        # a loopback world's ranks are threads of one process (one device):
+        # only a substituted engine can stand in for RCCL there
+        if want and (engine_cls is not None or (self.device.type == "cuda" and not lb)):
+            self.native = native_communicator(self.device, engine_cls)
+            if self.native is not None:
+                self.native.users += 1
+                self.kind = "rccl-native"
 
     @contextlib.contextmanager
     def _bound(self):
@@ -543,11 +684,11 @@ class Exchanger:
             _tls.state = prev
 
     def allgather_(self, out: torch.Tensor, inp: torch.Tensor) -> None:
-        if self.kind == "local":
+        if self.native is not None:
+            self.native.allgather_(out, inp)
+        elif self.kind == "local":
             if out.data_ptr() != inp.data_ptr():
                 out.view(-1)[: inp.numel()].copy_(inp.view(-1))
-        elif self.native is not None:
-            self.native.allgather_(out, inp)
         else:
             with self._bound():
                 allgather_into_(out, inp, async_op=False)
@@ -567,29 +708,34 @@ class Exchanger:
     def stats(self) -> Dict[str, Dict[str, float]]:
         return self.native.stats() if self.native is not None else {}
 
+    def reset_stats(self) -> None:
+        """Start a fresh statistics window (the communicator is shared, so a
+        phase's collectives are counted from here)."""
+        if self.native is not None:
+            self.native.reset_stats()
+
     def allreduce_(self, t: torch.Tensor, average: bool = True) -> None:
-        if self.kind == "local":
-            return
         if self.native is not None:
             self.native.allreduce_(t, average)
+        elif self.kind == "local":
+            return
         else:
             with self._bound():
                 allreduce_(t, average)
 
     def broadcast_(self, t: torch.Tensor, root: int = 0) -> None:
-        if self.kind == "local":
-            return
         if self.native is not None:
             self.native.broadcast_(t, root)
+        elif self.kind == "local":
+            return
         else:
             with self._bound():
                 broadcast_(t, root)
 
     def close(self) -> None:
-        """Release the native communicator (after the device is idle)."""
+        """Detach from the shared native communicator (it stays alive for the
+        next optimizer of the process; ``comm.shutdown()`` destroys it)."""
         if self.native is not None:
-            if self.device.type == "cuda":
-                torch.cuda.synchronize(self.device)
-            self.native.destroy()
+            self.native.users -= 1
             self.native = None
-            self.kind = "torch"
+            self.kind = ("loopback" if self._lb_state is not None else "torch") if self.P > 1 else "local"

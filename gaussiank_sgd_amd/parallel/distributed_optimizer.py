@@ -126,7 +126,11 @@ class _DistributedOptimizer(torch.optim.Optimizer):
             # autograd runs GPU backward (and so the grad hooks) on one shared
             # device thread, not on the virtual rank's thread: exchange in step()
             self._overlap = False
-        self._prefer_native_rccl = bool(opts.get("native_rccl", True))
+        # native_rccl: True (native engine when world > 1), False, or "force"
+        # (native engine even in a world of one: GPU tests of the shared communicator)
+        nr = opts.get("native_rccl", True)
+        self._force_native_rccl = nr == "force"
+        self._prefer_native_rccl = bool(nr)
         self._planner_preset = opts.get("planner_preset", "mi355x")
         # planner: "threshold" (reference default), "mgs" / "mgwfbp" (use the
         # layer-wise times even without settings.ADAPTIVE_MERGE), "auto"
@@ -262,7 +266,8 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         dev = self._arena.device
         self._device = dev
         self._is_cuda = dev.type == "cuda"
-        self._exchanger = comm.Exchanger(dev, prefer_native=self._prefer_native_rccl) if self._hooks_on else None
+        self._exchanger = comm.Exchanger(dev, prefer_native=self._prefer_native_rccl,
+                                         force_native=self._force_native_rccl) if self._hooks_on else None
         self._comm_stream = None
         # GKSGD_COMM_STREAM=0: compression / exchange inline on the compute stream
         # (no overlap; a single-stream step, e.g. for whole-step graph capture)

@@ -53,3 +53,57 @@ def test_bert_default_threshold_gives_buckets(bench):
     sizes = {n: p.numel() for n, p in net.named_parameters()}
     groups = group_with_threshold(names, sizes, bench.DEFAULT_THRESHOLD["bert"])
     assert len(groups) >= 4
+
+
+def _asym_worker(rank, port, outdir):
+    """Rank 1 fails the phase (GKSGD_BENCH_FAIL_PHASE_RANK) while rank 0 waits
+    in the phase's own point-to-point exchange for it: the agreement
+    collective cannot pair up, so only the phase deadline ends the run."""
+    import time
+    import torch
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2",
+                      LOCAL_RANK=str(rank), GKSGD_BENCH_FAIL_PHASE="dense", GKSGD_BENCH_FAIL_PHASE_RANK="1",
+                      GKSGD_BENCH_PHASE_TIMEOUT_S="3")
+    spec = importlib.util.spec_from_file_location("gk_bench", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    from gaussiank_sgd_amd.parallel import comm
+    comm.init(device="cpu")
+    bench._EMIT["json_out"] = os.path.join(outdir, "line.json")
+    out = {"metric": "m", "value": 1.0}
+
+    def phase(holder):
+        t = torch.zeros(1)
+        torch.distributed.recv(t, src=1)     # rank 1 never sends: it failed before
+    t0 = time.time()
+    bench.optional_phase("dense", out, 2, phase)
+    # not reached when the deadline fired (os._exit); reached only if the ranks agreed
+    with open(os.path.join(outdir, "returned%d" % rank), "w") as f:
+        f.write("%.1f" % (time.time() - t0))
+
+
+def test_asymmetric_phase_failure_keeps_the_headline_line():
+    import json
+    import socket
+    import tempfile
+    import time
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    with tempfile.TemporaryDirectory() as d:
+        t0 = time.time()
+        mp.spawn(_asym_worker, args=(port, d), nprocs=2, join=True)
+        assert time.time() - t0 < 60
+        line = json.loads(open(os.path.join(d, "line.json")).read())
+        assert line["value"] == 1.0 and "timeout" in line["dense_error"], line
+        assert not os.path.exists(os.path.join(d, "returned0"))
+
+
+def test_per_rank_injection(bench, monkeypatch):
+    monkeypatch.setenv("GKSGD_BENCH_FAIL_PHASE", "bf16")
+    monkeypatch.setenv("GKSGD_BENCH_FAIL_PHASE_RANK", "1")
+    assert not bench._injected("bf16")          # this process is rank 0
+    monkeypatch.setenv("GKSGD_BENCH_FAIL_PHASE_RANK", "0")
+    assert bench._injected("bf16") and not bench._injected("dense")

@@ -3,6 +3,7 @@
 Run on the MI355X box: ``pytest -m gpu``.
 """
 import math
+import os
 
 import pytest
 import torch
@@ -403,13 +404,83 @@ def test_momentum_correct_and_mask(cuda):
 
 
 def test_rccl_communicator_self_test_world1(cuda):
-    """RcclCommunicator bootstrap + its start-up all-gather self-test."""
+    """The non-blocking bootstrap (init_async / init_poll with a deadline) +
+    its start-up all-gather self-test, through the process-wide cache."""
     from gaussiank_sgd_amd.parallel import comm
     comm.init()
-    c = comm.RcclCommunicator(cuda)
-    c.self_test()
+    c = comm.native_communicator(cuda)
+    assert c is not None
+    c.self_test(30.0)
+    assert comm.native_communicator(cuda) is c
     torch.cuda.synchronize()
-    c.destroy()
+    comm.release_native()
+
+
+def test_two_optimizers_share_one_communicator(cuda):
+    """Every DistributedOptimizer of the process reuses ONE native
+    communicator (bench.py's phases, a re-created trainer): one init per
+    process, like hvd.init() (reference dist_trainer.py:125-126)."""
+    from gaussiank_sgd_amd.compression import compressors
+    from gaussiank_sgd_amd.parallel import comm
+    from gaussiank_sgd_amd.parallel.distributed_optimizer import DistributedOptimizer
+    comm.init()
+    opts = []
+    for _ in range(2):
+        net = torch.nn.Sequential(torch.nn.Linear(64, 32), torch.nn.ReLU(), torch.nn.Linear(32, 8)).to(cuda)
+        opts.append(DistributedOptimizer(torch.optim.SGD(net.parameters(), lr=0.1, momentum=0.9),
+                                         named_parameters=net.named_parameters(),
+                                         compression=compressors["gaussian"], is_sparse=True, density=0.05,
+                                         compress_single_rank=True, density_warmup=False, native_rccl="force"))
+        x = torch.randn(16, 64, device=cuda)
+        opts[-1].zero_grad()
+        net(x).square().mean().backward()
+        opts[-1].step()
+    torch.cuda.synchronize()
+    e0, e1 = opts[0]._exchanger, opts[1]._exchanger
+    assert e0.kind == e1.kind == "rccl-native"
+    assert e0.native is e1.native and e0.native.users == 2
+    inp = torch.arange(8, dtype=torch.int32, device=cuda)
+    out = torch.zeros_like(inp)
+    e0.reset_stats()
+    e0.allgather_(out, inp)
+    e1.allgather_(out, inp)
+    torch.cuda.synchronize()
+    assert torch.equal(out, inp)
+    assert e1.stats()["allgather"]["calls"] == 2      # one communicator counts both Exchangers' calls
+    e0.close()
+    assert e1.native is not None and e1.native.users == 1
+    comm.release_native()
+
+
+_INIT_TIMEOUT_PROBE = """
+import sys, time, torch
+from gaussiank_sgd_amd import ops
+torch.cuda.set_device(0)
+cls = ops.rccl_engine_class()
+e = cls()
+t0 = time.time()
+e.init_async(cls.unique_id(), 0, 2, 0)      # world 2, the peer never arrives
+try:
+    e.init_wait(3.0)
+except RuntimeError as err:
+    print("raised after %.1f s: %s" % (time.time() - t0, err), flush=True)
+    sys.exit(0)
+print("init completed without a peer", flush=True)
+sys.exit(1)
+"""
+
+
+def test_rccl_init_deadline_aborts_without_peer(cuda):
+    """The hang the bootstrap guards against, on the real engine: rank 0 of a
+    world of 2 whose peer never joins.  The non-blocking init must end in
+    ncclCommAbort + an exception at the deadline (run in a child process with
+    its own time limit so a regression cannot hang the test session)."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, "-c", _INIT_TIMEOUT_PROBE], capture_output=True, text=True, timeout=90,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0, (r.stdout, r.stderr[-2000:])
+    assert "raised after" in r.stdout and "not complete" in r.stdout, r.stdout
 
 
 def test_rccl_engine_failure_races_enqueue(cuda):
