@@ -370,8 +370,9 @@ class DeviceLoader:
         self._stream = torch.cuda.Stream(self.device) if self._pin else None
         self._q: "queue.Queue" = queue.Queue(maxsize=max(1, prefetch))
         self._stop = threading.Event()
-        self._thread = threading.Thread(target=self._producer, name="gk-data", daemon=True)
-        self._thread.start()
+        # the prefetch thread starts on the first next(): an evaluation split
+        # that is only walked by full_pass() never runs one
+        self._thread: Optional[threading.Thread] = None
 
     def num_samples(self) -> int:
         return self.sampler.n
@@ -380,13 +381,13 @@ class DeviceLoader:
         return self.sampler.batches_per_epoch()
 
     def _gather(self, idx: torch.Tensor):
-        xs = (self.batch_size,) + tuple(self.x.shape[1:])
+        xs = (idx.numel(),) + tuple(self.x.shape[1:])
         xb = torch.empty(xs, dtype=self.x.dtype, pin_memory=self._pin)
         if isinstance(self.x, (_MmapRows, ImageFolderRows)):   # memory-mapped arrays, decoded image folders
             self.x.gather(idx, xb)
         else:
             torch.index_select(self.x, 0, idx, out=xb)
-        yb = torch.empty((self.batch_size,) + tuple(self.y.shape[1:]), dtype=self.y.dtype, pin_memory=self._pin)
+        yb = torch.empty((idx.numel(),) + tuple(self.y.shape[1:]), dtype=self.y.dtype, pin_memory=self._pin)
         torch.index_select(self.y, 0, idx, out=yb)
         return xb, yb
 
@@ -408,10 +409,15 @@ class DeviceLoader:
         return self
 
     def __next__(self):
+        if self._thread is None:
+            self._thread = threading.Thread(target=self._producer, name="gk-data", daemon=True)
+            self._thread.start()
         item = self._q.get()
         if isinstance(item, BaseException):
             raise item
-        xb, yb = item
+        return self._deliver(*item)
+
+    def _deliver(self, xb: torch.Tensor, yb: torch.Tensor):
         if self._stream is not None:
             with torch.cuda.stream(self._stream):
                 xd = xb.to(self.device, non_blocking=True)
@@ -439,6 +445,18 @@ class DeviceLoader:
 
     def test_batches(self, n: int = 2):
         return [next(self) for _ in range(n)]
+
+    def full_pass(self):
+        """Every sample of the split exactly once, in storage order, in
+        batches of ``batch_size`` with the ragged last batch INCLUDED -- the
+        reference's ``testloader`` (DataLoader(shuffle=False), drop_last
+        False; dl_trainer.py:339-342,376-377,753) that ``test()`` walks whole.
+        Synchronous (no prefetch thread), independent of the training stream
+        of batches."""
+        n = self.sampler.n
+        for s in range(0, n, self.batch_size):
+            idx = torch.arange(s, min(n, s + self.batch_size))
+            yield self._deliver(*self._gather(idx))
 
 
 def open_dataset(dataset: str, data_dir: str, batch_size: int, device, rank: int = 0, world: int = 1,
@@ -476,7 +494,9 @@ def open_dataset(dataset: str, data_dir: str, batch_size: int, device, rank: int
         if not os.path.isfile(os.path.join(data_dir, "ptb.train.txt")):
             return None
         tr, va, te, w2i, _ = ptb_raw_data(data_dir)
-        x, y = ptb_windows(tr if train else te, num_steps, batch_size)
+        # evaluation on the validation split, as the reference's test() does
+        # (dl_trainer.py ptb_prepare: TestDataset(valid_data, ...))
+        x, y = ptb_windows(tr if train else va, num_steps, batch_size)
         return DeviceLoader(x, y, batch_size, device, rank, world, seed, None, train, shuffle=train, seq_first=True)
     if x is None:
         return None

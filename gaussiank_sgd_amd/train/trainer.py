@@ -42,6 +42,52 @@ _support_dnns = ["resnet50", "googlenet", "inceptionv4", "inceptionv3", "vgg16i"
                  "bert_tiny", "resnet18", "resnet34", "resnet101", "resnet152", "densenet100", "resnext29"]
 
 
+# AN4 character set (the reference's labels.json): index 0 is the CTC blank
+AN4_LABELS = "_'ABCDEFGHIJKLMNOPQRSTUVWXYZ "
+
+
+def AN4_LABELS_STR(ids) -> str:
+    return "".join(AN4_LABELS[int(i)] for i in ids if 0 < int(i) < len(AN4_LABELS))
+
+
+def ctc_greedy_decode(outputs: torch.Tensor, out_lens: torch.Tensor):
+    """Best-path CTC decode of [N, T, C] scores: per-frame argmax, repeats
+    collapsed, blanks (0) dropped; one id list per utterance."""
+    best = outputs.argmax(-1).cpu()
+    lens = out_lens.cpu().tolist()
+    res = []
+    for n in range(best.shape[0]):
+        seq, prev = [], -1
+        for t in best[n, : int(lens[n])].tolist():
+            if t != prev and t != 0:
+                seq.append(t)
+            prev = t
+        res.append(seq)
+    return res
+
+
+def split_targets(targets: torch.Tensor, tgt_lens: torch.Tensor):
+    """Concatenated CTC targets -> one id list per utterance."""
+    out, o = [], 0
+    flat = targets.reshape(-1).cpu().tolist()
+    for n in tgt_lens.cpu().tolist():
+        out.append(flat[o:o + int(n)])
+        o += int(n)
+    return out
+
+
+def word_errors(hyp: str, ref: str) -> int:
+    """Word-level Levenshtein distance (the WER numerator)."""
+    h, r = hyp.split(), ref.split()
+    prev = list(range(len(h) + 1))
+    for i in range(1, len(r) + 1):
+        cur = [i] + [0] * len(h)
+        for j in range(1, len(h) + 1):
+            cur[j] = min(prev[j] + 1, cur[j - 1] + 1, prev[j - 1] + (r[i - 1] != h[j - 1]))
+        prev = cur
+    return prev[-1]
+
+
 class DLTrainer:
     def __init__(self, rank, size, master="gpu10", dist=True, ngpus=1, batch_size=32, is_weak_scaling=True,
                  data_dir="./data", dataset="cifar10", dnn="resnet20", lr=0.04, nworkers=1, prefix=None,
@@ -356,19 +402,46 @@ class DLTrainer:
         """Loss of the last train() call (host sync)."""
         return float(self._loss_acc) if self._loss_acc is not None else float("nan")
 
+    def _eval_batches(self, num_batches: Optional[int]):
+        """Evaluation batches: the WHOLE test split, each sample once, when a
+        real one is loaded (the reference's test() walks its testloader,
+        dl_trainer.py:753); synthetic data has no split -> ``num_batches``
+        sampled batches (default 2)."""
+        src = self.test_data if getattr(self, "test_data", None) is not None else self.data
+        if num_batches is None and hasattr(src, "full_pass"):
+            return src.full_pass()
+        return src.test_batches(num_batches if num_batches is not None else 2)
+
     @torch.no_grad()
-    def test(self, epoch, num_batches: int = 2):
+    def test(self, epoch, num_batches: Optional[int] = None):
+        """Reference dl_trainer.py:742-824: mean over batches of the batch loss
+        and top-1 / top-5 accuracy; LSTM perplexity exp(sum cost / steps);
+        lstman4 word error rate of the greedy CTC decode (sum over utterances
+        of edit distance / reference words, over the number of utterances)."""
         self.net.eval()
         top1, top5, losses = [], [], []
         costs, steps = 0.0, 0
-        src = self.test_data if getattr(self, "test_data", None) is not None else self.data
-        for inputs, labels in src.test_batches(num_batches):
+        wer_sum, utterances = 0.0, 0
+        for inputs, labels in self._eval_batches(num_batches):
+            if self.dnn == "lstman4":
+                targets, tgt_lens, in_lens = labels
+                with self._autocast():
+                    outputs, out_lens = self.net(inputs, in_lens)
+                hyps = ctc_greedy_decode(outputs.float(), out_lens)
+                refs = split_targets(targets, tgt_lens)
+                for h, r in zip(hyps, refs):
+                    ref_s = AN4_LABELS_STR(r)
+                    wer_sum += word_errors(AN4_LABELS_STR(h), ref_s) / float(max(1, len(ref_s.split())))
+                utterances += len(refs)
+                logp = outputs.float().log_softmax(-1).transpose(0, 1)
+                losses.append(float(self.criterion(logp, targets, out_lens, tgt_lens) / inputs.size(0)))
+                continue
             outputs, loss, _ = self.forward_loss(inputs, labels, None)
             losses.append(float(loss))
             if self.dnn == "lstm":
                 costs += float(loss) * self.num_steps
                 steps += self.num_steps
-            elif not self.dnn.startswith("bert") and self.dnn != "lstman4":
+            elif not self.dnn.startswith("bert"):
                 k5 = min(5, outputs.shape[1])
                 a1, a5 = self.cal_accuracy(outputs.float(), labels, topk=(1, k5))
                 top1.append(float(a1))
@@ -377,7 +450,7 @@ class DLTrainer:
         if self.dnn == "lstm":
             acc, acc5 = float(np.exp(costs / max(1, steps))), 0.0
         elif self.dnn == "lstman4":
-            acc, acc5 = test_loss, 0.0
+            acc, acc5 = wer_sum / max(1, utterances), 0.0
         elif self.dnn.startswith("bert"):
             acc, acc5 = float(np.exp(test_loss)), 0.0
         else:

@@ -177,7 +177,8 @@ def test_evaluate_checkpoints(tmp_path):
     for e in (1, 2):
         t.train_epoch = e
         t.save_checkpoint(t.checkpoint_state(), os.path.join(d, "fcn5net-rank0-epoch%d.pth" % e))
-    best, ep, res = evaluate("fcn5net", "mnist", d, 3, batch_size=16, device="cpu", num_batches=1)
+    best, ep, res = evaluate(d, "fcn5net", "mnist", data_dir=None, nepochs=3, batch_size=16, device="cpu",
+                             num_batches=1)
     assert set(res) == {1, 2} and ep in (1, 2)
 
 
