@@ -522,7 +522,7 @@ def compress_(g: torch.Tensor, r: torch.Tensor, bufs: CompressBuffers, mode: int
               zero_g: bool = True, loops: int = 3, z: float = 0.0, k: int = 1, k_cap: Optional[int] = None,
               seed: int = 0, fixed_thr: float = 0.0, sample_p: float = 0.01, n_stats: int = 0,
               valid: Optional[torch.Tensor] = None, mc: Optional[dict] = None,
-              seed_dev: Optional[torch.Tensor] = None) -> None:
+              seed_dev: Optional[torch.Tensor] = None, handoff: int = -1) -> None:
     """Sparsify ``g`` (+ residual ``r``) into ``bufs.record``.  Async on GPU.
 
     ``seed_dev``: optional int32 device word holding the seed (read by the
@@ -557,7 +557,7 @@ def compress_(g: torch.Tensor, r: torch.Tensor, bufs: CompressBuffers, mode: int
                       mc_wd=[float(p.get("weight_decay", 0.0)) for p in mc["groups"]])
         _ops().compress(g, r, bufs.ctrl, bufs.ws, bufs.record, int(mode), bool(ec), bool(zero_g), int(loops),
                         float(z), float(fixed_thr), float(sample_p), int(k), int(k_cap), int(seed) & 0xFFFFFFFF,
-                        int(n_stats), bufs.stats, **kw)
+                        int(n_stats), bufs.stats, handoff=int(handoff), **kw)
     else:
         if seed_dev is not None:
             seed = int(seed_dev.view(-1)[0]) & 0xFFFFFFFF

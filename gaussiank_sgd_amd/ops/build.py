@@ -62,6 +62,7 @@ HIP_SOURCES = [
     "kernels/xent.hip",
     "kernels/winograd.hip",
     "kernels/stem_f32.hip",
+    "kernels/prep.hip",
 ]
 CXX_SOURCES = [
     "comm/rccl_engine.cpp",

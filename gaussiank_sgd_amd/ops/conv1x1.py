@@ -37,6 +37,7 @@ import torch.nn.functional as F
 
 from . import load
 from . import streams
+from . import weight_prep
 
 _CL = torch.channels_last
 _TUNE = os.environ.get("GKSGD_GEMM_TUNE", "1") != "0"
@@ -252,14 +253,16 @@ def _wino_shape_fits(N: int, H: int, W: int, C: int, K: int) -> bool:
     return N * H * W * max(C, K) * 4 < (1 << 31) and N * ((H + 1) // 2) * ((W + 1) // 2) < (1 << 31)
 
 
-def _wino_cands(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, flip: bool, st=None, bn=()) -> list:
-    """Winograd candidates: filter transform (per call: the weights change
-    every step) + wino_conv; ``bn`` = (h, dy2, mask) of the BN-backward epilogue."""
+def _wino_cands(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, flip: bool, st=None, bn=(),
+                wp: bool = False) -> list:
+    """Winograd candidates: filter transform (the weights change every step:
+    rebuilt once per step for the whole model by ops/weight_prep.py when ``wp``,
+    the weight being persistent storage) + wino_conv; ``bn`` = (h, dy2, mask)
+    of the BN-backward epilogue."""
     g = _g()
-    u = torch.empty(16 * w.shape[0] * w.shape[1], dtype=torch.float32, device=x.device)
 
     def run(mb, sp=1):
-        g.wino_weights(w, u, flip)
+        u = weight_prep.wino_filter(w, flip, wp)
         return g.wino_conv(x, u, out, mb, st, *bn, splits=sp)
     cands = [(("wino", 0, mb), (lambda mb=mb: run(mb))) for mb in _WINO_GRIDS]
     # small batches: fewer (64-tile x 64-channel) blocks than CUs -> also offer
@@ -279,7 +282,7 @@ def _forced(cands: list) -> list:
     return cands
 
 
-def _fwd(x: torch.Tensor, w: torch.Tensor, s: int, stats_box=None, bias=None) -> torch.Tensor:
+def _fwd(x: torch.Tensor, w: torch.Tensor, s: int, stats_box=None, bias=None, wp: bool = False) -> torch.Tensor:
     """y = conv(x, w).  With ``stats_box`` (a list) and the HIP kernel chosen,
     the kernel's epilogue also reduces the BatchNorm batch statistics of y
     and ``(partials [2, rows_max, K], rows)`` is appended to the box
@@ -306,7 +309,7 @@ def _fwd(x: torch.Tensor, w: torch.Tensor, s: int, stats_box=None, bias=None) ->
     cands += [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in split for mb in _SPLITK_GRIDS]
     wino = bias is None and _wino_ok(dt, k, s, C, K) and _wino_shape_fits(N, H, W, C, K)
     if wino:
-        cands += _wino_cands(x, w, y, False, st)
+        cands += _wino_cands(x, w, y, False, st, wp=wp)
 
     def miopen():
         out = F.conv2d(x, w, b16, stride=s, padding=p)
@@ -340,7 +343,7 @@ def _lz_kw(lz, rows: bool = False) -> dict:
     return dict(lz_x=_rows(x) if rows else x, lz_coef=coef, lz_padz=padz, lz_padx=padx)
 
 
-def _dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, lz=None, plink=None) -> torch.Tensor:
+def _dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, lz=None, plink=None, wp: bool = False) -> torch.Tensor:
     """Grad-input.  ``lz``: dy is the dz of a lazy BN backward (the kernels
     compute dx from dz and the BN input themselves); the "mat" candidate
     materialises dx (``plink.materialize()``) and runs the plain path."""
@@ -366,27 +369,27 @@ def _dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, lz=None, plink=No
         dx = xs
         if k == 1:
             DY, DX = _rows(dy), _rows(dx)
-            Wt = _lazy(lambda: w.reshape(K, C).t().contiguous())
+            Wt = _lazy(lambda: weight_prep.transposed_1x1(w, wp))
             run = lambda c, mb: g.gemm_nt(DY, Wt(), DX, c, mb, **kw)  # noqa: E731
             if lz is None:
                 split = _splitk_cfgs(dt, N * H * W, C, K)
         else:
             # dX = conv(dY, W') with W'[c][kh][kw][k] = W[k][KH-1-kh][KW-1-kw][c]
-            wf = _lazy(lambda: w.flip(2, 3).transpose(0, 1).contiguous(memory_format=_CL))
+            wf = _lazy(lambda: weight_prep.flipped_3x3(w, wp))
             z = _zero(dy.device)
             run = lambda c, mb: g.conv_nt(dy, wf(), dx, z, 1, p, c, mb, **kw)  # noqa: E731
         cands = [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in _nt_cfgs(dt) for mb in _NT_GRIDS]
         cands += [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in split for mb in _SPLITK_GRIDS]
     if lz is not None:
-        cands.append((("mat", 0, 0), lambda: _dgrad(plink.materialize(), w, x_shape, s)))
+        cands.append((("mat", 0, 0), lambda: _dgrad(plink.materialize(), w, x_shape, s, wp=wp)))
         ch = _pick(("dgrad", N, C, H, W, K, k, s) + _dkey(dt) + ("lz",), cands)
         if ch[0] == "mat":
-            return _dgrad(plink.materialize(), w, x_shape, s)
+            return _dgrad(plink.materialize(), w, x_shape, s, wp=wp)
         run(ch[1], ch[2])
         return dx
     wino = _wino_ok(dt, k, s, K, C) and _wino_shape_fits(N, H, W, C, K)
     if wino:
-        cands += _wino_cands(dy, w, dx, True)
+        cands += _wino_cands(dy, w, dx, True, wp=wp)
     cands.append((("miopen", 0, 0), miopen))
     ch = _pick(_dgrad_key(N, C, H, W, K, k, s, dt), _forced(cands))
     if ch[0] == "miopen":
@@ -415,7 +418,8 @@ def _dgrad_key(N, C, H, W, K, k, s, dt) -> tuple:
     return ("dgrad", N, C, H, W, K, k, s) + _dkey(dt) + (("wino",) if wino else ())
 
 
-def _dgrad_bn(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, link, lz=None, plink=None) -> torch.Tensor:
+def _dgrad_bn(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, link, lz=None, plink=None,
+              wp: bool = False) -> torch.Tensor:
     """Grad-input with the producing BatchNorm's backward reduction fused into
     the epilogue (gemm.hip BnBwd; ops/bn.py BnLink): returns dz = ReLU-masked
     (dX + dy2) and leaves the partials in ``link.part``.  Stride 1 only; the
@@ -431,14 +435,14 @@ def _dgrad_bn(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, link, lz=None,
     h, mask, dy2 = link.h, link.mask, link.dy2
     if k == 1:
         DY, DZ = _rows(dy), _rows(dz)
-        Wt = _lazy(lambda: w.reshape(K, C).t().contiguous())
+        Wt = _lazy(lambda: weight_prep.transposed_1x1(w, wp))
         H2 = _rows(h)
         D2 = _rows(dy2) if dy2 is not None else None
         run = lambda c, mb: g.gemm_nt(DY, Wt(), DZ, c, mb, st, None, H2, D2, mask, **kw)  # noqa: E731
         split = _splitk_cfgs(dt, M, C, K) if lz is None else []
     else:
         split = []
-        wf = _lazy(lambda: w.flip(2, 3).transpose(0, 1).contiguous(memory_format=_CL))
+        wf = _lazy(lambda: weight_prep.flipped_3x3(w, wp))
         z = _zero(dy.device)
         run = lambda c, mb: g.conv_nt(dy, wf(), dz, z, 1, p, c, mb, st, None, h, dy2, mask, **kw)  # noqa: E731
     # 64x64-per-wave tiles (cfg digit 1-4) and the fp32 32x64 family (cfg >= 1000) carry the
@@ -448,13 +452,13 @@ def _dgrad_bn(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, link, lz=None,
     cands += [(("hip", c, mb), (lambda c=c, mb=mb: run(c, mb))) for c in split for mb in _SPLITK_GRIDS]
     key = ("dgrad_bn", N, C, H, W, K, k, s, dy2 is not None) + _dkey(dt)
     if lz is not None:
-        cands.append((("mat", 0, 0), lambda: _dgrad_bn(plink.materialize(), w, x_shape, s, link)))
+        cands.append((("mat", 0, 0), lambda: _dgrad_bn(plink.materialize(), w, x_shape, s, link, wp=wp)))
         ch = _pick(key + ("lz",), cands)
         if ch[0] == "mat":
-            return _dgrad_bn(plink.materialize(), w, x_shape, s, link)
+            return _dgrad_bn(plink.materialize(), w, x_shape, s, link, wp=wp)
     else:
         if _wino_ok(dt, k, s, K, C) and _wino_shape_fits(N, H, W, C, K):
-            cands += _wino_cands(dy, w, dz, True, st, (h, dy2, mask))
+            cands += _wino_cands(dy, w, dz, True, st, (h, dy2, mask), wp=wp)
             key = key + ("wino",)
         ch = _pick(key, _forced(cands))
     if ch[0] == "wino":
@@ -573,8 +577,12 @@ class _FastConvFn(torch.autograd.Function):
         else:
             w = param.detach()
         w = w.contiguous(memory_format=_CL)
+        # persistent weight storage (the parameter or its bf16 shadow view): its
+        # per-step re-layouts are batched by ops/weight_prep.py
+        wp = w.data_ptr() == param.data_ptr() or (w_bf16 is not None and w.data_ptr() == w_bf16.data_ptr())
         b = bias.detach().float().contiguous() if bias is not None else None
-        y = _fwd(x, w, stride, stats_box, b)
+        y = _fwd(x, w, stride, stats_box, b, wp=wp)
+        ctx.wp = wp
         ctx.sink = sink
         ctx.bias_sink = bias_sink
         ctx.has_bias = bias is not None
@@ -622,9 +630,9 @@ class _FastConvFn(torch.autograd.Function):
             N, C, H, W = x.shape
             key = _dgrad_key(N, C, H, W, w.shape[0], w.shape[2], s, ctx.dt)
             if _bn_fusable(link, s, key):
-                dx = _dgrad_bn(dy, w, x.shape, s, link, lz, plink)
+                dx = _dgrad_bn(dy, w, x.shape, s, link, lz, plink, wp=ctx.wp)
             else:
-                dx = _dgrad(dy, w, x.shape, s, lz, plink)
+                dx = _dgrad(dy, w, x.shape, s, lz, plink, wp=ctx.wp)
         gparam = None
         if ctx.needs_input_grad[1] and not wgrad_done:
             if direct:

@@ -41,7 +41,7 @@ void compress(at::Tensor g, at::Tensor r, at::Tensor ctrl, at::Tensor ws, at::Te
               int64_t seed, int64_t n_stats, c10::optional<at::Tensor> stats_out, c10::optional<at::Tensor> valid,
               c10::optional<at::Tensor> u, c10::optional<at::Tensor> w, c10::optional<at::Tensor> chunks,
               int64_t chunk_begin, int64_t chunk_count, int64_t chunk_base, std::vector<double> mc_mu,
-              std::vector<double> mc_wd, c10::optional<at::Tensor> seed_dev) {
+              std::vector<double> mc_wd, c10::optional<at::Tensor> seed_dev, int64_t handoff) {
   check_f32(g, "g");
   check_f32(r, "r");
   check_dev(ctrl, "ctrl");
@@ -120,6 +120,7 @@ void compress(at::Tensor g, at::Tensor r, at::Tensor ctrl, at::Tensor ws, at::Te
       a.mc_wd[i] = (float)mc_wd[i];
     }
   }
+  a.handoff = (int)handoff;
   gk::compress(a, cur_stream(g));
 }
 
@@ -1147,6 +1148,23 @@ int64_t conv_nt(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor zero, int64
 // [K, C, 3, 3] channels-last fp32; flip = false: u = transform of w for the
 // forward (Ci = C, Co = K); flip = true: of the grad-input filter (Ci = K,
 // Co = C).  u: contiguous fp32 with 16 * K * C elements.
+// ---------------------------------------------------------------------------
+// batched per-step weight re-layouts (prep.hip; table packed by ops/weight_prep.py)
+// ---------------------------------------------------------------------------
+int64_t weight_prep_blocks(int64_t kind, int64_t R, int64_t S) { return gk::weight_prep_blocks((int)kind, (int)R, (int)S); }
+
+void weight_prep(at::Tensor table, int64_t ndesc, int64_t total_blocks) {
+  TORCH_CHECK(table.is_cuda() && table.scalar_type() == at::kByte && table.is_contiguous() &&
+                  table.numel() == ndesc * (int64_t)sizeof(gk::PrepDesc),
+              "weight_prep: table must be a contiguous GPU uint8 tensor of ndesc descriptors");
+  TORCH_CHECK(ndesc > 0 && ndesc <= gk::weight_prep_max_descs(), "weight_prep: 1..", gk::weight_prep_max_descs(),
+              " descriptors");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(table.data_ptr()) % 8 == 0, "weight_prep: table must be 8-byte aligned");
+  c10::DeviceGuard guard(table.device());
+  gk::weight_prep(reinterpret_cast<const gk::PrepDesc*>(table.data_ptr()), (int)ndesc, total_blocks,
+                  cur_stream(table));
+}
+
 void wino_weights(at::Tensor w, at::Tensor u, bool flip) {
   TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3 &&
                   w.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -1758,7 +1776,7 @@ TORCH_LIBRARY(gksgd, m) {
       "bool zero_g, int loops, float z, float fixed_thr, float sample_p, int k, int k_cap, int seed, "
       "int n_stats, Tensor(f!)? stats_out=None, Tensor? valid=None, Tensor(g!)? u=None, Tensor? w=None, "
       "Tensor? chunks=None, int chunk_begin=0, int chunk_count=0, int chunk_base=0, float[] mc_mu=[], "
-      "float[] mc_wd=[], Tensor? seed_dev=None) -> ()");
+      "float[] mc_wd=[], Tensor? seed_dev=None, int handoff=-1) -> ()");
   m.def("apply_records_sgd(Tensor(a!) w, Tensor(b!)? w_bf16, Tensor records, int P, int k_cap, float scale, float lr, "
         "Tensor? lr_mult=None) -> ()");
   m.def("arena_digest(Tensor x, Tensor(a!) out, Tensor(b!) ws) -> ()");
@@ -1828,6 +1846,8 @@ TORCH_LIBRARY(gksgd, m) {
   m.def("wgrad3_ws(int N, int H, int W, int C, int K) -> int", &wgrad3_ws);
   m.def("conv3_wgrad(Tensor dy, Tensor x, Tensor(a!) out, Tensor(b!) part, Tensor zero) -> ()");
   m.def("wino_weights(Tensor w, Tensor(a!) u, bool flip) -> ()");
+  m.def("weight_prep(Tensor table, int ndesc, int total_blocks) -> ()");
+  m.def("weight_prep_blocks(int kind, int R, int S) -> int", &weight_prep_blocks);
   m.def("wino_wgrad_ws(int N, int H, int W, int C, int K, int splits=0) -> int", &wino_wgrad_ws);
   m.def("wino_wgrad(Tensor x, Tensor dy, Tensor(a!) out, Tensor(b!) part, int splits=0) -> ()");
   m.def("wino_conv(Tensor x, Tensor u, Tensor(a!) y, int max_blocks=0, Tensor(b!)? stats=None, Tensor? bn_h=None, "
@@ -1949,6 +1969,7 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("gemm_tn_acc", &gemm_tn_acc);
   m.impl("conv_nt", &conv_nt);
   m.impl("wino_weights", &wino_weights);
+  m.impl("weight_prep", &weight_prep);
   m.impl("wino_conv", &wino_conv);
   m.impl("wino_wgrad", &wino_wgrad);
   m.impl("conv_tn_acc", &conv_tn_acc);

@@ -1418,17 +1418,19 @@ int count_cands(const CompressArgs& a, int cond) { return cond ? kFallbackCands 
 // launch costs ~5 us.  Default: launches (GKSGD_HANDOFF=lastblock restores
 // the in-grid hand-off).  The conditional fallback chain keeps the in-grid
 // form: it must cost nothing extra when it does not fire.
-bool handoff_by_launch() {
+bool handoff_by_launch_env() {
   const char* e = getenv("GKSGD_HANDOFF");
   return !(e != nullptr && strcmp(e, "lastblock") == 0);
 }
+
+bool handoff_by_launch(const CompressArgs& a) { return a.handoff < 0 ? handoff_by_launch_env() : a.handoff == 0; }
 
 template <int KEYKIND>
 void launch_count(const CompressArgs& a, const Ws& w, bool vec, int G, int64_t chunk_tiles, GkCtrl* ctrl, int cond,
                   hipStream_t s) {
   const int nc = count_cands(a, cond);
   DecArgs da;
-  da.in_kernel = (cond || !handoff_by_launch()) ? 1 : 0;
+  da.in_kernel = (cond || !handoff_by_launch(a)) ? 1 : 0;
   da.ctrl = ctrl; da.mode = a.mode; da.loops = a.loops; da.k = a.k; da.k_cap = a.k_cap;
   da.offsets = w.offsets; da.eqtake = w.eqtake; da.blocksel = w.blocksel; da.hdr = a.record;
   da.hist_reset = w.hist; da.counter = w.sync + (cond ? 3 : 1);
@@ -1523,7 +1525,7 @@ void compress(const CompressArgs& a, hipStream_t s) {
   //    correction when a chunk table is given); threshold modes finalize in
   //    the last stats block (radix modes need the histograms first)
   const bool radix_mode = a.mode == kModeTopK || a.mode == kModeRandomK || a.mode == kModeDGC;
-  const bool fin_in = !radix_mode && !handoff_by_launch();   // finalize in the stats pass's last block
+  const bool fin_in = !radix_mode && !handoff_by_launch(a);   // finalize in the stats pass's last block
   const int64_t keff = a.k < a.n ? a.k : a.n;
   const int64_t n_stats = a.n_stats > 0 ? a.n_stats : a.n;
   FinArgs fa;

@@ -109,6 +109,12 @@ struct CompressArgs {
   int64_t chunk_base = 0;
   float mc_mu[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   float mc_wd[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // single-workgroup hand-offs (finalize / decide): -1 = GKSGD_HANDOFF
+  // (default: separate 1-workgroup launches), 0 = launches, 1 = in the last
+  // block of the producing grid (no new dispatch: the bucket compressions
+  // that overlap the backward pass, where a 1-workgroup launch waits behind
+  // the GEMM blocks filling the chip)
+  int handoff = -1;
 };
 
 size_t compress_workspace_bytes(int64_t n);
@@ -378,6 +384,24 @@ int stem_f32_forward(const float* x, int N, int H, int W, const float* w, int64_
 void stem_f32_wgrad(const float* x, const float* dy, int N, int H, int W, float* part, float* out, int64_t s0,
                     int64_t s1, int64_t s2, int64_t s3, hipStream_t stream);
 void wino_weights(const float* w, float* u, int Co, int Ci, int flip, hipStream_t stream);
+// Batched per-step weight re-layouts (prep.hip): one launch over a table of
+// descriptors (device memory, block_begin ascending).  kind kPrepWino /
+// kPrepWinoFlip: Winograd filter transform (R = Co, S = Ci of the conv run,
+// as wino_weights); kPrepT32 / kPrepT16: out[s * ld_out + r] = in[r * ld_in + s]
+// for an R x S matrix of 4- / 2-byte elements (64 x 64 LDS tiles, tiles_s =
+// ceil(S / 64)).
+enum PrepKind : int32_t { kPrepWino = 0, kPrepWinoFlip = 1, kPrepT32 = 2, kPrepT16 = 3 };
+struct PrepDesc {
+  const void* src;
+  void* dst;
+  int64_t ld_in, ld_out;
+  int64_t block_begin;
+  int32_t kind, R, S, tiles_s;
+};
+static_assert(sizeof(PrepDesc) == 56, "PrepDesc layout is packed by ops/weight_prep.py");
+int64_t weight_prep_blocks(int kind, int R, int S);
+int weight_prep_max_descs();
+void weight_prep(const PrepDesc* descs, int ndesc, int64_t total_blocks, hipStream_t stream);
 int wino_conv(const float* x, const float* u, float* y, int N, int H, int W, int Ci, int Co, int max_blocks,
               float* stats, int stats_rows, const BnBwdArgs* bn, hipStream_t stream, int splits = 1,
               float* split_ws = nullptr);

@@ -53,6 +53,10 @@ from .comm import (allgather, allgather_async, allreduce, allreduce_, allreduce_
 from .planner import models_for, plan_mgs, plan_mgwfbp
 
 DEFAULT_DYNAMIC_DENSITIES = [0.015625, 0.004, 0.001]
+# compress hand-off mode of the buckets that overlap the backward pass
+# (ops.compress_ handoff: 1 = in-grid last block, 0 = separate launches,
+# -1 = GKSGD_HANDOFF); GKSGD_OVERLAP_HANDOFF=launch restores launches
+_OVERLAP_HANDOFF = {"lastblock": 1, "launch": 0, "env": -1}.get(os.environ.get("GKSGD_OVERLAP_HANDOFF", "lastblock"), 1)
 
 
 def _env_flag(name: str, default: bool) -> bool:
@@ -465,6 +469,13 @@ class _DistributedOptimizer(torch.optim.Optimizer):
     # ------------------------------------------------------------------
     def _launch_bucket(self, b):
         b.launched = True
+        # a bucket compressed while the backward still runs (another bucket is
+        # not launched yet) hands its single-workgroup steps over inside the
+        # producing grids: a separate 1-workgroup launch on the comm stream
+        # waits behind the backward GEMM blocks that fill the chip (BERT fp32:
+        # decide 104 us per call overlapped vs 12 us alone,
+        # profiles/r04_bert_fp32_kernel_stats.csv)
+        b.extra["overlapped"] = self._overlap and any(not o.launched for o in self._arena.buckets)
         with trace.range("gk/b%d/launch" % b.index):
             if self._comm_stream is not None:
                 cur = torch.cuda.current_stream(self._device)
@@ -547,7 +558,8 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         with trace.range("gk/b%d/compress" % b.index):
             ops.compress_(g, r, b.bufs, comp.mode, ec=comp.ec, zero_g=True, loops=comp.loops,
                           z=comp.z_for(density), k=k, k_cap=k_cap, seed=seed, sample_p=getattr(comp, "sample_p", 0.01),
-                          n_stats=b.numel, valid=b.extra.get("valid"), mc=mc, seed_dev=seed_dev)
+                          n_stats=b.numel, valid=b.extra.get("valid"), mc=mc, seed_dev=seed_dev,
+                          handoff=_OVERLAP_HANDOFF if b.extra.get("overlapped") else -1)
         rec_words = ops.REC_HDR + 2 * k_cap
         return b.bufs.record[:rec_words], k_cap
 
@@ -588,6 +600,7 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         collective launch instead of len(bs)."""
         for b in bs:
             b.launched = True
+            b.extra["overlapped"] = False
         cur = torch.cuda.current_stream(self._device) if self._comm_stream is not None else None
         ctx = torch.cuda.stream(self._comm_stream) if self._comm_stream is not None else contextlib.nullcontext()
         if cur is not None:
@@ -751,6 +764,7 @@ class _DistributedOptimizer(torch.optim.Optimizer):
                     b.extra["agg_done"] = True
                 b.ready = 0
                 b.launched = False
+                b.extra["overlapped"] = False
             if any_ready:
                 self.train_iter += 1
             self._flush_dumps()

@@ -183,6 +183,10 @@ class DLTrainer:
         self._acc_acc = None
         self._acc_n = 0
         self.display = 40
+        # per-step weight re-layouts of the convolutions, rebuilt in one batched
+        # launch at the start of every step (ops/weight_prep.py)
+        from ..ops.weight_prep import WeightPrep
+        self.weight_prep = WeightPrep()
         logger.info("num_batches_per_epoch: %d" % self.num_batches_per_epoch)
 
     # ------------------------------------------------------------------
@@ -368,14 +372,15 @@ class DLTrainer:
                 inputs = inputs.to(self.device, non_blocking=True)
                 labels = labels.to(self.device, non_blocking=True) if torch.is_tensor(labels) else labels
             self.iotime += time.time() - ss
-            sf = time.time()
-            with trace.range("gk/forward"):
-                outputs, loss, hidden = self.forward_loss(inputs, labels, hidden)
-            self.forwardtime += time.time() - sf
-            sb = time.time()
-            with trace.range("gk/backward"):
-                loss.backward()
-            self.backwardtime += time.time() - sb
+            with self.weight_prep.step(self.device):
+                sf = time.time()
+                with trace.range("gk/forward"):
+                    outputs, loss, hidden = self.forward_loss(inputs, labels, hidden)
+                self.forwardtime += time.time() - sf
+                sb = time.time()
+                with trace.range("gk/backward"):
+                    loss.backward()
+                self.backwardtime += time.time() - sb
             ld = loss.detach()
             loss_sum = ld if loss_sum is None else loss_sum + ld
             self._epoch_loss_acc = ld.clone() if self._epoch_loss_acc is None else self._epoch_loss_acc + ld
@@ -422,30 +427,31 @@ class DLTrainer:
         top1, top5, losses = [], [], []
         costs, steps = 0.0, 0
         wer_sum, utterances = 0.0, 0
-        for inputs, labels in self._eval_batches(num_batches):
-            if self.dnn == "lstman4":
-                targets, tgt_lens, in_lens = labels
-                with self._autocast():
-                    outputs, out_lens = self.net(inputs, in_lens)
-                hyps = ctc_greedy_decode(outputs.float(), out_lens)
-                refs = split_targets(targets, tgt_lens)
-                for h, r in zip(hyps, refs):
-                    ref_s = AN4_LABELS_STR(r)
-                    wer_sum += word_errors(AN4_LABELS_STR(h), ref_s) / float(max(1, len(ref_s.split())))
-                utterances += len(refs)
-                logp = outputs.float().log_softmax(-1).transpose(0, 1)
-                losses.append(float(self.criterion(logp, targets, out_lens, tgt_lens) / inputs.size(0)))
-                continue
-            outputs, loss, _ = self.forward_loss(inputs, labels, None)
-            losses.append(float(loss))
-            if self.dnn == "lstm":
-                costs += float(loss) * self.num_steps
-                steps += self.num_steps
-            elif not self.dnn.startswith("bert"):
-                k5 = min(5, outputs.shape[1])
-                a1, a5 = self.cal_accuracy(outputs.float(), labels, topk=(1, k5))
-                top1.append(float(a1))
-                top5.append(float(a5))
+        with self.weight_prep.step(self.device):
+            for inputs, labels in self._eval_batches(num_batches):
+                if self.dnn == "lstman4":
+                    targets, tgt_lens, in_lens = labels
+                    with self._autocast():
+                        outputs, out_lens = self.net(inputs, in_lens)
+                    hyps = ctc_greedy_decode(outputs.float(), out_lens)
+                    refs = split_targets(targets, tgt_lens)
+                    for h, r in zip(hyps, refs):
+                        ref_s = AN4_LABELS_STR(r)
+                        wer_sum += word_errors(AN4_LABELS_STR(h), ref_s) / float(max(1, len(ref_s.split())))
+                    utterances += len(refs)
+                    logp = outputs.float().log_softmax(-1).transpose(0, 1)
+                    losses.append(float(self.criterion(logp, targets, out_lens, tgt_lens) / inputs.size(0)))
+                    continue
+                outputs, loss, _ = self.forward_loss(inputs, labels, None)
+                losses.append(float(loss))
+                if self.dnn == "lstm":
+                    costs += float(loss) * self.num_steps
+                    steps += self.num_steps
+                elif not self.dnn.startswith("bert"):
+                    k5 = min(5, outputs.shape[1])
+                    a1, a5 = self.cal_accuracy(outputs.float(), labels, topk=(1, k5))
+                    top1.append(float(a1))
+                    top5.append(float(a5))
         test_loss = float(np.mean(losses)) if losses else 0.0
         if self.dnn == "lstm":
             acc, acc5 = float(np.exp(costs / max(1, steps))), 0.0
