@@ -12,6 +12,7 @@ semantics, so models built with it run anywhere.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -21,6 +22,7 @@ import torch.nn.functional as F
 from . import load, require_native
 
 _CL = torch.channels_last
+_FIN_FUSE = os.environ.get("GKSGD_BN_FIN_FUSE", "1") != "0"
 
 
 def _ops():
@@ -127,7 +129,7 @@ def _lazy_ok(x: torch.Tensor, plink) -> bool:
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, relu, direct=None,
-                nbt=None, twin=False, pre=None, link=None, res_link=None, plink=None):
+                nbt=None, twin=False, pre=None, link=None, res_link=None, plink=None, fin=None):
         # direct = (gw_view, gb_view): weight/bias gradients are accumulated
         # straight into the optimizer's fp32 arena by the backward kernel and
         # None is returned for them, so AccumulateGrad launches nothing (its
@@ -153,7 +155,9 @@ class _BNActFn(torch.autograd.Function):
         # the producing convolution's epilogue (ops/conv1x1.py) -- no stats pass
         pre_t, pre_rows = pre if pre is not None else (None, 0)
         _ops().bn_act_forward(x, residual, y, mask, weight, bias, running_mean, running_var, stats[0], stats[1],
-                              stats[2], stats[3], ws, float(eps), float(momentum), bool(relu), nbt, pre_t, pre_rows)
+                              stats[2], stats[3], ws, float(eps), float(momentum), bool(relu), nbt, pre_t, pre_rows,
+                              fin)
+        ctx.fin = fin
         ctx.relu = bool(relu)
         ctx.has_res = residual is not None
         ctx.save_for_backward(x, mask, weight, stats[0], stats[1])
@@ -191,20 +195,20 @@ class _BNActFn(torch.autograd.Function):
                 dx = dz
             else:
                 dx = torch.empty_like(x, memory_format=_CL)
-                _ops().bn_act_backward_pre(dz, x, dx, weight, mean, invstd, g[0], g[1], part, rows, gw, gb)
+                _ops().bn_act_backward_pre(dz, x, dx, weight, mean, invstd, g[0], g[1], part, rows, gw, gb, ctx.fin)
             dres = dz if ctx.has_res and ctx.needs_input_grad[1] else None
             if res_link is not None and dres is not None:
                 res_link.dy2 = dres
             if ctx.direct is not None:
-                return (dx, dres) + (None,) * 14
+                return (dx, dres) + (None,) * 15
             dgamma = g[0] if weight is not None and ctx.needs_input_grad[2] else None
             dbeta = g[1] if ctx.needs_input_grad[3] else None
-            return (dx, dres, dgamma, dbeta) + (None,) * 12
+            return (dx, dres, dgamma, dbeta) + (None,) * 13
         if link is not None:
             link.clear()
         dy, dy2 = _grad_pair(grads, x)
         if dy is None:
-            return (None,) * 16
+            return (None,) * 17
         C = x.shape[1]
         M = x.numel() // C
         g = torch.empty(2, C, dtype=torch.float32, device=x.device)
@@ -223,14 +227,14 @@ class _BNActFn(torch.autograd.Function):
             dx = torch.empty_like(x, memory_format=_CL)
             dres = torch.empty_like(x, memory_format=_CL) if ctx.has_res and ctx.needs_input_grad[1] else None
             _ops().bn_act_backward(dy, mask, x, dx, dres, weight, mean, invstd, g[0], g[1], ws, ctx.relu, gw, gb,
-                                   dy2)
+                                   dy2, ctx.fin)
         if res_link is not None and dres is not None:
             res_link.dy2 = dres
         if ctx.direct is not None:
-            return (dx, dres) + (None,) * 14
+            return (dx, dres) + (None,) * 15
         dgamma = g[0] if weight is not None and ctx.needs_input_grad[2] else None
         dbeta = g[1] if ctx.needs_input_grad[3] else None
-        return (dx, dres, dgamma, dbeta) + (None,) * 12
+        return (dx, dres, dgamma, dbeta) + (None,) * 13
 
 
 class _BNReLUPoolFn(torch.autograd.Function):
@@ -353,7 +357,8 @@ class BNAct(nn.BatchNorm2d):
             res_link = getattr(residual, "_gk_res_link", None) if residual is not None else None
             plink = getattr(x, "_gk_plink", None) if torch.is_grad_enabled() else None
             out = _BNActFn.apply(x, residual, self.weight, self.bias, self.running_mean, self.running_var, mom,
-                                 self.eps, relu, direct, nbt, self.twin, stats, link, res_link, plink)
+                                 self.eps, relu, direct, nbt, self.twin, stats, link, res_link, plink,
+                                 self._fin_state(x))
             if link is not None:
                 main = out[0] if self.twin else out
                 main._gk_bn_link = link
@@ -368,6 +373,20 @@ class BNAct(nn.BatchNorm2d):
         if pool is not None:
             out = F.max_pool2d(out, pool[0], pool[1], pool[2])
         return (out, out) if self.twin else out
+
+    def _fin_state(self, x: torch.Tensor) -> Optional[torch.Tensor]:
+        """Per-layer state of the in-launch finalize (bn_act.hip FinSync: a
+        ticket counter and one flag per 16-channel group, zeroed ONCE): the
+        statistics finalize runs inside the apply pass instead of as its own
+        launch (2 launches per BN and step fewer; GKSGD_BN_FIN_FUSE=0 off)."""
+        if not _FIN_FUSE:
+            return None
+        st = getattr(self, "_gk_fin", None)
+        if st is None or st.device != x.device:
+            n = int(_ops().bn_fin_state_bytes(self.num_features))
+            st = torch.zeros((n + 15) // 16 * 16, dtype=torch.uint8, device=x.device)
+            self._gk_fin = st
+        return st
 
     def extra_repr(self) -> str:
         return super().extra_repr() + ", act=%s" % self.act + (", pool=%s" % (self.pool,) if self.pool else "")

@@ -376,15 +376,29 @@ int64_t bn_mask_bytes(int64_t M, int64_t C, int64_t elem_bytes) {
   return (int64_t)gk::bn_mask_bytes(M, (int)C, (int)elem_bytes);
 }
 
+// per-layer in-launch finalize state (bn_act.hip FinSync): a zero-initialised
+// uint8 GPU tensor of at least bn_fin_state_bytes(C), kept by the layer
+void* fin_state(const c10::optional<at::Tensor>& fin, int64_t C) {
+  if (!fin.has_value() || !fin->defined()) return nullptr;
+  TORCH_CHECK(fin->is_cuda() && fin->is_contiguous() && fin->nbytes() >= gk::bn_fin_state_bytes((int)C) &&
+                  reinterpret_cast<uintptr_t>(fin->data_ptr()) % 16 == 0,
+              "fin: a contiguous, 16-byte aligned GPU tensor of bn_fin_state_bytes(C) bytes");
+  return fin->data_ptr();
+}
+
+int64_t bn_fin_state_bytes(int64_t C) { return (int64_t)gk::bn_fin_state_bytes((int)C); }
+
 void bn_act_forward(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, c10::optional<at::Tensor> mask,
                     c10::optional<at::Tensor> w,
                     c10::optional<at::Tensor> b, c10::optional<at::Tensor> run_mean,
                     c10::optional<at::Tensor> run_var, at::Tensor save_mean, at::Tensor save_invstd,
                     at::Tensor scale, at::Tensor shift, at::Tensor ws, double eps, double momentum, bool relu,
-                    c10::optional<at::Tensor> nbt, c10::optional<at::Tensor> pre, int64_t pre_rows) {
+                    c10::optional<at::Tensor> nbt, c10::optional<at::Tensor> pre, int64_t pre_rows,
+                    c10::optional<at::Tensor> fin) {
   check_cl(x, "x");
   check_cl(y, "y");
   const int64_t C = channels_of(x);
+  void* fs = fin_state(fin, C);
   const int64_t M = x.numel() / C;
   const int eb = x.element_size();
   TORCH_CHECK(gk::bn_supported((int)C, eb), "channel count not supported by the fused kernel");
@@ -417,24 +431,25 @@ void bn_act_forward(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, c
                            (int)pre_rows, opt_f32(w), opt_f32(b), (float)eps, (float)momentum, opt_f32_mut(run_mean),
                            opt_f32_mut(run_var), save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(),
                            scale.data_ptr<float>(), shift.data_ptr<float>(), relu ? 1 : 0, opt_i64(nbt),
-                           cur_stream(x));
+                           cur_stream(x), fs);
     return;
   }
   gk::bn_act_forward(x.data_ptr(), rp, y.data_ptr(), mp, M, (int)C, eb, opt_f32(w), opt_f32(b), (float)eps,
                      (float)momentum, opt_f32_mut(run_mean), opt_f32_mut(run_var), save_mean.data_ptr<float>(),
                      save_invstd.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(),
-                     ws.data_ptr<float>(), relu ? 1 : 0, opt_i64(nbt), cur_stream(x));
+                     ws.data_ptr<float>(), relu ? 1 : 0, opt_i64(nbt), cur_stream(x), fs);
 }
 
 void bn_act_backward(at::Tensor dy, c10::optional<at::Tensor> mask, at::Tensor x, at::Tensor dx,
                      c10::optional<at::Tensor> dres, c10::optional<at::Tensor> w, at::Tensor mean, at::Tensor invstd,
                      at::Tensor dgamma, at::Tensor dbeta, at::Tensor ws, bool relu,
                      c10::optional<at::Tensor> gw_acc, c10::optional<at::Tensor> gb_acc,
-                     c10::optional<at::Tensor> dy2) {
+                     c10::optional<at::Tensor> dy2, c10::optional<at::Tensor> fin) {
   check_cl(dy, "dy");
   check_cl(x, "x");
   check_cl(dx, "dx");
   const int64_t C = channels_of(x);
+  void* fs = fin_state(fin, C);
   const int64_t M = x.numel() / C;
   const int eb = x.element_size();
   TORCH_CHECK(dy.scalar_type() == x.scalar_type() && dx.scalar_type() == x.scalar_type(), "dtype mismatch");
@@ -457,16 +472,18 @@ void bn_act_backward(at::Tensor dy, c10::optional<at::Tensor> mask, at::Tensor x
   gk::bn_act_backward(dy.data_ptr(), d2, mp, x.data_ptr(), dx.data_ptr(), rp, M, (int)C, eb, opt_f32(w),
                       mean.data_ptr<float>(), invstd.data_ptr<float>(), dgamma.data_ptr<float>(),
                       dbeta.data_ptr<float>(), ws.data_ptr<float>(), relu ? 1 : 0, opt_f32_mut(gw_acc),
-                      opt_f32_mut(gb_acc), cur_stream(x));
+                      opt_f32_mut(gb_acc), cur_stream(x), fs);
 }
 
 void bn_act_backward_pre(at::Tensor dz, at::Tensor x, at::Tensor dx, c10::optional<at::Tensor> w, at::Tensor mean,
                          at::Tensor invstd, at::Tensor dgamma, at::Tensor dbeta, at::Tensor part, int64_t rows,
-                         c10::optional<at::Tensor> gw_acc, c10::optional<at::Tensor> gb_acc) {
+                         c10::optional<at::Tensor> gw_acc, c10::optional<at::Tensor> gb_acc,
+                         c10::optional<at::Tensor> fin) {
   check_cl(dz, "dz");
   check_cl(x, "x");
   check_cl(dx, "dx");
   const int64_t C = channels_of(x);
+  void* fs = fin_state(fin, C);
   const int64_t M = x.numel() / C;
   TORCH_CHECK((x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat) &&
                   dz.scalar_type() == x.scalar_type() && dx.scalar_type() == x.scalar_type() &&
@@ -483,7 +500,8 @@ void bn_act_backward_pre(at::Tensor dz, at::Tensor x, at::Tensor dx, c10::option
   const float* ps = part.data_ptr<float>();
   gk::bn_act_backward_pre(dz.data_ptr(), x.data_ptr(), dx.data_ptr(), M, (int)C, eb, opt_f32(w), mean.data_ptr<float>(),
                           invstd.data_ptr<float>(), dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), ps,
-                          ps + part.size(1) * C, (int)rows, opt_f32_mut(gw_acc), opt_f32_mut(gb_acc), cur_stream(x));
+                          ps + part.size(1) * C, (int)rows, opt_f32_mut(gw_acc), opt_f32_mut(gb_acc), cur_stream(x),
+                          fs);
 }
 
 // ---- lazy BN backward (bn_act.hip bn_bwd_finalize_lazy): no apply pass ----
@@ -1804,7 +1822,7 @@ TORCH_LIBRARY(gksgd, m) {
       "bn_act_forward(Tensor x, Tensor? res, Tensor(a!) y, Tensor(i!)? mask, Tensor? w, Tensor? b, Tensor(b!)? run_mean, "
       "Tensor(c!)? run_var, Tensor(d!) save_mean, Tensor(e!) save_invstd, Tensor(f!) scale, Tensor(g!) shift, "
       "Tensor(h!) ws, float eps, float momentum, bool relu, Tensor(j!)? nbt=None, Tensor? pre=None, "
-      "int pre_rows=0) -> ()");
+      "int pre_rows=0, Tensor(k!)? fin=None) -> ()");
   m.def(
       "bn_relu_pool_forward(Tensor x, Tensor(a!) y, Tensor(b!) amax, Tensor? w, Tensor? b, Tensor(c!)? run_mean, "
       "Tensor(d!)? run_var, Tensor(e!) save_mean, Tensor(f!) save_invstd, Tensor(g!) scale, Tensor(h!) shift, "
@@ -1817,7 +1835,7 @@ TORCH_LIBRARY(gksgd, m) {
   m.def(
       "bn_act_backward(Tensor dy, Tensor? mask, Tensor x, Tensor(a!) dx, Tensor(b!)? dres, Tensor? w, Tensor mean, "
       "Tensor invstd, Tensor(c!) dgamma, Tensor(d!) dbeta, Tensor(e!) ws, bool relu, Tensor(f!)? gw_acc=None, "
-      "Tensor(g!)? gb_acc=None, Tensor? dy2=None) -> ()");
+      "Tensor(g!)? gb_acc=None, Tensor? dy2=None, Tensor(h!)? fin=None) -> ()");
   m.def("accum_grad(Tensor(a!) dst, Tensor src) -> ()");
   m.def(
       "momentum_correct(Tensor(a!) u, Tensor(b!) g, Tensor w, Tensor chunks, int begin, int count, "
@@ -1864,7 +1882,8 @@ TORCH_LIBRARY(gksgd, m) {
   m.def("bn_stats_partials(Tensor x, Tensor(a!) ws) -> ()");
   m.def("bn_act_backward_pre(Tensor dz, Tensor x, Tensor(a!) dx, Tensor? w, Tensor mean, Tensor invstd, "
         "Tensor(b!) dgamma, Tensor(c!) dbeta, Tensor part, int rows, Tensor(d!)? gw_acc=None, "
-        "Tensor(e!)? gb_acc=None) -> ()");
+        "Tensor(e!)? gb_acc=None, Tensor(f!)? fin=None) -> ()");
+  m.def("bn_fin_state_bytes(int C) -> int", &bn_fin_state_bytes);
   m.def("attn_supported(int T, int D) -> bool",
         [](int64_t T, int64_t D) { return gk::attn_supported((int)T, (int)D); });
   m.def("attn_fwd(Tensor qkv, Tensor(a!) out, Tensor(b!) lse, int heads, float p, int seed, Tensor? seed_dev=None) -> ()");

@@ -20,11 +20,15 @@
 // accumulated in fp32 per thread and combined in fp64.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include "common.h"
 #include "gk_kernels.h"
 
 namespace gk {
 namespace {
+
+constexpr size_t kFinStateFlagsOffset = 16;   // per-layer state: [u64 ticket | pad | u32 flags[ngroups]]
 
 __device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 __device__ __forceinline__ uint16_t f32_to_bf16(float f);
@@ -216,11 +220,12 @@ constexpr int kFinC = 16;
 constexpr int kFinParts = kBlock / kFinC;
 
 __device__ __forceinline__ void reduce_partials2(const float* __restrict__ pa, const float* __restrict__ pb, int gy,
-                                                 int C, double* out_a, double* out_b, bool* owner, int* c_out) {
+                                                 int C, double* out_a, double* out_b, bool* owner, int* c_out,
+                                                 int grp) {
   __shared__ double sh[2][kFinParts][kFinC];
   const int cl = threadIdx.x % kFinC;
   const int part = threadIdx.x / kFinC;
-  const int c = blockIdx.x * kFinC + cl;
+  const int c = grp * kFinC + cl;
   double a = 0.0, b = 0.0;
   if (c < C) {
     int j = part;
@@ -259,6 +264,71 @@ __device__ __forceinline__ void reduce_partials2(const float* __restrict__ pa, c
   }
 }
 
+// Device-coherent (agent-scope, `sc1`) accesses of the in-launch finalize
+// hand-off below: they bypass the per-XCD L2s, so no L2 write-back /
+// invalidate fence is needed (MI355X_MICROARCH.md, inter-workgroup
+// visibility: all-`sc1` stores and loads, drained stores, one flag per
+// producing workgroup).
+template <typename T>
+__device__ __forceinline__ void st_dev(T* p, T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+template <typename T>
+__device__ __forceinline__ T ld_dev(const T* p) {
+  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// pipelined `sc1` loads (an agent-scope atomic load waits for each one)
+__device__ __forceinline__ float ld_coh_f32(const float* base, int idx) {
+  const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7fffffff, 0x00020000);
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, idx * 4, 0, 16 /* SC1 */));
+}
+template <bool COH>
+__device__ __forceinline__ void put(float* p, float v) {
+  if (COH) st_dev(p, v);
+  else *p = v;
+}
+
+struct FwdFin {   // forward finalize: partials -> mean, invstd, scale, shift, running stats
+  const float* psum;
+  const float* psq;
+  int gy;
+  const float* w;
+  const float* b;
+  float eps, momentum;
+  float* run_mean;
+  float* run_var;
+  float* save_mean;
+  float* save_invstd;
+  float* scale;
+  float* shift;
+  int64_t* nbt;
+};
+
+// channel group `grp` (kFinC channels) of the forward finalize; COH: the
+// outputs are read back inside the same launch (in-launch finalize)
+template <bool COH>
+__device__ __forceinline__ void fwd_fin_group(const FwdFin& f, int64_t M, int C, int grp) {
+  double s = 0.0, q = 0.0;
+  bool owner;
+  int c;
+  reduce_partials2(f.psum, f.psq, f.gy, C, &s, &q, &owner, &c, grp);
+  if (f.nbt && grp == 0 && threadIdx.x == 0) *f.nbt += 1;  // BatchNorm num_batches_tracked
+  if (!owner) return;
+  const double mean = s / (double)M;
+  double var = q / (double)M - mean * mean;
+  if (var < 0.0) var = 0.0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
+  const float gam = f.w ? f.w[c] : 1.f;
+  const float bet = f.b ? f.b[c] : 0.f;
+  f.save_mean[c] = (float)mean;
+  f.save_invstd[c] = invstd;
+  put<COH>(f.scale + c, gam * invstd);
+  put<COH>(f.shift + c, bet - (float)mean * gam * invstd);
+  if (f.run_mean) {
+    const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    f.run_mean[c] = (1.f - f.momentum) * f.run_mean[c] + f.momentum * (float)mean;
+    f.run_var[c] = (1.f - f.momentum) * f.run_var[c] + f.momentum * (float)unbiased;
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void bn_finalize_kernel(const float* __restrict__ psum,
                                                              const float* __restrict__ psq, int gy, int64_t M, int C,
                                                              const float* __restrict__ w, const float* __restrict__ b,
@@ -266,41 +336,74 @@ __global__ __launch_bounds__(kBlock) void bn_finalize_kernel(const float* __rest
                                                              float* __restrict__ run_var, float* __restrict__ save_mean,
                                                              float* __restrict__ save_invstd, float* __restrict__ scale,
                                                              float* __restrict__ shift, int64_t* __restrict__ nbt) {
-  double s = 0.0, q = 0.0;
-  bool owner;
-  int c;
-  reduce_partials2(psum, psq, gy, C, &s, &q, &owner, &c);
-  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;  // BatchNorm num_batches_tracked
-  if (!owner) return;
-  const double mean = s / (double)M;
-  double var = q / (double)M - mean * mean;
-  if (var < 0.0) var = 0.0;
-  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
-  const float gam = w ? w[c] : 1.f;
-  const float bet = b ? b[c] : 0.f;
-  save_mean[c] = (float)mean;
-  save_invstd[c] = invstd;
-  scale[c] = gam * invstd;
-  shift[c] = bet - (float)mean * gam * invstd;
-  if (run_mean) {
-    const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
-    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
-    run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unbiased;
-  }
+  const FwdFin f{psum, psq, gy, w, b, eps, momentum, run_mean, run_var, save_mean, save_invstd, scale, shift, nbt};
+  fwd_fin_group<false>(f, M, C, blockIdx.x);
 }
 
-template <typename T, bool RELU, bool RES, int U = kBnUnroll>
+// In-launch finalize (the separate 1-row finalize launch folded into the
+// apply pass that consumes it): every workgroup draws a ticket; tickets
+// 0 .. ngroups-1 run the finalize of one kFinC-channel group and publish a
+// flag = epoch (all outputs stored `sc1` and drained first); every workgroup
+// then waits for the flags of the groups its channel tile covers and reads
+// the finalized values with `sc1` loads.  A leader waits only after its own
+// flag is out and a waiter only for groups whose leaders drew their ticket
+// -- i.e. are running -- so no workgroup waits on one that is not resident.
+// The ticket counter is reset by the holder of the last ticket; the flags
+// are per-layer persistent (ops/bn.py) and `epoch` is unique per launch
+// (host counter), so they need no reset.  Not used under graph capture
+// (the epoch would be frozen into the replays).
+struct FinSync {
+  unsigned long long* ticket;
+  uint32_t* flags;
+  uint32_t epoch;
+  uint32_t nblocks;
+  int ngroups;
+};
+
+template <typename F>
+__device__ __forceinline__ void fin_prologue(const FinSync& fs, int g0, int g1, F&& finalize_group) {
+  __shared__ uint32_t s_ticket;
+  if (threadIdx.x == 0) {
+    const unsigned long long t = __hip_atomic_fetch_add(fs.ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == (unsigned long long)fs.nblocks - 1ull) st_dev(fs.ticket, 0ull);   // every ticket of this launch is out
+    s_ticket = (uint32_t)t;
+  }
+  __syncthreads();
+  const uint32_t t = s_ticket;
+  if (t < (uint32_t)fs.ngroups) {
+    finalize_group((int)t);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's sc1 stores completed
+    __syncthreads();
+    if (threadIdx.x == 0) st_dev(fs.flags + t, fs.epoch);
+  }
+  const int gi = g0 + (int)threadIdx.x;
+  if (gi < g1) {
+    uint32_t spins = 0;
+    while (ld_dev(fs.flags + gi) != fs.epoch && ++spins < (1u << 24)) __builtin_amdgcn_s_sleep(1);
+  }
+  __syncthreads();
+}
+
+template <typename T, bool RELU, bool RES, bool FIN = false, int U = kBnUnroll>
 __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res,
                                                           T* __restrict__ y, uint8_t* __restrict__ mask, int64_t M,
                                                           int C, Geo g, const float* __restrict__ scale,
-                                                          const float* __restrict__ shift) {
+                                                          const float* __restrict__ shift, FinSync fs = FinSync{},
+                                                          FwdFin ff = FwdFin{}) {
   constexpr int V = Vec<T>::N;
   const int tc = threadIdx.x % g.tpr;
   const int lane_r = threadIdx.x / g.tpr;
   const int c0 = blockIdx.x * g.ct + tc * V;
   float sc[V], sf[V];
+  if (FIN) {
+    fin_prologue(fs, (blockIdx.x * g.ct) / kFinC, ((blockIdx.x + 1) * g.ct + kFinC - 1) / kFinC,
+                 [&](int grp) { fwd_fin_group<true>(ff, M, C, grp); });
 #pragma unroll
-  for (int i = 0; i < V; ++i) { sc[i] = scale[c0 + i]; sf[i] = shift[c0 + i]; }
+    for (int i = 0; i < V; ++i) { sc[i] = ld_coh_f32(scale, c0 + i); sf[i] = ld_coh_f32(shift, c0 + i); }
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) { sc[i] = scale[c0 + i]; sf[i] = shift[c0 + i]; }
+  }
   const int64_t r0 = (int64_t)blockIdx.y * g.rows_per_block;
   int64_t r1 = r0 + g.rows_per_block;
   if (r1 > M) r1 = M;
@@ -611,6 +714,34 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(Src src, const T*
   }
 }
 
+struct BwdFin {   // backward finalize: partials -> dbeta, dgamma (+ arena accumulation)
+  const float* pdb;
+  const float* pdg;
+  int gy;
+  float* dbeta;
+  float* dgamma;
+  float* gb_acc;
+  float* gw_acc;
+  const float* cmean;     // non-null: the dgamma partials are sum(dz * x) (GEMM epilogue)
+  const float* cinvstd;
+};
+
+template <bool COH>
+__device__ __forceinline__ void bwd_fin_group(const BwdFin& f, int C, int grp) {
+  double a = 0.0, b = 0.0;
+  bool owner;
+  int c;
+  reduce_partials2(f.pdb, f.pdg, f.gy, C, &a, &b, &owner, &c, grp);
+  if (!owner) return;
+  // partials of sum(dz * x) from a GEMM epilogue: sum(dz * xhat) = invstd * (sum(dz x) - mean sum(dz))
+  if (f.cmean) b = (double)f.cinvstd[c] * (b - (double)f.cmean[c] * a);
+  put<COH>(f.dbeta + c, (float)a);
+  put<COH>(f.dgamma + c, (float)b);
+  // direct-to-arena parameter gradients (AccumulateGrad semantics)
+  if (f.gb_acc) f.gb_acc[c] += (float)a;
+  if (f.gw_acc) f.gw_acc[c] += (float)b;
+}
+
 __global__ __launch_bounds__(kBlock) void bn_bwd_finalize_kernel(const float* __restrict__ pdb,
                                                                  const float* __restrict__ pdg, int gy, int C,
                                                                  float* __restrict__ dbeta, float* __restrict__ dgamma,
@@ -618,18 +749,8 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_finalize_kernel(const float* __
                                                                  float* __restrict__ gw_acc,
                                                                  const float* __restrict__ cmean = nullptr,
                                                                  const float* __restrict__ cinvstd = nullptr) {
-  double a = 0.0, b = 0.0;
-  bool owner;
-  int c;
-  reduce_partials2(pdb, pdg, gy, C, &a, &b, &owner, &c);
-  if (!owner) return;
-  // partials of sum(dz * x) from a GEMM epilogue: sum(dz * xhat) = invstd * (sum(dz x) - mean sum(dz))
-  if (cmean) b = (double)cinvstd[c] * (b - (double)cmean[c] * a);
-  dbeta[c] = (float)a;
-  dgamma[c] = (float)b;
-  // direct-to-arena parameter gradients (AccumulateGrad semantics)
-  if (gb_acc) gb_acc[c] += (float)a;
-  if (gw_acc) gw_acc[c] += (float)b;
+  const BwdFin f{pdb, pdg, gy, dbeta, dgamma, gb_acc, gw_acc, cmean, cinvstd};
+  bwd_fin_group<false>(f, C, blockIdx.x);
 }
 
 // Lazy backward apply (the consumer kernels compute dx themselves): finalize as
@@ -649,7 +770,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_finalize_lazy_kernel(
   double a = 0.0, b = 0.0;
   bool owner;
   int c;
-  reduce_partials2(pdb, pdg, gy, C, &a, &b, &owner, &c);
+  reduce_partials2(pdb, pdg, gy, C, &a, &b, &owner, &c, blockIdx.x);
   if (!owner) return;
   const float is = invstd[c];
   if (center) b = (double)is * (b - (double)mean[c] * a);
@@ -673,19 +794,23 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_finalize_lazy_kernel(
   store_elem(padx + c, mu);
 }
 
-template <typename T, typename Src, bool DRES, int U = kBnUnroll>
+template <typename T, typename Src, bool DRES, bool FIN = false, int U = kBnUnroll>
 __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(Src src, const T* __restrict__ x, T* __restrict__ dx,
                                                               T* __restrict__ dres, int64_t M, int C, Geo g,
                                                               const float* __restrict__ w,
                                                               const float* __restrict__ mean,
                                                               const float* __restrict__ invstd,
                                                               const float* __restrict__ dbeta,
-                                                              const float* __restrict__ dgamma) {
+                                                              const float* __restrict__ dgamma,
+                                                              FinSync fs = FinSync{}, BwdFin bf = BwdFin{}) {
   constexpr int V = Vec<T>::N;
   const int tc = threadIdx.x % g.tpr;
   const int lane_r = threadIdx.x / g.tpr;
   const int c0 = blockIdx.x * g.ct + tc * V;
   const float invM = 1.f / (float)M;
+  if (FIN)
+    fin_prologue(fs, (blockIdx.x * g.ct) / kFinC, ((blockIdx.x + 1) * g.ct + kFinC - 1) / kFinC,
+                 [&](int grp) { bwd_fin_group<true>(bf, C, grp); });
   float mu[V], is[V], k1[V], k2[V], k3[V];
 #pragma unroll
   for (int i = 0; i < V; ++i) {
@@ -693,9 +818,9 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(Src src, const T* 
     mu[i] = mean[c];
     is[i] = invstd[c];
     const float gam = w ? w[c] : 1.f;
-    k1[i] = gam * is[i];                 // scale
-    k2[i] = dbeta[c] * invM;             // mean of dz
-    k3[i] = dgamma[c] * invM;            // mean of dz * xhat
+    k1[i] = gam * is[i];                                              // scale
+    k2[i] = (FIN ? ld_coh_f32(dbeta, c) : dbeta[c]) * invM;          // mean of dz
+    k3[i] = (FIN ? ld_coh_f32(dgamma, c) : dgamma[c]) * invM;        // mean of dz * xhat
   }
   const int64_t r0 = (int64_t)blockIdx.y * g.rows_per_block;
   int64_t r1 = r0 + g.rows_per_block;
@@ -867,7 +992,32 @@ constexpr int kPoolTargetBlocks = 4096;
 int g_bn_blocks = 1024;
 #define kTargetBlocks g_bn_blocks
 
+// In-launch finalize for one launch of grid g, or a FinSync with ticket ==
+// nullptr (separate finalize launch): needs the per-layer state, no stream
+// capture (the epoch argument would be frozen into the replays), and at least
+// one workgroup per finalize group.
+FinSync make_fin(void* state, const Geo& g, int C, hipStream_t s) {
+  static std::atomic<uint32_t> epoch{0};
+  FinSync fs{};
+  if (state == nullptr) return fs;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return fs;
+  const int ngroups = (C + kFinC - 1) / kFinC;
+  const int64_t nb = (int64_t)g.gx * g.gy;
+  if (nb < ngroups || nb > 0x7fffffff) return fs;
+  uint32_t e = epoch.fetch_add(1) + 1;
+  if (e == 0) e = epoch.fetch_add(1) + 1;   // 0 is the flags' initial value
+  fs.ticket = reinterpret_cast<unsigned long long*>(state);
+  fs.flags = reinterpret_cast<uint32_t*>(static_cast<char*>(state) + kFinStateFlagsOffset);
+  fs.epoch = e;
+  fs.nblocks = (uint32_t)nb;
+  fs.ngroups = ngroups;
+  return fs;
+}
+
 }  // namespace
+
+size_t bn_fin_state_bytes(int C) { return kFinStateFlagsOffset + sizeof(uint32_t) * (size_t)((C + kFinC - 1) / kFinC); }
 
 size_t bn_workspace_floats(int64_t M, int C, int elem_bytes) {
   // sized for the larger (pool-backward) grid so one workspace fits every pass
@@ -896,44 +1046,70 @@ void bn_stats_t(const T* x, int64_t M, int C, const float* w, const float* b, fl
 }
 
 template <typename T>
+void launch_apply(const T* x, const T* res, T* y, uint8_t* mask, int64_t M, int C, const Geo& g, float* scale,
+                  float* shift, int relu, const FinSync& fs, const FwdFin& ff, hipStream_t s) {
+#define GK_APPLY(R, D, F)                                                                                           \
+  hipLaunchKernelGGL((bn_apply_kernel<T, R, D, F>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, x, res, y, mask, M, C, g, \
+                     scale, shift, fs, ff)
+#define GK_APPLY2(R, D) if (fs.ticket) GK_APPLY(R, D, true); else GK_APPLY(R, D, false);
+  if (relu && res) { GK_APPLY2(true, true) }
+  else if (relu) { GK_APPLY2(true, false) }
+  else if (res) { GK_APPLY2(false, true) }
+  else { GK_APPLY2(false, false) }
+#undef GK_APPLY2
+#undef GK_APPLY
+}
+
+template <typename T>
 void bn_forward_t(const T* x, const T* res, T* y, uint8_t* mask, int64_t M, int C, const float* w, const float* b, float eps,
                   float momentum, float* run_mean, float* run_var, float* save_mean, float* save_invstd,
-                  float* scale, float* shift, float* ws, int relu, int64_t* nbt, hipStream_t s) {
+                  float* scale, float* shift, float* ws, int relu, int64_t* nbt, void* fin_state, hipStream_t s) {
   const Geo g = make_geo<T>(M, C, kTargetBlocks);
-  bn_stats_t<T>(x, M, C, w, b, eps, momentum, run_mean, run_var, save_mean, save_invstd, scale, shift, ws, nbt, s);
-#define GK_APPLY(R, D)                                                                                             \
-  hipLaunchKernelGGL((bn_apply_kernel<T, R, D>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, x, res, y, mask, M, C, g, scale, \
-                     shift)
-  if (relu && res) GK_APPLY(true, true);
-  else if (relu) GK_APPLY(true, false);
-  else if (res) GK_APPLY(false, true);
-  else GK_APPLY(false, false);
-#undef GK_APPLY
+  const FinSync fs = make_fin(fin_state, g, C, s);
+  const FwdFin ff{ws, ws + (int64_t)g.gy * C, g.gy, w, b, eps, momentum, run_mean, run_var, save_mean, save_invstd,
+                  scale, shift, nbt};
+  if (fs.ticket) {
+    hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(g.gx, g.gy), dim3(kBlock), 0, s, x, M, C, g, ws, ws + (int64_t)g.gy * C);
+  } else {
+    bn_stats_t<T>(x, M, C, w, b, eps, momentum, run_mean, run_var, save_mean, save_invstd, scale, shift, ws, nbt, s);
+  }
+  launch_apply<T>(x, res, y, mask, M, C, g, scale, shift, relu, fs, ff, s);
+}
+
+// finalize (separate launch unless fs carries the in-launch state) + apply
+template <typename T, typename Src, bool DRES>
+void launch_bwd_apply(Src src, const T* x, T* dx, T* dres, int64_t M, int C, const Geo& g, const float* w,
+                      const float* mean, const float* invstd, const BwdFin& bf, const FinSync& fs, hipStream_t s) {
+  if (fs.ticket) {
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, Src, DRES, true>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, src, x, dx,
+                       dres, M, C, g, w, mean, invstd, bf.dbeta, bf.dgamma, fs, bf);
+    return;
+  }
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(kBlock), 0, s, bf.pdb, bf.pdg, bf.gy,
+                     C, bf.dbeta, bf.dgamma, bf.gb_acc, bf.gw_acc, bf.cmean, bf.cinvstd);
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, Src, DRES, false>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, src, x, dx,
+                     dres, M, C, g, w, mean, invstd, bf.dbeta, bf.dgamma, FinSync{}, BwdFin{});
 }
 
 template <typename T, typename Src>
 void bn_backward_src(Src src, const T* x, T* dx, T* dres, int64_t M, int C, const float* w, const float* mean,
                      const float* invstd, float* dgamma, float* dbeta, float* ws, float* gw_acc, float* gb_acc,
-                     hipStream_t s, int target_blocks = kTargetBlocks) {
+                     void* fin_state, hipStream_t s, int target_blocks = kTargetBlocks) {
   const Geo g = make_geo<T>(M, C, target_blocks);
   float* pdb = ws;
   float* pdg = ws + (int64_t)g.gy * C;
   hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, Src>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, src, x, M, C, g, mean,
                      invstd, pdb, pdg);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(kBlock), 0, s, pdb, pdg, g.gy, C,
-                     dbeta, dgamma, gb_acc, gw_acc);
-  if (dres)
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, Src, true>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, src, x, dx, dres, M,
-                       C, g, w, mean, invstd, dbeta, dgamma);
-  else
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, Src, false>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, src, x, dx, dres,
-                       M, C, g, w, mean, invstd, dbeta, dgamma);
+  const FinSync fs = make_fin(fin_state, g, C, s);
+  const BwdFin bf{pdb, pdg, g.gy, dbeta, dgamma, gb_acc, gw_acc, nullptr, nullptr};
+  if (dres) launch_bwd_apply<T, Src, true>(src, x, dx, dres, M, C, g, w, mean, invstd, bf, fs, s);
+  else launch_bwd_apply<T, Src, false>(src, x, dx, dres, M, C, g, w, mean, invstd, bf, fs, s);
 }
 
 template <typename T>
 void bn_backward_t(const T* dy, const T* dy2, const uint8_t* mask, const T* x, T* dx, T* dres, int64_t M, int C,
                    const float* w, const float* mean, const float* invstd, float* dgamma, float* dbeta, float* ws,
-                   int relu, float* gw_acc, float* gb_acc, hipStream_t s) {
+                   int relu, float* gw_acc, float* gb_acc, void* fin_state, hipStream_t s) {
   if (dy2 && dres) {
     // twin + residual (ResNet block output): the reduce pass writes dz = dres
     // and the apply pass reads it back (one tensor instead of dy, dy2, mask)
@@ -946,16 +1122,15 @@ void bn_backward_t(const T* dy, const T* dy2, const uint8_t* mask, const T* x, T
     if (relu) GK_RED(true);
     else GK_RED(false);
 #undef GK_RED
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(kBlock), 0, s, pdb, pdg, g.gy, C,
-                       dbeta, dgamma, gb_acc, gw_acc);
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, DyPlain<T, false, false>, false>), dim3(g.gx, g.gy), dim3(kBlock), 0, s,
-                       DyPlain<T, false, false>{dres, nullptr, nullptr}, x, dx, (T*)nullptr, M, C, g, w, mean, invstd,
-                       dbeta, dgamma);
+    const FinSync fs = make_fin(fin_state, g, C, s);
+    const BwdFin bf{pdb, pdg, g.gy, dbeta, dgamma, gb_acc, gw_acc, nullptr, nullptr};
+    launch_bwd_apply<T, DyPlain<T, false, false>, false>(DyPlain<T, false, false>{dres, nullptr, nullptr}, x, dx,
+                                                         (T*)nullptr, M, C, g, w, mean, invstd, bf, fs, s);
     return;
   }
 #define GK_BWD(R, TW)                                                                                              \
   bn_backward_src<T>(DyPlain<T, R, TW>{dy, dy2, mask}, x, dx, dres, M, C, w, mean, invstd, dgamma, dbeta, ws, gw_acc, \
-                     gb_acc, s)
+                     gb_acc, fin_state, s)
   if (relu && dy2) GK_BWD(true, true);
   else if (relu) GK_BWD(true, false);
   else if (dy2) GK_BWD(false, true);
@@ -980,50 +1155,53 @@ void bn_stats_partials(const void* x, int64_t M, int C, int elem_bytes, float* w
 void bn_act_forward(const void* x, const void* res, void* y, uint8_t* mask, int64_t M, int C, int elem_bytes,
                     const float* w, const float* b, float eps, float momentum, float* run_mean, float* run_var,
                     float* save_mean, float* save_invstd, float* scale, float* shift, float* ws, int relu,
-                    int64_t* nbt, hipStream_t s) {
+                    int64_t* nbt, hipStream_t s, void* fin_state) {
   if (elem_bytes == 2)
     bn_forward_t<uint16_t>((const uint16_t*)x, (const uint16_t*)res, (uint16_t*)y, mask, M, C, w, b, eps, momentum,
-                           run_mean, run_var, save_mean, save_invstd, scale, shift, ws, relu, nbt, s);
+                           run_mean, run_var, save_mean, save_invstd, scale, shift, ws, relu, nbt, fin_state, s);
   else
     bn_forward_t<float>((const float*)x, (const float*)res, (float*)y, mask, M, C, w, b, eps, momentum, run_mean,
-                        run_var, save_mean, save_invstd, scale, shift, ws, relu, nbt, s);
+                        run_var, save_mean, save_invstd, scale, shift, ws, relu, nbt, fin_state, s);
+}
+
+template <typename T>
+void bn_forward_pre_t(const T* x, const T* res, T* y, uint8_t* mask, int64_t M, int C, const float* psum,
+                      const float* psq, int gy, const float* w, const float* b, float eps, float momentum,
+                      float* run_mean, float* run_var, float* save_mean, float* save_invstd, float* scale, float* shift,
+                      int relu, int64_t* nbt, void* fin_state, hipStream_t s) {
+  const Geo g = make_geo<T>(M, C, kTargetBlocks);
+  const FinSync fs = make_fin(fin_state, g, C, s);
+  const FwdFin ff{psum, psq, gy, w, b, eps, momentum, run_mean, run_var, save_mean, save_invstd, scale, shift, nbt};
+  if (!fs.ticket)
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(kBlock), 0, s, psum, psq, gy, M, C, w,
+                       b, eps, momentum, run_mean, run_var, save_mean, save_invstd, scale, shift, nbt);
+  launch_apply<T>(x, res, y, mask, M, C, g, scale, shift, relu, fs, ff, s);
 }
 
 void bn_act_forward_pre(const void* x, const void* res, void* y, uint8_t* mask, int64_t M, int C, int elem_bytes,
                         const float* psum, const float* psq, int gy, const float* w, const float* b, float eps, float momentum,
                         float* run_mean, float* run_var, float* save_mean, float* save_invstd, float* scale,
-                        float* shift, int relu, int64_t* nbt, hipStream_t s) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(kBlock), 0, s, psum, psq, gy, M, C, w, b, eps, momentum, run_mean, run_var, save_mean,
-                     save_invstd, scale, shift, nbt);
-#define GK_APPLY(T, R, D)                                                                                        \
-  do {                                                                                                           \
-    const Geo g = make_geo<T>(M, C, kTargetBlocks);                                                              \
-    hipLaunchKernelGGL((bn_apply_kernel<T, R, D>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, (const T*)x,            \
-                       (const T*)res, (T*)y, mask, M, C, g, scale, shift);                                       \
-  } while (0)
-#define GK_APPLY_T(T)                     \
-  if (relu && res) GK_APPLY(T, true, true);    \
-  else if (relu) GK_APPLY(T, true, false);     \
-  else if (res) GK_APPLY(T, false, true);      \
-  else GK_APPLY(T, false, false);
-  if (elem_bytes == 2) {
-    GK_APPLY_T(uint16_t)
-  } else {
-    GK_APPLY_T(float)
-  }
-#undef GK_APPLY_T
-#undef GK_APPLY
+                        float* shift, int relu, int64_t* nbt, hipStream_t s, void* fin_state) {
+  if (elem_bytes == 2)
+    bn_forward_pre_t<uint16_t>((const uint16_t*)x, (const uint16_t*)res, (uint16_t*)y, mask, M, C, psum, psq, gy, w,
+                               b, eps, momentum, run_mean, run_var, save_mean, save_invstd, scale, shift, relu, nbt,
+                               fin_state, s);
+  else
+    bn_forward_pre_t<float>((const float*)x, (const float*)res, (float*)y, mask, M, C, psum, psq, gy, w, b, eps,
+                            momentum, run_mean, run_var, save_mean, save_invstd, scale, shift, relu, nbt, fin_state, s);
 }
 
 void bn_act_backward(const void* dy, const void* dy2, const uint8_t* mask, const void* x, void* dx, void* dres,
                      int64_t M, int C, int elem_bytes, const float* w, const float* mean, const float* invstd,
-                     float* dgamma, float* dbeta, float* ws, int relu, float* gw_acc, float* gb_acc, hipStream_t s) {
+                     float* dgamma, float* dbeta, float* ws, int relu, float* gw_acc, float* gb_acc, hipStream_t s,
+                     void* fin_state) {
   if (elem_bytes == 2)
     bn_backward_t<uint16_t>((const uint16_t*)dy, (const uint16_t*)dy2, mask, (const uint16_t*)x, (uint16_t*)dx,
-                            (uint16_t*)dres, M, C, w, mean, invstd, dgamma, dbeta, ws, relu, gw_acc, gb_acc, s);
+                            (uint16_t*)dres, M, C, w, mean, invstd, dgamma, dbeta, ws, relu, gw_acc, gb_acc, fin_state,
+                            s);
   else
     bn_backward_t<float>((const float*)dy, (const float*)dy2, mask, (const float*)x, (float*)dx, (float*)dres, M, C, w,
-                         mean, invstd, dgamma, dbeta, ws, relu, gw_acc, gb_acc, s);
+                         mean, invstd, dgamma, dbeta, ws, relu, gw_acc, gb_acc, fin_state, s);
 }
 
 // dz (already gated and twin-summed) and its partials sum(dz), sum(dz*(x-mean))
@@ -1031,11 +1209,13 @@ void bn_act_backward(const void* dy, const void* dy2, const uint8_t* mask, const
 // BnBwd): no reduction pass, only finalize + apply.
 template <typename T>
 void bn_bwd_apply_pre_t(const T* dz, const T* x, T* dx, int64_t M, int C, const float* w, const float* mean,
-                        const float* invstd, float* dgamma, float* dbeta, hipStream_t s) {
+                        const float* invstd, float* dgamma, float* dbeta, const float* pdb, const float* pdg, int gy,
+                        float* gw_acc, float* gb_acc, void* fin_state, hipStream_t s) {
   const Geo g = make_geo<T>(M, C, kTargetBlocks);
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, DyPlain<T, false, false>, false>), dim3(g.gx, g.gy), dim3(kBlock), 0, s,
-                     DyPlain<T, false, false>{dz, nullptr, nullptr}, x, dx, (T*)nullptr, M, C, g, w, mean, invstd,
-                     dbeta, dgamma);
+  const FinSync fs = make_fin(fin_state, g, C, s);
+  const BwdFin bf{pdb, pdg, gy, dbeta, dgamma, gb_acc, gw_acc, mean, invstd};
+  launch_bwd_apply<T, DyPlain<T, false, false>, false>(DyPlain<T, false, false>{dz, nullptr, nullptr}, x, dx,
+                                                       (T*)nullptr, M, C, g, w, mean, invstd, bf, fs, s);
 }
 
 void bn_bwd_finalize_lazy(const float* pdb, const float* pdg, int gy, int64_t M, int C, int elem_bytes, int center,
@@ -1127,14 +1307,13 @@ void bn_lazy_apply(const void* dz, const void* x, void* dx, int64_t M, int C, in
 
 void bn_act_backward_pre(const void* dz, const void* x, void* dx, int64_t M, int C, int elem_bytes, const float* w,
                          const float* mean, const float* invstd, float* dgamma, float* dbeta, const float* pdb,
-                         const float* pdg, int gy, float* gw_acc, float* gb_acc, hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(kBlock), 0, s, pdb, pdg, gy, C,
-                     dbeta, dgamma, gb_acc, gw_acc, mean, invstd);
+                         const float* pdg, int gy, float* gw_acc, float* gb_acc, hipStream_t s, void* fin_state) {
   if (elem_bytes == 2)
     bn_bwd_apply_pre_t<uint16_t>((const uint16_t*)dz, (const uint16_t*)x, (uint16_t*)dx, M, C, w, mean, invstd, dgamma,
-                                 dbeta, s);
+                                 dbeta, pdb, pdg, gy, gw_acc, gb_acc, fin_state, s);
   else
-    bn_bwd_apply_pre_t<float>((const float*)dz, (const float*)x, (float*)dx, M, C, w, mean, invstd, dgamma, dbeta, s);
+    bn_bwd_apply_pre_t<float>((const float*)dz, (const float*)x, (float*)dx, M, C, w, mean, invstd, dgamma, dbeta, pdb,
+                              pdg, gy, gw_acc, gb_acc, fin_state, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -1221,10 +1400,10 @@ void bn_pool_backward_tw(const T* dy, const T* dy2, const uint8_t* amax, const T
   // generic k, s: per-pixel gather (latency-bound: more workgroups than the plain BN passes)
   if ((pg.k + pg.s - 1) / pg.s <= 2)
     bn_backward_src<T>(DyPool<T, TWIN, 2>{dy, dy2, amax, pg}, x, dx, (T*)nullptr, M, C, w, mean, invstd, dgamma,
-                       dbeta, ws, gw_acc, gb_acc, s, kPoolTargetBlocks);
+                       dbeta, ws, gw_acc, gb_acc, nullptr, s, kPoolTargetBlocks);
   else
     bn_backward_src<T>(DyPool<T, TWIN, 0>{dy, dy2, amax, pg}, x, dx, (T*)nullptr, M, C, w, mean, invstd, dgamma,
-                       dbeta, ws, gw_acc, gb_acc, s, kPoolTargetBlocks);
+                       dbeta, ws, gw_acc, gb_acc, nullptr, s, kPoolTargetBlocks);
 }
 
 template <typename T>

@@ -230,6 +230,11 @@ void clip_grad_norm(float* g, int64_t n, float max_norm, double* ws, float* coef
 // elem_bytes: 2 (bf16) or 4 (fp32).  ws: bn_workspace_floats() floats.
 // ---------------------------------------------------------------------------
 size_t bn_workspace_floats(int64_t M, int C, int elem_bytes);
+// fin_state (optional, bn_fin_state_bytes(C), zero-initialised once, kept per
+// layer): the finalize of the statistics runs inside the apply pass that
+// consumes it (bn_act.hip FinSync) instead of as a separate launch; ignored
+// under stream capture.
+size_t bn_fin_state_bytes(int C);
 bool bn_supported(int C, int elem_bytes);
 // workgroups per streaming BN pass (default 1024, clamped to [64, 4096]; bench/bn_probe.py)
 void bn_set_blocks(int blocks);
@@ -241,7 +246,7 @@ void bn_stats_partials(const void* x, int64_t M, int C, int elem_bytes, float* w
 void bn_act_forward(const void* x, const void* res, void* y, uint8_t* mask, int64_t M, int C, int elem_bytes,
                     const float* w, const float* b, float eps, float momentum, float* run_mean, float* run_var,
                     float* save_mean, float* save_invstd, float* scale, float* shift, float* ws, int relu,
-                    int64_t* nbt, hipStream_t stream);
+                    int64_t* nbt, hipStream_t stream, void* fin_state = nullptr);
 // dy2 (optional): a second upstream gradient of the same output, summed on load.
 // bn_act_forward with the batch statistics already reduced to per-row
 // partials (psum / psq: [gy][C] each), e.g. by the producing
@@ -249,7 +254,7 @@ void bn_act_forward(const void* x, const void* res, void* y, uint8_t* mask, int6
 void bn_act_forward_pre(const void* x, const void* res, void* y, uint8_t* mask, int64_t M, int C, int elem_bytes,
                         const float* psum, const float* psq, int gy, const float* w, const float* b, float eps, float momentum,
                         float* run_mean, float* run_var, float* save_mean, float* save_invstd, float* scale,
-                        float* shift, int relu, int64_t* nbt, hipStream_t stream);
+                        float* shift, int relu, int64_t* nbt, hipStream_t stream, void* fin_state = nullptr);
 // dz and its [2][gy][C] partials sum(dz), sum(dz * x) come from a grad-input
 // GEMM's BatchNorm-backward epilogue (BnBwdArgs below); finalize (centring
 // with the mean) + apply only.  bf16 (elem_bytes 2) or fp32 (4).
@@ -271,11 +276,12 @@ void bn_lazy_apply(const void* dz, const void* x, void* dx, int64_t M, int C, in
                    hipStream_t stream);
 void bn_act_backward_pre(const void* dz, const void* x, void* dx, int64_t M, int C, int elem_bytes, const float* w,
                          const float* mean, const float* invstd, float* dgamma, float* dbeta, const float* pdb,
-                         const float* pdg, int gy, float* gw_acc, float* gb_acc, hipStream_t stream);
+                         const float* pdg, int gy, float* gw_acc, float* gb_acc, hipStream_t stream,
+                         void* fin_state = nullptr);
 void bn_act_backward(const void* dy, const void* dy2, const uint8_t* mask, const void* x, void* dx, void* dres,
                      int64_t M, int C, int elem_bytes, const float* w, const float* mean, const float* invstd,
                      float* dgamma, float* dbeta, float* ws, int relu, float* gw_acc, float* gb_acc,
-                     hipStream_t stream);
+                     hipStream_t stream, void* fin_state = nullptr);
 
 // BN (training) + ReLU + k x k / stride s / pad p max-pool, channels-last
 // [N, H, W, C] -> [N, OH, OW, C].  amax: one byte per OUTPUT element (window

@@ -135,3 +135,40 @@ def test_bnact_twin_sums_both_gradients(cuda, pool):
         outs.append((a.detach(), x.grad, m.weight.grad, m.bias.grad))
     for u, v in zip(*outs):
         assert torch.allclose(u, v, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_in_launch_finalize_matches_separate_launch(cuda, dtype, monkeypatch):
+    """The finalize folded into the apply pass (bn_act.hip FinSync: ticketed
+    leader workgroups + per-layer flags) gives bit-identical outputs,
+    gradients and running statistics to the separate finalize launch, over
+    many back-to-back launches of several layers and shapes (the ticket
+    counter reset and the per-launch epoch are exercised every iteration)."""
+    import gaussiank_sgd_amd.ops.bn as bnmod
+    torch.manual_seed(0)
+    shapes = [(8, 64, 14, 14), (4, 2048, 3, 3), (3, 96, 5, 5), (16, 256, 7, 7)]
+    mods = {}
+    for fused in (True, False):
+        torch.manual_seed(1)
+        mods[fused] = [BNAct(s[1], act="relu").to(cuda) for s in shapes]
+    for it in range(12):
+        si = it % len(shapes)
+        shape = shapes[si]
+        x0 = (torch.randn(shape, device=cuda) * 2 + 0.3).to(dtype).contiguous(memory_format=torch.channels_last)
+        r0 = torch.randn(shape, device=cuda).to(dtype).contiguous(memory_format=torch.channels_last)
+        g0 = torch.randn(shape, device=cuda).to(dtype).contiguous(memory_format=torch.channels_last)
+        outs = {}
+        for fused in (True, False):
+            monkeypatch.setattr(bnmod, "_FIN_FUSE", fused)
+            m = mods[fused][si]
+            x = x0.clone().requires_grad_(True)
+            r = r0.clone().requires_grad_(True)
+            y = m(x, r if it % 2 else None)
+            y.backward(g0)
+            outs[fused] = (y.detach(), x.grad, m.weight.grad.clone(), m.bias.grad.clone(), m.running_mean.clone(),
+                           m.running_var.clone())
+            m.weight.grad = None
+            m.bias.grad = None
+        assert getattr(mods[True][si], "_gk_fin", None) is not None
+        for a, b in zip(outs[True], outs[False]):
+            assert torch.equal(a, b), it
