@@ -58,6 +58,7 @@ import json
 import os
 import sys
 import time
+from typing import Optional
 
 # MIOpen tuning state lives in the repo so a fresh box reuses the convolution
 # solutions found once by `bench.py --cudnn-benchmark` (tuning/miopen/*.udb).
@@ -122,6 +123,8 @@ def parse():
                     help="per-GPU batch of the reference-batch phases (default: the reference's exp_configs "
                          "batch of the model, ResNet-50 32; 0 skips them)")
     ap.add_argument("--ref-steps", type=int, default=10, help="timed steps of each reference-batch phase")
+    ap.add_argument("--ref-graph", default="auto", choices=["auto", "on", "off"],
+                    help="replay the reference-batch steps as one HIP graph (auto: on one GPU)")
     ap.add_argument("--dense-bucket-mb", type=float, default=25.0,
                     help="bucket size of the dense comparator's overlapped all-reduce (MB of fp32 gradients)")
     ap.add_argument("--no-channels-last", action="store_true")
@@ -242,7 +245,7 @@ def build(args, amp: str, dense: bool, threshold: int, P: int, rank: int, batch:
     return Phase(trainer, opt, comp_name, is_sparse, batch)
 
 
-def run_phase(args, ph: Phase, steps: int, warmup: int, P: int):
+def run_phase(args, ph: Phase, steps: int, warmup: int, P: int, graph: Optional[bool] = None):
     """W untimed warm-up steps, then EXACTLY K steps bracketed by a barrier +
     synchronize on both sides; returns (elapsed seconds, max over ranks;
     exposed-comm ms per step, max over ranks).  The step callable is kept
@@ -273,10 +276,11 @@ def run_phase(args, ph: Phase, steps: int, warmup: int, P: int):
             e2.record()
             marks.append((ev, e2))
 
-    if args.graph and args.model == "lstm":
+    graph = args.graph if graph is None else graph
+    if graph and args.model == "lstm":
         raise SystemExit("bench.py --graph: the LSTM carries hidden state across steps; not graph-capturable")
     run = step
-    if args.graph:
+    if graph:
         # whole-step HIP graph: capture after the eager warm-up, replay in the timed loop
         from gaussiank_sgd_amd.train.graph import GraphedStep
         for _ in range(warmup):
@@ -289,7 +293,7 @@ def run_phase(args, ph: Phase, steps: int, warmup: int, P: int):
     opt._collect_selected()  # drop warm-up counts
     if opt._exchanger is not None:
         opt._exchanger.reset_stats()   # shared communicator: count this phase's timed loop only
-    state["mark"] = not args.graph
+    state["mark"] = not graph
     comm.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -311,6 +315,9 @@ def phase_info(ph: Phase) -> dict:
     loop (native engine; empty for torch.distributed / local)."""
     ex = ph.opt._exchanger if ph is not None and ph.opt is not None else None
     info = {"exchange": ex.kind if ex is not None else "none", "buckets": len(ph.opt.arena.buckets) if ph else None}
+    wp = getattr(ph.trainer, "weight_prep", None) if ph is not None else None
+    if wp is not None:
+        info["weight_prep"] = {"relayouts": len(wp.entries), "batched_launches": wp.launches}
     if ex is not None:
         try:
             info["timed_loop"] = ex.stats() or None
@@ -587,11 +594,12 @@ def main() -> int:
     release(ph)
     ph = None
 
-    def timed(holder, name, amp_, dense, threshold, batch, steps, warmup):
+    def timed(holder, name, amp_, dense, threshold, batch, steps, warmup, graph=None):
         p = build(args, amp_, dense, threshold, P, rank, batch)
         holder.append(p)
-        el, exp_ = run_phase(args, p, steps, warmup, P)
+        el, exp_ = run_phase(args, p, steps, warmup, P, graph)
         info = phase_info(p)
+        info["hip_graph"] = bool(args.graph if graph is None else graph)
         info.update(ms_per_step=round(el / steps * 1e3, 3),
                     value=round(P * batch * tok_per_sample * steps / el, 2),
                     exposed_comm_ms=round(exp_, 3) if exp_ == exp_ else None, per_gpu_batch=batch, steps=steps)
@@ -625,15 +633,19 @@ def main() -> int:
     if alive and ref_bs and not args.dense:
         tag = "ref_bs%d" % ref_bs
         rsteps, rwarm = max(1, args.ref_steps), max(2, min(args.warmup, 5))
+        # the reference batch is launch-bound: the whole step replays as one HIP
+        # graph (train/graph.py) by default on one GPU; at N > 1 eager, with the
+        # side-stream overlap (--ref-graph on|off overrides)
+        ref_graph = (P == 1 and args.model != "lstm") if args.ref_graph == "auto" else args.ref_graph == "on"
 
         def ref_sparse(holder):
-            i = timed(holder, tag, amp, False, args.threshold, ref_bs, rsteps, rwarm)
+            i = timed(holder, tag, amp, False, args.threshold, ref_bs, rsteps, rwarm, graph=ref_graph)
             out[tag + "_value"] = i["value"]
             out[tag + "_ms_per_step"] = i["ms_per_step"]
             out[tag + "_exposed_comm_ms"] = i["exposed_comm_ms"]
 
         def ref_dense(holder):
-            i = timed(holder, tag + "_dense", amp, True, dense_elems, ref_bs, rsteps, rwarm)
+            i = timed(holder, tag + "_dense", amp, True, dense_elems, ref_bs, rsteps, rwarm, graph=ref_graph)
             out[tag + "_dense_value"] = i["value"]
             out[tag + "_dense_ms_per_step"] = i["ms_per_step"]
             if (tag + "_ms_per_step") in out:

@@ -4,8 +4,8 @@ set -u
 D=gpurun_out/r5c2
 mkdir -p $D
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_weight_prep_gpu.py \
-  tests/test_winograd_gpu.py tests/test_conv1x1_gpu.py tests/test_kernels_gpu.py -k "not stress" > $D/pytest.log 2>&1
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_weight_prep_gpu.py tests/test_bn_gpu.py tests/test_bnlink_gpu.py \
+  tests/test_winograd_gpu.py tests/test_conv1x1_gpu.py tests/test_kernels_gpu.py tests/test_graph_gpu.py -k "not stress" > $D/pytest.log 2>&1
 rc=$?; tail -4 $D/pytest.log; [ $rc -eq 0 ] || exit $rc
 B="python3 bench.py --batch-size 32 --steps 40 --warmup 10 --no-bf16-phase --ref-batch 0"
 timeout -k 10 300 $B --json-out $D/bs32_eager.json > $D/bs32_eager.log 2>&1
@@ -19,3 +19,5 @@ rc=$?; echo prof_rc=$rc; [ $rc -eq 0 ] || exit $rc
 python3 scripts/rocpd_summary.py --marker reduce_records_kernel --steps 10 $(find $D/prof -name '*.db' | head -1) $D/prof_summary.txt > $D/sum.log 2>&1; echo sum_rc=$?
 find $D/prof -name '*.db' -delete
 head -14 $D/prof_summary.txt
+GKSGD_BN_FIN_FUSE=0 timeout -k 10 300 $B --json-out $D/bs32_eager_nofin.json > $D/bs32_eager_nofin.log 2>&1
+rc=$?; echo nofin_rc=$rc; python3 -c "import json;d=json.load(open('$D/bs32_eager_nofin.json'));print('nofin', d['value'], d['ms_per_step'])"

@@ -30,14 +30,15 @@ def _free_port():
     return p
 
 
-def _bench(*extra, gpus=2, timeout=480, probe=False, env_extra=None):
+def _bench(*extra, gpus=2, timeout=480, probe=False, env_extra=None, native=False):
     env = dict(os.environ, GKSGD_DIST_BACKEND="gloo", MASTER_PORT=str(_free_port()), HSA_ENABLE_IPC_MODE_LEGACY="0",
                GKSGD_BENCH_PROBE="1" if probe else "0")
     env.update(env_extra or {})
     env.pop("WORLD_SIZE", None)
     env.pop("RANK", None)
     env.pop("LOCAL_RANK", None)
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--no-native-rccl"] + list(extra)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus)] + \
+        ([] if native else ["--no-native-rccl"]) + list(extra)
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
     assert p.returncode == 0, "bench.py failed (%d):\n%s\n%s" % (p.returncode, p.stdout[-3000:], p.stderr[-3000:])
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
@@ -95,3 +96,18 @@ def test_bench_dense_two_ranks_one_gpu(cuda):
     # the post-run fabric probe (alpha-beta of all-gather / all-reduce through the bench's exchanger)
     c = out["collectives"]
     assert c["allgather"]["points_bytes_us"] and c["allreduce"]["dense_grad_us"] > 0
+
+
+def test_bench_native_bootstrap_failure_falls_back(cuda):
+    """The native RCCL engine's bootstrap on real hardware where it CANNOT
+    succeed: two ranks on one device (RCCL refuses duplicate GPUs, or its
+    init never completes).  The non-blocking init must fail or hit its
+    deadline on both ranks, the ranks agree, and every phase runs on the
+    torch.distributed exchanger -- one bootstrap per process, no hang."""
+    out = _bench("--model", "resnet20", "--steps", "2", "--warmup", "1", "--batch-size", "32", "--ref-batch", "0",
+                 "--no-bf16-phase", "--no-dense-phase", native=True, timeout=400,
+                 env_extra={"GKSGD_RCCL_INIT_TIMEOUT_S": "30"})
+    assert out["value"] > 0 and out["n_gpus"] == 2
+    assert out["exchange"] == "torch" and out["replicas_consistent"] is True
+    assert out["native_inits"] == 1
+    assert not [k for k in out if k.endswith("_error")]
