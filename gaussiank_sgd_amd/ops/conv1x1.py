@@ -583,6 +583,7 @@ class _FastConvFn(torch.autograd.Function):
         b = bias.detach().float().contiguous() if bias is not None else None
         y = _fwd(x, w, stride, stats_box, b, wp=wp)
         ctx.wp = wp
+        ctx.prep = weight_prep.current() if wp else None
         ctx.sink = sink
         ctx.bias_sink = bias_sink
         ctx.has_bias = bias is not None
@@ -629,10 +630,12 @@ class _FastConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             N, C, H, W = x.shape
             key = _dgrad_key(N, C, H, W, w.shape[0], w.shape[2], s, ctx.dt)
-            if _bn_fusable(link, s, key):
-                dx = _dgrad_bn(dy, w, x.shape, s, link, lz, plink, wp=ctx.wp)
-            else:
-                dx = _dgrad(dy, w, x.shape, s, lz, plink, wp=ctx.wp)
+            prep, ctx.prep = ctx.prep, None
+            with weight_prep.use(prep):      # the step scope of the forward (autograd thread)
+                if _bn_fusable(link, s, key):
+                    dx = _dgrad_bn(dy, w, x.shape, s, link, lz, plink, wp=ctx.wp)
+                else:
+                    dx = _dgrad(dy, w, x.shape, s, lz, plink, wp=ctx.wp)
         gparam = None
         if ctx.needs_input_grad[1] and not wgrad_done:
             if direct:

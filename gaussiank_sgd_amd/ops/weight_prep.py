@@ -12,7 +12,8 @@ ResNet-50 step at the reference's batch of 32.
 convolutions asked for, and ``with prep.step():`` (``DLTrainer.train`` /
 ``test`` wrap their forward + backward in it) rebuilds ALL of them in one
 launch at the start of the step; inside the scope the call sites receive the
-prepared buffers.  A re-layout asked for the first time (or while a HIP graph
+prepared buffers (a backward function re-enters the scope its forward
+recorded, ``use()``: autograd runs a GPU backward on its own thread).  A re-layout asked for the first time (or while a HIP graph
 is being captured, when the descriptor table cannot be re-uploaded) is built
 by the call site itself and registered for the next step.  Outside a scope
 nothing is cached, so a weight update between scopes can never be missed.
@@ -72,7 +73,7 @@ class WeightPrep:
             for kind, src, dst, ld_in, ld_out, R, S in part:
                 packed += _DESC.pack(src, dst, ld_in, ld_out, begin, kind, R, S, (S + 63) // 64)
                 begin += int(_ops().weight_prep_blocks(kind, R, S))
-            host = torch.frombuffer(bytes(packed), dtype=torch.uint8)
+            host = torch.frombuffer(packed, dtype=torch.uint8)
             self._tables.append((host.to(device), len(part), begin))
         self._built_for = len(self.entries)
 
@@ -129,6 +130,19 @@ class WeightPrep:
 def current() -> Optional[WeightPrep]:
     """The WeightPrep of the step scope running on this thread, if any."""
     return getattr(_tls, "cur", None)
+
+
+@contextlib.contextmanager
+def use(prep: Optional[WeightPrep]):
+    """Make ``prep`` current on this thread while its step scope is open: the
+    autograd engine runs a GPU backward on its own device thread, so a
+    backward function re-enters the scope its forward recorded."""
+    prev = getattr(_tls, "cur", None)
+    _tls.cur = prep if (prep is not None and prep.active) else None
+    try:
+        yield
+    finally:
+        _tls.cur = prev
 
 
 def _key(kind: str, w: torch.Tensor) -> tuple:

@@ -80,8 +80,17 @@ def test_transposes_ragged_tiles():
     assert prep.launches == 1
 
 
-def test_resnet50_step_same_with_and_without_batching(monkeypatch):
+@pytest.mark.parametrize("force", ["hip", "wino"])
+def test_resnet50_step_same_with_and_without_batching(monkeypatch, force):
+    """Three ResNet-50 training steps with every re-layout built per call and
+    with the batched per-step launch give the same weights.  The kernel
+    families are forced (fresh autotuner table) so the re-layouts the test
+    needs are the ones registered: "hip" -> 1x1 transposes + 3x3 flips,
+    "wino" -> Winograd filter transforms."""
+    from gaussiank_sgd_amd.ops import conv1x1
     from gaussiank_sgd_amd.train import DLTrainer
+    monkeypatch.setattr(conv1x1, "_choices", {})
+    monkeypatch.setattr(conv1x1, "_FORCE", force)
 
     def run(enabled):
         monkeypatch.setattr(wpm, "ENABLED", enabled)
@@ -95,6 +104,7 @@ def test_resnet50_step_same_with_and_without_batching(monkeypatch):
         return t, torch.cat([p.detach().flatten() for p in t.net.parameters()])
     t0, ref = run(False)
     t1, got = run(True)
-    # (bs 4: the autotuner keeps MIOpen for most tiny grad-inputs; the Winograd forwards register)
-    assert t0.weight_prep.launches == 0 and t1.weight_prep.launches >= 1 and len(t1.weight_prep.entries) >= 1
+    kinds = {k[0] for k in t1.weight_prep.entries}
+    assert t0.weight_prep.launches == 0 and t1.weight_prep.launches == 2, t1.weight_prep.launches
+    assert kinds >= ({"t1", "f3"} if force == "hip" else {"wino0", "wino1"}), kinds
     assert torch.allclose(got, ref, rtol=1e-5, atol=1e-6)
