@@ -22,7 +22,11 @@ import torch.nn.functional as F
 from . import load, require_native
 
 _CL = torch.channels_last
-_FIN_FUSE = os.environ.get("GKSGD_BN_FIN_FUSE", "1") != "0"
+# In-launch finalize (bn_act.hip FinSync) is opt-in: measured on ResNet-50 bs32
+# fp32 (r5c2) the fused apply passes ran 35 us per call against 17 + 5 for
+# finalize + apply as two launches -- ~1000 workgroups polling the leaders'
+# flags slow the leaders' partial reductions -- 14.38 vs 12.99 ms per step.
+_FIN_FUSE = os.environ.get("GKSGD_BN_FIN_FUSE", "0") == "1"
 
 
 def _ops():
@@ -378,7 +382,7 @@ class BNAct(nn.BatchNorm2d):
         """Per-layer state of the in-launch finalize (bn_act.hip FinSync: a
         ticket counter and one flag per 16-channel group, zeroed ONCE): the
         statistics finalize runs inside the apply pass instead of as its own
-        launch (2 launches per BN and step fewer; GKSGD_BN_FIN_FUSE=0 off)."""
+        launch (2 launches per BN and step fewer; opt-in: GKSGD_BN_FIN_FUSE=1)."""
         if not _FIN_FUSE:
             return None
         st = getattr(self, "_gk_fin", None)
