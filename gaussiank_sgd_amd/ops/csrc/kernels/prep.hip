@@ -31,9 +31,14 @@ constexpr int kMaxDescs = 512;
 // of winograd.hip (wino_wt_kernel: same arithmetic, same slots).
 __device__ __forceinline__ int wsw(int r) { return (r >> 2) & 3; }
 
+// Work item idx -> (co, ci) with 8 consecutive input channels innermost, then
+// the output channel: a wave covers 8 co x 8 ci, so each of its 16 stores
+// writes one contiguous 256-byte run of u ([Ci/8][16][Co][8]) and its 9 loads
+// read 8 runs of 32 bytes for either filter orientation (Ci % 8 == 0).
 __device__ __forceinline__ void wino_pair(const float* __restrict__ w, float* __restrict__ u, int Co, int Ci, int flip,
                                           int64_t idx) {
-  const int co = (int)(idx / Ci), ci = (int)(idx - (int64_t)co * Ci);
+  const int64_t rest = idx >> 3;
+  const int co = (int)(rest % Co), ci = (int)(rest / Co) * 8 + (int)(idx & 7);
   float g[3][3];
 #pragma unroll
   for (int kh = 0; kh < 3; ++kh)

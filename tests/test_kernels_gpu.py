@@ -21,7 +21,12 @@ def _pair(n, seed=0, dist="normal", scale=1e-3):
         x = torch.randn(n, generator=g) * scale
         r = torch.randn(n, generator=g) * scale * 0.3
     else:
-        x = torch.distributions.StudentT(2.0).sample((n,)) * scale
+        # Student-t(2) from the seeded generator (t = z / sqrt(chi2_2 / 2),
+        # chi2_2 = -2 log U): the data must not depend on the global RNG,
+        # i.e. on which tests ran before
+        z = torch.randn(n, generator=g, dtype=torch.float64)
+        v = -2.0 * torch.log(torch.rand(n, generator=g, dtype=torch.float64).clamp_min(1e-300))
+        x = (z / torch.sqrt(v / 2.0)).float() * scale
         r = torch.zeros(n)
     return x, r
 
@@ -589,7 +594,12 @@ def test_last_block_handoff_stress(cuda, mode, handoff, monkeypatch):
         assert abs(float(st[0]) - float(acc.double().mean())) < 1e-5 * float(acc.abs().max()), it
         assert math.isclose(float(st[1]), float(acc.double().std()), rel_tol=1e-5), it
         sent, total, idx, val = _sel(recg, k_cap)
-        assert 0 < sent <= k_cap and sent == min(total, k_cap), it
+        # total = the reference rule's count; past k_cap the selection is the
+        # tighter candidate with the largest count in [2k/3, k_cap] (sent <
+        # k_cap) or the exact top-k_cap key (sent == k_cap)
+        overflow_alt = total > k_cap and sent < k_cap
+        assert 0 < sent <= k_cap, it
+        assert sent == min(total, k_cap) or (overflow_alt and 3 * sent >= 2 * k), (it, sent, total)
         assert bool((idx[1:] > idx[:-1]).all()), it
         assert torch.equal(val, acc[idx]), it
         res = acc.clone()
@@ -603,7 +613,7 @@ def test_last_block_handoff_stress(cuda, mode, handoff, monkeypatch):
         elif chosen not in (ops.OVERFLOW_EXACT, ops.CAL_FALLBACK) and mode != ops.MODE_DGC:
             thr = float(recg[3:4].view(torch.float32))
             expect = (acc.abs() > thr).nonzero().view(-1)
-            assert total == expect.numel() and torch.equal(idx, expect[:sent]), it
+            assert (sent if overflow_alt else total) == expect.numel() and torch.equal(idx, expect[:sent]), it
         else:
             # exact-key selections: every sent magnitude >= every unsent one
             unsent = torch.ones(n, dtype=torch.bool)
