@@ -4,7 +4,7 @@ set -u
 D=gpurun_out/r5c6
 mkdir -p $D
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests/test_weight_prep_gpu.py tests/test_kernels_gpu.py tests -m gpu -p no:randomly -x -q --timeout 300 --timeout-method thread > $D/pytest.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $D/pytest.log 2>&1
 rc=$?; echo pytest_rc=$rc; tail -5 $D/pytest.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $D/smoke.log 2>&1
 rc=$?; echo smoke_rc=$rc; tail -2 $D/smoke.log; [ $rc -eq 0 ] || exit $rc
