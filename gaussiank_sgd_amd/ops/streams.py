@@ -53,7 +53,9 @@ AUTO_MAX_BATCH = 64
 def enabled(device: torch.device, batch: Optional[int] = None) -> bool:
     """Fork this convolution's grad-weight?  ``batch``: its per-GPU batch
     (``auto`` mode forks only at batch <= AUTO_MAX_BATCH)."""
-    if device.type != "cuda" or torch.cuda.is_current_stream_capturing():
+    if device.type != "cuda":
+        return False
+    if torch.cuda.is_current_stream_capturing() and os.environ.get("GKSGD_WGRAD_STREAM_GRAPH", "0") != "1":
         return False
     mode = os.environ.get("GKSGD_WGRAD_STREAM", "0")
     if mode == "auto":

@@ -16,7 +16,10 @@ def category(n: str) -> str:
         return "gk LSTM (split-K step GEMM + fused cells)"
     if "gk::" in n and "colsum" in n:
         return "gk linear bias-grad column sums"
-    if "gk::" in n and ("gemm_nt" in n or "gemm_tn" in n or "stem_" in n or "wgrad3" in n or "wino_" in n):
+    if "gk::" in n and "weight_prep" in n:
+        return "gk per-step weight re-layouts (prep.hip)"
+    if "gk::" in n and ("gemm_nt" in n or "gemm_tn" in n or "stem_" in n or "wgrad3" in n or "wino_" in n or
+                        "splitk_reduce" in n):
         return "gk HIP conv GEMMs (1x1 / implicit-GEMM 3x3 / Winograd, MFMA)"
     if "gk::" in n and "attn_" in n:
         return "gk fused attention (flash fwd / dQ / dK-dV, MFMA)"
