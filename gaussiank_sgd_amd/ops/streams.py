@@ -31,7 +31,12 @@ occupied, so a BN pass issued on the other stream finds few free wave slots
 until the GEMM drains and little actually runs concurrently.  At bs32 the
 grids are small and the fork usually pays (13.38 -> 13.21 ms/step, r4c6;
 12.85 vs 13.15 / 13.06 off in an interleaved A/B, r4c34) but one of the two
-``auto`` runs of that A/B took 17.1 ms/step, so it stays opt-in.  MIOpen grad-weights on the side stream were
+``auto`` runs of that A/B took 17.1 ms/step, so it stays opt-in.  Inside a captured HIP graph
+(``GKSGD_WGRAD_STREAM_GRAPH=1`` lifts the capture exclusion) the forked
+grad-weights become parallel graph branches and the bs32 step DOUBLES: 23.2 /
+23.8 ms against 12.59 / 12.59 inline, interleaved A/B/A/B (r5c8) -- the graph
+executor's cross-branch synchronisation costs more than the overlap gains, so
+the graph path stays single-stream.  MIOpen grad-weights on the side stream were
 worse still (532 ms/step: its handle and workspace follow the stream), so a
 fork only ever carries a HIP-kernel choice.
 """
