@@ -51,6 +51,8 @@ HIP_SOURCES = [
     "kernels/optim.hip",
     "kernels/bn_act.hip",
     "kernels/gemm.hip",
+    # gemm_inst.hip: one object per GEMM instantiation unit (-DGK_GEMM_UNIT=<n>, gemm_kern.h)
+    *["kernels/gemm_inst.hip#%d" % u for u in range(5)],
     "kernels/ln.hip",
     "kernels/linear.hip",
     "kernels/lstm.hip",
@@ -68,7 +70,8 @@ CXX_SOURCES = [
     "comm/rccl_engine.cpp",
     "bindings.cpp",
 ]
-HEADERS = ["kernels/common.h", "kernels/gk_kernels.h", "kernels/mfma_util.h", "comm/rccl_engine.h"]
+HEADERS = ["kernels/common.h", "kernels/gk_kernels.h", "kernels/mfma_util.h", "kernels/gemm_kern.h",
+           "comm/rccl_engine.h"]
 # per-file extra flags: the sparse aggregation must round product and sum
 # separately (bit-identical to the reference arithmetic and the CPU mirror)
 EXTRA_FLAGS = {"kernels/scatter.hip": ["-ffp-contract=off"]}
@@ -137,13 +140,16 @@ def _digest(src: Path, flags: List[str]) -> str:
 
 
 def _compile(src_rel: str, kind: str, verbose: bool) -> Path:
+    # "<file>#<n>": instantiation unit n of a file compiled once per unit (-DGK_GEMM_UNIT=n)
+    src_rel, _, unit = src_rel.partition("#")
     src = CSRC / src_rel
     if kind == "hip":
         cc, flags = _hipcc(), _hip_flags()
     else:
         cc, flags = os.environ.get("CXX", "g++"), _cxx_flags()
-    flags = flags + EXTRA_FLAGS.get(src_rel, [])
-    obj = BUILD / (src_rel.replace("/", "_") + "." + _digest(src, flags) + ".o")
+    flags = flags + EXTRA_FLAGS.get(src_rel, []) + (["-DGK_GEMM_UNIT=" + unit] if unit else [])
+    tag = src_rel.replace("/", "_") + ("." + unit if unit else "")
+    obj = BUILD / (tag + "." + _digest(src, flags) + ".o")
     if obj.exists():
         return obj
     BUILD.mkdir(parents=True, exist_ok=True)
@@ -157,7 +163,9 @@ def _compile(src_rel: str, kind: str, verbose: bool) -> Path:
     return obj
 
 
-def build(verbose: bool = False, force: bool = False, jobs: int = 4) -> Path:
+def build(verbose: bool = False, force: bool = False, jobs: int = 0) -> Path:
+    # the GEMM units dominate (minutes each): one job per CPU, at most 8
+    jobs = jobs or min(8, os.cpu_count() or 4)
     if force and BUILD.exists():
         shutil.rmtree(BUILD)
     _, _, tlib = _torch_dirs()
@@ -199,7 +207,7 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("-v", "--verbose", action="store_true")
     ap.add_argument("--force", action="store_true")
-    ap.add_argument("-j", "--jobs", type=int, default=4)
+    ap.add_argument("-j", "--jobs", type=int, default=0)
     ap.add_argument("--asan", action="store_true", help="host ASan+UBSan variant under build/asan/ (re-execs)")
     args = ap.parse_args(argv)
     if args.asan and not ASAN:
