@@ -116,6 +116,10 @@ def parse():
                     help="world size the planner's cost models assume (default: this world)")
     ap.add_argument("--amp", default="none", choices=["bf16", "none"],
                     help="headline compute precision: none = fp32 (the reference's), bf16 = bf16 autocast")
+    ap.add_argument("--f32-matmul", default=os.environ.get("GKSGD_F32_MATMUL", "native"),
+                    choices=["native", "bf16x6"],
+                    help="fp32 convolution / linear GEMM algorithm: native = fp32 MFMA only; bf16x6 = also the "
+                         "fp32-accurate bf16x6 product kernels (ops/conv1x1.py set_f32_matmul)")
     ap.add_argument("--no-bf16-phase", action="store_true",
                     help="skip the secondary bf16 phase of an fp32 headline run")
     ap.add_argument("--no-dense-phase", action="store_true", help="skip the dense comparator at N > 1")
@@ -484,6 +488,8 @@ def main() -> int:
         args.threshold = DEFAULT_THRESHOLD.get(args.model, 524288000)
     ref_bs = REF_BATCH.get(args.model) if args.ref_batch is None else args.ref_batch
     amp = "bf16" if args.amp == "bf16" else "fp32"
+    from gaussiank_sgd_amd.ops import conv1x1
+    conv1x1.set_f32_matmul(args.f32_matmul)
 
     # ---- headline phase: any failure here is fatal (non-zero exit, no JSON line)
     ph = build(args, amp, args.dense, args.threshold, P, rank, args.batch_size)
@@ -545,6 +551,7 @@ def main() -> int:
             "exchange": kind,
             "momentum_correction": bool(opt._mc),
             "hip_graph": bool(args.graph),
+            "f32_matmul": args.f32_matmul if amp == "fp32" else None,
         },
         "graph_captures": getattr(ph.step, "captures", None),
         "world": P,

@@ -76,8 +76,48 @@ _TN_SMALL_M = 1 << 17
 _TN_SMALL_F32 = [(c, s) for c in (4, 5, 11, 14, 15) for s in (16, 32, 128)]
 
 
+# fp32 matmul algorithm (GKSGD_F32_MATMUL / set_f32_matmul):
+#   "native" -- fp32 operands on v_mfma_f32_16x16x4_f32 only;
+#   "bf16x6" -- the fp32 GEMM / implicit-GEMM candidates also include the bf16x6
+#   kernels (gemm_kern.h X6, cfg digit 100000): every fp32 operand split exactly
+#   into three bf16 parts, the six part products of order <= 2 accumulated in
+#   fp32 on v_mfma_f32_16x16x32_bf16 -- measured MORE accurate than the fp32
+#   MFMA against an fp64 reference on every ResNet-50 / BERT shape
+#   (bench/x6_probe.py, profiles/r05_x6_probe.json), so it is an fp32 algorithm,
+#   not a reduced precision; the tuner picks the faster kernel per shape.
+X6 = 100000
+_NT_CFGS_X6 = [c + X6 for c in (1, 2, 3, 4, 12, 13, 101, 102, 103, 104, 202, 203, 1001, 1002, 1003)]
+_F32MM = os.environ.get("GKSGD_F32_MATMUL", "native")
+
+
+def set_f32_matmul(mode: str) -> str:
+    """Select the fp32 matmul algorithm ("native" or "bf16x6"); returns the
+    previous one.  Autotune keys carry the mode, so each mode is tuned once."""
+    global _F32MM
+    if mode not in ("native", "bf16x6"):
+        raise ValueError("f32 matmul mode must be 'native' or 'bf16x6', got %r" % (mode,))
+    prev, _F32MM = _F32MM, mode
+    return prev
+
+
+def f32_matmul() -> str:
+    return _F32MM
+
+
+def _x6() -> bool:
+    return _F32MM == "bf16x6"
+
+
+def _tn_cfgs(dt: torch.dtype) -> List[Tuple[int, int]]:
+    if dt == torch.float32:
+        return _TN_CFGS_F32 + ([(c + X6, sp) for c, sp in _TN_CFGS_F32] if _x6() else [])
+    return _TN_CFGS
+
+
 def _nt_cfgs(dt: torch.dtype) -> List[int]:
-    return _NT_CFGS_F32 if dt == torch.float32 else _NT_CFGS
+    if dt == torch.float32:
+        return _NT_CFGS_F32 + (_NT_CFGS_X6 if _x6() else [])
+    return _NT_CFGS
 
 
 # fp32 split-K (cfg + 10000 S: S fp32 partial planes over K slices, then one
@@ -95,7 +135,8 @@ def _splitk_cfgs(dt: torch.dtype, M: int, N: int, K: int) -> List[int]:
     its output alone fills the chip)."""
     if dt != torch.float32 or M * N > _SPLITK_MAX_OUT:
         return []
-    return [c + 10000 * S for S in (2, 4, 8) if K % (64 * S) == 0 and K // S >= 128 for c in _SPLITK_BASE]
+    base = list(_SPLITK_BASE) + ([c + X6 for c in _SPLITK_BASE] if _x6() else [])
+    return [c + 10000 * S for S in (2, 4, 8) if K % (64 * S) == 0 and K // S >= 128 for c in base]
 
 
 # (the implicit-GEMM convolutions split the same way over their (tap, channel)
@@ -105,7 +146,9 @@ def _splitk_cfgs(dt: torch.dtype, M: int, N: int, K: int) -> List[int]:
 def _dkey(dt: torch.dtype) -> tuple:
     """Autotune key suffix: fp32 keys are tagged, bf16 keys keep their
     round-2 form so the shipped tuning cache stays valid."""
-    return ("f32",) if dt == torch.float32 else ()
+    if dt == torch.float32:
+        return ("f32", "x6") if _x6() else ("f32",)
+    return ()
 _zeros: Dict[torch.device, torch.Tensor] = {}
 
 
@@ -513,9 +556,11 @@ def _wgrad_into(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, s: int, out_
     else:
         z = _zero(x.device)
         run = lambda o, c, sp: g.conv_tn_acc(dy, x, o, z, s, p, c, sp, **kw)  # noqa: E731
-    tn = list(_TN_CFGS_F32 if dt == torch.float32 else _TN_CFGS)
+    tn = list(_tn_cfgs(dt))
     if dt == torch.float32 and N * OH * OW <= _TN_SMALL_M:
         tn += _TN_SMALL_F32   # small batches: more / fewer pixel splits than the two-rounds default
+        if _x6():
+            tn += [(c + X6, sp) for c, sp in _TN_SMALL_F32]
     cands = [(("hip", c, sp), (lambda c=c, sp=sp: run(scratch, c, sp))) for c, sp in tn]
     if lz is not None:
         cands.append((("mat", 0, 0), lambda: _wgrad_into(plink.materialize(), x, w, s, scratch)))

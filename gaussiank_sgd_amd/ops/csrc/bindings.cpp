@@ -1069,8 +1069,9 @@ int64_t gemm_nt(at::Tensor A, at::Tensor B, at::Tensor C, int64_t cfg, int64_t m
   gk::LazyArgs lz{};
   const bool has_lz = lazy_args(lz_x, lz_coef, lz_padz, lz_padx, A, K, &lz);
   c10::DeviceGuard guard(A.device());
-  // cfg >= 10000: split-K over S = cfg / 10000 fp32 partial planes (gemm.hip nt_splitk_reduce_kernel)
-  const int64_t S = cfg / 10000;
+  // cfg digit 10000: split-K over S = (cfg / 10000) % 10 fp32 partial planes (gemm.hip nt_splitk_reduce_kernel);
+  // digit 100000: fp32 operands multiplied as bf16x6 products (gemm_kern.h X6)
+  const int64_t S = (cfg / 10000) % 10;
   at::Tensor ws;
   if (S > 1) {
     TORCH_CHECK(A.scalar_type() == at::kFloat && !has_lz && S <= 16 && K % (64 * S) == 0,
@@ -1145,8 +1146,8 @@ int64_t conv_nt(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor zero, int64
   gk::LazyArgs lz{};
   const bool has_lz = lazy_args(lz_x, lz_coef, lz_padz, lz_padx, x, C, &lz);
   c10::DeviceGuard guard(x.device());
-  // cfg >= 10000: split-K over S = cfg / 10000 fp32 partial planes of the (tap, channel) slices
-  const int64_t S = cfg / 10000;
+  // cfg digit 10000: split-K over S = (cfg / 10000) % 10 fp32 partial planes of the (tap, channel) slices
+  const int64_t S = (cfg / 10000) % 10;
   at::Tensor ws;
   if (S > 1) {
     TORCH_CHECK(x.scalar_type() == at::kFloat && !has_lz && S <= 16 && C % 32 == 0 && (KH * KW * C / 32) % S == 0,

@@ -34,8 +34,20 @@ static int nt_unit_b16(bool gather, GK_NT_UNIT_ARGS) {
   return gather ? nt_b16_gat(GK_NT_UNIT_PASS) : nt_b16_row(GK_NT_UNIT_PASS);
 }
 
+// fp32 operands: cfg digit 100000 selects the bf16x6 products (gemm_kern.h X6)
 static int nt_unit_f32(bool gather, GK_NT_UNIT_ARGS) {
+  const bool x6 = (cfg / 100000) % 10 == 1;
+  cfg %= 100000;
+  if (x6) return gather ? nt_x6_gat(GK_NT_UNIT_PASS) : nt_x6_row(GK_NT_UNIT_PASS);
   return gather ? nt_f32_gat(GK_NT_UNIT_PASS) : nt_f32_row(GK_NT_UNIT_PASS);
+}
+
+// fp32 grad-weight: cfg digit 100000 selects the bf16x6 products
+static void tn_unit_f32x(bool gather, const float* G, int64_t ldg, const float* X, int64_t ldx, float* W, int64_t ldw,
+                         int64_t M, int N, int K, int cfg, int splits, const ConvGeo& geo, const LazyArgs* lza,
+                         hipStream_t stream) {
+  if ((cfg / 100000) % 10 == 1) tn_unit_x6(gather, G, ldg, X, ldx, W, ldw, M, N, K, cfg % 100000, splits, geo, lza, stream);
+  else tn_unit_f32(gather, G, ldg, X, ldx, W, ldw, M, N, K, cfg % 100000, splits, geo, lza, stream);
 }
 
 bool gemm_supported(int64_t N, int64_t K) { return N >= 64 && K >= 64 && N % 64 == 0 && K % 64 == 0; }
@@ -130,14 +142,15 @@ int gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int
   g.bias = bias;
   const BnBwd bb = bn ? BnBwd{bn->h, bn->dy2, bn->mask} : BnBwd{};
   const int64_t sld = (int64_t)stats_rows * N;
-  const int S = cfg / 10000;
+  const int S = (cfg / 10000) % 10;
+  const int x6 = cfg / 100000 * 100000;   // bf16x6 digit, kept for the split-K planes
   if (S > 1) {
     // split-K (fp32 row GEMM, host-checked: K % (64 S) == 0, no lazy operand):
     // KZ plain partial planes into splitk_ws [S][M][N], then the reduce epilogue
     if (!f32 || lazy || splitk_ws == nullptr || K % (64 * S) != 0) return -1;
     ConvGeo gz{};
     gz.KZ = S;
-    const int r = nt_unit_f32(false, A, lda, B, ldb, splitk_ws, N, M, N, K / S, cfg % 10000, max_blocks, gz,
+    const int r = nt_unit_f32(false, A, lda, B, ldb, splitk_ws, N, M, N, K / S, x6 + cfg % 10000, max_blocks, gz,
                                             nullptr, 0, 0, BnBwd{}, nullptr, stream);
     if (r < 0) return r;
     return splitk_reduce(splitk_ws, S, M, N, static_cast<float*>(C), ldc, bias, stats, stats_rows, bn, stream);
@@ -151,14 +164,15 @@ int conv_nt(const void* X, const void* zero, int H, int W, int C, int OH, int OW
             const float* bias, const BnBwdArgs* bn, const LazyArgs* lazy, hipStream_t stream, float* splitk_ws) {
   ConvGeo g{zero, H, W, C, OH, OW, S, P, KW, bias};
   const int K = KH * KW * C;
-  const int SK = cfg / 10000;
+  const int SK = (cfg / 10000) % 10;
+  const int x6 = cfg / 100000 * 100000;
   if (SK > 1) {
     // split-K over the (tap, channel) slices: plain partial planes, then the reduce epilogue
     const int nks = K / 32;   // fp32 K slices
     if (!f32 || lazy || splitk_ws == nullptr || nks % SK != 0 || C % 32 != 0) return -1;
     ConvGeo gz{zero, H, W, C, OH, OW, S, P, KW, nullptr};
     gz.KZ = SK;
-    const int r = nt_unit_f32(true, X, C, B, K, splitk_ws, N, M, N, K / SK, cfg % 10000, max_blocks, gz,
+    const int r = nt_unit_f32(true, X, C, B, K, splitk_ws, N, M, N, K / SK, x6 + cfg % 10000, max_blocks, gz,
                                            nullptr, 0, 0, BnBwd{}, nullptr, stream);
     if (r < 0) return r;
     return splitk_reduce(splitk_ws, SK, M, N, static_cast<float*>(Y), N, bias, stats, stats_rows, bn, stream);
@@ -185,7 +199,7 @@ int conv_nt_remap(const void* X, int64_t ldx, const void* zero, int H, int W, in
 void gemm_tn_acc(const void* G, int64_t ldg, const void* X, int64_t ldx, float* W, int64_t ldw, int64_t M, int N,
                  int K, bool f32, int cfg, int splits, const LazyArgs* lazy, hipStream_t stream) {
   if (f32)
-    tn_unit_f32(false, static_cast<const float*>(G), ldg, static_cast<const float*>(X), ldx, W, ldw, M, N, K, cfg,
+    tn_unit_f32x(false, static_cast<const float*>(G), ldg, static_cast<const float*>(X), ldx, W, ldw, M, N, K, cfg,
                            splits, ConvGeo{}, lazy, stream);
   else
     tn_unit_b16(false, G, ldg, X, ldx, W, ldw, M, N, K, cfg, splits, ConvGeo{}, stream);
@@ -197,7 +211,7 @@ void conv_tn_acc(const void* G, const void* X, const void* zero, int H, int W_, 
   ConvGeo g{zero, H, W_, C, OH, OW, S, P, KW, nullptr};
   const int K = KH * KW * C;
   if (f32)
-    tn_unit_f32(true, static_cast<const float*>(G), N, static_cast<const float*>(X), C, Wout, K, M, N, K, cfg,
+    tn_unit_f32x(true, static_cast<const float*>(G), N, static_cast<const float*>(X), C, Wout, K, M, N, K, cfg,
                           splits, g, lazy, stream);
   else
     tn_unit_b16(true, G, N, X, C, Wout, K, M, N, K, cfg, splits, g, stream);

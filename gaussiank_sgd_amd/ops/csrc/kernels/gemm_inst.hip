@@ -29,6 +29,17 @@ void tn_unit_f32(bool gather, const float* G, int64_t ldg, const float* X, int64
   if (gather) tn_f32_dispatch<true>(G, ldg, X, ldx, W, ldw, M, N, K, cfg, splits, geo, lza, stream);
   else tn_f32_dispatch<false>(G, ldg, X, ldx, W, ldw, M, N, K, cfg, splits, geo, lza, stream);
 }
+#elif GK_GEMM_UNIT == 5
+int nt_x6_row(GK_NT_UNIT_ARGS) { return nt_dispatch<false, float, true>(GK_NT_UNIT_PASS); }
+#elif GK_GEMM_UNIT == 6
+int nt_x6_gat(GK_NT_UNIT_ARGS) { return nt_dispatch<true, float, true>(GK_NT_UNIT_PASS); }
+#elif GK_GEMM_UNIT == 7
+void tn_unit_x6(bool gather, const float* G, int64_t ldg, const float* X, int64_t ldx, float* W, int64_t ldw,
+                int64_t M, int N, int K, int cfg, int splits, const ConvGeo& geo, const LazyArgs* lza,
+                hipStream_t stream) {
+  if (gather) tn_f32_dispatch<true, true>(G, ldg, X, ldx, W, ldw, M, N, K, cfg, splits, geo, lza, stream);
+  else tn_f32_dispatch<false, true>(G, ldg, X, ldx, W, ldw, M, N, K, cfg, splits, geo, lza, stream);
+}
 #else
 #error "unknown GK_GEMM_UNIT"
 #endif

@@ -103,6 +103,12 @@ int nt_b16_row(GK_NT_UNIT_ARGS);   // unit 0
 int nt_b16_gat(GK_NT_UNIT_ARGS);   // unit 1
 int nt_f32_row(GK_NT_UNIT_ARGS);   // unit 2
 int nt_f32_gat(GK_NT_UNIT_ARGS);   // unit 3
+int nt_x6_row(GK_NT_UNIT_ARGS);    // unit 5: fp32 operands, bf16x6 products
+int nt_x6_gat(GK_NT_UNIT_ARGS);    // unit 6
+// unit 7: fp32 grad-weight (TN) GEMMs with bf16x6 products
+void tn_unit_x6(bool gather, const float* G, int64_t ldg, const float* X, int64_t ldx, float* W, int64_t ldw,
+                int64_t M, int N, int K, int cfg, int splits, const ConvGeo& geo, const LazyArgs* lza,
+                hipStream_t stream);
 // unit 4: grad-weight (TN) GEMMs, both operand types and forms
 void tn_unit_b16(bool gather, const void* G, int64_t ldg, const void* X, int64_t ldx, float* W, int64_t ldw, int64_t M,
                  int N, int K, int cfg, int splits, const ConvGeo& geo, hipStream_t stream);
@@ -196,7 +202,7 @@ struct NtCfg {
 };
 
 template <int WM, int WN, bool BRES, int NS, bool GATHER, int MSB = 4, bool BNB = false, typename T = uint16_t,
-          bool LZ = false>
+          bool LZ = false, bool X6 = false>
 __global__ void __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(WM * WN >= 8 ? 1 : 2)))
 gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
                T* __restrict__ C, int64_t ldc, int64_t M, int K, ConvGeo geo, float* __restrict__ stats,
@@ -210,6 +216,7 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
   using E = Elem<T>;
   constexpr bool F32 = E::F32;
   static_assert(!LZ || F32, "lazy BN operand: fp32 kernels");
+  static_assert(!X6 || F32, "bf16x6 products: fp32 operands");
   constexpr int EPC = E::EPC;
   constexpr int KS = E::KS;
   static_assert(!BNB || MSB == 4 || F32, "bf16 BN-backward epilogue: 64x64 wave tiles");
@@ -555,6 +562,40 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
     } else {
 #pragma unroll
       for (int kk = 0; kk < NBB; ++kk) ldB(kk, bv[kk]);
+      if constexpr (X6) {
+        // fp32-accurate products on the bf16 matrix cores: every fp32 operand
+        // is split exactly into bf16 parts x = hi + mid + lo (split3x8) and the
+        // six part products of order <= 2 -- all but mid*lo, lo*mid, lo*lo,
+        // each < 2^-24 |a b| -- are accumulated in fp32.  Lane (fr, fq) holds
+        // K elements 4 fq + 0..3 (half 0) and 16 + 4 fq + 0..3 (half 1) of its
+        // row, the same permutation on both operands.  One K slice = one
+        // 16x16x32 bf16 step: 6 x 16 cycles against 8 x 32 for the fp32 MFMA.
+        bf16x8 bh[4], bm[4], bl[4];
+#pragma unroll
+        for (int ns = 0; ns < 4; ++ns) split3x8(bv[0][ns], bv[1][ns], bh[ns], bm[ns], bl[ns]);
+        Frag a0n = ldA(0, 0), a1n = ldA(1, 0);
+#pragma unroll
+        for (int ms = 0; ms < MSB; ++ms) {
+          bf16x8 ah, am, al;
+          split3x8(a0n, a1n, ah, am, al);
+          if (ms + 1 < MSB) {
+            a0n = ldA(0, ms + 1);
+            a1n = ldA(1, ms + 1);
+          }
+#pragma unroll
+          for (int ns = 0; ns < 4; ++ns) {
+            f32x4 c = acc[ms][ns];
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[ns], ah, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[ns], al, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm[ns], am, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm[ns], ah, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[ns], am, c, 0, 0, 0);
+            acc[ms][ns] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[ns], ah, c, 0, 0, 0);
+          }
+          issue_group(2 * ms);
+          issue_group(2 * ms + 1);
+        }
+      } else {
       Frag an = ldA(0, 0);
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
@@ -578,6 +619,7 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
           }
           issue_group(kk * MSB + ms);
         }
+      }
       }
     }
     if (pf) stage_advance();
@@ -797,7 +839,7 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
 }
 
 template <int WM, int WN, bool BRES, int NS, bool GATHER, int MSB = 4, bool BNB = false, typename T = uint16_t,
-          bool LZ = false>
+          bool LZ = false, bool X6 = false>
 int launch_nt(const T* A, int64_t lda, const T* B, int64_t ldb, T* C, int64_t ldc, int64_t M,
               int N, int K, int max_blocks, const ConvGeo& geo, float* stats, int64_t stats_ld, int stats_rows,
               const BnBwd& bb, const LazyA& lz, hipStream_t stream) {
@@ -814,16 +856,17 @@ int launch_nt(const T* A, int64_t lda, const T* B, int64_t ldb, T* C, int64_t ld
   if (stats && gx > stats_rows) gx = stats_rows;   // one partial row per block
   dim3 grid((unsigned)gx, (unsigned)ntiles, (unsigned)kz);
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<WM, WN, BRES, NS, GATHER, MSB, BNB, T, LZ>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<WM, WN, BRES, NS, GATHER, MSB, BNB, T, LZ, X6>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL((gemm_nt_kernel<WM, WN, BRES, NS, GATHER, MSB, BNB, T, LZ>), grid, dim3(Cfg::THREADS), lds, stream,
+  hipLaunchKernelGGL((gemm_nt_kernel<WM, WN, BRES, NS, GATHER, MSB, BNB, T, LZ, X6>), grid, dim3(Cfg::THREADS), lds, stream,
                      A, lda, B, ldb, C, ldc, M, K, geo, stats, stats_ld, bb, lz);
   return (int)gx;
 }
 
-template <int WM, int WN, bool GATHER, int MSB = 4, bool BNB = false, typename T = uint16_t, bool LZ = false>
+template <int WM, int WN, bool GATHER, int MSB = 4, bool BNB = false, typename T = uint16_t, bool LZ = false,
+          bool X6 = false>
 int launch_nt_any(const T* A, int64_t lda, const T* B, int64_t ldb, T* C, int64_t ldc,
                   int64_t M, int N, int K, int max_blocks, int bres, int ns, const ConvGeo& geo, float* stats,
                   int64_t stats_ld, int stats_rows, const BnBwd& bb, const LazyA& lz, hipStream_t stream) {
@@ -835,7 +878,7 @@ int launch_nt_any(const T* A, int64_t lda, const T* B, int64_t ldb, T* C, int64_
   if (bres && CR::lds_bytes(K, 2, cc) > 160 * 1024) bres = 0;
   constexpr int L = 160 * 1024;
 #define GK_NT(BR, S) \
-  launch_nt<WM, WN, BR, S, GATHER, MSB, BNB, T, LZ>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, bb, lz, stream)
+  launch_nt<WM, WN, BR, S, GATHER, MSB, BNB, T, LZ, X6>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, bb, lz, stream)
   if (ns == 4 && bres && CR::NS4_OK && CR::lds_bytes(K, 4, cc) <= L) return GK_NT(true, 4);
   if (ns == 4 && !bres && CS::NS4_OK && CS::lds_bytes(K, 4, cc) <= L) return GK_NT(false, 4);
   if (bres) {
@@ -1235,7 +1278,7 @@ struct TnF32Cfg {
 
 __device__ __forceinline__ int swz4(int r) { return r & 4; }
 
-template <int WN, int WK, int NS, bool GATHER, bool LZ = false>
+template <int WN, int WK, int NS, bool GATHER, bool LZ = false, bool X6 = false>
 __global__ void __launch_bounds__(64 * WN * WK) __attribute__((amdgpu_waves_per_eu(1)))
 gemm_tn_f32_kernel(const float* __restrict__ G, int64_t ldg, const float* __restrict__ X, int64_t ldx,
                    float* __restrict__ W, int64_t ldw, int64_t M, int64_t rows_per_split, ConvGeo geo, LazyA lz) {
@@ -1388,6 +1431,35 @@ gemm_tn_f32_kernel(const float* __restrict__ G, int64_t ldg, const float* __rest
         }
       }
     };
+    if constexpr (X6) {
+      // bf16x6 products (gemm_nt_kernel X6): the lane's 8 rows {16 kg + 4 fg + j}
+      // of a column form one 16x16x32 bf16 operand (the same row permutation on
+      // G and X), split exactly into hi + mid + lo parts
+      load(0, gv[0], xv[0]);
+      load(1, gv[1], xv[1]);
+      bf16x8 gh[4], gm[4], gl[4];
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2)
+        split3x8(f32x4{gv[0][0][s2], gv[0][1][s2], gv[0][2][s2], gv[0][3][s2]},
+                 f32x4{gv[1][0][s2], gv[1][1][s2], gv[1][2][s2], gv[1][3][s2]}, gh[s2], gm[s2], gl[s2]);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        bf16x8 xh, xm, xl;
+        split3x8(f32x4{xv[0][0][ks], xv[0][1][ks], xv[0][2][ks], xv[0][3][ks]},
+                 f32x4{xv[1][0][ks], xv[1][1][ks], xv[1][2][ks], xv[1][3][ks]}, xh, xm, xl);
+#pragma unroll
+        for (int ns = 0; ns < 4; ++ns) {
+          f32x4 c = acc[ns][ks];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gl[ns], xh, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gh[ns], xl, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gm[ns], xm, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gm[ns], xh, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gh[ns], xm, c, 0, 0, 0);
+          acc[ns][ks] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gh[ns], xh, c, 0, 0, 0);
+        }
+      }
+      continue;
+    }
     load(0, gv[0], xv[0]);
 #pragma unroll
     for (int kg = 0; kg < Cfg::ROWS / 16; ++kg) {
@@ -1415,7 +1487,7 @@ gemm_tn_f32_kernel(const float* __restrict__ G, int64_t ldg, const float* __rest
     }
 }
 
-template <int WN, int WK, int NS, bool GATHER, bool LZ = false>
+template <int WN, int WK, int NS, bool GATHER, bool LZ = false, bool X6 = false>
 void launch_tn_f32(const float* G, int64_t ldg, const float* X, int64_t ldx, float* W, int64_t ldw, int64_t M, int N,
                    int K, int splits, const ConvGeo& geo, const LazyA& lz, hipStream_t stream) {
   using Cfg = TnF32Cfg<WN, WK, NS, LZ>;
@@ -1440,15 +1512,15 @@ void launch_tn_f32(const float* G, int64_t ldg, const float* X, int64_t ldx, flo
   const int64_t nsplit = (M + rows - 1) / rows;
   dim3 grid((unsigned)(N / Cfg::BN), (unsigned)(K / Cfg::BK), (unsigned)nsplit);
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_f32_kernel<WN, WK, NS, GATHER, LZ>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_f32_kernel<WN, WK, NS, GATHER, LZ, X6>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL((gemm_tn_f32_kernel<WN, WK, NS, GATHER, LZ>), grid, dim3(Cfg::THREADS), Cfg::LDS, stream, G, ldg,
+  hipLaunchKernelGGL((gemm_tn_f32_kernel<WN, WK, NS, GATHER, LZ, X6>), grid, dim3(Cfg::THREADS), Cfg::LDS, stream, G, ldg,
                      X, ldx, W, ldw, M, rows, geo, lz);
 }
 
-template <bool GATHER>
+template <bool GATHER, bool X6 = false>
 void tn_f32_dispatch(const float* G, int64_t ldg, const float* X, int64_t ldx, float* W, int64_t ldw, int64_t M, int N,
                      int K, int cfg, int splits, const ConvGeo& geo, const LazyArgs* lza, hipStream_t stream) {
   // cfg = tile + 10 * stages (0/2: three, 1: two).  tiles (WN, WK), 64x64 per wave:
@@ -1464,13 +1536,13 @@ void tn_f32_dispatch(const float* G, int64_t ldg, const float* X, int64_t ldx, f
   do {                                                                                                        \
     if (lza) {                                                                                                \
       if (ns3 && TnF32Cfg<WN_, WK_, 3, true>::LDS <= 160 * 1024)                                              \
-        launch_tn_f32<WN_, WK_, 3, GATHER, true>(G, ldg, X, ldx, W, ldw, M, N, K, splits, geo, lz, stream);   \
+        launch_tn_f32<WN_, WK_, 3, GATHER, true, X6>(G, ldg, X, ldx, W, ldw, M, N, K, splits, geo, lz, stream);   \
       else                                                                                                    \
-        launch_tn_f32<WN_, WK_, 2, GATHER, true>(G, ldg, X, ldx, W, ldw, M, N, K, splits, geo, lz, stream);   \
+        launch_tn_f32<WN_, WK_, 2, GATHER, true, X6>(G, ldg, X, ldx, W, ldw, M, N, K, splits, geo, lz, stream);   \
     } else if (ns3 && TnF32Cfg<WN_, WK_, 3>::LDS <= 160 * 1024)                                               \
-      launch_tn_f32<WN_, WK_, 3, GATHER>(G, ldg, X, ldx, W, ldw, M, N, K, splits, geo, lz, stream);           \
+      launch_tn_f32<WN_, WK_, 3, GATHER, false, X6>(G, ldg, X, ldx, W, ldw, M, N, K, splits, geo, lz, stream);           \
     else                                                                                                      \
-      launch_tn_f32<WN_, WK_, 2, GATHER>(G, ldg, X, ldx, W, ldw, M, N, K, splits, geo, lz, stream);           \
+      launch_tn_f32<WN_, WK_, 2, GATHER, false, X6>(G, ldg, X, ldx, W, ldw, M, N, K, splits, geo, lz, stream);           \
   } while (0)
   switch (cfg) {
     case 2: GK_TNF(2, 1); break;
@@ -1484,9 +1556,9 @@ void tn_f32_dispatch(const float* G, int64_t ldg, const float* X, int64_t ldx, f
       if (lza) {
         GK_TNF(2, 4);   // the lazy 256x256 tile does not fit in LDS
       } else if (ns3 && TnF32Cfg<4, 4, 3>::LDS <= 160 * 1024) {
-        launch_tn_f32<4, 4, 3, GATHER>(G, ldg, X, ldx, W, ldw, M, N, K, splits, geo, lz, stream);
+        launch_tn_f32<4, 4, 3, GATHER, false, X6>(G, ldg, X, ldx, W, ldw, M, N, K, splits, geo, lz, stream);
       } else {
-        launch_tn_f32<4, 4, 2, GATHER>(G, ldg, X, ldx, W, ldw, M, N, K, splits, geo, lz, stream);
+        launch_tn_f32<4, 4, 2, GATHER, false, X6>(G, ldg, X, ldx, W, ldw, M, N, K, splits, geo, lz, stream);
       }
       break;
     default: GK_TNF(1, 1); break;
@@ -1494,7 +1566,7 @@ void tn_f32_dispatch(const float* G, int64_t ldg, const float* X, int64_t ldx, f
 #undef GK_TNF
 }
 
-template <bool GATHER, typename T>
+template <bool GATHER, typename T, bool X6 = false>
 int nt_dispatch(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N,
                 int K, int cfg, int max_blocks, const ConvGeo& geo, float* stats, int64_t stats_ld, int stats_rows,
                 const BnBwd& bb, const LazyArgs* lza, hipStream_t stream) {
@@ -1518,7 +1590,7 @@ int nt_dispatch(const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
   if (cfg > 7 || N % cfg_bn[cfg] != 0) cfg = 1;   // the tile must divide N (B rows are not clamped)
   const LazyA lz = lza ? LazyA{lza->x, lza->coef, lza->padz, lza->padx, lza->C} : LazyA{};
 #define GK_NTA(WM_, WN_, MSB_, BNB_, LZ_) \
-  return launch_nt_any<WM_, WN_, GATHER, MSB_, BNB_, T, LZ_>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, bb, lz, stream)
+  return launch_nt_any<WM_, WN_, GATHER, MSB_, BNB_, T, LZ_, X6>(a, lda, b, ldb, c, ldc, M, N, K, max_blocks, bres, ns, geo, stats, stats_ld, stats_rows, bb, lz, stream)
   if constexpr (sizeof(T) == 4) {
     if (lza) {   // lazy BN-backward A operand (fp32)
       if (bb.h) {

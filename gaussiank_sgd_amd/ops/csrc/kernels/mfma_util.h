@@ -22,6 +22,31 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{lo, hi}, bf16x2_t));
 }
 
+// Exact split of eight fp32 values (x0: elements 0-3, x1: 4-7) into bf16 parts
+// x = hi + mid + lo, each part the round-to-nearest-even bf16 of the residual
+// left by the previous ones: the residuals are exact in fp32 (|x - hi| <=
+// 2^-8 |x|, |x - hi - mid| <= 2^-16 |x|), so the three parts hold all 24
+// mantissa bits.  Products of parts are exact in fp32 (8 x 8 significant bits).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void split3x8(const f32x4& x0, const f32x4& x1, bf16x8& hi, bf16x8& mid, bf16x8& lo) {
+  u32x4 h, m, l;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const float a = p < 2 ? x0[2 * p] : x1[2 * p - 4];
+    const float b = p < 2 ? x0[2 * p + 1] : x1[2 * p - 3];
+    const uint32_t hp = pack_bf16x2(a, b);
+    const float ra = a - __uint_as_float(hp << 16), rb = b - __uint_as_float(hp & 0xffff0000u);
+    const uint32_t mp = pack_bf16x2(ra, rb);
+    const float sa = ra - __uint_as_float(mp << 16), sb = rb - __uint_as_float(mp & 0xffff0000u);
+    h[p] = hp;
+    m[p] = mp;
+    l[p] = pack_bf16x2(sa, sb);
+  }
+  hi = __builtin_bit_cast(bf16x8, h);
+  mid = __builtin_bit_cast(bf16x8, m);
+  lo = __builtin_bit_cast(bf16x8, l);
+}
+
 __device__ __forceinline__ void glds16(const void* src, GK_LDS void* dst) {
   __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
 }

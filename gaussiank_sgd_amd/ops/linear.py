@@ -151,7 +151,7 @@ def _wgrad_into(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor) -> None:
     cands = []
     if _hip_gemm_ok(K, N):
         cands = [(("hip", c, sp), (lambda c=c, sp=sp: g.gemm_tn_acc(dy2, x2, scratch, c, sp)))
-                 for c, sp in (_cv._TN_CFGS_F32 if f32 else _cv._TN_CFGS)]
+                 for c, sp in _cv._tn_cfgs(torch.float32 if f32 else torch.bfloat16)]
     cands.append((("blas32", 0, 0), lambda: blas32(scratch)))
     cands.append((("blas", 0, 0), lambda: blas(scratch)))
     ch = _cv._pick(key, cands)
