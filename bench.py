@@ -116,7 +116,7 @@ def parse():
                     help="world size the planner's cost models assume (default: this world)")
     ap.add_argument("--amp", default="none", choices=["bf16", "none"],
                     help="headline compute precision: none = fp32 (the reference's), bf16 = bf16 autocast")
-    ap.add_argument("--f32-matmul", default=os.environ.get("GKSGD_F32_MATMUL", "native"),
+    ap.add_argument("--f32-matmul", default=os.environ.get("GKSGD_F32_MATMUL", "bf16x6"),
                     choices=["native", "bf16x6"],
                     help="fp32 convolution / linear GEMM algorithm: native = fp32 MFMA only; bf16x6 = also the "
                          "fp32-accurate bf16x6 product kernels (ops/conv1x1.py set_f32_matmul)")

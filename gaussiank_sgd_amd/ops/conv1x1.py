@@ -86,7 +86,7 @@ _TN_SMALL_F32 = [(c, s) for c in (4, 5, 11, 14, 15) for s in (16, 32, 128)]
 #   (bench/x6_probe.py, profiles/r05_x6_probe.json), so it is an fp32 algorithm,
 #   not a reduced precision; the tuner picks the faster kernel per shape.
 X6 = 100000
-_NT_CFGS_X6 = [c + X6 for c in (1, 2, 3, 4, 12, 13, 101, 102, 103, 104, 202, 203, 1001, 1002, 1003)]
+_NT_CFGS_X6 = [c + X6 for c in (1, 2, 3, 4, 5, 6, 7, 12, 13, 101, 102, 103, 104, 105, 106, 107, 202, 203, 1001, 1002, 1003)]
 _F32MM = os.environ.get("GKSGD_F32_MATMUL", "native")
 
 

@@ -31,6 +31,10 @@
 //   Each block reduces a contiguous slice of M for one output tile and adds
 //   its fp32 partial into the (gradient-arena) output with float atomics.
 #pragma once
+
+#ifndef GK_X6_EXP
+#define GK_X6_EXP 0   // bf16x6 kernel experiments (variant builds only)
+#endif
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
@@ -192,7 +196,8 @@ struct NtCfg {
   static_assert((BM / 8) % NW == 0, "A rows split evenly over the waves");
   static constexpr int LPWA = BRES ? LPW : NACOPY * (BM / 8) / NW;   // of which A-row instructions (j < LPWA)
   static constexpr int NST = Elem<T>::ST_PER_SUB * MSB;     // 16-byte epilogue stores per wave per tile
-  static_assert(LPW + 2 * NST <= 63, "wait_vmcnt range (vmcnt is 6 bits)");
+  static_assert(NST <= 63, "wait_vmcnt range (vmcnt is 6 bits)");
+  static constexpr bool NS3_OK = LPW + 2 * NST <= 63;       // three stages: 1 stage + 2 tiles of stores in flight
   static constexpr bool NS4_OK = 2 * LPW + 3 * NST <= 63;   // four stages: 2 stages + 3 tiles of stores in flight
   // LDS: [lazy coefficient table][resident weight panel][stages]
   __host__ __device__ static int coef_bytes(int C) { return LZ ? ((C * 16 + 1023) / 1024) * 1024 : 0; }
@@ -220,7 +225,8 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
   constexpr int EPC = E::EPC;
   constexpr int KS = E::KS;
   static_assert(!BNB || MSB == 4 || F32, "bf16 BN-backward epilogue: 64x64 wave tiles");
-  static_assert(!F32 || MSB == 4 || MSB == 2, "fp32: 64x64 or 32x64 wave tiles");
+  static_assert(!F32 || MSB == 4 || MSB == 2 || (X6 && MSB == 8), "fp32: 64x64 or 32x64 wave tiles (bf16x6: 128x64)");
+  static_assert(NS == 2 || (NS == 3 && Cfg::NS3_OK) || (NS == 4 && Cfg::NS4_OK), "wait_vmcnt range (vmcnt is 6 bits)");
   constexpr bool bnb = BNB;
   static_assert(NS >= 2 && NS <= 4, "stages");
   constexpr int LPW = Cfg::LPW;
@@ -572,12 +578,26 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
         // 16x16x32 bf16 step: 6 x 16 cycles against 8 x 32 for the fp32 MFMA.
         bf16x8 bh[4], bm[4], bl[4];
 #pragma unroll
-        for (int ns = 0; ns < 4; ++ns) split3x8(bv[0][ns], bv[1][ns], bh[ns], bm[ns], bl[ns]);
+        for (int ns = 0; ns < 4; ++ns) {
+#if GK_X6_EXP == 1
+          bh[ns] = __builtin_bit_cast(bf16x8, f32x4{bv[0][ns][0], bv[0][ns][1], bv[1][ns][0], bv[1][ns][1]});
+          bm[ns] = __builtin_bit_cast(bf16x8, f32x4{bv[0][ns][2], bv[0][ns][3], bv[1][ns][2], bv[1][ns][3]});
+          bl[ns] = bh[ns];
+#else
+          split3x8(bv[0][ns], bv[1][ns], bh[ns], bm[ns], bl[ns]);
+#endif
+        }
         Frag a0n = ldA(0, 0), a1n = ldA(1, 0);
 #pragma unroll
         for (int ms = 0; ms < MSB; ++ms) {
           bf16x8 ah, am, al;
+#if GK_X6_EXP == 1   // experiment: bit-slice instead of the exact split (VALU cost probe)
+          ah = __builtin_bit_cast(bf16x8, f32x4{a0n[0], a0n[1], a1n[0], a1n[1]});
+          am = __builtin_bit_cast(bf16x8, f32x4{a0n[2], a0n[3], a1n[2], a1n[3]});
+          al = ah;
+#else
           split3x8(a0n, a1n, ah, am, al);
+#endif
           if (ms + 1 < MSB) {
             a0n = ldA(0, ms + 1);
             a1n = ldA(1, ms + 1);
@@ -585,11 +605,13 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
 #pragma unroll
           for (int ns = 0; ns < 4; ++ns) {
             f32x4 c = acc[ms][ns];
+#if GK_X6_EXP != 2   // experiment 2: one product only (data-movement probe)
             c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[ns], ah, c, 0, 0, 0);
             c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[ns], al, c, 0, 0, 0);
             c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm[ns], am, c, 0, 0, 0);
             c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm[ns], ah, c, 0, 0, 0);
             c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[ns], am, c, 0, 0, 0);
+#endif
             acc[ms][ns] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[ns], ah, c, 0, 0, 0);
           }
           issue_group(2 * ms);
@@ -879,13 +901,17 @@ int launch_nt_any(const T* A, int64_t lda, const T* B, int64_t ldb, T* C, int64_
   constexpr int L = 160 * 1024;
 #define GK_NT(BR, S) \
   launch_nt<WM, WN, BR, S, GATHER, MSB, BNB, T, LZ, X6>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, geo, stats, stats_ld, stats_rows, bb, lz, stream)
-  if (ns == 4 && bres && CR::NS4_OK && CR::lds_bytes(K, 4, cc) <= L) return GK_NT(true, 4);
-  if (ns == 4 && !bres && CS::NS4_OK && CS::lds_bytes(K, 4, cc) <= L) return GK_NT(false, 4);
+  if constexpr (CR::NS4_OK)
+    if (ns == 4 && bres && CR::lds_bytes(K, 4, cc) <= L) return GK_NT(true, 4);
+  if constexpr (CS::NS4_OK)
+    if (ns == 4 && !bres && CS::lds_bytes(K, 4, cc) <= L) return GK_NT(false, 4);
   if (bres) {
-    if (ns != 2 && CR::lds_bytes(K, 3, cc) <= L) return GK_NT(true, 3);
+    if constexpr (CR::NS3_OK)
+      if (ns != 2 && CR::lds_bytes(K, 3, cc) <= L) return GK_NT(true, 3);
     return GK_NT(true, 2);
   }
-  if (ns != 2 && CS::lds_bytes(K, 3, cc) <= L) return GK_NT(false, 3);
+  if constexpr (CS::NS3_OK)
+    if (ns != 2 && CS::lds_bytes(K, 3, cc) <= L) return GK_NT(false, 3);
   if (CS::lds_bytes(K, 2, cc) > L) return -1;   // does not fit (lazy coefficient table too large)
   return GK_NT(false, 2);
 #undef GK_NT
@@ -1647,6 +1673,14 @@ int nt_dispatch(const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
     }
   }
   if constexpr (sizeof(T) == 4) {
+    if constexpr (X6) {   // bf16x6: 128x64 wave tiles (fewer operand splits and LDS reads per product)
+      switch (cfg) {
+        case 5: GK_NTA(2, 4, 8, false, false);
+        case 6: GK_NTA(2, 2, 8, false, false);
+        case 7: GK_NTA(1, 4, 8, false, false);
+        default: break;
+      }
+    }
     switch (cfg) {
       case 2: GK_NTA(4, 2, 4, false, false);
       case 3: case 5: GK_NTA(2, 4, 4, false, false);
