@@ -32,6 +32,9 @@
 //   its fp32 partial into the (gradient-arena) output with float atomics.
 #pragma once
 
+#ifndef GK_X6_SCHED
+#define GK_X6_SCHED 1   // software-pipelined bf16x6 loop (0: the first form, A/B builds)
+#endif
 #ifndef GK_X6_EXP
 #define GK_X6_EXP 0   // bf16x6 kernel experiments (variant builds only)
 #endif
@@ -577,6 +580,65 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
         // row, the same permutation on both operands.  One K slice = one
         // 16x16x32 bf16 step: 6 x 16 cycles against 8 x 32 for the fp32 MFMA.
         bf16x8 bh[4], bm[4], bl[4];
+#if GK_X6_SCHED
+        // Software-pipelined: the B splits of ns = 1..3 are interleaved with the
+        // MFMAs of subtile row 0, the A split of subtile row ms + 1 with the
+        // MFMAs of row ms (sched_group_barrier: 1 MFMA, then a few VALU) -- a
+        // wave issues in order, so VALU placed after a run of MFMAs would wait
+        // for the matrix pipe instead of filling its 16-cycle shadow.
+        split3x8(bv[0][0], bv[1][0], bh[0], bm[0], bl[0]);
+        bf16x8 ah, am, al;
+        {
+          const Frag a0 = ldA(0, 0), a1 = ldA(1, 0);
+          split3x8(a0, a1, ah, am, al);
+        }
+#pragma unroll
+        for (int ms = 0; ms < MSB; ++ms) {
+          Frag n0, n1;
+          if (ms + 1 < MSB) {
+            n0 = ldA(0, ms + 1);
+            n1 = ldA(1, ms + 1);
+          }
+          bf16x8 nh, nm, nl;
+#pragma unroll
+          for (int ns = 0; ns < 4; ++ns) {
+            if (ms == 0 && ns + 1 < 4) split3x8(bv[0][ns + 1], bv[1][ns + 1], bh[ns + 1], bm[ns + 1], bl[ns + 1]);
+            if (ns == 1 && ms + 1 < MSB) split3x8(n0, n1, nh, nm, nl);
+            f32x4 c = acc[ms][ns];
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[ns], ah, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[ns], al, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm[ns], am, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm[ns], ah, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[ns], am, c, 0, 0, 0);
+            acc[ms][ns] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[ns], ah, c, 0, 0, 0);
+          }
+          // schedule of this region: the next row's fragment reads first, then
+          // the 24 MFMAs each followed by up to V VALU (ms 0: three B splits +
+          // one A split, ~150 VALU; later rows: one A split, ~40)
+          constexpr int V = 6;
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // DS reads
+          if (ms == 0) {
+#pragma unroll
+            for (int q = 0; q < 24; ++q) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+              __builtin_amdgcn_sched_group_barrier(0x002, V, 0);   // VALU
+            }
+          } else {
+#pragma unroll
+            for (int q = 0; q < 24; ++q) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+            }
+          }
+          if (ms + 1 < MSB) {
+            ah = nh;
+            am = nm;
+            al = nl;
+          }
+          issue_group(2 * ms);
+          issue_group(2 * ms + 1);
+        }
+#else
 #pragma unroll
         for (int ns = 0; ns < 4; ++ns) {
 #if GK_X6_EXP == 1
@@ -617,6 +679,7 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
           issue_group(2 * ms);
           issue_group(2 * ms + 1);
         }
+#endif
       } else {
       Frag an = ldA(0, 0);
 #pragma unroll
