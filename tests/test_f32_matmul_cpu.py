@@ -1,0 +1,104 @@
+"""fp32 matmul algorithm selection (ops/conv1x1.py set_f32_matmul) on the CPU:
+the bf16x6 candidates are offered only in "bf16x6" mode and only for fp32
+operands, their cfgs carry the 100000 digit (gemm.hip nt_unit_f32 /
+tn_unit_f32x), split-K keeps both digits, autotune keys are tagged so the two
+modes never share a cached choice, and bench.py defaults to bf16x6.
+
+The split itself (exact hi + mid + lo decomposition, six products of order
+<= 2) is mirrored here in numpy/torch to pin its error bound; the kernels are
+checked against fp64 on the GPU (tests/test_gemm_x6_gpu.py)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from gaussiank_sgd_amd.ops import conv1x1 as cv  # noqa: E402
+
+
+@pytest.fixture
+def mode():
+    prev = cv.f32_matmul()
+    yield
+    cv.set_f32_matmul(prev)
+
+
+def test_modes_and_candidates(mode):
+    cv.set_f32_matmul("native")
+    nat = cv._nt_cfgs(torch.float32)
+    assert all(c < cv.X6 for c in nat)
+    assert cv._dkey(torch.float32) == ("f32",)
+    assert all(c < cv.X6 for c, _ in cv._tn_cfgs(torch.float32))
+    prev = cv.set_f32_matmul("bf16x6")
+    assert prev == "native" and cv.f32_matmul() == "bf16x6"
+    x6 = cv._nt_cfgs(torch.float32)
+    assert set(nat) < set(x6)
+    extra = [c for c in x6 if c >= cv.X6]
+    assert extra and all(c // cv.X6 == 1 and (c % cv.X6) // 10000 == 0 for c in extra)
+    assert cv._dkey(torch.float32) == ("f32", "x6")
+    assert any(c >= cv.X6 for c, _ in cv._tn_cfgs(torch.float32))
+    # bf16 operands are untouched by the fp32 algorithm choice
+    assert cv._nt_cfgs(torch.bfloat16) == cv._NT_CFGS and cv._dkey(torch.bfloat16) == ()
+    assert cv._tn_cfgs(torch.bfloat16) == cv._TN_CFGS
+    # split-K: S in the 10000 digit, the bf16x6 flag in the 100000 digit
+    sk = cv._splitk_cfgs(torch.float32, 1568, 512, 2048)
+    assert any(c >= cv.X6 for c in sk)
+    for c in sk:
+        assert (c // 10000) % 10 in (2, 4, 8)
+    with pytest.raises(ValueError):
+        cv.set_f32_matmul("tf32")
+
+
+def test_keys_do_not_collide(mode):
+    cv.set_f32_matmul("native")
+    k1 = cv._dgrad_key(512, 256, 14, 14, 1024, 1, 1, torch.float32)
+    cv.set_f32_matmul("bf16x6")
+    k2 = cv._dgrad_key(512, 256, 14, 14, 1024, 1, 1, torch.float32)
+    assert k1 != k2 and k2[:len(k1)] == k1
+    assert cv.dgrad_key_dtype(k2) == torch.float32
+
+
+def _split3(x: np.ndarray):
+    """numpy mirror of mfma_util.h split3x8: round-to-nearest-even bf16 parts."""
+    def rne_bf16(v):
+        u = v.astype(np.float32).view(np.uint32).astype(np.uint64)
+        u = (u + 0x7FFF + ((u >> 16) & 1)) & 0xFFFF0000
+        return u.astype(np.uint32).view(np.float32)
+    hi = rne_bf16(x)
+    r = (x - hi).astype(np.float32)
+    mid = rne_bf16(r)
+    lo = rne_bf16((r - mid).astype(np.float32))
+    return hi, mid, lo
+
+
+def test_split_is_exact_and_products_bound():
+    rng = np.random.default_rng(0)
+    x = (rng.standard_normal(100000) * np.exp(rng.uniform(-20, 20, 100000))).astype(np.float32)
+    hi, mid, lo = _split3(x)
+    # exact: the three parts sum back to x in fp64
+    assert np.array_equal(hi.astype(np.float64) + mid + lo, x.astype(np.float64))
+    assert np.all(np.abs(mid) <= 2.0 ** -8 * np.abs(x))
+    assert np.all(np.abs(lo) <= 2.0 ** -16 * np.abs(x))
+    # the dropped products (mid*lo, lo*mid, lo*lo) stay below ~2^-23 |a b|
+    y = (rng.standard_normal(100000)).astype(np.float32)
+    h2, m2, l2 = _split3(y)
+    a = [v.astype(np.float64) for v in (hi, mid, lo)]
+    b = [v.astype(np.float64) for v in (h2, m2, l2)]
+    kept = sum(a[i] * b[j] for i in range(3) for j in range(3) if i + j <= 2)
+    exact = x.astype(np.float64) * y
+    rel = np.abs(kept - exact) / np.maximum(np.abs(exact), 1e-300)
+    assert rel.max() <= 1.01 * 2.0 ** -23
+
+
+def test_bench_defaults_to_bf16x6(monkeypatch):
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    monkeypatch.delenv("GKSGD_F32_MATMUL", raising=False)
+    import importlib
+    import bench
+    importlib.reload(bench)
+    assert bench.parse().f32_matmul == "bf16x6"
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--f32-matmul", "native"])
+    assert bench.parse().f32_matmul == "native"
