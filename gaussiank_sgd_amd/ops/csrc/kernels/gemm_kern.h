@@ -32,6 +32,9 @@
 //   its fp32 partial into the (gradient-arena) output with float atomics.
 #pragma once
 
+#ifndef GK_XCD_REMAP
+#define GK_XCD_REMAP 1   // XCD-aware block order of gemm_nt (0: identity, A/B builds)
+#endif
 #ifndef GK_X6_SCHED
 #define GK_X6_SCHED 1   // software-pipelined bf16x6 loop (0: the first form, A/B builds)
 #endif
@@ -127,6 +130,31 @@ namespace {
 
 __device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
 
+// XCD-aware block order.  The hardware deals workgroups round-robin over the 8
+// XCDs (linear id L -> XCD L % 8; relied on for speed only, never for
+// correctness) and every XCD has its own L2.  With the identity order each XCD
+// gets 1/8 of every row and column of the (x = M start, y = N tile) grid, so
+// every XCD streams every A tile and every weight panel from HBM.  Instead XCD
+// k runs the contiguous logical range [k G/8, (k+1) G/8): x fastest when there
+// are >= 8 N tiles (an XCD keeps gy/8 weight panels in its L2 and its blocks
+// read each A tile once per XCD), y fastest otherwise (every panel, a slice of
+// the M tiles).  A bijection whenever 8 divides the grid; identity otherwise.
+__device__ __forceinline__ void xcd_remap2(int& bx, int& by) {
+  const int gx = (int)gridDim.x, gy = (int)gridDim.y, G = gx * gy;
+  bx = (int)blockIdx.x;
+  by = (int)blockIdx.y;
+  if (!GK_XCD_REMAP || (G & 7) != 0 || G < 16) return;
+  const int L = bx + by * gx;
+  const int q = (L & 7) * (G >> 3) + (L >> 3);
+  if (gy >= 8) {
+    bx = q % gx;
+    by = q / gx;
+  } else {
+    by = q % gy;
+    bx = q / gy;
+  }
+}
+
 // s_waitcnt vmcnt(n) for a wave-uniform runtime n: waits until at most n of
 // this wave's vector-memory operations (loads, stores, LDS-DMA; they retire
 // in issue order) are still in flight.
@@ -216,7 +244,7 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
                T* __restrict__ C, int64_t ldc, int64_t M, int K, ConvGeo geo, float* __restrict__ stats,
                int64_t stats_ld, BnBwd bb, LazyA lz) {
   // stats != nullptr: per-block BatchNorm partials of the (dtype-rounded)
-  // output, psum at stats[blockIdx.x * N + n], psq at stats[stats_ld + ...]
+  // output, psum at stats[bx * N + n], psq at stats[stats_ld + ...]
   // (the [gy][C] layout bn_finalize_kernel reduces).  With bb.h (BN-backward
   // epilogue, MSB == 4 tiles only) the partials are sum(dz), sum(dz*h); the
   // finalize centres the second with the mean.
@@ -254,21 +282,23 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
     }
   }
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  int bx, by;   // logical block coordinates (XCD-aware order)
+  xcd_remap2(bx, by);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: LDS-DMA M0 and fragment bases in SGPRs
   const int wm = wave / WN, wn = wave % WN;
-  const int n0 = blockIdx.y * Cfg::BN;
+  const int n0 = by * Cfg::BN;
   const int64_t mtiles = (M + Cfg::BM - 1) / Cfg::BM;
   const int nk = K / KS;
-  // this block's work: M tiles blockIdx.x, +gridDim.x, ...; each has nk K slices
-  const int64_t my_tiles = blockIdx.x < mtiles ? (mtiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+  // this block's work: M tiles bx, +gridDim.x, ...; each has nk K slices
+  const int64_t my_tiles = bx < mtiles ? (mtiles - 1 - bx) / gridDim.x + 1 : 0;
   const int T_ = (int)(my_tiles * nk);
   const int Ntot = gridDim.y * Cfg::BN;
   if (T_ == 0) {
     if (stats)
       for (int c = threadIdx.x; c < Cfg::BN; c += Cfg::THREADS) {
-        stats[(int64_t)blockIdx.x * Ntot + n0 + c] = 0.f;
-        stats[stats_ld + (int64_t)blockIdx.x * Ntot + n0 + c] = 0.f;
+        stats[(int64_t)bx * Ntot + n0 + c] = 0.f;
+        stats[stats_ld + (int64_t)bx * Ntot + n0 + c] = 0.f;
       }
     return;
   }
@@ -353,7 +383,7 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
       }
     }
   };
-  int64_t s_mt = blockIdx.x;    // tile of the next stage to issue
+  int64_t s_mt = bx;    // tile of the next stage to issue
   int s_ks = 0;                 // its K slice
   int s_kh = kz_kh, s_kw = kz_kw, s_c0 = kz_c0;   // gather: tap and channel offset of that slice
   int s_t = 0;
@@ -470,7 +500,7 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
       }
     }
   };
-  int64_t mt = blockIdx.x;
+  int64_t mt = bx;
   for (int t = 0; t < T_; ++t) {
     // ops issued after stage(t), in order: NS=2: stores(t-1);
     // NS=3: stores(t-2), stage(t+1), stores(t-1).  Retire stage(t) only.
@@ -917,8 +947,8 @@ gemm_nt_kernel(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, in
         sa += red[w2 * Cfg::BN + c];
         sb += red[(WM + w2) * Cfg::BN + c];
       }
-      stats[(int64_t)blockIdx.x * Ntot + n0 + c] = sa;
-      stats[stats_ld + (int64_t)blockIdx.x * Ntot + n0 + c] = sb;
+      stats[(int64_t)bx * Ntot + n0 + c] = sa;
+      stats[stats_ld + (int64_t)bx * Ntot + n0 + c] = sb;
     }
   }
 }
