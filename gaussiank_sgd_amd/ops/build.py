@@ -74,7 +74,10 @@ HEADERS = ["kernels/common.h", "kernels/gk_kernels.h", "kernels/mfma_util.h", "k
            "comm/rccl_engine.h"]
 # per-file extra flags: the sparse aggregation must round product and sum
 # separately (bit-identical to the reference arithmetic and the CPU mirror)
-EXTRA_FLAGS = {"kernels/scatter.hip": ["-ffp-contract=off"]}
+# the GEMM units: no SLP vectorisation -- packed fp32 VALU (v_pk_add_f32) beside
+# MFMAs costs more issue cycles than scalar pairs (MI355X_MICROARCH.md constants);
+# measured on the bf16x6 split: GEMMs 2.5-4.5% faster (r5c20)
+EXTRA_FLAGS = {"kernels/scatter.hip": ["-ffp-contract=off"], "kernels/gemm_inst.hip": ["-fno-slp-vectorize"]}
 
 
 def _torch_dirs():

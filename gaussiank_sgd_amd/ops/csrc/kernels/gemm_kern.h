@@ -155,6 +155,23 @@ __device__ __forceinline__ void xcd_remap2(int& bx, int& by) {
   }
 }
 
+// The same for the grad-weight grids (x = N tile, y = K tile, z = M split):
+// XCD k runs a contiguous range of the x-fastest logical order, i.e. whole
+// M splits, so the G and X rows of a split are fetched by one XCD instead of
+// by every XCD holding one of its (x, y) tiles.
+__device__ __forceinline__ void xcd_remap3(int& bx, int& by, int& bz) {
+  const int gx = (int)gridDim.x, gy = (int)gridDim.y, gz = (int)gridDim.z, G = gx * gy * gz;
+  bx = (int)blockIdx.x;
+  by = (int)blockIdx.y;
+  bz = (int)blockIdx.z;
+  if (!GK_XCD_REMAP || (G & 7) != 0 || G < 16) return;
+  const int L = bx + (by + bz * gy) * gx;
+  const int q = (L & 7) * (G >> 3) + (L >> 3);
+  bx = q % gx;
+  by = (q / gx) % gy;
+  bz = q / (gx * gy);
+}
+
 // s_waitcnt vmcnt(n) for a wave-uniform runtime n: waits until at most n of
 // this wave's vector-memory operations (loads, stores, LDS-DMA; they retire
 // in issue order) are still in flight.
@@ -1112,9 +1129,11 @@ gemm_tn_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __re
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int wk = wave % WK, wn = (wave / WK) % WN, ws = wave / (WK * WN);
-  const int n0 = blockIdx.x * Cfg::BN;
-  const int c0 = blockIdx.y * Cfg::BK;
-  const int64_t mbeg = (int64_t)blockIdx.z * rows_per_split;
+  int bx, by, bz;   // logical block coordinates (XCD-aware order)
+  xcd_remap3(bx, by, bz);
+  const int n0 = bx * Cfg::BN;
+  const int c0 = by * Cfg::BK;
+  const int64_t mbeg = (int64_t)bz * rows_per_split;
   int64_t mend = mbeg + rows_per_split;
   if (mend > M) mend = M;
   if (mbeg >= mend) return;
@@ -1407,9 +1426,11 @@ gemm_tn_f32_kernel(const float* __restrict__ G, int64_t ldg, const float* __rest
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wk = wave % WK, wn = wave / WK;
-  const int n0 = blockIdx.x * Cfg::BN;
-  const int c0 = blockIdx.y * Cfg::BK;
-  const int64_t mbeg = (int64_t)blockIdx.z * rows_per_split;
+  int bx, by, bz;   // logical block coordinates (XCD-aware order)
+  xcd_remap3(bx, by, bz);
+  const int n0 = bx * Cfg::BN;
+  const int c0 = by * Cfg::BK;
+  const int64_t mbeg = (int64_t)bz * rows_per_split;
   int64_t mend = mbeg + rows_per_split;
   if (mend > M) mend = M;
   if (mbeg >= mend) return;
