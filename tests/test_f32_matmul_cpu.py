@@ -102,3 +102,48 @@ def test_bench_defaults_to_bf16x6(monkeypatch):
     assert bench.parse().f32_matmul == "bf16x6"
     monkeypatch.setattr(sys, "argv", ["bench.py", "--f32-matmul", "native"])
     assert bench.parse().f32_matmul == "native"
+
+
+def _xcd_remap2(L_x, L_y, gx, gy):
+    """Python mirror of gemm_kern.h xcd_remap2 (GK_XCD_REMAP = 1)."""
+    G = gx * gy
+    if G % 8 or G < 16:
+        return L_x, L_y
+    L = L_x + L_y * gx
+    q = (L & 7) * (G >> 3) + (L >> 3)
+    return (q % gx, q // gx) if gy >= 8 else (q // gy, q % gy)
+
+
+def _xcd_remap3(x, y, z, gx, gy, gz):
+    G = gx * gy * gz
+    if G % 8 or G < 16:
+        return x, y, z
+    L = x + (y + z * gy) * gx
+    q = (L & 7) * (G >> 3) + (L >> 3)
+    return q % gx, (q // gx) % gy, q // (gx * gy)
+
+
+@pytest.mark.parametrize("gx,gy", [(21, 24), (512, 2), (256, 1), (7, 3), (64, 12), (128, 8), (5, 16), (3, 1)])
+def test_xcd_block_order_is_a_bijection(gx, gy):
+    """Every logical (M start, N tile) of the grid is run by exactly one block,
+    and (grids of >= 8 N tiles) an XCD's blocks cover a contiguous run of N
+    tiles: the XCD-aware order changes only which CU runs a tile."""
+    seen = {}
+    for by in range(gy):
+        for bx in range(gx):
+            seen.setdefault(_xcd_remap2(bx, by, gx, gy), []).append((bx, by))
+    assert len(seen) == gx * gy and all(len(v) == 1 for v in seen.values())
+    assert all(0 <= x < gx and 0 <= y < gy for x, y in seen)
+    G = gx * gy
+    if G % 8 == 0 and G >= 16 and gy >= 8 and gy % 8 == 0:
+        for xcd in range(8):
+            ys = {_xcd_remap2(L % gx, L // gx, gx, gy)[1] for L in range(G) if L % 8 == xcd}
+            assert len(ys) == gy // 8
+
+
+@pytest.mark.parametrize("g", [(1, 4, 256), (2, 1, 1024), (4, 8, 32), (3, 5, 7), (1, 1, 16)])
+def test_xcd_block_order_3d_is_a_bijection(g):
+    gx, gy, gz = g
+    out = {_xcd_remap3(x, y, z, gx, gy, gz) for z in range(gz) for y in range(gy) for x in range(gx)}
+    assert len(out) == gx * gy * gz
+    assert all(0 <= a < gx and 0 <= b < gy and 0 <= c < gz for a, b, c in out)
