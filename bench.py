@@ -19,7 +19,10 @@ gradients -- the reference trained in fp32, settings.py:28 USE_FP16=False),
 on the hand-written fp32-MFMA convolutions (ops/conv1x1.py); a second timed
 phase in the same process measures the bf16-autocast step and reports it as
 ``bf16_value`` / ``bf16_ms_per_step`` (``--no-bf16-phase`` skips it;
-``--amp bf16`` makes bf16 the headline).
+``--amp bf16`` makes bf16 the headline).  fp32 GEMMs: ``--f32-matmul bf16x6``
+(default) also offers the fp32-accurate bf16x6 kernels to the per-shape tuner
+(ops/conv1x1.py set_f32_matmul); a further phase then times the same step with
+the fp32-MFMA GEMMs only (``fp32_native_value``; ``--no-native-phase`` skips).
 
 N > 1 also times, after the sparse loop, a dense comparator: the same model
 with a bucketed (``--dense-bucket-mb``, 25 MB), backward-overlapped RCCL
@@ -120,6 +123,8 @@ def parse():
                     choices=["native", "bf16x6"],
                     help="fp32 convolution / linear GEMM algorithm: native = fp32 MFMA only; bf16x6 = also the "
                          "fp32-accurate bf16x6 product kernels (ops/conv1x1.py set_f32_matmul)")
+    ap.add_argument("--no-native-phase", action="store_true",
+                    help="skip the secondary fp32-MFMA-only phase of a bf16x6 headline run")
     ap.add_argument("--no-bf16-phase", action="store_true",
                     help="skip the secondary bf16 phase of an fp32 headline run")
     ap.add_argument("--no-dense-phase", action="store_true", help="skip the dense comparator at N > 1")
@@ -621,6 +626,20 @@ def main() -> int:
             out["bf16_value"] = i["value"]
             out["bf16_exposed_comm_ms"] = i["exposed_comm_ms"]
         alive = optional_phase("bf16", out, P, bf16_phase)
+
+    # ---- secondary fp32 phase with the fp32-MFMA GEMMs only (the bf16x6 kernels
+    # off): the same step on the other fp32 GEMM algorithm, for comparison
+    if alive and amp == "fp32" and args.f32_matmul == "bf16x6" and not args.no_native_phase:
+        def native_phase(holder):
+            prev = conv1x1.set_f32_matmul("native")
+            try:
+                i = timed(holder, "fp32_native", "fp32", args.dense, args.threshold, args.batch_size,
+                          max(5, min(args.steps, 10)), max(3, min(args.warmup, 5)))
+            finally:
+                conv1x1.set_f32_matmul(prev)
+            out["fp32_native_ms_per_step"] = i["ms_per_step"]
+            out["fp32_native_value"] = i["value"]
+        alive = optional_phase("fp32_native", out, P, native_phase)
 
     # ---- dense comparator (N > 1): bucketed, backward-overlapped RCCL all-reduce
     dense_elems = max(1, int(args.dense_bucket_mb * 1e6 / 4))
