@@ -87,6 +87,9 @@ _TN_SMALL_F32 = [(c, s) for c in (4, 5, 11, 14, 15) for s in (16, 32, 128)]
 #   not a reduced precision; the tuner picks the faster kernel per shape.
 X6 = 100000
 _NT_CFGS_X6 = [c + X6 for c in (1, 2, 3, 4, 5, 6, 7, 12, 13, 101, 102, 103, 104, 105, 106, 107, 202, 203, 1001, 1002, 1003)]
+# register-staged bf16x6 row GEMMs (gemm_kern.h gemm_nt_x62_kernel, cfg digit 200000; tiles 1-7):
+# plain row GEMMs only -- an implicit-GEMM / lazy / split-K call refuses them and the tuner moves on
+_NT_CFGS_X62 = [2 * X6 + t for t in range(1, 8)]
 _F32MM = os.environ.get("GKSGD_F32_MATMUL", "native")
 
 
@@ -116,7 +119,7 @@ def _tn_cfgs(dt: torch.dtype) -> List[Tuple[int, int]]:
 
 def _nt_cfgs(dt: torch.dtype) -> List[int]:
     if dt == torch.float32:
-        return _NT_CFGS_F32 + (_NT_CFGS_X6 if _x6() else [])
+        return _NT_CFGS_F32 + (_NT_CFGS_X6 + _NT_CFGS_X62 if _x6() else [])
     return _NT_CFGS
 
 

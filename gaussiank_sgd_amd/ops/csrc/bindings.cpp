@@ -1082,6 +1082,7 @@ int64_t gemm_nt(at::Tensor A, at::Tensor B, at::Tensor C, int64_t cfg, int64_t m
                             (int)K, A.scalar_type() == at::kFloat, (int)cfg, (int)max_blocks, sp, rows,
                             bias_ptr(bias, N), has_bn ? &bn : nullptr, has_lz ? &lz : nullptr, cur_stream(A),
                             S > 1 ? ws.data_ptr<float>() : nullptr);
+  TORCH_CHECK(r != -2, "gemm_nt: the register-staged bf16x6 kernels (cfg digit 200000) take plain row GEMMs only");
   TORCH_CHECK(r >= 0, "gemm_nt: the lazy operand's coefficient table does not fit this tile configuration");
   return r;
 }
@@ -1159,6 +1160,7 @@ int64_t conv_nt(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor zero, int64
                             x.scalar_type() == at::kFloat, (int)cfg, (int)max_blocks, sp, rows, bias_ptr(bias, Co),
                             has_bn ? &bn : nullptr, has_lz ? &lz : nullptr, cur_stream(x),
                             S > 1 ? ws.data_ptr<float>() : nullptr);
+  TORCH_CHECK(r != -2, "conv_nt: the register-staged bf16x6 kernels (cfg digit 200000) take plain row GEMMs only");
   TORCH_CHECK(r >= 0, "conv_nt: the lazy operand's coefficient table does not fit this tile configuration");
   return r;
 }

@@ -36,6 +36,12 @@ static int nt_unit_b16(bool gather, GK_NT_UNIT_ARGS) {
 
 // fp32 operands: cfg digit 100000 selects the bf16x6 products (gemm_kern.h X6)
 static int nt_unit_f32(bool gather, GK_NT_UNIT_ARGS) {
+  if ((cfg / 100000) % 10 == 2) {
+    // bf16x6 with register staging: plain row GEMMs only (the tuner skips it elsewhere)
+    if (gather || lza || geo.KZ > 1 || geo.RH) return -2;
+    return nt_x62_row(static_cast<const float*>(A), lda, static_cast<const float*>(B), ldb, static_cast<float*>(C),
+                      ldc, M, N, K, cfg % 100000, max_blocks, geo.bias, stats, stats_ld, stats_rows, bb, stream);
+  }
   const bool x6 = (cfg / 100000) % 10 == 1;
   cfg %= 100000;
   if (x6) return gather ? nt_x6_gat(GK_NT_UNIT_PASS) : nt_x6_row(GK_NT_UNIT_PASS);

@@ -40,6 +40,12 @@ void tn_unit_x6(bool gather, const float* G, int64_t ldg, const float* X, int64_
   if (gather) tn_f32_dispatch<true, true>(G, ldg, X, ldx, W, ldw, M, N, K, cfg, splits, geo, lza, stream);
   else tn_f32_dispatch<false, true>(G, ldg, X, ldx, W, ldw, M, N, K, cfg, splits, geo, lza, stream);
 }
+#elif GK_GEMM_UNIT == 8
+int nt_x62_row(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M, int N, int K,
+               int cfg, int max_blocks, const float* bias, float* stats, int64_t stats_ld, int stats_rows,
+               const BnBwd& bb, hipStream_t stream) {
+  return nt_x62_dispatch(A, lda, B, ldb, C, ldc, M, N, K, cfg, max_blocks, bias, stats, stats_ld, stats_rows, bb, stream);
+}
 #else
 #error "unknown GK_GEMM_UNIT"
 #endif

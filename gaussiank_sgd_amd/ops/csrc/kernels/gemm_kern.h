@@ -115,6 +115,10 @@ int nt_f32_row(GK_NT_UNIT_ARGS);   // unit 2
 int nt_f32_gat(GK_NT_UNIT_ARGS);   // unit 3
 int nt_x6_row(GK_NT_UNIT_ARGS);    // unit 5: fp32 operands, bf16x6 products
 int nt_x6_gat(GK_NT_UNIT_ARGS);    // unit 6
+// unit 8: fp32 row GEMMs, bf16x6 with register staging (gemm_nt_x62_kernel)
+int nt_x62_row(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M, int N, int K,
+               int cfg, int max_blocks, const float* bias, float* stats, int64_t stats_ld, int stats_rows,
+               const BnBwd& bb, hipStream_t stream);
 // unit 7: fp32 grad-weight (TN) GEMMs with bf16x6 products
 void tn_unit_x6(bool gather, const float* G, int64_t ldg, const float* X, int64_t ldx, float* W, int64_t ldw,
                 int64_t M, int N, int K, int cfg, int splits, const ConvGeo& geo, const LazyArgs* lza,
@@ -1704,6 +1708,335 @@ void tn_f32_dispatch(const float* G, int64_t ldg, const float* X, int64_t ldx, f
     default: GK_TNF(1, 1); break;
   }
 #undef GK_TNF
+}
+
+// --------------------------------------------------------------------------
+// gemm_nt, bf16x6 with register staging ("x62"): C[M, N] = A[M, K] B[N, K]^T,
+// fp32 operands, row GEMMs only
+// --------------------------------------------------------------------------
+// The X6 form of gemm_nt_kernel stages fp32 tiles by LDS-DMA and every wave
+// splits the fragments it reads, so each element is split once per wave that
+// reads it (twice on a 2x2 wave grid) and every 1 KiB of fp32 costs one
+// LDS-DMA issue (~60-185 cycles among MFMAs, MI355X_MICROARCH.md).  Here
+// each thread loads 8 consecutive K elements of a row pair-wise into
+// registers (global_load_dwordx4), splits them ONCE (split3x8) and writes the
+// three bf16 planes to LDS; the MFMA loop reads bf16 fragments directly.  The
+// next slice's loads are in flight during the current slice's MFMAs and its
+// split + LDS writes are issued in the middle of them (two LDS stages of
+// 3 x (BM + BN) x 64 bytes, one barrier per 32-deep K slice).  Persistent over
+// M tiles like gemm_nt_kernel; XCD-aware block order; epilogue: bias, the
+// BatchNorm statistics partials or the BN-backward dz (fp32 layouts of
+// gemm_nt_kernel).
+template <int WM, int WN>
+struct X62Cfg {
+  static constexpr int NW = WM * WN;
+  static constexpr int THREADS = 64 * NW;
+  static constexpr int BM = 64 * WM;
+  static constexpr int BN = 64 * WN;
+  static constexpr int PA = BM * 64;                 // bytes of one A plane (BM rows x 32 bf16)
+  static constexpr int PB = BN * 64;
+  static constexpr int STAGE = 3 * (PA + PB);
+  static constexpr int LDS = 2 * STAGE;
+  static constexpr int PRA = BM * 4 / THREADS;       // 8-element row pieces of A per thread per slice
+  static constexpr int PRB = BN * 4 / THREADS;
+  static_assert(PRA >= 1 && PRB >= 1 && (BM * 4) % THREADS == 0 && (BN * 4) % THREADS == 0, "pieces per thread");
+  static_assert(LDS <= 160 * 1024, "LDS");
+};
+
+// 16-byte chunk q of a 64-byte plane row r lives at chunk q ^ x62_swz(r): the
+// 16 rows of an MFMA fragment read then cover every bank once
+__device__ __forceinline__ int x62_swz(int r) { return (r >> 2) & 3; }
+
+template <int WM, int WN, bool BNB>
+__global__ void __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(1)))
+gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb,
+                   float* __restrict__ C, int64_t ldc, int64_t M, int K, const float* __restrict__ bias,
+                   float* __restrict__ stats, int64_t stats_ld, BnBwd bb) {
+  using Cfg = X62Cfg<WM, WN>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int bx, by;
+  xcd_remap2(bx, by);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int n0 = by * Cfg::BN;
+  const int Ntot = (int)gridDim.y * Cfg::BN;
+  const int64_t mtiles = (M + Cfg::BM - 1) / Cfg::BM;
+  const int nk = K / 32;
+  const int64_t my_tiles = bx < mtiles ? (mtiles - 1 - bx) / gridDim.x + 1 : 0;
+  const int T_ = (int)(my_tiles * nk);
+  if (T_ == 0) {
+    if (stats)
+      for (int c = tid; c < Cfg::BN; c += Cfg::THREADS) {
+        stats[(int64_t)bx * Ntot + n0 + c] = 0.f;
+        stats[stats_ld + (int64_t)bx * Ntot + n0 + c] = 0.f;
+      }
+    return;
+  }
+
+  // ---- register staging: piece p of A is row cid >> 2, K elements 8 (cid & 3) .. +7
+  // of the slice (cid = tid + THREADS p); same for B (rows of the weight panel)
+  f32x4 ra[Cfg::PRA][2], rb[Cfg::PRB][2];
+  int64_t l_mt = bx;   // load cursor: M tile and K slice of the next loads
+  int l_ks = 0;
+  auto issue_loads = [&]() {
+    const int64_t m0 = l_mt * Cfg::BM;
+    const int k0 = l_ks * 32;
+#pragma unroll
+    for (int p = 0; p < Cfg::PRA; ++p) {
+      const int cid = tid + Cfg::THREADS * p;
+      int64_t gr = m0 + (cid >> 2);
+      gr = gr < M ? gr : M - 1;   // tail rows: computed, never stored
+      const float* src = A + gr * lda + k0 + (cid & 3) * 8;
+      ra[p][0] = *reinterpret_cast<const f32x4*>(src);
+      ra[p][1] = *reinterpret_cast<const f32x4*>(src + 4);
+    }
+#pragma unroll
+    for (int p = 0; p < Cfg::PRB; ++p) {
+      const int cid = tid + Cfg::THREADS * p;
+      const float* src = B + (int64_t)(n0 + (cid >> 2)) * ldb + k0 + (cid & 3) * 8;
+      rb[p][0] = *reinterpret_cast<const f32x4*>(src);
+      rb[p][1] = *reinterpret_cast<const f32x4*>(src + 4);
+    }
+    if (++l_ks == nk) {
+      l_ks = 0;
+      l_mt += gridDim.x;
+    }
+  };
+  // split the staged registers once and write the three bf16 planes of LDS stage buf
+  auto split_write = [&](int buf) {
+    char* st = smem + buf * Cfg::STAGE;
+#pragma unroll
+    for (int p = 0; p < Cfg::PRA; ++p) {
+      const int cid = tid + Cfg::THREADS * p;
+      const int r = cid >> 2;
+      bf16x8 h, m, l;
+      split3x8(ra[p][0], ra[p][1], h, m, l);
+      const int off = r * 64 + (((cid & 3) ^ x62_swz(r)) << 4);
+      *reinterpret_cast<bf16x8*>(st + off) = h;
+      *reinterpret_cast<bf16x8*>(st + Cfg::PA + off) = m;
+      *reinterpret_cast<bf16x8*>(st + 2 * Cfg::PA + off) = l;
+    }
+    char* sb = st + 3 * Cfg::PA;
+#pragma unroll
+    for (int p = 0; p < Cfg::PRB; ++p) {
+      const int cid = tid + Cfg::THREADS * p;
+      const int r = cid >> 2;
+      bf16x8 h, m, l;
+      split3x8(rb[p][0], rb[p][1], h, m, l);
+      const int off = r * 64 + (((cid & 3) ^ x62_swz(r)) << 4);
+      *reinterpret_cast<bf16x8*>(sb + off) = h;
+      *reinterpret_cast<bf16x8*>(sb + Cfg::PB + off) = m;
+      *reinterpret_cast<bf16x8*>(sb + 2 * Cfg::PB + off) = l;
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float ssum[4][4], ssq[4][4], bia[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      ssum[a][b] = ssq[a][b] = 0.f;
+      bia[a][b] = bias ? bias[n0 + wn * 64 + a * 16 + fq * 4 + b] : 0.f;
+    }
+
+  auto epilogue = [&](int64_t mt) {
+    const int64_t mbase = mt * Cfg::BM;
+#pragma unroll
+    for (int ms = 0; ms < 4; ++ms) {
+      const int64_t m = mbase + wm * 64 + ms * 16 + fr;
+      const bool live = m < M;
+      f32x4 ehv[4], ed2[4];
+      uint32_t ebits[4];
+      if constexpr (BNB) {
+#pragma unroll
+        for (int ns = 0; ns < 4; ++ns) {
+          ehv[ns] = ed2[ns] = f32x4{0.f, 0.f, 0.f, 0.f};
+          ebits[ns] = 0u;
+        }
+        if (live) {
+#pragma unroll
+          for (int ns = 0; ns < 4; ++ns) {
+            const int n = n0 + wn * 64 + ns * 16 + fq * 4;
+            ehv[ns] = *reinterpret_cast<const f32x4*>(static_cast<const float*>(bb.h) + m * ldc + n);
+            if (bb.dy2) ed2[ns] = *reinterpret_cast<const f32x4*>(static_cast<const float*>(bb.dy2) + m * ldc + n);
+            ebits[ns] = bb.mask ? (uint32_t)bb.mask[m * (Ntot >> 2) + (n >> 2)] : 0xfu;
+          }
+        }
+      }
+#pragma unroll
+      for (int ns = 0; ns < 4; ++ns) {
+        const int n = n0 + wn * 64 + ns * 16 + fq * 4;
+        f32x4 v = acc[ms][ns];
+        acc[ms][ns] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += bia[ns][r];
+        if constexpr (BNB) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float dz = (ebits[ns] >> r) & 1u ? v[r] + ed2[ns][r] : 0.f;
+            v[r] = dz;
+            ssum[ns][r] += dz;
+            ssq[ns][r] = fmaf(dz, ehv[ns][r], ssq[ns][r]);
+          }
+        } else {
+          if (stats && live) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              ssum[ns][r] += v[r];
+              ssq[ns][r] = fmaf(v[r], v[r], ssq[ns][r]);
+            }
+          }
+        }
+        if (live) *reinterpret_cast<f32x4*>(C + m * ldc + n) = v;
+      }
+    }
+  };
+
+  // prologue: slice 0 into LDS stage 0, slice 1's loads in flight
+  issue_loads();
+  split_write(0);
+  if (T_ > 1) issue_loads();
+  __syncthreads();
+  int ks = 0;
+  int64_t mt = bx;
+  for (int t = 0; t < T_; ++t) {
+    const int cur = t & 1;
+    const char* st = smem + cur * Cfg::STAGE;
+    const char* pa = st;
+    const char* pb = st + 3 * Cfg::PA;
+    auto frag = [&](const char* plane, int row) -> bf16x8 {
+      return *reinterpret_cast<const bf16x8*>(plane + row * 64 + ((fq ^ x62_swz(row)) << 4));
+    };
+    bf16x8 bh[4], bm[4], bl[4];
+#pragma unroll
+    for (int ns = 0; ns < 4; ++ns) {
+      const int row = wn * 64 + ns * 16 + fr;
+      bh[ns] = frag(pb, row);
+      bm[ns] = frag(pb + Cfg::PB, row);
+      bl[ns] = frag(pb + 2 * Cfg::PB, row);
+    }
+#pragma unroll
+    for (int ms = 0; ms < 4; ++ms) {
+      const int row = wm * 64 + ms * 16 + fr;
+      const bf16x8 ah = frag(pa, row), am = frag(pa + Cfg::PA, row), al = frag(pa + 2 * Cfg::PA, row);
+#pragma unroll
+      for (int ns = 0; ns < 4; ++ns) {
+        f32x4 c = acc[ms][ns];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[ns], ah, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[ns], al, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm[ns], am, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm[ns], ah, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[ns], am, c, 0, 0, 0);
+        acc[ms][ns] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[ns], ah, c, 0, 0, 0);
+      }
+      if (ms == 0) {
+        // the next slice: split the landed registers into the other stage, then
+        // put the slice after it in flight (their VALU / LDS writes / loads
+        // issue between this slice's remaining MFMAs)
+        if (t + 1 < T_) {
+          split_write(cur ^ 1);
+          if (t + 2 < T_) issue_loads();
+        }
+      }
+    }
+    if (++ks == nk) {
+      ks = 0;
+      epilogue(mt);
+      mt += gridDim.x;
+    }
+    __syncthreads();
+  }
+
+  if (stats) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+          ssum[a][b] += __shfl_xor(ssum[a][b], off, 64);
+          ssq[a][b] += __shfl_xor(ssq[a][b], off, 64);
+        }
+    float* red = reinterpret_cast<float*>(smem);   // [2][WM][BN]; every stage is consumed
+    if (fr == 0) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int col = wn * 64 + a * 16 + fq * 4 + b;
+          red[wm * Cfg::BN + col] = ssum[a][b];
+          red[(WM + wm) * Cfg::BN + col] = ssq[a][b];
+        }
+    }
+    __syncthreads();
+    for (int c = tid; c < Cfg::BN; c += Cfg::THREADS) {
+      float sa = 0.f, sb = 0.f;
+#pragma unroll
+      for (int w2 = 0; w2 < WM; ++w2) {
+        sa += red[w2 * Cfg::BN + c];
+        sb += red[(WM + w2) * Cfg::BN + c];
+      }
+      stats[(int64_t)bx * Ntot + n0 + c] = sa;
+      stats[stats_ld + (int64_t)bx * Ntot + n0 + c] = sb;
+    }
+  }
+}
+
+template <int WM, int WN, bool BNB>
+int launch_nt_x62(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M, int N,
+                  int K, int max_blocks, const float* bias, float* stats, int64_t stats_ld, int stats_rows,
+                  const BnBwd& bb, hipStream_t stream) {
+  using Cfg = X62Cfg<WM, WN>;
+  const int ntiles = N / Cfg::BN;
+  const int64_t mtiles = (M + Cfg::BM - 1) / Cfg::BM;
+  const int per_cu = (160 * 1024) / Cfg::LDS > 0 ? (160 * 1024) / Cfg::LDS : 1;
+  int64_t gx = ((int64_t)256 * per_cu + ntiles - 1) / ntiles;
+  if (max_blocks > 0) gx = max_blocks;
+  if (gx < 1) gx = 1;
+  if (gx > mtiles) gx = mtiles;
+  if (stats && gx > stats_rows) gx = stats_rows;   // one partial row per block
+  static bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_x62_kernel<WM, WN, BNB>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL((gemm_nt_x62_kernel<WM, WN, BNB>), dim3((unsigned)gx, (unsigned)ntiles), dim3(Cfg::THREADS),
+                     Cfg::LDS, stream, A, lda, B, ldb, C, ldc, M, K, bias, stats, stats_ld, bb);
+  return (int)gx;
+}
+
+// cfg % 10: tile (WM, WN) of 64x64 wave tiles: 1 (2,2) 128x128, 2 (2,4) 128x256, 3 (4,2) 256x128,
+// 4 (1,4) 64x256, 5 (4,1) 256x64, 6 (1,2) 64x128, 7 (2,1) 128x64
+inline int nt_x62_dispatch(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M,
+                           int N, int K, int cfg, int max_blocks, const float* bias, float* stats, int64_t stats_ld,
+                           int stats_rows, const BnBwd& bb, hipStream_t stream) {
+  static const int cfg_bn[8] = {128, 128, 256, 128, 256, 64, 128, 64};
+  cfg %= 10;
+  if (cfg < 1 || cfg > 7 || N % cfg_bn[cfg] != 0) cfg = N % 128 == 0 ? 1 : 7;
+  if (N % cfg_bn[cfg] != 0) cfg = 5;
+#define GK_X62(WM_, WN_)                                                                                       \
+  return bb.h ? launch_nt_x62<WM_, WN_, true>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, bias, stats, stats_ld,  \
+                                              stats_rows, bb, stream)                                          \
+              : launch_nt_x62<WM_, WN_, false>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, bias, stats, stats_ld, \
+                                               stats_rows, bb, stream)
+  switch (cfg) {
+    case 2: GK_X62(2, 4);
+    case 3: GK_X62(4, 2);
+    case 4: GK_X62(1, 4);
+    case 5: GK_X62(4, 1);
+    case 6: GK_X62(1, 2);
+    case 7: GK_X62(2, 1);
+    default: GK_X62(2, 2);
+  }
+#undef GK_X62
 }
 
 template <bool GATHER, typename T, bool X6 = false>

@@ -234,3 +234,64 @@ def test_fastconv_autograd_x6_mode(g):
             assert (conv.weight.grad.double() - wr.grad).abs().max().item() <= tol(wr.grad)
     finally:
         conv1x1.set_f32_matmul(prev)
+
+
+X62 = [2 * X6 + t for t in range(1, 8)]   # register-staged bf16x6 row GEMMs (gemm_nt_x62_kernel), tiles 1-7
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 64, 64), (4096, 256, 64), (777, 128, 192), (2048, 512, 128),
+                                   (513, 192, 320), (300, 256, 1024), (5000, 768, 768)])
+@pytest.mark.parametrize("cfg", X62)
+@pytest.mark.parametrize("mb", [0, 3])
+def test_gemm_nt_x62(g, M, N, K, cfg, mb):
+    torch.manual_seed(M + N + K + cfg)
+    A = torch.randn(M, K, device="cuda")
+    B = torch.randn(N, K, device="cuda") * K ** -0.5
+    bias = torch.randn(N, device="cuda")
+    C = torch.full((M, N), float("nan"), device="cuda")
+    st = torch.full((2, 64, N), float("nan"), device="cuda")
+    rows = g.gemm_nt(A, B, C, cfg, mb, st, bias)
+    ref = A.double() @ B.double().t() + bias.double()
+    assert (C.double() - ref).abs().max().item() <= _tol(A.double().abs() @ B.double().abs().t() + 1)
+    s = st[:, :rows].double().sum(1)
+    Cd = C.double()
+    assert torch.allclose(s[0], Cd.sum(0), rtol=1e-5, atol=1e-3)
+    assert torch.allclose(s[1], (Cd * Cd).sum(0), rtol=1e-5, atol=1e-3)
+    C2 = torch.full((M, N), float("nan"), device="cuda")
+    g.gemm_nt(A, B, C2, cfg, mb)
+    assert (C2.double() - (ref - bias.double())).abs().max().item() <= _tol(A.double().abs() @ B.double().abs().t() + 1)
+
+
+@pytest.mark.parametrize("cfg", X62)
+@pytest.mark.parametrize("dy2", [False, True])
+def test_gemm_nt_x62_bn_backward_epilogue(g, cfg, dy2):
+    torch.manual_seed(cfg + dy2)
+    M, N, K = 3000, 256, 256
+    A = torch.randn(M, K, device="cuda")
+    B = torch.randn(N, K, device="cuda") * K ** -0.5
+    h = torch.randn(M, N, device="cuda")
+    d2 = torch.randn(M, N, device="cuda") if dy2 else None
+    keep = torch.rand(M, N // 4, 4, device="cuda") > 0.3
+    mask = (keep.to(torch.uint8) * torch.tensor([1, 2, 4, 8], dtype=torch.uint8, device="cuda")).sum(-1).to(torch.uint8)
+    C = torch.full((M, N), float("nan"), device="cuda")
+    st = torch.full((2, min(1280, (M + 63) // 64), N), float("nan"), device="cuda")
+    rows = g.gemm_nt(A, B, C, cfg, 0, st, None, h, d2, mask)
+    dx = A.double() @ B.double().t() + (d2.double() if dy2 else 0)
+    dz = torch.where(keep.reshape(M, N), dx, torch.zeros_like(dx))
+    assert (C.double() - dz).abs().max().item() <= _tol(A.double().abs() @ B.double().abs().t() + 4)
+    s = st[:, :rows].double().sum(1)
+    assert torch.allclose(s[0], dz.sum(0), rtol=1e-5, atol=1e-3)
+    assert torch.allclose(s[1], (dz * h.double()).sum(0), rtol=1e-5, atol=1e-3)
+
+
+def test_x62_refuses_non_row_calls(g):
+    x = torch.randn(2, 64, 9, 9, device="cuda").contiguous(memory_format=CL)
+    w = torch.randn(64, 64, 3, 3, device="cuda").contiguous(memory_format=CL)
+    y = torch.empty(2, 64, 9, 9, device="cuda").contiguous(memory_format=CL)
+    with pytest.raises(RuntimeError):
+        g.conv_nt(x, w, y, torch.zeros(64, device="cuda"), 1, 1, 2 * X6 + 1, 0)
+    A = torch.randn(1568, 2048, device="cuda")
+    B = torch.randn(512, 2048, device="cuda")
+    C = torch.empty(1568, 512, device="cuda")
+    with pytest.raises(RuntimeError):
+        g.gemm_nt(A, B, C, 2 * X6 + 20001, 0)     # split-K
