@@ -1747,7 +1747,7 @@ struct X62Cfg {
 // 16 rows of an MFMA fragment read then cover every bank once
 __device__ __forceinline__ int x62_swz(int r) { return (r >> 2) & 3; }
 
-template <int WM, int WN, bool BNB>
+template <int WM, int WN, bool BNB, int NPF = 1>
 __global__ void __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(1)))
 gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb,
                    float* __restrict__ C, int64_t ldc, int64_t M, int K, const float* __restrict__ bias,
@@ -1778,10 +1778,13 @@ gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
 
   // ---- register staging: piece p of A is row cid >> 2, K elements 8 (cid & 3) .. +7
   // of the slice (cid = tid + THREADS p); same for B (rows of the weight panel)
-  f32x4 ra[Cfg::PRA][2], rb[Cfg::PRB][2];
+  // NPF register sets: the loads of slice s go to set s % NPF (NPF = 2: two
+  // slices in flight ahead of the one being multiplied)
+  f32x4 ra[NPF][Cfg::PRA][2], rb[NPF][Cfg::PRB][2];
   int64_t l_mt = bx;   // load cursor: M tile and K slice of the next loads
   int l_ks = 0;
-  auto issue_loads = [&]() {
+  auto issue_loads = [&](auto SET) __attribute__((always_inline)) {
+    constexpr int q = decltype(SET)::value;
     const int64_t m0 = l_mt * Cfg::BM;
     const int k0 = l_ks * 32;
 #pragma unroll
@@ -1790,15 +1793,15 @@ gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
       int64_t gr = m0 + (cid >> 2);
       gr = gr < M ? gr : M - 1;   // tail rows: computed, never stored
       const float* src = A + gr * lda + k0 + (cid & 3) * 8;
-      ra[p][0] = *reinterpret_cast<const f32x4*>(src);
-      ra[p][1] = *reinterpret_cast<const f32x4*>(src + 4);
+      ra[q][p][0] = *reinterpret_cast<const f32x4*>(src);
+      ra[q][p][1] = *reinterpret_cast<const f32x4*>(src + 4);
     }
 #pragma unroll
     for (int p = 0; p < Cfg::PRB; ++p) {
       const int cid = tid + Cfg::THREADS * p;
       const float* src = B + (int64_t)(n0 + (cid >> 2)) * ldb + k0 + (cid & 3) * 8;
-      rb[p][0] = *reinterpret_cast<const f32x4*>(src);
-      rb[p][1] = *reinterpret_cast<const f32x4*>(src + 4);
+      rb[q][p][0] = *reinterpret_cast<const f32x4*>(src);
+      rb[q][p][1] = *reinterpret_cast<const f32x4*>(src + 4);
     }
     if (++l_ks == nk) {
       l_ks = 0;
@@ -1806,14 +1809,15 @@ gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
     }
   };
   // split the staged registers once and write the three bf16 planes of LDS stage buf
-  auto split_write = [&](int buf) {
+  auto split_write = [&](int buf, auto SET) __attribute__((always_inline)) {
+    constexpr int q = decltype(SET)::value;
     char* st = smem + buf * Cfg::STAGE;
 #pragma unroll
     for (int p = 0; p < Cfg::PRA; ++p) {
       const int cid = tid + Cfg::THREADS * p;
       const int r = cid >> 2;
       bf16x8 h, m, l;
-      split3x8(ra[p][0], ra[p][1], h, m, l);
+      split3x8(ra[q][p][0], ra[q][p][1], h, m, l);
       const int off = r * 64 + (((cid & 3) ^ x62_swz(r)) << 4);
       *reinterpret_cast<bf16x8*>(st + off) = h;
       *reinterpret_cast<bf16x8*>(st + Cfg::PA + off) = m;
@@ -1825,7 +1829,7 @@ gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
       const int cid = tid + Cfg::THREADS * p;
       const int r = cid >> 2;
       bf16x8 h, m, l;
-      split3x8(rb[p][0], rb[p][1], h, m, l);
+      split3x8(rb[q][p][0], rb[q][p][1], h, m, l);
       const int off = r * 64 + (((cid & 3) ^ x62_swz(r)) << 4);
       *reinterpret_cast<bf16x8*>(sb + off) = h;
       *reinterpret_cast<bf16x8*>(sb + Cfg::PB + off) = m;
@@ -1847,7 +1851,7 @@ gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
       bia[a][b] = bias ? bias[n0 + wn * 64 + a * 16 + fq * 4 + b] : 0.f;
     }
 
-  auto epilogue = [&](int64_t mt) {
+  auto epilogue = [&](int64_t mt) __attribute__((always_inline)) {
     const int64_t mbase = mt * Cfg::BM;
 #pragma unroll
     for (int ms = 0; ms < 4; ++ms) {
@@ -1900,19 +1904,25 @@ gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
     }
   };
 
-  // prologue: slice 0 into LDS stage 0, slice 1's loads in flight
-  issue_loads();
-  split_write(0);
-  if (T_ > 1) issue_loads();
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, (NPF > 1 ? 1 : 0)>;
+  // prologue: slice 0 into LDS stage 0, slices 1 .. NPF in flight
+  issue_loads(I0{});
+  split_write(0, I0{});
+  if (T_ > 1) issue_loads(I1{});
+  if (NPF > 1 && T_ > 2) issue_loads(I0{});
   __syncthreads();
   int ks = 0;
   int64_t mt = bx;
-  for (int t = 0; t < T_; ++t) {
-    const int cur = t & 1;
+  // one K slice t (register set of slice t + 1: (t + 1) % NPF, compile-time through PAR = t % 2)
+  auto slice = [&](int t, auto PAR) __attribute__((always_inline)) {
+    constexpr int par = decltype(PAR)::value;
+    using SN = std::integral_constant<int, (NPF > 1 ? (par ^ 1) : 0)>;   // set holding slice t + 1
+    const int cur = par;
     const char* st = smem + cur * Cfg::STAGE;
     const char* pa = st;
     const char* pb = st + 3 * Cfg::PA;
-    auto frag = [&](const char* plane, int row) -> bf16x8 {
+    auto frag = [&](const char* plane, int row) __attribute__((always_inline)) -> bf16x8 {
       return *reinterpret_cast<const bf16x8*>(plane + row * 64 + ((fq ^ x62_swz(row)) << 4));
     };
     bf16x8 bh[4], bm[4], bl[4];
@@ -1938,12 +1948,12 @@ gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
         acc[ms][ns] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[ns], ah, c, 0, 0, 0);
       }
       if (ms == 0) {
-        // the next slice: split the landed registers into the other stage, then
-        // put the slice after it in flight (their VALU / LDS writes / loads
-        // issue between this slice's remaining MFMAs)
+        // the next slice: split its landed registers into the other stage, then
+        // put slice t + 1 + NPF in flight in the freed set (their VALU / LDS
+        // writes / loads issue between this slice's remaining MFMAs)
         if (t + 1 < T_) {
-          split_write(cur ^ 1);
-          if (t + 2 < T_) issue_loads();
+          split_write(cur ^ 1, SN{});
+          if (t + 1 + NPF < T_) issue_loads(SN{});
         }
       }
     }
@@ -1953,6 +1963,10 @@ gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
       mt += gridDim.x;
     }
     __syncthreads();
+  };
+  for (int t = 0; t < T_; t += 2) {
+    slice(t, I0{});
+    if (t + 1 < T_) slice(t + 1, std::integral_constant<int, 1>{});
   }
 
   if (stats) {
@@ -1990,7 +2004,7 @@ gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
   }
 }
 
-template <int WM, int WN, bool BNB>
+template <int WM, int WN, bool BNB, int NPF>
 int launch_nt_x62(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M, int N,
                   int K, int max_blocks, const float* bias, float* stats, int64_t stats_ld, int stats_rows,
                   const BnBwd& bb, hipStream_t stream) {
@@ -2004,11 +2018,11 @@ int launch_nt_x62(const float* A, int64_t lda, const float* B, int64_t ldb, floa
   if (gx > mtiles) gx = mtiles;
   if (stats && gx > stats_rows) gx = stats_rows;   // one partial row per block
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_x62_kernel<WM, WN, BNB>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_x62_kernel<WM, WN, BNB, NPF>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL((gemm_nt_x62_kernel<WM, WN, BNB>), dim3((unsigned)gx, (unsigned)ntiles), dim3(Cfg::THREADS),
+  hipLaunchKernelGGL((gemm_nt_x62_kernel<WM, WN, BNB, NPF>), dim3((unsigned)gx, (unsigned)ntiles), dim3(Cfg::THREADS),
                      Cfg::LDS, stream, A, lda, B, ldb, C, ldc, M, K, bias, stats, stats_ld, bb);
   return (int)gx;
 }
@@ -2019,14 +2033,20 @@ inline int nt_x62_dispatch(const float* A, int64_t lda, const float* B, int64_t 
                            int N, int K, int cfg, int max_blocks, const float* bias, float* stats, int64_t stats_ld,
                            int stats_rows, const BnBwd& bb, hipStream_t stream) {
   static const int cfg_bn[8] = {128, 128, 256, 128, 256, 64, 128, 64};
+  const bool pf2 = (cfg / 10) % 10 == 1;   // cfg digit 10: two register sets in flight
   cfg %= 10;
   if (cfg < 1 || cfg > 7 || N % cfg_bn[cfg] != 0) cfg = N % 128 == 0 ? 1 : 7;
   if (N % cfg_bn[cfg] != 0) cfg = 5;
-#define GK_X62(WM_, WN_)                                                                                       \
-  return bb.h ? launch_nt_x62<WM_, WN_, true>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, bias, stats, stats_ld,  \
-                                              stats_rows, bb, stream)                                          \
-              : launch_nt_x62<WM_, WN_, false>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, bias, stats, stats_ld, \
-                                               stats_rows, bb, stream)
+#define GK_X62N(WM_, WN_, NPF_)                                                                                  \
+  return bb.h ? launch_nt_x62<WM_, WN_, true, NPF_>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, bias, stats,       \
+                                                    stats_ld, stats_rows, bb, stream)                              \
+              : launch_nt_x62<WM_, WN_, false, NPF_>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, bias, stats,      \
+                                                     stats_ld, stats_rows, bb, stream)
+#define GK_X62(WM_, WN_)          \
+  do {                            \
+    if (pf2) GK_X62N(WM_, WN_, 2); \
+    GK_X62N(WM_, WN_, 1);         \
+  } while (0)
   switch (cfg) {
     case 2: GK_X62(2, 4);
     case 3: GK_X62(4, 2);
@@ -2037,6 +2057,7 @@ inline int nt_x62_dispatch(const float* A, int64_t lda, const float* B, int64_t 
     default: GK_X62(2, 2);
   }
 #undef GK_X62
+#undef GK_X62N
 }
 
 template <bool GATHER, typename T, bool X6 = false>

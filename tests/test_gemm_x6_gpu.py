@@ -236,7 +236,7 @@ def test_fastconv_autograd_x6_mode(g):
         conv1x1.set_f32_matmul(prev)
 
 
-X62 = [2 * X6 + t for t in range(1, 8)]   # register-staged bf16x6 row GEMMs (gemm_nt_x62_kernel), tiles 1-7
+X62 = [2 * X6 + t for t in range(1, 8)] + [2 * X6 + 10 + t for t in (1, 2, 3)]   # register-staged bf16x6 (gemm_nt_x62_kernel): tiles 1-7, +10 two slices in flight
 
 
 @pytest.mark.parametrize("M,N,K", [(1000, 64, 64), (4096, 256, 64), (777, 128, 192), (2048, 512, 128),
