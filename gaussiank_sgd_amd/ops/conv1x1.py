@@ -111,9 +111,14 @@ def _x6() -> bool:
     return _F32MM == "bf16x6"
 
 
+# register-staged bf16x6 grad-weight (gemm_kern.h gemm_tn_x62_kernel, cfg digit 200000; tiles 1-8):
+# plain row form only -- an implicit-GEMM / lazy call refuses them and the tuner moves on
+_TN_CFGS_X62 = [(2 * X6 + t, sp) for t in (1, 2, 3, 4, 5, 6, 7, 8) for sp in (0, 64)]
+
+
 def _tn_cfgs(dt: torch.dtype) -> List[Tuple[int, int]]:
     if dt == torch.float32:
-        return _TN_CFGS_F32 + ([(c + X6, sp) for c, sp in _TN_CFGS_F32] if _x6() else [])
+        return _TN_CFGS_F32 + ([(c + X6, sp) for c, sp in _TN_CFGS_F32] + _TN_CFGS_X62 if _x6() else [])
     return _TN_CFGS
 
 

@@ -1101,8 +1101,9 @@ void gemm_tn_acc(at::Tensor G, at::Tensor X, at::Tensor W, int64_t cfg, int64_t 
   gk::LazyArgs lz{};
   const bool has_lz = lazy_args(lz_x, lz_coef, lz_padz, lz_padx, G, N, &lz);
   c10::DeviceGuard guard(G.device());
-  gk::gemm_tn_acc(G.data_ptr(), G.stride(0), X.data_ptr(), X.stride(0), W.data_ptr<float>(), W.stride(0), M, (int)N,
+  const int rc = gk::gemm_tn_acc(G.data_ptr(), G.stride(0), X.data_ptr(), X.stride(0), W.data_ptr<float>(), W.stride(0), M, (int)N,
                   (int)K, G.scalar_type() == at::kFloat, (int)cfg, (int)splits, has_lz ? &lz : nullptr, cur_stream(G));
+  TORCH_CHECK(rc != -2, "gemm_tn_acc: the register-staged bf16x6 kernels (cfg digit 200000) take plain row GEMMs only");
 }
 
 // implicit-GEMM convolution over NHWC bf16 (x: [N, C, H, W] channels-last,
@@ -1377,9 +1378,10 @@ void conv_tn_acc(at::Tensor dy, at::Tensor x, at::Tensor wout, at::Tensor zero, 
   gk::LazyArgs lz{};
   const bool has_lz = lazy_args(lz_x, lz_coef, lz_padz, lz_padx, dy, Co, &lz);
   c10::DeviceGuard guard(x.device());
-  gk::conv_tn_acc(dy.data_ptr(), x.data_ptr(), zero.data_ptr(), (int)H, (int)W, (int)C, (int)OH, (int)OW,
+  const int rc = gk::conv_tn_acc(dy.data_ptr(), x.data_ptr(), zero.data_ptr(), (int)H, (int)W, (int)C, (int)OH, (int)OW,
                   (int)stride, (int)pad, (int)KH, (int)KW, wout.data_ptr<float>(), M, (int)Co,
                   x.scalar_type() == at::kFloat, (int)cfg, (int)splits, has_lz ? &lz : nullptr, cur_stream(x));
+  TORCH_CHECK(rc != -2, "conv_tn_acc: the register-staged bf16x6 kernels (cfg digit 200000) take plain row GEMMs only");
 }
 
 // fused residual add (+ dropout) + LayerNorm (ln.hip)

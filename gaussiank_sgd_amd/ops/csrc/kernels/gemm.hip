@@ -49,11 +49,20 @@ static int nt_unit_f32(bool gather, GK_NT_UNIT_ARGS) {
 }
 
 // fp32 grad-weight: cfg digit 100000 selects the bf16x6 products
-static void tn_unit_f32x(bool gather, const float* G, int64_t ldg, const float* X, int64_t ldx, float* W, int64_t ldw,
-                         int64_t M, int N, int K, int cfg, int splits, const ConvGeo& geo, const LazyArgs* lza,
-                         hipStream_t stream) {
-  if ((cfg / 100000) % 10 == 1) tn_unit_x6(gather, G, ldg, X, ldx, W, ldw, M, N, K, cfg % 100000, splits, geo, lza, stream);
-  else tn_unit_f32(gather, G, ldg, X, ldx, W, ldw, M, N, K, cfg % 100000, splits, geo, lza, stream);
+// (digit 200000: register-staged bf16x6, plain row form only; -2 = refused)
+static int tn_unit_f32x(bool gather, const float* G, int64_t ldg, const float* X, int64_t ldx, float* W, int64_t ldw,
+                        int64_t M, int N, int K, int cfg, int splits, const ConvGeo& geo, const LazyArgs* lza,
+                        hipStream_t stream) {
+  const int fam = (cfg / 100000) % 10;
+  if (fam == 2) {
+    if (gather || lza) return -2;
+    tn_x62_row(G, ldg, X, ldx, W, ldw, M, N, K, cfg % 100000, splits, stream);
+  } else if (fam == 1) {
+    tn_unit_x6(gather, G, ldg, X, ldx, W, ldw, M, N, K, cfg % 100000, splits, geo, lza, stream);
+  } else {
+    tn_unit_f32(gather, G, ldg, X, ldx, W, ldw, M, N, K, cfg % 100000, splits, geo, lza, stream);
+  }
+  return 0;
 }
 
 bool gemm_supported(int64_t N, int64_t K) { return N >= 64 && K >= 64 && N % 64 == 0 && K % 64 == 0; }
@@ -202,25 +211,25 @@ int conv_nt_remap(const void* X, int64_t ldx, const void* zero, int H, int W, in
              : nt_unit_b16(true, X, C, B, K, Y, N, M, N, K, cfg, max_blocks, g, nullptr, 0, 0, BnBwd{}, nullptr, stream);
 }
 
-void gemm_tn_acc(const void* G, int64_t ldg, const void* X, int64_t ldx, float* W, int64_t ldw, int64_t M, int N,
+int gemm_tn_acc(const void* G, int64_t ldg, const void* X, int64_t ldx, float* W, int64_t ldw, int64_t M, int N,
                  int K, bool f32, int cfg, int splits, const LazyArgs* lazy, hipStream_t stream) {
   if (f32)
-    tn_unit_f32x(false, static_cast<const float*>(G), ldg, static_cast<const float*>(X), ldx, W, ldw, M, N, K, cfg,
+    return tn_unit_f32x(false, static_cast<const float*>(G), ldg, static_cast<const float*>(X), ldx, W, ldw, M, N, K, cfg,
                            splits, ConvGeo{}, lazy, stream);
-  else
-    tn_unit_b16(false, G, ldg, X, ldx, W, ldw, M, N, K, cfg, splits, ConvGeo{}, stream);
+  tn_unit_b16(false, G, ldg, X, ldx, W, ldw, M, N, K, cfg, splits, ConvGeo{}, stream);
+  return 0;
 }
 
-void conv_tn_acc(const void* G, const void* X, const void* zero, int H, int W_, int C, int OH, int OW, int S, int P,
+int conv_tn_acc(const void* G, const void* X, const void* zero, int H, int W_, int C, int OH, int OW, int S, int P,
                  int KH, int KW, float* Wout, int64_t M, int N, bool f32, int cfg, int splits, const LazyArgs* lazy,
                  hipStream_t stream) {
   ConvGeo g{zero, H, W_, C, OH, OW, S, P, KW, nullptr};
   const int K = KH * KW * C;
   if (f32)
-    tn_unit_f32x(true, static_cast<const float*>(G), N, static_cast<const float*>(X), C, Wout, K, M, N, K, cfg,
+    return tn_unit_f32x(true, static_cast<const float*>(G), N, static_cast<const float*>(X), C, Wout, K, M, N, K, cfg,
                           splits, g, lazy, stream);
-  else
-    tn_unit_b16(true, G, N, X, C, Wout, K, M, N, K, cfg, splits, g, stream);
+  tn_unit_b16(true, G, N, X, C, Wout, K, M, N, K, cfg, splits, g, stream);
+  return 0;
 }
 
 }  // namespace gk

@@ -46,6 +46,11 @@ int nt_x62_row(const float* A, int64_t lda, const float* B, int64_t ldb, float* 
                const BnBwd& bb, hipStream_t stream) {
   return nt_x62_dispatch(A, lda, B, ldb, C, ldc, M, N, K, cfg, max_blocks, bias, stats, stats_ld, stats_rows, bb, stream);
 }
+#elif GK_GEMM_UNIT == 9
+void tn_x62_row(const float* G, int64_t ldg, const float* X, int64_t ldx, float* W, int64_t ldw, int64_t M, int N,
+                int K, int cfg, int splits, hipStream_t stream) {
+  tn_x62_dispatch(G, ldg, X, ldx, W, ldw, M, N, K, cfg, splits, stream);
+}
 #else
 #error "unknown GK_GEMM_UNIT"
 #endif

@@ -119,6 +119,9 @@ int nt_x6_gat(GK_NT_UNIT_ARGS);    // unit 6
 int nt_x62_row(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M, int N, int K,
                int cfg, int max_blocks, const float* bias, float* stats, int64_t stats_ld, int stats_rows,
                const BnBwd& bb, hipStream_t stream);
+// unit 9: fp32 row grad-weight GEMMs, bf16x6 with register staging (gemm_tn_x62_kernel)
+void tn_x62_row(const float* G, int64_t ldg, const float* X, int64_t ldx, float* W, int64_t ldw, int64_t M, int N,
+                int K, int cfg, int splits, hipStream_t stream);
 // unit 7: fp32 grad-weight (TN) GEMMs with bf16x6 products
 void tn_unit_x6(bool gather, const float* G, int64_t ldg, const float* X, int64_t ldx, float* W, int64_t ldw,
                 int64_t M, int N, int K, int cfg, int splits, const ConvGeo& geo, const LazyArgs* lza,
@@ -2072,6 +2075,223 @@ inline int nt_x62_dispatch(const float* A, int64_t lda, const float* B, int64_t 
   }
 #undef GK_X62
 #undef GK_X62N
+}
+
+// --------------------------------------------------------------------------
+// gemm_tn, bf16x6 with register staging ("x62"): W[N, K] += G[M, N]^T X[M, K]
+// --------------------------------------------------------------------------
+// The grad-weight counterpart of gemm_nt_x62_kernel (row form: 1x1 stride-1
+// convolutions, linear layers).  The contraction runs over the pixel rows M,
+// so a bf16 MFMA operand wants 8 consecutive ROWS of one column per lane: a
+// staging thread loads 8 rows x 4 columns (eight 16-byte loads, each wave
+// instruction one contiguous row segment), splits every column's 8 rows once
+// (split3x8) and writes them as one 16-byte chunk of that column's 64-byte
+// plane row -- the transpose happens in registers, the LDS image is the NT
+// kernel's ([column][32 rows] per plane, same conflict-free swizzle).  Each
+// block reduces a contiguous slice of M for one output tile and adds its fp32
+// partial into W with float atomics, like gemm_tn_f32_kernel.
+template <int WN, int WK>
+struct TnX62Cfg {
+  static constexpr int NW = WN * WK;
+  static constexpr int THREADS = 64 * NW;
+  static constexpr int BN = 64 * WN;
+  static constexpr int BK = 64 * WK;
+  static constexpr int PG = BN * 64;                  // bytes of one G plane (BN columns x 32 rows)
+  static constexpr int PX = BK * 64;
+  static constexpr int STAGE = 3 * (PG + PX);
+  static constexpr int LDS = 2 * STAGE;
+  static constexpr int PIECES = BN + BK;              // 8 rows x 4 columns each: BN / 4 x 4 for G, BK / 4 x 4 for X
+  static constexpr int PPT = (PIECES + THREADS - 1) / THREADS;
+  static constexpr int ROWS = 32;
+  static_assert(LDS <= 160 * 1024, "LDS");
+};
+
+template <int WN, int WK>
+__global__ void __launch_bounds__(64 * WN * WK) __attribute__((amdgpu_waves_per_eu(1)))
+gemm_tn_x62_kernel(const float* __restrict__ G, int64_t ldg, const float* __restrict__ X, int64_t ldx,
+                   float* __restrict__ W, int64_t ldw, int64_t M, int64_t rows_per_split) {
+  using Cfg = TnX62Cfg<WN, WK>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int bx, by, bz;
+  xcd_remap3(bx, by, bz);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wk = wave % WK, wn = wave / WK;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int n0 = bx * Cfg::BN;
+  const int c0 = by * Cfg::BK;
+  const int64_t mbeg = (int64_t)bz * rows_per_split;
+  int64_t mend = mbeg + rows_per_split;
+  if (mend > M) mend = M;
+  if (mbeg >= mend) return;
+  const int T_ = (int)((mend - mbeg + Cfg::ROWS - 1) / Cfg::ROWS);
+
+  // piece pid: G pieces first (column chunk pid % (BN/4), row group pid / (BN/4)), then X
+  f32x4 rv[Cfg::PPT][8];
+  int64_t l_row = mbeg;   // first row of the next slice to load
+  auto issue_loads = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < Cfg::PPT; ++j) {
+      const int pid = tid + Cfg::THREADS * j;
+      if (pid >= Cfg::PIECES) break;   // wave-uniform (PIECES is a multiple of 64)
+      const bool isg = pid < Cfg::BN;
+      const int q = isg ? pid : pid - Cfg::BN;
+      const int nchunk = (isg ? Cfg::BN : Cfg::BK) / 4;
+      const int cc = q % nchunk, rg = q / nchunk;
+      const float* base = isg ? G + n0 + 4 * cc : X + c0 + 4 * cc;
+      const int64_t ld = isg ? ldg : ldx;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int64_t r = l_row + 8 * rg + i;
+        const int64_t rc = r < mend ? r : mend - 1;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(base + rc * ld);
+        rv[j][i] = r < mend ? v : f32x4{0.f, 0.f, 0.f, 0.f};   // rows past the split contribute 0
+      }
+    }
+    l_row += Cfg::ROWS;
+  };
+  auto split_write = [&](int buf, int jj) __attribute__((always_inline)) {
+    char* st = smem + buf * Cfg::STAGE;
+#pragma unroll
+    for (int j = 0; j < Cfg::PPT; ++j) {
+      if (jj >= 0 && j != jj) continue;
+      const int pid = tid + Cfg::THREADS * j;
+      if (pid >= Cfg::PIECES) break;
+      const bool isg = pid < Cfg::BN;
+      const int q = isg ? pid : pid - Cfg::BN;
+      const int nchunk = (isg ? Cfg::BN : Cfg::BK) / 4;
+      const int cc = q % nchunk, rg = q / nchunk;
+      char* pl = isg ? st : st + 3 * Cfg::PG;
+      const int psz = isg ? Cfg::PG : Cfg::PX;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        bf16x8 h, m, l;
+        split3x8(f32x4{rv[j][0][c], rv[j][1][c], rv[j][2][c], rv[j][3][c]},
+                 f32x4{rv[j][4][c], rv[j][5][c], rv[j][6][c], rv[j][7][c]}, h, m, l);
+        const int col = 4 * cc + c;
+        const int off = col * 64 + ((rg ^ x62_swz(col)) << 4);
+        *reinterpret_cast<bf16x8*>(pl + off) = h;
+        *reinterpret_cast<bf16x8*>(pl + psz + off) = m;
+        *reinterpret_cast<bf16x8*>(pl + 2 * psz + off) = l;
+      }
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue_loads();
+  split_write(0, -1);
+  issue_loads();
+  __syncthreads();
+  auto slice = [&](int t, auto PAR) __attribute__((always_inline)) {
+    constexpr int cur = decltype(PAR)::value;
+    const char* st = smem + cur * Cfg::STAGE;
+    const char* pg = st;
+    const char* px = st + 3 * Cfg::PG;
+    auto frag = [&](const char* plane, int col) __attribute__((always_inline)) -> bf16x8 {
+      return *reinterpret_cast<const bf16x8*>(plane + col * 64 + ((fq ^ x62_swz(col)) << 4));
+    };
+    bf16x8 gh[4], gm[4], gl[4];
+#pragma unroll
+    for (int ns = 0; ns < 4; ++ns) {
+      const int col = wn * 64 + ns * 16 + fr;
+      gh[ns] = frag(pg, col);
+      gm[ns] = frag(pg + Cfg::PG, col);
+      gl[ns] = frag(pg + 2 * Cfg::PG, col);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int col = wk * 64 + ks * 16 + fr;
+      const bf16x8 xh = frag(px, col), xm = frag(px + Cfg::PX, col), xl = frag(px + 2 * Cfg::PX, col);
+#pragma unroll
+      for (int ns = 0; ns < 4; ++ns) {
+        f32x4 c = acc[ns][ks];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gl[ns], xh, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gh[ns], xl, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gm[ns], xm, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gm[ns], xh, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gh[ns], xm, c, 0, 0, 0);
+        acc[ns][ks] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gh[ns], xh, c, 0, 0, 0);
+        // next slice's pieces between the MFMA groups (branch-free: past the
+        // split's end the loads read clamped rows and zero them; the writes go
+        // to the stage nobody reads again)
+        const int gstep = 4 * ks + ns;
+        if (gstep >= 1 && gstep <= Cfg::PPT) split_write(cur ^ 1, gstep - 1);
+        if (gstep == Cfg::PPT + 1) issue_loads();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    __syncthreads();
+  };
+  for (int t = 0; t < T_; t += 2) {
+    slice(t, std::integral_constant<int, 0>{});
+    if (t + 1 < T_) slice(t + 1, std::integral_constant<int, 1>{});
+  }
+  // D[i = n][j = k]: lane holds column k = .. + fr, rows n = .. + 4 fq + r
+#pragma unroll
+  for (int ns = 0; ns < 4; ++ns)
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int c = c0 + wk * 64 + ks * 16 + fr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wn * 64 + ns * 16 + fq * 4 + r;
+        atomicAdd(W + (int64_t)n * ldw + c, acc[ns][ks][r]);
+      }
+    }
+}
+
+template <int WN, int WK>
+void launch_tn_x62(const float* G, int64_t ldg, const float* X, int64_t ldx, float* W, int64_t ldw, int64_t M, int N,
+                   int K, int splits, hipStream_t stream) {
+  using Cfg = TnX62Cfg<WN, WK>;
+  const int tiles = (N / Cfg::BN) * (K / Cfg::BK);
+  if (splits <= 0) {
+    static const int cus = [] {
+      int d = 0, n = 0;
+      (void)hipGetDevice(&d);
+      return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && n > 0 ? n : 256;
+    }();
+    const int bpc = (160 * 1024) / Cfg::LDS > 0 ? (160 * 1024) / Cfg::LDS : 1;
+    splits = (int)(2 * (int64_t)cus * bpc / tiles);
+    if (splits < 1) splits = 1;
+  }
+  int64_t rows = (M + splits - 1) / splits;
+  rows = (rows + Cfg::ROWS - 1) / Cfg::ROWS * Cfg::ROWS;
+  if (rows < 4 * Cfg::ROWS) rows = 4 * Cfg::ROWS;
+  const int64_t nsplit = (M + rows - 1) / rows;
+  static bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_x62_kernel<WN, WK>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL((gemm_tn_x62_kernel<WN, WK>), dim3((unsigned)(N / Cfg::BN), (unsigned)(K / Cfg::BK), (unsigned)nsplit),
+                     dim3(Cfg::THREADS), Cfg::LDS, stream, G, ldg, X, ldx, W, ldw, M, rows);
+}
+
+// cfg % 10: tile (WN, WK) of 64x64 wave tiles: 1 (1,1) 64x64  2 (2,1) 128x64  3 (1,2) 64x128  4 (2,2) 128x128
+// 5 (4,1) 256x64  6 (1,4) 64x256  7 (4,2) 256x128  8 (2,4) 128x256
+inline void tn_x62_dispatch(const float* G, int64_t ldg, const float* X, int64_t ldx, float* W, int64_t ldw, int64_t M,
+                            int N, int K, int cfg, int splits, hipStream_t stream) {
+  static const int cfg_bn[9] = {64, 64, 128, 64, 128, 256, 64, 256, 128};
+  static const int cfg_bk[9] = {64, 64, 64, 128, 128, 64, 256, 128, 256};
+  cfg %= 10;
+  if (cfg < 1 || cfg > 8 || N % cfg_bn[cfg] != 0 || K % cfg_bk[cfg] != 0) cfg = 1;
+  switch (cfg) {
+    case 2: launch_tn_x62<2, 1>(G, ldg, X, ldx, W, ldw, M, N, K, splits, stream); break;
+    case 3: launch_tn_x62<1, 2>(G, ldg, X, ldx, W, ldw, M, N, K, splits, stream); break;
+    case 4: launch_tn_x62<2, 2>(G, ldg, X, ldx, W, ldw, M, N, K, splits, stream); break;
+    case 5: launch_tn_x62<4, 1>(G, ldg, X, ldx, W, ldw, M, N, K, splits, stream); break;
+    case 6: launch_tn_x62<1, 4>(G, ldg, X, ldx, W, ldw, M, N, K, splits, stream); break;
+    case 7: launch_tn_x62<4, 2>(G, ldg, X, ldx, W, ldw, M, N, K, splits, stream); break;
+    case 8: launch_tn_x62<2, 4>(G, ldg, X, ldx, W, ldw, M, N, K, splits, stream); break;
+    default: launch_tn_x62<1, 1>(G, ldg, X, ldx, W, ldw, M, N, K, splits, stream); break;
+  }
 }
 
 template <bool GATHER, typename T, bool X6 = false>

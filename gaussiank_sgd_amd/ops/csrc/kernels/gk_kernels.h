@@ -349,7 +349,7 @@ int gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int
 // returns the number of partial rows written (<= stats_rows)
 int splitk_reduce(const float* ws, int S, int64_t M, int N, float* C, int64_t ldc, const float* bias, float* stats,
                   int stats_rows, const BnBwdArgs* bn, hipStream_t stream);
-void gemm_tn_acc(const void* G, int64_t ldg, const void* X, int64_t ldx, float* W, int64_t ldw, int64_t M, int N,
+int gemm_tn_acc(const void* G, int64_t ldg, const void* X, int64_t ldx, float* W, int64_t ldw, int64_t M, int N,
                  int K, bool f32, int cfg, int splits, const LazyArgs* lazy, hipStream_t stream);
 // Implicit-GEMM KHxKW convolution (stride S, zero padding P) over NHWC:
 //   conv_nt    : Y[M = N*OH*OW, Cout] = im2col(X) . Wt[Cout, KH*KW*C]^T
@@ -368,7 +368,7 @@ int conv_nt(const void* X, const void* zero, int H, int W, int C, int OH, int OW
 int conv_nt_remap(const void* X, int64_t ldx, const void* zero, int H, int W, int C, int OH, int OW, int KH, int KW,
                   const void* B, void* Y, int64_t M, int N, int RH, int RW, int RA, int RB, int RZ, bool f32, int cfg,
                   int max_blocks, const LazyArgs* lazy, hipStream_t stream);
-void conv_tn_acc(const void* G, const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P,
+int conv_tn_acc(const void* G, const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P,
                  int KH, int KW, float* Wout, int64_t M, int N, bool f32, int cfg, int splits, const LazyArgs* lazy,
                  hipStream_t stream);
 // Winograd F(2x2, 3x3) fp32 convolution, stride 1, padding 1 (winograd.hip).

@@ -295,3 +295,30 @@ def test_x62_refuses_non_row_calls(g):
     C = torch.empty(1568, 512, device="cuda")
     with pytest.raises(RuntimeError):
         g.gemm_nt(A, B, C, 2 * X6 + 20001, 0)     # split-K
+
+
+TN_X62 = [2 * X6 + t for t in range(1, 9)]   # register-staged bf16x6 grad-weight (gemm_tn_x62_kernel), tiles 1-8
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 64, 64), (4096, 256, 64), (2500, 512, 256), (130, 64, 128),
+                                   (3001, 256, 256), (777, 128, 512)])
+@pytest.mark.parametrize("cfg", TN_X62)
+@pytest.mark.parametrize("splits", [0, 1, 7])
+def test_gemm_tn_acc_x62(g, M, N, K, cfg, splits):
+    torch.manual_seed(M * 3 + N + K + cfg)
+    G = torch.randn(M, N, device="cuda")
+    X = torch.randn(M, K, device="cuda")
+    W0 = torch.randn(N, K, device="cuda")
+    W = W0.clone()
+    g.gemm_tn_acc(G, X, W, cfg, splits)
+    ref = W0.double() + G.double().t() @ X.double()
+    err = (W.double() - ref).abs().max().item()
+    assert err <= _tol(G.double().abs().t() @ X.double().abs() + 1), err
+
+
+def test_tn_x62_refuses_implicit_gemm(g):
+    x = torch.randn(2, 64, 9, 9, device="cuda").contiguous(memory_format=CL)
+    dy = torch.randn(2, 64, 9, 9, device="cuda").contiguous(memory_format=CL)
+    out = torch.zeros(64, 64, 3, 3, device="cuda").contiguous(memory_format=CL)
+    with pytest.raises(RuntimeError):
+        g.conv_tn_acc(dy, x, out, torch.zeros(64, device="cuda"), 1, 1, 2 * X6 + 1, 0)
