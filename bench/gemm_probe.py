@@ -25,15 +25,15 @@ def make(a, cfg):
     K = a.K or a.C
     k, s = a.k, a.stride
     p = k // 2
-    x = torch.randn(a.batch, a.C, a.H, a.H, device="cuda", dtype=dt).contiguous(memory_format=cl)
-    OH = (a.H + 2 * p - k) // s + 1
-    z = torch.zeros(256, device="cuda", dtype=torch.bfloat16)
     if a.op == "lwgrad":   # linear grad-weight (BERT ffn): W[N, K] += G[M, N]^T X[M, K]
         M = a.batch * a.H
         G = torch.randn(M, K, device="cuda", dtype=dt)
         X = torch.randn(M, a.C, device="cuda", dtype=dt)
         out = torch.zeros(K, a.C, device="cuda")
         return (lambda: g.gemm_tn_acc(G, X, out, cfg, a.splits)), 2.0 * M * K * a.C
+    x = torch.randn(a.batch, a.C, a.H, a.H, device="cuda", dtype=dt).contiguous(memory_format=cl)
+    OH = (a.H + 2 * p - k) // s + 1
+    z = torch.zeros(256, device="cuda", dtype=torch.bfloat16)
     if a.op in ("wgrad3", "cwgrad"):
         dy = torch.randn(a.batch, K, OH, OH, device="cuda", dtype=dt).contiguous(memory_format=cl)
         out = torch.zeros(K, a.C, k, k, device="cuda").contiguous(memory_format=cl)

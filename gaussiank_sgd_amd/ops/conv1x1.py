@@ -118,7 +118,10 @@ _TN_CFGS_X62 = [(2 * X6 + t, sp) for t in (1, 2, 3, 4, 5, 6, 7, 8) for sp in (0,
 
 def _tn_cfgs(dt: torch.dtype) -> List[Tuple[int, int]]:
     if dt == torch.float32:
-        return _TN_CFGS_F32 + ([(c + X6, sp) for c, sp in _TN_CFGS_F32] + _TN_CFGS_X62 if _x6() else [])
+        # (_TN_CFGS_X62 measured no faster than the LDS-DMA bf16x6 grad-weight on any ResNet-50 /
+        # BERT shape, r5c27: not offered by default, GKSGD_TN_X62=1 adds them)
+        extra = _TN_CFGS_X62 if os.environ.get("GKSGD_TN_X62", "0") == "1" else []
+        return _TN_CFGS_F32 + ([(c + X6, sp) for c, sp in _TN_CFGS_F32] + extra if _x6() else [])
     return _TN_CFGS
 
 
