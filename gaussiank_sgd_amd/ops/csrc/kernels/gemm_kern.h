@@ -1791,34 +1791,51 @@ gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
   // NPF register sets: the loads of slice s go to set s % NPF (NPF = 2: two
   // slices in flight ahead of the one being multiplied)
   f32x4 ra[NPF][Cfg::PRA][2], rb[NPF][Cfg::PRB][2];
-  int64_t l_mt = bx;   // load cursor: M tile and K slice of the next loads
+  // load cursor: per-piece pointers to the next slice's 8 floats, advanced by
+  // 32 floats per slice; the 64-bit row arithmetic runs only at an M-tile
+  // change (a wave-uniform branch), not for every slice
+  int64_t l_mt = bx;
   int l_ks = 0;
-  auto issue_loads = [&](auto SET) __attribute__((always_inline)) {
-    constexpr int q = decltype(SET)::value;
+  const float* lpa[Cfg::PRA];
+  const float* lpb[Cfg::PRB];
+  auto set_a_rows = [&]() __attribute__((always_inline)) {
     const int64_t m0 = l_mt * Cfg::BM;
-    const int k0 = l_ks * 32;
 #pragma unroll
     for (int p = 0; p < Cfg::PRA; ++p) {
       const int cid = tid + Cfg::THREADS * p;
       int64_t gr = m0 + (cid >> 2);
       gr = gr < M ? gr : M - 1;   // tail rows: computed, never stored
-      const float* src = A + gr * lda + k0 + (cid & 3) * 8;
-      ra[q][p][0] = *reinterpret_cast<const f32x4*>(src);
-      ra[q][p][1] = *reinterpret_cast<const f32x4*>(src + 4);
+      lpa[p] = A + gr * lda + (cid & 3) * 8;
+    }
+  };
+  set_a_rows();
+#pragma unroll
+  for (int p = 0; p < Cfg::PRB; ++p) {
+    const int cid = tid + Cfg::THREADS * p;
+    lpb[p] = B + (int64_t)(n0 + (cid >> 2)) * ldb + (cid & 3) * 8;
+  }
+  auto issue_loads = [&](auto SET) __attribute__((always_inline)) {
+    constexpr int q = decltype(SET)::value;
+#pragma unroll
+    for (int p = 0; p < Cfg::PRA; ++p) {
+      ra[q][p][0] = *reinterpret_cast<const f32x4*>(lpa[p]);
+      ra[q][p][1] = *reinterpret_cast<const f32x4*>(lpa[p] + 4);
+      lpa[p] += 32;
     }
 #pragma unroll
     for (int p = 0; p < Cfg::PRB; ++p) {
-      const int cid = tid + Cfg::THREADS * p;
-      const float* src = B + (int64_t)(n0 + (cid >> 2)) * ldb + k0 + (cid & 3) * 8;
-      rb[q][p][0] = *reinterpret_cast<const f32x4*>(src);
-      rb[q][p][1] = *reinterpret_cast<const f32x4*>(src + 4);
+      rb[q][p][0] = *reinterpret_cast<const f32x4*>(lpb[p]);
+      rb[q][p][1] = *reinterpret_cast<const f32x4*>(lpb[p] + 4);
+      lpb[p] += 32;
     }
     if (++l_ks == nk) {
       l_ks = 0;
       l_mt += gridDim.x;
+      set_a_rows();
+#pragma unroll
+      for (int p = 0; p < Cfg::PRB; ++p) lpb[p] -= K;
     }
   };
-  // split the staged registers once and write the three bf16 planes of LDS stage buf
   // piece pc of the slice (A pieces 0 .. PRA-1, then B pieces), or all of them (pc < 0)
   auto split_write = [&](int buf, auto SET, int pc = -1) __attribute__((always_inline)) {
     constexpr int q = decltype(SET)::value;
