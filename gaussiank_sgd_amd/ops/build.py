@@ -52,7 +52,7 @@ HIP_SOURCES = [
     "kernels/bn_act.hip",
     "kernels/gemm.hip",
     # gemm_inst.hip: one object per GEMM instantiation unit (-DGK_GEMM_UNIT=<n>, gemm_kern.h)
-    *["kernels/gemm_inst.hip#%d" % u for u in range(10)],
+    *["kernels/gemm_inst.hip#%d" % u for u in range(11)],
     "kernels/ln.hip",
     "kernels/linear.hip",
     "kernels/lstm.hip",

@@ -37,8 +37,14 @@ static int nt_unit_b16(bool gather, GK_NT_UNIT_ARGS) {
 // fp32 operands: cfg digit 100000 selects the bf16x6 products (gemm_kern.h X6)
 static int nt_unit_f32(bool gather, GK_NT_UNIT_ARGS) {
   if ((cfg / 100000) % 10 == 2) {
-    // bf16x6 with register staging: plain row GEMMs only (the tuner skips it elsewhere)
-    if (gather || lza || geo.KZ > 1 || geo.RH) return -2;
+    // bf16x6 with register staging: row GEMMs and stride / padding implicit
+    // GEMMs (C a multiple of 32) without a lazy operand, split-K or remap
+    if (lza || geo.KZ > 1 || geo.RH) return -2;
+    if (gather) {
+      if (geo.C % 32 != 0) return -2;
+      return nt_x62_gat(static_cast<const float*>(A), static_cast<const float*>(B), static_cast<float*>(C), M, N, K,
+                        cfg % 100000, max_blocks, geo, stats, stats_ld, stats_rows, bb, stream);
+    }
     return nt_x62_row(static_cast<const float*>(A), lda, static_cast<const float*>(B), ldb, static_cast<float*>(C),
                       ldc, M, N, K, cfg % 100000, max_blocks, geo.bias, stats, stats_ld, stats_rows, bb, stream);
   }

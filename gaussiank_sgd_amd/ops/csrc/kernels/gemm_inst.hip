@@ -44,12 +44,20 @@ void tn_unit_x6(bool gather, const float* G, int64_t ldg, const float* X, int64_
 int nt_x62_row(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M, int N, int K,
                int cfg, int max_blocks, const float* bias, float* stats, int64_t stats_ld, int stats_rows,
                const BnBwd& bb, hipStream_t stream) {
-  return nt_x62_dispatch(A, lda, B, ldb, C, ldc, M, N, K, cfg, max_blocks, bias, stats, stats_ld, stats_rows, bb, stream);
+  return nt_x62_dispatch<false>(A, lda, B, ldb, C, ldc, M, N, K, cfg, max_blocks, bias, stats, stats_ld, stats_rows, bb,
+                                ConvGeo{}, stream);
 }
 #elif GK_GEMM_UNIT == 9
 void tn_x62_row(const float* G, int64_t ldg, const float* X, int64_t ldx, float* W, int64_t ldw, int64_t M, int N,
                 int K, int cfg, int splits, hipStream_t stream) {
   tn_x62_dispatch(G, ldg, X, ldx, W, ldw, M, N, K, cfg, splits, stream);
+}
+#elif GK_GEMM_UNIT == 10
+int nt_x62_gat(const float* A, const float* B, float* C, int64_t M, int N, int K, int cfg, int max_blocks,
+               const ConvGeo& geo, float* stats, int64_t stats_ld, int stats_rows, const BnBwd& bb,
+               hipStream_t stream) {
+  return nt_x62_dispatch<true>(A, geo.C, B, K, C, N, M, N, K, cfg, max_blocks, geo.bias, stats, stats_ld, stats_rows,
+                               bb, geo, stream);
 }
 #else
 #error "unknown GK_GEMM_UNIT"

@@ -119,6 +119,10 @@ int nt_x6_gat(GK_NT_UNIT_ARGS);    // unit 6
 int nt_x62_row(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M, int N, int K,
                int cfg, int max_blocks, const float* bias, float* stats, int64_t stats_ld, int stats_rows,
                const BnBwd& bb, hipStream_t stream);
+// unit 10: implicit-GEMM convolutions, bf16x6 with register staging
+int nt_x62_gat(const float* A, const float* B, float* C, int64_t M, int N, int K, int cfg, int max_blocks,
+               const ConvGeo& geo, float* stats, int64_t stats_ld, int stats_rows, const BnBwd& bb,
+               hipStream_t stream);
 // unit 9: fp32 row grad-weight GEMMs, bf16x6 with register staging (gemm_tn_x62_kernel)
 void tn_x62_row(const float* G, int64_t ldg, const float* X, int64_t ldx, float* W, int64_t ldw, int64_t M, int N,
                 int K, int cfg, int splits, hipStream_t stream);
@@ -1757,11 +1761,15 @@ struct X62Cfg {
 // conflict-free under any per-row permutation.
 __device__ __forceinline__ int x62_swz(int r) { return ((r >> 3) & 1) << 1; }
 
-template <int WM, int WN, bool BNB, int NPF = 1>
+template <int WM, int WN, bool BNB, int NPF = 1, bool GATHER = false>
 __global__ void __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(1)))
 gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb,
                    float* __restrict__ C, int64_t ldc, int64_t M, int K, const float* __restrict__ bias,
-                   float* __restrict__ stats, int64_t stats_ld, BnBwd bb) {
+                   float* __restrict__ stats, int64_t stats_ld, BnBwd bb, ConvGeo geo) {
+  // GATHER: implicit-GEMM convolution over channels-last A = x [N, H, W, C]
+  // (gemm_nt_kernel's ConvGeo, C a multiple of 32): row m is output pixel
+  // (n, oh, ow), K slice ks is tap (kh, kw) of channels c0 .. c0 + 31; a tap
+  // outside the image loads geo.zero
   using Cfg = X62Cfg<WM, WN>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int bx, by;
@@ -1798,6 +1806,10 @@ gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
   int l_ks = 0;
   const float* lpa[Cfg::PRA];
   const float* lpb[Cfg::PRB];
+  // gather: tap / channel offset of the next slice (wave-uniform) and, per
+  // piece, its output pixel's in-image taps (bit kh of okh / kw of okw)
+  int l_kh = 0, l_kw = 0, l_c0 = 0;
+  uint32_t okh[Cfg::PRA], okw[Cfg::PRA];
   auto set_a_rows = [&]() __attribute__((always_inline)) {
     const int64_t m0 = l_mt * Cfg::BM;
 #pragma unroll
@@ -1805,7 +1817,24 @@ gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
       const int cid = tid + Cfg::THREADS * p;
       int64_t gr = m0 + (cid >> 2);
       gr = gr < M ? gr : M - 1;   // tail rows: computed, never stored
-      lpa[p] = A + gr * lda + (cid & 3) * 8;
+      if constexpr (GATHER) {
+        const uint32_t ohw = (uint32_t)(geo.OH * geo.OW);
+        const uint32_t mu = (uint32_t)gr;
+        const uint32_t n = mu / ohw, rem = mu - n * ohw;
+        const uint32_t oh = rem / (uint32_t)geo.OW, ow = rem - oh * (uint32_t)geo.OW;
+        const int ih0 = (int)oh * geo.S - geo.P, iw0 = (int)ow * geo.S - geo.P;
+        uint32_t bh = 0u, bw = 0u;
+#pragma unroll
+        for (int t = 0; t < kMaxTaps; ++t) {
+          bh |= (uint32_t)((unsigned)(ih0 + t) < (unsigned)geo.H) << t;
+          bw |= (uint32_t)((unsigned)(iw0 + t) < (unsigned)geo.W) << t;
+        }
+        okh[p] = bh;
+        okw[p] = bw;
+        lpa[p] = A + (((int64_t)n * geo.H + ih0) * geo.W + iw0) * geo.C + (cid & 3) * 8;
+      } else {
+        lpa[p] = A + gr * lda + (cid & 3) * 8;
+      }
     }
   };
   set_a_rows();
@@ -1814,13 +1843,20 @@ gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
     const int cid = tid + Cfg::THREADS * p;
     lpb[p] = B + (int64_t)(n0 + (cid >> 2)) * ldb + (cid & 3) * 8;
   }
+  const float* zrow = static_cast<const float*>(geo.zero);
   auto issue_loads = [&](auto SET) __attribute__((always_inline)) {
     constexpr int q = decltype(SET)::value;
+    const int64_t toff = GATHER ? (int64_t)(l_kh * geo.W + l_kw) * geo.C + l_c0 : 0;   // wave-uniform
 #pragma unroll
     for (int p = 0; p < Cfg::PRA; ++p) {
-      ra[q][p][0] = *reinterpret_cast<const f32x4*>(lpa[p]);
-      ra[q][p][1] = *reinterpret_cast<const f32x4*>(lpa[p] + 4);
-      lpa[p] += 32;
+      const float* src = lpa[p];
+      if constexpr (GATHER) {
+        const bool ok = ((okh[p] >> l_kh) & (okw[p] >> l_kw) & 1u) != 0u;
+        src = ok ? src + toff : zrow;
+      }
+      ra[q][p][0] = *reinterpret_cast<const f32x4*>(src);
+      ra[q][p][1] = *reinterpret_cast<const f32x4*>(src + 4);
+      if constexpr (!GATHER) lpa[p] += 32;
     }
 #pragma unroll
     for (int p = 0; p < Cfg::PRB; ++p) {
@@ -1828,8 +1864,19 @@ gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
       rb[q][p][1] = *reinterpret_cast<const f32x4*>(lpb[p] + 4);
       lpb[p] += 32;
     }
+    if constexpr (GATHER) {
+      l_c0 += 32;
+      if (l_c0 == geo.C) {
+        l_c0 = 0;
+        if (++l_kw == geo.KW) {
+          l_kw = 0;
+          ++l_kh;
+        }
+      }
+    }
     if (++l_ks == nk) {
       l_ks = 0;
+      l_kh = l_kw = l_c0 = 0;
       l_mt += gridDim.x;
       set_a_rows();
 #pragma unroll
@@ -2038,10 +2085,10 @@ gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
   }
 }
 
-template <int WM, int WN, bool BNB, int NPF>
+template <int WM, int WN, bool BNB, int NPF, bool GATHER>
 int launch_nt_x62(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M, int N,
                   int K, int max_blocks, const float* bias, float* stats, int64_t stats_ld, int stats_rows,
-                  const BnBwd& bb, hipStream_t stream) {
+                  const BnBwd& bb, const ConvGeo& geo, hipStream_t stream) {
   using Cfg = X62Cfg<WM, WN>;
   const int ntiles = N / Cfg::BN;
   const int64_t mtiles = (M + Cfg::BM - 1) / Cfg::BM;
@@ -2052,30 +2099,31 @@ int launch_nt_x62(const float* A, int64_t lda, const float* B, int64_t ldb, floa
   if (gx > mtiles) gx = mtiles;
   if (stats && gx > stats_rows) gx = stats_rows;   // one partial row per block
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_x62_kernel<WM, WN, BNB, NPF>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_x62_kernel<WM, WN, BNB, NPF, GATHER>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL((gemm_nt_x62_kernel<WM, WN, BNB, NPF>), dim3((unsigned)gx, (unsigned)ntiles), dim3(Cfg::THREADS),
-                     Cfg::LDS, stream, A, lda, B, ldb, C, ldc, M, K, bias, stats, stats_ld, bb);
+  hipLaunchKernelGGL((gemm_nt_x62_kernel<WM, WN, BNB, NPF, GATHER>), dim3((unsigned)gx, (unsigned)ntiles), dim3(Cfg::THREADS),
+                     Cfg::LDS, stream, A, lda, B, ldb, C, ldc, M, K, bias, stats, stats_ld, bb, geo);
   return (int)gx;
 }
 
 // cfg % 10: tile (WM, WN) of 64x64 wave tiles: 1 (2,2) 128x128, 2 (2,4) 128x256, 3 (4,2) 256x128,
 // 4 (1,4) 64x256, 5 (4,1) 256x64, 6 (1,2) 64x128, 7 (2,1) 128x64
-inline int nt_x62_dispatch(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M,
-                           int N, int K, int cfg, int max_blocks, const float* bias, float* stats, int64_t stats_ld,
-                           int stats_rows, const BnBwd& bb, hipStream_t stream) {
+template <bool GATHER>
+int nt_x62_dispatch(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M,
+                    int N, int K, int cfg, int max_blocks, const float* bias, float* stats, int64_t stats_ld,
+                    int stats_rows, const BnBwd& bb, const ConvGeo& geo, hipStream_t stream) {
   static const int cfg_bn[8] = {128, 128, 256, 128, 256, 64, 128, 64};
   const bool pf2 = (cfg / 10) % 10 == 1;   // cfg digit 10: two register sets in flight
   cfg %= 10;
   if (cfg < 1 || cfg > 7 || N % cfg_bn[cfg] != 0) cfg = N % 128 == 0 ? 1 : 7;
   if (N % cfg_bn[cfg] != 0) cfg = 5;
 #define GK_X62N(WM_, WN_, NPF_)                                                                                  \
-  return bb.h ? launch_nt_x62<WM_, WN_, true, NPF_>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, bias, stats,       \
-                                                    stats_ld, stats_rows, bb, stream)                              \
-              : launch_nt_x62<WM_, WN_, false, NPF_>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, bias, stats,      \
-                                                     stats_ld, stats_rows, bb, stream)
+  return bb.h ? launch_nt_x62<WM_, WN_, true, NPF_, GATHER>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, bias, stats, \
+                                                            stats_ld, stats_rows, bb, geo, stream)                   \
+              : launch_nt_x62<WM_, WN_, false, NPF_, GATHER>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, bias,      \
+                                                             stats, stats_ld, stats_rows, bb, geo, stream)
 #define GK_X62(WM_, WN_)          \
   do {                            \
     if (pf2) GK_X62N(WM_, WN_, 2); \

@@ -284,17 +284,32 @@ def test_gemm_nt_x62_bn_backward_epilogue(g, cfg, dy2):
     assert torch.allclose(s[1], (dz * h.double()).sum(0), rtol=1e-5, atol=1e-3)
 
 
-def test_x62_refuses_non_row_calls(g):
-    x = torch.randn(2, 64, 9, 9, device="cuda").contiguous(memory_format=CL)
-    w = torch.randn(64, 64, 3, 3, device="cuda").contiguous(memory_format=CL)
-    y = torch.empty(2, 64, 9, 9, device="cuda").contiguous(memory_format=CL)
-    with pytest.raises(RuntimeError):
-        g.conv_nt(x, w, y, torch.zeros(64, device="cuda"), 1, 1, 2 * X6 + 1, 0)
+def test_x62_refuses_unsupported_calls(g):
     A = torch.randn(1568, 2048, device="cuda")
     B = torch.randn(512, 2048, device="cuda")
     C = torch.empty(1568, 512, device="cuda")
     with pytest.raises(RuntimeError):
         g.gemm_nt(A, B, C, 2 * X6 + 20001, 0)     # split-K
+
+
+@pytest.mark.parametrize("N,C,H,Co,k,s,p", CONV_CASES + [(2, 128, 7, 128, 3, 1, 1), (1, 64, 6, 64, 3, 2, 1)])
+@pytest.mark.parametrize("cfg", X62)
+def test_conv_nt_x62(g, N, C, H, Co, k, s, p, cfg):
+    """Register-staged bf16x6 implicit GEMM: per-pixel tap validity, zero
+    padding rows, stride 2, tail tiles; with the BN-statistics epilogue."""
+    torch.manual_seed(N + C + H + Co + cfg)
+    x, w = _conv_case(N, C, H, Co, k)
+    zero = torch.zeros(64, device="cuda")
+    ref = F.conv2d(x.double(), w.double(), stride=s, padding=p)
+    bound = F.conv2d(x.double().abs(), w.double().abs(), stride=s, padding=p)
+    y = torch.full(ref.shape, float("nan"), device="cuda").contiguous(memory_format=CL)
+    M = ref.shape[0] * ref.shape[2] * ref.shape[3]
+    st = torch.full((2, min(1280, (M + 63) // 64), Co), float("nan"), device="cuda")
+    rows = g.conv_nt(x, w, y, zero, s, p, cfg, 0, st)
+    assert (y.double() - ref).abs().max().item() <= _tol(bound)
+    yd = y.double().permute(0, 2, 3, 1).reshape(-1, Co)
+    sm = st[:, :rows].double().sum(1)
+    assert torch.allclose(sm[0], yd.sum(0), rtol=1e-5, atol=1e-3)
 
 
 TN_X62 = [2 * X6 + t for t in range(1, 9)]   # register-staged bf16x6 grad-weight (gemm_tn_x62_kernel), tiles 1-8
