@@ -88,8 +88,10 @@ _TN_SMALL_F32 = [(c, s) for c in (4, 5, 11, 14, 15) for s in (16, 32, 128)]
 X6 = 100000
 _NT_CFGS_X6 = [c + X6 for c in (1, 2, 3, 4, 5, 6, 7, 12, 13, 101, 102, 103, 104, 105, 106, 107, 202, 203, 1001, 1002, 1003)]
 # register-staged bf16x6 row GEMMs (gemm_kern.h gemm_nt_x62_kernel, cfg digit 200000; tiles 1-7):
-# plain row GEMMs only -- an implicit-GEMM / lazy / split-K call refuses them and the tuner moves on
-_NT_CFGS_X62 = [2 * X6 + t for t in range(1, 8)] + [2 * X6 + 10 + t for t in (1, 2, 3)]   # +10: 2 slices in flight
+# plain row GEMMs only -- an implicit-GEMM / lazy / split-K call refuses them and the tuner moves on.
+# Digit 300000: the same kernels with B split into bf16 planes once per call by the binding
+# (split3_rows), no B split in the kernel: within +-3% of 200000, up to 8% faster on a few shapes (r5c33)
+_NT_CFGS_X62 = [2 * X6 + t for t in range(1, 8)] + [3 * X6 + t for t in range(1, 8)]
 _F32MM = os.environ.get("GKSGD_F32_MATMUL", "native")
 
 

@@ -1078,11 +1078,18 @@ int64_t gemm_nt(at::Tensor A, at::Tensor B, at::Tensor C, int64_t cfg, int64_t m
                 "gemm_nt split-K: fp32, no lazy operand, S <= 16 and K % (64 S) == 0");
     ws = at::empty({S, M, N}, A.options().dtype(at::kFloat));
   }
+  // digit 300000: register-staged bf16x6 with B split into bf16 planes here, once per call
+  at::Tensor b3;
+  if ((cfg / 100000) % 10 == 3) {
+    TORCH_CHECK(B.scalar_type() == at::kFloat && K % 32 == 0, "gemm_nt: cfg family 3 takes fp32 operands");
+    b3 = at::empty({N, 3 * K}, B.options().dtype(at::kBFloat16));
+    gk::split3_rows(B.data_ptr<float>(), B.stride(0), b3.data_ptr(), N, (int)K, cur_stream(A));
+  }
   const int r = gk::gemm_nt(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), M, (int)N,
                             (int)K, A.scalar_type() == at::kFloat, (int)cfg, (int)max_blocks, sp, rows,
                             bias_ptr(bias, N), has_bn ? &bn : nullptr, has_lz ? &lz : nullptr, cur_stream(A),
-                            S > 1 ? ws.data_ptr<float>() : nullptr);
-  TORCH_CHECK(r != -2, "gemm_nt: the register-staged bf16x6 kernels (cfg digit 200000) take plain row GEMMs only");
+                            S > 1 ? ws.data_ptr<float>() : nullptr, b3.defined() ? b3.data_ptr() : nullptr);
+  TORCH_CHECK(r != -2, "gemm_nt: the register-staged bf16x6 kernels (cfg digit 200000/300000) take plain row GEMMs only");
   TORCH_CHECK(r >= 0, "gemm_nt: the lazy operand's coefficient table does not fit this tile configuration");
   return r;
 }
@@ -1156,12 +1163,19 @@ int64_t conv_nt(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor zero, int64
                 "conv_nt split-K: fp32, no lazy operand, S <= 16 dividing the K slices");
     ws = at::empty({S, M, Co}, x.options());
   }
+  at::Tensor b3;
+  if ((cfg / 100000) % 10 == 3) {
+    const int64_t K = KH * KW * C;
+    TORCH_CHECK(x.scalar_type() == at::kFloat, "conv_nt: cfg family 3 takes fp32 operands");
+    b3 = at::empty({Co, 3 * K}, w.options().dtype(at::kBFloat16));
+    gk::split3_rows(w.data_ptr<float>(), K, b3.data_ptr(), Co, (int)K, cur_stream(x));
+  }
   const int r = gk::conv_nt(x.data_ptr(), zero.data_ptr(), (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)stride,
                             (int)pad, (int)KH, (int)KW, w.data_ptr(), y.data_ptr(), M, (int)Co,
                             x.scalar_type() == at::kFloat, (int)cfg, (int)max_blocks, sp, rows, bias_ptr(bias, Co),
                             has_bn ? &bn : nullptr, has_lz ? &lz : nullptr, cur_stream(x),
-                            S > 1 ? ws.data_ptr<float>() : nullptr);
-  TORCH_CHECK(r != -2, "conv_nt: the register-staged bf16x6 kernels (cfg digit 200000) take plain row GEMMs only");
+                            S > 1 ? ws.data_ptr<float>() : nullptr, b3.defined() ? b3.data_ptr() : nullptr);
+  TORCH_CHECK(r != -2, "conv_nt: the register-staged bf16x6 kernels (cfg digit 200000/300000) take plain row GEMMs only");
   TORCH_CHECK(r >= 0, "conv_nt: the lazy operand's coefficient table does not fit this tile configuration");
   return r;
 }

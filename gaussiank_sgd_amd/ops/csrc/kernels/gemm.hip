@@ -36,17 +36,19 @@ static int nt_unit_b16(bool gather, GK_NT_UNIT_ARGS) {
 
 // fp32 operands: cfg digit 100000 selects the bf16x6 products (gemm_kern.h X6)
 static int nt_unit_f32(bool gather, GK_NT_UNIT_ARGS) {
-  if ((cfg / 100000) % 10 == 2) {
+  const int fam = (cfg / 100000) % 10;
+  if (fam == 2 || fam == 3) {
     // bf16x6 with register staging: row GEMMs and stride / padding implicit
-    // GEMMs (C a multiple of 32) without a lazy operand, split-K or remap
-    if (lza || geo.KZ > 1 || geo.RH) return -2;
+    // GEMMs (C a multiple of 32) without a lazy operand, split-K or remap;
+    // family 3: B pre-split (geo.b3, the binding's split3_rows)
+    if (lza || geo.KZ > 1 || geo.RH || (fam == 3) != (geo.b3 != nullptr)) return -2;
     if (gather) {
       if (geo.C % 32 != 0) return -2;
       return nt_x62_gat(static_cast<const float*>(A), static_cast<const float*>(B), static_cast<float*>(C), M, N, K,
                         cfg % 100000, max_blocks, geo, stats, stats_ld, stats_rows, bb, stream);
     }
     return nt_x62_row(static_cast<const float*>(A), lda, static_cast<const float*>(B), ldb, static_cast<float*>(C),
-                      ldc, M, N, K, cfg % 100000, max_blocks, geo.bias, stats, stats_ld, stats_rows, bb, stream);
+                      ldc, M, N, K, cfg % 100000, max_blocks, geo.bias, stats, stats_ld, stats_rows, bb, geo.b3, stream);
   }
   const bool x6 = (cfg / 100000) % 10 == 1;
   cfg %= 100000;
@@ -60,6 +62,7 @@ static int tn_unit_f32x(bool gather, const float* G, int64_t ldg, const float* X
                         int64_t M, int N, int K, int cfg, int splits, const ConvGeo& geo, const LazyArgs* lza,
                         hipStream_t stream) {
   const int fam = (cfg / 100000) % 10;
+  if (fam == 3) return -2;   // pre-split B: forward / grad-input kernels only
   if (fam == 2) {
     if (gather || lza) return -2;
     tn_x62_row(G, ldg, X, ldx, W, ldw, M, N, K, cfg % 100000, splits, stream);
@@ -69,6 +72,32 @@ static int tn_unit_f32x(bool gather, const float* G, int64_t ldg, const float* X
     tn_unit_f32(gather, G, ldg, X, ldx, W, ldw, M, N, K, cfg % 100000, splits, geo, lza, stream);
   }
   return 0;
+}
+
+// fp32 [R, S] (row stride ld) -> three bf16 planes [R][S / 32][3][32] (the B
+// operand layout of the register-staged bf16x6 kernels, cfg family 3): one
+// thread splits 8 consecutive elements (split3x8) and writes 3 x 16 bytes
+__global__ __launch_bounds__(256) void split3_rows_kernel(const float* __restrict__ src, int64_t ld,
+                                                          uint16_t* __restrict__ dst, int64_t R, int S) {
+  const int64_t g8 = S / 8;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= R * g8) return;
+  const int64_t r = t / g8;
+  const int g = (int)(t - r * g8);
+  const float* p = src + r * ld + 8 * g;
+  bf16x8 h, m, l;
+  split3x8(*reinterpret_cast<const f32x4*>(p), *reinterpret_cast<const f32x4*>(p + 4), h, m, l);
+  uint16_t* d = dst + (r * (S / 32) + g / 4) * 96 + (g % 4) * 8;
+  *reinterpret_cast<bf16x8*>(d) = h;
+  *reinterpret_cast<bf16x8*>(d + 32) = m;
+  *reinterpret_cast<bf16x8*>(d + 64) = l;
+}
+
+void split3_rows(const float* src, int64_t ld, void* dst, int64_t R, int S, hipStream_t stream) {
+  const int64_t n = R * (S / 8);
+  if (n <= 0) return;
+  hipLaunchKernelGGL(split3_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, src, ld,
+                     static_cast<uint16_t*>(dst), R, S);
 }
 
 bool gemm_supported(int64_t N, int64_t K) { return N >= 64 && K >= 64 && N % 64 == 0 && K % 64 == 0; }
@@ -158,9 +187,10 @@ int splitk_reduce(const float* ws, int S, int64_t M, int N, float* C, int64_t ld
 
 int gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N, int K,
             bool f32, int cfg, int max_blocks, float* stats, int stats_rows, const float* bias, const BnBwdArgs* bn,
-            const LazyArgs* lazy, hipStream_t stream, float* splitk_ws) {
+            const LazyArgs* lazy, hipStream_t stream, float* splitk_ws, const void* b3) {
   ConvGeo g{};
   g.bias = bias;
+  g.b3 = static_cast<const uint16_t*>(b3);
   const BnBwd bb = bn ? BnBwd{bn->h, bn->dy2, bn->mask} : BnBwd{};
   const int64_t sld = (int64_t)stats_rows * N;
   const int S = (cfg / 10000) % 10;
@@ -182,8 +212,9 @@ int gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int
 
 int conv_nt(const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P, int KH, int KW,
             const void* B, void* Y, int64_t M, int N, bool f32, int cfg, int max_blocks, float* stats, int stats_rows,
-            const float* bias, const BnBwdArgs* bn, const LazyArgs* lazy, hipStream_t stream, float* splitk_ws) {
+            const float* bias, const BnBwdArgs* bn, const LazyArgs* lazy, hipStream_t stream, float* splitk_ws, const void* b3) {
   ConvGeo g{zero, H, W, C, OH, OW, S, P, KW, bias};
+  g.b3 = static_cast<const uint16_t*>(b3);
   const int K = KH * KW * C;
   const int SK = (cfg / 10000) % 10;
   const int x6 = cfg / 100000 * 100000;

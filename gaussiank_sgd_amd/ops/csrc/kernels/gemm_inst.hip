@@ -43,9 +43,11 @@ void tn_unit_x6(bool gather, const float* G, int64_t ldg, const float* X, int64_
 #elif GK_GEMM_UNIT == 8
 int nt_x62_row(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M, int N, int K,
                int cfg, int max_blocks, const float* bias, float* stats, int64_t stats_ld, int stats_rows,
-               const BnBwd& bb, hipStream_t stream) {
+               const BnBwd& bb, const uint16_t* b3, hipStream_t stream) {
+  ConvGeo g{};
+  g.b3 = b3;
   return nt_x62_dispatch<false>(A, lda, B, ldb, C, ldc, M, N, K, cfg, max_blocks, bias, stats, stats_ld, stats_rows, bb,
-                                ConvGeo{}, stream);
+                                g, stream);
 }
 #elif GK_GEMM_UNIT == 9
 void tn_x62_row(const float* G, int64_t ldg, const float* X, int64_t ldx, float* W, int64_t ldw, int64_t M, int N,

@@ -70,6 +70,9 @@ struct ConvGeo {
   // multiplies K slices [z K, (z + 1) K) of A and B into its own fp32 output
   // plane C + z M ldc (plain epilogue); nt_splitk_reduce_kernel sums the planes
   int KZ;
+  // bf16x6 register-staged kernels, cfg family 3: the B operand already split
+  // into three bf16 planes, [N][K / 32][3][32] (split3_rows); nullptr otherwise
+  const uint16_t* b3;
 };
 
 // BatchNorm-backward epilogue (grad-input GEMM of the convolution that consumes
@@ -118,7 +121,7 @@ int nt_x6_gat(GK_NT_UNIT_ARGS);    // unit 6
 // unit 8: fp32 row GEMMs, bf16x6 with register staging (gemm_nt_x62_kernel)
 int nt_x62_row(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M, int N, int K,
                int cfg, int max_blocks, const float* bias, float* stats, int64_t stats_ld, int stats_rows,
-               const BnBwd& bb, hipStream_t stream);
+               const BnBwd& bb, const uint16_t* b3, hipStream_t stream);
 // unit 10: implicit-GEMM convolutions, bf16x6 with register staging
 int nt_x62_gat(const float* A, const float* B, float* C, int64_t M, int N, int K, int cfg, int max_blocks,
                const ConvGeo& geo, float* stats, int64_t stats_ld, int stats_rows, const BnBwd& bb,
@@ -1761,7 +1764,7 @@ struct X62Cfg {
 // conflict-free under any per-row permutation.
 __device__ __forceinline__ int x62_swz(int r) { return ((r >> 3) & 1) << 1; }
 
-template <int WM, int WN, bool BNB, int NPF = 1, bool GATHER = false>
+template <int WM, int WN, bool BNB, int NPF = 1, bool GATHER = false, bool P3 = false>
 __global__ void __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(1)))
 gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb,
                    float* __restrict__ C, int64_t ldc, int64_t M, int K, const float* __restrict__ bias,
@@ -1798,7 +1801,11 @@ gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
   // of the slice (cid = tid + THREADS p); same for B (rows of the weight panel)
   // NPF register sets: the loads of slice s go to set s % NPF (NPF = 2: two
   // slices in flight ahead of the one being multiplied)
-  f32x4 ra[NPF][Cfg::PRA][2], rb[NPF][Cfg::PRB][2];
+  // P3: B arrives pre-split (geo.b3, [N][K/32][3][32] bf16): a B piece is three
+  // 16-byte loads written to the planes as they are -- no split VALU for B
+  f32x4 ra[NPF][Cfg::PRA][2], rb[NPF][P3 ? 1 : Cfg::PRB][2];
+  u32x4 rb3[NPF][P3 ? Cfg::PRB : 1][3];
+  const uint16_t* lpb3[P3 ? Cfg::PRB : 1];
   // load cursor: per-piece pointers to the next slice's 8 floats, advanced by
   // 32 floats per slice; the 64-bit row arithmetic runs only at an M-tile
   // change (a wave-uniform branch), not for every slice
@@ -1841,7 +1848,8 @@ gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
 #pragma unroll
   for (int p = 0; p < Cfg::PRB; ++p) {
     const int cid = tid + Cfg::THREADS * p;
-    lpb[p] = B + (int64_t)(n0 + (cid >> 2)) * ldb + (cid & 3) * 8;
+    if constexpr (P3) lpb3[p] = geo.b3 + (int64_t)(n0 + (cid >> 2)) * (3 * K) + (cid & 3) * 8;
+    else lpb[p] = B + (int64_t)(n0 + (cid >> 2)) * ldb + (cid & 3) * 8;
   }
   const float* zrow = static_cast<const float*>(geo.zero);
   auto issue_loads = [&](auto SET) __attribute__((always_inline)) {
@@ -1860,9 +1868,15 @@ gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
     }
 #pragma unroll
     for (int p = 0; p < Cfg::PRB; ++p) {
-      rb[q][p][0] = *reinterpret_cast<const f32x4*>(lpb[p]);
-      rb[q][p][1] = *reinterpret_cast<const f32x4*>(lpb[p] + 4);
-      lpb[p] += 32;
+      if constexpr (P3) {
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) rb3[q][p][pl] = *reinterpret_cast<const u32x4*>(lpb3[p] + pl * 32);
+        lpb3[p] += 96;
+      } else {
+        rb[q][p][0] = *reinterpret_cast<const f32x4*>(lpb[p]);
+        rb[q][p][1] = *reinterpret_cast<const f32x4*>(lpb[p] + 4);
+        lpb[p] += 32;
+      }
     }
     if constexpr (GATHER) {
       l_c0 += 32;
@@ -1880,7 +1894,10 @@ gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
       l_mt += gridDim.x;
       set_a_rows();
 #pragma unroll
-      for (int p = 0; p < Cfg::PRB; ++p) lpb[p] -= K;
+      for (int p = 0; p < Cfg::PRB; ++p) {
+        if constexpr (P3) lpb3[p] -= 3 * K;
+        else lpb[p] -= K;
+      }
     }
   };
   // piece pc of the slice (A pieces 0 .. PRA-1, then B pieces), or all of them (pc < 0)
@@ -1905,12 +1922,18 @@ gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
       if (pc >= 0 && pc != Cfg::PRA + p) continue;
       const int cid = tid + Cfg::THREADS * p;
       const int r = cid >> 2;
-      bf16x8 h, m, l;
-      split3x8(rb[q][p][0], rb[q][p][1], h, m, l);
       const int off = r * 64 + (((cid & 3) ^ x62_swz(r)) << 4);
-      *reinterpret_cast<bf16x8*>(sb + off) = h;
-      *reinterpret_cast<bf16x8*>(sb + Cfg::PB + off) = m;
-      *reinterpret_cast<bf16x8*>(sb + 2 * Cfg::PB + off) = l;
+      if constexpr (P3) {
+        *reinterpret_cast<u32x4*>(sb + off) = rb3[q][p][0];
+        *reinterpret_cast<u32x4*>(sb + Cfg::PB + off) = rb3[q][p][1];
+        *reinterpret_cast<u32x4*>(sb + 2 * Cfg::PB + off) = rb3[q][p][2];
+      } else {
+        bf16x8 h, m, l;
+        split3x8(rb[q][p][0], rb[q][p][1], h, m, l);
+        *reinterpret_cast<bf16x8*>(sb + off) = h;
+        *reinterpret_cast<bf16x8*>(sb + Cfg::PB + off) = m;
+        *reinterpret_cast<bf16x8*>(sb + 2 * Cfg::PB + off) = l;
+      }
     }
   };
 
@@ -2085,7 +2108,7 @@ gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
   }
 }
 
-template <int WM, int WN, bool BNB, int NPF, bool GATHER>
+template <int WM, int WN, bool BNB, int NPF, bool GATHER, bool P3 = false>
 int launch_nt_x62(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M, int N,
                   int K, int max_blocks, const float* bias, float* stats, int64_t stats_ld, int stats_rows,
                   const BnBwd& bb, const ConvGeo& geo, hipStream_t stream) {
@@ -2099,11 +2122,11 @@ int launch_nt_x62(const float* A, int64_t lda, const float* B, int64_t ldb, floa
   if (gx > mtiles) gx = mtiles;
   if (stats && gx > stats_rows) gx = stats_rows;   // one partial row per block
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_x62_kernel<WM, WN, BNB, NPF, GATHER>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_x62_kernel<WM, WN, BNB, NPF, GATHER, P3>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL((gemm_nt_x62_kernel<WM, WN, BNB, NPF, GATHER>), dim3((unsigned)gx, (unsigned)ntiles), dim3(Cfg::THREADS),
+  hipLaunchKernelGGL((gemm_nt_x62_kernel<WM, WN, BNB, NPF, GATHER, P3>), dim3((unsigned)gx, (unsigned)ntiles), dim3(Cfg::THREADS),
                      Cfg::LDS, stream, A, lda, B, ldb, C, ldc, M, K, bias, stats, stats_ld, bb, geo);
   return (int)gx;
 }
@@ -2115,19 +2138,19 @@ int nt_x62_dispatch(const float* A, int64_t lda, const float* B, int64_t ldb, fl
                     int N, int K, int cfg, int max_blocks, const float* bias, float* stats, int64_t stats_ld,
                     int stats_rows, const BnBwd& bb, const ConvGeo& geo, hipStream_t stream) {
   static const int cfg_bn[8] = {128, 128, 256, 128, 256, 64, 128, 64};
-  const bool pf2 = (cfg / 10) % 10 == 1;   // cfg digit 10: two register sets in flight
   cfg %= 10;
   if (cfg < 1 || cfg > 7 || N % cfg_bn[cfg] != 0) cfg = N % 128 == 0 ? 1 : 7;
   if (N % cfg_bn[cfg] != 0) cfg = 5;
-#define GK_X62N(WM_, WN_, NPF_)                                                                                  \
-  return bb.h ? launch_nt_x62<WM_, WN_, true, NPF_, GATHER>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, bias, stats, \
-                                                            stats_ld, stats_rows, bb, geo, stream)                   \
-              : launch_nt_x62<WM_, WN_, false, NPF_, GATHER>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, bias,      \
-                                                             stats, stats_ld, stats_rows, bb, geo, stream)
-#define GK_X62(WM_, WN_)          \
-  do {                            \
-    if (pf2) GK_X62N(WM_, WN_, 2); \
-    GK_X62N(WM_, WN_, 1);         \
+#define GK_X62N(WM_, WN_, P3_)                                                                                      \
+  return bb.h ? launch_nt_x62<WM_, WN_, true, 1, GATHER, P3_>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, bias, stats, \
+                                                              stats_ld, stats_rows, bb, geo, stream)                  \
+              : launch_nt_x62<WM_, WN_, false, 1, GATHER, P3_>(A, lda, B, ldb, C, ldc, M, N, K, max_blocks, bias,     \
+                                                               stats, stats_ld, stats_rows, bb, geo, stream)
+  // (two register sets in flight, cfg digit 10, measured slower everywhere: no longer instantiated)
+#define GK_X62(WM_, WN_)                  \
+  do {                                    \
+    if (geo.b3) GK_X62N(WM_, WN_, true);  \
+    GK_X62N(WM_, WN_, false);             \
   } while (0)
   switch (cfg) {
     case 2: GK_X62(2, 4);

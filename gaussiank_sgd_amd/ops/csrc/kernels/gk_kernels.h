@@ -343,7 +343,7 @@ struct LazyArgs {
 // bias (optional): fp32 [N] added in the epilogue (before rounding and statistics)
 int gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int N, int K,
             bool f32, int cfg, int max_blocks, float* stats, int stats_rows, const float* bias, const BnBwdArgs* bn,
-            const LazyArgs* lazy, hipStream_t stream, float* splitk_ws = nullptr);
+            const LazyArgs* lazy, hipStream_t stream, float* splitk_ws = nullptr, const void* b3 = nullptr);
 // C[M, N] (row stride ldc) = sum of the S fp32 planes ws[S][M][N] (+ bias), with the
 // BatchNorm statistics partials (stats != nullptr) or the BN-backward epilogue (bn);
 // returns the number of partial rows written (<= stats_rows)
@@ -359,7 +359,10 @@ int gemm_tn_acc(const void* G, int64_t ldg, const void* X, int64_t ldx, float* W
 int conv_nt(const void* X, const void* zero, int H, int W, int C, int OH, int OW, int S, int P, int KH, int KW,
             const void* B, void* Y, int64_t M, int N, bool f32, int cfg, int max_blocks, float* stats, int stats_rows,
             const float* bias, const BnBwdArgs* bn, const LazyArgs* lazy, hipStream_t stream,
-            float* splitk_ws = nullptr);
+            float* splitk_ws = nullptr, const void* b3 = nullptr);
+// fp32 [R, S] (row stride ld, S % 32 == 0) -> bf16 planes [R][S / 32][3][32]:
+// the pre-split B operand of the bf16x6 register-staged kernels (cfg family 3)
+void split3_rows(const float* src, int64_t ld, void* dst, int64_t R, int S, hipStream_t stream);
 // One parity class (RA, RB) of a stride-2 convolution's grad-input as a stride-1,
 // padding-0 KHxKW implicit GEMM over dY (H x W x C, the forward output) whose
 // OH x OW output grid is stored at rows (n*RH + 2 oh + RA) * RW + 2 ow + RB of

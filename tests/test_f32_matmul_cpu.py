@@ -37,7 +37,7 @@ def test_modes_and_candidates(mode):
     x6 = cv._nt_cfgs(torch.float32)
     assert set(nat) < set(x6)
     extra = [c for c in x6 if c >= cv.X6]
-    assert extra and all(c // cv.X6 in (1, 2) and (c % cv.X6) // 10000 == 0 for c in extra)
+    assert extra and all(c // cv.X6 in (1, 2, 3) and (c % cv.X6) // 10000 == 0 for c in extra)
     assert cv._dkey(torch.float32) == ("f32", "x6")
     assert any(c >= cv.X6 for c, _ in cv._tn_cfgs(torch.float32))
     # bf16 operands are untouched by the fp32 algorithm choice

@@ -236,7 +236,9 @@ def test_fastconv_autograd_x6_mode(g):
         conv1x1.set_f32_matmul(prev)
 
 
-X62 = [2 * X6 + t for t in range(1, 8)] + [2 * X6 + 10 + t for t in (1, 2, 3)]   # register-staged bf16x6 (gemm_nt_x62_kernel): tiles 1-7, +10 two slices in flight
+# register-staged bf16x6 (gemm_nt_x62_kernel), tiles 1-7: family 2 splits both
+# operands in the kernel, family 3 reads B pre-split by the binding (split3_rows)
+X62 = [2 * X6 + t for t in range(1, 8)] + [3 * X6 + t for t in range(1, 8)]
 
 
 @pytest.mark.parametrize("M,N,K", [(1000, 64, 64), (4096, 256, 64), (777, 128, 192), (2048, 512, 128),
@@ -290,6 +292,28 @@ def test_x62_refuses_unsupported_calls(g):
     C = torch.empty(1568, 512, device="cuda")
     with pytest.raises(RuntimeError):
         g.gemm_nt(A, B, C, 2 * X6 + 20001, 0)     # split-K
+    with pytest.raises(RuntimeError):
+        g.gemm_nt(A, B, C, 3 * X6 + 20001, 0)
+    with pytest.raises(RuntimeError):
+        g.gemm_nt(A.bfloat16(), B.bfloat16(), C.bfloat16(), 3 * X6 + 1, 0)   # pre-split B: fp32 only
+    W = torch.zeros(512, 2048, device="cuda")
+    with pytest.raises(RuntimeError):
+        g.gemm_tn_acc(torch.randn(1568, 512, device="cuda"), A, W, 3 * X6 + 1, 0)   # forward / dgrad kernels only
+
+
+@pytest.mark.parametrize("R,S,ld", [(64, 768, 768), (192, 256, 320), (1024, 3072, 3072)])
+def test_split3_rows_layout(g, R, S, ld):
+    """The pre-split B of cfg family 3 equals the kernel-side split: a family-3
+    GEMM and a family-2 GEMM over the same operands agree bit for bit."""
+    torch.manual_seed(R + S)
+    A = torch.randn(300, S, device="cuda")
+    Bfull = torch.randn(R, ld, device="cuda") * S ** -0.5
+    B = Bfull[:, :S]   # strided rows when ld > S
+    C2 = torch.empty(300, R, device="cuda")
+    C3 = torch.empty(300, R, device="cuda")
+    g.gemm_nt(A, B, C2, 2 * X6 + 1, 0)
+    g.gemm_nt(A, B, C3, 3 * X6 + 1, 0)
+    assert torch.equal(C2, C3)
 
 
 @pytest.mark.parametrize("N,C,H,Co,k,s,p", CONV_CASES + [(2, 128, 7, 128, 3, 1, 1), (1, 64, 6, 64, 3, 2, 1)])
