@@ -16,11 +16,14 @@
 //   select  (grid)   ballot/popcount block scan, writes ascending indices +
 //                    values into the record, zeroes sent entries of r [K5]
 //
-// The 1-workgroup steps run in the LAST block of the preceding grid pass
-// (last_block(): device-coherent partials + an arrival counter, no spin):
-// finalize in the stats pass (threshold modes; radix modes keep a separate
-// finalize after the histograms), decide in the count pass, and the fallback
-// key in the conditional radix pass 2 -- 7 launches per threshold-mode call.
+// The 1-workgroup steps run as their own launches or (handoff = lastblock) in
+// the LAST block of the preceding grid pass (last_block(): device-coherent
+// partials + a two-level arrival counter, no spin).  Threshold modes fold the
+// decide and the conditional exact fallback (three radix passes, key resolve,
+// second count / decide) into ONE launch, decide_fb_kernel, whose grid
+// barriers run only when the fallback fires: stats, finalize, count,
+// decide_fb, select -- 5 launches per call (r5c36: 132 us span on the
+// 25.6 M bucket, from 144 us with the decide and four early-exit launches).
 //
 // Reference semantics reproduced (compression.py):
 //   gaussian  :358-389  threshold mu + |ppf(ratio/2)| * sigma, <=3 loops
@@ -50,7 +53,17 @@ constexpr int kKeyAbs = 0, kKeyHash = 1, kKeySample = 2;
 // the count pass as cheap as the reference ladder's 6
 constexpr int kCalCand = 8;
 constexpr int kHistSet = kRadixBins0 + kRadixBins1 + kRadixBins2;
-constexpr int kSyncCounters = 4;   // stats->finalize, count->decide, radix2->fallback key, cond count->decide
+// stats->finalize, count->decide, radix2->fallback key, cond count->decide,
+// fused-fallback grid barrier, fused-fallback exit
+constexpr int kSyncCounters = 6;
+// Each arrival counter is two-level: kSyncSub sub-counters (block b counts in
+// at sub b % kSyncSub) and one top counter the last arrival of every sub
+// counts in at.  Agent-scope atomics on ONE address serialise (~19 ns each,
+// 1024 blocks finishing together queue ~20 us behind the last block);
+// sub-counters kSyncStride words apart land in different memory channels and
+// proceed in parallel: 32 + 32 serial adds instead of 1024.
+constexpr int kSyncSub = 32, kSyncStride = 1024;
+constexpr int kSyncWords = (kSyncSub + 1) * kSyncStride;   // words per counter
 
 struct Ws {
   double* partials;   // kMaxStatsBlocks * 4
@@ -59,7 +72,7 @@ struct Ws {
   int64_t* eqtake;    // kMaxCountBlocks
   int64_t* blocksel;  // kMaxCountBlocks
   uint32_t* hist;     // 2 * kHistSet (set 0: exact/hash, set 1: DGC sample)
-  uint32_t* sync;     // kSyncCounters arrival counters (last-block hand-off), zero between kernels
+  uint32_t* sync;     // kSyncCounters two-level arrival counters of kSyncWords (last-block hand-off), zero between kernels
 };
 
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -116,7 +129,7 @@ size_t ws_bytes() {
   o = align_up(o + sizeof(int64_t) * kMaxCountBlocks, 256);
   o = align_up(o + sizeof(int64_t) * kMaxCountBlocks, 256);
   o = align_up(o + sizeof(uint32_t) * 2 * kHistSet, 256);
-  o += sizeof(uint32_t) * kSyncCounters;
+  o += sizeof(uint32_t) * (kSyncCounters * kSyncWords + 2 * 64);   // + fused-fallback flag / generation words
   return align_up(o, 256);
 }
 
@@ -307,16 +320,41 @@ __device__ __forceinline__ void load4(const float* __restrict__ p, int64_t e, in
 // atomic loads / stores across the add.  tests/test_kernels_gpu.py
 // (test_last_block_handoff_stress) replays the hand-offs at the largest grid
 // sizes, back to back, and checks every header and record against the host.
+// Two levels (kSyncSub): the last arrival at a sub-counter resets it and
+// counts in at the top counter; the last arrival there is the last block.
+// Every add is issued after the adding lane's earlier adds returned, so the
+// order above carries over: a block's stores completed -> its sub add -> the
+// sub's last add -> the top add -> the last block's loads.
+// (one lane) count block `bid` of `G` in at a two-level counter; true for the
+// last arrival.  The resets complete (vmcnt) before the next add, so a counter
+// reused right after (the fused fallback's grid barriers) never loses an add
+// to a late reset store.
+__device__ __forceinline__ bool arrive(uint32_t* counter, uint32_t G, uint32_t bid) {
+  const uint32_t nsub = G < (uint32_t)kSyncSub ? G : (uint32_t)kSyncSub;
+  const uint32_t j = bid % nsub;
+  const uint32_t expect = (G - j + nsub - 1) / nsub;   // blocks b with b % nsub == j
+  uint32_t* sub = counter + j * kSyncStride;
+  const uint32_t prev = __hip_atomic_fetch_add(sub, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  bool last = false;
+  if (prev == expect - 1) {
+    st_dev(sub, 0u);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t* top = counter + kSyncSub * kSyncStride;
+    const uint32_t p2 = __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = p2 == nsub - 1;
+    if (last) {
+      st_dev(top, 0u);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  return last;
+}
+
 __device__ __forceinline__ bool last_block(uint32_t* counter) {
   __shared__ uint32_t s_last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's st_dev / atomics completed
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool last = prev == gridDim.x - 1;
-    if (last) st_dev(counter, 0u);
-    s_last = last ? 1u : 0u;
-  }
+  if (threadIdx.x == 0) s_last = arrive(counter, gridDim.x, blockIdx.x) ? 1u : 0u;
   __syncthreads();
   return s_last != 0u;
 }
@@ -524,18 +562,18 @@ __device__ __forceinline__ uint32_t radix_digit(uint32_t key) {
   return key & 0x3ffu;
 }
 
-template <int PASS, int KEYKIND, bool VEC, bool FB = false>
-__global__ __launch_bounds__(kBlock) void radix_hist_kernel(const float* __restrict__ x, int64_t n, uint32_t seed,
-                                                            uint32_t sample_thr, int64_t k, uint32_t* hist_set,
-                                                            const uint32_t* __restrict__ valid,
-                                                            GkCtrl* __restrict__ cond,
-                                                            const uint32_t* __restrict__ seed_dev,
-                                                            uint32_t* __restrict__ fb_counter = nullptr) {
+// One histogram pass over the grid-stride slice of block `bid` of `nblk`
+// (radix_hist_kernel, and the fused conditional fallback of decide_fb_kernel).
+// sh: kWavesPerBlock x (the pass's bins) words of LDS, one copy per wave.
+constexpr int kRadixShWords = kWavesPerBlock * (kRadixBins0 > kRadixBins1 ? kRadixBins0 : kRadixBins1);
+template <int PASS, int KEYKIND, bool VEC>
+__device__ __forceinline__ void radix_hist_body(const float* __restrict__ x, int64_t n, uint32_t seed,
+                                                uint32_t sample_thr, int64_t k, uint32_t* hist_set,
+                                                const uint32_t* __restrict__ valid, int bid, int nblk,
+                                                uint32_t* sh) {
   constexpr int NB = PASS == 0 ? kRadixBins0 : (PASS == 1 ? kRadixBins1 : kRadixBins2);
-  __shared__ uint32_t sh_hist[kWavesPerBlock][NB];
+  static_assert(kWavesPerBlock * NB <= kRadixShWords, "radix LDS");
   __shared__ uint64_t sh_scan[kWavesPerBlock];
-  if (cond != nullptr && cond->fallback == 0) return;   // conditional pass (calibrated mode), grid-uniform
-  if (seed_dev != nullptr) seed = __builtin_amdgcn_readfirstlane(*seed_dev);
   uint32_t* hist0 = hist_set;
   uint32_t* hist1 = hist_set + kRadixBins0;
   uint32_t* hist2 = hist1 + kRadixBins1;
@@ -563,11 +601,11 @@ __global__ __launch_bounds__(kBlock) void radix_hist_kernel(const float* __restr
       prefix = (prefix << 11) | (uint32_t)d1;
     }
   }
-  for (int i = threadIdx.x; i < kWavesPerBlock * NB; i += kBlock) (&sh_hist[0][0])[i] = 0u;
+  for (int i = threadIdx.x; i < kWavesPerBlock * NB; i += kBlock) sh[i] = 0u;
   __syncthreads();
-  uint32_t* my = sh_hist[wave_id()];
-  const int64_t tid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  uint32_t* my = sh + wave_id() * NB;
+  const int64_t tid = (int64_t)bid * kBlock + threadIdx.x;
+  const int64_t stride = (int64_t)nblk * kBlock;
   const int64_t n4 = (n + 3) >> 2;
   for (int64_t i4 = tid; i4 < n4; i4 += stride) {
     const int64_t e = i4 << 2;
@@ -593,9 +631,25 @@ __global__ __launch_bounds__(kBlock) void radix_hist_kernel(const float* __restr
   __syncthreads();
   uint32_t* out = PASS == 0 ? hist0 : (PASS == 1 ? hist1 : hist2);
   for (int b = threadIdx.x; b < NB; b += kBlock) {
-    const uint32_t c = sh_hist[0][b] + sh_hist[1][b] + sh_hist[2][b] + sh_hist[3][b];
+    const uint32_t c = sh[b] + sh[NB + b] + sh[2 * NB + b] + sh[3 * NB + b];
     if (c) atomicAdd(&out[b], c);
   }
+  __syncthreads();   // the LDS copies are reused by the next pass (fused fallback)
+}
+
+template <int PASS, int KEYKIND, bool VEC, bool FB = false>
+__global__ __launch_bounds__(kBlock) void radix_hist_kernel(const float* __restrict__ x, int64_t n, uint32_t seed,
+                                                            uint32_t sample_thr, int64_t k, uint32_t* hist_set,
+                                                            const uint32_t* __restrict__ valid,
+                                                            GkCtrl* __restrict__ cond,
+                                                            const uint32_t* __restrict__ seed_dev,
+                                                            uint32_t* __restrict__ fb_counter = nullptr) {
+  if (cond != nullptr && cond->fallback == 0) return;   // conditional pass (calibrated mode), grid-uniform
+  if (seed_dev != nullptr) seed = __builtin_amdgcn_readfirstlane(*seed_dev);
+  constexpr int NB = PASS == 0 ? kRadixBins0 : (PASS == 1 ? kRadixBins1 : kRadixBins2);
+  __shared__ uint32_t sh_hist[kWavesPerBlock * NB];
+  radix_hist_body<PASS, KEYKIND, VEC>(x, n, seed, sample_thr, k, hist_set, valid, (int)blockIdx.x, (int)gridDim.x,
+                                      sh_hist);
   // conditional chain: the last block of pass 2 resolves the fallback key
   if (FB && PASS == 2 && last_block(fb_counter)) cal_fallback_body(cond, hist_set, k);
 }
@@ -862,14 +916,14 @@ __device__ __forceinline__ void cal_fallback_body(GkCtrl* __restrict__ ctrl, con
 // --------------------------------------------------------------------------
 // K4: one-pass multi-threshold count (counters in registers)
 // --------------------------------------------------------------------------
-template <int KEYKIND, bool VEC, int NC, int NX = 0, bool DEC = true>
-__global__ __launch_bounds__(kBlock) void count_kernel(const float* __restrict__ x, int64_t n, uint32_t seed,
-                                                       GkCtrl* __restrict__ ctrl, int64_t chunk_tiles,
-                                                       uint32_t* __restrict__ blockcnt,
-                                                       const uint32_t* __restrict__ valid, int cond,
-                                                       const uint32_t* __restrict__ seed_dev, DecArgs da) {
-  if (cond && ctrl->fallback == 0) return;
-  if (seed_dev != nullptr) seed = __builtin_amdgcn_readfirstlane(*seed_dev);
+// Block `bid`'s tile chunk: per-candidate counts -> blockcnt row bid (and the
+// lane-max sketch).  The candidate bounds are read device-coherent (the fused
+// fallback writes them inside the same grid).
+template <int KEYKIND, bool VEC, int NC, int NX>
+__device__ __forceinline__ void count_body(const float* __restrict__ x, int64_t n, uint32_t seed,
+                                           const GkCtrl* __restrict__ ctrl, int64_t chunk_tiles,
+                                           uint32_t* __restrict__ blockcnt, const uint32_t* __restrict__ valid,
+                                           int bid) {
   // Per-lane counters, summed over the wave once per block.  |x| keys are
   // < 2^31, so [key < b] is the sign bit of key - b (b <= 2^31): one v_sub +
   // one v_lshr_add per (element, candidate), independent chains, and
@@ -884,7 +938,7 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const float* __restrict__
   constexpr bool SIGN = KEYKIND == kKeyAbs;
   uint32_t bnd[NC];
 #pragma unroll
-  for (int j = 0; j < NC; ++j) bnd[j] = __builtin_amdgcn_readfirstlane(ctrl->bound[j]);
+  for (int j = 0; j < NC; ++j) bnd[j] = __builtin_amdgcn_readfirstlane(ld_coh(ctrl->bound, j));
   uint32_t cnt[NC];   // SIGN: elements below bound j; else: elements at or above it
 #pragma unroll
   for (int j = 0; j < NC; ++j) cnt[j] = 0u;
@@ -896,7 +950,7 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const float* __restrict__
   uint32_t xb[NXA], xc[NXA];
 #pragma unroll
   for (int j = 0; j < NXA; ++j) {
-    xb[j] = NX > 0 ? __builtin_amdgcn_readfirstlane(ctrl->bound[NC + j]) : 0xffffffffu;
+    xb[j] = NX > 0 ? __builtin_amdgcn_readfirstlane(ld_coh(ctrl->bound, NC + j)) : 0xffffffffu;
     xc[j] = 0u;
   }
   auto test_ext = [&](uint32_t key, bool in) {
@@ -915,7 +969,7 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const float* __restrict__
     if (NX > 0 && in && key >= xb[0]) test_ext(key, true);
   };
   const int64_t ntiles = (n + kTileElems - 1) / kTileElems;
-  const int64_t t0 = (int64_t)blockIdx.x * chunk_tiles;
+  const int64_t t0 = (int64_t)bid * chunk_tiles;
   const int64_t t1 = t0 + chunk_tiles < ntiles ? t0 + chunk_tiles : ntiles;
   int64_t tile = t0;
   if (VEC && KEYKIND != kKeyHash) {
@@ -1025,8 +1079,19 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const float* __restrict__
   block_totals_u32<NC + NX>(all, sh, s_bt);
   if (threadIdx.x < kMaxCand) {
     const int j = threadIdx.x;
-    st_dev(&blockcnt[blockIdx.x * kMaxCand + j], j < NC + NX ? s_bt[j] : 0u);
+    st_dev(&blockcnt[bid * kMaxCand + j], j < NC + NX ? s_bt[j] : 0u);
   }
+}
+
+template <int KEYKIND, bool VEC, int NC, int NX = 0, bool DEC = true>
+__global__ __launch_bounds__(kBlock) void count_kernel(const float* __restrict__ x, int64_t n, uint32_t seed,
+                                                       GkCtrl* __restrict__ ctrl, int64_t chunk_tiles,
+                                                       uint32_t* __restrict__ blockcnt,
+                                                       const uint32_t* __restrict__ valid, int cond,
+                                                       const uint32_t* __restrict__ seed_dev, DecArgs da) {
+  if (cond && ctrl->fallback == 0) return;
+  if (seed_dev != nullptr) seed = __builtin_amdgcn_readfirstlane(*seed_dev);
+  count_body<KEYKIND, VEC, NC, NX>(x, n, seed, ctrl, chunk_tiles, blockcnt, valid, (int)blockIdx.x);
   if constexpr (DEC) {   // decide on the totals in the last block (else: decide_kernel after this grid)
     if (last_block(da.counter))
       decide_body(ctrl, blockcnt, (int)gridDim.x, da.mode, da.loops, da.k, da.k_cap, da.offsets, da.eqtake,
@@ -1215,7 +1280,8 @@ __device__ __forceinline__ void decide_body(GkCtrl* __restrict__ gctrl, const ui
     // fallback to the exact key: clear the exact-key histograms for the
     // conditional radix passes; offsets and header come from the second
     // (conditional) count / decide
-    for (int i = threadIdx.x; i < kHistSet; i += kBlock) hist_reset[i] = 0u;
+    if (hist_reset != nullptr)   // (the fused fallback clears them device-coherent itself)
+      for (int i = threadIdx.x; i < kHistSet; i += kBlock) hist_reset[i] = 0u;
     return;
   }
   const int gt = s_gt, ge = s_ge;
@@ -1277,6 +1343,111 @@ __device__ __forceinline__ void decide_body(GkCtrl* __restrict__ gctrl, const ui
     hdr[1] = (int32_t)(rt > 0x7fffffff ? 0x7fffffff : rt);
     hdr[2] = s_chosen;
     hdr[3] = __float_as_int(s_thr);
+  }
+}
+
+// --------------------------------------------------------------------------
+// Fused decide + conditional exact fallback (threshold modes): ONE launch in
+// place of decide_kernel and the four early-exit launches of the fallback
+// chain (radix passes 0-2, conditional count), which cost ~4.7 us each even
+// when they exit at once (r5c34: 19 us of a 142 us pipeline).  Block 0 runs
+// the decision and publishes its fallback flag; every other block polls it.
+// No fallback (the common case): every block exits.  Fallback: the grid runs
+// the three histogram passes, the key resolve, the conditional count over
+// the count pass's block chunks and the second decide, separated by grid
+// barriers.  The grid is sized to be co-resident on an idle device (host:
+// occupancy x CUs, <= 512 blocks); kernels sharing the device (backward
+// GEMMs) delay dispatch of the last blocks but never wait on this grid, so
+// the barriers drain.  Every spin is bounded (s_sleep, 2^24 polls).
+// --------------------------------------------------------------------------
+struct FbArgs {
+  uint32_t* flag;       // 0 until block 0 decided, then 1 + ctrl->fallback; cleared by the last block out
+  uint32_t* gen;        // grid-barrier generation
+  uint32_t* bar;        // grid-barrier arrival counter (two-level)
+  uint32_t* exit_ctr;   // exit arrival counter (two-level)
+  uint32_t* hist;       // exact-key histogram set
+  uint32_t* blockcnt;
+  const float* x;
+  int64_t n, kfb, chunk_tiles;
+  int G;                // count-pass blocks (the select grid)
+};
+
+// MI355X_MICROARCH.md "inter-workgroup visibility": every storing wave waits
+// for its stores, barrier, lane 0 releases (agent; the explicit wait after
+// the fence, which ROCm 7.2 can drop), counts in; the last arrival bumps the
+// generation, the others poll it relaxed; then ONE agent acquire + wait and a
+// barrier before any load of another block's bytes.
+__device__ __forceinline__ void grid_sync(const FbArgs& f) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t g0 = ld_dev(f.gen);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // generation read before this block counts in
+    if (arrive(f.bar, gridDim.x, blockIdx.x)) {
+      st_dev(f.gen, g0 + 1u);
+    } else {
+      uint32_t spins = 0;
+      while (ld_dev(f.gen) == g0 && ++spins < (1u << 24)) __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+template <bool VEC, bool DECIDE>
+__global__ __launch_bounds__(kBlock) void decide_fb_kernel(DecArgs da, FbArgs f) {
+  GkCtrl* ctrl = da.ctrl;
+  const int bid = blockIdx.x, nblk = gridDim.x;
+  __shared__ uint32_t s_fb;
+  if (DECIDE) {
+    if (bid == 0) {
+      decide_body(ctrl, f.blockcnt, f.G, da.mode, da.loops, da.k, da.k_cap, da.offsets, da.eqtake, da.blocksel,
+                  da.hdr, 0, nullptr);
+      __syncthreads();
+      if (threadIdx.x == 0) s_fb = (uint32_t)ctrl->fallback;   // this lane wrote it in decide_body
+      __syncthreads();
+      if (s_fb != 0u)
+        for (int i = threadIdx.x; i < kHistSet; i += kBlock) st_dev(&f.hist[i], 0u);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) st_dev(f.flag, 1u + s_fb);
+    } else {
+      if (threadIdx.x == 0) {
+        uint32_t v, spins = 0;
+        while ((v = ld_dev(f.flag)) == 0u && ++spins < (1u << 24)) __builtin_amdgcn_s_sleep(2);
+        s_fb = v == 0u ? 0u : v - 1u;
+      }
+      __syncthreads();
+    }
+  } else {
+    // decided in the count grid's last block (kernel boundary since)
+    if (threadIdx.x == 0) s_fb = (uint32_t)ctrl->fallback;
+    __syncthreads();
+  }
+  if (s_fb != 0u) {
+    __shared__ uint32_t sh_rad[kRadixShWords];   // one LDS histogram buffer for the three passes
+    radix_hist_body<0, kKeyAbs, VEC>(f.x, f.n, 0u, 0u, f.kfb, f.hist, nullptr, bid, nblk, sh_rad);
+    grid_sync(f);
+    radix_hist_body<1, kKeyAbs, VEC>(f.x, f.n, 0u, 0u, f.kfb, f.hist, nullptr, bid, nblk, sh_rad);
+    grid_sync(f);
+    radix_hist_body<2, kKeyAbs, VEC>(f.x, f.n, 0u, 0u, f.kfb, f.hist, nullptr, bid, nblk, sh_rad);
+    grid_sync(f);
+    if (bid == 0) cal_fallback_body(ctrl, f.hist, f.kfb);
+    grid_sync(f);
+    for (int vb = bid; vb < f.G; vb += nblk)
+      count_body<kKeyAbs, VEC, kFallbackCands, 0>(f.x, f.n, 0u, ctrl, f.chunk_tiles, f.blockcnt, nullptr, vb);
+    grid_sync(f);
+    if (bid == 0)
+      decide_body(ctrl, f.blockcnt, f.G, da.mode, da.loops, da.k, da.k_cap, da.offsets, da.eqtake, da.blocksel,
+                  da.hdr, 1, nullptr);
+  }
+  if (DECIDE) {   // the last block out clears the flag for the next call
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0 && arrive(f.exit_ctr, nblk, bid)) st_dev(f.flag, 0u);
   }
 }
 
@@ -1425,15 +1596,21 @@ bool handoff_by_launch_env() {
 
 bool handoff_by_launch(const CompressArgs& a) { return a.handoff < 0 ? handoff_by_launch_env() : a.handoff == 0; }
 
-template <int KEYKIND>
-void launch_count(const CompressArgs& a, const Ws& w, bool vec, int G, int64_t chunk_tiles, GkCtrl* ctrl, int cond,
-                  hipStream_t s) {
-  const int nc = count_cands(a, cond);
+DecArgs make_dec(const CompressArgs& a, const Ws& w, GkCtrl* ctrl, int cond) {
   DecArgs da;
   da.in_kernel = (cond || !handoff_by_launch(a)) ? 1 : 0;
   da.ctrl = ctrl; da.mode = a.mode; da.loops = a.loops; da.k = a.k; da.k_cap = a.k_cap;
   da.offsets = w.offsets; da.eqtake = w.eqtake; da.blocksel = w.blocksel; da.hdr = a.record;
-  da.hist_reset = w.hist; da.counter = w.sync + (cond ? 3 : 1);
+  da.hist_reset = w.hist; da.counter = w.sync + (cond ? 3 : 1) * kSyncWords;
+  return da;
+}
+
+// defer_decide: a launch-hand-off decide is left to decide_fb_kernel
+template <int KEYKIND>
+void launch_count(const CompressArgs& a, const Ws& w, bool vec, int G, int64_t chunk_tiles, GkCtrl* ctrl, int cond,
+                  hipStream_t s, bool defer_decide = false) {
+  const int nc = count_cands(a, cond);
+  const DecArgs da = make_dec(a, w, ctrl, cond);
 #define GK_COUNT3(NC, NX, DEC)                                                                                    \
   if (vec)                                                                                                        \
     hipLaunchKernelGGL((count_kernel<KEYKIND, true, NC, NX, DEC>), dim3(G), dim3(kBlock), 0, s, a.r, a.n, a.seed,  \
@@ -1456,8 +1633,55 @@ void launch_count(const CompressArgs& a, const Ws& w, bool vec, int G, int64_t c
 #undef GK_COUNT
 #undef GK_COUNT2
 #undef GK_COUNT3
-  if (!da.in_kernel)
+  if (!da.in_kernel && !defer_decide)
     hipLaunchKernelGGL(decide_kernel, dim3(1), dim3(kBlock), 0, s, w.blockcnt, G, cond, da);
+}
+
+// fused decide + fallback: GKSGD_FB_FUSED=0 restores the separate launches
+bool fb_fused_env() {
+  const char* e = getenv("GKSGD_FB_FUSED");
+  return !(e != nullptr && strcmp(e, "0") == 0);
+}
+
+// co-resident grid of decide_fb_kernel on an idle device (<= 512); 0: unavailable
+template <bool VEC, bool DECIDE>
+int fb_grid() {
+  static int g = -1;
+  if (g < 0) {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, decide_fb_kernel<VEC, DECIDE>, kBlock, 0) != hipSuccess)
+      per = 0;
+    const int64_t v = (int64_t)per * cus;
+    g = v < 1 ? 0 : (v > 512 ? 512 : (int)v);
+  }
+  return g;
+}
+
+// decide (unless the count grid's last block did) + the conditional exact
+// fallback as one launch; false: not available, nothing launched
+bool launch_decide_fb(const CompressArgs& a, const Ws& w, bool vec, int G, int64_t chunk_tiles, GkCtrl* ctrl,
+                      int64_t kfb, hipStream_t s) {
+  const DecArgs da = make_dec(a, w, ctrl, 0);
+  const bool decide = !da.in_kernel;
+  const int Gf = vec ? (decide ? fb_grid<true, true>() : fb_grid<true, false>())
+                     : (decide ? fb_grid<false, true>() : fb_grid<false, false>());
+  if (Gf < 1) return false;
+  FbArgs f;
+  f.flag = w.sync + kSyncCounters * kSyncWords;
+  f.gen = f.flag + 64;
+  f.bar = w.sync + 4 * kSyncWords;
+  f.exit_ctr = w.sync + 5 * kSyncWords;
+  f.hist = w.hist; f.blockcnt = w.blockcnt; f.x = a.r; f.n = a.n; f.kfb = kfb; f.chunk_tiles = chunk_tiles; f.G = G;
+  if (vec) {
+    if (decide) hipLaunchKernelGGL((decide_fb_kernel<true, true>), dim3(Gf), dim3(kBlock), 0, s, da, f);
+    else hipLaunchKernelGGL((decide_fb_kernel<true, false>), dim3(Gf), dim3(kBlock), 0, s, da, f);
+  } else {
+    if (decide) hipLaunchKernelGGL((decide_fb_kernel<false, true>), dim3(Gf), dim3(kBlock), 0, s, da, f);
+    else hipLaunchKernelGGL((decide_fb_kernel<false, false>), dim3(Gf), dim3(kBlock), 0, s, da, f);
+  }
+  return true;
 }
 
 template <int KEYKIND>
@@ -1533,7 +1757,7 @@ void compress(const CompressArgs& a, hipStream_t s) {
   const int64_t n_stats = a.n_stats > 0 ? a.n_stats : a.n;
   FinArgs fa;
   fa.ctrl = ctrl; fa.n = n_stats; fa.mode = a.mode; fa.loops = a.loops; fa.z = a.z; fa.fixed_thr = a.fixed_thr;
-  fa.k = keff; fa.stats_out = a.stats_out; fa.counter = w.sync + 0;
+  fa.k = keff; fa.stats_out = a.stats_out; fa.counter = w.sync;
   int Gs;
   if (a.u != nullptr && a.chunks != nullptr) {
     Gs = a.chunk_count < kMaxStatsBlocks ? a.chunk_count : kMaxStatsBlocks;
@@ -1597,15 +1821,23 @@ void compress(const CompressArgs& a, hipStream_t s) {
     launch_count<kKeyHash>(a, w, vec_r, G, chunk_tiles, ctrl, 0, s);
     launch_select<kKeyHash>(a, w, vec_r, G, chunk_tiles, ctrl, out_idx, out_val, s);
   } else {
-    launch_count<kKeyAbs>(a, w, vec_r, G, chunk_tiles, ctrl, 0, s);
-    if (a.mode != kModeTopK) {
-      // conditional exact fallback: every kernel below exits at once unless
-      // the decide above set ctrl->fallback -- calibrated mode without a
-      // candidate in [2k/3, 4k/3] (top-k), or a threshold mode whose every
-      // candidate overflows k_cap (top-k_cap)
+    if (a.mode == kModeTopK) {
+      launch_count<kKeyAbs>(a, w, vec_r, G, chunk_tiles, ctrl, 0, s);
+    } else {
+      // conditional exact fallback: calibrated mode without a candidate in
+      // [2k/3, 4k/3] (top-k), or a threshold mode whose every candidate
+      // overflows k_cap (top-k_cap) -- one fused launch (decide_fb_kernel), or
+      // a chain of kernels that exit at once unless the decide set ctrl->fallback
       const int64_t kfb = a.mode == kModeGaussianCal ? keff : (a.k_cap < a.n ? a.k_cap : a.n);
-      launch_radix<kKeyAbs>(a.r, a.n, a.seed, 0u, kfb, hist_exact, vec_r, nullptr, ctrl, a.seed_dev, s, w.sync + 2);
-      launch_count<kKeyAbs>(a, w, vec_r, G, chunk_tiles, ctrl, 1, s);
+      const bool fused = fb_fused_env();
+      launch_count<kKeyAbs>(a, w, vec_r, G, chunk_tiles, ctrl, 0, s, fused);
+      if (!fused || !launch_decide_fb(a, w, vec_r, G, chunk_tiles, ctrl, kfb, s)) {
+        if (fused && !make_dec(a, w, ctrl, 0).in_kernel)   // the deferred decide, after all
+          hipLaunchKernelGGL(decide_kernel, dim3(1), dim3(kBlock), 0, s, w.blockcnt, G, 0, make_dec(a, w, ctrl, 0));
+        launch_radix<kKeyAbs>(a.r, a.n, a.seed, 0u, kfb, hist_exact, vec_r, nullptr, ctrl, a.seed_dev, s,
+                              w.sync + 2 * kSyncWords);
+        launch_count<kKeyAbs>(a, w, vec_r, G, chunk_tiles, ctrl, 1, s);
+      }
     }
     launch_select<kKeyAbs>(a, w, vec_r, G, chunk_tiles, ctrl, out_idx, out_val, s);
   }

@@ -637,3 +637,45 @@ def test_gaussian_overflow_extension_gpu_matches_mirror(cuda):
     assert 6 <= int(recg[2]) < ops.MAX_CAND and int(recg[1]) > k_cap
     assert torch.equal(recg, recc)
     assert torch.equal(rg, rc)
+
+
+@pytest.mark.parametrize("fused", ["1", "0"])
+@pytest.mark.parametrize("handoff", ["launch", "lastblock"])
+def test_fused_fallback_fires_under_load(cuda, fused, handoff, monkeypatch):
+    """The conditional exact fallback FIRING in decide_fb_kernel (one launch:
+    decide, three radix passes, key resolve, conditional count, second decide,
+    separated by grid barriers) on a bucket large enough for every grid at its
+    cap, with GEMMs loading the chip from a second stream: the record, header
+    and residual equal the CPU mirror's word for word, call after call on one
+    set of buffers (the flag / barrier words are reused).  fused=0: the chain
+    of separate launches; handoff: decide in the fused kernel or in the count
+    grid's last block."""
+    monkeypatch.setenv("GKSGD_FB_FUSED", fused)
+    monkeypatch.setenv("GKSGD_HANDOFF", handoff)
+    n = 6_000_000
+    k = 300
+    k_cap = 400
+    gb = ops.CompressBuffers(k_cap, cuda)
+    cb = ops.CompressBuffers(k_cap, "cpu")
+    side = torch.cuda.Stream()
+    a = torch.randn(4096, 4096, device=cuda)
+    for it in range(3):
+        g = torch.Generator().manual_seed(50 + it)
+        x = torch.randn(n, generator=g) * 1e-4
+        hot = torch.randperm(n, generator=g)[: n // 100]
+        x[hot] = (1.0 + torch.rand(hot.numel(), generator=g)) * torch.sign(torch.randn(hot.numel(), generator=g))
+        r = torch.zeros(n)
+        xg, rg = x.to(cuda), r.to(cuda)
+        with torch.cuda.stream(side):
+            for _ in range(4):
+                a = torch.tanh(a @ a * 1e-3)
+        ops.compress_(xg, rg, gb, ops.MODE_GAUSSIAN, ec=True, zero_g=True, loops=3, z=gaussian_z(0.001), k=k,
+                      k_cap=k_cap, seed=it)
+        xc, rc = x.clone(), r.clone()
+        ops.compress_(xc, rc, cb, ops.MODE_GAUSSIAN, ec=True, zero_g=True, loops=3, z=gaussian_z(0.001), k=k,
+                      k_cap=k_cap, seed=it)
+        torch.cuda.synchronize()
+        recg = gb.record.cpu()
+        assert int(recg[2]) == ops.OVERFLOW_EXACT, (it, recg[:4].tolist())
+        assert torch.equal(recg, cb.record), it
+        assert torch.equal(rg.cpu(), rc), it
