@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Run ONE gemm.hip kernel configuration repeatedly (for rocprofv3 counter
-passes): python bench/gemm_probe.py --op conv|gemm|wgrad3|lwgrad|cwgrad --cfg N [--iters 20]
+passes): python bench/gemm_probe.py --op conv|gemm|gemm_bnb|wgrad3|lwgrad|cwgrad --cfg N [--iters 20]
 [--dtype bf16|f32] [--k 3] [--stride 1]
 
 ``--sweep 1,2,3``: time every listed cfg with HIP events instead and print
@@ -45,6 +45,13 @@ def make(a, cfg):
     X = x.permute(0, 2, 3, 1).reshape(-1, a.C)
     W = torch.randn(K, a.C, device="cuda", dtype=dt)
     Y = torch.empty(X.shape[0], K, device="cuda", dtype=dt)
+    if a.op == "gemm_bnb":   # grad-input GEMM with the BN-backward epilogue (dz = mask ? acc + dy2 : 0, stats)
+        M = X.shape[0]
+        h = torch.randn(M, K, device="cuda", dtype=dt)
+        d2 = torch.randn(M, K, device="cuda", dtype=dt)
+        mask = torch.randint(0, 16, (M, K // 4), device="cuda", dtype=torch.uint8)
+        st = torch.empty(2, 1280, K, device="cuda")
+        return (lambda: g.gemm_nt(X, W, Y, cfg, a.mb, st, None, h, d2, mask)), 2.0 * M * K * a.C
     return (lambda: g.gemm_nt(X, W, Y, cfg, a.mb)), 2.0 * X.shape[0] * K * a.C
 
 

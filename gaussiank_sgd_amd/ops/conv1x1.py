@@ -264,6 +264,11 @@ _CACHE = os.environ.get("GKSGD_GEMM_CACHE", os.path.join(os.path.dirname(os.path
     os.path.abspath(__file__)))), "tuning", "gemm_choices.json"))
 if _TUNE and _CACHE and os.path.exists(_CACHE) and os.environ.get("GKSGD_GEMM_RETUNE", "0") == "0":
     load_choices(_CACHE)
+    # GKSGD_GEMM_RETUNE_ONLY=dgrad_bn,...: retune only the keys of these directions
+    _only = {d for d in os.environ.get("GKSGD_GEMM_RETUNE_ONLY", "").split(",") if d}
+    if _only:
+        for _k in [k for k in _choices if k and k[0] in _only]:
+            del _choices[_k]
 
 
 def tuned_choices() -> Dict[tuple, tuple]:

@@ -1942,53 +1942,63 @@ gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float ssum[4][4], ssq[4][4], bia[4][4];
+  // (BN-backward epilogue: no bias -- the binding makes them exclusive -- so
+  // no 16 bias registers beside its operand loads)
+  float ssum[4][4], ssq[4][4], bia[BNB ? 1 : 4][4];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       ssum[a][b] = ssq[a][b] = 0.f;
-      bia[a][b] = bias ? bias[n0 + wn * 64 + a * 16 + fq * 4 + b] : 0.f;
+      if constexpr (!BNB) bia[a][b] = bias ? bias[n0 + wn * 64 + a * 16 + fq * 4 + b] : 0.f;
     }
 
   auto epilogue = [&](int64_t mt) __attribute__((always_inline)) {
     const int64_t mbase = mt * Cfg::BM;
+    // BN-backward operands two fragments at a time (all four beside the
+    // accumulators and the staged next slice spill at 256 VGPRs)
+    constexpr int EH = BNB ? 1 : 4;
 #pragma unroll
     for (int ms = 0; ms < 4; ++ms) {
       const int64_t m = mbase + wm * 64 + ms * 16 + fr;
       const bool live = m < M;
-      f32x4 ehv[4], ed2[4];
-      uint32_t ebits[4];
+#pragma unroll
+      for (int nh = 0; nh < 4; nh += EH) {
+      f32x4 ehv[EH], ed2[EH];
+      uint32_t ebits[EH];
       if constexpr (BNB) {
 #pragma unroll
-        for (int ns = 0; ns < 4; ++ns) {
-          ehv[ns] = ed2[ns] = f32x4{0.f, 0.f, 0.f, 0.f};
-          ebits[ns] = 0u;
+        for (int e = 0; e < EH; ++e) {
+          ehv[e] = ed2[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+          ebits[e] = 0u;
         }
         if (live) {
 #pragma unroll
-          for (int ns = 0; ns < 4; ++ns) {
-            const int n = n0 + wn * 64 + ns * 16 + fq * 4;
-            ehv[ns] = *reinterpret_cast<const f32x4*>(static_cast<const float*>(bb.h) + m * ldc + n);
-            if (bb.dy2) ed2[ns] = *reinterpret_cast<const f32x4*>(static_cast<const float*>(bb.dy2) + m * ldc + n);
-            ebits[ns] = bb.mask ? (uint32_t)bb.mask[m * (Ntot >> 2) + (n >> 2)] : 0xfu;
+          for (int e = 0; e < EH; ++e) {
+            const int n = n0 + wn * 64 + (nh + e) * 16 + fq * 4;
+            ehv[e] = *reinterpret_cast<const f32x4*>(static_cast<const float*>(bb.h) + m * ldc + n);
+            if (bb.dy2) ed2[e] = *reinterpret_cast<const f32x4*>(static_cast<const float*>(bb.dy2) + m * ldc + n);
+            ebits[e] = bb.mask ? (uint32_t)bb.mask[m * (Ntot >> 2) + (n >> 2)] : 0xfu;
           }
         }
       }
 #pragma unroll
-      for (int ns = 0; ns < 4; ++ns) {
+      for (int e = 0; e < EH; ++e) {
+        const int ns = nh + e;
         const int n = n0 + wn * 64 + ns * 16 + fq * 4;
         f32x4 v = acc[ms][ns];
         acc[ms][ns] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (!BNB) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += bia[ns][r];
+          for (int r = 0; r < 4; ++r) v[r] += bia[ns][r];
+        }
         if constexpr (BNB) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float dz = (ebits[ns] >> r) & 1u ? v[r] + ed2[ns][r] : 0.f;
+            const float dz = (ebits[e] >> r) & 1u ? v[r] + ed2[e][r] : 0.f;
             v[r] = dz;
             ssum[ns][r] += dz;
-            ssq[ns][r] = fmaf(dz, ehv[ns][r], ssq[ns][r]);
+            ssq[ns][r] = fmaf(dz, ehv[e][r], ssq[ns][r]);
           }
         } else {
           if (stats && live) {
@@ -2000,6 +2010,7 @@ gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
           }
         }
         if (live) *reinterpret_cast<f32x4*>(C + m * ldc + n) = v;
+      }
       }
     }
   };
