@@ -43,7 +43,9 @@ static int nt_unit_f32(bool gather, GK_NT_UNIT_ARGS) {
     // family 3: B pre-split (geo.b3, the binding's split3_rows)
     if (lza || geo.KZ > 1 || geo.RH || (fam == 3) != (geo.b3 != nullptr)) return -2;
     if (gather) {
-      if (geo.C % 32 != 0) return -2;
+      // 32-bit element offsets into x (gemm_kern.h x62 gather)
+      const int64_t nimg = M / ((int64_t)geo.OH * geo.OW);
+      if (geo.C % 32 != 0 || nimg * geo.H * geo.W * geo.C >= ((int64_t)1 << 31)) return -2;
       return nt_x62_gat(static_cast<const float*>(A), static_cast<const float*>(B), static_cast<float*>(C), M, N, K,
                         cfg % 100000, max_blocks, geo, stats, stats_ld, stats_rows, bb, stream);
     }

@@ -1811,12 +1811,16 @@ gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
   // change (a wave-uniform branch), not for every slice
   int64_t l_mt = bx;
   int l_ks = 0;
-  const float* lpa[Cfg::PRA];
+  const float* lpa[GATHER ? 1 : Cfg::PRA];
   const float* lpb[Cfg::PRB];
   // gather: tap / channel offset of the next slice (wave-uniform) and, per
-  // piece, its output pixel's in-image taps (bit kh of okh / kw of okw)
+  // piece, its output pixel's in-image taps (bits kh of okhw, bits 8 + kw) and
+  // its 32-bit element offset into x (the host refuses x of >= 2^31 elements):
+  // two registers per piece instead of four -- the 4x2-wave gather tiles
+  // spilled with 64-bit pointers and separate tap masks
   int l_kh = 0, l_kw = 0, l_c0 = 0;
-  uint32_t okh[Cfg::PRA], okw[Cfg::PRA];
+  uint32_t okhw[GATHER ? Cfg::PRA : 1];
+  int32_t aoff[GATHER ? Cfg::PRA : 1];
   auto set_a_rows = [&]() __attribute__((always_inline)) {
     const int64_t m0 = l_mt * Cfg::BM;
 #pragma unroll
@@ -1836,9 +1840,8 @@ gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
           bh |= (uint32_t)((unsigned)(ih0 + t) < (unsigned)geo.H) << t;
           bw |= (uint32_t)((unsigned)(iw0 + t) < (unsigned)geo.W) << t;
         }
-        okh[p] = bh;
-        okw[p] = bw;
-        lpa[p] = A + (((int64_t)n * geo.H + ih0) * geo.W + iw0) * geo.C + (cid & 3) * 8;
+        okhw[p] = bh | (bw << 8);
+        aoff[p] = (((int)n * geo.H + ih0) * geo.W + iw0) * geo.C + (cid & 3) * 8;
       } else {
         lpa[p] = A + gr * lda + (cid & 3) * 8;
       }
@@ -1857,14 +1860,16 @@ gemm_nt_x62_kernel(const float* __restrict__ A, int64_t lda, const float* __rest
     const int64_t toff = GATHER ? (int64_t)(l_kh * geo.W + l_kw) * geo.C + l_c0 : 0;   // wave-uniform
 #pragma unroll
     for (int p = 0; p < Cfg::PRA; ++p) {
-      const float* src = lpa[p];
+      const float* src;
       if constexpr (GATHER) {
-        const bool ok = ((okh[p] >> l_kh) & (okw[p] >> l_kw) & 1u) != 0u;
-        src = ok ? src + toff : zrow;
+        const bool ok = ((okhw[p] >> l_kh) & (okhw[p] >> (8 + l_kw)) & 1u) != 0u;
+        src = ok ? A + ((int64_t)aoff[p] + toff) : zrow;
+      } else {
+        src = lpa[p];
+        lpa[p] += 32;
       }
       ra[q][p][0] = *reinterpret_cast<const f32x4*>(src);
       ra[q][p][1] = *reinterpret_cast<const f32x4*>(src + 4);
-      if constexpr (!GATHER) lpa[p] += 32;
     }
 #pragma unroll
     for (int p = 0; p < Cfg::PRB; ++p) {
