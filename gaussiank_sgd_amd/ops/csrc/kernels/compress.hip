@@ -18,12 +18,13 @@
 //
 // The 1-workgroup steps run as their own launches or (handoff = lastblock) in
 // the LAST block of the preceding grid pass (last_block(): device-coherent
-// partials + a two-level arrival counter, no spin).  Threshold modes fold the
-// decide and the conditional exact fallback (three radix passes, key resolve,
-// second count / decide) into ONE launch, decide_fb_kernel, whose grid
-// barriers run only when the fallback fires: stats, finalize, count,
-// decide_fb, select -- 5 launches per call (r5c36: 132 us span on the
-// 25.6 M bucket, from 144 us with the decide and four early-exit launches).
+// partials + a two-level arrival counter, no spin).  With launch hand-offs,
+// threshold modes fold the decide and the conditional exact fallback (three
+// radix passes, key resolve, second count / decide) into ONE launch,
+// decide_fb_kernel, whose grid barriers run only when the fallback fires:
+// stats, finalize, count, decide_fb, select -- 5 launches per call (r5c39:
+// 125.6 us kernel span on the 25.6 M bucket, from 142.0 us with the decide and
+// four early-exit launches).
 //
 // Reference semantics reproduced (compression.py):
 //   gaussian  :358-389  threshold mu + |ppf(ratio/2)| * sigma, <=3 loops
@@ -1355,10 +1356,14 @@ __device__ __forceinline__ void decide_body(GkCtrl* __restrict__ gctrl, const ui
 // No fallback (the common case): every block exits.  Fallback: the grid runs
 // the three histogram passes, the key resolve, the conditional count over
 // the count pass's block chunks and the second decide, separated by grid
-// barriers.  The grid is sized to be co-resident on an idle device (host:
-// occupancy x CUs, <= 512 blocks); kernels sharing the device (backward
-// GEMMs) delay dispatch of the last blocks but never wait on this grid, so
-// the barriers drain.  Every spin is bounded (s_sleep, 2^24 polls).
+// barriers.  The grid is HALF of what is co-resident on an idle device
+// (host: occupancy x CUs / 2, <= 512 blocks), so two such grids -- two ranks
+// sharing one GPU in the multi-rank rehearsals -- are resident together.
+// Used for the calls with launch hand-offs only: a bucket compressed while
+// the backward still runs (handoff = lastblock) keeps the launch chain, whose
+// blocks do not hold CU slots while GEMM blocks they share the device with
+// drain (and whose extra launches are hidden under the backward anyway).
+// Every spin is bounded (s_sleep, 2^24 polls).
 // --------------------------------------------------------------------------
 struct FbArgs {
   uint32_t* flag;       // 0 until block 0 decided, then 1 + ctrl->fallback; cleared by the last block out
@@ -1397,12 +1402,12 @@ __device__ __forceinline__ void grid_sync(const FbArgs& f) {
   __syncthreads();
 }
 
-template <bool VEC, bool DECIDE>
+template <bool VEC>
 __global__ __launch_bounds__(kBlock) void decide_fb_kernel(DecArgs da, FbArgs f) {
   GkCtrl* ctrl = da.ctrl;
   const int bid = blockIdx.x, nblk = gridDim.x;
   __shared__ uint32_t s_fb;
-  if (DECIDE) {
+  {
     if (bid == 0) {
       decide_body(ctrl, f.blockcnt, f.G, da.mode, da.loops, da.k, da.k_cap, da.offsets, da.eqtake, da.blocksel,
                   da.hdr, 0, nullptr);
@@ -1422,10 +1427,6 @@ __global__ __launch_bounds__(kBlock) void decide_fb_kernel(DecArgs da, FbArgs f)
       }
       __syncthreads();
     }
-  } else {
-    // decided in the count grid's last block (kernel boundary since)
-    if (threadIdx.x == 0) s_fb = (uint32_t)ctrl->fallback;
-    __syncthreads();
   }
   if (s_fb != 0u) {
     __shared__ uint32_t sh_rad[kRadixShWords];   // one LDS histogram buffer for the three passes
@@ -1444,11 +1445,10 @@ __global__ __launch_bounds__(kBlock) void decide_fb_kernel(DecArgs da, FbArgs f)
       decide_body(ctrl, f.blockcnt, f.G, da.mode, da.loops, da.k, da.k_cap, da.offsets, da.eqtake, da.blocksel,
                   da.hdr, 1, nullptr);
   }
-  if (DECIDE) {   // the last block out clears the flag for the next call
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0 && arrive(f.exit_ctr, nblk, bid)) st_dev(f.flag, 0u);
-  }
+  // the last block out clears the flag for the next call
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0 && arrive(f.exit_ctr, nblk, bid)) st_dev(f.flag, 0u);
 }
 
 // --------------------------------------------------------------------------
@@ -1643,30 +1643,29 @@ bool fb_fused_env() {
   return !(e != nullptr && strcmp(e, "0") == 0);
 }
 
-// co-resident grid of decide_fb_kernel on an idle device (<= 512); 0: unavailable
-template <bool VEC, bool DECIDE>
+// half the co-resident grid of decide_fb_kernel on an idle device (<= 512);
+// 0: unavailable
+template <bool VEC>
 int fb_grid() {
   static int g = -1;
   if (g < 0) {
     int dev = 0, cus = 0, per = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, decide_fb_kernel<VEC, DECIDE>, kBlock, 0) != hipSuccess)
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, decide_fb_kernel<VEC>, kBlock, 0) != hipSuccess)
       per = 0;
-    const int64_t v = (int64_t)per * cus;
+    const int64_t v = (int64_t)per * cus / 2;
     g = v < 1 ? 0 : (v > 512 ? 512 : (int)v);
   }
   return g;
 }
 
-// decide (unless the count grid's last block did) + the conditional exact
-// fallback as one launch; false: not available, nothing launched
+// decide + the conditional exact fallback as one launch (launch hand-offs
+// only); false: not available, nothing launched
 bool launch_decide_fb(const CompressArgs& a, const Ws& w, bool vec, int G, int64_t chunk_tiles, GkCtrl* ctrl,
                       int64_t kfb, hipStream_t s) {
   const DecArgs da = make_dec(a, w, ctrl, 0);
-  const bool decide = !da.in_kernel;
-  const int Gf = vec ? (decide ? fb_grid<true, true>() : fb_grid<true, false>())
-                     : (decide ? fb_grid<false, true>() : fb_grid<false, false>());
+  const int Gf = vec ? fb_grid<true>() : fb_grid<false>();
   if (Gf < 1) return false;
   FbArgs f;
   f.flag = w.sync + kSyncCounters * kSyncWords;
@@ -1674,13 +1673,8 @@ bool launch_decide_fb(const CompressArgs& a, const Ws& w, bool vec, int G, int64
   f.bar = w.sync + 4 * kSyncWords;
   f.exit_ctr = w.sync + 5 * kSyncWords;
   f.hist = w.hist; f.blockcnt = w.blockcnt; f.x = a.r; f.n = a.n; f.kfb = kfb; f.chunk_tiles = chunk_tiles; f.G = G;
-  if (vec) {
-    if (decide) hipLaunchKernelGGL((decide_fb_kernel<true, true>), dim3(Gf), dim3(kBlock), 0, s, da, f);
-    else hipLaunchKernelGGL((decide_fb_kernel<true, false>), dim3(Gf), dim3(kBlock), 0, s, da, f);
-  } else {
-    if (decide) hipLaunchKernelGGL((decide_fb_kernel<false, true>), dim3(Gf), dim3(kBlock), 0, s, da, f);
-    else hipLaunchKernelGGL((decide_fb_kernel<false, false>), dim3(Gf), dim3(kBlock), 0, s, da, f);
-  }
+  if (vec) hipLaunchKernelGGL((decide_fb_kernel<true>), dim3(Gf), dim3(kBlock), 0, s, da, f);
+  else hipLaunchKernelGGL((decide_fb_kernel<false>), dim3(Gf), dim3(kBlock), 0, s, da, f);
   return true;
 }
 
@@ -1829,10 +1823,10 @@ void compress(const CompressArgs& a, hipStream_t s) {
       // overflows k_cap (top-k_cap) -- one fused launch (decide_fb_kernel), or
       // a chain of kernels that exit at once unless the decide set ctrl->fallback
       const int64_t kfb = a.mode == kModeGaussianCal ? keff : (a.k_cap < a.n ? a.k_cap : a.n);
-      const bool fused = fb_fused_env();
+      const bool fused = fb_fused_env() && handoff_by_launch(a);
       launch_count<kKeyAbs>(a, w, vec_r, G, chunk_tiles, ctrl, 0, s, fused);
       if (!fused || !launch_decide_fb(a, w, vec_r, G, chunk_tiles, ctrl, kfb, s)) {
-        if (fused && !make_dec(a, w, ctrl, 0).in_kernel)   // the deferred decide, after all
+        if (fused)   // the deferred decide, after all
           hipLaunchKernelGGL(decide_kernel, dim3(1), dim3(kBlock), 0, s, w.blockcnt, G, 0, make_dec(a, w, ctrl, 0));
         launch_radix<kKeyAbs>(a.r, a.n, a.seed, 0u, kfb, hist_exact, vec_r, nullptr, ctrl, a.seed_dev, s,
                               w.sync + 2 * kSyncWords);

@@ -647,9 +647,9 @@ def test_fused_fallback_fires_under_load(cuda, fused, handoff, monkeypatch):
     separated by grid barriers) on a bucket large enough for every grid at its
     cap, with GEMMs loading the chip from a second stream: the record, header
     and residual equal the CPU mirror's word for word, call after call on one
-    set of buffers (the flag / barrier words are reused).  fused=0: the chain
-    of separate launches; handoff: decide in the fused kernel or in the count
-    grid's last block."""
+    set of buffers (the flag / barrier words are reused).  fused=0, or the
+    in-grid hand-off (handoff=lastblock: the buckets compressed while the
+    backward runs), take the chain of separate launches instead."""
     monkeypatch.setenv("GKSGD_FB_FUSED", fused)
     monkeypatch.setenv("GKSGD_HANDOFF", handoff)
     n = 6_000_000
