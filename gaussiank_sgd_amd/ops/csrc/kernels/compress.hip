@@ -1402,15 +1402,18 @@ __device__ __forceinline__ void grid_sync(const FbArgs& f) {
   __syncthreads();
 }
 
-template <bool VEC>
+// DECIDED: the count pass already decided in its last block (kernel boundary
+// in between), block 0 only reads the flag.
+template <bool VEC, bool DECIDED>
 __global__ __launch_bounds__(kBlock) void decide_fb_kernel(DecArgs da, FbArgs f) {
   GkCtrl* ctrl = da.ctrl;
   const int bid = blockIdx.x, nblk = gridDim.x;
   __shared__ uint32_t s_fb;
   {
     if (bid == 0) {
-      decide_body(ctrl, f.blockcnt, f.G, da.mode, da.loops, da.k, da.k_cap, da.offsets, da.eqtake, da.blocksel,
-                  da.hdr, 0, nullptr);
+      if constexpr (!DECIDED)
+        decide_body(ctrl, f.blockcnt, f.G, da.mode, da.loops, da.k, da.k_cap, da.offsets, da.eqtake, da.blocksel,
+                    da.hdr, 0, nullptr);
       __syncthreads();
       if (threadIdx.x == 0) s_fb = (uint32_t)ctrl->fallback;   // this lane wrote it in decide_body
       __syncthreads();
@@ -1643,6 +1646,20 @@ bool fb_fused_env() {
   return !(e != nullptr && strcmp(e, "0") == 0);
 }
 
+// GKSGD_STEP_INGRID=1 (opt-in, measured slower): launch hand-offs with the
+// 1-workgroup steps in-grid -- the finalize in the stats pass's last block, the
+// decide in the count pass's last block, the fused fallback launch only
+// reading the decision.  25.6 M bucket, same box (r5c54): stats + finalize
+// 72.8 us in-grid vs 62.6 + 7.9 as launches, count + decide_fb 33.0 + 4.7 vs
+// 21.6 + 14.4; kernel span 131.8 vs 130.0 us, wall 134.2 / 136.1 vs 137.1 /
+// 139.6 us (two fewer launches) -- within noise either way: the last block's
+// wait for the arrivals and its serial reduction cost about the kernel
+// boundary they replace, so the default keeps the unchanged launch chain.
+bool step_ingrid_env() {
+  const char* e = getenv("GKSGD_STEP_INGRID");
+  return e != nullptr && strcmp(e, "1") == 0;
+}
+
 // half the co-resident grid of decide_fb_kernel on an idle device (<= 512);
 // 0: unavailable
 template <bool VEC>
@@ -1652,7 +1669,7 @@ int fb_grid() {
     int dev = 0, cus = 0, per = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, decide_fb_kernel<VEC>, kBlock, 0) != hipSuccess)
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, decide_fb_kernel<VEC, false>, kBlock, 0) != hipSuccess)
       per = 0;
     const int64_t v = (int64_t)per * cus / 2;
     g = v < 1 ? 0 : (v > 512 ? 512 : (int)v);
@@ -1663,7 +1680,7 @@ int fb_grid() {
 // decide + the conditional exact fallback as one launch (launch hand-offs
 // only); false: not available, nothing launched
 bool launch_decide_fb(const CompressArgs& a, const Ws& w, bool vec, int G, int64_t chunk_tiles, GkCtrl* ctrl,
-                      int64_t kfb, hipStream_t s) {
+                      int64_t kfb, hipStream_t s, bool decided) {
   const DecArgs da = make_dec(a, w, ctrl, 0);
   const int Gf = vec ? fb_grid<true>() : fb_grid<false>();
   if (Gf < 1) return false;
@@ -1673,8 +1690,13 @@ bool launch_decide_fb(const CompressArgs& a, const Ws& w, bool vec, int G, int64
   f.bar = w.sync + 4 * kSyncWords;
   f.exit_ctr = w.sync + 5 * kSyncWords;
   f.hist = w.hist; f.blockcnt = w.blockcnt; f.x = a.r; f.n = a.n; f.kfb = kfb; f.chunk_tiles = chunk_tiles; f.G = G;
-  if (vec) hipLaunchKernelGGL((decide_fb_kernel<true>), dim3(Gf), dim3(kBlock), 0, s, da, f);
-  else hipLaunchKernelGGL((decide_fb_kernel<false>), dim3(Gf), dim3(kBlock), 0, s, da, f);
+  if (decided) {
+    if (vec) hipLaunchKernelGGL((decide_fb_kernel<true, true>), dim3(Gf), dim3(kBlock), 0, s, da, f);
+    else hipLaunchKernelGGL((decide_fb_kernel<false, true>), dim3(Gf), dim3(kBlock), 0, s, da, f);
+  } else {
+    if (vec) hipLaunchKernelGGL((decide_fb_kernel<true, false>), dim3(Gf), dim3(kBlock), 0, s, da, f);
+    else hipLaunchKernelGGL((decide_fb_kernel<false, false>), dim3(Gf), dim3(kBlock), 0, s, da, f);
+  }
   return true;
 }
 
@@ -1746,7 +1768,12 @@ void compress(const CompressArgs& a, hipStream_t s) {
   //    correction when a chunk table is given); threshold modes finalize in
   //    the last stats block (radix modes need the histograms first)
   const bool radix_mode = a.mode == kModeTopK || a.mode == kModeRandomK || a.mode == kModeDGC;
-  const bool fin_in = !radix_mode && !handoff_by_launch(a);   // finalize in the stats pass's last block
+  const bool by_launch = handoff_by_launch(a);
+  const bool fb_fused = fb_fused_env() && by_launch;
+  // finalize in the stats pass's last block: in-grid hand-offs, or launch
+  // hand-offs with the fused fallback and the in-grid steps
+  const bool step_in = fb_fused && step_ingrid_env();
+  const bool fin_in = !radix_mode && (!by_launch || step_in);
   const int64_t keff = a.k < a.n ? a.k : a.n;
   const int64_t n_stats = a.n_stats > 0 ? a.n_stats : a.n;
   FinArgs fa;
@@ -1823,10 +1850,13 @@ void compress(const CompressArgs& a, hipStream_t s) {
       // overflows k_cap (top-k_cap) -- one fused launch (decide_fb_kernel), or
       // a chain of kernels that exit at once unless the decide set ctrl->fallback
       const int64_t kfb = a.mode == kModeGaussianCal ? keff : (a.k_cap < a.n ? a.k_cap : a.n);
-      const bool fused = fb_fused_env() && handoff_by_launch(a);
-      launch_count<kKeyAbs>(a, w, vec_r, G, chunk_tiles, ctrl, 0, s, fused);
-      if (!fused || !launch_decide_fb(a, w, vec_r, G, chunk_tiles, ctrl, kfb, s)) {
-        if (fused)   // the deferred decide, after all
+      const bool fused = fb_fused;
+      // step_in: the count pass decides in its last block, decide_fb reads it
+      CompressArgs ac = a;
+      if (step_in) ac.handoff = 1;
+      launch_count<kKeyAbs>(ac, w, vec_r, G, chunk_tiles, ctrl, 0, s, fused && !step_in);
+      if (!fused || !launch_decide_fb(a, w, vec_r, G, chunk_tiles, ctrl, kfb, s, step_in)) {
+        if (fused && !step_in)   // the deferred decide, after all
           hipLaunchKernelGGL(decide_kernel, dim3(1), dim3(kBlock), 0, s, w.blockcnt, G, 0, make_dec(a, w, ctrl, 0));
         launch_radix<kKeyAbs>(a.r, a.n, a.seed, 0u, kfb, hist_exact, vec_r, nullptr, ctrl, a.seed_dev, s,
                               w.sync + 2 * kSyncWords);

@@ -559,7 +559,16 @@ def test_compress_reused_buffers_varying_sizes(cuda, mode):
         assert torch.equal(rg.cpu(), rc)
 
 
-@pytest.mark.parametrize("handoff", ["launch", "lastblock"])
+def _set_handoff(monkeypatch, handoff):
+    """launch: launch hand-offs (finalize / decide as their own launches, the
+    default); launch_ingrid: the same with the finalize / decide in the stats /
+    count passes' last blocks (GKSGD_STEP_INGRID=1); lastblock: the in-grid
+    hand-off of the buckets compressed during the backward."""
+    monkeypatch.setenv("GKSGD_HANDOFF", "lastblock" if handoff == "lastblock" else "launch")
+    monkeypatch.setenv("GKSGD_STEP_INGRID", "1" if handoff == "launch_ingrid" else "0")
+
+
+@pytest.mark.parametrize("handoff", ["launch", "launch_ingrid", "lastblock"])
 @pytest.mark.parametrize("mode", [ops.MODE_GAUSSIAN, ops.MODE_GAUSSIAN_CAL, ops.MODE_TOPK, ops.MODE_DGC])
 def test_last_block_handoff_stress(cuda, mode, handoff, monkeypatch):
     """The last-block hand-offs (stats -> finalize, count -> decide, radix ->
@@ -571,7 +580,7 @@ def test_last_block_handoff_stress(cuda, mode, handoff, monkeypatch):
     against the count above its own threshold (count -> decide), the record's
     indices / values / residual against that selection (decide's offsets),
     and for exact top-k the whole record against the CPU mirror."""
-    monkeypatch.setenv("GKSGD_HANDOFF", handoff)   # compress.hip handoff_by_launch()
+    _set_handoff(monkeypatch, handoff)   # compress.hip handoff_by_launch() / step_ingrid_env()
     n = 2048 * 4096 * 2 + 4093          # > kMaxStatsBlocks full tiles: every grid at its cap
     k = n // 1000
     k_cap = (4 * k + 2) // 3 if mode != ops.MODE_TOPK else k
@@ -640,7 +649,7 @@ def test_gaussian_overflow_extension_gpu_matches_mirror(cuda):
 
 
 @pytest.mark.parametrize("fused", ["1", "0"])
-@pytest.mark.parametrize("handoff", ["launch", "lastblock"])
+@pytest.mark.parametrize("handoff", ["launch", "launch_ingrid", "lastblock"])
 def test_fused_fallback_fires_under_load(cuda, fused, handoff, monkeypatch):
     """The conditional exact fallback FIRING in decide_fb_kernel (one launch:
     decide, three radix passes, key resolve, conditional count, second decide,
@@ -651,7 +660,7 @@ def test_fused_fallback_fires_under_load(cuda, fused, handoff, monkeypatch):
     in-grid hand-off (handoff=lastblock: the buckets compressed while the
     backward runs), take the chain of separate launches instead."""
     monkeypatch.setenv("GKSGD_FB_FUSED", fused)
-    monkeypatch.setenv("GKSGD_HANDOFF", handoff)
+    _set_handoff(monkeypatch, handoff)
     n = 6_000_000
     k = 300
     k_cap = 400
