@@ -319,6 +319,18 @@ def run_phase(args, ph: Phase, steps: int, warmup: int, P: int, graph: Optional[
     return float(t[0]), float(t[1])
 
 
+def sync_timeouts(opt) -> int:
+    """Expired bounded spins of the fused compression decide / fallback grid
+    over every compressed bucket (0 unless a grid was not co-resident)."""
+    from gaussiank_sgd_amd import ops
+    n = 0
+    for b in opt.arena.buckets:
+        bufs = getattr(b, "bufs", None)
+        if bufs is not None and getattr(bufs, "ctrl", None) is not None and bufs.ctrl.is_cuda:
+            n += ops.sync_timeouts(bufs)
+    return n
+
+
 def phase_info(ph: Phase) -> dict:
     """Exchanger kind and the event-timed collectives of the phase's timed
     loop (native engine; empty for torch.distributed / local)."""
@@ -327,6 +339,8 @@ def phase_info(ph: Phase) -> dict:
     wp = getattr(ph.trainer, "weight_prep", None) if ph is not None else None
     if wp is not None:
         info["weight_prep"] = {"relayouts": len(wp.entries), "batched_launches": wp.launches}
+    if ph is not None and ph.opt is not None:
+        info["compress_sync_timeouts"] = sync_timeouts(ph.opt)
     if ex is not None:
         try:
             info["timed_loop"] = ex.stats() or None
@@ -562,6 +576,7 @@ def main() -> int:
         "world": P,
         "exchange": kind,
         "replicas_consistent": replicas,
+        "compress_sync_timeouts": sync_timeouts(opt),
         "exposed_comm_ms": round(exposed, 3) if exposed == exposed else None,
         "collectives": None,
         "effective_compression_ratio": round(ratio, 1),

@@ -41,6 +41,7 @@ OVERFLOW_EXACT = 17  # ... when a threshold mode overflowed k_cap with every can
 CAL_CAND = 8        # calibrated ladder size (gk::kCalCand)
 
 MAX_CAND = 16
+CTRL_SYNC_TIMEOUTS_U32 = 364 // 4   # GkCtrl::sync_timeouts (static_assert in gk_kernels.h)
 CHUNK_ELEMS = 16384
 REC_HDR = 4
 
@@ -583,7 +584,14 @@ def ctrl_fields(bufs: CompressBuffers) -> dict:
     out["bounds"] = [int(x) for x in u32[16:16 + MAX_CAND]]
     out["ncand"] = int(raw.numpy().view("int32")[16 + MAX_CAND])
     out["chosen"] = int(raw.numpy().view("int32")[17 + MAX_CAND])
+    out["sync_timeouts"] = int(u32[CTRL_SYNC_TIMEOUTS_U32])
     return out
+
+
+def sync_timeouts(bufs: CompressBuffers) -> int:
+    """Sticky count of expired bounded spins in the fused decide / fallback
+    grid of this bucket's calls (compress.hip sync_timeout; host sync)."""
+    return int(bufs.ctrl.detach().cpu().numpy().view("uint32")[CTRL_SYNC_TIMEOUTS_U32])
 
 
 # ---------------------------------------------------------------------------

@@ -1370,6 +1370,7 @@ struct FbArgs {
   uint32_t* gen;        // grid-barrier generation
   uint32_t* bar;        // grid-barrier arrival counter (two-level)
   uint32_t* exit_ctr;   // exit arrival counter (two-level)
+  GkCtrl* ctrl;         // sync_timeouts
   uint32_t* hist;       // exact-key histogram set
   uint32_t* blockcnt;
   const float* x;
@@ -1382,6 +1383,12 @@ struct FbArgs {
 // the fence, which ROCm 7.2 can drop), counts in; the last arrival bumps the
 // generation, the others poll it relaxed; then ONE agent acquire + wait and a
 // barrier before any load of another block's bytes.
+// an expired bounded spin: counted (sticky) in the control block, so a grid
+// that was not co-resident shows up instead of passing silently
+__device__ __forceinline__ void sync_timeout(const FbArgs& f) {
+  __hip_atomic_fetch_add(&f.ctrl->sync_timeouts, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ void grid_sync(const FbArgs& f) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1395,6 +1402,7 @@ __device__ __forceinline__ void grid_sync(const FbArgs& f) {
     } else {
       uint32_t spins = 0;
       while (ld_dev(f.gen) == g0 && ++spins < (1u << 24)) __builtin_amdgcn_s_sleep(2);
+      if (spins >= (1u << 24)) sync_timeout(f);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1426,6 +1434,7 @@ __global__ __launch_bounds__(kBlock) void decide_fb_kernel(DecArgs da, FbArgs f)
       if (threadIdx.x == 0) {
         uint32_t v, spins = 0;
         while ((v = ld_dev(f.flag)) == 0u && ++spins < (1u << 24)) __builtin_amdgcn_s_sleep(2);
+        if (v == 0u) sync_timeout(f);
         s_fb = v == 0u ? 0u : v - 1u;
       }
       __syncthreads();
@@ -1689,7 +1698,7 @@ bool launch_decide_fb(const CompressArgs& a, const Ws& w, bool vec, int G, int64
   f.gen = f.flag + 64;
   f.bar = w.sync + 4 * kSyncWords;
   f.exit_ctr = w.sync + 5 * kSyncWords;
-  f.hist = w.hist; f.blockcnt = w.blockcnt; f.x = a.r; f.n = a.n; f.kfb = kfb; f.chunk_tiles = chunk_tiles; f.G = G;
+  f.ctrl = ctrl; f.hist = w.hist; f.blockcnt = w.blockcnt; f.x = a.r; f.n = a.n; f.kfb = kfb; f.chunk_tiles = chunk_tiles; f.G = G;
   if (decided) {
     if (vec) hipLaunchKernelGGL((decide_fb_kernel<true, true>), dim3(Gf), dim3(kBlock), 0, s, da, f);
     else hipLaunchKernelGGL((decide_fb_kernel<false, true>), dim3(Gf), dim3(kBlock), 0, s, da, f);

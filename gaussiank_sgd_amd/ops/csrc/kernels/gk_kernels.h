@@ -65,12 +65,17 @@ struct GkCtrl {
   double cal_step;      // log spacing of the ladder
   int64_t cal_k;        // k the state was calibrated for (re-initialised when k changes)
   int32_t fallback;     // this call fell back to the exact radix key (1: top-k, 2: top-k_cap)
-  int32_t pad1;
+  // sticky count of bounded spins that expired in decide_fb_kernel (a grid
+  // that was not co-resident: that call's selection is not trustworthy);
+  // never reset by the kernels, read by ops.ctrl_fields / bench.py
+  uint32_t sync_timeouts;
   // entries above the reference rule's threshold when that exceeded k_cap and
   // the selection moved to a tighter candidate / the exact key (header word
   // `total`); -1 when the reference choice fitted
   int64_t ref_total;
 };
+
+static_assert(offsetof(GkCtrl, sync_timeouts) == 364, "ops/__init__.py CTRL_SYNC_TIMEOUTS_U32 = 364 / 4");
 
 struct Chunk;
 

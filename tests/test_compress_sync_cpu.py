@@ -38,3 +38,17 @@ def test_exactly_the_last_arrival_is_last(G):
         lasts = [i for i, b in enumerate(order) if arrive(counters, G, b)]
         assert lasts == [G - 1], (G, rep, lasts)
         assert counters["top"] == 0 and not any(counters["sub"])
+
+
+def test_ctrl_sync_timeouts_offset_matches_header():
+    """ops.CTRL_SYNC_TIMEOUTS_U32 is the word the kernels count expired
+    bounded spins into (GkCtrl::sync_timeouts, static_assert in gk_kernels.h);
+    a fresh control block reports none."""
+    import os
+    import re
+    from gaussiank_sgd_amd import ops
+    hdr = os.path.join(os.path.dirname(ops.__file__), "csrc", "kernels", "gk_kernels.h")
+    m = re.search(r"offsetof\(GkCtrl, sync_timeouts\) == (\d+)", open(hdr).read())
+    assert m and int(m.group(1)) == ops.CTRL_SYNC_TIMEOUTS_U32 * 4
+    b = ops.CompressBuffers(8, "cpu")
+    assert ops.sync_timeouts(b) == 0 and ops.ctrl_fields(b)["sync_timeouts"] == 0

@@ -688,3 +688,4 @@ def test_fused_fallback_fires_under_load(cuda, fused, handoff, monkeypatch):
         assert int(recg[2]) == ops.OVERFLOW_EXACT, (it, recg[:4].tolist())
         assert torch.equal(recg, cb.record), it
         assert torch.equal(rg.cpu(), rc), it
+        assert ops.sync_timeouts(gb) == 0, it   # every grid barrier / flag poll completed
