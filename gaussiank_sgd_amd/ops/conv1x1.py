@@ -680,7 +680,7 @@ class _FastConvFn(torch.autograd.Function):
         direct = sink is not None and getattr(sink, "grad_view", None) is not None and \
             sink.grad_view.is_contiguous(memory_format=_CL)
         wgrad_done = False
-        if direct and lz is None and streams.enabled(x.device, x.shape[0]) and \
+        if direct and lz is None and streams.enabled(x.device) and \
                 _choices.get(_wgrad_key(x, w, s), ("",))[0] in ("hip", "w3"):
             sink.check()
             side = streams.fork(x.device)

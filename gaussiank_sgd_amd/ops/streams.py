@@ -21,9 +21,8 @@ Contract (ops/conv1x1.py, parallel/distributed_optimizer.py):
   stream -- consumers that read gradients mid-backward (a bucket launch on the
   communication stream) call it first.
 
-``GKSGD_WGRAD_STREAM``: ``0`` (default) never forks, ``auto`` forks only for
-small per-GPU batches (N <= 64, e.g. the reference's bs32), ``1`` always;
-never during HIP-graph capture.  Measured on MI355X, fp32 ResNet-50 bs512
+``GKSGD_WGRAD_STREAM``: ``0`` (default) never forks, ``1`` always; never
+during HIP-graph capture.  Measured on MI355X, fp32 ResNet-50 bs512
 (bench/stream_probe.py): 146.0 ms/step inline vs 147.8 ms with the side
 stream, and 2x the reserved memory; bf16 41.0 vs 41.8 ms.  Most likely cause
 (not traced): the persistent GEMM grids keep the CUs' register files and LDS
@@ -31,7 +30,10 @@ occupied, so a BN pass issued on the other stream finds few free wave slots
 until the GEMM drains and little actually runs concurrently.  At bs32 the
 grids are small and the fork usually pays (13.38 -> 13.21 ms/step, r4c6;
 12.85 vs 13.15 / 13.06 off in an interleaved A/B, r4c34) but one of the two
-``auto`` runs of that A/B took 17.1 ms/step, so it stays opt-in.  Inside a captured HIP graph
+forked runs of that A/B took 17.1 ms/step -- not root-caused, so the small-batch
+``auto`` mode of round 4 was removed (round 5) and the fork is opt-in only.
+The reference batch now replays as one HIP graph on one GPU anyway
+(bench.py ``--ref-graph``), where the fork does not apply (below).  Inside a captured HIP graph
 (``GKSGD_WGRAD_STREAM_GRAPH=1`` lifts the capture exclusion) the forked
 grad-weights become parallel graph branches and the bs32 step DOUBLES: 23.2 /
 23.8 ms against 12.59 / 12.59 inline, interleaved A/B/A/B (r5c8) -- the graph
@@ -52,20 +54,13 @@ _pending: Dict[int, bool] = {}
 _callback_queued: Dict[int, bool] = {}
 
 
-AUTO_MAX_BATCH = 64
-
-
-def enabled(device: torch.device, batch: Optional[int] = None) -> bool:
-    """Fork this convolution's grad-weight?  ``batch``: its per-GPU batch
-    (``auto`` mode forks only at batch <= AUTO_MAX_BATCH)."""
+def enabled(device: torch.device) -> bool:
+    """Fork this convolution's grad-weight onto the side stream?"""
     if device.type != "cuda":
         return False
     if torch.cuda.is_current_stream_capturing() and os.environ.get("GKSGD_WGRAD_STREAM_GRAPH", "0") != "1":
         return False
-    mode = os.environ.get("GKSGD_WGRAD_STREAM", "0")
-    if mode == "auto":
-        return batch is not None and batch <= AUTO_MAX_BATCH
-    return mode != "0"
+    return os.environ.get("GKSGD_WGRAD_STREAM", "0") == "1"
 
 
 def _index(device) -> int:

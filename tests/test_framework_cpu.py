@@ -402,21 +402,22 @@ def test_winograd_split_candidates_small_grids_only():
 
 def test_wgrad_side_stream_policy(monkeypatch):
     """ops/streams.py: the grad-weight side stream is off by default, forked
-    only for small per-GPU batches with GKSGD_WGRAD_STREAM=auto, always with 1,
-    and never while a HIP graph is being captured."""
+    with GKSGD_WGRAD_STREAM=1 only (any other value, including round 4's
+    removed "auto", is off), never for a CPU tensor and never while a HIP
+    graph is being captured."""
     import torch
     from gaussiank_sgd_amd.ops import streams
     dev = torch.device("cuda")
     monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: False)
     monkeypatch.delenv("GKSGD_WGRAD_STREAM", raising=False)
-    assert not streams.enabled(dev, 32) and not streams.enabled(dev, 512)
+    assert not streams.enabled(dev)
     monkeypatch.setenv("GKSGD_WGRAD_STREAM", "auto")
-    assert streams.enabled(dev, 32) and not streams.enabled(dev, 512) and not streams.enabled(dev)
+    assert not streams.enabled(dev)
     monkeypatch.setenv("GKSGD_WGRAD_STREAM", "1")
-    assert streams.enabled(dev, 512) and streams.enabled(dev)
+    assert streams.enabled(dev)
+    assert not streams.enabled(torch.device("cpu"))
     monkeypatch.setenv("GKSGD_WGRAD_STREAM", "0")
-    assert not streams.enabled(dev, 32)
-    monkeypatch.setenv("GKSGD_WGRAD_STREAM", "auto")
-    assert not streams.enabled(torch.device("cpu"), 32)
+    assert not streams.enabled(dev)
+    monkeypatch.setenv("GKSGD_WGRAD_STREAM", "1")
     monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: True)
-    assert not streams.enabled(dev, 32)
+    assert not streams.enabled(dev)
