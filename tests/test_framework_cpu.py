@@ -421,3 +421,20 @@ def test_wgrad_side_stream_policy(monkeypatch):
     monkeypatch.setenv("GKSGD_WGRAD_STREAM", "1")
     monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: True)
     assert not streams.enabled(dev)
+
+
+def test_cal_accuracy_top1_argmax_matches_topk():
+    """DLTrainer.cal_accuracy: the k = 1 argmax path scores exactly what the
+    sorted top-k path scores (untied logits), alone and beside a top-5."""
+    import torch
+    from gaussiank_sgd_amd.train.trainer import DLTrainer
+    g = torch.Generator().manual_seed(3)
+    out = torch.randn(257, 1000, generator=g)
+    tgt = torch.randint(0, 1000, (257,), generator=g)
+    tgt[:40] = out[:40].argmax(1)            # some hits
+    _, p = out.topk(5, 1, True, True)
+    ref1 = float(p[:, :1].eq(tgt.view(-1, 1)).sum()) * 100.0 / 257
+    ref5 = float(p.eq(tgt.view(-1, 1)).sum()) * 100.0 / 257
+    a1, = DLTrainer.cal_accuracy(None, out, tgt, topk=(1,))
+    b1, b5 = DLTrainer.cal_accuracy(None, out, tgt, topk=(1, 5))
+    assert abs(float(a1) - ref1) < 1e-4 and abs(float(b1) - ref1) < 1e-4 and abs(float(b5) - ref5) < 1e-4
