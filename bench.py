@@ -404,9 +404,14 @@ def _phase_deadline(name: str, out: dict, rank: int):
     line.  Every rank arms its own timer, so every rank exits."""
     import threading
     s = float(os.environ.get("GKSGD_BENCH_PHASE_TIMEOUT_S", "240"))
+    if os.environ.get("GKSGD_GEMM_RETUNE"):
+        s *= 4      # a first-time GEMM autotune is slow but healthy
 
     def fire():
         out[name + "_error"] = "timeout: phase not finished after %.0f s on rank %d" % (s, rank)
+        # machine-readable: the line is cut short (the process still exits 0 so
+        # the headline, measured and complete, is not discarded with the phase)
+        out["bench_incomplete"] = True
         print("bench.py: phase %s timed out after %.0f s; exiting" % (name, s), file=sys.stderr, flush=True)
         if rank == 0:
             try:

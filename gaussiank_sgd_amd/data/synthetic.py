@@ -46,7 +46,8 @@ DATASETS = {
 class SyntheticData:
     def __init__(self, dataset: str, batch_size: int, device="cpu", seed: int = 0, pool: int = 4,
                  learnable: bool = False, seq_len: Optional[int] = None, channels_last: bool = False,
-                 dtype: torch.dtype = torch.float32, vocab_size: Optional[int] = None):
+                 dtype: torch.dtype = torch.float32, vocab_size: Optional[int] = None,
+                 train_samples: Optional[int] = None):
         if dataset not in DATASETS:
             raise ValueError("Unsupport dataset: %s" % dataset)
         self.spec = DATASETS[dataset]
@@ -55,6 +56,8 @@ class SyntheticData:
         self.learnable = learnable
         self.seq_len = seq_len or (self.spec.shape[0] if self.spec.kind != "image" else None)
         self.vocab = vocab_size or self.spec.num_classes
+        # epoch length override (short synthetic epochs: resume / schedule tests)
+        self.train_samples = train_samples
         g = torch.Generator(device="cpu")
         g.manual_seed(1234 + seed)
         self._batches = []
@@ -120,7 +123,14 @@ class SyntheticData:
     def get_batch(self):
         return next(self)
 
+    def seek(self, position: int) -> None:
+        """Continue from batch ``position`` (a resumed run reads the batch the
+        uninterrupted run would have read at that iteration)."""
+        self._i = int(position)
+
     def num_samples(self) -> int:
+        if self.train_samples is not None:
+            return int(self.train_samples)
         if self.spec.kind == "tokens":
             return self.spec.train_samples // self.seq_len
         return self.spec.train_samples

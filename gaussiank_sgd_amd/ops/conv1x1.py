@@ -92,7 +92,9 @@ _NT_CFGS_X6 = [c + X6 for c in (1, 2, 3, 4, 5, 6, 7, 12, 13, 101, 102, 103, 104,
 # Digit 300000: the same kernels with B split into bf16 planes once per call by the binding
 # (split3_rows), no B split in the kernel: within +-3% of 200000, up to 8% faster on a few shapes (r5c33)
 _NT_CFGS_X62 = [2 * X6 + t for t in range(1, 8)] + [3 * X6 + t for t in range(1, 8)]
-_F32MM = os.environ.get("GKSGD_F32_MATMUL", "native")
+# default bf16x6: the library, the trainers (dist_trainer --f32-matmul) and
+# bench.py all run the same fp32 GEMM family unless told otherwise
+_F32MM = os.environ.get("GKSGD_F32_MATMUL", "bf16x6")
 
 
 def set_f32_matmul(mode: str) -> str:

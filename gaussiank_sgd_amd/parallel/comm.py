@@ -22,7 +22,7 @@ import datetime
 import os
 import threading
 import time
-from typing import Any, Callable, Dict, List, Optional
+from typing import Any, Callable, Dict, List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -437,6 +437,40 @@ def _all_ok(ok: bool) -> bool:
     t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MIN)
     return int(t.item()) == 1
+
+
+def agree_ints(vals: List[int]) -> Tuple[bool, List[int], List[int]]:
+    """Do all ranks hold the same integer vector?  Returns ``(all equal, mins,
+    maxs)`` -- the per-entry minimum and maximum over the ranks -- identically
+    on every rank.  Two small all-reduces (MIN of ``[x, -x]`` gives both
+    extremes at once): the vector LENGTH first, so ranks holding vectors of
+    different lengths agree on "unequal" without ever entering a collective
+    of mismatched size; then the entries."""
+    v = [int(x) for x in vals]
+    if _loopback() is not None:
+        parts = _lb_exchange(list(v))
+        if len({len(p) for p in parts}) != 1:
+            return False, [], []
+        mins = [min(col) for col in zip(*parts)]
+        maxs = [max(col) for col in zip(*parts)]
+        return mins == maxs, mins, maxs
+    if not _distributed():
+        return True, v, v
+    dev = torch.device("cuda", torch.cuda.current_device()) if backend() == "nccl" else torch.device("cpu")
+
+    def minmax(x: List[int]) -> Tuple[List[int], List[int]]:
+        t = torch.tensor(x + [-y for y in x], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        h = t.cpu().tolist()
+        return h[:len(x)], [-y for y in h[len(x):]]
+
+    lmin, lmax = minmax([len(v)])
+    if lmin != lmax:
+        return False, [], []
+    if not v:
+        return True, [], []
+    mins, maxs = minmax(v)
+    return mins == maxs, mins, maxs
 
 
 def _wait_event(ev, timeout_s: float, what: str) -> None:

@@ -161,6 +161,17 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         self._pending_apply = False
         self._base_cls = opts.get("base_cls", None)
         self._state_dirty = False
+        # cross-rank agreement on every bucket's record size and density before
+        # the first exchange, and again after every event that can change them
+        # (epoch boundary of the density schedule, a resume): a mismatch raises
+        # on every rank instead of pairing records of different sizes inside
+        # one all-gather (an RCCL hang, or garbage) -- GKSGD_PLAN_CHECK=0 skips
+        self._plan_check = _env_flag("GKSGD_PLAN_CHECK", True)
+        self._plan_check_due = True
+        # GKSGD_CHECK_ORDER=1: also agree on (bucket index, record words) before
+        # EVERY exchange (one blocking collective per exchange: a debug mode)
+        self._check_order = _env_flag("GKSGD_CHECK_ORDER", False)
+        self._next_launch = 0     # buckets launch strictly in index order
 
         named_parameters = list(named_parameters) if named_parameters is not None else []
         if any(not isinstance(p, tuple) for p in named_parameters):
@@ -323,8 +334,25 @@ class _DistributedOptimizer(torch.optim.Optimizer):
             b = self._arena.buckets[bi]
             b.ready += 1
             if b.ready == len(b.params) and not b.launched and self._overlap:
-                self._launch_bucket(b)
+                self._launch_in_order()
         return hook
+
+    def _launch_in_order(self):
+        """Launch every complete bucket from the next one due, strictly in
+        bucket-index order: a bucket whose gradients complete early waits for
+        its predecessors and is launched by the launch of the last of them.
+        The collective sequence is then the bucket sequence on every rank,
+        whatever order autograd runs the hooks in (Horovod gets the same
+        guarantee by negotiating tensor names through its coordinator; the
+        reference relies on it, distributed_optimizer.py:426-427,461-463)."""
+        bs = self._arena.buckets
+        while self._next_launch < len(bs):
+            b = bs[self._next_launch]
+            if not b.launched:
+                if b.ready != len(b.params):
+                    return
+                self._launch_bucket(b)
+            self._next_launch += 1
 
     # ------------------------------------------------------------------
     # bf16 shadow weights (parallel/shadow.py)
@@ -368,8 +396,10 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         # the epoch's counts are those of the density in force during it (logged
         # before the schedule moves on)
         self._drain_selected()
+        self.check_compress_sync()
         density = self.get_current_density()
         self.train_epoch += 1
+        self._plan_check_due = True
         counts = self._selected_num_gradients
         if rank() == 0:
             sz = int(np.sum(self._sizes))
@@ -384,6 +414,33 @@ class _DistributedOptimizer(torch.optim.Optimizer):
                 logger.info("Effective compression ratio: %.1fx", self.wire_compression_ratio(density))
         self._selected_num_gradients = []
         self._epoch_sel = []
+
+    def check_compress_sync(self) -> int:
+        """New expired bounded spins of the fused decide / fallback grid
+        (compress.hip decide_fb_kernel: a grid that was not co-resident) since
+        the last check; one small D2H per compressed bucket.  A bucket that
+        had one gets its workspace back to the at-rest state (every arrival
+        counter and flag zero -- a timed-out block may have left a grid barrier
+        half counted) and compresses with in-grid hand-offs from then on, which
+        do not use that grid.  Called at every epoch boundary."""
+        if not (self._is_cuda and self._fused_sparse):
+            return 0
+        new = 0
+        for b in self._arena.buckets:
+            bufs = getattr(b, "bufs", None)
+            if bufs is None or getattr(bufs, "ctrl", None) is None:
+                continue
+            n = ops.sync_timeouts(bufs)
+            seen = b.extra.get("sync_seen", 0)
+            if n > seen:
+                new += n - seen
+                b.extra["sync_seen"] = n
+                torch.cuda.synchronize(self._device)
+                bufs.ws.zero_()
+                b.extra["handoff"] = 1
+                logger.warning("bucket %d: %d expired grid-barrier spins in the fused compression decide; "
+                               "workspace reset, in-grid hand-offs from now on", b.index, n - seen)
+        return new
 
     def _drain_selected(self) -> List[tuple]:
         """(sent, total) per bucket-step logged since the last drain (one D2H
@@ -467,7 +524,54 @@ class _DistributedOptimizer(torch.optim.Optimizer):
     # ------------------------------------------------------------------
     # per-bucket pipeline
     # ------------------------------------------------------------------
+    def _plan_signature(self) -> List[int]:
+        """What every rank must agree on before exchanging: the world, the
+        compressor, and per bucket its element count, density (parts per
+        billion) and the int32 words of the record (or dense payload) it puts
+        into the collective."""
+        comp = self._compression
+        sig = [self._world, len(self._arena.buckets), int(getattr(comp, "mode", -1) or 0)]
+        for b in self._arena.buckets:
+            d = self.get_current_density(b.name)
+            sig += [b.numel, int(round(d * 1e9)), self._exchange_words(b, d)]
+        return sig
+
+    def _exchange_words(self, b, density: float) -> int:
+        comp = self._compression
+        if self._fused_sparse and self._sparse and density < 1:
+            k = comp.k_of(b.numel, density)
+            return ops.REC_HDR + 2 * min(comp.k_cap_for(k, b.numel), b.bufs.k_cap)
+        if getattr(comp, "name", None) == "bucket":
+            return 2
+        return b.numel
+
+    def _ensure_plan_agreed(self):
+        if not (self._plan_check_due and self._plan_check and self._world > 1):
+            return
+        if self._is_cuda and torch.cuda.is_current_stream_capturing():
+            return      # a captured step replays what the eager warm-up agreed on
+        self._plan_check_due = False
+        ok, mins, maxs = comm.agree_ints(self._plan_signature())
+        if not ok:
+            sig = self._plan_signature()
+            raise RuntimeError(
+                "DistributedOptimizer: the ranks disagree on the exchange plan (rank %d: epoch %d, iter %d, "
+                "signature %s; min over ranks %s, max %s). Every rank must run the same model, bucket plan and "
+                "density schedule position (after a resume: the same train_epoch); refusing to enter the "
+                "collective." % (self._rank, self.train_epoch, self.train_iter, sig, mins, maxs))
+
+    def _check_exchange_order(self, pairs):
+        """GKSGD_CHECK_ORDER=1: agree on the (bucket index, payload words) of
+        this exchange on every rank before entering it."""
+        sig = [x for p in pairs for x in p]
+        ok, mins, maxs = comm.agree_ints(sig)
+        if not ok:
+            raise RuntimeError("DistributedOptimizer: exchange order mismatch at iter %d on rank %d: this rank "
+                               "exchanges (bucket, words) %s; min over ranks %s, max %s" % (
+                                   self.train_iter, self._rank, sig, mins, maxs))
+
     def _launch_bucket(self, b):
+        self._ensure_plan_agreed()
         b.launched = True
         # a bucket compressed while the backward still runs (another bucket is
         # not launched yet) hands its single-workgroup steps over inside the
@@ -559,7 +663,7 @@ class _DistributedOptimizer(torch.optim.Optimizer):
             ops.compress_(g, r, b.bufs, comp.mode, ec=comp.ec, zero_g=True, loops=comp.loops,
                           z=comp.z_for(density), k=k, k_cap=k_cap, seed=seed, sample_p=getattr(comp, "sample_p", 0.01),
                           n_stats=b.numel, valid=b.extra.get("valid"), mc=mc, seed_dev=seed_dev,
-                          handoff=_OVERLAP_HANDOFF if b.extra.get("overlapped") else -1)
+                          handoff=_OVERLAP_HANDOFF if b.extra.get("overlapped") else b.extra.get("handoff", -1))
         rec_words = ops.REC_HDR + 2 * k_cap
         return b.bufs.record[:rec_words], k_cap
 
@@ -568,6 +672,8 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         if self._world <= 1:
             return list(recs)
         outs = [b.gathered[: self._world * (ops.REC_HDR + 2 * kc)] for b, kc in zip(bs, k_caps)]
+        if self._check_order:
+            self._check_exchange_order([(b.index, ops.REC_HDR + 2 * kc) for b, kc in zip(bs, k_caps)])
         with trace.range("gk/allgather/%s" % ",".join("b%d" % b.index for b in bs)):
             if len(bs) == 1:
                 self._exchanger.allgather_(outs[0], recs[0])
@@ -598,6 +704,7 @@ class _DistributedOptimizer(torch.optim.Optimizer):
         """Several due buckets at once (synchronize() without overlap): compress
         each, ONE grouped all-gather of all records, then finish each -- one
         collective launch instead of len(bs)."""
+        self._ensure_plan_agreed()
         for b in bs:
             b.launched = True
             b.extra["overlapped"] = False
@@ -662,12 +769,12 @@ class _DistributedOptimizer(torch.optim.Optimizer):
             mask, means, ws = b.extra["mask"], b.extra["means"], b.extra["ws"]
             ops.sign_bucket_compress_(g, mask, means, ws)
             t1 = self._timer()
-            self._allreduce_avg(means)
+            self._allreduce_avg(means, b)
             t2 = self._timer()
             ops.sign_bucket_decompress_(g, mask, means)
         else:
             t1 = self._timer()
-            self._allreduce_avg(g)
+            self._allreduce_avg(g, b)
             t2 = self._timer()
         t3 = self._timer()
         if self._norm_clip is not None:
@@ -677,9 +784,11 @@ class _DistributedOptimizer(torch.optim.Optimizer):
             self._pending_timers = getattr(self, "_pending_timers", [])
             self._pending_timers.append((b.name, t0, t1, t2, t3))
 
-    def _allreduce_avg(self, t):
+    def _allreduce_avg(self, t, b=None):
         if self._world <= 1:
             return
+        if self._check_order and b is not None:
+            self._check_exchange_order([(b.index, t.numel())])
         self._exchanger.allreduce_(t, average=True)
 
     def _log_selected(self, hdr: torch.Tensor):
@@ -765,6 +874,7 @@ class _DistributedOptimizer(torch.optim.Optimizer):
                 b.ready = 0
                 b.launched = False
                 b.extra["overlapped"] = False
+            self._next_launch = 0
             if any_ready:
                 self.train_iter += 1
             self._flush_dumps()
@@ -1026,6 +1136,7 @@ class _DistributedOptimizer(torch.optim.Optimizer):
     def load_compression_state(self, st: dict) -> None:
         self.train_epoch = int(st.get("train_epoch", self.train_epoch))
         self.train_iter = int(st.get("train_iter", self.train_iter))
+        self._plan_check_due = True
         for key, arena_t in (("residuals", self._arena.residuals),
                              ("velocity", getattr(self._arena, "velocity", None))):
             res = st.get(key)
@@ -1042,6 +1153,54 @@ class _DistributedOptimizer(torch.optim.Optimizer):
                         n = self._named_parameters[k].numel()
                         dst[o:o + n].copy_(flat[pos:pos + n])
                         pos += n
+
+    def broadcast_state(self, root_rank: int = 0) -> None:
+        """Make the REPLICATED optimizer state identical on every rank after a
+        resume: the density-schedule / iteration position (``train_epoch``,
+        ``train_iter``) and the global momentum (or LARS acceleration) buffers
+        are taken from ``root_rank``.  Per-rank state -- error-feedback
+        residuals and DGC local velocities -- is NOT touched: every rank loads
+        its own (``load_compression_state``).
+
+        The reference restores only rank 0's weights and epoch / iteration
+        (dist_trainer.py:26-33,57; dl_trainer.py:285-290), so its resume is
+        lossy but consistent; restoring momentum on rank 0 alone would make the
+        replicas diverge, and a density epoch that differs between ranks gives
+        records of different sizes inside one all-gather."""
+        dev = self._device
+        pos = torch.tensor([self.train_epoch, self.train_iter], dtype=torch.int64,
+                           device=dev if comm.backend() == "nccl" else "cpu")
+        pos = broadcast(pos, root_rank)
+        self.train_epoch, self.train_iter = int(pos[0]), int(pos[1])
+        self._plan_check_due = True
+        if self._world <= 1 and comm.backend() != "loopback":
+            return
+        kind = self._fused_kind
+        if kind is None:
+            broadcast_optimizer_state(self, root_rank)
+            return
+        key = "momentum_buffer" if kind == "sgd" else "acceleration"
+        # per param group: does the root hold the buffer of every parameter?
+        have = [all(key in self.state.get(p, {}) for p in g["params"] if p in self._parameter_names)
+                and (kind != "sgd" or g["momentum"] != 0) for g in self.param_groups]
+        have = broadcast_object(have, root_rank)
+        if not any(have):
+            return
+        with torch.no_grad():
+            if self._state_dirty or self._arena.momentum is None:
+                self._adopt_state()    # root: buffers -> arena views; others: a zero arena
+            m = self._arena.momentum
+            if m is None:
+                m = self._arena.ensure_momentum(0.0 if kind == "sgd" else 1.0)
+            broadcast_(m, root_rank)   # the whole momentum arena: one collective
+            for gi, g in enumerate(self.param_groups):
+                if not have[gi]:
+                    continue
+                for p in g["params"]:
+                    if p in self._parameter_names:
+                        self.state[p][key] = self._arena.view_of(m, self._parameter_names[p])
+                self._group_first[gi] = False
+        self._state_dirty = False
 
     @property
     def arena(self) -> GradArena:

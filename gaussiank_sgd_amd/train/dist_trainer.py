@@ -30,30 +30,49 @@ from .. import settings, utils
 from ..compression import compressors
 from ..parallel import distributed_optimizer as hvd
 from ..settings import formatter, logger
-from .trainer import DLTrainer, _support_datasets, _support_dnns
+from .trainer import DLTrainer, _support_datasets, _support_dnns, rank_checkpoint_path
 
 
 def ssgd(dnn, dataset, data_dir, nworkers, lr, batch_size, nsteps_update, max_epochs, nwpernode, pretrain,
          num_steps, compressor, density, threshold, gradient_path=None, amp=None, channels_last=False,
          density_warmup=True, deterministic=False, max_iters=None, compress_single_rank=False, saved_dir=".",
          bf16_shadow=True, momentum_correction=False, k_cap_factor=None, overlap=True, dump_grad_every=None,
-         metrics_dir=None):
+         metrics_dir=None, f32_matmul=None, train_samples=None, checkpoint_every=2, save_final=False):
     rank = hvd.rank()
     device = "cpu"
     if torch.cuda.is_available():
         torch.cuda.set_device(hvd.local_rank() % torch.cuda.device_count())
         device = "cuda"
+    if f32_matmul is not None:
+        from ..ops import conv1x1
+        conv1x1.set_f32_matmul(f32_matmul)
+    # Resume: rank 0 loads the model, momentum and its own compressor state
+    # (reference dist_trainer.py:26-27 loads on rank 0 only); every other rank
+    # reads ITS OWN per-rank file for its residuals / DGC velocities -- those
+    # are per-rank state nobody else holds.  Weights, momentum and the schedule
+    # position are then broadcast from rank 0 (below).
+    own_ck = None
+    if pretrain is not None and rank != 0:
+        own = rank_checkpoint_path(pretrain, rank)
+        if own is not None and os.path.isfile(own):
+            own_ck = own
+        else:
+            logger.warning("rank %d: no per-rank checkpoint for %s: its residuals / velocities start from zero",
+                           rank, pretrain)
+    resumed = pretrain is not None
     if rank != 0:
         pretrain = None
     trainer = DLTrainer(rank, nworkers, dist=False, batch_size=batch_size, is_weak_scaling=True, ngpus=1,
                         data_dir=data_dir, dataset=dataset, dnn=dnn, lr=lr, nworkers=nworkers, prefix="allreduce",
                         pretrain=pretrain, num_steps=num_steps, device=device, amp=amp,
-                        channels_last=channels_last, seed=rank, weights_dir=os.path.join(saved_dir, "weights"))
+                        channels_last=channels_last, seed=rank, weights_dir=os.path.join(saved_dir, "weights"),
+                        train_samples=train_samples, checkpoint_every=checkpoint_every)
     init = torch.tensor([trainer.get_train_epoch(), trainer.get_train_iter()], dtype=torch.int64,
                         device=trainer.device)
     init = hvd.broadcast(init, root_rank=0)
     trainer.set_train_epoch(int(init[0]))
     trainer.set_train_iter(int(init[1]))
+    trainer.seek_data()
     is_sparse = density < 1
 
     if settings.ADAPTIVE_MERGE or settings.ADAPTIVE_SPARSE:
@@ -85,9 +104,17 @@ def ssgd(dnn, dataset, data_dir, nworkers, lr, batch_size, nsteps_update, max_ep
                                          gradient_path=gradient_path, density_warmup=density_warmup,
                                          deterministic=deterministic, compress_single_rank=compress_single_rank,
                                          momentum_correction=momentum_correction, overlap=overlap)
-    if getattr(trainer, "_pending_compression", None):
-        optimizer.load_compression_state(trainer._pending_compression)
+    comp_state = getattr(trainer, "_pending_compression", None)
+    if own_ck is not None:
+        from ..utils.checkpoint import load_checkpoint
+        comp_state = load_checkpoint(own_ck, map_location="cpu").get("compression")
+        logger.info("rank %d: per-rank compressor state from %s", rank, own_ck)
+    if comp_state:
+        optimizer.load_compression_state(comp_state)
     hvd.broadcast_parameters(trainer.net.state_dict(), root_rank=0)
+    # momentum arena and train_epoch / train_iter from rank 0: replicas step
+    # identically and agree on the density (record size) of every bucket
+    optimizer.broadcast_state(root_rank=0)
     if bf16_shadow and trainer.is_cuda:
         # bf16: weight shadows + arena gradient sinks; fp32: the kernels' weight
         # gradients straight into the arena (parallel/shadow.py)
@@ -105,11 +132,15 @@ def ssgd(dnn, dataset, data_dir, nworkers, lr, batch_size, nsteps_update, max_ep
     logger.info("max_epochs: %d", max_epochs)
     display = 40 if iters_per_epoch > 40 else max(1, iters_per_epoch - 1)
     done = 0
-    for epoch in range(max_epochs):
+    # a resumed run continues where the checkpoint stopped (max_epochs is the
+    # total); the reference re-ran max_epochs epochs from wherever it resumed
+    done_iters = trainer.get_train_iter() // max(1, nsteps_update) if resumed else 0
+    start_epoch, first_i = divmod(done_iters, iters_per_epoch)
+    for epoch in range(start_epoch, max_epochs):
         hidden = None
         if dnn == "lstm":
             hidden = trainer.net.init_hidden()
-        for i in range(iters_per_epoch):
+        for i in range(first_i if epoch == start_epoch else 0, iters_per_epoch):
             s = time.time()
             optimizer.zero_grad()
             for j in range(nsteps_update):
@@ -144,9 +175,23 @@ def ssgd(dnn, dataset, data_dir, nworkers, lr, batch_size, nsteps_update, max_ep
                 times = []
             done += 1
             if max_iters is not None and done >= max_iters:
-                optimizer.increase_one_epoch()
-                return trainer, optimizer
+                if i == iters_per_epoch - 1:
+                    optimizer.increase_one_epoch()
+                return _finish(trainer, optimizer, save_final)
         optimizer.increase_one_epoch()
+    return _finish(trainer, optimizer, save_final)
+
+
+def _finish(trainer, optimizer, save_final):
+    """End of the run: with ``save_final`` every rank writes its checkpoint
+    (weights, momentum, its residuals / velocities, schedule position) so the
+    run can be resumed with ``--pretrain <...-rank0-epoch<e>.pth>``."""
+    if save_final:
+        if trainer.is_cuda:
+            torch.cuda.synchronize()
+        fn = trainer.save_epoch_checkpoint()
+        if fn:
+            logger.info("final checkpoint: %s", fn)
     return trainer, optimizer
 
 
@@ -188,6 +233,17 @@ def build_parser():
     p.add_argument("--no-bf16-shadow", action="store_true",
                    help="with --amp bf16: keep plain autocast casts instead of the bf16 shadow weight arena")
     p.add_argument("--logdir-root", type=str, default="./logs")
+    p.add_argument("--f32-matmul", type=str, default=os.environ.get("GKSGD_F32_MATMUL", "bf16x6"),
+                   choices=["native", "bf16x6"],
+                   help="fp32 convolution / linear GEMM algorithm (default: %(default)s, the same as bench.py and "
+                        "the library): native = fp32 MFMA only; bf16x6 = the tuner may also pick the "
+                        "fp32-accurate bf16x6 product kernels (ops/conv1x1.py set_f32_matmul)")
+    p.add_argument("--train-samples", type=int, default=None,
+                   help="synthetic epoch length in samples (default: the dataset's real size)")
+    p.add_argument("--checkpoint-every", type=int, default=2,
+                   help="save a checkpoint every N trainer epochs (reference: 2)")
+    p.add_argument("--save-final", action="store_true",
+                   help="every rank saves its checkpoint at the end of the run (resume with --pretrain)")
     return p
 
 
@@ -223,7 +279,8 @@ def main(argv=None):
                 max_iters=args.max_iters, compress_single_rank=args.compress_single_rank, saved_dir=args.saved_dir,
                 bf16_shadow=not args.no_bf16_shadow, momentum_correction=args.momentum_correction,
                 k_cap_factor=args.k_cap_factor, overlap=not args.no_overlap, dump_grad_every=args.dump_grad_every,
-                metrics_dir=relative_path)
+                metrics_dir=relative_path, f32_matmul=args.f32_matmul, train_samples=args.train_samples,
+                checkpoint_every=args.checkpoint_every, save_final=args.save_final)
 
 
 if __name__ == "__main__":

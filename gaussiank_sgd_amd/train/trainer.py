@@ -88,12 +88,23 @@ def word_errors(hyp: str, ref: str) -> int:
     return prev[-1]
 
 
+def rank_checkpoint_path(path: str, rank: int) -> Optional[str]:
+    """``.../<dnn>-rank0-epoch<e>.pth`` -> the same checkpoint of ``rank``
+    (every rank saves its own residuals / velocity, save_epoch_checkpoint);
+    None when the file name carries no ``-rank<r>-`` tag."""
+    import re
+    d, base = os.path.split(path)
+    new, n = re.subn(r"-rank\d+-", "-rank%d-" % int(rank), base, count=1)
+    return os.path.join(d, new) if n else None
+
+
 class DLTrainer:
     def __init__(self, rank, size, master="gpu10", dist=True, ngpus=1, batch_size=32, is_weak_scaling=True,
                  data_dir="./data", dataset="cifar10", dnn="resnet20", lr=0.04, nworkers=1, prefix=None,
                  sparsity=0.95, pretrain=None, num_steps=35, tb_writer=None, amp_handle=None, device=None,
                  amp: Optional[str] = None, channels_last: bool = False, learnable_data: bool = False,
-                 seed: int = 0, data_pool: int = 4, weights_dir: str = "./weights", seq_len: Optional[int] = None):
+                 seed: int = 0, data_pool: int = 4, weights_dir: str = "./weights", seq_len: Optional[int] = None,
+                 train_samples: Optional[int] = None, checkpoint_every: int = 2):
         # data_dir: real datasets (data/real.py: CIFAR-10 binary, MNIST idx, PTB text, .npz / .npy
         # arrays), sharded by (rank, nworkers); absent or unrecognised -> synthetic, shape-exact
         self.size = size
@@ -106,6 +117,9 @@ class DLTrainer:
         self.writer = tb_writer
         self.amp_handle = amp_handle
         self.weights_dir = weights_dir
+        self.train_samples = train_samples
+        # save a checkpoint every N trainer epochs (reference: 2, dl_trainer.py:660)
+        self.checkpoint_every = max(1, int(checkpoint_every))
         if device is None:
             device = "cuda" if (ngpus > 0 and torch.cuda.is_available()) else "cpu"
         self.device = torch.device(device)
@@ -222,7 +236,8 @@ class DLTrainer:
         else:
             self.data = SyntheticData(ds, self.batch_size, self.device, seed=self.seed * 1000 + self.rank, pool=pool,
                                       learnable=learnable, seq_len=(self.num_steps if ds == "ptb" else seq_len),
-                                      channels_last=self.channels_last and self.is_cuda, vocab_size=vocab)
+                                      channels_last=self.channels_last and self.is_cuda, vocab_size=vocab,
+                                      train_samples=self.train_samples)
         self.trainset_len = self.data.num_samples()
         self._input_shape = (self.batch_size,) + tuple(DATASETS[ds].shape)
         self._output_shape = (self.batch_size, self.num_classes)
@@ -252,6 +267,14 @@ class DLTrainer:
 
     def set_train_iter(self, iteration):
         self.train_iter = iteration
+
+    def seek_data(self, position: Optional[int] = None) -> None:
+        """Point the (synthetic) batch stream at iteration ``position``
+        (default: ``train_iter``) so a resumed run reads the batches the
+        uninterrupted one would have; real loaders restart their epoch."""
+        fn = getattr(self.data, "seek", None)
+        if fn is not None:
+            fn(self.train_iter if position is None else position)
 
     def get_num_of_training_samples(self):
         return self.trainset_len
@@ -346,7 +369,7 @@ class DLTrainer:
         if self.rank == 0:
             self.test(self.train_epoch)
         self.epochs_info.append(avg_loss)
-        if self.train_iter > 0 and self.train_epoch % 2 == 0:
+        if self.train_iter > 0 and self.train_epoch % self.checkpoint_every == 0:
             self.save_epoch_checkpoint()
 
     def _read_epoch_loss(self) -> float:
@@ -534,3 +557,9 @@ class DLTrainer:
     def finish(self):
         if self.writer is not None:
             self.writer.close()
+
+
+if __name__ == "__main__":
+    # the reference's single-GPU entry is `python dl_trainer.py ...` (dl_trainer.py:907-927)
+    from gaussiank_sgd_amd.train.single import main
+    main()

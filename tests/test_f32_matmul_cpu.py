@@ -147,3 +147,26 @@ def test_xcd_block_order_3d_is_a_bijection(g):
     out = {_xcd_remap3(x, y, z, gx, gy, gz) for z in range(gz) for y in range(gy) for x in range(gx)}
     assert len(out) == gx * gy * gz
     assert all(0 <= a < gx and 0 <= b < gy and 0 <= c < gz for a, b, c in out)
+
+
+def test_library_trainer_and_bench_share_one_default(monkeypatch):
+    """The fp32 GEMM family a user trains with is the one bench.py times:
+    library default, ``dist_trainer --f32-matmul`` default and bench.py agree."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k != "GKSGD_F32_MATMUL"}
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env["PYTHONPATH"] = root
+    lib = subprocess.run([sys.executable, "-c", "from gaussiank_sgd_amd.ops import conv1x1; print(conv1x1.f32_matmul())"],
+                         capture_output=True, text=True, env=env, timeout=300)
+    assert lib.returncode == 0, lib.stderr[-1500:]
+    assert lib.stdout.strip() == "bf16x6"
+    monkeypatch.delenv("GKSGD_F32_MATMUL", raising=False)
+    from gaussiank_sgd_amd.train.dist_trainer import build_parser
+    assert build_parser().parse_args([]).f32_matmul == "bf16x6"
+    helptext = build_parser().format_help()
+    assert "--f32-matmul" in helptext and "default: bf16x6" in helptext
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    import importlib
+    import bench
+    importlib.reload(bench)
+    assert bench.parse().f32_matmul == build_parser().parse_args([]).f32_matmul
