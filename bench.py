@@ -35,6 +35,14 @@ at the reference's own per-worker batch (``REF_BATCH``: ResNet-50 32,
 larger share of the step: ``ref_bs32_value`` / ``ref_bs32_dense_value`` /
 ``ref_bs32_speedup_vs_dense``.
 
+After those, the other BASELINE configs are timed in the same process at the
+headline's precision with the same compressor, density and momentum
+correction (``--model-phases``, default ``vgg16,lstm,bert``): VGG-16 CIFAR
+bs512 and the reference's bs128, the 2-layer LSTM on PTB bs128 x 35 and the
+reference's bs20, BERT-base MLM seq 512 bs32 in ~25 MB buckets -- keys
+``<model>_value`` (images/s or tokens/s), ``_ms_per_step``, ``_dtype``,
+``_selected_over_k``, ``<model>_ref_bs<B>_value``.
+
 Fail-soft: only the headline phase is fatal.  Every secondary phase (fabric
 probe, dense comparator, reference-batch phases, bf16) runs under
 ``optional_phase``: an exception is recorded as ``<phase>_error`` in the one
@@ -146,6 +154,14 @@ def parse():
                     help="disable bf16 shadow weights / direct arena gradients (plain autocast)")
     ap.add_argument("--graph", action="store_true",
                     help="capture the whole training step in a HIP graph and replay it (train/graph.py)")
+    ap.add_argument("--k-cap-factor", type=float, default=None,
+                    help="record capacity k_cap = factor * k of the sparse compressor (default: the compressor's, "
+                         "Gaussian-k 4/3); 1.0 sends at most k entries (what the reference's 500x assumes), the "
+                         "overflow staying in the residual")
+    ap.add_argument("--model-phases", default="vgg16,lstm,bert",
+                    help="comma list of further BASELINE models timed after the headline in the same process "
+                         "(same precision / compressor / density); 'none' skips them")
+    ap.add_argument("--model-steps", type=int, default=10, help="timed steps of each further model phase")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -211,26 +227,30 @@ class Phase:
     here (trainer, optimizer, step closure / GraphedStep with its graph pool)
     so the next phase is timed without the previous one's memory resident."""
 
-    def __init__(self, trainer, opt, comp_name: str, is_sparse: bool, batch: int):
+    def __init__(self, trainer, opt, comp_name: str, is_sparse: bool, batch: int, model: str):
         self.trainer, self.opt, self.comp_name, self.is_sparse, self.batch = trainer, opt, comp_name, is_sparse, batch
+        self.model = model
         self.step = None
 
 
-def build(args, amp: str, dense: bool, threshold: int, P: int, rank: int, batch: int) -> Phase:
-    """Trainer + DistributedOptimizer of one timed phase.  amp: "fp32" / "bf16"."""
+def build(args, amp: str, dense: bool, threshold: int, P: int, rank: int, batch: int,
+          model: Optional[str] = None) -> Phase:
+    """Trainer + DistributedOptimizer of one timed phase.  amp: "fp32" / "bf16";
+    model: a MODELS key (default: --model)."""
     from gaussiank_sgd_amd.compression import compressors
     from gaussiank_sgd_amd.parallel import comm
     from gaussiank_sgd_amd.parallel.distributed_optimizer import DistributedOptimizer
     from gaussiank_sgd_amd.train import DLTrainer
 
-    dataset, _, _, _, _ = MODELS[args.model]
-    trainer = DLTrainer(rank, P, dnn=args.model, dataset=dataset, batch_size=batch,
+    model = model or args.model
+    dataset, _, _, _, _ = MODELS[model]
+    trainer = DLTrainer(rank, P, dnn=model, dataset=dataset, batch_size=batch,
                         lr=0.1, nworkers=P, device="cuda", amp="bf16" if amp == "bf16" else None,
                         channels_last=not args.no_channels_last, seed=0)
     comp_name = "none" if dense else args.compressor
     is_sparse = not dense and comp_name not in ("none", "bucket")
     seq_names = layer_times = None
-    if args.planner != "threshold" and not dense:
+    if args.planner != "threshold" and not dense and model == args.model:
         # reference dist_trainer.py:38-47: layer-wise backward profile, shared from rank 0
         from gaussiank_sgd_amd.utils.profiler import benchmark
         seq_names, layer_times, _ = benchmark(trainer, warmup=3, iterations=10)
@@ -239,7 +259,8 @@ def build(args, amp: str, dense: bool, threshold: int, P: int, rank: int, batch:
                                compression=compressors[comp_name], is_sparse=is_sparse, density=args.density,
                                threshold=threshold, compress_single_rank=True, density_warmup=False,
                                native_rccl=not args.no_native_rccl, seq_layernames=seq_names,
-                               layerwise_times=layer_times, planner=args.planner if not dense else "threshold",
+                               layerwise_times=layer_times,
+                               planner=args.planner if not dense and model == args.model else "threshold",
                                planner_world=args.plan_world,
                                momentum_correction=is_sparse and not args.no_momentum_correction)
     comm.broadcast_parameters(trainer.net.state_dict(), root_rank=0)
@@ -251,7 +272,7 @@ def build(args, amp: str, dense: bool, threshold: int, P: int, rank: int, batch:
             install_direct_grads(trainer.net, opt)
     trainer.update_optimizer(opt)
     trainer.display = 10 ** 9  # no host-syncing log lines inside the timed loop
-    return Phase(trainer, opt, comp_name, is_sparse, batch)
+    return Phase(trainer, opt, comp_name, is_sparse, batch, model)
 
 
 def run_phase(args, ph: Phase, steps: int, warmup: int, P: int, graph: Optional[bool] = None):
@@ -263,12 +284,13 @@ def run_phase(args, ph: Phase, steps: int, warmup: int, P: int, graph: Optional[
 
     trainer, opt = ph.trainer, ph.opt
     state = {"hidden": None}
-    clip = 0.25 if args.model == "lstm" else None  # reference dist_trainer.py:80-85
+    lstm = ph.model == "lstm"
+    clip = 0.25 if lstm else None  # reference dist_trainer.py:80-85
     marks = []   # (end of backward, end of update) event pairs of the timed steps
 
     def step():
         opt.zero_grad()
-        if args.model == "lstm":
+        if lstm:
             _, state["hidden"] = trainer.train(1, hidden=state["hidden"])
         else:
             trainer.train(1)
@@ -286,7 +308,7 @@ def run_phase(args, ph: Phase, steps: int, warmup: int, P: int, graph: Optional[
             marks.append((ev, e2))
 
     graph = args.graph if graph is None else graph
-    if graph and args.model == "lstm":
+    if graph and lstm:
         raise SystemExit("bench.py --graph: the LSTM carries hidden state across steps; not graph-capturable")
     run = step
     if graph:
@@ -329,6 +351,23 @@ def sync_timeouts(opt) -> int:
         if bufs is not None and getattr(bufs, "ctrl", None) is not None and bufs.ctrl.is_cuda:
             n += ops.sync_timeouts(bufs)
     return n
+
+
+def selection(ph: Phase, steps: int, density: float) -> dict:
+    """Entries sent per step over k, and the per-rank wire compression ratio,
+    of a phase's timed loop (its selected counts since the warm-up drain)."""
+    opt = ph.opt
+    if not ph.is_sparse:
+        return {}
+    from gaussiank_sgd_amd.compression import compressors
+    comp = compressors[ph.comp_name]
+    pairs = opt._collect_selected(with_totals=True)
+    k_total = sum(comp.k_of(b.numel, density) for b in opt.arena.buckets)
+    sent = sum(p[0] for p in pairs) / max(1, steps)
+    nparams = sum(b.numel for b in opt.arena.buckets)
+    wb = opt.wire_bytes_per_step(density)
+    return {"selected_over_k": round(sent / k_total, 4) if k_total else None,
+            "effective_compression_ratio": round(nparams * 4.0 / wb, 1) if wb else None}
 
 
 def phase_info(ph: Phase) -> dict:
@@ -512,6 +551,8 @@ def main() -> int:
         args.threshold = DEFAULT_THRESHOLD.get(args.model, 524288000)
     ref_bs = REF_BATCH.get(args.model) if args.ref_batch is None else args.ref_batch
     amp = "bf16" if args.amp == "bf16" else "fp32"
+    if args.k_cap_factor is not None:
+        compressors[args.compressor].kcap_factor = float(args.k_cap_factor)
     from gaussiank_sgd_amd.ops import conv1x1
     conv1x1.set_f32_matmul(args.f32_matmul)
 
@@ -576,6 +617,7 @@ def main() -> int:
             "momentum_correction": bool(opt._mc),
             "hip_graph": bool(args.graph),
             "f32_matmul": args.f32_matmul if amp == "fp32" else None,
+            "k_cap_factor": round(float(getattr(compressors[comp_name], "kcap_factor", 0.0)), 4) if is_sparse else None,
         },
         "graph_captures": getattr(ph.step, "captures", None),
         "world": P,
@@ -626,15 +668,17 @@ def main() -> int:
     release(ph)
     ph = None
 
-    def timed(holder, name, amp_, dense, threshold, batch, steps, warmup, graph=None):
-        p = build(args, amp_, dense, threshold, P, rank, batch)
+    def timed(holder, name, amp_, dense, threshold, batch, steps, warmup, graph=None, model=None):
+        p = build(args, amp_, dense, threshold, P, rank, batch, model)
         holder.append(p)
         el, exp_ = run_phase(args, p, steps, warmup, P, graph)
         info = phase_info(p)
         info["hip_graph"] = bool(args.graph if graph is None else graph)
+        tps = MODELS[p.model][3]
         info.update(ms_per_step=round(el / steps * 1e3, 3),
-                    value=round(P * batch * tok_per_sample * steps / el, 2),
+                    value=round(P * batch * tps * steps / el, 2),
                     exposed_comm_ms=round(exp_, 3) if exp_ == exp_ else None, per_gpu_batch=batch, steps=steps)
+        info.update(selection(p, steps, args.density))
         phases[name] = info
         return info
 
@@ -699,6 +743,43 @@ def main() -> int:
         alive = optional_phase(tag, out, P, ref_sparse)
         if alive:
             alive = optional_phase(tag + "_dense", out, P, ref_dense)
+
+    # ---- the other BASELINE configs (3-5) in the same process, at the same
+    # precision as the headline and the same compressor / density / momentum
+    # correction: VGG-16 CIFAR bs512 (+ the reference's bs128), 2-layer LSTM
+    # PTB bs128 x 35 (+ the reference's bs20), BERT-base MLM seq512 bs32 (14
+    # buckets of ~25 MB).  Each is fail-soft and adds <model>_value /
+    # _ms_per_step / _dtype / _unit / _selected_over_k (and _ref_bs<B>_value).
+    if alive and not args.dense and args.model_phases != "none":
+        for m in [x for x in args.model_phases.split(",") if x and x != args.model]:
+            if not alive:
+                break
+            if m not in MODELS:
+                out[m + "_error"] = "unknown model"
+                continue
+            mbatch = MODELS[m][1]
+            mthr = DEFAULT_THRESHOLD.get(m, 524288000)
+            msteps, mwarm = max(3, min(args.steps, args.model_steps)), max(2, min(args.warmup, 3))
+
+            def model_phase(holder, m=m, mbatch=mbatch, mthr=mthr, msteps=msteps, mwarm=mwarm):
+                i = timed(holder, m, amp, False, mthr, mbatch, msteps, mwarm, graph=False, model=m)
+                out[m + "_value"] = i["value"]
+                out[m + "_unit"] = MODELS[m][2]
+                out[m + "_ms_per_step"] = i["ms_per_step"]
+                out[m + "_dtype"] = amp
+                out[m + "_per_gpu_batch"] = mbatch
+                out[m + "_selected_over_k"] = i.get("selected_over_k")
+                out[m + "_effective_compression_ratio"] = i.get("effective_compression_ratio")
+            alive = optional_phase(m, out, P, model_phase)
+            rb = REF_BATCH.get(m)
+            if alive and rb and rb != mbatch and args.ref_batch != 0:
+                tag = "%s_ref_bs%d" % (m, rb)
+
+                def model_ref_phase(holder, m=m, rb=rb, mthr=mthr, msteps=msteps, mwarm=mwarm, tag=tag):
+                    i = timed(holder, tag, amp, False, mthr, rb, msteps, mwarm, graph=False, model=m)
+                    out[tag + "_value"] = i["value"]
+                    out[tag + "_ms_per_step"] = i["ms_per_step"]
+                alive = optional_phase(tag, out, P, model_ref_phase)
 
     # every phase's shapes (the reference-batch phases tune their own keys)
     if rank == 0 and os.environ.get("GKSGD_GEMM_DUMP"):

@@ -163,7 +163,7 @@ def test_library_trainer_and_bench_share_one_default(monkeypatch):
     monkeypatch.delenv("GKSGD_F32_MATMUL", raising=False)
     from gaussiank_sgd_amd.train.dist_trainer import build_parser
     assert build_parser().parse_args([]).f32_matmul == "bf16x6"
-    helptext = build_parser().format_help()
+    helptext = " ".join(build_parser().format_help().split())
     assert "--f32-matmul" in helptext and "default: bf16x6" in helptext
     monkeypatch.setattr(sys, "argv", ["bench.py"])
     import importlib
