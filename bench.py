@@ -775,8 +775,13 @@ def main() -> int:
             if alive and rb and rb != mbatch and args.ref_batch != 0:
                 tag = "%s_ref_bs%d" % (m, rb)
 
-                def model_ref_phase(holder, m=m, rb=rb, mthr=mthr, msteps=msteps, mwarm=mwarm, tag=tag):
-                    i = timed(holder, tag, amp, False, mthr, rb, msteps, mwarm, graph=False, model=m)
+                # the reference batch replays as one HIP graph on one GPU, as the
+                # headline model's reference-batch phase (--ref-graph)
+                rgraph = (P == 1 and m != "lstm") if args.ref_graph == "auto" else (args.ref_graph == "on"
+                                                                                    and m != "lstm")
+
+                def model_ref_phase(holder, m=m, rb=rb, mthr=mthr, msteps=msteps, mwarm=mwarm, tag=tag, rgraph=rgraph):
+                    i = timed(holder, tag, amp, False, mthr, rb, msteps, mwarm, graph=rgraph, model=m)
                     out[tag + "_value"] = i["value"]
                     out[tag + "_ms_per_step"] = i["ms_per_step"]
                 alive = optional_phase(tag, out, P, model_ref_phase)
