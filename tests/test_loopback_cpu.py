@@ -152,3 +152,54 @@ def test_loopback_momentum_correction_sparse_apply_matches_dense():
             assert torch.allclose(sp[0][k], dn[0][k], atol=1e-6, rtol=1e-5), k
 
 
+
+
+@pytest.mark.parametrize("kind", ["sgd", "lars", "plain"])
+def test_broadcast_state_replicates_momentum_and_schedule_position(kind):
+    """DistributedOptimizer.broadcast_state (multi-rank resume): rank 0 holds
+    momentum (or LARS acceleration) and a later schedule position; after the
+    broadcast every rank holds rank 0's buffers and train_epoch / train_iter,
+    and one more identical step keeps the replicas identical."""
+    from gaussiank_sgd_amd.compression import compressors
+    from gaussiank_sgd_amd.optim.lars import LARS
+    from gaussiank_sgd_amd.parallel.distributed_optimizer import DistributedOptimizer
+
+    def body(r):
+        torch.manual_seed(0)
+        net = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.ReLU(), torch.nn.Linear(32, 4))
+        if kind == "lars":
+            base = LARS(net.parameters(), lr=0.1, momentum=0.9)
+        else:
+            base = torch.optim.SGD(net.parameters(), lr=0.1, momentum=0.9)
+        opt = DistributedOptimizer(base, named_parameters=net.named_parameters(), compression=compressors["none"],
+                                   is_sparse=False, density=1.0, threshold=10 ** 9, density_warmup=False,
+                                   fused_optimizer=kind != "plain")
+        if r == 0:
+            # rank 0 "resumed": two local steps of state and a later position
+            g = torch.Generator().manual_seed(7)
+            for _ in range(2):
+                opt.zero_grad()
+                net(torch.randn(8, 16, generator=g)).pow(2).mean().backward()
+                opt.local = True     # no exchange: rank 0 alone
+                opt.step()
+                opt.local = False
+            opt.train_epoch, opt.train_iter = 3, 57
+        opt.broadcast_state(0)
+        comm.broadcast_parameters(net.state_dict(), root_rank=0)
+        key = "acceleration" if kind == "lars" else "momentum_buffer"
+        bufs = [opt.state[p][key].detach().clone() for p in net.parameters()]
+        x = torch.randn(8, 16, generator=torch.Generator().manual_seed(11))
+        opt.zero_grad()
+        net(x).pow(2).mean().backward()
+        opt.step()
+        return (opt.train_epoch, opt.train_iter), bufs, [p.detach().clone() for p in net.parameters()]
+
+    res = comm.loopback_world(2, body)
+    (pos0, b0, w0), (pos1, b1, w1) = res
+    assert pos0[0] == pos1[0] == 3
+    assert pos0[1] == pos1[1]
+    for a, b in zip(b0, b1):
+        assert torch.equal(a, b)
+    assert any(float(a.abs().sum()) > 0 for a in b0)
+    for a, b in zip(w0, w1):
+        assert torch.equal(a, b)
