@@ -395,11 +395,18 @@ class _DistributedOptimizer(torch.optim.Optimizer):
     def increase_one_epoch(self):
         # the epoch's counts are those of the density in force during it (logged
         # before the schedule moves on)
-        self._drain_selected()
+        self.log_selection_summary()
         self.check_compress_sync()
-        density = self.get_current_density()
         self.train_epoch += 1
         self._plan_check_due = True
+
+    def log_selection_summary(self):
+        """The reference's per-epoch selected-count lines (:136-144) for the
+        bucket-steps since the last summary; the counts are then reset (the
+        schedule position is not touched: a run stopped mid-epoch logs its
+        partial epoch without advancing the density schedule)."""
+        self._drain_selected()
+        density = self.get_current_density()
         counts = self._selected_num_gradients
         if rank() == 0:
             sz = int(np.sum(self._sizes))

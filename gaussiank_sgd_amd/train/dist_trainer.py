@@ -177,6 +177,8 @@ def ssgd(dnn, dataset, data_dir, nworkers, lr, batch_size, nsteps_update, max_ep
             if max_iters is not None and done >= max_iters:
                 if i == iters_per_epoch - 1:
                     optimizer.increase_one_epoch()
+                elif hasattr(optimizer, "log_selection_summary"):
+                    optimizer.log_selection_summary()
                 return _finish(trainer, optimizer, save_final)
         optimizer.increase_one_epoch()
     return _finish(trainer, optimizer, save_final)

@@ -366,6 +366,17 @@ def test_splitk_candidates_only_for_underfilled_deep_gemms():
     planes; bf16 never gets them (partial planes are fp32)."""
     import torch
     from gaussiank_sgd_amd.ops import conv1x1 as cv
+    prev = cv.set_f32_matmul("native")     # the S digit alone (bf16x6 adds the 100000 digit)
+    try:
+        _splitk_checks(cv, torch)
+        cv.set_f32_matmul("bf16x6")
+        x6 = cv._splitk_cfgs(torch.float32, 1568, 512, 2048)
+        assert {(x % cv.X6) // 10000 for x in x6} == {2, 4, 8} and any(x >= cv.X6 for x in x6)
+    finally:
+        cv.set_f32_matmul(prev)
+
+
+def _splitk_checks(cv, torch):
     c = cv._splitk_cfgs(torch.float32, 1568, 512, 2048)          # stage-4 1x1 at bs32
     assert c and all(x >= 20000 for x in c)
     S = sorted({x // 10000 for x in c})
