@@ -1735,6 +1735,25 @@ void lstm_rec_gemm(at::Tensor A, at::Tensor Bm, at::Tensor P, int64_t S) {
                       (int)K, (int)S, cur_stream(A));
 }
 
+// bf16x6 split-K recurrent GEMM: A fp32 [M, K]; B3 bf16 [3, N, K] = the exact
+// hi / mid / lo split of an fp32 B (ops/lstm.py split3)
+void lstm_rec_gemm_x6(at::Tensor A, at::Tensor B3, at::Tensor P, int64_t S) {
+  TORCH_CHECK(A.dim() == 2 && B3.dim() == 3 && B3.size(0) == 3 && A.size(1) == B3.size(2),
+              "lstm_rec_gemm_x6: A [M, K] fp32 and B3 [3, N, K] bf16 expected");
+  const int64_t M = A.size(0), K = A.size(1), N = B3.size(1);
+  TORCH_CHECK(S >= 1 && K % (64 * S) == 0 && N % 64 == 0, "lstm_rec_gemm_x6: K % (64 S) and N % 64 must be 0");
+  TORCH_CHECK(A.is_cuda() && A.scalar_type() == at::kFloat && A.stride(1) == 1 && A.stride(0) % 4 == 0 &&
+                  B3.is_cuda() && B3.scalar_type() == at::kBFloat16 && B3.stride(2) == 1 && B3.stride(1) % 8 == 0 &&
+                  B3.stride(0) % 8 == 0,
+              "lstm_rec_gemm_x6: fp32 A / bf16 B3 GPU operands with unit column stride and 16-byte aligned rows");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(B3.data_ptr()) % 16 == 0,
+              "lstm_rec_gemm_x6: 16-byte aligned operands");
+  check_lstm(P, at::kFloat, S * M * N, "P");
+  c10::DeviceGuard guard(A.device());
+  gk::lstm_rec_gemm_x6(A.data_ptr<float>(), A.stride(0), static_cast<const uint16_t*>(B3.data_ptr()), B3.stride(1),
+                       B3.stride(0), P.data_ptr<float>(), (int)M, (int)N, (int)K, (int)S, cur_stream(A));
+}
+
 void lstm_cell_fwd(at::Tensor xg, c10::optional<at::Tensor> hg, c10::optional<at::Tensor> P, int64_t S, at::Tensor c_prev, at::Tensor c,
                    at::Tensor h, c10::optional<at::Tensor> h_pad, at::Tensor gates) {
   TORCH_CHECK(xg.dim() == 2 && xg.size(1) % 4 == 0, "xg must be [B, 4H]");
@@ -1936,6 +1955,7 @@ TORCH_LIBRARY(gksgd, m) {
   m.def("colsum_acc(Tensor dy, Tensor(a!) db) -> ()");
   m.def("gelu_bwd_colsum(Tensor dy, Tensor pre, Tensor(a!) dpre, Tensor(b!)? db=None) -> ()");
   m.def("lstm_rec_gemm(Tensor A, Tensor B, Tensor(a!) P, int S) -> ()");
+  m.def("lstm_rec_gemm_x6(Tensor A, Tensor B3, Tensor(a!) P, int S) -> ()");
   m.def("lstm_cell_fwd(Tensor xg, Tensor? hg, Tensor? P, int S, Tensor c_prev, Tensor(a!) c, Tensor(b!) h, Tensor(c!)? h_pad, "
         "Tensor(d!) gates) -> ()");
   m.def("lstm_cell_bwd(Tensor? dout, Tensor? dh_rec, Tensor? P, int S, Tensor? dc_next, Tensor gates, Tensor c, Tensor c_prev, "
@@ -2025,6 +2045,7 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("colsum_acc", &colsum_acc);
   m.impl("gelu_bwd_colsum", &gelu_bwd_colsum);
   m.impl("lstm_rec_gemm", &lstm_rec_gemm);
+  m.impl("lstm_rec_gemm_x6", &lstm_rec_gemm_x6);
   m.impl("lstm_cell_fwd", &lstm_cell_fwd);
   m.impl("lstm_cell_bwd", &lstm_cell_bwd);
 }

@@ -558,6 +558,10 @@ void lstm_cell_bwd(const uint16_t* dout, const uint16_t* dh_rec, const float* P,
                    const float* c, const float* c_prev, uint16_t* dG, uint16_t* dG_pad, float* dc_prev, int B, int H,
                    int Hp, hipStream_t stream);
 // fp32 variants (the reference's precision): fp32 operands, same layouts
+// bf16x6 (fp32-accurate) split-K step GEMM: A fp32 [M][K] (split in registers),
+// B3 = three bf16 planes [3][N][K] (plane stride bplane elements) of the fp32 B
+void lstm_rec_gemm_x6(const float* A, int64_t lda, const uint16_t* B3, int64_t ldb, int64_t bplane, float* P, int M,
+                      int N, int K, int S, hipStream_t stream);
 void lstm_rec_gemm_f32(const float* A, int64_t lda, const float* B, int64_t ldb, float* P, int M, int N, int K, int S,
                        hipStream_t stream);
 void lstm_cell_fwd_f32(const float* xg, const float* hg, const float* P, int S, const float* c_prev, float* c, float* h,

@@ -22,6 +22,7 @@
 // padded copies of W_hh); the cell kernels sum its fp32 K-slices on load.
 #include "common.h"
 #include "gk_kernels.h"
+#include "mfma_util.h"
 
 namespace gk {
 namespace {
@@ -175,6 +176,92 @@ __global__ __launch_bounds__(kBlock) void rec_gemm_f32_kernel(const float* __res
     }
 }
 
+// bf16x6 twin (fp32-accurate, the reference's precision, on the bf16 matrix
+// cores): A is the fp32 [M][K] operand (h_pad / dG_pad), split exactly into
+// bf16 parts hi + mid + lo in registers (mfma_util.h split3x8); B arrives
+// pre-split as three bf16 planes [3][N][K] (W_hh is constant over the
+// sequence: split ONCE per forward / backward on the host side).  The six part
+// products of order <= 2 are accumulated in fp32, smallest first (the dropped
+// mid*lo, lo*mid, lo*lo are each < 2^-24 |a b|) -- six 16-cycle bf16 MFMAs per
+// 32-deep step against eight 32-cycle fp32 ones (2.67x on the matrix pipe).
+// Lane (fr, fq) holds K elements 8 fq .. 8 fq + 7 of its row in both operands.
+template <int D>
+__global__ __launch_bounds__(kBlock) void rec_gemm_x6_kernel(const float* __restrict__ A, int64_t lda,
+                                                             const uint16_t* __restrict__ B3, int64_t ldb,
+                                                             int64_t bplane, float* __restrict__ P, int M, int N,
+                                                             int kslice) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int n0 = blockIdx.x * 64;
+  const int s = blockIdx.y;
+  const int m0 = blockIdx.z * 128 + w * 32;
+  if (m0 >= M) return;  // no LDS / barriers: a wave past the last row just leaves
+  const int64_t kb = (int64_t)s * kslice + fq * 8;
+  const float* ap[2];
+  const uint16_t* bp[4];
+#pragma unroll
+  for (int ms = 0; ms < 2; ++ms) {
+    int r = m0 + ms * 16 + fr;
+    r = r < M ? r : M - 1;
+    ap[ms] = A + (int64_t)r * lda + kb;
+  }
+#pragma unroll
+  for (int ns = 0; ns < 4; ++ns) bp[ns] = B3 + (int64_t)(n0 + ns * 16 + fr) * ldb + kb;
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+    for (int ns = 0; ns < 4; ++ns) acc[ms][ns] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < kslice; k += 32 * D) {
+    f32x4 a[D][2][2];
+    bf16x8 bh[D][4], bm[D][4], bl[D][4];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+#pragma unroll
+      for (int ns = 0; ns < 4; ++ns) {
+        const uint16_t* q = bp[ns] + k + 32 * d;
+        bh[d][ns] = *reinterpret_cast<const bf16x8*>(q);
+        bm[d][ns] = *reinterpret_cast<const bf16x8*>(q + bplane);
+        bl[d][ns] = *reinterpret_cast<const bf16x8*>(q + 2 * bplane);
+      }
+#pragma unroll
+      for (int ms = 0; ms < 2; ++ms) {
+        a[d][ms][0] = *reinterpret_cast<const f32x4*>(ap[ms] + k + 32 * d);
+        a[d][ms][1] = *reinterpret_cast<const f32x4*>(ap[ms] + k + 32 * d + 4);
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+      for (int ms = 0; ms < 2; ++ms) {
+        bf16x8 ah, am, al;
+        split3x8(a[d][ms][0], a[d][ms][1], ah, am, al);
+#pragma unroll
+        for (int ns = 0; ns < 4; ++ns) {
+          f32x4 c = acc[ms][ns];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[d][ns], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[d][ns], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bm[d][ns], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bm[d][ns], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bh[d][ns], c, 0, 0, 0);
+          acc[ms][ns] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[d][ns], c, 0, 0, 0);
+        }
+      }
+  }
+  // D[row = 4 fq + r][col = fr] of every 16x16 subtile
+  float* Ps = P + (int64_t)s * M * N;
+#pragma unroll
+  for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + ms * 16 + fq * 4 + r;
+      if (m < M) {
+#pragma unroll
+        for (int ns = 0; ns < 4; ++ns) Ps[(int64_t)m * N + n0 + ns * 16 + fr] = acc[ms][ns][r];
+      }
+    }
+}
+
 // element storage of the cell kernels' bf16 / fp32 operands
 __device__ __forceinline__ float ld_e(const uint16_t* p, int64_t i) { return bf2f(p[i]); }
 __device__ __forceinline__ float ld_e(const float* p, int64_t i) { return p[i]; }
@@ -273,6 +360,17 @@ void lstm_rec_gemm_f32(const float* A, int64_t lda, const float* B, int64_t ldb,
     hipLaunchKernelGGL(rec_gemm_f32_kernel<8>, grid, dim3(kBlock), 0, stream, A, lda, B, ldb, P, M, N, ks);
   else
     hipLaunchKernelGGL(rec_gemm_f32_kernel<4>, grid, dim3(kBlock), 0, stream, A, lda, B, ldb, P, M, N, ks);
+}
+
+void lstm_rec_gemm_x6(const float* A, int64_t lda, const uint16_t* B3, int64_t ldb, int64_t bplane, float* P, int M,
+                      int N, int K, int S, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || S <= 0) return;
+  dim3 grid((unsigned)(N / 64), (unsigned)S, (unsigned)ceil_div(M, 128));
+  const int ks = K / S;
+  if (ks % 64 == 0)
+    hipLaunchKernelGGL(rec_gemm_x6_kernel<2>, grid, dim3(kBlock), 0, stream, A, lda, B3, ldb, bplane, P, M, N, ks);
+  else
+    hipLaunchKernelGGL(rec_gemm_x6_kernel<1>, grid, dim3(kBlock), 0, stream, A, lda, B3, ldb, bplane, P, M, N, ks);
 }
 
 template <typename T>

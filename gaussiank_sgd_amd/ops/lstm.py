@@ -99,6 +99,27 @@ def _splitk(direction: str, batch: int) -> bool:
     return batch <= SPLITK_MAX_BATCH[direction]
 
 
+# fp32 layers (the reference's precision): the step GEMMs run on the bf16x6
+# split-K kernel (lstm.hip rec_gemm_x6_kernel: fp32-accurate on the bf16 matrix
+# cores, W_hh split into three bf16 planes once per forward / backward) at
+# every batch; GKSGD_LSTM_X6=0 keeps the fp32-MFMA kernel / hipBLASLt choice.
+_X6 = os.environ.get("GKSGD_LSTM_X6", "1") != "0"
+# split-K workgroup targets of the x6 step GEMMs (forward, backward)
+_X6_TARGET = {"fwd": int(os.environ.get("GKSGD_LSTM_X6_FWD_WG", "512")),
+              "bwd": int(os.environ.get("GKSGD_LSTM_X6_BWD_WG", "256"))}
+
+
+def split3(w: torch.Tensor) -> torch.Tensor:
+    """Exact fp32 -> three bf16 planes [3, *w.shape] with w = hi + mid + lo
+    (round-to-nearest-even at each step, as mfma_util.h split3x8: every
+    residual is exact in fp32, so the three parts hold all 24 mantissa bits)."""
+    hi = w.to(torch.bfloat16)
+    r = w - hi.float()
+    mid = r.to(torch.bfloat16)
+    lo = (r - mid.float()).to(torch.bfloat16)
+    return torch.stack([hi, mid, lo]).contiguous()
+
+
 def _splits(kblocks: int, nblocks: int, target: int = 512) -> int:
     """K-slice count S for the split-K step GEMM: the largest divisor of the
     64-deep K-block count keeping S * nblocks <= target workgroups (two per
@@ -133,19 +154,25 @@ class _LSTMLayerFn(torch.autograd.Function):
         gates = torch.empty(T, B, 4 * H, dtype=torch.float32, device=dev)
         h = h0.to(cd).contiguous()
         h0c = h
-        if fast and _splitk("fwd", B):
-            # split-K step GEMM over 64-padded operands (lstm.hip rec_gemm_kernel)
+        x6 = fast and cd == torch.float32 and _X6
+        if fast and (x6 or _splitk("fwd", B)):
+            # split-K step GEMM over 64-padded operands (lstm.hip rec_gemm_kernel;
+            # fp32: rec_gemm_x6_kernel on the three bf16 planes of W_hh)
             ops = _g()
             Hp = _pad64(H)
             wpf = torch.zeros(4, Hp, Hp, dtype=cd, device=dev)
             wpf[:, :H, :H] = whh.view(4, H, H)
             wpf = wpf.view(4 * Hp, Hp)
-            S = _splits(Hp // 64, (4 * Hp // 64) * _cdiv(B, 128))
+            wpf3 = split3(wpf) if x6 else None
+            S = _splits(Hp // 64, (4 * Hp // 64) * _cdiv(B, 128), target=_X6_TARGET["fwd"] if x6 else 512)
             P = torch.empty(S, B, 4 * Hp, dtype=torch.float32, device=dev)
             h_pad = torch.zeros(B, Hp, dtype=cd, device=dev)
             h_pad[:, :H] = h
             for t in range(T):
-                ops.lstm_rec_gemm(h_pad, wpf, P, S)
+                if x6:
+                    ops.lstm_rec_gemm_x6(h_pad, wpf3, P, S)
+                else:
+                    ops.lstm_rec_gemm(h_pad, wpf, P, S)
                 ops.lstm_cell_fwd(xg[t], None, P, S, c_all[t], c_all[t + 1], out[t], h_pad, gates[t])
         else:
             whh_t = whh.t()
@@ -174,14 +201,16 @@ class _LSTMLayerFn(torch.autograd.Function):
         dc = dc_n.float().contiguous() if dc_n is not None else None
         bufs = [torch.empty(B, H, dtype=torch.float32, device=dev) for _ in range(2)]
         need_dh0 = ctx.needs_input_grad[1]
-        if fast and _splitk("bwd", B):
+        x6 = fast and cd == torch.float32 and _X6
+        if fast and (x6 or _splitk("bwd", B)):
             ops = _g()
             Hp = _pad64(H)
             # wpb[j'][k Hp + j] = W_hh[k H + j][j']: dh = dG_pad wpb^T
             wpb = torch.zeros(Hp, 4, Hp, dtype=cd, device=dev)
             wpb[:H, :, :H] = whh.view(4, H, H).permute(2, 0, 1)
             wpb = wpb.view(Hp, 4 * Hp)
-            S = _splits(4 * Hp // 64, (Hp // 64) * _cdiv(B, 128), target=256)
+            wpb3 = split3(wpb) if x6 else None
+            S = _splits(4 * Hp // 64, (Hp // 64) * _cdiv(B, 128), target=_X6_TARGET["bwd"] if x6 else 256)
             P = torch.empty(S, B, Hp, dtype=torch.float32, device=dev)
             dG_pad = torch.zeros(B, 4 * Hp, dtype=cd, device=dev)
             for t in range(T - 1, -1, -1):
@@ -193,7 +222,10 @@ class _LSTMLayerFn(torch.autograd.Function):
                                   dG[t], dG_pad, dc_prev)
                 dc = dc_prev
                 if t > 0 or need_dh0:
-                    ops.lstm_rec_gemm(dG_pad, wpb, P, S)
+                    if x6:
+                        ops.lstm_rec_gemm_x6(dG_pad, wpb3, P, S)
+                    else:
+                        ops.lstm_rec_gemm(dG_pad, wpb, P, S)
             dh_rec = P.sum(0)[:, :H] if need_dh0 else None
         else:
             dh_rec = dh_n.to(cd).contiguous() if dh_n is not None else None

@@ -255,14 +255,45 @@ def test_lstm_rec_gemm_f32_vs_fp64(M, N, K, S):
     assert (P[0].double() - ref0).abs().max().item() <= 2e-6 * scale
 
 
-@pytest.mark.parametrize("fwd_max,bwd_max", [(1 << 30, 1 << 30), (0, 0), (0, 1 << 30)],
-                         ids=["splitk", "blas", "mixed"])
-def test_gklstm_f32_vs_fp64_nn_lstm(monkeypatch, fwd_max, bwd_max):
-    """fp32 GkLSTM (HIP step GEMM + fp32 cells) vs an fp64 nn.LSTM."""
+@pytest.mark.parametrize("M,N,K,S", [(128, 6144, 1536, 4), (128, 1536, 6144, 16), (20, 6144, 1536, 8),
+                                     (20, 1536, 6144, 16), (3, 256, 64, 1), (200, 128, 256, 2)])
+def test_lstm_rec_gemm_x6_vs_fp64(M, N, K, S):
+    """bf16x6 split-K step GEMM (fp32 A split in registers, B as three exact
+    bf16 planes): every K slice against fp64, and no less accurate than the
+    fp32-MFMA kernel on the same operands."""
+    from gaussiank_sgd_amd.ops.lstm import split3
+    g = torch.ops.gksgd
+    torch.manual_seed(M + N + K + 7)
+    A = torch.randn(M, K, device="cuda")
+    Bm = torch.randn(N, K, device="cuda") / K ** 0.5
+    B3 = split3(Bm)
+    assert torch.equal(B3[0].float() + B3[1].float() + B3[2].float(), Bm)   # the split is exact
+    P = torch.full((S, M, N), float("nan"), device="cuda")
+    g.lstm_rec_gemm_x6(A, B3, P, S)
+    Pf = torch.full((S, M, N), float("nan"), device="cuda")
+    g.lstm_rec_gemm(A, Bm, Pf, S)
+    ref = A.double() @ Bm.double().t()
+    scale = (A.double().abs() @ Bm.double().abs().t()).max().item()
+    err = (P.double().sum(0) - ref).abs()
+    assert err.max().item() <= 2e-6 * scale
+    ks = K // S
+    ref0 = A[:, :ks].double() @ Bm[:, :ks].double().t()
+    assert (P[0].double() - ref0).abs().max().item() <= 2e-6 * scale
+    e_x6 = float((P.double().sum(0) - ref).norm() / ref.norm())
+    e_f32 = float((Pf.double().sum(0) - ref).norm() / ref.norm())
+    assert e_x6 <= 1.05 * e_f32 + 1e-12, (e_x6, e_f32)
+
+
+@pytest.mark.parametrize("fwd_max,bwd_max,x6", [(1 << 30, 1 << 30, False), (0, 0, False), (0, 1 << 30, False),
+                                                (0, 0, True)],
+                         ids=["splitk", "blas", "mixed", "x6"])
+def test_gklstm_f32_vs_fp64_nn_lstm(monkeypatch, fwd_max, bwd_max, x6):
+    """fp32 GkLSTM (HIP step GEMM -- fp32 MFMA or bf16x6 -- + fp32 cells) vs an fp64 nn.LSTM."""
     from gaussiank_sgd_amd.ops import lstm as L_
     from gaussiank_sgd_amd.ops.lstm import GkLSTM
     monkeypatch.setitem(L_.SPLITK_MAX_BATCH, "fwd", fwd_max)
     monkeypatch.setitem(L_.SPLITK_MAX_BATCH, "bwd", bwd_max)
+    monkeypatch.setattr(L_, "_X6", x6)
     torch.manual_seed(0)
     T, B, I, H, L = 35, 16, 256, 320, 2
     ref = torch.nn.LSTM(I, H, num_layers=L).cuda().double()
