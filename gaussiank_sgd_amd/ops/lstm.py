@@ -82,31 +82,75 @@ def _cdiv(a: int, b: int) -> int:
     return (a + b - 1) // b
 
 
-# Largest batch per direction that runs the step GEMM split-K (else one
-# hipBLASLt GEMM with a bf16 output read by the cell kernel).  Measured on
-# MI355X (bench/lstm_gemm_probe.py, H = 1500): B = 20 -> 5 us split-K vs 19 us
-# hipBLASLt both ways; B = 128 -> forward 19.5 (+12 MB of fp32 slices for the
-# cell to read) vs 20.7 us, backward 20 vs 31 us.  Override with
-# GKSGD_LSTM_SPLITK="fwd:<maxB>,bwd:<maxB>".
-SPLITK_MAX_BATCH = {"fwd": 64, "bwd": 1 << 30}
+# Step GEMM per direction: None = autotuned once per (direction, dtype, batch,
+# H) among hipBLASLt and the split-K kernel at every K-slice count S (cached
+# with the other GEMM choices, ops/conv1x1.py _pick).  An int forces the
+# round-5 rule instead: split-K with the default S up to that batch, hipBLASLt
+# above.  Measured on MI355X (bench/lstm_x6_probe.py, profiles/r06_lstm_step_probe.json),
+# fp32 H = 1500: B = 20 forward split-K S = 8 11.9 us vs the rule's S = 4 18.5,
+# backward S = 24 14.2 vs S = 8 33.6 (hipBLASLt 19 / 22); B = 128 hipBLASLt
+# 29 / 28.5 vs split-K 34 / 39.5 -- no single rule is right for every shape.
+# GKSGD_LSTM_SPLITK="fwd:<maxB>,bwd:<maxB>" forces the rule.
+SPLITK_MAX_BATCH = {"fwd": None, "bwd": None}
 for _kv in os.environ.get("GKSGD_LSTM_SPLITK", "").split(","):
     if ":" in _kv:
         _k, _v = _kv.split(":", 1)
         SPLITK_MAX_BATCH[_k.strip()] = int(_v)
 
 
-def _splitk(direction: str, batch: int) -> bool:
-    return batch <= SPLITK_MAX_BATCH[direction]
+def _splits(kblocks: int, nblocks: int, target: int = 512) -> int:
+    """K-slice count S for the split-K step GEMM: the largest divisor of the
+    64-deep K-block count keeping S * nblocks <= target workgroups (two per
+    CU) and every slice >= two K-blocks deep."""
+    best = 1
+    for d in range(2, kblocks + 1):
+        if kblocks % d == 0 and d * nblocks <= target and kblocks // d >= 2:
+            best = d
+    return best
 
 
-# fp32 layers (the reference's precision): the step GEMMs run on the bf16x6
-# split-K kernel (lstm.hip rec_gemm_x6_kernel: fp32-accurate on the bf16 matrix
-# cores, W_hh split into three bf16 planes once per forward / backward) at
-# every batch; GKSGD_LSTM_X6=0 keeps the fp32-MFMA kernel / hipBLASLt choice.
-_X6 = os.environ.get("GKSGD_LSTM_X6", "1") != "0"
-# split-K workgroup targets of the x6 step GEMMs (forward, backward)
-_X6_TARGET = {"fwd": int(os.environ.get("GKSGD_LSTM_X6_FWD_WG", "512")),
-              "bwd": int(os.environ.get("GKSGD_LSTM_X6_BWD_WG", "256"))}
+def _step_plan(direction: str, cd: torch.dtype, B: int, H: int, dev) -> Tuple[str, int]:
+    """("hip", S): the split-K kernel with S K-slices on the 64-padded
+    operands; ("blas", 0): hipBLASLt on the unpadded ones."""
+    Hp = _pad64(H)
+    fwd = direction == "fwd"
+    kb, nb = (Hp // 64, 4 * Hp // 64) if fwd else (4 * Hp // 64, Hp // 64)
+    mb = _cdiv(B, 128)
+    mx = SPLITK_MAX_BATCH[direction]
+    if mx is not None:
+        if B > mx:
+            return ("blas", 0)
+        return ("hip", _splits(kb, nb * mb, target=512 if fwd else 256))
+    from . import conv1x1 as _cv
+    key = ("lstm_step", direction, B, H, "f32" if cd == torch.float32 else "bf16")
+    got = _cv._choices.get(key)
+    if got is not None:
+        return (got[0], int(got[1]))
+    g = _g()
+    M, N, K = (B, 4 * Hp, Hp) if fwd else (B, Hp, 4 * Hp)
+    a = torch.zeros(M, K, dtype=cd, device=dev)
+    w = torch.zeros(N, K, dtype=cd, device=dev)
+    cands = []
+    for S in range(1, kb + 1):
+        if kb % S or (S > 1 and kb // S < 2) or S * nb * mb > 2048:
+            continue
+        P = torch.empty(S, M, N, dtype=torch.float32, device=dev)
+        cands.append((("hip", S, 0), (lambda S=S, P=P: g.lstm_rec_gemm(a, w, P, S))))
+    ab = torch.zeros(B, H if fwd else 4 * H, dtype=cd, device=dev)
+    wb = torch.zeros(4 * H, H, dtype=cd, device=dev)
+    cands.append((("blas", 0, 0), (lambda: torch.mm(ab, wb.t())) if fwd else (lambda: torch.mm(ab, wb))))
+    ch = _cv._pick(key, cands)
+    return (ch[0], int(ch[1]))
+
+
+# fp32 step GEMM on the bf16x6 split-K kernel (lstm.hip rec_gemm_x6_kernel:
+# fp32-accurate on the bf16 matrix cores, W_hh split once into three bf16
+# planes).  Opt-in (GKSGD_LSTM_X6=1): the step GEMM is bound by its operand
+# loads, not by the matrix pipe, and the three planes are 1.5x the bytes of
+# fp32 -- measured 37 / 47 us (B = 128 forward / backward, best S) against
+# 34 / 39.5 for the fp32-MFMA kernel and 29 / 28.5 for hipBLASLt, and the
+# LSTM step 20.9 vs 16.3 ms (r6c4, profiles/r06_lstm_step_probe.json).
+_X6 = os.environ.get("GKSGD_LSTM_X6", "0") == "1"
 
 
 def split3(w: torch.Tensor) -> torch.Tensor:
@@ -155,7 +199,8 @@ class _LSTMLayerFn(torch.autograd.Function):
         h = h0.to(cd).contiguous()
         h0c = h
         x6 = fast and cd == torch.float32 and _X6
-        if fast and (x6 or _splitk("fwd", B)):
+        plan = _step_plan("fwd", cd, B, H, dev) if fast else ("blas", 0)
+        if fast and (x6 or plan[0] == "hip"):
             # split-K step GEMM over 64-padded operands (lstm.hip rec_gemm_kernel;
             # fp32: rec_gemm_x6_kernel on the three bf16 planes of W_hh)
             ops = _g()
@@ -164,7 +209,7 @@ class _LSTMLayerFn(torch.autograd.Function):
             wpf[:, :H, :H] = whh.view(4, H, H)
             wpf = wpf.view(4 * Hp, Hp)
             wpf3 = split3(wpf) if x6 else None
-            S = _splits(Hp // 64, (4 * Hp // 64) * _cdiv(B, 128), target=_X6_TARGET["fwd"] if x6 else 512)
+            S = _splits(Hp // 64, (4 * Hp // 64) * _cdiv(B, 128)) if x6 else plan[1]
             P = torch.empty(S, B, 4 * Hp, dtype=torch.float32, device=dev)
             h_pad = torch.zeros(B, Hp, dtype=cd, device=dev)
             h_pad[:, :H] = h
@@ -202,7 +247,8 @@ class _LSTMLayerFn(torch.autograd.Function):
         bufs = [torch.empty(B, H, dtype=torch.float32, device=dev) for _ in range(2)]
         need_dh0 = ctx.needs_input_grad[1]
         x6 = fast and cd == torch.float32 and _X6
-        if fast and (x6 or _splitk("bwd", B)):
+        plan = _step_plan("bwd", cd, B, H, dev) if fast else ("blas", 0)
+        if fast and (x6 or plan[0] == "hip"):
             ops = _g()
             Hp = _pad64(H)
             # wpb[j'][k Hp + j] = W_hh[k H + j][j']: dh = dG_pad wpb^T
@@ -210,7 +256,7 @@ class _LSTMLayerFn(torch.autograd.Function):
             wpb[:H, :, :H] = whh.view(4, H, H).permute(2, 0, 1)
             wpb = wpb.view(Hp, 4 * Hp)
             wpb3 = split3(wpb) if x6 else None
-            S = _splits(4 * Hp // 64, (Hp // 64) * _cdiv(B, 128), target=_X6_TARGET["bwd"] if x6 else 256)
+            S = _splits(4 * Hp // 64, (Hp // 64) * _cdiv(B, 128), target=256) if x6 else plan[1]
             P = torch.empty(S, B, Hp, dtype=torch.float32, device=dev)
             dG_pad = torch.zeros(B, 4 * Hp, dtype=cd, device=dev)
             for t in range(T - 1, -1, -1):

@@ -285,8 +285,8 @@ def test_lstm_rec_gemm_x6_vs_fp64(M, N, K, S):
 
 
 @pytest.mark.parametrize("fwd_max,bwd_max,x6", [(1 << 30, 1 << 30, False), (0, 0, False), (0, 1 << 30, False),
-                                                (0, 0, True)],
-                         ids=["splitk", "blas", "mixed", "x6"])
+                                                (0, 0, True), (None, None, False)],
+                         ids=["splitk", "blas", "mixed", "x6", "tuned"])
 def test_gklstm_f32_vs_fp64_nn_lstm(monkeypatch, fwd_max, bwd_max, x6):
     """fp32 GkLSTM (HIP step GEMM -- fp32 MFMA or bf16x6 -- + fp32 cells) vs an fp64 nn.LSTM."""
     from gaussiank_sgd_amd.ops import lstm as L_
