@@ -17,7 +17,8 @@ Each (direction, M, K, N) times the HIP kernel configurations and
 fastest (cache and switches shared with the convolutions: ``GKSGD_GEMM_TUNE``,
 ``tuning/gemm_choices.json``; ``GKSGD_FASTLINEAR=0`` disables the path).
 Dimensions that are not multiples of 64 (the LSTM's 1500 -> 10000 softmax
-layer) keep hipBLASLt for the GEMMs and still get the fused bias gradient.
+layer, BERT's vocabulary) also offer the HIP kernels on zero-padded operands
+(timed with their copies against hipBLASLt, ``_fwd_padded``).
 ``FastLinear`` is a drop-in ``nn.Linear`` (same parameters and state_dict
 keys).  fp32 inputs without autocast (the reference's precision) take the same
 path on the fp32 MFMA kernels (``v_mfma_f32_16x16x4_f32``) and the fp32 column
@@ -78,6 +79,32 @@ def _hip_gemm_ok(K: int, N: int) -> bool:
     return K % 64 == 0 and N % 64 == 0
 
 
+# Dimensions that are not multiples of 64 (the LSTM's 1500 hidden units and
+# 10,000-word softmax, BERT's 30,522-word vocabulary) can still run the HIP
+# kernels on zero-padded copies of the operands: K and N are padded to the
+# next multiple of 64 (zero columns add nothing to the products), the output
+# is the [:, :N] view of the padded result.  The padded candidates are timed
+# WITH their copies against hipBLASLt, so the tuner keeps whichever is faster
+# per shape; GKSGD_LINEAR_PAD=0 restores hipBLASLt-only for these shapes.
+_PAD = os.environ.get("GKSGD_LINEAR_PAD", "1") != "0"
+
+
+def _p64(n: int) -> int:
+    return (n + 63) // 64 * 64
+
+
+def _pad2(t: torch.Tensor, rows: int, cols: int) -> torch.Tensor:
+    """Zero-padded contiguous copy of a 2-D tensor to [rows, cols] (one kernel)."""
+    r, c = t.shape
+    if r == rows and c == cols and t.is_contiguous():
+        return t
+    return F.pad(t, (0, cols - c, 0, rows - r))
+
+
+def _pad_ok(t: torch.Tensor) -> bool:
+    return _PAD and t.is_cuda
+
+
 def _fwd(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor],
          b16: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = x2 . w^T (+ bias) in x2's dtype (bf16, or fp32: the fp32 MFMA
@@ -92,7 +119,9 @@ def _fwd(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor],
     def blas():
         return torch.addmm(b16, x2, w.t()) if b16 is not None else torch.mm(x2, w.t())
     if not _hip_gemm_ok(K, N):
-        return blas()
+        if not _pad_ok(x2):
+            return blas()
+        return _fwd_padded(x2, w, bias, blas)
     g = _g()
     y = torch.empty(M, N, dtype=dt, device=x2.device)
     cands = [(("hip", c, mb), (lambda c=c, mb=mb: g.gemm_nt(x2, w, y, c, mb, None, bias)))
@@ -105,6 +134,60 @@ def _fwd(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor],
     return y
 
 
+def _fwd_padded(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], blas) -> torch.Tensor:
+    """y = x2 . w^T (+ bias) with K / N not multiples of 64: the HIP kernels on
+    zero-padded operands (the copies timed with them) vs hipBLASLt."""
+    M, K = x2.shape
+    N = w.shape[0]
+    Kp, Np = _p64(K), _p64(N)
+    dt = x2.dtype
+    g = _g()
+
+    def padded(c, mb):
+        xp = _pad2(x2, M, Kp)
+        wp = _pad2(w, Np, Kp)
+        bp = F.pad(bias, (0, Np - N)) if bias is not None else None
+        yp = torch.empty(M, Np, dtype=dt, device=x2.device)
+        g.gemm_nt(xp, wp, yp, c, mb, None, bp)
+        return yp[:, :N]
+    key = ("lin_fwd", M, K, N, bias is not None) + _cv._dkey(dt) + ("pad",)
+    got = _cv._choices.get(key)
+    if got is not None and got[0] == "blas":
+        return blas()
+    cands = [(("hip", c, mb), (lambda c=c, mb=mb: padded(c, mb))) for c in _cv._nt_cfgs(dt) for mb in _cv._NT_GRIDS]
+    cands.append((("blas", 0, 0), blas))
+    ch = _cv._pick(key, cands)
+    if ch[0] == "blas":
+        return blas()
+    return padded(ch[1], ch[2])
+
+
+def _dgrad_padded(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """dx = dy2 . w with K / N not multiples of 64 (see _fwd_padded)."""
+    M, N = dy2.shape
+    K = w.shape[1]
+    Kp, Np = _p64(K), _p64(N)
+    dt = dy2.dtype
+    g = _g()
+    key = ("lin_dgrad", M, K, N) + _cv._dkey(dt) + ("pad",)
+    got = _cv._choices.get(key)
+    if got is not None and got[0] == "blas":
+        return torch.mm(dy2, w)
+
+    def padded(c, mb):
+        dyp = _pad2(dy2, M, Np)
+        wtp = _pad2(w.t(), Kp, Np)
+        dxp = torch.empty(M, Kp, dtype=dt, device=dy2.device)
+        g.gemm_nt(dyp, wtp, dxp, c, mb)
+        return dxp[:, :K]
+    cands = [(("hip", c, mb), (lambda c=c, mb=mb: padded(c, mb))) for c in _cv._nt_cfgs(dt) for mb in _cv._NT_GRIDS]
+    cands.append((("blas", 0, 0), lambda: torch.mm(dy2, w)))
+    ch = _cv._pick(key, cands)
+    if ch[0] == "blas":
+        return torch.mm(dy2, w)
+    return padded(ch[1], ch[2])
+
+
 def _dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """dx = dy2 . w in dy2's dtype."""
     M, N = dy2.shape
@@ -112,6 +195,8 @@ def _dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     dt = dy2.dtype
     key = ("lin_dgrad", M, K, N) + _cv._dkey(dt)
     got = _cv._choices.get(key)
+    if not _hip_gemm_ok(K, N) and _pad_ok(dy2):
+        return _dgrad_padded(dy2, w)
     if not _hip_gemm_ok(K, N) or (got is not None and got[0] == "blas"):
         return torch.mm(dy2, w)
     g = _g()
@@ -149,8 +234,24 @@ def _wgrad_into(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor) -> None:
     key = ("lin_wgrad", M, K, N) + _cv._dkey(dy2.dtype)
     scratch = torch.zeros_like(out) if key not in _cv._choices else None
     cands = []
+    padded = None
     if _hip_gemm_ok(K, N):
         cands = [(("hip", c, sp), (lambda c=c, sp=sp: g.gemm_tn_acc(dy2, x2, scratch, c, sp)))
+                 for c, sp in _cv._tn_cfgs(torch.float32 if f32 else torch.bfloat16)]
+    elif _pad_ok(dy2):
+        # zero-padded operands into a padded fp32 scratch, then one add of its
+        # [:N, :K] block into the target (see _fwd_padded)
+        key = key + ("pad",)
+        Kp, Np = _p64(K), _p64(N)
+
+        def padded(o, c, sp):
+            dyp = _pad2(dy2, M, Np)
+            xp = _pad2(x2, M, Kp)
+            op = torch.zeros(Np, Kp, dtype=torch.float32, device=dy2.device)
+            g.gemm_tn_acc(dyp, xp, op, c, sp)
+            o.add_(op[:N, :K])
+        scratch = torch.zeros_like(out) if key not in _cv._choices else None
+        cands = [(("hip", c, sp), (lambda c=c, sp=sp: padded(scratch, c, sp)))
                  for c, sp in _cv._tn_cfgs(torch.float32 if f32 else torch.bfloat16)]
     cands.append((("blas32", 0, 0), lambda: blas32(scratch)))
     cands.append((("blas", 0, 0), lambda: blas(scratch)))
@@ -159,6 +260,8 @@ def _wgrad_into(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor) -> None:
         blas(out)
     elif ch[0] == "blas32":
         blas32(out)
+    elif padded is not None:
+        padded(out, ch[1], ch[2])
     else:
         g.gemm_tn_acc(dy2, x2, out, ch[1], ch[2])
 

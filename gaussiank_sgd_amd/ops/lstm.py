@@ -41,6 +41,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import load, require_native
+from .linear import _dgrad as _lin_dgrad
+from .linear import _fwd as _lin_fwd
 from .linear import _target, _wgrad_into, bias_grad_acc_
 
 
@@ -190,8 +192,15 @@ class _LSTMLayerFn(torch.autograd.Function):
         wih = shadows[0] if shadows[0] is not None else w_ih.detach().to(cd)
         whh = shadows[1] if shadows[1] is not None else w_hh.detach().to(cd)
         x2 = x.reshape(T * B, -1).to(cd).contiguous()
-        bias = (b_ih.detach().float() + b_hh.detach().float()).to(cd)
-        xg = torch.addmm(bias, x2, wih.t()).view(T, B, 4 * H)
+        if fast:
+            # the autotuned GEMM of ops/linear.py: HIP kernels on zero-padded
+            # operands (H = 1500 is not a multiple of 64) or hipBLASLt, whichever
+            # is faster for the shape; the bias in its epilogue
+            bias32 = (b_ih.detach().float() + b_hh.detach().float()).contiguous()
+            xg = _lin_fwd(x2, wih.contiguous(), bias32).contiguous().view(T, B, 4 * H)
+        else:
+            bias = (b_ih.detach().float() + b_hh.detach().float()).to(cd)
+            xg = torch.addmm(bias, x2, wih.t()).view(T, B, 4 * H)
         out = torch.empty(T, B, H, dtype=cd, device=dev)
         c_all = torch.empty(T + 1, B, H, dtype=torch.float32, device=dev)
         c_all[0].copy_(c0)
@@ -287,7 +296,9 @@ class _LSTMLayerFn(torch.autograd.Function):
                 dh_rec = torch.mm(dG[t], whh)
         dG2 = dG.view(T * B, 4 * H)
         xdt, hdt, cdt, wdt = ctx.dtypes
-        dx = torch.mm(dG2, wih).view(ctx.in_shape) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = (_lin_dgrad(dG2, wih.contiguous()) if fast else torch.mm(dG2, wih)).view(ctx.in_shape)
         dh0 = dh_rec.to(hdt) if need_dh0 else None
         dc0 = dc if ctx.needs_input_grad[2] else None
         grads: List[Optional[torch.Tensor]] = [None, None, None, None]

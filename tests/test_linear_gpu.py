@@ -253,3 +253,37 @@ def test_fastlinear_f32_autotuned_and_direct_arena():
         assert p.grad is not None, n
         err = (p.grad - q.grad).abs().max().item()
         assert err <= 1e-5 * q.grad.abs().max().item() + 1e-6, (n, err)
+
+
+@pytest.mark.parametrize("M,K,N", [(448, 1500, 1000), (130, 200, 106), (64, 1536, 10000)])
+@pytest.mark.parametrize("bias", [True, False])
+def test_fp32_linear_padded_operands_vs_fp64(hip_only, M, K, N, bias):
+    """fp32 FastLinear with K / N not multiples of 64 (the LSTM's 1500-unit
+    layers and 10k softmax): the HIP kernels on zero-padded operand copies
+    (forward, grad-input, grad-weight into a padded scratch) against fp64."""
+    from gaussiank_sgd_amd.ops import conv1x1
+    from gaussiank_sgd_amd.ops.linear import FastLinear
+    torch.manual_seed(M + K + N)
+    m = FastLinear(K, N, bias=bias).cuda()
+    x = torch.randn(M, K, device="cuda", requires_grad=True)
+    y = m(x)
+    assert y.shape == (M, N)
+    # the padded HIP path ran (its tuner keys carry "pad")
+    assert any(k[0] == "lin_fwd" and k[-1] == "pad" for k in conv1x1._choices)
+    gy = torch.randn(M, N, device="cuda")
+    (y * gy).sum().backward()
+    assert any(k[0] == "lin_dgrad" and k[-1] == "pad" for k in conv1x1._choices)
+    assert any(k[0] == "lin_wgrad" and k[-1] == "pad" for k in conv1x1._choices)
+    xd = x.detach().double().requires_grad_(True)
+    wd = m.weight.detach().double().requires_grad_(True)
+    bd = m.bias.detach().double().requires_grad_(True) if bias else None
+    yd = F.linear(xd, wd, bd)
+    (yd * gy.double()).sum().backward()
+
+    def close(a, b):
+        return (a.double() - b).abs().max().item() <= 2e-5 * b.abs().max().item() + 1e-6
+    assert close(y.detach(), yd.detach())
+    assert close(x.grad, xd.grad)
+    assert close(m.weight.grad, wd.grad)
+    if bias:
+        assert close(m.bias.grad, bd.grad)
