@@ -37,7 +37,8 @@ def ssgd(dnn, dataset, data_dir, nworkers, lr, batch_size, nsteps_update, max_ep
          num_steps, compressor, density, threshold, gradient_path=None, amp=None, channels_last=False,
          density_warmup=True, deterministic=False, max_iters=None, compress_single_rank=False, saved_dir=".",
          bf16_shadow=True, momentum_correction=False, k_cap_factor=None, overlap=True, dump_grad_every=None,
-         metrics_dir=None, f32_matmul=None, train_samples=None, checkpoint_every=2, save_final=False):
+         metrics_dir=None, f32_matmul=None, train_samples=None, checkpoint_every=2, save_final=False,
+         hip_graph=False):
     rank = hvd.rank()
     device = "cpu"
     if torch.cuda.is_available():
@@ -131,6 +132,19 @@ def ssgd(dnn, dataset, data_dir, nworkers, lr, batch_size, nsteps_update, max_ep
     times = []
     logger.info("max_epochs: %d", max_epochs)
     display = 40 if iters_per_epoch > 40 else max(1, iters_per_epoch - 1)
+    # --hip-graph: the whole step (forward, backward, compression, update)
+    # replayed as one HIP graph, as bench.py's reference-batch phases do on one
+    # GPU (train/graph.py GraphedStep: lr schedule, compressor seeds, dropout
+    # and the density schedule stay live); one process, no gradient
+    # accumulation, no recurrent state carried across steps
+    graphed = None
+    if hip_graph:
+        if trainer.is_cuda and nworkers == 1 and nsteps_update == 1 and dnn not in ("lstm", "lstman4"):
+            from .graph import GraphedStep
+            graphed = GraphedStep(trainer, optimizer, norm_clip)
+        else:
+            logger.warning("--hip-graph needs one GPU process, --nsteps-update 1 and a non-recurrent model: "
+                           "running eagerly")
     done = 0
     # a resumed run continues where the checkpoint stopped (max_epochs is the
     # total); the reference re-ran max_epochs epochs from wherever it resumed
@@ -142,17 +156,20 @@ def ssgd(dnn, dataset, data_dir, nworkers, lr, batch_size, nsteps_update, max_ep
             hidden = trainer.net.init_hidden()
         for i in range(first_i if epoch == start_epoch else 0, iters_per_epoch):
             s = time.time()
-            optimizer.zero_grad()
-            for j in range(nsteps_update):
-                optimizer.local = j < nsteps_update - 1 and nsteps_update > 1
-                if dnn == "lstm":
-                    _, hidden = trainer.train(1, hidden=hidden)
-                else:
-                    trainer.train(1)
-            if norm_clip is not None:
-                optimizer.synchronize()
-                optimizer.clip_grad_norm_(norm_clip)
-            trainer.update_model()
+            if graphed is not None:
+                graphed()
+            else:
+                optimizer.zero_grad()
+                for j in range(nsteps_update):
+                    optimizer.local = j < nsteps_update - 1 and nsteps_update > 1
+                    if dnn == "lstm":
+                        _, hidden = trainer.train(1, hidden=hidden)
+                    else:
+                        trainer.train(1)
+                if norm_clip is not None:
+                    optimizer.synchronize()
+                    optimizer.clip_grad_norm_(norm_clip)
+                trainer.update_model()
             times.append(time.time() - s)
             if i % display == 0 and i > 0:
                 if trainer.is_cuda:
@@ -244,6 +261,9 @@ def build_parser():
                    help="synthetic epoch length in samples (default: the dataset's real size)")
     p.add_argument("--checkpoint-every", type=int, default=2,
                    help="save a checkpoint every N trainer epochs (reference: 2)")
+    p.add_argument("--hip-graph", action="store_true",
+                   help="replay the whole training step as one HIP graph (one GPU process, non-recurrent models; "
+                        "what bench.py does for its reference-batch phases)")
     p.add_argument("--save-final", action="store_true",
                    help="every rank saves its checkpoint at the end of the run (resume with --pretrain)")
     return p
@@ -282,7 +302,7 @@ def main(argv=None):
                 bf16_shadow=not args.no_bf16_shadow, momentum_correction=args.momentum_correction,
                 k_cap_factor=args.k_cap_factor, overlap=not args.no_overlap, dump_grad_every=args.dump_grad_every,
                 metrics_dir=relative_path, f32_matmul=args.f32_matmul, train_samples=args.train_samples,
-                checkpoint_every=args.checkpoint_every, save_final=args.save_final)
+                checkpoint_every=args.checkpoint_every, save_final=args.save_final, hip_graph=args.hip_graph)
 
 
 if __name__ == "__main__":

@@ -128,3 +128,23 @@ def test_graph_attention_dropout_changes_per_replay():
         outs[p] = res
     assert torch.equal(outs[0.0][0], outs[0.0][1])
     assert not torch.equal(outs[0.1][0], outs[0.1][1])
+
+
+def test_dist_trainer_hip_graph_cli(tmp_path):
+    """``dist_trainer --hip-graph`` (one GPU process): the whole step replays
+    as a HIP graph -- the execution bench.py times for its reference-batch
+    phases -- through an epoch boundary of the density warm-up (recapture)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root)
+    cmd = [sys.executable, "-m", "gaussiank_sgd_amd.train.dist_trainer", "--dnn", "resnet20", "--dataset", "cifar10",
+           "--batch-size", "32", "--density", "0.001", "--compressor", "gaussian", "--max-epochs", "2",
+           "--train-samples", "640", "--compress-single-rank", "--hip-graph", "--logdir-root", str(tmp_path / "logs"),
+           "--saved-dir", str(tmp_path), "--data-dir", str(tmp_path / "nodata")]
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=600, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "Speed:" in r.stderr
+    assert "running eagerly" not in r.stderr
+    assert "Average number of selected gradients" in r.stderr
