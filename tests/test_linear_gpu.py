@@ -255,7 +255,7 @@ def test_fastlinear_f32_autotuned_and_direct_arena():
         assert err <= 1e-5 * q.grad.abs().max().item() + 1e-6, (n, err)
 
 
-@pytest.mark.parametrize("M,K,N", [(448, 1500, 1000), (130, 200, 106), (64, 1536, 10000)])
+@pytest.mark.parametrize("M,K,N", [(448, 1500, 1000), (130, 200, 104), (64, 1536, 10000)])
 @pytest.mark.parametrize("bias", [True, False])
 def test_fp32_linear_padded_operands_vs_fp64(hip_only, M, K, N, bias):
     """fp32 FastLinear with K / N not multiples of 64 (the LSTM's 1500-unit
