@@ -715,11 +715,28 @@ class _FastConvFn(torch.autograd.Function):
                     gparam = out.to(ctx.param_dtype)
         gbias = None
         if ctx.has_bias and ctx.needs_input_grad[6]:
-            db = (plink.materialize() if lz is not None else dy).sum(dim=(0, 2, 3), dtype=torch.float32)
+            src = plink.materialize() if lz is not None else dy
             bs = ctx.bias_sink
+            gv = getattr(bs, "grad_view", None) if bs is not None else None
+            if src.is_contiguous(memory_format=_CL):
+                # one HIP column pass over the [N*H*W, C] rows of the channels-last
+                # gradient (linear.hip colsum_acc), added straight into the arena
+                # view when there is one (torch's NHWC sum(0, 2, 3) reduction took
+                # 22.6 us per VGG-16 bs512 layer, profiles/r06_vgg16_bs512_fp32_kernel_stats.csv)
+                from .linear import bias_grad_acc_
+                if gv is not None and gv.is_contiguous():
+                    bs.check()
+                    bias_grad_acc_(gv, _rows(src))
+                    bs = None
+                    db = None
+                else:
+                    db = torch.zeros(src.shape[1], dtype=torch.float32, device=src.device)
+                    bias_grad_acc_(db, _rows(src))
+            else:
+                db = src.sum(dim=(0, 2, 3), dtype=torch.float32)
             if bs is not None:
                 bs(db)          # into the optimizer's fp32 arena (shadow path)
-            else:
+            elif db is not None:
                 gbias = db
         if plink is not None:
             plink.clear()
