@@ -139,7 +139,23 @@ class BertForMaskedLM(nn.Module):
         if masked_positions is not None:
             x = x.gather(1, masked_positions.unsqueeze(-1).expand(-1, -1, x.shape[-1]))
         h = self.mlm_ln(self.mlm_dense(x, act="gelu"))
-        return F.linear(h, self.word_embeddings.weight, self.mlm_bias)
+        return vocab_projection(h, self.word_embeddings.weight, self.mlm_bias)
+
+
+def vocab_projection(h: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
+    """Logits = h W_emb^T + b with the (tied) word-embedding matrix.  fp32 on
+    the GPU (the headline precision): the autotuned GEMMs of ops/linear.py,
+    which offer the HIP kernels on zero-padded operands for the 30,522-word
+    vocabulary (not a multiple of 64) against hipBLASLt; the gradients flow
+    to the tied parameter through autograd as with F.linear."""
+    dev = h.device.type
+    if (h.is_cuda and h.dtype == torch.float32 and weight.dtype == torch.float32 and
+            not torch.is_autocast_enabled(dev)):
+        from ..ops import load
+        from ..ops.linear import _LinearFn
+        if load():
+            return _LinearFn.apply(h, weight, None, None, bias, None, False, None, torch.float32)
+    return F.linear(h, weight, bias)
 
 
 class MaskedLMLoss(nn.Module):

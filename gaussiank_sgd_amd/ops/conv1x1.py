@@ -50,6 +50,8 @@ _choices: Dict[tuple, tuple] = {}
 # code this package owns; 0 = fastest wins)
 _OWN = ("hip", "w3", "mat", "wino")
 _GK_MARGIN = float(os.environ.get("GKSGD_GK_MARGIN", "0.05"))
+# convolution bias gradients through the fused column pass (GKSGD_CONV_BIAS_COLSUM=0: torch's reduction)
+_BIAS_COLSUM = os.environ.get("GKSGD_CONV_BIAS_COLSUM", "1") != "0"
 _timings: Dict[tuple, list] = {}      # key -> [(tag, ms or error)] of the search
 # fp32 3x3 stride-1 forward / grad-input: Winograd F(2x2, 3x3) candidates
 # (winograd.hip, 2.25x fewer MFMA FLOPs); GKSGD_WINO=0 leaves them out.  Their
@@ -718,7 +720,7 @@ class _FastConvFn(torch.autograd.Function):
             src = plink.materialize() if lz is not None else dy
             bs = ctx.bias_sink
             gv = getattr(bs, "grad_view", None) if bs is not None else None
-            if src.is_contiguous(memory_format=_CL):
+            if src.is_contiguous(memory_format=_CL) and _BIAS_COLSUM:
                 # one HIP column pass over the [N*H*W, C] rows of the channels-last
                 # gradient (linear.hip colsum_acc), added straight into the arena
                 # view when there is one (torch's NHWC sum(0, 2, 3) reduction took
