@@ -308,8 +308,6 @@ def run_phase(args, ph: Phase, steps: int, warmup: int, P: int, graph: Optional[
             marks.append((ev, e2))
 
     graph = args.graph if graph is None else graph
-    if graph and lstm:
-        raise SystemExit("bench.py --graph: the LSTM carries hidden state across steps; not graph-capturable")
     run = step
     if graph:
         # whole-step HIP graph: capture after the eager warm-up, replay in the timed loop
@@ -726,7 +724,7 @@ def main() -> int:
         # the reference batch is launch-bound: the whole step replays as one HIP
         # graph (train/graph.py) by default on one GPU; at N > 1 eager, with the
         # side-stream overlap (--ref-graph on|off overrides)
-        ref_graph = (P == 1 and args.model != "lstm") if args.ref_graph == "auto" else args.ref_graph == "on"
+        ref_graph = (P == 1) if args.ref_graph == "auto" else args.ref_graph == "on"
 
         def ref_sparse(holder):
             i = timed(holder, tag, amp, False, args.threshold, ref_bs, rsteps, rwarm, graph=ref_graph)
@@ -777,8 +775,7 @@ def main() -> int:
 
                 # the reference batch replays as one HIP graph on one GPU, as the
                 # headline model's reference-batch phase (--ref-graph)
-                rgraph = (P == 1 and m != "lstm") if args.ref_graph == "auto" else (args.ref_graph == "on"
-                                                                                    and m != "lstm")
+                rgraph = (P == 1) if args.ref_graph == "auto" else args.ref_graph == "on"
 
                 def model_ref_phase(holder, m=m, rb=rb, mthr=mthr, msteps=msteps, mwarm=mwarm, tag=tag, rgraph=rgraph):
                     i = timed(holder, tag, amp, False, mthr, rb, msteps, mwarm, graph=rgraph, model=m)

@@ -135,16 +135,16 @@ def ssgd(dnn, dataset, data_dir, nworkers, lr, batch_size, nsteps_update, max_ep
     # --hip-graph: the whole step (forward, backward, compression, update)
     # replayed as one HIP graph, as bench.py's reference-batch phases do on one
     # GPU (train/graph.py GraphedStep: lr schedule, compressor seeds, dropout
-    # and the density schedule stay live); one process, no gradient
-    # accumulation, no recurrent state carried across steps
+    # and the density schedule stay live; the LSTM's hidden state is carried in
+    # static buffers); one process, no gradient accumulation
     graphed = None
     if hip_graph:
-        if trainer.is_cuda and nworkers == 1 and nsteps_update == 1 and dnn not in ("lstm", "lstman4"):
+        if trainer.is_cuda and nworkers == 1 and nsteps_update == 1 and dnn != "lstman4":
             from .graph import GraphedStep
             graphed = GraphedStep(trainer, optimizer, norm_clip)
         else:
-            logger.warning("--hip-graph needs one GPU process, --nsteps-update 1 and a non-recurrent model: "
-                           "running eagerly")
+            logger.warning("--hip-graph needs one GPU process, --nsteps-update 1 and a fixed-shape model "
+                           "(not lstman4): running eagerly")
     done = 0
     # a resumed run continues where the checkpoint stopped (max_epochs is the
     # total); the reference re-ran max_epochs epochs from wherever it resumed
@@ -154,6 +154,8 @@ def ssgd(dnn, dataset, data_dir, nworkers, lr, batch_size, nsteps_update, max_ep
         hidden = None
         if dnn == "lstm":
             hidden = trainer.net.init_hidden()
+            if graphed is not None:
+                graphed.reset_hidden()     # the reference re-initialises the state every epoch
         for i in range(first_i if epoch == start_epoch else 0, iters_per_epoch):
             s = time.time()
             if graphed is not None:

@@ -25,8 +25,11 @@ the branch edges from the host), the same step captured on one stream at
 1.43 ms (eager: 4.9 ms; scripts/gpurun/graph_probe.sh, profiles/r02_graph_probe.txt).
 Overlap buys nothing in a replay whose launches are already on the device.
 ``GKSGD_GRAPH_COMM_STREAM=1`` keeps the side stream.
-Not for recurrent models that carry hidden state across steps (bench.py
-refuses ``--graph`` for the LSTM).
+Recurrent models (the PTB LSTM) carry their hidden state across steps in
+static buffers: the captured step reads them as the initial state and
+copies the final state back into them (``reset_hidden()`` zeroes them, e.g.
+at an epoch start as the reference re-initialises its hidden state,
+dist_trainer.py:64-67).
 Requirements: every op of the step is stream-ordered without host syncs
 (true for the DistributedOptimizer / fused kernels of this package) and the
 autotuned convolution choices are cached by the eager warm-up steps.
@@ -64,6 +67,10 @@ class GraphedStep:
         d = trainer.data_iter()
         self.x = d[0].clone()
         self.y = _clone(d[1])
+        # recurrent state (LSTM): static (h, c) the captured step reads and rewrites
+        self.hidden = None
+        if getattr(trainer, "dnn", None) == "lstm":
+            self.hidden = tuple(v.detach().clone() for v in trainer.net.init_hidden(self.x.shape[1]))
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.lr0 = None            # lr baked into the captured update
         self.density = None
@@ -78,12 +85,31 @@ class GraphedStep:
 
     def _body(self) -> None:
         t, opt = self.trainer, self.opt
+        t._graph_body = True    # epoch boundaries / log lines are this class's job (no host syncs in a capture)
+        try:
+            self._step(t, opt)
+        finally:
+            t._graph_body = False
+
+    def _step(self, t, opt) -> None:
         opt.zero_grad()
-        t.train(1, data=(self.x, self.y))
+        if self.hidden is not None:
+            _, new = t.train(1, data=(self.x, self.y), hidden=self.hidden)
+            with torch.no_grad():        # after the backward: the saved initial state is consumed
+                for dst, src in zip(self.hidden, new):
+                    dst.copy_(src.detach())
+        else:
+            t.train(1, data=(self.x, self.y))
         if self.clip is not None:
             opt.synchronize()
             opt.clip_grad_norm_(self.clip)
         t.update_model()
+
+    def reset_hidden(self) -> None:
+        """Zero the carried recurrent state (stream-ordered; no recapture)."""
+        if self.hidden is not None:
+            for v in self.hidden:
+                v.zero_()
 
     def _density(self):
         f = getattr(self.opt, "get_current_density", None)

@@ -197,6 +197,7 @@ class DLTrainer:
         self._acc_acc = None
         self._acc_n = 0
         self.display = 40
+        self._graph_body = False     # set while train/graph.py runs / captures its step body
         # per-step weight re-layouts of the convolutions, rebuilt in one batched
         # launch at the start of every step (ops/weight_prep.py)
         from ..ops.weight_prep import WeightPrep
@@ -392,7 +393,10 @@ class DLTrainer:
         loss_sum = None
         for _ in range(num_of_iters):
             self.adjust_learning_rate(self.train_epoch, self.optimizer)
-            if self.train_iter % self.num_batches_per_epoch == 0 and self.train_iter > 0:
+            # (a HIP-graph step, train/graph.py, runs the epoch-boundary logic --
+            # eval, checkpoint, host syncs -- itself, outside its captured body)
+            if self.train_iter % self.num_batches_per_epoch == 0 and self.train_iter > 0 and \
+                    not self._graph_body:
                 self._on_epoch_boundary()
             ss = time.time()
             d = data if data is not None else self.data_iter()
@@ -420,7 +424,7 @@ class DLTrainer:
             self.train_iter += 1
         self._loss_acc = loss_sum / num_of_iters
         self.timer += time.time() - s
-        if self.train_iter % self.display == 0:
+        if self.train_iter % self.display == 0 and not self._graph_body:
             self.loss = float(self._loss_acc)
             logger.warning("[%3d][%5d/%5d][rank:%d] loss: %.3f, average forward (%f) and backward (%f) time: %f, "
                            "iotime: %f " % (self.train_epoch, self.train_iter, self.num_batches_per_epoch, self.rank,

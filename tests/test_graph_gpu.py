@@ -148,3 +148,38 @@ def test_dist_trainer_hip_graph_cli(tmp_path):
     assert "Speed:" in r.stderr
     assert "running eagerly" not in r.stderr
     assert "Average number of selected gradients" in r.stderr
+
+
+def test_graph_lstm_carries_hidden_state():
+    """The PTB LSTM (BASELINE config 4) replays as a HIP graph: its hidden
+    state lives in static buffers the captured step reads and rewrites, so
+    consecutive replays continue the sequence; reset_hidden() zeroes it."""
+    from gaussiank_sgd_amd.compression import compressors
+    from gaussiank_sgd_amd.parallel import comm
+    from gaussiank_sgd_amd.parallel.distributed_optimizer import DistributedOptimizer
+    from gaussiank_sgd_amd.train import DLTrainer
+    from gaussiank_sgd_amd.train.graph import GraphedStep
+    comm.init()
+    torch.manual_seed(0)
+    t = DLTrainer(0, 1, dnn="lstm", dataset="ptb", batch_size=8, lr=1.0, device="cuda:0", data_pool=4)
+    opt = DistributedOptimizer(t.optimizer, named_parameters=t.net.named_parameters(),
+                               compression=compressors["gaussian"], is_sparse=True, density=0.01,
+                               compress_single_rank=True, density_warmup=False, threshold=524288000)
+    t.update_optimizer(opt)
+    g = GraphedStep(t, opt, clip=0.25)
+    assert g.hidden is not None
+    w0 = opt.arena.weights.clone()
+    g()
+    h1 = [v.clone() for v in g.hidden]
+    g()
+    torch.cuda.synchronize()
+    assert g.captures == 1 and g.replays == 2
+    assert not torch.equal(h1[0], g.hidden[0]), "the replay did not advance the hidden state"
+    assert float(h1[0].abs().sum()) > 0
+    assert not torch.equal(w0, opt.arena.weights)
+    assert t.current_loss() == t.current_loss()
+    g.reset_hidden()
+    assert all(float(v.abs().sum()) == 0 for v in g.hidden)
+    g()
+    torch.cuda.synchronize()
+    assert float(g.hidden[0].abs().sum()) > 0
