@@ -433,7 +433,11 @@ class DLTrainer:
                                             self.iotime / self.display))
             self.timer = self.iotime = self.forwardtime = self.backwardtime = 0.0
         if self.dnn == "lstm":
-            return num_of_iters, hidden
+            # detached (the next call repackages it anyway): a caller holding the
+            # state must not keep this step's autograd graph -- and its
+            # AccumulateGrad nodes -- alive (a HIP-graph capture on another
+            # stream refuses stale AccumulateGrad nodes)
+            return num_of_iters, repackage_hidden(hidden)
         return num_of_iters
 
     def current_loss(self) -> float:

@@ -6,7 +6,7 @@ set -u
 D=gpurun_out/r6c8
 mkdir -p $D
 export TMPDIR=/tmp
-timeout -k 10 900 python3 -u -m pytest tests/test_graph_gpu.py tests/test_lstm_gpu.py -x -q --timeout 600 --timeout-method thread > $D/tests.log 2>&1
+timeout -k 10 900 python3 -u -m pytest tests/test_graph_gpu.py -x -q --timeout 600 --timeout-method thread > $D/tests.log 2>&1
 rc=$?; echo tests_rc=$rc; tail -3 $D/tests.log; [ $rc -eq 0 ] || exit $rc
 B="python3 bench.py --gpus 1 --model lstm --steps 20 --warmup 5 --model-phases none --no-native-phase --no-bf16-phase"
 timeout -k 10 300 $B --json-out $D/lstm_graph.json > $D/lstm_graph.log 2>&1 || exit 1

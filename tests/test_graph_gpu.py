@@ -165,7 +165,17 @@ def test_graph_lstm_carries_hidden_state():
     opt = DistributedOptimizer(t.optimizer, named_parameters=t.net.named_parameters(),
                                compression=compressors["gaussian"], is_sparse=True, density=0.01,
                                compress_single_rank=True, density_warmup=False, threshold=524288000)
+    from gaussiank_sgd_amd.parallel import install_direct_grads
+    install_direct_grads(t.net, opt)
     t.update_optimizer(opt)
+    # eager steps first, the caller keeping the returned state (as bench.py's
+    # warm-up does): no autograd graph of theirs may survive into the capture
+    hidden = None
+    for _ in range(2):
+        opt.zero_grad()
+        _, hidden = t.train(1, hidden=hidden)
+        t.update_model()
+    assert hidden[0].grad_fn is None
     g = GraphedStep(t, opt, clip=0.25)
     assert g.hidden is not None
     w0 = opt.arena.weights.clone()
