@@ -958,6 +958,32 @@ int64_t stem_f32_fwd(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at:
                               cur_stream(x));
 }
 
+// bf16x6 stem forward: as stem_f32_fwd, plus wp3 = bf16 workspace of
+// stem_f32x6_wplanes() elements for the split weight planes
+int64_t stem_f32x6_wplanes() { return gk::stem_f32x6_wplanes(); }
+
+int64_t stem_f32x6_fwd(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tensor> stats, at::Tensor wp3) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.dim() == 4 && x.size(1) == 3 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast) && gk::stem_f32_supported((int)x.size(2), (int)x.size(3)) &&
+                  reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "stem_f32x6_fwd: x must be a channels-last fp32 [N, 3, 224, 224] GPU tensor (16-byte aligned)");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.dim() == 4 && w.size(0) == 64 && w.size(1) == 3 &&
+                  w.size(2) == 7 && w.size(3) == 7, "stem_f32x6_fwd: w must be fp32 [64, 3, 7, 7]");
+  const int64_t N = x.size(0);
+  TORCH_CHECK(y.is_cuda() && y.scalar_type() == at::kFloat && y.dim() == 4 && y.size(0) == N && y.size(1) == 64 &&
+                  y.size(2) == 112 && y.size(3) == 112 && y.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "stem_f32x6_fwd: y must be a channels-last fp32 [N, 64, 112, 112] GPU tensor");
+  TORCH_CHECK(wp3.is_cuda() && wp3.scalar_type() == at::kBFloat16 && wp3.is_contiguous() &&
+                  wp3.numel() >= gk::stem_f32x6_wplanes() && reinterpret_cast<uintptr_t>(wp3.data_ptr()) % 16 == 0,
+              "stem_f32x6_fwd: wp3 must be a contiguous bf16 GPU tensor of stem_f32x6_wplanes() elements");
+  int rows = 0;
+  float* sp = stats_ptr(stats, 64, &rows);
+  c10::DeviceGuard guard(x.device());
+  return gk::stem_f32x6_forward(x.data_ptr<float>(), (int)N, (int)x.size(2), (int)x.size(3), w.data_ptr<float>(),
+                                w.stride(0), w.stride(1), w.stride(2), w.stride(3),
+                                static_cast<uint16_t*>(wp3.data_ptr()), y.data_ptr<float>(), sp, rows, cur_stream(x));
+}
+
 int64_t stem_f32_wgrad_ws(int64_t N) { return (int64_t)gk::stem_f32_wgrad_blocks((int)N) * 64 * 148; }
 
 void stem_f32_wgrad(at::Tensor x, at::Tensor dy, at::Tensor out, at::Tensor part) {
@@ -1894,6 +1920,8 @@ TORCH_LIBRARY(gksgd, m) {
   m.def("stem_wgrad(Tensor x, Tensor dy, Tensor(a!) out, Tensor(b!) part) -> ()");
   m.def("stem_f32_supported(int H, int W) -> bool", [](int64_t H, int64_t W) { return gk::stem_f32_supported((int)H, (int)W); });
   m.def("stem_f32_fwd(Tensor x, Tensor w, Tensor(a!) y, Tensor(b!)? stats=None) -> int");
+  m.def("stem_f32x6_wplanes() -> int", &stem_f32x6_wplanes);
+  m.def("stem_f32x6_fwd(Tensor x, Tensor w, Tensor(a!) y, Tensor(b!)? stats, Tensor(c!) wp3) -> int");
   m.def("stem_f32_wgrad_ws(int N) -> int", &stem_f32_wgrad_ws);
   m.def("stem_f32_wgrad(Tensor x, Tensor dy, Tensor(a!) out, Tensor(b!) part) -> ()");
   m.def("wgrad3_supported(int H, int W, int C, int K) -> bool", [](int64_t H, int64_t W, int64_t C, int64_t K) {
@@ -2016,6 +2044,7 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("stem_fwd", &stem_fwd);
   m.impl("stem_wgrad", &stem_wgrad);
   m.impl("stem_f32_fwd", &stem_f32_fwd);
+  m.impl("stem_f32x6_fwd", &stem_f32x6_fwd);
   m.impl("stem_f32_wgrad", &stem_f32_wgrad);
   m.impl("bn_relu_pool_forward", &bn_relu_pool_forward);
   m.impl("bn_relu_pool_backward", &bn_relu_pool_backward);

@@ -393,6 +393,11 @@ int conv_tn_acc(const void* G, const void* X, const void* zero, int H, int W, in
 // (strided like w) through per-block partials (stem_f32_wgrad_blocks(N) x 64 x 148).
 bool stem_f32_supported(int H, int W);
 int stem_f32_wgrad_blocks(int N);
+// bf16x6 stem forward (fp32-accurate): wp3 = a workspace of stem_f32x6_wplanes()
+// bf16 elements that receives the three split planes of w
+int stem_f32x6_wplanes();
+int stem_f32x6_forward(const float* x, int N, int H, int W, const float* w, int64_t s0, int64_t s1, int64_t s2,
+                       int64_t s3, uint16_t* wp3, float* y, float* stats, int stats_rows, hipStream_t stream);
 int stem_f32_forward(const float* x, int N, int H, int W, const float* w, int64_t s0, int64_t s1, int64_t s2,
                      int64_t s3, float* y, float* stats, int stats_rows, hipStream_t stream);
 void stem_f32_wgrad(const float* x, const float* dy, int N, int H, int W, float* part, float* out, int64_t s0,

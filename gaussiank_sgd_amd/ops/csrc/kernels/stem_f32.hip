@@ -27,6 +27,8 @@
 //   (deterministic) into the (arena) gradient.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "common.h"
 #include "gk_kernels.h"
 #include "mfma_util.h"
@@ -262,6 +264,161 @@ stem_f32_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy,
   }
 }
 
+// ---------------------------------------------------------------------------
+// bf16x6 forward (fp32-accurate on the bf16 matrix cores, as gemm_kern.h X6):
+// the weights are split ONCE per call into three exact bf16 planes [3][64][160]
+// (stem_w_split3_kernel; taps >= 147 zero), the band's activations are split
+// in registers (mfma_util.h split3x8), and the six part products of order
+// <= 2 are accumulated in fp32, smallest first.  K = 160 taps = five 32-deep
+// v_mfma_f32_16x16x32_bf16 steps (6 x 16 cycles each) against 37 4-deep fp32
+// steps (32 cycles each): 2.5x fewer matrix-pipe cycles.  Same band walk,
+// output layout and statistics epilogue as stem_f32_fwd_kernel; the weight
+// fragments come straight from global memory (61 KiB, L2-resident), so LDS
+// holds the input band only.
+// ---------------------------------------------------------------------------
+constexpr int kXK = 160;                  // taps padded to five 32-deep steps
+constexpr int kXPlane = 64 * kXK;         // elements of one weight plane
+
+__device__ __forceinline__ uint16_t bf16_rne(float v) { return (uint16_t)(pack_bf16x2(v, 0.f) & 0xffffu); }
+
+__global__ void __launch_bounds__(256) stem_w_split3_kernel(const float* __restrict__ w, int64_t s0, int64_t s1,
+                                                            int64_t s2, int64_t s3, uint16_t* __restrict__ wp3) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= kXPlane) return;
+  const int n = i / kXK, k = i - n * kXK;
+  float v = 0.f;
+  if (k < kFK) {
+    const int kh = k / 21, r = k - kh * 21, kw = r / 3, c = r - kw * 3;
+    v = w[n * s0 + c * s1 + kh * s2 + kw * s3];
+  }
+  const uint16_t hi = bf16_rne(v);
+  const float r1 = v - __uint_as_float((uint32_t)hi << 16);
+  const uint16_t mid = bf16_rne(r1);
+  const float r2 = r1 - __uint_as_float((uint32_t)mid << 16);
+  wp3[i] = hi;
+  wp3[kXPlane + i] = mid;
+  wp3[2 * kXPlane + i] = bf16_rne(r2);
+}
+
+// OCC: waves per SIMD the register budget is set for (1: 179 VGPR + 112 AGPR,
+// no spills; 2: 256 registers with a 40-byte spill) -- GKSGD_STEM_X6_OCC picks
+template <int OCC>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC)))
+stem_f32x6_fwd_kernel(const float* __restrict__ x, const uint16_t* __restrict__ wp3, float* __restrict__ y,
+                      StemF32Geo g, float* __restrict__ stats, int64_t stats_ld) {
+  extern __shared__ __attribute__((aligned(16))) float fl[];
+  float* band = fl;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fi = lane & 15, fq = lane >> 4;
+  float ssum[4][4], ssq[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ssum[a][r] = ssq[a][r] = 0.f;
+  const int bpi = g.OH / kFR;
+  for (int b = blockIdx.x; b < g.nbands; b += gridDim.x) {
+    const int n = b / bpi, orow0 = (b - n * bpi) * kFR;
+    __syncthreads();   // the previous band's reads are done
+    load_band(band, x, g, n, orow0);
+    __syncthreads();
+    f32x4 acc[7][4];
+#pragma unroll
+    for (int t = 0; t < 7; ++t)
+#pragma unroll
+      for (int a = 0; a < 4; ++a) acc[t][a] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int pb[7];
+#pragma unroll
+    for (int t = 0; t < 7; ++t) pb[t] = (2 * wave * kFPW + 2 * (t * 16 + fi)) * 3;
+    for (int c = 0; c < kXK / 32; ++c) {
+      // lane (fi, fq): taps 32 c + 8 fq + e, e = 0..7, of output channel a * 16 + fi
+      // (first operand) and of pixel t * 16 + fi (second operand)
+      const int k0 = 32 * c + 8 * fq;
+      bf16x8 wh[4], wm[4], wl[4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const uint16_t* q = wp3 + (a * 16 + fi) * kXK + k0;
+        wh[a] = *reinterpret_cast<const bf16x8*>(q);
+        wm[a] = *reinterpret_cast<const bf16x8*>(q + kXPlane);
+        wl[a] = *reinterpret_cast<const bf16x8*>(q + 2 * kXPlane);
+      }
+      int ko[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ko[e] = tap_off(k0 + e);
+#pragma unroll
+      for (int t = 0; t < 7; ++t) {
+        f32x4 x0, x1;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          x0[e] = band[pb[t] + ko[e]];
+          x1[e] = band[pb[t] + ko[4 + e]];
+        }
+        bf16x8 xh, xm, xl;
+        split3x8(x0, x1, xh, xm, xl);
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          f32x4 cc = acc[t][a];
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl[a], xh, cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[a], xl, cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm[a], xm, cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm[a], xh, cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[a], xm, cc, 0, 0, 0);
+          acc[t][a] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[a], xh, cc, 0, 0, 0);
+        }
+      }
+    }
+    // lane: channels a * 16 + 4 fq + r of pixel t * 16 + fi of output row orow0 + wave
+    const int orow = orow0 + wave;
+#pragma unroll
+    for (int t = 0; t < 7; ++t) {
+      const int ocol = t * 16 + fi;
+      float* yp = y + (((int64_t)n * g.OH + orow) * g.OW + ocol) * 64;
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const f32x4 v = acc[t][a];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          ssum[a][r] += v[r];
+          ssq[a][r] = fmaf(v[r], v[r], ssq[a][r]);
+        }
+        *reinterpret_cast<f32x4*>(yp + a * 16 + 4 * fq) = v;
+      }
+    }
+  }
+  if (stats) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+          ssum[a][r] += __shfl_xor(ssum[a][r], off, 64);
+          ssq[a][r] += __shfl_xor(ssq[a][r], off, 64);
+        }
+    __syncthreads();
+    float* red = fl;   // [sum | sq][wave][64]
+    if (fi == 0) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          red[wave * 64 + a * 16 + 4 * fq + r] = ssum[a][r];
+          red[(4 + wave) * 64 + a * 16 + 4 * fq + r] = ssq[a][r];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      float sa = 0.f, sb = 0.f;
+#pragma unroll
+      for (int w2 = 0; w2 < 4; ++w2) {
+        sa += red[w2 * 64 + threadIdx.x];
+        sb += red[(4 + w2) * 64 + threadIdx.x];
+      }
+      stats[(int64_t)blockIdx.x * 64 + threadIdx.x] = sa;
+      stats[stats_ld + (int64_t)blockIdx.x * 64 + threadIdx.x] = sb;
+    }
+  }
+}
+
 // out[n][c][kh][kw] (strided fp32, the (arena) gradient) += sum over blocks
 __global__ void __launch_bounds__(256) stem_f32_wgrad_reduce_kernel(const float* __restrict__ part, int blocks,
                                                                     float* __restrict__ out, int64_t s0, int64_t s1,
@@ -296,6 +453,28 @@ int stem_f32_forward(const float* x, int N, int H, int W, const float* w, int64_
   (void)attr;
   hipLaunchKernelGGL(stem_f32_fwd_kernel, dim3((unsigned)grid), dim3(256), kFFwdLds, stream, x, w, s0, s1, s2, s3, y, g,
                      stats, (int64_t)stats_rows * 64);
+  return grid;
+}
+
+int stem_f32x6_wplanes() { return 3 * kXPlane; }
+
+int stem_f32x6_forward(const float* x, int N, int H, int W, const float* w, int64_t s0, int64_t s1, int64_t s2,
+                       int64_t s3, uint16_t* wp3, float* y, float* stats, int stats_rows, hipStream_t stream) {
+  StemF32Geo g{N, H, W, kFOW, kFOW, N * (kFOW / kFR)};
+  int grid = g.nbands < 512 ? g.nbands : 512;
+  if (stats && grid > stats_rows) grid = stats_rows;
+  constexpr int lds = kFBand * 4;
+  hipLaunchKernelGGL(stem_w_split3_kernel, dim3((kXPlane + 255) / 256), dim3(256), 0, stream, w, s0, s1, s2, s3, wp3);
+  static const int occ = [] {
+    const char* e = getenv("GKSGD_STEM_X6_OCC");
+    return (e != nullptr && e[0] == '2') ? 2 : 1;
+  }();
+  if (occ == 2)
+    hipLaunchKernelGGL(stem_f32x6_fwd_kernel<2>, dim3((unsigned)grid), dim3(256), lds, stream, x, wp3, y, g, stats,
+                       (int64_t)stats_rows * 64);
+  else
+    hipLaunchKernelGGL(stem_f32x6_fwd_kernel<1>, dim3((unsigned)grid), dim3(256), lds, stream, x, wp3, y, g, stats,
+                       (int64_t)stats_rows * 64);
   return grid;
 }
 

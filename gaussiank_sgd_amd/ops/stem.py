@@ -32,6 +32,12 @@ from . import load
 _CL = torch.channels_last
 _ENABLED = os.environ.get("GKSGD_STEM", "1") != "0"
 _F32 = os.environ.get("GKSGD_STEM_F32", "1") != "0"   # fp32 stem kernels (else MIOpen at fp32)
+# fp32 stem forward on the bf16x6 kernel when the fp32 GEMM family is bf16x6
+# (ops/conv1x1.py set_f32_matmul; GKSGD_STEM_X6=0 keeps the fp32-MFMA kernel)
+_X6 = os.environ.get("GKSGD_STEM_X6", "1") != "0"
+
+
+from . import conv1x1 as _cv  # noqa: E402
 
 
 def _g():
@@ -94,7 +100,13 @@ class _StemF32Fn(torch.autograd.Function):
         st = None
         if stats_box is not None:
             st = torch.empty(2, 512, 64, dtype=torch.float32, device=x.device)
-        rows = g.stem_f32_fwd(x, param.detach(), y, st)
+        if _X6 and _cv.f32_matmul() == "bf16x6":
+            # bf16x6 products (fp32-accurate, stem_f32.hip stem_f32x6_fwd_kernel):
+            # the weight planes are split into a per-call workspace
+            wp3 = torch.empty(int(g.stem_f32x6_wplanes()), dtype=torch.bfloat16, device=x.device)
+            rows = g.stem_f32x6_fwd(x, param.detach(), y, st, wp3)
+        else:
+            rows = g.stem_f32_fwd(x, param.detach(), y, st)
         if st is not None:
             stats_box.append((st, int(rows)))
         ctx.sink = sink

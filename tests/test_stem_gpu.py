@@ -181,3 +181,55 @@ def test_resnet50_stem_f32_bn_stats_match_pass():
     assert (out_a - out_b).abs().max().item() <= 1e-4
     assert torch.allclose(bn_a.running_mean, bn_b.running_mean, rtol=1e-5, atol=1e-6)
     assert torch.allclose(bn_a.running_var, bn_b.running_var, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("N", [1, 4])
+def test_stem_f32x6_fwd_vs_fp64_and_f32_kernel(N):
+    """bf16x6 stem forward (stem_f32.hip stem_f32x6_fwd_kernel: hi/mid/lo bf16
+    splits of band and weights, six MFMA products) vs fp64 torch: no less
+    accurate than the fp32-MFMA kernel (1.1x its max error), same BatchNorm
+    statistics partials."""
+    g = torch.ops.gksgd
+    torch.manual_seed(11 + N)
+    x = torch.randn(N, 3, 224, 224, device="cuda").contiguous(memory_format=CL)
+    w = torch.randn(64, 3, 7, 7, device="cuda") * 0.1
+    ref = F.conv2d(x.double(), w.double(), stride=2, padding=3)
+    bound = F.conv2d(x.double().abs(), w.double().abs(), stride=2, padding=3).max().item()
+    y32 = torch.full((N, 64, 112, 112), float("nan"), device="cuda").contiguous(memory_format=CL)
+    st32 = torch.full((2, 512, 64), float("nan"), device="cuda")
+    r32 = g.stem_f32_fwd(x, w, y32, st32)
+    y6 = torch.full_like(y32, float("nan"))
+    st6 = torch.full_like(st32, float("nan"))
+    wp3 = torch.empty(int(g.stem_f32x6_wplanes()), dtype=torch.bfloat16, device="cuda")
+    r6 = g.stem_f32x6_fwd(x, w, y6, st6, wp3)
+    torch.cuda.synchronize()
+    assert r6 == r32
+    e32 = (y32.double() - ref).abs().max().item()
+    e6 = (y6.double() - ref).abs().max().item()
+    assert e6 <= 1.1 * e32 + 1e-7 * bound, (e6, e32)
+    assert e6 <= 2e-6 * bound + 1e-6
+    s = st6[:, :r6].double().sum(1)
+    yd = ref.permute(0, 2, 3, 1).reshape(-1, 64)
+    assert torch.allclose(s[0], yd.sum(0), rtol=1e-5, atol=1e-3)
+    assert torch.allclose(s[1], (yd * yd).sum(0), rtol=1e-5, atol=1e-3)
+
+
+def test_stem_conv_f32_module_bf16x6_mode():
+    """StemConv at fp32 under set_f32_matmul('bf16x6') (bench.py's mode) runs
+    the x6 forward and matches fp64; 'native' runs the fp32-MFMA forward."""
+    from gaussiank_sgd_amd.ops import conv1x1
+    from gaussiank_sgd_amd.ops.stem import StemConv
+    torch.manual_seed(4)
+    conv = StemConv().cuda()
+    x = torch.randn(2, 3, 224, 224, device="cuda").contiguous(memory_format=CL)
+    yd = F.conv2d(x.double(), conv.weight.detach().double(), stride=2, padding=3)
+    outs = {}
+    for mode in ("bf16x6", "native"):
+        prev = conv1x1.set_f32_matmul(mode)
+        try:
+            outs[mode] = conv(x).detach()
+        finally:
+            conv1x1.set_f32_matmul(prev)
+    for mode, y in outs.items():
+        assert (y.double() - yd).abs().max().item() <= 1e-5 * yd.abs().max().item() + 1e-5, mode
+    assert not torch.equal(outs["bf16x6"], outs["native"])   # two different kernels ran
