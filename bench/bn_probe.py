@@ -83,6 +83,13 @@ def main():
                 g.bn_act_forward(x, res, y, mask, w, b, None, None, st[0], st[1], st[2], st[3], ws, 1e-5, 0.1, True,
                                  None, part, 256)
 
+            def fwd_pre_norelu():
+                g.bn_act_forward(x, None, y, mask, w, b, None, None, st[0], st[1], st[2], st[3], ws, 1e-5, 0.1, False,
+                                 None, part, 256)
+
+            def copy():
+                y.copy_(x)
+
             def bwd_pre():
                 g.bn_act_backward_pre(dz, x, dx, w, st[0], st[1], gg[0], gg[1], part, 256, None, None)
 
@@ -94,7 +101,7 @@ def main():
             # tensor passes: fwd reads x twice (stats, apply) + res, writes y: 4;
             # fwd_pre 2; bwd_pre reads dz, x, writes dx: 3; bwd reduce reads dy, dy2, x,
             # writes dz; apply reads dz, x, writes dx: 7
-            for name, fn, passes in (("fwd", fwd, 4), ("fwd_pre", fwd_pre, 2), ("fwd_res_pre", fwd_res_pre, 3), ("bwd_pre", bwd_pre, 3), ("bwd", bwd, 7)):
+            for name, fn, passes in (("fwd", fwd, 4), ("fwd_pre", fwd_pre, 2), ("fwd_pre_norelu", fwd_pre_norelu, 2), ("copy", copy, 2), ("fwd_res_pre", fwd_res_pre, 3), ("bwd_pre", bwd_pre, 3), ("bwd", bwd, 7)):
                 us = timeit(fn)
                 row[name + "_us"] = round(us, 1)
                 row[name + "_TBs"] = round(passes * mb / us, 3)
