@@ -986,7 +986,7 @@ int64_t stem_f32x6_fwd(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<a
 
 int64_t stem_f32_wgrad_ws(int64_t N) { return (int64_t)gk::stem_f32_wgrad_blocks((int)N) * 64 * 148; }
 
-void stem_f32_wgrad(at::Tensor x, at::Tensor dy, at::Tensor out, at::Tensor part) {
+void stem_f32_wgrad(at::Tensor x, at::Tensor dy, at::Tensor out, at::Tensor part, bool x6) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.dim() == 4 && x.size(1) == 3 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast) && gk::stem_f32_supported((int)x.size(2), (int)x.size(3)) &&
                   reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
@@ -1003,7 +1003,7 @@ void stem_f32_wgrad(at::Tensor x, at::Tensor dy, at::Tensor out, at::Tensor part
   c10::DeviceGuard guard(x.device());
   gk::stem_f32_wgrad(x.data_ptr<float>(), dy.data_ptr<float>(), (int)N, (int)x.size(2), (int)x.size(3),
                      part.data_ptr<float>(), out.data_ptr<float>(), out.stride(0), out.stride(1), out.stride(2),
-                     out.stride(3), cur_stream(x));
+                     out.stride(3), x6, cur_stream(x));
 }
 
 // optional device seed word (graph replays): int32[>=1] on the GPU
@@ -1923,7 +1923,7 @@ TORCH_LIBRARY(gksgd, m) {
   m.def("stem_f32x6_wplanes() -> int", &stem_f32x6_wplanes);
   m.def("stem_f32x6_fwd(Tensor x, Tensor w, Tensor(a!) y, Tensor(b!)? stats, Tensor(c!) wp3) -> int");
   m.def("stem_f32_wgrad_ws(int N) -> int", &stem_f32_wgrad_ws);
-  m.def("stem_f32_wgrad(Tensor x, Tensor dy, Tensor(a!) out, Tensor(b!) part) -> ()");
+  m.def("stem_f32_wgrad(Tensor x, Tensor dy, Tensor(a!) out, Tensor(b!) part, bool x6=False) -> ()");
   m.def("wgrad3_supported(int H, int W, int C, int K) -> bool", [](int64_t H, int64_t W, int64_t C, int64_t K) {
     return gk::wgrad3_supported((int)H, (int)W, (int)C, (int)K);
   });

@@ -401,7 +401,7 @@ int stem_f32x6_forward(const float* x, int N, int H, int W, const float* w, int6
 int stem_f32_forward(const float* x, int N, int H, int W, const float* w, int64_t s0, int64_t s1, int64_t s2,
                      int64_t s3, float* y, float* stats, int stats_rows, hipStream_t stream);
 void stem_f32_wgrad(const float* x, const float* dy, int N, int H, int W, float* part, float* out, int64_t s0,
-                    int64_t s1, int64_t s2, int64_t s3, hipStream_t stream);
+                    int64_t s1, int64_t s2, int64_t s3, bool x6, hipStream_t stream);
 void wino_weights(const float* w, float* u, int Co, int Ci, int flip, hipStream_t stream);
 // Batched per-step weight re-layouts (prep.hip): one launch over a table of
 // descriptors (device memory, block_begin ascending).  kind kPrepWino /

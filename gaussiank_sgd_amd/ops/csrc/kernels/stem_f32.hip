@@ -301,7 +301,9 @@ __global__ void __launch_bounds__(256) stem_w_split3_kernel(const float* __restr
 }
 
 // OCC: waves per SIMD the register budget is set for (1: 179 VGPR + 112 AGPR,
-// no spills; 2: 256 registers with a 40-byte spill) -- GKSGD_STEM_X6_OCC picks
+// no spills; 2: 256 registers with a 40-byte spill) -- GKSGD_STEM_X6_OCC picks;
+// default 2: bs128 0.249 ms vs 0.309 (OCC 1) vs 0.339 for the fp32-MFMA kernel
+// (bench/stem_x6_probe.py, profiles/r06_stem_x6.txt)
 template <int OCC>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC)))
 stem_f32x6_fwd_kernel(const float* __restrict__ x, const uint16_t* __restrict__ wp3, float* __restrict__ y,
@@ -419,6 +421,197 @@ stem_f32x6_fwd_kernel(const float* __restrict__ x, const uint16_t* __restrict__ 
   }
 }
 
+// bf16x6 grad-weight: the contraction over pixels runs 32 at a time on
+// v_mfma_f32_16x16x32_bf16.  Lane (fi, fq) holds pixels 32 s + 8 fq .. + 7 of
+// its wave's output row: dY of channel a * 16 + fi (straight from global, as
+// the fp32 kernel) and the band values of tap ks * 16 + fi, each split once
+// into three exact bf16 parts; six part products per (a, ks) subtile, smallest
+// first.  112 pixels = three full steps and a half step (lanes fq >= 2 hold
+// zeros).  The next step's dY loads are issued before this step's MFMAs and
+// the next band's loads before this band's (double-buffered band in LDS).  Same band walk, accumulator layout and per-block partials as
+// stem_f32_wgrad_kernel (stem_f32_wgrad_reduce sums them).
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1)))
+stem_f32x6_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ part,
+                        StemF32Geo g) {
+  extern __shared__ __attribute__((aligned(16))) float fl[];
+  // two band buffers (the next band is loaded into registers during this
+  // band's MFMAs and stored to the other buffer after them); buffer 0 is also
+  // the cross-wave reduction area [64][160]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fi = lane & 15, fq = lane >> 4;
+  int ko[kFKS];
+#pragma unroll
+  for (int ks = 0; ks < kFKS; ++ks) ko[ks] = tap_off(ks * 16 + fi);   // taps >= 147: gradient dropped
+  f32x4 acc[4][kFKS];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int ks = 0; ks < kFKS; ++ks) acc[a][ks] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int bpi = g.OH / kFR;
+  constexpr int kSteps = (kFOW + 31) / 32;
+  constexpr int RV = 2 * kFOW * 3 / 4;               // float4 per input row
+  constexpr int RW = kFPW * 3;                       // floats per band row
+  constexpr int kBandV = kFIn * RV;
+  constexpr int kBandPer = (kBandV + 255) / 256;
+  // the zero borders of both buffers, once
+  for (int i = threadIdx.x; i < 2 * kFIn * 18; i += blockDim.x) {
+    const int bf = i / (kFIn * 18), q = i - bf * (kFIn * 18);
+    const int rr = q / 18, j = q - rr * 18;
+    fl[bf * kFBand + rr * RW + (j < 9 ? j : RW - 18 + j)] = 0.f;
+  }
+  float4 bv[kBandPer];
+  auto fetch_band = [&](int bb) __attribute__((always_inline)) {
+    const int n = bb / bpi, ih0 = 2 * ((bb - n * bpi) * kFR) - 3;
+#pragma unroll
+    for (int j = 0; j < kBandPer; ++j) {
+      const int i = threadIdx.x + 256 * j;
+      const int rr = i / RV, jj = i - rr * RV;
+      const int ih = ih0 + rr;
+      bv[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < kBandV && (unsigned)ih < (unsigned)g.H)
+        bv[j] = reinterpret_cast<const float4*>(x + ((int64_t)n * g.H + ih) * g.W * 3)[jj];
+    }
+  };
+  auto store_band = [&](float* band) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < kBandPer; ++j) {
+      const int i = threadIdx.x + 256 * j;
+      if (i < kBandV) {
+        const int rr = i / RV, jj = i - rr * RV;
+        float* d = band + rr * RW + 9 + 4 * jj;
+        d[0] = bv[j].x; d[1] = bv[j].y; d[2] = bv[j].z; d[3] = bv[j].w;
+      }
+    }
+  };
+  // dY of the NEXT pixel step is loaded while this step's MFMAs run (the
+  // global round trip would otherwise stall every step)
+  float dn[4][8];
+  auto load_dy = [&](int bb, int s) __attribute__((always_inline)) {
+    const int n = bb / bpi, orow = (bb - n * bpi) * kFR + wave;
+    const float* dyr = dy + (((int64_t)n * g.OH + orow) * g.OW) * 64;
+    const int px = 32 * s + 8 * fq;
+    const int pxc = px < kFOW ? px : 0;              // dead lanes read valid addresses (zeroed at use)
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dn[a][e] = dyr[(int64_t)(pxc + e) * 64 + a * 16 + fi];
+  };
+  int cur = 0;
+  if (blockIdx.x < g.nbands) {
+    load_dy(blockIdx.x, 0);
+    fetch_band(blockIdx.x);
+    store_band(fl);
+  }
+  __syncthreads();
+  for (int b = blockIdx.x; b < g.nbands; b += gridDim.x) {
+    const int bnext = b + (int)gridDim.x;
+    if (bnext < g.nbands) fetch_band(bnext);
+    const float* band = fl + cur * kFBand;
+    for (int s = 0; s < kSteps; ++s) {
+      const int px = 32 * s + 8 * fq;
+      const bool live = px < kFOW;                   // kFOW % 8 == 0: a lane's 8 pixels are all in or all out
+      const int pxc = live ? px : 0;
+      bf16x8 gh[4], gm[4], gl[4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        f32x4 d0, d1;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          d0[e] = live ? dn[a][e] : 0.f;
+          d1[e] = live ? dn[a][4 + e] : 0.f;
+        }
+        split3x8(d0, d1, gh[a], gm[a], gl[a]);
+      }
+      if (s + 1 < kSteps) load_dy(b, s + 1);
+      else if (bnext < g.nbands) load_dy(bnext, 0);
+      const int pb = (2 * wave * kFPW + 2 * pxc) * 3;
+      // band operand of tap subtile ks (dead lanes read valid band values:
+      // their dY parts are zero, so the products vanish)
+      auto rd = [&](int ks, float (&xv)[8]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xv[e] = band[pb + 6 * e + ko[ks]];
+      };
+      // one wave per SIMD issues in order, so a VALU run behind an MFMA run
+      // waits for the matrix pipe: the split of subtile ks + 1 is cut into 20
+      // one-to-two-instruction stages placed between the 24 MFMAs of subtile ks
+      // (sched_barrier fixes the order), and the band values of ks + 2 are read
+      // meanwhile (a whole subtile of LDS latency)
+      float xr[2][8];
+      uint32_t sh[4], sm[4], sl[4];
+      float s1[8], s2[8];
+      auto split_stage = [&](const float (&xv)[8], int j) __attribute__((always_inline)) {
+        const int p = j / 5, stg = j % 5;
+        if (stg == 0) {
+          sh[p] = pack_bf16x2(xv[2 * p], xv[2 * p + 1]);
+        } else if (stg == 1) {
+          s1[2 * p] = xv[2 * p] - __uint_as_float(sh[p] << 16);
+          s1[2 * p + 1] = xv[2 * p + 1] - __uint_as_float(sh[p] & 0xffff0000u);
+        } else if (stg == 2) {
+          sm[p] = pack_bf16x2(s1[2 * p], s1[2 * p + 1]);
+        } else if (stg == 3) {
+          s2[2 * p] = s1[2 * p] - __uint_as_float(sm[p] << 16);
+          s2[2 * p + 1] = s1[2 * p + 1] - __uint_as_float(sm[p] & 0xffff0000u);
+        } else {
+          sl[p] = pack_bf16x2(s2[2 * p], s2[2 * p + 1]);
+        }
+      };
+      auto planes = [&](bf16x8& h, bf16x8& m, bf16x8& l) __attribute__((always_inline)) {
+        h = __builtin_bit_cast(bf16x8, u32x4{sh[0], sh[1], sh[2], sh[3]});
+        m = __builtin_bit_cast(bf16x8, u32x4{sm[0], sm[1], sm[2], sm[3]});
+        l = __builtin_bit_cast(bf16x8, u32x4{sl[0], sl[1], sl[2], sl[3]});
+      };
+      rd(0, xr[0]);
+      rd(1, xr[1]);
+      bf16x8 xh, xm, xl;
+#pragma unroll
+      for (int j = 0; j < 20; ++j) split_stage(xr[0], j);
+      planes(xh, xm, xl);
+#pragma unroll
+      for (int ks = 0; ks < kFKS; ++ks) {
+        const int nx = (ks + 1) & 1;                 // buffer of subtile ks + 1
+        if (ks + 2 < kFKS) rd(ks + 2, xr[ks & 1]);   // subtile ks's buffer is free: its split is done
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 24; ++i) {
+          const int a = i / 6, t = i % 6;
+          const bf16x8 ga = t == 0 ? gl[a] : (t == 1 || t == 5 || t == 4 ? gh[a] : gm[a]);
+          const bf16x8 xb = t == 0 ? xh : (t == 1 ? xl : (t == 2 || t == 4 ? xm : xh));
+          acc[a][ks] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga, xb, acc[a][ks], 0, 0, 0);
+          if (ks + 1 < kFKS && i >= 2 && i < 22) split_stage(xr[nx], i - 2);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (ks + 1 < kFKS) planes(xh, xm, xl);
+      }
+    }
+    // the other buffer was last read before the previous barrier
+    if (bnext < g.nbands) store_band(fl + (cur ^ 1) * kFBand);
+    __syncthreads();
+    cur ^= 1;
+  }
+  // lane: dW[n = a * 16 + 4 fq + r][k = ks * 16 + fi]; sum the 4 waves in order through LDS
+  float* red = fl;
+  for (int w2 = 0; w2 < 4; ++w2) {
+    __syncthreads();
+    if (wave == w2) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int ks = 0; ks < kFKS; ++ks)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float* p = red + (a * 16 + 4 * fq + r) * 160 + ks * 16 + fi;
+            *p = (w2 == 0 ? 0.f : *p) + acc[a][ks][r];
+          }
+    }
+  }
+  __syncthreads();
+  float* dst = part + (int64_t)blockIdx.x * 64 * kFKP;
+  for (int i = threadIdx.x; i < 64 * kFKP; i += blockDim.x) {
+    const int nn = i / kFKP, k = i - nn * kFKP;
+    dst[i] = red[nn * 160 + k];
+  }
+}
+
 // out[n][c][kh][kw] (strided fp32, the (arena) gradient) += sum over blocks
 __global__ void __launch_bounds__(256) stem_f32_wgrad_reduce_kernel(const float* __restrict__ part, int blocks,
                                                                     float* __restrict__ out, int64_t s0, int64_t s1,
@@ -434,6 +627,7 @@ __global__ void __launch_bounds__(256) stem_f32_wgrad_reduce_kernel(const float*
 
 constexpr int kFFwdLds = (kFBand + kFWg) * 4;
 constexpr int kFWgLds = (kFBand > 64 * 160 ? kFBand : 64 * 160) * 4;
+constexpr int kFWg6Lds = (2 * kFBand > 64 * 160 ? 2 * kFBand : 64 * 160) * 4;
 
 }  // namespace
 
@@ -467,7 +661,7 @@ int stem_f32x6_forward(const float* x, int N, int H, int W, const float* w, int6
   hipLaunchKernelGGL(stem_w_split3_kernel, dim3((kXPlane + 255) / 256), dim3(256), 0, stream, w, s0, s1, s2, s3, wp3);
   static const int occ = [] {
     const char* e = getenv("GKSGD_STEM_X6_OCC");
-    return (e != nullptr && e[0] == '2') ? 2 : 1;
+    return (e != nullptr && e[0] == '1') ? 1 : 2;
   }();
   if (occ == 2)
     hipLaunchKernelGGL(stem_f32x6_fwd_kernel<2>, dim3((unsigned)grid), dim3(256), lds, stream, x, wp3, y, g, stats,
@@ -479,7 +673,7 @@ int stem_f32x6_forward(const float* x, int N, int H, int W, const float* w, int6
 }
 
 void stem_f32_wgrad(const float* x, const float* dy, int N, int H, int W, float* part, float* out, int64_t s0,
-                    int64_t s1, int64_t s2, int64_t s3, hipStream_t stream) {
+                    int64_t s1, int64_t s2, int64_t s3, bool x6, hipStream_t stream) {
   StemF32Geo g{N, H, W, kFOW, kFOW, N * (kFOW / kFR)};
   const int grid = stem_f32_wgrad_blocks(N);
   static bool attr = [] {
@@ -487,7 +681,17 @@ void stem_f32_wgrad(const float* x, const float* dy, int N, int H, int W, float*
                                hipFuncAttributeMaxDynamicSharedMemorySize, kFWgLds) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL(stem_f32_wgrad_kernel, dim3((unsigned)grid), dim3(256), kFWgLds, stream, x, dy, part, g);
+  // bf16x6: one wave per SIMD (the prefetched dY and next band live in
+  // registers beside the 160 accumulators)
+  static bool attr6 = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_f32x6_wgrad_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, kFWg6Lds) == hipSuccess;
+  }();
+  (void)attr6;
+  if (x6)
+    hipLaunchKernelGGL(stem_f32x6_wgrad_kernel, dim3((unsigned)grid), dim3(256), kFWg6Lds, stream, x, dy, part, g);
+  else
+    hipLaunchKernelGGL(stem_f32_wgrad_kernel, dim3((unsigned)grid), dim3(256), kFWgLds, stream, x, dy, part, g);
   hipLaunchKernelGGL(stem_f32_wgrad_reduce_kernel, dim3((64 * kFK + 255) / 256), dim3(256), 0, stream, part, grid, out,
                      s0, s1, s2, s3);
 }

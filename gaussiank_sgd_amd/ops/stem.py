@@ -100,7 +100,8 @@ class _StemF32Fn(torch.autograd.Function):
         st = None
         if stats_box is not None:
             st = torch.empty(2, 512, 64, dtype=torch.float32, device=x.device)
-        if _X6 and _cv.f32_matmul() == "bf16x6":
+        x6 = _X6 and _cv.f32_matmul() == "bf16x6"
+        if x6:
             # bf16x6 products (fp32-accurate, stem_f32.hip stem_f32x6_fwd_kernel):
             # the weight planes are split into a per-call workspace
             wp3 = torch.empty(int(g.stem_f32x6_wplanes()), dtype=torch.bfloat16, device=x.device)
@@ -110,6 +111,7 @@ class _StemF32Fn(torch.autograd.Function):
         if st is not None:
             stats_box.append((st, int(rows)))
         ctx.sink = sink
+        ctx.x6 = x6     # the grad-weight runs the same family (stem_f32x6_wgrad_kernel)
         ctx.save_for_backward(x)
         return y
 
@@ -124,10 +126,10 @@ class _StemF32Fn(torch.autograd.Function):
             sink = ctx.sink
             if sink is not None and getattr(sink, "grad_view", None) is not None:
                 sink.check()
-                g.stem_f32_wgrad(x, dy, sink.grad_view, part)
+                g.stem_f32_wgrad(x, dy, sink.grad_view, part, ctx.x6)
             else:
                 out = torch.zeros(64, 3, 7, 7, dtype=torch.float32, device=x.device)
-                g.stem_f32_wgrad(x, dy, out, part)
+                g.stem_f32_wgrad(x, dy, out, part, ctx.x6)
                 if sink is not None:
                     sink(out)
                 else:
