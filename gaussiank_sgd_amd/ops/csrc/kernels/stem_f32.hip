@@ -23,7 +23,7 @@
 //   A fragments gathered from the LDS band; each wave accumulates 64 x 160
 //   (4 x 10 subtiles, 160 registers) over its rows of every band of the
 //   block; the 4 waves are summed through LDS and every block writes one
-//   partial; stem_f32_wgrad_reduce sums the partials in block order
+//   partial; stem_f32_wgrad_reduce sums the partials in a fixed order
 //   (deterministic) into the (arena) gradient.
 #include <hip/hip_runtime.h>
 
@@ -612,18 +612,36 @@ stem_f32x6_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ d
   }
 }
 
-// out[n][c][kh][kw] (strided fp32, the (arena) gradient) += sum over blocks
+// out[n][c][kh][kw] (strided fp32, the (arena) gradient) += sum over blocks.
+// A workgroup owns 16 consecutive outputs of the padded [64][148] partial
+// rows; its 16 lane groups each sum every 16th block (independent loads in
+// flight instead of one serial chain of `blocks` loads per output: 130 us ->
+// a few us at bs512), then lane group 0 adds the 16 group sums in order --
+// a fixed order, so the result is deterministic.
+constexpr int kRedOut = 16, kRedSplit = 16;
 __global__ void __launch_bounds__(256) stem_f32_wgrad_reduce_kernel(const float* __restrict__ part, int blocks,
                                                                     float* __restrict__ out, int64_t s0, int64_t s1,
                                                                     int64_t s2, int64_t s3) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= 64 * kFK) return;
-  const int n = i / kFK, k = i - n * kFK;
-  float s = 0.f;
-  for (int b = 0; b < blocks; ++b) s += part[((int64_t)b * 64 + n) * kFKP + k];
-  const int kh = k / 21, r = k - kh * 21, kw = r / 3, c = r - kw * 3;
-  out[n * s0 + c * s1 + kh * s2 + kw * s3] += s;
+  __shared__ float sh[kRedSplit][kRedOut];
+  const int ol = threadIdx.x % kRedOut, sp = threadIdx.x / kRedOut;
+  const int o = blockIdx.x * kRedOut + ol;          // < 64 * kFKP (grid covers it exactly)
+  float acc = 0.f;
+#pragma unroll 8
+  for (int b = sp; b < blocks; b += kRedSplit) acc += part[(int64_t)b * 64 * kFKP + o];
+  sh[sp][ol] = acc;
+  __syncthreads();
+  if (sp == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < kRedSplit; ++j) t += sh[j][ol];
+    const int n = o / kFKP, k = o - n * kFKP;
+    if (k < kFK) {
+      const int kh = k / 21, r = k - kh * 21, kw = r / 3, c = r - kw * 3;
+      out[n * s0 + c * s1 + kh * s2 + kw * s3] += t;
+    }
+  }
 }
+static_assert((64 * kFKP) % kRedOut == 0, "reduce grid covers the partial rows exactly");
 
 constexpr int kFFwdLds = (kFBand + kFWg) * 4;
 constexpr int kFWgLds = (kFBand > 64 * 160 ? kFBand : 64 * 160) * 4;
@@ -692,7 +710,7 @@ void stem_f32_wgrad(const float* x, const float* dy, int N, int H, int W, float*
     hipLaunchKernelGGL(stem_f32x6_wgrad_kernel, dim3((unsigned)grid), dim3(256), kFWg6Lds, stream, x, dy, part, g);
   else
     hipLaunchKernelGGL(stem_f32_wgrad_kernel, dim3((unsigned)grid), dim3(256), kFWgLds, stream, x, dy, part, g);
-  hipLaunchKernelGGL(stem_f32_wgrad_reduce_kernel, dim3((64 * kFK + 255) / 256), dim3(256), 0, stream, part, grid, out,
+  hipLaunchKernelGGL(stem_f32_wgrad_reduce_kernel, dim3(64 * kFKP / kRedOut), dim3(256), 0, stream, part, grid, out,
                      s0, s1, s2, s3);
 }
 
