@@ -155,9 +155,9 @@ def parse():
     ap.add_argument("--graph", action="store_true",
                     help="capture the whole training step in a HIP graph and replay it (train/graph.py)")
     ap.add_argument("--k-cap-factor", type=float, default=None,
-                    help="record capacity k_cap = factor * k of the sparse compressor (default: the compressor's, "
-                         "Gaussian-k 4/3); 1.0 sends at most k entries (what the reference's 500x assumes), the "
-                         "overflow staying in the residual")
+                    help="record capacity k_cap = factor * k of the sparse compressor (default: the compressor's: "
+                         "Gaussian-k 1.0 -- at most k entries, what the reference's 500x assumes, the overflow "
+                         "staying in the residual; gaussian_cal 4/3)")
     ap.add_argument("--model-phases", default="vgg16,lstm,bert",
                     help="comma list of further BASELINE models timed after the headline in the same process "
                          "(same precision / compressor / density); 'none' skips them")
