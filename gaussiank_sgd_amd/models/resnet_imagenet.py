@@ -48,7 +48,7 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         x, xs = x if isinstance(x, tuple) else (x, x)   # (main, shortcut) handles, see BNAct twin
-        identity = xs if self.downsample is None else self.downsample(xs)
+        identity = xs if self.downsample is None else _shortcut(self.downsample, xs, self.bn2)
         y, st = conv_stats(self.conv1, x)   # BN statistics from the conv epilogue when fused
         out = self.bn1(y, stats=st)
         y, st = conv_stats(self.conv2, out)
@@ -71,7 +71,7 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         x, xs = x if isinstance(x, tuple) else (x, x)   # (main, shortcut) handles, see BNAct twin
-        identity = xs if self.downsample is None else self.downsample(xs)
+        identity = xs if self.downsample is None else _shortcut(self.downsample, xs, self.bn3)
         y, st = conv_stats(self.conv1, x)   # BN statistics from the conv epilogue when fused
         out = self.bn1(y, stats=st)
         y, st = conv_stats(self.conv2, out)
@@ -87,6 +87,23 @@ class ConvBN(nn.Sequential):
     def forward(self, x):
         y, st = conv_stats(self[0], x)
         return self[1](y, stats=st)
+
+    def forward_deferred(self, x, consumer: BNAct):
+        """The shortcut with its BN apply deferred into ``consumer`` (the block's
+        last BN, which adds it as its residual): the pending handle of
+        ``BNAct.deferred``, or the plain output when either BN is not fused."""
+        y, st = conv_stats(self[0], x)
+        if consumer.fused_ok(y):
+            h = self[1].deferred(y, stats=st)
+            if h is not None:
+                return h
+        return self[1](y, stats=st)
+
+
+def _shortcut(ds: nn.Module, xs: torch.Tensor, consumer: BNAct) -> torch.Tensor:
+    if isinstance(ds, ConvBN):
+        return ds.forward_deferred(xs, consumer)
+    return ds(xs)
 
 
 class ResNet(nn.Module):

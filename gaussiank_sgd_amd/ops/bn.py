@@ -133,7 +133,7 @@ def _lazy_ok(x: torch.Tensor, plink) -> bool:
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, relu, direct=None,
-                nbt=None, twin=False, pre=None, link=None, res_link=None, plink=None, fin=None):
+                nbt=None, twin=False, pre=None, link=None, res_link=None, plink=None, fin=None, rbn=None):
         # direct = (gw_view, gb_view): weight/bias gradients are accumulated
         # straight into the optimizer's fp32 arena by the backward kernel and
         # None is returned for them, so AccumulateGrad launches nothing (its
@@ -148,6 +148,10 @@ class _BNActFn(torch.autograd.Function):
         y = torch.empty_like(x, memory_format=_CL)
         stats = torch.empty(4, C, dtype=torch.float32, device=x.device)
         ws = torch.empty(int(_ops().bn_workspace_floats(M, C, eb)), dtype=torch.float32, device=x.device)
+        # a deferred residual BN (_BNDeferFn): residual = r * rscale + rshift formed on load
+        rscale, rshift = rbn if rbn is not None else (None, None)
+        if rbn is not None and (residual.dtype != x.dtype or not residual.is_contiguous(memory_format=_CL)):
+            raise RuntimeError("deferred residual BN: the pending tensor must match x (dtype, channels-last)")
         if residual is not None and residual.dtype != x.dtype:
             residual = residual.to(x.dtype)
         if residual is not None and not residual.is_contiguous(memory_format=_CL):
@@ -160,7 +164,7 @@ class _BNActFn(torch.autograd.Function):
         pre_t, pre_rows = pre if pre is not None else (None, 0)
         _ops().bn_act_forward(x, residual, y, mask, weight, bias, running_mean, running_var, stats[0], stats[1],
                               stats[2], stats[3], ws, float(eps), float(momentum), bool(relu), nbt, pre_t, pre_rows,
-                              fin)
+                              fin, rscale, rshift)
         ctx.fin = fin
         ctx.relu = bool(relu)
         ctx.has_res = residual is not None
@@ -204,15 +208,15 @@ class _BNActFn(torch.autograd.Function):
             if res_link is not None and dres is not None:
                 res_link.dy2 = dres
             if ctx.direct is not None:
-                return (dx, dres) + (None,) * 15
+                return (dx, dres) + (None,) * 16
             dgamma = g[0] if weight is not None and ctx.needs_input_grad[2] else None
             dbeta = g[1] if ctx.needs_input_grad[3] else None
-            return (dx, dres, dgamma, dbeta) + (None,) * 13
+            return (dx, dres, dgamma, dbeta) + (None,) * 14
         if link is not None:
             link.clear()
         dy, dy2 = _grad_pair(grads, x)
         if dy is None:
-            return (None,) * 17
+            return (None,) * 18
         C = x.shape[1]
         M = x.numel() // C
         g = torch.empty(2, C, dtype=torch.float32, device=x.device)
@@ -235,10 +239,68 @@ class _BNActFn(torch.autograd.Function):
         if res_link is not None and dres is not None:
             res_link.dy2 = dres
         if ctx.direct is not None:
-            return (dx, dres) + (None,) * 15
+            return (dx, dres) + (None,) * 16
         dgamma = g[0] if weight is not None and ctx.needs_input_grad[2] else None
         dbeta = g[1] if ctx.needs_input_grad[3] else None
-        return (dx, dres, dgamma, dbeta) + (None,) * 13
+        return (dx, dres, dgamma, dbeta) + (None,) * 14
+
+
+class _BNDeferFn(torch.autograd.Function):
+    """A plain BN (no ReLU, no residual) whose apply pass is deferred into its
+    only consumer: the forward runs the statistics + finalize (running stats,
+    saved mean / invstd, per-channel scale / shift) and returns a view of the
+    UN-normalised input tagged ``_gk_pending_bn = (scale, shift)``; the
+    consumer -- the block's last fused BN, which takes it as its residual --
+    adds ``x * scale + shift`` on load (bn_act.hip ``bn_apply_kernel`` RBN).
+    The BN output is never written: one streaming pass (read x, write y) less
+    per ResNet downsample shortcut.  The backward is the plain BN backward of
+    the gradient the consumer hands back for its residual (d out / d residual
+    = the consumer's dz), so it is unchanged.
+
+    The handle is only valid as the residual of a fused BNAct; model code that
+    wires it (models/resnet_imagenet.py Bottleneck) guarantees that."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, stats, direct=None, nbt=None,
+                pre=None):
+        # stats: fp32 [4, C] (mean, invstd, scale, shift), allocated by the caller, which
+        # tags the returned handle with its scale / shift rows
+        ctx.direct = direct
+        ctx.set_materialize_grads(False)
+        C = x.shape[1]
+        M = x.numel() // C
+        ws = torch.empty(int(_ops().bn_workspace_floats(M, C, x.element_size())), dtype=torch.float32,
+                         device=x.device)
+        pre_t, pre_rows = pre if pre is not None else (None, 0)
+        _ops().bn_act_finalize(x, weight, bias, running_mean, running_var, stats[0], stats[1], stats[2], stats[3], ws,
+                               float(eps), float(momentum), nbt, pre_t, pre_rows)
+        ctx.save_for_backward(x, weight, stats[0], stats[1])
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, mean, invstd = ctx.saved_tensors
+        if dy is None:
+            return (None,) * 11
+        dy = dy.contiguous(memory_format=_CL)
+        if dy.dtype != x.dtype:
+            dy = dy.to(x.dtype)
+        C = x.shape[1]
+        M = x.numel() // C
+        g = torch.empty(2, C, dtype=torch.float32, device=x.device)
+        ws = torch.empty(int(_ops().bn_workspace_floats(M, C, x.element_size())), dtype=torch.float32,
+                         device=x.device)
+        gw, gb = ctx.direct if ctx.direct is not None else (None, None)
+        dx = torch.empty_like(x, memory_format=_CL)
+        _ops().bn_act_backward(dy, None, x, dx, None, weight, mean, invstd, g[0], g[1], ws, False, gw, gb, None, None)
+        if ctx.direct is not None:
+            return (dx,) + (None,) * 10
+        dgamma = g[0] if weight is not None and ctx.needs_input_grad[1] else None
+        dbeta = g[1] if ctx.needs_input_grad[2] else None
+        return (dx, dgamma, dbeta) + (None,) * 8
+
+
+_DEFER = os.environ.get("GKSGD_BN_DEFER", "1") != "0"
 
 
 class _BNReLUPoolFn(torch.autograd.Function):
@@ -360,9 +422,10 @@ class BNAct(nn.BatchNorm2d):
             link = BnLink() if self.bwd_link and torch.is_grad_enabled() else None
             res_link = getattr(residual, "_gk_res_link", None) if residual is not None else None
             plink = getattr(x, "_gk_plink", None) if torch.is_grad_enabled() else None
+            rbn = getattr(residual, "_gk_pending_bn", None) if residual is not None else None
             out = _BNActFn.apply(x, residual, self.weight, self.bias, self.running_mean, self.running_var, mom,
                                  self.eps, relu, direct, nbt, self.twin, stats, link, res_link, plink,
-                                 self._fin_state(x))
+                                 self._fin_state(x), rbn)
             if link is not None:
                 main = out[0] if self.twin else out
                 main._gk_bn_link = link
@@ -371,12 +434,43 @@ class BNAct(nn.BatchNorm2d):
             return out
         out = super().forward(x)
         if residual is not None:
+            pend = getattr(residual, "_gk_pending_bn", None)
+            if pend is not None:   # a deferred BN output (BNAct.deferred): apply it here
+                C = residual.shape[1]
+                residual = residual * pend[0].view(1, C, 1, 1).to(residual.dtype) + \
+                    pend[1].view(1, C, 1, 1).to(residual.dtype)
             out = out + residual
         if relu:
             out = F.relu(out)
         if pool is not None:
             out = F.max_pool2d(out, pool[0], pool[1], pool[2])
         return (out, out) if self.twin else out
+
+    def fused_ok(self, x: torch.Tensor) -> bool:
+        """Will ``forward(x)`` take the fused training path?"""
+        return bool(self.training and self.fused and self.track_running_stats and fused_bn_available(x))
+
+    def deferred(self, x: torch.Tensor, stats=None) -> Optional[torch.Tensor]:
+        """BN of ``x`` with the apply pass deferred into the consumer (see
+        ``_BNDeferFn``): returns the pending handle, or None when this BN
+        cannot defer (then call ``forward``).  Only for a plain BN (no act,
+        pool or twin) whose output is the residual of a fused BNAct."""
+        if not (_DEFER and self.act is None and self.pool is None and not self.twin and self.fused_ok(x)):
+            return None
+        nbt = self.num_batches_tracked
+        if self.momentum is None:
+            nbt.add_(1)
+            mom = 1.0 / float(nbt)
+            nbt = None
+        else:
+            mom = self.momentum
+        if stats is not None and stats[0].shape[2] != x.shape[1]:
+            stats = None
+        st = torch.empty(4, x.shape[1], dtype=torch.float32, device=x.device)
+        out = _BNDeferFn.apply(x, self.weight, self.bias, self.running_mean, self.running_var, mom, self.eps, st,
+                               getattr(self, "_gk_direct", None), nbt, stats)
+        out._gk_pending_bn = (st[2], st[3])
+        return out
 
     def _fin_state(self, x: torch.Tensor) -> Optional[torch.Tensor]:
         """Per-layer state of the in-launch finalize (bn_act.hip FinSync: a

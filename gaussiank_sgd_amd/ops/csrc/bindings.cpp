@@ -394,7 +394,8 @@ void bn_act_forward(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, c
                     c10::optional<at::Tensor> run_var, at::Tensor save_mean, at::Tensor save_invstd,
                     at::Tensor scale, at::Tensor shift, at::Tensor ws, double eps, double momentum, bool relu,
                     c10::optional<at::Tensor> nbt, c10::optional<at::Tensor> pre, int64_t pre_rows,
-                    c10::optional<at::Tensor> fin) {
+                    c10::optional<at::Tensor> fin, c10::optional<at::Tensor> rscale,
+                    c10::optional<at::Tensor> rshift) {
   check_cl(x, "x");
   check_cl(y, "y");
   const int64_t C = channels_of(x);
@@ -408,6 +409,16 @@ void bn_act_forward(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, c
     check_cl(*res, "residual");
     TORCH_CHECK(res->scalar_type() == x.scalar_type() && res->numel() == x.numel(), "residual must match x");
     rp = res->data_ptr();
+  }
+  // deferred residual BN: res * rscale + rshift (ops/bn.py _BNDeferFn)
+  const float* rsc = opt_f32(rscale);
+  const float* rsh = opt_f32(rshift);
+  TORCH_CHECK((rsc == nullptr) == (rsh == nullptr), "rscale and rshift go together");
+  if (rsc) {
+    TORCH_CHECK(rp != nullptr, "rscale / rshift need a residual");
+    for (const at::Tensor* t : {&*rscale, &*rshift})
+      TORCH_CHECK(t->scalar_type() == at::kFloat && t->numel() >= C && t->is_cuda() && t->is_contiguous(),
+                  "rscale / rshift: fp32[C]");
   }
   for (const at::Tensor* t : {&save_mean, &save_invstd, &scale, &shift})
     TORCH_CHECK(t->scalar_type() == at::kFloat && t->numel() >= C && t->is_cuda(), "stat buffers: fp32[C]");
@@ -431,13 +442,43 @@ void bn_act_forward(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, c
                            (int)pre_rows, opt_f32(w), opt_f32(b), (float)eps, (float)momentum, opt_f32_mut(run_mean),
                            opt_f32_mut(run_var), save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(),
                            scale.data_ptr<float>(), shift.data_ptr<float>(), relu ? 1 : 0, opt_i64(nbt),
-                           cur_stream(x), fs);
+                           cur_stream(x), fs, rsc, rsh);
     return;
   }
   gk::bn_act_forward(x.data_ptr(), rp, y.data_ptr(), mp, M, (int)C, eb, opt_f32(w), opt_f32(b), (float)eps,
                      (float)momentum, opt_f32_mut(run_mean), opt_f32_mut(run_var), save_mean.data_ptr<float>(),
                      save_invstd.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(),
-                     ws.data_ptr<float>(), relu ? 1 : 0, opt_i64(nbt), cur_stream(x), fs);
+                     ws.data_ptr<float>(), relu ? 1 : 0, opt_i64(nbt), cur_stream(x), fs, rsc, rsh);
+}
+
+// statistics + finalize of a BN whose apply is deferred into its consumer
+void bn_act_finalize(at::Tensor x, c10::optional<at::Tensor> w, c10::optional<at::Tensor> b,
+                     c10::optional<at::Tensor> run_mean, c10::optional<at::Tensor> run_var, at::Tensor save_mean,
+                     at::Tensor save_invstd, at::Tensor scale, at::Tensor shift, at::Tensor ws, double eps,
+                     double momentum, c10::optional<at::Tensor> nbt, c10::optional<at::Tensor> pre, int64_t pre_rows) {
+  check_cl(x, "x");
+  const int64_t C = channels_of(x);
+  const int64_t M = x.numel() / C;
+  const int eb = x.element_size();
+  TORCH_CHECK(gk::bn_supported((int)C, eb), "channel count not supported by the fused kernel");
+  for (const at::Tensor* t : {&save_mean, &save_invstd, &scale, &shift})
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->numel() >= C && t->is_cuda(), "stat buffers: fp32[C]");
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() >= (int64_t)gk::bn_workspace_floats(M, (int)C, eb),
+              "workspace too small");
+  const float* ps = nullptr;
+  const float* pq = nullptr;
+  if (pre.has_value() && pre->defined()) {
+    TORCH_CHECK(pre->is_cuda() && pre->scalar_type() == at::kFloat && pre->is_contiguous() && pre->dim() == 3 &&
+                    pre->size(0) == 2 && pre->size(2) == C && pre_rows > 0 && pre_rows <= pre->size(1),
+                "pre must be fp32 [2, rows, C] partials with 0 < pre_rows <= rows");
+    ps = pre->data_ptr<float>();
+    pq = ps + pre->size(1) * C;
+  }
+  c10::DeviceGuard guard(x.device());
+  gk::bn_act_finalize(x.data_ptr(), M, (int)C, eb, ps, pq, (int)pre_rows, opt_f32(w), opt_f32(b), (float)eps,
+                      (float)momentum, opt_f32_mut(run_mean), opt_f32_mut(run_var), save_mean.data_ptr<float>(),
+                      save_invstd.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(),
+                      ws.data_ptr<float>(), opt_i64(nbt), cur_stream(x));
 }
 
 void bn_act_backward(at::Tensor dy, c10::optional<at::Tensor> mask, at::Tensor x, at::Tensor dx,
@@ -1886,7 +1927,11 @@ TORCH_LIBRARY(gksgd, m) {
       "bn_act_forward(Tensor x, Tensor? res, Tensor(a!) y, Tensor(i!)? mask, Tensor? w, Tensor? b, Tensor(b!)? run_mean, "
       "Tensor(c!)? run_var, Tensor(d!) save_mean, Tensor(e!) save_invstd, Tensor(f!) scale, Tensor(g!) shift, "
       "Tensor(h!) ws, float eps, float momentum, bool relu, Tensor(j!)? nbt=None, Tensor? pre=None, "
-      "int pre_rows=0, Tensor(k!)? fin=None) -> ()");
+      "int pre_rows=0, Tensor(k!)? fin=None, Tensor? rscale=None, Tensor? rshift=None) -> ()");
+  m.def(
+      "bn_act_finalize(Tensor x, Tensor? w, Tensor? b, Tensor(a!)? run_mean, Tensor(b!)? run_var, "
+      "Tensor(c!) save_mean, Tensor(d!) save_invstd, Tensor(e!) scale, Tensor(f!) shift, Tensor(g!) ws, float eps, "
+      "float momentum, Tensor(h!)? nbt=None, Tensor? pre=None, int pre_rows=0) -> ()");
   m.def(
       "bn_relu_pool_forward(Tensor x, Tensor(a!) y, Tensor(b!) amax, Tensor? w, Tensor? b, Tensor(c!)? run_mean, "
       "Tensor(d!)? run_var, Tensor(e!) save_mean, Tensor(f!) save_invstd, Tensor(g!) scale, Tensor(h!) shift, "
@@ -2032,6 +2077,7 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("fused_lars", &fused_lars);
   m.impl("clip_grad_norm", &clip_grad_norm);
   m.impl("bn_act_forward", &bn_act_forward);
+  m.impl("bn_act_finalize", &bn_act_finalize);
   m.impl("bn_act_backward", &bn_act_backward);
   m.impl("bn_act_backward_pre", &bn_act_backward_pre);
   m.impl("bn_bwd_lazy_pre", &bn_bwd_lazy_pre);

@@ -384,12 +384,17 @@ __device__ __forceinline__ void fin_prologue(const FinSync& fs, int g0, int g1, 
   __syncthreads();
 }
 
-template <typename T, bool RELU, bool RES, bool FIN = false, int U = kBnUnroll>
+// RBN: the residual is itself a batch-normalised tensor whose apply pass was
+// deferred to here (ResNet downsample shortcut, ops/bn.py _BNDeferFn):
+// res = r * rscale + rshift is formed on load, so the shortcut BN output is
+// never written and read back (one streaming pass less per downsample block).
+template <typename T, bool RELU, bool RES, bool FIN = false, int U = kBnUnroll, bool RBN = false>
 __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res,
                                                           T* __restrict__ y, uint8_t* __restrict__ mask, int64_t M,
                                                           int C, Geo g, const float* __restrict__ scale,
                                                           const float* __restrict__ shift, FinSync fs = FinSync{},
-                                                          FwdFin ff = FwdFin{}) {
+                                                          FwdFin ff = FwdFin{}, const float* __restrict__ rscale = nullptr,
+                                                          const float* __restrict__ rshift = nullptr) {
   constexpr int V = Vec<T>::N;
   const int tc = threadIdx.x % g.tpr;
   const int lane_r = threadIdx.x / g.tpr;
@@ -403,6 +408,11 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const T* __restrict__ 
   } else {
 #pragma unroll
     for (int i = 0; i < V; ++i) { sc[i] = scale[c0 + i]; sf[i] = shift[c0 + i]; }
+  }
+  float rsc[RBN ? V : 1], rsf[RBN ? V : 1];
+  if constexpr (RBN) {
+#pragma unroll
+    for (int i = 0; i < V; ++i) { rsc[i] = rscale[c0 + i]; rsf[i] = rshift[c0 + i]; }
   }
   const int64_t r0 = (int64_t)blockIdx.y * g.rows_per_block;
   int64_t r1 = r0 + g.rows_per_block;
@@ -420,7 +430,8 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const T* __restrict__ 
 #pragma unroll
         for (int i = 0; i < V; ++i) {
           float t = fmaf(w.v[i], sc[i], sf[i]);
-          if (RES) t += w.rv[i];
+          if constexpr (RBN) t += fmaf(w.rv[i], rsc[i], rsf[i]);
+          else if (RES) t += w.rv[i];
           if (RELU) {
             bits |= (t > 0.f ? 1u : 0u) << i;
             t = fmaxf(t, 0.f);
@@ -1047,10 +1058,21 @@ void bn_stats_t(const T* x, int64_t M, int C, const float* w, const float* b, fl
 
 template <typename T>
 void launch_apply(const T* x, const T* res, T* y, uint8_t* mask, int64_t M, int C, const Geo& g, float* scale,
-                  float* shift, int relu, const FinSync& fs, const FwdFin& ff, hipStream_t s) {
+                  float* shift, int relu, const FinSync& fs, const FwdFin& ff, hipStream_t s,
+                  const float* rscale = nullptr, const float* rshift = nullptr) {
+  if (res && rscale) {
+    // deferred residual BN (its scale / shift finalized by an earlier launch)
+    if (relu)
+      hipLaunchKernelGGL((bn_apply_kernel<T, true, true, false, kBnUnroll, true>), dim3(g.gx, g.gy), dim3(kBlock), 0, s,
+                         x, res, y, mask, M, C, g, scale, shift, fs, ff, rscale, rshift);
+    else
+      hipLaunchKernelGGL((bn_apply_kernel<T, false, true, false, kBnUnroll, true>), dim3(g.gx, g.gy), dim3(kBlock), 0,
+                         s, x, res, y, mask, M, C, g, scale, shift, fs, ff, rscale, rshift);
+    return;
+  }
 #define GK_APPLY(R, D, F)                                                                                           \
   hipLaunchKernelGGL((bn_apply_kernel<T, R, D, F>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, x, res, y, mask, M, C, g, \
-                     scale, shift, fs, ff)
+                     scale, shift, fs, ff, nullptr, nullptr)
 #define GK_APPLY2(R, D) if (fs.ticket) GK_APPLY(R, D, true); else GK_APPLY(R, D, false);
   if (relu && res) { GK_APPLY2(true, true) }
   else if (relu) { GK_APPLY2(true, false) }
@@ -1063,8 +1085,10 @@ void launch_apply(const T* x, const T* res, T* y, uint8_t* mask, int64_t M, int 
 template <typename T>
 void bn_forward_t(const T* x, const T* res, T* y, uint8_t* mask, int64_t M, int C, const float* w, const float* b, float eps,
                   float momentum, float* run_mean, float* run_var, float* save_mean, float* save_invstd,
-                  float* scale, float* shift, float* ws, int relu, int64_t* nbt, void* fin_state, hipStream_t s) {
+                  float* scale, float* shift, float* ws, int relu, int64_t* nbt, void* fin_state, hipStream_t s,
+                  const float* rscale = nullptr, const float* rshift = nullptr) {
   const Geo g = make_geo<T>(M, C, kTargetBlocks);
+  if (rscale) fin_state = nullptr;   // the deferred-residual apply has no in-launch finalize form
   const FinSync fs = make_fin(fin_state, g, C, s);
   const FwdFin ff{ws, ws + (int64_t)g.gy * C, g.gy, w, b, eps, momentum, run_mean, run_var, save_mean, save_invstd,
                   scale, shift, nbt};
@@ -1073,7 +1097,7 @@ void bn_forward_t(const T* x, const T* res, T* y, uint8_t* mask, int64_t M, int 
   } else {
     bn_stats_t<T>(x, M, C, w, b, eps, momentum, run_mean, run_var, save_mean, save_invstd, scale, shift, ws, nbt, s);
   }
-  launch_apply<T>(x, res, y, mask, M, C, g, scale, shift, relu, fs, ff, s);
+  launch_apply<T>(x, res, y, mask, M, C, g, scale, shift, relu, fs, ff, s, rscale, rshift);
 }
 
 // finalize (separate launch unless fs carries the in-launch state) + apply
@@ -1155,40 +1179,64 @@ void bn_stats_partials(const void* x, int64_t M, int C, int elem_bytes, float* w
 void bn_act_forward(const void* x, const void* res, void* y, uint8_t* mask, int64_t M, int C, int elem_bytes,
                     const float* w, const float* b, float eps, float momentum, float* run_mean, float* run_var,
                     float* save_mean, float* save_invstd, float* scale, float* shift, float* ws, int relu,
-                    int64_t* nbt, hipStream_t s, void* fin_state) {
+                    int64_t* nbt, hipStream_t s, void* fin_state, const float* rscale, const float* rshift) {
   if (elem_bytes == 2)
     bn_forward_t<uint16_t>((const uint16_t*)x, (const uint16_t*)res, (uint16_t*)y, mask, M, C, w, b, eps, momentum,
-                           run_mean, run_var, save_mean, save_invstd, scale, shift, ws, relu, nbt, fin_state, s);
+                           run_mean, run_var, save_mean, save_invstd, scale, shift, ws, relu, nbt, fin_state, s,
+                           rscale, rshift);
   else
     bn_forward_t<float>((const float*)x, (const float*)res, (float*)y, mask, M, C, w, b, eps, momentum, run_mean,
-                        run_var, save_mean, save_invstd, scale, shift, ws, relu, nbt, fin_state, s);
+                        run_var, save_mean, save_invstd, scale, shift, ws, relu, nbt, fin_state, s, rscale, rshift);
+}
+
+// Statistics (or the producer's partials) + finalize only: the BN whose apply
+// pass is deferred into its consumer (bn_apply_kernel RBN).
+void bn_act_finalize(const void* x, int64_t M, int C, int elem_bytes, const float* psum, const float* psq, int gy,
+                     const float* w, const float* b, float eps, float momentum, float* run_mean, float* run_var,
+                     float* save_mean, float* save_invstd, float* scale, float* shift, float* ws, int64_t* nbt,
+                     hipStream_t s) {
+  if (!psum) {
+    if (elem_bytes == 2)
+      bn_stats_t<uint16_t>((const uint16_t*)x, M, C, w, b, eps, momentum, run_mean, run_var, save_mean, save_invstd,
+                           scale, shift, ws, nbt, s);
+    else
+      bn_stats_t<float>((const float*)x, M, C, w, b, eps, momentum, run_mean, run_var, save_mean, save_invstd, scale,
+                        shift, ws, nbt, s);
+    return;
+  }
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(kBlock), 0, s, psum, psq, gy, M, C, w, b,
+                     eps, momentum, run_mean, run_var, save_mean, save_invstd, scale, shift, nbt);
 }
 
 template <typename T>
 void bn_forward_pre_t(const T* x, const T* res, T* y, uint8_t* mask, int64_t M, int C, const float* psum,
                       const float* psq, int gy, const float* w, const float* b, float eps, float momentum,
                       float* run_mean, float* run_var, float* save_mean, float* save_invstd, float* scale, float* shift,
-                      int relu, int64_t* nbt, void* fin_state, hipStream_t s) {
+                      int relu, int64_t* nbt, void* fin_state, hipStream_t s, const float* rscale = nullptr,
+                      const float* rshift = nullptr) {
   const Geo g = make_geo<T>(M, C, kTargetBlocks);
+  if (rscale) fin_state = nullptr;
   const FinSync fs = make_fin(fin_state, g, C, s);
   const FwdFin ff{psum, psq, gy, w, b, eps, momentum, run_mean, run_var, save_mean, save_invstd, scale, shift, nbt};
   if (!fs.ticket)
     hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(kBlock), 0, s, psum, psq, gy, M, C, w,
                        b, eps, momentum, run_mean, run_var, save_mean, save_invstd, scale, shift, nbt);
-  launch_apply<T>(x, res, y, mask, M, C, g, scale, shift, relu, fs, ff, s);
+  launch_apply<T>(x, res, y, mask, M, C, g, scale, shift, relu, fs, ff, s, rscale, rshift);
 }
 
 void bn_act_forward_pre(const void* x, const void* res, void* y, uint8_t* mask, int64_t M, int C, int elem_bytes,
                         const float* psum, const float* psq, int gy, const float* w, const float* b, float eps, float momentum,
                         float* run_mean, float* run_var, float* save_mean, float* save_invstd, float* scale,
-                        float* shift, int relu, int64_t* nbt, hipStream_t s, void* fin_state) {
+                        float* shift, int relu, int64_t* nbt, hipStream_t s, void* fin_state, const float* rscale,
+                        const float* rshift) {
   if (elem_bytes == 2)
     bn_forward_pre_t<uint16_t>((const uint16_t*)x, (const uint16_t*)res, (uint16_t*)y, mask, M, C, psum, psq, gy, w,
                                b, eps, momentum, run_mean, run_var, save_mean, save_invstd, scale, shift, relu, nbt,
-                               fin_state, s);
+                               fin_state, s, rscale, rshift);
   else
     bn_forward_pre_t<float>((const float*)x, (const float*)res, (float*)y, mask, M, C, psum, psq, gy, w, b, eps,
-                            momentum, run_mean, run_var, save_mean, save_invstd, scale, shift, relu, nbt, fin_state, s);
+                            momentum, run_mean, run_var, save_mean, save_invstd, scale, shift, relu, nbt, fin_state, s,
+                            rscale, rshift);
 }
 
 void bn_act_backward(const void* dy, const void* dy2, const uint8_t* mask, const void* x, void* dx, void* dres,

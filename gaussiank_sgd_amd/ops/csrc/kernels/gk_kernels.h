@@ -251,7 +251,17 @@ void bn_stats_partials(const void* x, int64_t M, int C, int elem_bytes, float* w
 void bn_act_forward(const void* x, const void* res, void* y, uint8_t* mask, int64_t M, int C, int elem_bytes,
                     const float* w, const float* b, float eps, float momentum, float* run_mean, float* run_var,
                     float* save_mean, float* save_invstd, float* scale, float* shift, float* ws, int relu,
-                    int64_t* nbt, hipStream_t stream, void* fin_state = nullptr);
+                    int64_t* nbt, hipStream_t stream, void* fin_state = nullptr, const float* rscale = nullptr,
+                    const float* rshift = nullptr);
+// rscale / rshift (optional, with res): the residual is a batch-normalised
+// tensor whose apply was deferred here -- res * rscale + rshift is added.
+// bn_act_finalize: the statistics (psum == nullptr: the stats pass over x;
+// else the producer's [gy][C] partials) and the finalize of a BN whose apply
+// pass is deferred into its consumer; no apply.
+void bn_act_finalize(const void* x, int64_t M, int C, int elem_bytes, const float* psum, const float* psq, int gy,
+                     const float* w, const float* b, float eps, float momentum, float* run_mean, float* run_var,
+                     float* save_mean, float* save_invstd, float* scale, float* shift, float* ws, int64_t* nbt,
+                     hipStream_t stream);
 // dy2 (optional): a second upstream gradient of the same output, summed on load.
 // bn_act_forward with the batch statistics already reduced to per-row
 // partials (psum / psq: [gy][C] each), e.g. by the producing
@@ -259,7 +269,8 @@ void bn_act_forward(const void* x, const void* res, void* y, uint8_t* mask, int6
 void bn_act_forward_pre(const void* x, const void* res, void* y, uint8_t* mask, int64_t M, int C, int elem_bytes,
                         const float* psum, const float* psq, int gy, const float* w, const float* b, float eps, float momentum,
                         float* run_mean, float* run_var, float* save_mean, float* save_invstd, float* scale,
-                        float* shift, int relu, int64_t* nbt, hipStream_t stream, void* fin_state = nullptr);
+                        float* shift, int relu, int64_t* nbt, hipStream_t stream, void* fin_state = nullptr,
+                        const float* rscale = nullptr, const float* rshift = nullptr);
 // dz and its [2][gy][C] partials sum(dz), sum(dz * x) come from a grad-input
 // GEMM's BatchNorm-backward epilogue (BnBwdArgs below); finalize (centring
 // with the mean) + apply only.  bf16 (elem_bytes 2) or fp32 (4).

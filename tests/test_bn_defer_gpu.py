@@ -1,0 +1,95 @@
+"""Deferred shortcut BN (ops/bn.py _BNDeferFn, bn_act.hip bn_apply_kernel RBN):
+relu(bn3(y3) + bn_ds(y_ds)) with the shortcut BN's apply folded into the last
+BN's apply pass, vs an fp32 torch reference of the same two BNs; and a ResNet
+downsample block with the deferral on vs off."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from gaussiank_sgd_amd.ops import bn as bn_mod
+from gaussiank_sgd_amd.ops.bn import BNAct
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(8, 256, 14, 14), (4, 512, 7, 7), (2, 2048, 3, 3), (3, 96, 5, 5)])
+def test_deferred_residual_bn_matches_torch(cuda, dtype, shape):
+    torch.manual_seed(0)
+    N, C, H, W = shape
+    bn3, bnd = BNAct(C, act="relu").to(cuda), BNAct(C).to(cuda)
+    r3, rd = torch.nn.BatchNorm2d(C).to(cuda), torch.nn.BatchNorm2d(C).to(cuda)
+    with torch.no_grad():
+        for m, r in ((bn3, r3), (bnd, rd)):
+            m.weight.uniform_(0.5, 1.5)
+            m.bias.uniform_(-0.5, 0.5)
+            r.weight.copy_(m.weight)
+            r.bias.copy_(m.bias)
+    cl = torch.channels_last
+    a0 = (torch.randn(shape, device=cuda) * 2 + 0.3).to(dtype).contiguous(memory_format=cl)
+    b0 = (torch.randn(shape, device=cuda) * 1.5 - 0.2).to(dtype).contiguous(memory_format=cl)
+    g0 = torch.randn(shape, device=cuda).to(dtype).contiguous(memory_format=cl)
+    a = a0.clone().requires_grad_(True)
+    b = b0.clone().requires_grad_(True)
+    h = bnd.deferred(b)
+    assert h is not None and hasattr(h, "_gk_pending_bn")
+    y = bn3(a, h)
+    y.backward(g0)
+    ar = a0.float().clone().requires_grad_(True)
+    br = b0.float().clone().requires_grad_(True)
+    yr = F.relu(r3(ar) + rd(br))
+    yr.backward(g0.float())
+    bf = dtype == torch.bfloat16
+    tol = dict(atol=3e-2, rtol=2e-2) if bf else dict(atol=1e-4, rtol=1e-4)
+    gtol = dict(atol=6e-2, rtol=5e-2) if bf else dict(atol=1e-4, rtol=1e-4)
+    assert y.dtype == dtype and y.is_contiguous(memory_format=cl)
+    assert torch.allclose(y.float(), yr, **tol)
+    assert torch.allclose(a.grad.float(), ar.grad, **gtol)
+    assert torch.allclose(b.grad.float(), br.grad, **gtol)
+    ptol = dict(rtol=2e-2, atol=2e-1) if bf else dict(rtol=1e-4, atol=1e-3)
+    for m, r in ((bn3, r3), (bnd, rd)):
+        assert torch.allclose(m.weight.grad, r.weight.grad, **ptol)
+        assert torch.allclose(m.bias.grad, r.bias.grad, **ptol)
+        assert torch.allclose(m.running_mean, r.running_mean, atol=1e-3, rtol=1e-3)
+        assert torch.allclose(m.running_var, r.running_var, atol=1e-3, rtol=1e-3)
+        assert int(m.num_batches_tracked) == 1
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_downsample_block_defer_on_off(cuda, dtype, monkeypatch):
+    """ResNet-50 layer-2 entry block (stride-2 downsample): output, input
+    gradient and every parameter gradient with the deferred shortcut BN equal
+    the two-pass form (fp32 to rounding; bf16 within the rounding of the
+    intermediate shortcut tensor the deferred form never stores)."""
+    from gaussiank_sgd_amd.models.resnet_imagenet import Bottleneck, ConvBN, conv1x1
+    torch.manual_seed(0)
+    ds = ConvBN(conv1x1(256, 512, 2), BNAct(512))
+    blk = Bottleneck(256, 128, 2, ds).to(cuda).to(memory_format=torch.channels_last)
+    x0 = torch.randn(8, 256, 28, 28, device=cuda).contiguous(memory_format=torch.channels_last)
+    g0 = torch.randn(8, 512, 14, 14, device=cuda).contiguous(memory_format=torch.channels_last)
+    outs = []
+    for defer in (True, False):
+        monkeypatch.setattr(bn_mod, "_DEFER", defer)
+        blk.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dtype == torch.bfloat16):
+            y = blk(x)
+        y.float().backward(g0)
+        outs.append((y.detach().float(), x.grad.float(), [p.grad.detach().clone() for p in blk.parameters()]))
+    (y1, dx1, gp1), (y2, dx2, gp2) = outs
+    bf = dtype == torch.bfloat16
+    if not bf:
+        tol = dict(atol=1e-4, rtol=1e-4)
+        assert torch.allclose(y1, y2, **tol)
+        assert torch.allclose(dx1, dx2, **tol)
+        for a, b in zip(gp1, gp2):
+            assert float((a - b).abs().max()) / (float(b.abs().max()) + 1e-6) < 1e-4
+        return
+    # bf16: the two forms round differently (the deferred one never rounds the
+    # shortcut BN output to bf16), which moves a few ReLU decisions: compare norms
+    def rel(a, b):
+        return float((a.float() - b.float()).norm() / (b.float().norm() + 1e-12))
+    assert rel(y1, y2) < 1e-2, rel(y1, y2)
+    assert rel(dx1, dx2) < 3e-2, rel(dx1, dx2)
+    for a, b in zip(gp1, gp2):
+        assert rel(a, b) < 3e-2, rel(a, b)
