@@ -149,7 +149,8 @@ class _BNActFn(torch.autograd.Function):
         stats = torch.empty(4, C, dtype=torch.float32, device=x.device)
         ws = torch.empty(int(_ops().bn_workspace_floats(M, C, eb)), dtype=torch.float32, device=x.device)
         # a deferred residual BN (_BNDeferFn): residual = r * rscale + rshift formed on load
-        rscale, rshift = rbn if rbn is not None else (None, None)
+        rscale, rshift, dlink = rbn if rbn is not None else (None, None, None)
+        ctx.dlink = dlink
         if rbn is not None and (residual.dtype != x.dtype or not residual.is_contiguous(memory_format=_CL)):
             raise RuntimeError("deferred residual BN: the pending tensor must match x (dtype, channels-last)")
         if residual is not None and residual.dtype != x.dtype:
@@ -182,8 +183,8 @@ class _BNActFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, *grads):
         x, mask, weight, mean, invstd = ctx.saved_tensors
-        link, res_link, plink = ctx.link, ctx.res_link, ctx.plink
-        ctx.link = ctx.res_link = ctx.plink = None
+        link, res_link, plink, dlink = ctx.link, ctx.res_link, ctx.plink, ctx.dlink
+        ctx.link = ctx.res_link = ctx.plink = ctx.dlink = None
         gw, gb = ctx.direct if ctx.direct is not None else (None, None)
         lazy = _lazy_ok(x, plink) and ctx.needs_input_grad[0]
         if link is not None and link.part is not None:
@@ -201,6 +202,20 @@ class _BNActFn(torch.autograd.Function):
                 _ops().bn_bwd_lazy_pre(x, part, rows, weight, mean, invstd, g[0], g[1], coef, padz, padx, gw, gb)
                 plink.lazy = (dz, x, coef, padz, padx)
                 dx = dz
+            elif dlink is not None and ctx.needs_input_grad[1]:
+                # residual = a deferred BN: its backward in this apply pass too
+                dx = torch.empty_like(x, memory_format=_CL)
+                x2 = dlink.x
+                dx2 = torch.empty_like(x2, memory_format=_CL)
+                g2 = torch.empty(2, x2.shape[1], dtype=torch.float32, device=x.device)
+                ws2 = torch.empty(int(_ops().bn_workspace_floats(x2.numel() // x2.shape[1], x2.shape[1],
+                                                                 x2.element_size())),
+                                  dtype=torch.float32, device=x.device)
+                gw2, gb2 = dlink.direct if dlink.direct is not None else (None, None)
+                _ops().bn_act_backward_pre_dual(dz, x, dx, weight, mean, invstd, g[0], g[1], part, rows, gw, gb, x2,
+                                                dx2, dlink.weight, dlink.mean, dlink.invstd, g2[0], g2[1], ws2, gw2,
+                                                gb2)
+                dlink.dz, dlink.dx, dlink.g = dz, dx2, g2
             else:
                 dx = torch.empty_like(x, memory_format=_CL)
                 _ops().bn_act_backward_pre(dz, x, dx, weight, mean, invstd, g[0], g[1], part, rows, gw, gb, ctx.fin)
@@ -245,11 +260,27 @@ class _BNActFn(torch.autograd.Function):
         return (dx, dres, dgamma, dbeta) + (None,) * 14
 
 
+class DeferLink:
+    """Backward hand-off between a deferred BN (``_BNDeferFn``) and the fused BN
+    that applied it as its residual: when that BN's backward is linked (dz and
+    its partials from the consumer conv's GEMM epilogue) it also runs the
+    deferred BN's reduce + finalize and writes its dx in the SAME apply pass
+    (``bn_act_backward_pre_dual``: dz read once), leaving dx and the parameter
+    gradients here; the deferred BN's backward then returns them when its
+    incoming gradient is that dz."""
+
+    __slots__ = ("x", "weight", "mean", "invstd", "direct", "dz", "dx", "g")
+
+    def __init__(self, x, weight, mean, invstd, direct):
+        self.x, self.weight, self.mean, self.invstd, self.direct = x, weight, mean, invstd, direct
+        self.dz = self.dx = self.g = None
+
+
 class _BNDeferFn(torch.autograd.Function):
     """A plain BN (no ReLU, no residual) whose apply pass is deferred into its
     only consumer: the forward runs the statistics + finalize (running stats,
     saved mean / invstd, per-channel scale / shift) and returns a view of the
-    UN-normalised input tagged ``_gk_pending_bn = (scale, shift)``; the
+    UN-normalised input tagged ``_gk_pending_bn = (scale, shift, DeferLink)``; the
     consumer -- the block's last fused BN, which takes it as its residual --
     adds ``x * scale + shift`` on load (bn_act.hip ``bn_apply_kernel`` RBN).
     The BN output is never written: one streaming pass (read x, write y) less
@@ -262,7 +293,7 @@ class _BNDeferFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, stats, direct=None, nbt=None,
-                pre=None):
+                pre=None, dlink=None):
         # stats: fp32 [4, C] (mean, invstd, scale, shift), allocated by the caller, which
         # tags the returned handle with its scale / shift rows
         ctx.direct = direct
@@ -275,13 +306,27 @@ class _BNDeferFn(torch.autograd.Function):
         _ops().bn_act_finalize(x, weight, bias, running_mean, running_var, stats[0], stats[1], stats[2], stats[3], ws,
                                float(eps), float(momentum), nbt, pre_t, pre_rows)
         ctx.save_for_backward(x, weight, stats[0], stats[1])
+        ctx.dlink = dlink
         return x.view_as(x)
 
     @staticmethod
     def backward(ctx, dy):
         x, weight, mean, invstd = ctx.saved_tensors
+        dl, ctx.dlink = ctx.dlink, None
         if dy is None:
-            return (None,) * 11
+            return (None,) * 12
+        if dl is not None and dl.dx is not None and dl.dz is not None and dy.data_ptr() == dl.dz.data_ptr():
+            # computed by the consumer BN's dual apply pass
+            dx, g = dl.dx, dl.g
+            dl.dz = dl.dx = dl.g = None
+            if ctx.direct is not None:
+                return (dx,) + (None,) * 11
+            dgamma = g[0] if weight is not None and ctx.needs_input_grad[1] else None
+            dbeta = g[1] if ctx.needs_input_grad[2] else None
+            return (dx, dgamma, dbeta) + (None,) * 9
+        if dl is not None and dl.dx is not None:
+            # the dual pass already ran (and may have accumulated into the arena)
+            raise RuntimeError("deferred BN: the consumer's gradient reached the shortcut BN as another tensor")
         dy = dy.contiguous(memory_format=_CL)
         if dy.dtype != x.dtype:
             dy = dy.to(x.dtype)
@@ -294,13 +339,15 @@ class _BNDeferFn(torch.autograd.Function):
         dx = torch.empty_like(x, memory_format=_CL)
         _ops().bn_act_backward(dy, None, x, dx, None, weight, mean, invstd, g[0], g[1], ws, False, gw, gb, None, None)
         if ctx.direct is not None:
-            return (dx,) + (None,) * 10
+            return (dx,) + (None,) * 11
         dgamma = g[0] if weight is not None and ctx.needs_input_grad[1] else None
         dbeta = g[1] if ctx.needs_input_grad[2] else None
-        return (dx, dgamma, dbeta) + (None,) * 8
+        return (dx, dgamma, dbeta) + (None,) * 9
 
 
 _DEFER = os.environ.get("GKSGD_BN_DEFER", "1") != "0"
+# the deferred BN's backward in the consumer's linked apply pass (bn_act_backward_pre_dual)
+_DEFER_BWD = os.environ.get("GKSGD_BN_DEFER_BWD", "1") != "0"
 
 
 class _BNReLUPoolFn(torch.autograd.Function):
@@ -467,9 +514,11 @@ class BNAct(nn.BatchNorm2d):
         if stats is not None and stats[0].shape[2] != x.shape[1]:
             stats = None
         st = torch.empty(4, x.shape[1], dtype=torch.float32, device=x.device)
+        direct = getattr(self, "_gk_direct", None)
+        dlink = DeferLink(x, self.weight, st[0], st[1], direct) if _DEFER_BWD and torch.is_grad_enabled() else None
         out = _BNDeferFn.apply(x, self.weight, self.bias, self.running_mean, self.running_var, mom, self.eps, st,
-                               getattr(self, "_gk_direct", None), nbt, stats)
-        out._gk_pending_bn = (st[2], st[3])
+                               direct, nbt, stats, dlink)
+        out._gk_pending_bn = (st[2], st[3], dlink)
         return out
 
     def _fin_state(self, x: torch.Tensor) -> Optional[torch.Tensor]:

@@ -545,6 +545,39 @@ void bn_act_backward_pre(at::Tensor dz, at::Tensor x, at::Tensor dx, c10::option
                           fs);
 }
 
+// bn_act_backward_pre + the deferred residual BN of x2 (dx2 from the same apply pass)
+void bn_act_backward_pre_dual(at::Tensor dz, at::Tensor x, at::Tensor dx, c10::optional<at::Tensor> w, at::Tensor mean,
+                              at::Tensor invstd, at::Tensor dgamma, at::Tensor dbeta, at::Tensor part, int64_t rows,
+                              c10::optional<at::Tensor> gw_acc, c10::optional<at::Tensor> gb_acc, at::Tensor x2,
+                              at::Tensor dx2, c10::optional<at::Tensor> w2, at::Tensor mean2, at::Tensor invstd2,
+                              at::Tensor dgamma2, at::Tensor dbeta2, at::Tensor ws2,
+                              c10::optional<at::Tensor> gw2_acc, c10::optional<at::Tensor> gb2_acc) {
+  for (const at::Tensor* t : {&dz, &x, &dx, &x2, &dx2}) check_cl(*t, "dz / x / dx / x2 / dx2");
+  const int64_t C = channels_of(x);
+  const int64_t M = x.numel() / C;
+  for (const at::Tensor* t : {&dz, &dx, &x2, &dx2})
+    TORCH_CHECK(t->scalar_type() == x.scalar_type() && t->numel() == x.numel(),
+                "bn_act_backward_pre_dual: dz / x / dx / x2 / dx2 of one shape and dtype");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat, "bf16 or fp32");
+  const int eb = (int)x.element_size();
+  TORCH_CHECK(gk::bn_supported((int)C, eb), "channel count not supported by the fused kernel");
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() == 3 &&
+                  part.size(0) == 2 && part.size(2) == C && rows > 0 && rows <= part.size(1),
+              "part must be fp32 [2, rows, C] partials with 0 < rows <= part.size(1)");
+  for (const at::Tensor* t : {&mean, &invstd, &dgamma, &dbeta, &mean2, &invstd2, &dgamma2, &dbeta2})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->numel() >= C, "per-channel buffers: fp32[C]");
+  TORCH_CHECK(ws2.scalar_type() == at::kFloat && ws2.numel() >= (int64_t)gk::bn_workspace_floats(M, (int)C, eb),
+              "workspace too small");
+  c10::DeviceGuard guard(x.device());
+  const float* ps = part.data_ptr<float>();
+  gk::bn_act_backward_pre_dual(dz.data_ptr(), x.data_ptr(), dx.data_ptr(), M, (int)C, eb, opt_f32(w),
+                               mean.data_ptr<float>(), invstd.data_ptr<float>(), dgamma.data_ptr<float>(),
+                               dbeta.data_ptr<float>(), ps, ps + part.size(1) * C, (int)rows, opt_f32_mut(gw_acc),
+                               opt_f32_mut(gb_acc), x2.data_ptr(), dx2.data_ptr(), opt_f32(w2), mean2.data_ptr<float>(),
+                               invstd2.data_ptr<float>(), dgamma2.data_ptr<float>(), dbeta2.data_ptr<float>(),
+                               ws2.data_ptr<float>(), opt_f32_mut(gw2_acc), opt_f32_mut(gb2_acc), cur_stream(x));
+}
+
 // ---- lazy BN backward (bn_act.hip bn_bwd_finalize_lazy): no apply pass ----
 void check_lazy_out(const at::Tensor& x, int64_t C, const at::Tensor& coef, const at::Tensor& padz,
                     const at::Tensor& padx) {
@@ -1991,6 +2024,11 @@ TORCH_LIBRARY(gksgd, m) {
         "Tensor(e!) coef, Tensor(f!) padz, Tensor(g!) padx, Tensor(h!)? gw_acc=None, Tensor(i!)? gb_acc=None) -> ()");
   m.def("bn_lazy_apply(Tensor dz, Tensor x, Tensor(a!) dx, Tensor coef) -> ()");
   m.def("bn_stats_partials(Tensor x, Tensor(a!) ws) -> ()");
+  m.def(
+      "bn_act_backward_pre_dual(Tensor dz, Tensor x, Tensor(a!) dx, Tensor? w, Tensor mean, Tensor invstd, "
+      "Tensor(b!) dgamma, Tensor(c!) dbeta, Tensor part, int rows, Tensor(d!)? gw_acc, Tensor(e!)? gb_acc, Tensor x2, "
+      "Tensor(f!) dx2, Tensor? w2, Tensor mean2, Tensor invstd2, Tensor(g!) dgamma2, Tensor(h!) dbeta2, "
+      "Tensor(i!) ws2, Tensor(j!)? gw2_acc, Tensor(k!)? gb2_acc) -> ()");
   m.def("bn_act_backward_pre(Tensor dz, Tensor x, Tensor(a!) dx, Tensor? w, Tensor mean, Tensor invstd, "
         "Tensor(b!) dgamma, Tensor(c!) dbeta, Tensor part, int rows, Tensor(d!)? gw_acc=None, "
         "Tensor(e!)? gb_acc=None, Tensor(f!)? fin=None) -> ()");
@@ -2080,6 +2118,7 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("bn_act_finalize", &bn_act_finalize);
   m.impl("bn_act_backward", &bn_act_backward);
   m.impl("bn_act_backward_pre", &bn_act_backward_pre);
+  m.impl("bn_act_backward_pre_dual", &bn_act_backward_pre_dual);
   m.impl("bn_bwd_lazy_pre", &bn_bwd_lazy_pre);
   m.impl("bn_act_backward_lazy", &bn_act_backward_lazy);
   m.impl("bn_lazy_apply", &bn_lazy_apply);

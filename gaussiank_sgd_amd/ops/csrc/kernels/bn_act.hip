@@ -805,7 +805,21 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_finalize_lazy_kernel(
   store_elem(padx + c, mu);
 }
 
-template <typename T, typename Src, bool DRES, bool FIN = false, int U = kBnUnroll>
+// DUAL: a second BN whose output gradient is the same dz (the deferred
+// ResNet shortcut BN, ops/bn.py _BNDeferFn: out = relu(bn3(x) + bn_ds(x2)))
+// gets its dx2 in the same pass -- dz is read once for both.
+template <typename T>
+struct BwdDual {
+  const T* x;
+  T* dx;
+  const float* w;
+  const float* mean;
+  const float* invstd;
+  const float* dbeta;
+  const float* dgamma;
+};
+
+template <typename T, typename Src, bool DRES, bool FIN = false, int U = kBnUnroll, bool DUAL = false>
 __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(Src src, const T* __restrict__ x, T* __restrict__ dx,
                                                               T* __restrict__ dres, int64_t M, int C, Geo g,
                                                               const float* __restrict__ w,
@@ -813,7 +827,8 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(Src src, const T* 
                                                               const float* __restrict__ invstd,
                                                               const float* __restrict__ dbeta,
                                                               const float* __restrict__ dgamma,
-                                                              FinSync fs = FinSync{}, BwdFin bf = BwdFin{}) {
+                                                              FinSync fs = FinSync{}, BwdFin bf = BwdFin{},
+                                                              BwdDual<T> d2 = BwdDual<T>{}) {
   constexpr int V = Vec<T>::N;
   const int tc = threadIdx.x % g.tpr;
   const int lane_r = threadIdx.x / g.tpr;
@@ -833,15 +848,29 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(Src src, const T* 
     k2[i] = (FIN ? ld_coh_f32(dbeta, c) : dbeta[c]) * invM;          // mean of dz
     k3[i] = (FIN ? ld_coh_f32(dgamma, c) : dgamma[c]) * invM;        // mean of dz * xhat
   }
+  constexpr int V2 = DUAL ? V : 1;
+  float mu2[V2], is2[V2], q1[V2], q2[V2], q3[V2];
+  if constexpr (DUAL) {
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      const int c = c0 + i;
+      mu2[i] = d2.mean[c];
+      is2[i] = d2.invstd[c];
+      q1[i] = (d2.w ? d2.w[c] : 1.f) * is2[i];
+      q2[i] = d2.dbeta[c] * invM;
+      q3[i] = d2.dgamma[c] * invM;
+    }
+  }
   const int64_t r0 = (int64_t)blockIdx.y * g.rows_per_block;
   int64_t r1 = r0 + g.rows_per_block;
   if (r1 > M) r1 = M;
-  struct Row { float d[V], xv[V]; };
+  struct Row { float d[V], xv[V], x2[V2]; };
   stream_rows<U, Row>(
       lane_r < g.rl ? r0 + lane_r : r1, r1, g.rl,
       [&](Row& w, int64_t r) {
         src.load(r, C, c0, w.d);
         Vec<T>::load(x + r * C + c0, w.xv);
+        if constexpr (DUAL) Vec<T>::load(d2.x + r * C + c0, w.x2);
       },
       [&](const Row& w, int64_t r) {
         float o[V];
@@ -852,6 +881,15 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(Src src, const T* 
         }
         Vec<T>::store(dx + r * C + c0, o);
         if (DRES) Vec<T>::store(dres + r * C + c0, w.d);
+        if constexpr (DUAL) {
+          float o2[V];
+#pragma unroll
+          for (int i = 0; i < V; ++i) {
+            const float xh = (w.x2[i] - mu2[i]) * is2[i];
+            o2[i] = q1[i] * (w.d[i] - q2[i] - xh * q3[i]);
+          }
+          Vec<T>::store(d2.dx + r * C + c0, o2);
+        }
       });
 }
 
@@ -1351,6 +1389,48 @@ void bn_lazy_apply(const void* dz, const void* x, void* dx, int64_t M, int C, in
     hipLaunchKernelGGL(bn_lazy_apply_kernel<float>, dim3(g.gx, g.gy), dim3(kBlock), 0, s, (const float*)dz,
                        (const float*)x, (float*)dx, M, C, g, reinterpret_cast<const float4*>(coef));
   }
+}
+
+// Linked backward (dz + partials from the consumer's GEMM epilogue) of a BN
+// whose residual was a deferred BN of x2 (bn_apply_kernel RBN): the second
+// BN's reduce pass over (dz, x2) and both finalizes, then ONE apply pass
+// writing dx and dx2 (dz read once).
+template <typename T>
+void bn_bwd_pre_dual_t(const T* dz, const T* x, T* dx, int64_t M, int C, const float* w, const float* mean,
+                       const float* invstd, float* dgamma, float* dbeta, const float* pdb, const float* pdg, int gy,
+                       float* gw_acc, float* gb_acc, const T* x2, T* dx2, const float* w2, const float* mean2,
+                       const float* invstd2, float* dgamma2, float* dbeta2, float* ws2, float* gw2_acc,
+                       float* gb2_acc, hipStream_t s) {
+  const Geo g = make_geo<T>(M, C, kTargetBlocks);
+  float* pdb2 = ws2;
+  float* pdg2 = ws2 + (int64_t)g.gy * C;
+  using Src = DyPlain<T, false, false>;
+  const Src src{dz, nullptr, nullptr};
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, Src>), dim3(g.gx, g.gy), dim3(kBlock), 0, s, src, x2, M, C, g, mean2,
+                     invstd2, pdb2, pdg2, (T*)nullptr);
+  const dim3 fg((C + kFinC - 1) / kFinC);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, fg, dim3(kBlock), 0, s, pdb2, pdg2, g.gy, C, dbeta2, dgamma2, gb2_acc,
+                     gw2_acc, nullptr, nullptr);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, fg, dim3(kBlock), 0, s, pdb, pdg, gy, C, dbeta, dgamma, gb_acc, gw_acc,
+                     mean, invstd);
+  const BwdDual<T> d2{x2, dx2, w2, mean2, invstd2, dbeta2, dgamma2};
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, Src, false, false, kBnUnroll, true>), dim3(g.gx, g.gy), dim3(kBlock), 0,
+                     s, src, x, dx, (T*)nullptr, M, C, g, w, mean, invstd, dbeta, dgamma, FinSync{}, BwdFin{}, d2);
+}
+
+void bn_act_backward_pre_dual(const void* dz, const void* x, void* dx, int64_t M, int C, int elem_bytes,
+                              const float* w, const float* mean, const float* invstd, float* dgamma, float* dbeta,
+                              const float* pdb, const float* pdg, int gy, float* gw_acc, float* gb_acc, const void* x2,
+                              void* dx2, const float* w2, const float* mean2, const float* invstd2, float* dgamma2,
+                              float* dbeta2, float* ws2, float* gw2_acc, float* gb2_acc, hipStream_t s) {
+  if (elem_bytes == 2)
+    bn_bwd_pre_dual_t<uint16_t>((const uint16_t*)dz, (const uint16_t*)x, (uint16_t*)dx, M, C, w, mean, invstd, dgamma,
+                                dbeta, pdb, pdg, gy, gw_acc, gb_acc, (const uint16_t*)x2, (uint16_t*)dx2, w2, mean2,
+                                invstd2, dgamma2, dbeta2, ws2, gw2_acc, gb2_acc, s);
+  else
+    bn_bwd_pre_dual_t<float>((const float*)dz, (const float*)x, (float*)dx, M, C, w, mean, invstd, dgamma, dbeta, pdb,
+                             pdg, gy, gw_acc, gb_acc, (const float*)x2, (float*)dx2, w2, mean2, invstd2, dgamma2,
+                             dbeta2, ws2, gw2_acc, gb2_acc, s);
 }
 
 void bn_act_backward_pre(const void* dz, const void* x, void* dx, int64_t M, int C, int elem_bytes, const float* w,

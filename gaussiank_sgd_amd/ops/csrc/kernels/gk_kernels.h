@@ -290,6 +290,14 @@ void bn_act_backward_lazy(const void* dy, const void* dy2, const uint8_t* mask, 
                           void* padz, void* padx, hipStream_t stream);
 void bn_lazy_apply(const void* dz, const void* x, void* dx, int64_t M, int C, int elem_bytes, const float* coef,
                    hipStream_t stream);
+// bn_act_backward_pre of a BN whose residual was the deferred BN of x2
+// (bn_act_forward rscale / rshift): also that BN's reduce (over dz, x2) and
+// finalize, and its dx2 written by the same apply pass; ws2 >= bn_workspace_floats.
+void bn_act_backward_pre_dual(const void* dz, const void* x, void* dx, int64_t M, int C, int elem_bytes,
+                              const float* w, const float* mean, const float* invstd, float* dgamma, float* dbeta,
+                              const float* pdb, const float* pdg, int gy, float* gw_acc, float* gb_acc, const void* x2,
+                              void* dx2, const float* w2, const float* mean2, const float* invstd2, float* dgamma2,
+                              float* dbeta2, float* ws2, float* gw2_acc, float* gb2_acc, hipStream_t stream);
 void bn_act_backward_pre(const void* dz, const void* x, void* dx, int64_t M, int C, int elem_bytes, const float* w,
                          const float* mean, const float* invstd, float* dgamma, float* dbeta, const float* pdb,
                          const float* pdg, int gy, float* gw_acc, float* gb_acc, hipStream_t stream,

@@ -93,3 +93,43 @@ def test_downsample_block_defer_on_off(cuda, dtype, monkeypatch):
     assert rel(dx1, dx2) < 3e-2, rel(dx1, dx2)
     for a, b in zip(gp1, gp2):
         assert rel(a, b) < 3e-2, rel(a, b)
+
+
+def _resnet50_grads(cuda, monkeypatch, defer, defer_bwd, bf16):
+    from gaussiank_sgd_amd.models import resnet50
+    torch.manual_seed(0)
+    net = resnet50(num_classes=10).to(cuda).to(memory_format=torch.channels_last)
+    x0 = torch.randn(4, 3, 96, 96, device=cuda).contiguous(memory_format=torch.channels_last)
+    t = torch.randint(0, 10, (4,), device=cuda)
+    monkeypatch.setattr(bn_mod, "_DEFER", defer)
+    monkeypatch.setattr(bn_mod, "_DEFER_BWD", defer_bwd)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=bf16):
+        loss = F.cross_entropy(net(x0), t)
+    loss.backward()
+    return float(loss), torch.cat([p.grad.detach().float().flatten() for p in net.parameters()])
+
+
+def test_resnet50_defer_linked_fp32(cuda, monkeypatch):
+    """Whole ResNet-50 (the model's BN links set, so the block-output BN of
+    each downsample block runs the linked backward with the dual apply pass):
+    loss and every parameter gradient with the deferral (forward + backward)
+    equal the two-pass shortcut BN."""
+    l1, g1 = _resnet50_grads(cuda, monkeypatch, True, True, False)
+    l2, g2 = _resnet50_grads(cuda, monkeypatch, False, False, False)
+    assert abs(l1 - l2) <= 1e-4 * max(1.0, abs(l2))
+    rel = float((g1 - g2).norm() / g2.norm())
+    assert rel < 1e-3, rel
+
+
+def test_resnet50_defer_linked_bf16(cuda, monkeypatch):
+    """bf16: the forms round differently, and a whole ResNet-50 at batch 4
+    amplifies that -- so each is compared with the fp32 gradient: the deferred
+    forms' error must be no worse than the two-pass form's (x1.5 + 0.05)."""
+    _, ref = _resnet50_grads(cuda, monkeypatch, False, False, False)
+    errs = {}
+    for tag, d, db in (("two-pass", False, False), ("defer-fwd", True, False), ("defer", True, True)):
+        _, g = _resnet50_grads(cuda, monkeypatch, d, db, True)
+        errs[tag] = float((g - ref).norm() / ref.norm())
+    print(errs)
+    for tag in ("defer-fwd", "defer"):
+        assert errs[tag] <= 1.5 * errs["two-pass"] + 0.05, errs
