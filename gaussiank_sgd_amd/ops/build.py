@@ -63,6 +63,7 @@ HIP_SOURCES = [
     "kernels/embed.hip",
     "kernels/xent.hip",
     "kernels/winograd.hip",
+    "kernels/wino_x6.hip",
     "kernels/stem_f32.hip",
     "kernels/prep.hip",
 ]
@@ -71,6 +72,7 @@ CXX_SOURCES = [
     "bindings.cpp",
 ]
 HEADERS = ["kernels/common.h", "kernels/gk_kernels.h", "kernels/mfma_util.h", "kernels/gemm_kern.h",
+           "kernels/wino_x6_common.h",
            "comm/rccl_engine.h"]
 # per-file extra flags: the sparse aggregation must round product and sum
 # separately (bit-identical to the reference arithmetic and the CPU mirror)

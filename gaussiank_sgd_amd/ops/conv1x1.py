@@ -48,7 +48,7 @@ _choices: Dict[tuple, tuple] = {}
 # of its time (GKSGD_GK_MARGIN, default 5%: the fp32 implicit-GEMM kernels
 # trail MIOpen's by 1-5% on some 3x3 shapes -- kept, so the fp32 step runs on
 # code this package owns; 0 = fastest wins)
-_OWN = ("hip", "w3", "mat", "wino")
+_OWN = ("hip", "w3", "mat", "wino", "wx6")
 _GK_MARGIN = float(os.environ.get("GKSGD_GK_MARGIN", "0.05"))
 # convolution bias gradients through the fused column pass (GKSGD_CONV_BIAS_COLSUM=0: torch's reduction)
 _BIAS_COLSUM = os.environ.get("GKSGD_CONV_BIAS_COLSUM", "1") != "0"
@@ -308,6 +308,25 @@ def _wino_ok(dt: torch.dtype, k: int, s: int, C: int, K: int) -> bool:
     return _WINO and dt == torch.float32 and k == 3 and s == 1 and C % 8 == 0 and K % 64 == 0
 
 
+# bf16x6 Winograd (wino_x6.hip: the 16 element-wise GEMMs on v_mfma_f32_16x16x32_bf16
+# with split operands, fp32-accurate), offered beside the fp32-MFMA Winograd in the
+# bf16x6 fp32 matmul mode with GKSGD_WINO_X6=1.  Opt-in: measured 1.5-1.7x SLOWER
+# than the fp32-MFMA Winograd on every ResNet-50 bs512 shape (profiles/r06_wino_x6.txt:
+# 7.7 VALU per MFMA for the per-wave transform + split, and the per-wave patch loads
+# not hidden at one wave per SIMD)
+_WX6 = os.environ.get("GKSGD_WINO_X6", "0") == "1"
+
+
+def _wx6_ok(Ci: int, Co: int) -> bool:
+    return _WX6 and _x6() and Ci % 32 == 0 and Co % 32 == 0
+
+
+def _wino_tag(Ci: int, Co: int) -> tuple:
+    """Autotune-key suffix of a Winograd-eligible convolution (Ci -> Co as run):
+    the x6 candidates get their own tag so choices tuned without them are not reused."""
+    return ("wino", "wx6") if _wx6_ok(Ci, Co) else ("wino",)
+
+
 def _wino_shape_fits(N: int, H: int, W: int, C: int, K: int) -> bool:
     """Every operand a Winograd stride-1 3x3 kernel addresses through a 32-bit
     buffer descriptor is < 2^31 bytes: forward x [N, C, H, W] and y
@@ -336,6 +355,11 @@ def _wino_cands(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, flip: bool,
     blocks = -(-(N * ((H + 1) // 2) * ((W + 1) // 2)) // 64) * (out.shape[1] // 64)
     if blocks < 256:
         cands += [(("wino", sp, 0), (lambda sp=sp: run(0, sp))) for sp in (2, 4) if Ci % (8 * sp) == 0]
+    if _wx6_ok(Ci, out.shape[1]):
+        def run6(mb):
+            u3 = weight_prep.wino_x6_filter(w, flip, wp)
+            return g.wino_x6_conv(x, u3, out, mb, st, *bn)
+        cands += [(("wx6", 0, mb), (lambda mb=mb: run6(mb))) for mb in _WINO_GRIDS]
     return cands
 
 
@@ -387,11 +411,11 @@ def _fwd(x: torch.Tensor, w: torch.Tensor, s: int, stats_box=None, bias=None, wp
             g.bn_supported(K, x.element_size()):
         ws = torch.empty(int(g.bn_workspace_floats(M, K, x.element_size())), dtype=torch.float32, device=x.device)
     cands.append((("miopen", 0, 0), miopen))
-    ch = _pick(("fwd", N, C, H, W, K, k, s, st is not None) + _dkey(dt) + (("wino",) if wino else ()),
+    ch = _pick(("fwd", N, C, H, W, K, k, s, st is not None) + _dkey(dt) + (_wino_tag(C, K) if wino else ()),
                _forced(cands))
     if ch[0] == "miopen":
         return F.conv2d(x, w, b16, stride=s, padding=p).contiguous(memory_format=_CL)
-    if ch[0] == "wino":
+    if ch[0] in ("wino", "wx6"):
         rows = dict(cands)[ch]()
     else:
         rows = run(ch[1], ch[2])
@@ -459,7 +483,7 @@ def _dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, lz=None, plink=No
     ch = _pick(_dgrad_key(N, C, H, W, K, k, s, dt), _forced(cands))
     if ch[0] == "miopen":
         return miopen().contiguous(memory_format=_CL)
-    if ch[0] == "wino":
+    if ch[0] in ("wino", "wx6"):
         dict(cands)[ch]()
         return dx
     run(ch[1], ch[2])
@@ -480,7 +504,7 @@ def _lazy(make):
 
 def _dgrad_key(N, C, H, W, K, k, s, dt) -> tuple:
     wino = _wino_ok(dt, k, s, K, C) and _wino_shape_fits(N, H, W, C, K)
-    return ("dgrad", N, C, H, W, K, k, s) + _dkey(dt) + (("wino",) if wino else ())
+    return ("dgrad", N, C, H, W, K, k, s) + _dkey(dt) + (_wino_tag(K, C) if wino else ())
 
 
 def _dgrad_bn(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, link, lz=None, plink=None,
@@ -524,9 +548,9 @@ def _dgrad_bn(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, link, lz=None,
     else:
         if _wino_ok(dt, k, s, K, C) and _wino_shape_fits(N, H, W, C, K):
             cands += _wino_cands(dy, w, dz, True, st, (h, dy2, mask), wp=wp)
-            key = key + ("wino",)
+            key = key + _wino_tag(K, C)
         ch = _pick(key, _forced(cands))
-    if ch[0] == "wino":
+    if ch[0] in ("wino", "wx6"):
         rows = dict(cands)[ch]()
     else:
         rows = run(ch[1], ch[2])
@@ -544,7 +568,7 @@ def _bn_fusable(link, s: int, dgrad_key: tuple) -> bool:
     if link.h.dtype != dgrad_key_dtype(dgrad_key):
         return False
     ch = _choices.get(dgrad_key)
-    return ch is None or ch[0] in ("hip", "wino")
+    return ch is None or ch[0] in ("hip", "wino", "wx6")
 
 
 def dgrad_key_dtype(key: tuple) -> torch.dtype:

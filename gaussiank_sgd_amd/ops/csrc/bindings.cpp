@@ -1351,6 +1351,51 @@ int64_t wino_conv(at::Tensor x, at::Tensor u, at::Tensor y, int64_t max_blocks, 
   return r;
 }
 
+// bf16x6 Winograd (wino_x6.hip): u3 = bf16 [Ci/32 * 16 * 3 * Co * 32]
+void wino_x6_weights(at::Tensor w, at::Tensor u3, bool flip) {
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3 &&
+                  w.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "wino_x6_weights: w must be a channels-last fp32 [K, C, 3, 3] GPU tensor");
+  const int64_t K = w.size(0), C = w.size(1);
+  const int64_t Co = flip ? C : K, Ci = flip ? K : C;
+  TORCH_CHECK(Ci % 32 == 0 && Co % 32 == 0, "wino_x6_weights: input and output channels % 32");
+  TORCH_CHECK(u3.is_cuda() && u3.scalar_type() == at::kBFloat16 && u3.is_contiguous() && u3.numel() == 48 * K * C,
+              "wino_x6_weights: u3 must be a contiguous bf16 tensor of 48 * K * C elements");
+  c10::DeviceGuard guard(w.device());
+  gk::wino_x6_weights(w.data_ptr<float>(), reinterpret_cast<uint16_t*>(u3.data_ptr()), (int)Co, (int)Ci,
+                      flip ? 1 : 0, cur_stream(w));
+}
+
+int64_t wino_x6_conv(at::Tensor x, at::Tensor u3, at::Tensor y, int64_t max_blocks, c10::optional<at::Tensor> stats,
+                     c10::optional<at::Tensor> bn_h, c10::optional<at::Tensor> bn_dy2,
+                     c10::optional<at::Tensor> bn_mask) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.dim() == 4 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "wino_x6_conv: x must be a channels-last fp32 GPU tensor");
+  const int64_t N = x.size(0), Ci = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(y.is_cuda() && y.scalar_type() == at::kFloat && y.dim() == 4 &&
+                  y.is_contiguous(at::MemoryFormat::ChannelsLast) && y.size(0) == N && y.size(2) == H &&
+                  y.size(3) == W,
+              "wino_x6_conv: y must be a channels-last fp32 [N, Co, H, W] GPU tensor");
+  const int64_t Co = y.size(1);
+  TORCH_CHECK(Ci % 32 == 0 && Co % 32 == 0, "wino_x6_conv: Ci % 32 == 0 and Co % 32 == 0");
+  TORCH_CHECK(u3.is_cuda() && u3.scalar_type() == at::kBFloat16 && u3.is_contiguous() && u3.numel() == 48 * Ci * Co,
+              "wino_x6_conv: u3 must hold 48 * Ci * Co bf16 (wino_x6_weights)");
+  TORCH_CHECK(N * ((H + 1) / 2) * ((W + 1) / 2) < (int64_t(1) << 31) && x.numel() > 0 &&
+                  x.numel() * 4 < (int64_t(1) << 31) && y.numel() * 4 < (int64_t(1) << 31),
+              "wino_x6_conv: size out of range (input / output bytes < 2^31: buffer-descriptor addressing)");
+  int rows = 0;
+  float* sp = stats_ptr(stats, Co, &rows);
+  gk::BnBwdArgs bn{};
+  const bool has_bn = bn_bwd_args(bn_h, bn_dy2, bn_mask, N * H * W, Co, Co, sp != nullptr, at::kFloat, &bn);
+  c10::DeviceGuard guard(x.device());
+  const int r = gk::wino_x6_conv(x.data_ptr<float>(), reinterpret_cast<const uint16_t*>(u3.data_ptr()),
+                                 y.data_ptr<float>(), (int)N, (int)H, (int)W, (int)Ci, (int)Co, (int)max_blocks, sp,
+                                 rows, has_bn ? &bn : nullptr, cur_stream(x));
+  TORCH_CHECK(r >= 0, "wino_x6_conv: configuration refused");
+  return r;
+}
+
 // out ([K, C, 3, 3] channels-last fp32) += dW of the 3x3 stride-1 convolution
 // x [N, C, H, W] -> dy [N, K, H, W] (channels-last fp32), Winograd F(2x2, 3x3);
 // part: >= wino_wgrad_ws(...) fp32 workspace
@@ -2014,6 +2059,9 @@ TORCH_LIBRARY(gksgd, m) {
   m.def("wino_wgrad(Tensor x, Tensor dy, Tensor(a!) out, Tensor(b!) part, int splits=0) -> ()");
   m.def("wino_conv(Tensor x, Tensor u, Tensor(a!) y, int max_blocks=0, Tensor(b!)? stats=None, Tensor? bn_h=None, "
         "Tensor? bn_dy2=None, Tensor? bn_mask=None, int splits=1) -> int");
+  m.def("wino_x6_weights(Tensor w, Tensor(a!) u3, bool flip) -> ()");
+  m.def("wino_x6_conv(Tensor x, Tensor u3, Tensor(a!) y, int max_blocks=0, Tensor(b!)? stats=None, "
+        "Tensor? bn_h=None, Tensor? bn_dy2=None, Tensor? bn_mask=None) -> int");
   m.def("conv_dgrad_s2(Tensor dy, Tensor w, Tensor(a!) dx, Tensor zero, int cfg=0, int max_blocks=0, "
         "Tensor? lz_x=None, Tensor? lz_coef=None, Tensor? lz_padz=None, Tensor? lz_padx=None) -> ()");
   m.def("bn_bwd_lazy_pre(Tensor x, Tensor part, int rows, Tensor? w, Tensor mean, Tensor invstd, "
@@ -2143,6 +2191,8 @@ TORCH_LIBRARY_IMPL(gksgd, CUDA, m) {
   m.impl("wino_weights", &wino_weights);
   m.impl("weight_prep", &weight_prep);
   m.impl("wino_conv", &wino_conv);
+  m.impl("wino_x6_weights", &wino_x6_weights);
+  m.impl("wino_x6_conv", &wino_x6_conv);
   m.impl("wino_wgrad", &wino_wgrad);
   m.impl("conv_tn_acc", &conv_tn_acc);
   m.impl("attn_fwd", &attn_fwd);

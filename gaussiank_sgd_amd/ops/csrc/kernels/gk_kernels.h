@@ -428,7 +428,9 @@ void wino_weights(const float* w, float* u, int Co, int Ci, int flip, hipStream_
 // as wino_weights); kPrepT32 / kPrepT16: out[s * ld_out + r] = in[r * ld_in + s]
 // for an R x S matrix of 4- / 2-byte elements (64 x 64 LDS tiles, tiles_s =
 // ceil(S / 64)).
-enum PrepKind : int32_t { kPrepWino = 0, kPrepWinoFlip = 1, kPrepT32 = 2, kPrepT16 = 3 };
+// kPrepWinoX6 / kPrepWinoX6Flip: the bf16x6 Winograd filter planes (wino_x6_weights).
+enum PrepKind : int32_t { kPrepWino = 0, kPrepWinoFlip = 1, kPrepT32 = 2, kPrepT16 = 3, kPrepWinoX6 = 4,
+                          kPrepWinoX6Flip = 5 };
 struct PrepDesc {
   const void* src;
   void* dst;
@@ -443,6 +445,13 @@ void weight_prep(const PrepDesc* descs, int ndesc, int64_t total_blocks, hipStre
 int wino_conv(const float* x, const float* u, float* y, int N, int H, int W, int Ci, int Co, int max_blocks,
               float* stats, int stats_rows, const BnBwdArgs* bn, hipStream_t stream, int splits = 1,
               float* split_ws = nullptr);
+// bf16x6 (fp32-accurate) Winograd (wino_x6.hip): u3 = the filter transform
+// split into three bf16 planes, [Ci/32][16][3][Co][32] (wino_x6_weights, flip
+// as wino_weights); wino_x6_conv as wino_conv with Ci % 32 == 0, Co % 32 == 0
+// (returns -1 otherwise).
+void wino_x6_weights(const float* w, uint16_t* u3, int Co, int Ci, int flip, hipStream_t stream);
+int wino_x6_conv(const float* x, const uint16_t* u3, float* y, int N, int H, int W, int Ci, int Co, int max_blocks,
+                 float* stats, int stats_rows, const BnBwdArgs* bn, hipStream_t stream);
 //   wino_wgrad  : out[K][3][3][C] (fp32, channels-last) += dW of the 3x3 stride-1
 //                 convolution x[N, H, W, C] -> dy[N, H, W, K] (C, K % 64 == 0);
 //                 part: wino_wgrad_splits(...) * 16 * K * C fp32 workspace

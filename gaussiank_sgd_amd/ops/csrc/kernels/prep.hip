@@ -19,6 +19,7 @@
 
 #include "common.h"
 #include "gk_kernels.h"
+#include "wino_x6_common.h"
 
 namespace gk {
 namespace {
@@ -103,6 +104,14 @@ __global__ void __launch_bounds__(kBlock) weight_prep_kernel(const PrepDesc* __r
   __syncthreads();
   const PrepDesc& d = sd[s_d];
   const int64_t unit = b - d.block_begin;
+  if (d.kind == kPrepWinoX6 || d.kind == kPrepWinoX6Flip) {
+    // bf16x6 Winograd filter planes (wino_x6.hip): consecutive threads, consecutive rows co
+    const int64_t idx = unit * kBlock + threadIdx.x;
+    if (idx < (int64_t)d.R * d.S)
+      wino_x6_pair(static_cast<const float*>(d.src), static_cast<uint16_t*>(d.dst), d.R, d.S,
+                   d.kind == kPrepWinoX6Flip, (int)(idx % d.R), (int)(idx / d.R));
+    return;
+  }
   if (d.kind == kPrepWino || d.kind == kPrepWinoFlip) {
     const int64_t idx = unit * kBlock + threadIdx.x;
     if (idx < (int64_t)d.R * d.S)
@@ -124,7 +133,8 @@ __global__ void __launch_bounds__(kBlock) weight_prep_kernel(const PrepDesc* __r
 }  // namespace
 
 int64_t weight_prep_blocks(int kind, int R, int S) {
-  if (kind == kPrepWino || kind == kPrepWinoFlip) return ((int64_t)R * S + kBlock - 1) / kBlock;
+  if (kind == kPrepWino || kind == kPrepWinoFlip || kind == kPrepWinoX6 || kind == kPrepWinoX6Flip)
+    return ((int64_t)R * S + kBlock - 1) / kBlock;
   return (int64_t)((R + kTile - 1) / kTile) * ((S + kTile - 1) / kTile);
 }
 

@@ -31,7 +31,7 @@ from typing import Callable, Dict, List, Optional, Tuple
 
 import torch
 
-KIND_WINO, KIND_WINO_FLIP, KIND_T32, KIND_T16 = 0, 1, 2, 3
+KIND_WINO, KIND_WINO_FLIP, KIND_T32, KIND_T16, KIND_WINO_X6, KIND_WINO_X6_FLIP = 0, 1, 2, 3, 4, 5
 _DESC = struct.Struct("<QQqqqiiii")      # gk::PrepDesc (gk_kernels.h): 56 bytes
 _MAX_DESCS = 512                          # prep.hip kMaxDescs (descriptor table in LDS)
 _tls = threading.local()
@@ -168,6 +168,27 @@ def wino_filter(w: torch.Tensor, flip: bool, persistent: bool) -> torch.Tensor:
     kind = KIND_WINO_FLIP if flip else KIND_WINO
     return p.acquire(_key("wino%d" % int(flip), w), w, make,
                      lambda u: [(kind, w.data_ptr(), u.data_ptr(), 0, 0, Co, Ci)], fill)
+
+
+def wino_x6_filter(w: torch.Tensor, flip: bool, persistent: bool) -> torch.Tensor:
+    """bf16x6 Winograd filter planes of the fp32 3x3 weight ``w`` ([K, C, 3, 3]
+    channels-last; ``flip``: of the grad-input filter) -- gksgd.wino_x6_weights."""
+    K, C = w.shape[0], w.shape[1]
+
+    def make():
+        return torch.empty(48 * K * C, dtype=torch.bfloat16, device=w.device)
+
+    def fill(u3):
+        _ops().wino_x6_weights(w, u3, flip)
+    p = current()
+    if p is None or not persistent:
+        u3 = make()
+        fill(u3)
+        return u3
+    Co, Ci = (C, K) if flip else (K, C)
+    kind = KIND_WINO_X6_FLIP if flip else KIND_WINO_X6
+    return p.acquire(_key("wx6%d" % int(flip), w), w, make,
+                     lambda u3: [(kind, w.data_ptr(), u3.data_ptr(), 0, 0, Co, Ci)], fill)
 
 
 def transposed_1x1(w: torch.Tensor, persistent: bool) -> torch.Tensor:
