@@ -112,13 +112,31 @@ def _resnet50_grads(cuda, monkeypatch, defer, defer_bwd, bf16):
 def test_resnet50_defer_linked_fp32(cuda, monkeypatch):
     """Whole ResNet-50 (the model's BN links set, so the block-output BN of
     each downsample block runs the linked backward with the dual apply pass):
-    loss and every parameter gradient with the deferral (forward + backward)
-    equal the two-pass shortcut BN."""
-    l1, g1 = _resnet50_grads(cuda, monkeypatch, True, True, False)
-    l2, g2 = _resnet50_grads(cuda, monkeypatch, False, False, False)
-    assert abs(l1 - l2) <= 1e-4 * max(1.0, abs(l2))
-    rel = float((g1 - g2).norm() / g2.norm())
-    assert rel < 1e-3, rel
+    the parameter-gradient error against an fp64 model with the deferral
+    (forward + backward) is no worse than the two-pass shortcut BN's.  (Two
+    fp32 runs are not compared with each other: the split-K grad-weight
+    atomics make run-to-run differences that a deep BN stack amplifies.)"""
+    from gaussiank_sgd_amd.models import resnet50
+    torch.manual_seed(0)
+    net = resnet50(num_classes=10).to(cuda).to(memory_format=torch.channels_last)
+    ref = resnet50(num_classes=10).to(cuda).double().to(memory_format=torch.channels_last)
+    ref.load_state_dict(net.state_dict())
+    for m in ref.modules():
+        if isinstance(m, BNAct):
+            m.fused = False
+    x0 = torch.randn(4, 3, 96, 96, device=cuda).contiguous(memory_format=torch.channels_last)
+    t = torch.randint(0, 10, (4,), device=cuda)
+    F.cross_entropy(ref(x0.double()), t).backward()
+    gref = torch.cat([p.grad.detach().flatten() for p in ref.parameters()])
+    errs = {}
+    for tag, d, db in (("two-pass", False, False), ("defer", True, True)):
+        monkeypatch.setattr(bn_mod, "_DEFER", d)
+        monkeypatch.setattr(bn_mod, "_DEFER_BWD", db)
+        net.zero_grad(set_to_none=True)
+        F.cross_entropy(net(x0), t).backward()
+        g = torch.cat([p.grad.detach().double().flatten() for p in net.parameters()])
+        errs[tag] = float((g - gref).norm() / gref.norm())
+    assert errs["defer"] <= 1.5 * errs["two-pass"] + 1e-4, errs
 
 
 def test_resnet50_defer_linked_bf16(cuda, monkeypatch):
