@@ -322,7 +322,7 @@ def run_phase(args, ph: Phase, steps: int, warmup: int, P: int, graph: Optional[
     opt._collect_selected()  # drop warm-up counts
     if opt._exchanger is not None:
         opt._exchanger.reset_stats()   # shared communicator: count this phase's timed loop only
-    state["mark"] = not graph
+    state["mark"] = not graph and os.environ.get("GKSGD_BENCH_NO_MARKS", "0") != "1"
     comm.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()

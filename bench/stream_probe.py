@@ -24,7 +24,12 @@ amp = "bf16" if args.amp == "bf16" else "fp32"
 from gaussiank_sgd_amd import ops  # noqa: E402
 assert ops.load()
 torch.cuda.set_device(0)
-trainer, opt, _, _ = gb.build(args, amp, False, args.threshold, 1, 0)
+if args.threshold is None:
+    args.threshold = gb.DEFAULT_THRESHOLD.get(args.model, 524288000)
+from gaussiank_sgd_amd.ops import conv1x1  # noqa: E402
+conv1x1.set_f32_matmul(args.f32_matmul)
+ph = gb.build(args, amp, False, args.threshold, 1, 0, args.batch_size)
+trainer, opt = ph.trainer, ph.opt
 
 
 def step():

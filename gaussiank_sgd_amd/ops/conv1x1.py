@@ -490,6 +490,12 @@ def _dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, lz=None, plink=No
     return dx
 
 
+# grad-weight choices issued on the side stream (HIP kernels only: MIOpen's handle and
+# workspace follow the stream it was set up on); GKSGD_WGRAD_STREAM_WINO=0 keeps the
+# Winograd grad-weight inline
+_FORKABLE = ("hip", "w3") + (("wino",) if os.environ.get("GKSGD_WGRAD_STREAM_WINO", "1") == "1" else ())
+
+
 def _lazy(make):
     """Memoised weight re-layout: built on first use only, so a Winograd /
     MIOpen choice does not pay the transpose / flip copy it never reads."""
@@ -709,13 +715,12 @@ class _FastConvFn(torch.autograd.Function):
             sink.grad_view.is_contiguous(memory_format=_CL)
         wgrad_done = False
         if direct and lz is None and streams.enabled(x.device) and \
-                _choices.get(_wgrad_key(x, w, s), ("",))[0] in ("hip", "w3"):
+                _choices.get(_wgrad_key(x, w, s), ("",))[0] in _FORKABLE:
             sink.check()
             side = streams.fork(x.device)
             with torch.cuda.stream(side):
                 _wgrad_into(dy, x, w, s, sink.grad_view)
-            for t in (dy, x, w):
-                t.record_stream(side)
+            streams.hold(x.device, dy, x, w)    # alive until the side work is done / joined
             wgrad_done = True
         dx = None
         if ctx.needs_input_grad[0]:

@@ -38,6 +38,7 @@ import torch.nn.functional as F
 
 from . import accum_grad_, load, require_native
 from . import conv1x1 as _cv
+from . import streams
 
 _ENABLED = os.environ.get("GKSGD_FASTLINEAR", "1") != "0"
 
@@ -266,6 +267,21 @@ def _wgrad_into(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor) -> None:
         g.gemm_tn_acc(dy2, x2, out, ch[1], ch[2])
 
 
+def _wgrad_forkable(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
+    """Is this grad-weight's tuned choice a HIP kernel (direct or padded), so it
+    may run on the side stream (ops/streams.py)?  hipBLASLt choices stay on the
+    stream their handle / workspace belong to, untuned keys are timed inline."""
+    if not streams.enabled(dy2.device):
+        return False
+    M, N = dy2.shape
+    K = x2.shape[1]
+    key = ("lin_wgrad", M, K, N) + _cv._dkey(dy2.dtype)
+    if not _hip_gemm_ok(K, N):
+        key = key + ("pad",)
+    ch = _cv._choices.get(key)
+    return ch is not None and ch[0] == "hip"
+
+
 def _target(sink) -> Optional[torch.Tensor]:
     """The fp32 arena gradient view a shadow sink accumulates into (None: no direct path)."""
     if sink is None:
@@ -332,7 +348,13 @@ class _LinearFn(torch.autograd.Function):
         gweight = None
         if ctx.needs_input_grad[1]:
             gw = _target(ctx.wsink)
-            if gw is not None:
+            if gw is not None and _wgrad_forkable(dpre, x2):
+                # off the critical path: the grad-weight only feeds the optimizer
+                side = streams.fork(dpre.device)
+                with torch.cuda.stream(side):
+                    _wgrad_into(dpre, x2, gw)
+                streams.hold(dpre.device, dpre, x2)
+            elif gw is not None:
                 _wgrad_into(dpre, x2, gw)
             else:
                 gw = torch.zeros(N, K, dtype=torch.float32, device=dy2.device)

@@ -43,7 +43,8 @@ import torch.nn.functional as F
 from . import load, require_native
 from .linear import _dgrad as _lin_dgrad
 from .linear import _fwd as _lin_fwd
-from .linear import _target, _wgrad_into, bias_grad_acc_
+from .linear import _target, _wgrad_forkable, _wgrad_into, bias_grad_acc_
+from . import streams
 
 
 def _g():
@@ -313,12 +314,18 @@ class _LSTMLayerFn(torch.autograd.Function):
             if own:
                 shape = (4 * H, x2.shape[1]) if k == 0 else ((4 * H, H) if k == 1 else (4 * H,))
                 tgt = torch.zeros(shape, dtype=torch.float32, device=dev)
-            if k == 0:
-                _wgrad_into(dG2, x2, tgt)
-            elif k == 1:
-                if h_prev is None:
+            if k < 2:
+                if k == 1 and h_prev is None:
                     h_prev = torch.cat([h0c.unsqueeze(0), out[:-1]]).view(T * B, H)
-                _wgrad_into(dG2, h_prev, tgt)
+                xk = x2 if k == 0 else h_prev
+                if not own and fast and _wgrad_forkable(dG2, xk):
+                    # on the side stream: overlaps the next layer's serial recurrence
+                    side = streams.fork(dev)
+                    with torch.cuda.stream(side):
+                        _wgrad_into(dG2, xk, tgt)
+                    streams.hold(dev, dG2, xk)
+                else:
+                    _wgrad_into(dG2, xk, tgt)
             else:
                 bias_grad_acc_(tgt, dG2)
             if own:

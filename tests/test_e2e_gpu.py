@@ -126,6 +126,7 @@ def test_wgrad_side_stream_matches_inline(cuda, monkeypatch, amp):
             t.train(1, data=(x, y))
             forked = forked or bool(streams._side)
             assert not streams.pending("cuda")       # joined at the end of backward
+            assert streams.held("cuda") == 0         # and the forked operands released
             t.update_model()
         torch.cuda.synchronize()
         if side == "1":
@@ -133,3 +134,36 @@ def test_wgrad_side_stream_matches_inline(cuda, monkeypatch, amp):
         results.append(opt.arena.weights.clone())
     err = (results[0] - results[1]).abs().max().item()
     assert err <= 1e-3 * results[1].abs().max().item(), err
+
+
+def test_wgrad_side_stream_pool_bounded(cuda, monkeypatch):
+    """With the host running steps ahead of the GPU (no synchronisation between
+    steps), the side stream's operands go back to the caching allocator in
+    stream order: the reserved pool stops growing after the first steps
+    (record_stream kept every forked block out of reuse while its free-time
+    event was pending and grew the pool by a step's operands per step until
+    allocations retried, r6c28 / r6c30)."""
+    monkeypatch.setenv("GKSGD_WGRAD_STREAM", "1")
+    torch.manual_seed(0)
+    comm.init()
+    # the headline shape (its tuned GEMM choices are committed): the GPU step (~100 ms)
+    # is longer than the host's, so the host runs ahead as in training
+    t = DLTrainer(0, 1, dnn="resnet50", dataset="imagenet", batch_size=512, lr=0.05, device="cuda",
+                  amp="none", channels_last=True, data_pool=2)
+    opt = DistributedOptimizer(t.optimizer, named_parameters=t.net.named_parameters(),
+                               compression=compressors["gaussian"], is_sparse=True, density=0.01,
+                               compress_single_rank=True, density_warmup=False)
+    from gaussiank_sgd_amd.parallel import install_direct_grads
+    install_direct_grads(t.net, opt)
+    t.update_optimizer(opt)
+    reserved = []
+    for i in range(12):
+        opt.zero_grad()
+        t.train(1)
+        t.update_model()
+        reserved.append(torch.cuda.memory_reserved())
+    torch.cuda.synchronize()
+    from gaussiank_sgd_amd.ops import streams
+    assert streams._side, "side stream never used"
+    assert torch.cuda.memory_stats().get("num_alloc_retries", 0) == 0
+    assert reserved[-1] <= reserved[3], [r >> 20 for r in reserved]

@@ -412,8 +412,8 @@ def test_winograd_split_candidates_small_grids_only():
 
 
 def test_wgrad_side_stream_policy(monkeypatch):
-    """ops/streams.py: the grad-weight side stream is off by default, forked
-    with GKSGD_WGRAD_STREAM=1 only (any other value, including round 4's
+    """ops/streams.py: the grad-weight side stream is on by default, off with
+    GKSGD_WGRAD_STREAM=0 (any value other than 1, including round 4's
     removed "auto", is off), never for a CPU tensor and never while a HIP
     graph is being captured."""
     import torch
@@ -421,7 +421,7 @@ def test_wgrad_side_stream_policy(monkeypatch):
     dev = torch.device("cuda")
     monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: False)
     monkeypatch.delenv("GKSGD_WGRAD_STREAM", raising=False)
-    assert not streams.enabled(dev)
+    assert streams.enabled(dev)
     monkeypatch.setenv("GKSGD_WGRAD_STREAM", "auto")
     assert not streams.enabled(dev)
     monkeypatch.setenv("GKSGD_WGRAD_STREAM", "1")
