@@ -271,10 +271,10 @@ def _wgrad_forkable(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
     """Is this grad-weight's tuned choice a HIP kernel (direct or padded), so it
     may run on the side stream (ops/streams.py)?  hipBLASLt choices stay on the
     stream their handle / workspace belong to, untuned keys are timed inline."""
-    if not streams.enabled(dy2.device):
-        return False
     M, N = dy2.shape
     K = x2.shape[1]
+    if not streams.worth(dy2.device, 2.0 * M * N * K):
+        return False
     key = ("lin_wgrad", M, K, N) + _cv._dkey(dy2.dtype)
     if not _hip_gemm_ok(K, N):
         key = key + ("pad",)

@@ -76,6 +76,21 @@ def enabled(device: torch.device) -> bool:
     return os.environ.get("GKSGD_WGRAD_STREAM", "1") == "1"
 
 
+# Forks of smaller grad-weights are not worth their host cost (an event query,
+# a stream wait and an event record per fork): a step whose grad-weights are
+# this small is launch-bound, and the fork made it slower and erratic -- ResNet-50
+# at the reference's batch of 32, eager: 15.2 / 20.7 ms per step forked vs 14.5 /
+# 15.9 inline (r6c32).  Every ResNet-50 bs512 grad-weight is >= 13 GFLOP, at bs32
+# <= 7.4 GFLOP (BERT seq512 bs32 linears >= 19, LSTM bs20 12.6, VGG-16 bs128 >= 9.6).
+# ``GKSGD_WGRAD_STREAM_MIN_GFLOP`` (default 8) sets the bound.
+
+
+def worth(device: torch.device, flops: float) -> bool:
+    """Fork a grad-weight of ``flops`` onto the side stream?  ``enabled`` and
+    large enough to pay for the fork."""
+    return flops >= float(os.environ.get("GKSGD_WGRAD_STREAM_MIN_GFLOP", "8")) * 1e9 and enabled(device)
+
+
 def _index(device) -> int:
     d = torch.device(device)
     return d.index if d.index is not None else torch.cuda.current_device()
@@ -93,6 +108,8 @@ def side_stream(device) -> "torch.cuda.Stream":
 def _reap(i: int) -> None:
     """Release held tensors whose side work has completed (in issue order)."""
     h = _held.get(i)
+    if h and torch.cuda.is_current_stream_capturing():
+        return      # events recorded in a capture cannot be queried (GKSGD_WGRAD_STREAM_GRAPH=1)
     while h and h[0][0].query():
         h.pop(0)
 

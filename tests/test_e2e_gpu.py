@@ -104,7 +104,8 @@ def test_wgrad_side_stream_matches_inline(cuda, monkeypatch, amp):
     atomic-accumulation order of the grad-weight kernels)."""
     from gaussiank_sgd_amd.ops import streams
     results = []
-    for side in ("1", "0"):   # forced on / off (default off, ops/streams.py)
+    monkeypatch.setenv("GKSGD_WGRAD_STREAM_MIN_GFLOP", "0")   # fork every grad-weight of this small batch
+    for side in ("1", "0"):   # forced on / off (default on, ops/streams.py)
         monkeypatch.setenv("GKSGD_WGRAD_STREAM", side)
         torch.manual_seed(0)
         comm.init()

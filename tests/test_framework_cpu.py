@@ -430,8 +430,15 @@ def test_wgrad_side_stream_policy(monkeypatch):
     monkeypatch.setenv("GKSGD_WGRAD_STREAM", "0")
     assert not streams.enabled(dev)
     monkeypatch.setenv("GKSGD_WGRAD_STREAM", "1")
+    # size gate: ResNet-50 grad-weights fork at bs512 (>= 13 GFLOP), not at bs32 (<= 7.4)
+    monkeypatch.delenv("GKSGD_WGRAD_STREAM_MIN_GFLOP", raising=False)
+    assert streams.worth(dev, 13.2e9) and not streams.worth(dev, 7.4e9)
+    assert not streams.worth(torch.device("cpu"), 1e12)
+    monkeypatch.setenv("GKSGD_WGRAD_STREAM_MIN_GFLOP", "0")
+    assert streams.worth(dev, 1.0)
     monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: True)
     assert not streams.enabled(dev)
+    assert not streams.worth(dev, 1e12)
 
 
 def test_cal_accuracy_top1_argmax_matches_topk():
