@@ -54,12 +54,28 @@ def main():
         p[1] += (e - s)
         p[2] = (gx // max(wx, 1), gy, gz, wx, vg, ag, lds)
     tot = sum(p[1] for p in per.values())
+    # concurrency (several streams, e.g. the grad-weight side stream): union of
+    # the kernel intervals vs their sum, over the counted window
+    busy, cur_s, cur_e = 0, None, None
+    for r in sorted(rows, key=lambda r: r[1]):
+        if cur_e is None or r[1] > cur_e:
+            if cur_e is not None:
+                busy += cur_e - cur_s
+            cur_s, cur_e = r[1], r[2]
+        else:
+            cur_e = max(cur_e, r[2])
+    if cur_e is not None:
+        busy += cur_e - cur_s
+    wall = (max(r[2] for r in rows) - min(r[1] for r in rows)) if rows else 0
     cats = collections.Counter()
     for n, p in per.items():
         cats[category(n)] += p[1]
     with open(a.out, "w") as f:
         f.write("# %s\n" % a.title)
         f.write("# total kernel time %.1f ms over %d steps = %.2f ms/step\n" % (tot / 1e6, a.steps, tot / 1e6 / a.steps))
+        f.write("# GPU wall %.2f ms/step, busy (union of kernel intervals) %.2f ms/step, kernel time run "
+                "concurrently with another kernel %.2f ms/step\n" % (wall / 1e6 / a.steps, busy / 1e6 / a.steps,
+                                                                     (tot - busy) / 1e6 / a.steps))
         f.write("category,ms_per_step,pct\n")
         for k, v in cats.most_common():
             f.write("%s,%.3f,%.1f\n" % (k, v / 1e6 / a.steps, 100.0 * v / tot))
