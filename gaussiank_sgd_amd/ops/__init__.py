@@ -60,6 +60,9 @@ def load(build_if_missing: bool = False) -> bool:
                 _b.build()
             torch.ops.load_library(str(_LIB))
             _loaded = True
+            if os.environ.get("GKSGD_BN_BLOCKS"):
+                # workgroups per BatchNorm streaming pass (bn_act.hip, default 1024)
+                torch.ops.gksgd.bn_set_blocks(int(os.environ["GKSGD_BN_BLOCKS"]))
         except BaseException as e:  # noqa: BLE001
             _load_error = e
     return _loaded
