@@ -714,7 +714,7 @@ class _FastConvFn(torch.autograd.Function):
         direct = sink is not None and getattr(sink, "grad_view", None) is not None and \
             sink.grad_view.is_contiguous(memory_format=_CL)
         wgrad_done = False
-        if direct and lz is None and \
+        if direct and lz is None and not getattr(sink, "shared", False) and \
                 streams.worth(x.device, 2.0 * dy.numel() * x.shape[1] * w.shape[2] * w.shape[3]) and \
                 _choices.get(_wgrad_key(x, w, s), ("",))[0] in _FORKABLE:
             sink.check()

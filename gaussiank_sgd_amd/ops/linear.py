@@ -348,7 +348,7 @@ class _LinearFn(torch.autograd.Function):
         gweight = None
         if ctx.needs_input_grad[1]:
             gw = _target(ctx.wsink)
-            if gw is not None and _wgrad_forkable(dpre, x2):
+            if gw is not None and not getattr(ctx.wsink, "shared", False) and _wgrad_forkable(dpre, x2):
                 # off the critical path: the grad-weight only feeds the optimizer
                 side = streams.fork(dpre.device)
                 with torch.cuda.stream(side):

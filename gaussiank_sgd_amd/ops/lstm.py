@@ -318,7 +318,7 @@ class _LSTMLayerFn(torch.autograd.Function):
                 if k == 1 and h_prev is None:
                     h_prev = torch.cat([h0c.unsqueeze(0), out[:-1]]).view(T * B, H)
                 xk = x2 if k == 0 else h_prev
-                if not own and fast and _wgrad_forkable(dG2, xk):
+                if not own and fast and not getattr(sink, "shared", False) and _wgrad_forkable(dG2, xk):
                     # on the side stream: overlaps the next layer's serial recurrence
                     side = streams.fork(dev)
                     with torch.cuda.stream(side):

@@ -73,6 +73,27 @@ def _linear_forward(self, x):
     return F.linear(x, w, b)
 
 
+def _mark_shared_sinks(model: nn.Module) -> None:
+    """A parameter that several modules hold (tied weights) has its gradient
+    accumulated by each of them into the same arena view: such sinks are
+    flagged ``shared`` so their grad-weight is never forked onto the side
+    stream (ops/streams.py), where it could race the other module's
+    accumulation on the main stream."""
+    uses = {}
+    for m in model.modules():
+        for p in m.parameters(recurse=False):
+            uses[id(p)] = uses.get(id(p), 0) + 1
+    for m in model.modules():
+        for attr in ("_gk_shadow", "_gk_direct_grads"):
+            table = getattr(m, attr, None)
+            if not table:
+                continue
+            for pname, entry in table.items():
+                sink = entry[1] if isinstance(entry, tuple) else entry
+                p = getattr(m, pname, None)
+                sink.shared = p is not None and uses.get(id(p), 0) > 1
+
+
 def install_bf16_shadow(model: nn.Module, opt) -> int:
     """Attach the shadow path to ``model``'s Conv2d / Linear / BNAct modules.
 
@@ -133,6 +154,7 @@ def install_bf16_shadow(model: nn.Module, opt) -> int:
                 kw, kb = names[mod.weight], names[mod.bias]
                 mod._gk_direct = (arena.grad_views[kw], arena.grad_views[kb])
                 count += 2
+    _mark_shared_sinks(model)
     opt.refresh_shadow()
     if not getattr(model, "_gk_shadow_hooked", False):
         # model.load_state_dict copies into the fp32 arena: keep the shadow in sync
@@ -183,4 +205,5 @@ def install_direct_grads(model: nn.Module, opt) -> int:
                     count += 1
             if table:
                 mod._gk_direct_grads = table
+    _mark_shared_sinks(model)
     return count

@@ -456,3 +456,29 @@ def test_cal_accuracy_top1_argmax_matches_topk():
     a1, = DLTrainer.cal_accuracy(None, out, tgt, topk=(1,))
     b1, b5 = DLTrainer.cal_accuracy(None, out, tgt, topk=(1, 5))
     assert abs(float(a1) - ref1) < 1e-4 and abs(float(b1) - ref1) < 1e-4 and abs(float(b5) - ref5) < 1e-4
+
+
+def test_tied_weight_sinks_never_fork():
+    """parallel/shadow.py: a parameter held by two modules (tied weights) gets
+    its direct-gradient sink flagged ``shared`` by both installers, so its
+    grad-weight is never forked onto the side stream (it would race the other
+    module's accumulation into the same arena view); untied sinks are not."""
+    import torch
+    import torch.nn as nn
+    from gaussiank_sgd_amd.ops.linear import FastLinear
+    from gaussiank_sgd_amd.parallel import comm, install_bf16_shadow, install_direct_grads
+    from gaussiank_sgd_amd.parallel.distributed_optimizer import DistributedOptimizer
+
+    comm.init()
+    for install in (install_direct_grads, install_bf16_shadow):
+        torch.manual_seed(0)
+        enc, dec, mid = FastLinear(16, 16), FastLinear(16, 16), FastLinear(16, 16)
+        dec.weight = enc.weight                      # tied
+        net = nn.Sequential(enc, mid, dec)
+        opt = DistributedOptimizer(torch.optim.SGD(net.parameters(), lr=0.1),
+                                   named_parameters=net.named_parameters(), compression=None)
+        assert install(net, opt) > 0
+        table = lambda m: getattr(m, "_gk_direct_grads", None) or getattr(m, "_gk_shadow")  # noqa: E731
+        sink = lambda e: e[1] if isinstance(e, tuple) else e  # noqa: E731
+        assert sink(table(enc)["weight"]).shared and sink(table(dec)["weight"]).shared
+        assert not sink(table(mid)["weight"]).shared and not sink(table(enc)["bias"]).shared
