@@ -492,8 +492,9 @@ def _dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, lz=None, plink=No
 
 # grad-weight choices issued on the side stream (HIP kernels only: MIOpen's handle and
 # workspace follow the stream it was set up on); GKSGD_WGRAD_STREAM_WINO=0 keeps the
-# Winograd grad-weight inline
-_FORKABLE = ("hip", "w3") + (("wino",) if os.environ.get("GKSGD_WGRAD_STREAM_WINO", "1") == "1" else ())
+# Winograd grad-weight inline, GKSGD_WGRAD_STREAM_KINDS restricts the forked choice kinds
+_FORKABLE = tuple(k for k in os.environ.get("GKSGD_WGRAD_STREAM_KINDS", "hip,w3,wino").split(",")
+                  if k and (k != "wino" or os.environ.get("GKSGD_WGRAD_STREAM_WINO", "1") == "1"))
 
 
 def _lazy(make):
