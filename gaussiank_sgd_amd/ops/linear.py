@@ -94,11 +94,23 @@ def _p64(n: int) -> int:
     return (n + 63) // 64 * 64
 
 
-def _pad2(t: torch.Tensor, rows: int, cols: int) -> torch.Tensor:
-    """Zero-padded contiguous copy of a 2-D tensor to [rows, cols] (one kernel)."""
+_PAD_SHARE = os.environ.get("GKSGD_LINEAR_PAD_SHARE", "1") == "1"
+
+
+def _pad2(t: torch.Tensor, rows: int, cols: int, cache: Optional[dict] = None) -> torch.Tensor:
+    """Zero-padded contiguous copy of a 2-D tensor to [rows, cols] (one kernel).
+    ``cache``: a dict scoped to one backward call (the tensor is not modified
+    inside it), so the grad-input and grad-weight GEMMs share one padded copy
+    of the output gradient."""
     r, c = t.shape
     if r == rows and c == cols and t.is_contiguous():
         return t
+    if cache is not None:
+        key = (t.data_ptr(), tuple(t.shape), tuple(t.stride()), t.dtype, rows, cols)
+        got = cache.get(key)
+        if got is None:
+            got = cache[key] = F.pad(t, (0, cols - c, 0, rows - r))
+        return got
     return F.pad(t, (0, cols - c, 0, rows - r))
 
 
@@ -163,7 +175,7 @@ def _fwd_padded(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor],
     return padded(ch[1], ch[2])
 
 
-def _dgrad_padded(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+def _dgrad_padded(dy2: torch.Tensor, w: torch.Tensor, pads: Optional[dict] = None) -> torch.Tensor:
     """dx = dy2 . w with K / N not multiples of 64 (see _fwd_padded)."""
     M, N = dy2.shape
     K = w.shape[1]
@@ -175,8 +187,8 @@ def _dgrad_padded(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     if got is not None and got[0] == "blas":
         return torch.mm(dy2, w)
 
-    def padded(c, mb):
-        dyp = _pad2(dy2, M, Np)
+    def padded(c, mb, cache=None):
+        dyp = _pad2(dy2, M, Np, cache)
         wtp = _pad2(w.t(), Kp, Np)
         dxp = torch.empty(M, Kp, dtype=dt, device=dy2.device)
         g.gemm_nt(dyp, wtp, dxp, c, mb)
@@ -186,18 +198,18 @@ def _dgrad_padded(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     ch = _cv._pick(key, cands)
     if ch[0] == "blas":
         return torch.mm(dy2, w)
-    return padded(ch[1], ch[2])
+    return padded(ch[1], ch[2], pads)
 
 
-def _dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """dx = dy2 . w in dy2's dtype."""
+def _dgrad(dy2: torch.Tensor, w: torch.Tensor, pads: Optional[dict] = None) -> torch.Tensor:
+    """dx = dy2 . w in dy2's dtype.  ``pads``: see _pad2."""
     M, N = dy2.shape
     K = w.shape[1]
     dt = dy2.dtype
     key = ("lin_dgrad", M, K, N) + _cv._dkey(dt)
     got = _cv._choices.get(key)
     if not _hip_gemm_ok(K, N) and _pad_ok(dy2):
-        return _dgrad_padded(dy2, w)
+        return _dgrad_padded(dy2, w, pads)
     if not _hip_gemm_ok(K, N) or (got is not None and got[0] == "blas"):
         return torch.mm(dy2, w)
     g = _g()
@@ -213,8 +225,8 @@ def _dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return dx
 
 
-def _wgrad_into(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor) -> None:
-    """out (fp32 [N, K]) += dy2^T . x2."""
+def _wgrad_into(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor, pads: Optional[dict] = None) -> None:
+    """out (fp32 [N, K]) += dy2^T . x2.  ``pads``: see _pad2."""
     M, N = dy2.shape
     K = x2.shape[1]
 
@@ -245,8 +257,8 @@ def _wgrad_into(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor) -> None:
         key = key + ("pad",)
         Kp, Np = _p64(K), _p64(N)
 
-        def padded(o, c, sp):
-            dyp = _pad2(dy2, M, Np)
+        def padded(o, c, sp, cache=None):
+            dyp = _pad2(dy2, M, Np, cache)
             xp = _pad2(x2, M, Kp)
             op = torch.zeros(Np, Kp, dtype=torch.float32, device=dy2.device)
             g.gemm_tn_acc(dyp, xp, op, c, sp)
@@ -262,7 +274,7 @@ def _wgrad_into(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor) -> None:
     elif ch[0] == "blas32":
         blas32(out)
     elif padded is not None:
-        padded(out, ch[1], ch[2])
+        padded(out, ch[1], ch[2], pads)
     else:
         g.gemm_tn_acc(dy2, x2, out, ch[1], ch[2])
 
@@ -344,7 +356,9 @@ class _LinearFn(torch.autograd.Function):
             dpre = dy2
             if db is not None:
                 bias_grad_acc_(db, dpre)
-        dx = _dgrad(dpre, w).view(ctx.in_shape) if ctx.needs_input_grad[0] else None
+        # one zero-padded copy of dpre for both GEMMs (K / N not multiples of 64)
+        pads = {} if _PAD_SHARE else None
+        dx = _dgrad(dpre, w, pads).view(ctx.in_shape) if ctx.needs_input_grad[0] else None
         gweight = None
         if ctx.needs_input_grad[1]:
             gw = _target(ctx.wsink)
@@ -352,13 +366,13 @@ class _LinearFn(torch.autograd.Function):
                 # off the critical path: the grad-weight only feeds the optimizer
                 side = streams.fork(dpre.device)
                 with torch.cuda.stream(side):
-                    _wgrad_into(dpre, x2, gw)
-                streams.hold(dpre.device, dpre, x2)
+                    _wgrad_into(dpre, x2, gw, pads)
+                streams.hold(dpre.device, dpre, x2, *(pads.values() if pads else ()))
             elif gw is not None:
-                _wgrad_into(dpre, x2, gw)
+                _wgrad_into(dpre, x2, gw, pads)
             else:
                 gw = torch.zeros(N, K, dtype=torch.float32, device=dy2.device)
-                _wgrad_into(dpre, x2, gw)
+                _wgrad_into(dpre, x2, gw, pads)
                 if ctx.wsink is not None:
                     ctx.wsink(gw)
                 else:
