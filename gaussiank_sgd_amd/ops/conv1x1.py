@@ -493,6 +493,8 @@ def _dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, lz=None, plink=No
 # grad-weight choices issued on the side stream (HIP kernels only: MIOpen's handle and
 # workspace follow the stream it was set up on); GKSGD_WGRAD_STREAM_WINO=0 keeps the
 # Winograd grad-weight inline, GKSGD_WGRAD_STREAM_KINDS restricts the forked choice kinds
+# GKSGD_WGRAD_AFTER_DGRAD=1: fork the grad-weight after the grad-input is issued
+_WGRAD_AFTER = os.environ.get("GKSGD_WGRAD_AFTER_DGRAD", "0") == "1"
 _FORKABLE = tuple(k for k in os.environ.get("GKSGD_WGRAD_STREAM_KINDS", "hip,w3,wino").split(",")
                   if k and (k != "wino" or os.environ.get("GKSGD_WGRAD_STREAM_WINO", "1") == "1"))
 
@@ -714,16 +716,18 @@ class _FastConvFn(torch.autograd.Function):
         sink = ctx.sink if ctx.needs_input_grad[1] else None
         direct = sink is not None and getattr(sink, "grad_view", None) is not None and \
             sink.grad_view.is_contiguous(memory_format=_CL)
-        wgrad_done = False
-        if direct and lz is None and not getattr(sink, "shared", False) and \
-                streams.worth(x.device, 2.0 * dy.numel() * x.shape[1] * w.shape[2] * w.shape[3]) and \
-                _choices.get(_wgrad_key(x, w, s), ("",))[0] in _FORKABLE:
+        fork = direct and lz is None and not getattr(sink, "shared", False) and \
+            streams.worth(x.device, 2.0 * dy.numel() * x.shape[1] * w.shape[2] * w.shape[3]) and \
+            _choices.get(_wgrad_key(x, w, s), ("",))[0] in _FORKABLE
+
+        def fork_wgrad():
             sink.check()
             side = streams.fork(x.device)
             with torch.cuda.stream(side):
                 _wgrad_into(dy, x, w, s, sink.grad_view)
             streams.hold(x.device, dy, x, w)    # alive until the side work is done / joined
-            wgrad_done = True
+        if fork and not _WGRAD_AFTER:
+            fork_wgrad()
         dx = None
         if ctx.needs_input_grad[0]:
             N, C, H, W = x.shape
@@ -734,8 +738,10 @@ class _FastConvFn(torch.autograd.Function):
                     dx = _dgrad_bn(dy, w, x.shape, s, link, lz, plink, wp=ctx.wp)
                 else:
                     dx = _dgrad(dy, w, x.shape, s, lz, plink, wp=ctx.wp)
+        if fork and _WGRAD_AFTER:
+            fork_wgrad()    # waits for the grad-input: overlaps the BN passes that follow it
         gparam = None
-        if ctx.needs_input_grad[1] and not wgrad_done:
+        if ctx.needs_input_grad[1] and not fork:
             if direct:
                 sink.check()
                 _wgrad_into(dy, x, w, s, sink.grad_view, lz, plink)
