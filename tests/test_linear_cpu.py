@@ -80,3 +80,21 @@ def test_split_heads_matches_permute_unbind():
     sum((o * g).sum() for o, g in zip(outs, gs)).backward()
     sum((r * g).sum() for r, g in zip(ref, gs)).backward()
     assert torch.equal(y.grad, y2.grad)
+
+
+def test_pad2_cache_shares_one_padded_copy():
+    """ops/linear.py _pad2: with a backward-scoped cache the grad-input and
+    grad-weight GEMMs get the SAME zero-padded copy (one fill + copy instead of
+    two); without it every call pads afresh; values match F.pad."""
+    import torch
+    import torch.nn.functional as F
+    from gaussiank_sgd_amd.ops.linear import _pad2
+    t = torch.randn(7, 10)
+    cache = {}
+    a = _pad2(t, 8, 64, cache)
+    b = _pad2(t, 8, 64, cache)
+    assert a is b and len(cache) == 1
+    assert torch.equal(a, F.pad(t, (0, 54, 0, 1)))
+    assert _pad2(t, 8, 128, cache) is not a and len(cache) == 2   # another target shape
+    assert _pad2(t, 8, 64) is not _pad2(t, 8, 64)                  # no cache: fresh copies
+    assert _pad2(a, 8, 64, cache) is a                             # already padded + contiguous
