@@ -490,10 +490,11 @@ def _dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, lz=None, plink=No
     return dx
 
 
-# grad-weight choices issued on the side stream (HIP kernels only: MIOpen's handle and
-# workspace follow the stream it was set up on); GKSGD_WGRAD_STREAM_WINO=0 keeps the
-# Winograd grad-weight inline, GKSGD_WGRAD_STREAM_KINDS restricts the forked choice kinds
-# GKSGD_WGRAD_AFTER_DGRAD=1: fork the grad-weight after the grad-input is issued
+# Grad-weight choices issued on the side stream (ops/streams.py; HIP kernels only: MIOpen's
+# handle and workspace follow the stream it was set up on).  GKSGD_WGRAD_STREAM_WINO=0 keeps
+# the Winograd grad-weight inline, GKSGD_WGRAD_STREAM_KINDS restricts the forked choice kinds
+# (only "wino": -3%, r6c43).  The fork is issued BEFORE the grad-input GEMM;
+# GKSGD_WGRAD_AFTER_DGRAD=1 issues it after (measured -1.4% fp32 / -1.5% bf16, r6c46).
 _WGRAD_AFTER = os.environ.get("GKSGD_WGRAD_AFTER_DGRAD", "0") == "1"
 _FORKABLE = tuple(k for k in os.environ.get("GKSGD_WGRAD_STREAM_KINDS", "hip,w3,wino").split(",")
                   if k and (k != "wino" or os.environ.get("GKSGD_WGRAD_STREAM_WINO", "1") == "1"))
