@@ -496,6 +496,9 @@ def _dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, s: int, lz=None, plink=No
 # (only "wino": -3%, r6c43).  The fork is issued BEFORE the grad-input GEMM;
 # GKSGD_WGRAD_AFTER_DGRAD=1 issues it after (measured -1.4% fp32 / -1.5% bf16, r6c46).
 _WGRAD_AFTER = os.environ.get("GKSGD_WGRAD_AFTER_DGRAD", "0") == "1"
+# GKSGD_WGRAD_SIDE_QROUNDS=q: a forked TN grad-weight whose tuned split is auto (two rounds
+# of the chip's block slots) launches q quarter rounds instead (0: unchanged)
+_SIDE_QROUNDS = int(os.environ.get("GKSGD_WGRAD_SIDE_QROUNDS", "0"))
 _FORKABLE = tuple(k for k in os.environ.get("GKSGD_WGRAD_STREAM_KINDS", "hip,w3,wino").split(",")
                   if k and (k != "wino" or os.environ.get("GKSGD_WGRAD_STREAM_WINO", "1") == "1"))
 
@@ -593,7 +596,7 @@ def _wgrad_key(x: torch.Tensor, w: torch.Tensor, s: int, lz=None) -> tuple:
 
 
 def _wgrad_into(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, s: int, out_f32: torch.Tensor, lz=None,
-                plink=None) -> None:
+                plink=None, side: bool = False) -> None:
     """out_f32 ([K, C, k, k] channels-last fp32) += dW.  ``lz``: dy is a lazy
     BN-backward dz (see _dgrad)."""
     N, C, H, W, K, k, p, OH, OW = _geom(x.shape, w, s)
@@ -657,7 +660,10 @@ def _wgrad_into(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, s: int, out_
     if ch[0] == "w3" and w3 is not None:
         w3(out_f32)
         return
-    run(out_f32, ch[1], ch[2])
+    sp = ch[2]
+    if side and sp == 0 and _SIDE_QROUNDS > 0:
+        sp = -_SIDE_QROUNDS     # a smaller auto grid beside the critical path (gemm_kern.h launch_tn*)
+    run(out_f32, ch[1], sp)
 
 
 class _FastConvFn(torch.autograd.Function):
@@ -725,7 +731,7 @@ class _FastConvFn(torch.autograd.Function):
             sink.check()
             side = streams.fork(x.device)
             with torch.cuda.stream(side):
-                _wgrad_into(dy, x, w, s, sink.grad_view)
+                _wgrad_into(dy, x, w, s, sink.grad_view, side=True)
             streams.hold(x.device, dy, x, w)    # alive until the side work is done / joined
         if fork and not _WGRAD_AFTER:
             fork_wgrad()

@@ -1370,7 +1370,10 @@ void launch_tn(const uint16_t* G, int64_t ldg, const uint16_t* X, int64_t ldx, f
     }();
     const int64_t bpc = Cfg::NW >= 8 ? 1 : 8 / Cfg::NW;
     const int64_t slots = (int64_t)cus * bpc;
-    splits = (int)(2 * slots / tiles);
+    // splits < 0: -splits quarter rounds (a grad-weight on the side stream that
+    // should leave CUs to the critical path); 0: two rounds
+    const int64_t quarters = splits == 0 ? 8 : -(int64_t)splits;
+    splits = (int)(quarters * slots / (4 * (int64_t)tiles));
     if (splits < 1) splits = 1;
   }
   int64_t rows = (M + splits - 1) / splits;
@@ -1657,7 +1660,9 @@ void launch_tn_f32(const float* G, int64_t ldg, const float* X, int64_t ldx, flo
     const int by_waves = 16 / Cfg::NW;
     if (bpc > by_waves) bpc = by_waves;
     if (bpc < 1) bpc = 1;
-    splits = (int)(2 * (int64_t)cus * bpc / tiles);
+    // splits < 0: -splits quarter rounds (see launch_tn); 0: two rounds
+    const int64_t quarters = splits == 0 ? 8 : -(int64_t)splits;
+    splits = (int)(quarters * (int64_t)cus * bpc / (4 * (int64_t)tiles));
     if (splits < 1) splits = 1;
   }
   int64_t rows = (M + splits - 1) / splits;
