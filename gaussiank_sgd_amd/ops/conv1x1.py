@@ -499,6 +499,9 @@ _WGRAD_AFTER = os.environ.get("GKSGD_WGRAD_AFTER_DGRAD", "0") == "1"
 # GKSGD_WGRAD_SIDE_QROUNDS=q: a forked TN grad-weight whose tuned split is auto (two rounds
 # of the chip's block slots) launches q quarter rounds instead (0: unchanged)
 _SIDE_QROUNDS = int(os.environ.get("GKSGD_WGRAD_SIDE_QROUNDS", "0"))
+# GKSGD_WGRAD_STREAM_BIAS=1: a forked convolution's bias gradient goes to the side stream with
+# its grad-weight (measured slower: VGG-16 bs512 76.4-77.1k vs 78.5k img/s on the main stream, r6c53)
+_FORK_BIAS = os.environ.get("GKSGD_WGRAD_STREAM_BIAS", "0") == "1"
 _FORKABLE = tuple(k for k in os.environ.get("GKSGD_WGRAD_STREAM_KINDS", "hip,w3,wino").split(",")
                   if k and (k != "wino" or os.environ.get("GKSGD_WGRAD_STREAM_WINO", "1") == "1"))
 
@@ -727,11 +730,22 @@ class _FastConvFn(torch.autograd.Function):
             streams.worth(x.device, 2.0 * dy.numel() * x.shape[1] * w.shape[2] * w.shape[3]) and \
             _choices.get(_wgrad_key(x, w, s), ("",))[0] in _FORKABLE
 
+        # the bias gradient (a column pass over dy into its arena view) rides along
+        bs0 = ctx.bias_sink if ctx.has_bias and ctx.needs_input_grad[6] else None
+        gvb = getattr(bs0, "grad_view", None) if bs0 is not None else None
+        bias_fork = fork and _FORK_BIAS and _BIAS_COLSUM and gvb is not None and gvb.is_contiguous() and \
+            not getattr(bs0, "shared", False) and dy.is_contiguous(memory_format=_CL)
+
         def fork_wgrad():
             sink.check()
+            if bias_fork:
+                bs0.check()
             side = streams.fork(x.device)
             with torch.cuda.stream(side):
                 _wgrad_into(dy, x, w, s, sink.grad_view, side=True)
+                if bias_fork:
+                    from .linear import bias_grad_acc_
+                    bias_grad_acc_(gvb, _rows(dy))
             streams.hold(x.device, dy, x, w)    # alive until the side work is done / joined
         if fork and not _WGRAD_AFTER:
             fork_wgrad()
@@ -760,7 +774,7 @@ class _FastConvFn(torch.autograd.Function):
                 else:
                     gparam = out.to(ctx.param_dtype)
         gbias = None
-        if ctx.has_bias and ctx.needs_input_grad[6]:
+        if ctx.has_bias and ctx.needs_input_grad[6] and not bias_fork:
             src = plink.materialize() if lz is not None else dy
             bs = ctx.bias_sink
             gv = getattr(bs, "grad_view", None) if bs is not None else None

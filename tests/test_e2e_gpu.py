@@ -96,12 +96,14 @@ def test_overlap_on_off_bitwise_deterministic(cuda, comp):
     assert torch.equal(results[0], results[1])
 
 
-@pytest.mark.parametrize("amp", ["none", "bf16"])
-def test_wgrad_side_stream_matches_inline(cuda, monkeypatch, amp):
+@pytest.mark.parametrize("amp,dnn", [("none", "resnet50"), ("bf16", "resnet50"), ("none", "vgg16")])
+def test_wgrad_side_stream_matches_inline(cuda, monkeypatch, amp, dnn):
     """Grad-weight GEMMs on the side HIP stream (ops/streams.py), joined by the
     bucket launches on the comm stream and the end-of-backward callback, give
     the same weights as the inline single-stream backward (up to the fp32
-    atomic-accumulation order of the grad-weight kernels)."""
+    atomic-accumulation order of the grad-weight kernels).  VGG-16's convs
+    carry biases (their gradient stays on the main stream by default)."""
+    dataset, hw, ncls = ("imagenet", 224, 1000) if dnn == "resnet50" else ("cifar10", 32, 10)
     from gaussiank_sgd_amd.ops import streams
     results = []
     monkeypatch.setenv("GKSGD_WGRAD_STREAM_MIN_GFLOP", "0")   # fork every grad-weight of this small batch
@@ -109,7 +111,7 @@ def test_wgrad_side_stream_matches_inline(cuda, monkeypatch, amp):
         monkeypatch.setenv("GKSGD_WGRAD_STREAM", side)
         torch.manual_seed(0)
         comm.init()
-        t = DLTrainer(0, 1, dnn="resnet50", dataset="imagenet", batch_size=8, lr=0.05, device="cuda",
+        t = DLTrainer(0, 1, dnn=dnn, dataset=dataset, batch_size=8, lr=0.05, device="cuda",
                       amp=amp, channels_last=True, data_pool=1)
         opt = DistributedOptimizer(t.optimizer, named_parameters=t.net.named_parameters(),
                                    compression=compressors["gaussian"], is_sparse=True, density=0.01,
@@ -121,8 +123,8 @@ def test_wgrad_side_stream_matches_inline(cuda, monkeypatch, amp):
         g = torch.Generator(device="cuda").manual_seed(5)
         forked = False
         for _ in range(3):
-            x = torch.randn(8, 3, 224, 224, device="cuda", generator=g).contiguous(memory_format=torch.channels_last)
-            y = torch.randint(0, 1000, (8,), device="cuda", generator=g)
+            x = torch.randn(8, 3, hw, hw, device="cuda", generator=g).contiguous(memory_format=torch.channels_last)
+            y = torch.randint(0, ncls, (8,), device="cuda", generator=g)
             opt.zero_grad()
             t.train(1, data=(x, y))
             forked = forked or bool(streams._side)
